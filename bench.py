@@ -1,0 +1,149 @@
+#!/usr/bin/env python
+"""Flagship benchmark: Llama-2-7B pretraining step, Fleet sharding stage 3, bf16, synthetic data.
+
+Metric (BASELINE.json): tokens/sec for the whole node, Llama-2-7B Fleet sharding-3 bf16 at
+1/2/4/8 MI355X.  Weak scaling: every rank trains ``--micro-batch`` sequences of ``--seq-len`` tokens
+per step, so global_batch = micro_batch * N.
+
+Launch:  python bench.py --gpus 1 --steps K --warmup W
+         python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+             --master-port P bench.py --gpus N --steps K --warmup W
+
+The timed region is exactly K full steps (forward + backward + sharding-3 grad reduce-scatter +
+global-norm clip + fused AdamW with fp32 master weights), bracketed by barrier +
+torch.cuda.synchronize(); the reported time is the max over ranks.  Data: synthetic token ids
+(uniform over the 32000-token vocab), random-init weights of the exact Llama-2-7B architecture.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--seq-len", type=int, default=4096)
+    ap.add_argument("--micro-batch", type=int, default=4, help="sequences per GPU per step")
+    ap.add_argument("--model", default="llama2-7b", choices=["llama2-7b", "llama2-13b", "tiny"])
+    ap.add_argument("--layers", type=int, default=None, help="DEBUG ONLY: override layer count (invalid for the metric)")
+    ap.add_argument("--sharding-stage", type=int, default=3)
+    ap.add_argument("--recompute", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+
+    import paddle2_amd as paddle
+    from paddle2_amd.distributed import fleet
+    from paddle2_amd.models import LlamaConfig, LlamaForCausalLM, llama_flops_per_token
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+
+    strategy = fleet.DistributedStrategy()
+    strategy.hybrid_configs = {"dp_degree": 1, "mp_degree": 1, "pp_degree": 1, "sharding_degree": world}
+    fleet.init(is_collective=True, strategy=strategy)
+    paddle.seed(1234 + rank)
+
+    if args.model == "llama2-7b":
+        cfg = LlamaConfig.llama2_7b()
+    elif args.model == "llama2-13b":
+        cfg = LlamaConfig.llama2_13b()
+    else:
+        cfg = LlamaConfig.tiny()
+    cfg.max_position_embeddings = max(cfg.max_position_embeddings, args.seq_len)
+    if args.layers:
+        cfg.num_hidden_layers = args.layers
+    cfg.recompute = args.recompute
+
+    model = LlamaForCausalLM(cfg)
+    decay = {p.name for n, p in model.named_parameters() if "norm" not in n}
+    opt = paddle.optimizer.AdamW(learning_rate=3e-4, beta1=0.9, beta2=0.95, epsilon=1e-8,
+                                 parameters=model.parameters(), weight_decay=0.1,
+                                 apply_decay_param_fun=lambda n: n in decay,
+                                 grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0), multi_precision=True)
+    model, opt = fleet.distributed_model(model, opt, level=f"stage{args.sharding_stage}") if world > 1 else (model, opt)
+
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    b, s = args.micro_batch, args.seq_len
+    gen = torch.Generator(device=dev).manual_seed(rank)
+    ids = paddle.Tensor._wrap(torch.randint(0, cfg.vocab_size, (b, s + 1), generator=gen, device=dev))
+    inputs, labels = ids[:, :-1], ids[:, 1:]
+
+    def step():
+        loss = model(inputs, labels=labels)
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        return loss
+
+    for _ in range(args.warmup):
+        loss = step()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    from paddle2_amd.distributed import collective as C
+
+    if world > 1:
+        C.barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if world > 1:
+        C.barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(el.item())
+    final_loss = float(loss)
+
+    tokens = b * s * args.steps * world
+    tps = tokens / elapsed
+    ms = elapsed / args.steps * 1000.0
+    fpt = llama_flops_per_token(cfg, s)
+    mfu = tps / world * fpt / 2.5e15
+    if rank == 0:
+        out = {
+            "metric": "tokens/sec (whole node) Llama-2-7B Fleet sharding-3 bf16",
+            "value": round(tps, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uniform random token ids), random-init weights",
+            "config": {"model": args.model if not args.layers else f"{args.model}-L{args.layers}(debug)",
+                       "global_batch": b * world, "seq_len": s, "micro_batch_per_gpu": b,
+                       "parallelism": f"sharding{args.sharding_stage}x{world}" if world > 1 else "single",
+                       "layers": cfg.num_hidden_layers},
+            "mfu_vs_2.5PF_dense": round(mfu, 4),
+            "final_loss": round(final_loss, 4),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        C.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,163 @@
+// pybind11 module `paddle2_amd._C`: thin host entry points for the CDNA4 kernels.
+//
+// Tensors cross the boundary as raw device pointers (ints) + shapes + the caller's HIP stream
+// handle, so this module does not depend on libtorch's C++ ABI (it is built with hipcc alone
+// and loads into the process after torch has brought up the HIP runtime). Every entry point is
+// asynchronous on the given stream and safe to capture in a hipGraph (no allocation, no sync).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+
+extern "C" {
+int pd_norm_fwd(int, int, int, const void*, const void*, const void*, const void*, void*, void*, float*, float*, int,
+                int, float, void*);
+int pd_norm_bwd_blocks(int);
+int pd_norm_bwd(int, int, int, const void*, const void*, const void*, const float*, const float*, const void*, void*,
+                float*, float*, void*, void*, int, int, int, void*);
+int pd_swiglu_fwd(int, const void*, const void*, void*, long, int, long, long, void*);
+int pd_swiglu_bwd(int, const void*, const void*, const void*, void*, void*, long, int, long, long, long, long, void*);
+int pd_rope(int, int, int, const void*, void*, const float*, const float*, const int64_t*, int, int, int, int, int,
+            void*);
+int pd_opt_chunk_size();
+int pd_opt_meta_bytes();
+int pd_adamw_mt(int, int, int, const void*, const long*, int, long, float, float, float, float, float, float,
+                const float*, const float*, void*);
+int pd_unscale_mt(int, const void*, const long*, int, long, const float*, float*, void*);
+int pd_sqnorm_mt(int, const void*, const long*, int, long, float*, void*);
+int pd_scale_mt(int, const void*, const long*, int, long, const float*, void*);
+int pd_update_loss_scaling(const float*, float*, int*, int*, int, int, float, float, void*);
+int pd_ce_stats(int, const void*, const int64_t*, float*, float*, float*, long, long, long, void*);
+int pd_ce_bwd(int, const void*, const int64_t*, const float*, const float*, void*, long, long, long, long, int, void*);
+int pd_embed_fwd(int, const int64_t*, const void*, void*, long, int, long, long, void*);
+int pd_embed_bwd(int, const int64_t*, const void*, float*, long, int, long, long, long, void*);
+int pd_cast_from_f32(int, const float*, void*, long, void*);
+int pd_flash_fwd(int, const void*, const void*, const void*, void*, float*, int, int, int, int, int, int, long, long,
+                 long, long, float, int, void*);
+int pd_flash_bwd(int, const void*, const void*, const void*, const void*, const void*, const float*, float*, void*,
+                 void*, void*, float*, int, int, int, int, int, int, long, long, long, long, float, int, void*);
+}
+
+template <typename T>
+static inline T P(uintptr_t v) {
+  return reinterpret_cast<T>(v);
+}
+
+static void check(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string("paddle2_amd._C.") + what + " failed with code " + std::to_string(rc));
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "paddle2_amd native CDNA4 (gfx950) kernels";
+  m.attr("__arch__") = "gfx950";
+
+  m.def("norm_fwd", [](int ln, int dt, int wdt, uintptr_t x, uintptr_t res, uintptr_t w, uintptr_t b, uintptr_t y,
+                       uintptr_t res_out, uintptr_t mean, uintptr_t rstd, int M, int N, float eps, uintptr_t st) {
+    check(pd_norm_fwd(ln, dt, wdt, P<const void*>(x), P<const void*>(res), P<const void*>(w), P<const void*>(b),
+                      P<void*>(y), P<void*>(res_out), P<float*>(mean), P<float*>(rstd), M, N, eps, P<void*>(st)),
+          "norm_fwd");
+  });
+  m.def("norm_bwd_blocks", &pd_norm_bwd_blocks);
+  m.def("norm_bwd", [](int ln, int dt, int wdt, uintptr_t dy, uintptr_t x, uintptr_t w, uintptr_t mean, uintptr_t rstd,
+                       uintptr_t dres, uintptr_t dx, uintptr_t dw_part, uintptr_t db_part, uintptr_t dw, uintptr_t db,
+                       int M, int N, int nblocks, uintptr_t st) {
+    check(pd_norm_bwd(ln, dt, wdt, P<const void*>(dy), P<const void*>(x), P<const void*>(w), P<const float*>(mean),
+                      P<const float*>(rstd), P<const void*>(dres), P<void*>(dx), P<float*>(dw_part),
+                      P<float*>(db_part), P<void*>(dw), P<void*>(db), M, N, nblocks, P<void*>(st)),
+          "norm_bwd");
+  });
+  m.def("swiglu_fwd", [](int dt, uintptr_t x, uintptr_t y, uintptr_t out, long rows, int H, long sx, long sy,
+                         uintptr_t st) {
+    check(pd_swiglu_fwd(dt, P<const void*>(x), P<const void*>(y), P<void*>(out), rows, H, sx, sy, P<void*>(st)),
+          "swiglu_fwd");
+  });
+  m.def("swiglu_bwd", [](int dt, uintptr_t x, uintptr_t y, uintptr_t dout, uintptr_t dx, uintptr_t dy, long rows,
+                         int H, long sx, long sy, long sdx, long sdy, uintptr_t st) {
+    check(pd_swiglu_bwd(dt, P<const void*>(x), P<const void*>(y), P<const void*>(dout), P<void*>(dx), P<void*>(dy),
+                        rows, H, sx, sy, sdx, sdy, P<void*>(st)),
+          "swiglu_bwd");
+  });
+  m.def("rope", [](int dt, int style, int bwd, uintptr_t x, uintptr_t out, uintptr_t cosv, uintptr_t sinv,
+                   uintptr_t pos, int B, int S, int Hn, int D, int time_major, uintptr_t st) {
+    check(pd_rope(dt, style, bwd, P<const void*>(x), P<void*>(out), P<const float*>(cosv), P<const float*>(sinv),
+                  P<const int64_t*>(pos), B, S, Hn, D, time_major, P<void*>(st)),
+          "rope");
+  });
+  m.def("opt_chunk_size", &pd_opt_chunk_size);
+  m.def("opt_meta_bytes", &pd_opt_meta_bytes);
+  m.def("adamw_mt", [](int pdt, int gdt, int master, uintptr_t meta, uintptr_t prefix, int T, long chunks, float lr,
+                       float b1, float b2, float eps, float bc1, float bc2, uintptr_t found_inf, uintptr_t inv_scale,
+                       uintptr_t st) {
+    check(pd_adamw_mt(pdt, gdt, master, P<const void*>(meta), P<const long*>(prefix), T, chunks, lr, b1, b2, eps, bc1,
+                      bc2, P<const float*>(found_inf), P<const float*>(inv_scale), P<void*>(st)),
+          "adamw_mt");
+  });
+  m.def("unscale_mt", [](int gdt, uintptr_t meta, uintptr_t prefix, int T, long chunks, uintptr_t scale,
+                         uintptr_t found_inf, uintptr_t st) {
+    check(pd_unscale_mt(gdt, P<const void*>(meta), P<const long*>(prefix), T, chunks, P<const float*>(scale),
+                        P<float*>(found_inf), P<void*>(st)),
+          "unscale_mt");
+  });
+  m.def("sqnorm_mt", [](int gdt, uintptr_t meta, uintptr_t prefix, int T, long chunks, uintptr_t out, uintptr_t st) {
+    check(pd_sqnorm_mt(gdt, P<const void*>(meta), P<const long*>(prefix), T, chunks, P<float*>(out), P<void*>(st)),
+          "sqnorm_mt");
+  });
+  m.def("scale_mt", [](int gdt, uintptr_t meta, uintptr_t prefix, int T, long chunks, uintptr_t coef, uintptr_t st) {
+    check(pd_scale_mt(gdt, P<const void*>(meta), P<const long*>(prefix), T, chunks, P<const float*>(coef),
+                      P<void*>(st)),
+          "scale_mt");
+  });
+  m.def("update_loss_scaling", [](uintptr_t found_inf, uintptr_t scale, uintptr_t good, uintptr_t bad, int incr_n,
+                                  int decr_n, float incr_ratio, float decr_ratio, uintptr_t st) {
+    check(pd_update_loss_scaling(P<const float*>(found_inf), P<float*>(scale), P<int*>(good), P<int*>(bad), incr_n,
+                                 decr_n, incr_ratio, decr_ratio, P<void*>(st)),
+          "update_loss_scaling");
+  });
+  m.def("ce_stats", [](int dt, uintptr_t logits, uintptr_t labels, uintptr_t mx, uintptr_t se, uintptr_t tgt, long N,
+                       long V, long start, uintptr_t st) {
+    check(pd_ce_stats(dt, P<const void*>(logits), P<const int64_t*>(labels), P<float*>(mx), P<float*>(se),
+                      P<float*>(tgt), N, V, start, P<void*>(st)),
+          "ce_stats");
+  });
+  m.def("ce_bwd", [](int dt, uintptr_t logits, uintptr_t labels, uintptr_t lse, uintptr_t dloss, uintptr_t dx, long N,
+                     long V, long start, long ignore_index, int dloss_scalar, uintptr_t st) {
+    check(pd_ce_bwd(dt, P<const void*>(logits), P<const int64_t*>(labels), P<const float*>(lse),
+                    P<const float*>(dloss), P<void*>(dx), N, V, start, ignore_index, dloss_scalar, P<void*>(st)),
+          "ce_bwd");
+  });
+  m.def("embed_fwd", [](int dt, uintptr_t ids, uintptr_t w, uintptr_t out, long Ntok, int H, long start, long Vl,
+                        uintptr_t st) {
+    check(pd_embed_fwd(dt, P<const int64_t*>(ids), P<const void*>(w), P<void*>(out), Ntok, H, start, Vl, P<void*>(st)),
+          "embed_fwd");
+  });
+  m.def("embed_bwd", [](int dt, uintptr_t ids, uintptr_t dout, uintptr_t dw32, long Ntok, int H, long start, long Vl,
+                        long padding_idx, uintptr_t st) {
+    check(pd_embed_bwd(dt, P<const int64_t*>(ids), P<const void*>(dout), P<float*>(dw32), Ntok, H, start, Vl,
+                       padding_idx, P<void*>(st)),
+          "embed_bwd");
+  });
+  m.def("cast_from_f32", [](int dt, uintptr_t src, uintptr_t dst, long n, uintptr_t st) {
+    check(pd_cast_from_f32(dt, P<const float*>(src), P<void*>(dst), n, P<void*>(st)), "cast_from_f32");
+  });
+  m.def("flash_fwd", [](int dt, uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t lse, int B, int Sq,
+                        int Sk, int Hq, int Hk, int D, long sq_row, long sk_row, long sv_row, long so_row, float scale,
+                        int causal, uintptr_t st) {
+    check(pd_flash_fwd(dt, P<const void*>(q), P<const void*>(k), P<const void*>(v), P<void*>(o), P<float*>(lse), B, Sq,
+                       Sk, Hq, Hk, D, sq_row, sk_row, sv_row, so_row, scale, causal, P<void*>(st)),
+          "flash_fwd");
+  });
+  m.def("flash_bwd", [](int dt, uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t dout, uintptr_t lse,
+                        uintptr_t delta, uintptr_t dq, uintptr_t dk, uintptr_t dv, uintptr_t dq32, int B, int Sq,
+                        int Sk, int Hq, int Hk, int D, long sq_row, long sk_row, long sv_row, long so_row, float scale,
+                        int causal, uintptr_t st) {
+    check(pd_flash_bwd(dt, P<const void*>(q), P<const void*>(k), P<const void*>(v), P<const void*>(o),
+                       P<const void*>(dout), P<const float*>(lse), P<float*>(delta), P<void*>(dq), P<void*>(dk),
+                       P<void*>(dv), P<float*>(dq32), B, Sq, Sk, Hq, Hk, D, sq_row, sk_row, sv_row, so_row, scale,
+                       causal, P<void*>(st)),
+          "flash_bwd");
+  });
+}

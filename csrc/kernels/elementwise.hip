@@ -1,0 +1,213 @@
+// SwiGLU and rotary position embedding (fwd + bwd) for gfx950.
+//
+// Reference behaviour: phi/kernels/gpu/swiglu_kernel.cu (out = silu(x) * y; y optional ->
+// split x in halves) and fusion/gpu/fused_rope_kernel.cu / fused_rope_utils.h (rotate-half and
+// rotate-every-two styles, sin/cos tables, optional position_ids).
+// MI355X design: memory-bound, so every lane moves 16 B per access, grid is capped at
+// 256 CUs x 8 blocks and grid-strides (Guideline 11); RoPE reads cos/sin once per (s, d) tile
+// and rotates all heads of q and k in the same block so the table stays in L1.
+#include "common.h"
+
+namespace pd {
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// ------------------------------------------------------------------------------ SwiGLU
+// x, y: [rows, H] with row strides sx, sy (elements) — for the packed form y = x + H.
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ x, const T* __restrict__ y,
+                                                         T* __restrict__ out, long rows, int H, long sx, long sy) {
+  constexpr int V = 16 / sizeof(T);
+  const int hv = H / V;
+  const long total = rows * hv;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long r = i / hv;
+    const int c = (int)(i - r * hv) * V;
+    float a[V], b[V], o[V];
+    load_vec<T, V>(x + r * sx + c, a);
+    load_vec<T, V>(y + r * sy + c, b);
+#pragma unroll
+    for (int j = 0; j < V; ++j) o[j] = a[j] * sigmoidf_(a[j]) * b[j];
+    store_vec<T, V>(out + r * H + c, o);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ x, const T* __restrict__ y,
+                                                         const T* __restrict__ dout, T* __restrict__ dx,
+                                                         T* __restrict__ dy, long rows, int H, long sx, long sy,
+                                                         long sdx, long sdy) {
+  constexpr int V = 16 / sizeof(T);
+  const int hv = H / V;
+  const long total = rows * hv;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long r = i / hv;
+    const int c = (int)(i - r * hv) * V;
+    float a[V], b[V], g[V], da[V], db[V];
+    load_vec<T, V>(x + r * sx + c, a);
+    load_vec<T, V>(y + r * sy + c, b);
+    load_vec<T, V>(dout + r * H + c, g);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float s = sigmoidf_(a[j]);
+      const float silu = a[j] * s;
+      db[j] = g[j] * silu;
+      da[j] = g[j] * b[j] * s * (1.f + a[j] * (1.f - s));
+    }
+    store_vec<T, V>(dx + r * sdx + c, da);
+    store_vec<T, V>(dy + r * sdy + c, db);
+  }
+}
+
+static inline int ew_grid(long work) {
+  long g = (work + 255) / 256;
+  return (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
+}
+
+// ------------------------------------------------------------------------------ RoPE
+// x: [B, S, Hn, D] (or time-major [S, B, Hn, D]); cos/sin: [S, D] fp32 (already expanded per
+// style); pos: optional [B, S] int64 position ids. One thread handles one (token, head) x 8
+// rotation pairs with 16-byte loads (D % 16 == 0 fast path; scalar path otherwise).
+// STYLE 0 = rotate-half (front/back halves), 1 = rotate-every-two (adjacent pairs).
+// BWD applies the transposed rotation (R^T = rotation by -theta with partner sines swapped).
+__device__ __forceinline__ void rot8(const float (&xa)[8], const float (&xb)[8], const float (&ca)[8],
+                                     const float (&cb)[8], const float (&sa)[8], const float (&sb)[8],
+                                     float (&oa)[8], float (&ob)[8], bool bwd) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (!bwd) { oa[k] = xa[k] * ca[k] - xb[k] * sa[k]; ob[k] = xb[k] * cb[k] + xa[k] * sb[k]; }
+    else { oa[k] = xa[k] * ca[k] + xb[k] * sb[k]; ob[k] = xb[k] * cb[k] - xa[k] * sa[k]; }
+  }
+}
+
+__device__ __forceinline__ void ld8f(const float* p, float (&o)[8]) {
+  float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float (&o)[8]) {
+  if constexpr (sizeof(T) == 4) ld8f((const float*)p, o);
+  else load_vec<T, 8>(p, o);
+}
+
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const float (&o)[8]) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4*>((float*)p + 4) = make_float4(o[4], o[5], o[6], o[7]);
+  } else store_vec<T, 8>(p, o);
+}
+
+template <typename T, int STYLE, bool BWD, bool VEC>
+__global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, T* __restrict__ out,
+                                                   const float* __restrict__ cosv, const float* __restrict__ sinv,
+                                                   const int64_t* __restrict__ pos, int B, int S, int Hn, int D,
+                                                   int time_major) {
+  const int half = D / 2;
+  const int chunks = (half + 7) / 8;
+  const long total = (long)B * S * Hn * chunks;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int ch = (int)(i % chunks);
+    long t = i / chunks;
+    const int h = (int)(t % Hn);
+    t /= Hn;  // token index in storage order
+    int b, s;
+    if (time_major) { s = (int)(t / B); b = (int)(t % B); }
+    else { b = (int)(t / S); s = (int)(t % S); }
+    const int p = pos ? (int)pos[(long)b * S + s] : s;
+    const T* xr = x + (t * Hn + h) * (long)D;
+    T* orow = out + (t * Hn + h) * (long)D;
+    const float* cr = cosv + (long)p * D;
+    const float* sr = sinv + (long)p * D;
+    if constexpr (VEC) {
+      const int q0 = ch * 8;
+      float xa[8], xb[8], ca[8], cb[8], sa[8], sb[8], oa[8], ob[8];
+      if constexpr (STYLE == 0) {
+        ld8<T>(xr + q0, xa); ld8<T>(xr + q0 + half, xb);
+        ld8f(cr + q0, ca); ld8f(cr + q0 + half, cb); ld8f(sr + q0, sa); ld8f(sr + q0 + half, sb);
+        rot8(xa, xb, ca, cb, sa, sb, oa, ob, BWD);
+        st8<T>(orow + q0, oa); st8<T>(orow + q0 + half, ob);
+      } else {
+        float e0[8], e1[8], c0[8], c1[8], s0[8], s1[8];
+        ld8<T>(xr + 2 * q0, e0); ld8<T>(xr + 2 * q0 + 8, e1);
+        ld8f(cr + 2 * q0, c0); ld8f(cr + 2 * q0 + 8, c1); ld8f(sr + 2 * q0, s0); ld8f(sr + 2 * q0 + 8, s1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          xa[k] = e0[2 * k]; xb[k] = e0[2 * k + 1]; xa[k + 4] = e1[2 * k]; xb[k + 4] = e1[2 * k + 1];
+          ca[k] = c0[2 * k]; cb[k] = c0[2 * k + 1]; ca[k + 4] = c1[2 * k]; cb[k + 4] = c1[2 * k + 1];
+          sa[k] = s0[2 * k]; sb[k] = s0[2 * k + 1]; sa[k + 4] = s1[2 * k]; sb[k + 4] = s1[2 * k + 1];
+        }
+        rot8(xa, xb, ca, cb, sa, sb, oa, ob, BWD);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          e0[2 * k] = oa[k]; e0[2 * k + 1] = ob[k]; e1[2 * k] = oa[k + 4]; e1[2 * k + 1] = ob[k + 4];
+        }
+        st8<T>(orow + 2 * q0, e0); st8<T>(orow + 2 * q0 + 8, e1);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int q = ch * 8 + k;
+        if (q >= half) break;
+        int ia, ib;
+        if (STYLE == 0) { ia = q; ib = q + half; }
+        else { ia = 2 * q; ib = 2 * q + 1; }
+        const float xa = Elt<T>::ld(xr + ia), xb = Elt<T>::ld(xr + ib);
+        const float ca = cr[ia], cb = cr[ib], sa = sr[ia], sb = sr[ib];
+        float oa, ob;
+        if (!BWD) { oa = xa * ca - xb * sa; ob = xb * cb + xa * sb; }
+        else { oa = xa * ca + xb * sb; ob = xb * cb - xa * sa; }
+        Elt<T>::st(orow + ia, oa);
+        Elt<T>::st(orow + ib, ob);
+      }
+    }
+  }
+}
+
+}  // namespace pd
+
+using namespace pd;
+
+extern "C" int pd_swiglu_fwd(int dt, const void* x, const void* y, void* out, long rows, int H, long sx, long sy,
+                             void* stream) {
+  const int V = dt == kF32 ? 4 : 8;
+  if (H % V) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  const int g = ew_grid(rows * (H / V));
+  PD_DISPATCH_FLOAT(dt, T, swiglu_fwd_kernel<T><<<g, 256, 0, st>>>((const T*)x, (const T*)y, (T*)out, rows, H, sx, sy));
+  return (int)hipGetLastError();
+}
+
+extern "C" int pd_swiglu_bwd(int dt, const void* x, const void* y, const void* dout, void* dx, void* dy, long rows,
+                             int H, long sx, long sy, long sdx, long sdy, void* stream) {
+  const int V = dt == kF32 ? 4 : 8;
+  if (H % V) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  const int g = ew_grid(rows * (H / V));
+  PD_DISPATCH_FLOAT(dt, T, swiglu_bwd_kernel<T><<<g, 256, 0, st>>>((const T*)x, (const T*)y, (const T*)dout, (T*)dx,
+                                                                    (T*)dy, rows, H, sx, sy, sdx, sdy));
+  return (int)hipGetLastError();
+}
+
+extern "C" int pd_rope(int dt, int style, int bwd, const void* x, void* out, const float* cosv, const float* sinv,
+                       const int64_t* pos, int B, int S, int Hn, int D, int time_major, void* stream) {
+  if (D % 2) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  const long work = (long)B * S * Hn * ((D / 2 + 7) / 8);
+  const int g = ew_grid(work);
+  const bool vec = (D % 16) == 0;
+#define PD_ROPE1(T, SY, BW, VE) rope_kernel<T, SY, BW, VE><<<g, 256, 0, st>>>((const T*)x, (T*)out, cosv, sinv, pos, B, S, Hn, D, time_major)
+#define PD_ROPE(T)                                                                                    \
+  if (vec) {                                                                                          \
+    if (style == 0) { if (bwd) PD_ROPE1(T, 0, true, true); else PD_ROPE1(T, 0, false, true); }        \
+    else { if (bwd) PD_ROPE1(T, 1, true, true); else PD_ROPE1(T, 1, false, true); }                   \
+  } else {                                                                                            \
+    if (style == 0) { if (bwd) PD_ROPE1(T, 0, true, false); else PD_ROPE1(T, 0, false, false); }      \
+    else { if (bwd) PD_ROPE1(T, 1, true, false); else PD_ROPE1(T, 1, false, false); }                 \
+  }
+  PD_DISPATCH_FLOAT(dt, T, PD_ROPE(T));
+#undef PD_ROPE
+#undef PD_ROPE1
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,537 @@
+// Flash attention forward + backward on CDNA4 MFMA (gfx950), bf16 in / fp32 accumulate.
+//
+// Reference behaviour: phi/kernels/gpu/flash_attn_kernel.cu / flash_attn_grad_kernel.cu
+// (q/k/v [b, s, nh, hd], causal, GQA via num_heads_k, returns softmax_lse [b, nh, s]).  The
+// reference dlopens an external flash-attn fork; this is a from-scratch CDNA4 design:
+//
+// Forward (per workgroup: 4 waves x 32 query rows = 128 rows of one (b, head)):
+//  * swapped product S^T = K . Q^T with v_mfma_f32_32x32x16_bf16 so each lane owns ONE query
+//    row's scores (16 keys per lane-half): the softmax row max/sum is 16 in-register ops plus
+//    one lane^32 exchange — no LDS round trip for P;
+//  * the S^T accumulator feeds the P.V product directly as the MFMA B operand (guide §3
+//    "accumulator tile as the next MFMA's operand"), with V^T fragments read by
+//    ds_read_b64_tr_b16 (T10) from a row-major V tile;
+//  * K/V tiles (64 keys) are register-staged global->LDS with the issue-early/write-late split
+//    (T14), double-buffered, one barrier per tile; every LDS image uses the dual-use XOR swizzle
+//    off = 256*row + 16*(ch ^ ((row&3)<<2 | (row>>2)&3)) so both ds_read_b128 row reads and
+//    ds_read_b64_tr_b16 column reads are conflict-free (T10 (b));
+//  * O^T accumulators are per-lane (lane = query) so the online-softmax rescale is a scalar
+//    multiply; exp2 with the 1/sqrt(d)*log2(e) scale folded into one multiply;
+//  * 1-D grid with an XCD-aware bijective remap (T1): all query blocks of a KV head land on one
+//    XCD so K/V are served from that XCD's L2; causal grids start with the heaviest blocks.
+//
+// Backward (per workgroup: 4 waves x 32 keys = 128 keys of one (b, kv-head)):
+//  * key on the lane: S = Q.K^T and dP = dO.V^T have the key as the accumulator column, so
+//    P and dS are directly the B operands of dV^T += dO^T.P and dK^T += Q^T.dS (tr-reads of the
+//    Q / dO tiles give the A operands); K^T / V^T fragments stay in VGPRs for the whole sweep;
+//  * the workgroup sweeps every query head of its GQA group x every 32-row query tile, so dK/dV
+//    are complete in registers and written once (no cross-workgroup sum for dK/dV);
+//  * dS goes through LDS once for dQ = dS.K (4 waves split D), summed across key blocks with
+//    fp32 atomics in the full-rate two-128B-segment shape (Guideline 12), cast to bf16 after.
+#include "common.h"
+
+namespace pd {
+namespace fa {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) char lds_char;
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+__device__ __forceinline__ int swz(int row, int ch, int nch) {
+  return ch ^ ((((row & 3) << 2) | ((row >> 2) & 3)) & (nch - 1));
+}
+
+// byte offset of element (row, col) (16-bit elements) in a swizzled [rows][D] tile
+template <int D>
+__device__ __forceinline__ int tile_off(int row, int col) {
+  constexpr int NCH = D / 8;
+  return row * (D * 2) + swz(row, col >> 3, NCH) * 16 + (col & 7) * 2;
+}
+
+__device__ __forceinline__ bf16x8 lds_b128(const char* base, int off) {
+  return *reinterpret_cast<const bf16x8*>(base + off);
+}
+
+__device__ __forceinline__ s16x4 lds_tr(const char* base, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)((lds_char*)base + off));
+}
+
+__device__ __forceinline__ bf16x8 cat4(s16x4 a, s16x4 b) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 r = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// Pack 8 fp32 accumulator registers [8s, 8s+8) into a bf16 MFMA operand fragment.
+__device__ __forceinline__ bf16x8 pack8(const f32x16& acc, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)acc[8 * s + j];
+  return r;
+}
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// XCD-aware bijective remap of a 1-D block id (cdna guide §5 "XCD swizzle must be bijective").
+__device__ __forceinline__ int xcd_remap(int bid, int n) {
+  const int q = n / 8, r = n % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+// Transposed-read address for the A operand V^T / dO^T / Q^T / K^T-column fragments:
+// 32x16 operand whose row = column `c0 + (lane&31)` of a row-major tile, k rows = `r0 + k`.
+// PERM selects the permuted k order required when the B operand is an accumulator tile.
+template <int D, bool PERM>
+__device__ __forceinline__ bf16x8 tr_frag(const char* tile, int r0, int c0, int lane) {
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  const int h = g >> 1;
+  const int col = c0 + ((g & 1) << 4) + 4 * pp;
+  int ra, rb;
+  if (PERM) { ra = r0 + 4 * h + qq; rb = ra + 8; }       // keys 16s + 8(j>>2) + 4h + (j&3)
+  else { ra = r0 + 8 * h + qq; rb = ra + 4; }            // natural k = 8h + j
+  return cat4(lds_tr(tile, tile_off<D>(ra, col)), lds_tr(tile, tile_off<D>(rb, col)));
+}
+
+// =====================================================================================
+//                                       FORWARD
+// =====================================================================================
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+                                                     const bf16* __restrict__ Vv, bf16* __restrict__ O,
+                                                     float* __restrict__ LSE, int B, int Sq, int Sk, int Hq, int Hk,
+                                                     long sq, long sk, long sv, long so, float scale) {
+  constexpr int BM = 128, BN = 64, NCH = D / 8, KS = D / 16, DT = D / 32;
+  constexpr int TILE = BN * D * 2;
+  constexpr int NLOAD = BN * NCH / 256;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][K|V]
+
+  const int nmb = (Sq + BM - 1) / BM;
+  const int total = nmb * Hq * B;
+  const int w_id = xcd_remap(blockIdx.x, total);
+  int mb = w_id % nmb;
+  const int hq = (w_id / nmb) % Hq;
+  const int b = w_id / (nmb * Hq);
+  if (CAUSAL) mb = nmb - 1 - mb;  // heaviest query blocks first
+  const int hk = hq / (Hq / Hk);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int m0 = mb * BM;
+  const int off = Sk - Sq;  // bottom-right causal alignment
+
+  const bf16* Qb = Q + (long)b * Sq * sq + hq * D;
+  const bf16* Kb = K + (long)b * Sk * sk + hk * D;
+  const bf16* Vb = Vv + (long)b * Sk * sv + hk * D;
+
+  // Q fragments (B operand of S^T = K.Q^T): lane holds Q[q][16ks + 8h .. +8]
+  const int qrow = m0 + wv * 32 + r;
+  bf16x8 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (qrow < Sq) qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (long)qrow * sq + ks * 16 + 8 * h);
+    else qf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+
+  int n_end = Sk;
+  if (CAUSAL) n_end = min(Sk, m0 + BM + off);
+  const int ntiles = n_end > 0 ? (n_end + BN - 1) / BN : 0;
+
+  u16x8 stk[NLOAD], stv[NLOAD];
+  auto gload = [&](int n0) {
+#pragma unroll
+    for (int i = 0; i < NLOAD; ++i) {
+      const int c = tid + 256 * i, row = c / NCH, ch = c % NCH, key = n0 + row;
+      if (key < Sk) {
+        stk[i] = *reinterpret_cast<const u16x8*>(Kb + (long)key * sk + ch * 8);
+        stv[i] = *reinterpret_cast<const u16x8*>(Vb + (long)key * sv + ch * 8);
+      } else {
+        stk[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        stv[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* kt = smem + buf * 2 * TILE;
+    char* vt = kt + TILE;
+#pragma unroll
+    for (int i = 0; i < NLOAD; ++i) {
+      const int c = tid + 256 * i, row = c / NCH, ch = c % NCH;
+      const int o = row * (D * 2) + swz(row, ch, NCH) * 16;
+      *reinterpret_cast<u16x8*>(kt + o) = stk[i];
+      *reinterpret_cast<u16x8*>(vt + o) = stv[i];
+    }
+  };
+
+  f32x16 oacc[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) oacc[dt] = f32x16{};
+  float m_i = -INFINITY, l_i = 0.f;
+  const float sl2 = scale * kLog2e;
+
+  if (ntiles > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int n0 = t * BN;
+    const bool has_next = t + 1 < ntiles;
+    if (has_next) gload(n0 + BN);  // issue early; lands while we compute (T14)
+    const char* kt = smem + (t & 1) * 2 * TILE;
+    const char* vt = kt + TILE;
+
+    // ---- S^T = K . Q^T for two 32-key sub-blocks
+    f32x16 s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      s[kb] = f32x16{};
+      const int krow = kb * 32 + r;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        bf16x8 a = lds_b128(kt, krow * (D * 2) + swz(krow, 2 * ks + h, NCH) * 16);
+        s[kb] = mfma(a, qf[ks], s[kb]);
+      }
+    }
+    // ---- scale, mask, online softmax (lane owns query qrow; 32 of the 64 keys)
+    const bool need_mask = (n0 + BN > Sk) || (CAUSAL && (n0 + BN - 1 > m0 + off));
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float v = s[kb][i] * sl2;
+        if (need_mask) {
+          const int key = n0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (key >= Sk || (CAUSAL && key > qrow + off)) v = -INFINITY;
+        }
+        s[kb][i] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_i, mx);
+    const float base = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = exp2f(m_i - base);
+    float ls = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = exp2f(s[kb][i] - base);
+        s[kb][i] = p;
+        ls += p;
+      }
+    }
+    l_i = l_i * alpha + ls;  // per lane-half partial; halves combined at the end
+    m_i = m_new;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) oacc[dt] *= alpha;
+
+    // ---- O^T += V^T . P^T
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 pb = pack8(s[kb], ss);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const bf16x8 a = tr_frag<D, true>(vt, kb * 32 + 16 * ss, dt * 32, lane);
+          oacc[dt] = mfma(a, pb, oacc[dt]);
+        }
+      }
+    }
+    if (has_next) lstore((t + 1) & 1);  // write late (T14)
+    __syncthreads();
+  }
+
+  // ---- epilogue: normalise, store O (row = query, 4 consecutive d per store) and LSE
+  const float l_tot = l_i + __shfl_xor(l_i, 32, 64);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (qrow < Sq) {
+    bf16* orow = O + (long)b * Sq * so + (long)qrow * so + hq * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int d = dt * 32 + 8 * c + 4 * h;
+        ushort4 v;
+        v.x = f2bf(oacc[dt][4 * c + 0] * inv);
+        v.y = f2bf(oacc[dt][4 * c + 1] * inv);
+        v.z = f2bf(oacc[dt][4 * c + 2] * inv);
+        v.w = f2bf(oacc[dt][4 * c + 3] * inv);
+        *reinterpret_cast<ushort4*>(orow + d) = v;
+      }
+    }
+    if (h == 0) {
+      LSE[((long)b * Hq + hq) * Sq + qrow] = l_tot > 0.f ? (m_i + log2f(l_tot)) * kLn2 : INFINITY;
+    }
+  }
+}
+
+// =====================================================================================
+//                                       BACKWARD
+// =====================================================================================
+// delta[b, h, q] = sum_d dO . O  (fp32), one wave per row
+__global__ __launch_bounds__(256) void bwd_delta_kernel(const bf16* __restrict__ O, const bf16* __restrict__ dO,
+                                                        float* __restrict__ delta, int B, int Sq, int Hq, int D,
+                                                        long so) {
+  const long rowid = blockIdx.x * 4L + (threadIdx.x >> 6);
+  const long total = (long)B * Hq * Sq;
+  if (rowid >= total) return;
+  const int lane = threadIdx.x & 63;
+  const int q = (int)(rowid % Sq);
+  const int hq = (int)((rowid / Sq) % Hq);
+  const int b = (int)(rowid / ((long)Sq * Hq));
+  const long base = ((long)b * Sq + q) * so + (long)hq * D;
+  float acc = 0.f;
+  for (int d = lane * 8; d < D; d += 512) {
+    float a[8], c[8];
+    load_vec<bf16, 8>(O + base + d, a);
+    load_vec<bf16, 8>(dO + base + d, c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += a[j] * c[j];
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) delta[rowid] = acc;
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void bwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+                                                     const bf16* __restrict__ Vv, const bf16* __restrict__ dO,
+                                                     const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                                                     float* __restrict__ dQ32, bf16* __restrict__ dK,
+                                                     bf16* __restrict__ dV, int B, int Sq, int Sk, int Hq, int Hk,
+                                                     long sq, long sk, long sv, long so, float scale) {
+  constexpr int BNK = 128, BMQ = 32, NCH = D / 8, KS = D / 16, DT = D / 32;
+  constexpr int KTILE = BNK * D * 2;     // K block image (for dQ = dS.K)
+  constexpr int QTILE = BMQ * D * 2;     // Q / dO tile image
+  constexpr int STILE = BMQ * BNK * 2;   // dS tile [32 q][128 keys]
+  __shared__ __attribute__((aligned(16))) char smem[KTILE + 2 * QTILE + STILE + 2 * BMQ * 4];
+  char* kimg = smem;
+  char* qimg = smem + KTILE;
+  char* doimg = qimg + QTILE;
+  char* simg = doimg + QTILE;
+  float* lse_s = reinterpret_cast<float*>(simg + STILE);
+  float* del_s = lse_s + BMQ;
+
+  const int nkb = (Sk + BNK - 1) / BNK;
+  const int total = nkb * Hk * B;
+  const int w_id = xcd_remap(blockIdx.x, total);
+  const int kblk = w_id % nkb;
+  const int hk = (w_id / nkb) % Hk;
+  const int b = w_id / (nkb * Hk);
+  const int group = Hq / Hk;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int k0 = kblk * BNK;
+  const int off = Sk - Sq;
+  const int mykey = k0 + wv * 32 + r;  // key owned by this lane's accumulator column
+
+  const bf16* Kb = K + (long)b * Sk * sk + hk * D;
+  const bf16* Vb = Vv + (long)b * Sk * sv + hk * D;
+
+  // K block -> LDS (for dQ), K/V fragments -> registers (B operands of S and dP)
+  for (int c = tid; c < BNK * NCH; c += 256) {
+    const int row = c / NCH, ch = c % NCH, key = k0 + row;
+    u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (key < Sk) v = *reinterpret_cast<const u16x8*>(Kb + (long)key * sk + ch * 8);
+    *reinterpret_cast<u16x8*>(kimg + row * (D * 2) + swz(row, ch, NCH) * 16) = v;
+  }
+  bf16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (mykey < Sk) {
+      kf[ks] = *reinterpret_cast<const bf16x8*>(Kb + (long)mykey * sk + ks * 16 + 8 * h);
+      vf[ks] = *reinterpret_cast<const bf16x8*>(Vb + (long)mykey * sv + ks * 16 + 8 * h);
+    } else {
+      kf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      vf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  f32x16 dkacc[DT], dvacc[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) { dkacc[dt] = f32x16{}; dvacc[dt] = f32x16{}; }
+  const float sl2 = scale * kLog2e;
+
+  int q_begin = 0;
+  if (CAUSAL) q_begin = max(0, k0 - off) / BMQ * BMQ;
+  const int nqt = Sq > q_begin ? (Sq - q_begin + BMQ - 1) / BMQ : 0;
+  constexpr int NL = BMQ * NCH / 256;  // 16-B chunks per thread per tile (2 for D=128)
+
+  for (int hh = 0; hh < group; ++hh) {
+    const int hq = hk * group + hh;
+    const bf16* Qb = Q + (long)b * Sq * sq + hq * D;
+    const bf16* dOb = dO + (long)b * Sq * so + hq * D;
+    float* dQb = dQ32 + (long)b * Sq * Hq * D + (long)hq * D;
+    const float* lseb = LSE + ((long)b * Hq + hq) * Sq;
+    const float* delb = DELTA + ((long)b * Hq + hq) * Sq;
+    for (int t = 0; t < nqt; ++t) {
+      const int q0 = q_begin + t * BMQ;
+      __syncthreads();  // previous tile's readers are done
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        const int c = tid + 256 * i, row = c / NCH, ch = c % NCH, q = q0 + row;
+        u16x8 a = u16x8{0, 0, 0, 0, 0, 0, 0, 0}, d2 = a;
+        if (q < Sq) {
+          a = *reinterpret_cast<const u16x8*>(Qb + (long)q * sq + ch * 8);
+          d2 = *reinterpret_cast<const u16x8*>(dOb + (long)q * so + ch * 8);
+        }
+        const int o = row * (D * 2) + swz(row, ch, NCH) * 16;
+        *reinterpret_cast<u16x8*>(qimg + o) = a;
+        *reinterpret_cast<u16x8*>(doimg + o) = d2;
+      }
+      if (tid < BMQ) {
+        const int q = q0 + tid;
+        lse_s[tid] = q < Sq ? lseb[q] * kLog2e : INFINITY;
+        del_s[tid] = q < Sq ? delb[q] : 0.f;
+      }
+      __syncthreads();
+
+      // S = Q.K^T and dP = dO.V^T : rows = q (regs), cols = this wave's 32 keys (lanes)
+      f32x16 sacc = f32x16{}, dpacc = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int o = r * (D * 2) + swz(r, 2 * ks + h, NCH) * 16;
+        sacc = mfma(lds_b128(qimg, o), kf[ks], sacc);
+        dpacc = mfma(lds_b128(doimg, o), vf[ks], dpacc);
+      }
+      // P = exp2(S*scale*log2e - lse*log2e), dS = P * (dP - delta)
+      const bool need_mask = (k0 + BNK > Sk) || (CAUSAL && (k0 + BNK - 1 > q0 + off));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qi = (i & 3) + 8 * (i >> 2) + 4 * h;
+        float p = exp2f(sacc[i] * sl2 - lse_s[qi]);
+        if (need_mask) {
+          const int q = q0 + qi;
+          if (mykey >= Sk || (CAUSAL && mykey > q + off)) p = 0.f;
+        }
+        sacc[i] = p;
+        dpacc[i] = p * (dpacc[i] - del_s[qi]);
+      }
+      // dV^T += dO^T . P ; dK^T += Q^T . dS   (A operands by transposed reads, permuted k)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 pb = pack8(sacc, ss);
+        const bf16x8 db = pack8(dpacc, ss);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          dvacc[dt] = mfma(tr_frag<D, true>(doimg, 16 * ss, dt * 32, lane), pb, dvacc[dt]);
+          dkacc[dt] = mfma(tr_frag<D, true>(qimg, 16 * ss, dt * 32, lane), db, dkacc[dt]);
+        }
+      }
+      // dS -> LDS image [32 q][128 keys] (bf16) for dQ
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qi = (i & 3) + 8 * (i >> 2) + 4 * h;
+        const int col = wv * 32 + r;
+        *reinterpret_cast<__bf16*>(simg + tile_off<BNK>(qi, col)) = (__bf16)dpacc[i];
+      }
+      __syncthreads();
+      // dQ[32 q][d in wave's 32-col slice] = dS[32 q][128 keys] . K[128 keys][d]
+      if (wv < DT) {
+        f32x16 dq = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < BNK / 16; ++ks) {
+          const bf16x8 a = lds_b128(simg, r * (BNK * 2) + swz(r, 2 * ks + h, BNK / 8) * 16);
+          const bf16x8 bb = tr_frag<D, false>(kimg, 16 * ks, wv * 32, lane);
+          dq = mfma(a, bb, dq);
+        }
+        // accumulator: row q = (i&3)+8(i>>2)+4h, col d = wv*32 + r -> fp32 atomics
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int q = q0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (q < Sq) atomicAdd(dQb + (long)q * Hq * D + wv * 32 + r, dq[i] * scale);
+        }
+      }
+    }
+  }
+  // write dK (scaled) and dV for this lane's key: accumulator row = d, column = key
+  if (mykey < Sk) {
+    bf16* dkr = dK + ((long)b * Sk + mykey) * Hk * D + hk * D;
+    bf16* dvr = dV + ((long)b * Sk + mykey) * Hk * D + hk * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int d = dt * 32 + 8 * c + 4 * h;
+        ushort4 kv, vv;
+        kv.x = f2bf(dkacc[dt][4 * c + 0] * scale); kv.y = f2bf(dkacc[dt][4 * c + 1] * scale);
+        kv.z = f2bf(dkacc[dt][4 * c + 2] * scale); kv.w = f2bf(dkacc[dt][4 * c + 3] * scale);
+        vv.x = f2bf(dvacc[dt][4 * c + 0]); vv.y = f2bf(dvacc[dt][4 * c + 1]);
+        vv.z = f2bf(dvacc[dt][4 * c + 2]); vv.w = f2bf(dvacc[dt][4 * c + 3]);
+        *reinterpret_cast<ushort4*>(dkr + d) = kv;
+        *reinterpret_cast<ushort4*>(dvr + d) = vv;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void f32_to_bf16_strided(const float* __restrict__ src, bf16* __restrict__ dst,
+                                                           long rows, int D, int H, long sdst) {
+  // src: [rows(b*s), H, D] contiguous ; dst row stride sdst (elements) per (b*s) row
+  const long total = rows * H * (D / 4);
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long e = i * 4;
+    const long row = e / ((long)H * D);
+    const long rem = e - row * H * D;
+    float4 v = *reinterpret_cast<const float4*>(src + e);
+    ushort4 o;
+    o.x = f2bf(v.x); o.y = f2bf(v.y); o.z = f2bf(v.z); o.w = f2bf(v.w);
+    *reinterpret_cast<ushort4*>(dst + row * sdst + rem) = o;
+  }
+}
+
+}  // namespace fa
+}  // namespace pd
+
+using namespace pd;
+
+extern "C" int pd_flash_fwd(int dt, const void* q, const void* k, const void* v, void* o, float* lse, int B, int Sq,
+                            int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, float scale, int causal,
+                            void* stream) {
+  if (dt != kBF16 || (D != 64 && D != 128) || Hq % Hk) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  const int nmb = (Sq + 127) / 128;
+  dim3 grid(nmb * Hq * B), block(256);
+#define PD_FA_FWD(DD, CC)                                                                                       \
+  fa::fwd_kernel<DD, CC><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, B, \
+                                                 Sq, Sk, Hq, Hk, sq, sk, sv, so, scale)
+  if (D == 128) { if (causal) PD_FA_FWD(128, true); else PD_FA_FWD(128, false); }
+  else { if (causal) PD_FA_FWD(64, true); else PD_FA_FWD(64, false); }
+#undef PD_FA_FWD
+  return (int)hipGetLastError();
+}
+
+// dq32 must be a zeroed [B, Sq, Hq, D] fp32 workspace; delta a [B, Hq, Sq] fp32 workspace;
+// dq/dk/dv are written contiguous ([B, S, H, D]); q/k/v/o/dout may be strided row views.
+extern "C" int pd_flash_bwd(int dt, const void* q, const void* k, const void* v, const void* o, const void* dout,
+                            const float* lse, float* delta, void* dq, void* dk, void* dv, float* dq32, int B, int Sq,
+                            int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, float scale, int causal,
+                            void* stream) {
+  if (dt != kBF16 || (D != 64 && D != 128) || Hq % Hk) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  const long rows = (long)B * Hq * Sq;
+  fa::bwd_delta_kernel<<<(int)((rows + 3) / 4), 256, 0, st>>>((const bf16*)o, (const bf16*)dout, delta, B, Sq, Hq, D,
+                                                               so);
+  const int nkb = (Sk + 127) / 128;
+  dim3 grid(nkb * Hk * B), block(256);
+#define PD_FA_BWD(DD, CC)                                                                                        \
+  fa::bwd_kernel<DD, CC><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
+                                                 lse, delta, dq32, (bf16*)dk, (bf16*)dv, B, Sq, Sk, Hq, Hk, sq, sk, \
+                                                 sv, so, scale)
+  if (D == 128) { if (causal) PD_FA_BWD(128, true); else PD_FA_BWD(128, false); }
+  else { if (causal) PD_FA_BWD(64, true); else PD_FA_BWD(64, false); }
+#undef PD_FA_BWD
+  long work = (long)B * Sq * Hq * (D / 4);
+  long g = (work + 255) / 256;
+  if (g > 4096) g = 4096;
+  fa::f32_to_bf16_strided<<<(int)g, 256, 0, st>>>(dq32, (bf16*)dq, (long)B * Sq, D, Hq, (long)Hq * D);
+  return (int)hipGetLastError();
+}

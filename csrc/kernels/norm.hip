@@ -1,0 +1,324 @@
+// RMSNorm / LayerNorm forward + backward for gfx950.
+//
+// Reference behaviour: phi/kernels/gpu/rms_norm_kernel.cu (RmsNormBlockSMemImpl, residual
+// fusion) and funcs/layer_norm_impl.cu.h.  Design here is MI355X-first:
+//  * one 64-lane wave per row (no __syncthreads in the row reduction), 4 rows per 256-thread
+//    block, row cached in VGPRs (MAXV x 16 B per lane) so x is read from HBM exactly once;
+//  * 16-byte vector loads/stores for bf16/f16/f32;
+//  * backward is a persistent grid-stride over rows (one 256-thread block per row); each block
+//    keeps its dW/dB partials in registers across rows and writes one fp32 partial row at the
+//    end; a second tiny kernel reduces the partials (no float atomics: deterministic and not
+//    bound by the chip-wide float-atomic rate).
+#include "common.h"
+
+namespace pd {
+
+constexpr int kNormBlock = 256;            // 4 waves
+constexpr int kRowsPerBlock = kNormBlock / 64;
+
+// ------------------------------------------------------------------------------------ fwd
+template <typename T, typename WT, int MAXV, bool LAYERNORM, bool HAS_RES, bool HAS_BIAS>
+__global__ __launch_bounds__(kNormBlock) void norm_fwd_kernel(
+    const T* __restrict__ x, const T* __restrict__ res, const WT* __restrict__ w, const WT* __restrict__ b,
+    T* __restrict__ y, T* __restrict__ res_out, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+    int M, int N, float eps) {
+  constexpr int V = 16 / sizeof(T);
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nv = N / V;
+  const long off = (long)row * N;
+  float buf[MAXV][V];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = lane + k * 64;
+    if (vi < nv) {
+      load_vec<T, V>(x + off + vi * V, buf[k]);
+      if constexpr (HAS_RES) {
+        float r[V];
+        load_vec<T, V>(res + off + vi * V, r);
+#pragma unroll
+        for (int j = 0; j < V; ++j) buf[k][j] += r[j];
+        store_vec<T, V>(res_out + off + vi * V, buf[k]);
+        // normalise the *rounded* h so forward and backward (which re-reads h) agree
+#pragma unroll
+        for (int j = 0; j < V; ++j) buf[k][j] = round_to<T>(buf[k][j]);
+      }
+#pragma unroll
+      for (int j = 0; j < V; ++j) s += LAYERNORM ? buf[k][j] : buf[k][j] * buf[k][j];
+    }
+  }
+  float mu = 0.f, rstd;
+  if constexpr (LAYERNORM) {
+    mu = wave_sum(s) / N;
+    float v2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int vi = lane + k * 64;
+      if (vi < nv) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) { float d = buf[k][j] - mu; v2 += d * d; }
+      }
+    }
+    rstd = rsqrtf(wave_sum(v2) / N + eps);
+  } else {
+    rstd = rsqrtf(wave_sum(s) / N + eps);
+  }
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = lane + k * 64;
+    if (vi < nv) {
+      constexpr int WV = 16 / sizeof(WT);
+      float wv[V], bv[V];
+      if constexpr (WV == V) {
+        load_vec<WT, V>(w + vi * V, wv);
+        if constexpr (HAS_BIAS) load_vec<WT, V>(b + vi * V, bv);
+      } else {  // fp32 weight with 16-bit activations: two 16 B loads
+        float t0[4], t1[4];
+        load_vec<WT, 4>(w + vi * V, t0); load_vec<WT, 4>(w + vi * V + 4, t1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { wv[j] = t0[j]; wv[j + 4] = t1[j]; }
+        if constexpr (HAS_BIAS) {
+          load_vec<WT, 4>(b + vi * V, t0); load_vec<WT, 4>(b + vi * V + 4, t1);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { bv[j] = t0[j]; bv[j + 4] = t1[j]; }
+        }
+      }
+      float o[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        o[j] = (buf[k][j] - mu) * rstd * wv[j];
+        if constexpr (HAS_BIAS) o[j] += bv[j];
+      }
+      store_vec<T, V>(y + off + vi * V, o);
+    }
+  }
+  if (lane == 0) {
+    rstd_out[row] = rstd;
+    if constexpr (LAYERNORM) mean_out[row] = mu;
+  }
+}
+
+// ------------------------------------------------------------------------------------ bwd
+// dx = rstd * (g - xhat*mean(g*xhat) [- mean(g) for LN]),  g = dy*w
+// One 256-thread block per row (persistent over rows): per-thread register footprint stays
+// at ~4 x MAXV x V floats, so N=4096 bf16 needs MAXV=2 (no spills at any N <= 16K).
+template <typename T, typename WT, int MAXV, bool LAYERNORM, bool HAS_DRES>
+__global__ __launch_bounds__(kNormBlock) void norm_bwd_kernel(
+    const T* __restrict__ dy, const T* __restrict__ x, const WT* __restrict__ w,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const T* __restrict__ dres,
+    T* __restrict__ dx, float* __restrict__ dw_part, float* __restrict__ db_part, int M, int N) {
+  constexpr int V = 16 / sizeof(T);
+  __shared__ float red[2 * kRowsPerBlock];
+  const int tid = threadIdx.x;
+  const int nv = N / V;
+  float wreg[MAXV][V];
+  float dwacc[MAXV][V];
+  float dbacc[MAXV][V];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = tid + k * kNormBlock;
+#pragma unroll
+    for (int j = 0; j < V; ++j) { dwacc[k][j] = 0.f; dbacc[k][j] = 0.f; wreg[k][j] = 0.f; }
+    if (vi < nv) {
+      constexpr int WV = 16 / sizeof(WT);
+      if constexpr (WV == V) load_vec<WT, V>(w + vi * V, wreg[k]);
+      else {
+        float t0[4], t1[4];
+        load_vec<WT, 4>(w + vi * V, t0); load_vec<WT, 4>(w + vi * V + 4, t1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { wreg[k][j] = t0[j]; wreg[k][j + 4] = t1[j]; }
+      }
+    }
+  }
+  for (int row = blockIdx.x; row < M; row += gridDim.x) {
+    const long off = (long)row * N;
+    const float r = rstd[row];
+    const float mu = LAYERNORM ? mean[row] : 0.f;
+    float xh[MAXV][V], g[MAXV][V];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int vi = tid + k * kNormBlock;
+      if (vi < nv) {
+        float dyv[V];
+        load_vec<T, V>(dy + off + vi * V, dyv);
+        load_vec<T, V>(x + off + vi * V, xh[k]);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          xh[k][j] = (xh[k][j] - mu) * r;
+          g[k][j] = dyv[j] * wreg[k][j];
+          s1 += g[k][j] * xh[k][j];
+          dwacc[k][j] += dyv[j] * xh[k][j];
+          if constexpr (LAYERNORM) { s2 += g[k][j]; dbacc[k][j] += dyv[j]; }
+        }
+      }
+    }
+    // block reduction of (s1, s2) in one LDS round trip
+    s1 = wave_sum(s1);
+    if constexpr (LAYERNORM) s2 = wave_sum(s2);
+    __syncthreads();
+    if ((tid & 63) == 0) { red[tid >> 6] = s1; red[kRowsPerBlock + (tid >> 6)] = s2; }
+    __syncthreads();
+    s1 = 0.f; s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < kRowsPerBlock; ++i) { s1 += red[i]; s2 += red[kRowsPerBlock + i]; }
+    s1 /= N; s2 /= N;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int vi = tid + k * kNormBlock;
+      if (vi < nv) {
+        float o[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] = r * (g[k][j] - xh[k][j] * s1 - (LAYERNORM ? s2 : 0.f));
+        if constexpr (HAS_DRES) {
+          float d2[V];
+          load_vec<T, V>(dres + off + vi * V, d2);
+#pragma unroll
+          for (int j = 0; j < V; ++j) o[j] += d2[j];
+        }
+        store_vec<T, V>(dx + off + vi * V, o);
+      }
+    }
+  }
+  // one fp32 partial row per block
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = tid + k * kNormBlock;
+    if (vi < nv) {
+      float* dst = dw_part + (long)blockIdx.x * N + vi * V;
+#pragma unroll
+      for (int j = 0; j < V; j += 4)
+        *reinterpret_cast<float4*>(dst + j) = make_float4(dwacc[k][j], dwacc[k][j + 1], dwacc[k][j + 2], dwacc[k][j + 3]);
+      if constexpr (LAYERNORM) {
+        float* dsb = db_part + (long)blockIdx.x * N + vi * V;
+#pragma unroll
+        for (int j = 0; j < V; j += 4)
+          *reinterpret_cast<float4*>(dsb + j) = make_float4(dbacc[k][j], dbacc[k][j + 1], dbacc[k][j + 2], dbacc[k][j + 3]);
+      }
+    }
+  }
+}
+
+// Reduce P partial rows [P, N] (fp32) into out [N] (type WT); column-parallel, 4 columns/thread.
+template <typename WT>
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, WT* __restrict__ out, int P, int N) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= N) return;
+  float4 acc = make_float4(0, 0, 0, 0);
+  for (int p = 0; p < P; ++p) {
+    float4 v = *reinterpret_cast<const float4*>(part + (long)p * N + c);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  Elt<WT>::st(out + c, acc.x); Elt<WT>::st(out + c + 1, acc.y);
+  Elt<WT>::st(out + c + 2, acc.z); Elt<WT>::st(out + c + 3, acc.w);
+}
+
+// ------------------------------------------------------------------------------------ host
+template <typename T, typename WT, bool LN>
+static void fwd_launch(const void* x, const void* res, const void* w, const void* b, void* y, void* res_out,
+                       float* mean, float* rstd, int M, int N, float eps, hipStream_t st) {
+  constexpr int V = 16 / sizeof(T);
+  const int nv = N / V;
+  const int maxv = (nv + 63) / 64;
+  dim3 grid(ceil_div(M, kRowsPerBlock)), block(kNormBlock);
+#define PD_NORM_FWD(MV)                                                                                      \
+  if (res) {                                                                                                 \
+    if (b) norm_fwd_kernel<T, WT, MV, LN, true, true><<<grid, block, 0, st>>>((const T*)x, (const T*)res,   \
+             (const WT*)w, (const WT*)b, (T*)y, (T*)res_out, mean, rstd, M, N, eps);                         \
+    else norm_fwd_kernel<T, WT, MV, LN, true, false><<<grid, block, 0, st>>>((const T*)x, (const T*)res,    \
+             (const WT*)w, (const WT*)b, (T*)y, (T*)res_out, mean, rstd, M, N, eps);                         \
+  } else {                                                                                                   \
+    if (b) norm_fwd_kernel<T, WT, MV, LN, false, true><<<grid, block, 0, st>>>((const T*)x, nullptr,        \
+             (const WT*)w, (const WT*)b, (T*)y, nullptr, mean, rstd, M, N, eps);                             \
+    else norm_fwd_kernel<T, WT, MV, LN, false, false><<<grid, block, 0, st>>>((const T*)x, nullptr,         \
+             (const WT*)w, (const WT*)b, (T*)y, nullptr, mean, rstd, M, N, eps);                             \
+  }
+  if (maxv <= 1) { PD_NORM_FWD(1) }
+  else if (maxv <= 2) { PD_NORM_FWD(2) }
+  else if (maxv <= 4) { PD_NORM_FWD(4) }
+  else if (maxv <= 8) { PD_NORM_FWD(8) }
+  else { PD_NORM_FWD(16) }
+#undef PD_NORM_FWD
+}
+
+template <typename T, typename WT, bool LN>
+static void bwd_launch(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
+                       const void* dres, void* dx, float* dw_part, float* db_part, void* dw, void* db,
+                       int M, int N, int nblocks, hipStream_t st) {
+  constexpr int V = 16 / sizeof(T);
+  const int nv = N / V;
+  const int maxv = (nv + kNormBlock - 1) / kNormBlock;
+  dim3 grid(nblocks), block(kNormBlock);
+#define PD_NORM_BWD(MV)                                                                                     \
+  if (dres) norm_bwd_kernel<T, WT, MV, LN, true><<<grid, block, 0, st>>>((const T*)dy, (const T*)x,        \
+        (const WT*)w, mean, rstd, (const T*)dres, (T*)dx, dw_part, db_part, M, N);                          \
+  else norm_bwd_kernel<T, WT, MV, LN, false><<<grid, block, 0, st>>>((const T*)dy, (const T*)x,            \
+        (const WT*)w, mean, rstd, nullptr, (T*)dx, dw_part, db_part, M, N);
+  if (maxv <= 1) { PD_NORM_BWD(1) }
+  else if (maxv <= 2) { PD_NORM_BWD(2) }
+  else if (maxv <= 4) { PD_NORM_BWD(4) }
+  else { PD_NORM_BWD(4) }
+#undef PD_NORM_BWD
+  const int P = nblocks;
+  dim3 g2(ceil_div(N / 4, 256));
+  colsum_kernel<WT><<<g2, 256, 0, st>>>(dw_part, (WT*)dw, P, N);
+  if (db_part) colsum_kernel<WT><<<g2, 256, 0, st>>>(db_part, (WT*)db, P, N);
+}
+
+}  // namespace pd
+
+// C ABI entry points (bound in bindings.cpp). dtype codes: 0 f32, 1 bf16, 2 f16.
+// Weight dtype may be the activation dtype or f32.
+extern "C" int pd_norm_fwd(int layernorm, int dt, int wdt, const void* x, const void* res, const void* w,
+                           const void* b, void* y, void* res_out, float* mean, float* rstd, int M, int N,
+                           float eps, void* stream) {
+  using namespace pd;
+  hipStream_t st = (hipStream_t)stream;
+  const int V = dt == kF32 ? 4 : 8;
+  if (N % V != 0 || N / V > 64 * 16) return -1;
+  if (wdt != dt && wdt != kF32) return -2;
+#define PD_FWD_CASE(T)                                                                                   \
+  if (wdt == kF32 && dt != kF32) {                                                                       \
+    if (layernorm) fwd_launch<T, float, true>(x, res, w, b, y, res_out, mean, rstd, M, N, eps, st);       \
+    else fwd_launch<T, float, false>(x, res, w, b, y, res_out, mean, rstd, M, N, eps, st);                \
+  } else {                                                                                               \
+    if (layernorm) fwd_launch<T, T, true>(x, res, w, b, y, res_out, mean, rstd, M, N, eps, st);           \
+    else fwd_launch<T, T, false>(x, res, w, b, y, res_out, mean, rstd, M, N, eps, st);                    \
+  }
+  if (dt == kF32) { using T = float; if (layernorm) fwd_launch<T, T, true>(x, res, w, b, y, res_out, mean, rstd, M, N, eps, st);
+                    else fwd_launch<T, T, false>(x, res, w, b, y, res_out, mean, rstd, M, N, eps, st); }
+  else if (dt == kBF16) { PD_FWD_CASE(bf16) }
+  else { PD_FWD_CASE(half16) }
+#undef PD_FWD_CASE
+  return (int)hipGetLastError();
+}
+
+// Number of blocks the backward uses; caller allocates partials of nblocks x N floats.
+extern "C" int pd_norm_bwd_blocks(int M) { return M < 512 ? M : 512; }
+
+extern "C" int pd_norm_bwd(int layernorm, int dt, int wdt, const void* dy, const void* x, const void* w,
+                           const float* mean, const float* rstd, const void* dres, void* dx, float* dw_part,
+                           float* db_part, void* dw, void* db, int M, int N, int nblocks, void* stream) {
+  using namespace pd;
+  hipStream_t st = (hipStream_t)stream;
+  const int V = dt == kF32 ? 4 : 8;
+  if (N % V != 0 || N / V > kNormBlock * 4 || N % 4 != 0) return -1;
+#define PD_BWD_CASE(T)                                                                                           \
+  if (wdt == kF32 && dt != kF32) {                                                                               \
+    if (layernorm) bwd_launch<T, float, true>(dy, x, w, mean, rstd, dres, dx, dw_part, db_part, dw, db, M, N, nblocks, st); \
+    else bwd_launch<T, float, false>(dy, x, w, mean, rstd, dres, dx, dw_part, nullptr, dw, nullptr, M, N, nblocks, st);   \
+  } else {                                                                                                       \
+    if (layernorm) bwd_launch<T, T, true>(dy, x, w, mean, rstd, dres, dx, dw_part, db_part, dw, db, M, N, nblocks, st);     \
+    else bwd_launch<T, T, false>(dy, x, w, mean, rstd, dres, dx, dw_part, nullptr, dw, nullptr, M, N, nblocks, st);       \
+  }
+  if (dt == kF32) {
+    using T = float;
+    if (layernorm) bwd_launch<T, T, true>(dy, x, w, mean, rstd, dres, dx, dw_part, db_part, dw, db, M, N, nblocks, st);
+    else bwd_launch<T, T, false>(dy, x, w, mean, rstd, dres, dx, dw_part, nullptr, dw, nullptr, M, N, nblocks, st);
+  } else if (dt == kBF16) { PD_BWD_CASE(bf16) }
+  else { PD_BWD_CASE(half16) }
+#undef PD_BWD_CASE
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,588 @@
+"""Process groups + collective communication API (paddle.distributed.communication.*).
+
+Reference: python/paddle/distributed/communication/ (all_reduce, all_gather, alltoall, broadcast,
+reduce, reduce_scatter, scatter, gather, send/recv, isend/irecv, batch_isend_irecv, barrier),
+collective.py:150 ``_new_process_group_impl`` and parallel.py:978 ``init_parallel_env``.
+
+MI355X design: one process per GPU, ``torch.distributed`` with backend ``"nccl"`` which IS RCCL on
+ROCm (xGMI peer links inside the node).  RCCL already runs its kernels on dedicated
+communicator streams with calc/comm stream events, so Paddle's ``use_calc_stream`` /
+``sync_op=False`` semantics map onto RCCL's async ``Work`` handles.  CPU runs (tests, the LeNet
+plumbing config) use gloo with the same code path.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..framework.tensor import Tensor
+
+_wrap = Tensor._wrap
+
+
+class ReduceOp:
+    SUM = 0
+    MAX = 1
+    MIN = 2
+    PROD = 3
+    AVG = 4
+
+
+_TORCH_OP = {
+    ReduceOp.SUM: dist.ReduceOp.SUM, ReduceOp.MAX: dist.ReduceOp.MAX, ReduceOp.MIN: dist.ReduceOp.MIN,
+    ReduceOp.PROD: dist.ReduceOp.PRODUCT,
+}
+
+
+def _top(op, backend):
+    if op == ReduceOp.AVG:
+        return dist.ReduceOp.AVG if backend == "nccl" else None
+    return _TORCH_OP[op]
+
+
+class Group:
+    """paddle.distributed.collective.Group."""
+
+    def __init__(self, rank_in_group, gid, ranks, pg=None, name=None):
+        self.rank = rank_in_group
+        self.id = gid
+        self.ranks = list(ranks)
+        self.nranks = len(ranks)
+        self.pg = pg
+        self.name = name or f"group_{gid}"
+
+    @property
+    def world_size(self):
+        return self.nranks
+
+    @property
+    def process_group(self):
+        return self.pg
+
+    @property
+    def backend(self):
+        if self.pg is None:
+            return "nccl" if torch.cuda.is_available() else "gloo"
+        return dist.get_backend(self.pg)
+
+    def is_member(self):
+        return self.rank >= 0
+
+    def get_group_rank(self, rank):
+        return self.ranks.index(rank) if rank in self.ranks else -1
+
+    def __repr__(self):
+        return f"Group(rank={self.rank}, nranks={self.nranks}, id={self.id}, ranks={self.ranks})"
+
+
+_default_group: Group | None = None
+_groups: dict[int, Group] = {}
+_next_gid = 1
+_initialized = False
+
+
+def _env_int(*names, default=None):
+    for n in names:
+        if n in os.environ:
+            return int(os.environ[n])
+    return default
+
+
+def _backend_for_device():
+    if os.environ.get("PADDLE_DISTRI_BACKEND"):
+        b = os.environ["PADDLE_DISTRI_BACKEND"].lower()
+        return "nccl" if b in ("nccl", "rccl", "xccl") else b
+    return "nccl" if torch.cuda.is_available() else "gloo"
+
+
+class ParallelEnv:
+    """paddle.distributed.ParallelEnv."""
+
+    @property
+    def rank(self):
+        return get_rank()
+
+    local_rank = rank
+
+    @property
+    def world_size(self):
+        return get_world_size()
+
+    nranks = world_size
+
+    @property
+    def device_id(self):
+        return _env_int("LOCAL_RANK", "PADDLE_LOCAL_RANK", default=0)
+
+    dev_id = device_id
+
+    @property
+    def current_endpoint(self):
+        return os.environ.get("PADDLE_CURRENT_ENDPOINT", "127.0.0.1:0")
+
+    @property
+    def trainer_endpoints(self):
+        return os.environ.get("PADDLE_TRAINER_ENDPOINTS", "").split(",")
+
+
+def is_initialized():
+    return _initialized and dist.is_initialized()
+
+
+def init_parallel_env(backend=None, timeout_s=None):
+    """Rendezvous (TCPStore on the master) + default RCCL/gloo process group (parallel.py:978)."""
+    global _default_group, _initialized
+    if _initialized:
+        return _default_group
+    rank = _env_int("RANK", "PADDLE_TRAINER_ID", default=0)
+    world = _env_int("WORLD_SIZE", "PADDLE_TRAINERS_NUM", default=1)
+    backend = backend or _backend_for_device()
+    if backend == "nccl" and torch.cuda.is_available():
+        local = _env_int("LOCAL_RANK", "PADDLE_LOCAL_RANK", default=rank % max(torch.cuda.device_count(), 1))
+        torch.cuda.set_device(local)
+        from ..framework.place import set_device
+
+        set_device(f"gpu:{local}")
+    if world > 1:
+        if "MASTER_ADDR" not in os.environ:
+            master = os.environ.get("PADDLE_MASTER", "127.0.0.1:29500")
+            host, port = master.rsplit(":", 1)
+            os.environ["MASTER_ADDR"] = host
+            os.environ["MASTER_PORT"] = port
+        os.environ.setdefault("MASTER_PORT", "29500")
+        if not dist.is_initialized():
+            tout = datetime.timedelta(seconds=timeout_s or int(os.environ.get("FLAGS_comm_timeout_s", "1800")))
+            kw = {}
+            if backend == "nccl" and torch.cuda.is_available():
+                kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+            dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=tout, **kw)
+    _default_group = Group(rank, 0, list(range(world)), dist.group.WORLD if dist.is_initialized() else None,
+                           name="_default_pg")
+    _groups[0] = _default_group
+    _initialized = True
+    from . import watchdog
+
+    watchdog.maybe_start()
+    return _default_group
+
+
+def get_rank(group=None):
+    if group is not None:
+        return group.rank
+    if dist.is_initialized():
+        return dist.get_rank()
+    return _env_int("RANK", "PADDLE_TRAINER_ID", default=0)
+
+
+def get_world_size(group=None):
+    if group is not None:
+        return group.nranks
+    if dist.is_initialized():
+        return dist.get_world_size()
+    return _env_int("WORLD_SIZE", "PADDLE_TRAINERS_NUM", default=1)
+
+
+def _get_default_group():
+    if _default_group is None:
+        init_parallel_env()
+    return _default_group
+
+
+def new_group(ranks=None, backend=None, timeout=None, nccl_comm_init_option=0):
+    """Create a sub-group; every process must call it (RCCL communicators are created lazily)."""
+    global _next_gid
+    g0 = _get_default_group()
+    if ranks is None:
+        ranks = list(range(get_world_size()))
+    ranks = sorted(int(r) for r in ranks)
+    gid = _next_gid
+    _next_gid += 1
+    if get_world_size() == 1 or ranks == list(range(get_world_size())):
+        pg = g0.pg  # the world communicator already exists; avoid a duplicate RCCL comm init
+    else:
+        kw = {}
+        if timeout is not None:
+            kw["timeout"] = timeout if isinstance(timeout, datetime.timedelta) else datetime.timedelta(seconds=timeout)
+        pg = dist.new_group(ranks=ranks, backend=backend if backend not in (None, "rccl") else None, **kw)
+    me = get_rank()
+    g = Group(ranks.index(me) if me in ranks else -1, gid, ranks, pg)
+    _groups[gid] = g
+    return g
+
+
+def get_group(gid=0):
+    return _groups.get(gid)
+
+
+def destroy_process_group(group=None):
+    global _initialized, _default_group
+    if group is None or group is _default_group:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        _groups.clear()
+        _default_group = None
+        _initialized = False
+    else:
+        dist.destroy_process_group(group.pg)
+        _groups.pop(group.id, None)
+
+
+def _pg(group):
+    g = group if group is not None else _get_default_group()
+    return g, g.pg
+
+
+class _Task:
+    """Async collective handle (reference ProcessGroup::Task: wait/is_completed/synchronize)."""
+
+    def __init__(self, work, post=None):
+        self._w = work
+        self._post = post
+
+    def wait(self, timeout=None):
+        if self._w is not None:
+            self._w.wait()
+        if self._post is not None:
+            self._post()
+            self._post = None
+        return True
+
+    def is_completed(self):
+        return self._w is None or self._w.is_completed()
+
+    def synchronize(self):
+        return self.wait()
+
+
+def _single(g):
+    return g.nranks == 1
+
+
+def _all_reduce_torch(t: torch.Tensor, op=ReduceOp.SUM, group=None, sync_op=True):
+    g, pg = _pg(group)
+    if _single(g):
+        return _Task(None)
+    top = _top(op, g.backend)
+    if top is None:  # AVG on gloo
+        w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg, async_op=not sync_op)
+        post = lambda: t.div_(g.nranks)  # noqa: E731
+        if sync_op:
+            post()
+            return _Task(None)
+        return _Task(w, post)
+    w = dist.all_reduce(t, op=top, group=pg, async_op=not sync_op)
+    return _Task(w)
+
+
+def all_reduce(tensor, op=ReduceOp.SUM, group=None, sync_op=True, use_calc_stream=False):
+    from . import watchdog
+
+    with watchdog.track("all_reduce", group, tensor):
+        return _all_reduce_torch(tensor._t, op, group, sync_op)
+
+
+def broadcast(tensor, src=0, group=None, sync_op=True):
+    g, pg = _pg(group)
+    if _single(g):
+        return _Task(None)
+    w = dist.broadcast(tensor._t, src=src, group=pg, async_op=not sync_op)
+    return _Task(w)
+
+
+def reduce(tensor, dst=0, op=ReduceOp.SUM, group=None, sync_op=True):
+    g, pg = _pg(group)
+    if _single(g):
+        return _Task(None)
+    top = _top(op, g.backend)
+    if top is None:
+        w = dist.reduce(tensor._t, dst=dst, op=dist.ReduceOp.SUM, group=pg, async_op=False)
+        if get_rank() == dst:
+            tensor._t.div_(g.nranks)
+        return _Task(None)
+    w = dist.reduce(tensor._t, dst=dst, op=top, group=pg, async_op=not sync_op)
+    return _Task(w)
+
+
+def all_gather(tensor_list, tensor, group=None, sync_op=True):
+    """Paddle semantics: fills ``tensor_list`` (a python list, cleared first) with nranks tensors."""
+    g, pg = _pg(group)
+    t = tensor._t
+    if _single(g):
+        tensor_list.clear()
+        tensor_list.append(_wrap(t.clone()))
+        return _Task(None)
+    out = torch.empty((g.nranks,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+    w = dist.all_gather_into_tensor(out, t.contiguous(), group=pg, async_op=not sync_op)
+
+    def post():
+        tensor_list.clear()
+        tensor_list.extend(_wrap(out[i]) for i in range(g.nranks))
+
+    if sync_op:
+        post()
+        return _Task(None)
+    return _Task(w, post)
+
+
+def all_gather_into_tensor(out_tensor, in_tensor, group=None, sync_op=True):
+    g, pg = _pg(group)
+    if _single(g):
+        out_tensor._t.copy_(in_tensor._t.reshape(out_tensor._t.shape))
+        return _Task(None)
+    w = dist.all_gather_into_tensor(out_tensor._t, in_tensor._t.contiguous(), group=pg, async_op=not sync_op)
+    return _Task(w)
+
+
+def all_gather_object(object_list, obj, group=None):
+    g, pg = _pg(group)
+    if _single(g):
+        object_list.clear()
+        object_list.append(obj)
+        return
+    out = [None] * g.nranks
+    dist.all_gather_object(out, obj, group=pg)
+    object_list.clear()
+    object_list.extend(out)
+
+
+def reduce_scatter(tensor, tensor_list, op=ReduceOp.SUM, group=None, sync_op=True):
+    g, pg = _pg(group)
+    if _single(g):
+        tensor._t.copy_(tensor_list[0]._t)
+        return _Task(None)
+    inp = torch.cat([x._t.reshape(-1) for x in tensor_list]) if isinstance(tensor_list, (list, tuple)) else tensor_list._t
+    top = _top(op, g.backend)
+    avg = top is None
+    w = dist.reduce_scatter_tensor(tensor._t, inp.contiguous(), op=dist.ReduceOp.SUM if avg else top, group=pg,
+                                   async_op=not sync_op)
+    if avg:
+        if sync_op:
+            tensor._t.div_(g.nranks)
+            return _Task(None)
+        return _Task(w, lambda: tensor._t.div_(g.nranks))
+    return _Task(w)
+
+
+def _reduce_scatter_base(output, input, op=ReduceOp.SUM, group=None, sync_op=True):
+    g, pg = _pg(group)
+    if _single(g):
+        output._t.copy_(input._t.reshape(output._t.shape))
+        return _Task(None)
+    w = dist.reduce_scatter_tensor(output._t, input._t.contiguous(), op=_top(op, g.backend) or dist.ReduceOp.SUM,
+                                   group=pg, async_op=not sync_op)
+    return _Task(w)
+
+
+def alltoall(out_tensor_list, in_tensor_list, group=None, sync_op=True):
+    g, pg = _pg(group)
+    ins = [x._t.contiguous() for x in in_tensor_list]
+    if _single(g):
+        out_tensor_list.clear()
+        out_tensor_list.extend(_wrap(x.clone()) for x in ins)
+        return _Task(None)
+    outs = [torch.empty_like(x) for x in ins]
+    w = dist.all_to_all(outs, ins, group=pg, async_op=not sync_op)
+
+    def post():
+        out_tensor_list.clear()
+        out_tensor_list.extend(_wrap(x) for x in outs)
+
+    if sync_op:
+        post()
+        return _Task(None)
+    return _Task(w, post)
+
+
+def alltoall_single(out_tensor, in_tensor, in_split_sizes=None, out_split_sizes=None, group=None, sync_op=True):
+    g, pg = _pg(group)
+    if _single(g):
+        out_tensor._t.copy_(in_tensor._t)
+        return _Task(None)
+    w = dist.all_to_all_single(out_tensor._t, in_tensor._t.contiguous(), out_split_sizes, in_split_sizes, group=pg,
+                               async_op=not sync_op)
+    return _Task(w)
+
+
+def scatter(tensor, tensor_list=None, src=0, group=None, sync_op=True):
+    g, pg = _pg(group)
+    if _single(g):
+        tensor._t.copy_(tensor_list[0]._t)
+        return _Task(None)
+    sl = [x._t.contiguous() for x in tensor_list] if (tensor_list is not None and get_rank() == src) else None
+    w = dist.scatter(tensor._t, sl, src=src, group=pg, async_op=not sync_op)
+    return _Task(w)
+
+
+def scatter_object_list(out_object_list, in_object_list=None, src=0, group=None):
+    g, pg = _pg(group)
+    if _single(g):
+        out_object_list[:] = [in_object_list[0]]
+        return
+    out = [None]
+    dist.scatter_object_list(out, in_object_list if get_rank() == src else None, src=src, group=pg)
+    out_object_list[:] = out
+
+
+def gather(tensor, gather_list=None, dst=0, group=None, sync_op=True):
+    g, pg = _pg(group)
+    if _single(g):
+        if gather_list is not None:
+            gather_list.clear()
+            gather_list.append(_wrap(tensor._t.clone()))
+        return _Task(None)
+    t = tensor._t.contiguous()
+    gl = [torch.empty_like(t) for _ in range(g.nranks)] if get_rank() == dst else None
+    if g.backend == "nccl":
+        out = torch.empty((g.nranks,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=pg)
+        gl = [out[i] for i in range(g.nranks)] if get_rank() == dst else None
+    else:
+        dist.gather(t, gl, dst=dst, group=pg)
+    if gather_list is not None and gl is not None:
+        gather_list.clear()
+        gather_list.extend(_wrap(x) for x in gl)
+    return _Task(None)
+
+
+def broadcast_object_list(object_list, src=0, group=None):
+    g, pg = _pg(group)
+    if _single(g):
+        return
+    dist.broadcast_object_list(object_list, src=src, group=pg)
+
+
+def send(tensor, dst=0, group=None, sync_op=True):
+    g, pg = _pg(group)
+    gdst = g.ranks[dst] if group is not None else dst
+    w = dist.isend(tensor._t.contiguous(), gdst, group=pg)
+    if sync_op:
+        w.wait()
+        return _Task(None)
+    return _Task(w)
+
+
+def recv(tensor, src=0, group=None, sync_op=True):
+    g, pg = _pg(group)
+    gsrc = g.ranks[src] if group is not None else src
+    w = dist.irecv(tensor._t, gsrc, group=pg)
+    if sync_op:
+        w.wait()
+        return _Task(None)
+    return _Task(w)
+
+
+def isend(tensor, dst, group=None):
+    return send(tensor, dst, group, sync_op=False)
+
+
+def irecv(tensor, src=None, group=None):
+    return recv(tensor, src, group, sync_op=False)
+
+
+class P2POp:
+    def __init__(self, op, tensor, peer, group=None):
+        self.op, self.tensor, self.peer, self.group = op, tensor, peer, group
+
+
+def batch_isend_irecv(p2p_op_list):
+    """Coalesced p2p (reference: ProcessGroupNCCL GroupStart/End, process_group_nccl.cc:166-183)."""
+    ops = []
+    for p in p2p_op_list:
+        g, pg = _pg(p.group)
+        peer = g.ranks[p.peer] if p.group is not None else p.peer
+        fn = dist.isend if p.op in (isend, dist.isend, send) else dist.irecv
+        ops.append(dist.P2POp(fn, p.tensor._t, peer, group=pg))
+    if not ops:
+        return []
+    works = dist.batch_isend_irecv(ops)
+    return [_Task(w) for w in works]
+
+
+def barrier(group=None):
+    g, pg = _pg(group)
+    if _single(g):
+        return
+    if g.backend == "nccl":
+        t = torch.zeros(1, device=torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(t, group=pg)
+        torch.cuda.synchronize()
+    else:
+        dist.barrier(group=pg)
+
+
+def wait(tensor, group=None, use_calc_stream=True):
+    if torch.cuda.is_available():
+        torch.cuda.current_stream().synchronize() if not use_calc_stream else None
+
+
+def is_available():
+    return dist.is_available()
+
+
+def get_backend(group=None):
+    g, pg = _pg(group)
+    return "NCCL" if g.backend == "nccl" else g.backend.upper()
+
+
+class stream:
+    """paddle.distributed.stream.* — same collectives with ``use_calc_stream`` (RCCL orders them on its
+    own stream; ``use_calc_stream=True`` makes the call synchronous w.r.t. the compute stream)."""
+
+    @staticmethod
+    def all_reduce(tensor, op=ReduceOp.SUM, group=None, sync_op=True, use_calc_stream=False):
+        return all_reduce(tensor, op, group, sync_op or use_calc_stream)
+
+    @staticmethod
+    def all_gather(tensor_or_tensor_list, tensor, group=None, sync_op=True, use_calc_stream=False):
+        if isinstance(tensor_or_tensor_list, Tensor):
+            return all_gather_into_tensor(tensor_or_tensor_list, tensor, group, sync_op or use_calc_stream)
+        return all_gather(tensor_or_tensor_list, tensor, group, sync_op or use_calc_stream)
+
+    @staticmethod
+    def reduce_scatter(tensor, tensor_or_tensor_list, op=ReduceOp.SUM, group=None, sync_op=True,
+                       use_calc_stream=False):
+        if isinstance(tensor_or_tensor_list, Tensor):
+            return _reduce_scatter_base(tensor, tensor_or_tensor_list, op, group, sync_op or use_calc_stream)
+        return reduce_scatter(tensor, tensor_or_tensor_list, op, group, sync_op or use_calc_stream)
+
+    @staticmethod
+    def broadcast(tensor, src=0, group=None, sync_op=True, use_calc_stream=False):
+        return broadcast(tensor, src, group, sync_op or use_calc_stream)
+
+    @staticmethod
+    def reduce(tensor, dst=0, op=ReduceOp.SUM, group=None, sync_op=True, use_calc_stream=False):
+        return reduce(tensor, dst, op, group, sync_op or use_calc_stream)
+
+    @staticmethod
+    def alltoall(out_tensor_or_tensor_list, in_tensor_or_tensor_list, group=None, sync_op=True,
+                 use_calc_stream=False):
+        if isinstance(out_tensor_or_tensor_list, Tensor):
+            return alltoall_single(out_tensor_or_tensor_list, in_tensor_or_tensor_list, group=group,
+                                   sync_op=sync_op or use_calc_stream)
+        return alltoall(out_tensor_or_tensor_list, in_tensor_or_tensor_list, group, sync_op or use_calc_stream)
+
+    @staticmethod
+    def alltoall_single(out_tensor, in_tensor, out_split_sizes=None, in_split_sizes=None, group=None, sync_op=True,
+                        use_calc_stream=False):
+        return alltoall_single(out_tensor, in_tensor, in_split_sizes, out_split_sizes, group,
+                               sync_op or use_calc_stream)
+
+    @staticmethod
+    def send(tensor, dst=0, group=None, sync_op=True, use_calc_stream=False):
+        return send(tensor, dst, group, sync_op or use_calc_stream)
+
+    @staticmethod
+    def recv(tensor, src=0, group=None, sync_op=True, use_calc_stream=False):
+        return recv(tensor, src, group, sync_op or use_calc_stream)
+
+    @staticmethod
+    def scatter(tensor, tensor_or_tensor_list=None, src=0, group=None, sync_op=True, use_calc_stream=False):
+        return scatter(tensor, tensor_or_tensor_list, src, group, sync_op or use_calc_stream)
+
+    @staticmethod
+    def gather(tensor, gather_list=None, dst=0, group=None, sync_op=True, use_calc_stream=False):
+        return gather(tensor, gather_list, dst, group, sync_op or use_calc_stream)

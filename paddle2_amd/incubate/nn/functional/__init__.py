@@ -1,0 +1,284 @@
+"""paddle.incubate.nn.functional fused ops (reference: python/paddle/incubate/nn/functional/).
+
+Each maps onto a hand-written CDNA4 kernel in :mod:`paddle2_amd.ops` where the hot path needs one
+(rms_norm, layer_norm, rotary embedding, swiglu, flash attention); the GEMM parts use hipBLASLt.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ....framework.tensor import Tensor
+from ....ops import torch_ops as T
+
+_wrap = Tensor._wrap
+
+
+def _u(x):
+    return None if x is None else x._t
+
+
+def fused_rms_norm(x, norm_weight, norm_bias, epsilon, begin_norm_axis, bias=None, residual=None, quant_scale=-1,
+                   quant_round_type=0, quant_max_bound=0, quant_min_bound=0):
+    """Returns (out, residual_out) like ``_C_ops.rms_norm`` in dygraph (fused_rms_norm.py:106)."""
+    t = x._t
+    if bias is not None:
+        t = t + bias._t
+    lead = list(t.shape[:begin_norm_axis])
+    n = int(torch.tensor(t.shape[begin_norm_axis:]).prod())
+    t2 = t.reshape(lead + [n])
+    res = None if residual is None else residual._t.reshape(lead + [n])
+    w = norm_weight._t.reshape(-1)
+    if res is not None:
+        y, h = T.rms_norm(t2, w, epsilon, res)
+        h = h.reshape(t.shape)
+    else:
+        y, h = T.rms_norm(t2, w, epsilon), None
+    if norm_bias is not None:
+        y = y + norm_bias._t.reshape(-1)
+    y = y.reshape(t.shape)
+    if quant_scale > 0:
+        q = torch.clamp(torch.round(y.float() * quant_scale * quant_max_bound), quant_min_bound, quant_max_bound)
+        y = q.to(torch.int8)
+    return _wrap(y), (None if h is None else _wrap(h))
+
+
+def fused_layer_norm(x, norm_weight, norm_bias, epsilon, residual_alpha=1.0, begin_norm_axis=1, bias=None,
+                     residual=None, quant_scale=-1, quant_round_type=0, quant_max_bound=0, quant_min_bound=0):
+    t = x._t
+    if bias is not None:
+        t = t + bias._t
+    if residual is not None:
+        t = t + residual_alpha * residual._t
+    lead = list(t.shape[:begin_norm_axis])
+    n = int(torch.tensor(t.shape[begin_norm_axis:]).prod())
+    y = T.layer_norm(t.reshape(lead + [n]), _u(norm_weight), _u(norm_bias), epsilon).reshape(t.shape)
+    return _wrap(y), (_wrap(t) if residual is not None else None)
+
+
+def _rope_one(x, sin, cos, position_ids, use_neox_rotary_style, time_major, rotary_emb_base):
+    if x is None:
+        return None
+    t = x._t
+    D = t.shape[-1]
+    style = 1 if use_neox_rotary_style else 0
+    if sin is None or cos is None:
+        S = t.shape[0] if time_major else t.shape[1]
+        c, s = T.rope_tables(S, D, rotary_emb_base, interleaved=bool(use_neox_rotary_style), device=t.device)
+    else:
+        c, s = cos._t.reshape(-1, D), sin._t.reshape(-1, D)
+    pos = None if position_ids is None else position_ids._t
+    return _wrap(T.rope(t, c, s, pos, style, time_major))
+
+
+def fused_rotary_position_embedding(q, k=None, v=None, sin=None, cos=None, position_ids=None,
+                                    use_neox_rotary_style=True, time_major=False, rotary_emb_base=10000.0):
+    """Rotary embedding on q/k/v ([b, s, h, d] or time-major). Returns a 3-tuple like the reference."""
+    args = (sin, cos, position_ids, use_neox_rotary_style, time_major, rotary_emb_base)
+    return _rope_one(q, *args), _rope_one(k, *args), _rope_one(v, *args)
+
+
+def swiglu(x, y=None, name=None):
+    return _wrap(T.swiglu(x._t, None if y is None else y._t))
+
+
+def fused_matmul_bias(x, y, bias=None, transpose_x=False, transpose_y=False, name=None):
+    a = x._t.transpose(-1, -2) if transpose_x else x._t
+    b = y._t.transpose(-1, -2) if transpose_y else y._t
+    if bias is not None and a.dim() == 2:
+        return _wrap(torch.addmm(bias._t, a, b))
+    out = torch.matmul(a, b)
+    return _wrap(out if bias is None else out + bias._t)
+
+
+def fused_linear(x, weight, bias=None, transpose_weight=False, name=None):
+    return fused_matmul_bias(x, weight, bias, False, transpose_weight)
+
+
+def fused_linear_activation(x, y, bias, trans_x=False, trans_y=False, activation=None):
+    out = fused_matmul_bias(x, y, bias, trans_x, trans_y)._t
+    if activation == "gelu":
+        out = torch.nn.functional.gelu(out)
+    elif activation == "relu":
+        out = torch.relu(out)
+    return _wrap(out)
+
+
+def fused_dropout_add(x, y, p=0.5, training=True, mode="upscale_in_train", name=None):
+    t = x._t
+    if training and p > 0:
+        t = torch.nn.functional.dropout(t, p, True) if mode == "upscale_in_train" else t * torch.bernoulli(
+            torch.full_like(t, 1 - p))
+    elif mode == "downscale_in_infer" and not training:
+        t = t * (1 - p)
+    return _wrap(t + y._t)
+
+
+def fused_bias_act(x, bias=None, dequant_scales=None, shift=None, smooth=None, act_method="gelu",
+                   compute_dtype="default", quant_scale=-1, quant_round_type=0, quant_max_bound=0,
+                   quant_min_bound=0):
+    t = x._t if bias is None else x._t + bias._t
+    if act_method in ("swiglu", "geglu"):
+        a, b = t.chunk(2, -1)
+        act = torch.nn.functional.silu(a.float()) if act_method == "swiglu" else torch.nn.functional.gelu(a.float())
+        return _wrap((act * b.float()).to(t.dtype))
+    fn = {"gelu": torch.nn.functional.gelu, "relu": torch.relu, "silu": torch.nn.functional.silu,
+          "swish": torch.nn.functional.silu, "identity": lambda v: v}[act_method]
+    return _wrap(fn(t))
+
+
+def fused_feedforward(x, linear1_weight, linear2_weight, linear1_bias=None, linear2_bias=None, ln1_scale=None,
+                      ln1_bias=None, ln2_scale=None, ln2_bias=None, dropout1_rate=0.5, dropout2_rate=0.5,
+                      activation="relu", ln1_epsilon=1e-5, ln2_epsilon=1e-5, pre_layer_norm=False, training=True,
+                      mode="upscale_in_train", ring_id=-1, add_residual=True, name=None):
+    t = x._t
+    res = t
+    if pre_layer_norm:
+        t = T.layer_norm(t, _u(ln1_scale), _u(ln1_bias), ln1_epsilon)
+    h = torch.matmul(t, linear1_weight._t)
+    if linear1_bias is not None:
+        h = h + linear1_bias._t
+    h = getattr(torch.nn.functional, activation)(h)
+    if training and dropout1_rate:
+        h = torch.nn.functional.dropout(h, dropout1_rate)
+    o = torch.matmul(h, linear2_weight._t)
+    if linear2_bias is not None:
+        o = o + linear2_bias._t
+    if training and dropout2_rate:
+        o = torch.nn.functional.dropout(o, dropout2_rate)
+    if add_residual:
+        o = o + res
+    if not pre_layer_norm:
+        o = T.layer_norm(o, _u(ln2_scale), _u(ln2_bias), ln2_epsilon)
+    return _wrap(o)
+
+
+def fused_multi_head_attention(x, qkv_weight, linear_weight, pre_layer_norm=False, pre_ln_scale=None,
+                               pre_ln_bias=None, ln_scale=None, ln_bias=None, pre_ln_epsilon=1e-05, qkv_bias=None,
+                               linear_bias=None, cache_kv=None, attn_mask=None, dropout_rate=0.5,
+                               attn_dropout_rate=0.5, ln_epsilon=1e-05, training=True, mode="upscale_in_train",
+                               ring_id=-1, add_residual=True, num_heads=-1, transpose_qkv_wb=False, name=None):
+    t = x._t
+    b, s, e = t.shape
+    res = t
+    if pre_layer_norm:
+        t = T.layer_norm(t, _u(pre_ln_scale), _u(pre_ln_bias), pre_ln_epsilon)
+    w = qkv_weight._t  # [3, nh, hd, e]
+    nh, hd = w.shape[1], w.shape[2]
+    qkv = torch.einsum("bse,tnde->bstnd", t, w)
+    if qkv_bias is not None:
+        qkv = qkv + qkv_bias._t
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    if attn_mask is None and q.dtype == torch.bfloat16:
+        o, _ = T.flash_attention(q.contiguous(), k.contiguous(), v.contiguous(), False)
+    else:
+        sc = torch.einsum("bqnd,bknd->bnqk", q.float(), k.float()) / math.sqrt(hd)
+        if attn_mask is not None:
+            sc = sc + attn_mask._t.float()
+        o = torch.einsum("bnqk,bknd->bqnd", torch.softmax(sc, -1), v.float()).to(t.dtype)
+    o = torch.matmul(o.reshape(b, s, nh * hd), linear_weight._t)
+    if linear_bias is not None:
+        o = o + linear_bias._t
+    if add_residual:
+        o = o + res
+    if not pre_layer_norm:
+        o = T.layer_norm(o, _u(ln_scale), _u(ln_bias), ln_epsilon)
+    return _wrap(o)
+
+
+def variable_length_memory_efficient_attention(query, key, value, seq_lens, kv_seq_lens, mask=None, scale=None,
+                                               causal=False, pre_cache_length=0):
+    """[b, h, s, d] layout with per-batch lengths (reference uses CUTLASS; here masked flash path)."""
+    q, k, v = query._t, key._t, value._t
+    b, h, s, d = q.shape
+    scale = scale or 1.0 / math.sqrt(d)
+    out = torch.zeros_like(q)
+    sl = seq_lens._t.reshape(-1).tolist()
+    kl = kv_seq_lens._t.reshape(-1).tolist()
+    for i in range(b):
+        qs = q[i:i + 1, :, : sl[i]].transpose(1, 2)
+        ks = k[i:i + 1, :, : kl[i]].transpose(1, 2)
+        vs = v[i:i + 1, :, : kl[i]].transpose(1, 2)
+        if mask is None:
+            o, _ = T.flash_attention(qs.contiguous(), ks.contiguous(), vs.contiguous(), causal, scale)
+        else:
+            sc = torch.einsum("bqhd,bkhd->bhqk", qs.float(), ks.float()) * scale + mask._t[i:i + 1, :, : sl[i], : kl[i]].float()
+            o = torch.einsum("bhqk,bkhd->bqhd", torch.softmax(sc, -1), vs.float()).to(q.dtype)
+        out[i, :, : sl[i]] = o[0].transpose(0, 1)
+    return _wrap(out)
+
+
+def masked_multihead_attention(x, cache_kv=None, bias=None, src_mask=None, cum_offsets=None, sequence_lengths=None,
+                               rotary_tensor=None, beam_cache_offset=None, qkv_out_scale=None, out_shift=None,
+                               out_smooth=None, seq_len=1, rotary_emb_dims=0, use_neox_rotary_style=False,
+                               compute_dtype="default", out_scale=-1, quant_round_type=1, quant_max_bound=127.0,
+                               quant_min_bound=-127.0):
+    """Single-token decode attention over a [2, b, nh, max_s, hd] KV cache (masked_multihead_attention_kernel.cu).
+
+    x: [b, 3*nh*hd] for the new token; writes k/v at position ``sequence_lengths`` and attends over
+    the valid prefix. Returns (out [b, nh*hd], cache_kv).
+    """
+    t = x._t if bias is None else x._t + bias._t
+    ck = cache_kv._t
+    _, b, nh, max_s, hd = ck.shape
+    qkv = t.reshape(b, 3, nh, hd)
+    q, k, v = qkv[:, 0], qkv[:, 1], qkv[:, 2]
+    lens = sequence_lengths._t.reshape(-1).long() if sequence_lengths is not None else torch.zeros(
+        b, dtype=torch.long, device=t.device)
+    bi = torch.arange(b, device=t.device)
+    ck[0, bi, :, lens] = k.to(ck.dtype)
+    ck[1, bi, :, lens] = v.to(ck.dtype)
+    keys = ck[0].float()
+    vals = ck[1].float()
+    sc = torch.einsum("bnd,bnsd->bns", q.float(), keys) / math.sqrt(hd)
+    valid = torch.arange(max_s, device=t.device)[None, :] <= lens[:, None]
+    sc = sc.masked_fill(~valid[:, None, :], float("-inf"))
+    if src_mask is not None:
+        sc = sc + src_mask._t.reshape(b, 1, -1)[..., :max_s].float()
+    p = torch.softmax(sc, -1)
+    o = torch.einsum("bns,bnsd->bnd", p, vals).to(t.dtype).reshape(b, nh * hd)
+    return _wrap(o), cache_kv
+
+
+def block_multihead_attention(*args, **kwargs):
+    from ....serving import block_multihead_attention as _bma
+
+    return _bma(*args, **kwargs)
+
+
+def fused_multi_transformer(*args, **kwargs):
+    from ....serving import fused_multi_transformer as _fmt
+
+    return _fmt(*args, **kwargs)
+
+
+def fused_moe(x, gate_weight, ffn1_weight, ffn1_scale=None, ffn1_bias=None, ffn2_weight=None, ffn2_scale=None,
+              ffn2_bias=None, quant_method="None", moe_topk=2, group_moe=False, norm_topk_prob=True):
+    """Top-k gated MoE FFN (reference: fusion/cutlass/fused_moe_kernel.cu) as grouped GEMMs."""
+    t = x._t
+    shp = t.shape
+    t2 = t.reshape(-1, shp[-1])
+    logits = t2.float() @ gate_weight._t.float()
+    probs = torch.softmax(logits, -1)
+    w, idx = torch.topk(probs, moe_topk, -1)
+    if norm_topk_prob:
+        w = w / w.sum(-1, keepdim=True)
+    out = torch.zeros_like(t2, dtype=torch.float32)
+    E = ffn1_weight._t.shape[0]
+    for e in range(E):
+        sel = (idx == e)
+        rows = sel.any(-1).nonzero().squeeze(-1)
+        if rows.numel() == 0:
+            continue
+        h = t2[rows] @ ffn1_weight._t[e]
+        if ffn1_bias is not None:
+            h = h + ffn1_bias._t[e]
+        a, g = h.chunk(2, -1)
+        h = torch.nn.functional.silu(a) * g
+        o = h @ ffn2_weight._t[e]
+        if ffn2_bias is not None:
+            o = o + ffn2_bias._t[e]
+        we = (w * sel).sum(-1)[rows]
+        out.index_add_(0, rows, o.float() * we[:, None])
+    return _wrap(out.to(t.dtype).reshape(shp))

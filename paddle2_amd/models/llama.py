@@ -1,0 +1,289 @@
+"""Llama-2 for causal LM pretraining, built on paddle2_amd's Paddle-style API.
+
+Structure follows the reference's Llama test/auto-parallel models
+(test/auto_parallel/hybrid_strategy/semi_auto_parallel_llama_model.py:55-640: RMSNorm ->
+q/k/v proj -> RoPE -> flash_attn -> o_proj -> RMSNorm -> gate/up -> swiglu -> down) with the
+fused variants PaddleNLP uses (``fuse_attention_qkv``, ``fuse_attention_ffn``, fused residual
+RMSNorm).  MI355X mapping of every op:
+
+  RMSNorm (+ residual add)   -> csrc/kernels/norm.hip        (wave-per-row, fused residual)
+  QKV / gate-up / o / down   -> hipBLASLt GEMM (plain library GEMMs, bf16 MFMA)
+  RoPE                       -> csrc/kernels/elementwise.hip (rotate-half, fp32 cos/sin table)
+  causal attention (GQA)     -> csrc/kernels/flash_attn.hip  (MFMA 32x32x16 fwd + bwd)
+  SwiGLU                     -> csrc/kernels/elementwise.hip (packed [gate|up] input)
+  embedding / softmax-CE     -> csrc/kernels/loss_embed.hip  (one-pass online LSE)
+
+Tensor parallelism: when ``config.tensor_parallel_degree > 1`` the projections become
+Column/RowParallelLinear and the embedding / LM head vocab-parallel (paddle2_amd.distributed.fleet).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+import torch
+
+from .. import nn
+from ..framework.tensor import Tensor
+from ..nn import functional as F
+from ..nn import initializer as I
+from ..ops import torch_ops as T
+
+_wrap = Tensor._wrap
+
+
+@dataclasses.dataclass
+class LlamaConfig:
+    vocab_size: int = 32000
+    hidden_size: int = 4096
+    intermediate_size: int = 11008
+    num_hidden_layers: int = 32
+    num_attention_heads: int = 32
+    num_key_value_heads: int = 32
+    max_position_embeddings: int = 4096
+    rms_norm_eps: float = 1e-5
+    rope_theta: float = 10000.0
+    initializer_range: float = 0.02
+    tie_word_embeddings: bool = False
+    fuse_attention_qkv: bool = True
+    fuse_attention_ffn: bool = True
+    use_flash_attention: bool = True
+    dtype: str = "bfloat16"
+    tensor_parallel_degree: int = 1
+    sequence_parallel: bool = False
+    recompute: bool = False
+    pad_token_id: int = 0
+    ignore_index: int = -100
+
+    @property
+    def head_dim(self):
+        return self.hidden_size // self.num_attention_heads
+
+    @classmethod
+    def llama2_7b(cls, **kw):
+        return cls(**kw)
+
+    @classmethod
+    def llama2_13b(cls, **kw):
+        d = dict(hidden_size=5120, intermediate_size=13824, num_hidden_layers=40, num_attention_heads=40,
+                 num_key_value_heads=40)
+        d.update(kw)
+        return cls(**d)
+
+    @classmethod
+    def tiny(cls, **kw):
+        d = dict(vocab_size=512, hidden_size=256, intermediate_size=688, num_hidden_layers=2, num_attention_heads=2,
+                 num_key_value_heads=2, max_position_embeddings=256)
+        d.update(kw)
+        return cls(**d)
+
+
+def _linear(cfg, fin, fout, kind):
+    """kind: 'col' (output-sharded) | 'row' (input-sharded) | None."""
+    init = I.Normal(0.0, cfg.initializer_range)
+    attr = nn.ParamAttr(initializer=init)
+    if cfg.tensor_parallel_degree > 1 and kind is not None:
+        from ..distributed.fleet.layers.mpu import ColumnParallelLinear, RowParallelLinear
+
+        if kind == "col":
+            return ColumnParallelLinear(fin, fout, weight_attr=attr, has_bias=False, gather_output=False)
+        return RowParallelLinear(fin, fout, weight_attr=attr, has_bias=False, input_is_parallel=True)
+    return nn.Linear(fin, fout, weight_attr=attr, bias_attr=False)
+
+
+class LlamaRotaryEmbedding:
+    """cos/sin tables (fp32, [max_pos, head_dim], rotate-half layout) cached per device."""
+
+    def __init__(self, dim, max_pos, base):
+        self.dim, self.max_pos, self.base = dim, max_pos, base
+        self._cache = {}
+
+    def tables(self, device, seq_len):
+        n = max(seq_len, self.max_pos)
+        key = (device, n)
+        if key not in self._cache:
+            self._cache[key] = T.rope_tables(n, self.dim, self.base, interleaved=False, device=device)
+        return self._cache[key]
+
+
+class LlamaRMSNorm(nn.Layer):
+    def __init__(self, config):
+        super().__init__()
+        self.eps = config.rms_norm_eps
+        self.weight = self.create_parameter([config.hidden_size], dtype=config.dtype,
+                                            default_initializer=I.Constant(1.0))
+
+    def forward(self, x, residual=None):
+        if residual is None:
+            return _wrap(T.rms_norm(x._t, self.weight._t, self.eps))
+        y, h = T.rms_norm(x._t, self.weight._t, self.eps, residual._t)
+        return _wrap(y), _wrap(h)
+
+
+class LlamaAttention(nn.Layer):
+    def __init__(self, config, rope):
+        super().__init__()
+        self.config = config
+        tp = config.tensor_parallel_degree
+        self.num_heads = config.num_attention_heads // tp
+        self.num_kv = config.num_key_value_heads // tp
+        self.head_dim = config.head_dim
+        h = config.hidden_size
+        self.rope = rope
+        if config.fuse_attention_qkv:
+            self.qkv_proj = _linear(config, h, h + 2 * config.num_key_value_heads * self.head_dim, "col")
+        else:
+            self.q_proj = _linear(config, h, h, "col")
+            self.k_proj = _linear(config, h, config.num_key_value_heads * self.head_dim, "col")
+            self.v_proj = _linear(config, h, config.num_key_value_heads * self.head_dim, "col")
+        self.o_proj = _linear(config, h, h, "row")
+
+    def forward(self, x, position_ids=None):
+        b, s = x.shape[0], x.shape[1]
+        nh, nkv, d = self.num_heads, self.num_kv, self.head_dim
+        if self.config.fuse_attention_qkv:
+            qkv = self.qkv_proj(x)._t.view(b, s, nh + 2 * nkv, d)
+            q, k, v = qkv[:, :, :nh], qkv[:, :, nh:nh + nkv], qkv[:, :, nh + nkv:]
+        else:
+            q = self.q_proj(x)._t.view(b, s, nh, d)
+            k = self.k_proj(x)._t.view(b, s, nkv, d)
+            v = self.v_proj(x)._t.view(b, s, nkv, d)
+        cos, sin = self.rope.tables(q.device, s)
+        pos = None if position_ids is None else position_ids._t
+        q = T.rope(q, cos, sin, pos, style=0)
+        k = T.rope(k, cos, sin, pos, style=0)
+        o, _ = T.flash_attention(q, k, v, causal=True)
+        return self.o_proj(_wrap(o.reshape(b, s, nh * d)))
+
+
+class LlamaMLP(nn.Layer):
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        h, f = config.hidden_size, config.intermediate_size
+        if config.fuse_attention_ffn:
+            self.gate_up_fused_proj = _linear(config, h, 2 * f, "col")
+        else:
+            self.gate_proj = _linear(config, h, f, "col")
+            self.up_proj = _linear(config, h, f, "col")
+        self.down_proj = _linear(config, f, h, "row")
+
+    def forward(self, x):
+        if self.config.fuse_attention_ffn:
+            gu = self.gate_up_fused_proj(x)._t
+            if self.config.tensor_parallel_degree > 1:
+                # column-sharded output is [gate_shard | up_shard] per rank already
+                pass
+            a = T.swiglu(gu)
+        else:
+            a = T.swiglu(self.gate_proj(x)._t, self.up_proj(x)._t)
+        return self.down_proj(_wrap(a))
+
+
+class LlamaDecoderLayer(nn.Layer):
+    def __init__(self, config, rope):
+        super().__init__()
+        self.self_attn = LlamaAttention(config, rope)
+        self.mlp = LlamaMLP(config)
+        self.input_layernorm = LlamaRMSNorm(config)
+        self.post_attention_layernorm = LlamaRMSNorm(config)
+
+    def forward(self, hidden, residual=None, position_ids=None):
+        """Returns (mlp_out, residual) so the next layer can fuse ``residual + mlp_out`` into its norm."""
+        if residual is None:
+            residual = hidden
+            x = self.input_layernorm(hidden)
+        else:
+            x, residual = self.input_layernorm(hidden, residual)
+        attn = self.self_attn(x, position_ids)
+        x, residual = self.post_attention_layernorm(attn, residual)
+        return self.mlp(x), residual
+
+
+class LlamaModel(nn.Layer):
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        init = nn.ParamAttr(initializer=I.Normal(0.0, config.initializer_range))
+        if config.tensor_parallel_degree > 1:
+            from ..distributed.fleet.layers.mpu import VocabParallelEmbedding
+
+            self.embed_tokens = VocabParallelEmbedding(config.vocab_size, config.hidden_size, weight_attr=init)
+        else:
+            self.embed_tokens = nn.Embedding(config.vocab_size, config.hidden_size, weight_attr=init)
+        rope = LlamaRotaryEmbedding(config.head_dim, config.max_position_embeddings, config.rope_theta)
+        self.layers = nn.LayerList([LlamaDecoderLayer(config, rope) for _ in range(config.num_hidden_layers)])
+        self.norm = LlamaRMSNorm(config)
+
+    def forward(self, input_ids, position_ids=None):
+        h = self.embed_tokens(input_ids)
+        residual = None
+        for layer in self.layers:
+            if self.config.recompute and self.training:
+                from ..distributed.fleet.recompute import recompute
+
+                h, residual = recompute(layer, h, residual, position_ids)
+            else:
+                h, residual = layer(h, residual, position_ids)
+        out, _ = self.norm(h, residual)
+        return out
+
+
+class LlamaLMHead(nn.Layer):
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        vocab = config.vocab_size // config.tensor_parallel_degree
+        self.weight = self.create_parameter([config.hidden_size, vocab], dtype=config.dtype,
+                                            default_initializer=I.Normal(0.0, config.initializer_range))
+        if config.tensor_parallel_degree > 1:
+            self.weight.is_distributed = True
+
+    def forward(self, h):
+        return _wrap(torch.matmul(h._t, self.weight._t))
+
+
+class LlamaPretrainingCriterion(nn.Layer):
+    """Token-mean softmax cross entropy (vocab-parallel when TP > 1)."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+
+    def forward(self, logits, labels):
+        if self.config.tensor_parallel_degree > 1:
+            from ..distributed.fleet.layers.mpu import ParallelCrossEntropy
+
+            loss = ParallelCrossEntropy(ignore_index=self.config.ignore_index)(logits, labels)._t
+        else:
+            loss = T.softmax_cross_entropy(logits._t, labels._t, self.config.ignore_index)
+        valid = (labels._t != self.config.ignore_index).sum().clamp_min(1)
+        return _wrap(loss.sum() / valid)
+
+
+class LlamaForCausalLM(nn.Layer):
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        self.llama = LlamaModel(config)
+        self.lm_head = LlamaLMHead(config)
+        self.criterion = LlamaPretrainingCriterion(config)
+        if config.dtype in ("bfloat16", "float16"):
+            self.to(dtype=config.dtype)
+
+    def forward(self, input_ids, labels=None, position_ids=None):
+        h = self.llama(input_ids, position_ids)
+        logits = self.lm_head(h)
+        if labels is None:
+            return logits
+        return self.criterion(logits, labels)
+
+
+def llama_flops_per_token(cfg: LlamaConfig, seq_len: int) -> float:
+    """Training FLOPs/token: 6 * N_matmul_params + causal attention (fwd 2*2*s*h/2 per layer, x3 for bwd)."""
+    h, f, L, V = cfg.hidden_size, cfg.intermediate_size, cfg.num_hidden_layers, cfg.vocab_size
+    kvh = cfg.num_key_value_heads * cfg.head_dim
+    per_layer = h * (h + 2 * kvh) + h * h + 3 * h * f
+    n = L * per_layer + h * V
+    attn = L * 2 * 2 * seq_len * h / 2  # QK^T + PV, causal half, fwd
+    return 6.0 * n + 3.0 * attn

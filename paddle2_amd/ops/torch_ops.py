@@ -1,0 +1,469 @@
+"""torch-level fused ops: HIP kernel on the MI355X, PyTorch reference on CPU.
+
+Each op is a ``torch.autograd.Function`` whose forward/backward call the CDNA4 kernels of
+``paddle2_amd._C`` when the inputs are on the GPU (``_native.use_native`` raises if the extension
+is missing there, so GPU runs never silently fall back).  The CPU branches are the fp32
+reference implementations that the numerics tests compare against.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _native as N
+
+_DT = N.DT_CODE
+
+
+def _rows(x: torch.Tensor):
+    n = x.shape[-1]
+    return x.numel() // max(n, 1), n
+
+
+# ============================================================================ RMSNorm / LayerNorm
+class _NormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, residual, eps, layernorm):
+        shape = x.shape
+        M, Nn = _rows(x)
+        x2 = x.reshape(M, Nn).contiguous()
+        res2 = residual.reshape(M, Nn).contiguous() if residual is not None else None
+        if w is None:
+            w = torch.ones(Nn, dtype=x.dtype, device=x.device)
+        wc = w.contiguous()
+        if wc.dtype not in (x.dtype, torch.float32):
+            wc = wc.to(x.dtype)
+        bc = None
+        if b is not None:
+            bc = b.contiguous().to(wc.dtype)
+        if N.use_native(x) and x.dtype in _DT and (Nn % (4 if x.dtype == torch.float32 else 8) == 0) and \
+                Nn <= (4096 if x.dtype == torch.float32 else 8192):
+            C = N.native()
+            y = torch.empty_like(x2)
+            rstd = torch.empty(M, dtype=torch.float32, device=x.device)
+            mean = torch.empty(M, dtype=torch.float32, device=x.device) if layernorm else None
+            h = torch.empty_like(x2) if res2 is not None else None
+            C.norm_fwd(int(layernorm), _DT[x.dtype], _DT[wc.dtype], x2.data_ptr(), N.ptr(res2), wc.data_ptr(),
+                       N.ptr(bc), y.data_ptr(), N.ptr(h), N.ptr(mean), rstd.data_ptr(), M, Nn, float(eps), N.stream())
+            hh = h if h is not None else x2
+            ctx.native = True
+        else:
+            hh = (x2.float() + res2.float()).to(x.dtype) if res2 is not None else x2
+            hf = hh.float()
+            if layernorm:
+                mean = hf.mean(-1)
+                var = ((hf - mean[:, None]) ** 2).mean(-1)
+                rstd = torch.rsqrt(var + eps)
+                yf = (hf - mean[:, None]) * rstd[:, None] * wc.float()
+            else:
+                mean = None
+                rstd = torch.rsqrt((hf * hf).mean(-1) + eps)
+                yf = hf * rstd[:, None] * wc.float()
+            if bc is not None:
+                yf = yf + bc.float()
+            y = yf.to(x.dtype)
+            h = hh if res2 is not None else None
+            ctx.native = False
+        ctx.save_for_backward(hh, wc, mean, rstd)
+        ctx.layernorm = layernorm
+        ctx.has_res = res2 is not None
+        ctx.has_b = bc is not None
+        ctx.shape = shape
+        ctx.wdtype = w.dtype
+        if res2 is not None:
+            return y.reshape(shape), h.reshape(shape)
+        return y.reshape(shape), None
+
+    @staticmethod
+    def backward(ctx, dy, dh):
+        hh, wc, mean, rstd = ctx.saved_tensors
+        M, Nn = hh.shape
+        dy2 = dy.reshape(M, Nn).contiguous()
+        dh2 = dh.reshape(M, Nn).contiguous() if (dh is not None and ctx.has_res) else None
+        if ctx.native:
+            C = N.native()
+            nb = C.norm_bwd_blocks(M)
+            dx = torch.empty_like(hh)
+            dw_part = torch.empty(nb, Nn, dtype=torch.float32, device=hh.device)
+            db_part = torch.empty(nb, Nn, dtype=torch.float32, device=hh.device) if ctx.layernorm else None
+            dw = torch.empty(Nn, dtype=wc.dtype, device=hh.device)
+            db = torch.empty(Nn, dtype=wc.dtype, device=hh.device) if ctx.layernorm else None
+            C.norm_bwd(int(ctx.layernorm), _DT[hh.dtype], _DT[wc.dtype], dy2.data_ptr(), hh.data_ptr(), wc.data_ptr(),
+                       N.ptr(mean), rstd.data_ptr(), N.ptr(dh2), dx.data_ptr(), dw_part.data_ptr(), N.ptr(db_part),
+                       dw.data_ptr(), N.ptr(db), M, Nn, nb, N.stream())
+        else:
+            hf = hh.float()
+            xh = (hf - mean[:, None]) * rstd[:, None] if ctx.layernorm else hf * rstd[:, None]
+            g = dy2.float() * wc.float()
+            dxf = g - xh * (g * xh).mean(-1, keepdim=True)
+            if ctx.layernorm:
+                dxf = dxf - g.mean(-1, keepdim=True)
+            dxf = dxf * rstd[:, None]
+            if dh2 is not None:
+                dxf = dxf + dh2.float()
+            dx = dxf.to(hh.dtype)
+            dw = (dy2.float() * xh).sum(0).to(wc.dtype)
+            db = dy2.float().sum(0).to(wc.dtype) if ctx.layernorm else None
+        dx = dx.reshape(ctx.shape)
+        dres = dx if ctx.has_res else None
+        dw = dw.to(ctx.wdtype)
+        return dx, dw, (db if ctx.has_b else None), dres, None, None
+
+
+def rms_norm(x, w, eps=1e-6, residual=None):
+    y, h = _NormFn.apply(x, w, None, residual, eps, False)
+    return (y, h) if residual is not None else y
+
+
+def layer_norm(x, w, b, eps=1e-5, residual=None):
+    y, h = _NormFn.apply(x, w, b, residual, eps, True)
+    return (y, h) if residual is not None else y
+
+
+# ============================================================================ SwiGLU
+class _SwiGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, y):
+        packed = y is None
+        if packed:
+            H = x.shape[-1] // 2
+            rows = x.numel() // x.shape[-1]
+            xc = x.contiguous()
+            out_shape = list(x.shape[:-1]) + [H]
+        else:
+            H = x.shape[-1]
+            rows = x.numel() // H
+            xc, yc = x.contiguous(), y.contiguous()
+            out_shape = list(x.shape)
+        ctx.packed, ctx.H, ctx.rows = packed, H, rows
+        if N.use_native(x) and x.dtype in _DT and H % (4 if x.dtype == torch.float32 else 8) == 0:
+            C = N.native()
+            out = torch.empty(out_shape, dtype=x.dtype, device=x.device)
+            if packed:
+                C.swiglu_fwd(_DT[x.dtype], xc.data_ptr(), xc.data_ptr() + H * xc.element_size(), out.data_ptr(), rows, H,
+                             2 * H, 2 * H, N.stream())
+                ctx.save_for_backward(xc)
+            else:
+                C.swiglu_fwd(_DT[x.dtype], xc.data_ptr(), yc.data_ptr(), out.data_ptr(), rows, H, H, H, N.stream())
+                ctx.save_for_backward(xc, yc)
+            ctx.native = True
+            return out
+        ctx.native = False
+        if packed:
+            a, b = xc[..., :H], xc[..., H:]
+            ctx.save_for_backward(xc)
+        else:
+            a, b = xc, yc
+            ctx.save_for_backward(xc, yc)
+        return (F.silu(a.float()) * b.float()).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        H, rows = ctx.H, ctx.rows
+        gc = g.contiguous()
+        if ctx.packed:
+            (xc,) = ctx.saved_tensors
+        else:
+            xc, yc = ctx.saved_tensors
+        if ctx.native:
+            C = N.native()
+            es = xc.element_size()
+            if ctx.packed:
+                dxy = torch.empty_like(xc)
+                C.swiglu_bwd(_DT[xc.dtype], xc.data_ptr(), xc.data_ptr() + H * es, gc.data_ptr(), dxy.data_ptr(),
+                             dxy.data_ptr() + H * es, rows, H, 2 * H, 2 * H, 2 * H, 2 * H, N.stream())
+                return dxy, None
+            dx = torch.empty_like(xc)
+            dy = torch.empty_like(yc)
+            C.swiglu_bwd(_DT[xc.dtype], xc.data_ptr(), yc.data_ptr(), gc.data_ptr(), dx.data_ptr(), dy.data_ptr(), rows,
+                         H, H, H, H, H, N.stream())
+            return dx, dy
+        if ctx.packed:
+            a, b = xc[..., :H].float(), xc[..., H:].float()
+        else:
+            a, b = xc.float(), yc.float()
+        s = torch.sigmoid(a)
+        gf = gc.float()
+        da = gf * b * s * (1 + a * (1 - s))
+        db = gf * a * s
+        if ctx.packed:
+            return torch.cat([da, db], -1).to(xc.dtype), None
+        return da.to(xc.dtype), db.to(yc.dtype)
+
+
+def swiglu(x, y=None):
+    return _SwiGLUFn.apply(x, y)
+
+
+# ============================================================================ RoPE
+def rope_tables(seq_len, head_dim, base=10000.0, interleaved=True, device=None, position_scale=1.0):
+    """cos/sin fp32 tables [S, D] laid out for the chosen rotation style."""
+    inv = 1.0 / (base ** (torch.arange(0, head_dim, 2, dtype=torch.float32, device=device) / head_dim))
+    t = torch.arange(seq_len, dtype=torch.float32, device=device) * position_scale
+    freqs = torch.outer(t, inv)  # [S, D/2]
+    if interleaved:
+        emb = torch.repeat_interleave(freqs, 2, dim=-1)
+    else:
+        emb = torch.cat([freqs, freqs], dim=-1)
+    return emb.cos(), emb.sin()
+
+
+class _RopeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cos, sin, pos, style, time_major):
+        ctx.save_for_backward(cos, sin, pos)
+        ctx.style, ctx.tm = style, time_major
+        return _rope_apply(x, cos, sin, pos, style, time_major, False)
+
+    @staticmethod
+    def backward(ctx, g):
+        cos, sin, pos = ctx.saved_tensors
+        return _rope_apply(g, cos, sin, pos, ctx.style, ctx.tm, True), None, None, None, None, None
+
+
+def _rope_apply(x, cos, sin, pos, style, time_major, bwd):
+    xc = x.contiguous()
+    if time_major:
+        S, B, Hn, D = xc.shape
+    else:
+        B, S, Hn, D = xc.shape
+    if N.use_native(x) and x.dtype in _DT:
+        C = N.native()
+        out = torch.empty_like(xc)
+        C.rope(_DT[x.dtype], style, int(bwd), xc.data_ptr(), out.data_ptr(), cos.data_ptr(), sin.data_ptr(),
+               N.ptr(pos), B, S, Hn, D, int(time_major), N.stream())
+        return out
+    # reference
+    xf = xc.float()
+    if pos is not None:
+        c = cos[pos]  # [B, S, D]
+        s_ = sin[pos]
+        c = c[:, :, None, :]
+        s_ = s_[:, :, None, :]
+        if time_major:
+            c, s_ = c.transpose(0, 1), s_.transpose(0, 1)
+    else:
+        c = cos[:S][:, None, :]
+        s_ = sin[:S][:, None, :]
+        if not time_major:
+            c, s_ = c[None], s_[None]
+    if style == 0:
+        half = D // 2
+        xa, xb = xf[..., :half], xf[..., half:]
+        ca, cb = c[..., :half], c[..., half:]
+        sa, sb = s_[..., :half], s_[..., half:]
+    else:
+        xa, xb = xf[..., 0::2], xf[..., 1::2]
+        ca, cb = c[..., 0::2], c[..., 1::2]
+        sa, sb = s_[..., 0::2], s_[..., 1::2]
+    if not bwd:
+        oa = xa * ca - xb * sa
+        ob = xb * cb + xa * sb
+    else:
+        oa = xa * ca + xb * sb
+        ob = xb * cb - xa * sa
+    if style == 0:
+        out = torch.cat([oa, ob], -1)
+    else:
+        out = torch.stack([oa, ob], -1).flatten(-2)
+    return out.to(x.dtype)
+
+
+def rope(x, cos, sin, pos=None, style=0, time_major=False):
+    """Apply rotary embedding. style 0 = rotate-half, 1 = rotate-every-two (interleaved)."""
+    cos = cos.reshape(-1, x.shape[-1]).float().contiguous()
+    sin = sin.reshape(-1, x.shape[-1]).float().contiguous()
+    if pos is not None:
+        pos = pos.to(torch.int64).contiguous()
+    return _RopeFn.apply(x, cos, sin, pos, style, time_major)
+
+
+# ============================================================================ softmax cross entropy
+class _SCEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        V = logits.shape[-1]
+        x2 = logits.reshape(-1, V).contiguous()
+        lab = labels.reshape(-1).to(torch.int64).contiguous()
+        Nr = x2.shape[0]
+        if N.use_native(logits) and logits.dtype in _DT:
+            C = N.native()
+            mx = torch.empty(Nr, dtype=torch.float32, device=x2.device)
+            se = torch.empty_like(mx)
+            tgt = torch.empty_like(mx)
+            C.ce_stats(_DT[x2.dtype], x2.data_ptr(), lab.data_ptr(), mx.data_ptr(), se.data_ptr(), tgt.data_ptr(), Nr,
+                       V, 0, N.stream())
+            lse = mx + torch.log(se)
+            ctx.native = True
+        else:
+            xf = x2.float()
+            lse = torch.logsumexp(xf, -1)
+            safe = lab.clamp(0, V - 1)
+            tgt = xf.gather(1, safe[:, None]).squeeze(1)
+            ctx.native = False
+        valid = lab != ignore_index
+        loss = torch.where(valid, lse - tgt, torch.zeros_like(lse))
+        ctx.save_for_backward(x2, lab, lse)
+        ctx.ignore = ignore_index
+        ctx.shape = logits.shape
+        return loss.reshape(labels.shape)
+
+    @staticmethod
+    def backward(ctx, dloss):
+        x2, lab, lse = ctx.saved_tensors
+        Nr, V = x2.shape
+        dl = dloss.reshape(-1).float().contiguous()
+        if ctx.native:
+            C = N.native()
+            dx = torch.empty_like(x2)
+            C.ce_bwd(_DT[x2.dtype], x2.data_ptr(), lab.data_ptr(), lse.data_ptr(), dl.data_ptr(), dx.data_ptr(), Nr, V,
+                     0, ctx.ignore, 0, N.stream())
+        else:
+            p = torch.exp(x2.float() - lse[:, None])
+            valid = lab != ctx.ignore
+            p[torch.arange(Nr, device=x2.device)[valid], lab[valid]] -= 1.0
+            dx = (p * (dl * valid)[:, None]).to(x2.dtype)
+        return dx.reshape(ctx.shape), None, None
+
+
+def softmax_cross_entropy(logits, labels, ignore_index=-100):
+    """Per-token fp32 loss (0 at ignore_index); logits [..., V], labels [...]."""
+    return _SCEFn.apply(logits, labels, ignore_index)
+
+
+# ============================================================================ embedding
+class _EmbFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, w, padding_idx, start):
+        Vl, H = w.shape
+        idc = ids.reshape(-1).to(torch.int64).contiguous()
+        wc = w.contiguous()
+        if N.use_native(w) and w.dtype in _DT and (H * w.element_size()) % 16 == 0:
+            C = N.native()
+            out = torch.empty(idc.numel(), H, dtype=w.dtype, device=w.device)
+            C.embed_fwd(_DT[w.dtype], idc.data_ptr(), wc.data_ptr(), out.data_ptr(), idc.numel(), H, start, Vl,
+                        N.stream())
+            ctx.native = True
+        else:
+            local = idc - start
+            ok = (local >= 0) & (local < Vl)
+            out = wc[local.clamp(0, Vl - 1)] * ok[:, None].to(w.dtype)
+            ctx.native = False
+        ctx.save_for_backward(idc)
+        ctx.meta = (Vl, H, padding_idx if padding_idx is not None else -(2 ** 62), start, w.dtype, ids.shape)
+        return out.reshape(list(ids.shape) + [H])
+
+    @staticmethod
+    def backward(ctx, g):
+        (idc,) = ctx.saved_tensors
+        Vl, H, pad, start, wdt, ishape = ctx.meta
+        gc = g.reshape(-1, H).contiguous()
+        if ctx.native:
+            C = N.native()
+            dw32 = torch.zeros(Vl, H, dtype=torch.float32, device=g.device)
+            C.embed_bwd(_DT[gc.dtype], idc.data_ptr(), gc.data_ptr(), dw32.data_ptr(), idc.numel(), H, start, Vl, pad,
+                        N.stream())
+        else:
+            dw32 = torch.zeros(Vl, H, dtype=torch.float32, device=g.device)
+            local = idc - start
+            ok = (local >= 0) & (local < Vl) & (idc != pad)
+            dw32.index_add_(0, local[ok], gc[ok].float())
+        return None, dw32.to(wdt), None, None
+
+
+def embedding(ids, w, padding_idx=None, start=0):
+    if padding_idx is not None and padding_idx < 0:
+        padding_idx = padding_idx + w.shape[0]
+    return _EmbFn.apply(ids, w, padding_idx, start)
+
+
+# ============================================================================ flash attention
+def _attn_reference(q, k, v, causal, scale):
+    """fp32 math attention on [B, S, H, D] with GQA; returns (out, lse[B, H, Sq])."""
+    B, Sq, Hq, D = q.shape
+    Sk, Hk = k.shape[1], k.shape[2]
+    qf = q.float().transpose(1, 2)
+    kf = k.float().transpose(1, 2)
+    vf = v.float().transpose(1, 2)
+    if Hk != Hq:
+        rep = Hq // Hk
+        kf = kf.repeat_interleave(rep, 1)
+        vf = vf.repeat_interleave(rep, 1)
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if causal:
+        off = Sk - Sq
+        i = torch.arange(Sq, device=q.device)[:, None]
+        j = torch.arange(Sk, device=q.device)[None, :]
+        s = s.masked_fill(j > i + off, float("-inf"))
+    lse = torch.logsumexp(s, -1)
+    p = torch.exp(s - lse[..., None])
+    p = torch.nan_to_num(p, nan=0.0)
+    out = torch.matmul(p, vf).transpose(1, 2)
+    return out.to(q.dtype), lse
+
+
+def _row_view_ok(t):
+    # [B, S, H, D] with unit stride on D, stride D on H, uniform row stride on S, batch = S*row
+    B, S, H, D = t.shape
+    st = t.stride()
+    return st[3] == 1 and st[2] == D and st[0] == S * st[1]
+
+
+class _FlashFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        B, Sq, Hq, D = q.shape
+        Sk, Hk = k.shape[1], k.shape[2]
+        native = (N.use_native(q) and q.dtype == torch.bfloat16 and D in (64, 128) and Hq % Hk == 0)
+        if native:
+            q_ = q if _row_view_ok(q) else q.contiguous()
+            k_ = k if _row_view_ok(k) else k.contiguous()
+            v_ = v if _row_view_ok(v) else v.contiguous()
+            out = torch.empty(B, Sq, Hq, D, dtype=q.dtype, device=q.device)
+            lse = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
+            N.native().flash_fwd(1, q_.data_ptr(), k_.data_ptr(), v_.data_ptr(), out.data_ptr(), lse.data_ptr(), B, Sq,
+                                 Sk, Hq, Hk, D, q_.stride(1), k_.stride(1), v_.stride(1), out.stride(1), float(scale),
+                                 int(causal), N.stream())
+            ctx.save_for_backward(q_, k_, v_, out, lse)
+        else:
+            out, lse = _attn_reference(q, k, v, causal, scale)
+            ctx.save_for_backward(q, k, v, out, lse)
+        ctx.native, ctx.causal, ctx.scale = native, causal, scale
+        return out, lse
+
+    @staticmethod
+    def backward(ctx, dout, dlse):
+        q, k, v, out, lse = ctx.saved_tensors
+        B, Sq, Hq, D = q.shape
+        Sk, Hk = k.shape[1], k.shape[2]
+        if ctx.native:
+            do = dout.contiguous()
+            dq = torch.empty(B, Sq, Hq, D, dtype=q.dtype, device=q.device)
+            dk = torch.empty(B, Sk, Hk, D, dtype=q.dtype, device=q.device)
+            dv = torch.empty(B, Sk, Hk, D, dtype=q.dtype, device=q.device)
+            dq32 = torch.zeros(B, Sq, Hq, D, dtype=torch.float32, device=q.device)
+            delta = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
+            if not _row_view_ok(out):
+                out = out.contiguous()
+            assert out.stride(1) == do.stride(1), "out/dout row strides must match"
+            N.native().flash_bwd(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), do.data_ptr(),
+                                 lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+                                 dq32.data_ptr(), B, Sq, Sk, Hq, Hk, D, q.stride(1), k.stride(1), v.stride(1),
+                                 do.stride(1), float(ctx.scale), int(ctx.causal), N.stream())
+            return dq, dk, dv, None, None
+        with torch.enable_grad():
+            qq = q.detach().float().requires_grad_(True)
+            kk = k.detach().float().requires_grad_(True)
+            vv = v.detach().float().requires_grad_(True)
+            o, _ = _attn_reference(qq, kk, vv, ctx.causal, ctx.scale)
+            gq, gk, gv = torch.autograd.grad(o, (qq, kk, vv), dout.float())
+        return gq.to(q.dtype), gk.to(k.dtype), gv.to(v.dtype), None, None
+
+
+def flash_attention(q, k, v, causal=False, scale=None):
+    """q [B, Sq, Hq, D], k/v [B, Sk, Hk, D] -> (out [B, Sq, Hq, D], lse [B, Hq, Sq] fp32)."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    return _FlashFn.apply(q, k, v, bool(causal), float(scale))
