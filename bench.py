@@ -73,7 +73,12 @@ def main():
                                  parameters=model.parameters(), weight_decay=0.1,
                                  apply_decay_param_fun=lambda n: n in decay,
                                  grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0), multi_precision=True)
-    model, opt = fleet.distributed_model(model, opt, level=f"stage{args.sharding_stage}") if world > 1 else (model, opt)
+    if world > 1:
+        from paddle2_amd.distributed.sharding import group_sharded_parallel
+
+        level = {1: "os", 2: "os_g", 3: "p_g_os"}[args.sharding_stage]
+        model, opt, _ = group_sharded_parallel(model, opt, level,
+                                               group=fleet.get_hybrid_communicate_group().get_sharding_parallel_group())
 
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     b, s = args.micro_batch, args.seq_len

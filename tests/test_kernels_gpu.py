@@ -192,7 +192,10 @@ def test_fused_adamw(pdt, gdt, master):
     for step in range(3):
         for i, (a, b) in enumerate(zip(ps_g, ps_c)):
             g = torch.randn(a.shape, generator=torch.Generator().manual_seed(100 + 10 * step + i))
-            a._t.grad = g.to(DEV, gdt)
+            if gdt != pdt:  # fp32 grads of bf16 params travel as Paddle's main_grad
+                a.main_grad = g.to(DEV, gdt)
+            else:
+                a._t.grad = g.to(DEV, gdt)
             b._t.grad = g.to(gdt).float()
         og.step()
         oc.step()

@@ -43,3 +43,23 @@ def test_llama_gpu_matches_cpu_reference():
     ids_g = ids.cuda()
     lg = float(mg(ids_g, labels=ids_g))
     assert abs(lg - lc) < 0.05 * abs(lc), (lg, lc)
+
+
+def test_llama_is_causal():
+    """Changing token t must not change logits at positions < t (catches any attention leak)."""
+    import paddle2_amd as paddle
+    from paddle2_amd.models import LlamaConfig, LlamaForCausalLM
+
+    paddle.set_device("gpu:0")
+    paddle.seed(3)
+    cfg = LlamaConfig.tiny(num_hidden_layers=2)
+    m = LlamaForCausalLM(cfg)
+    ids = paddle.randint(0, cfg.vocab_size, [1, 256])
+    ids2 = ids.clone()
+    t = 150
+    ids2[0, t] = (int(ids[0, t]) + 7) % cfg.vocab_size
+    with paddle.no_grad():
+        a = m(ids)._t.float()
+        b = m(ids2)._t.float()
+    assert torch.allclose(a[:, :t], b[:, :t], atol=1e-3), (a[:, :t] - b[:, :t]).abs().max()
+    assert not torch.allclose(a[:, t:], b[:, t:], atol=1e-3)

@@ -1,0 +1,63 @@
+"""Rank worker: tiny Llama trained with group_sharded_parallel(level) vs. a single-process run on the
+concatenated global batch; every rank writes its losses + a parameter checksum."""
+import os
+import sys
+
+sys.path.insert(0, os.environ.get("PYTHONPATH", "."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+
+import torch  # noqa: E402
+
+import paddle2_amd as paddle  # noqa: E402
+from paddle2_amd.distributed import collective as C  # noqa: E402
+from paddle2_amd.distributed.sharding import group_sharded_parallel  # noqa: E402
+from paddle2_amd.models import LlamaConfig, LlamaForCausalLM  # noqa: E402
+from _dist import write_result  # noqa: E402
+
+level = sys.argv[1]
+steps = 3
+C.init_parallel_env()
+rank, world = C.get_rank(), C.get_world_size()
+cfg = LlamaConfig.tiny(dtype="float32", num_hidden_layers=2)
+
+
+def make():
+    paddle.seed(7)
+    m = LlamaForCausalLM(cfg)
+    o = paddle.optimizer.AdamW(1e-2, parameters=m.parameters(), weight_decay=0.01,
+                               grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
+    return m, o
+
+
+g = torch.Generator().manual_seed(99)
+data = [torch.randint(0, cfg.vocab_size, (world * 2, 33), generator=g) for _ in range(steps)]
+
+# sharded run: each rank takes its 2 sequences
+m, o = make()
+m, o, _ = group_sharded_parallel(m, o, level)
+losses = []
+for s in range(steps):
+    ids = paddle.Tensor._wrap(data[s][rank * 2:(rank + 1) * 2])
+    loss = m(ids[:, :-1], labels=ids[:, 1:])
+    loss.backward()
+    o.step()
+    o.clear_grad()
+    t = loss._t.detach().clone()
+    C._all_reduce_torch(t)
+    losses.append(float(t) / world)
+sd = m.state_dict()
+csum = float(sum(v._t.double().sum() for v in sd.values()))
+
+# single-process reference on the full batch
+m2, o2 = make()
+ref = []
+for s in range(steps):
+    ids = paddle.Tensor._wrap(data[s])
+    loss = m2(ids[:, :-1], labels=ids[:, 1:])
+    loss.backward()
+    o2.step()
+    o2.clear_grad()
+    ref.append(float(loss))
+csum_ref = float(sum(v._t.double().sum() for v in m2.state_dict().values()))
+write_result({"losses": losses, "ref": ref, "csum": csum, "csum_ref": csum_ref})
+C.destroy_process_group()
