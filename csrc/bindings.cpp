@@ -22,7 +22,7 @@ int pd_norm_bwd(int, int, int, const void*, const void*, const void*, const floa
 int pd_swiglu_fwd(int, const void*, const void*, void*, long, int, long, long, void*);
 int pd_swiglu_bwd(int, const void*, const void*, const void*, void*, void*, long, int, long, long, long, long, void*);
 int pd_rope(int, int, int, const void*, void*, const float*, const float*, const int64_t*, int, int, int, int, int,
-            void*);
+            long, long, void*);
 int pd_opt_chunk_size();
 int pd_opt_meta_bytes();
 int pd_adamw_mt(int, int, int, const void*, const long*, int, long, float, float, float, float, float, float,
@@ -39,7 +39,8 @@ int pd_cast_from_f32(int, const float*, void*, long, void*);
 int pd_flash_fwd(int, const void*, const void*, const void*, void*, float*, int, int, int, int, int, int, long, long,
                  long, long, float, int, void*);
 int pd_flash_bwd(int, const void*, const void*, const void*, const void*, const void*, const float*, float*, void*,
-                 void*, void*, float*, int, int, int, int, int, int, long, long, long, long, float, int, void*);
+                 void*, void*, float*, int, int, int, int, int, int, long, long, long, long, long, long, long, float,
+                 int, void*);
 }
 
 template <typename T>
@@ -82,9 +83,9 @@ PYBIND11_MODULE(_C, m) {
           "swiglu_bwd");
   });
   m.def("rope", [](int dt, int style, int bwd, uintptr_t x, uintptr_t out, uintptr_t cosv, uintptr_t sinv,
-                   uintptr_t pos, int B, int S, int Hn, int D, int time_major, uintptr_t st) {
+                   uintptr_t pos, int B, int S, int Hn, int D, int time_major, long sx, long so, uintptr_t st) {
     check(pd_rope(dt, style, bwd, P<const void*>(x), P<void*>(out), P<const float*>(cosv), P<const float*>(sinv),
-                  P<const int64_t*>(pos), B, S, Hn, D, time_major, P<void*>(st)),
+                  P<const int64_t*>(pos), B, S, Hn, D, time_major, sx, so, P<void*>(st)),
           "rope");
   });
   m.def("opt_chunk_size", &pd_opt_chunk_size);
@@ -152,12 +153,12 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("flash_bwd", [](int dt, uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t dout, uintptr_t lse,
                         uintptr_t delta, uintptr_t dq, uintptr_t dk, uintptr_t dv, uintptr_t dq32, int B, int Sq,
-                        int Sk, int Hq, int Hk, int D, long sq_row, long sk_row, long sv_row, long so_row, float scale,
-                        int causal, uintptr_t st) {
+                        int Sk, int Hq, int Hk, int D, long sq_row, long sk_row, long sv_row, long so_row,
+                        long sdq_row, long sdk_row, long sdv_row, float scale, int causal, uintptr_t st) {
     check(pd_flash_bwd(dt, P<const void*>(q), P<const void*>(k), P<const void*>(v), P<const void*>(o),
                        P<const void*>(dout), P<const float*>(lse), P<float*>(delta), P<void*>(dq), P<void*>(dk),
-                       P<void*>(dv), P<float*>(dq32), B, Sq, Sk, Hq, Hk, D, sq_row, sk_row, sv_row, so_row, scale,
-                       causal, P<void*>(st)),
+                       P<void*>(dv), P<float*>(dq32), B, Sq, Sk, Hq, Hk, D, sq_row, sk_row, sv_row, so_row, sdq_row,
+                       sdk_row, sdv_row, scale, causal, P<void*>(st)),
           "flash_bwd");
   });
 }

@@ -103,7 +103,9 @@ template <typename T, int STYLE, bool BWD, bool VEC>
 __global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, T* __restrict__ out,
                                                    const float* __restrict__ cosv, const float* __restrict__ sinv,
                                                    const int64_t* __restrict__ pos, int B, int S, int Hn, int D,
-                                                   int time_major) {
+                                                   int time_major, long sx, long so) {
+  // sx / so: elements between consecutive tokens of x / out (heads are D apart), so q/k can be
+  // read straight out of a fused QKV projection and gradients written straight into dQKV.
   const int half = D / 2;
   const int chunks = (half + 7) / 8;
   const long total = (long)B * S * Hn * chunks;
@@ -116,8 +118,8 @@ __global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, T* _
     if (time_major) { s = (int)(t / B); b = (int)(t % B); }
     else { b = (int)(t / S); s = (int)(t % S); }
     const int p = pos ? (int)pos[(long)b * S + s] : s;
-    const T* xr = x + (t * Hn + h) * (long)D;
-    T* orow = out + (t * Hn + h) * (long)D;
+    const T* xr = x + t * sx + (long)h * D;
+    T* orow = out + t * so + (long)h * D;
     const float* cr = cosv + (long)p * D;
     const float* sr = sinv + (long)p * D;
     if constexpr (VEC) {
@@ -191,13 +193,15 @@ extern "C" int pd_swiglu_bwd(int dt, const void* x, const void* y, const void* d
 }
 
 extern "C" int pd_rope(int dt, int style, int bwd, const void* x, void* out, const float* cosv, const float* sinv,
-                       const int64_t* pos, int B, int S, int Hn, int D, int time_major, void* stream) {
+                       const int64_t* pos, int B, int S, int Hn, int D, int time_major, long sx, long so,
+                       void* stream) {
   if (D % 2) return -1;
   hipStream_t st = (hipStream_t)stream;
   const long work = (long)B * S * Hn * ((D / 2 + 7) / 8);
   const int g = ew_grid(work);
-  const bool vec = (D % 16) == 0;
-#define PD_ROPE1(T, SY, BW, VE) rope_kernel<T, SY, BW, VE><<<g, 256, 0, st>>>((const T*)x, (T*)out, cosv, sinv, pos, B, S, Hn, D, time_major)
+  const int es = dt == kF32 ? 4 : 2;
+  const bool vec = (D % 16) == 0 && ((sx * es) % 16) == 0 && ((so * es) % 16) == 0;
+#define PD_ROPE1(T, SY, BW, VE) rope_kernel<T, SY, BW, VE><<<g, 256, 0, st>>>((const T*)x, (T*)out, cosv, sinv, pos, B, S, Hn, D, time_major, sx, so)
 #define PD_ROPE(T)                                                                                    \
   if (vec) {                                                                                          \
     if (style == 0) { if (bwd) PD_ROPE1(T, 0, true, true); else PD_ROPE1(T, 0, false, true); }        \

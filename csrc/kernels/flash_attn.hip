@@ -308,7 +308,8 @@ __global__ __launch_bounds__(256, 1) void bwd_kernel(const bf16* __restrict__ Q,
                                                      const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                      float* __restrict__ dQ32, bf16* __restrict__ dK,
                                                      bf16* __restrict__ dV, int B, int Sq, int Sk, int Hq, int Hk,
-                                                     long sq, long sk, long sv, long so, float scale) {
+                                                     long sq, long sk, long sv, long so, long sdk, long sdv,
+                                                     float scale) {
   constexpr int BNK = 128, BMQ = 32, NCH = D / 8, KS = D / 16, DT = D / 32;
   constexpr int KTILE = BNK * D * 2;     // K block image (for dQ = dS.K)
   constexpr int QTILE = BMQ * D * 2;     // Q / dO tile image
@@ -454,8 +455,8 @@ __global__ __launch_bounds__(256, 1) void bwd_kernel(const bf16* __restrict__ Q,
   }
   // write dK (scaled) and dV for this lane's key: accumulator row = d, column = key
   if (mykey < Sk) {
-    bf16* dkr = dK + ((long)b * Sk + mykey) * Hk * D + hk * D;
-    bf16* dvr = dV + ((long)b * Sk + mykey) * Hk * D + hk * D;
+    bf16* dkr = dK + ((long)b * Sk + mykey) * sdk + hk * D;
+    bf16* dvr = dV + ((long)b * Sk + mykey) * sdv + hk * D;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
 #pragma unroll
@@ -509,12 +510,13 @@ extern "C" int pd_flash_fwd(int dt, const void* q, const void* k, const void* v,
   return (int)hipGetLastError();
 }
 
-// dq32 must be a zeroed [B, Sq, Hq, D] fp32 workspace; delta a [B, Hq, Sq] fp32 workspace;
-// dq/dk/dv are written contiguous ([B, S, H, D]); q/k/v/o/dout may be strided row views.
+// dq32 must be a zeroed [B, Sq, Hq, D] fp32 workspace; delta a [B, Hq, Sq] fp32 workspace.
+// q/k/v/o/dout and dq/dk/dv may all be row-strided views ([B, S, H, D] with token strides
+// sq/sk/sv/so and sdq/sdk/sdv), e.g. slices of one fused QKV / dQKV buffer.
 extern "C" int pd_flash_bwd(int dt, const void* q, const void* k, const void* v, const void* o, const void* dout,
                             const float* lse, float* delta, void* dq, void* dk, void* dv, float* dq32, int B, int Sq,
-                            int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, float scale, int causal,
-                            void* stream) {
+                            int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, long sdq, long sdk,
+                            long sdv, float scale, int causal, void* stream) {
   if (dt != kBF16 || (D != 64 && D != 128) || Hq % Hk) return -1;
   hipStream_t st = (hipStream_t)stream;
   const long rows = (long)B * Hq * Sq;
@@ -525,13 +527,13 @@ extern "C" int pd_flash_bwd(int dt, const void* q, const void* k, const void* v,
 #define PD_FA_BWD(DD, CC)                                                                                        \
   fa::bwd_kernel<DD, CC><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
                                                  lse, delta, dq32, (bf16*)dk, (bf16*)dv, B, Sq, Sk, Hq, Hk, sq, sk, \
-                                                 sv, so, scale)
+                                                 sv, so, sdk, sdv, scale)
   if (D == 128) { if (causal) PD_FA_BWD(128, true); else PD_FA_BWD(128, false); }
   else { if (causal) PD_FA_BWD(64, true); else PD_FA_BWD(64, false); }
 #undef PD_FA_BWD
   long work = (long)B * Sq * Hq * (D / 4);
   long g = (work + 255) / 256;
   if (g > 4096) g = 4096;
-  fa::f32_to_bf16_strided<<<(int)g, 256, 0, st>>>(dq32, (bf16*)dq, (long)B * Sq, D, Hq, (long)Hq * D);
+  fa::f32_to_bf16_strided<<<(int)g, 256, 0, st>>>(dq32, (bf16*)dq, (long)B * Sq, D, Hq, sdq);
   return (int)hipGetLastError();
 }

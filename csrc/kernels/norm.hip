@@ -201,18 +201,34 @@ __global__ __launch_bounds__(kNormBlock) void norm_bwd_kernel(
   }
 }
 
-// Reduce P partial rows [P, N] (fp32) into out [N] (type WT); column-parallel, 4 columns/thread.
+// Reduce P partial rows [P, N] (fp32) into out [N] (type WT). Block = 16 column-quads (64 columns)
+// x 16 row lanes; each lane streams P/16 rows with 16-B loads, then one LDS reduction. Deterministic
+// (fixed summation order) and ~P/16 loads in flight per lane instead of a serial P-long chain.
 template <typename WT>
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, WT* __restrict__ out, int P, int N) {
-  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
-  if (c >= N) return;
+  __shared__ float4 red[16][16];
+  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int c = (blockIdx.x * 16 + cq) * 4;
   float4 acc = make_float4(0, 0, 0, 0);
-  for (int p = 0; p < P; ++p) {
-    float4 v = *reinterpret_cast<const float4*>(part + (long)p * N + c);
-    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  if (c < N) {
+#pragma unroll 8
+    for (int p = rl; p < P; p += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (long)p * N + c);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
   }
-  Elt<WT>::st(out + c, acc.x); Elt<WT>::st(out + c + 1, acc.y);
-  Elt<WT>::st(out + c + 2, acc.z); Elt<WT>::st(out + c + 3, acc.w);
+  red[rl][cq] = acc;
+  __syncthreads();
+  if (rl == 0 && c < N) {
+    float4 s = red[0][cq];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) {
+      const float4 v = red[i][cq];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    Elt<WT>::st(out + c, s.x); Elt<WT>::st(out + c + 1, s.y);
+    Elt<WT>::st(out + c + 2, s.z); Elt<WT>::st(out + c + 3, s.w);
+  }
 }
 
 // ------------------------------------------------------------------------------------ host
@@ -262,7 +278,7 @@ static void bwd_launch(const void* dy, const void* x, const void* w, const float
   else { PD_NORM_BWD(4) }
 #undef PD_NORM_BWD
   const int P = nblocks;
-  dim3 g2(ceil_div(N / 4, 256));
+  dim3 g2(ceil_div(N, 64));
   colsum_kernel<WT><<<g2, 256, 0, st>>>(dw_part, (WT*)dw, P, N);
   if (db_part) colsum_kernel<WT><<<g2, 256, 0, st>>>(db_part, (WT*)db, P, N);
 }

@@ -156,11 +156,17 @@ __global__ __launch_bounds__(kOptBlock) void sqnorm_mt_kernel(const TensorMeta* 
     const int t = find_tensor(prefix, T, c);
     const TensorMeta mt = meta[t];
     const long base = (c - prefix[t]) * (long)kChunk;
-    for (int it = 0; it < kChunk / kOptBlock; ++it) {
-      const long i = base + it * kOptBlock + threadIdx.x;
+#pragma unroll 2
+    for (int it = 0; it < kChunk / (kOptBlock * 4); ++it) {
+      const long i = base + ((long)it * kOptBlock + threadIdx.x) * 4;
       if (i >= mt.n) break;
-      const float v = ldg_<GT>(mt.g, i);
-      acc += v * v;
+      if (i + 4 <= mt.n) {
+        float v[4];
+        ld4<GT>(mt.g, i, v);
+        acc += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+      } else {
+        for (long k = i; k < mt.n; ++k) { const float v = ldg_<GT>(mt.g, k); acc += v * v; }
+      }
     }
   }
   acc = wave_sum(acc);

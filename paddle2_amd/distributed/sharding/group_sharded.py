@@ -393,7 +393,7 @@ class GroupShardedOptimizer:
     def _global_sq_norm(self):
         sq = torch.zeros(1, dtype=torch.float32, device=self._model._units[0].device)
         for u in self._model._units:
-            sq += (u.grad_shard * u.grad_shard).sum()
+            sq += torch.dot(u.grad_shard, u.grad_shard)
         g = self._model._group
         if g.nranks > 1:
             dist.all_reduce(sq, group=g.pg)
@@ -404,11 +404,10 @@ class GroupShardedOptimizer:
         inner = self._inner
         inner._step += 1
         clip = inner._grad_clip
+        coef = None
         if clip is not None and hasattr(clip, "clip_norm"):
             norm = torch.sqrt(self._global_sq_norm())
-            coef = torch.clamp(clip.clip_norm / torch.clamp(norm, min=1e-6), max=1.0)
-            for u in self._model._units:
-                u.grad_shard.mul_(coef)
+            coef = torch.clamp(clip.clip_norm / torch.clamp(norm, min=1e-6), max=1.0).float().reshape(1)
         lr = inner.get_lr()
         b1, b2 = getattr(inner, "_beta1", 0.9), getattr(inner, "_beta2", 0.999)
         eps = getattr(inner, "_epsilon", 1e-8)
@@ -449,9 +448,13 @@ class GroupShardedOptimizer:
                 self._table = ("ref", list(zip(params, grads, ms, vs, masters, lrrs, decs)))
         kind, tabs = self._table
         if kind == "native":
+            # clip coefficient folded into the fused AdamW pass (device scalar, no extra grad pass)
             for t in tabs:
-                t.adamw(lr, b1, b2, eps, bc1, bc2, getattr(inner, "_found_inf", None))
+                t.adamw(lr, b1, b2, eps, bc1, bc2, getattr(inner, "_found_inf", None), coef)
         else:
+            if coef is not None:
+                for u in self._model._units:
+                    u.grad_shard.mul_(coef)
             for (p, g, m, v, mw, lrr, dec) in tabs:
                 m.mul_(b1).add_(g, alpha=1 - b1)
                 v.mul_(b2).addcmul_(g, g, value=1 - b2)

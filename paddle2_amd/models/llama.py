@@ -141,15 +141,17 @@ class LlamaAttention(nn.Layer):
     def forward(self, x, position_ids=None):
         b, s = x.shape[0], x.shape[1]
         nh, nkv, d = self.num_heads, self.num_kv, self.head_dim
+        cos, sin = self.rope.tables(x._t.device, s)
+        pos = None if position_ids is None else position_ids._t
         if self.config.fuse_attention_qkv:
+            # one autograd node: strided q/k/v views -> RoPE -> flash attention; backward fills one dQKV
             qkv = self.qkv_proj(x)._t.view(b, s, nh + 2 * nkv, d)
-            q, k, v = qkv[:, :, :nh], qkv[:, :, nh:nh + nkv], qkv[:, :, nh + nkv:]
+            o = T.qkv_rope_attention(qkv, nh, nkv, cos, sin, pos, causal=True)
+            return self.o_proj(_wrap(o.reshape(b, s, nh * d)))
         else:
             q = self.q_proj(x)._t.view(b, s, nh, d)
             k = self.k_proj(x)._t.view(b, s, nkv, d)
             v = self.v_proj(x)._t.view(b, s, nkv, d)
-        cos, sin = self.rope.tables(q.device, s)
-        pos = None if position_ids is None else position_ids._t
         q = T.rope(q, cos, sin, pos, style=0)
         k = T.rope(k, cos, sin, pos, style=0)
         o, _ = T.flash_attention(q, k, v, causal=True)

@@ -61,6 +61,21 @@ class ClipGradByGlobalNorm(ClipGradBase):
             return self._cache[1].sqnorm()
         return sum((g.float() ** 2).sum() for g in grads)
 
+    # The fused optimizers take the clip coefficient as a device scalar and fold it into their
+    # single pass over the gradients (no separate scale pass over 2x the grad bytes).
+    _fusable = True
+
+    def global_coef(self, params_grads):
+        """Device fp32 [1] tensor min(1, clip_norm / ||g||) over clippable grads (no host sync)."""
+        grads = [g._t for p, g in params_grads if g is not None and getattr(p, "need_clip", True)]
+        if not grads:
+            return None
+        if len(grads) != len(params_grads):
+            return None  # some grads excluded from clipping: fall back to the explicit scale pass
+        sq = self._reduce_global(self._global_sq_norm(grads))
+        norm = torch.sqrt(sq)
+        return torch.clamp(self.clip_norm / torch.clamp(norm, min=1e-6), max=1.0).float().reshape(1)
+
     def _dygraph_clip(self, params_grads):
         grads = [g._t for p, g in params_grads if g is not None and getattr(p, "need_clip", True)]
         if not grads:

@@ -223,17 +223,29 @@ class _RopeFn(torch.autograd.Function):
         return _rope_apply(g, cos, sin, pos, ctx.style, ctx.tm, True), None, None, None, None, None
 
 
-def _rope_apply(x, cos, sin, pos, style, time_major, bwd):
-    xc = x.contiguous()
+def _tok_view_ok(t):
+    """[A, B, H, D] with unit stride on D, stride D on H and uniform token stride (A*B tokens)."""
+    st = t.stride()
+    return st[3] == 1 and st[2] == t.shape[3] and st[0] == t.shape[1] * st[1]
+
+
+def _rope_apply(x, cos, sin, pos, style, time_major, bwd, out=None):
+    """Rotate x ([B,S,H,D] or time-major); x and ``out`` may be token-strided views."""
     if time_major:
-        S, B, Hn, D = xc.shape
+        S, B, Hn, D = x.shape
     else:
-        B, S, Hn, D = xc.shape
+        B, S, Hn, D = x.shape
     if N.use_native(x) and x.dtype in _DT:
+        xc = x if _tok_view_ok(x) else x.contiguous()
         C = N.native()
-        out = torch.empty_like(xc)
+        if out is None:
+            out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
         C.rope(_DT[x.dtype], style, int(bwd), xc.data_ptr(), out.data_ptr(), cos.data_ptr(), sin.data_ptr(),
-               N.ptr(pos), B, S, Hn, D, int(time_major), N.stream())
+               N.ptr(pos), B, S, Hn, D, int(time_major), xc.stride(1), out.stride(1), N.stream())
+        return out
+    xc = x.contiguous()
+    if out is not None:
+        out.copy_(_rope_apply(xc, cos, sin, pos, style, time_major, bwd))
         return out
     # reference
     xf = xc.float()
@@ -448,10 +460,7 @@ class _FlashFn(torch.autograd.Function):
             if not _row_view_ok(out):
                 out = out.contiguous()
             assert out.stride(1) == do.stride(1), "out/dout row strides must match"
-            N.native().flash_bwd(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), do.data_ptr(),
-                                 lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
-                                 dq32.data_ptr(), B, Sq, Sk, Hq, Hk, D, q.stride(1), k.stride(1), v.stride(1),
-                                 do.stride(1), float(ctx.scale), int(ctx.causal), N.stream())
+            _flash_bwd_native(q, k, v, out, do, lse, dq, dk, dv, ctx.scale, ctx.causal)
             return dq, dk, dv, None, None
         with torch.enable_grad():
             qq = q.detach().float().requires_grad_(True)
@@ -467,3 +476,79 @@ def flash_attention(q, k, v, causal=False, scale=None):
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
     return _FlashFn.apply(q, k, v, bool(causal), float(scale))
+
+
+def _flash_fwd_native(q, k, v, causal, scale):
+    B, Sq, Hq, D = q.shape
+    Sk, Hk = k.shape[1], k.shape[2]
+    out = torch.empty(B, Sq, Hq, D, dtype=q.dtype, device=q.device)
+    lse = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
+    N.native().flash_fwd(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr(), B, Sq, Sk, Hq,
+                         Hk, D, q.stride(1), k.stride(1), v.stride(1), out.stride(1), float(scale), int(causal),
+                         N.stream())
+    return out, lse
+
+
+def _flash_bwd_native(q, k, v, out, do, lse, dq, dk, dv, scale, causal):
+    """dq/dk/dv may be token-strided views (e.g. slices of a dQKV buffer)."""
+    B, Sq, Hq, D = q.shape
+    Sk, Hk = k.shape[1], k.shape[2]
+    dq32 = torch.zeros(B, Sq, Hq, D, dtype=torch.float32, device=q.device)
+    delta = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
+    N.native().flash_bwd(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), do.data_ptr(), lse.data_ptr(),
+                         delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dq32.data_ptr(), B, Sq, Sk,
+                         Hq, Hk, D, q.stride(1), k.stride(1), v.stride(1), do.stride(1), dq.stride(1), dk.stride(1),
+                         dv.stride(1), float(scale), int(causal), N.stream())
+
+
+class _QKVRopeAttnFn(torch.autograd.Function):
+    """Fused QKV split -> RoPE(q, k) -> causal flash attention, one autograd node.
+
+    Forward reads q/k/v straight out of the fused projection output ``qkv`` [B, S, Hq+2Hk, D]
+    (token-strided views, no split copies); backward writes dV, RoPE^T(dQ), RoPE^T(dK) straight
+    into a single dQKV buffer — no zero-fill + slice-add of per-view gradients.
+    """
+
+    @staticmethod
+    def forward(ctx, qkv, nh, nkv, cos, sin, pos, causal, scale):
+        B, S, _, D = qkv.shape
+        q_in = qkv[:, :, :nh]
+        k_in = qkv[:, :, nh:nh + nkv]
+        v = qkv[:, :, nh + nkv:]
+        q = _rope_apply(q_in, cos, sin, pos, 0, False, False)
+        k = _rope_apply(k_in, cos, sin, pos, 0, False, False)
+        out, lse = _flash_fwd_native(q, k, v, causal, scale)
+        ctx.save_for_backward(q, k, qkv, out, lse, cos, sin, pos)
+        ctx.meta = (nh, nkv, causal, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, qkv, out, lse, cos, sin, pos = ctx.saved_tensors
+        nh, nkv, causal, scale = ctx.meta
+        v = qkv[:, :, nh + nkv:]
+        dqkv = torch.empty_like(qkv)
+        dq = torch.empty_like(q)
+        dk = torch.empty_like(k)
+        _flash_bwd_native(q, k, v, out, dout.contiguous(), lse, dq, dk, dqkv[:, :, nh + nkv:], scale, causal)
+        _rope_apply(dq, cos, sin, pos, 0, False, True, out=dqkv[:, :, :nh])
+        _rope_apply(dk, cos, sin, pos, 0, False, True, out=dqkv[:, :, nh:nh + nkv])
+        return dqkv, None, None, None, None, None, None, None
+
+
+def qkv_rope_attention(qkv, num_heads, num_kv_heads, cos, sin, position_ids=None, causal=True, scale=None):
+    """qkv [B, S, Hq+2Hk, D] (fused projection output) -> attention output [B, S, Hq, D]."""
+    D = qkv.shape[-1]
+    if scale is None:
+        scale = 1.0 / math.sqrt(D)
+    native = (qkv.device.type == "cuda" and N.use_native(qkv) and qkv.dtype == torch.bfloat16 and D in (64, 128)
+              and num_heads % num_kv_heads == 0)
+    cos = cos.reshape(-1, D).float().contiguous()
+    sin = sin.reshape(-1, D).float().contiguous()
+    pos = None if position_ids is None else position_ids.to(torch.int64).contiguous()
+    if native:
+        return _QKVRopeAttnFn.apply(qkv, num_heads, num_kv_heads, cos, sin, pos, bool(causal), float(scale))
+    q = rope(qkv[:, :, :num_heads], cos, sin, pos, 0)
+    k = rope(qkv[:, :, num_heads:num_heads + num_kv_heads], cos, sin, pos, 0)
+    o, _ = flash_attention(q, k, qkv[:, :, num_heads + num_kv_heads:], causal, scale)
+    return o

@@ -134,11 +134,20 @@ class Optimizer:
         return None
 
     # ------------------------------------------------------------ step
+    _fused_clip = False  # optimizers that consume a device-side clip coefficient in their update pass
+
     @torch.no_grad()
     def step(self):
         pg = self._params_grads()
+        self._clip_coef = None
         if self._grad_clip is not None and pg:
-            pg = self._grad_clip(pg)
+            if self._fused_clip and getattr(self._grad_clip, "_fusable", False) and all(
+                    g._t.device.type == "cuda" for _, g in pg):
+                self._clip_coef = self._grad_clip.global_coef(pg)
+                if self._clip_coef is None:
+                    pg = self._grad_clip(pg)
+            else:
+                pg = self._grad_clip(pg)
         self._step += 1
         if pg:
             self._apply(pg)
@@ -261,6 +270,16 @@ class Adam(Optimizer):
     """Adam with L2 ``weight_decay`` folded into the gradient (paddle semantics)."""
 
     _decoupled = False
+    _fused_clip = True
+
+    def _grad_mult(self):
+        """Device scalar multiplying every gradient in the update: AMP 1/scale x global-norm clip coef."""
+        a, b = self._inv_scale, getattr(self, "_clip_coef", None)
+        if a is None:
+            return b
+        if b is None:
+            return a
+        return a * b
 
     def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8, parameters=None, weight_decay=None,
                  grad_clip=None, lazy_mode=False, multi_precision=False, use_multi_tensor=False, amsgrad=False,
@@ -271,6 +290,8 @@ class Adam(Optimizer):
         self._amsgrad = amsgrad
         self._found_inf = None   # set by GradScaler for fused skip
         self._inv_scale = None
+        # L2 regularisation is added after clipping in Paddle, so it cannot share the fused multiplier
+        self._fused_clip = weight_decay is None
 
     # per-parameter decoupled-decay coefficient and lr ratio
     def _decay_of(self, p):
@@ -298,8 +319,9 @@ class Adam(Optimizer):
         m1 = self._acc("moment1", p)
         m2 = self._acc("moment2", p)
         gf = g.float()
-        if self._inv_scale is not None:
-            gf = gf * self._inv_scale
+        mult = self._grad_mult()
+        if mult is not None:
+            gf = gf * mult.to(gf.device)
         m1.mul_(b1).add_(gf, alpha=1 - b1)
         m2.mul_(b2).addcmul_(gf, gf, value=1 - b2)
         lr_t = lr * self._lr_ratio_of(p)
@@ -344,9 +366,10 @@ class Adam(Optimizer):
                 dec = [self._decay_of(p) for p, g, m in items]
                 tables.append(("mt", MultiTensorTable(ps, gs, m1, m2, ms, lrr, dec)))
             self._mt_cache = (key, tables)
+        mult = self._grad_mult()
         for kind, tab in self._mt_cache[1]:
             if kind == "mt":
-                tab.adamw(lr, b1, b2, self._epsilon, bc1, bc2, self._found_inf, self._inv_scale)
+                tab.adamw(lr, b1, b2, self._epsilon, bc1, bc2, self._found_inf, mult)
             else:
                 for p, g, m in tab:
                     self._apply_ref(p, g._t, lr, b1, b2, bc1, bc2)

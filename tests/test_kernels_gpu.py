@@ -233,3 +233,18 @@ def test_grad_scaler_unscale_and_skip():
     sc.update()
     assert torch.equal(before, p._t)
     assert float(sc._scale) == 1024.0 or float(sc._scale) == 512.0
+
+
+@pytest.mark.parametrize("nh,nkv", [(4, 4), (4, 2)])
+def test_qkv_rope_attention_fused(nh, nkv):
+    """Fused QKV->RoPE->flash node (strided views, one dQKV buffer) vs. fp32 CPU reference."""
+    B, S, D = 2, 160, 128
+    cos, sin = T.rope_tables(256, D, 10000.0, interleaved=False)
+    xg, xc = _pair((B, S, nh + 2 * nkv, D), torch.bfloat16, seed=21)
+    og = T.qkv_rope_attention(xg, nh, nkv, cos.to(DEV), sin.to(DEV), causal=True)
+    oc = T.qkv_rope_attention(xc.to(torch.bfloat16).float(), nh, nkv, cos, sin, causal=True)
+    _close(og, oc, 2e-2, 2e-2)
+    go = torch.randn(oc.shape)
+    og.backward(go.to(DEV, torch.bfloat16))
+    oc.backward(go.to(torch.bfloat16).float())
+    _close(xg.grad, xc.grad, 5e-2, 3e-2)
