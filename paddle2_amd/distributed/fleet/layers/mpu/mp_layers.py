@@ -1,0 +1,153 @@
+"""Tensor-parallel layers (reference: fleet/layers/mpu/mp_layers.py — ``VocabParallelEmbedding`` :49,
+``ColumnParallelLinear`` :336, ``RowParallelLinear`` :543, ``ParallelCrossEntropy`` :744).
+
+Weights are stored Paddle-style ([in, out]) and already sharded: column-parallel shards the
+output dim, row-parallel the input dim, vocab-parallel the vocab rows.  Distributed params carry
+``is_distributed=True`` / ``split_axis`` so the hybrid optimizer and checkpoint code know they
+are not replicated.  Shard initialisation draws from the tracker's ``model_parallel_rng`` state
+so shards differ across the mp group while replicated params match.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+
+from ..... import nn
+from .....framework.tensor import Tensor
+from .....nn import initializer as I
+from . import mp_ops
+from .random import MODEL_PARALLEL_RNG, get_rng_state_tracker
+
+_wrap = Tensor._wrap
+
+
+def _mp_info(mp_group):
+    if mp_group is not None:
+        return mp_group, mp_group.nranks, max(mp_group.rank, 0)
+    from .... import fleet
+
+    hcg = fleet.get_hybrid_communicate_group()
+    if hcg is None:
+        return None, 1, 0
+    return hcg.get_model_parallel_group(), hcg.get_model_parallel_world_size(), hcg.get_model_parallel_rank()
+
+
+def _init_ctx(world):
+    tr = get_rng_state_tracker()
+    if world > 1 and MODEL_PARALLEL_RNG in tr.states_:
+        return tr.rng_state(MODEL_PARALLEL_RNG)
+    return contextlib.nullcontext()
+
+
+class VocabParallelEmbedding(nn.Layer):
+    def __init__(self, num_embeddings, embedding_dim, weight_attr=None, mp_group=None, name=None):
+        super().__init__()
+        self.model_parallel_group, self.world_size, self.rank = _mp_info(mp_group)
+        self.origin_num_embeddings = num_embeddings
+        self.is_mp = self.world_size > 1
+        assert num_embeddings % self.world_size == 0, "vocab size must be divisible by mp degree"
+        per = num_embeddings // self.world_size
+        self.vocab_start_index = self.rank * per
+        self._dtype = self._helper_dtype()
+        with _init_ctx(self.world_size):
+            self.weight = self.create_parameter([per, embedding_dim], attr=weight_attr, dtype=self._dtype,
+                                                default_initializer=I.XavierNormal())
+        self.weight.is_distributed = self.is_mp
+        self.weight.split_axis = 0
+
+    @staticmethod
+    def _helper_dtype():
+        from .....framework.dtype import get_default_dtype
+
+        return get_default_dtype()
+
+    def forward(self, x):
+        out = mp_ops._c_lookup_table(self.weight, x, start_index=self.vocab_start_index)
+        if self.is_mp:
+            out = mp_ops._mp_allreduce(out, group=self.model_parallel_group)
+        return out
+
+
+class ColumnParallelLinear(nn.Layer):
+    def __init__(self, in_features, out_features, weight_attr=None, has_bias=None, gather_output=True,
+                 fuse_matmul_bias=False, mp_group=None, name=None):
+        super().__init__()
+        self.model_parallel_group, self.world_size, self.rank = _mp_info(mp_group)
+        self.is_mp = self.world_size > 1
+        assert out_features % self.world_size == 0, "out_features must be divisible by mp degree"
+        self.output_size_per_partition = out_features // self.world_size
+        self.gather_output = gather_output
+        self.in_features, self.out_features = in_features, out_features
+        dt = VocabParallelEmbedding._helper_dtype()
+        with _init_ctx(self.world_size):
+            self.weight = self.create_parameter([in_features, self.output_size_per_partition], attr=weight_attr,
+                                                dtype=dt, default_initializer=I.XavierUniform())
+        self.weight.is_distributed = self.is_mp
+        self.weight.split_axis = 1
+        if has_bias is None or has_bias:
+            self.bias = self.create_parameter([self.output_size_per_partition], dtype=dt, is_bias=True,
+                                              default_initializer=I.Constant(0.0))
+            self.bias.is_distributed = self.is_mp
+            self.bias.split_axis = 0
+        else:
+            self.bias = None
+
+    def forward(self, x):
+        b = None if self.bias is None else self.bias._t
+        if self.is_mp:
+            y = mp_ops._ColumnLinear.apply(x._t, self.weight._t, b, self.model_parallel_group)
+        else:
+            y = torch.matmul(x._t, self.weight._t)
+            if b is not None:
+                y = y + b
+        out = _wrap(y)
+        if self.gather_output and self.is_mp:
+            out = mp_ops._c_concat(out, group=self.model_parallel_group)
+        return out
+
+
+class RowParallelLinear(nn.Layer):
+    def __init__(self, in_features, out_features, weight_attr=None, has_bias=True, input_is_parallel=False,
+                 fuse_matmul_bias=False, mp_group=None, name=None):
+        super().__init__()
+        self.model_parallel_group, self.world_size, self.rank = _mp_info(mp_group)
+        self.is_mp = self.world_size > 1
+        assert in_features % self.world_size == 0, "in_features must be divisible by mp degree"
+        self.input_size_per_partition = in_features // self.world_size
+        self.input_is_parallel = input_is_parallel
+        self.in_features, self.out_features = in_features, out_features
+        dt = VocabParallelEmbedding._helper_dtype()
+        with _init_ctx(self.world_size):
+            self.weight = self.create_parameter([self.input_size_per_partition, out_features], attr=weight_attr,
+                                                dtype=dt, default_initializer=I.XavierUniform())
+        self.weight.is_distributed = self.is_mp
+        self.weight.split_axis = 0
+        self.bias = self.create_parameter([out_features], dtype=dt, is_bias=True,
+                                          default_initializer=I.Constant(0.0)) if has_bias else None
+
+    def forward(self, x):
+        if self.is_mp and not self.input_is_parallel:
+            x = mp_ops._c_split(x, group=self.model_parallel_group)
+        y = _wrap(torch.matmul(x._t, self.weight._t))
+        if self.is_mp:
+            y = mp_ops._mp_allreduce(y, group=self.model_parallel_group)
+        if self.bias is not None:
+            y = _wrap(y._t + self.bias._t)
+        return y
+
+
+class ParallelCrossEntropy(nn.Layer):
+    """Softmax CE over vocab-sharded logits (per-token loss, shape [..., 1] like the reference)."""
+
+    def __init__(self, mp_group=None, name=None, ignore_index=-100):
+        super().__init__()
+        self.model_parallel_group, self.world_size, self.rank = _mp_info(mp_group)
+        self.ignore_index = ignore_index
+
+    def forward(self, input, label):
+        lab = label._t
+        if lab.dim() == input._t.dim():
+            lab = lab.squeeze(-1)
+        loss = mp_ops._VocabParallelCE.apply(input._t, lab, self.model_parallel_group, self.ignore_index)
+        return _wrap(loss.unsqueeze(-1))

@@ -1,0 +1,257 @@
+"""Hybrid-parallel optimizer wrappers.
+
+Reference: fleet/meta_optimizers/dygraph_optimizer/hybrid_parallel_optimizer.py —
+``HybridParallelClipGrad`` :42 (global norm over check/mp/pp/sharding groups),
+``HybridParallelOptimizer`` :266 (``_hybrid_sync_grad`` :509: sharding reduce, then dp/sep fused
+all-reduce), and dygraph_sharding_optimizer.py:54 ``DygraphShardingOptimizer`` (stage 1: params
+partitioned to owner ranks :250, grads reduced to owners :320-369, owners step and broadcast
+:378-444).
+
+MI355X design of sharding stage 1: parameters are partitioned greedily by size so every rank owns
+≈1/N of the bytes; each step packs all grads owner-by-owner into ONE padded flat buffer and runs
+a single ``reduce_scatter_tensor`` (each owner receives exactly its region, averaged) instead of
+one ``reduce`` per owner, then a single ``all_gather_into_tensor`` redistributes the updated
+params — two large collectives per dtype per step, which is what a per-link-bound xGMI ring wants.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .....framework.tensor import Tensor
+from .....nn.clip import ClipGradByGlobalNorm
+from ...utils.hybrid_parallel_util import _grad_tensor, fused_allreduce_gradients, \
+    fused_allreduce_gradients_with_group
+
+_wrap = Tensor._wrap
+
+
+class HybridParallelClipGrad(ClipGradByGlobalNorm):
+    """Global-norm clip whose norm spans the whole hybrid-parallel model.
+
+    sum-of-squares of mp-distributed grads is all-reduced over the mp group, replicated grads are
+    counted once, then the total is all-reduced over the pp group (different layers) and, when the
+    optimizer is sharded, over the sharding group (different owned params)."""
+
+    def __init__(self, clip, hcg, sharded=False):
+        super().__init__(clip.clip_norm)
+        self._clip = clip
+        self._hcg = hcg
+        self._sharded = sharded
+
+    def _total_sq(self, params_grads):
+        pgs = [(p, g._t) for p, g in params_grads if g is not None and getattr(p, "need_clip", True)]
+        if not pgs:
+            return None
+        dev = pgs[0][1].device
+        dist_g = [g for p, g in pgs if getattr(p, "is_distributed", False)]
+        rep_g = [g for p, g in pgs if not getattr(p, "is_distributed", False)]
+        total = torch.zeros(1, dtype=torch.float32, device=dev)
+        hcg = self._hcg
+        if dist_g:
+            sq = self._sq_norm(dist_g).reshape(1).float()
+            mp = hcg.get_model_parallel_group()
+            if mp is not None and mp.nranks > 1:
+                dist.all_reduce(sq, group=mp.pg)
+            total = total + sq
+        if rep_g:
+            total = total + self._sq_norm(rep_g).reshape(1).float()
+        pp = hcg.get_pipe_parallel_group()
+        if pp is not None and pp.nranks > 1:
+            dist.all_reduce(total, group=pp.pg)
+        if self._sharded:
+            sh = hcg.get_sharding_parallel_group()
+            if sh is not None and sh.nranks > 1:
+                dist.all_reduce(total, group=sh.pg)
+        return total
+
+
+class DygraphShardingOptimizer:
+    """ZeRO stage 1 over the hcg sharding group."""
+
+    def __init__(self, optimizer, hcg):
+        self._inner_opt = optimizer
+        self._hcg = hcg
+        self._group = hcg.get_sharding_parallel_group()
+        self._nranks = self._group.nranks
+        self._rank = self._group.rank
+        self._all_params = list(optimizer._parameter_list)
+        self._rank2params = self._partition_parameters()
+        self._param2rank = {id(p): r for r, ps in self._rank2params.items() for p in ps}
+        owned = set(id(p) for p in self._rank2params[self._rank])
+        for g in optimizer._param_groups:
+            g["params"] = [p for p in g["params"] if id(p) in owned]
+        optimizer._parameter_list = [p for g in optimizer._param_groups for p in g["params"]]
+        optimizer._mt_cache = None
+        self._layouts = self._build_layouts()
+
+    def _partition_parameters(self):
+        sizes = [0] * self._nranks
+        mapping = {r: [] for r in range(self._nranks)}
+        for p in sorted(self._all_params, key=lambda q: -q._t.numel()):
+            r = min(range(self._nranks), key=lambda i: sizes[i])
+            mapping[r].append(p)
+            sizes[r] += p._t.numel()
+        # keep each owner's list in model order (deterministic on every rank)
+        order = {id(p): i for i, p in enumerate(self._all_params)}
+        for r in mapping:
+            mapping[r].sort(key=lambda q: order[id(q)])
+        return mapping
+
+    def _build_layouts(self):
+        """Per (dtype, device): region size R and [(param, owner, offset-in-region)]."""
+        lay = {}
+        for r, ps in self._rank2params.items():
+            for p in ps:
+                key = (p._t.dtype, p._t.device)
+                d = lay.setdefault(key, {"sizes": [0] * self._nranks, "items": []})
+                d["items"].append((p, r, d["sizes"][r]))
+                d["sizes"][r] += p._t.numel()
+        for d in lay.values():
+            d["R"] = max(d["sizes"]) if d["sizes"] else 0
+        return lay
+
+    def _flat(self, key, d, getter):
+        t = torch.zeros(self._nranks * d["R"], dtype=key[0], device=key[1])
+        for p, r, off in d["items"]:
+            src = getter(p)
+            if src is not None:
+                t[r * d["R"] + off: r * d["R"] + off + p._t.numel()].copy_(src.reshape(-1))
+        return t
+
+    def reduce_gradients(self, parameter_list=None, hcg=None):
+        if self._nranks <= 1:
+            return
+        for key, d in self._layouts.items():
+            gdt = None
+            for p, r, off in d["items"]:
+                g = _grad_tensor(p)
+                if g is not None:
+                    gdt = g.dtype
+                    break
+            if gdt is None:
+                continue
+            full = self._flat((gdt, key[1]), d, _grad_tensor)
+            mine = torch.empty(d["R"], dtype=gdt, device=key[1])
+            if self._group.backend == "nccl":
+                dist.reduce_scatter_tensor(mine, full, op=dist.ReduceOp.AVG, group=self._group.pg)
+            else:
+                dist.reduce_scatter_tensor(mine, full, group=self._group.pg)
+                mine.div_(self._nranks)
+            for p, r, off in d["items"]:
+                if r != self._rank:
+                    continue
+                g = _grad_tensor(p)
+                if g is None:
+                    g = torch.zeros_like(p._t)
+                    p._t.grad = g
+                g.copy_(mine[off: off + p._t.numel()].view_as(g))
+
+    def _sharding_sync_parameters(self):
+        if self._nranks <= 1:
+            return
+        for key, d in self._layouts.items():
+            mine = torch.zeros(d["R"], dtype=key[0], device=key[1])
+            for p, r, off in d["items"]:
+                if r == self._rank:
+                    mine[off: off + p._t.numel()].copy_(p._t.reshape(-1))
+            full = torch.empty(self._nranks * d["R"], dtype=key[0], device=key[1])
+            dist.all_gather_into_tensor(full, mine, group=self._group.pg)
+            with torch.no_grad():
+                for p, r, off in d["items"]:
+                    if r != self._rank:
+                        p._t.copy_(full[r * d["R"] + off: r * d["R"] + off + p._t.numel()].view_as(p._t))
+
+    @torch.no_grad()
+    def step(self):
+        self._inner_opt.step()
+        self._sharding_sync_parameters()
+
+    def clear_grad(self, set_to_zero=True):
+        for p in self._all_params:
+            if getattr(p, "main_grad", None) is not None:
+                if set_to_zero:
+                    (p.main_grad._t if isinstance(p.main_grad, Tensor) else p.main_grad).zero_()
+                else:
+                    p.main_grad = None
+            if p._t.grad is not None:
+                if set_to_zero:
+                    p._t.grad.zero_()
+                else:
+                    p._t.grad = None
+
+    clear_gradients = clear_grad
+
+    def __getattr__(self, name):
+        return getattr(self._inner_opt, name)
+
+
+class HybridParallelOptimizer:
+    def __init__(self, optimizer, hcg, strategy):
+        self._hcg = hcg
+        self._strategy = strategy
+        self._sharding = hcg.get_sharding_parallel_world_size() > 1
+        self._inner_opt = DygraphShardingOptimizer(optimizer, hcg) if self._sharding else optimizer
+        self._base_opt = optimizer
+        clip = optimizer._grad_clip
+        if isinstance(clip, ClipGradByGlobalNorm) and not isinstance(clip, HybridParallelClipGrad):
+            optimizer._grad_clip = HybridParallelClipGrad(clip, hcg, sharded=self._sharding)
+        self._all_params = list(self._inner_opt._all_params) if self._sharding else list(optimizer._parameter_list)
+        self._dp_enable = hcg.get_data_parallel_world_size() > 1
+        self._sep_enable = hcg.get_sep_parallel_world_size() > 1
+
+    def _sp_params(self):
+        return [p for p in self._all_params if getattr(p, "sequence_parallel", False)]
+
+    def _hybrid_sync_grad(self):
+        hcg = self._hcg
+        sp = self._sp_params()
+        if sp and hcg.get_model_parallel_world_size() > 1:
+            # SP params (norm weights/biases) see only the local sequence shard: sum over mp
+            grads = [_grad_tensor(p) for p in sp]
+            mp = hcg.get_model_parallel_group()
+            for g in grads:
+                if g is not None:
+                    dist.all_reduce(g, group=mp.pg)
+        if self._sharding:
+            self._inner_opt.reduce_gradients(self._all_params, hcg)
+            if self._dp_enable or self._sep_enable:
+                owned = self._inner_opt._rank2params[self._inner_opt._rank]
+                fused_allreduce_gradients(owned, hcg)
+        elif self._dp_enable or self._sep_enable:
+            fused_allreduce_gradients(self._all_params, hcg)
+
+    @torch.no_grad()
+    def step(self):
+        self._hybrid_sync_grad()
+        self._inner_opt.step()
+
+    def minimize(self, loss, startup_program=None, parameters=None, no_grad_set=None):
+        self.step()
+        return None, None
+
+    def clear_grad(self, set_to_zero=True):
+        self._inner_opt.clear_grad(set_to_zero)
+
+    clear_gradients = clear_grad
+
+    def state_dict(self):
+        return self._base_opt.state_dict()
+
+    def set_state_dict(self, sd):
+        return self._base_opt.set_state_dict(sd)
+
+    def get_lr(self):
+        return self._base_opt.get_lr()
+
+    def set_lr(self, v):
+        return self._base_opt.set_lr(v)
+
+    @property
+    def _parameter_list(self):
+        return self._all_params
+
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+        return getattr(self._base_opt, name)

@@ -34,8 +34,8 @@ def sync_params_buffers(model, comm_group=None, src_rank=0, is_model_parallel=Fa
     g = comm_group or C._get_default_group()
     if g.nranks <= 1:
         return
-    tensors = [p._t for p in model.parameters()] + [b._t for b in model.buffers()]
-    tensors = [t for t in tensors if not getattr(t, "is_distributed", False)]
+    objs = list(model.parameters()) + list(model.buffers())
+    tensors = [o._t for o in objs if not (is_model_parallel and getattr(o, "is_distributed", False))]
     by_dt = {}
     for t in tensors:
         by_dt.setdefault((t.dtype, t.device), []).append(t)

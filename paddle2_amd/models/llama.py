@@ -15,9 +15,12 @@ RMSNorm).  MI355X mapping of every op:
 
 Tensor parallelism: when ``config.tensor_parallel_degree > 1`` the projections become
 Column/RowParallelLinear and the embedding / LM head vocab-parallel (paddle2_amd.distributed.fleet).
+Fused weights are laid out per mp rank: rank r's shard of ``qkv_proj`` is ``[q_r | k_r | v_r]`` and
+of ``gate_up_fused_proj`` is ``[gate_r | up_r]``, so the local views need no reshuffle.
 """
 from __future__ import annotations
 
+import contextlib
 import dataclasses
 import math
 
@@ -172,11 +175,7 @@ class LlamaMLP(nn.Layer):
 
     def forward(self, x):
         if self.config.fuse_attention_ffn:
-            gu = self.gate_up_fused_proj(x)._t
-            if self.config.tensor_parallel_degree > 1:
-                # column-sharded output is [gate_shard | up_shard] per rank already
-                pass
-            a = T.swiglu(gu)
+            a = T.swiglu(self.gate_up_fused_proj(x)._t)  # per-rank [gate_r | up_r]
         else:
             a = T.swiglu(self.gate_proj(x)._t, self.up_proj(x)._t)
         return self.down_proj(_wrap(a))
@@ -235,13 +234,28 @@ class LlamaLMHead(nn.Layer):
     def __init__(self, config):
         super().__init__()
         self.config = config
-        vocab = config.vocab_size // config.tensor_parallel_degree
-        self.weight = self.create_parameter([config.hidden_size, vocab], dtype=config.dtype,
-                                            default_initializer=I.Normal(0.0, config.initializer_range))
-        if config.tensor_parallel_degree > 1:
+        tp = config.tensor_parallel_degree
+        vocab = config.vocab_size // tp
+        self._mp_group = None
+        ctx = contextlib.nullcontext()
+        if tp > 1:
+            from ..distributed.fleet.layers.mpu.mp_layers import _init_ctx, _mp_info
+
+            self._mp_group = _mp_info(None)[0]
+            ctx = _init_ctx(tp)
+        with ctx:
+            self.weight = self.create_parameter([config.hidden_size, vocab], dtype=config.dtype,
+                                                default_initializer=I.Normal(0.0, config.initializer_range))
+        if tp > 1:
             self.weight.is_distributed = True
+            self.weight.split_axis = 1
 
     def forward(self, h):
+        if self._mp_group is not None:
+            # vocab-sharded logits; dX all-reduced over mp overlapping the dW GEMM
+            from ..distributed.fleet.layers.mpu.mp_ops import _ColumnLinear
+
+            return _wrap(_ColumnLinear.apply(h._t, self.weight._t, None, self._mp_group))
         return _wrap(torch.matmul(h._t, self.weight._t))
 
 

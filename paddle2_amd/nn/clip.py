@@ -47,19 +47,37 @@ class ClipGradByGlobalNorm(ClipGradBase):
     def __init__(self, clip_norm, group_name="default_group", auto_skip_clip=False):
         self.clip_norm = float(clip_norm)
         self.group_name = group_name
-        self._cache = None
+        self._tables = {}
 
-    def _global_sq_norm(self, grads):
-        """Sum of squares over all grads (fp32 device scalar)."""
+    def _table(self, grads):
+        """Cached multi-tensor table for a grad list (keyed on pointers/sizes; rebuilt if they move)."""
         from ..optimizer.multi_tensor import MultiTensorTable
 
-        dev = grads[0].device
-        if dev.type == "cuda":
-            key = tuple((g.data_ptr(), g.numel(), g.dtype) for g in grads)
-            if self._cache is None or self._cache[0] != key:
-                self._cache = (key, MultiTensorTable.for_grads(grads))
-            return self._cache[1].sqnorm()
-        return sum((g.float() ** 2).sum() for g in grads)
+        key = tuple((g.data_ptr(), g.numel(), g.dtype) for g in grads)
+        t = self._tables.get(key)
+        if t is None:
+            if len(self._tables) > 8:
+                self._tables.clear()
+            t = self._tables[key] = MultiTensorTable.for_grads(grads)
+        return t
+
+    def _sq_norm(self, grads):
+        """Sum of squares over ``grads`` (fp32 device scalar, one multi-tensor launch on GPU)."""
+        if not grads:
+            return None
+        if grads[0].device.type == "cuda":
+            return self._table(grads).sqnorm()
+        return sum((g.float() ** 2).sum() for g in grads).reshape(1)
+
+    def _total_sq(self, params_grads):
+        """Global sum of squares of all clippable grads (overridden by HybridParallelClipGrad)."""
+        grads = [g._t for p, g in params_grads if g is not None and getattr(p, "need_clip", True)]
+        sq = self._sq_norm(grads)
+        return None if sq is None else self._reduce_global(sq)
+
+    def _coef(self, sq):
+        norm = torch.sqrt(sq)
+        return torch.clamp(self.clip_norm / torch.clamp(norm, min=1e-6), max=1.0).float().reshape(1)
 
     # The fused optimizers take the clip coefficient as a device scalar and fold it into their
     # single pass over the gradients (no separate scale pass over 2x the grad bytes).
@@ -67,32 +85,26 @@ class ClipGradByGlobalNorm(ClipGradBase):
 
     def global_coef(self, params_grads):
         """Device fp32 [1] tensor min(1, clip_norm / ||g||) over clippable grads (no host sync)."""
-        grads = [g._t for p, g in params_grads if g is not None and getattr(p, "need_clip", True)]
-        if not grads:
-            return None
-        if len(grads) != len(params_grads):
+        n_clip = sum(1 for p, g in params_grads if g is not None and getattr(p, "need_clip", True))
+        if n_clip == 0 or n_clip != len(params_grads):
             return None  # some grads excluded from clipping: fall back to the explicit scale pass
-        sq = self._reduce_global(self._global_sq_norm(grads))
-        norm = torch.sqrt(sq)
-        return torch.clamp(self.clip_norm / torch.clamp(norm, min=1e-6), max=1.0).float().reshape(1)
+        sq = self._total_sq(params_grads)
+        return None if sq is None else self._coef(sq)
 
     def _dygraph_clip(self, params_grads):
         grads = [g._t for p, g in params_grads if g is not None and getattr(p, "need_clip", True)]
         if not grads:
             return params_grads
-        sq = self._global_sq_norm(grads)
-        sq = self._reduce_global(sq)
-        norm = torch.sqrt(sq)
-        coef = torch.clamp(self.clip_norm / torch.clamp(norm, min=1e-6), max=1.0).float().reshape(1)
+        coef = self._coef(self._total_sq(params_grads))
         if grads[0].device.type == "cuda":
-            self._cache[1].scale(coef)
+            self._table(grads).scale(coef)
         else:
             for g in grads:
                 g.mul_(coef.to(g.dtype))
         return params_grads
 
     def _reduce_global(self, sq):
-        """Hook for hybrid-parallel global norm (overridden by HybridParallelClipGrad)."""
+        """Hook for cross-rank norm reduction (overridden by hybrid-parallel clipping)."""
         return sq
 
 

@@ -1,0 +1,221 @@
+"""Rank worker for hybrid-parallel tests (TP / PP / sharding-1 / DP via fleet) on gloo.
+
+mode tp:   mp_degree=world; tiny Llama with TP layers trained 3 steps vs. a single-process model
+           built from the gathered shards.
+mode pp:   pp_degree=world; PipelineLayer MLP stack trained with 1F1B / FThenB / VPP vs. the same
+           stack run single-process with gradient accumulation.
+mode dpsh: dp=1, sharding_degree=world via fleet (DygraphShardingOptimizer) vs single process.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.environ.get("PYTHONPATH", "."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import paddle2_amd as paddle  # noqa: E402
+from paddle2_amd.distributed import fleet  # noqa: E402
+from paddle2_amd.distributed import collective as C  # noqa: E402
+from _dist import write_result  # noqa: E402
+
+mode = sys.argv[1]
+C.init_parallel_env()
+rank, world = C.get_rank(), C.get_world_size()
+steps = 3
+
+
+def gather_full(t, axis, group):
+    parts = [torch.empty_like(t) for _ in range(group.nranks)]
+    dist.all_gather(parts, t.contiguous(), group=group.pg)
+    return parts
+
+
+def run_tp():
+    from paddle2_amd.models import LlamaConfig, LlamaForCausalLM
+
+    strategy = fleet.DistributedStrategy()
+    strategy.hybrid_configs = {"dp_degree": 1, "mp_degree": world, "pp_degree": 1}
+    fleet.init(is_collective=True, strategy=strategy)
+    hcg = fleet.get_hybrid_communicate_group()
+    mpg = hcg.get_model_parallel_group()
+    cfg = LlamaConfig.tiny(dtype="float32", num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2,
+                           tensor_parallel_degree=world)
+    paddle.seed(3)
+    m = LlamaForCausalLM(cfg)
+    m = fleet.distributed_model(m)
+    # gather the initial shards into a single-process state dict
+    nh, nkv, d = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+    full = {}
+    for name, p in m._layers.named_parameters():
+        t = p._t.detach()
+        if not getattr(p, "is_distributed", False):
+            full[name] = t.clone()
+            continue
+        ax = p.split_axis
+        parts = gather_full(t, ax, mpg)
+        if "qkv_proj" in name:
+            ql, kl = nh // world * d, nkv // world * d
+            qs = [x[:, :ql] for x in parts]
+            ks = [x[:, ql:ql + kl] for x in parts]
+            vs = [x[:, ql + kl:] for x in parts]
+            full[name] = torch.cat(qs + ks + vs, 1)
+        elif "gate_up" in name:
+            h = parts[0].shape[1] // 2
+            full[name] = torch.cat([x[:, :h] for x in parts] + [x[:, h:] for x in parts], 1)
+        else:
+            full[name] = torch.cat(parts, ax)
+    opt = paddle.optimizer.AdamW(1e-2, parameters=m.parameters(), weight_decay=0.01,
+                                 grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    opt = fleet.distributed_optimizer(opt)
+    g = torch.Generator().manual_seed(5)
+    data = [torch.randint(0, cfg.vocab_size, (2, 17), generator=g) for _ in range(steps)]
+    losses = []
+    for s in range(steps):
+        ids = paddle.Tensor._wrap(data[s])
+        loss = m(ids[:, :-1], labels=ids[:, 1:])
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        losses.append(float(loss))
+    # reference
+    cfg1 = LlamaConfig.tiny(dtype="float32", num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2)
+    ref_m = LlamaForCausalLM(cfg1)
+    ref_m.set_state_dict({k: paddle.Tensor._wrap(v) for k, v in full.items()})
+    ref_o = paddle.optimizer.AdamW(1e-2, parameters=ref_m.parameters(), weight_decay=0.01,
+                                   grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    ref = []
+    for s in range(steps):
+        ids = paddle.Tensor._wrap(data[s])
+        loss = ref_m(ids[:, :-1], labels=ids[:, 1:])
+        loss.backward()
+        ref_o.step()
+        ref_o.clear_grad()
+        ref.append(float(loss))
+    write_result({"losses": losses, "ref": ref})
+
+
+class Blk(paddle.nn.Layer):
+    def __init__(self, h):
+        super().__init__()
+        self.l1 = paddle.nn.Linear(h, 2 * h)
+        self.l2 = paddle.nn.Linear(2 * h, h)
+
+    def forward(self, x):
+        return x + self.l2(paddle.nn.functional.gelu(self.l1(x)))
+
+
+class Head(paddle.nn.Layer):
+    def __init__(self, h, c):
+        super().__init__()
+        self.fc = paddle.nn.Linear(h, c)
+
+    def forward(self, x):
+        return self.fc(x)
+
+
+def run_pp(schedule, vpp):
+    from paddle2_amd.distributed.fleet.meta_parallel import LayerDesc, PipelineLayer
+
+    M = 4
+    strategy = fleet.DistributedStrategy()
+    strategy.hybrid_configs = {"dp_degree": 1, "mp_degree": 1, "pp_degree": world}
+    strategy.pipeline_configs = {"accumulate_steps": M, "micro_batch_size": 2}
+    fleet.init(is_collective=True, strategy=strategy)
+    H, Cn, L = 16, 5, 8
+    loss_fn = lambda out, lab: paddle.nn.functional.cross_entropy(out, lab)  # noqa: E731
+    descs = [LayerDesc(Blk, H) for _ in range(L)] + [LayerDesc(Head, H, Cn)]
+    paddle.seed(11)
+    # build the full stack once (same RNG order on every rank) to get reference weights
+    ref_layers = [Blk(H) for _ in range(L)] + [Head(H, Cn)]
+    ref_sd = [l.state_dict() for l in ref_layers]
+    pl = PipelineLayer(descs, loss_fn=loss_fn, seg_method="uniform", num_virtual_pipeline_stages=vpp)
+    # copy reference weights into the locally built pieces
+    S = world
+    for c, vs in enumerate(pl._chunk_vstages):
+        lo = pl.segment_parts[vs]
+        for i, item in enumerate(pl._model_chunks[c]._items):
+            item.set_state_dict(ref_sd[lo + i])
+    model = fleet.distributed_model(pl)
+    if schedule == "FThenB":
+        from paddle2_amd.distributed.fleet.meta_parallel import PipelineParallelFThenB
+
+        model.__class__ = PipelineParallelFThenB
+    opt = paddle.optimizer.SGD(0.1, parameters=model.parameters())
+    opt = fleet.distributed_optimizer(opt)
+    g = torch.Generator().manual_seed(2)
+    xs = [torch.randn(M * 2, 3, H, generator=g) for _ in range(steps)]
+    ys = [torch.randint(0, Cn, (M * 2, 3), generator=g) for _ in range(steps)]
+    losses = []
+    for s in range(steps):
+        loss = model.train_batch([paddle.Tensor._wrap(xs[s]), paddle.Tensor._wrap(ys[s])], opt)
+        losses.append(float(loss))
+    # reference: plain gradient accumulation
+    seq = paddle.nn.Sequential(*ref_layers)
+    ro = paddle.optimizer.SGD(0.1, parameters=seq.parameters())
+    ref = []
+    for s in range(steps):
+        tot = 0.0
+        for mb in range(M):
+            x = paddle.Tensor._wrap(xs[s][mb * 2:(mb + 1) * 2])
+            y = paddle.Tensor._wrap(ys[s][mb * 2:(mb + 1) * 2])
+            l = loss_fn(seq(x), y) / M
+            l.backward()
+            tot += float(l)
+        ro.step()
+        ro.clear_grad()
+        ref.append(tot)
+    write_result({"losses": losses, "ref": ref})
+
+
+def run_dpsh():
+    from paddle2_amd.models import LlamaConfig, LlamaForCausalLM
+
+    strategy = fleet.DistributedStrategy()
+    strategy.hybrid_configs = {"dp_degree": 1, "mp_degree": 1, "pp_degree": 1, "sharding_degree": world}
+    fleet.init(is_collective=True, strategy=strategy)
+    cfg = LlamaConfig.tiny(dtype="float32", num_hidden_layers=2)
+
+    def make():
+        paddle.seed(7)
+        m = LlamaForCausalLM(cfg)
+        o = paddle.optimizer.AdamW(1e-2, parameters=m.parameters(), weight_decay=0.01,
+                                   grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
+        return m, o
+
+    g = torch.Generator().manual_seed(99)
+    data = [torch.randint(0, cfg.vocab_size, (world * 2, 33), generator=g) for _ in range(steps)]
+    m, o = make()
+    m = fleet.distributed_model(m)
+    o = fleet.distributed_optimizer(o)
+    losses = []
+    for s in range(steps):
+        ids = paddle.Tensor._wrap(data[s][rank * 2:(rank + 1) * 2])
+        loss = m(ids[:, :-1], labels=ids[:, 1:])
+        loss.backward()
+        o.step()
+        o.clear_grad()
+        t = loss._t.detach().clone()
+        C._all_reduce_torch(t)
+        losses.append(float(t) / world)
+    csum = float(sum(p._t.double().sum() for p in m.parameters()))
+    m2, o2 = make()
+    ref = []
+    for s in range(steps):
+        ids = paddle.Tensor._wrap(data[s])
+        loss = m2(ids[:, :-1], labels=ids[:, 1:])
+        loss.backward()
+        o2.step()
+        o2.clear_grad()
+        ref.append(float(loss))
+    csum_ref = float(sum(p._t.double().sum() for p in m2.parameters()))
+    write_result({"losses": losses, "ref": ref, "csum": csum, "csum_ref": csum_ref})
+
+
+if mode == "tp":
+    run_tp()
+elif mode == "pp":
+    run_pp(sys.argv[2], int(sys.argv[3]))
+elif mode == "dpsh":
+    run_dpsh()
