@@ -315,8 +315,9 @@ def all_gather(tensor_list, tensor, group=None, sync_op=True):
         tensor_list.clear()
         tensor_list.append(_wrap(t.clone()))
         return _Task(None)
-    out = torch.empty((g.nranks,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-    w = dist.all_gather_into_tensor(out, t.contiguous(), group=pg, async_op=not sync_op)
+    flat = torch.empty(g.nranks * t.numel(), dtype=t.dtype, device=t.device)
+    w = dist.all_gather_into_tensor(flat, t.contiguous().reshape(-1), group=pg, async_op=not sync_op)
+    out = flat.view((g.nranks,) + tuple(t.shape))
 
     def post():
         tensor_list.clear()
@@ -384,12 +385,15 @@ def alltoall(out_tensor_list, in_tensor_list, group=None, sync_op=True):
         out_tensor_list.clear()
         out_tensor_list.extend(_wrap(x.clone()) for x in ins)
         return _Task(None)
-    outs = [torch.empty_like(x) for x in ins]
-    w = dist.all_to_all(outs, ins, group=pg, async_op=not sync_op)
+    # one flat all_to_all_single (a single RCCL group of p2p transfers; gloo has no list alltoall)
+    sizes = [x.numel() for x in ins]
+    flat_in = torch.cat([x.reshape(-1) for x in ins])
+    flat_out = torch.empty_like(flat_in)
+    w = dist.all_to_all_single(flat_out, flat_in, sizes, sizes, group=pg, async_op=not sync_op)
 
     def post():
         out_tensor_list.clear()
-        out_tensor_list.extend(_wrap(x) for x in outs)
+        out_tensor_list.extend(_wrap(x.view_as(i)) for x, i in zip(flat_out.split(sizes), ins))
 
     if sync_op:
         post()

@@ -212,7 +212,17 @@ class DistributedBatchSampler(BatchSampler):
             rs = np.random.RandomState(self.epoch)
             rs.shuffle(idx)
             self.epoch += 1
-        idx = idx[self.local_rank * self.num_samples:(self.local_rank + 1) * self.num_samples]
+        # batch-strided subsample: rank r takes every nranks-th block of batch_size indices, and an
+        # equal slice of the ragged tail (same assignment as the reference sampler)
+        bs, nr, r = self.batch_size, self.nranks, self.local_rank
+        tail = self.total_size % (bs * nr)
+        mine = []
+        for i in range(r * bs, len(idx) - tail, bs * nr):
+            mine.extend(idx[i:i + bs])
+        lt = tail // nr
+        rest = idx[len(idx) - tail:]
+        mine.extend(rest[r * lt:(r + 1) * lt])
+        idx = mine
         batch = []
         for i in idx:
             batch.append(i)

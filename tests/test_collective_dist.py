@@ -1,0 +1,22 @@
+"""Collective API + DataParallel on 2 gloo ranks."""
+from _dist import run_workers
+
+
+def test_collectives_and_dataparallel():
+    res = run_workers("collective_worker.py", 2)
+    r0, r1 = res
+    for r in res:
+        assert r["all_reduce"] == [3.0, 3.0, 3.0]
+        assert r["all_reduce_max"] == [2.0]
+        assert r["all_gather"] == [[0, 0], [1, 10]]
+        assert r["broadcast"] == [6.0]
+        assert r["all_gather_object"] == [{"rank": 0}, {"rank": 1}]
+        assert r["broadcast_object_list"] == [{"x": 1}]
+        assert r["group_sum"] == [2.0]
+        assert r["dp_diff"] < 1e-5
+    assert r0["reduce"] == [3.0]
+    assert r0["reduce_scatter"] == [1.0, 4.0] and r1["reduce_scatter"] == [6.0, 4.0]
+    assert r0["alltoall"] == [[0], [10]] and r1["alltoall"] == [[1], [11]]
+    assert r0["scatter"] == [1.0, 1.0] and r1["scatter"] == [2.0, 2.0]
+    assert r1["p2p"] == [42.0]
+    assert r0["batch_p2p"] == [1.0] and r1["batch_p2p"] == [0.0]
