@@ -26,8 +26,13 @@
 //    Q / dO tiles give the A operands); K^T / V^T fragments stay in VGPRs for the whole sweep;
 //  * the workgroup sweeps every query head of its GQA group x every 32-row query tile, so dK/dV
 //    are complete in registers and written once (no cross-workgroup sum for dK/dV);
-//  * dS goes through LDS once for dQ = dS.K (4 waves split D), summed across key blocks with
-//    fp32 atomics in the full-rate two-128B-segment shape (Guideline 12), cast to bf16 after.
+//  * dS goes through LDS once for dQ = dS.K (4 waves split D).  dQ is NOT summed with float atomics:
+//    at the ≈1.3 TB/s chip-wide atomic rate the 2.2 GB/layer of fp32 adds (B2 S4096 H32) was the
+//    floor of the whole kernel; each key block instead writes its dQ tile with plain non-temporal
+//    stores into its own fp32 slab and dq_reduce_kernel sums the slabs a row actually received
+//    (plain stores run ≈4-5x the atomic rate, and the sum is bitwise reproducible);
+//  * the next (head, q-tile) step's Q / dO / lse / delta are prefetched into registers while the
+//    current step computes (T14 issue-early / write-late).
 #include "common.h"
 
 namespace pd {
@@ -306,10 +311,10 @@ template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, 1) void bwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ Vv, const bf16* __restrict__ dO,
                                                      const float* __restrict__ LSE, const float* __restrict__ DELTA,
-                                                     float* __restrict__ dQ32, bf16* __restrict__ dK,
+                                                     float* __restrict__ dQP, bf16* __restrict__ dK,
                                                      bf16* __restrict__ dV, int B, int Sq, int Sk, int Hq, int Hk,
                                                      long sq, long sk, long sv, long so, long sdk, long sdv,
-                                                     float scale) {
+                                                     long pslab, float scale) {
   constexpr int BNK = 128, BMQ = 32, NCH = D / 8, KS = D / 16, DT = D / 32;
   constexpr int KTILE = BNK * D * 2;     // K block image (for dQ = dS.K)
   constexpr int QTILE = BMQ * D * 2;     // Q / dO tile image
@@ -365,91 +370,110 @@ __global__ __launch_bounds__(256, 1) void bwd_kernel(const bf16* __restrict__ Q,
   if (CAUSAL) q_begin = max(0, k0 - off) / BMQ * BMQ;
   const int nqt = Sq > q_begin ? (Sq - q_begin + BMQ - 1) / BMQ : 0;
   constexpr int NL = BMQ * NCH / 256;  // 16-B chunks per thread per tile (2 for D=128)
+  const int ntot = nqt * group;        // (head, q-tile) steps, head-major
+  // this workgroup's dQ partial slab: plain stores, summed by dq_reduce_kernel (no atomics)
+  float* dQs = dQP + (long)kblk * pslab + (long)b * Sq * Hq * D;
 
-  for (int hh = 0; hh < group; ++hh) {
-    const int hq = hk * group + hh;
+  // register-staged prefetch of the next (head, q-tile) step (issue early / write late, T14)
+  u16x8 pq[NL], pd[NL];
+  float plse = INFINITY, pdel = 0.f;
+  auto gload = [&](int step) {
+    const int hq = hk * group + step / nqt;
+    const int q0 = q_begin + (step % nqt) * BMQ;
     const bf16* Qb = Q + (long)b * Sq * sq + hq * D;
     const bf16* dOb = dO + (long)b * Sq * so + hq * D;
-    float* dQb = dQ32 + (long)b * Sq * Hq * D + (long)hq * D;
-    const float* lseb = LSE + ((long)b * Hq + hq) * Sq;
-    const float* delb = DELTA + ((long)b * Hq + hq) * Sq;
-    for (int t = 0; t < nqt; ++t) {
-      const int q0 = q_begin + t * BMQ;
-      __syncthreads();  // previous tile's readers are done
 #pragma unroll
-      for (int i = 0; i < NL; ++i) {
-        const int c = tid + 256 * i, row = c / NCH, ch = c % NCH, q = q0 + row;
-        u16x8 a = u16x8{0, 0, 0, 0, 0, 0, 0, 0}, d2 = a;
-        if (q < Sq) {
-          a = *reinterpret_cast<const u16x8*>(Qb + (long)q * sq + ch * 8);
-          d2 = *reinterpret_cast<const u16x8*>(dOb + (long)q * so + ch * 8);
-        }
-        const int o = row * (D * 2) + swz(row, ch, NCH) * 16;
-        *reinterpret_cast<u16x8*>(qimg + o) = a;
-        *reinterpret_cast<u16x8*>(doimg + o) = d2;
+    for (int i = 0; i < NL; ++i) {
+      const int c = tid + 256 * i, row = c / NCH, ch = c % NCH, q = q0 + row;
+      if (q < Sq) {
+        pq[i] = *reinterpret_cast<const u16x8*>(Qb + (long)q * sq + ch * 8);
+        pd[i] = *reinterpret_cast<const u16x8*>(dOb + (long)q * so + ch * 8);
+      } else {
+        pq[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        pd[i] = pq[i];
       }
-      if (tid < BMQ) {
-        const int q = q0 + tid;
-        lse_s[tid] = q < Sq ? lseb[q] * kLog2e : INFINITY;
-        del_s[tid] = q < Sq ? delb[q] : 0.f;
-      }
-      __syncthreads();
+    }
+    if (tid < BMQ) {
+      const int q = q0 + tid;
+      plse = q < Sq ? LSE[((long)b * Hq + hq) * Sq + q] * kLog2e : INFINITY;
+      pdel = q < Sq ? DELTA[((long)b * Hq + hq) * Sq + q] : 0.f;
+    }
+  };
+  if (ntot > 0) gload(0);
 
-      // S = Q.K^T and dP = dO.V^T : rows = q (regs), cols = this wave's 32 keys (lanes)
-      f32x16 sacc = f32x16{}, dpacc = f32x16{};
+  for (int step = 0; step < ntot; ++step) {
+    const int hq = hk * group + step / nqt;
+    const int q0 = q_begin + (step % nqt) * BMQ;
+    __syncthreads();  // previous step's readers are done
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int o = r * (D * 2) + swz(r, 2 * ks + h, NCH) * 16;
-        sacc = mfma(lds_b128(qimg, o), kf[ks], sacc);
-        dpacc = mfma(lds_b128(doimg, o), vf[ks], dpacc);
+    for (int i = 0; i < NL; ++i) {
+      const int c = tid + 256 * i, row = c / NCH, ch = c % NCH;
+      const int o = row * (D * 2) + swz(row, ch, NCH) * 16;
+      *reinterpret_cast<u16x8*>(qimg + o) = pq[i];
+      *reinterpret_cast<u16x8*>(doimg + o) = pd[i];
+    }
+    if (tid < BMQ) {
+      lse_s[tid] = plse;
+      del_s[tid] = pdel;
+    }
+    __syncthreads();
+    if (step + 1 < ntot) gload(step + 1);  // lands while this step computes
+
+    // S = Q.K^T and dP = dO.V^T : rows = q (regs), cols = this wave's 32 keys (lanes)
+    f32x16 sacc = f32x16{}, dpacc = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int o = r * (D * 2) + swz(r, 2 * ks + h, NCH) * 16;
+      sacc = mfma(lds_b128(qimg, o), kf[ks], sacc);
+      dpacc = mfma(lds_b128(doimg, o), vf[ks], dpacc);
+    }
+    // P = exp2(S*scale*log2e - lse*log2e), dS = P * (dP - delta)
+    const bool need_mask = (k0 + BNK > Sk) || (CAUSAL && (k0 + BNK - 1 > q0 + off));
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qi = (i & 3) + 8 * (i >> 2) + 4 * h;
+      float p = exp2f(sacc[i] * sl2 - lse_s[qi]);
+      if (need_mask) {
+        const int q = q0 + qi;
+        if (mykey >= Sk || (CAUSAL && mykey > q + off)) p = 0.f;
       }
-      // P = exp2(S*scale*log2e - lse*log2e), dS = P * (dP - delta)
-      const bool need_mask = (k0 + BNK > Sk) || (CAUSAL && (k0 + BNK - 1 > q0 + off));
+      sacc[i] = p;
+      dpacc[i] = p * (dpacc[i] - del_s[qi]);
+    }
+    // dV^T += dO^T . P ; dK^T += Q^T . dS   (A operands by transposed reads, permuted k)
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const bf16x8 pb = pack8(sacc, ss);
+      const bf16x8 db = pack8(dpacc, ss);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        dvacc[dt] = mfma(tr_frag<D, true>(doimg, 16 * ss, dt * 32, lane), pb, dvacc[dt]);
+        dkacc[dt] = mfma(tr_frag<D, true>(qimg, 16 * ss, dt * 32, lane), db, dkacc[dt]);
+      }
+    }
+    // dS -> LDS image [32 q][128 keys] (bf16) for dQ
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qi = (i & 3) + 8 * (i >> 2) + 4 * h;
+      const int col = wv * 32 + r;
+      *reinterpret_cast<__bf16*>(simg + tile_off<BNK>(qi, col)) = (__bf16)dpacc[i];
+    }
+    __syncthreads();
+    // dQ[32 q][d in wave's 32-col slice] = dS[32 q][128 keys] . K[128 keys][d]
+    if (wv < DT) {
+      f32x16 dq = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < BNK / 16; ++ks) {
+        const bf16x8 a = lds_b128(simg, r * (BNK * 2) + swz(r, 2 * ks + h, BNK / 8) * 16);
+        const bf16x8 bb = tr_frag<D, false>(kimg, 16 * ks, wv * 32, lane);
+        dq = mfma(a, bb, dq);
+      }
+      // accumulator: row q = (i&3)+8(i>>2)+4h, col d = wv*32 + r -> two 128-B row segments per store
+      float* dqh = dQs + (long)hq * D + wv * 32 + r;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int qi = (i & 3) + 8 * (i >> 2) + 4 * h;
-        float p = exp2f(sacc[i] * sl2 - lse_s[qi]);
-        if (need_mask) {
-          const int q = q0 + qi;
-          if (mykey >= Sk || (CAUSAL && mykey > q + off)) p = 0.f;
-        }
-        sacc[i] = p;
-        dpacc[i] = p * (dpacc[i] - del_s[qi]);
-      }
-      // dV^T += dO^T . P ; dK^T += Q^T . dS   (A operands by transposed reads, permuted k)
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 pb = pack8(sacc, ss);
-        const bf16x8 db = pack8(dpacc, ss);
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          dvacc[dt] = mfma(tr_frag<D, true>(doimg, 16 * ss, dt * 32, lane), pb, dvacc[dt]);
-          dkacc[dt] = mfma(tr_frag<D, true>(qimg, 16 * ss, dt * 32, lane), db, dkacc[dt]);
-        }
-      }
-      // dS -> LDS image [32 q][128 keys] (bf16) for dQ
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qi = (i & 3) + 8 * (i >> 2) + 4 * h;
-        const int col = wv * 32 + r;
-        *reinterpret_cast<__bf16*>(simg + tile_off<BNK>(qi, col)) = (__bf16)dpacc[i];
-      }
-      __syncthreads();
-      // dQ[32 q][d in wave's 32-col slice] = dS[32 q][128 keys] . K[128 keys][d]
-      if (wv < DT) {
-        f32x16 dq = f32x16{};
-#pragma unroll
-        for (int ks = 0; ks < BNK / 16; ++ks) {
-          const bf16x8 a = lds_b128(simg, r * (BNK * 2) + swz(r, 2 * ks + h, BNK / 8) * 16);
-          const bf16x8 bb = tr_frag<D, false>(kimg, 16 * ks, wv * 32, lane);
-          dq = mfma(a, bb, dq);
-        }
-        // accumulator: row q = (i&3)+8(i>>2)+4h, col d = wv*32 + r -> fp32 atomics
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int q = q0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (q < Sq) atomicAdd(dQb + (long)q * Hq * D + wv * 32 + r, dq[i] * scale);
-        }
+        const int q = q0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (q < Sq) __builtin_nontemporal_store(dq[i] * scale, dqh + (long)q * Hq * D);
       }
     }
   }
@@ -474,18 +498,36 @@ __global__ __launch_bounds__(256, 1) void bwd_kernel(const bf16* __restrict__ Q,
   }
 }
 
-__global__ __launch_bounds__(256) void f32_to_bf16_strided(const float* __restrict__ src, bf16* __restrict__ dst,
-                                                           long rows, int D, int H, long sdst) {
-  // src: [rows(b*s), H, D] contiguous ; dst row stride sdst (elements) per (b*s) row
-  const long total = rows * H * (D / 4);
+// dQ[b, q, h, :] = sum over the key blocks that wrote row q of their partial slabs; bf16 out with row
+// stride sdq.  Causal: key block kb wrote rows q >= qbegin(kb) = floor(max(0, kb*BNK - off) / BMQ) * BMQ.
+__global__ __launch_bounds__(256) void dq_reduce_kernel(const float* __restrict__ P, bf16* __restrict__ dq, int B,
+                                                        int Sq, int Hq, int D, int nkb, long pslab, long sdq,
+                                                        int causal, int off) {
+  const long per_row = (long)Hq * D / 8;  // 8 floats per thread
+  const long total = (long)B * Sq * per_row;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long e = i * 4;
-    const long row = e / ((long)H * D);
-    const long rem = e - row * H * D;
-    float4 v = *reinterpret_cast<const float4*>(src + e);
-    ushort4 o;
-    o.x = f2bf(v.x); o.y = f2bf(v.y); o.z = f2bf(v.z); o.w = f2bf(v.w);
-    *reinterpret_cast<ushort4*>(dst + row * sdst + rem) = o;
+    const long row = i / per_row;              // b*Sq + q
+    const long e = (i - row * per_row) * 8;    // offset inside the [Hq*D] row
+    const int q = (int)(row % Sq);
+    int kb_end = nkb;
+    if (causal) {
+      // last key block whose q_begin <= q
+      const int lim = q + off;                 // max key index visible to this row
+      kb_end = lim < 0 ? 0 : min(nkb, lim / 128 + 1);
+      // rounding: block kb also wrote rows down to floor((kb*128-off)/32)*32
+      while (kb_end < nkb && (max(0, kb_end * 128 - off) / 32) * 32 <= q) ++kb_end;
+    }
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const float* src = P + row * (long)Hq * D + e;
+    for (int kb = 0; kb < kb_end; ++kb) {
+      typedef float f32x4 __attribute__((ext_vector_type(4)));
+      const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + kb * pslab));
+      const f32x4 c = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + kb * pslab + 4));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { acc[j] += a[j]; acc[4 + j] += c[j]; }
+    }
+    const long b = row / Sq;
+    store_vec<bf16, 8>(dq + (b * Sq + q) * sdq + e, acc);
   }
 }
 
@@ -510,11 +552,11 @@ extern "C" int pd_flash_fwd(int dt, const void* q, const void* k, const void* v,
   return (int)hipGetLastError();
 }
 
-// dq32 must be a zeroed [B, Sq, Hq, D] fp32 workspace; delta a [B, Hq, Sq] fp32 workspace.
-// q/k/v/o/dout and dq/dk/dv may all be row-strided views ([B, S, H, D] with token strides
-// sq/sk/sv/so and sdq/sdk/sdv), e.g. slices of one fused QKV / dQKV buffer.
+// dqp: fp32 workspace of nkb * B*Sq*Hq*D floats (nkb = ceil(Sk/128)) for per-key-block dQ partials
+// (need not be zeroed); delta a [B, Hq, Sq] fp32 workspace.  q/k/v/o/dout and dq/dk/dv may all be
+// row-strided views ([B, S, H, D] with token strides), e.g. slices of one fused QKV / dQKV buffer.
 extern "C" int pd_flash_bwd(int dt, const void* q, const void* k, const void* v, const void* o, const void* dout,
-                            const float* lse, float* delta, void* dq, void* dk, void* dv, float* dq32, int B, int Sq,
+                            const float* lse, float* delta, void* dq, void* dk, void* dv, float* dqp, int B, int Sq,
                             int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, long sdq, long sdk,
                             long sdv, float scale, int causal, void* stream) {
   if (dt != kBF16 || (D != 64 && D != 128) || Hq % Hk) return -1;
@@ -523,17 +565,18 @@ extern "C" int pd_flash_bwd(int dt, const void* q, const void* k, const void* v,
   fa::bwd_delta_kernel<<<(int)((rows + 3) / 4), 256, 0, st>>>((const bf16*)o, (const bf16*)dout, delta, B, Sq, Hq, D,
                                                                so);
   const int nkb = (Sk + 127) / 128;
+  const long pslab = (long)B * Sq * Hq * D;
   dim3 grid(nkb * Hk * B), block(256);
 #define PD_FA_BWD(DD, CC)                                                                                        \
   fa::bwd_kernel<DD, CC><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
-                                                 lse, delta, dq32, (bf16*)dk, (bf16*)dv, B, Sq, Sk, Hq, Hk, sq, sk, \
-                                                 sv, so, sdk, sdv, scale)
+                                                 lse, delta, dqp, (bf16*)dk, (bf16*)dv, B, Sq, Sk, Hq, Hk, sq, sk, \
+                                                 sv, so, sdk, sdv, pslab, scale)
   if (D == 128) { if (causal) PD_FA_BWD(128, true); else PD_FA_BWD(128, false); }
   else { if (causal) PD_FA_BWD(64, true); else PD_FA_BWD(64, false); }
 #undef PD_FA_BWD
-  long work = (long)B * Sq * Hq * (D / 4);
+  long work = (long)B * Sq * Hq * D / 8;
   long g = (work + 255) / 256;
-  if (g > 4096) g = 4096;
-  fa::f32_to_bf16_strided<<<(int)g, 256, 0, st>>>(dq32, (bf16*)dq, (long)B * Sq, D, Hq, sdq);
+  if (g > 8192) g = 8192;
+  fa::dq_reduce_kernel<<<(int)g, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, D, nkb, pslab, sdq, causal, Sk - Sq);
   return (int)hipGetLastError();
 }

@@ -145,7 +145,7 @@ def test_embedding():
 
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("D", [128, 64])
-@pytest.mark.parametrize("shape", [(2, 256, 256, 4, 4), (1, 200, 200, 4, 2), (1, 130, 300, 2, 1)])
+@pytest.mark.parametrize("shape", [(2, 256, 256, 4, 4), (1, 200, 200, 4, 2), (1, 130, 300, 2, 1), (1, 1100, 1100, 2, 1)])
 def test_flash_attention(causal, D, shape):
     B, Sq, Sk, Hq, Hk = shape
     qg, qc = _pair((B, Sq, Hq, D), torch.bfloat16, seed=12)
