@@ -20,10 +20,12 @@
 //  * 1-D grid with an XCD-aware bijective remap (T1): all query blocks of a KV head land on one
 //    XCD so K/V are served from that XCD's L2; causal grids start with the heaviest blocks.
 //
-// Backward (per workgroup: 4 waves x 32 keys = 128 keys of one (b, kv-head)):
+// Backward (per workgroup: 8 waves x 32 keys = 256 keys of one (b, kv-head); two waves per SIMD so
+// one wave's LDS/VALU phases hide under the other's MFMAs):
 //  * key on the lane: S = Q.K^T and dP = dO.V^T have the key as the accumulator column, so
 //    P and dS are directly the B operands of dV^T += dO^T.P and dK^T += Q^T.dS (tr-reads of the
-//    Q / dO tiles give the A operands); K^T / V^T fragments stay in VGPRs for the whole sweep;
+//    Q / dO tiles give the A operands); V fragments stay in VGPRs for the whole sweep, K is read
+//    from its one LDS image both by rows (S) and by columns (dQ), keeping the wave under 256 VGPRs;
 //  * the workgroup sweeps every query head of its GQA group x every 32-row query tile, so dK/dV
 //    are complete in registers and written once (no cross-workgroup sum for dK/dV);
 //  * dS goes through LDS once for dQ = dS.K (4 waves split D).  dQ is NOT summed with float atomics:
@@ -308,17 +310,17 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const bf16* __restrict__
 }
 
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void bwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+__global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ Vv, const bf16* __restrict__ dO,
                                                      const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                      float* __restrict__ dQP, bf16* __restrict__ dK,
                                                      bf16* __restrict__ dV, int B, int Sq, int Sk, int Hq, int Hk,
                                                      long sq, long sk, long sv, long so, long sdk, long sdv,
                                                      long pslab, float scale) {
-  constexpr int BNK = 128, BMQ = 32, NCH = D / 8, KS = D / 16, DT = D / 32;
-  constexpr int KTILE = BNK * D * 2;     // K block image (for dQ = dS.K)
+  constexpr int NW = 8, BNK = NW * 32, BMQ = 32, NCH = D / 8, KS = D / 16, DT = D / 32;
+  constexpr int KTILE = BNK * D * 2;     // K block image: B operand of S (row reads) and of dQ (tr reads)
   constexpr int QTILE = BMQ * D * 2;     // Q / dO tile image
-  constexpr int STILE = BMQ * BNK * 2;   // dS tile [32 q][128 keys]
+  constexpr int STILE = BMQ * BNK * 2;   // dS tile [32 q][256 keys]
   __shared__ __attribute__((aligned(16))) char smem[KTILE + 2 * QTILE + STILE + 2 * BMQ * 4];
   char* kimg = smem;
   char* qimg = smem + KTILE;
@@ -327,39 +329,34 @@ __global__ __launch_bounds__(256, 1) void bwd_kernel(const bf16* __restrict__ Q,
   float* lse_s = reinterpret_cast<float*>(simg + STILE);
   float* del_s = lse_s + BMQ;
 
+  // heaviest (lowest, under the causal mask) key blocks first, round-robin over the XCDs
   const int nkb = (Sk + BNK - 1) / BNK;
-  const int total = nkb * Hk * B;
-  const int w_id = xcd_remap(blockIdx.x, total);
-  const int kblk = w_id % nkb;
-  const int hk = (w_id / nkb) % Hk;
-  const int b = w_id / (nkb * Hk);
+  const int kblk = blockIdx.x / (Hk * B);
+  const int rest = blockIdx.x % (Hk * B);
+  const int hk = rest % Hk;
+  const int b = rest / Hk;
   const int group = Hq / Hk;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int k0 = kblk * BNK;
   const int off = Sk - Sq;
-  const int mykey = k0 + wv * 32 + r;  // key owned by this lane's accumulator column
+  const int lkey = wv * 32 + r;          // key (within the block) owned by this lane's accumulator column
+  const int mykey = k0 + lkey;
 
   const bf16* Kb = K + (long)b * Sk * sk + hk * D;
   const bf16* Vb = Vv + (long)b * Sk * sv + hk * D;
 
-  // K block -> LDS (for dQ), K/V fragments -> registers (B operands of S and dP)
-  for (int c = tid; c < BNK * NCH; c += 256) {
+  for (int c = tid; c < BNK * NCH; c += NW * 64) {
     const int row = c / NCH, ch = c % NCH, key = k0 + row;
     u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
     if (key < Sk) v = *reinterpret_cast<const u16x8*>(Kb + (long)key * sk + ch * 8);
     *reinterpret_cast<u16x8*>(kimg + row * (D * 2) + swz(row, ch, NCH) * 16) = v;
   }
-  bf16x8 kf[KS], vf[KS];
+  bf16x8 vf[KS];  // V fragments of this lane's key stay in VGPRs (B operand of dP)
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    if (mykey < Sk) {
-      kf[ks] = *reinterpret_cast<const bf16x8*>(Kb + (long)mykey * sk + ks * 16 + 8 * h);
-      vf[ks] = *reinterpret_cast<const bf16x8*>(Vb + (long)mykey * sv + ks * 16 + 8 * h);
-    } else {
-      kf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      vf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
+    if (mykey < Sk) vf[ks] = *reinterpret_cast<const bf16x8*>(Vb + (long)mykey * sv + ks * 16 + 8 * h);
+    else vf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
   f32x16 dkacc[DT], dvacc[DT];
 #pragma unroll
@@ -369,7 +366,7 @@ __global__ __launch_bounds__(256, 1) void bwd_kernel(const bf16* __restrict__ Q,
   int q_begin = 0;
   if (CAUSAL) q_begin = max(0, k0 - off) / BMQ * BMQ;
   const int nqt = Sq > q_begin ? (Sq - q_begin + BMQ - 1) / BMQ : 0;
-  constexpr int NL = BMQ * NCH / 256;  // 16-B chunks per thread per tile (2 for D=128)
+  constexpr int NL = (BMQ * NCH + NW * 64 - 1) / (NW * 64);  // 16-B chunks per thread per tile
   const int ntot = nqt * group;        // (head, q-tile) steps, head-major
   // this workgroup's dQ partial slab: plain stores, summed by dq_reduce_kernel (no atomics)
   float* dQs = dQP + (long)kblk * pslab + (long)b * Sq * Hq * D;
@@ -384,8 +381,8 @@ __global__ __launch_bounds__(256, 1) void bwd_kernel(const bf16* __restrict__ Q,
     const bf16* dOb = dO + (long)b * Sq * so + hq * D;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
-      const int c = tid + 256 * i, row = c / NCH, ch = c % NCH, q = q0 + row;
-      if (q < Sq) {
+      const int c = tid + NW * 64 * i, row = c / NCH, ch = c % NCH, q = q0 + row;
+      if (c < BMQ * NCH && q < Sq) {
         pq[i] = *reinterpret_cast<const u16x8*>(Qb + (long)q * sq + ch * 8);
         pd[i] = *reinterpret_cast<const u16x8*>(dOb + (long)q * so + ch * 8);
       } else {
@@ -401,16 +398,43 @@ __global__ __launch_bounds__(256, 1) void bwd_kernel(const bf16* __restrict__ Q,
   };
   if (ntot > 0) gload(0);
 
+  // ---- per-lane LDS byte offsets.  Every operand address below is one of these bases XOR/plus a
+  // compile-time constant (folded into the ds_* immediate offset where it is an add), so the loop
+  // carries ~8 address VGPRs instead of ~50 hoisted per-(ks, dt) offsets (which spilled).
+  const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3, hh = g4 >> 1;
+  const int cb = ((g4 & 1) << 1) | (pp >> 1);
+  auto msk = [](int row) { return ((row & 3) << 2) | ((row >> 2) & 3); };
+  // row reads of Q / dO (row r) and K (row lkey): chunk (2ks + h) ^ m(row) = (h ^ m) ^ 2ks
+  int o_qrow = r * (D * 2) + (((h ^ msk(r)) & (NCH - 1)) << 4);
+  int o_krow = lkey * (D * 2) + (((h ^ msk(lkey)) & (NCH - 1)) << 4);
+  // transposed A-operand reads (dV / dK, permuted k): rows 16ss + 4hh + qq (+8); chunk dt*4 + cb
+  const int ra = 4 * hh + qq, rb = ra + 8;
+  int o_trA = ra * (D * 2) + (((cb ^ msk(ra)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
+  int o_trB = rb * (D * 2) + (((cb ^ msk(rb)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
+  // transposed K^T reads for dQ (natural k): rows 16ks + 8hh + qq (+4); chunk wv*4 + cb
+  const int rqa = 8 * hh + qq, rqb = rqa + 4;
+  int o_kqA = rqa * (D * 2) + ((((wv * 4 + cb) ^ msk(rqa)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
+  int o_kqB = rqb * (D * 2) + ((((wv * 4 + cb) ^ msk(rqb)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
+  // dS image [32 q][BNK keys]: A-operand row reads and this lane's column writes
+  constexpr int SNCH = BNK / 8;
+  int o_srow = r * (BNK * 2) + (((h ^ msk(r)) & (SNCH - 1)) << 4);
+  int o_scol = 4 * h * (BNK * 2) + ((((lkey >> 3) ^ h) & (SNCH - 1)) << 4) + ((lkey & 7) << 1);
+
   for (int step = 0; step < ntot; ++step) {
     const int hq = hk * group + step / nqt;
     const int q0 = q_begin + (step % nqt) * BMQ;
+    // keep the bases opaque per step so derived offsets are recomputed (1 VALU each), not hoisted
+    asm volatile("" : "+v"(o_qrow), "+v"(o_krow), "+v"(o_trA), "+v"(o_trB));
+    asm volatile("" : "+v"(o_kqA), "+v"(o_kqB), "+v"(o_srow), "+v"(o_scol));
     __syncthreads();  // previous step's readers are done
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
-      const int c = tid + 256 * i, row = c / NCH, ch = c % NCH;
-      const int o = row * (D * 2) + swz(row, ch, NCH) * 16;
-      *reinterpret_cast<u16x8*>(qimg + o) = pq[i];
-      *reinterpret_cast<u16x8*>(doimg + o) = pd[i];
+      const int c = tid + NW * 64 * i, row = c / NCH, ch = c % NCH;
+      if (c < BMQ * NCH) {
+        const int o = row * (D * 2) + swz(row, ch, NCH) * 16;
+        *reinterpret_cast<u16x8*>(qimg + o) = pq[i];
+        *reinterpret_cast<u16x8*>(doimg + o) = pd[i];
+      }
     }
     if (tid < BMQ) {
       lse_s[tid] = plse;
@@ -423,8 +447,8 @@ __global__ __launch_bounds__(256, 1) void bwd_kernel(const bf16* __restrict__ Q,
     f32x16 sacc = f32x16{}, dpacc = f32x16{};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      const int o = r * (D * 2) + swz(r, 2 * ks + h, NCH) * 16;
-      sacc = mfma(lds_b128(qimg, o), kf[ks], sacc);
+      const int o = o_qrow ^ (ks << 5);
+      sacc = mfma(lds_b128(qimg, o), lds_b128(kimg, o_krow ^ (ks << 5)), sacc);
       dpacc = mfma(lds_b128(doimg, o), vf[ks], dpacc);
     }
     // P = exp2(S*scale*log2e - lse*log2e), dS = P * (dP - delta)
@@ -447,25 +471,29 @@ __global__ __launch_bounds__(256, 1) void bwd_kernel(const bf16* __restrict__ Q,
       const bf16x8 db = pack8(dpacc, ss);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        dvacc[dt] = mfma(tr_frag<D, true>(doimg, 16 * ss, dt * 32, lane), pb, dvacc[dt]);
-        dkacc[dt] = mfma(tr_frag<D, true>(qimg, 16 * ss, dt * 32, lane), db, dkacc[dt]);
+        const int oa = (o_trA ^ (dt << 6)) + ss * 16 * (D * 2);
+        const int ob = (o_trB ^ (dt << 6)) + ss * 16 * (D * 2);
+        dvacc[dt] = mfma(cat4(lds_tr(doimg, oa), lds_tr(doimg, ob)), pb, dvacc[dt]);
+        dkacc[dt] = mfma(cat4(lds_tr(qimg, oa), lds_tr(qimg, ob)), db, dkacc[dt]);
       }
     }
-    // dS -> LDS image [32 q][128 keys] (bf16) for dQ
+    // dS -> LDS image [32 q][BNK keys] (bf16) for dQ: row qi = (i&3) + 8(i>>2) + 4h, column lkey
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int qi = (i & 3) + 8 * (i >> 2) + 4 * h;
-      const int col = wv * 32 + r;
-      *reinterpret_cast<__bf16*>(simg + tile_off<BNK>(qi, col)) = (__bf16)dpacc[i];
+      const int xc = ((((i & 3) << 2) | (((i >> 2) & 1) << 1)) << 4);
+      const int ac = ((i & 3) + 8 * (i >> 2)) * (BNK * 2);
+      *reinterpret_cast<__bf16*>(simg + ((o_scol ^ xc) + ac)) = (__bf16)dpacc[i];
     }
     __syncthreads();
-    // dQ[32 q][d in wave's 32-col slice] = dS[32 q][128 keys] . K[128 keys][d]
+    // dQ[32 q][32-col slice] = dS[32 q][BNK keys] . K[BNK keys][d]; waves 0..DT-1 (one per SIMD for
+    // D=128, so every SIMD's matrix pipe carries the same 16 MFMAs)
     if (wv < DT) {
       f32x16 dq = f32x16{};
 #pragma unroll
       for (int ks = 0; ks < BNK / 16; ++ks) {
-        const bf16x8 a = lds_b128(simg, r * (BNK * 2) + swz(r, 2 * ks + h, BNK / 8) * 16);
-        const bf16x8 bb = tr_frag<D, false>(kimg, 16 * ks, wv * 32, lane);
+        const bf16x8 a = lds_b128(simg, o_srow ^ (ks << 5));
+        const int kb16 = ks * 16 * (D * 2);
+        const bf16x8 bb = cat4(lds_tr(kimg, o_kqA + kb16), lds_tr(kimg, o_kqB + kb16));
         dq = mfma(a, bb, dq);
       }
       // accumulator: row q = (i&3)+8(i>>2)+4h, col d = wv*32 + r -> two 128-B row segments per store
@@ -502,7 +530,7 @@ __global__ __launch_bounds__(256, 1) void bwd_kernel(const bf16* __restrict__ Q,
 // stride sdq.  Causal: key block kb wrote rows q >= qbegin(kb) = floor(max(0, kb*BNK - off) / BMQ) * BMQ.
 __global__ __launch_bounds__(256) void dq_reduce_kernel(const float* __restrict__ P, bf16* __restrict__ dq, int B,
                                                         int Sq, int Hq, int D, int nkb, long pslab, long sdq,
-                                                        int causal, int off) {
+                                                        int causal, int off, int bnk) {
   const long per_row = (long)Hq * D / 8;  // 8 floats per thread
   const long total = (long)B * Sq * per_row;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -513,9 +541,9 @@ __global__ __launch_bounds__(256) void dq_reduce_kernel(const float* __restrict_
     if (causal) {
       // last key block whose q_begin <= q
       const int lim = q + off;                 // max key index visible to this row
-      kb_end = lim < 0 ? 0 : min(nkb, lim / 128 + 1);
-      // rounding: block kb also wrote rows down to floor((kb*128-off)/32)*32
-      while (kb_end < nkb && (max(0, kb_end * 128 - off) / 32) * 32 <= q) ++kb_end;
+      kb_end = lim < 0 ? 0 : min(nkb, lim / bnk + 1);
+      // rounding: block kb also wrote rows down to floor((kb*bnk-off)/32)*32
+      while (kb_end < nkb && (max(0, kb_end * bnk - off) / 32) * 32 <= q) ++kb_end;
     }
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const float* src = P + row * (long)Hq * D + e;
@@ -552,7 +580,7 @@ extern "C" int pd_flash_fwd(int dt, const void* q, const void* k, const void* v,
   return (int)hipGetLastError();
 }
 
-// dqp: fp32 workspace of nkb * B*Sq*Hq*D floats (nkb = ceil(Sk/128)) for per-key-block dQ partials
+// dqp: fp32 workspace of nkb * B*Sq*Hq*D floats (nkb = ceil(Sk/256)) for per-key-block dQ partials
 // (need not be zeroed); delta a [B, Hq, Sq] fp32 workspace.  q/k/v/o/dout and dq/dk/dv may all be
 // row-strided views ([B, S, H, D] with token strides), e.g. slices of one fused QKV / dQKV buffer.
 extern "C" int pd_flash_bwd(int dt, const void* q, const void* k, const void* v, const void* o, const void* dout,
@@ -564,9 +592,10 @@ extern "C" int pd_flash_bwd(int dt, const void* q, const void* k, const void* v,
   const long rows = (long)B * Hq * Sq;
   fa::bwd_delta_kernel<<<(int)((rows + 3) / 4), 256, 0, st>>>((const bf16*)o, (const bf16*)dout, delta, B, Sq, Hq, D,
                                                                so);
-  const int nkb = (Sk + 127) / 128;
+  constexpr int BNK = 256;
+  const int nkb = (Sk + BNK - 1) / BNK;
   const long pslab = (long)B * Sq * Hq * D;
-  dim3 grid(nkb * Hk * B), block(256);
+  dim3 grid(nkb * Hk * B), block(512);
 #define PD_FA_BWD(DD, CC)                                                                                        \
   fa::bwd_kernel<DD, CC><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
                                                  lse, delta, dqp, (bf16*)dk, (bf16*)dv, B, Sq, Sk, Hq, Hk, sq, sk, \
@@ -577,6 +606,6 @@ extern "C" int pd_flash_bwd(int dt, const void* q, const void* k, const void* v,
   long work = (long)B * Sq * Hq * D / 8;
   long g = (work + 255) / 256;
   if (g > 8192) g = 8192;
-  fa::dq_reduce_kernel<<<(int)g, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, D, nkb, pslab, sdq, causal, Sk - Sq);
+  fa::dq_reduce_kernel<<<(int)g, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, D, nkb, pslab, sdq, causal, Sk - Sq, BNK);
   return (int)hipGetLastError();
 }

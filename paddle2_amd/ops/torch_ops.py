@@ -493,7 +493,7 @@ def _flash_bwd_native(q, k, v, out, do, lse, dq, dk, dv, scale, causal):
     """dq/dk/dv may be token-strided views (e.g. slices of a dQKV buffer)."""
     B, Sq, Hq, D = q.shape
     Sk, Hk = k.shape[1], k.shape[2]
-    nkb = (Sk + 127) // 128
+    nkb = (Sk + 255) // 256
     dq32 = torch.empty(nkb * B * Sq * Hq * D, dtype=torch.float32, device=q.device)  # per-key-block dQ partials
     delta = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
     N.native().flash_bwd(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), do.data_ptr(), lse.data_ptr(),
