@@ -35,6 +35,8 @@ def parse():
     ap.add_argument("--sharding-stage", type=int, default=3)
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--gemm-autotune", default="auto", choices=["auto", "tune", "off"],
+                    help="hipBLASLt solution cache (tuning/gemm_gfx950.csv): auto = use it if present")
     return ap.parse_args()
 
 
@@ -50,6 +52,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+
+    if args.gemm_autotune != "off" and torch.cuda.is_available():
+        from paddle2_amd.incubate import autotune
+
+        if args.gemm_autotune == "tune" or os.path.exists(autotune.DEFAULT_GEMM_CACHE):
+            autotune.enable_gemm_autotune(tuning=args.gemm_autotune == "tune")
 
     strategy = fleet.DistributedStrategy()
     strategy.hybrid_configs = {"dp_degree": 1, "mp_degree": 1, "pp_degree": 1, "sharding_degree": world}
