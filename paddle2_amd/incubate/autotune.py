@@ -17,7 +17,7 @@ DEFAULT_GEMM_CACHE = os.path.join(_ROOT, "tuning", "gemm_gfx950.csv")
 _state = {"kernel": False, "tuning": False, "file": None}
 
 
-def enable_gemm_autotune(tuning=False, filename=None, max_tuning_ms=30, max_iters=100):
+def enable_gemm_autotune(tuning=False, filename=None, max_tuning_ms=10, max_iters=20):
     """Use (and with ``tuning=True`` extend) the GEMM selection cache."""
     import torch.cuda.tunable as tun
 

@@ -4,7 +4,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out tuning
 export TMPDIR=/tmp
 for b in 4 2; do
-  timeout -k 10 1500 python bench.py --steps 1 --warmup 1 --micro-batch $b --gemm-autotune tune > gpurun_out/tune_b$b.log 2>&1
+  PYTORCH_TUNABLEOP_VERBOSE=1 timeout -k 10 1500 python bench.py --steps 1 --warmup 1 --micro-batch $b --gemm-autotune tune > gpurun_out/tune_b$b.log 2>&1
   rc=$?; echo "tune b$b rc=$rc"; tail -2 gpurun_out/tune_b$b.log
   [ $rc -eq 0 ] || exit $rc
 done
