@@ -26,3 +26,8 @@ def test_fleet_sharding_stage1_matches_single():
     _close(res)
     for r in res:
         assert abs(r["csum"] - r["csum_ref"]) < 1e-2 * max(1.0, abs(r["csum_ref"]))
+
+
+def test_moe_expert_parallel_matches_single():
+    for r in run_workers("hybrid_worker.py", 2, ["moe"]):
+        assert r["out_diff"] < 1e-5 and r["xg_diff"] < 1e-5 and r["eg"] < 1e-4, r

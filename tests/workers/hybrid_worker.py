@@ -213,9 +213,47 @@ def run_dpsh():
     write_result({"losses": losses, "ref": ref, "csum": csum, "csum_ref": csum_ref})
 
 
+def run_moe():
+    from paddle2_amd.incubate.distributed.models.moe import MoELayer
+
+    class E(paddle.nn.Layer):
+        def __init__(self):
+            super().__init__()
+            self.l1 = paddle.nn.Linear(8, 16)
+            self.l2 = paddle.nn.Linear(16, 8)
+
+        def forward(self, x):
+            return self.l2(paddle.nn.functional.gelu(self.l1(x)))
+
+    group = C._get_default_group()
+    paddle.seed(21)
+    experts = [E() for _ in range(2 * world)]
+    gate_ref = MoELayer(8, paddle.nn.LayerList(experts), gate={"type": "naive", "top_k": 2})
+    local = paddle.nn.LayerList(experts[2 * rank:2 * rank + 2])
+    moe = MoELayer(8, local, gate={"type": "naive", "top_k": 2}, moe_group=group)
+    moe.gate.set_state_dict(gate_ref.gate.state_dict())
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(2 * world, 5, 8, generator=g)
+    x = paddle.Tensor._wrap(X[2 * rank:2 * rank + 2].clone().requires_grad_(True))
+    y = moe(x)
+    (y * y).sum().backward()
+    ep_grads = [p._t.grad.clone() for p in local.parameters()]
+    for p in local.parameters():
+        p.clear_gradient()
+    xr = paddle.Tensor._wrap(X.clone().requires_grad_(True))
+    yr = gate_ref(xr)
+    (yr * yr).sum().backward()
+    out_diff = float((y._t - yr._t[2 * rank:2 * rank + 2]).abs().max())
+    xg_diff = float((x._t.grad - xr._t.grad[2 * rank:2 * rank + 2]).abs().max())
+    eg = max(float((a - p._t.grad).abs().max()) for a, p in zip(ep_grads, local.parameters()))
+    write_result({"out_diff": out_diff, "xg_diff": xg_diff, "eg": eg})
+
+
 if mode == "tp":
     run_tp()
 elif mode == "pp":
     run_pp(sys.argv[2], int(sys.argv[3]))
 elif mode == "dpsh":
     run_dpsh()
+elif mode == "moe":
+    run_moe()
