@@ -20,7 +20,8 @@ def __getattr__(name):
         return mod
     if name in ("shard_tensor", "reshard", "dtensor_from_fn", "shard_layer", "shard_optimizer", "ProcessMesh",
                 "Shard", "Replicate", "Partial", "to_static", "unshard_dtensor", "shard_dataloader", "DistModel",
-                "Strategy", "ShardingStage1", "ShardingStage2", "ShardingStage3"):
+                "Strategy", "ShardingStage1", "ShardingStage2", "ShardingStage3", "dtensor_from_local",
+                "shard_scaler", "set_mesh", "get_mesh", "Placement", "is_dist_tensor"):
         mod = importlib.import_module(".auto_parallel", __name__)
         return getattr(mod, name)
     if name in ("save_state_dict", "load_state_dict"):

@@ -1,0 +1,5 @@
+"""paddle.distributed.auto_parallel (semi-automatic parallelism on DistTensors)."""
+from .api import (DistModel, Partial, Placement, ProcessMesh, Replicate, Shard, ShardDataloader,  # noqa
+                  ShardingStage1, ShardingStage2, ShardingStage3, Strategy, dtensor_from_fn, dtensor_from_local,
+                  get_mesh, is_dist_tensor, local_tensor, placements_of, reshard, set_mesh, shard_dataloader,
+                  shard_layer, shard_optimizer, shard_scaler, shard_tensor, to_static, unshard_dtensor)

@@ -1,0 +1,491 @@
+"""Semi-automatic parallelism: ProcessMesh, placements and DistTensor (reference:
+python/paddle/distributed/auto_parallel/api.py — ``shard_tensor`` :206, ``dtensor_from_fn`` :665,
+``reshard`` :705, ``shard_layer`` :806, ``shard_optimizer`` :1261-1641 (ShardingStage1/2/3),
+``shard_dataloader`` :3208, ``to_static``/``DistModel`` :2110/:2693, ``unshard_dtensor`` :2854;
+process_mesh.py; placement_type.py).
+
+MI355X design: a Paddle DistTensor is our Tensor whose storage is a torch ``DTensor`` over a
+``DeviceMesh`` built from the ProcessMesh's rank grid (RCCL sub-communicators per mesh dim).
+Operator-level sharding propagation (the reference's SPMD rules + reshard functions s->r, p->r,
+p->s, s->s) is torch's DTensor dispatcher; ``reshard`` is ``redistribute`` (all-gather /
+reduce-scatter / all-to-all over the mesh dim's communicator).
+"""
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+import torch
+from torch.distributed import tensor as _dt
+
+from ...framework.tensor import Tensor
+from ...framework.place import current_torch_device
+
+_wrap = Tensor._wrap
+
+
+# ----------------------------------------------------------------------------- placements
+class Placement:
+    def is_shard(self, dim=None):
+        return False
+
+    def is_replicated(self):
+        return False
+
+    def is_partial(self):
+        return False
+
+
+class Shard(Placement):
+    def __init__(self, dim, **kw):
+        self.dim = int(dim)
+
+    def get_dim(self):
+        return self.dim
+
+    def is_shard(self, dim=None):
+        return dim is None or dim == self.dim
+
+    def _torch(self):
+        return _dt.Shard(self.dim)
+
+    def __eq__(self, o):
+        return isinstance(o, Shard) and o.dim == self.dim
+
+    def __hash__(self):
+        return hash(("S", self.dim))
+
+    def __repr__(self):
+        return f"Shard(dim={self.dim})"
+
+
+class Replicate(Placement):
+    def is_replicated(self):
+        return True
+
+    def _torch(self):
+        return _dt.Replicate()
+
+    def __eq__(self, o):
+        return isinstance(o, Replicate)
+
+    def __hash__(self):
+        return hash("R")
+
+    def __repr__(self):
+        return "Replicate()"
+
+
+class Partial(Placement):
+    def __init__(self, reduce_type=None):
+        from ..collective import ReduceOp
+
+        self.reduce_type = ReduceOp.SUM if reduce_type is None else reduce_type
+
+    def is_partial(self):
+        return True
+
+    def _torch(self):
+        from ..collective import ReduceOp
+
+        op = {ReduceOp.SUM: "sum", ReduceOp.AVG: "avg", ReduceOp.MAX: "max", ReduceOp.MIN: "min"}[self.reduce_type]
+        return _dt.Partial(op)
+
+    def __eq__(self, o):
+        return isinstance(o, Partial) and o.reduce_type == self.reduce_type
+
+    def __hash__(self):
+        return hash(("P", self.reduce_type))
+
+    def __repr__(self):
+        return f"Partial(reduce_type={self.reduce_type})"
+
+
+def _from_torch_placement(p):
+    if isinstance(p, _dt.Shard):
+        return Shard(p.dim)
+    if isinstance(p, _dt.Replicate):
+        return Replicate()
+    return Partial()
+
+
+# ----------------------------------------------------------------------------- ProcessMesh
+_MESH_CACHE: dict = {}
+
+
+class ProcessMesh:
+    def __init__(self, mesh=None, dim_names=None, shape=None, process_ids=None):
+        if mesh is None:
+            mesh = np.array(process_ids).reshape(shape)
+        self._mesh = np.array(mesh, dtype=np.int64)
+        if dim_names is None:
+            dim_names = [f"d{i}" for i in range(self._mesh.ndim)]
+        assert len(dim_names) == self._mesh.ndim
+        self._dim_names = list(dim_names)
+
+    @property
+    def mesh(self):
+        return self._mesh
+
+    @property
+    def shape(self):
+        return list(self._mesh.shape)
+
+    @property
+    def ndim(self):
+        return self._mesh.ndim
+
+    @property
+    def dim_names(self):
+        return self._dim_names
+
+    @property
+    def process_ids(self):
+        return self._mesh.reshape(-1).tolist()
+
+    def get_dim_size(self, dim):
+        if isinstance(dim, str):
+            dim = self._dim_names.index(dim)
+        return self._mesh.shape[dim]
+
+    def get_mesh_with_dim(self, dim_name, index=None):
+        ax = self._dim_names.index(dim_name)
+        order = [ax] + [i for i in range(self.ndim) if i != ax]
+        m = np.transpose(self._mesh, order)
+        names = [self._dim_names[i] for i in order]
+        if index is None:
+            return ProcessMesh(m, names)
+        return ProcessMesh(m[index], names[1:])
+
+    def __getitem__(self, idx):
+        sub = self._mesh[idx]
+        if np.ndim(sub) == 0:
+            return ProcessMesh(np.array([int(sub)]), [self._dim_names[-1]])
+        kept = [n for n, s in zip(self._dim_names, (idx if isinstance(idx, tuple) else (idx,)))
+                if isinstance(s, slice)]
+        kept += self._dim_names[len(idx) if isinstance(idx, tuple) else 1:]
+        return ProcessMesh(sub, kept[:np.ndim(sub)])
+
+    def contains(self, rank):
+        return rank in self.process_ids
+
+    def __eq__(self, o):
+        return isinstance(o, ProcessMesh) and np.array_equal(o._mesh, self._mesh) and o._dim_names == self._dim_names
+
+    def __hash__(self):
+        return hash((self._mesh.tobytes(), tuple(self._mesh.shape), tuple(self._dim_names)))
+
+    def __repr__(self):
+        return f"ProcessMesh(shape={self.shape}, process_ids={self.process_ids}, dim_names={self._dim_names})"
+
+    def _device_mesh(self):
+        """torch DeviceMesh for this rank grid (collective: every rank must call it in the same order)."""
+        key = hash(self)
+        dm = _MESH_CACHE.get(key)
+        if dm is None:
+            from .. import collective as C
+
+            C.init_parallel_env()
+            dev = current_torch_device().type
+            dm = _dt.DeviceMesh(dev, torch.tensor(self._mesh), mesh_dim_names=tuple(self._dim_names))
+            _MESH_CACHE[key] = dm
+        return dm
+
+
+_global_mesh = None
+
+
+def set_mesh(mesh):
+    global _global_mesh
+    _global_mesh = mesh
+
+
+def get_mesh():
+    return _global_mesh
+
+
+# ----------------------------------------------------------------------------- DistTensor API
+def _torch_placements(mesh, placements):
+    out = [p._torch() if isinstance(p, Placement) else p for p in placements]
+    while len(out) < mesh.ndim:
+        out.append(_dt.Replicate())
+    return out
+
+
+def is_dist_tensor(t):
+    return isinstance(getattr(t, "_t", None), _dt.DTensor)
+
+
+def _attach(w, mesh):
+    w.process_mesh = mesh
+    return w
+
+
+def shard_tensor(data, mesh, placements, dtype=None, place=None, stop_gradient=None):
+    """Distribute a (replicated, identical on every rank) global tensor by ``placements``."""
+    from ...framework.tensor import to_tensor
+
+    t = data if isinstance(data, Tensor) else to_tensor(data, dtype=dtype)
+    src = t._t
+    if dtype is not None:
+        from ...framework.dtype import convert_dtype
+
+        src = src.to(convert_dtype(dtype))
+    dm = mesh._device_mesh()
+    src = src.to(dm.device_type if dm.device_type == "cpu" else current_torch_device())
+    if isinstance(src, _dt.DTensor):
+        out = src.redistribute(dm, _torch_placements(mesh, placements))
+    else:
+        leaf = src.detach()
+        out = _dt.distribute_tensor(leaf, dm, _torch_placements(mesh, placements))
+    sg = t.stop_gradient if stop_gradient is None else stop_gradient
+    if isinstance(t, Tensor) and hasattr(t, "trainable") and type(t).__name__ in ("Parameter", "EagerParamBase"):
+        from ...framework.param import Parameter
+
+        p = Parameter(out.detach(), name=getattr(t, "name", None))
+        p.stop_gradient = sg
+        return _attach(p, mesh)
+    out = out.detach().requires_grad_(not sg) if not sg else out.detach()
+    return _attach(_wrap(out), mesh)
+
+
+def dtensor_from_local(local_tensor, mesh, placements):
+    lt = local_tensor._t if isinstance(local_tensor, Tensor) else local_tensor
+    out = _dt.DTensor.from_local(lt, mesh._device_mesh(), _torch_placements(mesh, placements), run_check=False)
+    return _attach(_wrap(out), mesh)
+
+
+def dtensor_from_fn(fn, mesh, placements, *args, **kwargs):
+    return shard_tensor(fn(*args, **kwargs), mesh, placements)
+
+
+def reshard(dist_tensor, mesh, placements):
+    t = dist_tensor._t
+    assert isinstance(t, _dt.DTensor), "reshard expects a DistTensor"
+    return _attach(_wrap(t.redistribute(mesh._device_mesh(), _torch_placements(mesh, placements))), mesh)
+
+
+def unshard_dtensor(dist_tensor):
+    t = dist_tensor._t
+    if isinstance(t, _dt.DTensor):
+        return _wrap(t.full_tensor())
+    return dist_tensor
+
+
+def local_tensor(dist_tensor):
+    t = dist_tensor._t
+    return _wrap(t.to_local()) if isinstance(t, _dt.DTensor) else dist_tensor
+
+
+def placements_of(dist_tensor):
+    t = dist_tensor._t
+    return [_from_torch_placement(p) for p in t.placements] if isinstance(t, _dt.DTensor) else None
+
+
+def shard_layer(layer, process_mesh, shard_fn=None, input_fn=None, output_fn=None):
+    """Convert every parameter of ``layer`` to a DistTensor: ``shard_fn(name, sublayer, mesh)`` may
+    shard some of them itself; the rest are replicated over the mesh."""
+    from ...framework.param import Parameter
+
+    if shard_fn is not None:
+        for name, sub in layer.named_sublayers(include_self=True):
+            shard_fn(name, sub, process_mesh)
+    for name, sub in layer.named_sublayers(include_self=True):
+        for pname, p in list(sub._parameters.items()):
+            if p is None or is_dist_tensor(p):
+                continue
+            d = _dt.distribute_tensor(p._t.detach(), process_mesh._device_mesh(),
+                                      _torch_placements(process_mesh, [Replicate()]))
+            np_ = Parameter(d, name=p.name)
+            np_.stop_gradient = p.stop_gradient
+            np_.process_mesh = process_mesh
+            sub._parameters[pname] = np_
+    if input_fn is not None:
+        layer.register_forward_pre_hook(lambda l, inp: input_fn(inp, process_mesh))
+    if output_fn is not None:
+        layer.register_forward_post_hook(lambda l, inp, out: output_fn(out, process_mesh))
+    return layer
+
+
+class _ShardingStageBase:
+    def __init__(self, mesh_dim=None, mesh=None, sharding_mesh_dim=None):
+        self._mesh = mesh or get_mesh()
+        self._dim = mesh_dim if mesh_dim is not None else sharding_mesh_dim
+        if self._dim is None:
+            self._dim = 0
+
+    def _placements_for(self, param):
+        """Optimizer-state placements: param's own placements with the sharding dim set to Shard(0)."""
+        t = param._t
+        mesh = getattr(param, "process_mesh", self._mesh)
+        if isinstance(t, _dt.DTensor):
+            pl = list(t.placements)
+        else:
+            pl = [_dt.Replicate()] * mesh.ndim
+        ax = mesh.dim_names.index(self._dim) if isinstance(self._dim, str) else int(self._dim)
+        if isinstance(pl[ax], _dt.Replicate) and t.shape[0] % mesh.shape[ax] == 0:
+            pl[ax] = _dt.Shard(0)
+        return mesh, pl
+
+
+class ShardingStage1(_ShardingStageBase):
+    stage = 1
+
+
+class ShardingStage2(_ShardingStageBase):
+    stage = 2
+
+
+class ShardingStage3(_ShardingStageBase):
+    stage = 3
+
+
+class _ShardOptimizer:
+    """Optimizer whose accumulators (and, for stage 3, parameters) are sharded over a mesh dim."""
+
+    def __init__(self, optimizer, shard_fn=None, gradient_accumulation_steps=1):
+        self._inner_opt = optimizer
+        self._shard_fn = shard_fn
+        self._gas = gradient_accumulation_steps
+        if shard_fn is not None:
+            orig_acc = optimizer._acc
+
+            def sharded_acc(name, p, like=None, dtype=torch.float32, fill=0.0, _orig=orig_acc):
+                d = optimizer._accumulators[name]
+                t = d.get(p.name)
+                if t is None and isinstance(p._t, _dt.DTensor):
+                    mesh, pl = shard_fn._placements_for(p)
+                    full = torch.full(tuple(p._t.shape), fill, dtype=dtype, device=p._t.to_local().device)
+                    t = _dt.distribute_tensor(full, mesh._device_mesh(), pl)
+                    d[p.name] = t
+                    return t
+                return _orig(name, p, like, dtype, fill)
+
+            optimizer._acc = sharded_acc
+
+    def step(self):
+        self._inner_opt.step()
+
+    def clear_grad(self, set_to_zero=True):
+        self._inner_opt.clear_grad(set_to_zero)
+
+    clear_gradients = clear_grad
+
+    def state_dict(self):
+        return self._inner_opt.state_dict()
+
+    def set_state_dict(self, sd):
+        return self._inner_opt.set_state_dict(sd)
+
+    def __getattr__(self, name):
+        return getattr(self._inner_opt, name)
+
+
+def shard_optimizer(optimizer, shard_fn=None, gradient_accumulation_steps=1):
+    return _ShardOptimizer(optimizer, shard_fn, gradient_accumulation_steps)
+
+
+def shard_scaler(scaler):
+    return scaler
+
+
+class ShardDataloader:
+    """Yields batches as DistTensors sharded on the batch dim over ``shard_dims`` of the mesh."""
+
+    def __init__(self, dataloader, meshes, input_keys=None, shard_dims=None, is_dataset_splitted=False):
+        self._dl = dataloader
+        self._mesh = meshes[0] if isinstance(meshes, (list, tuple)) else meshes
+        self._dims = shard_dims
+        self._split = is_dataset_splitted
+
+    def _convert(self, x):
+        if isinstance(x, Tensor):
+            mesh = self._mesh
+            pl = [Replicate()] * mesh.ndim
+            if self._dims is not None:
+                ax = mesh.dim_names.index(self._dims) if isinstance(self._dims, str) else int(self._dims)
+                pl[ax] = Shard(0)
+            if self._split:
+                return dtensor_from_local(x, mesh, pl)
+            return shard_tensor(x, mesh, pl)
+        if isinstance(x, (list, tuple)):
+            return type(x)(self._convert(e) for e in x)
+        if isinstance(x, dict):
+            return {k: self._convert(v) for k, v in x.items()}
+        return x
+
+    def __iter__(self):
+        for batch in self._dl:
+            yield self._convert(batch)
+
+    def __len__(self):
+        return len(self._dl)
+
+
+def shard_dataloader(dataloader, meshes, input_keys=None, shard_dims=None, is_dataset_splitted=False):
+    return ShardDataloader(dataloader, meshes, input_keys, shard_dims, is_dataset_splitted)
+
+
+class Strategy:
+    """auto_parallel Strategy (config namespaces only; the dygraph engine reads sharding/amp/gradient merge)."""
+
+    class _NS(dict):
+        def __getattr__(self, k):
+            return self.get(k)
+
+        def __setattr__(self, k, v):
+            self[k] = v
+
+    def __init__(self, config=None):
+        config = config or {}
+        for ns in ("sharding", "amp", "recompute", "pipeline", "gradient_merge", "fused_passes"):
+            setattr(self, ns, Strategy._NS(config.get(ns, {"enable": False})))
+
+
+class DistModel:
+    """Dygraph stand-in for the reference's static DistModel: ``__call__(inputs, labels)`` runs one
+    train step (forward, loss, backward, optimizer step) in train mode, or forward+loss in eval mode."""
+
+    def __init__(self, layer, loader=None, loss=None, optimizer=None, strategy=None, metrics=None):
+        self._layer = layer
+        self._loss = loss
+        self._opt = optimizer
+        self._mode = "train" if optimizer is not None else ("eval" if loss is not None else "predict")
+        self.dist_loader = loader
+
+    def train(self):
+        self._mode = "train"
+        self._layer.train()
+
+    def eval(self):
+        self._mode = "eval"
+        self._layer.eval()
+
+    def predict(self):
+        self._mode = "predict"
+        self._layer.eval()
+
+    def __call__(self, *args):
+        if self._mode == "predict":
+            return self._layer(*args)
+        inputs, labels = args[:-1], args[-1]
+        out = self._layer(*inputs)
+        loss = self._loss(out, labels)
+        if self._mode == "train":
+            loss.backward()
+            self._opt.step()
+            self._opt.clear_grad()
+        return loss
+
+    def state_dict(self, mode="all"):
+        sd = dict(self._layer.state_dict())
+        if mode in ("all", "opt") and self._opt is not None:
+            sd.update(self._opt.state_dict())
+        return sd
+
+    def set_state_dict(self, sd):
+        self._layer.set_state_dict(sd)
+
+
+def to_static(layer, loader=None, loss=None, optimizer=None, strategy=None, input_spec=None):
+    return DistModel(layer, loader, loss, optimizer, strategy)

@@ -120,7 +120,7 @@ class Optimizer:
         t = d.get(p.name)
         if t is None:
             ref = p._t if like is None else like
-            t = torch.full(ref.shape, fill, dtype=dtype, device=ref.device)
+            t = torch.full_like(ref, fill, dtype=dtype)  # DistTensor params get DistTensor state
             d[p.name] = t
         return t
 

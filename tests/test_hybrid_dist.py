@@ -31,3 +31,14 @@ def test_fleet_sharding_stage1_matches_single():
 def test_moe_expert_parallel_matches_single():
     for r in run_workers("hybrid_worker.py", 2, ["moe"]):
         assert r["out_diff"] < 1e-5 and r["xg_diff"] < 1e-5 and r["eg"] < 1e-4, r
+
+
+def test_auto_parallel_and_dist_checkpoint(tmp_path):
+    res = run_workers("autoparallel_worker.py", 2, extra_env={"PD_CKPT_DIR": str(tmp_path / "ckpt")})
+    r0, r1 = res
+    assert r0["local_rows"] == [[0, 1, 2, 3], [4, 5, 6, 7]] and r1["local_rows"][0] == [8, 9, 10, 11]
+    for r in res:
+        assert r["replicated_ok"] and r["unshard_ok"], r
+        assert r["linear_diff"] < 1e-5, r
+        assert r["ckpt_shard1_ok"] and r["ckpt_b_ok"] and r["ckpt_dense_ok"], r
+    assert r0["files"] == ["0.metadata", "0_0.distcp", "1_0.distcp"]
