@@ -1,0 +1,78 @@
+// Host-side native runtime of paddle2_amd (no GPU code): rendezvous store, comm watchdog,
+// host event tracer, and the bounded blocking queue used by the data loader.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace pdrt {
+
+// ------------------------------------------------------------------ TCPStore (tcp_store.cpp)
+class TCPStoreServer {
+ public:
+  TCPStoreServer(const std::string& host, int port);
+  ~TCPStoreServer();
+  int port() const;
+  void shutdown();
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
+};
+
+class TCPStoreClient {
+ public:
+  TCPStoreClient(const std::string& host, int port, double timeout_s);
+  ~TCPStoreClient();
+  void set(const std::string& k, const std::string& v);
+  std::string get(const std::string& k);  // blocks until the key exists (or timeout)
+  int64_t add(const std::string& k, int64_t inc);
+  bool check(const std::vector<std::string>& keys);
+  void wait(const std::vector<std::string>& keys);
+  bool remove(const std::string& k);
+  int64_t num_keys();
+  std::string compare_set(const std::string& k, const std::string& expected, const std::string& desired);
+  void set_timeout(double s);
+  double timeout() const { return timeout_s_; }
+
+ private:
+  void send_all(const std::string& b);
+  void recv_all(char* p, size_t n);
+  std::string recv_str();
+  int fd_ = -1;
+  double timeout_s_;
+  std::mutex mu_;
+};
+
+// ------------------------------------------------------------------ host tracer (tracer.cpp)
+struct HostEvent {
+  uint32_t name_id;
+  uint32_t type;  // 0 = user range (RecordEvent), 1 = op, 2 = comm, 3 = dataloader, 4 = optimizer
+  uint64_t tid;
+  uint64_t start_ns, end_ns;
+};
+
+void tracer_enable(bool on);
+bool tracer_enabled();
+void tracer_push(const std::string& name, uint32_t type);
+void tracer_pop();
+void tracer_instant(const std::string& name, uint32_t type, uint64_t start_ns, uint64_t end_ns);
+uint64_t tracer_now_ns();
+void tracer_clear();
+std::vector<HostEvent> tracer_events();
+std::string tracer_name(uint32_t id);
+std::string tracer_chrome_json(int pid);
+
+// ------------------------------------------------------------------ comm watchdog (watchdog.cpp)
+void watchdog_start(double poll_s, bool abort_on_timeout);
+void watchdog_stop();
+int64_t watchdog_begin(const std::string& desc, double timeout_s, uintptr_t hip_event = 0);
+std::vector<int64_t> watchdog_take_finished();
+void watchdog_end(int64_t id);
+std::vector<std::string> watchdog_timed_out();
+int64_t watchdog_inflight();
+
+}  // namespace pdrt

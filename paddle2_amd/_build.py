@@ -1,4 +1,5 @@
-"""Build the native extension ``paddle2_amd._C`` (HIP kernels for gfx950 + pybind11 host glue).
+"""Build the native extensions: ``paddle2_amd._C`` (HIP kernels for gfx950 + pybind11 host glue) and
+``paddle2_amd._runtime`` (host-only C++ runtime: TCPStore, comm watchdog, host tracer, blocking queue).
 
 Invoked by ``__graft_entry__.build()`` and ``python -m paddle2_amd._build``.  Objects are cached
 by content hash under ``build/`` so a rebuild only recompiles what changed.  Everything targets
@@ -99,6 +100,51 @@ def build(verbose=False, jobs=None):
     return out
 
 
+def runtime_target_path():
+    return os.path.join(ROOT, "paddle2_amd", "_runtime" + _ext_suffix())
+
+
+def build_runtime(verbose=False):
+    """Host-only runtime module (g++, pybind11, pthreads); no HIP so it loads on CPU machines too."""
+    rdir = os.path.join(CSRC, "runtime")
+    srcs = sorted(os.path.join(rdir, f) for f in os.listdir(rdir) if f.endswith(".cpp"))
+    import pybind11
+
+    flags = ["-O2", "-std=c++17", "-fPIC", "-I", sysconfig.get_paths()["include"], "-I", pybind11.get_include(),
+             "-I", rdir]
+    h = hashlib.sha1(" ".join(flags).encode())
+    for f in sorted(os.listdir(rdir)):
+        with open(os.path.join(rdir, f), "rb") as fh:
+            h.update(fh.read())
+    key = h.hexdigest()[:16]
+    out = runtime_target_path()
+    stamp = out + ".stamp"
+    if os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key:
+        return out
+    os.makedirs(BUILD, exist_ok=True)
+
+    def comp(src):
+        obj = os.path.join(BUILD, "rt_" + os.path.basename(src) + "." + key + ".o")
+        if not os.path.exists(obj):
+            cmd = ["g++"] + flags + ["-c", src, "-o", obj]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            _run(cmd)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(comp, srcs))
+    tmp = out + ".tmp"
+    _run(["g++", "-shared", "-fPIC"] + objs + ["-o", tmp, "-lpthread"])
+    os.replace(tmp, out)
+    with open(stamp, "w") as f:
+        f.write(key)
+    return out
+
+
+def build_all(verbose=False):
+    return build(verbose=verbose), build_runtime(verbose=verbose)
+
+
 if __name__ == "__main__":
-    p = build(verbose="-v" in sys.argv)
-    print(p)
+    print(build_all(verbose="-v" in sys.argv))

@@ -159,6 +159,12 @@ def init_parallel_env(backend=None, timeout_s=None):
             kw = {}
             if backend == "nccl" and torch.cuda.is_available():
                 kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+            if os.environ.get("PADDLE2_AMD_NATIVE_STORE", "0") == "1":
+                # rendezvous through the native C++ TCPStore (csrc/runtime/tcp_store.cpp)
+                from .store import TorchStore, create_or_get_global_tcp_store
+
+                st = create_or_get_global_tcp_store(rank, world, timeout=tout.total_seconds())
+                kw["store"] = TorchStore(st)
             dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=tout, **kw)
     _default_group = Group(rank, 0, list(range(world)), dist.group.WORLD if dist.is_initialized() else None,
                            name="_default_pg")

@@ -1,48 +1,51 @@
 """Collective hang watchdog (reference: phi/core/distributed/comm_task_manager.cc, nccl_comm_task.cc).
 
-With ``FLAGS_enable_async_trace`` every collective records a start event on the current HIP stream
-and an end event after launch; a background thread polls the events every 10 s and reports
-tasks that were started but not finished after ``FLAGS_comm_timeout_s`` (with op, group ranks,
-sequence number, shape/dtype) — the reference's "started-not-finished" classification.
+With ``FLAGS_enable_async_trace`` every collective records a HIP event on the current stream after
+its launch and registers (description, deadline, event) with the NATIVE watchdog
+(csrc/runtime/watchdog.cpp): a C++ thread polls ``hipEventQuery`` on the in-flight events and
+reports — or with ``FLAGS_comm_abort_on_timeout`` aborts the process — for any collective
+started but not finished after ``FLAGS_comm_timeout_s`` (the reference's "started-not-finished"
+classification), with op, group ranks, sequence number, shape and dtype.  CPU (gloo) collectives
+are host-synchronous; they register without an event and deregister on return.
 """
 from __future__ import annotations
 
 import contextlib
 import itertools
 import logging
-import os
 import threading
-import time
 
 import torch
 
 from ..framework import flags
 
 _log = logging.getLogger("paddle2_amd.distributed.watchdog")
-_tasks = {}
+_events = {}          # native task id -> torch Event kept alive until the native thread reports it done
 _lock = threading.Lock()
 _seq = itertools.count()
-_thread = None
-_stop = threading.Event()
+_started = False
 
 
-class CommTask:
-    __slots__ = ("seq", "op", "ranks", "shape", "dtype", "t0", "start_ev", "end_ev", "reported")
+def _rt():
+    from .. import _rt
 
-    def __init__(self, seq, op, ranks, shape, dtype):
-        self.seq, self.op, self.ranks, self.shape, self.dtype = seq, op, ranks, shape, dtype
-        self.t0 = time.time()
-        self.start_ev = self.end_ev = None
-        self.reported = False
-
-    def finished(self):
-        if self.end_ev is None:
-            return True
-        return self.end_ev.query()
+    return _rt.get()
 
 
 def enabled():
     return bool(flags.flag("FLAGS_enable_async_trace", False))
+
+
+def _timeout():
+    return float(flags.flag("FLAGS_comm_timeout_s", 1800))
+
+
+def _prune():
+    done = _rt().watchdog_take_finished()
+    if done:
+        with _lock:
+            for i in done:
+                _events.pop(i, None)
 
 
 @contextlib.contextmanager
@@ -50,57 +53,43 @@ def track(op, group, tensor):
     if not enabled():
         yield
         return
+    maybe_start()
     t = tensor._t if hasattr(tensor, "_t") else tensor
-    ranks = getattr(group, "ranks", None)
-    task = CommTask(next(_seq), op, ranks, tuple(t.shape), str(t.dtype))
-    if t.device.type == "cuda":
-        task.start_ev = torch.cuda.Event()
-        task.start_ev.record()
+    desc = (f"seq={next(_seq)} op={op} ranks={getattr(group, 'ranks', None)} shape={tuple(t.shape)} "
+            f"dtype={t.dtype}")
+    rt = _rt()
+    if t.device.type != "cuda":
+        tid = rt.watchdog_begin(desc, _timeout(), 0)
+        try:
+            yield
+        finally:
+            rt.watchdog_end(tid)
+        return
     try:
         yield
     finally:
-        if t.device.type == "cuda":
-            task.end_ev = torch.cuda.Event()
-            task.end_ev.record()
+        ev = torch.cuda.Event()
+        ev.record()
+        tid = rt.watchdog_begin(desc, _timeout(), int(ev.cuda_event))
         with _lock:
-            _tasks[task.seq] = task
+            _events[tid] = ev
+        _prune()
 
 
 def check_once(timeout_s=None):
-    """Return descriptions of tasks started but not finished past the timeout; drop finished ones."""
-    timeout_s = timeout_s if timeout_s is not None else float(flags.flag("FLAGS_comm_timeout_s", 1800))
-    now = time.time()
-    hung = []
-    with _lock:
-        for seq in list(_tasks):
-            tk = _tasks[seq]
-            if tk.finished():
-                del _tasks[seq]
-            elif now - tk.t0 > timeout_s and not tk.reported:
-                tk.reported = True
-                hung.append(f"[watchdog] collective seq={tk.seq} op={tk.op} ranks={tk.ranks} shape={tk.shape} "
-                            f"dtype={tk.dtype} started {now - tk.t0:.1f}s ago and has not finished")
-    for h in hung:
-        _log.error(h)
-    return hung
+    """Descriptions of every collective the native watchdog has reported as timed out."""
+    _prune()
+    return list(_rt().watchdog_timed_out())
 
 
-def _loop(interval):
-    while not _stop.wait(interval):
-        try:
-            check_once()
-        except Exception:  # pragma: no cover
-            pass
-
-
-def maybe_start(interval=10.0):
-    global _thread
-    if not enabled() or _thread is not None:
+def maybe_start(interval=1.0):
+    global _started
+    if _started or not enabled():
         return
-    _thread = threading.Thread(target=_loop, args=(interval,), daemon=True, name="pd-comm-watchdog")
-    _thread.start()
+    _rt().watchdog_start(float(interval), bool(flags.flag("FLAGS_comm_abort_on_timeout", False)))
+    _started = True
 
 
 def pending():
-    with _lock:
-        return len(_tasks)
+    _prune()
+    return int(_rt().watchdog_inflight())

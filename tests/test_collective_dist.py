@@ -20,3 +20,33 @@ def test_collectives_and_dataparallel():
     assert r0["scatter"] == [1.0, 1.0] and r1["scatter"] == [2.0, 2.0]
     assert r1["p2p"] == [42.0]
     assert r0["batch_p2p"] == [1.0] and r1["batch_p2p"] == [0.0]
+
+
+def test_collectives_over_native_store():
+    """Same collectives with the process group rendezvousing through the native C++ TCPStore."""
+    res = run_workers("collective_worker.py", 2, extra_env={"PADDLE2_AMD_NATIVE_STORE": "1"})
+    for r in res:
+        assert r["all_reduce"] == [3.0, 3.0, 3.0] and r["dp_diff"] < 1e-5
+
+
+def test_native_store_api():
+    import threading
+    import time
+
+    from paddle2_amd.distributed.store import TCPStore
+
+    master = TCPStore("127.0.0.1", 0, is_master=True, world_size=2, timeout=10)
+    peer = TCPStore("127.0.0.1", master.port, is_master=False, world_size=2, timeout=10)
+    master.set("k", "v")
+    assert peer.get("k") == b"v"
+    assert master.add("c", 2) == 2 and peer.add("c", 5) == 7
+    threading.Timer(0.2, lambda: peer.set("late", b"1")).start()
+    t = time.time()
+    master.wait("late")
+    assert time.time() - t >= 0.15
+    th = threading.Thread(target=peer.barrier, args=("b0",))
+    th.start()
+    master.barrier("b0")
+    th.join(5)
+    assert not th.is_alive()
+    master.shutdown()
