@@ -105,6 +105,7 @@ class Reducer:
         off = b.offsets[pi]
         n = p._t.numel()
         p._t.grad = b.buf[off:off + n].view_as(p._t)
+        p._keep_grad_storage = True  # optimizer.clear_grad zeroes the bucket view in place
 
     def rebind(self):
         """Re-point .grad at the bucket views (after user code replaced/cleared grads)."""

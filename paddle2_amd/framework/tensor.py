@@ -112,6 +112,10 @@ class Tensor:
     @property
     def grad(self):
         g = self._t.grad
+        if g is None and getattr(self, "_lazy_zero_grad", False):
+            # cleared with set_to_zero=True (optimizer.clear_grad): materialise the zeros on demand
+            g = torch.zeros_like(self._t)
+            self._t.grad = g
         return None if g is None else Tensor._wrap(g)
 
     @grad.setter

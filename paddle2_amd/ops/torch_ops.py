@@ -455,8 +455,6 @@ class _FlashFn(torch.autograd.Function):
             dq = torch.empty(B, Sq, Hq, D, dtype=q.dtype, device=q.device)
             dk = torch.empty(B, Sk, Hk, D, dtype=q.dtype, device=q.device)
             dv = torch.empty(B, Sk, Hk, D, dtype=q.dtype, device=q.device)
-            dq32 = torch.zeros(B, Sq, Hq, D, dtype=torch.float32, device=q.device)
-            delta = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
             if not _row_view_ok(out):
                 out = out.contiguous()
             assert out.stride(1) == do.stride(1), "out/dout row strides must match"

@@ -45,8 +45,11 @@ class MultiTensorTable:
         self.pdt = N.DT_CODE[params[0].dtype] if params[0] is not None else self.gdt
         self.device = dev
         self.has_master = master is not None and any(x is not None for x in master)
-        # keep referenced storages alive for the table's lifetime
-        self._refs = (params, grads, m, v, master)
+        # Keep the persistent storages (params, moments, master weights) alive for the table's
+        # lifetime.  Gradients are NOT referenced: they are re-created every step (lazy-zero
+        # clear_grad) and callers re-validate a cached table against the current grad pointers, so
+        # holding them here would pin a whole extra gradient set in HBM.
+        self._refs = (params, m, v, master)
 
     @classmethod
     def for_grads(cls, grads):

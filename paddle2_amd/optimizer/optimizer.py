@@ -89,10 +89,15 @@ class Optimizer:
             g = p._t.grad
             if g is None:
                 continue
-            if set_to_zero:
-                g.zero_()
+            if set_to_zero and getattr(p, "_keep_grad_storage", False):
+                g.zero_()  # grad is a view into a communication bucket: keep the storage
             else:
+                # Lazy zero: drop the buffer so the next backward's AccumulateGrad adopts the fresh
+                # gradient instead of launching a fill now and a read-modify-write add later (one
+                # fill + one add per parameter per step); reading ``p.grad`` before that backward
+                # materialises zeros, so set_to_zero semantics are unchanged.
                 p._t.grad = None
+                p._lazy_zero_grad = bool(set_to_zero)
 
     clear_gradients = clear_grad
 
