@@ -206,32 +206,36 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
         s[kb] = mfma(a, qf[ks], s[kb]);
       }
     }
-    // ---- scale, mask, online softmax (lane owns query qrow; 32 of the 64 keys)
+    // ---- mask, online softmax (lane owns query qrow; 32 of the 64 keys).  The max is taken on raw
+    // scores and the 1/sqrt(d)*log2(e) scale is folded into one FMA feeding v_exp_f32; masking is
+    // a separate, wave-uniformly skipped pass so the common (unmasked) tile has no branches.
     const bool need_mask = (n0 + BN > Sk) || (CAUSAL && (n0 + BN - 1 > m0 + off));
+    if (need_mask) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = n0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          s[kb][i] = (key >= Sk || (CAUSAL && key > qrow + off)) ? -INFINITY : s[kb][i];
+        }
+      }
+    }
     float mx = -INFINITY;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float v = s[kb][i] * sl2;
-        if (need_mask) {
-          const int key = n0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (key >= Sk || (CAUSAL && key > qrow + off)) v = -INFINITY;
-        }
-        s[kb][i] = v;
-        mx = fmaxf(mx, v);
-      }
+      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[kb][i]);
     }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_i, mx);
+    const float m_new = fmaxf(m_i, mx * sl2);
     const float base = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f(m_i - base);
+    const float alpha = __builtin_amdgcn_exp2f(m_i - base);
     float ls = 0.f;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = exp2f(s[kb][i] - base);
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[kb][i], sl2, -base));
         s[kb][i] = p;
         ls += p;
       }
@@ -392,8 +396,8 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
     }
     if (tid < BMQ) {
       const int q = q0 + tid;
-      plse = q < Sq ? LSE[((long)b * Hq + hq) * Sq + q] * kLog2e : INFINITY;
-      pdel = q < Sq ? DELTA[((long)b * Hq + hq) * Sq + q] : 0.f;
+      plse = q < Sq ? -LSE[((long)b * Hq + hq) * Sq + q] / scale : -INFINITY;
+      pdel = q < Sq ? -DELTA[((long)b * Hq + hq) * Sq + q] : 0.f;
     }
   };
   if (ntot > 0) gload(0);
@@ -443,26 +447,34 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
     __syncthreads();
     if (step + 1 < ntot) gload(step + 1);  // lands while this step computes
 
-    // S = Q.K^T and dP = dO.V^T : rows = q (regs), cols = this wave's 32 keys (lanes)
-    f32x16 sacc = f32x16{}, dpacc = f32x16{};
+    // S' = Q.K^T - lse/scale and dP' = dO.V^T - delta: the row constants are the accumulators'
+    // initial values (loaded straight from LDS into the accumulator registers), so P = exp2(S' *
+    // scale*log2e) and dS = P * dP' need no further per-element subtraction.
+    f32x16 sacc, dpacc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qi = (i & 3) + 8 * (i >> 2) + 4 * h;
+      sacc[i] = lse_s[qi];
+      dpacc[i] = del_s[qi];
+    }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int o = o_qrow ^ (ks << 5);
       sacc = mfma(lds_b128(qimg, o), lds_b128(kimg, o_krow ^ (ks << 5)), sacc);
       dpacc = mfma(lds_b128(doimg, o), vf[ks], dpacc);
     }
-    // P = exp2(S*scale*log2e - lse*log2e), dS = P * (dP - delta)
+    // P = exp2(S*scale*log2e - lse*log2e), dS = P * (dP - delta).  Branch-free mask: row q0+qi is
+    // masked for this lane's key iff dlim + qi < 0, dlim = q0 + off - key (causal; huge when the
+    // step needs no mask), -huge for keys past Sk.
     const bool need_mask = (k0 + BNK > Sk) || (CAUSAL && (k0 + BNK - 1 > q0 + off));
+    int dlim = (CAUSAL && need_mask) ? (q0 + off - mykey) : (1 << 30);
+    if (mykey >= Sk) dlim = -(1 << 30);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int qi = (i & 3) + 8 * (i >> 2) + 4 * h;
-      float p = exp2f(sacc[i] * sl2 - lse_s[qi]);
-      if (need_mask) {
-        const int q = q0 + qi;
-        if (mykey >= Sk || (CAUSAL && mykey > q + off)) p = 0.f;
-      }
-      sacc[i] = p;
-      dpacc[i] = p * (dpacc[i] - del_s[qi]);
+      const float p = __builtin_amdgcn_exp2f(sacc[i] * sl2);
+      sacc[i] = (dlim + qi < 0) ? 0.f : p;
+      dpacc[i] = sacc[i] * dpacc[i];
     }
     // dV^T += dO^T . P ; dK^T += Q^T . dS   (A operands by transposed reads, permuted k)
 #pragma unroll

@@ -16,3 +16,9 @@ for b in 2 4; do
   rc=$?; echo "bench b$b rc=$rc"; tail -2 gpurun_out/bench_b$b.log
   ok $rc || exit $rc
 done
+python - <<'PY' > gpurun_out/top_kernels.txt
+import csv
+rows = list(csv.DictReader(open("gpurun_out/prof/run_kernel_stats.csv")))
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:30]:
+    print(f"{float(r['TotalDurationNs'])/3e6:8.2f} ms/step {int(r['Calls'])/3:7.1f} calls {float(r['AverageNs'])/1e3:9.1f} us  {r['Name'][:100]}")
+PY
