@@ -1,0 +1,74 @@
+"""Launcher / spawn (reference tests: test/legacy_test/test_launch_coverage.py, test_spawn_and_init_parallel_env.py)."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+WORKER = r'''
+import os, sys
+sys.path.insert(0, %r)
+import paddle2_amd as paddle
+import paddle2_amd.distributed as dist
+dist.init_parallel_env()
+t = paddle.to_tensor([float(dist.get_rank() + 1)])
+dist.all_reduce(t)
+assert float(t) == sum(range(1, dist.get_world_size() + 1))
+assert os.environ["PADDLE_TRAINERS_NUM"] == str(dist.get_world_size())
+if os.environ.get("FAIL_ONCE") and not os.path.exists(os.environ["FAIL_ONCE"]) and dist.get_rank() == 1:
+    open(os.environ["FAIL_ONCE"], "w").close()
+    sys.exit(3)
+print("OK rank", dist.get_rank(), flush=True)
+''' % ROOT
+
+
+def _env():
+    env = dict(os.environ, PYTHONPATH=ROOT, PADDLE2_AMD_DEVICE="cpu", PADDLE_DISTRI_BACKEND="gloo")
+    return env
+
+
+def test_launch_single_node(tmp_path):
+    w = tmp_path / "w.py"
+    w.write_text(WORKER)
+    r = subprocess.run([sys.executable, "-m", "paddle2_amd.distributed.launch", "--nproc_per_node", "2", "--log_dir",
+                        str(tmp_path / "log"), str(w)], env=_env(), capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    assert "OK rank 0" in r.stdout
+    assert "OK rank 1" in (tmp_path / "log" / "workerlog.1").read_text()
+
+
+def test_launch_restarts_failed_pod(tmp_path):
+    w = tmp_path / "w.py"
+    w.write_text(WORKER)
+    env = _env()
+    env["FAIL_ONCE"] = str(tmp_path / "failed_once")
+    r = subprocess.run([sys.executable, "-m", "paddle2_amd.distributed.launch", "--nproc_per_node", "2",
+                        "--max_restart", "1", "--log_dir", str(tmp_path / "log"), str(w)], env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    assert "restarting pod" in r.stderr
+
+
+def test_launch_propagates_failure(tmp_path):
+    w = tmp_path / "w.py"
+    w.write_text("import sys; sys.exit(5)\n")
+    r = subprocess.run([sys.executable, "-m", "paddle2_amd.distributed.launch", "--nproc_per_node", "2", "--log_dir",
+                        str(tmp_path / "log"), str(w)], env=_env(), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 5
+
+
+def _spawn_fn(x):
+    import paddle2_amd as paddle
+    import paddle2_amd.distributed as dist
+
+    dist.init_parallel_env()
+    t = paddle.to_tensor([x])
+    dist.all_reduce(t)
+    assert float(t) == x * dist.get_world_size()
+
+
+def test_spawn():
+    os.environ["PADDLE2_AMD_DEVICE"] = "cpu"
+    import paddle2_amd.distributed as dist
+
+    dist.spawn(_spawn_fn, args=(2.0,), nprocs=2, backend="gloo")
