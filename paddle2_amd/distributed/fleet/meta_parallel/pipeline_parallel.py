@@ -247,11 +247,19 @@ class PipelineParallel(MetaParallelBase):
         return self.pp_group.backend == "nccl"
 
     def _exchange(self, ops):
-        """ops: list of (is_send, tensor, peer_stage) -> one batched group."""
+        """ops: list of (is_send, tensor, peer_stage) -> one batched group.  Each tensor of a transfer
+        gets its own tag (its index among the ops with that peer and direction) so transports that
+        match by (peer, tag) rather than by issue order (gloo) pair them correctly."""
         if not ops:
             return
-        p2p = [dist.P2POp(dist.isend if s else dist.irecv, t, self._peer(st), group=self.pp_group.pg)
-               for s, t, st in ops]
+        seen = {}
+        p2p = []
+        for s, t, st in ops:
+            k = (s, st)
+            tag = seen.get(k, 0)
+            seen[k] = tag + 1
+            p2p.append(dist.P2POp(dist.isend if s else dist.irecv, t, self._peer(st), group=self.pp_group.pg,
+                                  tag=tag))
         for w in dist.batch_isend_irecv(p2p):
             w.wait()
 

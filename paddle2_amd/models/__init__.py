@@ -1,3 +1,3 @@
 """Model zoo: Llama (flagship), GPT, LeNet/ResNet (vision)."""
-from .llama import (LlamaConfig, LlamaForCausalLM, LlamaModel, LlamaPretrainingCriterion,  # noqa: F401
-                    llama_flops_per_token)
+from .llama import (LlamaConfig, LlamaForCausalLM, LlamaForCausalLMPipe, LlamaModel,  # noqa: F401
+                    LlamaPretrainingCriterion, llama_flops_per_token)

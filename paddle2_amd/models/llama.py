@@ -303,3 +303,80 @@ def llama_flops_per_token(cfg: LlamaConfig, seq_len: int) -> float:
     n = L * per_layer + h * V
     attn = L * 2 * 2 * seq_len * h / 2  # QK^T + PV, causal half, fwd
     return 6.0 * n + 3.0 * attn
+
+
+# ============================================================================ pipeline-parallel form
+class LlamaEmbeddingPipe(nn.Layer):
+    """Stage-0 head of the pipeline: token ids -> hidden states."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        init = nn.ParamAttr(initializer=I.Normal(0.0, config.initializer_range))
+        if config.tensor_parallel_degree > 1:
+            from ..distributed.fleet.layers.mpu import VocabParallelEmbedding
+
+            self.embed_tokens = VocabParallelEmbedding(config.vocab_size, config.hidden_size, weight_attr=init)
+        else:
+            self.embed_tokens = nn.Embedding(config.vocab_size, config.hidden_size, weight_attr=init)
+        if config.dtype in ("bfloat16", "float16"):
+            self.to(dtype=config.dtype)
+
+    def forward(self, input_ids):
+        return self.embed_tokens(input_ids)
+
+
+class LlamaDecoderLayerPipe(LlamaDecoderLayer):
+    """Decoder layer exchanging ``(hidden, residual)`` between pipeline stages (the first layer gets
+    the bare embedding output)."""
+
+    def __init__(self, config, layer_idx=0):
+        rope = LlamaRotaryEmbedding(config.head_dim, config.max_position_embeddings, config.rope_theta)
+        super().__init__(config, rope)
+        self.config = config
+        if config.dtype in ("bfloat16", "float16"):
+            self.to(dtype=config.dtype)
+
+    def forward(self, hidden, residual=None):
+        if self.config.recompute and self.training:
+            from ..distributed.fleet.recompute import recompute
+
+            return recompute(super().forward, hidden, residual, None)
+        return super().forward(hidden, residual, None)
+
+
+class LlamaNormPipe(nn.Layer):
+    def __init__(self, config):
+        super().__init__()
+        self.norm = LlamaRMSNorm(config)
+        if config.dtype in ("bfloat16", "float16"):
+            self.to(dtype=config.dtype)
+
+    def forward(self, hidden, residual=None):
+        if residual is None:
+            return self.norm(hidden)
+        out, _ = self.norm(hidden, residual)
+        return out
+
+
+class LlamaLMHeadPipe(LlamaLMHead):
+    def __init__(self, config):
+        super().__init__(config)
+        if config.dtype in ("bfloat16", "float16"):
+            self.to(dtype=config.dtype)
+
+
+def LlamaForCausalLMPipe(config, num_stages=None, topology=None, seg_method="layer:LlamaDecoderLayerPipe",
+                         num_virtual_pipeline_stages=None, recompute_interval=0):
+    """Llama as a ``PipelineLayer`` (reference pattern: PaddleNLP LlamaForCausalLMPipe on
+    fleet.meta_parallel.PipelineLayer): embedding | decoder layers | norm | LM head, loss =
+    LlamaPretrainingCriterion; segmentation balances decoder layers across stages."""
+    from ..distributed.fleet.meta_parallel import LayerDesc, PipelineLayer
+
+    descs = [LayerDesc(LlamaEmbeddingPipe, config)]
+    descs += [LayerDesc(LlamaDecoderLayerPipe, config, i) for i in range(config.num_hidden_layers)]
+    descs += [LayerDesc(LlamaNormPipe, config), LayerDesc(LlamaLMHeadPipe, config)]
+    crit = LlamaPretrainingCriterion(config)
+    return PipelineLayer(descs, num_stages=num_stages, topology=topology, loss_fn=crit, seg_method=seg_method,
+                         num_virtual_pipeline_stages=num_virtual_pipeline_stages,
+                         recompute_interval=recompute_interval)

@@ -42,3 +42,14 @@ def test_auto_parallel_and_dist_checkpoint(tmp_path):
         assert r["linear_diff"] < 1e-5, r
         assert r["ckpt_shard1_ok"] and r["ckpt_b_ok"] and r["ckpt_dense_ok"], r
     assert r0["files"] == ["0.metadata", "0_0.distcp", "1_0.distcp"]
+
+
+def test_pipeline_llama_matches_single():
+    _close(run_workers("hybrid_worker.py", 2, ["pp_llama", "1"]), 1e-4)
+
+
+def test_tp2_pp2_llama_trains():
+    res = run_workers("hybrid_worker.py", 4, ["pp_llama", "2"])
+    for r in res:
+        assert r["losses"] == res[0]["losses"]  # loss broadcast over the pipe group, identical over mp
+        assert r["losses"][1] < r["losses"][0] + 1.0

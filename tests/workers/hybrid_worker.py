@@ -249,6 +249,68 @@ def run_moe():
     write_result({"out_diff": out_diff, "xg_diff": xg_diff, "eg": eg})
 
 
+def run_pp_llama(mp):
+    from paddle2_amd.models import LlamaConfig, LlamaForCausalLM, LlamaForCausalLMPipe
+
+    pp = world // mp
+    M = 2
+    strategy = fleet.DistributedStrategy()
+    strategy.hybrid_configs = {"dp_degree": 1, "mp_degree": mp, "pp_degree": pp}
+    strategy.pipeline_configs = {"accumulate_steps": M, "micro_batch_size": 1}
+    fleet.init(is_collective=True, strategy=strategy)
+    cfg = LlamaConfig.tiny(dtype="float32", num_hidden_layers=4, tensor_parallel_degree=mp)
+    g = torch.Generator().manual_seed(8)
+    data = [torch.randint(0, cfg.vocab_size, (M, 17), generator=g) for _ in range(2)]
+    paddle.seed(4)
+    pipe = LlamaForCausalLMPipe(cfg)
+    model = fleet.distributed_model(pipe)
+    opt = fleet.distributed_optimizer(paddle.optimizer.SGD(0.5, parameters=model.parameters()))
+    full = {}
+    if mp == 1:
+        # single-process reference with the same weights (pipe param names -> LlamaForCausalLM names)
+        for c, vs in enumerate(pipe._chunk_vstages):
+            lo = pipe.segment_parts[vs]
+            for i, item in enumerate(pipe._model_chunks[c]._items):
+                idx = lo + i
+                for k, v in item.state_dict().items():
+                    if idx == 0:
+                        name = "llama." + k
+                    elif idx <= cfg.num_hidden_layers:
+                        name = f"llama.layers.{idx - 1}." + k
+                    elif idx == cfg.num_hidden_layers + 1:
+                        name = "llama." + k
+                    else:
+                        name = "lm_head." + k
+                    full[name] = v._t.detach().clone()
+    losses = []
+    for ids in data:
+        ids = paddle.Tensor._wrap(ids)
+        losses.append(float(model.train_batch([ids[:, :-1], ids[:, 1:]], opt)))
+    out = {"losses": losses}
+    if mp == 1:
+        objs = [None] * world
+        torch.distributed.all_gather_object(objs, {k: v.numpy() for k, v in full.items()})
+        merged = {}
+        for o in objs:
+            merged.update(o)
+        ref = LlamaForCausalLM(LlamaConfig.tiny(dtype="float32", num_hidden_layers=4))
+        ref.set_state_dict({k: paddle.to_tensor(v) for k, v in merged.items()})
+        ro = paddle.optimizer.SGD(0.5, parameters=ref.parameters())
+        rl = []
+        for ids in data:
+            tot = 0.0
+            for mb in range(M):
+                x = paddle.Tensor._wrap(ids[mb:mb + 1])
+                l = ref(x[:, :-1], labels=x[:, 1:]) / M
+                l.backward()
+                tot += float(l)
+            ro.step()
+            ro.clear_grad()
+            rl.append(tot)
+        out["ref"] = rl
+    write_result(out)
+
+
 if mode == "tp":
     run_tp()
 elif mode == "pp":
@@ -257,3 +319,5 @@ elif mode == "dpsh":
     run_dpsh()
 elif mode == "moe":
     run_moe()
+elif mode == "pp_llama":
+    run_pp_llama(int(sys.argv[2]))
