@@ -36,6 +36,8 @@ int pd_ce_bwd(int, const void*, const int64_t*, const float*, const float*, void
 int pd_embed_fwd(int, const int64_t*, const void*, void*, long, int, long, long, void*);
 int pd_embed_bwd(int, const int64_t*, const void*, float*, long, int, long, long, long, void*);
 int pd_cast_from_f32(int, const float*, void*, long, void*);
+int pd_fp8_cast(int, int, const void*, void*, void*, long, long, const float*, float*, void*);
+int pd_fp8_update_scale(float*, int, float*, float*, float*, float, float, void*);
 int pd_flash_fwd(int, const void*, const void*, const void*, void*, float*, int, int, int, int, int, int, long, long,
                  long, long, float, int, void*);
 int pd_flash_bwd(int, const void*, const void*, const void*, const void*, const void*, const float*, float*, void*,
@@ -140,6 +142,18 @@ PYBIND11_MODULE(_C, m) {
     check(pd_embed_bwd(dt, P<const int64_t*>(ids), P<const void*>(dout), P<float*>(dw32), Ntok, H, start, Vl,
                        padding_idx, P<void*>(st)),
           "embed_bwd");
+  });
+  m.def("fp8_cast", [](int dt, int e5m2, uintptr_t x, uintptr_t y, uintptr_t yT, long R, long C, uintptr_t scale,
+                       uintptr_t amax, uintptr_t st) {
+    check(pd_fp8_cast(dt, e5m2, P<const void*>(x), P<void*>(y), P<void*>(yT), R, C, P<const float*>(scale),
+                      P<float*>(amax), P<void*>(st)),
+          "fp8_cast");
+  });
+  m.def("fp8_update_scale", [](uintptr_t hist, int len, uintptr_t amax, uintptr_t scale, uintptr_t inv,
+                               float fp8_max, float margin, uintptr_t st) {
+    check(pd_fp8_update_scale(P<float*>(hist), len, P<float*>(amax), P<float*>(scale), P<float*>(inv), fp8_max,
+                              margin, P<void*>(st)),
+          "fp8_update_scale");
   });
   m.def("cast_from_f32", [](int dt, uintptr_t src, uintptr_t dst, long n, uintptr_t st) {
     check(pd_cast_from_f32(dt, P<const float*>(src), P<void*>(dst), n, P<void*>(st)), "cast_from_f32");

@@ -1,0 +1,176 @@
+// FP8 (OCP e4m3fn / e5m2) casting for delayed-scaling fp8 GEMMs on gfx950.
+//
+// Reference behaviour: the fp8 GEMM path of the reference (tensor/linalg.py:329
+// fp8_fp8_half_gemm_fused; phi/kernels/fusion/gpu/fp8_*) quantizes activations/weights with a
+// per-tensor scale.  The MI355X design follows the delayed-scaling recipe: the scale used for
+// this step's cast comes from the amax HISTORY (known before the cast), and the cast kernel
+// computes this tensor's amax in the same pass (one read of the bf16 tensor), so quantization
+// is a single fused pass:
+//   * cast_amax:            y = sat(x * scale) -> fp8, amax = max|x|            (row-major)
+//   * cast_transpose_amax:  y = sat(x * scale) and yT = y^T -> fp8, amax       (64x64 LDS tiles)
+// The transposed copy is what the column-major B operand of the fp8 GEMM wants for the weight
+// (forward) and for x / dy (weight-gradient GEMM).  Conversion uses v_cvt_pk_fp8_f32 /
+// v_cvt_pk_bf8_f32 (OCP encodings on gfx950) after saturating to the format's max finite value.
+#include "common.h"
+
+namespace pd {
+namespace fp8 {
+
+template <bool E5M2>
+__device__ __forceinline__ unsigned pack4(float a, float b, float c, float d) {
+  constexpr float kMax = E5M2 ? 57344.f : 448.f;
+  a = fminf(fmaxf(a, -kMax), kMax);
+  b = fminf(fmaxf(b, -kMax), kMax);
+  c = fminf(fmaxf(c, -kMax), kMax);
+  d = fminf(fmaxf(d, -kMax), kMax);
+  int w;
+  if (E5M2) {
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, w, true);
+  } else {
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  }
+  return (unsigned)w;
+}
+
+// non-negative floats order like their bit patterns -> integer atomicMax
+__device__ __forceinline__ void atomic_max_pos(float* addr, float v) {
+  atomicMax(reinterpret_cast<unsigned*>(addr), __float_as_uint(v));
+}
+
+template <typename T, bool E5M2>
+__global__ __launch_bounds__(256) void cast_amax_kernel(const T* __restrict__ x, uint8_t* __restrict__ y, long n,
+                                                        const float* __restrict__ scale, float* __restrict__ amax) {
+  const float s = scale[0];
+  float m = 0.f;
+  const long n8 = n / 8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float v[8];
+    constexpr int W = 16 / sizeof(T);  // 8 bf16 or 4 fp32 per 16-B load
+#pragma unroll
+    for (int j = 0; j < 8; j += W) {
+      float t[W];
+      load_vec<T, W>(x + i * 8 + j, t);
+#pragma unroll
+      for (int q = 0; q < W; ++q) v[j + q] = t[q];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
+    uint2 o;
+    o.x = pack4<E5M2>(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
+    o.y = pack4<E5M2>(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
+    *reinterpret_cast<uint2*>(y + i * 8) = o;
+  }
+  for (long i = n8 * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {  // tail
+    const float v = Elt<T>::ld(x + i);
+    m = fmaxf(m, fabsf(v));
+    y[i] = (uint8_t)(pack4<E5M2>(v * s, 0.f, 0.f, 0.f) & 0xff);
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0 && amax) atomic_max_pos(amax, m);
+}
+
+// x [R, C] -> y [R, C] (optional) and yT [C, R]; one 64x64 tile per workgroup, staged through LDS
+template <typename T, bool E5M2>
+__global__ __launch_bounds__(256) void cast_transpose_amax_kernel(const T* __restrict__ x, uint8_t* __restrict__ y,
+                                                                  uint8_t* __restrict__ yT, int R, int C,
+                                                                  const float* __restrict__ scale,
+                                                                  float* __restrict__ amax) {
+  __shared__ float tile[64][65];
+  const float s = scale[0];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+  float m = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int r = r0 + ty + 4 * k, c = c0 + tx;
+    float v = 0.f;
+    if (r < R && c < C) v = Elt<T>::ld(x + (long)r * C + c);
+    m = fmaxf(m, fabsf(v));
+    tile[ty + 4 * k][tx] = v * s;
+  }
+  __syncthreads();
+  if (y) {
+    // row-major copy: each thread writes 4 consecutive bytes of one row
+    const int row = threadIdx.x >> 4, cq = (threadIdx.x & 15) * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int rr = row + 16 * k, r = r0 + rr, c = c0 + cq;
+      if (r < R) {
+        const unsigned w = pack4<E5M2>(tile[rr][cq], tile[rr][cq + 1], tile[rr][cq + 2], tile[rr][cq + 3]);
+        if (c + 3 < C) *reinterpret_cast<unsigned*>(y + (long)r * C + c) = w;
+        else
+          for (int j = 0; j < 4 && c + j < C; ++j) y[(long)r * C + c + j] = (uint8_t)((w >> (8 * j)) & 0xff);
+      }
+    }
+  }
+  {
+    // transposed copy: row of yT = column of x
+    const int col = threadIdx.x >> 4, rq = (threadIdx.x & 15) * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int cc = col + 16 * k, c = c0 + cc, r = r0 + rq;
+      if (c < C) {
+        const unsigned w = pack4<E5M2>(tile[rq][cc], tile[rq + 1][cc], tile[rq + 2][cc], tile[rq + 3][cc]);
+        if (r + 3 < R) *reinterpret_cast<unsigned*>(yT + (long)c * R + r) = w;
+        else
+          for (int j = 0; j < 4 && r + j < R; ++j) yT[(long)c * R + r + j] = (uint8_t)((w >> (8 * j)) & 0xff);
+      }
+    }
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0 && amax) atomic_max_pos(amax, m);
+}
+
+// delayed-scaling bookkeeping on device: roll the amax history, new scale = fp8_max / max(history)
+// / 2^margin (kept when the history is all zero), and the matching inverse scale for the GEMM.
+__global__ void update_scale_kernel(float* __restrict__ hist, int len, float* __restrict__ amax,
+                                    float* __restrict__ scale, float* __restrict__ inv_scale, float fp8_max,
+                                    float margin_pow2) {
+  if (threadIdx.x != 0) return;
+  for (int i = len - 1; i > 0; --i) hist[i] = hist[i - 1];
+  hist[0] = amax[0];
+  float m = 0.f;
+  for (int i = 0; i < len; ++i) m = fmaxf(m, hist[i]);
+  float s = scale[0];
+  if (m > 0.f && isfinite(m)) s = fp8_max / m / margin_pow2;
+  scale[0] = s;
+  inv_scale[0] = 1.f / s;
+  amax[0] = 0.f;
+}
+
+}  // namespace fp8
+}  // namespace pd
+
+using namespace pd;
+
+extern "C" int pd_fp8_cast(int dt, int e5m2, const void* x, void* y, void* yT, long R, long C, const float* scale,
+                           float* amax, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (yT == nullptr) {
+    const long n = R * C;
+    long g = (n / 8 + 255) / 256;
+    if (g < 1) g = 1;
+    if (g > 8192) g = 8192;
+#define PD_FP8_CAST(E)                                                                                           \
+  PD_DISPATCH_FLOAT(dt, T, fp8::cast_amax_kernel<T, E><<<(int)g, 256, 0, st>>>((const T*)x, (uint8_t*)y, n, scale, \
+                                                                               amax))
+    if (e5m2) { PD_FP8_CAST(true); } else { PD_FP8_CAST(false); }
+#undef PD_FP8_CAST
+  } else {
+    dim3 grid((unsigned)((C + 63) / 64), (unsigned)((R + 63) / 64));
+#define PD_FP8_CT(E)                                                                                        \
+  PD_DISPATCH_FLOAT(dt, T, fp8::cast_transpose_amax_kernel<T, E><<<grid, 256, 0, st>>>(                        \
+                               (const T*)x, (uint8_t*)y, (uint8_t*)yT, (int)R, (int)C, scale, amax))
+    if (e5m2) { PD_FP8_CT(true); } else { PD_FP8_CT(false); }
+#undef PD_FP8_CT
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int pd_fp8_update_scale(float* hist, int len, float* amax, float* scale, float* inv_scale, float fp8_max,
+                                   float margin_pow2, void* stream) {
+  fp8::update_scale_kernel<<<1, 64, 0, (hipStream_t)stream>>>(hist, len, amax, scale, inv_scale, fp8_max, margin_pow2);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,134 @@
+"""FP8 (OCP e4m3fn / e5m2) linear layers with delayed scaling on MI355X.
+
+Reference: the reference's fp8 GEMM entry ``fp8_fp8_half_gemm_fused`` (python/paddle/tensor/
+linalg.py:329 -> phi/kernels/fusion/gpu/fp8_gemm) with per-tensor scales; SURVEY §7.2 item 8
+("fp8 e4m3/e5m2 GEMM with per-tensor scales plus an amax history recipe").
+
+Recipe (HYBRID format): forward operands x, W in e4m3fn; the output gradient in e5m2.  Each
+tensor role keeps an amax history on the device; the scale used for a cast is derived from the
+history BEFORE the cast (delayed scaling), and the cast kernel (csrc/kernels/fp8.hip) records the
+tensor's amax in the same pass, so quantization is one fused read of the bf16 tensor — plus the
+transposed copy the column-major B operand needs.  The GEMMs are plain library fp8 GEMMs
+(hipBLASLt through ``torch._scaled_mm``) with the inverse scales as dequant factors and bf16 out.
+A CPU emulation (quantize -> dequantize -> fp32 matmul) keeps the recipe testable without a GPU.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as N
+
+E4M3 = torch.float8_e4m3fn
+E5M2 = torch.float8_e5m2
+_MAX = {E4M3: 448.0, E5M2: 57344.0}
+
+
+class FP8TensorMeta:
+    """Device-resident delayed-scaling state of one tensor role."""
+
+    def __init__(self, fmt=E4M3, history_len=16, margin=0, device=None):
+        dev = device or torch.device("cpu")
+        self.fmt = fmt
+        self.history = torch.zeros(history_len, dtype=torch.float32, device=dev)
+        self.amax = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.scale = torch.ones(1, dtype=torch.float32, device=dev)
+        self.inv_scale = torch.ones(1, dtype=torch.float32, device=dev)
+        self.margin = margin
+
+    def to(self, device):
+        for k in ("history", "amax", "scale", "inv_scale"):
+            setattr(self, k, getattr(self, k).to(device))
+        return self
+
+    def update(self):
+        """Roll the history, recompute scale = fp8_max / max(history) / 2^margin, reset amax."""
+        if self.amax.device.type == "cuda" and N.use_native(self.amax):
+            N.native().fp8_update_scale(self.history.data_ptr(), self.history.numel(), self.amax.data_ptr(),
+                                        self.scale.data_ptr(), self.inv_scale.data_ptr(), _MAX[self.fmt],
+                                        float(2 ** self.margin), N.stream())
+            return
+        self.history.copy_(torch.roll(self.history, 1))
+        self.history[0] = self.amax[0]
+        m = self.history.max()
+        if float(m) > 0 and torch.isfinite(m):
+            self.scale.fill_(_MAX[self.fmt] / float(m) / 2 ** self.margin)
+        self.inv_scale.copy_(1.0 / self.scale)
+        self.amax.zero_()
+
+
+def _dt_code(t):
+    return {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}[t.dtype]
+
+
+def cast(x2, meta: FP8TensorMeta, transpose=False, keep_rowmajor=True):
+    """x2 [R, C] -> (q [R, C] or None, qT [C, R] or None) in meta.fmt, recording amax into meta."""
+    R, C = x2.shape
+    if x2.device.type == "cuda" and N.use_native(x2):
+        x2 = x2.contiguous()
+        q = torch.empty(R, C, dtype=torch.uint8, device=x2.device) if (keep_rowmajor or not transpose) else None
+        qT = torch.empty(C, R, dtype=torch.uint8, device=x2.device) if transpose else None
+        N.native().fp8_cast(_dt_code(x2), int(meta.fmt == E5M2), x2.data_ptr(), N.ptr(q), N.ptr(qT), R, C,
+                            meta.scale.data_ptr(), meta.amax.data_ptr(), N.stream())
+        return (None if q is None else q.view(meta.fmt)), (None if qT is None else qT.view(meta.fmt))
+    xf = x2.float()
+    meta.amax.copy_(torch.maximum(meta.amax, xf.abs().max().reshape(1)))
+    q = (xf * meta.scale).clamp(-_MAX[meta.fmt], _MAX[meta.fmt]).to(meta.fmt)
+    return (q if (keep_rowmajor or not transpose) else None), (q.t().contiguous() if transpose else None)
+
+
+def _mm(a, b_colmajor, inv_a, inv_b, out_dtype, bias=None):
+    """(a * inv_a) @ (b * inv_b) with a row-major [M, K] fp8 and b a column-major [K, N] fp8 view."""
+    if a.device.type == "cuda":
+        return torch._scaled_mm(a, b_colmajor, scale_a=inv_a, scale_b=inv_b, bias=bias, out_dtype=out_dtype)
+    y = (a.float() * inv_a) @ (b_colmajor.float() * inv_b)
+    if bias is not None:
+        y = y + bias.float()
+    return y.to(out_dtype)
+
+
+class _FP8LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, bias, mx, mw, mg):
+        K = x.shape[-1]
+        N_ = w.shape[1]
+        x2 = x.reshape(-1, K)
+        xq, xqT = cast(x2, mx, transpose=True)                   # x [M, K] and x^T [K, M] (for dW)
+        wq, wqT = cast(w, mw, transpose=True)                    # W [K, N] (for dX) and W^T [N, K] (fwd B)
+        out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) else torch.float32
+        y = _mm(xq, wqT.t(), mx.inv_scale, mw.inv_scale, out_dtype,
+                None if bias is None else bias.to(out_dtype))
+        mx.update()
+        mw.update()
+        ctx.save_for_backward(xqT, wq, mx.inv_scale.clone(), mw.inv_scale.clone())
+        ctx.meta = (mg, x.shape, bias is not None, out_dtype, w.dtype)
+        return y.reshape(*x.shape[:-1], N_)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xqT, wq, inv_x, inv_w = ctx.saved_tensors
+        mg, xshape, has_b, out_dtype, wdt = ctx.meta
+        N_ = dy.shape[-1]
+        dy2 = dy.reshape(-1, N_)
+        gq, gqT = cast(dy2, mg, transpose=True)                  # dY [M, N] and dY^T [N, M]
+        dx = _mm(gq, wq.t(), mg.inv_scale, inv_w, out_dtype)     # [M, N] @ [N, K]
+        dw = _mm(xqT, gqT.t(), inv_x, mg.inv_scale, torch.float32)  # [K, M] @ [M, N]
+        db = dy2.float().sum(0).to(wdt) if has_b else None
+        mg.update()
+        return dx.reshape(xshape), dw.to(wdt), db, None, None, None
+
+
+def fp8_linear(x, w, bias, mx, mw, mg):
+    """y = x @ w + bias through e4m3 GEMMs (fwd) and e5m2-gradient GEMMs (bwd); w is [in, out]."""
+    return _FP8LinearFn.apply(x, w, bias, mx, mw, mg)
+
+
+def fp8_gemm(x, y, transpose_x=False, transpose_y=False, bias=None, scale=1.0, output_dtype="bfloat16"):
+    """Plain fp8 x fp8 -> half GEMM (the reference's fp8_fp8_half_gemm_fused): x, y already fp8."""
+    a = x.t() if transpose_x else x
+    b = y.t() if transpose_y else y
+    od = torch.bfloat16 if output_dtype in ("bfloat16", torch.bfloat16) else torch.float16
+    one = torch.ones(1, dtype=torch.float32, device=a.device)
+    sc = torch.full((1,), float(scale), dtype=torch.float32, device=a.device)
+    a = a.contiguous()
+    bcm = b.t().contiguous().t()  # column-major B
+    return _mm(a, bcm, sc, one, od, bias)

@@ -53,3 +53,7 @@ def test_tp2_pp2_llama_trains():
     for r in res:
         assert r["losses"] == res[0]["losses"]  # loss broadcast over the pipe group, identical over mp
         assert r["losses"][1] < r["losses"][0] + 1.0
+
+
+def test_gpt_sequence_parallel_matches_tensor_parallel():
+    _close(run_workers("hybrid_worker.py", 2, ["gpt_sp"]), 1e-4)

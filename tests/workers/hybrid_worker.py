@@ -311,6 +311,39 @@ def run_pp_llama(mp):
     write_result(out)
 
 
+def run_gpt_sp():
+    from paddle2_amd.models import GPTConfig, GPTForCausalLM
+
+    strategy = fleet.DistributedStrategy()
+    strategy.hybrid_configs = {"dp_degree": 1, "mp_degree": world, "pp_degree": 1}
+    fleet.init(is_collective=True, strategy=strategy)
+    g = torch.Generator().manual_seed(6)
+    data = [torch.randint(0, 512, (2, 33), generator=g) for _ in range(3)]
+
+    def run(sp, init_sd=None):
+        paddle.seed(9)
+        m = GPTForCausalLM(GPTConfig.tiny(dtype="float32", tensor_parallel_degree=world, sequence_parallel=sp))
+        if init_sd is not None:
+            m.set_state_dict(init_sd)
+        sd0 = {k: paddle.Tensor._wrap(v._t.detach().clone()) for k, v in m.state_dict().items()}
+        model = fleet.distributed_model(m)
+        opt = fleet.distributed_optimizer(paddle.optimizer.AdamW(1e-2, parameters=model.parameters(),
+                                                                 grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0)))
+        out = []
+        for ids in data:
+            ids = paddle.Tensor._wrap(ids)
+            loss = model(ids[:, :-1], labels=ids[:, 1:])
+            loss.backward()
+            opt.step()
+            opt.clear_grad()
+            out.append(float(loss))
+        return out, sd0
+
+    ref, sd0 = run(False)
+    sp, _ = run(True, sd0)
+    write_result({"losses": sp, "ref": ref})
+
+
 if mode == "tp":
     run_tp()
 elif mode == "pp":
@@ -319,5 +352,7 @@ elif mode == "dpsh":
     run_dpsh()
 elif mode == "moe":
     run_moe()
+elif mode == "gpt_sp":
+    run_gpt_sp()
 elif mode == "pp_llama":
     run_pp_llama(int(sys.argv[2]))
