@@ -30,7 +30,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--micro-batch", type=int, default=4, help="sequences per GPU per step")
-    ap.add_argument("--model", default="llama2-7b", choices=["llama2-7b", "llama2-13b", "tiny"])
+    ap.add_argument("--model", default="llama2-7b",
+                    choices=["llama2-7b", "llama2-13b", "tiny", "gpt3-13b", "gpt3-6.7b", "gpt3-1.3b"])
+    ap.add_argument("--fp8", action="store_true", help="GPT configs: fp8 (e4m3/e5m2 delayed scaling) linears")
     ap.add_argument("--layers", type=int, default=None, help="DEBUG ONLY: override layer count (invalid for the metric)")
     ap.add_argument("--sharding-stage", type=int, default=3)
     ap.add_argument("--recompute", action="store_true")
@@ -64,7 +66,13 @@ def main():
     fleet.init(is_collective=True, strategy=strategy)
     paddle.seed(1234 + rank)
 
-    if args.model == "llama2-7b":
+    is_gpt = args.model.startswith("gpt3")
+    if is_gpt:
+        from paddle2_amd.models import GPTConfig, GPTForCausalLM, gpt_flops_per_token
+
+        cfg = {"gpt3-13b": GPTConfig.gpt3_13b, "gpt3-6.7b": GPTConfig.gpt3_6_7b,
+               "gpt3-1.3b": GPTConfig.gpt3_1_3b}[args.model](use_fp8=args.fp8)
+    elif args.model == "llama2-7b":
         cfg = LlamaConfig.llama2_7b()
     elif args.model == "llama2-13b":
         cfg = LlamaConfig.llama2_13b()
@@ -75,7 +83,7 @@ def main():
         cfg.num_hidden_layers = args.layers
     cfg.recompute = args.recompute
 
-    model = LlamaForCausalLM(cfg)
+    model = GPTForCausalLM(cfg) if is_gpt else LlamaForCausalLM(cfg)
     decay = {p.name for n, p in model.named_parameters() if "norm" not in n}
     opt = paddle.optimizer.AdamW(learning_rate=3e-4, beta1=0.9, beta2=0.95, epsilon=1e-8,
                                  parameters=model.parameters(), weight_decay=0.1,
@@ -130,11 +138,12 @@ def main():
     tokens = b * s * args.steps * world
     tps = tokens / elapsed
     ms = elapsed / args.steps * 1000.0
-    fpt = llama_flops_per_token(cfg, s)
+    fpt = gpt_flops_per_token(cfg, s) if is_gpt else llama_flops_per_token(cfg, s)
     mfu = tps / world * fpt / 2.5e15
     if rank == 0:
         out = {
-            "metric": "tokens/sec (whole node) Llama-2-7B Fleet sharding-3 bf16",
+            "metric": ("tokens/sec (whole node) Llama-2-7B Fleet sharding-3 bf16" if args.model == "llama2-7b"
+                       else f"tokens/sec (whole node) {args.model} {'fp8' if args.fp8 else 'bf16'}"),
             "value": round(tps, 2),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -144,7 +153,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp8(e4m3/e5m2)+bf16" if (is_gpt and args.fp8) else "bf16",
             "data": "synthetic (uniform random token ids), random-init weights",
             "config": {"model": args.model if not args.layers else f"{args.model}-L{args.layers}(debug)",
                        "global_batch": b * world, "seq_len": s, "micro_batch_per_gpu": b,
