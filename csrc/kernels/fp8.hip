@@ -39,6 +39,16 @@ __device__ __forceinline__ void atomic_max_pos(float* addr, float v) {
   atomicMax(reinterpret_cast<unsigned*>(addr), __float_as_uint(v));
 }
 
+// block-wide max, then ONE atomic per workgroup (grids are capped at ~1k workgroups, so the
+// per-tensor amax costs ~1k same-address atomics instead of one per wave of every tile)
+__device__ __forceinline__ void block_amax(float m, float* amax) {
+  __shared__ float red[4];
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0 && amax) atomic_max_pos(amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
+
 template <typename T, bool E5M2>
 __global__ __launch_bounds__(256) void cast_amax_kernel(const T* __restrict__ x, uint8_t* __restrict__ y, long n,
                                                         const float* __restrict__ scale, float* __restrict__ amax) {
@@ -67,11 +77,12 @@ __global__ __launch_bounds__(256) void cast_amax_kernel(const T* __restrict__ x,
     m = fmaxf(m, fabsf(v));
     y[i] = (uint8_t)(pack4<E5M2>(v * s, 0.f, 0.f, 0.f) & 0xff);
   }
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0 && amax) atomic_max_pos(amax, m);
+  block_amax(m, amax);
 }
 
-// x [R, C] -> y [R, C] (optional) and yT [C, R]; one 64x64 tile per workgroup, staged through LDS
+// x [R, C] -> y [R, C] (optional) and yT [C, R].  Grid-stride over 64x64 tiles: each thread loads
+// 2 x 16 B of bf16 along a row, the scaled tile is staged in LDS as fp32 ([64][65], conflict-free
+// column reads), then written row-major and transposed as 4-byte fp8 words.
 template <typename T, bool E5M2>
 __global__ __launch_bounds__(256) void cast_transpose_amax_kernel(const T* __restrict__ x, uint8_t* __restrict__ y,
                                                                   uint8_t* __restrict__ yT, int R, int C,
@@ -79,48 +90,72 @@ __global__ __launch_bounds__(256) void cast_transpose_amax_kernel(const T* __res
                                                                   float* __restrict__ amax) {
   __shared__ float tile[64][65];
   const float s = scale[0];
-  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+  const int tilesC = (C + 63) / 64, tilesR = (R + 63) / 64;
+  const int ntiles = tilesC * tilesR;
   float m = 0.f;
+  const bool vec = (C % 8) == 0 && sizeof(T) == 2;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int r0 = (t / tilesC) * 64, c0 = (t % tilesC) * 64;
+    if (vec) {
+      // 64 rows x 8 chunks of 8 elements; 256 threads -> 2 chunks each
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int r = r0 + ty + 4 * k, c = c0 + tx;
-    float v = 0.f;
-    if (r < R && c < C) v = Elt<T>::ld(x + (long)r * C + c);
-    m = fmaxf(m, fabsf(v));
-    tile[ty + 4 * k][tx] = v * s;
-  }
-  __syncthreads();
-  if (y) {
-    // row-major copy: each thread writes 4 consecutive bytes of one row
-    const int row = threadIdx.x >> 4, cq = (threadIdx.x & 15) * 4;
+      for (int k = 0; k < 2; ++k) {
+        const int idx = threadIdx.x + 256 * k, rr = idx >> 3, cc = (idx & 7) * 8;
+        const int r = r0 + rr, c = c0 + cc;
+        float v[8];
+        if (r < R && c + 7 < C) {
+          if constexpr (sizeof(T) == 2) load_vec<T, 8>(x + (long)r * C + c, v);
+        } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int rr = row + 16 * k, r = r0 + rr, c = c0 + cq;
-      if (r < R) {
-        const unsigned w = pack4<E5M2>(tile[rr][cq], tile[rr][cq + 1], tile[rr][cq + 2], tile[rr][cq + 3]);
-        if (c + 3 < C) *reinterpret_cast<unsigned*>(y + (long)r * C + c) = w;
-        else
-          for (int j = 0; j < 4 && c + j < C; ++j) y[(long)r * C + c + j] = (uint8_t)((w >> (8 * j)) & 0xff);
+          for (int j = 0; j < 8; ++j) v[j] = (r < R && c + j < C) ? Elt<T>::ld(x + (long)r * C + c + j) : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          m = fmaxf(m, fabsf(v[j]));
+          tile[rr][cc + j] = v[j] * s;
+        }
+      }
+    } else {
+      const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int r = r0 + ty + 4 * k, c = c0 + tx;
+        float v = 0.f;
+        if (r < R && c < C) v = Elt<T>::ld(x + (long)r * C + c);
+        m = fmaxf(m, fabsf(v));
+        tile[ty + 4 * k][tx] = v * s;
       }
     }
-  }
-  {
-    // transposed copy: row of yT = column of x
-    const int col = threadIdx.x >> 4, rq = (threadIdx.x & 15) * 4;
+    __syncthreads();
+    if (y) {
+      const int row = threadIdx.x >> 4, cq = (threadIdx.x & 15) * 4;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int cc = col + 16 * k, c = c0 + cc, r = r0 + rq;
-      if (c < C) {
-        const unsigned w = pack4<E5M2>(tile[rq][cc], tile[rq + 1][cc], tile[rq + 2][cc], tile[rq + 3][cc]);
-        if (r + 3 < R) *reinterpret_cast<unsigned*>(yT + (long)c * R + r) = w;
-        else
-          for (int j = 0; j < 4 && r + j < R; ++j) yT[(long)c * R + r + j] = (uint8_t)((w >> (8 * j)) & 0xff);
+      for (int k = 0; k < 4; ++k) {
+        const int rr = row + 16 * k, r = r0 + rr, c = c0 + cq;
+        if (r < R) {
+          const unsigned w = pack4<E5M2>(tile[rr][cq], tile[rr][cq + 1], tile[rr][cq + 2], tile[rr][cq + 3]);
+          if (c + 3 < C) *reinterpret_cast<unsigned*>(y + (long)r * C + c) = w;
+          else
+            for (int j = 0; j < 4 && c + j < C; ++j) y[(long)r * C + c + j] = (uint8_t)((w >> (8 * j)) & 0xff);
+        }
       }
     }
+    {
+      const int col = threadIdx.x >> 4, rq = (threadIdx.x & 15) * 4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int cc = col + 16 * k, c = c0 + cc, r = r0 + rq;
+        if (c < C) {
+          const unsigned w = pack4<E5M2>(tile[rq][cc], tile[rq + 1][cc], tile[rq + 2][cc], tile[rq + 3][cc]);
+          if (r + 3 < R) *reinterpret_cast<unsigned*>(yT + (long)c * R + r) = w;
+          else
+            for (int j = 0; j < 4 && r + j < R; ++j) yT[(long)c * R + r + j] = (uint8_t)((w >> (8 * j)) & 0xff);
+        }
+      }
+    }
+    __syncthreads();  // tile reused by the next iteration
   }
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0 && amax) atomic_max_pos(amax, m);
+  block_amax(m, amax);
 }
 
 // delayed-scaling bookkeeping on device: roll the amax history, new scale = fp8_max / max(history)
@@ -152,14 +187,15 @@ extern "C" int pd_fp8_cast(int dt, int e5m2, const void* x, void* y, void* yT, l
     const long n = R * C;
     long g = (n / 8 + 255) / 256;
     if (g < 1) g = 1;
-    if (g > 8192) g = 8192;
+    if (g > 1024) g = 1024;
 #define PD_FP8_CAST(E)                                                                                           \
   PD_DISPATCH_FLOAT(dt, T, fp8::cast_amax_kernel<T, E><<<(int)g, 256, 0, st>>>((const T*)x, (uint8_t*)y, n, scale, \
                                                                                amax))
     if (e5m2) { PD_FP8_CAST(true); } else { PD_FP8_CAST(false); }
 #undef PD_FP8_CAST
   } else {
-    dim3 grid((unsigned)((C + 63) / 64), (unsigned)((R + 63) / 64));
+    long tiles = ((C + 63) / 64) * ((R + 63) / 64);
+    dim3 grid((unsigned)(tiles < 1024 ? tiles : 1024));
 #define PD_FP8_CT(E)                                                                                        \
   PD_DISPATCH_FLOAT(dt, T, fp8::cast_transpose_amax_kernel<T, E><<<grid, 256, 0, st>>>(                        \
                                (const T*)x, (uint8_t*)y, (uint8_t*)yT, (int)R, (int)C, scale, amax))

@@ -97,9 +97,10 @@ class _FP8LinearFn(torch.autograd.Function):
         out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) else torch.float32
         y = _mm(xq, wqT.t(), mx.inv_scale, mw.inv_scale, out_dtype,
                 None if bias is None else bias.to(out_dtype))
+        # dequant factors of THIS step's casts (update() below rolls the scales in place)
+        ctx.save_for_backward(xqT, wq, mx.inv_scale.clone(), mw.inv_scale.clone())
         mx.update()
         mw.update()
-        ctx.save_for_backward(xqT, wq, mx.inv_scale.clone(), mw.inv_scale.clone())
         ctx.meta = (mg, x.shape, bias is not None, out_dtype, w.dtype)
         return y.reshape(*x.shape[:-1], N_)
 
@@ -111,8 +112,8 @@ class _FP8LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, N_)
         gq, gqT = cast(dy2, mg, transpose=True)                  # dY [M, N] and dY^T [N, M]
         dx = _mm(gq, wq.t(), mg.inv_scale, inv_w, out_dtype)     # [M, N] @ [N, K]
-        dw = _mm(xqT, gqT.t(), inv_x, mg.inv_scale, torch.float32)  # [K, M] @ [M, N]
-        db = dy2.float().sum(0).to(wdt) if has_b else None
+        dw = _mm(xqT, gqT.t(), inv_x, mg.inv_scale, wdt if wdt in (torch.bfloat16, torch.float16) else torch.float32)
+        db = dy2.sum(0, dtype=torch.float32).to(wdt) if has_b else None
         mg.update()
         return dx.reshape(xshape), dw.to(wdt), db, None, None, None
 
