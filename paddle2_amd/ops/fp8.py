@@ -34,6 +34,16 @@ class FP8TensorMeta:
         self.scale = torch.ones(1, dtype=torch.float32, device=dev)
         self.inv_scale = torch.ones(1, dtype=torch.float32, device=dev)
         self.margin = margin
+        self.initialized = False
+
+    def init_from(self, x):
+        """First use: no history yet, so scale from the tensor itself (just-in-time) instead of 1.0 —
+        otherwise the first steps' tiny gradients underflow e5m2 and the early updates are lost."""
+        amax = x.detach().abs().amax().float().reshape(1)
+        s = torch.where(amax > 0, _MAX[self.fmt] / amax / 2 ** self.margin, torch.ones_like(amax))
+        self.scale.copy_(s)
+        self.inv_scale.copy_(1.0 / s)
+        self.initialized = True
 
     def to(self, device):
         for k in ("history", "amax", "scale", "inv_scale"):
@@ -63,6 +73,8 @@ def _dt_code(t):
 def cast(x2, meta: FP8TensorMeta, transpose=False, keep_rowmajor=True):
     """x2 [R, C] -> (q [R, C] or None, qT [C, R] or None) in meta.fmt, recording amax into meta."""
     R, C = x2.shape
+    if not meta.initialized:
+        meta.init_from(x2)
     if x2.device.type == "cuda" and N.use_native(x2):
         x2 = x2.contiguous()
         q = torch.empty(R, C, dtype=torch.uint8, device=x2.device) if (keep_rowmajor or not transpose) else None
