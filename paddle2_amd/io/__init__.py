@@ -332,6 +332,8 @@ class DataLoader:
                  prefetch_factor=2, use_shared_memory=True, timeout=0, worker_init_fn=None, persistent_workers=False):
         self.dataset = dataset
         self.return_list = return_list
+        self._use_buffer_reader = use_buffer_reader
+        self._buffer_size = max(2, prefetch_factor)
         self.collate_fn = collate_fn
         self.num_workers = num_workers
         self.batch_size = batch_size
@@ -359,12 +361,11 @@ class DataLoader:
 
     def __iter__(self):
         nb = self._device.type == "cuda"
-        for batch in self._loader:
-            out = _wrap_batch(batch, self._device, nb)
-            if not self.return_list and isinstance(out, list):
-                yield out
-            else:
-                yield out
+        if not self._use_buffer_reader:
+            for batch in self._loader:
+                yield _wrap_batch(batch, self._device, nb)
+            return
+        yield from _BufferedReader(self._loader, self._device, nb, self._buffer_size)
 
     def __call__(self):
         return self.__iter__()
@@ -373,6 +374,53 @@ class DataLoader:
     def from_generator(feed_list=None, capacity=None, use_double_buffer=True, iterable=True, return_list=False,
                        use_multiprocess=False, drop_last=True):
         return _GeneratorLoader()
+
+
+class _BufferedReader:
+    """Double-buffered reader (reference: LoDTensorBlockingQueue + BufferedReader, io/dataloader/
+    dataloader_iter.py:154): a producer thread drains the sampler/worker pipeline, moves each batch
+    to the device with non-blocking copies from pinned memory, and pushes it into the NATIVE bounded
+    blocking queue (csrc/runtime/py_runtime.cpp BlockingQueue, waits with the GIL released); the
+    training loop pops ready batches, so host collation and H2D copies overlap compute."""
+
+    _END = ("__paddle2_amd_end__",)
+
+    def __init__(self, loader, device, non_blocking, capacity):
+        from .. import _rt
+
+        self._q = _rt.get().BlockingQueue(capacity)
+        self._err = None
+
+        def produce():
+            from ..profiler import host_range
+
+            try:
+                for batch in loader:
+                    with host_range("DataLoader.prefetch", 3):
+                        out = _wrap_batch(batch, device, non_blocking)
+                    if not self._q.push(out):
+                        return
+            except BaseException as e:  # surfaced in the consumer
+                self._err = e
+            finally:
+                self._q.push(self._END, 5.0)
+
+        import threading
+
+        self._th = threading.Thread(target=produce, daemon=True, name="pd-buffered-reader")
+        self._th.start()
+
+    def __iter__(self):
+        try:
+            while True:
+                item = self._q.pop()
+                if item is self._END:
+                    break
+                yield item
+            if self._err is not None:
+                raise self._err
+        finally:
+            self._q.close()
 
 
 class _GeneratorLoader:

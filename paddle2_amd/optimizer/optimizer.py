@@ -143,6 +143,14 @@ class Optimizer:
 
     @torch.no_grad()
     def step(self):
+        from ..profiler import _host_on, host_range
+
+        if _host_on:
+            with host_range(f"{type(self).__name__}.step", 4):
+                return self._step_impl()
+        return self._step_impl()
+
+    def _step_impl(self):
         pg = self._params_grads()
         self._clip_coef = None
         if self._grad_clip is not None and pg:

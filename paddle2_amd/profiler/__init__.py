@@ -1,8 +1,11 @@
-"""paddle.profiler (reference: python/paddle/profiler/profiler.py, timer.py Benchmark).
+"""paddle.profiler (reference: python/paddle/profiler/profiler.py, timer.py Benchmark,
+phi/api/profiler/host_tracer.cc, chrome_tracing_logger.cc).
 
-Host events come from ``RecordEvent`` scopes; device activity is collected through torch's
-profiler, which on ROCm is backed by roctracer / rocprofiler-sdk — the reference's ROCm build has
-host-only traces, here HIP kernels (including ours) appear in the chrome trace.
+Host events: ``RecordEvent`` scopes and the framework's own ranges (optimizer step, data loader,
+collectives) go to the NATIVE host tracer (csrc/runtime/tracer.cpp — per-thread buffers, interned
+names, steady-clock ns), which costs one bool test when profiling is off.  Device activity comes
+from torch's profiler, backed on ROCm by rocprofiler-sdk, so HIP kernels (ours included) appear in
+the same chrome trace: ``export`` merges the native host events into the device trace file.
 """
 from __future__ import annotations
 
@@ -70,14 +73,57 @@ def export_protobuf(dir_name, worker_name=None):
     return export_chrome_tracing(dir_name, worker_name)
 
 
-class RecordEvent:
-    """Named host range (also visible in rocprof/roctx traces through torch's record_function)."""
+class TracerEventType(enum.Enum):
+    UserDefined = 0
+    Operator = 1
+    Communication = 2
+    Dataloader = 3
+    Optimization = 4
+    Forward = 5
+    Backward = 6
+    ProfileStep = 7
 
-    def __init__(self, name, event_type=None):
+
+_TYPE_CODE = {TracerEventType.UserDefined: 0, TracerEventType.Operator: 1, TracerEventType.Communication: 2,
+              TracerEventType.Dataloader: 3, TracerEventType.Optimization: 4, TracerEventType.Forward: 1,
+              TracerEventType.Backward: 1, TracerEventType.ProfileStep: 0}
+_host_on = False  # fast path: framework ranges cost one global read when profiling is off
+
+
+def _rt():
+    from .. import _rt as R
+
+    return R.get()
+
+
+@contextlib.contextmanager
+def host_range(name, etype=0):
+    """Framework-internal range for the native tracer (no-op unless a Profiler is recording)."""
+    if not _host_on:
+        yield
+        return
+    rt = _rt()
+    rt.tracer_push(name, etype)
+    try:
+        yield
+    finally:
+        rt.tracer_pop()
+
+
+class RecordEvent:
+    """Named host range: native host tracer + torch record_function (so it also brackets device work
+    in rocprofiler traces)."""
+
+    def __init__(self, name, event_type=TracerEventType.UserDefined):
         self.name = name
+        self._code = _TYPE_CODE.get(event_type, 0) if isinstance(event_type, TracerEventType) else 0
         self._cm = None
+        self._native = False
 
     def begin(self):
+        if _host_on:
+            _rt().tracer_push(self.name, self._code)
+            self._native = True
         self._cm = torch.profiler.record_function(self.name)
         self._cm.__enter__()
 
@@ -85,6 +131,9 @@ class RecordEvent:
         if self._cm is not None:
             self._cm.__exit__(None, None, None)
             self._cm = None
+        if self._native:
+            _rt().tracer_pop()
+            self._native = False
 
     def __enter__(self):
         self.begin()
@@ -117,16 +166,28 @@ class Profiler:
         return torch.profiler.profile(activities=self._acts, record_shapes=self._record_shapes,
                                       profile_memory=self._profile_memory)
 
+    def _host(self, on):
+        global _host_on
+        _host_on = on
+        rt = _rt()
+        if on:
+            rt.tracer_clear()
+        rt.tracer_enable(on)
+
     def start(self):
         self._benchmark.begin()
         if self._timer_only:
             return
+        self._host(True)
         if self._sched is None or self._sched(self._step) in (ProfilerState.RECORD, ProfilerState.RECORD_AND_RETURN):
             self._prof = self._make()
             self._prof.__enter__()
 
     def stop(self):
         self._benchmark.end()
+        if not self._timer_only:
+            self._host_events = _rt().tracer_events()
+            self._host(False)
         if self._prof is not None:
             self._prof.__exit__(None, None, None)
             if self._on_ready is not None:
@@ -157,19 +218,55 @@ class Profiler:
         return self._benchmark.step_info(unit)
 
     def _export(self, path):
+        """One chrome trace: torch/rocprofiler device+op events merged with the native host events."""
         p = getattr(self, "_last", None) or self._prof
+        trace = {"traceEvents": []}
         if p is not None:
-            p.export_chrome_trace(path)
+            tmp = path + ".tmp"
+            p.export_chrome_trace(tmp)
+            with open(tmp) as f:
+                trace = json.load(f)
+            os.remove(tmp)
+        host = getattr(self, "_host_events", None) or _rt().tracer_events()
+        if host:
+            # align the native steady clock to the device trace's time base by its earliest event
+            ev = trace.get("traceEvents", [])
+            ts0 = min((e.get("ts", 0) for e in ev if isinstance(e.get("ts"), (int, float))), default=0)
+            h0 = min(e[3] for e in host)
+            cats = ["UserDefined", "Operator", "Communication", "Dataloader", "Optimization"]
+            pid = os.getpid()
+            for name, code, tid, s_ns, e_ns in host:
+                ev.append({"name": name, "cat": cats[code] if code < 5 else "UserDefined", "ph": "X",
+                           "pid": f"host {pid}", "tid": tid, "ts": ts0 + (s_ns - h0) / 1000.0,
+                           "dur": (e_ns - s_ns) / 1000.0})
+            trace["traceEvents"] = ev
+        with open(path, "w") as f:
+            json.dump(trace, f)
 
     def export(self, path="", format="json"):
         self._export(path)
 
+    def host_statistics(self):
+        """{name: (calls, total_ms, avg_ms, max_ms, min_ms)} over the native host events."""
+        stats = {}
+        for name, code, tid, s_ns, e_ns in getattr(self, "_host_events", None) or []:
+            d = (e_ns - s_ns) / 1e6
+            c, t, mx, mn = stats.get(name, (0, 0.0, 0.0, float("inf")))
+            stats[name] = (c + 1, t + d, max(mx, d), min(mn, d))
+        return {k: (c, t, t / c, mx, mn) for k, (c, t, mx, mn) in stats.items()}
+
     def summary(self, sorted_by=SortedKeys.CPUTotal, op_detail=True, thread_sep=False, time_unit="ms", views=None):
+        lines = []
+        hs = self.host_statistics()
+        if hs:
+            lines.append(f"{'Event':<48}{'Calls':>8}{'Total(ms)':>12}{'Avg(ms)':>10}{'Max(ms)':>10}{'Min(ms)':>10}")
+            for k, (c, t, a, mx, mn) in sorted(hs.items(), key=lambda kv: -kv[1][1]):
+                lines.append(f"{k[:47]:<48}{c:>8}{t:>12.3f}{a:>10.3f}{mx:>10.3f}{mn:>10.3f}")
         p = getattr(self, "_last", None)
-        if p is None:
-            return ""
-        key = "cuda_time_total" if sorted_by in (SortedKeys.GPUTotal, SortedKeys.GPUAvg) else "cpu_time_total"
-        s = p.key_averages().table(sort_by=key, row_limit=50)
+        if p is not None:
+            key = "cuda_time_total" if sorted_by in (SortedKeys.GPUTotal, SortedKeys.GPUAvg) else "cpu_time_total"
+            lines.append(p.key_averages().table(sort_by=key, row_limit=50))
+        s = "\n".join(lines)
         print(s)
         return s
 
