@@ -38,6 +38,10 @@ int pd_embed_bwd(int, const int64_t*, const void*, float*, long, int, long, long
 int pd_cast_from_f32(int, const float*, void*, long, void*);
 int pd_fp8_cast(int, int, const void*, void*, void*, long, long, const float*, float*, void*);
 int pd_fp8_update_scale(float*, int, float*, float*, float*, float, float, void*);
+int pd_decode_attn(const void*, long, long, const void*, const void*, long, long, long, const int*, int, int,
+                   const int*, int, float*, float*, void*, long, long, int, int, int, int, int, float, void*);
+int pd_cache_write(const void*, const void*, long, long, void*, void*, long, long, long, const int*, int, int,
+                   const int*, const int*, int, int, int, void*);
 int pd_flash_fwd(int, const void*, const void*, const void*, void*, float*, int, int, int, int, int, int, long, long,
                  long, long, float, int, void*);
 int pd_flash_bwd(int, const void*, const void*, const void*, const void*, const void*, const float*, float*, void*,
@@ -154,6 +158,24 @@ PYBIND11_MODULE(_C, m) {
     check(pd_fp8_update_scale(P<float*>(hist), len, P<float*>(amax), P<float*>(scale), P<float*>(inv), fp8_max,
                               margin, P<void*>(st)),
           "fp8_update_scale");
+  });
+  m.def("decode_attn", [](uintptr_t q, long sq_b, long sq_h, uintptr_t kc, uintptr_t vc, long s_blk, long s_tok,
+                          long s_head, uintptr_t table, int max_blocks, int block_size, uintptr_t seq_lens, int max_len,
+                          uintptr_t part_o, uintptr_t part_ml, uintptr_t out, long so_b, long so_h, int B, int Hq,
+                          int Hk, int HD, int splits, float scale, uintptr_t st) {
+    check(pd_decode_attn(P<const void*>(q), sq_b, sq_h, P<const void*>(kc), P<const void*>(vc), s_blk, s_tok, s_head,
+                         P<const int*>(table), max_blocks, block_size, P<const int*>(seq_lens), max_len,
+                         P<float*>(part_o), P<float*>(part_ml), P<void*>(out), so_b, so_h, B, Hq, Hk, HD, splits,
+                         scale, P<void*>(st)),
+          "decode_attn");
+  });
+  m.def("cache_write", [](uintptr_t k, uintptr_t v, long sk, long sv, uintptr_t kc, uintptr_t vc, long s_blk,
+                          long s_tok, long s_head, uintptr_t table, int max_blocks, int block_size, uintptr_t tok_b,
+                          uintptr_t tok_p, int n_tok, int Hk, int HD, uintptr_t st) {
+    check(pd_cache_write(P<const void*>(k), P<const void*>(v), sk, sv, P<void*>(kc), P<void*>(vc), s_blk, s_tok,
+                         s_head, P<const int*>(table), max_blocks, block_size, P<const int*>(tok_b),
+                         P<const int*>(tok_p), n_tok, Hk, HD, P<void*>(st)),
+          "cache_write");
   });
   m.def("cast_from_f32", [](int dt, uintptr_t src, uintptr_t dst, long n, uintptr_t st) {
     check(pd_cast_from_f32(dt, P<const float*>(src), P<void*>(dst), n, P<void*>(st)), "cast_from_f32");

@@ -1,0 +1,196 @@
+"""Autoregressive generation for Llama models on a paged KV cache, with the per-token decode step
+captured in a HIP graph.
+
+Prefill runs each prompt through the training kernels (fused-residual RMSNorm, hipBLASLt GEMMs,
+RoPE, causal MFMA flash attention) and stores K/V rows in the paged cache; every decode step
+processes one token per sequence with the flash-decoding kernel.  The decode step has static
+shapes (fixed batch, device-side positions / sequence lengths / block tables, no host syncs),
+so it is captured once with ``torch.cuda.CUDAGraph`` (a hipGraph on ROCm) and replayed: one
+graph launch instead of ~10 kernel launches per layer per token.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..framework.tensor import Tensor
+from ..ops import torch_ops as T
+from . import PagedKVCache, decode_attention, write_kv
+
+
+def sample_logits(logits, temperature=1.0, top_k=0, top_p=1.0, generator=None):
+    """logits [B, V] -> token ids [B] (greedy when temperature == 0)."""
+    if temperature == 0:
+        return logits.argmax(-1)
+    x = logits.float() / max(temperature, 1e-6)
+    if top_k and top_k > 0:
+        kth = torch.topk(x, top_k, dim=-1).values[:, -1:]
+        x = x.masked_fill(x < kth, float("-inf"))
+    if top_p < 1.0:
+        sx, si = torch.sort(x, descending=True, dim=-1)
+        cp = torch.softmax(sx, -1).cumsum(-1)
+        drop = cp - torch.softmax(sx, -1) > top_p
+        sx = sx.masked_fill(drop, float("-inf"))
+        x = torch.full_like(x, float("-inf")).scatter(-1, si, sx)
+    return torch.multinomial(torch.softmax(x, -1), 1, generator=generator).squeeze(-1)
+
+
+class LlamaGenerator:
+    def __init__(self, model, max_batch=8, max_seq_len=4096, block_size=64, num_blocks=None, use_graph=True):
+        self.model = model
+        cfg = model.config
+        self.cfg = cfg
+        self.nh, self.nkv, self.d = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+        dev = model.llama.embed_tokens.weight._t.device
+        self.dev = dev
+        dt = model.llama.embed_tokens.weight._t.dtype
+        if num_blocks is None:
+            num_blocks = max_batch * ((max_seq_len + block_size - 1) // block_size)
+        self.cache = PagedKVCache(cfg.num_hidden_layers, num_blocks, block_size, self.nkv, self.d, max_batch,
+                                  max_seq_len, dtype=dt, device=dev)
+        self.max_batch = max_batch
+        self.max_seq_len = max_seq_len
+        self.cos, self.sin = T.rope_tables(max(max_seq_len, cfg.max_position_embeddings), self.d, cfg.rope_theta,
+                                           interleaved=False, device=dev)
+        self.use_graph = use_graph and dev.type == "cuda"
+        self._graph = None
+        # static decode-step buffers
+        self._tok = torch.zeros(max_batch, dtype=torch.long, device=dev)
+        self._pos = torch.zeros(max_batch, dtype=torch.int32, device=dev)
+        self._lens = torch.zeros(max_batch, dtype=torch.int32, device=dev)
+        self._logits = None
+
+    # ------------------------------------------------------------------ layer pieces
+    def _layer_qkv(self, layer, x, residual):
+        if residual is None:
+            residual = x
+            h = T.rms_norm(x, layer.input_layernorm.weight._t, self.cfg.rms_norm_eps)
+        else:
+            h, residual = T.rms_norm(x, layer.input_layernorm.weight._t, self.cfg.rms_norm_eps, residual)
+        qkv = torch.matmul(h, layer.self_attn.qkv_proj.weight._t)
+        return qkv, residual
+
+    def _layer_out(self, layer, o, residual):
+        a = torch.matmul(o, layer.self_attn.o_proj.weight._t)
+        h, residual = T.rms_norm(a, layer.post_attention_layernorm.weight._t, self.cfg.rms_norm_eps, residual)
+        f = T.swiglu(torch.matmul(h, layer.mlp.gate_up_fused_proj.weight._t))
+        return torch.matmul(f, layer.mlp.down_proj.weight._t), residual
+
+    def _logits_of(self, h, residual):
+        out, _ = T.rms_norm(h, self.model.llama.norm.weight._t, self.cfg.rms_norm_eps, residual)
+        return torch.matmul(out, self.model.lm_head.weight._t)
+
+    # ------------------------------------------------------------------ prefill
+    @torch.no_grad()
+    def prefill(self, slot, ids):
+        """Run prompt ``ids`` (1-D LongTensor) for sequence ``slot``; returns last-token logits [V]."""
+        n = ids.numel()
+        self.cache.allocate(slot, n + 1)
+        nh, nkv, d = self.nh, self.nkv, self.d
+        x = self.model.llama.embed_tokens.weight._t[ids.to(self.dev)][None]  # [1, n, h]
+        pos = torch.arange(n, device=self.dev)
+        residual = None
+        for li, layer in enumerate(self.model.llama.layers):
+            qkv, residual = self._layer_qkv(layer, x, residual)
+            qkv = qkv.view(1, n, nh + 2 * nkv, d)
+            q = T.rope(qkv[:, :, :nh], self.cos, self.sin, None, style=0)
+            k = T.rope(qkv[:, :, nh:nh + nkv], self.cos, self.sin, None, style=0)
+            v = qkv[:, :, nh + nkv:]
+            write_kv(k[0].contiguous(), v[0].contiguous(), self.cache.k[li], self.cache.v[li],
+                     torch.full((n,), slot, device=self.dev), pos, self.cache.block_table)
+            o, _ = T.flash_attention(q, k, v, causal=True)
+            x, residual = self._layer_out(layer, o.reshape(1, n, nh * d), residual)
+        self.cache.seq_lens[slot] = n
+        return self._logits_of(x[:, -1:], residual[:, -1:])[0, 0]
+
+    # ------------------------------------------------------------------ decode
+    def _decode_body(self):
+        nh, nkv, d = self.nh, self.nkv, self.d
+        B = self.max_batch
+        x = self.model.llama.embed_tokens.weight._t[self._tok][:, None]  # [B, 1, h]
+        pos = self._pos.long()
+        residual = None
+        for li, layer in enumerate(self.model.llama.layers):
+            qkv, residual = self._layer_qkv(layer, x, residual)
+            qkv = qkv.view(B, 1, nh + 2 * nkv, d)
+            q = T.rope(qkv[:, :, :nh], self.cos, self.sin, pos[:, None], style=0)
+            k = T.rope(qkv[:, :, nh:nh + nkv], self.cos, self.sin, pos[:, None], style=0)
+            write_kv(k[:, 0].contiguous(), qkv[:, 0, nh + nkv:].contiguous(), self.cache.k[li], self.cache.v[li],
+                     torch.arange(B, device=self.dev), self._pos, self.cache.block_table)
+            o = decode_attention(q[:, 0], self.cache.k[li], self.cache.v[li], self._lens, self.cache.block_table)
+            x, residual = self._layer_out(layer, o.reshape(B, 1, nh * d), residual)
+        return self._logits_of(x, residual)[:, 0]
+
+    @torch.no_grad()
+    def decode_step(self, tokens, positions):
+        """tokens/positions: [max_batch] (inactive slots may hold anything valid) -> logits [B, V]."""
+        self._tok.copy_(tokens)
+        self._pos.copy_(positions)
+        self._lens.copy_(positions + 1)
+        if not self.use_graph:
+            return self._decode_body()
+        if self._graph is None:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):  # warm up allocations outside the graph
+                    self._decode_body()
+            torch.cuda.current_stream().wait_stream(s)
+            self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._graph):
+                self._logits = self._decode_body()
+        self._graph.replay()
+        return self._logits
+
+    # ------------------------------------------------------------------ generate
+    @torch.no_grad()
+    def generate(self, prompts, max_new_tokens=32, temperature=0.0, top_k=0, top_p=1.0, eos_token_id=None,
+                 seed=0):
+        """prompts: list of 1-D id sequences (<= max_batch). Returns list of generated id lists."""
+        assert len(prompts) <= self.max_batch
+        gen = torch.Generator(device=self.dev).manual_seed(seed) if self.dev.type == "cuda" else \
+            torch.Generator().manual_seed(seed)
+        B = self.max_batch
+        toks = torch.zeros(B, dtype=torch.long, device=self.dev)
+        pos = torch.zeros(B, dtype=torch.int32, device=self.dev)
+        outs = [[] for _ in prompts]
+        done = [False] * len(prompts)
+        for i, p in enumerate(prompts):
+            p = torch.as_tensor(p, dtype=torch.long)
+            logits = self.prefill(i, p)
+            t = sample_logits(logits[None], temperature, top_k, top_p, gen)[0]
+            toks[i] = t
+            pos[i] = p.numel()
+            outs[i].append(int(t))
+            self.cache.allocate(i, p.numel() + max_new_tokens + 1)
+        for i in range(len(prompts), B):  # idle slots decode a dummy token at position 0
+            self.cache.allocate(i, max_new_tokens + 2)
+        for _ in range(max_new_tokens - 1):
+            logits = self.decode_step(toks, pos)
+            nxt = sample_logits(logits, temperature, top_k, top_p, gen)
+            pos = pos + 1
+            for i in range(len(prompts)):
+                if done[i]:
+                    continue
+                ti = int(nxt[i])
+                outs[i].append(ti)
+                if eos_token_id is not None and ti == eos_token_id:
+                    done[i] = True
+            toks = nxt
+            if all(done):
+                break
+        for i in range(B):
+            self.cache.free(i)
+        return outs
+
+
+def greedy_reference(model, prompt, max_new_tokens):
+    """Full-recompute greedy decoding with the training forward (test oracle)."""
+    ids = torch.as_tensor(prompt, dtype=torch.long, device=model.llama.embed_tokens.weight._t.device)[None]
+    out = []
+    with torch.no_grad():
+        for _ in range(max_new_tokens):
+            logits = model(Tensor._wrap(ids))._t[0, -1]
+            t = int(logits.argmax())
+            out.append(t)
+            ids = torch.cat([ids, torch.tensor([[t]], device=ids.device)], 1)
+    return out
