@@ -118,3 +118,12 @@ def check_shape(shape):
 
 def get_default_dtype_name():
     return get_default_dtype()
+
+
+def __getattr__(name):
+    # heavier sub-packages load on first use
+    import importlib
+
+    if name in ("inference", "serving", "text", "audio", "geometric", "quantization", "onnx", "hub"):
+        return importlib.import_module(f".{name}", __name__)
+    raise AttributeError(f"module 'paddle2_amd' has no attribute '{name}'")

@@ -52,6 +52,7 @@ class Parameter(Tensor):
         if not isinstance(t, torch.Tensor):
             t = torch.as_tensor(t)
         self._t = t.detach().requires_grad_(bool(trainable) and (t.is_floating_point() or t.is_complex()))
+        self._t._pd_param = self  # lets a static Program find the parameters it references
         self.name = name or _unique_param_name()
         self.optimize_attr = optimize_attr or {"learning_rate": 1.0}
         self.regularizer = regularizer

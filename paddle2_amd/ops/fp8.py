@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import torch
 
+from ..static.graph import graph_op as _graph_op
 from . import _native as N
 
 E4M3 = torch.float8_e4m3fn
@@ -130,6 +131,7 @@ class _FP8LinearFn(torch.autograd.Function):
         return dx.reshape(xshape), dw.to(wdt), db, None, None, None
 
 
+@_graph_op
 def fp8_linear(x, w, bias, mx, mw, mg):
     """y = x @ w + bias through e4m3 GEMMs (fwd) and e5m2-gradient GEMMs (bwd); w is [in, out]."""
     return _FP8LinearFn.apply(x, w, bias, mx, mw, mg)

@@ -551,3 +551,17 @@ def qkv_rope_attention(qkv, num_heads, num_kv_heads, cos, sin, position_ids=None
     k = rope(qkv[:, :, num_heads:num_heads + num_kv_heads], cos, sin, pos, 0)
     o, _ = flash_attention(q, k, qkv[:, :, num_heads + num_kv_heads:], causal, scale)
     return o
+
+
+# Static-graph capture: each native-kernel entry point is recorded as ONE op when called on symbolic
+# tensors (paddle2_amd.static.graph), so executed Programs use the same HIP kernels as dygraph.
+from ..static.graph import graph_op as _graph_op  # noqa: E402
+
+rms_norm = _graph_op(rms_norm)
+layer_norm = _graph_op(layer_norm)
+swiglu = _graph_op(swiglu)
+rope = _graph_op(rope)
+softmax_cross_entropy = _graph_op(softmax_cross_entropy)
+embedding = _graph_op(embedding)
+flash_attention = _graph_op(flash_attention)
+qkv_rope_attention = _graph_op(qkv_rope_attention)

@@ -166,6 +166,15 @@ class Optimizer:
             self._apply(pg)
 
     def minimize(self, loss, startup_program=None, parameters=None, no_grad_set=None):
+        from ..static.graph import SymTensor
+
+        if isinstance(getattr(loss, "_t", None), SymTensor):
+            # static graph: record backward + this optimizer's update into the loss's Program
+            from .. import static as _static
+
+            pg = _static.append_backward(loss, parameter_list=parameters)
+            loss._t._program.append_special("optimize", optimizer=self)
+            return [], pg
         pg = self._params_grads()
         self.step()
         return None, pg

@@ -1,0 +1,213 @@
+"""Program executor (reference: python/paddle/base/executor.py ``Executor.run`` over the
+StandaloneExecutor / PIR interpreter; ``CompiledProgram`` + ``BuildStrategy``).
+
+``run`` replays a recorded Program on real tensors: feeds bind the data variables, each op calls
+its recorded function (torch op or native-kernel entry point) with variable ids resolved, the
+``backward`` op runs the autograd engine from the loss, ``optimize`` runs the (fused) optimizer.
+With ``BuildStrategy.enable_cuda_graph`` a static-shape Program is captured once per feed
+signature in a HIP graph (torch.cuda.CUDAGraph) after a warm-up replay, and later runs copy the
+feeds into the graph's static input buffers and replay the whole step as one graph launch.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+from torch.utils import _pytree as pytree
+
+from ..framework.tensor import Tensor
+from .graph import Program, SymTensor, VarRef, default_main_program
+
+
+class Scope:
+    def __init__(self):
+        self.vars = {}
+
+    def var(self, name):
+        return self.vars.setdefault(name, None)
+
+    def find_var(self, name):
+        return self.vars.get(name)
+
+
+_global_scope = Scope()
+
+
+def global_scope():
+    return _global_scope
+
+
+class BuildStrategy:
+    def __init__(self):
+        self.enable_cuda_graph = False
+        self.fuse_all_optimizer_ops = True
+        self.fuse_elewise_add_act_ops = False
+        self.enable_inplace = True
+        self.memory_optimize = False
+        self.build_cinn_pass = False
+
+
+class ExecutionStrategy:
+    def __init__(self):
+        self.num_threads = 1
+        self.num_iteration_per_drop_scope = 1
+
+
+class CompiledProgram:
+    def __init__(self, program_or_graph, build_strategy=None):
+        self._program = program_or_graph
+        self._build_strategy = build_strategy or BuildStrategy()
+
+    def with_data_parallel(self, *a, **k):
+        return self
+
+
+def _feed_tensor(v, sym, device):
+    if isinstance(v, Tensor):
+        t = v._t
+    elif isinstance(v, torch.Tensor):
+        t = v
+    else:
+        t = torch.as_tensor(np.asarray(v))
+    if sym is not None and t.dtype != sym.dtype and not (t.dtype == torch.float64 and sym.dtype == torch.float32
+                                                         and False):
+        t = t.to(sym.dtype)
+    return t.to(device)
+
+
+class _GraphState:
+    def __init__(self):
+        self.graph = None
+        self.static_in = None
+        self.static_out = None
+
+
+class Executor:
+    def __init__(self, place=None):
+        from ..framework.place import _parse_device, current_torch_device
+
+        self._device = _parse_device(place) if place is not None else current_torch_device()
+        self._graphs = {}
+        self._pruned = {}
+
+    def close(self):
+        self._graphs.clear()
+
+    # ---------------------------------------------------------------- core replay
+    def _replay(self, program, env, grad=None):
+        needs_grad = any(o.kind in ("backward", "grad") for o in program.ops) or bool(grad)
+        ctx = torch.enable_grad() if needs_grad else torch.no_grad()
+
+        def res(x):
+            if isinstance(x, VarRef):
+                if x.vid not in env:
+                    raise RuntimeError(f"variable %{x.vid} has no value (missing feed?)")
+                return env[x.vid]
+            return x
+
+        with ctx:
+            for op in program.ops:
+                if op.kind in ("torch", "native"):
+                    args = pytree.tree_map(res, op.args)
+                    kw = pytree.tree_map(res, op.kwargs)
+                    out = op.fn(*args, **kw)
+                    leaves = pytree.tree_leaves(out)
+                    for vid, val in zip(op.outs, leaves):
+                        if vid is not None:
+                            env[vid] = val
+                elif op.kind == "backward":
+                    loss = env[op.attrs["loss"]]
+                    loss.backward()
+                elif op.kind == "grad":
+                    tgts = [env[v] for v in op.attrs["targets"]]
+                    ins = [env[v] if isinstance(v, int) else v for v in op.attrs["inputs"]]
+                    gs = torch.autograd.grad(tgts, ins, allow_unused=True, retain_graph=True)
+                    for vid, g in zip(op.attrs["outs"], gs):
+                        env[vid] = g if g is not None else torch.zeros_like(ins[0])
+                elif op.kind == "param_grad":
+                    p = op.attrs["param"]
+                    g = p._t.grad
+                    env[op.attrs["out"]] = g if g is not None else torch.zeros_like(p._t)
+                elif op.kind == "optimize":
+                    opt = op.attrs["optimizer"]
+                    with torch.no_grad():
+                        opt.step()
+                    opt.clear_grad(set_to_zero=False)
+        return env
+
+    def run(self, program=None, feed=None, fetch_list=None, feed_var_name="feed", fetch_var_name="fetch", scope=None,
+            return_numpy=True, use_program_cache=False, use_prune=False, _grad=None):
+        strategy = None
+        if isinstance(program, CompiledProgram):
+            strategy = program._build_strategy
+            program = program._program
+        program = program or default_main_program()
+        if not isinstance(program, Program):
+            raise TypeError("Executor.run expects a static Program")
+        feed = feed or {}
+        fetch_list = fetch_list or []
+        if not program.ops and not fetch_list:
+            return []  # startup program: parameters are initialised at creation
+        fetch_ids = [self._fetch_id(program, f) for f in fetch_list]
+        env = {}
+        for name, v in feed.items():
+            sym = program.feeds.get(name)
+            if sym is None:
+                raise KeyError(f"feed '{name}' is not a data variable of this program")
+            env[sym._vid] = _feed_tensor(v, sym, self._device)
+        if not any(o.kind in ("backward", "grad", "optimize", "param_grad") for o in program.ops):
+            # inference: run only the ops the fetch targets depend on (reference use_prune)
+            key = (id(program), len(program.ops), tuple(fetch_ids))
+            pruned = self._pruned.get(key)
+            if pruned is None:
+                from .io import _prune
+
+                pruned = Program()
+                pruned.ops = _prune(program, fetch_ids)
+                pruned.feeds, pruned.vars = program.feeds, program.vars
+                self._pruned[key] = pruned
+            program = pruned
+        if strategy is not None and strategy.enable_cuda_graph and self._device.type == "cuda":
+            outs = self._run_graph(program, env, fetch_ids)
+        else:
+            env = self._replay(program, env, _grad)
+            outs = [env[i] for i in fetch_ids]
+        if return_numpy:
+            return [o.detach().float().cpu().numpy() if o.dtype == torch.bfloat16 else o.detach().cpu().numpy()
+                    for o in outs]
+        return [Tensor._wrap(o if _grad else o.detach()) for o in outs]
+
+    @staticmethod
+    def _fetch_id(program, f):
+        if isinstance(f, Tensor):
+            f = f._t
+        if isinstance(f, SymTensor):
+            return f._vid
+        if isinstance(f, str):
+            for v in program.vars.values():
+                if v._name == f:
+                    return v._vid
+            if f in program.feeds:
+                return program.feeds[f]._vid
+        raise KeyError(f"cannot fetch {f!r}")
+
+    def _run_graph(self, program, env, fetch_ids):
+        key = (id(program), tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(env.items())), tuple(fetch_ids))
+        st = self._graphs.get(key)
+        if st is None:
+            st = _GraphState()
+            st.static_in = {k: v.clone() for k, v in env.items()}
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    e2 = self._replay(program, dict(st.static_in))
+            torch.cuda.current_stream().wait_stream(s)
+            st.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(st.graph):
+                e3 = self._replay(program, dict(st.static_in))
+            st.static_out = [e3[i] for i in fetch_ids]
+            self._graphs[key] = st
+        for k, v in env.items():
+            st.static_in[k].copy_(v)
+        st.graph.replay()
+        return [o.clone() for o in st.static_out]
