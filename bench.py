@@ -161,6 +161,7 @@ def main():
                        "layers": cfg.num_hidden_layers},
             "mfu_vs_2.5PF_dense": round(mfu, 4),
             "final_loss": round(final_loss, 4),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if torch.cuda.is_available() else None,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
