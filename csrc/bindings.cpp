@@ -42,6 +42,12 @@ int pd_decode_attn(const void*, long, long, const void*, const void*, long, long
                    const int*, int, float*, float*, void*, long, long, int, int, int, int, int, float, void*);
 int pd_cache_write(const void*, const void*, long, long, void*, void*, long, long, long, const int*, int, int,
                    const int*, const int*, int, int, int, void*);
+long pd_bn_workspace(int, long, int);
+int pd_bn_fwd_train(int, const void*, const void*, void*, long, int, float*, float*, const float*, const float*, float,
+                    float, float*, float*, float*, int, int, void*);
+int pd_bn_apply(int, const void*, const void*, void*, long, int, const float*, const float*, int, void*);
+int pd_bn_bwd(int, const void*, const void*, const void*, const float*, const float*, const float*, void*, void*,
+              float*, float*, long, int, float*, int, void*);
 int pd_flash_fwd(int, const void*, const void*, const void*, void*, float*, int, int, int, int, int, int, long, long,
                  long, long, float, int, void*);
 int pd_flash_bwd(int, const void*, const void*, const void*, const void*, const void*, const float*, float*, void*,
@@ -196,5 +202,28 @@ PYBIND11_MODULE(_C, m) {
                        P<void*>(dv), P<float*>(dq32), B, Sq, Sk, Hq, Hk, D, sq_row, sk_row, sv_row, so_row, sdq_row,
                        sdk_row, sdv_row, scale, causal, P<void*>(st)),
           "flash_bwd");
+  });
+  m.def("bn_workspace", &pd_bn_workspace);
+  m.def("bn_fwd_train", [](int dt, uintptr_t x, uintptr_t z, uintptr_t y, long M, int C, uintptr_t rm, uintptr_t rv,
+                           uintptr_t g, uintptr_t b, float momentum, float eps, uintptr_t sm, uintptr_t si,
+                           uintptr_t ws, int relu, int upd, uintptr_t st) {
+    check(pd_bn_fwd_train(dt, P<const void*>(x), P<const void*>(z), P<void*>(y), M, C, P<float*>(rm), P<float*>(rv),
+                          P<const float*>(g), P<const float*>(b), momentum, eps, P<float*>(sm), P<float*>(si),
+                          P<float*>(ws), relu, upd, P<void*>(st)),
+          "bn_fwd_train");
+  });
+  m.def("bn_apply", [](int dt, uintptr_t x, uintptr_t z, uintptr_t y, long M, int C, uintptr_t scale, uintptr_t shift,
+                       int relu, uintptr_t st) {
+    check(pd_bn_apply(dt, P<const void*>(x), P<const void*>(z), P<void*>(y), M, C, P<const float*>(scale),
+                      P<const float*>(shift), relu, P<void*>(st)),
+          "bn_apply");
+  });
+  m.def("bn_bwd", [](int dt, uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t mean, uintptr_t invstd, uintptr_t g,
+                     uintptr_t dx, uintptr_t dz, uintptr_t dg, uintptr_t db, long M, int C, uintptr_t ws, int relu,
+                     uintptr_t st) {
+    check(pd_bn_bwd(dt, P<const void*>(dy), P<const void*>(x), P<const void*>(y), P<const float*>(mean),
+                    P<const float*>(invstd), P<const float*>(g), P<void*>(dx), P<void*>(dz), P<float*>(dg),
+                    P<float*>(db), M, C, P<float*>(ws), relu, P<void*>(st)),
+          "bn_bwd");
   });
 }

@@ -14,17 +14,28 @@ _wrap = Tensor._wrap
 
 
 def batch_norm(x, running_mean, running_var, weight=None, bias=None, training=False, momentum=0.9,
-               epsilon=1e-05, data_format="NCHW", use_global_stats=None, name=None):
+               epsilon=1e-05, data_format="NCHW", use_global_stats=None, name=None, act=None, residual=None):
+    """Paddle batch_norm; ``act`` ('relu') and ``residual`` (added before the activation) are
+    fused into the HIP kernel for channels-last activations on the MI355X (the
+    fused_bn_add_activation op of the reference)."""
+    from ...ops.torch_ops import batch_norm_act
+
     t = x._t
     cl = data_format in ("NHWC", "NLC", "NDHWC")
-    if cl:
-        t = t.movedim(-1, 1)
     use_batch = training if use_global_stats is None else (not use_global_stats)
-    # paddle momentum is the weight of the *old* running stat
-    out = F.batch_norm(t, running_mean._t, running_var._t, None if weight is None else weight._t,
-                       None if bias is None else bias._t, use_batch, 1.0 - momentum, epsilon)
-    if cl:
-        out = out.movedim(1, -1)
+    z = residual._t if isinstance(residual, Tensor) else residual
+    w = None if weight is None else weight._t
+    b = None if bias is None else bias._t
+    if t.dim() >= 2:
+        tl = t if cl else t.movedim(1, -1)  # channels-last view (contiguous for channels_last memory)
+        zl = None if z is None else (z if cl else z.movedim(1, -1))
+        out = batch_norm_act(tl, running_mean._t, running_var._t, w, b, use_batch, momentum, epsilon, act, zl)
+        return _wrap(out if cl else out.movedim(-1, 1))
+    out = F.batch_norm(t, running_mean._t, running_var._t, w, b, use_batch, 1.0 - momentum, epsilon)
+    if z is not None:
+        out = out + z
+    if act == "relu":
+        out = torch.relu(out)
     return _wrap(out)
 
 

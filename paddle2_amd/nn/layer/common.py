@@ -654,9 +654,10 @@ class _BatchNormBase(Layer):
         self.register_buffer("_mean", zeros([num_features]))
         self.register_buffer("_variance", ones([num_features]))
 
-    def forward(self, x):
+    def forward(self, x, residual=None, act=None):
+        """``residual``/``act`` (optional, 'relu') fuse ``act(bn(x) + residual)`` into one kernel."""
         return F.batch_norm(x, self._mean, self._variance, self.weight, self.bias, self.training, self._momentum,
-                            self._epsilon, self._data_format, self._use_global_stats)
+                            self._epsilon, self._data_format, self._use_global_stats, act=act, residual=residual)
 
     def extra_repr(self):
         return f"num_features={self._num_features}, momentum={self._momentum}, epsilon={self._epsilon}"
@@ -687,20 +688,27 @@ class BatchNorm(_BatchNormBase):
         self._act = act
 
     def forward(self, x):
-        y = super().forward(x)
-        if self._act:
-            y = getattr(F, self._act)(y)
-        return y
+        if self._act in (None, "relu"):
+            return super().forward(x, act=self._act)
+        return getattr(F, self._act)(super().forward(x))
 
 
 class SyncBatchNorm(_BatchNormBase):
     """Cross-rank BN: batch statistics all-reduced over the default group (RCCL) in training."""
 
-    def forward(self, x):
+    def forward(self, x, residual=None, act=None):
         from ...distributed import collective as C
 
         if not self.training or C.get_world_size() == 1:
-            return super().forward(x)
+            return super().forward(x, residual, act)
+        y = self._sync_forward(x)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if act == "relu" else y
+
+    def _sync_forward(self, x):
+        from ...distributed import collective as C
+
         t = x._t
         cl = self._data_format in ("NHWC", "NLC", "NDHWC")
         if cl:

@@ -565,3 +565,92 @@ softmax_cross_entropy = _graph_op(softmax_cross_entropy)
 embedding = _graph_op(embedding)
 flash_attention = _graph_op(flash_attention)
 qkv_rope_attention = _graph_op(qkv_rope_attention)
+
+
+# ============================================================================ BatchNorm (+add +ReLU), channels-last
+class _BNActFn(torch.autograd.Function):
+    """Training-mode BN over the last (channel) dim of a contiguous [..., C] tensor, with the
+    residual add and ReLU fused (csrc/kernels/batch_norm.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, z, running_mean, running_var, momentum, eps, relu):
+        C_ = N.native()
+        Cn = x.shape[-1]
+        M = x.numel() // Cn
+        dt = _DT[x.dtype]
+        y = torch.empty_like(x)
+        ws = torch.empty(C_.bn_workspace(dt, M, Cn) + 3 * Cn, dtype=torch.float32, device=x.device)
+        mean = torch.empty(Cn, dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
+        w32 = weight.float().contiguous() if weight is not None else None
+        b32 = bias.float().contiguous() if bias is not None else None
+        C_.bn_fwd_train(dt, x.data_ptr(), N.ptr(z), y.data_ptr(), M, Cn, running_mean.data_ptr(),
+                        running_var.data_ptr(), N.ptr(w32), N.ptr(b32), float(momentum), float(eps),
+                        mean.data_ptr(), invstd.data_ptr(), ws.data_ptr(), int(relu), 1, N.stream())
+        ctx.save_for_backward(x, y if relu else None, mean, invstd, w32)
+        ctx.relu, ctx.has_z = relu, z is not None
+        ctx.wdt = weight.dtype if weight is not None else None
+        ctx.bdt = bias.dtype if bias is not None else None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, invstd, w32 = ctx.saved_tensors
+        C_ = N.native()
+        Cn = x.shape[-1]
+        M = x.numel() // Cn
+        dt = _DT[x.dtype]
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        dz = torch.empty_like(x) if (ctx.has_z and ctx.relu) else None
+        dg = torch.empty(Cn, dtype=torch.float32, device=x.device)
+        db = torch.empty_like(dg)
+        ws = torch.empty(C_.bn_workspace(dt, M, Cn) + 3 * Cn, dtype=torch.float32, device=x.device)
+        C_.bn_bwd(dt, dy.data_ptr(), x.data_ptr(), N.ptr(y), mean.data_ptr(), invstd.data_ptr(), N.ptr(w32),
+                  dx.data_ptr(), N.ptr(dz), dg.data_ptr(), db.data_ptr(), M, Cn, ws.data_ptr(), int(ctx.relu),
+                  N.stream())
+        if ctx.has_z and not ctx.relu:
+            dz = dy
+        return (dx, dg.to(ctx.wdt) if ctx.wdt is not None else None, db.to(ctx.bdt) if ctx.bdt is not None else None,
+                dz, None, None, None, None, None)
+
+
+def _bn_act_reference(x, running_mean, running_var, weight, bias, training, momentum, eps, relu, residual):
+    t = x.movedim(-1, 1)
+    y = F.batch_norm(t, running_mean, running_var, weight, bias, training, 1.0 - momentum, eps).movedim(1, -1)
+    if residual is not None:
+        y = y + residual
+    return torch.relu(y) if relu else y
+
+
+def batch_norm_act(x, running_mean, running_var, weight=None, bias=None, training=True, momentum=0.9, eps=1e-5,
+                   act=None, residual=None):
+    """y = act(BN(x) [+ residual]) for a channels-last [..., C] tensor (paddle momentum convention:
+    running = momentum * running + (1 - momentum) * batch).  On the MI355X this is the fused HIP
+    kernel whenever x is channels-last contiguous with fp32 running stats; otherwise the composite
+    PyTorch reference (F.batch_norm + add + relu)."""
+    if act not in (None, "relu"):
+        raise ValueError(f"fused batch norm supports act in (None, 'relu'), got {act!r}")
+    relu = act == "relu"
+    Cn = x.shape[-1]
+    ok = (x.device.type == "cuda" and x.dtype in _DT and x.is_contiguous() and Cn % (4 if x.dtype == torch.float32
+                                                                                     else 8) == 0
+          and running_mean.dtype == torch.float32 and running_var.dtype == torch.float32
+          and running_mean.is_contiguous() and running_var.is_contiguous()
+          and (residual is None or (residual.shape == x.shape and residual.dtype == x.dtype)))
+    if ok and N.use_native(x):
+        if residual is not None:
+            residual = residual.contiguous()
+        if training:
+            return _BNActFn.apply(x, weight, bias, residual, running_mean, running_var, momentum, eps, relu)
+        if not (torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad))):
+            inv = torch.rsqrt(running_var + eps)
+            scale = inv * (weight.float() if weight is not None else 1.0)
+            shift = (bias.float() if bias is not None else 0.0) - running_mean * scale
+            scale = scale.contiguous() if torch.is_tensor(scale) else torch.full_like(running_mean, scale)
+            shift = shift.contiguous()
+            y = torch.empty_like(x)
+            N.native().bn_apply(_DT[x.dtype], x.data_ptr(), N.ptr(residual), y.data_ptr(), x.numel() // Cn, Cn,
+                                scale.data_ptr(), shift.data_ptr(), int(relu), N.stream())
+            return y
+    return _bn_act_reference(x, running_mean, running_var, weight, bias, training, momentum, eps, relu, residual)

@@ -4,6 +4,15 @@ NCHW by default; ``data_format="NHWC"`` keeps activations channels-last, which i
 MIOpen's fastest bf16 convolutions want on the MI355X.
 """
 from ... import nn
+from ...nn.layer.common import _BatchNormBase
+
+
+def _bn_relu(bn, x, residual=None):
+    """relu(bn(x) [+ residual]); one fused HIP kernel for the built-in BatchNorm layers."""
+    if isinstance(bn, _BatchNormBase):
+        return bn(x, residual=residual, act="relu")
+    y = bn(x)
+    return nn.functional.relu(y if residual is None else y + residual)
 
 
 class BasicBlock(nn.Layer):
@@ -22,12 +31,9 @@ class BasicBlock(nn.Layer):
         self.stride = stride
 
     def forward(self, x):
-        identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        if self.downsample is not None:
-            identity = self.downsample(x)
-        return self.relu(out + identity)
+        identity = x if self.downsample is None else self.downsample(x)
+        out = _bn_relu(self.bn1, self.conv1(x))
+        return _bn_relu(self.bn2, self.conv2(out), identity)  # fused BN + add + ReLU
 
 
 class BottleneckBlock(nn.Layer):
@@ -50,13 +56,10 @@ class BottleneckBlock(nn.Layer):
         self.stride = stride
 
     def forward(self, x):
-        identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        if self.downsample is not None:
-            identity = self.downsample(x)
-        return self.relu(out + identity)
+        identity = x if self.downsample is None else self.downsample(x)
+        out = _bn_relu(self.bn1, self.conv1(x))
+        out = _bn_relu(self.bn2, self.conv2(out))
+        return _bn_relu(self.bn3, self.conv3(out), identity)  # fused BN + add + ReLU
 
 
 class ResNet(nn.Layer):
@@ -100,7 +103,7 @@ class ResNet(nn.Layer):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(_bn_relu(self.bn1, self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if self.with_pool:
             x = self.avgpool(x)

@@ -3,6 +3,8 @@
 set -e
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/resnet
+timeout -k 10 600 python -m pytest tests/test_batch_norm_gpu.py -x -q -m gpu > gpurun_out/resnet/bn_tests.log 2>&1 || { tail -30 gpurun_out/resnet/bn_tests.log; exit 1; }
+tail -2 gpurun_out/resnet/bn_tests.log
 timeout -k 10 600 python scripts/bench_resnet50.py --steps 20 --warmup 5 --batch 256 > gpurun_out/resnet/nhwc.json 2> gpurun_out/resnet/nhwc.err
 cat gpurun_out/resnet/nhwc.json
 timeout -k 10 600 python scripts/bench_resnet50.py --steps 20 --warmup 5 --batch 256 --data-format NCHW > gpurun_out/resnet/nchw.json 2> gpurun_out/resnet/nchw.err
