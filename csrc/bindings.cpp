@@ -43,6 +43,10 @@ int pd_decode_attn(const void*, long, long, const void*, const void*, long, long
 int pd_cache_write(const void*, const void*, long, long, void*, void*, long, long, long, const int*, int, int,
                    const int*, const int*, int, int, int, void*);
 long pd_bn_workspace(int, long, int);
+int pd_wo_splits(int, int, int, int);
+long pd_wo_workspace(int, int, int);
+int pd_wo_gemm(int, const void*, const void*, const float*, const float*, int, const void*, void*, float*, int, int, int,
+               int, void*);
 int pd_bn_fwd_train(int, const void*, const void*, void*, long, int, float*, float*, const float*, const float*, float,
                     float, float*, float*, float*, int, int, void*);
 int pd_bn_apply(int, const void*, const void*, void*, long, int, const float*, const float*, int, void*);
@@ -225,5 +229,13 @@ PYBIND11_MODULE(_C, m) {
                     P<const float*>(invstd), P<const float*>(g), P<void*>(dx), P<void*>(dz), P<float*>(dg),
                     P<float*>(db), M, C, P<float*>(ws), relu, P<void*>(st)),
           "bn_bwd");
+  });
+  m.def("wo_splits", &pd_wo_splits);
+  m.def("wo_workspace", &pd_wo_workspace);
+  m.def("wo_gemm", [](int int4, uintptr_t x, uintptr_t w, uintptr_t cs, uintptr_t gs, int group, uintptr_t bias,
+                      uintptr_t out, uintptr_t ws, int M, int N, int K, int S, uintptr_t st) {
+    check(pd_wo_gemm(int4, P<const void*>(x), P<const void*>(w), P<const float*>(cs), P<const float*>(gs), group,
+                     P<const void*>(bias), P<void*>(out), P<float*>(ws), M, N, K, S, P<void*>(st)),
+          "wo_gemm");
   });
 }

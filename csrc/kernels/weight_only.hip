@@ -1,0 +1,285 @@
+// Weight-only int8 / int4 GEMM for decode-sized token counts on gfx950:  Y[M,N] = X[M,K] . dequant(W)^T
+//
+// Reference behaviour: phi/kernels/fusion/gpu/weight_only_linear_kernel.cu (CUTLASS mixed-input
+// GEMM / weight-only GEMV) and python/paddle/nn/quant/quantized_linear.py:183.  MI355X-first design:
+//  * W is [N, K] int8 (each output channel's K weights contiguous) or [N/2, K] int4 (channel 2p in
+//    the low nibble, 2p+1 in the high nibble); scales per channel [N] or per group [K/G, N];
+//  * the kernel streams W from HBM exactly once: each lane loads 16 contiguous K-bytes of one
+//    channel per 64-wide K step, sign-extends + converts them to bf16 in registers (integers up
+//    to 8 bits are exact in bf16) and feeds v_mfma_f32_16x16x32_bf16 twice — the dot product is
+//    permutation-invariant, so the k order inside the step only has to match X's;
+//  * X[M, Kblk] (M <= 64) is staged once per block in LDS with a padded row pitch (conflict-free
+//    16-byte reads; lanes of rows >= M feed zeros); the dequantized W fragment is reused across
+//    the M tiles, and each wave keeps 2*D*RT 16-byte W loads in flight (double-buffered chunks);
+//  * 4 waves x 16 channels = 64 channels per block, split-K over gridDim.y so decode shapes put
+//    >= 1024 blocks (M <= 16) on the 256 CUs; fp32 partials go to a workspace and a second kernel
+//    sums them, applies the per-channel scale, adds the bias and writes bf16 (deterministic).
+//  * per-group scales are applied in the main loop: each group's MFMA partial is scaled into the
+//    running accumulator at the group boundary.
+#include "common.h"
+
+namespace pd {
+
+typedef __bf16 wo_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float wo_f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWoWaves = 4;
+constexpr int kWoRows = 16 * kWoWaves;  // output channels per block
+constexpr int kWoPad = 8;               // bf16 elements of LDS row padding
+
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+  // exact for small integers: the low 16 bits of the f32 are zero
+  return (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+}
+
+// 16 signed int8 (one uint4) -> two bf16x8 fragments (bytes 0-7, 8-15)
+__device__ __forceinline__ void i8x16_to_bf16(uint4 w, wo_bf16x8& f0, wo_bf16x8& f1) {
+  unsigned d[4] = {w.x, w.y, w.z, w.w};
+  unsigned p[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int v = (int)d[i];
+    const float b0 = (float)((v << 24) >> 24), b1 = (float)((v << 16) >> 24);
+    const float b2 = (float)((v << 8) >> 24), b3 = (float)(v >> 24);
+    p[2 * i] = pack_bf16x2(b0, b1);
+    p[2 * i + 1] = pack_bf16x2(b2, b3);
+  }
+  uint4 a = make_uint4(p[0], p[1], p[2], p[3]), b = make_uint4(p[4], p[5], p[6], p[7]);
+  f0 = __builtin_bit_cast(wo_bf16x8, a);
+  f1 = __builtin_bit_cast(wo_bf16x8, b);
+}
+
+// 16 bytes holding one nibble per byte for this lane's channel -> two bf16x8 fragments
+__device__ __forceinline__ void i4x16_to_bf16(uint4 w, int hi, wo_bf16x8& f0, wo_bf16x8& f1) {
+  unsigned d[4] = {w.x, w.y, w.z, w.w};
+  unsigned p[8];
+  const int sh = hi ? 4 : 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int v = (int)(d[i] >> sh);
+    const float b0 = (float)((v << 28) >> 28), b1 = (float)((v << 20) >> 28);
+    const float b2 = (float)((v << 12) >> 28), b3 = (float)((v << 4) >> 28);
+    p[2 * i] = pack_bf16x2(b0, b1);
+    p[2 * i + 1] = pack_bf16x2(b2, b3);
+  }
+  uint4 a = make_uint4(p[0], p[1], p[2], p[3]), b = make_uint4(p[4], p[5], p[6], p[7]);
+  f0 = __builtin_bit_cast(wo_bf16x8, a);
+  f1 = __builtin_bit_cast(wo_bf16x8, b);
+}
+
+// grid: (N / (64*RT), S). block: 256 = 4 waves; wave w owns RT 16-channel row tiles
+// (channels 64*RT*bx + 16*(w + 4*r) + lane&15) over its block's share of the K units.  RT > 1
+// amortises the per-block X staging (X bytes / W bytes = 2M / (64 RT)) and keeps RT independent
+// 16-byte W loads in flight per lane.
+template <bool INT4, int MT, int RT, int GSTEPS>
+__global__ __launch_bounds__(256) void wo_gemm_kernel(const unsigned short* __restrict__ X, const int8_t* __restrict__ W,
+                                                      const float* __restrict__ gscale, float* __restrict__ ws,
+                                                      int M, int N, int K, int unit, int kmax) {
+  extern __shared__ unsigned short xs[];  // [M][kmax + kWoPad] (rows >= M are never read)
+  const int pitch = kmax + kWoPad;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // uneven split-K in whole units (64 or the scale group): block y owns units [U*y/S, U*(y+1)/S)
+  const int U = K / unit, S = gridDim.y;
+  const int k0 = (int)((long)U * blockIdx.y / S) * unit;
+  const int Kblk = (int)((long)U * (blockIdx.y + 1) / S) * unit - k0;
+  // ---- stage X[:M, k0:k0+Kblk]
+  const int vpr = Kblk / 8;  // 16-byte vectors per row
+  for (int i = tid; i < M * vpr; i += 256) {
+    const int r = i / vpr, c = (i % vpr) * 8;
+    *reinterpret_cast<uint4*>(xs + r * pitch + c) = *reinterpret_cast<const uint4*>(X + (long)r * K + k0 + c);
+  }
+  __syncthreads();
+
+  const int g = lane >> 4;  // k sub-block of the step
+  const int nbase = blockIdx.x * kWoRows * RT + wave * 16;
+  const int8_t* wrow[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    const int n = nbase + r * kWoRows + (lane & 15);  // this lane's channel (A row) in tile r
+    wrow[r] = (INT4 ? W + (long)(n >> 1) * K : W + (long)n * K) + k0 + 16 * g;
+  }
+  const int hi = lane & 1;  // channel parity (row tiles start at multiples of 16)
+  wo_f32x4 acc[RT][MT], part[RT][MT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      acc[r][t] = wo_f32x4{0.f, 0.f, 0.f, 0.f};
+      part[r][t] = acc[r][t];
+    }
+  const int nsteps = Kblk / 64;
+  // W prefetch: chunks of D steps, double-buffered -> 2*D*RT 16-byte loads in flight per lane
+  constexpr int D = RT == 1 ? 4 : 2;
+  uint4 wb[RT][D];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      wb[r][d] = d < nsteps ? *reinterpret_cast<const uint4*>(wrow[r] + d * 64) : make_uint4(0, 0, 0, 0);
+  for (int c = 0; c < nsteps; c += D) {
+    uint4 nb[RT][D];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int d = 0; d < D; ++d)
+        nb[r][d] = c + D + d < nsteps ? *reinterpret_cast<const uint4*>(wrow[r] + (c + D + d) * 64)
+                                      : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int s = c + d;
+      if (s >= nsteps) break;
+      const int kk = s * 64 + 16 * g;
+      wo_bf16x8 b0[MT], b1[MT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int m = t * 16 + (lane & 15);
+        const unsigned short* xr = xs + m * pitch + kk;
+        const wo_bf16x8 z = {};
+        b0[t] = m < M ? *reinterpret_cast<const wo_bf16x8*>(xr) : z;
+        b1[t] = m < M ? *reinterpret_cast<const wo_bf16x8*>(xr + 8) : z;
+      }
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        wo_bf16x8 a0, a1;
+        if constexpr (INT4) i4x16_to_bf16(wb[r][d], hi, a0, a1);
+        else i8x16_to_bf16(wb[r][d], a0, a1);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          wo_f32x4& dst = GSTEPS ? part[r][t] : acc[r][t];
+          dst = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0[t], dst, 0, 0, 0);
+          dst = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[t], dst, 0, 0, 0);
+        }
+      }
+      if constexpr (GSTEPS > 0) {
+        if ((s + 1) % GSTEPS == 0) {
+          // C rows (lane>>4)*4 + i are channels; scale row-wise with this group's scales
+          const int grp = (k0 + s * 64) / (64 * GSTEPS);
+#pragma unroll
+          for (int r = 0; r < RT; ++r) {
+            const int nb2 = nbase + r * kWoRows + (lane >> 4) * 4;
+            const float4 sc = *reinterpret_cast<const float4*>(gscale + (long)grp * N + nb2);
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+              acc[r][t][0] = fmaf(part[r][t][0], sc.x, acc[r][t][0]);
+              acc[r][t][1] = fmaf(part[r][t][1], sc.y, acc[r][t][1]);
+              acc[r][t][2] = fmaf(part[r][t][2], sc.z, acc[r][t][2]);
+              acc[r][t][3] = fmaf(part[r][t][3], sc.w, acc[r][t][3]);
+              part[r][t] = wo_f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int d = 0; d < D; ++d) wb[r][d] = nb[r][d];
+  }
+  // ---- partial tiles -> ws[by][m][n]: lane holds col m = lane&15, rows (lane>>4)*4 + i
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    const int nb = nbase + r * kWoRows + (lane >> 4) * 4;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int m = t * 16 + (lane & 15);
+      if (m < M)
+        *reinterpret_cast<float4*>(ws + ((long)blockIdx.y * M + m) * N + nb) =
+            make_float4(acc[r][t][0], acc[r][t][1], acc[r][t][2], acc[r][t][3]);
+    }
+  }
+}
+
+// out[m, n] = (sum_s ws[s, m, n]) * cscale[n] + bias[n]   (bf16 out / bias)
+__global__ __launch_bounds__(256) void wo_reduce_kernel(const float* __restrict__ ws, int S, int M, int N,
+                                                        const float* __restrict__ cscale,
+                                                        const unsigned short* __restrict__ bias,
+                                                        unsigned short* __restrict__ out) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= (long)M * N) return;
+  float4 a = *reinterpret_cast<const float4*>(ws + i);
+  for (int s = 1; s < S; ++s) {
+    const float4 b = *reinterpret_cast<const float4*>(ws + (long)s * M * N + i);
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  const int n = (int)(i % N);
+  float v[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (cscale) v[j] *= cscale[n + j];
+    if (bias) v[j] += bf2f(bias[n + j]);
+    out[i + j] = f2bf(v[j]);
+  }
+}
+
+}  // namespace pd
+
+using namespace pd;
+
+// Split-K factor for a shape: enough blocks to fill the chip, X tile within the LDS budget.
+static inline int wo_unit(int group) { return group > 64 ? group : 64; }
+static inline int wo_kcap(int M) {
+  // X tile [M][Kblk] bf16 <= ~32 KB of LDS so several blocks fit per CU
+  int cap = 2048;
+  while (cap > 512 && (long)M * cap * 2 > 64 * 1024) cap >>= 1;
+  return cap;
+}
+
+static inline int wo_mt(int M) {
+  const int mt = (M + 15) / 16;
+  return mt <= 1 ? 1 : (mt <= 2 ? 2 : 4);
+}
+static inline int wo_rt(int M, int N) {
+  int rt = wo_mt(M);
+  while (rt > 1 && N % (kWoRows * rt)) rt >>= 1;
+  return rt;
+}
+
+extern "C" int pd_wo_splits(int M, int N, int K, int group) {
+  const int unit = wo_unit(group), U = K / unit;
+  const int nblk = N / (kWoRows * wo_rt(M, N));
+  int S = (K + wo_kcap(M) - 1) / wo_kcap(M);
+  const int target = M <= 16 ? 1024 : 384;
+  const int fill = (target + nblk - 1) / nblk;
+  if (S < fill) S = fill;
+  if (S > U) S = U;
+  return S < 1 ? 1 : S;
+}
+
+// ws: S*M*N floats of split-K partials.  (fp32 atomics into one [M, N] buffer were tried: the
+// device-scope fences a last-block epilogue needs write back the per-XCD L2s and cost ~10x.)
+extern "C" long pd_wo_workspace(int M, int N, int S) { return (long)S * M * N; }
+
+extern "C" int pd_wo_gemm(int int4, const void* X, const void* W, const float* cscale, const float* gscale, int group,
+                          const void* bias, void* out, float* ws, int M, int N, int K, int S, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int unit = wo_unit(group);
+  if (M < 1 || M > 64 || N % kWoRows || K % unit || S < 1 || S > K / unit) return -1;
+  if (group > 0 && group != 64 && group != 128) return -2;
+  const int kmax = ((K / unit + S - 1) / S) * unit;  // largest block K range
+  const int MT = wo_mt(M), RT = wo_rt(M, N);
+  const size_t lds = (size_t)M * (kmax + kWoPad) * 2;
+  if (lds > 160 * 1024) return -3;
+  dim3 grid(N / (kWoRows * RT), S);
+  const int gsteps = group > 0 ? group / 64 : 0;
+  auto launch = [&](auto kern) {
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    kern<<<grid, 256, lds, st>>>((const unsigned short*)X, (const int8_t*)W, gscale, ws, M, N, K, unit, kmax);
+  };
+#define PD_WO_G(I4, MT_, RT_)                                                  \
+  if (gsteps == 0) launch(wo_gemm_kernel<I4, MT_, RT_, 0>);                    \
+  else if (gsteps == 1) launch(wo_gemm_kernel<I4, MT_, RT_, 1>);               \
+  else launch(wo_gemm_kernel<I4, MT_, RT_, 2>);
+#define PD_WO_R(I4, MT_)                                                       \
+  if (RT == 1) { PD_WO_G(I4, MT_, 1) } else if (RT == 2) { PD_WO_G(I4, MT_, 2) } else { PD_WO_G(I4, MT_, 4) }
+  if (int4) {
+    if (MT == 1) { PD_WO_R(true, 1) } else if (MT == 2) { PD_WO_R(true, 2) } else { PD_WO_R(true, 4) }
+  } else {
+    if (MT == 1) { PD_WO_R(false, 1) } else if (MT == 2) { PD_WO_R(false, 2) } else { PD_WO_R(false, 4) }
+  }
+#undef PD_WO_R
+#undef PD_WO_G
+  const long total = (long)M * N;
+  wo_reduce_kernel<<<(int)((total / 4 + 255) / 256), 256, 0, st>>>(ws, S, M, N, group > 0 ? nullptr : cscale,
+                                                                 (const unsigned short*)bias, (unsigned short*)out);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,60 @@
+"""Weight-only int8/int4 matmul dispatch (kernel: csrc/kernels/weight_only.hip).
+
+``weight_only_matmul(x [M, K], w [N, K] int8 | [N/2, K] int4, scale [N] | [K/G, N])`` -> [M, N].
+On the MI355X with bf16 activations and M <= 64 it runs the fused dequant + MFMA kernel (weights
+read from HBM once, in their 1- or 0.5-byte form); larger M (prefill) dequantizes to bf16 once and
+uses the hipBLASLt GEMM.  On CPU it is the fp32 reference.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as N
+
+
+def dequantize(w, scale, weight_dtype="int8", group_size=-1, dtype=torch.float32):
+    q = w
+    if weight_dtype == "int4":
+        u = w.view(torch.uint8).to(torch.int16)
+        lo, hi = u & 0xF, (u >> 4) & 0xF
+        lo = torch.where(lo > 7, lo - 16, lo)
+        hi = torch.where(hi > 7, hi - 16, hi)
+        q = torch.stack([lo, hi], 1).reshape(-1, w.shape[1])
+    q = q.float()
+    s = scale.float()
+    if group_size in (-1, None) or s.dim() == 1:
+        out = q * s[:, None]
+    else:
+        out = q * s.t().repeat_interleave(group_size, 1)[:, : q.shape[1]]
+    return out.to(dtype)  # [N, K]
+
+
+def _native_ok(x, w, weight_dtype, group_size):
+    M, K = x.shape
+    Nn = w.shape[0] * (2 if weight_dtype == "int4" else 1)
+    return (x.device.type == "cuda" and x.dtype == torch.bfloat16 and M <= 64 and K % 64 == 0 and Nn % 64 == 0
+            and group_size in (-1, 64, 128) and w.is_contiguous())
+
+
+def weight_only_matmul(x, w, scale, weight_dtype="int8", group_size=-1, bias=None):
+    x = x.contiguous()
+    M, K = x.shape
+    if _native_ok(x, w, weight_dtype, group_size) and N.use_native(x):
+        C = N.native()
+        Nn = w.shape[0] * (2 if weight_dtype == "int4" else 1)
+        g = -1 if group_size in (-1, None) else int(group_size)
+        S = C.wo_splits(M, Nn, K, g)
+        ws = torch.empty(C.wo_workspace(M, Nn, S), dtype=torch.float32, device=x.device)
+        out = torch.empty(M, Nn, dtype=x.dtype, device=x.device)
+        sc = scale.float().contiguous()
+        if bias is not None:
+            bias = bias.to(torch.bfloat16).contiguous()
+        C.wo_gemm(int(weight_dtype == "int4"), x.data_ptr(), w.data_ptr(), sc.data_ptr() if g < 0 else 0,
+                  sc.data_ptr() if g > 0 else 0, max(g, 0), N.ptr(bias), out.data_ptr(), ws.data_ptr(), M, Nn, K,
+                  S, N.stream())
+        return out
+    wd = dequantize(w, scale, weight_dtype, group_size, x.dtype if x.device.type == "cuda" else torch.float32)
+    y = x.to(wd.dtype) @ wd.t()
+    if bias is not None:
+        y = y + bias.to(y.dtype)
+    return y.to(x.dtype)
