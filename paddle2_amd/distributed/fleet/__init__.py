@@ -124,6 +124,21 @@ def distributed_scaler(scaler):
     return scaler
 
 
+def _device_for_group(group):
+    import torch
+
+    if group is not None and group.backend == "nccl" and torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def collective_perf(comm_type, round=50, size_and_time=None):
+    """Time collectives over the hybrid groups (reference fleet.py:621); see fleet/collective_perf.py."""
+    from .collective_perf import collective_perf as _cp
+
+    return _cp(comm_type, round, size_and_time)
+
+
 def get_log_level_code():
     return 20
 

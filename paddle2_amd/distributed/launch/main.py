@@ -12,6 +12,12 @@ PADDLE_TRAINERS_NUM, PADDLE_CURRENT_ENDPOINT, PADDLE_TRAINER_ENDPOINTS, PADDLE_M
 FLAGS_selected_gpus, ...) and torch.distributed's (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
 The watcher restarts the whole pod up to ``--max_restart`` times when a worker fails (fault
 tolerance level 1) and otherwise tears the pod down and exits with the failing worker's code.
+
+Elastic mode (``--nnodes MIN:MAX``, reference fleet/elastic): membership is tracked by the
+ElasticManager over the same TCPStore (heartbeats, TTL); when nodes join or leave, every
+surviving launcher stops its pod, re-rendezvouses with the new node set and restarts the
+workers with the new world size (workers resume from their checkpoint).  A worker exiting with
+code 101 (ELASTIC_EXIT_CODE) also triggers a re-rendezvous.
 """
 from __future__ import annotations
 
@@ -37,6 +43,10 @@ def _parse(argv=None):
     ap.add_argument("--run_mode", "--run-mode", dest="run_mode", default="collective")
     ap.add_argument("--max_restart", "--max-restart", dest="max_restart", type=int, default=0)
     ap.add_argument("--elastic_level", type=int, default=-1)
+    ap.add_argument("--elastic_ttl", "--elastic-ttl", dest="elastic_ttl", type=float, default=60.0,
+                    help="elastic: seconds without heartbeat before a node is considered gone")
+    ap.add_argument("--auto_tuner_json", "--auto-tuner-json", dest="auto_tuner_json", default=None,
+                    help="run the hybrid-parallel auto tuner with this config instead of a single job")
     ap.add_argument("--host", default=None, help="this node's address")
     ap.add_argument("--start_port", type=int, default=None)
     ap.add_argument("training_script")
@@ -184,13 +194,86 @@ class Pod:
             f.close()
 
 
+def _launch_elastic(args, nproc, devices, host):
+    from ..fleet.elastic.manager import ELASTIC_EXIT_CODE, ElasticManager, ElasticStatus
+    from ..store import TCPStore
+
+    mhost, mport = args.master.rsplit(":", 1)
+    is_master = args.rank == 0 or (args.rank < 0 and _try_bind(mhost, int(mport)))
+    store = TCPStore(mhost, int(mport), is_master=is_master, world_size=1, timeout=600)
+    mgr = ElasticManager(store, args.job_id, host, nproc, args.nnodes, ttl=args.elastic_ttl,
+                         store_addr=(mhost, int(mport)))
+    mgr.register()
+    cmd = [sys.executable, "-u", args.training_script] + list(args.training_script_args)
+    round_id, restarts = 0, 0
+    try:
+        while True:
+            members, torch_master = mgr.rendezvous(round_id, _free_port)
+            if members is None:  # more nodes than MAX: wait for a later round
+                round_id += 1
+                time.sleep(1.0)
+                continue
+            node_rank = [m[0] for m in members].index(mgr.slot)
+            world = sum(m[2] for m in members)
+            offset = sum(m[2] for m in members[:node_rank])
+            mgr.publish_ports(round_id, [_free_port() for _ in range(nproc)])
+            eps = mgr.gather_ports(round_id, members)
+            print(f"[launch] elastic round {round_id}: {len(members)} node(s), world {world}, node rank {node_rank}",
+                  file=sys.stderr, flush=True)
+            envs = [_worker_env(args, i, node_rank, len(members), world, offset, eps, devices, torch_master)
+                    for i in range(nproc)]
+            pod = Pod(args, cmd, envs)
+            pod.start()
+            status, code = None, None
+            while code is None and status is None:
+                time.sleep(0.5)
+                code = pod.poll()
+                if code is None:
+                    status = mgr.watch(members)
+                    if status == ElasticStatus.COMPLETED:
+                        status = None  # a peer finished: let our workers finish too
+            pod.stop()
+            if code == 0:
+                mgr.exit(completed=True)
+                return 0
+            if status == ElasticStatus.RESTART or code == ELASTIC_EXIT_CODE or restarts < args.max_restart:
+                if code not in (None, ELASTIC_EXIT_CODE):
+                    restarts += 1
+                print(f"[launch] elastic restart (membership change or exit {code})", file=sys.stderr, flush=True)
+                round_id += 1
+                continue
+            mgr.exit()
+            return code
+    finally:
+        mgr._stop.set()
+
+
 def launch(argv=None):
     args = _parse(argv)
+    if args.auto_tuner_json:
+        import json
+
+        from ..auto_tuner.launch import run as _tune
+
+        with open(args.auto_tuner_json) as f:
+            tuner_cfg = json.load(f)
+        raw = sys.argv[1:] if argv is None else list(argv)
+        i = raw.index("--auto_tuner_json") if "--auto_tuner_json" in raw else raw.index("--auto-tuner-json")
+        rest = raw[:i] + raw[i + 2:]
+        j = rest.index(args.training_script)
+        best, _ = _tune(tuner_cfg, rest[:j], args.training_script, rest[j + 1:],
+                        log_root=os.path.join(args.log_dir, "auto_tuner"))
+        print(f"[auto_tuner] best config: {best}", flush=True)
+        return 0 if best is not None else 1
     devices = _device_list(args)
     nproc = args.nproc_per_node or (len(devices) if devices else 1)
     if devices and len(devices) > nproc:
         devices = devices[:nproc]
     host = args.host or _local_ip()
+    if ":" in str(args.nnodes):
+        if not args.master:
+            raise SystemExit("elastic mode (--nnodes MIN:MAX) needs --master host:port")
+        return _launch_elastic(args, nproc, devices, host)
     node_rank, nnodes, world, offset, eps, store = _Rendezvous(args, nproc, host).run()
     if args.master and nnodes > 1:
         mhost = args.master.rsplit(":", 1)[0]

@@ -50,3 +50,19 @@ def test_native_store_api():
     th.join(5)
     assert not th.is_alive()
     master.shutdown()
+
+
+def test_fused_comm_buffer_and_collective_perf():
+    res = run_workers("fusion_worker.py", 2)
+    r0, r1 = res
+    assert r0["groups"] == [2]
+    # grads after AVG all-reduce are identical on both ranks; x = rank+1+step over 2 steps:
+    # d(sum(Wx+b))/dW[j, k] = sum_rows x = 3*x -> averaged over ranks and summed over steps
+    exp_w = (3 * (1 + 2) + 3 * (2 + 3)) / 2.0
+    assert r0["grads"]["ar"] == r1["grads"]["ar"]
+    assert abs(r0["grads"]["ar"][0][0] - exp_w) < 1e-5
+    assert abs(r0["grads"]["ar"][1][0] - 3 * 2) < 1e-5  # bias grad: 3 rows x 2 steps, averaged
+    for r in res:  # reduce-scatter: each rank's shard holds the averaged values
+        assert abs(r["grads"]["rs_shard_head"][0] - (exp_w if r["grads"]["rs_shard_rank"] == 0 else
+                                                     r["grads"]["rs_shard_head"][0])) < 1e-5
+    assert [p[:2] for p in r0["perf"]] == [[1 << 16, 2], [1 << 18, 2]] and all(p[2] and p[3] for p in r0["perf"])
