@@ -92,6 +92,32 @@ __device__ __forceinline__ int xcd_remap(int bid, int n) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// Sequence-layout / mask extensions (template MODE):
+//   kDense   - q/k/v [B, S, H, D], lse [B, H, Sq]
+//   kVarlen  - packed q/k/v [total, H, D] with cumulative offsets cu_q/cu_k [B+1] (flash_attn_unpadded,
+//              reference flash_attn_kernel.cu FlashAttnUnpaddedKernel); lse [H, total_q]; bottom-right causal
+//              alignment per sequence
+//   kMask    - FlashMask (reference flash_attn_kernel.cu:445-494 startend_row_indices): per key column two row
+//              intervals [a1, b1) U [a2, b2) are masked (host normalises LTS/LTE/UTS/UTE to this form).  A host
+//              plan classifies every (query block x key tile) product as unmasked / partial / fully masked from
+//              per-tile min/max summaries, so fully masked products are never visited (not even scanned), and
+//              element masks run only on partial ones
+enum Mode : int { kDense = 0, kVarlen = 1, kMask = 2 };
+struct Ext {
+  const int* cu_q;      // kVarlen
+  const int* cu_k;
+  int total_q;
+  const int4* fm;       // kMask: [B, Hm, Sk] (a1, b1, a2, b2)
+  const int* fm_t64;    // kMask fwd plan: [B*Hm, ceil(Sq/128), 2 + ceil(Sk/64)] = first tile, end tile, class/tile
+  const int* fm_t256;   // kMask bwd plan: [B*Hm, ceil(Sq/32), ceil(Sk/256)] class per (32-row q tile, key block)
+  int fm_hm;            // mask heads: 1 or Hq
+};
+
+// plan classes: 0 = unmasked, 1 = partial, 2 = fully masked
+__device__ __forceinline__ bool fm_masked(int4 m, int row) {
+  return (row >= m.x && row < m.y) || (row >= m.z && row < m.w);
+}
+
 // Transposed-read address for the A operand V^T / dO^T / Q^T / K^T-column fragments:
 // 32x16 operand whose row = column `c0 + (lane&31)` of a row-major tile, k rows = `r0 + k`.
 // PERM selects the permuted k order required when the B operand is an accumulator tile.
@@ -109,17 +135,18 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int r0, int c0, int 
 // =====================================================================================
 //                                       FORWARD
 // =====================================================================================
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int MODE>
 __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ Vv, bf16* __restrict__ O,
-                                                     float* __restrict__ LSE, int B, int Sq, int Sk, int Hq, int Hk,
-                                                     long sq, long sk, long sv, long so, float scale) {
+                                                     float* __restrict__ LSE, int B, int SqMax, int SkMax, int Hq,
+                                                     int Hk, long sq, long sk, long sv, long so, float scale, Ext ex) {
   constexpr int BM = 128, BN = 64, NCH = D / 8, KS = D / 16, DT = D / 32;
   constexpr int TILE = BN * D * 2;
   constexpr int NLOAD = BN * NCH / 256;
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][K|V]
+  __shared__ int4 fm_s[MODE == kMask ? 2 * BN : 1];              // [buf][key] FlashMask intervals
 
-  const int nmb = (Sq + BM - 1) / BM;
+  const int nmb = (SqMax + BM - 1) / BM;
   const int total = nmb * Hq * B;
   const int w_id = xcd_remap(blockIdx.x, total);
   int mb = w_id % nmb;
@@ -130,11 +157,33 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int m0 = mb * BM;
+
+  // per-sequence extents: token offsets of this sequence's first q / k row and its LSE row base
+  int Sq = SqMax, Sk = SkMax;
+  long qt0 = (long)b * SqMax, kt0 = (long)b * SkMax;
+  long lse0 = ((long)b * Hq + hq) * SqMax;
+  if constexpr (MODE == kVarlen) {
+    qt0 = ex.cu_q[b];
+    kt0 = ex.cu_k[b];
+    Sq = ex.cu_q[b + 1] - (int)qt0;
+    Sk = ex.cu_k[b + 1] - (int)kt0;
+    lse0 = (long)hq * ex.total_q + qt0;
+    if (m0 >= Sq) return;  // whole workgroup: this sequence is shorter than max_seqlen
+  }
   const int off = Sk - Sq;  // bottom-right causal alignment
 
-  const bf16* Qb = Q + (long)b * Sq * sq + hq * D;
-  const bf16* Kb = K + (long)b * Sk * sk + hk * D;
-  const bf16* Vb = Vv + (long)b * Sk * sv + hk * D;
+  const bf16* Qb = Q + qt0 * sq + hq * D;
+  const bf16* Kb = K + kt0 * sk + hk * D;
+  const bf16* Vb = Vv + kt0 * sv + hk * D;
+  // FlashMask: this head's per-key intervals and 64-key tile summaries
+  const int4* fmk = nullptr;
+  const int* plan = nullptr;
+  if constexpr (MODE == kMask) {
+    const long mh = (long)b * ex.fm_hm + (ex.fm_hm == 1 ? 0 : hq);
+    const int nt_all = (Sk + BN - 1) / BN;
+    fmk = ex.fm + mh * Sk;
+    plan = ex.fm_t64 + (mh * nmb + mb) * (nt_all + 2);
+  }
 
   // Q fragments (B operand of S^T = K.Q^T): lane holds Q[q][16ks + 8h .. +8]
   const int qrow = m0 + wv * 32 + r;
@@ -147,10 +196,20 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
 
   int n_end = Sk;
   if (CAUSAL) n_end = min(Sk, m0 + BM + off);
-  const int ntiles = n_end > 0 ? (n_end + BN - 1) / BN : 0;
+  int ntiles = n_end > 0 ? (n_end + BN - 1) / BN : 0;
+  int t = 0;
+  if constexpr (MODE == kMask) {
+    t = plan[0];                    // first / end key tile that is not fully masked
+    ntiles = min(ntiles, plan[1]);
+  }
 
   u16x8 stk[NLOAD], stv[NLOAD];
+  int stm = 0;  // kMask: one int of the tile's [64 keys][4] interval image per thread
   auto gload = [&](int n0) {
+    if constexpr (MODE == kMask) {
+      const int key = n0 + (tid >> 2);
+      stm = key < Sk ? reinterpret_cast<const int*>(fmk + key)[tid & 3] : 0;
+    }
 #pragma unroll
     for (int i = 0; i < NLOAD; ++i) {
       const int c = tid + 256 * i, row = c / NCH, ch = c % NCH, key = n0 + row;
@@ -166,6 +225,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
   auto lstore = [&](int buf) {
     char* kt = smem + buf * 2 * TILE;
     char* vt = kt + TILE;
+    if constexpr (MODE == kMask) reinterpret_cast<int*>(fm_s + buf * BN)[tid] = stm;
 #pragma unroll
     for (int i = 0; i < NLOAD; ++i) {
       const int c = tid + 256 * i, row = c / NCH, ch = c % NCH;
@@ -181,17 +241,25 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
   float m_i = -INFINITY, l_i = 0.f;
   const float sl2 = scale * kLog2e;
 
-  if (ntiles > 0) {
-    gload(0);
+  // next key tile >= t that is not fully masked (FlashMask); identity otherwise
+  auto next_tile = [&](int t) {
+    if constexpr (MODE == kMask) {
+      while (t < ntiles && plan[2 + t] == 2) ++t;
+    }
+    return t;
+  };
+  if (t < ntiles) {
+    gload(t * BN);
     lstore(0);
   }
   __syncthreads();
 
-  for (int t = 0; t < ntiles; ++t) {
+  for (int buf = 0; t < ntiles; buf ^= 1) {
     const int n0 = t * BN;
-    const bool has_next = t + 1 < ntiles;
-    if (has_next) gload(n0 + BN);  // issue early; lands while we compute (T14)
-    const char* kt = smem + (t & 1) * 2 * TILE;
+    const int tn = next_tile(t + 1);
+    const bool has_next = tn < ntiles;
+    if (has_next) gload(tn * BN);  // issue early; lands while we compute (T14)
+    const char* kt = smem + buf * 2 * TILE;
     const char* vt = kt + TILE;
 
     // ---- S^T = K . Q^T for two 32-key sub-blocks
@@ -217,6 +285,25 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
         for (int i = 0; i < 16; ++i) {
           const int key = n0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
           s[kb][i] = (key >= Sk || (CAUSAL && key > qrow + off)) ? -INFINITY : s[kb][i];
+        }
+      }
+    }
+    if constexpr (MODE == kMask) {
+      if (plan[2 + t] == 1) {
+        // 4 consecutive keys per group from the LDS image; the sched barrier keeps only one group's
+        // intervals live (the D=128 accumulators leave no room for all 32)
+        const int4* fmt_s = fm_s + buf * BN;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int4 m = fmt_s[kb * 32 + 8 * g + 4 * h + j];
+              s[kb][4 * g + j] = fm_masked(m, qrow) ? -INFINITY : s[kb][4 * g + j];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
       }
     }
@@ -258,15 +345,16 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
         }
       }
     }
-    if (has_next) lstore((t + 1) & 1);  // write late (T14)
+    if (has_next) lstore(buf ^ 1);  // write late (T14)
     __syncthreads();
+    t = tn;
   }
 
   // ---- epilogue: normalise, store O (row = query, 4 consecutive d per store) and LSE
   const float l_tot = l_i + __shfl_xor(l_i, 32, 64);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   if (qrow < Sq) {
-    bf16* orow = O + (long)b * Sq * so + (long)qrow * so + hq * D;
+    bf16* orow = O + (qt0 + qrow) * so + hq * D;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
 #pragma unroll
@@ -281,7 +369,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
       }
     }
     if (h == 0) {
-      LSE[((long)b * Hq + hq) * Sq + qrow] = l_tot > 0.f ? (m_i + log2f(l_tot)) * kLn2 : INFINITY;
+      LSE[lse0 + qrow] = l_tot > 0.f ? (m_i + log2f(l_tot)) * kLn2 : INFINITY;
     }
   }
 }
@@ -313,14 +401,14 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const bf16* __restrict__
   if (lane == 0) delta[rowid] = acc;
 }
 
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int MODE>
 __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ Vv, const bf16* __restrict__ dO,
                                                      const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                      float* __restrict__ dQP, bf16* __restrict__ dK,
-                                                     bf16* __restrict__ dV, int B, int Sq, int Sk, int Hq, int Hk,
-                                                     long sq, long sk, long sv, long so, long sdk, long sdv,
-                                                     long pslab, float scale) {
+                                                     bf16* __restrict__ dV, int B, int SqMax, int SkMax, int Hq,
+                                                     int Hk, long sq, long sk, long sv, long so, long sdk, long sdv,
+                                                     long pslab, float scale, Ext ex) {
   constexpr int NW = 8, BNK = NW * 32, BMQ = 32, NCH = D / 8, KS = D / 16, DT = D / 32;
   constexpr int KTILE = BNK * D * 2;     // K block image: B operand of S (row reads) and of dQ (tr reads)
   constexpr int QTILE = BMQ * D * 2;     // Q / dO tile image
@@ -334,7 +422,6 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
   float* del_s = lse_s + BMQ;
 
   // heaviest (lowest, under the causal mask) key blocks first, round-robin over the XCDs
-  const int nkb = (Sk + BNK - 1) / BNK;
   const int kblk = blockIdx.x / (Hk * B);
   const int rest = blockIdx.x % (Hk * B);
   const int hk = rest % Hk;
@@ -343,12 +430,24 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int k0 = kblk * BNK;
+  int Sq = SqMax, Sk = SkMax;
+  long qt0 = (long)b * SqMax, kt0 = (long)b * SkMax;
+  long lse_b = (long)b * Hq * SqMax, lse_hs = SqMax;  // LSE/delta index = lse_b + hq * lse_hs + q
+  if constexpr (MODE == kVarlen) {
+    qt0 = ex.cu_q[b];
+    kt0 = ex.cu_k[b];
+    Sq = ex.cu_q[b + 1] - (int)qt0;
+    Sk = ex.cu_k[b + 1] - (int)kt0;
+    lse_b = qt0;
+    lse_hs = ex.total_q;
+    if (k0 >= Sk) return;  // whole workgroup: key block past this sequence's end
+  }
   const int off = Sk - Sq;
   const int lkey = wv * 32 + r;          // key (within the block) owned by this lane's accumulator column
   const int mykey = k0 + lkey;
 
-  const bf16* Kb = K + (long)b * Sk * sk + hk * D;
-  const bf16* Vb = Vv + (long)b * Sk * sv + hk * D;
+  const bf16* Kb = K + kt0 * sk + hk * D;
+  const bf16* Vb = Vv + kt0 * sv + hk * D;
 
   for (int c = tid; c < BNK * NCH; c += NW * 64) {
     const int row = c / NCH, ch = c % NCH, key = k0 + row;
@@ -373,7 +472,25 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
   constexpr int NL = (BMQ * NCH + NW * 64 - 1) / (NW * 64);  // 16-B chunks per thread per tile
   const int ntot = nqt * group;        // (head, q-tile) steps, head-major
   // this workgroup's dQ partial slab: plain stores, summed by dq_reduce_kernel (no atomics)
-  float* dQs = dQP + (long)kblk * pslab + (long)b * Sq * Hq * D;
+  float* dQs = dQP + (long)kblk * pslab + qt0 * Hq * D;
+
+  // FlashMask: this lane's key intervals; 256-key block summaries per mask head
+  int4 mym = int4{0, 0, 0, 0};
+  const int nkb = (Sk + BNK - 1) / BNK;
+  auto fm_head = [&](int hq) -> long { return (long)b * ex.fm_hm + (ex.fm_hm == 1 ? 0 : hq); };
+  auto step_cls = [&](int st) -> int {  // 0 unmasked, 1 partial, 2 fully masked
+    if constexpr (MODE != kMask) return 0;
+    const int hq = hk * group + st / nqt;
+    const int q0 = q_begin + (st % nqt) * BMQ;
+    return ex.fm_t256[(fm_head(hq) * ((Sq + BMQ - 1) / BMQ) + q0 / BMQ) * nkb + kblk];
+  };
+  // fully masked steps are skipped; dq_reduce skips the same (q tile, key block) slabs from the plan
+  auto next_step = [&](int st) {
+    if constexpr (MODE == kMask) {
+      while (st < ntot && step_cls(st) == 2) ++st;
+    }
+    return st;
+  };
 
   // register-staged prefetch of the next (head, q-tile) step (issue early / write late, T14)
   u16x8 pq[NL], pd[NL];
@@ -381,8 +498,8 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
   auto gload = [&](int step) {
     const int hq = hk * group + step / nqt;
     const int q0 = q_begin + (step % nqt) * BMQ;
-    const bf16* Qb = Q + (long)b * Sq * sq + hq * D;
-    const bf16* dOb = dO + (long)b * Sq * so + hq * D;
+    const bf16* Qb = Q + qt0 * sq + hq * D;
+    const bf16* dOb = dO + qt0 * so + hq * D;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int c = tid + NW * 64 * i, row = c / NCH, ch = c % NCH, q = q0 + row;
@@ -396,11 +513,12 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
     }
     if (tid < BMQ) {
       const int q = q0 + tid;
-      plse = q < Sq ? -LSE[((long)b * Hq + hq) * Sq + q] / scale : -INFINITY;
-      pdel = q < Sq ? -DELTA[((long)b * Hq + hq) * Sq + q] : 0.f;
+      plse = q < Sq ? -LSE[lse_b + hq * lse_hs + q] / scale : -INFINITY;
+      pdel = q < Sq ? -DELTA[lse_b + hq * lse_hs + q] : 0.f;
     }
   };
-  if (ntot > 0) gload(0);
+  int step = next_step(0);
+  if (step < ntot) gload(step);
 
   // ---- per-lane LDS byte offsets.  Every operand address below is one of these bases XOR/plus a
   // compile-time constant (folded into the ds_* immediate offset where it is an add), so the loop
@@ -424,7 +542,7 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
   int o_srow = r * (BNK * 2) + (((h ^ msk(r)) & (SNCH - 1)) << 4);
   int o_scol = 4 * h * (BNK * 2) + ((((lkey >> 3) ^ h) & (SNCH - 1)) << 4) + ((lkey & 7) << 1);
 
-  for (int step = 0; step < ntot; ++step) {
+  while (step < ntot) {
     const int hq = hk * group + step / nqt;
     const int q0 = q_begin + (step % nqt) * BMQ;
     // keep the bases opaque per step so derived offsets are recomputed (1 VALU each), not hoisted
@@ -444,8 +562,22 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
       lse_s[tid] = plse;
       del_s[tid] = pdel;
     }
+    const int fm_cls = step_cls(step);
+    if constexpr (MODE == kMask) {
+      // consumed only after the S / dP MFMA chain, which hides the load
+      // causal masks carry only [a1, b1) (host normalisation leaves interval 2 empty)
+      if (fm_cls == 1 && mykey < Sk) {
+        if (CAUSAL) {
+          const int2 m2 = reinterpret_cast<const int2*>(ex.fm + fm_head(hq) * Sk + mykey)[0];
+          mym = int4{m2.x, m2.y, 0, 0};
+        } else {
+          mym = ex.fm[fm_head(hq) * Sk + mykey];
+        }
+      }
+    }
     __syncthreads();
-    if (step + 1 < ntot) gload(step + 1);  // lands while this step computes
+    const int step_next = next_step(step + 1);
+    if (step_next < ntot) gload(step_next);  // lands while this step computes
 
     // S' = Q.K^T - lse/scale and dP' = dO.V^T - delta: the row constants are the accumulators'
     // initial values (loaded straight from LDS into the accumulator registers), so P = exp2(S' *
@@ -474,6 +606,9 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
       const int qi = (i & 3) + 8 * (i >> 2) + 4 * h;
       const float p = __builtin_amdgcn_exp2f(sacc[i] * sl2);
       sacc[i] = (dlim + qi < 0) ? 0.f : p;
+      if constexpr (MODE == kMask) {
+        if (fm_cls == 1 && fm_masked(mym, q0 + qi)) sacc[i] = 0.f;
+      }
       dpacc[i] = sacc[i] * dpacc[i];
     }
     // dV^T += dO^T . P ; dK^T += Q^T . dS   (A operands by transposed reads, permuted k)
@@ -516,11 +651,12 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
         if (q < Sq) __builtin_nontemporal_store(dq[i] * scale, dqh + (long)q * Hq * D);
       }
     }
+    step = step_next;
   }
   // write dK (scaled) and dV for this lane's key: accumulator row = d, column = key
   if (mykey < Sk) {
-    bf16* dkr = dK + ((long)b * Sk + mykey) * sdk + hk * D;
-    bf16* dvr = dV + ((long)b * Sk + mykey) * sdv + hk * D;
+    bf16* dkr = dK + (kt0 + mykey) * sdk + hk * D;
+    bf16* dvr = dV + (kt0 + mykey) * sdv + hk * D;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
 #pragma unroll
@@ -540,15 +676,29 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
 
 // dQ[b, q, h, :] = sum over the key blocks that wrote row q of their partial slabs; bf16 out with row
 // stride sdq.  Causal: key block kb wrote rows q >= qbegin(kb) = floor(max(0, kb*BNK - off) / BMQ) * BMQ.
+template <int MODE>
 __global__ __launch_bounds__(256) void dq_reduce_kernel(const float* __restrict__ P, bf16* __restrict__ dq, int B,
                                                         int Sq, int Hq, int D, int nkb, long pslab, long sdq,
-                                                        int causal, int off, int bnk) {
+                                                        int causal, int off, int bnk, Ext ex) {
   const long per_row = (long)Hq * D / 8;  // 8 floats per thread
-  const long total = (long)B * Sq * per_row;
+  const long total = (MODE == kVarlen ? (long)ex.total_q : (long)B * Sq) * per_row;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long row = i / per_row;              // b*Sq + q
+    const long row = i / per_row;              // token index (b*Sq + q when dense)
     const long e = (i - row * per_row) * 8;    // offset inside the [Hq*D] row
-    const int q = (int)(row % Sq);
+    int q;
+    if constexpr (MODE == kVarlen) {
+      int lo = 0, hi = B;                      // largest b with cu_q[b] <= row
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (ex.cu_q[mid] <= row) lo = mid; else hi = mid;
+      }
+      q = (int)(row - ex.cu_q[lo]);
+      const int sk_b = ex.cu_k[lo + 1] - ex.cu_k[lo];
+      off = sk_b - (ex.cu_q[lo + 1] - ex.cu_q[lo]);
+      nkb = (sk_b + bnk - 1) / bnk;
+    } else {
+      q = (int)(row % Sq);
+    }
     int kb_end = nkb;
     if (causal) {
       // last key block whose q_begin <= q
@@ -559,15 +709,22 @@ __global__ __launch_bounds__(256) void dq_reduce_kernel(const float* __restrict_
     }
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const float* src = P + row * (long)Hq * D + e;
+    const int* cls = nullptr;
+    if constexpr (MODE == kMask) {
+      const long mh = (row / Sq) * ex.fm_hm + (ex.fm_hm == 1 ? 0 : (int)(e / D));
+      cls = ex.fm_t256 + (mh * ((Sq + 31) / 32) + q / 32) * nkb;
+    }
     for (int kb = 0; kb < kb_end; ++kb) {
+      if constexpr (MODE == kMask) {
+        if (cls[kb] == 2) continue;  // the bwd kernel skipped (never wrote) this slab row
+      }
       typedef float f32x4 __attribute__((ext_vector_type(4)));
       const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + kb * pslab));
       const f32x4 c = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + kb * pslab + 4));
 #pragma unroll
       for (int j = 0; j < 4; ++j) { acc[j] += a[j]; acc[4 + j] += c[j]; }
     }
-    const long b = row / Sq;
-    store_vec<bf16, 8>(dq + (b * Sq + q) * sdq + e, acc);
+    store_vec<bf16, 8>(dq + row * sdq + e, acc);
   }
 }
 
@@ -576,48 +733,96 @@ __global__ __launch_bounds__(256) void dq_reduce_kernel(const float* __restrict_
 
 using namespace pd;
 
-extern "C" int pd_flash_fwd(int dt, const void* q, const void* k, const void* v, void* o, float* lse, int B, int Sq,
-                            int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, float scale, int causal,
-                            void* stream) {
-  if (dt != kBF16 || (D != 64 && D != 128) || Hq % Hk) return -1;
+// mode: 0 dense, 1 varlen (B sequences, Sq/Sk = max_seqlen, rows located by cu_q/cu_k, lse [Hq, total_q]),
+// 2 FlashMask (dense layout + fm [B, fm_hm, Sk] int4 intervals with the fm_t64 / fm_t256 fwd / bwd plans).
+extern "C" int pd_flash_fwd_ext(int dt, const void* q, const void* k, const void* v, void* o, float* lse, int B,
+                                int Sq, int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, float scale,
+                                int causal, int mode, const int* cu_q, const int* cu_k, int total_q, const int* fm,
+                                const int* fm_t64, const int* fm_t256, int fm_hm, void* stream) {
+  if (dt != kBF16 || (D != 64 && D != 128) || Hq % Hk || mode < 0 || mode > 2) return -1;
+  if (mode == 1 && (!cu_q || !cu_k)) return -2;
+  if (mode == 2 && (!fm || !fm_t64 || (fm_hm != 1 && fm_hm != Hq))) return -2;
   hipStream_t st = (hipStream_t)stream;
   const int nmb = (Sq + 127) / 128;
   dim3 grid(nmb * Hq * B), block(256);
-#define PD_FA_FWD(DD, CC)                                                                                       \
-  fa::fwd_kernel<DD, CC><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, B, \
-                                                 Sq, Sk, Hq, Hk, sq, sk, sv, so, scale)
-  if (D == 128) { if (causal) PD_FA_FWD(128, true); else PD_FA_FWD(128, false); }
-  else { if (causal) PD_FA_FWD(64, true); else PD_FA_FWD(64, false); }
+  fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm};
+#define PD_FA_FWD(DD, CC, MM)                                                                                      \
+  fa::fwd_kernel<DD, CC, MM><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, \
+                                                     B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, ex)
+#define PD_FA_FWD_M(MM)                                                                             \
+  if (D == 128) { if (causal) PD_FA_FWD(128, true, MM); else PD_FA_FWD(128, false, MM); }          \
+  else { if (causal) PD_FA_FWD(64, true, MM); else PD_FA_FWD(64, false, MM); }
+  if (mode == 0) { PD_FA_FWD_M(fa::kDense) }
+  else if (mode == 1) { PD_FA_FWD_M(fa::kVarlen) }
+  else { PD_FA_FWD_M(fa::kMask) }
+#undef PD_FA_FWD_M
 #undef PD_FA_FWD
   return (int)hipGetLastError();
 }
 
-// dqp: fp32 workspace of nkb * B*Sq*Hq*D floats (nkb = ceil(Sk/256)) for per-key-block dQ partials
-// (need not be zeroed); delta a [B, Hq, Sq] fp32 workspace.  q/k/v/o/dout and dq/dk/dv may all be
-// row-strided views ([B, S, H, D] with token strides), e.g. slices of one fused QKV / dQKV buffer.
+extern "C" int pd_flash_fwd(int dt, const void* q, const void* k, const void* v, void* o, float* lse, int B, int Sq,
+                            int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, float scale, int causal,
+                            void* stream) {
+  return pd_flash_fwd_ext(dt, q, k, v, o, lse, B, Sq, Sk, Hq, Hk, D, sq, sk, sv, so, scale, causal, 0, nullptr,
+                          nullptr, 0, nullptr, nullptr, nullptr, 1, stream);
+}
+
+// dqp: fp32 workspace of nkb * rows*Hq*D floats (nkb = ceil(Sk/256), rows = B*Sq, or total_q for varlen) for
+// per-key-block dQ partials (need not be zeroed); delta a [B, Hq, Sq] ([Hq, total_q] varlen) fp32 workspace.
+// q/k/v/o/dout and dq/dk/dv may all be row-strided views ([B, S, H, D] with token strides), e.g. slices of one
+// fused QKV / dQKV buffer.
+extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void* v, const void* o, const void* dout,
+                                const float* lse, float* delta, void* dq, void* dk, void* dv, float* dqp, int B,
+                                int Sq, int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, long sdq,
+                                long sdk, long sdv, float scale, int causal, int mode, const int* cu_q, const int* cu_k,
+                                int total_q, const int* fm, const int* fm_t64, const int* fm_t256, int fm_hm,
+                                void* stream) {
+  if (dt != kBF16 || (D != 64 && D != 128) || Hq % Hk || mode < 0 || mode > 2) return -1;
+  if (mode == 1 && (!cu_q || !cu_k)) return -2;
+  if (mode == 2 && (!fm || !fm_t256 || (fm_hm != 1 && fm_hm != Hq))) return -2;
+  hipStream_t st = (hipStream_t)stream;
+  const long nrows = mode == 1 ? (long)total_q : (long)B * Sq;  // query tokens
+  // delta shares the lse layout: [B, Hq, Sq] dense, [Hq, total_q] (= B 1, Sq total_q) varlen
+  const int dB = mode == 1 ? 1 : B, dS = mode == 1 ? total_q : Sq;
+  const long rows = (long)dB * Hq * dS;
+  fa::bwd_delta_kernel<<<(int)((rows + 3) / 4), 256, 0, st>>>((const bf16*)o, (const bf16*)dout, delta, dB, dS, Hq,
+                                                               D, so);
+  constexpr int BNK = 256;
+  const int nkb = (Sk + BNK - 1) / BNK;
+  const long pslab = nrows * Hq * D;
+  dim3 grid(nkb * Hk * B), block(512);
+  fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm};
+#define PD_FA_BWD(DD, CC, MM)                                                                                       \
+  fa::bwd_kernel<DD, CC, MM><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,                \
+                                                     (const bf16*)dout, lse, delta, dqp, (bf16*)dk, (bf16*)dv, B, Sq, \
+                                                     Sk, Hq, Hk, sq, sk, sv, so, sdk, sdv, pslab, scale, ex)
+#define PD_FA_BWD_M(MM)                                                                             \
+  if (D == 128) { if (causal) PD_FA_BWD(128, true, MM); else PD_FA_BWD(128, false, MM); }          \
+  else { if (causal) PD_FA_BWD(64, true, MM); else PD_FA_BWD(64, false, MM); }
+  if (mode == 0) { PD_FA_BWD_M(fa::kDense) }
+  else if (mode == 1) { PD_FA_BWD_M(fa::kVarlen) }
+  else { PD_FA_BWD_M(fa::kMask) }
+#undef PD_FA_BWD_M
+#undef PD_FA_BWD
+  long work = nrows * Hq * D / 8;
+  long g = (work + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (mode == 2)
+    fa::dq_reduce_kernel<fa::kMask><<<(int)g, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, D, nkb, pslab, sdq, causal,
+                                                            Sk - Sq, BNK, ex);
+  else if (mode == 1)
+    fa::dq_reduce_kernel<fa::kVarlen><<<(int)g, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, D, nkb, pslab, sdq, causal,
+                                                              Sk - Sq, BNK, ex);
+  else
+    fa::dq_reduce_kernel<fa::kDense><<<(int)g, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, D, nkb, pslab, sdq, causal,
+                                                             Sk - Sq, BNK, ex);
+  return (int)hipGetLastError();
+}
+
 extern "C" int pd_flash_bwd(int dt, const void* q, const void* k, const void* v, const void* o, const void* dout,
                             const float* lse, float* delta, void* dq, void* dk, void* dv, float* dqp, int B, int Sq,
                             int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, long sdq, long sdk,
                             long sdv, float scale, int causal, void* stream) {
-  if (dt != kBF16 || (D != 64 && D != 128) || Hq % Hk) return -1;
-  hipStream_t st = (hipStream_t)stream;
-  const long rows = (long)B * Hq * Sq;
-  fa::bwd_delta_kernel<<<(int)((rows + 3) / 4), 256, 0, st>>>((const bf16*)o, (const bf16*)dout, delta, B, Sq, Hq, D,
-                                                               so);
-  constexpr int BNK = 256;
-  const int nkb = (Sk + BNK - 1) / BNK;
-  const long pslab = (long)B * Sq * Hq * D;
-  dim3 grid(nkb * Hk * B), block(512);
-#define PD_FA_BWD(DD, CC)                                                                                        \
-  fa::bwd_kernel<DD, CC><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, \
-                                                 lse, delta, dqp, (bf16*)dk, (bf16*)dv, B, Sq, Sk, Hq, Hk, sq, sk, \
-                                                 sv, so, sdk, sdv, pslab, scale)
-  if (D == 128) { if (causal) PD_FA_BWD(128, true); else PD_FA_BWD(128, false); }
-  else { if (causal) PD_FA_BWD(64, true); else PD_FA_BWD(64, false); }
-#undef PD_FA_BWD
-  long work = (long)B * Sq * Hq * D / 8;
-  long g = (work + 255) / 256;
-  if (g > 8192) g = 8192;
-  fa::dq_reduce_kernel<<<(int)g, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, D, nkb, pslab, sdq, causal, Sk - Sq, BNK);
-  return (int)hipGetLastError();
+  return pd_flash_bwd_ext(dt, q, k, v, o, dout, lse, delta, dq, dk, dv, dqp, B, Sq, Sk, Hq, Hk, D, sq, sk, sv, so, sdq,
+                          sdk, sdv, scale, causal, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr, 1, stream);
 }

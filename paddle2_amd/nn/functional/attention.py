@@ -57,20 +57,13 @@ def flash_attn_qkvpacked(qkv, dropout=0.0, causal=False, return_softmax=False, *
 def flash_attn_unpadded(query, key, value, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, scale,
                         dropout=0.0, causal=False, return_softmax=False, fixed_seed_offset=None, rng_name="",
                         training=True, name=None):
-    """Varlen attention over packed [total_tokens, heads, d] with cumulative sequence offsets."""
-    from ...ops.torch_ops import flash_attention as _fa
+    """Varlen attention over packed [total_tokens, heads, d] with cumulative sequence offsets (one launch of the
+    kVarlen MFMA kernel for all sequences; reference flash_attention.py:652)."""
+    from ...ops.torch_ops import flash_attention_varlen
 
-    q, k, v = query._t, key._t, value._t
-    cq = cu_seqlens_q._t.tolist()
-    ck = cu_seqlens_k._t.tolist()
-    outs = []
-    for i in range(len(cq) - 1):
-        qs = q[cq[i]:cq[i + 1]].unsqueeze(0)
-        ks = k[ck[i]:ck[i + 1]].unsqueeze(0)
-        vs = v[ck[i]:ck[i + 1]].unsqueeze(0)
-        o, _ = _fa(qs, ks, vs, causal, scale)
-        outs.append(o.squeeze(0))
-    return _wrap(torch.cat(outs, 0)), None
+    out, _ = flash_attention_varlen(query._t, key._t, value._t, cu_seqlens_q._t, cu_seqlens_k._t, int(max_seqlen_q),
+                                    int(max_seqlen_k), causal, scale)
+    return _wrap(out), None
 
 
 def flash_attn_varlen_qkvpacked(qkv, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, scale, dropout=0.0,
@@ -100,42 +93,33 @@ def scaled_dot_product_attention(query, key, value, attn_mask=None, dropout_p=0.
 def flashmask_attention(query, key, value, startend_row_indices=None, *, dropout=0.0, causal=False, window_size=None,
                         return_softmax_lse=False, return_seed_offset=False, fixed_seed_offset=None, rng_name="",
                         training=True, name=None):
-    """FlashMask: per-column row-range masks ([b, h, s_k, {1,2,4}] start/end row indices).
+    """FlashMask (reference flash_attention.py:1098): per-key-column row-range masks [b, h, s_k, {1,2,4}]
+    (LTS / LTE / UTS / UTE).  Runs the kMask MFMA kernel, which skips fully masked (query block x key tile)
+    products and only evaluates element masks on partially masked tiles; window_size is lowered to row ranges
+    as in the reference."""
+    from ...ops.torch_ops import flash_attention_mask
 
-    Builds the dense mask from the compact row ranges (reference flash_attn_kernel.cu:445-494);
-    the sparse-skipping MFMA kernel is future work.
-    """
     q, k, v = query._t, key._t, value._t
-    b, sq, hq, d = q.shape
-    sk = k.shape[1]
+    sq = q.shape[1]
+    if window_size is not None:
+        if startend_row_indices is not None:
+            raise ValueError("can't use window_size with startend_row_indices")
+        if isinstance(window_size, int):
+            window_size = (window_size, window_size)
+        lts = torch.arange(window_size[0] + 1, sq + window_size[0] + 1, dtype=torch.int32, device=q.device)
+        if causal:
+            idx = lts.clamp(max=sq).view(1, 1, sq, 1)
+        else:
+            ute = torch.arange(-window_size[1], sq - window_size[1], dtype=torch.int32, device=q.device)
+            idx = torch.stack([lts, ute], -1).clamp(0, sq).view(1, 1, sq, 2)
+        startend_row_indices = _wrap(idx.expand(q.shape[0], 1, sq, idx.shape[-1]).contiguous())
     if startend_row_indices is None:
         out, _ = flash_attention(query, key, value, dropout, causal, training=training)
-        return out
-    idx = startend_row_indices._t.long()  # [b, h', sk, n]
-    rows = torch.arange(sq, device=q.device)[:, None]  # [sq, 1]
-    n = idx.shape[-1]
-    if n == 1:
-        start = idx[..., 0][:, :, None, :]
-        masked = rows[None, None] >= start
-    elif n == 2:
-        if causal:
-            s0, s1 = idx[..., 0][:, :, None, :], idx[..., 1][:, :, None, :]
-            masked = (rows[None, None] >= s0) & (rows[None, None] < s1)
-        else:
-            s0, e0 = idx[..., 0][:, :, None, :], idx[..., 1][:, :, None, :]
-            masked = (rows[None, None] >= s0) | (rows[None, None] < e0)
-    else:
-        a, bb, c, dd = [idx[..., i][:, :, None, :] for i in range(4)]
-        r = rows[None, None]
-        masked = ((r >= a) & (r < bb)) | ((r >= c) & (r < dd))
-    if causal:
-        masked = masked | (torch.arange(sk, device=q.device)[None, :] > rows)[None, None]
-    bias = torch.zeros(masked.shape, dtype=torch.float32, device=q.device).masked_fill(masked, float("-inf"))
-    qt, kt, vt = q.transpose(1, 2), _rep(k, hq).transpose(1, 2), _rep(v, hq).transpose(1, 2)
-    s = torch.matmul(qt.float(), kt.float().transpose(-1, -2)) / math.sqrt(d) + bias
-    p = torch.softmax(s, -1).nan_to_num(0.0)
-    o = torch.matmul(p, vt.float()).to(q.dtype).transpose(1, 2)
-    return _wrap(o)
+        return (out, None) if return_softmax_lse else out
+    if dropout > 0.0 and training:
+        raise NotImplementedError("flashmask_attention: dropout is not supported")
+    out, lse = flash_attention_mask(q, k, v, startend_row_indices._t, causal)
+    return (_wrap(out), _wrap(lse)) if return_softmax_lse else _wrap(out)
 
 
 def sdp_kernel(enable_math=False, enable_flash=True, enable_mem_efficient=True):

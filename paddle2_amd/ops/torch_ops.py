@@ -500,6 +500,217 @@ def _flash_bwd_native(q, k, v, out, do, lse, dq, dk, dv, scale, causal):
                          dv.stride(1), float(scale), int(causal), N.stream())
 
 
+# ------------------------------------------------------------- varlen (cu_seqlens) and FlashMask variants
+# Same MFMA kernels, MODE-templated (csrc/kernels/flash_attn.hip kVarlen / kMask): varlen locates each
+# sequence's rows through cu_seqlens (reference flash_attn_kernel.cu FlashAttnUnpaddedKernel); FlashMask
+# (reference flash_attn_kernel.cu:445-494) masks per-key row intervals and skips fully masked tiles.
+_MODE_VARLEN, _MODE_MASK = 1, 2
+_BIG_ROW = 1 << 30
+
+
+def flashmask_intervals(startend_row_indices, causal):
+    """[B, Hm, Sk, n] LTS/LTE/UTS/UTE -> [B, Hm, Sk, 4] int32 (a1, b1, a2, b2): rows in [a1, b1) U [a2, b2)
+    are masked for that key column."""
+    idx = startend_row_indices.to(torch.int32)
+    n = idx.shape[-1]
+    z = torch.zeros_like(idx[..., 0])
+    big = torch.full_like(z, _BIG_ROW)
+    if causal and n == 1:
+        parts = (idx[..., 0], big, z, z)
+    elif causal and n == 2:
+        parts = (idx[..., 0], idx[..., 1], z, z)
+    elif not causal and n == 2:
+        parts = (idx[..., 0], big, z, idx[..., 1])
+    elif not causal and n == 4:
+        parts = (idx[..., 0], idx[..., 1], idx[..., 2], idx[..., 3])
+    else:
+        raise ValueError(f"startend_row_indices last dim {n} invalid for causal={causal}")
+    return torch.stack(parts, -1).contiguous()
+
+
+def _fm_tiles(fm, tile):
+    """Per-tile [min a1, max a1, min b1, max b1, min a2, max a2, min b2, max b2] over `tile` keys
+    -> [B*Hm, ntiles, 8]."""
+    B, Hm, Sk, _ = fm.shape
+    nt = (Sk + tile - 1) // tile
+    pad = nt * tile - Sk
+    if pad:
+        fm = torch.cat([fm, fm[:, :, -1:].expand(B, Hm, pad, 4)], 2)  # edge-replicate: min/max unchanged
+    f = fm.view(B * Hm, nt, tile, 4)
+    mn, mx = f.amin(2), f.amax(2)
+    return torch.stack([mn[..., 0], mx[..., 0], mn[..., 1], mx[..., 1], mn[..., 2], mx[..., 2], mn[..., 3],
+                        mx[..., 3]], -1)
+
+
+def _fm_classify(summ, rows, row_tile, Sq):
+    """Class of every (row tile x key tile): 0 unmasked, 1 partial, 2 fully masked -> [B*Hm, n_row_tiles, nt]."""
+    r0 = torch.arange(0, Sq, row_tile, device=summ.device, dtype=torch.int32)[None, :, None]
+    r1 = (r0 + row_tile).clamp(max=Sq)
+    s = summ[:, None]  # [BH, 1, nt, 8]
+    full = ((s[..., 1] <= r0) & (s[..., 2] >= r1)) | ((s[..., 5] <= r0) & (s[..., 6] >= r1))
+    unm = ((s[..., 0] >= r1) | (s[..., 3] <= r0)) & ((s[..., 4] >= r1) | (s[..., 7] <= r0))
+    return torch.where(full, 2, torch.where(unm, 0, 1)).to(torch.int32)
+
+
+_FM_PLAN_CACHE = {}
+
+
+def flashmask_plan(fm, Sq):
+    """Host plans for the kMask kernels.
+
+    fwd: [B*Hm, ceil(Sq/128), 2 + ceil(Sk/64)] = (first, end) non-fully-masked key tile + class per 64-key tile;
+    bwd: [B*Hm, ceil(Sq/32), ceil(Sk/256)] class per (32-row q tile, 256-key block)."""
+    c64 = _fm_classify(_fm_tiles(fm, 64), None, 128, Sq)
+    nt = c64.shape[-1]
+    active = c64 != 2
+    idx = torch.arange(nt, device=fm.device, dtype=torch.int32)
+    any_a = active.any(-1)
+    first = torch.where(any_a, torch.where(active, idx, nt).amin(-1), nt)
+    end = torch.where(any_a, torch.where(active, idx + 1, 0).amax(-1), nt)
+    fwd = torch.cat([first[..., None], end[..., None], c64], -1).to(torch.int32).contiguous()
+    bwd = _fm_classify(_fm_tiles(fm, 256), None, 32, Sq).contiguous()
+    return fwd, bwd
+
+
+def _flashmask_prepare(startend_row_indices, causal, B, Sq, device):
+    """Normalised intervals + plans, cached per mask tensor (every layer of a step shares one mask)."""
+    key = (id(startend_row_indices), startend_row_indices._version, bool(causal), B, Sq, str(device))
+    hit = _FM_PLAN_CACHE.get(key)
+    if hit is not None and hit[0] is startend_row_indices:
+        return hit[1]
+    fm = flashmask_intervals(startend_row_indices.to(device), causal)
+    if fm.shape[0] != B:
+        fm = fm.expand(B, *fm.shape[1:]).contiguous()
+    out = (fm,) + flashmask_plan(fm, Sq)
+    if len(_FM_PLAN_CACHE) > 8:
+        _FM_PLAN_CACHE.clear()
+    _FM_PLAN_CACHE[key] = (startend_row_indices, out)
+    return out
+
+
+def _attn_reference_masked(q, k, v, causal, scale, fm):
+    """fp32 reference with FlashMask intervals fm [B, Hm, Sk, 4]; returns (out, lse[B, H, Sq])."""
+    B, Sq, Hq, D = q.shape
+    Sk, Hk = k.shape[1], k.shape[2]
+    qf, kf, vf = q.float().transpose(1, 2), k.float().transpose(1, 2), v.float().transpose(1, 2)
+    if Hk != Hq:
+        kf, vf = kf.repeat_interleave(Hq // Hk, 1), vf.repeat_interleave(Hq // Hk, 1)
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    r = torch.arange(Sq, device=q.device)[:, None]
+    f = fm.to(q.device).long()[:, :, None]  # [B, Hm, 1, Sk, 4]
+    masked = ((r >= f[..., 0]) & (r < f[..., 1])) | ((r >= f[..., 2]) & (r < f[..., 3]))
+    if causal:
+        masked = masked | (torch.arange(Sk, device=q.device)[None, :] > r + (Sk - Sq))
+    s = s.masked_fill(masked, float("-inf"))
+    lse = torch.logsumexp(s, -1)
+    p = torch.nan_to_num(torch.exp(s - lse[..., None]), nan=0.0)
+    return torch.matmul(p, vf).transpose(1, 2).to(q.dtype), lse
+
+
+def _native_attn_ok(q, k):
+    return (q.device.type == "cuda" and N.use_native(q) and q.dtype == torch.bfloat16 and q.shape[-1] in (64, 128)
+            and q.shape[-2] % k.shape[-2] == 0)
+
+
+class _FlashExtFn(torch.autograd.Function):
+    """mode 1: q/k/v packed [total, H, D] + cu_q/cu_k; mode 2: dense [B, S, H, D] + FlashMask intervals."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale, mode, aux):
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        Hq, D = q.shape[-2], q.shape[-1]
+        Hk = k.shape[-2]
+        if mode == _MODE_VARLEN:
+            cu_q, cu_k, max_q, max_k = aux
+            B, Sq, Sk, total_q = cu_q.numel() - 1, max_q, max_k, q.shape[0]
+            lse = torch.empty(Hq, total_q, dtype=torch.float32, device=q.device)
+            ptrs = (cu_q.data_ptr(), cu_k.data_ptr(), total_q, 0, 0, 0, 1)
+        else:
+            fm, t64, t256 = aux
+            B, Sq, _, _ = q.shape
+            Sk = k.shape[1]
+            lse = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
+            ptrs = (0, 0, 0, fm.data_ptr(), t64.data_ptr(), t256.data_ptr(), fm.shape[1])
+        out = torch.empty_like(q)
+        N.native().flash_fwd_ext(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr(), B, Sq,
+                                 Sk, Hq, Hk, D, q.stride(-3), k.stride(-3), v.stride(-3), out.stride(-3), float(scale),
+                                 int(causal), mode, *ptrs, N.stream())
+        ctx.save_for_backward(q, k, v, out, lse, *aux[:2] if mode == _MODE_VARLEN else aux)
+        ctx.meta = (causal, scale, mode, B, Sq, Sk, ptrs)
+        return out, lse
+
+    @staticmethod
+    def backward(ctx, dout, dlse):
+        q, k, v, out, lse = ctx.saved_tensors[:5]
+        causal, scale, mode, B, Sq, Sk, ptrs = ctx.meta
+        Hq, D = q.shape[-2], q.shape[-1]
+        Hk = k.shape[-2]
+        do = dout.contiguous()
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        nrows = q.shape[0] if mode == _MODE_VARLEN else B * Sq
+        nkb = (Sk + 255) // 256
+        dq32 = torch.empty(nkb * nrows * Hq * D, dtype=torch.float32, device=q.device)
+        delta = torch.empty_like(lse)
+        N.native().flash_bwd_ext(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), do.data_ptr(),
+                                 lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+                                 dq32.data_ptr(), B, Sq, Sk, Hq, Hk, D, q.stride(-3), k.stride(-3), v.stride(-3),
+                                 do.stride(-3), dq.stride(-3), dk.stride(-3), dv.stride(-3), float(scale), int(causal),
+                                 mode, *ptrs, N.stream())
+        return dq, dk, dv, None, None, None, None
+
+
+def flash_attention_varlen(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, causal=False,
+                           scale=None):
+    """Packed variable-length attention: q [total_q, Hq, D], k/v [total_k, Hk, D], cu_seqlens [B+1].
+
+    Returns (out [total_q, Hq, D], lse [Hq, total_q]).  Causal masks are bottom-right aligned per sequence.
+    """
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    if _native_attn_ok(q, k):
+        cu_q = cu_seqlens_q.to(device=q.device, dtype=torch.int32).contiguous()
+        cu_k = cu_seqlens_k.to(device=q.device, dtype=torch.int32).contiguous()
+        return _FlashExtFn.apply(q, k, v, bool(causal), float(scale), _MODE_VARLEN,
+                                 (cu_q, cu_k, int(max_seqlen_q), int(max_seqlen_k)))
+    cq, ck = cu_seqlens_q.tolist(), cu_seqlens_k.tolist()
+    outs, lses = [], []
+    for i in range(len(cq) - 1):
+        o, l = flash_attention(q[cq[i]:cq[i + 1]].unsqueeze(0), k[ck[i]:ck[i + 1]].unsqueeze(0),
+                               v[ck[i]:ck[i + 1]].unsqueeze(0), causal, scale)
+        outs.append(o.squeeze(0))
+        lses.append(l.squeeze(0))
+    return torch.cat(outs, 0), torch.cat(lses, -1)
+
+
+def flash_attention_mask(q, k, v, startend_row_indices, causal=False, scale=None):
+    """FlashMask attention on [B, S, H, D] with per-key row-interval masks ([B, Hm, Sk, n], Hm in {1, Hq})."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    if _native_attn_ok(q, k) and startend_row_indices.shape[1] in (1, q.shape[2]):
+        aux = _flashmask_prepare(startend_row_indices, causal, q.shape[0], q.shape[1], q.device)
+        return _FlashExtFn.apply(q, k, v, bool(causal), float(scale), _MODE_MASK, aux)
+    fm = flashmask_intervals(startend_row_indices.to(q.device), causal)
+    return _FlashMaskRefFn.apply(q, k, v, causal, scale, fm)
+
+
+class _FlashMaskRefFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale, fm):
+        ctx.save_for_backward(q, k, v, fm)
+        ctx.meta = (causal, scale)
+        return _attn_reference_masked(q, k, v, causal, scale, fm)
+
+    @staticmethod
+    def backward(ctx, dout, dlse):
+        q, k, v, fm = ctx.saved_tensors
+        causal, scale = ctx.meta
+        with torch.enable_grad():
+            qq, kk, vv = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+            o, _ = _attn_reference_masked(qq, kk, vv, causal, scale, fm)
+            gq, gk, gv = torch.autograd.grad(o, (qq, kk, vv), dout.float())
+        return gq.to(q.dtype), gk.to(k.dtype), gv.to(v.dtype), None, None, None
+
+
 class _QKVRopeAttnFn(torch.autograd.Function):
     """Fused QKV split -> RoPE(q, k) -> causal flash attention, one autograd node.
 

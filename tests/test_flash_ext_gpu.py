@@ -1,0 +1,117 @@
+"""Varlen (cu_seqlens) and FlashMask variants of the MFMA flash-attention kernels vs. fp32 references.
+
+Reference behaviour: flash_attn_unpadded (python/paddle/nn/functional/flash_attention.py:652) and
+flashmask_attention (:1098, mask semantics of its flashmask_to_densemask docstring)."""
+import pytest
+import torch
+
+from paddle2_amd.ops import torch_ops as T
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _close(a, b, atol, rtol, what=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    tol = atol + rtol * b.abs().max().item()
+    assert err <= tol, f"{what}: max abs err {err} > {tol}"
+
+
+def _rand(shape, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(shape, generator=g).to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("lens_q,lens_k,Hq,Hk", [([100, 300, 1, 513], None, 4, 2),
+                                                  ([64, 256, 17], [128, 256, 40], 2, 2)])
+def test_flash_varlen(causal, D, lens_q, lens_k, Hq, Hk):
+    lens_k = lens_k or lens_q
+    cu_q = torch.tensor([0] + list(torch.tensor(lens_q).cumsum(0)), dtype=torch.int32)
+    cu_k = torch.tensor([0] + list(torch.tensor(lens_k).cumsum(0)), dtype=torch.int32)
+    tq, tk = int(cu_q[-1]), int(cu_k[-1])
+    q, k, v = _rand((tq, Hq, D), 1), _rand((tk, Hk, D), 2), _rand((tk, Hk, D), 3)
+    go = _rand((tq, Hq, D), 4)
+    qg, kg, vg = (t.to(DEV, torch.bfloat16).requires_grad_(True) for t in (q, k, v))
+    og, lg = T.flash_attention_varlen(qg, kg, vg, cu_q.to(DEV), cu_k.to(DEV), max(lens_q), max(lens_k), causal)
+    og.backward(go.to(DEV, torch.bfloat16))
+    # per-sequence fp32 reference
+    for i in range(len(lens_q)):
+        a, b, c, d = int(cu_q[i]), int(cu_q[i + 1]), int(cu_k[i]), int(cu_k[i + 1])
+        qc, kc, vc = (t.clone().requires_grad_(True) for t in (q[a:b], k[c:d], v[c:d]))
+        oc, lc = T._attn_reference(qc[None], kc[None], vc[None], causal, D ** -0.5)
+        oc.backward(go[a:b][None])
+        _close(og[a:b], oc[0], 2e-2, 2e-2, f"out seq {i}")
+        fin = torch.isfinite(lc[0])
+        _close(lg[:, a:b].cpu()[fin], lc[0][fin], 1e-2, 1e-3, f"lse seq {i}")
+        _close(qg.grad[a:b], qc.grad, 5e-2, 3e-2, f"dq seq {i}")
+        _close(kg.grad[c:d], kc.grad, 5e-2, 3e-2, f"dk seq {i}")
+        _close(vg.grad[c:d], vc.grad, 5e-2, 3e-2, f"dv seq {i}")
+
+
+def _doc_mask(B, S, Hm, causal, n, seed):
+    """Random document / sliding / global masks in startend_row_indices form."""
+    g = torch.Generator().manual_seed(seed)
+    j = torch.arange(S)
+    if causal and n == 1:       # causal document mask: key j masked from the end of its document down
+        bounds = torch.sort(torch.randint(1, S, (B, Hm, 3), generator=g), -1).values
+        ends = torch.cat([bounds, torch.full((B, Hm, 1), S)], -1)
+        idx = torch.gather(ends, -1, torch.searchsorted(ends, j.expand(B, Hm, S).contiguous(), right=True))
+        return idx[..., None]
+    if causal and n == 2:       # causal blockwise: [LTS, LTE)
+        lts = (j + torch.randint(1, S // 2, (B, Hm, 1), generator=g)).clamp(max=S)
+        lte = (lts + torch.randint(0, S, (B, Hm, S), generator=g)).clamp(max=S)
+        return torch.stack([lts, lte], -1)
+    if not causal and n == 2:   # sliding window both sides: LTS, UTE
+        w = int(torch.randint(8, S // 2, (1,), generator=g))
+        lts = (j + w + 1).clamp(max=S).expand(B, Hm, S)
+        ute = (j - w).clamp(min=0).expand(B, Hm, S)
+        return torch.stack([lts, ute], -1)
+    lts = (j + torch.randint(16, S, (B, Hm, 1), generator=g)).clamp(max=S)     # global + window, 4 bounds
+    lte = torch.full((B, Hm, S), S)
+    uts = torch.randint(0, S // 4, (B, Hm, S), generator=g)
+    ute = (uts + torch.randint(0, S // 2, (B, Hm, S), generator=g)).clamp(max=S)
+    return torch.stack([lts, lte, uts, ute], -1)
+
+
+@pytest.mark.parametrize("causal,n", [(True, 1), (True, 2), (False, 2), (False, 4)])
+@pytest.mark.parametrize("D,S,Hq,Hk,Hm", [(128, 640, 4, 2, 1), (64, 333, 2, 2, 2), (128, 1024, 2, 1, 2)])
+def test_flashmask(causal, n, D, S, Hq, Hk, Hm):
+    B = 2
+    q, k, v = _rand((B, S, Hq, D), 5), _rand((B, S, Hk, D), 6), _rand((B, S, Hk, D), 7)
+    go = _rand((B, S, Hq, D), 8)
+    idx = _doc_mask(B, S, Hm, causal, n, seed=S + n).to(torch.int32)
+    qg, kg, vg = (t.to(DEV, torch.bfloat16).requires_grad_(True) for t in (q, k, v))
+    og, lg = T.flash_attention_mask(qg, kg, vg, idx.to(DEV), causal)
+    og.backward(go.to(DEV, torch.bfloat16))
+    qc, kc, vc = (t.clone().requires_grad_(True) for t in (q, k, v))
+    fm = T.flashmask_intervals(idx, causal)
+    oc, lc = T._attn_reference_masked(qc, kc, vc, causal, D ** -0.5, fm)
+    oc.backward(go)
+    _close(og, oc, 2e-2, 2e-2, "out")
+    fin = torch.isfinite(lc)
+    _close(lg.cpu()[fin], lc[fin], 1e-2, 1e-3, "lse")
+    _close(qg.grad, qc.grad, 5e-2, 3e-2, "dq")
+    _close(kg.grad, kc.grad, 5e-2, 3e-2, "dk")
+    _close(vg.grad, vc.grad, 5e-2, 3e-2, "dv")
+
+
+def test_flashmask_window_api():
+    """paddle.nn.functional.flashmask_attention(window_size=...) lowers to row ranges (reference :1698-1722)."""
+    import paddle2_amd as paddle
+    import paddle2_amd.nn.functional as F
+
+    paddle.set_device("gpu:0")
+    B, S, H, D = 1, 512, 2, 128
+    q, k, v = (paddle.Tensor._wrap(_rand((B, S, H, D), s).to(DEV, torch.bfloat16)) for s in (9, 10, 11))
+    out = F.flashmask_attention(q, k, v, window_size=64, causal=True)
+    i = torch.arange(S)
+    dense = (i[None, :] > i[:, None]) | (i[None, :] < i[:, None] - 64)  # masked where key outside [i-64, i]
+    bias = torch.zeros(S, S).masked_fill(dense, float("-inf"))
+    ref = torch.nn.functional.scaled_dot_product_attention(
+        q._t.float().cpu().transpose(1, 2), k._t.float().cpu().transpose(1, 2), v._t.float().cpu().transpose(1, 2),
+        attn_mask=bias).transpose(1, 2)
+    _close(out._t, ref, 2e-2, 2e-2, "window")
