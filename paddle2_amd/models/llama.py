@@ -54,6 +54,10 @@ class LlamaConfig:
     dtype: str = "bfloat16"
     tensor_parallel_degree: int = 1
     sequence_parallel: bool = False
+    # context parallelism over the fleet ``sep`` axis: "ulysses" (head<->sequence all-to-all) or "ring"
+    # (zigzag ring flash attention); inputs arrive as this rank's shard (shard_sequence)
+    sep_parallel_degree: int = 1
+    context_parallel: str = "ulysses"
     recompute: bool = False
     pad_token_id: int = 0
     ignore_index: int = -100
@@ -141,11 +145,33 @@ class LlamaAttention(nn.Layer):
             self.v_proj = _linear(config, h, config.num_key_value_heads * self.head_dim, "col")
         self.o_proj = _linear(config, h, h, "row")
 
+    def _sep_group(self):
+        from ..distributed import fleet
+
+        return fleet.get_hybrid_communicate_group().get_sep_parallel_group()
+
     def forward(self, x, position_ids=None):
         b, s = x.shape[0], x.shape[1]
         nh, nkv, d = self.num_heads, self.num_kv, self.head_dim
-        cos, sin = self.rope.tables(x._t.device, s)
+        sep = self.config.sep_parallel_degree
+        cos, sin = self.rope.tables(x._t.device, s * sep)
         pos = None if position_ids is None else position_ids._t
+        if sep > 1:
+            # context parallel: RoPE at the shard's global positions, then the sep-group attention exchange
+            from ..distributed.fleet.meta_parallel import context_parallel as CP
+
+            if self.config.fuse_attention_qkv:
+                qkv = self.qkv_proj(x)._t.view(b, s, nh + 2 * nkv, d)
+                q, k, v = qkv[:, :, :nh], qkv[:, :, nh:nh + nkv], qkv[:, :, nh + nkv:]
+            else:
+                q = self.q_proj(x)._t.view(b, s, nh, d)
+                k = self.k_proj(x)._t.view(b, s, nkv, d)
+                v = self.v_proj(x)._t.view(b, s, nkv, d)
+            q = T.rope(q, cos, sin, pos, style=0)
+            k = T.rope(k, cos, sin, pos, style=0)
+            attn = CP.ring_flash_attention if self.config.context_parallel == "ring" else CP.ulysses_attention
+            o = attn(q, k, v, self._sep_group(), causal=True)
+            return self.o_proj(_wrap(o.reshape(b, s, nh * d)))
         if self.config.fuse_attention_qkv:
             # one autograd node: strided q/k/v views -> RoPE -> flash attention; backward fills one dQKV
             qkv = self.qkv_proj(x)._t.view(b, s, nh + 2 * nkv, d)
@@ -218,6 +244,15 @@ class LlamaModel(nn.Layer):
 
     def forward(self, input_ids, position_ids=None):
         h = self.embed_tokens(input_ids)
+        if position_ids is None and self.config.sep_parallel_degree > 1:
+            from ..distributed import fleet
+            from ..distributed.fleet.meta_parallel.context_parallel import context_positions
+
+            hcg = fleet.get_hybrid_communicate_group()
+            b, s = input_ids.shape[0], input_ids.shape[1]
+            pos = context_positions(s, hcg.get_sep_parallel_world_size(), hcg.get_sep_parallel_rank(),
+                                    self.config.context_parallel, device=h._t.device)
+            position_ids = _wrap(pos[None].expand(b, s))
         residual = None
         for layer in self.layers:
             if self.config.recompute and self.training:

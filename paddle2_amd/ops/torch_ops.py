@@ -500,6 +500,49 @@ def _flash_bwd_native(q, k, v, out, do, lse, dq, dk, dv, scale, causal):
                          dv.stride(1), float(scale), int(causal), N.stream())
 
 
+# ------------------------------------------------------------- raw block primitives (ring / context parallel)
+def attn_block_fwd(q, k, v, causal, scale):
+    """One (query block x key block) flash forward, no autograd: (out [B, Sq, Hq, D], lse [B, Hq, Sq] fp32)."""
+    if _native_attn_ok(q, k):
+        q, k, v = (t if _row_view_ok(t) else t.contiguous() for t in (q, k, v))
+        return _flash_fwd_native(q, k, v, causal, scale)
+    return _attn_reference(q, k, v, causal, scale)
+
+
+def attn_block_bwd(q, k, v, out, do, lse, causal, scale):
+    """Gradients of one block product given the rows' FINAL out / lse (after merging every key block):
+    P = exp(S - lse) is then exactly this block's slice of the global softmax, so the per-block dQ/dK/dV
+    sum to the full-attention gradients.  Native flash bwd on the MI355X, fp32 math on CPU."""
+    if _native_attn_ok(q, k):
+        q, k, v, out, do = (t if _row_view_ok(t) else t.contiguous() for t in (q, k, v, out, do))
+        if out.stride(1) != do.stride(1):
+            out, do = out.contiguous(), do.contiguous()
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        _flash_bwd_native(q, k, v, out, do, lse.contiguous(), dq, dk, dv, scale, causal)
+        return dq, dk, dv
+    B, Sq, Hq, D = q.shape
+    Sk, Hk = k.shape[1], k.shape[2]
+    g = Hq // Hk
+    qf, kf, vf = q.float().transpose(1, 2), k.float().transpose(1, 2), v.float().transpose(1, 2)
+    kr, vr = kf.repeat_interleave(g, 1), vf.repeat_interleave(g, 1)
+    s = torch.matmul(qf, kr.transpose(-1, -2)) * scale
+    if causal:
+        i = torch.arange(Sq, device=q.device)[:, None]
+        j = torch.arange(Sk, device=q.device)[None, :]
+        s = s.masked_fill(j > i + (Sk - Sq), float("-inf"))
+    p = torch.nan_to_num(torch.exp(s - lse.float()[..., None]), nan=0.0)
+    dof, of = do.float().transpose(1, 2), out.float().transpose(1, 2)
+    dvr = torch.matmul(p.transpose(-1, -2), dof)
+    dp = torch.matmul(dof, vr.transpose(-1, -2))
+    delta = (dof * of).sum(-1, keepdim=True)
+    ds = p * (dp - delta)
+    dq = torch.matmul(ds, kr) * scale
+    dkr = torch.matmul(ds.transpose(-1, -2), qf) * scale
+    dk = dkr.view(B, Hk, g, Sk, D).sum(2)
+    dv = dvr.view(B, Hk, g, Sk, D).sum(2)
+    return (dq.transpose(1, 2).to(q.dtype), dk.transpose(1, 2).to(k.dtype), dv.transpose(1, 2).to(v.dtype))
+
+
 # ------------------------------------------------------------- varlen (cu_seqlens) and FlashMask variants
 # Same MFMA kernels, MODE-templated (csrc/kernels/flash_attn.hip kVarlen / kMask): varlen locates each
 # sequence's rows through cu_seqlens (reference flash_attn_kernel.cu FlashAttnUnpaddedKernel); FlashMask

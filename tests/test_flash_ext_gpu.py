@@ -115,3 +115,60 @@ def test_flashmask_window_api():
         q._t.float().cpu().transpose(1, 2), k._t.float().cpu().transpose(1, 2), v._t.float().cpu().transpose(1, 2),
         attn_mask=bias).transpose(1, 2)
     _close(out._t, ref, 2e-2, 2e-2, "window")
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_ring_attention_block_algebra(P):
+    """The zigzag ring schedule of context_parallel.ring_flash_attention, simulated for P virtual ranks in one
+    process on the native block primitives (flash fwd with lse merge; flash bwd with the final out / lse)."""
+    from paddle2_amd.distributed.fleet.meta_parallel import context_parallel as CP
+
+    B, S, Hq, Hk, D = 1, 256 * P, 4, 2, 128
+    q, k, v = _rand((B, S, Hq, D), 20), _rand((B, S, Hk, D), 21), _rand((B, S, Hk, D), 22)
+    go = _rand((B, S, Hq, D), 23)
+    qc, kc, vc = (t.clone().requires_grad_(True) for t in (q, k, v))
+    oc, _ = T._attn_reference(qc, kc, vc, True, D ** -0.5)
+    oc.backward(go)
+    dev = lambda t: t.to(DEV, torch.bfloat16)  # noqa: E731
+    sh = [[CP.zigzag_shard(dev(t), P, r) for r in range(P)] for t in (q, k, v, go)]
+    c = S // P // 2
+    outs, lses = [], []
+    for r in range(P):
+        ql = sh[0][r]
+        out = torch.zeros(ql.shape, dtype=torch.float32, device=DEV)
+        lse = torch.full((B, Hq, ql.shape[1]), float("-inf"), device=DEV)
+        for i in range(P):
+            src = (r - i) % P
+            kk, vv = sh[1][src], sh[2][src]
+            kind = CP._step_kind(i, r, P)
+            if kind == 0:
+                CP._merge(out, lse, *T.attn_block_fwd(ql, kk, vv, True, D ** -0.5))
+            elif kind == 1:
+                CP._merge(out, lse, *T.attn_block_fwd(ql, kk[:, :c], vv[:, :c], False, D ** -0.5))
+            else:
+                CP._merge(out, lse, *T.attn_block_fwd(ql[:, c:], kk, vv, False, D ** -0.5), slice(c, 2 * c))
+        outs.append(out.to(torch.bfloat16))
+        lses.append(lse)
+    _close(CP.zigzag_unshard(outs), oc, 2e-2, 2e-2, "ring out")
+    dq = [torch.zeros(sh[0][r].shape, device=DEV) for r in range(P)]
+    dk = [torch.zeros(sh[1][r].shape, device=DEV) for r in range(P)]
+    dv = [torch.zeros(sh[2][r].shape, device=DEV) for r in range(P)]
+    for r in range(P):
+        ql, o, do, l = sh[0][r], outs[r], sh[3][r], lses[r]
+        for i in range(P):
+            src = (r - i) % P
+            kk, vv = sh[1][src], sh[2][src]
+            kind = CP._step_kind(i, r, P)
+            if kind == 0:
+                a, b, e = T.attn_block_bwd(ql, kk, vv, o, do, l, True, D ** -0.5)
+                dq[r] += a.float(); dk[src] += b.float(); dv[src] += e.float()  # noqa: E702
+            elif kind == 1:
+                a, b, e = T.attn_block_bwd(ql, kk[:, :c], vv[:, :c], o, do, l, False, D ** -0.5)
+                dq[r] += a.float(); dk[src][:, :c] += b.float(); dv[src][:, :c] += e.float()  # noqa: E702
+            else:
+                a, b, e = T.attn_block_bwd(ql[:, c:], kk, vv, o[:, c:], do[:, c:], l[:, :, c:].contiguous(), False,
+                                           D ** -0.5)
+                dq[r][:, c:] += a.float(); dk[src] += b.float(); dv[src] += e.float()  # noqa: E702
+    _close(CP.zigzag_unshard(dq), qc.grad, 5e-2, 3e-2, "ring dq")
+    _close(CP.zigzag_unshard(dk), kc.grad, 5e-2, 3e-2, "ring dk")
+    _close(CP.zigzag_unshard(dv), vc.grad, 5e-2, 3e-2, "ring dv")
