@@ -20,6 +20,7 @@ int pd_norm_bwd_blocks(int);
 int pd_norm_bwd(int, int, int, const void*, const void*, const void*, const float*, const float*, const void*, void*,
                 float*, float*, void*, void*, int, int, int, void*);
 int pd_swiglu_fwd(int, const void*, const void*, void*, long, int, long, long, void*);
+int pd_transpose16(const void*, void*, long, long, long, long, void*);
 int pd_swiglu_bwd(int, const void*, const void*, const void*, void*, void*, long, int, long, long, long, long, void*);
 int pd_rope(int, int, int, const void*, void*, const float*, const float*, const int64_t*, int, int, int, int, int,
             long, long, void*);
@@ -236,6 +237,9 @@ PYBIND11_MODULE(_C, m) {
                            total_q, P<const int*>(fm), P<const int*>(fm_t64), P<const int*>(fm_t256), fm_hm,
                            P<void*>(st)),
           "flash_bwd_ext");
+  });
+  m.def("transpose16", [](uintptr_t in, uintptr_t out, long M, long N, long ld_in, long ld_out, uintptr_t st) {
+    check(pd_transpose16(P<const void*>(in), P<void*>(out), M, N, ld_in, ld_out, P<void*>(st)), "transpose16");
   });
   m.def("bn_workspace", &pd_bn_workspace);
   m.def("bn_fwd_train", [](int dt, uintptr_t x, uintptr_t z, uintptr_t y, long M, int C, uintptr_t rm, uintptr_t rv,

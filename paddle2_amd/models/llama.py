@@ -291,7 +291,7 @@ class LlamaLMHead(nn.Layer):
             from ..distributed.fleet.layers.mpu.mp_ops import _ColumnLinear
 
             return _wrap(_ColumnLinear.apply(h._t, self.weight._t, None, self._mp_group))
-        return _wrap(torch.matmul(h._t, self.weight._t))
+        return _wrap(T.linear(h._t, self.weight._t))
 
 
 class LlamaPretrainingCriterion(nn.Layer):

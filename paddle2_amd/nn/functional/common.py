@@ -17,6 +17,10 @@ _wrap = Tensor._wrap
 def linear(x, weight, bias=None, name=None):
     t = x._t
     w = weight._t
+    if t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and w.dim() == 2:
+        from ...ops import torch_ops as T
+
+        return _wrap(T.linear(t, w, None if bias is None else bias._t))
     if bias is not None:
         b = bias._t
         if t.dim() == 2:

@@ -292,6 +292,84 @@ def rope(x, cos, sin, pos=None, style=0, time_major=False):
     return _RopeFn.apply(x, cos, sin, pos, style, time_major)
 
 
+# ============================================================================ Linear (layout-aware GEMMs)
+def transpose2d(x):
+    """[M, N] (unit column stride) -> contiguous [N, M]; the HBM-speed HIP transpose for 16-bit tensors."""
+    M, N_ = x.shape
+    if (x.device.type == "cuda" and N.use_native(x) and x.element_size() == 2 and x.stride(1) == 1
+            and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and M % 8 == 0):
+        out = torch.empty(N_, M, dtype=x.dtype, device=x.device)
+        N.native().transpose16(x.data_ptr(), out.data_ptr(), M, N_, x.stride(0), M, N.stream())
+        return out
+    return x.t().contiguous()
+
+
+import os as _os  # noqa: E402
+
+_LINEAR_LAYOUT = _os.environ.get("PADDLE2_AMD_LINEAR_LAYOUT", "auto")  # auto | off | all
+
+
+def _linear_plan(M, K, Nn):
+    """(fwd via W^T, dW via X^T / dY^T).  hipBLASLt runs the layout with both operands contiguous along the
+    reduction dim fastest (profiles/r1_gemm_layouts.md); the transposes cost one HBM pass each, so they pay
+    only on token-heavy GEMMs (W^T: M >= 4096; dW: M >= 8192 and the dY transpose amortised, N >= 2K)."""
+    if _LINEAR_LAYOUT == "off":
+        return False, False
+    if _LINEAR_LAYOUT == "all":
+        return True, True
+    return M >= 4096 and K % 8 == 0, M >= 8192 and Nn >= 2 * K
+
+
+class _LinearFn(torch.autograd.Function):
+    """y = x @ W (+ b) with W [K, N] (Paddle layout) — GEMM layouts picked per shape (see _linear_plan)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        K, Nn = w.shape
+        x2 = x.reshape(-1, K)
+        M = x2.shape[0]
+        fwd_t, dw_t = _linear_plan(M, K, Nn)
+        if fwd_t:
+            y = torch.matmul(x2, transpose2d(w).t())
+        else:
+            y = torch.matmul(x2, w)
+        if b is not None:
+            y += b
+        ctx.save_for_backward(x2, w)
+        ctx.meta = (x.shape, dw_t, b is not None)
+        return y.view(*x.shape[:-1], Nn)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        xshape, dw_t, has_b = ctx.meta
+        Nn = w.shape[1]
+        dy2 = dy.reshape(-1, Nn)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.matmul(dy2, w.t()).view(xshape)
+        if ctx.needs_input_grad[1]:
+            if dw_t:
+                dw = torch.matmul(transpose2d(x2), transpose2d(dy2).t())
+            else:
+                dw = torch.matmul(x2.t(), dy2)
+        if has_b and ctx.needs_input_grad[2]:
+            db = dy2.sum(0)
+        return dx, dw, db
+
+
+def linear(x, w, b=None):
+    """Paddle-layout linear on bf16/fp16 GPU tensors through the layout-aware GEMM node; plain matmul
+    otherwise."""
+    if (x.device.type == "cuda" and x.dtype in (torch.bfloat16, torch.float16) and w.dtype == x.dtype
+            and w.dim() == 2 and x.shape[-1] == w.shape[0] and N.use_native(x)):
+        return _LinearFn.apply(x, w, b)
+    y = torch.matmul(x, w)
+    return y + b if b is not None else y
+
+
 # ============================================================================ softmax cross entropy
 class _SCEFn(torch.autograd.Function):
     @staticmethod

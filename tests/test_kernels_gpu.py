@@ -248,3 +248,33 @@ def test_qkv_rope_attention_fused(nh, nkv):
     og.backward(go.to(DEV, torch.bfloat16))
     oc.backward(go.to(torch.bfloat16).float())
     _close(xg.grad, xc.grad, 5e-2, 3e-2)
+
+
+@pytest.mark.parametrize("M,N", [(4096, 4096), (1000, 72), (136, 8), (8192, 264)])
+def test_transpose16(M, N):
+    x = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    assert torch.equal(T.transpose2d(x), x.t().contiguous())
+    big = torch.randn(M, N + 16, device=DEV, dtype=torch.float16)[:, :N]  # row-strided view
+    assert torch.equal(T.transpose2d(big), big.t().contiguous())
+
+
+@pytest.mark.parametrize("layout", ["off", "all", "auto"])
+def test_linear_layouts(layout, monkeypatch):
+    """Layout-aware Linear node (W^T forward GEMM, X^T/dY^T weight-gradient GEMM) vs fp32 reference."""
+    monkeypatch.setattr(T, "_LINEAR_LAYOUT", layout)
+    M, K, Nn = 8192, 256, 768
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn(2, M // 2, K, generator=g)).to(torch.bfloat16)
+    w = (torch.randn(K, Nn, generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(Nn, generator=g).to(torch.bfloat16)
+    go = torch.randn(2, M // 2, Nn, generator=g).to(torch.bfloat16)
+    xg, wg, bg = (t.to(DEV).requires_grad_(True) for t in (x, w, b))
+    y = T.linear(xg, wg, bg)
+    y.backward(go.to(DEV))
+    xc, wc, bc = (t.float().requires_grad_(True) for t in (x, w, b))
+    yc = xc @ wc + bc
+    yc.backward(go.float())
+    _close(y, yc, 5e-2, 1e-2)
+    _close(xg.grad, xc.grad, 5e-2, 1e-2)
+    _close(wg.grad, wc.grad, 5e-1, 1e-2)
+    _close(bg.grad, bc.grad, 5e-1, 1e-2)
