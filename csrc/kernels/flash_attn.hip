@@ -48,6 +48,7 @@ typedef __attribute__((address_space(3))) char lds_char;
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kDefer = 8.f;  // fwd defer-max threshold (log2 units)
 
 __device__ __forceinline__ int swz(int row, int ch, int nch) {
   return ch ^ ((((row & 3) << 2) | ((row >> 2) & 3)) & (nch - 1));
@@ -314,9 +315,18 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
       for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[kb][i]);
     }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_i, mx * sl2);
-    const float base = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = __builtin_amdgcn_exp2f(m_i - base);
+    // defer-max (T13): the running base moves only when some row of the wave grew past it by more than
+    // 2^kDefer; otherwise P <= 2^kDefer (exact in fp32 / bf16) and the l / O rescale — DT*16 multiplies
+    // per lane, a quarter of the tile's VALU issue — is skipped (wave-uniform branch)
+    const float m_cand = fmaxf(m_i, mx * sl2);
+    if (__any(m_cand > m_i + kDefer)) {
+      const float alpha = __builtin_amdgcn_exp2f(m_i - (m_cand == -INFINITY ? 0.f : m_cand));
+      l_i *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) oacc[dt] *= alpha;
+      m_i = m_cand;
+    }
+    const float base = m_i == -INFINITY ? 0.f : m_i;
     float ls = 0.f;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
@@ -327,10 +337,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
         ls += p;
       }
     }
-    l_i = l_i * alpha + ls;  // per lane-half partial; halves combined at the end
-    m_i = m_new;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) oacc[dt] *= alpha;
+    l_i += ls;  // per lane-half partial; halves combined at the end
 
     // ---- O^T += V^T . P^T
 #pragma unroll
