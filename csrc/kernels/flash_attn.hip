@@ -115,6 +115,13 @@ struct Ext {
 };
 
 // plan classes: 0 = unmasked, 1 = partial, 2 = fully masked
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// raw buffer resource over [p, p + bytes): out-of-range offsets read 0 / drop stores (gfx9 dword3)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes > 0 ? bytes : 0, 0x00020000);
+}
 __device__ __forceinline__ bool fm_masked(int4 m, int row) {
   return (row >= m.x && row < m.y) || (row >= m.z && row < m.w);
 }
@@ -205,22 +212,29 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
   }
 
   u16x8 stk[NLOAD], stv[NLOAD];
+  int voff_k[NLOAD], voff_v[NLOAD];
+#pragma unroll
+  for (int i = 0; i < NLOAD; ++i) {
+    const int c = tid + 256 * i, row = c / NCH, ch = c % NCH;
+    voff_k[i] = row * (int)sk * 2 + ch * 16;
+    voff_v[i] = row * (int)sv * 2 + ch * 16;
+  }
   int stm = 0;  // kMask: one int of the tile's [64 keys][4] interval image per thread
   auto gload = [&](int n0) {
     if constexpr (MODE == kMask) {
       const int key = n0 + (tid >> 2);
       stm = key < Sk ? reinterpret_cast<const int*>(fmk + key)[tid & 3] : 0;
     }
+    // SRSRC buffer loads (T8): the tile base is scalar (SGPRs), each lane's byte offset is a loop-invariant
+    // VGPR, and keys past Sk fall outside num_records and read as zero — no per-load 64-bit address math,
+    // compare or select
+    const int nrows = min(Sk - n0, BN);
+    const __amdgpu_buffer_rsrc_t rk = make_rsrc(Kb + (long)n0 * sk, nrows * (int)sk * 2);
+    const __amdgpu_buffer_rsrc_t rv = make_rsrc(Vb + (long)n0 * sv, nrows * (int)sv * 2);
 #pragma unroll
     for (int i = 0; i < NLOAD; ++i) {
-      const int c = tid + 256 * i, row = c / NCH, ch = c % NCH, key = n0 + row;
-      if (key < Sk) {
-        stk[i] = *reinterpret_cast<const u16x8*>(Kb + (long)key * sk + ch * 8);
-        stv[i] = *reinterpret_cast<const u16x8*>(Vb + (long)key * sv + ch * 8);
-      } else {
-        stk[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        stv[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      }
+      stk[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rk, voff_k[i], 0, 0));
+      stv[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rv, voff_v[i], 0, 0));
     }
   };
   auto lstore = [&](int buf) {
