@@ -398,28 +398,29 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
 // =====================================================================================
 //                                       BACKWARD
 // =====================================================================================
-// delta[b, h, q] = sum_d dO . O  (fp32), one wave per row
+// delta[b, h, q] = sum_d dO . O  (fp32).  D/8 lanes per row (16 for D = 128), so a wave covers 64*8/D rows and
+// every lane moves 2 x 16 B — the one-wave-per-row form left 3/4 of the lanes idle.
 __global__ __launch_bounds__(256) void bwd_delta_kernel(const bf16* __restrict__ O, const bf16* __restrict__ dO,
                                                         float* __restrict__ delta, int B, int Sq, int Hq, int D,
                                                         long so) {
-  const long rowid = blockIdx.x * 4L + (threadIdx.x >> 6);
+  const int lpr = D / 8;                       // lanes per row (power of two: 8 or 16)
+  const long rowid = (blockIdx.x * 256L + threadIdx.x) / lpr;
   const long total = (long)B * Hq * Sq;
-  if (rowid >= total) return;
-  const int lane = threadIdx.x & 63;
-  const int q = (int)(rowid % Sq);
-  const int hq = (int)((rowid / Sq) % Hq);
-  const int b = (int)(rowid / ((long)Sq * Hq));
-  const long base = ((long)b * Sq + q) * so + (long)hq * D;
+  const int sub = threadIdx.x & (lpr - 1);
   float acc = 0.f;
-  for (int d = lane * 8; d < D; d += 512) {
+  if (rowid < total) {
+    const int q = (int)(rowid % Sq);
+    const int hq = (int)((rowid / Sq) % Hq);
+    const int b = (int)(rowid / ((long)Sq * Hq));
+    const long base = ((long)b * Sq + q) * so + (long)hq * D + sub * 8;
     float a[8], c[8];
-    load_vec<bf16, 8>(O + base + d, a);
-    load_vec<bf16, 8>(dO + base + d, c);
+    load_vec<bf16, 8>(O + base, a);
+    load_vec<bf16, 8>(dO + base, c);
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc += a[j] * c[j];
   }
-  acc = wave_sum(acc);
-  if (lane == 0) delta[rowid] = acc;
+  for (int m = lpr / 2; m > 0; m >>= 1) acc += __shfl_xor(acc, m, 64);
+  if (rowid < total && sub == 0) delta[rowid] = acc;
 }
 
 template <int D, bool CAUSAL, int MODE>
@@ -434,13 +435,17 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
   constexpr int KTILE = BNK * D * 2;     // K block image: B operand of S (row reads) and of dQ (tr reads)
   constexpr int QTILE = BMQ * D * 2;     // Q / dO tile image
   constexpr int STILE = BMQ * BNK * 2;   // dS tile [32 q][256 keys]
-  __shared__ __attribute__((aligned(16))) char smem[KTILE + 2 * QTILE + STILE + 2 * BMQ * 4];
-  char* kimg = smem;
-  char* qimg = smem + KTILE;
+  // small, per-step images first so every ds_* address is a lane base + a 16-bit immediate (an LDS offset
+  // >= 64 KiB cost one v_add per read); the K image sits at a 256-B-aligned KOFF so XOR-ed row offsets
+  // compose with its base
+  constexpr int KOFF = (2 * QTILE + STILE + 2 * BMQ * 4 + 255) / 256 * 256;
+  __shared__ __attribute__((aligned(16))) char smem[KOFF + KTILE];
+  char* qimg = smem;
   char* doimg = qimg + QTILE;
   char* simg = doimg + QTILE;
   float* lse_s = reinterpret_cast<float*>(simg + STILE);
   float* del_s = lse_s + BMQ;
+  char* kimg = smem + KOFF;
 
   // heaviest (lowest, under the causal mask) key blocks first, round-robin over the XCDs
   const int kblk = blockIdx.x / (Hk * B);
@@ -486,6 +491,7 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) { dkacc[dt] = f32x16{}; dvacc[dt] = f32x16{}; }
   const float sl2 = scale * kLog2e;
+  const float inv_scale = 1.f / scale;
 
   int q_begin = 0;
   if (CAUSAL) q_begin = max(0, k0 - off) / BMQ * BMQ;
@@ -516,26 +522,34 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
   // register-staged prefetch of the next (head, q-tile) step (issue early / write late, T14)
   u16x8 pq[NL], pd[NL];
   float plse = INFINITY, pdel = 0.f;
+  // Q / dO tiles by SRSRC buffer loads (scalar tile base, loop-invariant lane offsets, rows past Sq read 0);
+  // the row constants are loaded raw and only scaled / masked when staged into LDS, so no arithmetic
+  // waits on the load inside this prefetch (that wait used to stall wave 0 — and with it the barrier)
+  int voff_q[NL], voff_o[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int c = tid + NW * 64 * i, row = c / NCH, ch = c % NCH;
+    voff_q[i] = row * (int)sq * 2 + ch * 16;
+    voff_o[i] = row * (int)so * 2 + ch * 16;
+  }
   auto gload = [&](int step) {
     const int hq = hk * group + step / nqt;
     const int q0 = q_begin + (step % nqt) * BMQ;
-    const bf16* Qb = Q + qt0 * sq + hq * D;
-    const bf16* dOb = dO + qt0 * so + hq * D;
+    const int nrows = min(Sq - q0, BMQ);
+    const __amdgpu_buffer_rsrc_t rq = make_rsrc(Q + (qt0 + q0) * sq + hq * D, nrows * (int)sq * 2);
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc(dO + (qt0 + q0) * so + hq * D, nrows * (int)so * 2);
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
-      const int c = tid + NW * 64 * i, row = c / NCH, ch = c % NCH, q = q0 + row;
-      if (c < BMQ * NCH && q < Sq) {
-        pq[i] = *reinterpret_cast<const u16x8*>(Qb + (long)q * sq + ch * 8);
-        pd[i] = *reinterpret_cast<const u16x8*>(dOb + (long)q * so + ch * 8);
-      } else {
-        pq[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        pd[i] = pq[i];
+      const int c = tid + NW * 64 * i;
+      if (c < BMQ * NCH) {
+        pq[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rq, voff_q[i], 0, 0));
+        pd[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rd, voff_o[i], 0, 0));
       }
     }
     if (tid < BMQ) {
-      const int q = q0 + tid;
-      plse = q < Sq ? -LSE[lse_b + hq * lse_hs + q] / scale : -INFINITY;
-      pdel = q < Sq ? -DELTA[lse_b + hq * lse_hs + q] : 0.f;
+      const long li = lse_b + hq * lse_hs + min(q0 + tid, Sq - 1);
+      plse = LSE[li];
+      pdel = DELTA[li];
     }
   };
   int step = next_step(0);
@@ -556,8 +570,9 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
   int o_trB = rb * (D * 2) + (((cb ^ msk(rb)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
   // transposed K^T reads for dQ (natural k): rows 16ks + 8hh + qq (+4); chunk wv*4 + cb
   const int rqa = 8 * hh + qq, rqb = rqa + 4;
-  int o_kqA = rqa * (D * 2) + ((((wv * 4 + cb) ^ msk(rqa)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
-  int o_kqB = rqb * (D * 2) + ((((wv * 4 + cb) ^ msk(rqb)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
+  // (relative to smem: KOFF folded into the lane base, the per-ks step stays an immediate < 64 KiB)
+  int o_kqA = KOFF + rqa * (D * 2) + ((((wv * 4 + cb) ^ msk(rqa)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
+  int o_kqB = KOFF + rqb * (D * 2) + ((((wv * 4 + cb) ^ msk(rqb)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
   // dS image [32 q][BNK keys]: A-operand row reads and this lane's column writes
   constexpr int SNCH = BNK / 8;
   int o_srow = r * (BNK * 2) + (((h ^ msk(r)) & (SNCH - 1)) << 4);
@@ -580,8 +595,9 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
       }
     }
     if (tid < BMQ) {
-      lse_s[tid] = plse;
-      del_s[tid] = pdel;
+      const bool ok = q0 + tid < Sq;
+      lse_s[tid] = ok ? -plse * inv_scale : -INFINITY;
+      del_s[tid] = ok ? -pdel : 0.f;
     }
     const int fm_cls = step_cls(step);
     if constexpr (MODE == kMask) {
@@ -661,15 +677,27 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
       for (int ks = 0; ks < BNK / 16; ++ks) {
         const bf16x8 a = lds_b128(simg, o_srow ^ (ks << 5));
         const int kb16 = ks * 16 * (D * 2);
-        const bf16x8 bb = cat4(lds_tr(kimg, o_kqA + kb16), lds_tr(kimg, o_kqB + kb16));
+        const bf16x8 bb = cat4(lds_tr(smem, o_kqA + kb16), lds_tr(smem, o_kqB + kb16));
         dq = mfma(a, bb, dq);
       }
-      // accumulator: row q = (i&3)+8(i>>2)+4h, col d = wv*32 + r -> two 128-B row segments per store
-      float* dqh = dQs + (long)hq * D + wv * 32 + r;
+      // accumulator: row q = (i&3)+8(i>>2)+4h, col d = wv*32 + r -> two 128-B row segments per store.
+      // Full 32-row tiles: non-temporal buffer stores, the per-row offset in the scalar soffset (no VALU);
+      // the tile that crosses Sq keeps the checked stores
+      if (q0 + BMQ <= Sq) {
+        const int hqd4 = Hq * D * 4;
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(dQs + (long)q0 * Hq * D + (long)hq * D, BMQ * hqd4);
+        const int vo = 4 * h * hqd4 + (wv * 32 + r) * 4;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int q = q0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (q < Sq) __builtin_nontemporal_store(dq[i] * scale, dqh + (long)q * Hq * D);
+        for (int i = 0; i < 16; ++i)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dq[i] * scale), rs, vo,
+                                                ((i & 3) + 8 * (i >> 2)) * hqd4, 2);
+      } else {
+        float* dqh = dQs + (long)hq * D + wv * 32 + r;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int q = q0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (q < Sq) __builtin_nontemporal_store(dq[i] * scale, dqh + (long)q * Hq * D);
+        }
       }
     }
     step = step_next;
@@ -806,8 +834,9 @@ extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void
   // delta shares the lse layout: [B, Hq, Sq] dense, [Hq, total_q] (= B 1, Sq total_q) varlen
   const int dB = mode == 1 ? 1 : B, dS = mode == 1 ? total_q : Sq;
   const long rows = (long)dB * Hq * dS;
-  fa::bwd_delta_kernel<<<(int)((rows + 3) / 4), 256, 0, st>>>((const bf16*)o, (const bf16*)dout, delta, dB, dS, Hq,
-                                                               D, so);
+  const long rows_per_blk = 256 / (D / 8);
+  fa::bwd_delta_kernel<<<(int)((rows + rows_per_blk - 1) / rows_per_blk), 256, 0, st>>>(
+      (const bf16*)o, (const bf16*)dout, delta, dB, dS, Hq, D, so);
   constexpr int BNK = 256;
   const int nkb = (Sk + BNK - 1) / BNK;
   const long pslab = nrows * Hq * D;
