@@ -201,6 +201,9 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
     if (qrow < Sq) qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (long)qrow * sq + ks * 16 + 8 * h);
     else qf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
+  // settle the Q fragment loads before the loop (see bwd_kernel: keeps vmcnt(0) out of the tile loop)
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(qf[ks]));
 
   int n_end = Sk;
   if (CAUSAL) n_end = min(Sk, m0 + BM + off);
@@ -273,7 +276,6 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
     const int n0 = t * BN;
     const int tn = next_tile(t + 1);
     const bool has_next = tn < ntiles;
-    if (has_next) gload(tn * BN);  // issue early; lands while we compute (T14)
     const char* kt = smem + buf * 2 * TILE;
     const char* vt = kt + TILE;
 
@@ -289,6 +291,8 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
         s[kb] = mfma(a, qf[ks], s[kb]);
       }
     }
+    // next tile's K/V loads issue after QK^T (T14): softmax + PV cover their flight, lstore waits at the end
+    if (has_next) gload(tn * BN);
     // ---- mask, online softmax (lane owns query qrow; 32 of the 64 keys).  The max is taken on raw
     // scores and the 1/sqrt(d)*log2(e) scale is folded into one FMA feeding v_exp_f32; masking is
     // a separate, wave-uniformly skipped pass so the common (unmasked) tile has no branches.
@@ -487,6 +491,10 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
     if (mykey < Sk) vf[ks] = *reinterpret_cast<const bf16x8*>(Vb + (long)mykey * sv + ks * 16 + 8 * h);
     else vf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
+  // settle the V fragment loads here: a VMEM result still in flight at the loop header makes the compiler's
+  // waitcnt pass fence the first in-loop use with vmcnt(0) — which would also drain every step's prefetch
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(vf[ks]));
   f32x16 dkacc[DT], dvacc[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) { dkacc[dt] = f32x16{}; dvacc[dt] = f32x16{}; }
