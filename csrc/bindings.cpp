@@ -21,6 +21,7 @@ int pd_norm_bwd(int, int, int, const void*, const void*, const void*, const floa
                 float*, float*, void*, void*, int, int, int, void*);
 int pd_swiglu_fwd(int, const void*, const void*, void*, long, int, long, long, void*);
 int pd_transpose16(const void*, void*, long, long, long, long, void*);
+int pd_swiglu_bwd_t(const void*, const void*, void*, void*, long, int, long, void*);
 int pd_swiglu_bwd(int, const void*, const void*, const void*, void*, void*, long, int, long, long, long, long, void*);
 int pd_rope(int, int, int, const void*, void*, const float*, const float*, const int64_t*, int, int, int, int, int,
             long, long, void*);
@@ -240,6 +241,11 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("transpose16", [](uintptr_t in, uintptr_t out, long M, long N, long ld_in, long ld_out, uintptr_t st) {
     check(pd_transpose16(P<const void*>(in), P<void*>(out), M, N, ld_in, ld_out, P<void*>(st)), "transpose16");
+  });
+  m.def("swiglu_bwd_t", [](uintptr_t x, uintptr_t g, uintptr_t dxy, uintptr_t dxyT, long M, int H, long sx,
+                           uintptr_t st) {
+    check(pd_swiglu_bwd_t(P<const void*>(x), P<const void*>(g), P<void*>(dxy), P<void*>(dxyT), M, H, sx, P<void*>(st)),
+          "swiglu_bwd_t");
   });
   m.def("bn_workspace", &pd_bn_workspace);
   m.def("bn_fwd_train", [](int dt, uintptr_t x, uintptr_t z, uintptr_t y, long M, int C, uintptr_t rm, uintptr_t rv,

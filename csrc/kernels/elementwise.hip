@@ -167,6 +167,70 @@ __global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, T* _
   }
 }
 
+
+// ------------------------------------------------------------------------------ SwiGLU bwd + transposed dXY
+// Packed gate|up input x [M, 2H] (row stride sx), upstream g [M, H] -> dxy [M, 2H] and dxyT [2H, M] (the
+// weight-gradient GEMM of the gate_up projection wants dY with tokens contiguous: writing it here costs one
+// extra 2-byte store per element instead of a separate read+write transpose pass).  One workgroup = a tile of
+// 64 tokens x 64 features of both halves; the transposed tiles go through XOR-swizzled LDS images so the
+// column gathers stay conflict-free and every wave-instruction stores whole 128-B runs of dxyT.
+__global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const bf16* __restrict__ x, const bf16* __restrict__ g,
+                                                           bf16* __restrict__ dxy, bf16* __restrict__ dxyT, long M,
+                                                           int H, long sx, long tiles_h, long ntiles) {
+  __shared__ __attribute__((aligned(16))) unsigned short tl[2][64][64];  // [gate|up][token][feature]
+  const int tid = threadIdx.x;
+  for (long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const long r0 = (t / tiles_h) * 64;
+    const int c0 = (int)(t % tiles_h) * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ch = tid + 256 * i;
+      const int r = ch >> 3, c8 = ch & 7;
+      const long row = r0 + r;
+      const int col = c0 + c8 * 8;
+      u16x8 og = u16x8{0, 0, 0, 0, 0, 0, 0, 0}, ou = og;
+      if (row < M) {
+        float a[8], b[8], gg[8], da[8], db[8];
+        load_vec<bf16, 8>(x + row * sx + col, a);
+        load_vec<bf16, 8>(x + row * sx + H + col, b);
+        load_vec<bf16, 8>(g + row * H + col, gg);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float sg = sigmoidf_(a[j]);
+          db[j] = gg[j] * a[j] * sg;
+          da[j] = gg[j] * b[j] * sg * (1.f + a[j] * (1.f - sg));
+        }
+        store_vec<bf16, 8>(dxy + row * 2 * H + col, da);
+        store_vec<bf16, 8>(dxy + row * 2 * H + H + col, db);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { og[j] = f2bf(da[j]); ou[j] = f2bf(db[j]); }
+      }
+      const int sw = (c8 ^ ((r >> 3) & 7)) * 8;
+      *reinterpret_cast<u16x8*>(&tl[0][r][sw]) = og;
+      *reinterpret_cast<u16x8*>(&tl[1][r][sw]) = ou;
+    }
+    __syncthreads();
+    // transposed: per half 64 feature rows x 8 chunks of 8 tokens; a wave stores 8 rows x 128 B
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ch = tid + 256 * i;
+      const int half = ch >> 9, f = (ch >> 3) & 63, gq = ch & 7;  // feature f, tokens 8gq..8gq+8
+      const int colsw = (((f >> 3) ^ gq) << 3) | (f & 7);
+      u16x8 w;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = tl[half][8 * gq + j][colsw];
+      const long orow = (long)half * H + c0 + f, ocol = r0 + 8 * gq;
+      if (ocol + 8 <= M) {
+        *reinterpret_cast<u16x8*>(dxyT + orow * M + ocol) = w;
+      } else {
+        for (int j = 0; j < 8; ++j)
+          if (ocol + j < M) reinterpret_cast<unsigned short*>(dxyT)[orow * M + ocol + j] = w[j];
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace pd
 
 using namespace pd;
@@ -189,6 +253,16 @@ extern "C" int pd_swiglu_bwd(int dt, const void* x, const void* y, const void* d
   const int g = ew_grid(rows * (H / V));
   PD_DISPATCH_FLOAT(dt, T, swiglu_bwd_kernel<T><<<g, 256, 0, st>>>((const T*)x, (const T*)y, (const T*)dout, (T*)dx,
                                                                     (T*)dy, rows, H, sx, sy, sdx, sdy));
+  return (int)hipGetLastError();
+}
+
+extern "C" int pd_swiglu_bwd_t(const void* x, const void* g, void* dxy, void* dxyT, long M, int H, long sx,
+                               void* stream) {
+  if (H % 64 || sx % 8) return -1;
+  const long tiles_h = H / 64, ntiles = ((M + 63) / 64) * tiles_h;
+  const long grid = ntiles < 256L * 16 ? ntiles : 256L * 16;
+  swiglu_bwd_t_kernel<<<(int)grid, 256, 0, (hipStream_t)stream>>>((const bf16*)x, (const bf16*)g, (bf16*)dxy,
+                                                                   (bf16*)dxyT, M, H, sx, tiles_h, ntiles);
   return (int)hipGetLastError();
 }
 

@@ -200,7 +200,9 @@ class LlamaMLP(nn.Layer):
         self.down_proj = _linear(config, f, h, "row")
 
     def forward(self, x):
-        if self.config.fuse_attention_ffn:
+        if self.config.fuse_attention_ffn and type(self.gate_up_fused_proj) is nn.Linear:
+            a = T.swiglu_linear(x._t, self.gate_up_fused_proj.weight._t)  # one node: GEMM + SwiGLU (+dY^T)
+        elif self.config.fuse_attention_ffn:
             a = T.swiglu(self.gate_up_fused_proj(x)._t)  # per-rank [gate_r | up_r]
         else:
             a = T.swiglu(self.gate_proj(x)._t, self.up_proj(x)._t)

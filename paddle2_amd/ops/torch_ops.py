@@ -370,6 +370,46 @@ def linear(x, w, b=None):
     return y + b if b is not None else y
 
 
+class _SwiGLULinearFn(torch.autograd.Function):
+    """a = swiglu(x @ W) for the packed gate|up projection W [K, 2H] (Llama MLP up half), one node:
+    forward through W^T (fast hipBLASLt layout); backward's SwiGLU kernel also writes dY^T, so the weight
+    gradient runs (X^T) @ (dY^T)^T without a separate dY transpose pass (csrc/kernels/elementwise.hip
+    swiglu_bwd_t_kernel)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        K, H2 = w.shape
+        x2 = x.reshape(-1, K)
+        gu = torch.matmul(x2, transpose2d(w).t())
+        a = swiglu(gu)
+        ctx.save_for_backward(x2, w, gu)
+        ctx.xshape = x.shape
+        return a.view(*x.shape[:-1], H2 // 2)
+
+    @staticmethod
+    def backward(ctx, da):
+        x2, w, gu = ctx.saved_tensors
+        M, H2 = gu.shape
+        da2 = da.reshape(M, H2 // 2).contiguous()
+        dgu = torch.empty_like(gu)
+        dguT = torch.empty(H2, M, dtype=gu.dtype, device=gu.device)
+        N.native().swiglu_bwd_t(gu.data_ptr(), da2.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), M, H2 // 2, H2,
+                                N.stream())
+        dx = torch.matmul(dgu, w.t()).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dw = torch.matmul(transpose2d(x2), dguT.t()) if ctx.needs_input_grad[1] else None
+        return dx, dw
+
+
+def swiglu_linear(x, w):
+    """swiglu(x @ W) with W [K, 2H] packed [gate | up]."""
+    K, H2 = w.shape
+    M = x.numel() // K
+    if (x.device.type == "cuda" and x.dtype == torch.bfloat16 and w.dtype == x.dtype and N.use_native(x)
+            and (H2 // 2) % 64 == 0 and M >= 4096 and M % 8 == 0 and _LINEAR_LAYOUT != "off"):
+        return _SwiGLULinearFn.apply(x, w)
+    return swiglu(linear(x, w))
+
+
 # ============================================================================ softmax cross entropy
 class _SCEFn(torch.autograd.Function):
     @staticmethod

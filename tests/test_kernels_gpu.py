@@ -278,3 +278,23 @@ def test_linear_layouts(layout, monkeypatch):
     _close(xg.grad, xc.grad, 5e-2, 1e-2)
     _close(wg.grad, wc.grad, 5e-1, 1e-2)
     _close(bg.grad, bc.grad, 5e-1, 1e-2)
+
+
+@pytest.mark.parametrize("M", [8192, 4100])
+def test_swiglu_linear_fused(M):
+    """GEMM + SwiGLU node whose backward kernel also writes dY^T for the weight gradient."""
+    K, H = 256, 192
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    w = (torch.randn(K, 2 * H, generator=g) * 0.05).to(torch.bfloat16)
+    go = torch.randn(M, H, generator=g).to(torch.bfloat16)
+    xg, wg = (t.to(DEV).requires_grad_(True) for t in (x, w))
+    a = T.swiglu_linear(xg, wg)
+    a.backward(go.to(DEV))
+    xc, wc = (t.float().requires_grad_(True) for t in (x, w))
+    gu = xc @ wc
+    ac = torch.nn.functional.silu(gu[:, :H]) * gu[:, H:]
+    ac.backward(go.float())
+    _close(a, ac, 3e-2, 1e-2)
+    _close(xg.grad, xc.grad, 5e-2, 1e-2)
+    _close(wg.grad, wc.grad, 5e-1, 1e-2)
