@@ -56,10 +56,11 @@ int pd_bn_bwd(int, const void*, const void*, const void*, const float*, const fl
               float*, float*, long, int, float*, int, void*);
 int pd_flash_fwd_ext(int, const void*, const void*, const void*, void*, float*, int, int, int, int, int, int, long,
                      long, long, long, float, int, int, const int*, const int*, int, const int*, const int*, const int*,
-                     int, void*);
+                     int, int, unsigned, float, void*);
 int pd_flash_bwd_ext(int, const void*, const void*, const void*, const void*, const void*, const float*, float*, void*,
                      void*, void*, float*, int, int, int, int, int, int, long, long, long, long, long, long, long, float,
-                     int, int, const int*, const int*, int, const int*, const int*, const int*, int, void*);
+                     int, int, const int*, const int*, int, const int*, const int*, const int*, int, int, unsigned,
+                     float, void*);
 int pd_flash_fwd(int, const void*, const void*, const void*, void*, float*, int, int, int, int, int, int, long, long,
                  long, long, float, int, void*);
 int pd_flash_bwd(int, const void*, const void*, const void*, const void*, const void*, const float*, float*, void*,
@@ -218,11 +219,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("flash_fwd_ext", [](int dt, uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t lse, int B, int Sq,
                             int Sk, int Hq, int Hk, int D, long sq_row, long sk_row, long sv_row, long so_row,
                             float scale, int causal, int mode, uintptr_t cu_q, uintptr_t cu_k, int total_q,
-                            uintptr_t fm, uintptr_t fm_t64, uintptr_t fm_t256, int fm_hm, uintptr_t st) {
+                            uintptr_t fm, uintptr_t fm_t64, uintptr_t fm_t256, int fm_hm, int drop, unsigned seed,
+                            float pdrop, uintptr_t st) {
     check(pd_flash_fwd_ext(dt, P<const void*>(q), P<const void*>(k), P<const void*>(v), P<void*>(o), P<float*>(lse), B,
                            Sq, Sk, Hq, Hk, D, sq_row, sk_row, sv_row, so_row, scale, causal, mode,
                            P<const int*>(cu_q), P<const int*>(cu_k), total_q, P<const int*>(fm),
-                           P<const int*>(fm_t64), P<const int*>(fm_t256), fm_hm, P<void*>(st)),
+                           P<const int*>(fm_t64), P<const int*>(fm_t256), fm_hm, drop, seed, pdrop, P<void*>(st)),
           "flash_fwd_ext");
   });
   m.def("flash_bwd_ext", [](int dt, uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t dout, uintptr_t lse,
@@ -230,13 +232,13 @@ PYBIND11_MODULE(_C, m) {
                             int Sk, int Hq, int Hk, int D, long sq_row, long sk_row, long sv_row, long so_row,
                             long sdq_row, long sdk_row, long sdv_row, float scale, int causal, int mode,
                             uintptr_t cu_q, uintptr_t cu_k, int total_q, uintptr_t fm, uintptr_t fm_t64,
-                            uintptr_t fm_t256, int fm_hm, uintptr_t st) {
+                            uintptr_t fm_t256, int fm_hm, int drop, unsigned seed, float pdrop, uintptr_t st) {
     check(pd_flash_bwd_ext(dt, P<const void*>(q), P<const void*>(k), P<const void*>(v), P<const void*>(o),
                            P<const void*>(dout), P<const float*>(lse), P<float*>(delta), P<void*>(dq), P<void*>(dk),
                            P<void*>(dv), P<float*>(dq32), B, Sq, Sk, Hq, Hk, D, sq_row, sk_row, sv_row, so_row,
                            sdq_row, sdk_row, sdv_row, scale, causal, mode, P<const int*>(cu_q), P<const int*>(cu_k),
-                           total_q, P<const int*>(fm), P<const int*>(fm_t64), P<const int*>(fm_t256), fm_hm,
-                           P<void*>(st)),
+                           total_q, P<const int*>(fm), P<const int*>(fm_t64), P<const int*>(fm_t256), fm_hm, drop,
+                           seed, pdrop, P<void*>(st)),
           "flash_bwd_ext");
   });
   m.def("transpose16", [](uintptr_t in, uintptr_t out, long M, long N, long ld_in, long ld_out, uintptr_t st) {

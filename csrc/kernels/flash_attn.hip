@@ -112,7 +112,25 @@ struct Ext {
   const int* fm_t64;    // kMask fwd plan: [B*Hm, ceil(Sq/128), 2 + ceil(Sk/64)] = first tile, end tile, class/tile
   const int* fm_t256;   // kMask bwd plan: [B*Hm, ceil(Sq/32), ceil(Sk/256)] class per (32-row q tile, key block)
   int fm_hm;            // mask heads: 1 or Hq
+  unsigned drop_seed;   // DROP: per-call seed (Paddle's seed/offset pair folded on the host)
+  unsigned drop_thresh; // DROP: element dropped iff hash < p * 2^32
+  float drop_rscale;    // DROP: 1 / (1 - p)
 };
+
+// Counter-based dropout mask: a stateless 32-bit hash of (seed, batch*head, query, key), so the backward
+// regenerates exactly the forward's mask with no stored bitmask (the reference uses Philox seed/offset,
+// flash_attn_kernel.cu; the stream differs but the contract -- same (seed, offset) => same mask -- holds)
+__device__ __forceinline__ bool drop_keep(const Ext& ex, unsigned bh, unsigned q, unsigned k) {
+  unsigned x = ex.drop_seed ^ (bh * 0x27D4EB2Du);
+  x += q * 0x9E3779B1u;
+  x ^= x >> 15;
+  x *= 0x85EBCA77u;
+  x += k * 0xC2B2AE3Du;
+  x ^= x >> 13;
+  x *= 0x27D4EB2Fu;
+  x ^= x >> 16;
+  return x >= ex.drop_thresh;
+}
 
 // plan classes: 0 = unmasked, 1 = partial, 2 = fully masked
 
@@ -143,7 +161,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int r0, int c0, int 
 // =====================================================================================
 //                                       FORWARD
 // =====================================================================================
-template <int D, bool CAUSAL, int MODE>
+template <int D, bool CAUSAL, int MODE, bool DROP>
 __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ Vv, bf16* __restrict__ O,
                                                      float* __restrict__ LSE, int B, int SqMax, int SkMax, int Hq,
@@ -356,6 +374,17 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
       }
     }
     l_i += ls;  // per lane-half partial; halves combined at the end
+    if constexpr (DROP) {  // row sums keep the undropped P; only the P.V operand is masked
+      const unsigned bh = (unsigned)(b * Hq + hq);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = n0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (!drop_keep(ex, bh, (unsigned)qrow, (unsigned)key)) s[kb][i] = 0.f;
+        }
+      }
+    }
 
     // ---- O^T += V^T . P^T
 #pragma unroll
@@ -377,7 +406,8 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
 
   // ---- epilogue: normalise, store O (row = query, 4 consecutive d per store) and LSE
   const float l_tot = l_i + __shfl_xor(l_i, 32, 64);
-  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if constexpr (DROP) inv *= ex.drop_rscale;
   if (qrow < Sq) {
     bf16* orow = O + (qt0 + qrow) * so + hq * D;
 #pragma unroll
@@ -427,7 +457,7 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const bf16* __restrict__
   if (rowid < total && sub == 0) delta[rowid] = acc;
 }
 
-template <int D, bool CAUSAL, int MODE>
+template <int D, bool CAUSAL, int MODE, bool DROP>
 __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ Vv, const bf16* __restrict__ dO,
                                                      const float* __restrict__ LSE, const float* __restrict__ DELTA,
@@ -654,7 +684,15 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
       if constexpr (MODE == kMask) {
         if (fm_cls == 1 && fm_masked(mym, q0 + qi)) sacc[i] = 0.f;
       }
-      dpacc[i] = sacc[i] * dpacc[i];
+      if constexpr (DROP) {
+        // dS = P (keep * r * dP - delta), dV operand = keep * r * P; dpacc holds dP - delta, nd = -delta
+        const float nd = del_s[qi];
+        const bool keep = drop_keep(ex, (unsigned)(b * Hq + hq), (unsigned)(q0 + qi), (unsigned)mykey);
+        dpacc[i] = sacc[i] * (keep ? fmaf(ex.drop_rscale, dpacc[i] - nd, nd) : nd);
+        sacc[i] = keep ? sacc[i] * ex.drop_rscale : 0.f;
+      } else {
+        dpacc[i] = sacc[i] * dpacc[i];
+      }
     }
     // dV^T += dO^T . P ; dK^T += Q^T . dS   (A operands by transposed reads, permuted k)
 #pragma unroll
@@ -795,23 +833,29 @@ using namespace pd;
 extern "C" int pd_flash_fwd_ext(int dt, const void* q, const void* k, const void* v, void* o, float* lse, int B,
                                 int Sq, int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, float scale,
                                 int causal, int mode, const int* cu_q, const int* cu_k, int total_q, const int* fm,
-                                const int* fm_t64, const int* fm_t256, int fm_hm, void* stream) {
+                                const int* fm_t64, const int* fm_t256, int fm_hm, int drop, unsigned seed, float pdrop,
+                                void* stream) {
   if (dt != kBF16 || (D != 64 && D != 128) || Hq % Hk || mode < 0 || mode > 2) return -1;
+  if (drop && (mode == 2 || !(pdrop > 0.f && pdrop < 1.f))) return -3;
   if (mode == 1 && (!cu_q || !cu_k)) return -2;
   if (mode == 2 && (!fm || !fm_t64 || (fm_hm != 1 && fm_hm != Hq))) return -2;
   hipStream_t st = (hipStream_t)stream;
   const int nmb = (Sq + 127) / 128;
   dim3 grid(nmb * Hq * B), block(256);
-  fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm};
-#define PD_FA_FWD(DD, CC, MM)                                                                                      \
-  fa::fwd_kernel<DD, CC, MM><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, \
-                                                     B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, ex)
-#define PD_FA_FWD_M(MM)                                                                             \
-  if (D == 128) { if (causal) PD_FA_FWD(128, true, MM); else PD_FA_FWD(128, false, MM); }          \
-  else { if (causal) PD_FA_FWD(64, true, MM); else PD_FA_FWD(64, false, MM); }
-  if (mode == 0) { PD_FA_FWD_M(fa::kDense) }
-  else if (mode == 1) { PD_FA_FWD_M(fa::kVarlen) }
-  else { PD_FA_FWD_M(fa::kMask) }
+  fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm, seed,
+             drop ? (unsigned)fminf(pdrop * 4294967296.f, 4294967040.f) : 0u, drop ? 1.f / (1.f - pdrop) : 1.f};
+#define PD_FA_FWD(DD, CC, MM, DR)                                                                                   \
+  fa::fwd_kernel<DD, CC, MM, DR><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o,  \
+                                                         lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, ex)
+#define PD_FA_FWD_M(MM, DR)                                                                              \
+  if (D == 128) { if (causal) PD_FA_FWD(128, true, MM, DR); else PD_FA_FWD(128, false, MM, DR); }       \
+  else { if (causal) PD_FA_FWD(64, true, MM, DR); else PD_FA_FWD(64, false, MM, DR); }
+  if (drop) {
+    if (mode == 0) { PD_FA_FWD_M(fa::kDense, true) }
+    else { PD_FA_FWD_M(fa::kVarlen, true) }
+  } else if (mode == 0) { PD_FA_FWD_M(fa::kDense, false) }
+  else if (mode == 1) { PD_FA_FWD_M(fa::kVarlen, false) }
+  else { PD_FA_FWD_M(fa::kMask, false) }
 #undef PD_FA_FWD_M
 #undef PD_FA_FWD
   return (int)hipGetLastError();
@@ -821,7 +865,7 @@ extern "C" int pd_flash_fwd(int dt, const void* q, const void* k, const void* v,
                             int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, float scale, int causal,
                             void* stream) {
   return pd_flash_fwd_ext(dt, q, k, v, o, lse, B, Sq, Sk, Hq, Hk, D, sq, sk, sv, so, scale, causal, 0, nullptr,
-                          nullptr, 0, nullptr, nullptr, nullptr, 1, stream);
+                          nullptr, 0, nullptr, nullptr, nullptr, 1, 0, 0u, 0.f, stream);
 }
 
 // dqp: fp32 workspace of nkb * rows*Hq*D floats (nkb = ceil(Sk/256), rows = B*Sq, or total_q for varlen) for
@@ -833,8 +877,9 @@ extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void
                                 int Sq, int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, long sdq,
                                 long sdk, long sdv, float scale, int causal, int mode, const int* cu_q, const int* cu_k,
                                 int total_q, const int* fm, const int* fm_t64, const int* fm_t256, int fm_hm,
-                                void* stream) {
+                                int drop, unsigned seed, float pdrop, void* stream) {
   if (dt != kBF16 || (D != 64 && D != 128) || Hq % Hk || mode < 0 || mode > 2) return -1;
+  if (drop && (mode == 2 || !(pdrop > 0.f && pdrop < 1.f))) return -3;
   if (mode == 1 && (!cu_q || !cu_k)) return -2;
   if (mode == 2 && (!fm || !fm_t256 || (fm_hm != 1 && fm_hm != Hq))) return -2;
   hipStream_t st = (hipStream_t)stream;
@@ -849,17 +894,21 @@ extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void
   const int nkb = (Sk + BNK - 1) / BNK;
   const long pslab = nrows * Hq * D;
   dim3 grid(nkb * Hk * B), block(512);
-  fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm};
-#define PD_FA_BWD(DD, CC, MM)                                                                                       \
-  fa::bwd_kernel<DD, CC, MM><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,                \
-                                                     (const bf16*)dout, lse, delta, dqp, (bf16*)dk, (bf16*)dv, B, Sq, \
-                                                     Sk, Hq, Hk, sq, sk, sv, so, sdk, sdv, pslab, scale, ex)
-#define PD_FA_BWD_M(MM)                                                                             \
-  if (D == 128) { if (causal) PD_FA_BWD(128, true, MM); else PD_FA_BWD(128, false, MM); }          \
-  else { if (causal) PD_FA_BWD(64, true, MM); else PD_FA_BWD(64, false, MM); }
-  if (mode == 0) { PD_FA_BWD_M(fa::kDense) }
-  else if (mode == 1) { PD_FA_BWD_M(fa::kVarlen) }
-  else { PD_FA_BWD_M(fa::kMask) }
+  fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm, seed,
+             drop ? (unsigned)fminf(pdrop * 4294967296.f, 4294967040.f) : 0u, drop ? 1.f / (1.f - pdrop) : 1.f};
+#define PD_FA_BWD(DD, CC, MM, DR)                                                                                  \
+  fa::bwd_kernel<DD, CC, MM, DR><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,           \
+                                                         (const bf16*)dout, lse, delta, dqp, (bf16*)dk, (bf16*)dv, \
+                                                         B, Sq, Sk, Hq, Hk, sq, sk, sv, so, sdk, sdv, pslab, scale, ex)
+#define PD_FA_BWD_M(MM, DR)                                                                             \
+  if (D == 128) { if (causal) PD_FA_BWD(128, true, MM, DR); else PD_FA_BWD(128, false, MM, DR); }      \
+  else { if (causal) PD_FA_BWD(64, true, MM, DR); else PD_FA_BWD(64, false, MM, DR); }
+  if (drop) {
+    if (mode == 0) { PD_FA_BWD_M(fa::kDense, true) }
+    else { PD_FA_BWD_M(fa::kVarlen, true) }
+  } else if (mode == 0) { PD_FA_BWD_M(fa::kDense, false) }
+  else if (mode == 1) { PD_FA_BWD_M(fa::kVarlen, false) }
+  else { PD_FA_BWD_M(fa::kMask, false) }
 #undef PD_FA_BWD_M
 #undef PD_FA_BWD
   long work = nrows * Hq * D / 8;
@@ -882,5 +931,6 @@ extern "C" int pd_flash_bwd(int dt, const void* q, const void* k, const void* v,
                             int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, long sdq, long sdk,
                             long sdv, float scale, int causal, void* stream) {
   return pd_flash_bwd_ext(dt, q, k, v, o, dout, lse, delta, dq, dk, dv, dqp, B, Sq, Sk, Hq, Hk, D, sq, sk, sv, so, sdq,
-                          sdk, sdv, scale, causal, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr, 1, stream);
+                          sdk, sdv, scale, causal, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr, 1, 0, 0u, 0.f,
+                          stream);
 }

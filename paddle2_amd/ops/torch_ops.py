@@ -665,7 +665,7 @@ def attn_block_bwd(q, k, v, out, do, lse, causal, scale):
 # Same MFMA kernels, MODE-templated (csrc/kernels/flash_attn.hip kVarlen / kMask): varlen locates each
 # sequence's rows through cu_seqlens (reference flash_attn_kernel.cu FlashAttnUnpaddedKernel); FlashMask
 # (reference flash_attn_kernel.cu:445-494) masks per-key row intervals and skips fully masked tiles.
-_MODE_VARLEN, _MODE_MASK = 1, 2
+_MODE_DENSE, _MODE_VARLEN, _MODE_MASK = 0, 1, 2
 _BIG_ROW = 1 << 30
 
 
@@ -774,14 +774,23 @@ def _native_attn_ok(q, k):
 
 
 class _FlashExtFn(torch.autograd.Function):
-    """mode 1: q/k/v packed [total, H, D] + cu_q/cu_k; mode 2: dense [B, S, H, D] + FlashMask intervals."""
+    """mode 0: dense [B, S, H, D]; mode 1: q/k/v packed [total, H, D] + cu_q/cu_k; mode 2: dense + FlashMask
+    intervals.  ``drop`` = None or (seed32, p): in-kernel attention dropout (modes 0/1) whose keep mask is a
+    counter hash of (seed, batch*head, query, key), regenerated by the backward instead of stored."""
 
     @staticmethod
-    def forward(ctx, q, k, v, causal, scale, mode, aux):
+    def forward(ctx, q, k, v, causal, scale, mode, aux, drop):
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
         Hq, D = q.shape[-2], q.shape[-1]
         Hk = k.shape[-2]
-        if mode == _MODE_VARLEN:
+        dargs = (0, 0, 0.0) if drop is None else (1, int(drop[0]) & 0xFFFFFFFF, float(drop[1]))
+        if mode == _MODE_DENSE:
+            B, Sq, _, _ = q.shape
+            Sk = k.shape[1]
+            lse = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
+            ptrs = (0, 0, 0, 0, 0, 0, 1)
+            aux = ()
+        elif mode == _MODE_VARLEN:
             cu_q, cu_k, max_q, max_k = aux
             B, Sq, Sk, total_q = cu_q.numel() - 1, max_q, max_k, q.shape[0]
             lse = torch.empty(Hq, total_q, dtype=torch.float32, device=q.device)
@@ -795,15 +804,15 @@ class _FlashExtFn(torch.autograd.Function):
         out = torch.empty_like(q)
         N.native().flash_fwd_ext(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr(), B, Sq,
                                  Sk, Hq, Hk, D, q.stride(-3), k.stride(-3), v.stride(-3), out.stride(-3), float(scale),
-                                 int(causal), mode, *ptrs, N.stream())
+                                 int(causal), mode, *ptrs, *dargs, N.stream())
         ctx.save_for_backward(q, k, v, out, lse, *aux[:2] if mode == _MODE_VARLEN else aux)
-        ctx.meta = (causal, scale, mode, B, Sq, Sk, ptrs)
+        ctx.meta = (causal, scale, mode, B, Sq, Sk, ptrs, dargs)
         return out, lse
 
     @staticmethod
     def backward(ctx, dout, dlse):
         q, k, v, out, lse = ctx.saved_tensors[:5]
-        causal, scale, mode, B, Sq, Sk, ptrs = ctx.meta
+        causal, scale, mode, B, Sq, Sk, ptrs, dargs = ctx.meta
         Hq, D = q.shape[-2], q.shape[-1]
         Hk = k.shape[-2]
         do = dout.contiguous()
@@ -816,28 +825,41 @@ class _FlashExtFn(torch.autograd.Function):
                                  lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
                                  dq32.data_ptr(), B, Sq, Sk, Hq, Hk, D, q.stride(-3), k.stride(-3), v.stride(-3),
                                  do.stride(-3), dq.stride(-3), dk.stride(-3), dv.stride(-3), float(scale), int(causal),
-                                 mode, *ptrs, N.stream())
-        return dq, dk, dv, None, None, None, None
+                                 mode, *ptrs, *dargs, N.stream())
+        return dq, dk, dv, None, None, None, None, None
 
 
 def flash_attention_varlen(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, causal=False,
-                           scale=None):
+                           scale=None, dropout=0.0, seed32=None):
     """Packed variable-length attention: q [total_q, Hq, D], k/v [total_k, Hk, D], cu_seqlens [B+1].
 
     Returns (out [total_q, Hq, D], lse [Hq, total_q]).  Causal masks are bottom-right aligned per sequence.
+    ``dropout`` > 0 masks P with the counter hash over (sequence * Hq + head, row, key) positions.
     """
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
+    if dropout > 0.0 and seed32 is None:
+        seed32 = attn_dropout_seed()
     if _native_attn_ok(q, k):
         cu_q = cu_seqlens_q.to(device=q.device, dtype=torch.int32).contiguous()
         cu_k = cu_seqlens_k.to(device=q.device, dtype=torch.int32).contiguous()
+        drop = (seed32, float(dropout)) if dropout > 0.0 else None
         return _FlashExtFn.apply(q, k, v, bool(causal), float(scale), _MODE_VARLEN,
-                                 (cu_q, cu_k, int(max_seqlen_q), int(max_seqlen_k)))
+                                 (cu_q, cu_k, int(max_seqlen_q), int(max_seqlen_k)), drop)
     cq, ck = cu_seqlens_q.tolist(), cu_seqlens_k.tolist()
     outs, lses = [], []
+    Hq = q.shape[1]
     for i in range(len(cq) - 1):
-        o, l = flash_attention(q[cq[i]:cq[i + 1]].unsqueeze(0), k[ck[i]:ck[i + 1]].unsqueeze(0),
-                               v[ck[i]:ck[i + 1]].unsqueeze(0), causal, scale)
+        qi, ki, vi = (q[cq[i]:cq[i + 1]].unsqueeze(0), k[ck[i]:ck[i + 1]].unsqueeze(0),
+                      v[ck[i]:ck[i + 1]].unsqueeze(0))
+        if dropout > 0.0:
+            # the kernel's batch*head index is sequence * Hq + head: shift the seed-free bh counter per sequence
+            ar = lambda n: torch.arange(n, dtype=torch.int64, device=q.device)  # noqa: E731
+            keep = attn_dropout_keep(seed32, (i * Hq + ar(Hq)).view(1, Hq, 1, 1), ar(qi.shape[1]).view(1, 1, -1, 1),
+                                     ar(ki.shape[1]).view(1, 1, 1, -1), dropout)
+            o, l = _attn_reference_dropout(qi, ki, vi, causal, scale, keep, dropout)
+        else:
+            o, l = flash_attention(qi, ki, vi, causal, scale)
         outs.append(o.squeeze(0))
         lses.append(l.squeeze(0))
     return torch.cat(outs, 0), torch.cat(lses, -1)
@@ -849,7 +871,7 @@ def flash_attention_mask(q, k, v, startend_row_indices, causal=False, scale=None
         scale = 1.0 / math.sqrt(q.shape[-1])
     if _native_attn_ok(q, k) and startend_row_indices.shape[1] in (1, q.shape[2]):
         aux = _flashmask_prepare(startend_row_indices, causal, q.shape[0], q.shape[1], q.device)
-        return _FlashExtFn.apply(q, k, v, bool(causal), float(scale), _MODE_MASK, aux)
+        return _FlashExtFn.apply(q, k, v, bool(causal), float(scale), _MODE_MASK, aux, None)
     fm = flashmask_intervals(startend_row_indices.to(q.device), causal)
     return _FlashMaskRefFn.apply(q, k, v, causal, scale, fm)
 
@@ -870,6 +892,125 @@ class _FlashMaskRefFn(torch.autograd.Function):
             o, _ = _attn_reference_masked(qq, kk, vv, causal, scale, fm)
             gq, gk, gv = torch.autograd.grad(o, (qq, kk, vv), dout.float())
         return gq.to(q.dtype), gk.to(k.dtype), gv.to(v.dtype), None, None, None
+
+
+# ------------------------------------------------------------- attention dropout (in-kernel, counter-based mask)
+# Reference: flash_attn_kernel.cu draws the dropout mask from Philox(seed, offset) inside the kernel and
+# regenerates it in the backward.  Ours keeps that contract (same (seed, offset) => same mask, no stored
+# bitmask) with a 32-bit counter hash evaluated per (batch*head, query, key) element in registers
+# (csrc/kernels/flash_attn.hip drop_keep); the mask functions below reproduce it bit-exactly on the host.
+_M32 = 0xFFFFFFFF
+
+
+def _mul32(x, c):
+    """(x * c) mod 2^32 for int64 tensors x in [0, 2^32) without int64 overflow."""
+    return (x * (c & 0xFFFF) + (((x * (c >> 16)) & 0xFFFF) << 16)) & _M32
+
+
+def attn_dropout_threshold(p):
+    """The kernel's keep threshold: float32(p) * 2^32 in float32, clamped below 2^32, truncated."""
+    t = torch.tensor(float(p), dtype=torch.float32) * torch.tensor(4294967296.0, dtype=torch.float32)
+    return int(min(float(t), 4294967040.0))
+
+
+def attn_dropout_keep(seed32, bh, q, k, p):
+    """Keep mask of drop_keep() for broadcastable int64 index tensors bh / q / k (all >= 0)."""
+    x = (int(seed32) & _M32) ^ _mul32(bh, 0x27D4EB2D)
+    x = (x + _mul32(q, 0x9E3779B1)) & _M32
+    x = x ^ (x >> 15)
+    x = _mul32(x, 0x85EBCA77)
+    x = (x + _mul32(k, 0xC2B2AE3D)) & _M32
+    x = x ^ (x >> 13)
+    x = _mul32(x, 0x27D4EB2F)
+    x = x ^ (x >> 16)
+    return x >= attn_dropout_threshold(p)
+
+
+def attn_dropout_mask(seed32, B, H, Sq, Sk, p, device="cpu"):
+    """[B, H, Sq, Sk] bool keep mask of the dense kernel (batch*head index b * H + h)."""
+    ar = lambda n: torch.arange(n, dtype=torch.int64, device=device)  # noqa: E731
+    return attn_dropout_keep(seed32, ar(B * H).view(B, H, 1, 1), ar(Sq).view(1, 1, Sq, 1), ar(Sk).view(1, 1, 1, Sk), p)
+
+
+def attn_dropout_seed(fixed_seed_offset=None):
+    """32-bit kernel seed from a Philox (seed, offset) pair: ``fixed_seed_offset`` when given, else the current
+    device generator's (seed, offset) -- so RNG-tracker states (TP local/global seeds) decorrelate the mask --
+    which is advanced like a torch dropout call; the global paddle (seed, offset) counter on CPU."""
+    if fixed_seed_offset is not None:
+        fso = fixed_seed_offset
+        fso = fso._t if hasattr(fso, "_t") else fso
+        seed, off = (int(v) for v in (fso.tolist() if isinstance(fso, torch.Tensor) else fso))
+    else:
+        seed = off = None
+        if torch.cuda.is_available():
+            try:
+                g = torch.cuda.default_generators[torch.cuda.current_device()]
+                seed, off = g.initial_seed(), g.get_offset()
+                g.set_offset(off + 4)
+            except (AttributeError, RuntimeError):
+                seed = None
+        if seed is None:
+            from ..framework.random import next_philox
+
+            seed, off = next_philox(4)
+    m64 = (1 << 64) - 1
+    x = (seed * 0x9E3779B97F4A7C15 + off * 0xD1B54A32D192ED03 + 0x632BE59BD9B4E019) & m64
+    x ^= x >> 31
+    x = (x * 0xBF58476D1CE4E5B9) & m64
+    x ^= x >> 27
+    return x & _M32
+
+
+def _attn_reference_dropout(q, k, v, causal, scale, keep, p):
+    """fp32 attention with the dropout keep mask [B, Hq, Sq, Sk] applied to P (not to the row sums)."""
+    B, Sq, Hq, D = q.shape
+    Sk, Hk = k.shape[1], k.shape[2]
+    qf, kf, vf = q.float().transpose(1, 2), k.float().transpose(1, 2), v.float().transpose(1, 2)
+    if Hk != Hq:
+        kf, vf = kf.repeat_interleave(Hq // Hk, 1), vf.repeat_interleave(Hq // Hk, 1)
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if causal:
+        i = torch.arange(Sq, device=q.device)[:, None]
+        j = torch.arange(Sk, device=q.device)[None, :]
+        s = s.masked_fill(j > i + (Sk - Sq), float("-inf"))
+    lse = torch.logsumexp(s, -1)
+    pr = torch.nan_to_num(torch.exp(s - lse[..., None]), nan=0.0)
+    pr = pr * keep.to(pr.device) / (1.0 - p)
+    return torch.matmul(pr, vf).transpose(1, 2).to(q.dtype), lse
+
+
+class _FlashDropRefFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale, p, seed32):
+        keep = attn_dropout_mask(seed32, q.shape[0], q.shape[2], q.shape[1], k.shape[1], p, q.device)
+        ctx.save_for_backward(q, k, v, keep)
+        ctx.meta = (causal, scale, p)
+        return _attn_reference_dropout(q, k, v, causal, scale, keep, p)
+
+    @staticmethod
+    def backward(ctx, dout, dlse):
+        q, k, v, keep = ctx.saved_tensors
+        causal, scale, p = ctx.meta
+        with torch.enable_grad():
+            qq, kk, vv = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+            o, _ = _attn_reference_dropout(qq, kk, vv, causal, scale, keep, p)
+            gq, gk, gv = torch.autograd.grad(o, (qq, kk, vv), dout.float())
+        return gq.to(q.dtype), gk.to(k.dtype), gv.to(v.dtype), None, None, None, None
+
+
+def flash_attention_dropout(q, k, v, p, causal=False, scale=None, seed32=None):
+    """Attention with dropout on the softmax probabilities (upscale_in_train): q [B, Sq, Hq, D], k/v [B, Sk, Hk, D]
+    -> (out, lse).  The MI355X path runs the DROP variant of the flash kernels (mask regenerated in the backward);
+    elsewhere an fp32 reference with the bit-identical mask."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    if seed32 is None:
+        seed32 = attn_dropout_seed()
+    if not 0.0 < p < 1.0:
+        raise ValueError(f"dropout probability must be in (0, 1), got {p}")
+    if _native_attn_ok(q, k):
+        return _FlashExtFn.apply(q, k, v, bool(causal), float(scale), _MODE_DENSE, None, (seed32, float(p)))
+    return _FlashDropRefFn.apply(q, k, v, bool(causal), float(scale), float(p), int(seed32))
 
 
 class _QKVRopeAttnFn(torch.autograd.Function):

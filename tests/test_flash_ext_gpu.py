@@ -172,3 +172,67 @@ def test_ring_attention_block_algebra(P):
     _close(CP.zigzag_unshard(dq), qc.grad, 5e-2, 3e-2, "ring dq")
     _close(CP.zigzag_unshard(dk), kc.grad, 5e-2, 3e-2, "ring dk")
     _close(CP.zigzag_unshard(dv), vc.grad, 5e-2, 3e-2, "ring dv")
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("D,Hq,Hk,Sq,Sk", [(128, 4, 2, 300, 300), (64, 2, 2, 200, 333)])
+def test_flash_dropout_dense(causal, D, Hq, Hk, Sq, Sk):
+    """In-kernel dropout (DROP variant) vs. an fp32 reference that applies the bit-identical host mask."""
+    B, p, seed = 2, 0.2, 0x1234ABCD
+    q, k, v = _rand((B, Sq, Hq, D), 11), _rand((B, Sk, Hk, D), 12), _rand((B, Sk, Hk, D), 13)
+    go = _rand((B, Sq, Hq, D), 14)
+    qg, kg, vg = (t.to(DEV, torch.bfloat16).requires_grad_(True) for t in (q, k, v))
+    og, lg = T.flash_attention_dropout(qg, kg, vg, p, causal, seed32=seed)
+    og.backward(go.to(DEV, torch.bfloat16))
+    keep = T.attn_dropout_mask(seed, B, Hq, Sq, Sk, p)
+    assert abs(1.0 - keep.float().mean().item() - p) < 0.01
+    qc, kc, vc = (t.clone().requires_grad_(True) for t in (q, k, v))
+    oc, lc = T._attn_reference_dropout(qc, kc, vc, causal, D ** -0.5, keep, p)
+    oc.backward(go)
+    _close(og, oc, 2e-2, 2e-2, "out")
+    _close(lg.cpu(), lc, 1e-2, 1e-3, "lse (undropped row sums)")
+    _close(qg.grad, qc.grad, 5e-2, 3e-2, "dq")
+    _close(kg.grad, kc.grad, 5e-2, 3e-2, "dk")
+    _close(vg.grad, vc.grad, 5e-2, 3e-2, "dv")
+    # same seed => same output (mask regenerated, not drawn from a stream)
+    o2, _ = T.flash_attention_dropout(qg.detach(), kg.detach(), vg.detach(), p, causal, seed32=seed)
+    assert torch.equal(o2, og.detach())
+
+
+def test_flash_dropout_varlen():
+    D, Hq, p, seed = 128, 2, 0.3, 99
+    lens = [70, 257, 130]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32)
+    tot = int(cu[-1])
+    q, k, v, go = (_rand((tot, Hq, D), 20 + i) for i in range(4))
+    qg, kg, vg = (t.to(DEV, torch.bfloat16).requires_grad_(True) for t in (q, k, v))
+    og, _ = T.flash_attention_varlen(qg, kg, vg, cu.to(DEV), cu.to(DEV), max(lens), max(lens), True, dropout=p,
+                                     seed32=seed)
+    og.backward(go.to(DEV, torch.bfloat16))
+    qc, kc, vc = (t.clone().requires_grad_(True) for t in (q, k, v))
+    oc, _ = T.flash_attention_varlen(qc, kc, vc, cu, cu, max(lens), max(lens), True, dropout=p, seed32=seed)
+    oc.backward(go)
+    _close(og, oc, 2e-2, 2e-2, "out")
+    _close(qg.grad, qc.grad, 5e-2, 3e-2, "dq")
+    _close(kg.grad, kc.grad, 5e-2, 3e-2, "dk")
+    _close(vg.grad, vc.grad, 5e-2, 3e-2, "dv")
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_flash_running_max_jumps(causal):
+    """Late keys with much larger scores force the deferred-max rescale branch (running max jumps mid-row)."""
+    B, S, H, D = 1, 512, 2, 128
+    q, k, v, go = (_rand((B, S, H, D), 30 + i) for i in range(4))
+    k[:, 300:310] *= 12.0  # score spike past the first key tiles
+    k[:, 450] *= 20.0
+    qg, kg, vg = (t.to(DEV, torch.bfloat16).requires_grad_(True) for t in (q, k, v))
+    og, lg = T.flash_attention(qg, kg, vg, causal)
+    og.backward(go.to(DEV, torch.bfloat16))
+    qc, kc, vc = (t.clone().requires_grad_(True) for t in (q, k, v))
+    oc, lc = T._attn_reference(qc, kc, vc, causal, D ** -0.5)
+    oc.backward(go)
+    _close(og, oc, 2e-2, 2e-2, "out")
+    _close(lg.cpu(), lc, 5e-2, 1e-3, "lse")
+    _close(qg.grad, qc.grad, 1e-1, 3e-2, "dq")
+    _close(kg.grad, kc.grad, 1e-1, 3e-2, "dk")
+    _close(vg.grad, vc.grad, 5e-2, 3e-2, "dv")
