@@ -37,6 +37,8 @@ def parse():
     ap.add_argument("--layers", type=int, default=None, help="DEBUG ONLY: override layer count (invalid for the metric)")
     ap.add_argument("--sharding-stage", type=int, default=3)
     ap.add_argument("--recompute", action="store_true")
+    ap.add_argument("--shard-single", action="store_true",
+                    help="wrap with group_sharded_parallel even on 1 GPU (measures the sharding machinery overhead)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--gemm-autotune", default="auto", choices=["auto", "tune", "off"],
                     help="hipBLASLt solution cache (tuning/gemm_gfx950.csv): auto = use it if present")
@@ -90,7 +92,7 @@ def main():
                                  parameters=model.parameters(), weight_decay=0.1,
                                  apply_decay_param_fun=lambda n: n in decay,
                                  grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0), multi_precision=True)
-    if world > 1:
+    if world > 1 or args.shard_single:
         from paddle2_amd.distributed.sharding import group_sharded_parallel
 
         level = {1: "os", 2: "os_g", 3: "p_g_os"}[args.sharding_stage]
@@ -158,7 +160,8 @@ def main():
             "data": "synthetic (uniform random token ids), random-init weights",
             "config": {"model": args.model if not args.layers else f"{args.model}-L{args.layers}(debug)",
                        "global_batch": b * world, "seq_len": s, "micro_batch_per_gpu": b,
-                       "parallelism": f"sharding{args.sharding_stage}x{world}" if world > 1 else "single",
+                       "parallelism": (f"sharding{args.sharding_stage}x{world}" if world > 1 or args.shard_single
+                                       else "single"),
                        "layers": cfg.num_hidden_layers},
             "mfu_vs_2.5PF_dense": round(mfu, 4),
             "final_loss": round(final_loss, 4),

@@ -599,8 +599,38 @@ class RAdam(Optimizer):
             p._t.add_(upd.to(p._t.dtype), alpha=-lr)
 
 
-class ASGD(SGD):
-    pass
+class ASGD(Optimizer):
+    """Averaged SGD over a window of ``batch_num`` gradients (reference: optimizer/asgd.py:239,
+    phi/kernels/cpu/asgd_kernel.cc): ``d += g - y[m % n]``, ``y[m % n] = g``,
+    ``p -= lr / min(m + 1, n) * d``."""
+
+    def __init__(self, learning_rate=0.001, batch_num=1, parameters=None, weight_decay=None, grad_clip=None,
+                 multi_precision=False, name=None):
+        if batch_num is None or batch_num <= 0:
+            raise ValueError("batch_num should be a positive integer")
+        super().__init__(learning_rate, parameters, weight_decay, grad_clip, name)
+        self._n = int(batch_num)
+        self._multi_precision = multi_precision
+
+    def _apply(self, pg):
+        lr = self.get_lr()
+        for p, g in pg:
+            gt = self._reg_grad(p, g._t).float()
+            d = self._acc("d", p)
+            m = self._acc("m", p, like=torch.zeros(1, device=p._t.device))
+            ys = self._accumulators["y"].get(p.name)
+            if ys is None:
+                ys = torch.zeros((self._n,) + tuple(p._t.shape), dtype=torch.float32, device=p._t.device)
+                self._accumulators["y"][p.name] = ys
+            idx = int(m.item()) % self._n
+            m.add_(1)
+            d.sub_(ys[idx]).add_(gt)
+            ys[idx].copy_(gt)
+            mw = self._master(p)
+            tgt = mw if mw is not None else p._t
+            tgt.sub_((d * (lr / min(float(m.item()), self._n))).to(tgt.dtype))
+            if mw is not None:
+                p._t.copy_(mw)
 
 
 class Rprop(Optimizer):
