@@ -102,6 +102,7 @@ class _Unit:
         self.shard = flat[lo:lo + self.S].clone()
         self.master = self.shard.float().clone() if self.dtype in (torch.bfloat16, torch.float16) else None
         self.grad_shard = torch.zeros(self.S, dtype=torch.float32, device=self.device)
+        self.grad_clean = True   # grad_shard logically zero (next accumulate overwrites instead of adding)
         self.full = None
         self.work = None
         self.rs_work = None
@@ -132,12 +133,12 @@ class _Unit:
     def gather(self, async_op=True):
         if self.full is not None or self.work is not None:
             return
-        buf = torch.empty(self.padded, dtype=self.dtype, device=self.device)
         if self.N == 1:
-            buf.copy_(self.shard)
-            self.full = buf
-            self._bind(buf)
+            # the single shard IS the full flat buffer: bind the parameters to it, no copy
+            self.full = self.shard
+            self._bind(self.shard)
             return
+        buf = torch.empty(self.padded, dtype=self.dtype, device=self.device)
         self.work = dist.all_gather_into_tensor(buf, self.shard, group=self.group.pg, async_op=async_op)
         self._pending = buf
         if not async_op:
@@ -168,15 +169,28 @@ class _Unit:
         if self.ready == self.n_trainable:
             self.reduce_grads()
 
+    def _accumulate(self, g):
+        """grad_shard (fp32) += g, or = g when the shard was lazily cleared (no zero-fill pass)."""
+        if self.grad_clean:
+            self.grad_shard.copy_(g)
+            self.grad_clean = False
+        else:
+            self.grad_shard.add_(g)
+
     def reduce_grads(self):
-        flat = torch.zeros(self.padded, dtype=self.dtype, device=self.device)
+        # one flat buffer per unit; only the gaps (missing grads, padding tail) are zero-filled
+        flat = torch.empty(self.padded, dtype=self.dtype, device=self.device)
+        if self.padded > self.total:
+            flat[self.total:].zero_()
         for p, o, n in zip(self.params, self.offsets, self.numels):
             g = p._t.grad
             if g is not None:
                 flat[o:o + n].copy_(g.reshape(-1))
                 p._t.grad = None
+            else:
+                flat[o:o + n].zero_()
         if self.N == 1:
-            self.grad_shard.add_(flat[: self.S].float())
+            self._accumulate(flat[: self.S])
             self.flat_grad = None
         else:
             out = torch.empty(self.S, dtype=self.dtype, device=self.device)
@@ -191,10 +205,10 @@ class _Unit:
             self.reduce_grads()
         if self.rs_work is not None:
             self.rs_work.wait()
-            g = self.rs_buf.float()
+            g = self.rs_buf
             if self.group.backend != "nccl":
-                g.div_(self.N)
-            self.grad_shard.add_(g)
+                g = g.float().div_(self.N)
+            self._accumulate(g)
             self.rs_work = None
             self.rs_buf = None
             self.flat_grad = None
@@ -390,6 +404,12 @@ class GroupShardedOptimizer:
                 out.append((u, p, o, n, dec, lrr))
         return out
 
+    def _materialize_grads(self):
+        for u in self._model._units:
+            if u.grad_clean:      # no gradient reached this unit since clear_grad: it is zero
+                u.grad_shard.zero_()
+                u.grad_clean = False
+
     def _global_sq_norm(self):
         sq = torch.zeros(1, dtype=torch.float32, device=self._model._units[0].device)
         for u in self._model._units:
@@ -403,6 +423,7 @@ class GroupShardedOptimizer:
     def step(self):
         inner = self._inner
         inner._step += 1
+        self._materialize_grads()
         clip = inner._grad_clip
         coef = None
         if clip is not None and hasattr(clip, "clip_norm"):
@@ -469,7 +490,10 @@ class GroupShardedOptimizer:
 
     def clear_grad(self, set_to_zero=True):
         for u in self._model._units:
-            u.grad_shard.zero_()
+            if set_to_zero:
+                u.grad_clean = True  # lazy zero: the next reduce overwrites the shard
+            else:
+                u.grad_shard.zero_()
             for p in u.params:
                 p._t.grad = None
 
