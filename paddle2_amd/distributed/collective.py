@@ -20,6 +20,7 @@ import torch
 import torch.distributed as dist
 
 from ..framework.tensor import Tensor
+from . import comm_check as _cc
 
 _wrap = Tensor._wrap
 
@@ -272,6 +273,7 @@ def _all_reduce_torch(t: torch.Tensor, op=ReduceOp.SUM, group=None, sync_op=True
     g, pg = _pg(group)
     if _single(g):
         return _Task(None)
+    _cc.dynamic_check("all_reduce", g, t)
     top = _top(op, g.backend)
     if top is None:  # AVG on gloo
         w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg, async_op=not sync_op)
@@ -295,6 +297,7 @@ def broadcast(tensor, src=0, group=None, sync_op=True):
     g, pg = _pg(group)
     if _single(g):
         return _Task(None)
+    _cc.dynamic_check("broadcast", g, tensor._t)
     w = dist.broadcast(tensor._t, src=src, group=pg, async_op=not sync_op)
     return _Task(w)
 
@@ -340,6 +343,8 @@ def all_gather_into_tensor(out_tensor, in_tensor, group=None, sync_op=True):
     if _single(g):
         out_tensor._t.copy_(in_tensor._t.reshape(out_tensor._t.shape))
         return _Task(None)
+    _cc.static_check("all_gather_into_tensor", g, in_tensor._t, out_tensor._t)
+    _cc.dynamic_check("all_gather_into_tensor", g, in_tensor._t)
     w = dist.all_gather_into_tensor(out_tensor._t, in_tensor._t.contiguous(), group=pg, async_op=not sync_op)
     return _Task(w)
 
@@ -362,6 +367,8 @@ def reduce_scatter(tensor, tensor_list, op=ReduceOp.SUM, group=None, sync_op=Tru
         tensor._t.copy_(tensor_list[0]._t)
         return _Task(None)
     inp = torch.cat([x._t.reshape(-1) for x in tensor_list]) if isinstance(tensor_list, (list, tuple)) else tensor_list._t
+    _cc.static_check("reduce_scatter", g, inp, tensor._t)
+    _cc.dynamic_check("reduce_scatter", g, inp)
     top = _top(op, g.backend)
     avg = top is None
     w = dist.reduce_scatter_tensor(tensor._t, inp.contiguous(), op=dist.ReduceOp.SUM if avg else top, group=pg,

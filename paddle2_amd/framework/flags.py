@@ -56,6 +56,10 @@ def _init():
 
 
 _init()
+if _flags.get("FLAGS_check_nan_inf"):
+    from . import nan_inf as _ni  # noqa: E402
+
+    _ni._sync_from_flags()
 
 
 def set_flags(flags: dict):
@@ -83,6 +87,10 @@ def flag(name, default=None):
 
 
 def _on_change(key):
+    if key in ("FLAGS_check_nan_inf", "FLAGS_check_nan_inf_level"):
+        from . import nan_inf
+
+        nan_inf._sync_from_flags()
     if key == "FLAGS_cudnn_deterministic":
         import torch
 

@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from ...framework import dtype as _dt
+from ...framework import nan_inf as _nan_inf
 from ...framework.param import Parameter, ParamAttr, create_parameter
 from ...framework.tensor import Tensor
 
@@ -254,6 +255,8 @@ class Layer:
                 if r is not None:
                     args = r if isinstance(r, tuple) else (r,)
         out = self.forward(*args, **kwargs)
+        if _nan_inf.enabled:
+            _nan_inf.check_layer(self, out)
         if self._forward_post_hooks:
             for hook in list(self._forward_post_hooks.values()):
                 r = hook(self, args, out)
