@@ -63,3 +63,36 @@ def test_llama_is_causal():
         b = m(ids2)._t.float()
     assert torch.allclose(a[:, :t], b[:, :t], atol=1e-3), (a[:, :t] - b[:, :t]).abs().max()
     assert not torch.allclose(a[:, t:], b[:, t:], atol=1e-3)
+
+
+def test_group_sharded_stage3_single_gpu_matches_plain():
+    """The stage-3 path bench.py takes for N>1 (flat units, gather/release hooks, fp32 grad shards,
+    sharded native multi-tensor AdamW) must train exactly like the plain step on one GPU."""
+    import paddle2_amd as paddle
+    from paddle2_amd.distributed.sharding import group_sharded_parallel
+    from paddle2_amd.models import LlamaConfig, LlamaForCausalLM
+
+    paddle.set_device("gpu:0")
+    cfg = LlamaConfig.tiny(num_hidden_layers=2)
+
+    def run(shard):
+        paddle.seed(11)
+        m = LlamaForCausalLM(cfg)
+        o = paddle.optimizer.AdamW(1e-3, parameters=m.parameters(), weight_decay=0.1, multi_precision=True,
+                                   grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
+        if shard:
+            m, o, _ = group_sharded_parallel(m, o, "p_g_os")
+        g = torch.Generator(device="cuda").manual_seed(5)
+        out = []
+        for _ in range(4):
+            ids = paddle.Tensor._wrap(torch.randint(0, cfg.vocab_size, (2, 129), generator=g, device="cuda"))
+            loss = m(ids[:, :-1], labels=ids[:, 1:])
+            loss.backward()
+            o.step()
+            o.clear_grad()
+            out.append(float(loss))
+        return out
+
+    a, b = run(False), run(True)
+    for x, y in zip(a, b):
+        assert abs(x - y) < 2e-2 * max(1.0, abs(x)), (a, b)
