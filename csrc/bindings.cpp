@@ -33,6 +33,8 @@ int pd_unscale_mt(int, const void*, const long*, int, long, const float*, float*
 int pd_sqnorm_mt(int, const void*, const long*, int, long, float*, void*);
 int pd_scale_mt(int, const void*, const long*, int, long, const float*, void*);
 int pd_update_loss_scaling(const float*, float*, int*, int*, int, int, float, float, void*);
+int pd_softmax_mask_fwd(int, int, const void*, const void*, void*, long, int, int, int, void*);
+int pd_softmax_mask_bwd(int, const void*, const void*, void*, long, int, void*);
 int pd_ce_stats(int, const void*, const int64_t*, float*, float*, float*, long, long, long, void*);
 int pd_ce_bwd(int, const void*, const int64_t*, const float*, const float*, void*, long, long, long, long, int, void*);
 int pd_embed_fwd(int, const int64_t*, const void*, void*, long, int, long, long, void*);
@@ -142,6 +144,16 @@ PYBIND11_MODULE(_C, m) {
     check(pd_update_loss_scaling(P<const float*>(found_inf), P<float*>(scale), P<int*>(good), P<int*>(bad), incr_n,
                                  decr_n, incr_ratio, decr_ratio, P<void*>(st)),
           "update_loss_scaling");
+  });
+  m.def("softmax_mask_fwd", [](int dt, int causal, uintptr_t x, uintptr_t mask, uintptr_t y, long rows, int H, int Sq,
+                                int Sk, uintptr_t st) {
+    check(pd_softmax_mask_fwd(dt, causal, P<const void*>(x), P<const void*>(mask), P<void*>(y), rows, H, Sq, Sk,
+                              P<void*>(st)),
+          "softmax_mask_fwd");
+  });
+  m.def("softmax_mask_bwd", [](int dt, uintptr_t y, uintptr_t dy, uintptr_t dx, long rows, int Sk, uintptr_t st) {
+    check(pd_softmax_mask_bwd(dt, P<const void*>(y), P<const void*>(dy), P<void*>(dx), rows, Sk, P<void*>(st)),
+          "softmax_mask_bwd");
   });
   m.def("ce_stats", [](int dt, uintptr_t logits, uintptr_t labels, uintptr_t mx, uintptr_t se, uintptr_t tgt, long N,
                        long V, long start, uintptr_t st) {

@@ -168,6 +168,42 @@ def _ce_softmax(input, label, soft_label=False, use_softmax=True, numeric_stable
 
 
 # ----------------------------------------------------------------------------- optimizer / AMP kernels
+@register_op("fused_softmax_mask", native_kernel="softmax_mask_fwd")
+def _fused_softmax_mask(x, mask):
+    return _w(T.softmax_mask(_t(x), _t(mask), causal=False))
+
+
+@register_op("fused_softmax_mask_upper_triangle", native_kernel="softmax_mask_fwd")
+def _fused_softmax_mask_ut(x):
+    return _w(T.softmax_mask(_t(x), None, causal=True))
+
+
+@register_op("fused_linear_param_grad_add", inplace=True)
+def _fused_linear_param_grad_add(x, dout, dweight=None, dbias=None, multi_precision=True, has_bias=True):
+    """dW += x^T dy (fp32 main_grad when multi_precision), db += sum(dy); returns (dweight, dbias).
+    Reference: phi/kernels/fusion/gpu/fused_linear_param_grad_add_kernel.cu:282.  The GEMM accumulates in
+    place through hipBLASLt's beta=1 epilogue (addmm_), so no temporary [K, N] product is materialised."""
+    xt, dy = _t(x), _t(dout)
+    x2 = xt.reshape(-1, xt.shape[-1])
+    d2 = dy.reshape(-1, dy.shape[-1])
+    acc_dt = torch.float32 if multi_precision else dy.dtype
+    if dweight is None:
+        dw = torch.zeros(x2.shape[1], d2.shape[1], dtype=acc_dt, device=dy.device)
+        dweight = _w(dw)
+    dw = _t(dweight)
+    if dw.dtype == x2.dtype:
+        dw.addmm_(x2.t(), d2)
+    else:
+        dw.add_(torch.matmul(x2.t(), d2).to(dw.dtype))
+    if has_bias:
+        db_new = d2.sum(0, dtype=torch.float32).to(acc_dt)
+        if dbias is None:
+            dbias = _w(db_new)
+        else:
+            _t(dbias).add_(db_new.to(_t(dbias).dtype))
+    return dweight, dbias
+
+
 @register_op("squared_l2_norm", native_kernel="sqnorm_mt")
 def _sq_l2(x):
     """sum(x^2) as a 1-element fp32 tensor."""

@@ -410,6 +410,62 @@ def swiglu_linear(x, w):
     return swiglu(linear(x, w))
 
 
+# ============================================================================ fused masked softmax
+def _softmax_mask_reference(x, mask, causal):
+    xf = x.float()
+    if causal:
+        Sq, Sk = x.shape[-2], x.shape[-1]
+        keep = torch.ones(Sq, Sk, dtype=torch.bool, device=x.device).tril()
+        xf = xf.masked_fill(~keep, float("-inf"))
+    else:
+        xf = xf + mask.float()
+    return torch.softmax(xf, -1).to(x.dtype)
+
+
+class _SoftmaxMaskFn(torch.autograd.Function):
+    """softmax(x + mask) / causal softmax over [B, H, Sq, Sk] scores (csrc/kernels/softmax_mask.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, mask, causal):
+        B, H, Sq, Sk = x.shape
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        mc = None
+        if not causal:
+            mc = mask.to(x.dtype).expand(B, 1, Sq, Sk).contiguous()
+        N.native().softmax_mask_fwd(_DT[x.dtype], int(causal), xc.data_ptr(), 0 if mc is None else mc.data_ptr(),
+                                    y.data_ptr(), B * H * Sq, H, Sq, Sk, N.stream())
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dyc = dy.contiguous()
+        dx = torch.empty_like(y)
+        Sk = y.shape[-1]
+        N.native().softmax_mask_bwd(_DT[y.dtype], y.data_ptr(), dyc.data_ptr(), dx.data_ptr(), y.numel() // Sk, Sk,
+                                    N.stream())
+        return dx, None, None
+
+
+def softmax_mask(x, mask=None, causal=False):
+    """Fused attention-score softmax. ``x`` [B, H, Sq, Sk]; ``mask`` additive, broadcastable to [B, 1, Sq, Sk]
+    (ignored when ``causal``: column c > row r is masked and gets probability exactly 0).  Sk <= 8192."""
+    if x.dim() != 4:
+        raise ValueError(f"softmax_mask expects [B, H, Sq, Sk] scores, got {tuple(x.shape)}")
+    B, H, Sq, Sk = x.shape
+    if causal and Sq != Sk:
+        raise ValueError("softmax_mask_fuse_upper_triangle needs square scores (Sq == Sk)")
+    if not causal and mask is None:
+        raise ValueError("softmax_mask_fuse needs a mask")
+    if Sk > 8192:
+        raise ValueError(f"fused masked softmax supports key length <= 8192, got {Sk}")
+    if N.use_native(x) and x.dtype in _DT:
+        return _SoftmaxMaskFn.apply(x, mask, causal)
+    return _softmax_mask_reference(x, mask, causal)
+
+
 # ============================================================================ softmax cross entropy
 class _SCEFn(torch.autograd.Function):
     @staticmethod
