@@ -255,30 +255,46 @@ def fused_multi_transformer(*args, **kwargs):
 
 def fused_moe(x, gate_weight, ffn1_weight, ffn1_scale=None, ffn1_bias=None, ffn2_weight=None, ffn2_scale=None,
               ffn2_bias=None, quant_method="None", moe_topk=2, group_moe=False, norm_topk_prob=True):
-    """Top-k gated MoE FFN (reference: fusion/cutlass/fused_moe_kernel.cu) as grouped GEMMs."""
+    """Top-k gated MoE FFN (reference: fusion/cutlass/fused_moe_kernel.cu, which is NVIDIA-only there).
+
+    MI355X path: the N*k (token, expert) assignments are sorted by expert ONCE, so each expert's rows are a
+    contiguous slice of one permuted activation matrix; a single host read of the per-expert counts sizes
+    the slices (the old per-expert ``nonzero`` cost one device sync per expert).  Each expert then runs two
+    dense hipBLASLt GEMMs on its slice with the SwiGLU HIP kernel between them, and the weighted outputs are
+    scattered back with one ``index_add_``.  ``ffn1_weight`` [E, H, 2F] packs [gate | up]; ``ffn2_weight``
+    [E, F, H]."""
     t = x._t
     shp = t.shape
     t2 = t.reshape(-1, shp[-1])
+    n_tok = t2.shape[0]
     logits = t2.float() @ gate_weight._t.float()
     probs = torch.softmax(logits, -1)
     w, idx = torch.topk(probs, moe_topk, -1)
     if norm_topk_prob:
         w = w / w.sum(-1, keepdim=True)
-    out = torch.zeros_like(t2, dtype=torch.float32)
-    E = ffn1_weight._t.shape[0]
-    for e in range(E):
-        sel = (idx == e)
-        rows = sel.any(-1).nonzero().squeeze(-1)
-        if rows.numel() == 0:
+    w1, w2 = ffn1_weight._t, ffn2_weight._t
+    E = w1.shape[0]
+    flat_e = idx.reshape(-1)
+    order = torch.argsort(flat_e, stable=True)
+    tok = order // moe_topk
+    gate = w.reshape(-1)[order]
+    counts = torch.bincount(flat_e, minlength=E).tolist()
+    xs = t2.index_select(0, tok)
+    ys = torch.empty(xs.shape[0], w2.shape[-1], dtype=t.dtype, device=t.device)
+    start = 0
+    for e, c in enumerate(counts):
+        if c == 0:
             continue
-        h = t2[rows] @ ffn1_weight._t[e]
+        seg = xs[start:start + c]
+        h = seg @ w1[e]
         if ffn1_bias is not None:
             h = h + ffn1_bias._t[e]
-        a, g = h.chunk(2, -1)
-        h = torch.nn.functional.silu(a) * g
-        o = h @ ffn2_weight._t[e]
+        h = T.swiglu(h)
+        o = h @ w2[e]
         if ffn2_bias is not None:
             o = o + ffn2_bias._t[e]
-        we = (w * sel).sum(-1)[rows]
-        out.index_add_(0, rows, o.float() * we[:, None])
+        ys[start:start + c] = o
+        start += c
+    out = torch.zeros(n_tok, ys.shape[-1], dtype=torch.float32, device=t.device)
+    out.index_add_(0, tok, ys.float() * gate[:, None])
     return _wrap(out.to(t.dtype).reshape(shp))
