@@ -119,9 +119,11 @@ def fused_bias_act(x, bias=None, dequant_scales=None, shift=None, smooth=None, a
                    compute_dtype="default", quant_scale=-1, quant_round_type=0, quant_max_bound=0,
                    quant_min_bound=0):
     t = x._t if bias is None else x._t + bias._t
-    if act_method in ("swiglu", "geglu"):
+    if act_method == "swiglu":
+        return _wrap(T.swiglu(t))  # SwiGLU HIP kernel on the GPU (csrc/kernels/elementwise.hip)
+    if act_method == "geglu":
         a, b = t.chunk(2, -1)
-        act = torch.nn.functional.silu(a.float()) if act_method == "swiglu" else torch.nn.functional.gelu(a.float())
+        act = torch.nn.functional.gelu(a.float())
         return _wrap((act * b.float()).to(t.dtype))
     fn = {"gelu": torch.nn.functional.gelu, "relu": torch.relu, "silu": torch.nn.functional.silu,
           "swish": torch.nn.functional.silu, "identity": lambda v: v}[act_method]
