@@ -5,58 +5,83 @@ Metric (BASELINE.json): tokens/sec for the whole node, Llama-2-7B Fleet sharding
 1/2/4/8 MI355X.  Weak scaling: every rank trains ``--micro-batch`` sequences of ``--seq-len`` tokens
 per step, so global_batch = micro_batch * N.
 
-Launch:  python bench.py --gpus 1 --steps K --warmup W
+Launch:  python bench.py --gpus N --steps K --warmup W
+           (N > 1 without WORLD_SIZE: this process starts N ranks through the in-tree launcher
+            ``python -m paddle2_amd.distributed.launch`` — one process per GPU, RCCL — and exits with
+            their status; only global rank 0 prints the JSON line)
          python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
              --master-port P bench.py --gpus N --steps K --warmup W
 
-The timed region is exactly K full steps (forward + backward + sharding-3 grad reduce-scatter +
+Every N (including N = 1) runs the same code path: the model is wrapped by
+``group_sharded_parallel(level="p_g_os")`` (stage 3: flat per-layer units, all-gather prefetch,
+fp32 main-grad accumulation straight from the weight-gradient GEMMs, reduce-scatter, sharded fused
+AdamW).  The timed region is exactly K full steps (forward + backward + grad reduce-scatter +
 global-norm clip + fused AdamW with fp32 master weights), bracketed by barrier +
-torch.cuda.synchronize(); the reported time is the max over ranks.  Data: synthetic token ids
-(uniform over the 32000-token vocab), random-init weights of the exact Llama-2-7B architecture.
+torch.cuda.synchronize(); the reported time is the max over ranks.  Data: a fresh batch of synthetic
+token ids (uniform over the 32000-token vocab) every step, pre-generated on the device before the
+timed region; random-init weights of the exact Llama-2-7B architecture.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
+ROOT = os.path.dirname(os.path.abspath(__file__))
 
-def parse():
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--micro-batch", type=int, default=8,
-                    help="sequences per GPU per step (8 x 4096 tokens: 241 GB peak on one 288 GB MI355X)")
+                    help="sequences per GPU per step (8 x 4096 tokens fits one 288 GB MI355X)")
     ap.add_argument("--model", default="llama2-7b",
                     choices=["llama2-7b", "llama2-13b", "tiny", "gpt3-13b", "gpt3-6.7b", "gpt3-1.3b"])
     ap.add_argument("--fp8", action="store_true", help="GPT configs: fp8 (e4m3/e5m2 delayed scaling) linears")
     ap.add_argument("--layers", type=int, default=None, help="DEBUG ONLY: override layer count (invalid for the metric)")
-    ap.add_argument("--sharding-stage", type=int, default=3)
+    ap.add_argument("--sharding-stage", type=int, default=3, choices=[0, 1, 2, 3],
+                    help="0 = no sharding wrapper (DEBUG: not the metric's code path)")
     ap.add_argument("--recompute", action="store_true")
-    ap.add_argument("--shard-single", action="store_true",
-                    help="wrap with group_sharded_parallel even on 1 GPU (measures the sharding machinery overhead)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--gemm-autotune", default="auto", choices=["auto", "tune", "off"],
                     help="hipBLASLt solution cache (tuning/gemm_gfx950.csv): auto = use it if present")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _self_launch(args) -> int:
+    """Start args.gpus ranks (one per GPU) via the in-tree launcher; never exec (GPU not touched here)."""
+    log_dir = tempfile.mkdtemp(prefix="bench_launch_")
+    cmd = [sys.executable, "-m", "paddle2_amd.distributed.launch", "--nproc_per_node", str(args.gpus),
+           "--log_dir", log_dir, os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env, cwd=ROOT)
 
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(_self_launch(args))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"error: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+
     import torch
 
     import paddle2_amd as paddle
     from paddle2_amd.distributed import fleet
     from paddle2_amd.models import LlamaConfig, LlamaForCausalLM, llama_flops_per_token
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
 
     if args.gemm_autotune != "off" and torch.cuda.is_available():
         from paddle2_amd.incubate import autotune
@@ -67,7 +92,7 @@ def main():
     strategy = fleet.DistributedStrategy()
     strategy.hybrid_configs = {"dp_degree": 1, "mp_degree": 1, "pp_degree": 1, "sharding_degree": world}
     fleet.init(is_collective=True, strategy=strategy)
-    paddle.seed(1234 + rank)
+    paddle.seed(1234)  # same init on every rank (stage 3 shards one replica)
 
     is_gpt = args.model.startswith("gpt3")
     if is_gpt:
@@ -92,7 +117,7 @@ def main():
                                  parameters=model.parameters(), weight_decay=0.1,
                                  apply_decay_param_fun=lambda n: n in decay,
                                  grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0), multi_precision=True)
-    if world > 1 or args.shard_single:
+    if args.sharding_stage > 0:
         from paddle2_amd.distributed.sharding import group_sharded_parallel
 
         level = {1: "os", 2: "os_g", 3: "p_g_os"}[args.sharding_stage]
@@ -101,19 +126,21 @@ def main():
 
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     b, s = args.micro_batch, args.seq_len
-    gen = torch.Generator(device=dev).manual_seed(rank)
-    ids = paddle.Tensor._wrap(torch.randint(0, cfg.vocab_size, (b, s + 1), generator=gen, device=dev))
-    inputs, labels = ids[:, :-1], ids[:, 1:]
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    # a fresh batch per step (pre-generated, outside the timed region); 8 x 4097 int64 = 262 KB each
+    batches = [torch.randint(0, cfg.vocab_size, (b, s + 1), generator=gen, device=dev)
+               for _ in range(args.warmup + args.steps)]
 
-    def step():
-        loss = model(inputs, labels=labels)
+    def step(i):
+        ids = paddle.Tensor._wrap(batches[i])
+        loss = model(ids[:, :-1], labels=ids[:, 1:])
         loss.backward()
         opt.step()
         opt.clear_grad()
         return loss
 
-    for _ in range(args.warmup):
-        loss = step()
+    for i in range(args.warmup):
+        loss = step(i)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     from paddle2_amd.distributed import collective as C
@@ -123,8 +150,8 @@ def main():
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
+    for i in range(args.steps):
+        loss = step(args.warmup + i)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     if world > 1:
@@ -144,6 +171,7 @@ def main():
     fpt = gpt_flops_per_token(cfg, s) if is_gpt else llama_flops_per_token(cfg, s)
     mfu = tps / world * fpt / 2.5e15
     if rank == 0:
+        par = f"sharding{args.sharding_stage}x{world}" if args.sharding_stage > 0 else f"single(no-sharding,debug)x{world}"
         out = {
             "metric": ("tokens/sec (whole node) Llama-2-7B Fleet sharding-3 bf16" if args.model == "llama2-7b"
                        else f"tokens/sec (whole node) {args.model} {'fp8' if args.fp8 else 'bf16'}"),
@@ -157,12 +185,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp8(e4m3/e5m2)+bf16" if (is_gpt and args.fp8) else "bf16",
-            "data": "synthetic (uniform random token ids), random-init weights",
+            "data": "synthetic (fresh uniform random token ids per step), random-init weights",
             "config": {"model": args.model if not args.layers else f"{args.model}-L{args.layers}(debug)",
                        "global_batch": b * world, "seq_len": s, "micro_batch_per_gpu": b,
-                       "parallelism": (f"sharding{args.sharding_stage}x{world}" if world > 1 or args.shard_single
-                                       else "single"),
-                       "layers": cfg.num_hidden_layers},
+                       "parallelism": par, "layers": cfg.num_hidden_layers},
             "mfu_vs_2.5PF_dense": round(mfu, 4),
             "final_loss": round(final_loss, 4),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if torch.cuda.is_available() else None,

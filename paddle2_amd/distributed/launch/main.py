@@ -154,7 +154,7 @@ def _tee(src, f):
 class Pod:
     def __init__(self, args, cmd, envs):
         self.args, self.cmd, self.envs = args, cmd, envs
-        self.procs, self.logs = [], []
+        self.procs, self.logs, self.tees = [], [], []
 
     def start(self):
         os.makedirs(self.args.log_dir, exist_ok=True)
@@ -165,7 +165,9 @@ class Pod:
             if env["RANK"] == "0":
                 # global rank 0: tee to the console and its log file
                 p = subprocess.Popen(self.cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
-                threading.Thread(target=_tee, args=(p.stdout, f), daemon=True).start()
+                t = threading.Thread(target=_tee, args=(p.stdout, f), daemon=True)
+                t.start()
+                self.tees.append(t)
             else:
                 p = subprocess.Popen(self.cmd, env=env, stdout=f, stderr=subprocess.STDOUT)
             self.procs.append(p)
@@ -190,6 +192,8 @@ class Pod:
                 time.sleep(0.1)
             if p.poll() is None:
                 p.kill()
+        for t in self.tees:  # rank 0's last console lines (e.g. a benchmark's JSON) must reach stdout
+            t.join(timeout=grace)
         for f in self.logs:
             f.close()
 

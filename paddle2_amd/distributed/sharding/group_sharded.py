@@ -74,6 +74,19 @@ def _find_units(model: Layer):
     return units, rest
 
 
+def _excluded_params(model, exclude_layer):
+    """ids of the parameters of every sublayer named in ``exclude_layer`` (class names or id(layer))."""
+    if not exclude_layer:
+        return set()
+    names = {e for e in exclude_layer if isinstance(e, str)}
+    ids = {e for e in exclude_layer if isinstance(e, int)}
+    out = set()
+    for _, sub in model.named_sublayers(include_self=True):
+        if type(sub).__name__ in names or id(sub) in ids:
+            out.update(id(p) for p in sub.parameters())
+    return out
+
+
 class _Unit:
     def __init__(self, idx, layer, params, group, stage, decay_fn, lr_ratio_fn):
         self.idx = idx
@@ -108,9 +121,15 @@ class _Unit:
         self.rs_work = None
         self.rs_buf = None
         self.flat_grad = None
-        self.ready = 0
+        self.written = set()
+        self.flat32 = None
+        self.rs_add = False
+        self.model = None
         self.n_trainable = sum(1 for p in self.params if not p.stop_gradient)
         self.bw_gathered = False
+        for i, p in enumerate(self.params):
+            if not p.stop_gradient and p._t.dim() == 2:
+                p._t._p2_gt = (self, i)  # weight-gradient GEMMs write straight into the fp32 target
         # optimizer pieces: (param, shard offset, length) for every param overlapping my slice
         self.pieces = []
         for p, o, n in zip(self.params, self.offsets, self.numels):
@@ -164,55 +183,85 @@ class _Unit:
         self.full = None
 
     # ------------------------------------------------------------ gradients
-    def on_param_grad(self):
-        self.ready += 1
-        if self.ready == self.n_trainable:
+    # Every trainable parameter's gradient lands ONCE per backward in an fp32 target: a view of the
+    # owned grad shard (N == 1: the shard is the whole flat unit) or of a per-backward flat fp32 unit
+    # buffer (N > 1) that one reduce_scatter(SUM) then folds into the owned shard.  Linear weights are
+    # written directly by their weight-gradient GEMM (fp32 accumulate, ops.torch_ops._main_grad_accumulate);
+    # the rest (norm weights, embeddings) arrive through autograd and are copied in by the grad hook.
+    # The same SUM + fp32 1/N scale runs on RCCL and gloo (the scale is folded into the optimizer).
+    def grad_target(self, i):
+        """-> (fp32 view of param i's gradient slot, beta): beta 0 = overwrite, 1 = accumulate."""
+        o, n, shp = self.offsets[i], self.numels[i], self.shapes[i]
+        if self.N == 1:
+            buf = self.grad_shard
+            beta = 0 if (self.grad_clean and i not in self.written) else 1
+        else:
+            if self.flat32 is None:
+                self.flat32 = torch.empty(self.padded, dtype=torch.float32, device=self.device)
+            buf = self.flat32
+            beta = 0 if i not in self.written else 1
+        return buf[o:o + n].view(shp), beta
+
+    def param_grad_done(self, i):
+        self.written.add(i)
+        if self.model is not None:
+            self.model._queue_cb()
+        if len(self.written) == self.n_trainable:
             self.reduce_grads()
 
-    def _accumulate(self, g):
-        """grad_shard (fp32) += g, or = g when the shard was lazily cleared (no zero-fill pass)."""
-        if self.grad_clean:
-            self.grad_shard.copy_(g)
-            self.grad_clean = False
+    def on_param_grad(self, i):
+        """autograd-path gradient (p.grad) -> fp32 target, then drop p.grad."""
+        p = self.params[i]
+        g = p._t.grad
+        if g is None:
+            return
+        view, beta = self.grad_target(i)
+        if beta == 0:
+            view.copy_(g.reshape(view.shape))
         else:
-            self.grad_shard.add_(g)
+            view.add_(g.reshape(view.shape))
+        p._t.grad = None
+        self.param_grad_done(i)
+
+    def _zero_unwritten(self, buf):
+        for i, (o, n) in enumerate(zip(self.offsets, self.numels)):
+            if i not in self.written:
+                buf[o:o + n].zero_()
+        if self.padded > self.total:
+            buf[self.total:].zero_()
 
     def reduce_grads(self):
-        # one flat buffer per unit; only the gaps (missing grads, padding tail) are zero-filled
-        flat = torch.empty(self.padded, dtype=self.dtype, device=self.device)
-        if self.padded > self.total:
-            flat[self.total:].zero_()
-        for p, o, n in zip(self.params, self.offsets, self.numels):
-            g = p._t.grad
-            if g is not None:
-                flat[o:o + n].copy_(g.reshape(-1))
-                p._t.grad = None
-            else:
-                flat[o:o + n].zero_()
         if self.N == 1:
-            self._accumulate(flat[: self.S])
-            self.flat_grad = None
+            if self.grad_clean:
+                self._zero_unwritten(self.grad_shard)
+                self.grad_clean = False
         else:
-            out = torch.empty(self.S, dtype=self.dtype, device=self.device)
-            op = dist.ReduceOp.AVG if self.group.backend == "nccl" else dist.ReduceOp.SUM
-            self.rs_work = dist.reduce_scatter_tensor(out, flat, op=op, group=self.group.pg, async_op=True)
+            if self.flat32 is None:
+                self.flat32 = torch.empty(self.padded, dtype=torch.float32, device=self.device)
+            self._zero_unwritten(self.flat32)
+            if self.grad_clean:
+                out, self.rs_add = self.grad_shard, False
+            else:
+                out, self.rs_add = torch.empty(self.S, dtype=torch.float32, device=self.device), True
+            self.rs_work = dist.reduce_scatter_tensor(out, self.flat32, op=dist.ReduceOp.SUM, group=self.group.pg,
+                                                      async_op=True)
             self.rs_buf = out
-            self.flat_grad = flat  # keep alive until the collective completes
+            self.flat_grad = self.flat32  # keep alive until the collective completes
+            self.flat32 = None
+            self.grad_clean = False
+        self.written = set()
         self.release()
 
     def finish_grads(self):
-        if self.ready < self.n_trainable and self.ready > 0:
+        if self.written:
             self.reduce_grads()
         if self.rs_work is not None:
             self.rs_work.wait()
-            g = self.rs_buf
-            if self.group.backend != "nccl":
-                g = g.float().div_(self.N)
-            self._accumulate(g)
+            if self.rs_add:
+                self.grad_shard.add_(self.rs_buf)
             self.rs_work = None
             self.rs_buf = None
             self.flat_grad = None
-        self.ready = 0
         self.bw_gathered = False
 
     # ------------------------------------------------------------ after the optimizer
@@ -229,7 +278,7 @@ class _Unit:
 class GroupShardedModel(Layer):
     """Wraps a Layer; owns the units and the forward/backward gather/release hooks."""
 
-    def __init__(self, layer, group, stage, optimizer, prefetch=True):
+    def __init__(self, layer, group, stage, optimizer, prefetch=True, exclude_layer=None):
         super().__init__()
         self._layer = layer
         self._group = group
@@ -237,14 +286,21 @@ class GroupShardedModel(Layer):
         self._prefetch = prefetch
         decay_fn = getattr(optimizer, "_decay_of", lambda p: 0.0)
         lr_fn = getattr(optimizer, "_lr_ratio_of", lambda p: 1.0)
+        excluded = _excluded_params(layer, exclude_layer) if stage == 3 else set()
         unit_layers, rest = _find_units(layer)
         self._units = []
         for i, l in enumerate(unit_layers):
-            ps = l.parameters()
+            ps = [p for p in l.parameters() if id(p) not in excluded]
             if ps:
                 self._units.append(_Unit(len(self._units), l, ps, group, stage, decay_fn, lr_fn))
+        rest = [p for p in rest if id(p) not in excluded]
         if rest:
             self._units.append(_Unit(len(self._units), None, rest, group, stage, decay_fn, lr_fn))
+        if excluded:
+            # exclude_layer (group_sharded_stage3.py:98): those parameters stay whole on every rank; their
+            # gradients and optimizer state are still reduce-scattered / sharded (one replicated unit)
+            ps = [p for p in layer.parameters() if id(p) in excluded]
+            self._units.append(_Unit(len(self._units), None, ps, group, 2, decay_fn, lr_fn))
         self._order = []       # unit call order in forward
         self._by_layer = {id(u.layer): u for u in self._units if u.layer is not None}
         self._cb_queued = False
@@ -253,9 +309,10 @@ class GroupShardedModel(Layer):
             if u.layer is not None:
                 self._hooks.append(u.layer.register_forward_pre_hook(self._make_pre(u)))
                 self._hooks.append(u.layer.register_forward_post_hook(self._make_post(u)))
-            for p in u.params:
+            u.model = self
+            for i, p in enumerate(u.params):
                 if not p.stop_gradient:
-                    self._hooks.append(p._t.register_post_accumulate_grad_hook(self._make_grad_hook(u)))
+                    self._hooks.append(p._t.register_post_accumulate_grad_hook(self._make_grad_hook(u, i)))
 
     # ------------------------------------------------------------ hooks
     def _make_pre(self, u):
@@ -315,12 +372,10 @@ class GroupShardedModel(Layer):
 
         return hook
 
-    def _make_grad_hook(self, u):
+    def _make_grad_hook(self, u, i):
         def hook(t):
             self._queue_cb()
-            if self._stage == 3 and u.full is None:
-                u.wait()
-            u.on_param_grad()
+            u.on_param_grad(i)
 
         return hook
 
@@ -378,14 +433,25 @@ class GroupShardedModel(Layer):
 
 
 class GroupShardedOptimizer:
-    """Steps the owned slices with the fused multi-tensor AdamW (or the wrapped optimizer's math)."""
+    """Steps the owned slices with the fused multi-tensor AdamW (or the wrapped optimizer's math).
 
-    def __init__(self, optimizer, model: GroupShardedModel):
+    Optimizer state per unit: fp32 moments (and the fp32 master of 16-bit params) for the owned slice
+    only, as flat shard-sized buffers the per-parameter pieces view.  ``offload=True``
+    (group_sharded_stage3.py:98 ``offload``): master weights and moments live in pinned host memory and
+    the AdamW update of the owned slice runs on the CPU; only the fp32 grad shard goes down and the
+    updated 16-bit param shard comes back up each step.
+
+    ``state_dict()`` is the plain optimizer's per-parameter layout (``{name}_moment1_0``,
+    ``{name}_moment2_0``, ``{name}_beta{1,2}_pow_acc_0``, ``master_weights``, ``LR_Scheduler``) with
+    full, unsharded tensors, so a checkpoint reloads at any sharding degree and into an unsharded run
+    (and vice versa)."""
+
+    def __init__(self, optimizer, model: GroupShardedModel, offload=False):
         self._inner = optimizer
         self._model = model
+        self._offload = offload
         self._table = None
-        self._m = {}
-        self._v = {}
+        self._state = {}   # unit idx -> (m, v, master)  flat, shard-sized
 
     @property
     def _parameter_list(self):
@@ -404,6 +470,24 @@ class GroupShardedOptimizer:
                 out.append((u, p, o, n, dec, lrr))
         return out
 
+    def _unit_state(self, u):
+        st = self._state.get(u.idx)
+        if st is None:
+            if self._offload:
+                mk = lambda: torch.zeros(u.S, dtype=torch.float32).pin_memory() if torch.cuda.is_available() \
+                    else torch.zeros(u.S, dtype=torch.float32)  # noqa: E731
+                m, v = mk(), mk()
+                master = mk()
+                master.copy_(u.shard.float().cpu())
+                u.master = None  # the device master is not kept when offloading
+            else:
+                m = torch.zeros(u.S, dtype=torch.float32, device=u.device)
+                v = torch.zeros(u.S, dtype=torch.float32, device=u.device)
+                master = u.master
+            st = (m, v, master)
+            self._state[u.idx] = st
+        return st
+
     def _materialize_grads(self):
         for u in self._model._units:
             if u.grad_clean:      # no gradient reached this unit since clear_grad: it is zero
@@ -419,6 +503,49 @@ class GroupShardedOptimizer:
             dist.all_reduce(sq, group=g.pg)
         return sq
 
+    def _build_table(self):
+        from ...ops import _native as N
+
+        params, grads, ms, vs, masters, lrrs, decs = [], [], [], [], [], [], []
+        for (u, p, o, n, dec, lrr) in self._pieces():
+            m, v, master = self._unit_state(u)
+            params.append(u.shard[o:o + n])
+            grads.append(u.grad_shard[o:o + n])
+            ms.append(m[o:o + n])
+            vs.append(v[o:o + n])
+            masters.append(None if master is None else master[o:o + n])
+            lrrs.append(lrr)
+            decs.append(dec)
+        dev = self._model._units[0].device
+        if self._offload:
+            return ("cpu", None)
+        use_native = dev.type == "cuda" and N.available() and all(
+            t.data_ptr() % 16 == 0 for t in params + grads + [m for m in masters if m is not None])
+        if use_native and params:
+            from ...optimizer.multi_tensor import MultiTensorTable
+
+            groups = {}
+            for i in range(len(params)):
+                groups.setdefault((params[i].dtype, masters[i] is not None), []).append(i)
+            tabs = []
+            for _, idx in groups.items():
+                tabs.append(MultiTensorTable([params[i] for i in idx], [grads[i] for i in idx],
+                                             [ms[i] for i in idx], [vs[i] for i in idx],
+                                             [masters[i] for i in idx] if masters[idx[0]] is not None else None,
+                                             [lrrs[i] for i in idx], [decs[i] for i in idx]))
+            return ("native", tabs)
+        return ("ref", list(zip(params, grads, ms, vs, masters, lrrs, decs)))
+
+    @staticmethod
+    def _adamw_ref(p, g, m, v, mw, lr_t, dec, b1, b2, eps, bc1, bc2):
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        tgt = mw if mw is not None else p
+        upd = tgt.float() * (1 - lr_t * dec) - (lr_t / bc1) * m / (v.sqrt() / math.sqrt(bc2) + eps)
+        tgt.copy_(upd.to(tgt.dtype))
+        if mw is not None:
+            p.copy_(mw)
+
     @torch.no_grad()
     def step(self):
         inner = self._inner
@@ -426,67 +553,47 @@ class GroupShardedOptimizer:
         self._materialize_grads()
         clip = inner._grad_clip
         coef = None
+        nr = self._model._group.nranks
+        inv = 1.0 / nr  # grads were reduce-scattered with SUM: the mean's 1/N is folded in here
         if clip is not None and hasattr(clip, "clip_norm"):
-            norm = torch.sqrt(self._global_sq_norm())
-            coef = torch.clamp(clip.clip_norm / torch.clamp(norm, min=1e-6), max=1.0).float().reshape(1)
+            norm = torch.sqrt(self._global_sq_norm()) * inv
+            coef = (torch.clamp(clip.clip_norm / torch.clamp(norm, min=1e-6), max=1.0) * inv).float().reshape(1)
+        elif nr > 1:
+            coef = torch.full((1,), inv, dtype=torch.float32, device=self._model._units[0].device)
         lr = inner.get_lr()
         b1, b2 = getattr(inner, "_beta1", 0.9), getattr(inner, "_beta2", 0.999)
         eps = getattr(inner, "_epsilon", 1e-8)
         bc1, bc2 = 1 - b1 ** inner._step, 1 - b2 ** inner._step
-        pieces = self._pieces()
-        from ...ops import _native as N
-
-        dev = self._model._units[0].device
         if self._table is None:
-            params, grads, ms, vs, masters, lrrs, decs = [], [], [], [], [], [], []
-            for (u, p, o, n, dec, lrr) in pieces:
-                params.append(u.shard[o:o + n])
-                grads.append(u.grad_shard[o:o + n])
-                key = (u.idx, o)
-                self._m[key] = torch.zeros(n, dtype=torch.float32, device=dev)
-                self._v[key] = torch.zeros(n, dtype=torch.float32, device=dev)
-                ms.append(self._m[key])
-                vs.append(self._v[key])
-                masters.append(None if u.master is None else u.master[o:o + n])
-                lrrs.append(lrr)
-                decs.append(dec)
-            use_native = dev.type == "cuda" and N.available() and all(
-                t.data_ptr() % 16 == 0 for t in params + grads + [m for m in masters if m is not None])
-            if use_native and params:
-                from ...optimizer.multi_tensor import MultiTensorTable
-
-                groups = {}
-                for i in range(len(params)):
-                    groups.setdefault((params[i].dtype, masters[i] is not None), []).append(i)
-                tabs = []
-                for _, idx in groups.items():
-                    tabs.append(MultiTensorTable([params[i] for i in idx], [grads[i] for i in idx],
-                                                 [ms[i] for i in idx], [vs[i] for i in idx],
-                                                 [masters[i] for i in idx] if masters[idx[0]] is not None else None,
-                                                 [lrrs[i] for i in idx], [decs[i] for i in idx]))
-                self._table = ("native", tabs)
-            else:
-                self._table = ("ref", list(zip(params, grads, ms, vs, masters, lrrs, decs)))
+            self._table = self._build_table()
         kind, tabs = self._table
         if kind == "native":
             # clip coefficient folded into the fused AdamW pass (device scalar, no extra grad pass)
             for t in tabs:
                 t.adamw(lr, b1, b2, eps, bc1, bc2, getattr(inner, "_found_inf", None), coef)
+        elif kind == "cpu":
+            self._step_offload(lr, b1, b2, eps, bc1, bc2, coef)
         else:
             if coef is not None:
                 for u in self._model._units:
                     u.grad_shard.mul_(coef)
             for (p, g, m, v, mw, lrr, dec) in tabs:
-                m.mul_(b1).add_(g, alpha=1 - b1)
-                v.mul_(b2).addcmul_(g, g, value=1 - b2)
-                tgt = mw if mw is not None else p
-                lr_t = lr * lrr
-                upd = tgt.float() * (1 - lr_t * dec) - (lr_t / bc1) * m / (v.sqrt() / math.sqrt(bc2) + eps)
-                tgt.copy_(upd.to(tgt.dtype))
-                if mw is not None:
-                    p.copy_(mw)
+                self._adamw_ref(p, g, m, v, mw, lr * lrr, dec, b1, b2, eps, bc1, bc2)
         for u in self._model._units:
             u.refresh_params()
+
+    def _step_offload(self, lr, b1, b2, eps, bc1, bc2, coef):
+        """Owned-slice AdamW on the host: grad shard D2H, update the pinned fp32 master, 16-bit shard H2D."""
+        c = None if coef is None else float(coef.reshape(-1)[0])
+        for u in self._model._units:
+            m, v, master = self._unit_state(u)
+            g = u.grad_shard.to("cpu", non_blocking=False)
+            if c is not None:
+                g.mul_(c)
+            for (p, o, n, dec, lrr) in u.pieces:
+                self._adamw_ref(master[o:o + n], g[o:o + n], m[o:o + n], v[o:o + n], None, lr * lrr, dec,
+                                b1, b2, eps, bc1, bc2)
+            u.shard.copy_(master.to(u.shard.dtype), non_blocking=True)
 
     def clear_grad(self, set_to_zero=True):
         for u in self._model._units:
@@ -494,28 +601,77 @@ class GroupShardedOptimizer:
                 u.grad_clean = True  # lazy zero: the next reduce overwrites the shard
             else:
                 u.grad_shard.zero_()
+            u.written = set()
             for p in u.params:
                 p._t.grad = None
 
     clear_gradients = clear_grad
 
+    # ------------------------------------------------------------ checkpoint (any sharding degree)
+    def _gather_full(self, u, shard):
+        """owned fp32 slice -> full padded flat (host), one all_gather per unit."""
+        src = shard.to(u.device)
+        if u.N == 1:
+            return src.detach().cpu().clone()
+        full = torch.empty(u.padded, dtype=src.dtype, device=u.device)
+        dist.all_gather_into_tensor(full, src.contiguous(), group=u.group.pg)
+        return full.cpu()
+
     def state_dict(self):
-        sd = {"step": self._inner._step}
-        for k in self._m:
-            sd[f"unit{k[0]}_off{k[1]}_moment1"] = Tensor._wrap(self._m[k])
-            sd[f"unit{k[0]}_off{k[1]}_moment2"] = Tensor._wrap(self._v[k])
+        from ...optimizer.lr import LRScheduler
+
+        inner = self._inner
+        sd = {}
+        masters = {}
         for u in self._model._units:
-            if u.master is not None:
-                sd[f"unit{u.idx}_master"] = Tensor._wrap(u.master)
+            m, v, master = self._unit_state(u)
+            fm, fv = self._gather_full(u, m), self._gather_full(u, v)
+            fmw = self._gather_full(u, master) if master is not None else None
+            for p, o, n, shp in zip(u.params, u.offsets, u.numels, u.shapes):
+                if p.stop_gradient:
+                    continue
+                sd[f"{p.name}_moment1_0"] = Tensor._wrap(fm[o:o + n].view(shp).clone())
+                sd[f"{p.name}_moment2_0"] = Tensor._wrap(fv[o:o + n].view(shp).clone())
+                sd[f"{p.name}_beta1_pow_acc_0"] = Tensor._wrap(torch.tensor([getattr(inner, "_beta1", 0.9) ** inner._step]))
+                sd[f"{p.name}_beta2_pow_acc_0"] = Tensor._wrap(torch.tensor([getattr(inner, "_beta2", 0.999) ** inner._step]))
+                if fmw is not None:
+                    masters[p.name] = Tensor._wrap(fmw[o:o + n].view(shp).clone())
+        if masters:
+            sd["master_weights"] = masters
+        if isinstance(inner._learning_rate, LRScheduler):
+            sd["LR_Scheduler"] = inner._learning_rate.state_dict()
         return sd
 
     def set_state_dict(self, sd):
-        self._inner._step = int(sd.get("step", 0))
-        for k in list(self._m):
-            a = sd.get(f"unit{k[0]}_off{k[1]}_moment1")
-            if a is not None:
-                self._m[k].copy_(a._t)
-                self._v[k].copy_(sd[f"unit{k[0]}_off{k[1]}_moment2"]._t)
+        from ...optimizer.lr import LRScheduler
+
+        inner = self._inner
+        b1 = getattr(inner, "_beta1", 0.9)
+        masters = sd.get("master_weights", {})
+        for u in self._model._units:
+            m, v, master = self._unit_state(u)
+            lo = u.rank * u.S
+            for (p, o, n, dec, lrr) in u.pieces:
+                pi = next(i for i, q in enumerate(u.params) if q is p)
+                po = o + lo - u.offsets[pi]  # offset of this piece inside the parameter
+                for key, dst in ((f"{p.name}_moment1_0", m), (f"{p.name}_moment2_0", v)):
+                    t = sd.get(key)
+                    if t is not None:
+                        tt = t._t if isinstance(t, Tensor) else torch.as_tensor(t)
+                        dst[o:o + n].copy_(tt.reshape(-1)[po:po + n].to(dst.device, torch.float32))
+                mw = masters.get(p.name)
+                if mw is not None and master is not None:
+                    tt = mw._t if isinstance(mw, Tensor) else torch.as_tensor(mw)
+                    master[o:o + n].copy_(tt.reshape(-1)[po:po + n].to(master.device, torch.float32))
+                bp = sd.get(f"{p.name}_beta1_pow_acc_0")
+                if bp is not None:
+                    val = float((bp._t if isinstance(bp, Tensor) else torch.as_tensor(bp)).reshape(-1)[0])
+                    if 0 < val < 1:
+                        inner._step = int(round(math.log(val) / math.log(b1)))
+        if "step" in sd:
+            inner._step = int(sd["step"])
+        if "LR_Scheduler" in sd and isinstance(inner._learning_rate, LRScheduler):
+            inner._learning_rate.set_state_dict(sd["LR_Scheduler"])
 
     def minimize(self, loss, *a, **k):
         self.step()
@@ -524,15 +680,17 @@ class GroupShardedOptimizer:
 def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, offload=False, sync_buffers=False,
                            buffer_max_size=2 ** 23, segment_size=2 ** 20, sync_comm=False, dp_group=None,
                            exclude_layer=None):
-    """level: 'os' (stage 1), 'os_g' (stage 2), 'p_g_os' (stage 3)."""
+    """level: 'os' (stage 1), 'os_g' (stage 2), 'p_g_os' (stage 3).  ``offload``: optimizer state and
+    update on the host (pinned memory).  ``exclude_layer``: class names / id(layer) whose parameters stay
+    unsharded under stage 3 (reference python/paddle/distributed/sharding/group_sharded.py:50)."""
     stage = {"os": 1, "os_g": 2, "p_g_os": 3}[level]
     g = group or C._get_default_group()
     if g.nranks > 1:
         from ..parallel import sync_params_buffers
 
         sync_params_buffers(model, g)
-    sm = GroupShardedModel(model, g, stage, optimizer, prefetch=not sync_comm)
-    so = GroupShardedOptimizer(optimizer, sm)
+    sm = GroupShardedModel(model, g, stage, optimizer, prefetch=not sync_comm, exclude_layer=exclude_layer)
+    so = GroupShardedOptimizer(optimizer, sm, offload=offload)
     return sm, so, scaler
 
 

@@ -17,7 +17,8 @@ _wrap = Tensor._wrap
 def linear(x, weight, bias=None, name=None):
     t = x._t
     w = weight._t
-    if t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and w.dim() == 2:
+    if (t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and w.dim() == 2) or \
+            getattr(w, "_p2_gt", None) is not None:  # weight grad -> fp32 main-grad buffer
         from ...ops import torch_ops as T
 
         return _wrap(T.linear(t, w, None if bias is None else bias._t))

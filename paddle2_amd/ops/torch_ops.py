@@ -337,6 +337,7 @@ class _LinearFn(torch.autograd.Function):
             y += b
         ctx.save_for_backward(x2, w)
         ctx.meta = (x.shape, dw_t, b is not None)
+        ctx.gt = getattr(w, "_p2_gt", None)
         return y.view(*x.shape[:-1], Nn)
 
     @staticmethod
@@ -351,7 +352,9 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.matmul(dy2, w.t()).view(xshape)
         if ctx.needs_input_grad[1]:
-            if dw_t:
+            if ctx.gt is not None:
+                _main_grad_accumulate(ctx.gt, x2, dy2)
+            elif dw_t:
                 dw = torch.matmul(transpose2d(x2), transpose2d(dy2).t())
             else:
                 dw = torch.matmul(x2.t(), dy2)
@@ -360,11 +363,33 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
+def wgrad_accumulate(out, x2, dy2, beta):
+    """out[K, N] (fp32 main grad) = x2^T @ dy2 + beta * out, with the product accumulated in fp32 — never
+    rounded to the activation dtype first (reference fused_linear_param_grad_add_kernel.cu:51, use_addto)."""
+    if out.device.type == "cuda":
+        torch.addmm(out, x2.t(), dy2, beta=float(beta), out_dtype=out.dtype, out=out)
+        return out
+    if beta == 0:
+        out.zero_()
+    out.addmm_(x2.t().to(out.dtype), dy2.to(out.dtype))
+    return out
+
+
+def _main_grad_accumulate(gt, x2, dy2):
+    """Weight gradient straight into the owner's fp32 main-grad buffer (group-sharded unit / main_grad):
+    ``gt`` = (owner, index) with owner.grad_target(index) -> (fp32 view, beta) and owner.param_grad_done."""
+    owner, idx = gt
+    view, beta = owner.grad_target(idx)
+    wgrad_accumulate(view, x2, dy2, beta)
+    owner.param_grad_done(idx)
+
+
 def linear(x, w, b=None):
-    """Paddle-layout linear on bf16/fp16 GPU tensors through the layout-aware GEMM node; plain matmul
-    otherwise."""
+    """Paddle-layout linear on bf16/fp16 GPU tensors through the layout-aware GEMM node (and on any device
+    when the weight's gradient goes to an fp32 main-grad buffer); plain matmul otherwise."""
     if (x.device.type == "cuda" and x.dtype in (torch.bfloat16, torch.float16) and w.dtype == x.dtype
-            and w.dim() == 2 and x.shape[-1] == w.shape[0] and N.use_native(x)):
+            and w.dim() == 2 and x.shape[-1] == w.shape[0] and N.use_native(x)) or \
+            (getattr(w, "_p2_gt", None) is not None and w.dim() == 2 and x.shape[-1] == w.shape[0]):
         return _LinearFn.apply(x, w, b)
     y = torch.matmul(x, w)
     return y + b if b is not None else y
@@ -384,6 +409,7 @@ class _SwiGLULinearFn(torch.autograd.Function):
         a = swiglu(gu)
         ctx.save_for_backward(x2, w, gu)
         ctx.xshape = x.shape
+        ctx.gt = getattr(w, "_p2_gt", None)
         return a.view(*x.shape[:-1], H2 // 2)
 
     @staticmethod
@@ -392,11 +418,21 @@ class _SwiGLULinearFn(torch.autograd.Function):
         M, H2 = gu.shape
         da2 = da.reshape(M, H2 // 2).contiguous()
         dgu = torch.empty_like(gu)
-        dguT = torch.empty(H2, M, dtype=gu.dtype, device=gu.device)
-        N.native().swiglu_bwd_t(gu.data_ptr(), da2.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), M, H2 // 2, H2,
-                                N.stream())
+        if ctx.gt is not None:  # main-grad GEMM reads dgu in place: no dY^T image needed
+            H, es = H2 // 2, gu.element_size()
+            N.native().swiglu_bwd(_DT[gu.dtype], gu.data_ptr(), gu.data_ptr() + H * es, da2.data_ptr(),
+                                  dgu.data_ptr(), dgu.data_ptr() + H * es, M, H, H2, H2, H2, H2, N.stream())
+        else:
+            dguT = torch.empty(H2, M, dtype=gu.dtype, device=gu.device)
+            N.native().swiglu_bwd_t(gu.data_ptr(), da2.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), M, H2 // 2, H2,
+                                    N.stream())
         dx = torch.matmul(dgu, w.t()).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        dw = torch.matmul(transpose2d(x2), dguT.t()) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            if ctx.gt is not None:
+                _main_grad_accumulate(ctx.gt, x2, dgu)
+            else:
+                dw = torch.matmul(transpose2d(x2), dguT.t())
         return dx, dw
 
 

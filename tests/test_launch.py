@@ -72,3 +72,41 @@ def test_spawn():
     import paddle2_amd.distributed as dist
 
     dist.spawn(_spawn_fn, args=(2.0,), nprocs=2, backend="gloo")
+
+
+def _bench_json(stdout):
+    import json
+
+    lines = [l for l in stdout.splitlines() if l.startswith("{") and '"metric"' in l]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def test_bench_self_launches_ranks():
+    """bench.py --gpus 2 (no WORLD_SIZE) starts 2 ranks through the in-tree launcher and reports n_gpus=2,
+    on the same stage-3 sharding path as every other N."""
+    env = _env()
+    env.pop("WORLD_SIZE", None)
+    args = ["--model", "tiny", "--steps", "2", "--warmup", "1", "--seq-len", "32", "--micro-batch", "2"]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + args, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = _bench_json(r.stdout)
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 4
+    assert out["config"]["parallelism"] == "sharding3x2"
+    assert out["steps"] == 2 and out["warmup"] == 1
+
+
+def test_bench_single_runs_sharding3_and_rejects_world_mismatch():
+    env = _env()
+    env.pop("WORLD_SIZE", None)
+    args = ["--model", "tiny", "--steps", "1", "--warmup", "1", "--seq-len", "32", "--micro-batch", "2"]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = _bench_json(r.stdout)
+    assert out["n_gpus"] == 1 and out["config"]["parallelism"] == "sharding3x1"
+    env["WORLD_SIZE"] = "2"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"] + args, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

@@ -12,3 +12,28 @@ def test_group_sharded_matches_single(level):
         for a, b in zip(r["losses"], r["ref"]):
             assert abs(a - b) < 1e-3 * max(1.0, abs(b)), (r["losses"], r["ref"])
         assert abs(r["csum"] - r["csum_ref"]) < 1e-2 * max(1.0, abs(r["csum_ref"])), (r["csum"], r["csum_ref"])
+
+
+def _close(a, b, tol=2e-3):
+    for x, y in zip(a, b):
+        assert abs(x - y) < tol * max(1.0, abs(y)), (a, b)
+
+
+@pytest.mark.parametrize("opt", ["offload", "exclude"])
+def test_stage3_offload_exclude_4ranks(opt, tmp_path):
+    """4 gloo ranks: stage 3 with host-offloaded optimizer state / exclude_layer matches one process."""
+    res = run_workers("sharding_ckpt_worker.py", 4, ["train", opt, str(tmp_path / "ck")])
+    for r in res:
+        _close(r["losses"], r["ref"])
+        if opt == "exclude":
+            assert r["norm_full"]
+
+
+def test_stage3_checkpoint_resumes_at_other_degree(tmp_path):
+    """Checkpoint written by 4 sharded ranks (reference per-parameter layout) resumes on 2 ranks and
+    continues exactly like an uninterrupted single-process run."""
+    ck = str(tmp_path / "ck")
+    run_workers("sharding_ckpt_worker.py", 4, ["train", "plain", ck])
+    res = run_workers("sharding_ckpt_worker.py", 2, ["resume", "plain", ck])
+    for r in res:
+        _close(r["losses"], r["ref"])
