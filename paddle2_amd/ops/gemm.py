@@ -1,0 +1,107 @@
+"""Python entry points of the hand-written gfx950 MFMA GEMM (csrc/kernels/gemm.hip).
+
+The three GEMMs of a Paddle-layout Linear (W is [in, out]) map onto one kernel template with no
+transpose pass (reference: paddle/phi/kernels/impl/matmul_kernel_impl.h:108 MatMulFunction and
+matmul_grad; fusion/gpu/fused_linear_param_grad_add_kernel.cu:282):
+
+  ``mm_fwd(x, w)``          y  = x @ W            A K-major, B N-major      (+bias epilogue)
+  ``mm_dgrad(dy, w)``       dx = dy @ W^T         A K-major, B K-major
+  ``mm_wgrad(x, dy, out)``  out = x^T @ dy (+ beta*out), fp32 main-grad epilogue; A M-major, B N-major
+  ``mm_swiglu(x, w)``       gu = x @ W (packed [gate | up]), a = silu(gate) * up, in one kernel
+
+Every function takes 2-D bf16 tensors with unit stride on the last dim.  ``supported(...)`` tells
+whether the kernel accepts a problem (K % 8 == 0, 16-B aligned rows); callers fall back to
+hipBLASLt (torch.matmul) otherwise.  On a GPU without the extension `_native.native()` raises.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import _native as N
+
+LAYOUT_AK, LAYOUT_BK = 1, 2
+EPI_BF16, EPI_F32, EPI_SWIGLU = 0, 1, 2
+GROUP_M = int(os.environ.get("PADDLE2_AMD_GEMM_GROUP_M", "8"))
+# "native" (default on the MI355X) | "blas": route the Linear GEMMs through hipBLASLt instead
+BACKEND = os.environ.get("PADDLE2_AMD_GEMM", "native")
+
+
+def enabled(t: torch.Tensor) -> bool:
+    return BACKEND == "native" and t.device.type == "cuda" and t.dtype == torch.bfloat16 and N.use_native(t)
+
+
+def _ok2d(t, inner):
+    return (t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0
+            and t.shape[1] == inner)
+
+
+def supported_fwd(x2, w):
+    M, K = x2.shape
+    return K % 8 == 0 and w.shape[0] == K and w.shape[1] % 8 == 0 and _ok2d(x2, K) and _ok2d(w, w.shape[1])
+
+
+def supported_dgrad(dy2, w):
+    return dy2.shape[1] % 8 == 0 and _ok2d(dy2, w.shape[1]) and _ok2d(w, w.shape[1])
+
+
+def supported_wgrad(x2, dy2):
+    # both operands are M/N-major here: any token count, 16-B column chunks
+    return x2.shape[1] % 8 == 0 and dy2.shape[1] % 8 == 0 and _ok2d(x2, x2.shape[1]) and _ok2d(dy2, dy2.shape[1])
+
+
+def _launch(layout, epi, a, lda, b, ldb, c, ldc, c2, ldc2, bias, M, Nn, K, beta=0.0, H=0):
+    N.native().gemm(layout, epi, a.data_ptr(), lda, b.data_ptr(), ldb, c.data_ptr(), ldc, N.ptr(c2), ldc2,
+                    N.ptr(bias), M, Nn, K, float(beta), H, GROUP_M, N.stream())
+
+
+def mm_fwd(x2, w, bias=None, out=None):
+    """y[M, N] = x2[M, K] @ w[K, N] (+ bias[N]), bf16."""
+    M, K = x2.shape
+    Nn = w.shape[1]
+    if out is None:
+        out = torch.empty(M, Nn, dtype=x2.dtype, device=x2.device)
+    _launch(LAYOUT_AK, EPI_BF16, x2, x2.stride(0), w, w.stride(0), out, out.stride(0), None, 0, bias, M, Nn, K)
+    return out
+
+
+def mm_dgrad(dy2, w, out=None):
+    """dx[M, K] = dy2[M, N] @ w[K, N]^T, bf16."""
+    M, Nn = dy2.shape
+    K = w.shape[0]
+    if out is None:
+        out = torch.empty(M, K, dtype=dy2.dtype, device=dy2.device)
+    _launch(LAYOUT_AK | LAYOUT_BK, EPI_BF16, dy2, dy2.stride(0), w, w.stride(0), out, out.stride(0), None, 0, None,
+            M, K, Nn)
+    return out
+
+
+def mm_wgrad(x2, dy2, out, beta=0.0):
+    """out[K, N] (fp32) = x2[M, K]^T @ dy2[M, N] + beta * out — dW accumulated in fp32, never rounded."""
+    M, K = x2.shape
+    Nn = dy2.shape[1]
+    assert out.dtype == torch.float32 and out.shape == (K, Nn) and out.stride(1) == 1
+    _launch(0, EPI_F32, x2, x2.stride(0), dy2, dy2.stride(0), out, out.stride(0), None, 0, None, K, Nn, M, beta)
+    return out
+
+
+def mm_wgrad_bf16(x2, dy2, out=None):
+    """out[K, N] (bf16) = x2^T @ dy2."""
+    M, K = x2.shape
+    Nn = dy2.shape[1]
+    if out is None:
+        out = torch.empty(K, Nn, dtype=x2.dtype, device=x2.device)
+    _launch(0, EPI_BF16, x2, x2.stride(0), dy2, dy2.stride(0), out, out.stride(0), None, 0, None, K, Nn, M)
+    return out
+
+
+def mm_swiglu(x2, w):
+    """gu[M, 2H] = x2 @ w (w = [gate | up] packed [K, 2H]); a[M, H] = silu(gate) * up.  -> (a, gu)."""
+    M, K = x2.shape
+    H = w.shape[1] // 2
+    gu = torch.empty(M, 2 * H, dtype=x2.dtype, device=x2.device)
+    a = torch.empty(M, H, dtype=x2.dtype, device=x2.device)
+    _launch(LAYOUT_AK, EPI_SWIGLU, x2, x2.stride(0), w, w.stride(0), a, a.stride(0), gu, gu.stride(0), None, M,
+            2 * H, K, 0.0, H)
+    return a, gu

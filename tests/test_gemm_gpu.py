@@ -1,0 +1,100 @@
+"""Hand-written MFMA GEMM (csrc/kernels/gemm.hip) vs an fp32 PyTorch reference of the same op.
+
+Covers the three Linear layouts (forward x@W, dgrad dy@W^T, wgrad x^T@dy into an fp32 main grad with
+beta 0/1), the bias and SwiGLU epilogues, ragged edges (M, N not multiples of the 256 tile, K a
+multiple of 8 but not of 64), and the 7B-width bench shapes at M = 32768 tokens.
+"""
+import pytest
+import torch
+
+from paddle2_amd.ops import gemm as G
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _rand(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    return (torch.randn(*shape, generator=g, device=dev) * scale).to(torch.bfloat16)
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
+
+
+SHAPES = [(256, 256, 64), (512, 768, 128), (300, 520, 72), (1000, 264, 1032), (64, 1024, 4096), (2048, 4096, 4096)]
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_fwd(M, N, K):
+    x, w = _rand(M, K, seed=1), _rand(K, N, seed=2, scale=0.05)
+    ref = x.float() @ w.float()
+    assert _rel(G.mm_fwd(x, w), ref) < 8e-3
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_fwd_bias(M, N, K):
+    x, w, b = _rand(M, K, seed=3), _rand(K, N, seed=4, scale=0.05), _rand(N, seed=5)
+    ref = x.float() @ w.float() + b.float()
+    assert _rel(G.mm_fwd(x, w, bias=b), ref) < 8e-3
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_dgrad(M, N, K):
+    # dx[M, K] = dy[M, N] @ w[K, N]^T
+    dy, w = _rand(M, N, seed=6), _rand(K, N, seed=7, scale=0.05)
+    ref = dy.float() @ w.float().t()
+    assert _rel(G.mm_dgrad(dy, w), ref) < 8e-3
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_wgrad_fp32_main_grad(M, N, K, beta):
+    # out[K, N] = x[M, K]^T @ dy[M, N] + beta * out  (M is the reduction: tokens)
+    x, dy = _rand(M, K, seed=8), _rand(M, N, seed=9)
+    out0 = torch.randn(K, N, device=dev) if beta else torch.full((K, N), float("nan"), device=dev)
+    ref = x.double().t() @ dy.double() + (beta * out0.double() if beta else 0)
+    out = out0.clone()
+    G.mm_wgrad(x, dy, out, beta=beta)
+    assert torch.isfinite(out).all()
+    assert _rel(out, ref) < 1e-5  # fp32 accumulation of exact bf16 products
+
+
+def test_identity_asymmetric_catches_transpose():
+    """A = I with an asymmetric B (guide §3): a row/col swap in the C write cannot pass."""
+    n = 256
+    eye = torch.eye(n, device=dev, dtype=torch.bfloat16)
+    b = (torch.arange(n * n, device=dev, dtype=torch.float32).reshape(n, n) % 251 - 125).to(torch.bfloat16)
+    assert torch.equal(G.mm_fwd(eye, b), b)
+    assert torch.equal(G.mm_dgrad(eye, b.t().contiguous()), b)
+    out = torch.empty(n, n, device=dev)
+    G.mm_wgrad(eye, b, out)
+    assert torch.equal(out, b.float())
+
+
+@pytest.mark.parametrize("M,K,H", [(512, 256, 256), (300, 136, 96), (4096, 4096, 11008)])
+def test_swiglu_epilogue(M, K, H):
+    x, w = _rand(M, K, seed=10), _rand(K, 2 * H, seed=11, scale=0.05)
+    a, gu = G.mm_swiglu(x, w)
+    gu_ref = x.float() @ w.float()
+    assert _rel(gu, gu_ref) < 8e-3
+    g, u = gu.float()[:, :H], gu.float()[:, H:]
+    a_ref = torch.nn.functional.silu(g) * u  # from the stored (rounded) pre-activation
+    assert _rel(a, a_ref) < 8e-3
+
+
+@pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 4096), (4096, 11008)])
+def test_llama7b_shapes_m32768(N, K):
+    """bench shapes at M = 32768 tokens: fwd, dgrad, fp32 wgrad vs fp32 references (row-sampled)."""
+    M = 32768
+    x, w, dy = _rand(M, K, seed=12), _rand(K, N, seed=13, scale=0.02), _rand(M, N, seed=14)
+    rows = torch.arange(0, M, 97, device=dev)
+    y = G.mm_fwd(x, w)
+    assert _rel(y[rows], x[rows].float() @ w.float()) < 8e-3
+    dx = G.mm_dgrad(dy, w)
+    assert _rel(dx[rows], dy[rows].float() @ w.float().t()) < 8e-3
+    out = torch.empty(K, N, device=dev)
+    G.mm_wgrad(x, dy, out)
+    cols = torch.arange(0, N, 61, device=dev)
+    ref = x.float().t() @ dy[:, cols].float()
+    assert _rel(out[:, cols], ref) < 1e-4
