@@ -329,12 +329,17 @@ class _LinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, K)
         M = x2.shape[0]
         fwd_t, dw_t = _linear_plan(M, K, Nn)
-        if fwd_t:
-            y = torch.matmul(x2, transpose2d(w).t())
+        from . import gemm as G
+
+        if _pass_native("fwd", x2) and G.supported_fwd(x2, w) and (b is None or b.dtype == x2.dtype):
+            y = G.mm_fwd(x2, w, bias=None if b is None else b.contiguous())
         else:
-            y = torch.matmul(x2, w)
-        if b is not None:
-            y += b
+            if fwd_t:
+                y = torch.matmul(x2, transpose2d(w).t())
+            else:
+                y = torch.matmul(x2, w)
+            if b is not None:
+                y += b
         ctx.save_for_backward(x2, w)
         ctx.meta = (x.shape, dw_t, b is not None)
         ctx.gt = getattr(w, "_p2_gt", None)
@@ -349,11 +354,18 @@ class _LinearFn(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         dx = dw = db = None
+        from . import gemm as G
+
         if ctx.needs_input_grad[0]:
-            dx = torch.matmul(dy2, w.t()).view(xshape)
+            if _pass_native("dgrad", dy2) and G.supported_dgrad(dy2, w):
+                dx = G.mm_dgrad(dy2, w).view(xshape)
+            else:
+                dx = torch.matmul(dy2, w.t()).view(xshape)
         if ctx.needs_input_grad[1]:
             if ctx.gt is not None:
                 _main_grad_accumulate(ctx.gt, x2, dy2)
+            elif _pass_native("wgrad", x2) and G.supported_wgrad(x2, dy2):
+                dw = G.mm_wgrad_bf16(x2, dy2)
             elif dw_t:
                 dw = torch.matmul(transpose2d(x2), transpose2d(dy2).t())
             else:
@@ -363,10 +375,30 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
+def _pass_native(name, t):
+    """Per-pass GEMM backend (PADDLE2_AMD_GEMM_{FWD,DGRAD,WGRAD} = native | blas): the hand-written MFMA
+    kernel (ops/gemm.py) or hipBLASLt, chosen per pass from measured speed (profiles/r2_gemm_native.md)."""
+    from . import gemm as G
+
+    return G.enabled(t) and _GEMM_PASS.get(name, "native") == "native"
+
+
+_GEMM_PASS = {"fwd": _os.environ.get("PADDLE2_AMD_GEMM_FWD", "blas"),
+              "dgrad": _os.environ.get("PADDLE2_AMD_GEMM_DGRAD", "blas"),
+              "wgrad": _os.environ.get("PADDLE2_AMD_GEMM_WGRAD", "native")}
+
+
 def wgrad_accumulate(out, x2, dy2, beta):
     """out[K, N] (fp32 main grad) = x2^T @ dy2 + beta * out, with the product accumulated in fp32 — never
-    rounded to the activation dtype first (reference fused_linear_param_grad_add_kernel.cu:51, use_addto)."""
+    rounded to the activation dtype first (reference fused_linear_param_grad_add_kernel.cu:51, use_addto).
+    GPU: the native MFMA GEMM's fp32 main-grad epilogue (M/N-major operands, no transpose pass)."""
     if out.device.type == "cuda":
+        from . import gemm as G
+
+        if (_pass_native("wgrad", x2) and out.dtype == torch.float32 and out.is_contiguous()
+                and G.supported_wgrad(x2, dy2)):
+            G.mm_wgrad(x2, dy2, out, beta)
+            return out
         torch.addmm(out, x2.t(), dy2, beta=float(beta), out_dtype=out.dtype, out=out)
         return out
     if beta == 0:
@@ -405,8 +437,13 @@ class _SwiGLULinearFn(torch.autograd.Function):
     def forward(ctx, x, w):
         K, H2 = w.shape
         x2 = x.reshape(-1, K)
-        gu = torch.matmul(x2, transpose2d(w).t())
-        a = swiglu(gu)
+        from . import gemm as G
+
+        if _pass_native("fwd", x2) and G.supported_fwd(x2, w):
+            a, gu = G.mm_swiglu(x2, w)  # one kernel: GEMM + SwiGLU epilogue (gu kept for the backward)
+        else:
+            gu = torch.matmul(x2, transpose2d(w).t())
+            a = swiglu(gu)
         ctx.save_for_backward(x2, w, gu)
         ctx.xshape = x.shape
         ctx.gt = getattr(w, "_p2_gt", None)
@@ -418,7 +455,10 @@ class _SwiGLULinearFn(torch.autograd.Function):
         M, H2 = gu.shape
         da2 = da.reshape(M, H2 // 2).contiguous()
         dgu = torch.empty_like(gu)
-        if ctx.gt is not None:  # main-grad GEMM reads dgu in place: no dY^T image needed
+        from . import gemm as G
+
+        native_w = _pass_native("wgrad", x2) and G.supported_wgrad(x2, gu)
+        if ctx.gt is not None or native_w:  # native / main-grad GEMM reads dgu in place: no dY^T image needed
             H, es = H2 // 2, gu.element_size()
             N.native().swiglu_bwd(_DT[gu.dtype], gu.data_ptr(), gu.data_ptr() + H * es, da2.data_ptr(),
                                   dgu.data_ptr(), dgu.data_ptr() + H * es, M, H, H2, H2, H2, H2, N.stream())
@@ -426,11 +466,18 @@ class _SwiGLULinearFn(torch.autograd.Function):
             dguT = torch.empty(H2, M, dtype=gu.dtype, device=gu.device)
             N.native().swiglu_bwd_t(gu.data_ptr(), da2.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), M, H2 // 2, H2,
                                     N.stream())
-        dx = torch.matmul(dgu, w.t()).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if _pass_native("dgrad", dgu) and G.supported_dgrad(dgu, w):
+                dx = G.mm_dgrad(dgu, w).view(ctx.xshape)
+            else:
+                dx = torch.matmul(dgu, w.t()).view(ctx.xshape)
         dw = None
         if ctx.needs_input_grad[1]:
             if ctx.gt is not None:
                 _main_grad_accumulate(ctx.gt, x2, dgu)
+            elif native_w:
+                dw = G.mm_wgrad_bf16(x2, dgu)
             else:
                 dw = torch.matmul(transpose2d(x2), dguT.t())
         return dx, dw
