@@ -242,6 +242,60 @@ __device__ __forceinline__ bf16x8 read_frag(const RdB<KMAJ>& r) {
   }
 }
 
+// Epilogue from the accumulators.  acc[i][j]: rows arow + 16i + 4*(lane>>4) + e, tile column
+// bcolw + 16j + (lane&15) (v_mfma_f32_16x16x32_bf16 C layout).
+template <int EPI>
+__device__ __forceinline__ void epilogue(const Params& p, f32x4v (&acc)[8][4], int tm, int tn, int arow, int bcolw,
+                                         int wn, int lane) {
+  const int row0 = tm * BM + arow + 4 * (lane >> 4);
+  if constexpr (EPI == kEpiSwiGLU) {
+    // gate = acc[i][0..1], up = acc[i][2..3] at the same lane position
+    unsigned short* out = (unsigned short*)p.C;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int gc = tn * 128 + wn * 32 + 16 * j + (lane & 15);  // gate column == output column
+      if (gc >= p.H) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = row0 + 16 * i + e;
+          if (r < p.M) {
+            const float g = bf2f(f2bf(acc[i][j][e]));
+            const float u = bf2f(f2bf(acc[i][2 + j][e]));
+            p.C2[(long)r * p.ldc2 + gc] = f2bf(g);
+            p.C2[(long)r * p.ldc2 + p.H + gc] = f2bf(u);
+            out[(long)r * p.ldc + gc] = f2bf(silu(g) * u);
+          }
+        }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = tn * BN + bcolw + 16 * j + (lane & 15);
+      if (c >= p.N) continue;
+      float bv = 0.f;
+      if constexpr (EPI == kEpiBF16) {
+        if (p.bias) bv = bf2f(p.bias[c]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = row0 + 16 * i + e;
+          if (r < p.M) {
+            if constexpr (EPI == kEpiBF16) {
+              ((unsigned short*)p.C)[(long)r * p.ldc + c] = f2bf(acc[i][j][e] + bv);
+            } else {
+              float* cp = (float*)p.C + (long)r * p.ldc + c;
+              *cp = p.beta != 0.f ? acc[i][j][e] + p.beta * *cp : acc[i][j][e];
+            }
+          }
+        }
+    }
+  }
+}
+
 template <bool AK, bool BKM, int EPI, int DBG = 0>
 __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(Params p) {
   __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
@@ -400,54 +454,273 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(Params p) {
     ktile(C1{}, t + 1);
   }
 
-  // ---- epilogue.  acc[i][j]: rows arow + 16i + 4*(lane>>4) + e, tile column bcolw + 16j + (lane&15)
-  const int row0 = tm * BM + arow + 4 * (lane >> 4);
-  if constexpr (EPI == kEpiSwiGLU) {
-    // gate = acc[i][0..1], up = acc[i][2..3] at the same lane position
-    unsigned short* out = (unsigned short*)p.C;
+  epilogue<EPI>(p, acc, tm, tn, arow, bcolw, wn, lane);
+}
+
+// ================================================================================================
+// Ping-pong variant.  The two wave groups (G0 = waves 0-3, A rows 0-127; G1 = waves 4-7, rows
+// 128-255) run one barrier apart: G1 executes one extra s_barrier first (G0 one at the end), so while
+// one group runs a 16-MFMA cluster (C slot) the other issues its LDS-DMA pieces and fragment reads
+// (M slot) — on every SIMD, which hosts one wave of each group, the MFMA pipe is fed by one wave while
+// the other pays the LDS-DMA issue cost (~60 cycles per 1-KiB piece).
+//   per K-tile and wave: 4 quadrants Q1 (A0,B0) Q2 (A0,B1) Q3 (A1,B1) Q4 (A1,B0), each = M slot
+//   [vmcnt(6); 2 DMA pieces; reads for Q] barrier, C slot [lgkmcnt(0); 16 MFMA] barrier.
+// LDS: each stage is split into 4 x 16 KiB "parts" (A0 = the A0 rows of both groups, A1, B0, B1), laid
+// out part-major [A0s0 A0s1 A1s0 A1s1 B0s0 B0s1 B1s0 B1s1] so every read address is a base VGPR + a
+// 16-bit immediate.  A part is refilled with tile t+2 as soon as both groups have read it in tile t:
+//   G0 M slots: Q1 B1(t+1)  Q2 A1(t+1)  Q3 A0(t+2)  Q4 B0(t+2)      (its 8 of each part's 16 pieces)
+//   G1 M slots: Q1 A1(t+1)  Q2 A0(t+2)  Q3 B0(t+2)  Q4 B1(t+2)
+// so every piece has 4 own M slots (8 slots ~ one K-tile of MFMA time) to land: vmcnt(6) at each M slot
+// retires the pieces issued 4 M slots earlier, one barrier before any group reads them.
+// Part images: K-major [128 part rows][64 k] (128-B rows, chunk ^ ((r>>1)&7)); MN-major [64 k][128 part
+// columns] (256-B rows, 32-B pair ^ hsw(k)) — both conflict-free for the fragment reads.
+namespace ppk {
+constexpr int PART = 16384;
+constexpr int B_REG = 4 * PART;  // B parts start at 64 KiB
+
+__device__ __forceinline__ constexpr int poff(int part, int st) { return (part * 2 + st) * PART; }
+
+// part-local index (0..127) of an operand part -> tile row (A) / tile column (B) (0..255)
+__device__ __forceinline__ int a_part_row(int part, int pr) { return (pr & 63) + (pr >> 6) * 128 + part * 64; }
+__device__ __forceinline__ int b_part_col(int part, int pc) { return (pc >> 5) * 64 + (pc & 31) + part * 32; }
+
+// Per-lane DMA source offsets of one operand: [part 0/1][piece parity e].  Group g issues pieces
+// j = 8g + 2w + e (w = wave in group) of every part; a piece is 8 part rows (K-major) or 4 k rows (MN).
+struct Ldp {
+  unsigned voff[2][2];
+  int kl[2];  // K-major: lane's first k (per parity); MN-major: lane's k (per parity)
+};
+
+template <bool KMAJ, bool ISB, int EPI>
+__device__ __forceinline__ Ldp lane_setup(long ld, int R, int t0, int H, int g, int w, int lane) {
+  Ldp o;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int gc = tn * 128 + wn * 32 + 16 * j + (lane & 15);  // gate column == output column
-      if (gc >= p.H) continue;
+  for (int part = 0; part < 2; ++part)
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int r = row0 + 16 * i + e;
-          if (r < p.M) {
-            const float g = bf2f(f2bf(acc[i][j][e]));
-            const float u = bf2f(f2bf(acc[i][2 + j][e]));
-            p.C2[(long)r * p.ldc2 + gc] = f2bf(g);
-            p.C2[(long)r * p.ldc2 + p.H + gc] = f2bf(u);
-            out[(long)r * p.ldc + gc] = f2bf(silu(g) * u);
-          }
-        }
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = tn * BN + bcolw + 16 * j + (lane & 15);
-      if (c >= p.N) continue;
-      float bv = 0.f;
-      if constexpr (EPI == kEpiBF16) {
-        if (p.bias) bv = bf2f(p.bias[c]);
+    for (int e = 0; e < 2; ++e) {
+      const int j = 8 * g + 2 * w + e;
+      if constexpr (KMAJ) {
+        const int pr = 8 * j + (lane >> 3);
+        const int lc = (lane & 7) ^ ((pr >> 1) & 7);
+        const int tr = ISB ? b_part_col(part, pr) : a_part_row(part, pr);   // tile row / col
+        const int gr = ISB ? bcol<EPI>(t0, tr, H) : t0 * BM + tr;
+        const int r0 = ISB ? (EPI == kEpiSwiGLU ? 0 : t0 * BN) : t0 * BM;
+        o.kl[e] = lc * 8;
+        o.voff[part][e] = (unsigned)(((long)(gr - r0) * ld + lc * 8) * 2) | ((unsigned)(gr >= R) << 31);
+      } else {
+        const int k = 4 * j + (lane >> 4);
+        const int pch = lane & 15;
+        const int lch = (((pch >> 1) ^ hsw(k)) << 1) | (pch & 1);
+        const int pc = lch * 8;  // first part column of the 16-B chunk
+        const int tc = ISB ? b_part_col(part, pc) : a_part_row(part, pc);
+        const int gc = ISB ? bcol<EPI>(t0, tc, H) : t0 * BM + tc;
+        const int c0 = ISB ? (EPI == kEpiSwiGLU ? 0 : t0 * BN) : t0 * BM;
+        o.kl[e] = k;
+        o.voff[part][e] = (unsigned)(((long)k * ld + (gc - c0)) * 2) | ((unsigned)(gc >= R) << 31);
       }
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int r = row0 + 16 * i + e;
-          if (r < p.M) {
-            if constexpr (EPI == kEpiBF16) {
-              ((unsigned short*)p.C)[(long)r * p.ldc + c] = f2bf(acc[i][j][e] + bv);
-            } else {
-              float* cp = (float*)p.C + (long)r * p.ldc + c;
-              *cp = p.beta != 0.f ? acc[i][j][e] + p.beta * *cp : acc[i][j][e];
-            }
-          }
-        }
     }
+  return o;
+}
+
+// Per-lane fragment-read bases (region-relative, stage 0, part 0) of one operand
+//  K-major: b[s] (k32 step s) for part row first + (lane&15); tile u of the wave adds u*16*128.
+//  MN-major: b[0] = x (row/offset part), b[1] = h (pair swizzle); pair = (T ^ h) for 16-col tile T.
+struct Rdp {
+  unsigned b[2];
+  int f;  // MN-major: first 16-column tile (part-local) of the wave
+};
+
+template <bool KMAJ>
+__device__ __forceinline__ Rdp rd_setup(unsigned region, int first, int lane) {
+  Rdp o;
+  if constexpr (KMAJ) {
+    const int rl = lane & 15;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = (4 * s + (lane >> 4)) ^ ((rl >> 1) & 7);
+      o.b[s] = region + (first + rl) * 128 + ch * 16;
+    }
+    o.f = 0;
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    o.b[0] = region + (8 * g + q) * 256 + (pp >> 1) * 16 + (pp & 1) * 8;
+    o.b[1] = q | ((g & 1) << 2);
+    o.f = first >> 4;
   }
+  return o;
+}
+
+template <bool KMAJ, int U, int S, int PART_, int ST>
+__device__ __forceinline__ bf16x8 read_frag(const Rdp& r) {
+  constexpr int base = poff(PART_, ST);
+  if constexpr (KMAJ) {
+    return rd128<base + U * 16 * 128>(r.b[S]);
+  } else {
+    unsigned h = r.b[1];
+    asm volatile("" : "+v"(h));  // keep the per-read XOR in the loop (no hoisted per-tile bases)
+    const unsigned a = r.b[0] + (((unsigned)(r.f + U) ^ h) << 5);
+    return cat(rdtr<base + S * 8192>(a), rdtr<base + S * 8192 + 1024>(a));
+  }
+}
+}  // namespace ppk
+
+template <bool AK, bool BKM, int EPI>
+__global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Params p) {
+  using namespace ppk;
+  __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
+  lds_char* smem = (lds_char*)smem_raw;
+  const unsigned sbase = (unsigned)(size_t)smem;
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int per_group = p.group_m * p.tiles_n;
+  const int gid = bid / per_group;
+  const int first_m = gid * p.group_m;
+  const int gsz = min(p.tiles_m - first_m, p.group_m);
+  const int tm = first_m + (bid % per_group) % gsz;
+  const int tn = (bid % per_group) / gsz;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;  // wm = group
+  const int Ncols = (EPI == kEpiSwiGLU) ? 2 * p.H : p.N;
+  const int nt = (((p.K + BK - 1) / BK) + 1) & ~1;
+
+  f32x4v acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  const Ldp LA = ppk::lane_setup<AK, false, EPI>(p.lda, p.M, tm, p.H, wm, wn, lane);
+  const Ldp LB = ppk::lane_setup<BKM, true, EPI>(p.ldb, Ncols, tn, p.H, wm, wn, lane);
+  const unsigned short* a_t0 = AK ? p.A + (long)tm * BM * p.lda : p.A + (long)tm * BM;
+  const unsigned short* b_t0 =
+      BKM ? p.B + (long)tn * BN * p.ldb : (EPI == kEpiSwiGLU ? p.B : p.B + (long)tn * BN);
+  const long a_step = AK ? BK : (long)BK * p.lda;
+  const long b_step = BKM ? BK : (long)BK * p.ldb;
+
+  // DMA: this wave's 2 pieces (parity e = 0, 1) of operand part `part` of tile t into stage t & 1
+  auto dmaPart = [&](bool isB, int part, int t) {
+    const unsigned short* base = isB ? b_t0 + b_step * t : a_t0 + a_step * t;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base);
+    const Ldp& L = isB ? LB : LA;
+    const bool kmaj = isB ? BKM : AK;
+    const int krem = p.K - t * BK;
+    const int st = t & 1;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int j = 8 * wm + 2 * wn + e;
+      const bool ok = krem >= BK || (kmaj ? L.kl[e] < krem : L.kl[e] < krem);
+      const unsigned voff = L.voff[part][e] | ((unsigned)(!ok) << 31);
+      lds_char* dst = smem + (isB ? B_REG : 0) + poff(part, st) + j * 1024;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, 0);
+    }
+  };
+
+  // prologue: tiles 0 and 1 completely, drained
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      dmaPart(false, part, t);
+      dmaPart(true, part, t);
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // the stagger: G1 runs one slot behind G0
+
+  const Rdp ra = ppk::rd_setup<AK>(sbase, AK ? wm * 64 : wm * 64, lane);
+  const Rdp rb = ppk::rd_setup<BKM>(sbase + B_REG, wn * 32, lane);
+
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];  // A half (4 m16 x 2 k32), B0 / B1 (2 n16 x 2 k32)
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+
+  auto readA = [&](auto PART_, auto ST) {
+    sfor<4>([&](auto U) {
+      sfor<2>([&](auto S) {
+        fa[U][S] = read_frag<AK, decltype(U)::value, decltype(S)::value, decltype(PART_)::value,
+                             decltype(ST)::value>(ra);
+      });
+    });
+  };
+  auto readB = [&](bf16x8 (&dst)[2][2], auto PART_, auto ST) {
+    sfor<2>([&](auto U) {
+      sfor<2>([&](auto S) {
+        dst[U][S] = read_frag<BKM, decltype(U)::value, decltype(S)::value, decltype(PART_)::value,
+                              decltype(ST)::value>(rb);
+      });
+    });
+  };
+  auto cslot = [&](auto MI, const bf16x8 (&b)[2][2], auto NI) {
+    constexpr int mi = decltype(MI)::value, ni = decltype(NI)::value;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 * mi + i][2 * ni + j] = mfma(fa[i][s], b[j][s], acc[4 * mi + i][2 * ni + j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  };
+  // vmcnt(6) retires the pieces issued 4 own M slots earlier only while every M slot issues its 2; in
+  // the last two K-tiles slots issue fewer, so there every M slot drains (vmcnt(0)).
+  auto mslot_begin = [&](bool steady) {
+    if (steady) {
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mslot_end = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  auto ktile = [&](auto ST, int t) {
+    const bool n1 = t >= 1 && t + 1 < nt;  // tile t+1 parts not covered by the prologue
+    const bool n2 = t + 2 < nt;
+    // Q1: (A0, B0)
+    mslot_begin(n2);
+    if (wm == 0) { if (n1) dmaPart(true, 1, t + 1); } else { if (n1) dmaPart(false, 1, t + 1); }
+    readA(C0{}, ST);
+    readB(fb0, C0{}, ST);
+    mslot_end();
+    cslot(C0{}, fb0, C0{});
+    // Q2: (A0, B1)
+    mslot_begin(n2);
+    if (wm == 0) { if (n1) dmaPart(false, 1, t + 1); } else { if (n2) dmaPart(false, 0, t + 2); }
+    readB(fb1, C1{}, ST);
+    mslot_end();
+    cslot(C0{}, fb1, C1{});
+    // Q3: (A1, B1)
+    mslot_begin(n2);
+    if (wm == 0) { if (n2) dmaPart(false, 0, t + 2); } else { if (n2) dmaPart(true, 0, t + 2); }
+    readA(C1{}, ST);
+    mslot_end();
+    cslot(C1{}, fb1, C1{});
+    // Q4: (A1, B0)
+    mslot_begin(n2);
+    if (wm == 0) { if (n2) dmaPart(true, 0, t + 2); } else { if (n2) dmaPart(true, 1, t + 2); }
+    mslot_end();
+    cslot(C1{}, fb0, C0{});
+  };
+
+  for (int t = 0; t < nt; t += 2) {
+    ktile(C0{}, t);
+    ktile(C1{}, t + 1);
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // balance G1's extra barrier
+
+  epilogue<EPI>(p, acc, tm, tn, wm * 128, wn * 64, wn, lane);
 }
 
 }  // namespace gm
@@ -456,7 +729,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(Params p) {
 // layout: bit0 = A K-major, bit1 = B K-major.  epi: 0 bf16 (+bias), 1 fp32 main grad (beta), 2 swiglu.
 extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
                        void* C2, long ldc2, const void* bias, int M, int N, int K, float beta, int H, int group_m,
-                       void* stream) {
+                       int variant, void* stream) {
   using namespace pd::gm;
   if (M <= 0 || N <= 0 || K <= 0) return -1;
   if ((layout & 3) && K % 8) return -1;   // K-major operands move 16-B chunks along k
@@ -478,8 +751,12 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   if (epi == kEpiSwiGLU && (bk || H % 32)) return -3;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(p.tiles_m * p.tiles_n);
-#define PD_GEMM_LAUNCH(AKV, BKV, EPIV) \
-  gemm_kernel<AKV, BKV, EPIV><<<grid, NTHR, 0, st>>>(p)
+#define PD_GEMM_LAUNCH(AKV, BKV, EPIV)                              \
+  if (variant == 1) {                                                \
+    gemm_pp_kernel<AKV, BKV, EPIV><<<grid, NTHR, 0, st>>>(p);       \
+  } else {                                                           \
+    gemm_kernel<AKV, BKV, EPIV><<<grid, NTHR, 0, st>>>(p);          \
+  }
   switch (epi * 4 + layout) {
     case 0 * 4 + 0: PD_GEMM_LAUNCH(false, false, kEpiBF16); break;
     case 0 * 4 + 1: PD_GEMM_LAUNCH(true, false, kEpiBF16); break;

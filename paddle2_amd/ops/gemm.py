@@ -24,6 +24,8 @@ from . import _native as N
 LAYOUT_AK, LAYOUT_BK = 1, 2
 EPI_BF16, EPI_F32, EPI_SWIGLU = 0, 1, 2
 GROUP_M = int(os.environ.get("PADDLE2_AMD_GEMM_GROUP_M", "8"))
+# kernel schedule: 0 = v2 (8 sub-phases, all waves stage), 1 = ping-pong (wave groups one barrier apart)
+VARIANT = int(os.environ.get("PADDLE2_AMD_GEMM_VARIANT", "0"))
 # "native" (default on the MI355X) | "blas": route the Linear GEMMs through hipBLASLt instead
 BACKEND = os.environ.get("PADDLE2_AMD_GEMM", "native")
 
@@ -53,7 +55,7 @@ def supported_wgrad(x2, dy2):
 
 def _launch(layout, epi, a, lda, b, ldb, c, ldc, c2, ldc2, bias, M, Nn, K, beta=0.0, H=0):
     N.native().gemm(layout, epi, a.data_ptr(), lda, b.data_ptr(), ldb, c.data_ptr(), ldc, N.ptr(c2), ldc2,
-                    N.ptr(bias), M, Nn, K, float(beta), H, GROUP_M, N.stream())
+                    N.ptr(bias), M, Nn, K, float(beta), H, GROUP_M, VARIANT, N.stream())
 
 
 def mm_fwd(x2, w, bias=None, out=None):

@@ -14,6 +14,7 @@ from paddle2_amd.ops import gemm as G  # noqa: E402
 
 dev = "cuda"
 M = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
+VARIANTS = [int(v) for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1"])]
 SHAPES = {"qkv": (4096, 12288), "o_proj": (4096, 4096), "gate_up": (4096, 22016), "down": (11008, 4096),
           "lm_head": (4096, 32000)}
 
@@ -38,15 +39,24 @@ for name, (K, N) in SHAPES.items():
     out32 = torch.zeros(K, N, device=dev)
     fl = 2.0 * M * N * K
     rows = []
-    rows.append(("fwd", timeit(lambda: G.mm_fwd(x, w)), timeit(lambda: torch.matmul(x, w))))
-    rows.append(("dgrad", timeit(lambda: G.mm_dgrad(dy, w)), timeit(lambda: torch.matmul(dy, w.t()))))
-    rows.append(("wgrad", timeit(lambda: G.mm_wgrad(x, dy, out32, 1.0)), timeit(lambda: torch.matmul(x.t(), dy))))
+
+    def nat(fn):
+        res = {}
+        for v in VARIANTS:
+            G.VARIANT = v
+            res[v] = timeit(fn)
+        return res
+
+    rows.append(("fwd", nat(lambda: G.mm_fwd(x, w)), timeit(lambda: torch.matmul(x, w))))
+    rows.append(("dgrad", nat(lambda: G.mm_dgrad(dy, w)), timeit(lambda: torch.matmul(dy, w.t()))))
+    rows.append(("wgrad", nat(lambda: G.mm_wgrad(x, dy, out32, 1.0)), timeit(lambda: torch.matmul(x.t(), dy))))
     if name == "gate_up":
-        rows.append(("fwd_swiglu", timeit(lambda: G.mm_swiglu(x, w)), None))
+        rows.append(("fwd_swiglu", nat(lambda: G.mm_swiglu(x, w)), None))
     for p, tn, tb in rows:
-        print(json.dumps({"shape": name, "M": M, "K": K, "N": N, "pass": p, "native_ms": round(tn, 4),
-                          "native_TFs": round(fl / tn / 1e9, 1),
-                          "hipblaslt_ms": None if tb is None else round(tb, 4),
-                          "hipblaslt_TFs": None if tb is None else round(fl / tb / 1e9, 1)}), flush=True)
+        rec = {"shape": name, "M": M, "K": K, "N": N, "pass": p}
+        for v, t in tn.items():
+            rec[f"native_v{v}_TFs"] = round(fl / t / 1e9, 1)
+        rec["hipblaslt_TFs"] = None if tb is None else round(fl / tb / 1e9, 1)
+        print(json.dumps(rec), flush=True)
     del x, w, dy, out32
     torch.cuda.empty_cache()

@@ -12,7 +12,7 @@ f = lib.pd_gemm
 f.restype = ctypes.c_int
 f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long,
               ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_int,
-              ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+              ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
 M, N, K = 32768, 4096, 4096
 dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
 w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
@@ -25,7 +25,7 @@ zero = torch.zeros(64, dtype=torch.uint8, device="cuda")
 
 def run(epi):
     rc = f(3, epi, dy.data_ptr(), K, w.data_ptr(), K, out.data_ptr(), N, None, 0, zero.data_ptr() if epi == 10 else None,
-           M, N, K, 0.0, 0, 8, st)
+           M, N, K, 0.0, 0, 8, 0, st)
     assert rc == 0, rc
 
 
