@@ -181,20 +181,28 @@ def _fused_softmax_mask_ut(x):
 @register_op("fused_linear_param_grad_add", inplace=True)
 def _fused_linear_param_grad_add(x, dout, dweight=None, dbias=None, multi_precision=True, has_bias=True):
     """dW += x^T dy (fp32 main_grad when multi_precision), db += sum(dy); returns (dweight, dbias).
-    Reference: phi/kernels/fusion/gpu/fused_linear_param_grad_add_kernel.cu:282.  The GEMM accumulates in
-    place through hipBLASLt's beta=1 epilogue (addmm_), so no temporary [K, N] product is materialised."""
+    Reference: phi/kernels/fusion/gpu/fused_linear_param_grad_add_kernel.cu:282 (use_addto into MT=fp32).
+    The product is accumulated straight into the fp32 main grad (native MFMA GEMM fp32 epilogue with
+    beta = 1 on the GPU; fp32 addmm on the CPU) — never rounded to bf16 first, no [K, N] temporary."""
     xt, dy = _t(x), _t(dout)
     x2 = xt.reshape(-1, xt.shape[-1])
     d2 = dy.reshape(-1, dy.shape[-1])
     acc_dt = torch.float32 if multi_precision else dy.dtype
-    if dweight is None:
-        dw = torch.zeros(x2.shape[1], d2.shape[1], dtype=acc_dt, device=dy.device)
+    fresh = dweight is None
+    if fresh:
+        dw = torch.empty(x2.shape[1], d2.shape[1], dtype=acc_dt, device=dy.device)
         dweight = _w(dw)
     dw = _t(dweight)
-    if dw.dtype == x2.dtype:
-        dw.addmm_(x2.t(), d2)
+    if dw.dtype == torch.float32:
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        if not d2.is_contiguous():
+            d2 = d2.contiguous()
+        T.wgrad_accumulate(dw, x2, d2, 0.0 if fresh else 1.0)
+    elif fresh:
+        torch.matmul(x2.t(), d2, out=dw)
     else:
-        dw.add_(torch.matmul(x2.t(), d2).to(dw.dtype))
+        dw.addmm_(x2.t(), d2)
     if has_bias:
         db_new = d2.sum(0, dtype=torch.float32).to(acc_dt)
         if dbias is None:

@@ -255,20 +255,30 @@ def fused_multi_transformer(*args, **kwargs):
     return _fmt(*args, **kwargs)
 
 
-def fused_moe(x, gate_weight, ffn1_weight, ffn1_scale=None, ffn1_bias=None, ffn2_weight=None, ffn2_scale=None,
-              ffn2_bias=None, quant_method="None", moe_topk=2, group_moe=False, norm_topk_prob=True):
-    """Top-k gated MoE FFN (reference: fusion/cutlass/fused_moe_kernel.cu, which is NVIDIA-only there).
+def fused_moe(x, gate_weight, ffn1_weight, ffn2_weight, ffn1_bias=None, ffn1_scale=None, ffn2_bias=None,
+              ffn2_scale=None, quant_method="None", moe_topk=2, norm_topk_prob=True):
+    """Top-k gated MoE FFN with the reference public signature
+    (python/paddle/incubate/nn/functional/fused_moe.py:20; kernel fusion/cutlass/fused_moe_kernel.cu).
+
+    ``gate_weight`` [H, E] (the router Linear's weight); ``ffn1_weight`` [E, H, 2F] packs [gate | up];
+    ``ffn2_weight`` [E, F, H].  ``quant_method`` "weight_only_int8" / "weight_only_int4": the expert
+    weights are ``nn.quant.weight_quantize`` outputs (int8 [N, K] / packed int4 [N/2, K] per expert, viewed
+    with the float weight's shape as in the reference test) with per-channel ``ffn*_scale`` [E, N]; each
+    expert's weights are dequantized once per call.
 
     MI355X path: the N*k (token, expert) assignments are sorted by expert ONCE, so each expert's rows are a
     contiguous slice of one permuted activation matrix; a single host read of the per-expert counts sizes
-    the slices (the old per-expert ``nonzero`` cost one device sync per expert).  Each expert then runs two
-    dense hipBLASLt GEMMs on its slice with the SwiGLU HIP kernel between them, and the weighted outputs are
-    scattered back with one ``index_add_``.  ``ffn1_weight`` [E, H, 2F] packs [gate | up]; ``ffn2_weight``
-    [E, F, H]."""
+    the slices.  Each expert runs two dense GEMMs on its slice with the SwiGLU HIP kernel between them, and
+    the weighted outputs are scattered back with one ``index_add_``."""
+    if quant_method not in ("None", "weight_only_int8", "weight_only_int4"):
+        raise NotImplementedError(f"fused_moe: quant_method {quant_method!r}")
+    quant = quant_method != "None"
+    if quant and (ffn1_scale is None or ffn2_scale is None):
+        raise ValueError(f"fused_moe: quant_method {quant_method!r} needs ffn1_scale and ffn2_scale")
     t = x._t
     shp = t.shape
     t2 = t.reshape(-1, shp[-1])
-    n_tok = t2.shape[0]
+    n_tok, Hd = t2.shape
     logits = t2.float() @ gate_weight._t.float()
     probs = torch.softmax(logits, -1)
     w, idx = torch.topk(probs, moe_topk, -1)
@@ -276,27 +286,41 @@ def fused_moe(x, gate_weight, ffn1_weight, ffn1_scale=None, ffn1_bias=None, ffn2
         w = w / w.sum(-1, keepdim=True)
     w1, w2 = ffn1_weight._t, ffn2_weight._t
     E = w1.shape[0]
+    wd = "int4" if quant_method == "weight_only_int4" else "int8"
+
+    def expert_w(wt, scale, e, K, N):
+        if not quant:
+            return wt[e]
+        from ....nn.quant import _dequant
+
+        rows = N // 2 if wd == "int4" else N
+        q = wt[e].reshape(rows, K)
+        return _dequant(q, scale._t[e], wd, -1, t.dtype).t()  # [K, N]
+
+    N1 = ffn1_scale._t.shape[-1] if quant else w1.shape[-1]
+    F = N1 // 2
+    N2 = ffn2_scale._t.shape[-1] if quant else w2.shape[-1]
     flat_e = idx.reshape(-1)
     order = torch.argsort(flat_e, stable=True)
     tok = order // moe_topk
     gate = w.reshape(-1)[order]
     counts = torch.bincount(flat_e, minlength=E).tolist()
     xs = t2.index_select(0, tok)
-    ys = torch.empty(xs.shape[0], w2.shape[-1], dtype=t.dtype, device=t.device)
+    ys = torch.empty(xs.shape[0], N2, dtype=t.dtype, device=t.device)
     start = 0
     for e, c in enumerate(counts):
         if c == 0:
             continue
         seg = xs[start:start + c]
-        h = seg @ w1[e]
+        h = seg @ expert_w(w1, ffn1_scale, e, Hd, N1)
         if ffn1_bias is not None:
-            h = h + ffn1_bias._t[e]
+            h = h + ffn1_bias._t[e].reshape(-1)
         h = T.swiglu(h)
-        o = h @ w2[e]
+        o = h @ expert_w(w2, ffn2_scale, e, F, N2)
         if ffn2_bias is not None:
-            o = o + ffn2_bias._t[e]
+            o = o + ffn2_bias._t[e].reshape(-1)
         ys[start:start + c] = o
         start += c
-    out = torch.zeros(n_tok, ys.shape[-1], dtype=torch.float32, device=t.device)
+    out = torch.zeros(n_tok, N2, dtype=torch.float32, device=t.device)
     out.index_add_(0, tok, ys.float() * gate[:, None])
-    return _wrap(out.to(t.dtype).reshape(shp))
+    return _wrap(out.to(t.dtype).reshape(*shp[:-1], N2))

@@ -515,7 +515,11 @@ class _SoftmaxMaskFn(torch.autograd.Function):
         y = torch.empty_like(xc)
         mc = None
         if not causal:
-            mc = mask.to(x.dtype).expand(B, 1, Sq, Sk).contiguous()
+            m = mask
+            if m.dtype != x.dtype:
+                # keep an fp32 mask's large negatives finite in a 16-bit x (fp16 would round -1e9 to -inf)
+                m = m.float().clamp(min=torch.finfo(x.dtype).min)
+            mc = m.to(x.dtype).expand(B, 1, Sq, Sk).contiguous()
         N.native().softmax_mask_fwd(_DT[x.dtype], int(causal), xc.data_ptr(), 0 if mc is None else mc.data_ptr(),
                                     y.data_ptr(), B * H * Sq, H, Sq, Sk, N.stream())
         ctx.save_for_backward(y)
@@ -544,6 +548,9 @@ def softmax_mask(x, mask=None, causal=False):
         raise ValueError("softmax_mask_fuse needs a mask")
     if Sk > 8192:
         raise ValueError(f"fused masked softmax supports key length <= 8192, got {Sk}")
+    if not causal and (mask.dim() != 4 or mask.shape[1] != 1):
+        # reference fused_softmax_mask_kernel.cu checks mask dim1 == 1 (one mask shared by all heads)
+        raise ValueError(f"softmax_mask_fuse expects a [B, 1, Sq, Sk] mask, got {tuple(mask.shape)}")
     if N.use_native(x) and x.dtype in _DT:
         return _SoftmaxMaskFn.apply(x, mask, causal)
     return _softmax_mask_reference(x, mask, causal)

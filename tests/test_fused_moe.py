@@ -38,7 +38,40 @@ def test_fused_moe_matches_dense(dev, k):
     w2 = torch.randn(E, F, H, generator=g) / F ** 0.5
     b2 = torch.randn(E, H, generator=g) * 0.1
     P = lambda a: paddle.to_tensor(a.to(dev, dt))  # noqa: E731
-    out = fused_moe(P(x), paddle.to_tensor(gw.to(dev)), P(w1), None, P(b1), P(w2), None, P(b2), moe_topk=k)
+    # positional call in the reference order (test_fused_moe_op.py:168): x, gate, w1, w2, b1, s1, b2, s2, quant, k, norm
+    out = fused_moe(P(x), paddle.to_tensor(gw.to(dev)), P(w1), P(w2), P(b1.reshape(E, 1, 2 * F)), None,
+                    P(b2.reshape(E, 1, H)), None, "None", k, True)
     ref = _dense_ref(x, gw, w1.to(dt).float(), b1.to(dt).float(), w2.to(dt).float(), b2.to(dt).float(), k)
     tol = 1e-4 if dt == torch.float32 else 5e-2
     torch.testing.assert_close(out._t.float().cpu(), ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("algo", ["weight_only_int8", "weight_only_int4"])
+def test_fused_moe_weight_only(algo):
+    """quant_method: expert weights from nn.quant.weight_quantize (reshaped to the float weight's shape as in
+    the reference test) + per-channel scales == the same MoE on the dequantized weights."""
+    from paddle2_amd.nn.quant import weight_dequantize, weight_quantize
+
+    g = torch.Generator().manual_seed(7)
+    B, S, H, F, E, k = 2, 8, 64, 64, 4, 2
+    x = torch.randn(B, S, H, generator=g)
+    gw = torch.randn(H, E, generator=g)
+    w1 = torch.randn(E, H, 2 * F, generator=g) / H ** 0.5
+    w2 = torch.randn(E, F, H, generator=g) / F ** 0.5
+    q1, s1, q2, s2, d1, d2 = [], [], [], [], [], []
+    for e in range(E):
+        qa, sa = weight_quantize(paddle.to_tensor(w1[e]), algo=algo)
+        qb, sb = weight_quantize(paddle.to_tensor(w2[e]), algo=algo)
+        d1.append(weight_dequantize(qa, sa, algo=algo, out_dtype="float32")._t)
+        d2.append(weight_dequantize(qb, sb, algo=algo, out_dtype="float32")._t)
+        q1.append(qa._t.reshape(H, -1))
+        q2.append(qb._t.reshape(F, -1))
+        s1.append(sa._t)
+        s2.append(sb._t)
+    P = paddle.to_tensor
+    out = fused_moe(P(x), P(gw), P(torch.stack(q1)), P(torch.stack(q2)), None, P(torch.stack(s1)), None,
+                    P(torch.stack(s2)), algo, k, True)
+    ref = fused_moe(P(x), P(gw), P(torch.stack(d1)), P(torch.stack(d2)), None, None, None, None, "None", k, True)
+    torch.testing.assert_close(out._t, ref._t, rtol=1e-4, atol=1e-4)
+    with pytest.raises(ValueError):
+        fused_moe(P(x), P(gw), P(torch.stack(q1)), P(torch.stack(q2)), None, None, None, None, algo, k, True)

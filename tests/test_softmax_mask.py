@@ -79,3 +79,49 @@ def test_softmax_mask_hip_max_len():
     m = torch.zeros(1, 1, 4, 8192, device="cuda", dtype=torch.bfloat16)
     y = paddle.incubate.softmax_mask_fuse(paddle.to_tensor(x), paddle.to_tensor(m))._t
     torch.testing.assert_close(y.float(), _ref(x, m, False), rtol=1e-2, atol=1e-4)
+
+
+def _flpga_bf16_case(device):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 300, 64, generator=g).to(torch.bfloat16)
+    dy = torch.randn(2, 300, 48, generator=g).to(torch.bfloat16)
+    dw0 = torch.randn(64, 48, generator=g)
+    ref = dw0.double() + x.reshape(-1, 64).double().t() @ dy.reshape(-1, 48).double()
+    dw, _ = _C_ops.fused_linear_param_grad_add(paddle.to_tensor(x.to(device)), paddle.to_tensor(dy.to(device)),
+                                               paddle.to_tensor(dw0.clone().to(device)), None, True, False)
+    assert dw._t.dtype == torch.float32
+    # fp32 accumulation of exact bf16 products: far below one bf16 ulp of the product
+    err = float((dw._t.double().cpu() - ref).abs().max() / ref.abs().max())
+    assert err < 1e-6, err
+
+
+def test_fused_linear_param_grad_add_bf16_fp32_main_grad_cpu():
+    _flpga_bf16_case("cpu")
+
+
+@pytest.mark.gpu
+def test_fused_linear_param_grad_add_bf16_fp32_main_grad_gpu():
+    _flpga_bf16_case("cuda")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [4097, 1001])
+def test_softmax_mask_ragged_long_rows_gpu(S):
+    """Sk not a multiple of the 16-byte vector (scalar-chunk path): fwd + bwd vs fp32."""
+    g = torch.Generator().manual_seed(S)
+    x = (torch.randn(1, 2, 8, S, generator=g) * 3).to("cuda", torch.bfloat16).requires_grad_(True)
+    m = torch.where(torch.rand(1, 1, 8, S, generator=g) > 0.2, 0.0, -1e9)  # fp32 mask, huge negatives
+    y = T.softmax_mask(x, m.to("cuda"), causal=False)
+    ref = _ref(x.detach(), m.to("cuda", torch.float32), False)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+    dy = torch.randn(1, 2, 8, S, generator=g).to("cuda", torch.bfloat16)
+    (dx,) = torch.autograd.grad(y, x, dy)
+    yf = ref
+    dref = yf * (dy.float() - (dy.float() * yf).sum(-1, keepdim=True))
+    torch.testing.assert_close(dx.float(), dref, rtol=2e-2, atol=2e-2)
+
+
+def test_softmax_mask_rejects_per_head_mask():
+    x = torch.randn(1, 2, 4, 8)
+    with pytest.raises(ValueError):
+        T.softmax_mask(x, torch.zeros(1, 2, 4, 8))
