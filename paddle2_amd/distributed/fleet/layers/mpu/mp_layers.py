@@ -98,9 +98,9 @@ class ColumnParallelLinear(nn.Layer):
         if self.is_mp:
             y = mp_ops._ColumnLinear.apply(x._t, self.weight._t, b, self.model_parallel_group)
         else:
-            y = torch.matmul(x._t, self.weight._t)
-            if b is not None:
-                y = y + b
+            from .....ops import torch_ops as T
+
+            y = T.linear(x._t, self.weight._t, b)
         out = _wrap(y)
         if self.gather_output and self.is_mp:
             out = mp_ops._c_concat(out, group=self.model_parallel_group)
@@ -129,7 +129,10 @@ class RowParallelLinear(nn.Layer):
     def forward(self, x):
         if self.is_mp and not self.input_is_parallel:
             x = mp_ops._c_split(x, group=self.model_parallel_group)
-        y = _wrap(torch.matmul(x._t, self.weight._t))
+        from .....ops import torch_ops as T
+
+        # the Linear node (native GEMMs, fp32 main-grad accumulation) then the mp all-reduce of the partials
+        y = _wrap(T.linear(x._t, self.weight._t))
         if self.is_mp:
             y = mp_ops._mp_allreduce(y, group=self.model_parallel_group)
         if self.bias is not None:

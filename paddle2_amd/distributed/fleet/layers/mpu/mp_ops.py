@@ -16,6 +16,7 @@ import torch.distributed as dist
 
 from .....framework.tensor import Tensor
 from .....ops import _native as N
+from .....ops import torch_ops as T
 from ....collective import _get_default_group
 
 _wrap = Tensor._wrap
@@ -154,19 +155,19 @@ class _ColumnLinear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, group):
-        ctx.save_for_backward(x, w)
-        ctx.group, ctx.has_b = group, b is not None
-        y = torch.matmul(x, w)
-        return y + b if b is not None else y
+        x2 = x.reshape(-1, x.shape[-1])
+        ctx.save_for_backward(x2, w)
+        ctx.group, ctx.has_b, ctx.xshape = group, b is not None, x.shape
+        ctx.gt = getattr(w, "_p2_gt", None)
+        return T.mm(x2, w, b).view(*x.shape[:-1], w.shape[1])
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
-        dx = torch.matmul(dy, w.t())
+        x2, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dx = T.mm_t(dy2, w).view(ctx.xshape)
         work = _allreduce_(dx, ctx.group, async_op=True)
-        x2 = x.reshape(-1, x.shape[-1])
-        dy2 = dy.reshape(-1, dy.shape[-1])
-        dw = torch.matmul(x2.t(), dy2) if ctx.needs_input_grad[1] else None
+        dw = T.weight_grad(x2, dy2, ctx.gt) if ctx.needs_input_grad[1] else None
         db = dy2.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
         if work is not None:
             work.wait()
@@ -182,19 +183,19 @@ class _SeqColumnLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, group):
         xf = _allgather_dim(x, group, 0)
-        ctx.save_for_backward(xf, w)
-        ctx.group, ctx.has_b = group, b is not None
-        y = torch.matmul(xf, w)
-        return y + b if b is not None else y
+        x2 = xf.reshape(-1, xf.shape[-1])
+        ctx.save_for_backward(x2, w)
+        ctx.group, ctx.has_b, ctx.xfshape = group, b is not None, xf.shape
+        ctx.gt = getattr(w, "_p2_gt", None)
+        return T.mm(x2, w, b).view(*xf.shape[:-1], w.shape[1])
 
     @staticmethod
     def backward(ctx, dy):
-        xf, w = ctx.saved_tensors
-        dxf = torch.matmul(dy, w.t())
+        x2, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dxf = T.mm_t(dy2, w).view(ctx.xfshape)
         dx, work = _reduce_scatter_dim0(dxf, ctx.group, async_op=True)
-        x2 = xf.reshape(-1, xf.shape[-1])
-        dy2 = dy.reshape(-1, dy.shape[-1])
-        dw = torch.matmul(x2.t(), dy2) if ctx.needs_input_grad[1] else None
+        dw = T.weight_grad(x2, dy2, ctx.gt) if ctx.needs_input_grad[1] else None
         db = dy2.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
         if work is not None:
             work.wait()
@@ -207,19 +208,21 @@ class _SeqRowLinear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, group):
-        ctx.save_for_backward(x, w)
-        ctx.group = group
-        y = torch.matmul(x, w)
+        x2 = x.reshape(-1, x.shape[-1])
+        ctx.save_for_backward(x2, w)
+        ctx.group, ctx.xshape = group, x.shape
+        ctx.gt = getattr(w, "_p2_gt", None)
+        y = T.mm(x2, w).view(*x.shape[:-1], w.shape[1])
         out, _ = _reduce_scatter_dim0(y, group)
         return out
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        x2, w = ctx.saved_tensors
         dyf = _allgather_dim(dy, ctx.group, 0)
-        dx = torch.matmul(dyf, w.t())
-        dw = torch.matmul(x.reshape(-1, x.shape[-1]).t(), dyf.reshape(-1, dyf.shape[-1])) \
-            if ctx.needs_input_grad[1] else None
+        dy2 = dyf.reshape(-1, dyf.shape[-1]).contiguous()
+        dx = T.mm_t(dy2, w).view(ctx.xshape)
+        dw = T.weight_grad(x2, dy2, ctx.gt) if ctx.needs_input_grad[1] else None
         return dx, dw, None
 
 

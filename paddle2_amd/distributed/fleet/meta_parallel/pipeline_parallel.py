@@ -16,6 +16,13 @@ the same simulation and post it in the same tick's group, the schedule is deadlo
 construction for any ordering (1F1B, FThenB, VPP with wrap-around ``S-1 -> 0`` hand-offs), and
 RCCL runs each group's transfers concurrently over the xGMI peer links.  Shapes/dtypes cross each
 stage boundary once (a small meta handshake on first use), then buffers are allocated directly.
+
+Overlap: a tick's group is posted and NOT waited — receives are waited only when the unit that
+consumes them runs (a stream dependency on RCCL, so compute of the next units overlaps the transfer),
+sends when the schedule drains.  With tensor parallelism the activations / input grads crossing a stage
+boundary are replicated over the mp group, so each mp rank sends only its 1/mp slice and the receiver
+all-gathers the slices over mp (the reference's partial_send / partial_recv / partial_allgather,
+pp_utils/p2p_communication.py:256-283): the xGMI pipe traffic drops by mp x.
 """
 from __future__ import annotations
 
@@ -147,6 +154,18 @@ def _is_float(t):
     return t.is_floating_point()
 
 
+class _GroupWait:
+    """Waits a batch's works exactly once (gloo send/recv works block on a second wait)."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works = []
+
+
 class PipelineParallel(MetaParallelBase):
     _schedule = "1F1B"
 
@@ -162,6 +181,8 @@ class PipelineParallel(MetaParallelBase):
         self._V = layers.get_num_virtual_stages() if hasattr(layers, "get_num_virtual_stages") else 1
         self._meta_cache = {}
         self._sim_cache = {}
+        self._send_works = []   # this schedule's posted groups, drained when it ends
+        self._send_keep = []    # send buffers kept alive until then
         self._device = None
         self._shared_groups = self._make_shared_groups()
         self._sync_shared_weights()
@@ -246,12 +267,13 @@ class PipelineParallel(MetaParallelBase):
     def _comm_on_device(self):
         return self.pp_group.backend == "nccl"
 
-    def _exchange(self, ops):
-        """ops: list of (is_send, tensor, peer_stage) -> one batched group.  Each tensor of a transfer
-        gets its own tag (its index among the ops with that peer and direction) so transports that
-        match by (peer, tag) rather than by issue order (gloo) pair them correctly."""
+    def _exchange(self, ops, wait=True, tick=0):
+        """ops: list of (is_send, tensor, peer_stage) -> one batched group; returns its works (waited here
+        when ``wait``).  Each tensor of a transfer gets its own tag (tick-salted index among the ops with
+        that peer and direction) so transports that match by (peer, tag) rather than by issue order (gloo)
+        pair them correctly even with several ticks' groups in flight."""
         if not ops:
-            return
+            return []
         seen = {}
         p2p = []
         for s, t, st in ops:
@@ -259,9 +281,39 @@ class PipelineParallel(MetaParallelBase):
             tag = seen.get(k, 0)
             seen[k] = tag + 1
             p2p.append(dist.P2POp(dist.isend if s else dist.irecv, t, self._peer(st), group=self.pp_group.pg,
-                                  tag=tag))
-        for w in dist.batch_isend_irecv(p2p):
-            w.wait()
+                                  tag=(tick % 4096) * 64 + tag))
+        works = dist.batch_isend_irecv(p2p)
+        if wait:
+            for w in works:
+                w.wait()
+            return []
+        return works
+
+    # ----------------------------------------------------------------- partial send / recv over mp
+    def _partial_mp(self):
+        """mp group when boundary tensors are replicated over it (TP without sequence parallel)."""
+        if not hasattr(self, "_pmp"):
+            pc = dict(self._strategy.pipeline_configs) if self._strategy is not None else {}
+            cfg = getattr(self._layers, "config", None) or getattr(self._layers, "_config", None)
+            sp = bool(getattr(cfg, "sequence_parallel", False))
+            g = self._hcg.get_model_parallel_group()
+            on = pc.get("enable_partial_send_recv", True) and not sp and g.nranks > 1
+            self._pmp = g if on else None
+        return self._pmp
+
+    def _slice_of(self, t):
+        g = self._partial_mp()
+        if g is None or t.numel() % g.nranks:
+            return None
+        n = t.numel() // g.nranks
+        return t.reshape(-1)[g.rank * n:(g.rank + 1) * n]
+
+    def _gather_partial(self, full):
+        g = self._partial_mp()
+        n = full.numel() // g.nranks
+        flat = full.reshape(-1)
+        mine = flat[g.rank * n:(g.rank + 1) * n].clone()
+        dist.all_gather_into_tensor(flat, mine, group=g.pg)
 
     # ----------------------------------------------------------------- engine
     def _run_schedule(self, data, scaler=None, forward_only=False, compute_loss=True):
@@ -294,7 +346,7 @@ class PipelineParallel(MetaParallelBase):
                         x = in_mb[mb]
                         xin = None
                     else:
-                        ts = recv_buf.pop(("F", vs - 1, mb))
+                        ts = self._take(recv_buf, ("F", vs - 1, mb))
                         xin = tuple(tt.requires_grad_(rg and _is_float(tt)) for tt, rg in ts)
                         x = _unflat(xin)
                     ctx = torch.enable_grad() if not forward_only else torch.no_grad()
@@ -327,7 +379,7 @@ class PipelineParallel(MetaParallelBase):
                             l = outs[0]
                         torch.autograd.backward(l)
                     else:
-                        grads = recv_buf.pop(("B", vs + 1, mb))
+                        grads = self._take(recv_buf, ("B", vs + 1, mb))
                         pairs = [(o, g) for o, g in zip(outs, grads) if isinstance(o, torch.Tensor) and o.requires_grad
                                  and g is not None]
                         if pairs:
@@ -337,13 +389,25 @@ class PipelineParallel(MetaParallelBase):
                         pending_send[("B", vs, mb)] = tuple(
                             (tt.grad if tt.grad is not None else torch.zeros_like(tt)) if tt.requires_grad else None
                             for tt in xin)
-            # ---- communication for this tick
+            # ---- communication for this tick (posted, not waited: see _take / the drain below)
             cl = my_comms.get(t)
             if cl:
-                self._tick_exchange(cl, pending_send, recv_buf)
+                self._tick_exchange(cl, pending_send, recv_buf, t)
+        for w in self._send_works:
+            w.wait()
+        self._send_works = []
+        self._send_keep = []
         return losses, outputs
 
-    def _tick_exchange(self, cl, pending_send, recv_buf):
+    def _take(self, recv_buf, key):
+        """Consume a received boundary: wait for its transfer (and all-gather partial slices over mp)."""
+        bufs, token, partial = recv_buf.pop(key)
+        token.wait()
+        for b in partial:
+            self._gather_partial(b)
+        return bufs
+
+    def _tick_exchange(self, cl, pending_send, recv_buf, tick=0):
         meta_ops, meta_recv = [], []
         for op, peer, key in cl:
             kind, vs, mb = key
@@ -363,27 +427,44 @@ class PipelineParallel(MetaParallelBase):
             for bkey, buf in meta_recv:
                 self._meta_cache[bkey] = self._decode_meta(buf)
         ops = []
+        partial_of = {}
         for op, peer, key in cl:
             kind, vs, mb = key
             if op == "send":
                 for t in pending_send[key]:
                     if t is not None:
-                        ops.append((True, t.detach().contiguous(), peer))
+                        src = t.detach().contiguous()
+                        part = self._slice_of(src)
+                        ops.append((True, src if part is None else part, peer))
+                        self._send_keep.append(src)
             else:
                 bmeta = self._meta_cache[vs if kind == "F" else vs - 1]
-                bufs = []
+                bufs, partial = [], []
                 for dt, rg, shp in bmeta:
                     if kind == "B" and not (rg and dt.is_floating_point):
                         bufs.append(None)
                         continue
                     b = torch.empty(shp, dtype=dt, device=self._device)
-                    ops.append((False, b, peer))
+                    part = self._slice_of(b)
+                    ops.append((False, b if part is None else part, peer))
+                    if part is not None:
+                        partial.append(b)
                     bufs.append(b)
                 if kind == "F":
                     recv_buf[key] = [(b, rg) for b, (dt, rg, shp) in zip(bufs, bmeta)]
                 else:
                     recv_buf[key] = bufs
-        self._exchange(ops)
+                partial_of[key] = partial
+        works = self._exchange(ops, wait=False, tick=tick)
+        # works pair 1:1 with ops; each is waited exactly once (a second wait on a gloo send/recv work
+        # blocks): receives when their consumer runs, sends when the schedule drains
+        recv_works = [w for w, (is_send, _, _) in zip(works, ops) if not is_send]
+        send_works = [w for w, (is_send, _, _) in zip(works, ops) if is_send]
+        token = _GroupWait(recv_works)  # the tick's receives complete together; waited once, by any consumer
+        for op, peer, key in cl:
+            if op == "recv":
+                recv_buf[key] = (recv_buf[key], token, partial_of[key])
+        self._send_works.extend(send_works)
         for op, peer, key in cl:
             if op == "send":
                 pending_send.pop(key, None)

@@ -407,6 +407,39 @@ def wgrad_accumulate(out, x2, dy2, beta):
     return out
 
 
+def mm(x2, w, b=None):
+    """y[M, N] = x2[M, K] @ w[K, N] (+ b): the Linear forward GEMM (native MFMA kernel or hipBLASLt per
+    _GEMM_PASS), shared by nn.Linear and the tensor-/sequence-parallel linears."""
+    from . import gemm as G
+
+    if x2.dim() == 2 and _pass_native("fwd", x2) and G.supported_fwd(x2, w) and (b is None or b.dtype == x2.dtype):
+        return G.mm_fwd(x2, w, bias=None if b is None else b.contiguous())
+    y = torch.matmul(x2, w)
+    return y + b if b is not None else y
+
+
+def mm_t(dy2, w):
+    """dx[M, K] = dy2[M, N] @ w[K, N]^T (the Linear input-gradient GEMM)."""
+    from . import gemm as G
+
+    if dy2.dim() == 2 and _pass_native("dgrad", dy2) and G.supported_dgrad(dy2, w):
+        return G.mm_dgrad(dy2, w)
+    return torch.matmul(dy2, w.t())
+
+
+def weight_grad(x2, dy2, gt=None):
+    """dW = x2^T @ dy2.  With a main-grad target ``gt`` the product accumulates in fp32 straight into it
+    and None is returned (the autograd engine then never materialises a 16-bit dW)."""
+    if gt is not None:
+        _main_grad_accumulate(gt, x2, dy2)
+        return None
+    from . import gemm as G
+
+    if _pass_native("wgrad", x2) and G.supported_wgrad(x2, dy2):
+        return G.mm_wgrad_bf16(x2, dy2)
+    return torch.matmul(x2.t(), dy2)
+
+
 def _main_grad_accumulate(gt, x2, dy2):
     """Weight gradient straight into the owner's fp32 main-grad buffer (group-sharded unit / main_grad):
     ``gt`` = (owner, index) with owner.grad_target(index) -> (fp32 view, beta) and owner.param_grad_done."""

@@ -48,11 +48,12 @@ def test_pipeline_llama_matches_single():
     _close(run_workers("hybrid_worker.py", 2, ["pp_llama", "1"]), 1e-4)
 
 
-def test_tp2_pp2_llama_trains():
+def test_tp2_pp2_llama_matches_single():
+    """TP2 x PP2 (1F1B, overlapped p2p with mp partial send/recv) == one process on the gathered weights."""
     res = run_workers("hybrid_worker.py", 4, ["pp_llama", "2"])
     for r in res:
         assert r["losses"] == res[0]["losses"]  # loss broadcast over the pipe group, identical over mp
-        assert r["losses"][1] < r["losses"][0] + 1.0
+    _close(res, 1e-3)
 
 
 def test_gpt_sequence_parallel_matches_tensor_parallel():

@@ -256,7 +256,8 @@ def run_pp_llama(mp):
     M = 2
     strategy = fleet.DistributedStrategy()
     strategy.hybrid_configs = {"dp_degree": 1, "mp_degree": mp, "pp_degree": pp}
-    strategy.pipeline_configs = {"accumulate_steps": M, "micro_batch_size": 1}
+    strategy.pipeline_configs = {"accumulate_steps": M, "micro_batch_size": 1,
+                                 "enable_partial_send_recv": os.environ.get("PD_PARTIAL", "1") == "1"}
     fleet.init(is_collective=True, strategy=strategy)
     cfg = LlamaConfig.tiny(dtype="float32", num_hidden_layers=4, tensor_parallel_degree=mp)
     g = torch.Generator().manual_seed(8)
@@ -266,13 +267,37 @@ def run_pp_llama(mp):
     model = fleet.distributed_model(pipe)
     opt = fleet.distributed_optimizer(paddle.optimizer.SGD(0.5, parameters=model.parameters()))
     full = {}
-    if mp == 1:
+    hcg = fleet.get_hybrid_communicate_group()
+    mpg = hcg.get_model_parallel_group()
+
+    def full_param(name, p):
+        """gather a tensor-parallel shard over the mp group (concat along its split axis); fused per-rank
+        [q_r|k_r|v_r] / [gate_r|up_r] column shards are re-assembled into the single-process layout"""
+        t = p._t.detach().contiguous()
+        if mp == 1 or not getattr(p, "is_distributed", False):
+            return t.clone()
+        parts = [torch.empty_like(t) for _ in range(mp)]
+        torch.distributed.all_gather(parts, t, group=mpg.pg)
+        if "qkv_proj" in name:
+            d = cfg.head_dim
+            nh, nkv = cfg.num_attention_heads // mp, cfg.num_key_value_heads // mp
+            qs = [x[:, :nh * d] for x in parts]
+            ks = [x[:, nh * d:(nh + nkv) * d] for x in parts]
+            vs = [x[:, (nh + nkv) * d:] for x in parts]
+            return torch.cat(qs + ks + vs, dim=1)
+        if "gate_up_fused_proj" in name:
+            f = t.shape[1] // 2
+            return torch.cat([x[:, :f] for x in parts] + [x[:, f:] for x in parts], dim=1)
+        return torch.cat(parts, dim=p.split_axis)
+
+    if True:
         # single-process reference with the same weights (pipe param names -> LlamaForCausalLM names)
         for c, vs in enumerate(pipe._chunk_vstages):
             lo = pipe.segment_parts[vs]
             for i, item in enumerate(pipe._model_chunks[c]._items):
                 idx = lo + i
-                for k, v in item.state_dict().items():
+                for k, p in item.named_parameters():
+                    v = paddle.Tensor._wrap(full_param(k, p))
                     if idx == 0:
                         name = "llama." + k
                     elif idx <= cfg.num_hidden_layers:
@@ -287,7 +312,7 @@ def run_pp_llama(mp):
         ids = paddle.Tensor._wrap(ids)
         losses.append(float(model.train_batch([ids[:, :-1], ids[:, 1:]], opt)))
     out = {"losses": losses}
-    if mp == 1:
+    if True:
         objs = [None] * world
         torch.distributed.all_gather_object(objs, {k: v.numpy() for k, v in full.items()})
         merged = {}
