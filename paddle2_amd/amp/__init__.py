@@ -16,11 +16,67 @@ import torch
 from ..framework import dtype as _dt
 from ..framework.tensor import Tensor
 
-_amp_state = {"enable": False, "level": "O0", "dtype": torch.bfloat16}
+_amp_state = {"enable": False, "level": "O0", "dtype": torch.bfloat16, "white": frozenset(), "black": frozenset()}
 
+# Default op lists (reference python/paddle/amp/amp_lists.py): white ops run in the AMP dtype, black ops
+# in fp32.  torch.autocast applies the equivalent defaults to the ATen ops underneath; the lists matter
+# for the ops the user moves with custom_white_list / custom_black_list, which ``amp_op`` enforces at
+# this framework's op entry points (nn.functional / tensor APIs decorated with @amp_op).
 WHITE_LIST = {"matmul", "linear", "conv2d", "conv1d", "conv3d", "einsum", "bmm", "mm", "flash_attn",
               "scaled_dot_product_attention"}
-BLACK_LIST = {"exp", "log", "softmax", "cross_entropy", "layer_norm", "batch_norm", "reduce_sum", "mean"}
+BLACK_LIST = {"exp", "log", "softmax", "log_softmax", "cross_entropy", "layer_norm", "batch_norm", "reduce_sum",
+              "sum", "mean"}
+
+
+def _effective_lists(custom_white, custom_black):
+    cw, cb = set(custom_white or ()), set(custom_black or ()),
+    if cw & cb:
+        raise ValueError(f"auto_cast: ops in both custom_white_list and custom_black_list: {sorted(cw & cb)}")
+    return frozenset((WHITE_LIST | cw) - cb), frozenset((BLACK_LIST | cb) - cw)
+
+
+def op_policy(name):
+    """'low' (run in the AMP dtype), 'fp32', or None (leave it to autocast) for op ``name`` now."""
+    st = _amp_state
+    if not st["enable"] or st["level"] not in ("O1", "O2"):
+        return None
+    if name in st["black"]:
+        return "fp32"
+    if name in st["white"]:
+        return "low"
+    return None
+
+
+def amp_op(name):
+    """Decorator for an op entry point: enforce the current auto_cast op lists for op ``name``
+    (the custom lists override torch.autocast's built-in choice for that op)."""
+    import functools
+
+    def deco(fn):
+        @functools.wraps(fn)
+        def inner(*args, **kw):
+            pol = op_policy(name)
+            if pol is None:
+                return fn(*args, **kw)
+            dt = torch.float32 if pol == "fp32" else _amp_state["dtype"]
+
+            def cast(a):
+                t = a._t if isinstance(a, Tensor) else a
+                if isinstance(t, torch.Tensor) and t.is_floating_point() and t.dtype != dt:
+                    t = t.to(dt)
+                    return Tensor._wrap(t) if isinstance(a, Tensor) else t
+                return a
+
+            args = tuple(cast(a) for a in args)
+            kw = {k: cast(v) for k, v in kw.items()}
+            from ..framework.place import current_torch_device
+
+            with torch.autocast(device_type=current_torch_device().type, enabled=False):
+                return fn(*args, **kw)
+
+        return inner
+
+    return deco
 
 
 def is_float16_supported(device=None):
@@ -40,7 +96,8 @@ def auto_cast(enable=True, custom_white_list=None, custom_black_list=None, level
               use_promote=True):
     dt = _dt.convert_dtype(dtype)
     prev = dict(_amp_state)
-    _amp_state.update(enable=enable, level=level, dtype=dt)
+    white, black = _effective_lists(custom_white_list, custom_black_list)
+    _amp_state.update(enable=enable, level=level, dtype=dt, white=white, black=black)
     from ..framework.place import current_torch_device
 
     dev = current_torch_device().type

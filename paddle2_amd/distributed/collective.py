@@ -603,3 +603,46 @@ class stream:
     @staticmethod
     def gather(tensor, gather_list=None, dst=0, group=None, sync_op=True, use_calc_stream=False):
         return gather(tensor, gather_list, dst, group, sync_op or use_calc_stream)
+
+
+# ----------------------------------------------------------------------------- debug / benchmark flags
+_comm_bench = {}
+
+
+def comm_benchmark_stats():
+    """{collective: [count, total seconds]} recorded while FLAGS_benchmark_nccl is on."""
+    return {k: list(v) for k, v in _comm_bench.items()}
+
+
+def _instrument(name, fn):
+    """FLAGS_nccl_blocking_wait: the collective completes (host-synchronous) before returning;
+    FLAGS_benchmark_nccl: additionally time it (wall, device-synchronised) into comm_benchmark_stats()."""
+    import functools
+    import time
+
+    from ..framework.flags import flag
+
+    @functools.wraps(fn)
+    def inner(*a, **k):
+        block, bench = flag("FLAGS_nccl_blocking_wait"), flag("FLAGS_benchmark_nccl")
+        if not (block or bench):
+            return fn(*a, **k)
+        t0 = time.perf_counter()
+        r = fn(*a, **k)
+        if isinstance(r, _Task):
+            r.wait()
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+        if bench:
+            st = _comm_bench.setdefault(name, [0, 0.0])
+            st[0] += 1
+            st[1] += time.perf_counter() - t0
+        return r
+
+    return inner
+
+
+for _n in ("all_reduce", "broadcast", "reduce", "all_gather", "all_gather_into_tensor", "reduce_scatter",
+           "alltoall", "alltoall_single", "scatter", "send", "recv", "barrier"):
+    if _n in globals() and callable(globals()[_n]):
+        globals()[_n] = _instrument(_n, globals()[_n])

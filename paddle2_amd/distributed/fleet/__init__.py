@@ -21,18 +21,17 @@ class PaddleCloudRoleMaker(UserDefinedRoleMaker):
 
 def init(role_maker=None, is_collective=True, strategy=None, log_level="INFO"):
     strategy = strategy or DistributedStrategy()
+    if not isinstance(strategy, DistributedStrategy):
+        raise TypeError("fleet.init: strategy must be a fleet.DistributedStrategy")
     _state["strategy"] = strategy
     C.init_parallel_env()
     world = C.get_world_size()
     hc = strategy.hybrid_configs
-    mp, pp = int(hc.get("mp_degree", 1)), int(hc.get("pp_degree", 1))
-    sh, sep = int(hc.get("sharding_degree", 1)), int(hc.get("sep_degree", 1))
-    dp = int(hc.get("dp_degree", -1))
-    if dp in (-1, 0):
-        dp = max(1, world // (mp * pp * sh * sep))
-    assert dp * mp * pp * sh * sep == world, f"degrees dp{dp}*mp{mp}*pp{pp}*sharding{sh}*sep{sep} != world {world}"
+    dp = strategy.validate_world(world)  # degrees multiply to the world size, order is a permutation
+    mp, pp = hc["mp_degree"], hc["pp_degree"]
+    sh, sep = hc["sharding_degree"], hc["sep_degree"]
     hc["dp_degree"] = dp
-    order = hc.get("order", ["dp", "pp", "sharding", "sep", "mp"])
+    order = list(hc["order"])
     name_map = {"dp": "data", "pp": "pipe", "sharding": "sharding", "sep": "sep", "mp": "model"}
     deg = {"dp": dp, "pp": pp, "sharding": sh, "sep": sep, "mp": mp}
     topo = CommunicateTopology([name_map[o] for o in order], [deg[o] for o in order])
@@ -79,11 +78,63 @@ def barrier_worker():
     C.barrier()
 
 
+def _apply_model_strategy(model, strategy):
+    """strategy.recompute (recompute_configs.checkpoints) and strategy.amp (amp_configs) on the model."""
+    if strategy.recompute:
+        ckpts = list(strategy.recompute_configs["checkpoints"])
+        cfg = getattr(model, "config", None)
+        if not ckpts and cfg is not None and hasattr(cfg, "recompute"):
+            cfg.recompute = True  # model-native per-layer recompute (e.g. Llama / GPT decoder layers)
+        else:
+            from .recompute import recompute
+
+            named = dict(model.named_sublayers())
+            missing = [c for c in ckpts if c not in named]
+            if missing:
+                raise ValueError(f"recompute_configs.checkpoints: no sublayer named {missing}")
+            for name in ckpts:
+                layer = named[name]
+                fwd = layer.forward
+
+                def wrapped(*a, _fwd=fwd, **k):
+                    return recompute(_fwd, *a, **k)
+
+                layer.forward = wrapped
+    if strategy.amp:
+        model = _AmpModel(model, strategy.amp_configs)
+    return model
+
+
+class _AmpModel:
+    """Runs the wrapped layer's forward under auto_cast with the strategy's amp_configs."""
+
+    def __init__(self, layer, cfg):
+        self._layer = layer
+        self._cfg = cfg
+
+    def __call__(self, *a, **k):
+        from ...amp import auto_cast
+
+        c = self._cfg
+        pure = c["use_pure_fp16"] or c["use_pure_bf16"]
+        with auto_cast(enable=True, custom_white_list=set(c["custom_white_list"]) or None,
+                       custom_black_list=set(c["custom_black_list"]) or None, level="O2" if pure else "O1",
+                       dtype="bfloat16" if c["use_pure_bf16"] else "float16"):
+            return self._layer(*a, **k)
+
+    forward = __call__
+
+    def __getattr__(self, name):
+        return getattr(self._layer, name)
+
+
 def distributed_model(model):
-    """Wrap by parallel mode (reference fleet/model.py:32-179)."""
+    """Wrap by parallel mode (reference fleet/model.py:32-179), after applying the strategy's recompute /
+    amp settings."""
     hcg = _hcg()
     mode = hcg.get_parallel_mode()
     strategy = _state["strategy"]
+    model = _apply_model_strategy(model, strategy)
     if mode == ParallelMode.DATA_PARALLEL:
         from ..parallel import DataParallel
 

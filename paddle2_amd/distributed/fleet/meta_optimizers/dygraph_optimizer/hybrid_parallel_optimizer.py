@@ -199,6 +199,13 @@ class HybridParallelOptimizer:
         self._all_params = list(self._inner_opt._all_params) if self._sharding else list(optimizer._parameter_list)
         self._dp_enable = hcg.get_data_parallel_world_size() > 1
         self._sep_enable = hcg.get_sep_parallel_world_size() > 1
+        # strategy knobs: fused dp all-reduce bucket (fuse_grad_size_in_MB), gradient merge (k-step
+        # accumulation; avg divides the merged grads by k)
+        self._dp_bucket_mb = int(getattr(strategy, "fuse_grad_size_in_MB", 32)) if strategy is not None else 32
+        gm = strategy is not None and bool(getattr(strategy, "gradient_merge", False))
+        self._gm_k = int(strategy.gradient_merge_configs["k_steps"]) if gm else 1
+        self._gm_avg = bool(strategy.gradient_merge_configs["avg"]) if gm else True
+        self._gm_count = 0
 
     def _sp_params(self):
         return [p for p in self._all_params if getattr(p, "sequence_parallel", False)]
@@ -217,12 +224,22 @@ class HybridParallelOptimizer:
             self._inner_opt.reduce_gradients(self._all_params, hcg)
             if self._dp_enable or self._sep_enable:
                 owned = self._inner_opt._rank2params[self._inner_opt._rank]
-                fused_allreduce_gradients(owned, hcg)
+                fused_allreduce_gradients(owned, hcg, self._dp_bucket_mb)
         elif self._dp_enable or self._sep_enable:
-            fused_allreduce_gradients(self._all_params, hcg)
+            fused_allreduce_gradients(self._all_params, hcg, self._dp_bucket_mb)
 
     @torch.no_grad()
     def step(self):
+        if self._gm_k > 1:
+            # gradient merge: the first k-1 calls only accumulate (clear_grad is a no-op for them)
+            self._gm_count += 1
+            if self._gm_count % self._gm_k:
+                return
+            if self._gm_avg:
+                for p in self._all_params:
+                    g = _grad_tensor(p)
+                    if g is not None:
+                        g.div_(self._gm_k)
         self._hybrid_sync_grad()
         self._inner_opt.step()
 
@@ -231,6 +248,8 @@ class HybridParallelOptimizer:
         return None, None
 
     def clear_grad(self, set_to_zero=True):
+        if self._gm_k > 1 and self._gm_count % self._gm_k:
+            return  # still merging gradients
         self._inner_opt.clear_grad(set_to_zero)
 
     clear_gradients = clear_grad

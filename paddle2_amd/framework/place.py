@@ -137,6 +137,9 @@ def set_device(device):
         if not _gpu_available():
             raise ValueError("no HIP/GPU device is available")
         torch.cuda.set_device(d)
+        from .flags import apply_memory_limit
+
+        apply_memory_limit(d.index or 0)  # FLAGS_gpu_memory_limit_mb / FLAGS_fraction_of_gpu_memory_to_use
     _current_device = d
     return place_of_device(d)
 

@@ -5,6 +5,7 @@ import torch
 import torch.nn.functional as F
 
 from ...framework.tensor import Tensor
+from ...amp import amp_op as _amp_op  # noqa: E402
 
 _wrap = Tensor._wrap
 
@@ -138,6 +139,7 @@ def maxout(x, groups, axis=1, name=None):
     return _wrap(t.reshape(new).amax(ax + 1))
 
 
+@_amp_op("softmax")
 def softmax(x, axis=-1, dtype=None, name=None):
     t = x._t
     if dtype is not None:
@@ -153,6 +155,7 @@ def softmax_(x, axis=-1, dtype=None, name=None):
     return x
 
 
+@_amp_op("log_softmax")
 def log_softmax(x, axis=-1, dtype=None, name=None):
     t = x._t
     if dtype is not None:

@@ -10,10 +10,12 @@ import torch.nn.functional as F
 
 from ...framework.tensor import Tensor
 from ...tensor._helpers import shape_arg, ut
+from ...amp import amp_op as _amp_op  # noqa: E402
 
 _wrap = Tensor._wrap
 
 
+@_amp_op("linear")
 def linear(x, weight, bias=None, name=None):
     t = x._t
     w = weight._t

@@ -11,6 +11,7 @@ import torch
 import torch.nn.functional as F
 
 from ...framework.tensor import Tensor
+from ...amp import amp_op as _amp_op  # noqa: E402
 
 _wrap = Tensor._wrap
 
@@ -88,14 +89,17 @@ def _conv(x, weight, bias, stride, padding, dilation, groups, data_format, n):
     return _wrap(out)
 
 
+@_amp_op("conv1d")
 def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCL", name=None):
     return _conv(x, weight, bias, stride, padding, dilation, groups, data_format, 1)
 
 
+@_amp_op("conv2d")
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCHW", name=None):
     return _conv(x, weight, bias, stride, padding, dilation, groups, data_format, 2)
 
 
+@_amp_op("conv3d")
 def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCDHW", name=None):
     return _conv(x, weight, bias, stride, padding, dilation, groups, data_format, 3)
 

@@ -9,6 +9,7 @@ import torch
 import torch.nn.functional as F
 
 from ...framework.tensor import Tensor
+from ...amp import amp_op as _amp_op  # noqa: E402
 
 _wrap = Tensor._wrap
 
@@ -21,6 +22,7 @@ def _reduce(t, reduction):
     return t
 
 
+@_amp_op("cross_entropy")
 def cross_entropy(input, label, weight=None, ignore_index=-100, reduction="mean", soft_label=False, axis=-1,
                   use_softmax=True, label_smoothing=0.0, name=None):
     logits = input._t

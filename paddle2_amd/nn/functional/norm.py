@@ -9,10 +9,12 @@ import torch
 import torch.nn.functional as F
 
 from ...framework.tensor import Tensor
+from ...amp import amp_op as _amp_op  # noqa: E402
 
 _wrap = Tensor._wrap
 
 
+@_amp_op("batch_norm")
 def batch_norm(x, running_mean, running_var, weight=None, bias=None, training=False, momentum=0.9,
                epsilon=1e-05, data_format="NCHW", use_global_stats=None, name=None, act=None, residual=None):
     """Paddle batch_norm; ``act`` ('relu') and ``residual`` (added before the activation) are
@@ -39,6 +41,7 @@ def batch_norm(x, running_mean, running_var, weight=None, bias=None, training=Fa
     return _wrap(out)
 
 
+@_amp_op("layer_norm")
 def layer_norm(x, normalized_shape, weight=None, bias=None, epsilon=1e-05, name=None):
     if isinstance(normalized_shape, int):
         normalized_shape = [normalized_shape]

@@ -669,6 +669,22 @@ class _EmbFn(torch.autograd.Function):
         (idc,) = ctx.saved_tensors
         Vl, H, pad, start, wdt, ishape = ctx.meta
         gc = g.reshape(-1, H).contiguous()
+        from ..framework.flags import flag
+
+        if flag("FLAGS_embedding_deterministic"):
+            # reproducible order: rows sorted by id, then a sort-based (atomics-free) accumulation
+            local = idc - start
+            ok = (local >= 0) & (local < Vl) & (idc != pad)
+            li, gi = local[ok], gc[ok].float()
+            order = torch.argsort(li, stable=True)
+            dw32 = torch.zeros(Vl, H, dtype=torch.float32, device=g.device)
+            prev = torch.are_deterministic_algorithms_enabled()
+            torch.use_deterministic_algorithms(True, warn_only=True)
+            try:
+                dw32.index_put_((li[order],), gi[order], accumulate=True)
+            finally:
+                torch.use_deterministic_algorithms(prev, warn_only=True)
+            return None, dw32.to(wdt), None, None
         if ctx.native:
             C = N.native()
             dw32 = torch.zeros(Vl, H, dtype=torch.float32, device=g.device)

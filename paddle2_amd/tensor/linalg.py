@@ -9,10 +9,12 @@ import torch
 
 from ..framework.tensor import Tensor
 from ._helpers import axis_arg, ut
+from ..amp import amp_op as _amp_op  # noqa: E402
 
 _wrap = Tensor._wrap
 
 
+@_amp_op("matmul")
 def matmul(x, y, transpose_x=False, transpose_y=False, name=None):
     a = x._t
     b = y._t

@@ -10,6 +10,7 @@ import torch
 from ..framework import dtype as _dt
 from ..framework.tensor import Tensor
 from ._helpers import axis_arg, dtype_arg, scalar, u, ut, w
+from ..amp import amp_op as _amp_op  # noqa: E402
 
 _wrap = Tensor._wrap
 
@@ -299,6 +300,7 @@ def _sum_dtype(t, dtype):
     return None
 
 
+@_amp_op("sum")
 def sum(x, axis=None, dtype=None, keepdim=False, name=None):
     t = x._t if isinstance(x, Tensor) else ut(x)
     ax = axis_arg(axis)
@@ -316,6 +318,7 @@ def nansum(x, axis=None, dtype=None, keepdim=False, name=None):
     return _wrap(torch.nansum(x._t, dim=ax, keepdim=keepdim, dtype=dtype_arg(dtype)))
 
 
+@_amp_op("mean")
 def mean(x, axis=None, keepdim=False, name=None):
     t = x._t
     ax = axis_arg(axis)

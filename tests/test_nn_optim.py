@@ -204,3 +204,27 @@ def test_multi_precision_master_weights_cpu():
     sd = opt.state_dict()
     assert "master_weights" in sd and len(sd["master_weights"]) == 2
     assert all(v.dtype == paddle.float32 for v in sd["master_weights"].values())
+
+
+def test_auto_cast_custom_lists_are_honoured():
+    """custom_white_list / custom_black_list (reference amp/auto_cast.py:1029) override the defaults at this
+    framework's op entry points: a black-listed matmul runs in fp32, a white-listed softmax in the AMP
+    dtype; an op in both lists is an error."""
+    import pytest
+    import torch
+
+    import paddle2_amd as paddle
+
+    x = paddle.to_tensor(torch.randn(4, 8))
+    w = paddle.to_tensor(torch.randn(8, 3))
+    with paddle.amp.auto_cast(custom_black_list={"matmul"}, dtype="bfloat16"):
+        y = paddle.matmul(x, w)
+        s = paddle.nn.functional.softmax(x)
+    assert y._t.dtype == torch.float32 and s._t.dtype == torch.float32
+    with paddle.amp.auto_cast(custom_white_list={"softmax"}, dtype="bfloat16"):
+        s = paddle.nn.functional.softmax(x)
+        m = paddle.mean(x)
+    assert s._t.dtype == torch.bfloat16 and m._t.dtype == torch.float32
+    with pytest.raises(ValueError):
+        with paddle.amp.auto_cast(custom_white_list={"exp"}, custom_black_list={"exp"}):
+            pass
