@@ -255,3 +255,91 @@ def max_unpool2d(x, indices, kernel_size, stride=None, padding=0, data_format="N
 
 def lp_pool2d(x, norm_type, kernel_size, stride=None, ceil_mode=False, data_format="NCHW", name=None):
     return _wrap(F.lp_pool2d(x._t, norm_type, kernel_size, stride, ceil_mode))
+
+
+def lp_pool1d(x, norm_type, kernel_size, stride=None, padding=0, ceil_mode=False, data_format="NCL", name=None):
+    """Power-average pooling (reference nn/functional/pooling.py lp_pool1d): (sum x^p)^(1/p) per window."""
+    t = x._t
+    if padding:
+        t = F.pad(t, (padding, padding))
+    return _wrap(F.lp_pool1d(t, float(norm_type), kernel_size, stride, ceil_mode))
+
+
+def max_unpool1d(x, indices, kernel_size, stride=None, padding=0, data_format="NCL", output_size=None, name=None):
+    return _wrap(F.max_unpool1d(x._t, indices._t, kernel_size, stride, padding, output_size))
+
+
+def max_unpool3d(x, indices, kernel_size, stride=None, padding=0, data_format="NCDHW", output_size=None, name=None):
+    return _wrap(F.max_unpool3d(x._t, indices._t, kernel_size, stride, padding, output_size))
+
+
+def _fractional_bounds(inp, out, pool, u):
+    """Window [start, end) per output index, the reference's pseudo-random sequence
+    (phi/kernels/funcs/pooling.h:142 FractionalRationalU / StartIndex / EndIndex)."""
+    alpha = float(inp - pool) / (out - (1 if pool > 0 else 0))
+    if pool <= 0:
+        base = inp // out
+        u = u * min((base + 2) / alpha - 1, (inp + 1 - base) / alpha - (out - 1))
+    st, en = [], []
+    for i in range(out):
+        s0 = int((i + u) * alpha) - int(u * alpha)
+        e0 = s0 + pool if pool > 0 else int((i + 1 + u) * alpha) - int(u * alpha)
+        st.append(max(s0, 0))
+        en.append(min(e0, inp))
+    return st, en
+
+
+def _fractional(x, output_size, kernel_size, random_u, return_mask, n):
+    t = x._t
+    sp = list(t.shape[2:])
+    outs = [output_size] * n if isinstance(output_size, int) else list(output_size)
+    pools = [0] * n if kernel_size is None else ([kernel_size] * n if isinstance(kernel_size, int) else list(kernel_size))
+    if random_u is None or float(random_u) == 0.0:
+        u = float(torch.rand(()))
+    else:
+        u = float(random_u)
+        if not 0.0 < u < 1.0:
+            raise ValueError("random_u must be in (0, 1)")
+    # per dim: gather index [out, win] (clamped) + validity mask, then a masked max over all window dims
+    y, flat = t, None
+    idx_dims, masks = [], []
+    for d in range(n):
+        st, en = _fractional_bounds(sp[d], outs[d], pools[d], u)
+        win = max(e - s for s, e in zip(st, en))
+        ar = torch.arange(win, device=t.device)
+        s_t = torch.tensor(st, device=t.device)[:, None]
+        e_t = torch.tensor(en, device=t.device)[:, None]
+        idx = (s_t + ar).clamp_max(sp[d] - 1)
+        idx_dims.append(idx)
+        masks.append((s_t + ar) < e_t)
+    # y[N, C, o0, w0, o1, w1, ...]
+    for d in range(n):
+        ax = 2 + 2 * d
+        y = y.index_select(ax, idx_dims[d].reshape(-1)).unflatten(ax, idx_dims[d].shape)
+    valid = masks[0]
+    lin = idx_dims[0]
+    for d in range(1, n):
+        valid = valid[(...,) + (None, None)] & masks[d][(None, None) * d]
+        lin = lin[(...,) + (None, None)] * sp[d] + idx_dims[d][(None, None) * d]
+    # move window axes last: [N, C, o0, o1, ..., w0, w1, ...]
+    perm = [0, 1] + [2 + 2 * d for d in range(n)] + [3 + 2 * d for d in range(n)]
+    y = y.permute(perm).flatten(2 + n)
+    pv = list(range(0, 2 * n, 2)) + list(range(1, 2 * n, 2))
+    valid = valid.permute(pv).flatten(n)
+    lin = lin.permute(pv).flatten(n)
+    y = y.masked_fill(~valid, float("-inf"))
+    val, arg = y.max(-1)
+    if not return_mask:
+        return _wrap(val)
+    mask = torch.gather(lin.expand(*val.shape, lin.shape[-1]), -1, arg.unsqueeze(-1)).squeeze(-1)
+    return _wrap(val), _wrap(mask)
+
+
+def fractional_max_pool2d(x, output_size, kernel_size=None, random_u=None, return_mask=False, name=None):
+    """Fractional max pooling (Graham 2014; reference nn/functional/pooling.py): pseudo-random window
+    boundaries, one shared ``random_u`` in (0, 1) makes the pooling sequence reproducible."""
+    return _fractional(x, output_size, kernel_size, random_u, return_mask, 2)
+
+
+def fractional_max_pool3d(x, output_size, kernel_size=None, random_u=None, return_mask=False, name=None):
+    return _fractional(x, output_size, kernel_size, random_u, return_mask, 3)

@@ -214,3 +214,78 @@ def npair_loss(anchor, positive, labels, l2_reg=0.002):
     ce = (-same * torch.log_softmax(logits, 1)).sum(1).mean()
     reg = l2_reg * ((a ** 2).sum(1).mean() + (p ** 2).sum(1).mean()) * 0.25
     return _wrap(ce + reg)
+
+
+def hsigmoid_loss(input, label, num_classes, weight, bias=None, path_table=None, path_code=None, is_sparse=False,
+                  name=None):
+    """Hierarchical sigmoid (reference nn/functional/loss.py hsigmoid_loss, phi hsigmoid_loss_kernel with
+    MatrixBitCodeFunctor).  Default tree: leaf c = label + num_classes of a complete binary tree; node j on
+    the path is (c >> (j+1)) - 1 with branch bit (c >> j) & 1, length floor(log2(c)).  Custom trees: rows of
+    ``path_table`` (node ids, -1 padded) and ``path_code`` (bits).  Loss per sample = sum over its path of
+    softplus(z) - bit * z, z = x . W[node] + b[node] (pre-activations clipped to [-40, 40]).  -> [N, 1]."""
+    x = input._t
+    W = weight._t
+    lab = label._t.reshape(-1).long()
+    N = x.shape[0]
+    if path_table is None:
+        c = lab + num_classes
+        L = int(torch.floor(torch.log2(c.float().max())).item()) if N else 0
+        j = torch.arange(L, device=x.device)
+        nodes = (c[:, None] >> (j[None, :] + 1)) - 1
+        bits = ((c[:, None] >> j[None, :]) & 1).to(x.dtype)
+        lens = torch.floor(torch.log2(c.float())).long()
+        valid = j[None, :] < lens[:, None]
+    else:
+        nodes = path_table._t.long()
+        bits = path_code._t.to(x.dtype)
+        valid = nodes >= 0
+    safe = nodes.clamp_min(0)
+    z = torch.einsum("nd,nld->nl", x, W[safe])
+    if bias is not None:
+        z = z + bias._t.reshape(-1)[safe]
+    z = z.clamp(-40.0, 40.0)
+    per = (F.softplus(z) - bits * z) * valid.to(x.dtype)
+    return _wrap(per.sum(1, keepdim=True))
+
+
+def rnnt_loss(input, label, input_lengths, label_lengths, blank=0, fastemit_lambda=0.001, reduction="mean",
+              name=None):
+    """RNN-Transducer loss (Graves 2012; reference nn/functional/loss.py rnnt_loss over warprnnt).
+    ``input`` [B, T, U+1, V] logits, ``label`` [B, U].  alpha(t, u) = logaddexp(alpha(t-1, u) + blank(t-1, u),
+    alpha(t, u-1) + emit(t, u-1)); loss = -(alpha(T-1, U) + blank(T-1, U)) per sequence, differentiated by
+    autograd through the log-space recursion.  ``fastemit_lambda`` adds the FastEmit regulariser's
+    emission weight to the emit transitions' gradient (lambda * dL/d emit), as warprnnt does.
+    reduction 'mean' divides by the target lengths' sum... the reference (warprnnt) 'mean' averages over
+    the batch; 'sum' / 'none' as usual."""
+    logits = input._t
+    lab = label._t.long()
+    tl = input_lengths._t.long().reshape(-1)
+    ul = label_lengths._t.long().reshape(-1)
+    B, T, U1, V = logits.shape
+    lp = torch.log_softmax(logits.float(), -1)
+    blank_lp = lp[..., blank]                                     # [B, T, U+1]
+    idx = lab.clamp_min(0)[:, None, :].expand(B, T, U1 - 1)[..., None]
+    emit_lp = lp[:, :, :U1 - 1, :].gather(-1, idx).squeeze(-1)   # [B, T, U]
+    if fastemit_lambda:
+        # FastEmit (Yu et al. 2021): scale the emit paths' gradient by (1 + lambda), value unchanged
+        emit_lp = emit_lp + fastemit_lambda * (emit_lp - emit_lp.detach())
+    neg = torch.finfo(torch.float32).min / 4
+    alpha = [[None] * U1 for _ in range(T)]
+    for t in range(T):
+        for u in range(U1):
+            if t == 0 and u == 0:
+                a = torch.zeros(B, device=logits.device)
+            else:
+                c1 = alpha[t - 1][u] + blank_lp[:, t - 1, u] if t > 0 else torch.full((B,), neg, device=logits.device)
+                c2 = alpha[t][u - 1] + emit_lp[:, t, u - 1] if u > 0 else torch.full((B,), neg, device=logits.device)
+                a = torch.logaddexp(c1, c2)
+            alpha[t][u] = a
+    ar = torch.stack([torch.stack(row, 1) for row in alpha], 1)   # [B, T, U+1]
+    bi = torch.arange(B, device=logits.device)
+    ll = ar[bi, tl - 1, ul] + blank_lp[bi, tl - 1, ul]
+    loss = -ll
+    if reduction == "mean":
+        return _wrap(loss.mean())
+    if reduction == "sum":
+        return _wrap(loss.sum())
+    return _wrap(loss)

@@ -449,8 +449,8 @@ def _act(name, fn, **defaults):
         vals.update({k: v for k, v in kwargs.items() if k in vals})
         self._kw = vals
 
-    def forward(self, x):
-        return fn(x, **self._kw)
+    def forward(self, x, *extra):  # extra: the indices of the MaxUnPool layers
+        return fn(x, *extra, **self._kw)
 
     def extra_repr(self):
         return ", ".join(f"{k}={v}" for k, v in self._kw.items())
@@ -610,8 +610,8 @@ def _pool_layer(name, fn, argnames):
         self._kw = dict(zip(argnames, args))
         self._kw.update(kwargs)
 
-    def forward(self, x):
-        return fn(x, **self._kw)
+    def forward(self, x, *extra):  # extra: the indices of the MaxUnPool layers
+        return fn(x, *extra, **self._kw)
 
     def extra_repr(self):
         return ", ".join(f"{k}={v}" for k, v in self._kw.items())
@@ -632,6 +632,14 @@ AdaptiveMaxPool1D = _pool_layer("AdaptiveMaxPool1D", F.adaptive_max_pool1d, ["ou
 AdaptiveMaxPool2D = _pool_layer("AdaptiveMaxPool2D", F.adaptive_max_pool2d, ["output_size", "return_mask"])
 AdaptiveMaxPool3D = _pool_layer("AdaptiveMaxPool3D", F.adaptive_max_pool3d, ["output_size", "return_mask"])
 MaxUnPool2D = _pool_layer("MaxUnPool2D", F.max_unpool2d, ["kernel_size", "stride", "padding", "data_format", "output_size"])
+MaxUnPool1D = _pool_layer("MaxUnPool1D", F.max_unpool1d, ["kernel_size", "stride", "padding", "data_format", "output_size"])
+MaxUnPool3D = _pool_layer("MaxUnPool3D", F.max_unpool3d, ["kernel_size", "stride", "padding", "data_format", "output_size"])
+LPPool1D = _pool_layer("LPPool1D", F.lp_pool1d, ["norm_type", "kernel_size", "stride", "padding", "ceil_mode", "data_format"])
+LPPool2D = _pool_layer("LPPool2D", F.lp_pool2d, ["norm_type", "kernel_size", "stride", "ceil_mode", "data_format"])
+FractionalMaxPool2D = _pool_layer("FractionalMaxPool2D", F.fractional_max_pool2d,
+                                  ["output_size", "kernel_size", "random_u", "return_mask"])
+FractionalMaxPool3D = _pool_layer("FractionalMaxPool3D", F.fractional_max_pool3d,
+                                  ["output_size", "kernel_size", "random_u", "return_mask"])
 
 
 # ------------------------------------------------------------------ norms
@@ -885,6 +893,33 @@ MultiMarginLoss = _loss("MultiMarginLoss", F.multi_margin_loss, ["p", "margin", 
 PoissonNLLLoss = _loss("PoissonNLLLoss", F.poisson_nll_loss, ["log_input", "full", "epsilon", "reduction"])
 GaussianNLLLoss = _loss("GaussianNLLLoss", F.gaussian_nll_loss, ["full", "epsilon", "reduction"])
 CTCLoss = _loss("CTCLoss", F.ctc_loss, ["blank", "reduction"])
+
+
+class HSigmoidLoss(Layer):
+    """Hierarchical sigmoid loss layer (reference nn/layer/loss.py HSigmoidLoss): owns the [num_classes-1,
+    feature_size] node weights (or [num_classes, feature_size] with a custom tree) and bias."""
+
+    def __init__(self, feature_size, num_classes, weight_attr=None, bias_attr=None, is_custom=False, is_sparse=False,
+                 name=None):
+        super().__init__()
+        if num_classes < 2 and not is_custom:
+            raise ValueError("HSigmoidLoss: num_classes must be >= 2")
+        self.num_classes = num_classes
+        rows = num_classes if is_custom else num_classes - 1
+        self.weight = self.create_parameter([rows, feature_size], attr=weight_attr)
+        self.bias = None if bias_attr is False else self.create_parameter([rows, 1], attr=bias_attr, is_bias=True)
+
+    def forward(self, input, label, path_table=None, path_code=None):
+        return F.hsigmoid_loss(input, label, self.num_classes, self.weight, self.bias, path_table, path_code)
+
+
+class RNNTLoss(Layer):
+    def __init__(self, blank=0, fastemit_lambda=0.001, reduction="mean", name=None):
+        super().__init__()
+        self.blank, self.fastemit_lambda, self.reduction = blank, fastemit_lambda, reduction
+
+    def forward(self, input, label, input_lengths, label_lengths):
+        return F.rnnt_loss(input, label, input_lengths, label_lengths, self.blank, self.fastemit_lambda, self.reduction)
 
 
 class CTCLoss(_Loss):  # noqa: F811  (paddle arg order: (log_probs, labels, input_lengths, label_lengths, norm_by_times))

@@ -251,11 +251,15 @@ class SimpleRNN(_RNNBase):
     _mode = "RNN"
 
 
-class _CellBase(Layer):
+from .rnn import RNNCellBase  # noqa: E402
+
+
+class _CellBase(RNNCellBase):
     def __init__(self, input_size, hidden_size, mode, activation="tanh"):
         super().__init__()
         g = {"LSTM": 4, "GRU": 3, "RNN": 1}[mode]
         self.mode, self.hidden_size, self.activation = mode, hidden_size, activation
+        self.input_size = input_size
         from .. import initializer as I
 
         k = 1.0 / hidden_size ** 0.5
@@ -263,6 +267,10 @@ class _CellBase(Layer):
         self.weight_hh = self.create_parameter([g * hidden_size, hidden_size], default_initializer=I.Uniform(-k, k))
         self.bias_ih = self.create_parameter([g * hidden_size], is_bias=True, default_initializer=I.Uniform(-k, k))
         self.bias_hh = self.create_parameter([g * hidden_size], is_bias=True, default_initializer=I.Uniform(-k, k))
+
+    @property
+    def state_shape(self):
+        return ((self.hidden_size,), (self.hidden_size,)) if self.mode == "LSTM" else (self.hidden_size,)
 
     def forward(self, inputs, states=None):
         x = inputs._t
