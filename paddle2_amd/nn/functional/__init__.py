@@ -5,3 +5,4 @@ from .conv import *  # noqa: F401,F403
 from .loss import *  # noqa: F401,F403
 from .norm import *  # noqa: F401,F403
 from .attention import *  # noqa: F401,F403
+from ..decode import gather_tree  # noqa: F401,E402

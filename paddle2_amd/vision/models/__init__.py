@@ -7,3 +7,6 @@ from .mobile import (DenseNet, MobileNetV1, MobileNetV3Large, MobileNetV3Small, 
                      mobilenet_v3_large, mobilenet_v3_small, shufflenet_v2_swish, shufflenet_v2_x0_5,
                      shufflenet_v2_x0_25, shufflenet_v2_x0_33, shufflenet_v2_x1_0, shufflenet_v2_x1_5,
                      shufflenet_v2_x2_0, squeezenet1_0, squeezenet1_1)
+from .resnet import (resnext50_64x4d, resnext101_32x4d, resnext101_64x4d, resnext152_32x4d,  # noqa: F401
+                     resnext152_64x4d, wide_resnet101_2)
+from .inception import GoogLeNet, InceptionV3, googlenet, inception_v3  # noqa: F401

@@ -131,3 +131,39 @@ def test_rnnt_loss_matches_path_enumeration():
     g = xl.grad._t
     assert torch.isfinite(g).all()
     torch.testing.assert_close(g.sum(-1), torch.zeros(B, T, U + 1), atol=1e-5, rtol=0)  # log-softmax grads
+
+
+def test_beam_search_decoder_finds_exhaustive_best():
+    """Bigram 'cell' (logits = table[prev token]); with beam >= V^(L-1) beam search is exact, so the top
+    beam must equal the best of all V^L sequences; gather_tree back-traces parents."""
+    torch.manual_seed(6)
+    V, L, start, end = 4, 3, 0, 3
+    table = torch.randn(V, V)
+    table[:, end] = -30.0  # never emitted: decoding runs to max_step_num
+
+    class Bigram(paddle.nn.RNNCellBase):
+        def forward(self, inputs, states):
+            return paddle.to_tensor(table[inputs._t]), states
+
+    dec = paddle.nn.BeamSearchDecoder(Bigram(), start, end, beam_size=V ** (L - 1))
+    ids, _, lens = paddle.nn.dynamic_decode(dec, inits=P(torch.zeros(2, 1)), max_step_num=L - 1, return_length=True)
+    assert tuple(ids.shape) == (2, L, V ** (L - 1))
+    lp = torch.log_softmax(table, -1)
+    best, best_s = None, -1e9
+    for seq in itertools.product(range(V - 1), repeat=L):
+        s, prev = 0.0, start
+        for tkn in seq:
+            s += float(lp[prev, tkn])
+            prev = tkn
+        if s > best_s:
+            best, best_s = seq, s
+    assert tuple(ids._t[0, :, 0].tolist()) == best and tuple(ids._t[1, :, 0].tolist()) == best
+    assert (lens._t == L).all()
+
+
+def test_gather_tree():
+    ids = torch.tensor([[[2, 2], [6, 1]], [[3, 9], [6, 1]], [[0, 1], [9, 0]]])
+    parents = torch.tensor([[[0, 0], [1, 1]], [[1, 0], [1, 0]], [[0, 0], [0, 1]]])
+    out = paddle.nn.functional.gather_tree(P(ids), P(parents))._t
+    # reference docstring example (python/paddle/nn/functional/extension.py gather_tree)
+    assert out.tolist() == [[[2, 2], [1, 6]], [[3, 3], [6, 1]], [[0, 1], [9, 0]]]

@@ -28,3 +28,26 @@ def test_headless_features():
     assert y.shape[:2] == [1, 576]
     with pytest.raises(ValueError):
         M.densenet121(pretrained=True)
+
+
+def test_googlenet_three_heads():
+    paddle.seed(0)
+    m = M.googlenet(num_classes=7)
+    out, a1, a2 = m(paddle.randn([2, 3, 224, 224]))
+    assert out.shape == a1.shape == a2.shape == [2, 7]
+    (out.mean() + a1.mean() + a2.mean()).backward()
+    assert m.aux2[0]._conv.weight.grad is not None
+
+
+def test_inception_v3_shape_and_size():
+    paddle.seed(0)
+    m = M.inception_v3(num_classes=5)
+    assert m(paddle.randn([1, 3, 299, 299])).shape == [1, 5]
+    # same parameter count as the reference InceptionV3 head-less trunk + 2048xC fc
+    assert int(sum(p.numel() for p in M.inception_v3().parameters())) == 23834568
+
+
+@pytest.mark.parametrize("name", ["resnext50_64x4d", "resnext101_32x4d", "wide_resnet101_2"])
+def test_resnet_variants_build(name):
+    m = getattr(M, name)(num_classes=3)
+    assert m(paddle.randn([2, 3, 64, 64])).shape == [2, 3]
