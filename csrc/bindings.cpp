@@ -67,6 +67,7 @@ int pd_flash_bwd_ext(int, const void*, const void*, const void*, const void*, co
                      float, void*);
 int pd_flash_fwd(int, const void*, const void*, const void*, void*, float*, int, int, int, int, int, int, long, long,
                  long, long, float, int, void*);
+int pd_flash_bwd_block(int);
 int pd_flash_bwd(int, const void*, const void*, const void*, const void*, const void*, const float*, float*, void*,
                  void*, void*, float*, int, int, int, int, int, int, long, long, long, long, long, long, long, float,
                  int, void*);
@@ -220,6 +221,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("cast_from_f32", [](int dt, uintptr_t src, uintptr_t dst, long n, uintptr_t st) {
     check(pd_cast_from_f32(dt, P<const float*>(src), P<void*>(dst), n, P<void*>(st)), "cast_from_f32");
   });
+  m.def("flash_bwd_block", [](int D) { return pd_flash_bwd_block(D); });
   m.def("flash_fwd", [](int dt, uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t lse, int B, int Sq,
                         int Sk, int Hq, int Hk, int D, long sq_row, long sk_row, long sv_row, long so_row, float scale,
                         int causal, uintptr_t st) {

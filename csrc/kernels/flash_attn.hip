@@ -1,4 +1,5 @@
-// Flash attention forward + backward on CDNA4 MFMA (gfx950), bf16 in / fp32 accumulate.
+// Flash attention forward + backward on CDNA4 MFMA (gfx950), bf16 or fp16 in / fp32 accumulate,
+// head dims 64 / 128 / 256 (other D <= 256 are zero-padded to the next one by the host wrapper).
 //
 // Reference behaviour: phi/kernels/gpu/flash_attn_kernel.cu / flash_attn_grad_kernel.cu
 // (q/k/v [b, s, nh, hd], causal, GQA via num_heads_k, returns softmax_lse [b, nh, s]).  The
@@ -75,16 +76,39 @@ __device__ __forceinline__ bf16x8 cat4(s16x4 a, s16x4 b) {
   return __builtin_bit_cast(bf16x8, r);
 }
 
-// Pack 8 fp32 accumulator registers [8s, 8s+8) into a bf16 MFMA operand fragment.
-__device__ __forceinline__ bf16x8 pack8(const f32x16& acc, int s) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (__bf16)acc[8 * s + j];
-  return r;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// Operand fragments travel as 16-byte bf16x8 bit containers for both element types; F16 selects the
+// fp16 conversions and the f16 MFMA (same 32x32x16 shape and operand layout, so every LDS image,
+// swizzle and lane mapping below is shared).
+template <bool F16>
+__device__ __forceinline__ unsigned short cvt16(float f) {
+  if constexpr (F16) return __builtin_bit_cast(unsigned short, (_Float16)f);
+  else return f2bf(f);
 }
 
+// Pack 8 fp32 accumulator registers [8s, 8s+8) into an MFMA operand fragment.
+template <bool F16>
+__device__ __forceinline__ bf16x8 pack8(const f32x16& acc, int s) {
+  if constexpr (F16) {
+    f16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (_Float16)acc[8 * s + j];
+    return __builtin_bit_cast(bf16x8, r);
+  } else {
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (__bf16)acc[8 * s + j];
+    return r;
+  }
+}
+
+template <bool F16>
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                  0);
+  else return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
 // XCD-aware bijective remap of a 1-D block id (cdna guide §5 "XCD swizzle must be bijective").
@@ -161,8 +185,8 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int r0, int c0, int 
 // =====================================================================================
 //                                       FORWARD
 // =====================================================================================
-template <int D, bool CAUSAL, int MODE, bool DROP>
-__global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+template <int D, bool CAUSAL, int MODE, bool DROP, bool F16>
+__global__ __launch_bounds__(256, (D > 128 ? 1 : 2)) void fwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ Vv, bf16* __restrict__ O,
                                                      float* __restrict__ LSE, int B, int SqMax, int SkMax, int Hq,
                                                      int Hk, long sq, long sk, long sv, long so, float scale, Ext ex) {
@@ -306,7 +330,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         bf16x8 a = lds_b128(kt, krow * (D * 2) + swz(krow, 2 * ks + h, NCH) * 16);
-        s[kb] = mfma(a, qf[ks], s[kb]);
+        s[kb] = mfma<F16>(a, qf[ks], s[kb]);
       }
     }
     // next tile's K/V loads issue after QK^T (T14): softmax + PV cover their flight, lstore waits at the end
@@ -391,11 +415,11 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 pb = pack8(s[kb], ss);
+        const bf16x8 pb = pack8<F16>(s[kb], ss);
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
           const bf16x8 a = tr_frag<D, true>(vt, kb * 32 + 16 * ss, dt * 32, lane);
-          oacc[dt] = mfma(a, pb, oacc[dt]);
+          oacc[dt] = mfma<F16>(a, pb, oacc[dt]);
         }
       }
     }
@@ -416,10 +440,10 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
       for (int c = 0; c < 4; ++c) {
         const int d = dt * 32 + 8 * c + 4 * h;
         ushort4 v;
-        v.x = f2bf(oacc[dt][4 * c + 0] * inv);
-        v.y = f2bf(oacc[dt][4 * c + 1] * inv);
-        v.z = f2bf(oacc[dt][4 * c + 2] * inv);
-        v.w = f2bf(oacc[dt][4 * c + 3] * inv);
+        v.x = cvt16<F16>(oacc[dt][4 * c + 0] * inv);
+        v.y = cvt16<F16>(oacc[dt][4 * c + 1] * inv);
+        v.z = cvt16<F16>(oacc[dt][4 * c + 2] * inv);
+        v.w = cvt16<F16>(oacc[dt][4 * c + 3] * inv);
         *reinterpret_cast<ushort4*>(orow + d) = v;
       }
     }
@@ -434,6 +458,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const bf16* __restrict__ Q,
 // =====================================================================================
 // delta[b, h, q] = sum_d dO . O  (fp32).  D/8 lanes per row (16 for D = 128), so a wave covers 64*8/D rows and
 // every lane moves 2 x 16 B — the one-wave-per-row form left 3/4 of the lanes idle.
+template <bool F16>
 __global__ __launch_bounds__(256) void bwd_delta_kernel(const bf16* __restrict__ O, const bf16* __restrict__ dO,
                                                         float* __restrict__ delta, int B, int Sq, int Hq, int D,
                                                         long so) {
@@ -448,8 +473,13 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const bf16* __restrict__
     const int b = (int)(rowid / ((long)Sq * Hq));
     const long base = ((long)b * Sq + q) * so + (long)hq * D + sub * 8;
     float a[8], c[8];
-    load_vec<bf16, 8>(O + base, a);
-    load_vec<bf16, 8>(dO + base, c);
+    if constexpr (F16) {
+      load_vec<half16, 8>(reinterpret_cast<const half16*>(O + base), a);
+      load_vec<half16, 8>(reinterpret_cast<const half16*>(dO + base), c);
+    } else {
+      load_vec<bf16, 8>(O + base, a);
+      load_vec<bf16, 8>(dO + base, c);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc += a[j] * c[j];
   }
@@ -457,15 +487,20 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const bf16* __restrict__
   if (rowid < total && sub == 0) delta[rowid] = acc;
 }
 
-template <int D, bool CAUSAL, int MODE, bool DROP>
-__global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+// D = 256 runs 4 waves x 32 keys (128-key blocks): the dK/dV accumulators alone are 256 VGPRs per lane, so
+// one wave per SIMD with the whole 512-entry register file; D <= 128 runs 8 waves (two per SIMD).
+template <int D>
+constexpr int bwd_waves() { return D > 128 ? 4 : 8; }
+
+template <int D, bool CAUSAL, int MODE, bool DROP, bool F16>
+__global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ Vv, const bf16* __restrict__ dO,
                                                      const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                      float* __restrict__ dQP, bf16* __restrict__ dK,
                                                      bf16* __restrict__ dV, int B, int SqMax, int SkMax, int Hq,
                                                      int Hk, long sq, long sk, long sv, long so, long sdk, long sdv,
                                                      long pslab, float scale, Ext ex) {
-  constexpr int NW = 8, BNK = NW * 32, BMQ = 32, NCH = D / 8, KS = D / 16, DT = D / 32;
+  constexpr int NW = bwd_waves<D>(), BNK = NW * 32, BMQ = 32, NCH = D / 8, KS = D / 16, DT = D / 32;
   constexpr int KTILE = BNK * D * 2;     // K block image: B operand of S (row reads) and of dQ (tr reads)
   constexpr int QTILE = BMQ * D * 2;     // Q / dO tile image
   constexpr int STILE = BMQ * BNK * 2;   // dS tile [32 q][256 keys]
@@ -667,8 +702,8 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int o = o_qrow ^ (ks << 5);
-      sacc = mfma(lds_b128(qimg, o), lds_b128(kimg, o_krow ^ (ks << 5)), sacc);
-      dpacc = mfma(lds_b128(doimg, o), vf[ks], dpacc);
+      sacc = mfma<F16>(lds_b128(qimg, o), lds_b128(kimg, o_krow ^ (ks << 5)), sacc);
+      dpacc = mfma<F16>(lds_b128(doimg, o), vf[ks], dpacc);
     }
     // P = exp2(S*scale*log2e - lse*log2e), dS = P * (dP - delta).  Branch-free mask: row q0+qi is
     // masked for this lane's key iff dlim + qi < 0, dlim = q0 + off - key (causal; huge when the
@@ -697,14 +732,14 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
     // dV^T += dO^T . P ; dK^T += Q^T . dS   (A operands by transposed reads, permuted k)
 #pragma unroll
     for (int ss = 0; ss < 2; ++ss) {
-      const bf16x8 pb = pack8(sacc, ss);
-      const bf16x8 db = pack8(dpacc, ss);
+      const bf16x8 pb = pack8<F16>(sacc, ss);
+      const bf16x8 db = pack8<F16>(dpacc, ss);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const int oa = (o_trA ^ (dt << 6)) + ss * 16 * (D * 2);
         const int ob = (o_trB ^ (dt << 6)) + ss * 16 * (D * 2);
-        dvacc[dt] = mfma(cat4(lds_tr(doimg, oa), lds_tr(doimg, ob)), pb, dvacc[dt]);
-        dkacc[dt] = mfma(cat4(lds_tr(qimg, oa), lds_tr(qimg, ob)), db, dkacc[dt]);
+        dvacc[dt] = mfma<F16>(cat4(lds_tr(doimg, oa), lds_tr(doimg, ob)), pb, dvacc[dt]);
+        dkacc[dt] = mfma<F16>(cat4(lds_tr(qimg, oa), lds_tr(qimg, ob)), db, dkacc[dt]);
       }
     }
     // dS -> LDS image [32 q][BNK keys] (bf16) for dQ: row qi = (i&3) + 8(i>>2) + 4h, column lkey
@@ -712,19 +747,23 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
     for (int i = 0; i < 16; ++i) {
       const int xc = ((((i & 3) << 2) | (((i >> 2) & 1) << 1)) << 4);
       const int ac = ((i & 3) + 8 * (i >> 2)) * (BNK * 2);
-      *reinterpret_cast<__bf16*>(simg + ((o_scol ^ xc) + ac)) = (__bf16)dpacc[i];
+      *reinterpret_cast<unsigned short*>(simg + ((o_scol ^ xc) + ac)) = cvt16<F16>(dpacc[i]);
     }
     __syncthreads();
-    // dQ[32 q][32-col slice] = dS[32 q][BNK keys] . K[BNK keys][d]; waves 0..DT-1 (one per SIMD for
-    // D=128, so every SIMD's matrix pipe carries the same 16 MFMAs)
-    if (wv < DT) {
+    // dQ[32 q][32-col slice] = dS[32 q][BNK keys] . K[BNK keys][d]; slice dsl on wave dsl % NW (one slice
+    // per SIMD for D=128, so every SIMD's matrix pipe carries the same 16 MFMAs; two per wave at D=256).
+    // Slice dsl's K^T chunk is (dsl*4 + cb) ^ m with m < 16: for dsl = wv + NW that is the wave's own
+    // chunk + 16 (bit 4 untouched by the XOR), i.e. +256 B on the lane base
+#pragma unroll
+    for (int dsl = wv; dsl < DT; dsl += NW) {
       f32x16 dq = f32x16{};
+      const int kq_shift = (dsl - wv) * 64;
 #pragma unroll
       for (int ks = 0; ks < BNK / 16; ++ks) {
         const bf16x8 a = lds_b128(simg, o_srow ^ (ks << 5));
-        const int kb16 = ks * 16 * (D * 2);
+        const int kb16 = ks * 16 * (D * 2) + kq_shift;
         const bf16x8 bb = cat4(lds_tr(smem, o_kqA + kb16), lds_tr(smem, o_kqB + kb16));
-        dq = mfma(a, bb, dq);
+        dq = mfma<F16>(a, bb, dq);
       }
       // accumulator: row q = (i&3)+8(i>>2)+4h, col d = wv*32 + r -> two 128-B row segments per store.
       // Full 32-row tiles: non-temporal buffer stores, the per-row offset in the scalar soffset (no VALU);
@@ -732,13 +771,13 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
       if (q0 + BMQ <= Sq) {
         const int hqd4 = Hq * D * 4;
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(dQs + (long)q0 * Hq * D + (long)hq * D, BMQ * hqd4);
-        const int vo = 4 * h * hqd4 + (wv * 32 + r) * 4;
+        const int vo = 4 * h * hqd4 + (dsl * 32 + r) * 4;
 #pragma unroll
         for (int i = 0; i < 16; ++i)
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dq[i] * scale), rs, vo,
                                                 ((i & 3) + 8 * (i >> 2)) * hqd4, 2);
       } else {
-        float* dqh = dQs + (long)hq * D + wv * 32 + r;
+        float* dqh = dQs + (long)hq * D + dsl * 32 + r;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int q = q0 + (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -758,10 +797,10 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
       for (int c = 0; c < 4; ++c) {
         const int d = dt * 32 + 8 * c + 4 * h;
         ushort4 kv, vv;
-        kv.x = f2bf(dkacc[dt][4 * c + 0] * scale); kv.y = f2bf(dkacc[dt][4 * c + 1] * scale);
-        kv.z = f2bf(dkacc[dt][4 * c + 2] * scale); kv.w = f2bf(dkacc[dt][4 * c + 3] * scale);
-        vv.x = f2bf(dvacc[dt][4 * c + 0]); vv.y = f2bf(dvacc[dt][4 * c + 1]);
-        vv.z = f2bf(dvacc[dt][4 * c + 2]); vv.w = f2bf(dvacc[dt][4 * c + 3]);
+        kv.x = cvt16<F16>(dkacc[dt][4 * c + 0] * scale); kv.y = cvt16<F16>(dkacc[dt][4 * c + 1] * scale);
+        kv.z = cvt16<F16>(dkacc[dt][4 * c + 2] * scale); kv.w = cvt16<F16>(dkacc[dt][4 * c + 3] * scale);
+        vv.x = cvt16<F16>(dvacc[dt][4 * c + 0]); vv.y = cvt16<F16>(dvacc[dt][4 * c + 1]);
+        vv.z = cvt16<F16>(dvacc[dt][4 * c + 2]); vv.w = cvt16<F16>(dvacc[dt][4 * c + 3]);
         *reinterpret_cast<ushort4*>(dkr + d) = kv;
         *reinterpret_cast<ushort4*>(dvr + d) = vv;
       }
@@ -771,7 +810,7 @@ __global__ __launch_bounds__(512, 1) void bwd_kernel(const bf16* __restrict__ Q,
 
 // dQ[b, q, h, :] = sum over the key blocks that wrote row q of their partial slabs; bf16 out with row
 // stride sdq.  Causal: key block kb wrote rows q >= qbegin(kb) = floor(max(0, kb*BNK - off) / BMQ) * BMQ.
-template <int MODE>
+template <int MODE, bool F16>
 __global__ __launch_bounds__(256) void dq_reduce_kernel(const float* __restrict__ P, bf16* __restrict__ dq, int B,
                                                         int Sq, int Hq, int D, int nkb, long pslab, long sdq,
                                                         int causal, int off, int bnk, Ext ex) {
@@ -819,7 +858,8 @@ __global__ __launch_bounds__(256) void dq_reduce_kernel(const float* __restrict_
 #pragma unroll
       for (int j = 0; j < 4; ++j) { acc[j] += a[j]; acc[4 + j] += c[j]; }
     }
-    store_vec<bf16, 8>(dq + row * sdq + e, acc);
+    if constexpr (F16) store_vec<half16, 8>(reinterpret_cast<half16*>(dq + row * sdq + e), acc);
+    else store_vec<bf16, 8>(dq + row * sdq + e, acc);
   }
 }
 
@@ -828,36 +868,85 @@ __global__ __launch_bounds__(256) void dq_reduce_kernel(const float* __restrict_
 
 using namespace pd;
 
+namespace {
+
+template <int D, bool F16>
+void launch_fwd(dim3 grid, hipStream_t st, const void* q, const void* k, const void* v, void* o, float* lse, int B,
+                int Sq, int Sk, int Hq, int Hk, long sq, long sk, long sv, long so, float scale, bool causal, int mode,
+                bool drop, const fa::Ext& ex) {
+#define PD_FA_FWD(CC, MM, DR)                                                                                     \
+  fa::fwd_kernel<D, CC, MM, DR, F16><<<grid, 256, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,       \
+                                                           (bf16*)o, lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, ex)
+#define PD_FA_FWD_C(MM, DR) \
+  if (causal) PD_FA_FWD(true, MM, DR); else PD_FA_FWD(false, MM, DR);
+  if (drop) {
+    if (mode == 0) { PD_FA_FWD_C(fa::kDense, true) } else { PD_FA_FWD_C(fa::kVarlen, true) }
+  } else if (mode == 0) { PD_FA_FWD_C(fa::kDense, false) }
+  else if (mode == 1) { PD_FA_FWD_C(fa::kVarlen, false) }
+  else if constexpr (D <= 128) { PD_FA_FWD_C(fa::kMask, false) }
+#undef PD_FA_FWD_C
+#undef PD_FA_FWD
+}
+
+template <int D, bool F16>
+void launch_bwd(dim3 grid, hipStream_t st, const void* q, const void* k, const void* v, const void* dout,
+                const float* lse, const float* delta, float* dqp, void* dk, void* dv, int B, int Sq, int Sk, int Hq,
+                int Hk, long sq, long sk, long sv, long so, long sdk, long sdv, long pslab, float scale, bool causal,
+                int mode, bool drop, const fa::Ext& ex) {
+  constexpr int NT = fa::bwd_waves<D>() * 64;
+#define PD_FA_BWD(CC, MM, DR)                                                                                    \
+  fa::bwd_kernel<D, CC, MM, DR, F16><<<grid, NT, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,       \
+                                                          (const bf16*)dout, lse, delta, dqp, (bf16*)dk, (bf16*)dv, \
+                                                          B, Sq, Sk, Hq, Hk, sq, sk, sv, so, sdk, sdv, pslab, scale, ex)
+#define PD_FA_BWD_C(MM, DR) \
+  if (causal) PD_FA_BWD(true, MM, DR); else PD_FA_BWD(false, MM, DR);
+  if (drop) {
+    if (mode == 0) { PD_FA_BWD_C(fa::kDense, true) } else { PD_FA_BWD_C(fa::kVarlen, true) }
+  } else if (mode == 0) { PD_FA_BWD_C(fa::kDense, false) }
+  else if (mode == 1) { PD_FA_BWD_C(fa::kVarlen, false) }
+  else if constexpr (D <= 128) { PD_FA_BWD_C(fa::kMask, false) }
+#undef PD_FA_BWD_C
+#undef PD_FA_BWD
+}
+
+// shape / mode validation shared by fwd and bwd: dt bf16 or f16, D in {64, 128, 256}, FlashMask only for
+// D <= 128 (its plans are built for 256-key backward blocks)
+int check_args(int dt, int D, int Hq, int Hk, int mode, int drop, float pdrop, const int* cu_q, const int* cu_k,
+               const int* fm, const int* plan, int fm_hm) {
+  if ((dt != kBF16 && dt != kF16) || (D != 64 && D != 128 && D != 256) || Hq % Hk || mode < 0 || mode > 2) return -1;
+  if (mode == 2 && D > 128) return -1;
+  if (drop && (mode == 2 || !(pdrop > 0.f && pdrop < 1.f))) return -3;
+  if (mode == 1 && (!cu_q || !cu_k)) return -2;
+  if (mode == 2 && (!fm || !plan || (fm_hm != 1 && fm_hm != Hq))) return -2;
+  return 0;
+}
+
+}  // namespace
+
+// Key-block width of the backward (rows of the dQ partial slabs): 256 keys for D <= 128, 128 for D = 256.
+extern "C" int pd_flash_bwd_block(int D) { return D > 128 ? 128 : 256; }
+
 // mode: 0 dense, 1 varlen (B sequences, Sq/Sk = max_seqlen, rows located by cu_q/cu_k, lse [Hq, total_q]),
 // 2 FlashMask (dense layout + fm [B, fm_hm, Sk] int4 intervals with the fm_t64 / fm_t256 fwd / bwd plans).
+// dt: kBF16 or kF16 (q/k/v/o share it).
 extern "C" int pd_flash_fwd_ext(int dt, const void* q, const void* k, const void* v, void* o, float* lse, int B,
                                 int Sq, int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, float scale,
                                 int causal, int mode, const int* cu_q, const int* cu_k, int total_q, const int* fm,
                                 const int* fm_t64, const int* fm_t256, int fm_hm, int drop, unsigned seed, float pdrop,
                                 void* stream) {
-  if (dt != kBF16 || (D != 64 && D != 128) || Hq % Hk || mode < 0 || mode > 2) return -1;
-  if (drop && (mode == 2 || !(pdrop > 0.f && pdrop < 1.f))) return -3;
-  if (mode == 1 && (!cu_q || !cu_k)) return -2;
-  if (mode == 2 && (!fm || !fm_t64 || (fm_hm != 1 && fm_hm != Hq))) return -2;
+  if (int e = check_args(dt, D, Hq, Hk, mode, drop, pdrop, cu_q, cu_k, fm, fm_t64, fm_hm)) return e;
   hipStream_t st = (hipStream_t)stream;
   const int nmb = (Sq + 127) / 128;
-  dim3 grid(nmb * Hq * B), block(256);
+  dim3 grid(nmb * Hq * B);
   fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm, seed,
              drop ? (unsigned)fminf(pdrop * 4294967296.f, 4294967040.f) : 0u, drop ? 1.f / (1.f - pdrop) : 1.f};
-#define PD_FA_FWD(DD, CC, MM, DR)                                                                                   \
-  fa::fwd_kernel<DD, CC, MM, DR><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o,  \
-                                                         lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, ex)
-#define PD_FA_FWD_M(MM, DR)                                                                              \
-  if (D == 128) { if (causal) PD_FA_FWD(128, true, MM, DR); else PD_FA_FWD(128, false, MM, DR); }       \
-  else { if (causal) PD_FA_FWD(64, true, MM, DR); else PD_FA_FWD(64, false, MM, DR); }
-  if (drop) {
-    if (mode == 0) { PD_FA_FWD_M(fa::kDense, true) }
-    else { PD_FA_FWD_M(fa::kVarlen, true) }
-  } else if (mode == 0) { PD_FA_FWD_M(fa::kDense, false) }
-  else if (mode == 1) { PD_FA_FWD_M(fa::kVarlen, false) }
-  else { PD_FA_FWD_M(fa::kMask, false) }
-#undef PD_FA_FWD_M
-#undef PD_FA_FWD
+#define PD_FWD(DD, FF) \
+  launch_fwd<DD, FF>(grid, st, q, k, v, o, lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, causal, mode, drop, ex)
+  const bool f16 = dt == kF16;
+  if (D == 128) { if (f16) PD_FWD(128, true); else PD_FWD(128, false); }
+  else if (D == 64) { if (f16) PD_FWD(64, true); else PD_FWD(64, false); }
+  else { if (f16) PD_FWD(256, true); else PD_FWD(256, false); }
+#undef PD_FWD
   return (int)hipGetLastError();
 }
 
@@ -868,61 +957,52 @@ extern "C" int pd_flash_fwd(int dt, const void* q, const void* k, const void* v,
                           nullptr, 0, nullptr, nullptr, nullptr, 1, 0, 0u, 0.f, stream);
 }
 
-// dqp: fp32 workspace of nkb * rows*Hq*D floats (nkb = ceil(Sk/256), rows = B*Sq, or total_q for varlen) for
-// per-key-block dQ partials (need not be zeroed); delta a [B, Hq, Sq] ([Hq, total_q] varlen) fp32 workspace.
-// q/k/v/o/dout and dq/dk/dv may all be row-strided views ([B, S, H, D] with token strides), e.g. slices of one
-// fused QKV / dQKV buffer.
+// dqp: fp32 workspace of nkb * rows*Hq*D floats (nkb = ceil(Sk / pd_flash_bwd_block(D)), rows = B*Sq, or total_q
+// for varlen) for per-key-block dQ partials (need not be zeroed); delta a [B, Hq, Sq] ([Hq, total_q] varlen) fp32
+// workspace.  q/k/v/o/dout and dq/dk/dv may all be row-strided views ([B, S, H, D] with token strides), e.g. slices
+// of one fused QKV / dQKV buffer.
 extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void* v, const void* o, const void* dout,
                                 const float* lse, float* delta, void* dq, void* dk, void* dv, float* dqp, int B,
                                 int Sq, int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, long sdq,
                                 long sdk, long sdv, float scale, int causal, int mode, const int* cu_q, const int* cu_k,
                                 int total_q, const int* fm, const int* fm_t64, const int* fm_t256, int fm_hm,
                                 int drop, unsigned seed, float pdrop, void* stream) {
-  if (dt != kBF16 || (D != 64 && D != 128) || Hq % Hk || mode < 0 || mode > 2) return -1;
-  if (drop && (mode == 2 || !(pdrop > 0.f && pdrop < 1.f))) return -3;
-  if (mode == 1 && (!cu_q || !cu_k)) return -2;
-  if (mode == 2 && (!fm || !fm_t256 || (fm_hm != 1 && fm_hm != Hq))) return -2;
+  if (int e = check_args(dt, D, Hq, Hk, mode, drop, pdrop, cu_q, cu_k, fm, fm_t256, fm_hm)) return e;
   hipStream_t st = (hipStream_t)stream;
+  const bool f16 = dt == kF16;
   const long nrows = mode == 1 ? (long)total_q : (long)B * Sq;  // query tokens
   // delta shares the lse layout: [B, Hq, Sq] dense, [Hq, total_q] (= B 1, Sq total_q) varlen
   const int dB = mode == 1 ? 1 : B, dS = mode == 1 ? total_q : Sq;
   const long rows = (long)dB * Hq * dS;
   const long rows_per_blk = 256 / (D / 8);
-  fa::bwd_delta_kernel<<<(int)((rows + rows_per_blk - 1) / rows_per_blk), 256, 0, st>>>(
-      (const bf16*)o, (const bf16*)dout, delta, dB, dS, Hq, D, so);
-  constexpr int BNK = 256;
+  const int dgrid = (int)((rows + rows_per_blk - 1) / rows_per_blk);
+  if (f16)
+    fa::bwd_delta_kernel<true><<<dgrid, 256, 0, st>>>((const bf16*)o, (const bf16*)dout, delta, dB, dS, Hq, D, so);
+  else
+    fa::bwd_delta_kernel<false><<<dgrid, 256, 0, st>>>((const bf16*)o, (const bf16*)dout, delta, dB, dS, Hq, D, so);
+  const int BNK = pd_flash_bwd_block(D);
   const int nkb = (Sk + BNK - 1) / BNK;
   const long pslab = nrows * Hq * D;
-  dim3 grid(nkb * Hk * B), block(512);
+  dim3 grid(nkb * Hk * B);
   fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm, seed,
              drop ? (unsigned)fminf(pdrop * 4294967296.f, 4294967040.f) : 0u, drop ? 1.f / (1.f - pdrop) : 1.f};
-#define PD_FA_BWD(DD, CC, MM, DR)                                                                                  \
-  fa::bwd_kernel<DD, CC, MM, DR><<<grid, block, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,           \
-                                                         (const bf16*)dout, lse, delta, dqp, (bf16*)dk, (bf16*)dv, \
-                                                         B, Sq, Sk, Hq, Hk, sq, sk, sv, so, sdk, sdv, pslab, scale, ex)
-#define PD_FA_BWD_M(MM, DR)                                                                             \
-  if (D == 128) { if (causal) PD_FA_BWD(128, true, MM, DR); else PD_FA_BWD(128, false, MM, DR); }      \
-  else { if (causal) PD_FA_BWD(64, true, MM, DR); else PD_FA_BWD(64, false, MM, DR); }
-  if (drop) {
-    if (mode == 0) { PD_FA_BWD_M(fa::kDense, true) }
-    else { PD_FA_BWD_M(fa::kVarlen, true) }
-  } else if (mode == 0) { PD_FA_BWD_M(fa::kDense, false) }
-  else if (mode == 1) { PD_FA_BWD_M(fa::kVarlen, false) }
-  else { PD_FA_BWD_M(fa::kMask, false) }
-#undef PD_FA_BWD_M
-#undef PD_FA_BWD
+#define PD_BWD(DD, FF)                                                                                              \
+  launch_bwd<DD, FF>(grid, st, q, k, v, dout, lse, delta, dqp, dk, dv, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, sdk, sdv, \
+                     pslab, scale, causal, mode, drop, ex)
+  if (D == 128) { if (f16) PD_BWD(128, true); else PD_BWD(128, false); }
+  else if (D == 64) { if (f16) PD_BWD(64, true); else PD_BWD(64, false); }
+  else { if (f16) PD_BWD(256, true); else PD_BWD(256, false); }
+#undef PD_BWD
   long work = nrows * Hq * D / 8;
   long g = (work + 255) / 256;
   if (g > 8192) g = 8192;
-  if (mode == 2)
-    fa::dq_reduce_kernel<fa::kMask><<<(int)g, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, D, nkb, pslab, sdq, causal,
-                                                            Sk - Sq, BNK, ex);
-  else if (mode == 1)
-    fa::dq_reduce_kernel<fa::kVarlen><<<(int)g, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, D, nkb, pslab, sdq, causal,
-                                                              Sk - Sq, BNK, ex);
-  else
-    fa::dq_reduce_kernel<fa::kDense><<<(int)g, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, D, nkb, pslab, sdq, causal,
-                                                             Sk - Sq, BNK, ex);
+#define PD_DQR(MM, FF)                                                                                             \
+  fa::dq_reduce_kernel<MM, FF><<<(int)g, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, D, nkb, pslab, sdq, causal, \
+                                                       Sk - Sq, BNK, ex)
+  if (mode == 2) { if (f16) PD_DQR(fa::kMask, true); else PD_DQR(fa::kMask, false); }
+  else if (mode == 1) { if (f16) PD_DQR(fa::kVarlen, true); else PD_DQR(fa::kVarlen, false); }
+  else { if (f16) PD_DQR(fa::kDense, true); else PD_DQR(fa::kDense, false); }
+#undef PD_DQR
   return (int)hipGetLastError();
 }
 

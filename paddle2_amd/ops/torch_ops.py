@@ -729,6 +729,26 @@ def _attn_reference(q, k, v, causal, scale):
     return out.to(q.dtype), lse
 
 
+_ATTN_DT = {torch.bfloat16: 1, torch.float16: 2}  # csrc/kernels/common.h DType: kBF16, kF16
+
+
+def _attn_dim(D):
+    """Kernel head dim for D: 64 / 128 / 256 run as they are; any other D <= 256 is zero-padded to the next
+    one (the padded columns add 0 to Q.K^T and produce 0 output / gradient columns)."""
+    for c in (64, 128, 256):
+        if D <= c:
+            return c
+    return None
+
+
+def _pad_d(t, Dp):
+    return t if t.shape[-1] == Dp else torch.nn.functional.pad(t, (0, Dp - t.shape[-1]))
+
+
+def _bwd_block(D):
+    return 128 if D > 128 else 256  # pd_flash_bwd_block: key-block width of the dQ partial slabs
+
+
 def _row_view_ok(t):
     # [B, S, H, D] with unit stride on D, stride D on H, uniform row stride on S, batch = S*row
     B, S, H, D = t.shape
@@ -741,21 +761,20 @@ class _FlashFn(torch.autograd.Function):
     def forward(ctx, q, k, v, causal, scale):
         B, Sq, Hq, D = q.shape
         Sk, Hk = k.shape[1], k.shape[2]
-        native = (N.use_native(q) and q.dtype == torch.bfloat16 and D in (64, 128) and Hq % Hk == 0)
+        Dp = _attn_dim(D)
+        native = (N.use_native(q) and q.dtype in _ATTN_DT and k.dtype == q.dtype and v.dtype == q.dtype
+                  and Dp is not None and Hq % Hk == 0)
         if native:
-            q_ = q if _row_view_ok(q) else q.contiguous()
-            k_ = k if _row_view_ok(k) else k.contiguous()
-            v_ = v if _row_view_ok(v) else v.contiguous()
-            out = torch.empty(B, Sq, Hq, D, dtype=q.dtype, device=q.device)
-            lse = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
-            N.native().flash_fwd(1, q_.data_ptr(), k_.data_ptr(), v_.data_ptr(), out.data_ptr(), lse.data_ptr(), B, Sq,
-                                 Sk, Hq, Hk, D, q_.stride(1), k_.stride(1), v_.stride(1), out.stride(1), float(scale),
-                                 int(causal), N.stream())
+            q_, k_, v_ = (_pad_d(t, Dp) for t in (q, k, v))
+            q_, k_, v_ = (t if _row_view_ok(t) else t.contiguous() for t in (q_, k_, v_))
+            out, lse = _flash_fwd_native(q_, k_, v_, causal, scale)
             ctx.save_for_backward(q_, k_, v_, out, lse)
+            if Dp != D:
+                out = out[..., :D]
         else:
             out, lse = _attn_reference(q, k, v, causal, scale)
             ctx.save_for_backward(q, k, v, out, lse)
-        ctx.native, ctx.causal, ctx.scale = native, causal, scale
+        ctx.native, ctx.causal, ctx.scale, ctx.D = native, causal, scale, D
         return out, lse
 
     @staticmethod
@@ -764,7 +783,7 @@ class _FlashFn(torch.autograd.Function):
         B, Sq, Hq, D = q.shape
         Sk, Hk = k.shape[1], k.shape[2]
         if ctx.native:
-            do = dout.contiguous()
+            do = _pad_d(dout, D).contiguous()
             dq = torch.empty(B, Sq, Hq, D, dtype=q.dtype, device=q.device)
             dk = torch.empty(B, Sk, Hk, D, dtype=q.dtype, device=q.device)
             dv = torch.empty(B, Sk, Hk, D, dtype=q.dtype, device=q.device)
@@ -772,6 +791,8 @@ class _FlashFn(torch.autograd.Function):
                 out = out.contiguous()
             assert out.stride(1) == do.stride(1), "out/dout row strides must match"
             _flash_bwd_native(q, k, v, out, do, lse, dq, dk, dv, ctx.scale, ctx.causal)
+            if D != ctx.D:
+                dq, dk, dv = dq[..., :ctx.D], dk[..., :ctx.D], dv[..., :ctx.D]
             return dq, dk, dv, None, None
         with torch.enable_grad():
             qq = q.detach().float().requires_grad_(True)
@@ -794,7 +815,7 @@ def _flash_fwd_native(q, k, v, causal, scale):
     Sk, Hk = k.shape[1], k.shape[2]
     out = torch.empty(B, Sq, Hq, D, dtype=q.dtype, device=q.device)
     lse = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
-    N.native().flash_fwd(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr(), B, Sq, Sk, Hq,
+    N.native().flash_fwd(_ATTN_DT[q.dtype], q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr(), B, Sq, Sk, Hq,
                          Hk, D, q.stride(1), k.stride(1), v.stride(1), out.stride(1), float(scale), int(causal),
                          N.stream())
     return out, lse
@@ -804,10 +825,11 @@ def _flash_bwd_native(q, k, v, out, do, lse, dq, dk, dv, scale, causal):
     """dq/dk/dv may be token-strided views (e.g. slices of a dQKV buffer)."""
     B, Sq, Hq, D = q.shape
     Sk, Hk = k.shape[1], k.shape[2]
-    nkb = (Sk + 255) // 256
+    bnk = _bwd_block(D)
+    nkb = (Sk + bnk - 1) // bnk
     dq32 = torch.empty(nkb * B * Sq * Hq * D, dtype=torch.float32, device=q.device)  # per-key-block dQ partials
     delta = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
-    N.native().flash_bwd(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), do.data_ptr(), lse.data_ptr(),
+    N.native().flash_bwd(_ATTN_DT[q.dtype], q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), do.data_ptr(), lse.data_ptr(),
                          delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dq32.data_ptr(), B, Sq, Sk,
                          Hq, Hk, D, q.stride(1), k.stride(1), v.stride(1), do.stride(1), dq.stride(1), dk.stride(1),
                          dv.stride(1), float(scale), int(causal), N.stream())
@@ -963,9 +985,9 @@ def _attn_reference_masked(q, k, v, causal, scale, fm):
     return torch.matmul(p, vf).transpose(1, 2).to(q.dtype), lse
 
 
-def _native_attn_ok(q, k):
-    return (q.device.type == "cuda" and N.use_native(q) and q.dtype == torch.bfloat16 and q.shape[-1] in (64, 128)
-            and q.shape[-2] % k.shape[-2] == 0)
+def _native_attn_ok(q, k, dims=(64, 128, 256)):
+    return (q.device.type == "cuda" and N.use_native(q) and q.dtype in _ATTN_DT and k.dtype == q.dtype
+            and q.shape[-1] in dims and q.shape[-2] % k.shape[-2] == 0)
 
 
 class _FlashExtFn(torch.autograd.Function):
@@ -997,7 +1019,7 @@ class _FlashExtFn(torch.autograd.Function):
             lse = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
             ptrs = (0, 0, 0, fm.data_ptr(), t64.data_ptr(), t256.data_ptr(), fm.shape[1])
         out = torch.empty_like(q)
-        N.native().flash_fwd_ext(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr(), B, Sq,
+        N.native().flash_fwd_ext(_ATTN_DT[q.dtype], q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr(), B, Sq,
                                  Sk, Hq, Hk, D, q.stride(-3), k.stride(-3), v.stride(-3), out.stride(-3), float(scale),
                                  int(causal), mode, *ptrs, *dargs, N.stream())
         ctx.save_for_backward(q, k, v, out, lse, *aux[:2] if mode == _MODE_VARLEN else aux)
@@ -1013,10 +1035,11 @@ class _FlashExtFn(torch.autograd.Function):
         do = dout.contiguous()
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         nrows = q.shape[0] if mode == _MODE_VARLEN else B * Sq
-        nkb = (Sk + 255) // 256
+        bnk = _bwd_block(D)
+        nkb = (Sk + bnk - 1) // bnk
         dq32 = torch.empty(nkb * nrows * Hq * D, dtype=torch.float32, device=q.device)
         delta = torch.empty_like(lse)
-        N.native().flash_bwd_ext(1, q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), do.data_ptr(),
+        N.native().flash_bwd_ext(_ATTN_DT[q.dtype], q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), do.data_ptr(),
                                  lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
                                  dq32.data_ptr(), B, Sq, Sk, Hq, Hk, D, q.stride(-3), k.stride(-3), v.stride(-3),
                                  do.stride(-3), dq.stride(-3), dk.stride(-3), dv.stride(-3), float(scale), int(causal),
@@ -1064,7 +1087,7 @@ def flash_attention_mask(q, k, v, startend_row_indices, causal=False, scale=None
     """FlashMask attention on [B, S, H, D] with per-key row-interval masks ([B, Hm, Sk, n], Hm in {1, Hq})."""
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
-    if _native_attn_ok(q, k) and startend_row_indices.shape[1] in (1, q.shape[2]):
+    if _native_attn_ok(q, k, (64, 128)) and startend_row_indices.shape[1] in (1, q.shape[2]):
         aux = _flashmask_prepare(startend_row_indices, causal, q.shape[0], q.shape[1], q.device)
         return _FlashExtFn.apply(q, k, v, bool(causal), float(scale), _MODE_MASK, aux, None)
     fm = flashmask_intervals(startend_row_indices.to(q.device), causal)
@@ -1248,7 +1271,8 @@ def qkv_rope_attention(qkv, num_heads, num_kv_heads, cos, sin, position_ids=None
     D = qkv.shape[-1]
     if scale is None:
         scale = 1.0 / math.sqrt(D)
-    native = (qkv.device.type == "cuda" and N.use_native(qkv) and qkv.dtype == torch.bfloat16 and D in (64, 128)
+    native = (qkv.device.type == "cuda" and N.use_native(qkv) and qkv.dtype in _ATTN_DT and qkv.dtype in _DT
+              and D in (64, 128, 256)
               and num_heads % num_kv_heads == 0)
     cos = cos.reshape(-1, D).float().contiguous()
     sin = sin.reshape(-1, D).float().contiguous()
