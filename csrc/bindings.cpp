@@ -22,6 +22,8 @@ int pd_norm_bwd(int, int, int, const void*, const void*, const void*, const floa
 int pd_swiglu_fwd(int, const void*, const void*, void*, long, int, long, long, void*);
 int pd_gemm(int, int, const void*, long, const void*, long, void*, long, void*, long, const void*, int, int, int, float,
             int, int, int, void*);
+int pd_gemm_grouped(int, int, const void*, long, const void*, long, long, void*, long, long, void*, long, const void*,
+                    long, const int*, int, int, int, int, int, int, float, int, int, void*);
 int pd_transpose16(const void*, void*, long, long, long, long, void*);
 int pd_swiglu_bwd_t(const void*, const void*, void*, void*, long, int, long, void*);
 int pd_swiglu_bwd(int, const void*, const void*, const void*, void*, void*, long, int, long, long, long, long, void*);
@@ -107,6 +109,15 @@ PYBIND11_MODULE(_C, m) {
     check(pd_gemm(layout, epi, P<const void*>(a), lda, P<const void*>(b), ldb, P<void*>(c), ldc, P<void*>(c2), ldc2,
                   P<const void*>(bias), M, N, K, beta, H, group_m, variant, P<void*>(st)),
           "gemm");
+  });
+  m.def("gemm_grouped", [](int layout, int epi, uintptr_t a, long lda, uintptr_t b, long ldb, long gsb, uintptr_t c,
+                           long ldc, long gsc, uintptr_t c2, long ldc2, uintptr_t bias, long gsbias, uintptr_t goff,
+                           int ngroups, int gmode, int M, int N, int K, int max_rows, float beta, int H, int group_m,
+                           uintptr_t st) {
+    check(pd_gemm_grouped(layout, epi, P<const void*>(a), lda, P<const void*>(b), ldb, gsb, P<void*>(c), ldc, gsc,
+                          P<void*>(c2), ldc2, P<const void*>(bias), gsbias, P<const int*>(goff), ngroups, gmode, M, N,
+                          K, max_rows, beta, H, group_m, P<void*>(st)),
+          "gemm_grouped");
   });
   m.def("swiglu_fwd", [](int dt, uintptr_t x, uintptr_t y, uintptr_t out, long rows, int H, long sx, long sy,
                          uintptr_t st) {

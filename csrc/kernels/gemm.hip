@@ -67,7 +67,55 @@ struct Params {
   float beta;
   int H;                        // swiglu: gate/up split (columns of the packed weight)
   const void* zero;             // (ablation 7) 16 zero bytes for out-of-range global_load_lds lanes
+  // grouped GEMM (MoE experts): goff [ngroups + 1] device offsets, never read back by the host.
+  //  gmode 0 (fwd / dgrad): group g owns rows [goff[g], goff[g+1]) of A and C; B (and bias) advance by gsb
+  //          (gsbias) elements per group; tiles_m is an upper bound (sum of ceil(rows_g / 256) <= it), so a
+  //          workgroup maps its row tile to (group, local tile) and leaves if it has none;
+  //  gmode 1 (wgrad): group g reduces over rows [goff[g], goff[g+1]) of both operands (A M-major, B
+  //          N-major) into its own C slab (C advances by gsc elements); grid = ngroups x the tile grid.
+  const int* goff;
+  int ngroups, gmode;
+  long gsb, gsc, gsbias;
 };
+
+// Grouped-GEMM set-up: rebase `p` onto this workgroup's group; returns false if the workgroup has no tile.
+// `bx` is the block index the tile decode below uses (gmode 1 strips the group part off it).
+template <int EPI>
+__device__ __forceinline__ bool group_setup(Params& p, int& bx) {
+  if (p.gmode == 1) {
+    const int per = p.tiles_m * p.tiles_n;
+    const int g = bx / per;
+    bx -= g * per;
+    const int r0 = p.goff[g];
+    p.K = p.goff[g + 1] - r0;
+    p.A += (long)r0 * p.lda;
+    p.B += (long)r0 * p.ldb;
+    p.C = (char*)p.C + g * p.gsc * (EPI == kEpiF32 ? 4 : 2);
+    return true;
+  }
+  return true;  // gmode 0 is resolved after the tile decode (it needs the row tile)
+}
+
+template <int EPI>
+__device__ __forceinline__ bool group_rows(Params& p, int& tm) {
+  int cum = 0, g = 0;
+  for (; g < p.ngroups; ++g) {
+    const int rows = p.goff[g + 1] - p.goff[g];
+    const int nt = (rows + BM - 1) / BM;
+    if (tm < cum + nt) break;
+    cum += nt;
+  }
+  if (g == p.ngroups) return false;
+  const int r0 = p.goff[g];
+  tm -= cum;
+  p.M = p.goff[g + 1] - r0;
+  p.A += (long)r0 * p.lda;  // gmode 0: A is K-major (rows = tokens)
+  p.C = (char*)p.C + (long)r0 * p.ldc * (EPI == kEpiF32 ? 4 : 2);
+  if (EPI == kEpiSwiGLU) p.C2 += (long)r0 * p.ldc2;
+  p.B += g * p.gsb;
+  if (p.bias) p.bias += g * p.gsbias;
+  return true;
+}
 
 __device__ __forceinline__ int xcd_remap(int bid, int n) {
   const int q = n / 8, r = n % 8, xcd = bid % 8;
@@ -302,15 +350,18 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(Params p) {
   lds_char* smem = (lds_char*)smem_raw;
   const unsigned sbase = (unsigned)(size_t)smem;
 
+  int bx = blockIdx.x;
+  if (p.goff) group_setup<EPI>(p, bx);
   const int nwg = p.tiles_m * p.tiles_n;
-  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int bid = xcd_remap(bx, nwg);
   // grouped order: group_m row-tiles sweep the column tiles together (L2 reuse within an XCD)
   const int per_group = p.group_m * p.tiles_n;
   const int gid = bid / per_group;
   const int first_m = gid * p.group_m;
   const int gsz = min(p.tiles_m - first_m, p.group_m);
-  const int tm = first_m + (bid % per_group) % gsz;
+  int tm = first_m + (bid % per_group) % gsz;
   const int tn = (bid % per_group) / gsz;
+  if (p.goff && p.gmode == 0 && !group_rows<EPI>(p, tm)) return;  // whole workgroup: no tile of any group
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -742,6 +793,7 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldc2 = ldc2;
   p.M = M; p.N = N; p.K = K; p.beta = beta; p.H = H;
   p.zero = bias;  // ablation 7 only: the caller passes a zeroed buffer in `bias`
+  p.goff = nullptr; p.ngroups = 0; p.gmode = 0; p.gsb = p.gsc = p.gsbias = 0;
   p.tiles_m = (M + BM - 1) / BM;
   p.tiles_n = epi == kEpiSwiGLU ? (H + 127) / 128 : (N + BN - 1) / BN;
   p.group_m = group_m > 0 ? group_m : 8;
@@ -778,5 +830,57 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
     default: return -4;
   }
 #undef PD_GEMM_LAUNCH
+  return (int)hipGetLastError();
+}
+
+// Grouped GEMM over expert-sorted rows (MoE): ONE launch for every group, offsets read on the device.
+//  gmode 0: C[goff[g]:goff[g+1], :N] = A[goff[g]:goff[g+1], :K] . B_g (+ bias_g), B_g = B + g*gsb
+//           (fwd: layout AK, B N-major [K, N]; dgrad: layout AK|BK, B_g read as [N, K] rows); max_rows = total
+//           rows (sizes the grid: ceil(max_rows / 256) + ngroups row tiles bound every split)
+//  gmode 1: C_g[M, N] (+)= A[goff[g]:goff[g+1], :M]^T . B[goff[g]:goff[g+1], :N], C_g = C + g*gsc (fp32 epilogue
+//           for main grads, bf16 otherwise); layout 0 (both operands token-major)
+extern "C" int pd_gemm_grouped(int layout, int epi, const void* A, long lda, const void* B, long ldb, long gsb,
+                               void* C, long ldc, long gsc, void* C2, long ldc2, const void* bias, long gsbias,
+                               const int* goff, int ngroups, int gmode, int M, int N, int K, int max_rows, float beta,
+                               int H, int group_m, void* stream) {
+  using namespace pd::gm;
+  if (ngroups <= 0 || !goff || N <= 0) return -1;
+  Params p;
+  p.A = (const unsigned short*)A;
+  p.B = (const unsigned short*)B;
+  p.C = C;
+  p.C2 = (unsigned short*)C2;
+  p.bias = (const unsigned short*)bias;
+  p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldc2 = ldc2;
+  p.N = N; p.beta = beta; p.H = H; p.zero = nullptr;
+  p.goff = goff; p.ngroups = ngroups; p.gmode = gmode; p.gsb = gsb; p.gsc = gsc; p.gsbias = gsbias;
+  p.group_m = group_m > 0 ? group_m : 8;
+  p.tiles_n = epi == kEpiSwiGLU ? (H + 127) / 128 : (N + BN - 1) / BN;
+  const bool ak = layout & 1, bk = (layout >> 1) & 1;
+  dim3 grid;
+  if (gmode == 0) {
+    if (!ak || K <= 0 || K % 8 || max_rows <= 0) return -1;
+    p.M = max_rows; p.K = K;
+    p.tiles_m = (max_rows + BM - 1) / BM + ngroups;
+    grid = dim3(p.tiles_m * p.tiles_n);
+    if (!bk && (ldb % 8 || (epi == kEpiSwiGLU ? (2 * H) % 8 : N % 8))) return -2;
+    if (epi == kEpiSwiGLU && (bk || H % 32)) return -3;
+  } else if (gmode == 1) {
+    if (layout != 0 || M <= 0 || M % 8 || N % 8 || lda % 8 || ldb % 8 || epi == kEpiSwiGLU) return -1;
+    p.M = M; p.K = 0;
+    p.tiles_m = (M + BM - 1) / BM;
+    grid = dim3(p.tiles_m * p.tiles_n * ngroups);
+  } else {
+    return -1;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  switch (epi * 4 + layout) {
+    case 0 * 4 + 0: gemm_kernel<false, false, kEpiBF16><<<grid, NTHR, 0, st>>>(p); break;
+    case 0 * 4 + 1: gemm_kernel<true, false, kEpiBF16><<<grid, NTHR, 0, st>>>(p); break;
+    case 0 * 4 + 3: gemm_kernel<true, true, kEpiBF16><<<grid, NTHR, 0, st>>>(p); break;
+    case 1 * 4 + 0: gemm_kernel<false, false, kEpiF32><<<grid, NTHR, 0, st>>>(p); break;
+    case 2 * 4 + 1: gemm_kernel<true, false, kEpiSwiGLU><<<grid, NTHR, 0, st>>>(p); break;
+    default: return -4;
+  }
   return (int)hipGetLastError();
 }

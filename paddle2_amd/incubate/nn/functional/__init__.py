@@ -191,56 +191,47 @@ def fused_multi_head_attention(x, qkv_weight, linear_weight, pre_layer_norm=Fals
 
 def variable_length_memory_efficient_attention(query, key, value, seq_lens, kv_seq_lens, mask=None, scale=None,
                                                causal=False, pre_cache_length=0):
-    """[b, h, s, d] layout with per-batch lengths (reference uses CUTLASS; here masked flash path)."""
+    """[b, h, s, d] padded layout with per-sequence query / key lengths (reference: CUTLASS
+    variable_length_memory_efficient_attention; causal = bottom-right aligned on the actual lengths).
+
+    MI355X path: ONE FlashMask launch for the whole batch — key columns past ``kv_seq_lens[b]`` are masked for
+    every row and the causal band is expressed per key column as the row interval [0, j - (kv_len - q_len)),
+    so there is no per-sequence loop and no host read of the lengths; rows past ``seq_lens[b]`` are zeroed.
+    An additive ``mask`` [b, 1 or h, s_q, s_k] takes the batched fp32 path."""
     q, k, v = query._t, key._t, value._t
-    b, h, s, d = q.shape
+    b, h, sq, d = q.shape
+    sk = k.shape[2]
     scale = scale or 1.0 / math.sqrt(d)
-    out = torch.zeros_like(q)
-    sl = seq_lens._t.reshape(-1).tolist()
-    kl = kv_seq_lens._t.reshape(-1).tolist()
-    for i in range(b):
-        qs = q[i:i + 1, :, : sl[i]].transpose(1, 2)
-        ks = k[i:i + 1, :, : kl[i]].transpose(1, 2)
-        vs = v[i:i + 1, :, : kl[i]].transpose(1, 2)
-        if mask is None:
-            o, _ = T.flash_attention(qs.contiguous(), ks.contiguous(), vs.contiguous(), causal, scale)
-        else:
-            sc = torch.einsum("bqhd,bkhd->bhqk", qs.float(), ks.float()) * scale + mask._t[i:i + 1, :, : sl[i], : kl[i]].float()
-            o = torch.einsum("bhqk,bkhd->bqhd", torch.softmax(sc, -1), vs.float()).to(q.dtype)
-        out[i, :, : sl[i]] = o[0].transpose(0, 1)
-    return _wrap(out)
+    sl = seq_lens._t.reshape(-1).to(q.device).long()
+    kl = kv_seq_lens._t.reshape(-1).to(q.device).long()
+    j = torch.arange(sk, device=q.device)[None, :]
+    key_ok = j < kl[:, None]                                           # [b, sk]
+    row_ok = torch.arange(sq, device=q.device)[None, :] < sl[:, None]  # [b, sq]
+    if mask is None:
+        lts = torch.where(key_ok, torch.full_like(j, 1 << 30), torch.zeros_like(j))
+        ute = (j - (kl - sl)[:, None]).clamp_min(0) if causal else torch.zeros_like(lts)
+        idx = torch.stack([lts, ute], -1)[:, None].to(torch.int32)       # [b, 1, sk, 2] (LTS, UTE)
+        o, _ = T.flash_attention_mask(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), idx, False, scale)
+        o = o.transpose(1, 2)
+    else:
+        sc = torch.einsum("bhqd,bhkd->bhqk", q.float(), k.float()) * scale + mask._t.float()
+        bad = ~key_ok[:, None, None, :]
+        if causal:
+            i = torch.arange(sq, device=q.device)[None, :, None]
+            bad = bad | (j[:, None, :] > i + (kl - sl)[:, None, None])[:, None]
+        sc = sc.masked_fill(bad, float("-inf"))
+        o = torch.nan_to_num(torch.softmax(sc, -1), nan=0.0)
+        o = torch.einsum("bhqk,bhkd->bhqd", o, v.float()).to(q.dtype)
+    return _wrap(o * row_ok[:, None, :, None].to(o.dtype))
 
 
-def masked_multihead_attention(x, cache_kv=None, bias=None, src_mask=None, cum_offsets=None, sequence_lengths=None,
-                               rotary_tensor=None, beam_cache_offset=None, qkv_out_scale=None, out_shift=None,
-                               out_smooth=None, seq_len=1, rotary_emb_dims=0, use_neox_rotary_style=False,
-                               compute_dtype="default", out_scale=-1, quant_round_type=1, quant_max_bound=127.0,
-                               quant_min_bound=-127.0):
-    """Single-token decode attention over a [2, b, nh, max_s, hd] KV cache (masked_multihead_attention_kernel.cu).
+def masked_multihead_attention(*args, **kwargs):
+    """Single-token decode attention over a [2, b, nh, max_s, hd] KV cache (reference
+    masked_multihead_attention_kernel.cu): writes k/v at ``sequence_lengths`` and runs the flash-decoding HIP
+    kernel (serving.masked_multihead_attention). Returns (out [b, nh*hd], cache_kv)."""
+    from ....serving import masked_multihead_attention as _mmha
 
-    x: [b, 3*nh*hd] for the new token; writes k/v at position ``sequence_lengths`` and attends over
-    the valid prefix. Returns (out [b, nh*hd], cache_kv).
-    """
-    t = x._t if bias is None else x._t + bias._t
-    ck = cache_kv._t
-    _, b, nh, max_s, hd = ck.shape
-    qkv = t.reshape(b, 3, nh, hd)
-    q, k, v = qkv[:, 0], qkv[:, 1], qkv[:, 2]
-    lens = sequence_lengths._t.reshape(-1).long() if sequence_lengths is not None else torch.zeros(
-        b, dtype=torch.long, device=t.device)
-    bi = torch.arange(b, device=t.device)
-    ck[0, bi, :, lens] = k.to(ck.dtype)
-    ck[1, bi, :, lens] = v.to(ck.dtype)
-    keys = ck[0].float()
-    vals = ck[1].float()
-    sc = torch.einsum("bnd,bnsd->bns", q.float(), keys) / math.sqrt(hd)
-    valid = torch.arange(max_s, device=t.device)[None, :] <= lens[:, None]
-    sc = sc.masked_fill(~valid[:, None, :], float("-inf"))
-    if src_mask is not None:
-        sc = sc + src_mask._t.reshape(b, 1, -1)[..., :max_s].float()
-    p = torch.softmax(sc, -1)
-    o = torch.einsum("bns,bnsd->bnd", p, vals).to(t.dtype).reshape(b, nh * hd)
-    return _wrap(o), cache_kv
+    return _mmha(*args, **kwargs)
 
 
 def block_multihead_attention(*args, **kwargs):
@@ -266,10 +257,11 @@ def fused_moe(x, gate_weight, ffn1_weight, ffn2_weight, ffn1_bias=None, ffn1_sca
     with the float weight's shape as in the reference test) with per-channel ``ffn*_scale`` [E, N]; each
     expert's weights are dequantized once per call.
 
-    MI355X path: the N*k (token, expert) assignments are sorted by expert ONCE, so each expert's rows are a
-    contiguous slice of one permuted activation matrix; a single host read of the per-expert counts sizes
-    the slices.  Each expert runs two dense GEMMs on its slice with the SwiGLU HIP kernel between them, and
-    the weighted outputs are scattered back with one ``index_add_``."""
+    MI355X path (ops/moe.py): routing, the expert sort and the per-expert offsets stay on the device; each
+    projection is ONE grouped launch of the native MFMA GEMM (the first with the SwiGLU epilogue when there is
+    no ffn1 bias) and the weighted outputs are scatter-added back — no host read of the expert counts."""
+    from ....ops import moe as MOE
+
     if quant_method not in ("None", "weight_only_int8", "weight_only_int4"):
         raise NotImplementedError(f"fused_moe: quant_method {quant_method!r}")
     quant = quant_method != "None"
@@ -278,49 +270,25 @@ def fused_moe(x, gate_weight, ffn1_weight, ffn2_weight, ffn1_bias=None, ffn1_sca
     t = x._t
     shp = t.shape
     t2 = t.reshape(-1, shp[-1])
-    n_tok, Hd = t2.shape
-    logits = t2.float() @ gate_weight._t.float()
-    probs = torch.softmax(logits, -1)
-    w, idx = torch.topk(probs, moe_topk, -1)
-    if norm_topk_prob:
-        w = w / w.sum(-1, keepdim=True)
     w1, w2 = ffn1_weight._t, ffn2_weight._t
     E = w1.shape[0]
-    wd = "int4" if quant_method == "weight_only_int4" else "int8"
-
-    def expert_w(wt, scale, e, K, N):
-        if not quant:
-            return wt[e]
+    Hd = t2.shape[1]
+    if quant:
         from ....nn.quant import _dequant
 
-        rows = N // 2 if wd == "int4" else N
-        q = wt[e].reshape(rows, K)
-        return _dequant(q, scale._t[e], wd, -1, t.dtype).t()  # [K, N]
+        wd = "int4" if quant_method == "weight_only_int4" else "int8"
 
-    N1 = ffn1_scale._t.shape[-1] if quant else w1.shape[-1]
-    F = N1 // 2
-    N2 = ffn2_scale._t.shape[-1] if quant else w2.shape[-1]
-    flat_e = idx.reshape(-1)
-    order = torch.argsort(flat_e, stable=True)
-    tok = order // moe_topk
-    gate = w.reshape(-1)[order]
-    counts = torch.bincount(flat_e, minlength=E).tolist()
-    xs = t2.index_select(0, tok)
-    ys = torch.empty(xs.shape[0], N2, dtype=t.dtype, device=t.device)
-    start = 0
-    for e, c in enumerate(counts):
-        if c == 0:
-            continue
-        seg = xs[start:start + c]
-        h = seg @ expert_w(w1, ffn1_scale, e, Hd, N1)
-        if ffn1_bias is not None:
-            h = h + ffn1_bias._t[e].reshape(-1)
-        h = T.swiglu(h)
-        o = h @ expert_w(w2, ffn2_scale, e, F, N2)
-        if ffn2_bias is not None:
-            o = o + ffn2_bias._t[e].reshape(-1)
-        ys[start:start + c] = o
-        start += c
-    out = torch.zeros(n_tok, N2, dtype=torch.float32, device=t.device)
-    out.index_add_(0, tok, ys.float() * gate[:, None])
-    return _wrap(out.to(t.dtype).reshape(*shp[:-1], N2))
+        def deq(wt, scale, K):
+            N_ = scale._t.shape[-1]
+            rows = N_ // 2 if wd == "int4" else N_
+            return torch.stack([_dequant(wt[e].reshape(rows, K), scale._t[e], wd, -1, t.dtype).t()
+                                for e in range(E)]).contiguous()  # [E, K, N], one dequant per call
+
+        w1 = deq(w1, ffn1_scale, Hd)
+        w2 = deq(w2, ffn2_scale, w1.shape[2] // 2)
+    b1 = None if ffn1_bias is None else ffn1_bias._t.reshape(E, -1)
+    b2 = None if ffn2_bias is None else ffn2_bias._t.reshape(E, -1)
+    out = MOE.moe_ffn(t2, gate_weight._t, w1.to(t.dtype).contiguous(), w2.to(t.dtype).contiguous(), moe_topk,
+                      norm_topk_prob, b1, b2)
+    N2 = out.shape[-1]
+    return _wrap(out.reshape(*shp[:-1], N2))

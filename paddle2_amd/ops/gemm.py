@@ -107,3 +107,66 @@ def mm_swiglu(x2, w):
     _launch(LAYOUT_AK, EPI_SWIGLU, x2, x2.stride(0), w, w.stride(0), a, a.stride(0), gu, gu.stride(0), None, M,
             2 * H, K, 0.0, H)
     return a, gu
+
+
+# ------------------------------------------------------------------------------------ grouped (MoE experts)
+# One launch over every expert: rows are sorted by expert and goff [E + 1] (int32, on the device) delimits
+# each expert's slice — no host read of the per-expert counts (reference fusion/cutlass/fused_moe_kernel.cu
+# runs a CUTLASS grouped GEMM from host-known problem sizes; here the kernel resolves them itself).
+def _goff_ok(goff, E):
+    return goff.dtype == torch.int32 and goff.is_contiguous() and goff.numel() == E + 1
+
+
+def grouped_fwd(xs, w, goff, bias=None, out=None):
+    """out[goff[e]:goff[e+1]] = xs[goff[e]:goff[e+1]] @ w[e] (+ bias[e]); xs [T, K], w [E, K, N] bf16."""
+    T, K = xs.shape
+    E, _, Nn = w.shape
+    assert _goff_ok(goff, E) and w.is_contiguous()
+    if out is None:
+        out = torch.empty(T, Nn, dtype=xs.dtype, device=xs.device)
+    if T:
+        N.native().gemm_grouped(LAYOUT_AK, EPI_BF16, xs.data_ptr(), xs.stride(0), w.data_ptr(), Nn, K * Nn,
+                                out.data_ptr(), out.stride(0), 0, 0, 0, N.ptr(bias), 0 if bias is None else Nn,
+                                goff.data_ptr(), E, 0, 0, Nn, K, T, 0.0, 0, GROUP_M, N.stream())
+    return out
+
+
+def grouped_swiglu(xs, w, goff):
+    """Grouped x @ w[e] with w[e] = [gate | up] ([E, K, 2F]) and the SwiGLU epilogue -> (a [T, F], gu [T, 2F])."""
+    T, K = xs.shape
+    E, _, F2 = w.shape
+    F = F2 // 2
+    assert _goff_ok(goff, E) and w.is_contiguous()
+    gu = torch.empty(T, F2, dtype=xs.dtype, device=xs.device)
+    a = torch.empty(T, F, dtype=xs.dtype, device=xs.device)
+    if T:
+        N.native().gemm_grouped(LAYOUT_AK, EPI_SWIGLU, xs.data_ptr(), xs.stride(0), w.data_ptr(), F2, K * F2,
+                                a.data_ptr(), a.stride(0), 0, gu.data_ptr(), gu.stride(0), 0, 0, goff.data_ptr(), E, 0,
+                                0, F2, K, T, 0.0, F, GROUP_M, N.stream())
+    return a, gu
+
+
+def grouped_dgrad(dy, w, goff):
+    """dx[goff[e]:goff[e+1]] = dy[...] @ w[e]^T; dy [T, N], w [E, K, N] -> dx [T, K]."""
+    T, Nn = dy.shape
+    E, K, _ = w.shape
+    assert _goff_ok(goff, E) and w.is_contiguous()
+    dx = torch.empty(T, K, dtype=dy.dtype, device=dy.device)
+    if T:
+        N.native().gemm_grouped(LAYOUT_AK | LAYOUT_BK, EPI_BF16, dy.data_ptr(), dy.stride(0), w.data_ptr(), Nn,
+                                K * Nn, dx.data_ptr(), dx.stride(0), 0, 0, 0, 0, 0, goff.data_ptr(), E, 0, 0, K, Nn, T,
+                                0.0, 0, GROUP_M, N.stream())
+    return dx
+
+
+def grouped_wgrad(xs, dy, goff, out, beta=0.0):
+    """out[e] (+)= xs[goff[e]:goff[e+1]]^T @ dy[...]; out [E, K, N] fp32 (main grad) or bf16."""
+    T, K = xs.shape
+    Nn = dy.shape[1]
+    E = out.shape[0]
+    assert _goff_ok(goff, E) and out.is_contiguous() and out.shape[1:] == (K, Nn)
+    epi = EPI_F32 if out.dtype == torch.float32 else EPI_BF16
+    N.native().gemm_grouped(0, epi, xs.data_ptr(), xs.stride(0), dy.data_ptr(), dy.stride(0), 0, out.data_ptr(), Nn,
+                            K * Nn, 0, 0, 0, 0, goff.data_ptr(), E, 1, K, Nn, 0, 0, float(beta), 0, GROUP_M,
+                            N.stream())
+    return out
