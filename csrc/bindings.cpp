@@ -25,6 +25,15 @@ int pd_gemm(int, int, const void*, long, const void*, long, void*, long, void*, 
 int pd_gemm_grouped(int, int, const void*, long, const void*, long, long, void*, long, long, void*, long, const void*,
                     long, const int*, int, int, int, int, int, int, float, int, int, void*);
 int pd_transpose16(const void*, void*, long, long, long, long, void*);
+long pd_ar_sig_bytes();
+int pd_memcpy_d2d(void*, const void*, long, void*);
+int pd_ar_alloc(long, void**);
+int pd_ar_free(void*);
+int pd_ar_get_handle(void*, void*);
+int pd_ar_open_handle(const void*, void**);
+int pd_ar_close_handle(void*);
+int pd_ar_allreduce(int, int, const void* const*, const void* const*, int, int, void*, long, long, long, unsigned,
+                    unsigned*, int, int, void*);
 int pd_swiglu_bwd_t(const void*, const void*, void*, void*, long, int, long, void*);
 int pd_swiglu_bwd(int, const void*, const void*, const void*, void*, void*, long, int, long, long, long, long, void*);
 int pd_rope(int, int, int, const void*, void*, const float*, const float*, const int64_t*, int, int, int, int, int,
@@ -118,6 +127,40 @@ PYBIND11_MODULE(_C, m) {
                           P<void*>(c2), ldc2, P<const void*>(bias), gsbias, P<const int*>(goff), ngroups, gmode, M, N,
                           K, max_rows, beta, H, group_m, P<void*>(st)),
           "gemm_grouped");
+  });
+  // ---- IPC all-reduce (csrc/kernels/ipc_allreduce.hip)
+  m.def("ar_sig_bytes", []() { return pd_ar_sig_bytes(); });
+  m.def("memcpy_d2d", [](uintptr_t dst, uintptr_t src, long bytes, uintptr_t st) {
+    check(pd_memcpy_d2d(P<void*>(dst), P<const void*>(src), bytes, P<void*>(st)), "memcpy_d2d");
+  });
+  m.def("ar_alloc", [](long bytes) {
+    void* p = nullptr;
+    check(pd_ar_alloc(bytes, &p), "ar_alloc");
+    return (uintptr_t)p;
+  });
+  m.def("ar_free", [](uintptr_t p) { check(pd_ar_free(P<void*>(p)), "ar_free"); });
+  m.def("ar_get_handle", [](uintptr_t p) {
+    char h[64];
+    check(pd_ar_get_handle(P<void*>(p), h), "ar_get_handle");
+    return py::bytes(h, 64);
+  });
+  m.def("ar_open_handle", [](py::bytes h) {
+    std::string s = h;
+    if (s.size() != 64) throw std::runtime_error("ar_open_handle: need a 64-byte IPC handle");
+    void* p = nullptr;
+    check(pd_ar_open_handle(s.data(), &p), "ar_open_handle");
+    return (uintptr_t)p;
+  });
+  m.def("ar_close_handle", [](uintptr_t p) { check(pd_ar_close_handle(P<void*>(p)), "ar_close_handle"); });
+  m.def("ar_allreduce", [](int mode, int dt, std::vector<uintptr_t> data, std::vector<uintptr_t> sig, int rank,
+                           uintptr_t out, long out_stride, long bytes, long red_off, unsigned epoch, uintptr_t err,
+                           int blocks, int timeout_ms, uintptr_t st) {
+    if (data.size() != sig.size()) throw std::runtime_error("ar_allreduce: data/sig length mismatch");
+    std::vector<const void*> d(data.size()), s(sig.size());
+    for (size_t i = 0; i < data.size(); ++i) { d[i] = P<const void*>(data[i]); s[i] = P<const void*>(sig[i]); }
+    check(pd_ar_allreduce(mode, dt, d.data(), s.data(), rank, (int)data.size(), P<void*>(out), out_stride, bytes,
+                          red_off, epoch, P<unsigned*>(err), blocks, timeout_ms, P<void*>(st)),
+          "ar_allreduce");
   });
   m.def("swiglu_fwd", [](int dt, uintptr_t x, uintptr_t y, uintptr_t out, long rows, int H, long sx, long sy,
                          uintptr_t st) {

@@ -274,6 +274,11 @@ def _all_reduce_torch(t: torch.Tensor, op=ReduceOp.SUM, group=None, sync_op=True
     if _single(g):
         return _Task(None)
     _cc.dynamic_check("all_reduce", g, t)
+    if op == ReduceOp.SUM and g.backend != "gloo" and t.is_cuda:
+        from . import ipc_allreduce  # opt-in xGMI one/two-shot path for latency-bound messages
+
+        if ipc_allreduce.maybe_all_reduce(t, pg):
+            return _Task(None)
     top = _top(op, g.backend)
     if top is None:  # AVG on gloo
         w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg, async_op=not sync_op)

@@ -1,0 +1,185 @@
+"""Latency-bound all-reduce over IPC-mapped peer buffers (csrc/kernels/ipc_allreduce.hip).
+
+Reference role: SURVEY §5.8 item 2 (custom xGMI collectives for small TP/SP messages; the reference always
+calls NCCL, process_group_nccl.cc:267).  On one MI355X node every GPU pair has its own xGMI link, so for a
+message that is latency bound (the TP all-reduce of one decode step, the ``[N, 1]`` CE statistics, the clip
+norm scalar) reading the peers' buffers directly beats a ring of 2(N-1) dependent hops:
+
+  * ``one-shot``  (<= ``oneshot_max`` bytes): each rank reads all N inputs and sums them in rank order;
+  * ``two-shot``  (<= ``capacity``): reduce-scatter + all-gather through the same mapped buffers;
+  * larger messages, non-SUM ops or groups wider than 8 go to RCCL (``dist.all_reduce``).
+
+Set-up (once per group): each rank allocates an uncached data buffer (2 x capacity) and a signal area,
+exports their 64-byte IPC handles, exchanges them with ``all_gather_object`` over the group, and maps the
+peers' buffers.  Every kernel wait is bounded; a peer that never arrives raises instead of hanging.
+
+``partition`` / ``block_ranges`` mirror the kernel's element ownership so the split logic is testable on CPU.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from ..ops import _native as N
+
+_ELT = {torch.float32: (0, 4), torch.bfloat16: (1, 2), torch.float16: (2, 2)}
+MAX_RANKS = 8
+MAX_BLOCKS = 64
+
+
+# ----------------------------------------------------------------------------------- partition model (CPU)
+def block_ranges(nv, blocks):
+    """[(lo, hi)] of 16-B vectors per workgroup for a range of nv vectors (kernel block_range)."""
+    per = (nv + blocks - 1) // blocks
+    out = []
+    for b in range(blocks):
+        lo = min(nv, per * b)
+        out.append((lo, min(nv, lo + per)))
+    return out
+
+
+def partition(nbytes, nranks, blocks, mode):
+    """Per (phase, rank, block) the vector ranges the kernel touches:
+    mode 0: {"reduce": {rank: [ranges]}}; mode 1: {"reduce": {rank: ...}, "gather": {rank: ...}}."""
+    nv = nbytes // 16
+    if mode == 0:
+        return {"reduce": {r: block_ranges(nv, blocks) for r in range(nranks)}}
+    sl = (nv + nranks - 1) // nranks
+    red, gat = {}, {}
+    for r in range(nranks):
+        s0 = min(nv, sl * r)
+        s1 = min(nv, s0 + sl)
+        red[r] = [(s0 + lo, s0 + hi) for lo, hi in block_ranges(s1 - s0, blocks)]
+    for r in range(nranks):
+        gat[r] = [rng for p in range(nranks) if p != r for rng in red[p]]
+    return {"reduce": red, "gather": gat}
+
+
+def choose_mode(nbytes, oneshot_max, capacity):
+    if nbytes > capacity:
+        return None
+    return 0 if nbytes <= oneshot_max else 1
+
+
+# ----------------------------------------------------------------------------------- communicator
+class IpcAllReduce:
+    """SUM all-reduce of CUDA tensors over a group of <= 8 ranks on one node."""
+
+    def __init__(self, group=None, capacity=32 << 20, oneshot_max=1 << 20, blocks=32, timeout_ms=10000,
+                 exchange=None):
+        import torch.distributed as dist
+
+        self.group = group
+        self.rank = dist.get_rank(group) if group is not None else dist.get_rank()
+        self.world = dist.get_world_size(group) if group is not None else dist.get_world_size()
+        if self.world > MAX_RANKS:
+            raise ValueError(f"IpcAllReduce: group of {self.world} ranks > {MAX_RANKS}")
+        self.capacity, self.oneshot_max = int(capacity), int(oneshot_max)
+        self.blocks, self.timeout_ms = min(int(blocks), MAX_BLOCKS), int(timeout_ms)
+        C = N.native()
+        if C is None:
+            raise RuntimeError("IpcAllReduce needs the native extension on a GPU")
+        self._C = C
+        self._data = C.ar_alloc(2 * self.capacity)   # [input | reduced slices (two-shot)]
+        self._sig = C.ar_alloc(C.ar_sig_bytes())
+        mine = (C.ar_get_handle(self._data), C.ar_get_handle(self._sig))
+        gather = exchange or self._exchange
+        handles = gather(mine)
+        self._opened = []
+        self.data_ptrs, self.sig_ptrs = [], []
+        for r, (hd, hs) in enumerate(handles):
+            if r == self.rank:
+                self.data_ptrs.append(self._data)
+                self.sig_ptrs.append(self._sig)
+            else:
+                pd_, ps_ = C.ar_open_handle(hd), C.ar_open_handle(hs)
+                self._opened += [pd_, ps_]
+                self.data_ptrs.append(pd_)
+                self.sig_ptrs.append(ps_)
+        self._err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        self.epoch = 0
+
+    def _exchange(self, mine):
+        import torch.distributed as dist
+
+        out = [None] * self.world
+        dist.all_gather_object(out, mine, group=self.group)
+        return out
+
+    def supports(self, t, op_sum=True):
+        return (op_sum and t.is_cuda and t.dtype in _ELT and t.is_contiguous()
+                and (t.numel() * t.element_size()) % 16 == 0 and 0 < t.numel() * t.element_size() <= self.capacity)
+
+    def all_reduce(self, t, check=False):
+        """In-place SUM of ``t`` over the group (t contiguous, CUDA, size % 16 B == 0, <= capacity)."""
+        nbytes = t.numel() * t.element_size()
+        mode = choose_mode(nbytes, self.oneshot_max, self.capacity)
+        if mode is None:
+            raise ValueError("IpcAllReduce: message larger than capacity")
+        C = self._C
+        st = N.stream()
+        C.memcpy_d2d(self._data, t.data_ptr(), nbytes, st)
+        self.epoch += 1
+        C.ar_allreduce(mode, _ELT[t.dtype][0], self.data_ptrs, self.sig_ptrs, self.rank, t.data_ptr(), 0, nbytes,
+                       self.capacity, self.epoch, self._err.data_ptr(), self.blocks, self.timeout_ms, st)
+        if check:
+            self.raise_on_timeout()
+        return t
+
+    def raise_on_timeout(self):
+        e = int(self._err.item())
+        if e:
+            raise RuntimeError(f"IpcAllReduce: peers {[p for p in range(self.world) if e >> p & 1]} did not arrive "
+                               f"within {self.timeout_ms} ms")
+
+    def close(self):
+        C = self._C
+        for p in self._opened:
+            C.ar_close_handle(p)
+        self._opened = []
+        if self._data:
+            C.ar_free(self._data)
+            C.ar_free(self._sig)
+            self._data = self._sig = 0
+
+
+def local_allreduce(tensors, mode=0, blocks=8, timeout_ms=5000):
+    """Run the kernel protocol for len(tensors) simulated ranks in ONE launch on one GPU (grid.y = rank; every
+    rank's blocks are co-resident, buffers addressed directly, flags through the same signal areas): the 1-GPU
+    test of the kernel and its flag barriers.  Returns the per-rank outputs and the error word."""
+    C = N.native()
+    R = len(tensors)
+    nbytes = tensors[0].numel() * tensors[0].element_size()
+    data = [C.ar_alloc(2 * nbytes) for _ in range(R)]
+    sig = [C.ar_alloc(C.ar_sig_bytes()) for _ in range(R)]
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    out = torch.empty(R, *tensors[0].shape, dtype=tensors[0].dtype, device="cuda")
+    try:
+        for r, t in enumerate(tensors):
+            C.memcpy_d2d(data[r], t.data_ptr(), nbytes, N.stream())
+        C.ar_allreduce(mode, _ELT[tensors[0].dtype][0], data, sig, -1, out.data_ptr(), nbytes, nbytes, nbytes, 1,
+                       err.data_ptr(), blocks, timeout_ms, N.stream())
+        torch.cuda.synchronize()
+    finally:
+        for p in data + sig:
+            C.ar_free(p)
+    return list(out.unbind(0)), int(err.item())
+
+
+_COMM = {}
+
+
+def maybe_all_reduce(t, group=None):
+    """collective.all_reduce hook: IPC path for small SUM messages when PADDLE2_AMD_IPC_ALLREDUCE=1 (opt-in);
+    returns True if it handled the tensor."""
+    if os.environ.get("PADDLE2_AMD_IPC_ALLREDUCE") != "1" or not t.is_cuda:
+        return False
+    key = id(group)
+    comm = _COMM.get(key)
+    if comm is None:
+        comm = _COMM[key] = IpcAllReduce(group)
+    if not comm.supports(t):
+        return False
+    comm.all_reduce(t)
+    return True
