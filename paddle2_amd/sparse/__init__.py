@@ -1,53 +1,23 @@
-"""paddle.sparse (COO/CSR) on torch sparse tensors (reference: python/paddle/sparse/)."""
+"""paddle.sparse — COO / CSR sparse tensors and their ops (reference: python/paddle/sparse/, 5.6 k LoC, and
+paddle/phi/kernels/sparse/).  See creation.py (storage + Tensor methods), ops.py (math), nn/ (sparse
+convolution via rulebook + grouped MFMA GEMM, pooling, activations, softmax, attention, batch norm)."""
 from __future__ import annotations
 
-import torch
+from . import nn  # noqa: F401
+from .creation import sparse_coo_tensor, sparse_csr_tensor  # noqa: F401
+from .ops import (abs, add, addmm, asin, asinh, atan, atanh, cast, coalesce, deg2rad, divide, expm1,  # noqa: F401
+                  is_same_shape, isnan, log1p, mask_as, masked_matmul, matmul, multiply, mv, neg, pca_lowrank,
+                  pow, rad2deg, reshape, sin, sinh, slice, sqrt, square, subtract, sum, tan, tanh, transpose)
 
-from ..framework.tensor import Tensor
-
-_w = Tensor._wrap
-
-
-def sparse_coo_tensor(indices, values, shape=None, dtype=None, place=None, stop_gradient=True):
-    i = indices._t if isinstance(indices, Tensor) else torch.as_tensor(indices)
-    v = values._t if isinstance(values, Tensor) else torch.as_tensor(values)
-    t = torch.sparse_coo_tensor(i, v, size=shape).coalesce()
-    return _w(t)
-
-
-def sparse_csr_tensor(crows, cols, values, shape, dtype=None, place=None, stop_gradient=True):
-    c = crows._t if isinstance(crows, Tensor) else torch.as_tensor(crows)
-    co = cols._t if isinstance(cols, Tensor) else torch.as_tensor(cols)
-    v = values._t if isinstance(values, Tensor) else torch.as_tensor(values)
-    return _w(torch.sparse_csr_tensor(c, co, v, size=shape))
-
-
-def matmul(x, y, name=None):
-    return _w(torch.sparse.mm(x._t, y._t) if x._t.is_sparse else torch.matmul(x._t, y._t))
-
-
-def add(x, y, name=None):
-    return _w(x._t + y._t)
-
-
-def multiply(x, y, name=None):
-    return _w(x._t * y._t)
+__all__ = ["sparse_coo_tensor", "sparse_csr_tensor", "sin", "tan", "asin", "atan", "sinh", "tanh", "asinh", "atanh",
+           "sqrt", "square", "log1p", "abs", "pow", "pca_lowrank", "cast", "neg", "deg2rad", "rad2deg", "expm1", "mv",
+           "matmul", "mask_as", "masked_matmul", "addmm", "add", "subtract", "transpose", "sum", "multiply", "divide",
+           "coalesce", "is_same_shape", "reshape", "isnan", "slice"]
 
 
 def to_dense(x):
-    return _w(x._t.to_dense())
+    return x.to_dense()
 
 
 def relu(x, name=None):
-    t = x._t.coalesce()
-    return _w(torch.sparse_coo_tensor(t.indices(), torch.relu(t.values()), t.shape))
-
-
-def is_same_shape(x, y):
-    return list(x.shape) == list(y.shape)
-
-
-class nn:
-    class ReLU:
-        def __call__(self, x):
-            return relu(x)
+    return nn.functional.relu(x)
