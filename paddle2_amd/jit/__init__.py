@@ -66,9 +66,11 @@ class StaticFunction:
         try:
             with static.program_guard(prog, static.Program()):
                 sym_args, feeds = [], []
+                specs = list(self._input_spec or [])
                 for i, a in enumerate(args):
                     if isinstance(a, Tensor):
-                        name = f"input_{i}"
+                        sp = specs[i] if i < len(specs) else None
+                        name = getattr(sp, "name", None) or f"input_{i}"
                         v = static.data(name, list(a.shape), a.dtype)
                         sym_args.append(v)
                         feeds.append(name)

@@ -141,6 +141,13 @@ class Executor:
             strategy = program._build_strategy
             program = program._program
         program = program or default_main_program()
+        from .pdmodel import PdProgram
+
+        if isinstance(program, PdProgram):  # a reference-format model loaded by load_inference_model
+            feed = feed or {}
+            xs = [_feed_tensor(feed[n], None, self._device) for n in program.feed_names]
+            outs = program.run(xs)
+            return [o.detach().cpu().numpy() if return_numpy else Tensor._wrap(o) for o in outs]
         if not isinstance(program, Program):
             raise TypeError("Executor.run expects a static Program")
         feed = feed or {}

@@ -133,10 +133,26 @@ def serialize_persistables(feed_vars, fetch_vars, executor=None, program=None, *
 
 
 def save_inference_model(path_prefix, feed_vars, fetch_vars, executor=None, program=None, **kwargs):
+    """Writes the reference format (ProgramDesc ``.pdmodel`` + save_combine ``.pdiparams``, static/pdmodel.py) when
+    every op lowers to a Paddle op type; otherwise (``format="native"`` or an op outside the lowering table) the
+    framework's own op-list program."""
     from ..framework.io import save as _save
+    from . import pdmodel
+    from .graph import default_main_program
 
     feed_vars = feed_vars if isinstance(feed_vars, (list, tuple)) else [feed_vars]
     fetch_vars = fetch_vars if isinstance(fetch_vars, (list, tuple)) else [fetch_vars]
+    if kwargs.get("format", "paddle") == "paddle":
+        prog = program or default_main_program()
+        fetch_ids = [f._t._vid for f in fetch_vars]
+        feeds = {v._t._name: v._t for v in feed_vars}
+        try:
+            pdmodel.save(path_prefix, prog, _prune(prog, fetch_ids), feeds, fetch_ids, _fn_name)
+            return
+        except pdmodel.Unmapped as e:
+            import warnings
+
+            warnings.warn(f"save_inference_model: {e} has no Paddle op mapping; writing the native program format")
     model, tensors = serialize_program(feed_vars, fetch_vars, program)
     with open(path_prefix + ".pdmodel", "wb") as f:
         f.write(model)
@@ -209,6 +225,13 @@ def load_inference_model(path_prefix, executor=None, **kwargs):
     from ..framework.place import current_torch_device
 
     dev = executor._device if executor is not None else current_torch_device()
+    with open(path_prefix + ".pdmodel", "rb") as f:
+        head = f.read(1)
+    from . import pdmodel
+
+    if pdmodel.is_program_desc(head):
+        prog = pdmodel.load(path_prefix, dev)
+        return [prog, prog.feed_names, prog.fetch_names]
     params = _load(path_prefix + ".pdiparams")
     params = {k: Tensor._wrap(v._t.to(dev)) for k, v in params.items()}
     with open(path_prefix + ".pdmodel", "rb") as f:
