@@ -41,3 +41,8 @@ res["grads"] = grads
 perf = fleet.collective_perf("allreduce", round=3, size_and_time={1 << 16: None, 1 << 18: 100.0})
 res["perf"] = [(r["bytes"], r["nranks"], r["time_ms"] > 0, r["busbw_GBs"] > 0) for r in perf]
 write_result(res)
+# leave together: a rank exiting while its peer's gloo threads still talk to it can abort the peer
+import torch.distributed as _tdist  # noqa: E402
+
+_tdist.barrier()
+_tdist.destroy_process_group()
