@@ -495,9 +495,21 @@ class GroupShardedOptimizer:
                 u.grad_clean = False
 
     def _global_sq_norm(self):
-        sq = torch.zeros(1, dtype=torch.float32, device=self._model._units[0].device)
-        for u in self._model._units:
-            sq += torch.dot(u.grad_shard, u.grad_shard)
+        from ...ops import _native as N
+
+        shards = [u.grad_shard for u in self._model._units]
+        if shards[0].is_cuda and N.use_native(shards[0]) and all(g.dtype == shards[0].dtype for g in shards):
+            # one multi-tensor launch over every unit's fp32 grad shard (csrc/kernels/optim.hip sqnorm_mt)
+            key = tuple(g.data_ptr() for g in shards)
+            if getattr(self, "_sq_key", None) != key:
+                from ...optimizer.multi_tensor import MultiTensorTable
+
+                self._sq_table, self._sq_key = MultiTensorTable.for_grads(shards), key
+            sq = self._sq_table.sqnorm()
+        else:
+            sq = torch.zeros(1, dtype=torch.float32, device=self._model._units[0].device)
+            for g in shards:
+                sq += torch.dot(g, g)
         g = self._model._group
         if g.nranks > 1:
             dist.all_reduce(sq, group=g.pg)
