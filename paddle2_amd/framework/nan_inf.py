@@ -1,11 +1,14 @@
 """NaN/Inf checker (reference: paddle/fluid/eager/nan_inf_utils.cc:84 ``CheckTensorHasNanOrInf``,
 ``FLAGS_check_nan_inf`` / ``FLAGS_check_nan_inf_level`` flags.cc:79).
 
-The reference scans every op output inside the generated ``<op>_ad_func``.  Our eager ops are
-PyTorch-ROCm kernels plus fused HIP nodes, so the scan sits at the Layer boundary: when the flag is
-on, every ``Layer.__call__`` output is scanned (one fused ``isfinite().all()`` reduction per tensor),
-and a gradient hook scans the gradient flowing back into that output, so a NaN is attributed to
-the first layer (forward) or the last layer (backward) that produced it.
+The reference scans every op output inside the generated ``<op>_ad_func``.  Here two granularities run
+together when the flag is on:
+  * per OP: a torch dispatch mode sees every ATen kernel the program runs — forward AND backward ops
+    (autograd's backward kernels dispatch through it too) — and scans each floating output, naming the
+    op (``aten.mm.default``) that produced the first NaN/Inf;
+  * per LAYER: every ``Layer.__call__`` output is scanned and a gradient hook scans the gradient flowing
+    back into it, which also covers the fused HIP nodes (their kernels write into buffers the dispatch mode
+    only sees allocated, so freshly allocated ``empty`` outputs are never scanned).
 
 Levels (reference semantics): 0 = raise on the first NaN/Inf; 1 = log and continue;
 2 = also log fp32 stats (min/max/mean) of offending tensors; 3 = log stats of every checked tensor.
@@ -28,6 +31,45 @@ def _sync_from_flags():
 
     enabled = bool(flags.flag("FLAGS_check_nan_inf", False))
     level = int(flags.flag("FLAGS_check_nan_inf_level", 0))
+    _set_op_mode(enabled)
+
+
+_SKIP = ("empty", "empty_like", "empty_strided", "new_empty", "new_empty_strided", "set_", "_local_scalar_dense",
+         "isfinite", "isnan", "isinf", "detach", "alias", "view", "_to_copy")
+
+
+def _make_mode():
+    from torch.utils._python_dispatch import TorchDispatchMode
+
+    class _OpChecker(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            out = func(*args, **(kwargs or {}))
+            name = func.overloadpacket.__name__
+            if name not in _SKIP and not _busy[0]:
+                _busy[0] = True
+                try:
+                    for i, t in enumerate(_tensors(out)):
+                        if t.device.type != "meta":
+                            check_tensor(t, f"op {func}", f"output[{i}]")
+                finally:
+                    _busy[0] = False
+            return out
+
+    return _OpChecker()
+
+
+_mode = [None]
+_busy = [False]
+
+
+def _set_op_mode(on):
+    if on and _mode[0] is None:
+        m = _make_mode()
+        m.__enter__()
+        _mode[0] = m
+    elif not on and _mode[0] is not None:
+        m, _mode[0] = _mode[0], None
+        m.__exit__(None, None, None)
 
 
 def _tensors(out):
