@@ -35,7 +35,8 @@ def _sync_from_flags():
 
 
 _SKIP = ("empty", "empty_like", "empty_strided", "new_empty", "new_empty_strided", "set_", "_local_scalar_dense",
-         "isfinite", "isnan", "isinf", "detach", "alias", "view", "_to_copy")
+         "isfinite", "isnan", "isinf", "detach", "alias", "view", "_to_copy", "lift_fresh", "lift",
+         "lift_fresh_copy", "scalar_tensor", "copy_", "clone")  # allocation / data-movement, not compute
 
 
 def _make_mode():
