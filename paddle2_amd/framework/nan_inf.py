@@ -49,9 +49,10 @@ def _make_mode():
             if name not in _SKIP and not _busy[0]:
                 _busy[0] = True
                 try:
+                    phase = "backward op" if torch._C._current_graph_task_id() != -1 else "op"
                     for i, t in enumerate(_tensors(out)):
                         if t.device.type != "meta":
-                            check_tensor(t, f"op {func}", f"output[{i}]")
+                            check_tensor(t, f"{phase} {func}", f"output[{i}]")
                 finally:
                     _busy[0] = False
             return out
