@@ -1,9 +1,12 @@
 // Host event tracer (reference: paddle/phi/api/profiler/host_tracer.cc + host_event_recorder.h —
 // per-thread lock-free event buffers merged at collection; chrome_tracing_logger.cc export).
 //
-// Each thread appends to its own chunked buffer (no lock on the hot path after the first event
-// of a thread); names are interned once.  RecordEvent in Python maps to push/pop; collection
-// walks every thread's buffer.
+// Each thread appends to its own buffer guarded by its own mutex — uncontended on the hot path (only a
+// collection takes it from another thread); names are interned once.  RecordEvent in Python maps to
+// push/pop; collection walks every thread's buffer.  (The first version appended lock-free and let a
+// concurrent collection copy a vector the owner was reallocating: found by the TSan/ASan stress build,
+// csrc/runtime/stress/runtime_stress.cpp.)
+#include <atomic>
 #include <chrono>
 #include <sstream>
 #include <thread>
@@ -16,15 +19,16 @@ namespace {
 
 struct ThreadBuf {
   uint64_t tid;
+  std::mutex mu;                 // owner appends, collectors copy / clear
   std::vector<HostEvent> done;
-  std::vector<HostEvent> stack;
+  std::vector<HostEvent> stack;  // owner-only
 };
 
 std::mutex g_mu;                       // guards the registry and the name table
 std::vector<std::shared_ptr<ThreadBuf>> g_bufs;
 std::unordered_map<std::string, uint32_t> g_name_ids;
 std::vector<std::string> g_names;
-bool g_on = false;
+std::atomic<bool> g_on{false};
 
 ThreadBuf& tbuf() {
   thread_local std::shared_ptr<ThreadBuf> b;
@@ -79,24 +83,33 @@ void tracer_pop() {
   b.stack.pop_back();
   if (!g_on) return;
   e.end_ns = tracer_now_ns();
+  std::lock_guard<std::mutex> g(b.mu);
   b.done.push_back(e);
 }
 
 void tracer_instant(const std::string& name, uint32_t type, uint64_t s, uint64_t e) {
   if (!g_on) return;
   auto& b = tbuf();
-  b.done.push_back({intern(name), type, b.tid, s, e});
+  const uint32_t id = intern(name);
+  std::lock_guard<std::mutex> g(b.mu);
+  b.done.push_back({id, type, b.tid, s, e});
 }
 
 void tracer_clear() {
   std::lock_guard<std::mutex> g(g_mu);
-  for (auto& b : g_bufs) b->done.clear();
+  for (auto& b : g_bufs) {
+    std::lock_guard<std::mutex> gb(b->mu);
+    b->done.clear();
+  }
 }
 
 std::vector<HostEvent> tracer_events() {
   std::lock_guard<std::mutex> g(g_mu);
   std::vector<HostEvent> out;
-  for (auto& b : g_bufs) out.insert(out.end(), b->done.begin(), b->done.end());
+  for (auto& b : g_bufs) {
+    std::lock_guard<std::mutex> gb(b->mu);
+    out.insert(out.end(), b->done.begin(), b->done.end());
+  }
   return out;
 }
 

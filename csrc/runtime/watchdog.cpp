@@ -10,7 +10,7 @@
 
 #include <atomic>
 #include <chrono>
-#include <condition_variable>
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -42,20 +42,30 @@ EventQueryFn event_query() {
 std::vector<int64_t> w_finished;
 
 std::mutex w_mu;
-std::condition_variable w_cv;
 std::map<int64_t, Task> w_tasks;
 std::vector<std::string> w_timed_out;
 std::atomic<int64_t> w_next{1};
 std::thread w_thread;
-bool w_run = false;
+std::atomic<bool> w_run{false};  // also read by the poller between condition-variable waits
 bool w_abort = false;
-double w_poll = 1.0;
+std::atomic<double> w_poll{1.0};
+
+// Sleep in <= 5 ms slices between scans (no condition variable: stop latency is one slice, and the loop
+// stays analysable by the sanitizer build, whose runtime does not model libstdc++'s clockwait waits).
+bool nap(double seconds) {
+  const auto until = std::chrono::steady_clock::now() + std::chrono::duration_cast<std::chrono::steady_clock::duration>(
+                                                            std::chrono::duration<double>(seconds));
+  while (w_run.load()) {
+    const auto now = std::chrono::steady_clock::now();
+    if (now >= until) return true;
+    std::this_thread::sleep_for(std::min<std::chrono::steady_clock::duration>(until - now, std::chrono::milliseconds(5)));
+  }
+  return false;
+}
 
 void loop() {
-  std::unique_lock<std::mutex> lk(w_mu);
-  while (w_run) {
-    w_cv.wait_for(lk, std::chrono::duration<double>(w_poll));
-    if (!w_run) break;
+  while (nap(w_poll)) {
+    std::lock_guard<std::mutex> lk(w_mu);
     auto now = std::chrono::steady_clock::now();
     EventQueryFn q = event_query();
     for (auto it = w_tasks.begin(); it != w_tasks.end();) {
@@ -96,7 +106,6 @@ void watchdog_stop() {
     if (!w_run) return;
     w_run = false;
   }
-  w_cv.notify_all();
   if (w_thread.joinable()) w_thread.join();
 }
 

@@ -114,8 +114,9 @@ def build_runtime(verbose=False):
              "-I", rdir]
     h = hashlib.sha1(" ".join(flags).encode())
     for f in sorted(os.listdir(rdir)):
-        with open(os.path.join(rdir, f), "rb") as fh:
-            h.update(fh.read())
+        if os.path.isfile(os.path.join(rdir, f)):
+            with open(os.path.join(rdir, f), "rb") as fh:
+                h.update(fh.read())
     key = h.hexdigest()[:16]
     out = runtime_target_path()
     stamp = out + ".stamp"
@@ -139,6 +140,28 @@ def build_runtime(verbose=False):
     os.replace(tmp, out)
     with open(stamp, "w") as f:
         f.write(key)
+    return out
+
+
+_SAN_FLAGS = {
+    "thread": ["-fsanitize=thread"],
+    "address": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
+}
+
+
+def build_sanitized(kind="thread", verbose=False):
+    """Sanitizer build of the host runtime (store, watchdog, tracer) linked into the stress driver
+    csrc/runtime/stress/runtime_stress.cpp: ``kind`` "thread" (TSan, data races) or "address" (ASan + UBSan).
+    Host code only — GPU sanitizers are not used on this hardware.  Returns the executable path."""
+    rdir = os.path.join(CSRC, "runtime")
+    srcs = [os.path.join(rdir, f) for f in ("tcp_store.cpp", "watchdog.cpp", "tracer.cpp")]
+    srcs.append(os.path.join(rdir, "stress", "runtime_stress.cpp"))
+    os.makedirs(BUILD, exist_ok=True)
+    out = os.path.join(BUILD, f"runtime_stress_{kind}")
+    cmd = ["g++", "-O1", "-g", "-std=c++17", "-I", rdir] + _SAN_FLAGS[kind] + srcs + ["-o", out, "-lpthread", "-ldl"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    _run(cmd)
     return out
 
 
