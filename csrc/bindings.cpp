@@ -26,6 +26,9 @@ int pd_gemm_grouped(int, int, const void*, long, const void*, long, long, void*,
                     long, const int*, int, int, int, int, int, int, float, int, int, void*);
 int pd_transpose16(const void*, void*, long, long, long, long, void*);
 long pd_ar_sig_bytes();
+int pd_bias_act(int, int, int, const void*, const void*, void*, long, int, long, long, void*);
+int pd_bias_act_bwd(int, int, int, const void*, const void*, const void*, void*, long, int, long, long, void*);
+int pd_dropout_add(int, int, const void*, const void*, void*, long, unsigned, float, void*);
 int pd_memcpy_d2d(void*, const void*, long, void*);
 int pd_ar_alloc(long, void**);
 int pd_ar_free(void*);
@@ -161,6 +164,21 @@ PYBIND11_MODULE(_C, m) {
     check(pd_ar_allreduce(mode, dt, d.data(), s.data(), rank, (int)data.size(), P<void*>(out), out_stride, bytes,
                           red_off, epoch, P<unsigned*>(err), blocks, timeout_ms, P<void*>(st)),
           "ar_allreduce");
+  });
+  m.def("bias_act", [](int dt, int gated, int act, uintptr_t x, uintptr_t b, uintptr_t out, long rows, int H, long sx,
+                       long so, uintptr_t st) {
+    check(pd_bias_act(dt, gated, act, P<const void*>(x), P<const void*>(b), P<void*>(out), rows, H, sx, so,
+                      P<void*>(st)), "bias_act");
+  });
+  m.def("bias_act_bwd", [](int dt, int gated, int act, uintptr_t x, uintptr_t b, uintptr_t dout, uintptr_t dx,
+                           long rows, int H, long sx, long sd, uintptr_t st) {
+    check(pd_bias_act_bwd(dt, gated, act, P<const void*>(x), P<const void*>(b), P<const void*>(dout), P<void*>(dx),
+                          rows, H, sx, sd, P<void*>(st)), "bias_act_bwd");
+  });
+  m.def("dropout_add", [](int dt, int bwd, uintptr_t x, uintptr_t y, uintptr_t out, long n, unsigned seed, float p,
+                          uintptr_t st) {
+    check(pd_dropout_add(dt, bwd, P<const void*>(x), P<const void*>(y), P<void*>(out), n, seed, p, P<void*>(st)),
+          "dropout_add");
   });
   m.def("swiglu_fwd", [](int dt, uintptr_t x, uintptr_t y, uintptr_t out, long rows, int H, long sx, long sy,
                          uintptr_t st) {

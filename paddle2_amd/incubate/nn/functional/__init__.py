@@ -134,23 +134,26 @@ def fused_feedforward(x, linear1_weight, linear2_weight, linear1_bias=None, line
                       ln1_bias=None, ln2_scale=None, ln2_bias=None, dropout1_rate=0.5, dropout2_rate=0.5,
                       activation="relu", ln1_epsilon=1e-5, ln2_epsilon=1e-5, pre_layer_norm=False, training=True,
                       mode="upscale_in_train", ring_id=-1, add_residual=True, name=None):
+    """Transformer FFN block (reference fused_feedforward_kernel.cu): [LN] -> x W1 -> bias+act (fused kernel) ->
+    dropout -> W2 -> bias -> dropout + residual (fused kernel) -> [LN]; GEMMs through the Linear GEMM path."""
+    from ....ops import fused as FU
+
     t = x._t
     res = t
     if pre_layer_norm:
         t = T.layer_norm(t, _u(ln1_scale), _u(ln1_bias), ln1_epsilon)
-    h = torch.matmul(t, linear1_weight._t)
-    if linear1_bias is not None:
-        h = h + linear1_bias._t
-    h = getattr(torch.nn.functional, activation)(h)
+    h = T.linear(t, linear1_weight._t)
+    h = FU.bias_act(h, _u(linear1_bias), activation)
     if training and dropout1_rate:
         h = torch.nn.functional.dropout(h, dropout1_rate)
-    o = torch.matmul(h, linear2_weight._t)
-    if linear2_bias is not None:
-        o = o + linear2_bias._t
-    if training and dropout2_rate:
-        o = torch.nn.functional.dropout(o, dropout2_rate)
-    if add_residual:
-        o = o + res
+    o = T.linear(h, linear2_weight._t, _u(linear2_bias))
+    if training and dropout2_rate and mode == "upscale_in_train" and add_residual:
+        o = FU.dropout_add(o, res, dropout2_rate)
+    else:
+        if training and dropout2_rate:
+            o = torch.nn.functional.dropout(o, dropout2_rate)
+        if add_residual:
+            o = o + res
     if not pre_layer_norm:
         o = T.layer_norm(o, _u(ln2_scale), _u(ln2_bias), ln2_epsilon)
     return _wrap(o)

@@ -1,0 +1,65 @@
+"""Fused bias+activation and dropout+add (csrc/kernels/fused_act.hip, ops/fused.py) vs fp32 PyTorch
+definitions; the dropout mask is a counter hash shared bit-for-bit by the kernel and the host model
+(reference: fused_bias_act_kernel.cu, fused_dropout_add_kernel.cu; test_fused_bias_act_op.py)."""
+import pytest
+import torch
+
+import paddle2_amd as paddle
+from paddle2_amd.incubate.nn import functional as IF
+from paddle2_amd.ops import fused as FU
+
+DEVS = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+def _ref_act(name, t):
+    F = torch.nn.functional
+    H = t.shape[-1] // 2
+    return {"gelu": F.gelu, "relu": torch.relu, "silu": F.silu, "identity": lambda v: v,
+            "swiglu": lambda v: F.silu(v[..., :H]) * v[..., H:],
+            "geglu": lambda v: F.gelu(v[..., :H]) * v[..., H:]}[name](t)
+
+
+@pytest.mark.parametrize("dev", DEVS)
+@pytest.mark.parametrize("act", ["gelu", "relu", "silu", "identity", "swiglu", "geglu"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bias_act_fwd_bwd(dev, act, dtype):
+    g = torch.Generator().manual_seed(0)
+    x0, b0 = torch.randn(37, 64, generator=g), torch.randn(64, generator=g)
+    dy0 = torch.randn(37, 32 if act in ("swiglu", "geglu") else 64, generator=g)
+    x = x0.to(dev, dtype).requires_grad_()
+    b = b0.to(dev, dtype).requires_grad_()
+    y = FU.bias_act(x, b, act)
+    y.backward(dy0.to(dev, dtype))
+    xr = x0.to(dtype).float().requires_grad_()
+    br = b0.to(dtype).float().requires_grad_()
+    yr = _ref_act(act, xr + br)
+    yr.backward(dy0.to(dtype).float())
+    tol = 1e-5 if dtype == torch.float32 else 3e-2
+    torch.testing.assert_close(y.float().cpu(), yr.detach(), rtol=tol, atol=tol)
+    torch.testing.assert_close(x.grad.float().cpu(), xr.grad, rtol=tol, atol=tol)
+    torch.testing.assert_close(b.grad.float().cpu(), br.grad, rtol=tol, atol=max(tol, 0.3 if dtype != torch.float32 else 0))
+
+
+@pytest.mark.parametrize("dev", DEVS)
+def test_dropout_add_mask_and_grads(dev):
+    n, p, seed = 4096, 0.3, 12345
+    x = torch.randn(16, 256, device=dev).requires_grad_()
+    y = torch.randn(16, 256, device=dev).requires_grad_()
+    out = FU.dropout_add(x, y, p, seed)
+    keep = FU.dropout_keep(seed, n, p).reshape(16, 256).to(dev)
+    torch.testing.assert_close(out, x.detach() * keep / (1 - p) + y.detach())
+    assert abs(keep.float().mean().item() - (1 - p)) < 0.03
+    out.sum().backward()
+    torch.testing.assert_close(x.grad, keep.float() / (1 - p))
+    torch.testing.assert_close(y.grad, torch.ones_like(y))
+
+
+def test_incubate_entry_points():
+    x = paddle.randn([4, 16])
+    b = paddle.randn([16])
+    out = IF.fused_bias_act(x, b, act_method="swiglu")
+    assert out.shape == [4, 8]
+    r = IF.fused_dropout_add(paddle.ones([4, 8]), paddle.zeros([4, 8]), p=0.5, training=True)
+    vals = set(r._t.unique().tolist())
+    assert vals <= {0.0, 2.0}
+    assert IF.fused_dropout_add(paddle.ones([2, 8]), paddle.ones([2, 8]), p=0.5, training=False)._t.eq(2).all()
