@@ -168,6 +168,34 @@ class PipelineLayer(Layer):
                 return vs % self._num_stages
         raise IndexError(layer_idx)
 
+    # ------------------------------------------------------------------ pipeline-agnostic checkpoints
+    def _global_key_map(self):
+        """local state-dict key -> "layers.{global layer index}.{param}" (shared layers keep
+        "shared_layers.{name}.*"), so a checkpoint does not depend on the pp / vpp split."""
+        m = {}
+        for c, vs in enumerate(self._chunk_vstages):
+            li = 0
+            for g in range(self.segment_parts[vs], self.segment_parts[vs + 1]):
+                item = self._model_chunks[c]._items[g - self.segment_parts[vs]]
+                if isinstance(item, Layer) and not isinstance(self._layers_desc[g], SharedLayerDesc):
+                    for k in item.state_dict():
+                        m[f"_model_chunks.{c}.run_function.{li}.{k}"] = f"layers.{g}.{k}"
+                        if self.run_function is not None and c == 0:  # the V == 1 alias of chunk 0
+                            m[f"run_function.{li}.{k}"] = f"layers.{g}.{k}"
+                if isinstance(item, Layer):
+                    li += 1
+        return m
+
+    def global_state_dict(self):
+        km = self._global_key_map()
+        return {km.get(k, k): v for k, v in self.state_dict().items()}
+
+    def set_global_state_dict(self, sd):
+        km = self._global_key_map()
+        local = {lk: sd[gk] for lk, gk in km.items() if gk in sd}
+        local.update({k: v for k, v in sd.items() if k in self.state_dict() and k not in km})
+        return self.set_state_dict(local)
+
     def get_num_virtual_stages(self):
         return self._num_virtual_pipeline_stages
 
