@@ -12,11 +12,29 @@ _wrap = Tensor._wrap
 
 
 def _reshape_shape(t, shape):
+    from ..framework import errors as E
+
     shp = shape_arg(shape)
     # paddle: 0 means "copy this dim from input"
     out = []
     for i, s in enumerate(shp):
         out.append(t.shape[i] if s == 0 and i < t.dim() else s)
+    E.enforce(sum(1 for s in out if s == -1) <= 1, E.InvalidArgumentError,
+              f"Only one dimension value of 'shape' in ReshapeOp can be -1, but received shape {list(shp)}.")
+    known = 1
+    for s in out:
+        E.enforce(s >= -1, E.InvalidArgumentError, f"Each dimension value of 'shape' must be >= -1, got {s}.")
+        known *= s if s > 0 else 1
+    n = t.numel()
+    if -1 in out:
+        E.enforce(known > 0 and n % known == 0, E.InvalidArgumentError,
+                  f"The 'shape' attribute in ReshapeOp is invalid: input numel {n} is not divisible by the known "
+                  f"dims product {known} (shape {list(shp)}).")
+    elif 0 not in out:
+        E.enforce(known == n, E.InvalidArgumentError,
+                  f"The 'shape' in ReshapeOp is invalid: the input tensor X's size is {n}, but the target shape "
+                  f"{list(shp)} has {known} elements.",
+                  hint=f"input shape {list(t.shape)}")
     return out
 
 
