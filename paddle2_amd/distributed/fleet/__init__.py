@@ -143,12 +143,16 @@ def distributed_model(model):
                                 find_unused_parameters=strategy.find_unused_parameters)
         return model
     if mode == ParallelMode.PIPELINE_PARALLEL:
-        from .meta_parallel.pipeline_parallel import PipelineParallel, PipelineParallelWithInterleave
+        from .meta_parallel import pipeline_parallel as PPm
 
-        acc = strategy.pipeline_configs.get("accumulate_steps", 1)
+        mode_s = str(strategy.pipeline_configs.get("schedule_mode", "1F1B"))
         if getattr(model, "_num_virtual_pipeline_stages", 1) > 1:
-            return PipelineParallelWithInterleave(model, hcg, strategy)
-        return PipelineParallel(model, hcg, strategy)
+            if mode_s == "FThenB":
+                return PPm.PipelineParallelWithInterleaveFthenB(model, hcg, strategy)
+            return PPm.PipelineParallelWithInterleave(model, hcg, strategy)
+        cls = {"FThenB": PPm.PipelineParallelFThenB, "ZBH1": PPm.PipelineParallelZeroBubble,
+               "ZB": PPm.PipelineParallelZeroBubble}.get(mode_s, PPm.PipelineParallel)
+        return cls(model, hcg, strategy)
     if mode == ParallelMode.TENSOR_PARALLEL:
         from .meta_parallel.tensor_parallel import TensorParallel
 

@@ -4,5 +4,5 @@ from .parallel_layers import (ColumnParallelLinear, LayerDesc, ParallelCrossEntr
                               RNGStatesTracker, RowParallelLinear, SharedLayerDesc, VocabParallelEmbedding,
                               get_rng_state_tracker, model_parallel_random_seed)
 from .pipeline_parallel import (PipelineParallel, PipelineParallelFThenB, PipelineParallelWithInterleave,  # noqa
-                                PipelineParallelWithInterleaveFthenB)
+                                PipelineParallelWithInterleaveFthenB, PipelineParallelZeroBubble)
 from .tensor_parallel import SegmentParallel, ShardingParallel, TensorParallel  # noqa

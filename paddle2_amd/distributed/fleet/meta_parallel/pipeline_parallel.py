@@ -1,4 +1,4 @@
-"""Pipeline parallelism: 1F1B, FThenB and interleaved (VPP) schedules.
+"""Pipeline parallelism: 1F1B, FThenB, interleaved (VPP) and zero-bubble (ZB-H1) schedules.
 
 Reference: fleet/meta_parallel/pipeline_parallel.py — ``PipelineParallel`` :255 (1F1B
 ``forward_backward_pipeline`` :575-763, ``train_batch`` :820, ``eval_batch``),
@@ -14,7 +14,13 @@ producer ran, and at the end of each tick a rank posts ONE ``batch_isend_irecv``
 exactly its sends and the matching receives.  Because both ends of every transfer derive it from
 the same simulation and post it in the same tick's group, the schedule is deadlock-free by
 construction for any ordering (1F1B, FThenB, VPP with wrap-around ``S-1 -> 0`` hand-offs), and
-RCCL runs each group's transfers concurrently over the xGMI peer links.  Shapes/dtypes cross each
+RCCL runs each group's transfers concurrently over the xGMI peer links.
+
+Zero bubble (ZB-H1, Qi et al. 2023; reference passes/pipeline_scheduler_pass/pipeline_zero_bubble.py): the
+backward splits into B (input gradient — what the previous stage waits for) and W (weight gradients, no
+cross-stage consumer).  B units run with ops.torch_ops.WeightGradStore deferring every Linear's weight GEMM;
+each stage delays its W units by (S - 1 - s) steady steps so they fill the cool-down bubble that 1F1B leaves
+idle on the later stages.  Shapes/dtypes cross each
 stage boundary once (a small meta handshake on first use), then buffers are allocated directly.
 
 Overlap: a tick's group is posted and NOT waited — receives are waited only when the unit that
@@ -33,6 +39,7 @@ from ....framework.tensor import Tensor
 from ...collective import ReduceOp
 from ..utils.hybrid_parallel_util import broadcast_dp_parameters, broadcast_mp_parameters, \
     broadcast_sep_parameters, broadcast_sharding_parameters
+from ....ops.torch_ops import WeightGradStore
 from .meta_parallel_base import MetaParallelBase
 
 _wrap = Tensor._wrap
@@ -56,6 +63,25 @@ def unit_orders(S, s, M, V, schedule="1F1B"):
         c, mb = fwd(k)
         return V - 1 - c, mb
 
+    if schedule == "ZBH1":
+        assert V == 1, "ZB-H1 is a single-chunk schedule"
+        warm = min(S - s - 1, M)
+        lag = S - s - 1   # W of micro-batch i runs after B of micro-batch i + lag
+        out = [("F", 0, k) for k in range(warm)]
+        nw = 0
+        for i in range(M - warm):
+            out.append(("F", 0, warm + i))
+            out.append(("B", 0, i))
+            if i >= lag:
+                out.append(("W", 0, nw))
+                nw += 1
+        for i in range(M - warm, M):
+            out.append(("B", 0, i))
+            if nw <= i:
+                out.append(("W", 0, nw))
+                nw += 1
+        out += [("W", 0, k) for k in range(nw, M)]
+        return out
     if schedule == "FThenB" or schedule == "F":
         out = [("F",) + fwd(k) for k in range(total)]
         if schedule == "FThenB":
@@ -97,6 +123,8 @@ def simulate(S, M, V, schedule="1F1B"):
             vs = c * S + r
             if kind == "F":
                 ready = vs == 0 or done.get(("F", vs - 1, mb), t) < t
+            elif kind == "W":
+                ready = done.get(("B", vs, mb), t) < t
             else:
                 ready = done.get(("F", vs, mb), t) < t and (vs == last or done.get(("B", vs + 1, mb), t) < t)
             if not ready:
@@ -333,6 +361,8 @@ class PipelineParallel(MetaParallelBase):
 
         self._device = current_torch_device()
         last_vs = S * V - 1
+        zb = sched == "ZBH1"
+        w_queues = {}
         act_in, act_out, losses, outputs = {}, {}, [], []
         pending_send, recv_buf = {}, {}
         loss_fn = getattr(self._layers, "_loss_fn", None)
@@ -350,8 +380,13 @@ class PipelineParallel(MetaParallelBase):
                         xin = tuple(tt.requires_grad_(rg and _is_float(tt)) for tt, rg in ts)
                         x = _unflat(xin)
                     ctx = torch.enable_grad() if not forward_only else torch.no_grad()
+                    WeightGradStore.route = zb
+                    try:
+                        with ctx:
+                            y = self._layers(x, chunk_id=c) if V > 1 else self._layers(x)
+                    finally:
+                        WeightGradStore.route = False
                     with ctx:
-                        y = self._layers(x, chunk_id=c) if V > 1 else self._layers(x)
                         if vs == last_vs:
                             if loss_fn is not None and compute_loss and lab_mb[mb] is not None:
                                 loss = loss_fn(y, lab_mb[mb])
@@ -370,20 +405,28 @@ class PipelineParallel(MetaParallelBase):
                             pending_send[("F", vs, mb)] = yt
                     if not forward_only:
                         act_in[(vs, mb)] = xin
-                else:  # backward
+                elif kind == "W":  # zero bubble: the deferred weight-gradient GEMMs of (vs, mb)
+                    WeightGradStore.run(w_queues.pop((vs, mb), []))
+                else:  # backward (ZB-H1: input gradients only, weight GEMMs queued for the W unit)
                     outs = act_out.pop((vs, mb))
-                    if vs == last_vs:
-                        if scaler is not None and hasattr(scaler, "scale"):
-                            l = scaler.scale(_wrap(outs[0]))._t
+                    WeightGradStore.defer = zb
+                    try:
+                        if vs == last_vs:
+                            if scaler is not None and hasattr(scaler, "scale"):
+                                l = scaler.scale(_wrap(outs[0]))._t
+                            else:
+                                l = outs[0]
+                            torch.autograd.backward(l)
                         else:
-                            l = outs[0]
-                        torch.autograd.backward(l)
-                    else:
-                        grads = self._take(recv_buf, ("B", vs + 1, mb))
-                        pairs = [(o, g) for o, g in zip(outs, grads) if isinstance(o, torch.Tensor) and o.requires_grad
-                                 and g is not None]
-                        if pairs:
-                            torch.autograd.backward([o for o, _ in pairs], [g for _, g in pairs])
+                            grads = self._take(recv_buf, ("B", vs + 1, mb))
+                            pairs = [(o, g) for o, g in zip(outs, grads)
+                                     if isinstance(o, torch.Tensor) and o.requires_grad and g is not None]
+                            if pairs:
+                                torch.autograd.backward([o for o, _ in pairs], [g for _, g in pairs])
+                    finally:
+                        WeightGradStore.defer = False
+                    if zb:
+                        w_queues[(vs, mb)] = WeightGradStore.take()
                     xin = act_in.pop((vs, mb))
                     if vs > 0 and xin is not None:
                         pending_send[("B", vs, mb)] = tuple(
@@ -527,3 +570,9 @@ class PipelineParallelWithInterleaveFthenB(PipelineParallel):
 
 class PipelineParallelFThenB(PipelineParallel):
     _schedule = "FThenB"
+
+
+class PipelineParallelZeroBubble(PipelineParallel):
+    """ZB-H1: B/W-split backward with the W units delayed into the cool-down bubble."""
+
+    _schedule = "ZBH1"

@@ -19,10 +19,10 @@ _wrap = Tensor._wrap
 def linear(x, weight, bias=None, name=None):
     t = x._t
     w = weight._t
-    if (t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and w.dim() == 2) or \
-            getattr(w, "_p2_gt", None) is not None:  # weight grad -> fp32 main-grad buffer
-        from ...ops import torch_ops as T
+    from ...ops import torch_ops as T
 
+    if (t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and w.dim() == 2) or \
+            getattr(w, "_p2_gt", None) is not None or T.WeightGradStore.route:  # main grad / zero-bubble split
         return _wrap(T.linear(t, w, None if bias is None else bias._t))
     if bias is not None:
         b = bias._t

@@ -320,6 +320,43 @@ def _linear_plan(M, K, Nn):
     return M >= 4096 and K % 8 == 0, M >= 8192 and Nn >= 2 * K
 
 
+class WeightGradStore:
+    """Zero-bubble pipeline support (reference: the ZB-H1 / ZBV schedules' split of backward into B = input
+    gradient and W = weight gradient, distributed/passes/pipeline_scheduler_pass/pipeline_zero_bubble.py).
+
+    ``route``: set during a zero-bubble stage's forward so every Linear runs through ``_LinearFn`` (whose
+    backward can split); ``defer``: set during a B unit — the Linear backward then computes only dX and
+    queues its weight-gradient GEMM; ``take()`` hands the queue to the W unit, which runs it later to fill a
+    pipeline bubble.  Weight grads land in ``param.grad`` (or the fp32 main-grad buffer) exactly as in a
+    normal backward."""
+
+    route = False
+    defer = False
+    _queue = []
+
+    @classmethod
+    def put(cls, fn):
+        cls._queue.append(fn)
+
+    @classmethod
+    def take(cls):
+        q, cls._queue = cls._queue, []
+        return q
+
+    @staticmethod
+    def run(queue):
+        for fn in queue:
+            fn()
+
+
+def _accumulate_grad(w, dw):
+    with torch.no_grad():
+        if w.grad is None:
+            w.grad = dw.to(w.dtype)
+        else:
+            w.grad.add_(dw.to(w.grad.dtype))
+
+
 class _LinearFn(torch.autograd.Function):
     """y = x @ W (+ b) with W [K, N] (Paddle layout) — GEMM layouts picked per shape (see _linear_plan)."""
 
@@ -343,6 +380,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x2, w)
         ctx.meta = (x.shape, dw_t, b is not None)
         ctx.gt = getattr(w, "_p2_gt", None)
+        ctx.w_leaf = w if WeightGradStore.route else None
         return y.view(*x.shape[:-1], Nn)
 
     @staticmethod
@@ -361,7 +399,17 @@ class _LinearFn(torch.autograd.Function):
                 dx = G.mm_dgrad(dy2, w).view(xshape)
             else:
                 dx = torch.matmul(dy2, w.t()).view(xshape)
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and WeightGradStore.defer and (ctx.gt is not None or ctx.w_leaf is not None):
+            gt, wl = ctx.gt, ctx.w_leaf
+
+            def _w_pass(x2=x2, dy2=dy2, gt=gt, wl=wl):
+                if gt is not None:
+                    _main_grad_accumulate(gt, x2, dy2)
+                else:
+                    _accumulate_grad(wl, weight_grad(x2, dy2))
+
+            WeightGradStore.put(_w_pass)
+        elif ctx.needs_input_grad[1]:
             if ctx.gt is not None:
                 _main_grad_accumulate(ctx.gt, x2, dy2)
             elif _pass_native("wgrad", x2) and G.supported_wgrad(x2, dy2):
@@ -454,7 +502,8 @@ def linear(x, w, b=None):
     when the weight's gradient goes to an fp32 main-grad buffer); plain matmul otherwise."""
     if (x.device.type == "cuda" and x.dtype in (torch.bfloat16, torch.float16) and w.dtype == x.dtype
             and w.dim() == 2 and x.shape[-1] == w.shape[0] and N.use_native(x)) or \
-            (getattr(w, "_p2_gt", None) is not None and w.dim() == 2 and x.shape[-1] == w.shape[0]):
+            (getattr(w, "_p2_gt", None) is not None and w.dim() == 2 and x.shape[-1] == w.shape[0]) or \
+            (WeightGradStore.route and w.dim() == 2 and x.shape[-1] == w.shape[0] and w.requires_grad):
         return _LinearFn.apply(x, w, b)
     y = torch.matmul(x, w)
     return y + b if b is not None else y

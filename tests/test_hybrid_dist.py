@@ -16,7 +16,8 @@ def test_tensor_parallel_llama_matches_single():
     _close(run_workers("hybrid_worker.py", 2, ["tp"]))
 
 
-@pytest.mark.parametrize("schedule,vpp,n", [("1F1B", 1, 2), ("FThenB", 1, 2), ("1F1B", 2, 2), ("1F1B", 1, 4)])
+@pytest.mark.parametrize("schedule,vpp,n", [("1F1B", 1, 2), ("FThenB", 1, 2), ("1F1B", 2, 2), ("1F1B", 1, 4),
+                                            ("ZBH1", 1, 2), ("ZBH1", 1, 4)])
 def test_pipeline_matches_grad_accumulation(schedule, vpp, n):
     _close(run_workers("hybrid_worker.py", n, ["pp", schedule, str(vpp)]), 1e-4)
 
@@ -58,3 +59,30 @@ def test_tp2_pp2_llama_matches_single():
 
 def test_gpt_sequence_parallel_matches_tensor_parallel():
     _close(run_workers("hybrid_worker.py", 2, ["gpt_sp"]), 1e-4)
+
+
+def test_weight_grad_store_splits_backward():
+    """ZB-H1's B/W split: with defer on, Linear backward leaves weight grads to the queued W pass."""
+    import paddle2_amd as paddle
+    from paddle2_amd.ops.torch_ops import WeightGradStore
+
+    paddle.seed(3)
+    lin = paddle.nn.Linear(8, 4)
+    x = paddle.randn([5, 8])
+    x.stop_gradient = False
+    WeightGradStore.route = True
+    try:
+        y = lin(x)
+    finally:
+        WeightGradStore.route = False
+    WeightGradStore.defer = True
+    try:
+        y.sum().backward()
+    finally:
+        WeightGradStore.defer = False
+    q = WeightGradStore.take()
+    assert len(q) == 1 and lin.weight.grad is None and x.grad is not None
+    WeightGradStore.run(q)
+    import torch
+
+    torch.testing.assert_close(lin.weight.grad._t, x._t.detach().t() @ torch.ones(5, 4))

@@ -142,6 +142,10 @@ def run_pp(schedule, vpp):
         from paddle2_amd.distributed.fleet.meta_parallel import PipelineParallelFThenB
 
         model.__class__ = PipelineParallelFThenB
+    if schedule == "ZBH1":
+        from paddle2_amd.distributed.fleet.meta_parallel import PipelineParallelZeroBubble
+
+        model.__class__ = PipelineParallelZeroBubble
     opt = paddle.optimizer.SGD(0.1, parameters=model.parameters())
     opt = fleet.distributed_optimizer(opt)
     g = torch.Generator().manual_seed(2)
