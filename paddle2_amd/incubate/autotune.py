@@ -60,3 +60,82 @@ def set_config(config=None):
 def status():
     """Newly tuned entries are written to the cache file when the process exits."""
     return dict(_state)
+
+
+# --------------------------------------------------------------------------------------------------
+# Native-vs-library routing of the Linear GEMMs (ops/torch_ops.py _pass_native): with routing autotune on,
+# the first time a (pass, M, N, K, dtype) is seen both the hand-written MFMA kernel (ops/gemm.py) and hipBLASLt
+# run it a few times on scratch outputs, timed with device events, and the faster one is cached (in memory
+# and in tuning/gemm_routing_gfx950.json, so later processes reuse the decision without re-timing).
+DEFAULT_ROUTING_CACHE = os.path.join(_ROOT, "tuning", "gemm_routing_gfx950.json")
+_routing = {"enable": False, "file": None, "table": {}, "iters": 3}
+
+
+def enable_routing_autotune(filename=None, iters=3):
+    filename = filename or DEFAULT_ROUTING_CACHE
+    _routing.update(enable=True, file=filename, iters=int(iters))
+    if os.path.exists(filename):
+        with open(filename) as f:
+            _routing["table"].update(json.load(f))
+    return filename
+
+
+def disable_routing_autotune():
+    _routing["enable"] = False
+
+
+def routing_table():
+    return dict(_routing["table"])
+
+
+def _bench(fn, iters):
+    import torch
+
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def route(pass_name, a, b):
+    """True -> native kernel for this GEMM, False -> hipBLASLt; None when routing autotune is off."""
+    if not _routing["enable"] or not a.is_cuda:
+        return None
+    import torch
+
+    from ..ops import gemm as G
+
+    if pass_name == "fwd":
+        M, K = a.shape
+        N = b.shape[1]
+        nat, lib = (lambda: G.mm_fwd(a, b)), (lambda: torch.matmul(a, b))
+    elif pass_name == "dgrad":
+        M, N = a.shape
+        K = b.shape[0]
+        nat, lib = (lambda: G.mm_dgrad(a, b)), (lambda: torch.matmul(a, b.t()))
+    elif pass_name in ("wgrad", "wgrad32"):
+        K, M = a.shape[1], a.shape[0]
+        N = b.shape[1]
+        if pass_name == "wgrad":
+            nat, lib = (lambda: G.mm_wgrad_bf16(a, b)), (lambda: torch.matmul(a.t(), b))
+        else:
+            scratch = torch.empty(K, N, dtype=torch.float32, device=a.device)
+            nat = lambda: G.mm_wgrad(a, b, scratch, 0.0)  # noqa: E731
+            lib = lambda: torch.addmm(scratch, a.t(), b, beta=0.0, out_dtype=torch.float32, out=scratch)  # noqa
+    else:
+        return None
+    key = f"{pass_name}:{M}x{N}x{K}:{str(a.dtype).replace('torch.', '')}"
+    hit = _routing["table"].get(key)
+    if hit is not None:
+        return hit == "native"
+    tn, tl = _bench(nat, _routing["iters"]), _bench(lib, _routing["iters"])
+    _routing["table"][key] = "native" if tn <= tl else "blas"
+    if _routing["file"]:
+        os.makedirs(os.path.dirname(_routing["file"]), exist_ok=True)
+        with open(_routing["file"], "w") as f:
+            json.dump(_routing["table"], f, indent=1, sort_keys=True)
+    return tn <= tl

@@ -368,7 +368,7 @@ class _LinearFn(torch.autograd.Function):
         fwd_t, dw_t = _linear_plan(M, K, Nn)
         from . import gemm as G
 
-        if _pass_native("fwd", x2) and G.supported_fwd(x2, w) and (b is None or b.dtype == x2.dtype):
+        if G.supported_fwd(x2, w) and (b is None or b.dtype == x2.dtype) and _pass_native("fwd", x2, w):
             y = G.mm_fwd(x2, w, bias=None if b is None else b.contiguous())
         else:
             if fwd_t:
@@ -395,7 +395,7 @@ class _LinearFn(torch.autograd.Function):
         from . import gemm as G
 
         if ctx.needs_input_grad[0]:
-            if _pass_native("dgrad", dy2) and G.supported_dgrad(dy2, w):
+            if G.supported_dgrad(dy2, w) and _pass_native("dgrad", dy2, w):
                 dx = G.mm_dgrad(dy2, w).view(xshape)
             else:
                 dx = torch.matmul(dy2, w.t()).view(xshape)
@@ -412,7 +412,7 @@ class _LinearFn(torch.autograd.Function):
         elif ctx.needs_input_grad[1]:
             if ctx.gt is not None:
                 _main_grad_accumulate(ctx.gt, x2, dy2)
-            elif _pass_native("wgrad", x2) and G.supported_wgrad(x2, dy2):
+            elif G.supported_wgrad(x2, dy2) and _pass_native("wgrad", x2, dy2):
                 dw = G.mm_wgrad_bf16(x2, dy2)
             elif dw_t:
                 dw = torch.matmul(transpose2d(x2), transpose2d(dy2).t())
@@ -423,12 +423,21 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
-def _pass_native(name, t):
+def _pass_native(name, t, other=None):
     """Per-pass GEMM backend (PADDLE2_AMD_GEMM_{FWD,DGRAD,WGRAD} = native | blas): the hand-written MFMA
-    kernel (ops/gemm.py) or hipBLASLt, chosen per pass from measured speed (profiles/r2_gemm_native.md)."""
+    kernel (ops/gemm.py) or hipBLASLt, chosen per pass from measured speed (profiles/r2_gemm_native.md) — or,
+    with routing autotune on (incubate.autotune.enable_routing_autotune), per shape from timing both."""
     from . import gemm as G
 
-    return G.enabled(t) and _GEMM_PASS.get(name, "native") == "native"
+    if not G.enabled(t):
+        return False
+    if other is not None:
+        from ..incubate import autotune as _at
+
+        r = _at.route(name, t, other)
+        if r is not None:
+            return r
+    return _GEMM_PASS.get("wgrad" if name == "wgrad32" else name, "native") == "native"
 
 
 _GEMM_PASS = {"fwd": _os.environ.get("PADDLE2_AMD_GEMM_FWD", "blas"),
@@ -443,8 +452,8 @@ def wgrad_accumulate(out, x2, dy2, beta):
     if out.device.type == "cuda":
         from . import gemm as G
 
-        if (_pass_native("wgrad", x2) and out.dtype == torch.float32 and out.is_contiguous()
-                and G.supported_wgrad(x2, dy2)):
+        if (out.dtype == torch.float32 and out.is_contiguous() and G.supported_wgrad(x2, dy2)
+                and _pass_native("wgrad32", x2, dy2)):
             G.mm_wgrad(x2, dy2, out, beta)
             return out
         torch.addmm(out, x2.t(), dy2, beta=float(beta), out_dtype=out.dtype, out=out)
@@ -460,7 +469,7 @@ def mm(x2, w, b=None):
     _GEMM_PASS), shared by nn.Linear and the tensor-/sequence-parallel linears."""
     from . import gemm as G
 
-    if x2.dim() == 2 and _pass_native("fwd", x2) and G.supported_fwd(x2, w) and (b is None or b.dtype == x2.dtype):
+    if x2.dim() == 2 and G.supported_fwd(x2, w) and (b is None or b.dtype == x2.dtype) and _pass_native("fwd", x2, w):
         return G.mm_fwd(x2, w, bias=None if b is None else b.contiguous())
     y = torch.matmul(x2, w)
     return y + b if b is not None else y
@@ -470,7 +479,7 @@ def mm_t(dy2, w):
     """dx[M, K] = dy2[M, N] @ w[K, N]^T (the Linear input-gradient GEMM)."""
     from . import gemm as G
 
-    if dy2.dim() == 2 and _pass_native("dgrad", dy2) and G.supported_dgrad(dy2, w):
+    if dy2.dim() == 2 and G.supported_dgrad(dy2, w) and _pass_native("dgrad", dy2, w):
         return G.mm_dgrad(dy2, w)
     return torch.matmul(dy2, w.t())
 
@@ -483,7 +492,7 @@ def weight_grad(x2, dy2, gt=None):
         return None
     from . import gemm as G
 
-    if _pass_native("wgrad", x2) and G.supported_wgrad(x2, dy2):
+    if G.supported_wgrad(x2, dy2) and _pass_native("wgrad", x2, dy2):
         return G.mm_wgrad_bf16(x2, dy2)
     return torch.matmul(x2.t(), dy2)
 
