@@ -35,6 +35,7 @@ from .distributed.parallel import DataParallel  # noqa: F401,E402
 from . import metric, vision, hapi, static, jit, profiler, incubate, utils, sparse, linalg, fft, signal  # noqa: F401,E402
 from . import distribution, regularizer, callbacks, version  # noqa: F401,E402
 from . import _C_ops  # noqa: F401,E402
+from . import pir, decomposition  # noqa: F401,E402
 from .hapi import Model, summary, flops  # noqa: F401,E402
 from .static import enable_static, disable_static, in_dynamic_mode  # noqa: F401,E402
 from .framework import dtype  # noqa: F401,E402

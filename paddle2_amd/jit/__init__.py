@@ -76,12 +76,25 @@ class StaticFunction:
                         feeds.append(name)
                     else:
                         sym_args.append(a)
-                out = self._fn(*sym_args) if self._layer is None else self._fn(self._layer, *sym_args)
+                fn = self._converted()
+                out = fn(*sym_args) if self._layer is None else fn(self._layer, *sym_args)
         finally:
             g._state.static = was
         single = isinstance(out, Tensor)
         outs = [out] if single else list(out)
         return prog, feeds, outs, single
+
+    def _converted(self):
+        """The dy2static-converted function: tensor-dependent ``if`` / ``while`` become static.nn.cond /
+        while_loop while recording (jit/dy2static.py); unconvertible functions are used as written."""
+        if not hasattr(self, "_conv"):
+            from .dy2static import convert_function
+
+            try:
+                self._conv = convert_function(self._fn)
+            except (SyntaxError, TypeError, ValueError):
+                self._conv = self._fn
+        return self._conv
 
     def get_program(self, *args):
         key = _sig(args)
@@ -101,24 +114,23 @@ class StaticFunction:
         res = exe.run(target, feed=feed, fetch_list=outs, return_numpy=False, _grad=torch.is_grad_enabled())
         return res[0] if single else tuple(res)
 
+    def __get__(self, obj, objtype=None):
+        """``@to_static`` on a method: bind the instance; the bound StaticFunction (and its per-signature
+        Program cache) lives on the instance so repeated calls replay instead of re-recording."""
+        if obj is None or self._layer is not None:
+            return self
+        key = f"_pd_static_{id(self)}"
+        bound = obj.__dict__.get(key)
+        if bound is None:
+            bound = StaticFunction(self._fn, self._input_spec, self._build_strategy, layer=obj)
+            obj.__dict__[key] = bound
+        return bound
+
     @property
     def concrete_program(self):
         if not self._cache:
             return None
         return next(iter(self._cache.values()))[0]
-
-
-class _BoundStatic:
-    """Descriptor so ``to_static`` applied to a method binds the layer."""
-
-    def __init__(self, sf):
-        self.sf = sf
-
-    def __get__(self, obj, objtype=None):
-        if obj is None:
-            return self.sf
-        return functools.partial(self.sf.__call__.__func__, StaticFunction(self.sf._fn, self.sf._input_spec,
-                                                                            self.sf._build_strategy, obj))
 
 
 def to_static(function=None, input_spec=None, build_strategy=None, backend=None, full_graph=True, **kwargs):
