@@ -5,6 +5,8 @@ from .io import load, save  # noqa: F401
 from .grad_mode import no_grad  # noqa: F401
 from .param import ParamAttr  # noqa: F401
 from .flags import get_flags, set_flags  # noqa: F401
+from . import tensor_types  # noqa: F401,E402
+from .tensor_types import SelectedRows, StringTensor, TensorArray  # noqa: F401,E402
 
 
 def in_dynamic_mode():

@@ -125,6 +125,9 @@ upsample = interpolate
 def embedding(x, weight, padding_idx=None, sparse=False, max_norm=None, norm_type=2.0, scale_grad_by_freq=False, name=None):
     from ...ops import embedding as _emb
 
+    if sparse:
+        # row-sparse weight gradient (SelectedRows): the optimizers update only the looked-up rows
+        return _wrap(F.embedding(x._t.long(), weight._t, padding_idx=padding_idx, sparse=True))
     return _emb(x, weight, padding_idx)
 
 

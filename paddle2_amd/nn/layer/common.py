@@ -250,6 +250,7 @@ class Embedding(Layer):
         from ...framework.dtype import get_default_dtype
 
         self._num, self._dim = num_embeddings, embedding_dim
+        self._sparse = sparse
         self._padding_idx = padding_idx if padding_idx is None or padding_idx >= 0 else padding_idx + num_embeddings
         self.weight = self.create_parameter([num_embeddings, embedding_dim], attr=weight_attr,
                                             dtype=get_default_dtype(), default_initializer=I.XavierUniform())
@@ -258,7 +259,7 @@ class Embedding(Layer):
                 self.weight._t[self._padding_idx] = 0
 
     def forward(self, x):
-        return F.embedding(x, self.weight, padding_idx=self._padding_idx)
+        return F.embedding(x, self.weight, padding_idx=self._padding_idx, sparse=self._sparse)
 
     def extra_repr(self):
         return f"{self._num}, {self._dim}"

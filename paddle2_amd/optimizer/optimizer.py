@@ -17,6 +17,7 @@ import torch
 from ..framework.tensor import Tensor
 from ..ops import _native as N
 from .lr import LRScheduler
+from ..framework.tensor_types import SelectedRows
 from .multi_tensor import MultiTensorTable, aligned16
 
 _wrap = Tensor._wrap
@@ -153,6 +154,14 @@ class Optimizer:
     def _step_impl(self):
         pg = self._params_grads()
         self._clip_coef = None
+        sparse = [(p, g) for p, g in pg if g._t.is_sparse]
+        if sparse:
+            # row-sparse (SelectedRows) gradients, e.g. nn.Embedding(sparse=True): clipping needs the dense
+            # norm, otherwise only the touched rows are updated
+            pg = [(p, g) for p, g in pg if not g._t.is_sparse]
+            if self._grad_clip is not None:
+                pg += [(p, _wrap(g._t.to_dense())) for p, g in sparse]
+                sparse = []
         if self._grad_clip is not None and pg:
             if self._fused_clip and getattr(self._grad_clip, "_fusable", False) and all(
                     g._t.device.type == "cuda" for _, g in pg):
@@ -164,6 +173,12 @@ class Optimizer:
         self._step += 1
         if pg:
             self._apply(pg)
+        for p, g in sparse:
+            self._apply_sparse(p, SelectedRows.from_torch_sparse(g._t).merge_add())
+
+    def _apply_sparse(self, p, sr):
+        """Update from a SelectedRows gradient; the default densifies it (exact for every optimizer)."""
+        self._apply([(p, _wrap(sr.to_dense()))])
 
     def minimize(self, loss, startup_program=None, parameters=None, no_grad_set=None):
         from ..static.graph import SymTensor
@@ -265,6 +280,20 @@ class SGD(Optimizer):
             else:
                 p._t.add_(gt.to(p._t.dtype), alpha=-lr * gl)
 
+    def _apply_sparse(self, p, sr):
+        """w[rows] -= lr * value: one index_add over the touched rows (reference sgd SelectedRows kernel)."""
+        if (getattr(p, "regularizer", None) or self.regularization) is not None:
+            return super()._apply_sparse(p, sr)
+        lr = self.get_lr()
+        gl = self._group_of(p).get("learning_rate", 1.0) * p.optimize_attr.get("learning_rate", 1.0) \
+            if hasattr(p, "optimize_attr") else 1.0
+        rows = sr._rows.to(p._t.device)
+        m = self._master(p)
+        tgt = m if m is not None else p._t
+        tgt.index_add_(0, rows, sr._value.to(tgt.dtype), alpha=-lr * gl)
+        if m is not None:
+            p._t.copy_(m)
+
 
 class Momentum(Optimizer):
     def __init__(self, learning_rate=0.001, momentum=0.9, parameters=None, use_nesterov=False, weight_decay=None,
@@ -310,6 +339,7 @@ class Adam(Optimizer):
         self._beta1, self._beta2, self._epsilon = float(beta1), float(beta2), float(epsilon)
         self._multi_precision = multi_precision
         self._amsgrad = amsgrad
+        self._lazy_mode = lazy_mode
         self._found_inf = None   # set by GradScaler for fused skip
         self._inv_scale = None
         # L2 regularisation is added after clipping in Paddle, so it cannot share the fused multiplier
@@ -336,6 +366,34 @@ class Adam(Optimizer):
             self._apply_fused(gpu, lr, b1, b2, bc1, bc2)
         for p, g in cpu:
             self._apply_ref(p, g._t, lr, b1, b2, bc1, bc2)
+
+    def _apply_sparse(self, p, sr):
+        """lazy_mode: moments and weights of the touched rows only (reference adam SelectedRows kernel with
+        lazy_mode); otherwise the dense update (untouched rows still decay their moments)."""
+        if not self._lazy_mode or self._amsgrad or (not self._decoupled and self.regularization is not None):
+            return super()._apply_sparse(p, sr)
+        lr = self.get_lr()
+        b1, b2 = self._beta1, self._beta2
+        bc1, bc2 = 1.0 - b1 ** self._step, 1.0 - b2 ** self._step
+        rows = sr._rows.to(p._t.device)
+        m1 = self._acc("moment1", p)
+        m2 = self._acc("moment2", p)
+        g = sr._value.float()
+        mult = self._grad_mult()
+        if mult is not None:
+            g = g * mult.to(g.device)
+        r1 = m1.index_select(0, rows).mul_(b1).add_(g, alpha=1 - b1)
+        r2 = m2.index_select(0, rows).mul_(b2).addcmul_(g, g, value=1 - b2)
+        m1.index_copy_(0, rows, r1)
+        m2.index_copy_(0, rows, r2)
+        lr_t = lr * self._lr_ratio_of(p)
+        mw = self._master(p)
+        tgt = mw if mw is not None else p._t
+        w = tgt.index_select(0, rows).float()
+        w = w * (1 - lr_t * self._decay_of(p)) - (lr_t / bc1) * r1 / (r2.sqrt() / math.sqrt(bc2) + self._epsilon)
+        tgt.index_copy_(0, rows, w.to(tgt.dtype))
+        if mw is not None:
+            p._t.copy_(mw)
 
     def _apply_ref(self, p, g, lr, b1, b2, bc1, bc2):
         m1 = self._acc("moment1", p)

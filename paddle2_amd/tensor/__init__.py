@@ -18,10 +18,12 @@ from .random import *  # noqa: F401,F403
 from .search import *  # noqa: F401,F403
 from .stat import *  # noqa: F401,F403
 from ._helpers import ut
+from . import array  # noqa: E402
+from .array import *  # noqa: F401,F403
 from . import creation, linalg, logic, manipulation, math, random, search, stat  # noqa: F811 (re-bind after star imports)
 
 __all__ = sorted(set(creation.__all__ + linalg.__all__ + logic.__all__ + manipulation.__all__ + math.__all__ +
-                     random.__all__ + search.__all__ + stat.__all__ + ["to_tensor", "Tensor"]))
+                     random.__all__ + search.__all__ + stat.__all__ + array.__all__ + ["to_tensor", "Tensor"]))
 
 _wrap = Tensor._wrap
 
