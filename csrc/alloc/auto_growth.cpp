@@ -1,0 +1,394 @@
+// Native auto-growth best-fit device allocator with stream-safe reuse
+// (reference: paddle/phi/core/memory/allocation/auto_growth_best_fit_allocator.cc,
+//             stream_safe_cuda_allocator.cc, retry_allocator.cc).
+//
+// Plugged into PyTorch-ROCm through torch.cuda.memory.CUDAPluggableAllocator (pd_alloc_malloc /
+// pd_alloc_free), so every framework tensor on the device is carved from it.  Design, sized for 288 GB HBM3E:
+//   * chunks: hipMalloc'd regions of max(request, chunk_size) bytes (chunk_size from
+//     FLAGS_auto_growth_chunk_size_in_mb; default 256 MiB so a 7B training step lives in ~1k chunks, not 100k
+//     hipMallocs); never returned to the driver except by pd_alloc_empty_cache / the OOM retry path;
+//   * blocks: each chunk is an address-ordered doubly-linked list of blocks; free blocks are indexed in a
+//     size-ordered multimap (best fit = lower_bound), split on allocation when the remainder is >= 1 KiB and
+//     coalesced with free neighbours of the same stream on release;
+//   * stream safety: a block remembers the stream it was freed on.  Reuse on that stream is ordered by the
+//     stream itself.  Once a second stream has been seen, every free also records a HIP event, and a block is
+//     handed to a different stream only after its event completed (hipEventQuery) — no host sync, no
+//     cross-stream hazard;
+//   * limit: an optional byte cap (FLAGS_fraction_of_gpu_memory_to_use / FLAGS_gpu_memory_limit_mb); on a
+//     failed growth the cache of fully-free chunks is released and the growth retried once.
+// Thread-safe (one mutex per device).  C ABI for ctypes; no Python dependency, loads on CPU-only machines.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+namespace pd {
+namespace alloc {
+
+constexpr size_t kAlign = 256;          // HBM transaction / LDS-DMA friendly alignment
+constexpr size_t kMinSplit = 1024;      // do not leave slivers smaller than this
+constexpr int kMaxDevices = 64;
+constexpr int kMaxScan = 64;            // candidates examined for a cross-stream reusable block
+
+struct Chunk;
+
+struct Block {
+  char* ptr;
+  size_t size;
+  bool free;
+  hipStream_t stream;
+  hipEvent_t event;      // recorded at free time when more than one stream is in use
+  bool event_pending;
+  Chunk* chunk;
+  Block* prev;
+  Block* next;
+  std::multimap<size_t, Block*>::iterator pos;  // position in the free index (valid when free)
+};
+
+struct Chunk {
+  char* base;
+  size_t size;
+  Block* head;
+};
+
+struct Stats {
+  uint64_t allocated = 0, reserved = 0, peak_allocated = 0, peak_reserved = 0;
+  uint64_t num_allocs = 0, num_frees = 0, num_chunks = 0, num_grow = 0, num_oom_retries = 0;
+  uint64_t cross_stream_reuse = 0;
+};
+
+struct Device {
+  std::mutex mu;
+  std::multimap<size_t, Block*> free_index;
+  std::unordered_map<void*, Block*> live;
+  std::vector<Chunk*> chunks;
+  std::vector<hipEvent_t> event_pool;
+  hipStream_t first_stream = nullptr;
+  bool seen_stream = false;
+  bool multi_stream = false;
+  Stats st;
+};
+
+static Device g_dev[kMaxDevices];
+static size_t g_chunk_bytes = size_t(256) << 20;
+static uint64_t g_limit_bytes = 0;   // 0 = unlimited
+static std::mutex g_cfg_mu;
+
+static inline size_t round_up(size_t n, size_t a) { return (n + a - 1) / a * a; }
+
+static hipEvent_t take_event(Device& d) {
+  if (!d.event_pool.empty()) {
+    hipEvent_t e = d.event_pool.back();
+    d.event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  return e;
+}
+
+static void give_event(Device& d, hipEvent_t e) {
+  if (e) d.event_pool.push_back(e);
+}
+
+static void index_free(Device& d, Block* b) {
+  b->free = true;
+  b->pos = d.free_index.emplace(b->size, b);
+}
+
+static void unindex_free(Device& d, Block* b) {
+  d.free_index.erase(b->pos);
+  b->free = false;
+}
+
+// a free block may be used by `stream` now
+static bool usable_on(Device& d, Block* b, hipStream_t stream) {
+  if (!d.multi_stream || b->stream == stream) return true;
+  if (!b->event_pending) return true;
+  if (hipEventQuery(b->event) == hipSuccess) {
+    b->event_pending = false;
+    give_event(d, b->event);
+    b->event = nullptr;
+    return true;
+  }
+  return false;
+}
+
+// the work that last used free block b has finished (or is ordered before anything that can reuse it)
+static bool fence_done(Device& d, Block* b) {
+  if (!d.multi_stream || !b->event_pending) return true;  // unfenced free blocks are settled (see usable_on)
+  if (hipEventQuery(b->event) == hipSuccess) {
+    b->event_pending = false;
+    give_event(d, b->event);
+    b->event = nullptr;
+    return true;
+  }
+  return false;
+}
+
+static Block* carve(Device& d, Block* b, size_t size, hipStream_t stream) {
+  unindex_free(d, b);
+  if (b->stream != stream) d.st.cross_stream_reuse++;
+  // usable_on() guaranteed: same stream (ordered) or the free-time event has completed
+  hipEvent_t ev = b->event;
+  bool pending = b->event_pending;
+  b->event = nullptr;
+  b->event_pending = false;
+  if (b->size - size >= kMinSplit) {
+    // the remainder stays "freed on b's stream" and keeps its fence for other streams
+    Block* rest = new Block{b->ptr + size, b->size - size, true, b->stream, ev, pending, b->chunk, b, b->next, {}};
+    ev = nullptr;
+    if (b->next) b->next->prev = rest;
+    b->next = rest;
+    b->size = size;
+    index_free(d, rest);
+  }
+  give_event(d, ev);
+  b->stream = stream;
+  return b;
+}
+
+static bool grow(Device& d, int dev, size_t size, hipStream_t stream) {
+  size_t bytes = size > g_chunk_bytes ? round_up(size, size_t(2) << 20) : g_chunk_bytes;
+  if (g_limit_bytes && d.st.reserved + bytes > g_limit_bytes) {
+    if (d.st.reserved + size > g_limit_bytes) return false;
+    bytes = round_up(size, kAlign);  // last chunk below the cap: exactly what is asked
+  }
+  int prev_dev = -1;
+  hipGetDevice(&prev_dev);
+  if (prev_dev != dev) hipSetDevice(dev);
+  void* p = nullptr;
+  hipError_t err = hipMalloc(&p, bytes);
+  if (prev_dev != dev) hipSetDevice(prev_dev);
+  if (err != hipSuccess || !p) {
+    (void)hipGetLastError();
+    return false;
+  }
+  Chunk* c = new Chunk{static_cast<char*>(p), bytes, nullptr};
+  Block* b = new Block{c->base, bytes, true, stream, nullptr, false, c, nullptr, nullptr, {}};
+  c->head = b;
+  d.chunks.push_back(c);
+  index_free(d, b);
+  d.st.reserved += bytes;
+  d.st.num_chunks++;
+  d.st.num_grow++;
+  if (d.st.reserved > d.st.peak_reserved) d.st.peak_reserved = d.st.reserved;
+  return true;
+}
+
+// merge adjacent free blocks whose fences have completed (run before growing: pending fences block
+// coalescing at free time, so fragmentation is settled lazily here); caller holds the lock
+static void coalesce_settled(Device& d) {
+  for (Chunk* c : d.chunks) {
+    Block* b = c->head;
+    while (b && b->next) {
+      Block* n = b->next;
+      if (b->free && n->free && fence_done(d, b) && fence_done(d, n)) {
+        unindex_free(d, b);
+        unindex_free(d, n);
+        b->size += n->size;
+        b->next = n->next;
+        if (n->next) n->next->prev = b;
+        delete n;
+        index_free(d, b);
+      } else {
+        b = n;
+      }
+    }
+  }
+}
+
+// return every chunk whose blocks are all free to the driver; caller holds the lock
+static uint64_t release_free_chunks(Device& d, int dev) {
+  uint64_t released = 0;
+  std::vector<Chunk*> keep;
+  bool synced = false;
+  for (Chunk* c : d.chunks) {
+    bool all_free = true;
+    for (Block* b = c->head; b; b = b->next) all_free = all_free && b->free;
+    if (!all_free) {
+      keep.push_back(c);
+      continue;
+    }
+    if (!synced) {  // pending kernels may still read freed blocks
+      int prev = -1;
+      hipGetDevice(&prev);
+      if (prev != dev) hipSetDevice(dev);
+      hipDeviceSynchronize();
+      if (prev != dev) hipSetDevice(prev);
+      synced = true;
+    }
+    for (Block* b = c->head; b;) {
+      Block* n = b->next;
+      unindex_free(d, b);
+      give_event(d, b->event);
+      delete b;
+      b = n;
+    }
+    hipFree(c->base);
+    released += c->size;
+    d.st.reserved -= c->size;
+    d.st.num_chunks--;
+    delete c;
+  }
+  d.chunks.swap(keep);
+  return released;
+}
+
+static Block* find_fit(Device& d, size_t size, hipStream_t stream) {
+  int scanned = 0;
+  for (auto it = d.free_index.lower_bound(size); it != d.free_index.end() && scanned < kMaxScan; ++it, ++scanned) {
+    if (usable_on(d, it->second, stream)) return it->second;
+  }
+  return nullptr;
+}
+
+static void* do_alloc(size_t size, int dev, hipStream_t stream) {
+  if (dev < 0 || dev >= kMaxDevices) return nullptr;
+  Device& d = g_dev[dev];
+  std::lock_guard<std::mutex> lk(d.mu);
+  if (!d.seen_stream) {
+    d.seen_stream = true;
+    d.first_stream = stream;
+  } else if (stream != d.first_stream && !d.multi_stream) {
+    // blocks freed so far carry no fence: settle the device once before any cross-stream hand-off
+    d.multi_stream = true;
+    hipDeviceSynchronize();
+  }
+  size_t need = round_up(size ? size : 1, kAlign);
+  Block* b = find_fit(d, need, stream);
+  if (!b) {
+    coalesce_settled(d);
+    b = find_fit(d, need, stream);
+  }
+  if (!b) {
+    if (!grow(d, dev, need, stream)) {
+      d.st.num_oom_retries++;
+      release_free_chunks(d, dev);
+      if (!grow(d, dev, need, stream)) return nullptr;
+    }
+    b = find_fit(d, need, stream);
+    if (!b) return nullptr;
+  }
+  b = carve(d, b, need, stream);
+  d.live.emplace(b->ptr, b);
+  d.st.allocated += b->size;
+  d.st.num_allocs++;
+  if (d.st.allocated > d.st.peak_allocated) d.st.peak_allocated = d.st.allocated;
+  return b->ptr;
+}
+
+static void do_free(void* ptr, int dev, hipStream_t stream) {
+  if (!ptr || dev < 0 || dev >= kMaxDevices) return;
+  Device& d = g_dev[dev];
+  std::lock_guard<std::mutex> lk(d.mu);
+  auto it = d.live.find(ptr);
+  if (it == d.live.end()) {
+    std::fprintf(stderr, "[pd_alloc] free of unknown pointer %p on device %d\n", ptr, dev);
+    return;
+  }
+  Block* b = it->second;
+  d.live.erase(it);
+  d.st.allocated -= b->size;
+  d.st.num_frees++;
+  b->stream = stream;
+  if (d.multi_stream) {
+    b->event = take_event(d);
+    if (b->event && hipEventRecord(b->event, stream) == hipSuccess) {
+      b->event_pending = true;
+    } else {
+      give_event(d, b->event);
+      b->event = nullptr;
+      hipStreamSynchronize(stream);  // could not fence: make the block safe the slow way
+    }
+  }
+  // coalesce with free neighbours that are either from the same stream (b's newer fence covers their earlier
+  // work) or already fenced complete (safe for anyone): the merged block carries b's stream and fence
+  Block* p = b->prev;
+  if (p && p->free && (p->stream == b->stream || fence_done(d, p))) {
+    unindex_free(d, p);
+    give_event(d, p->event);
+    p->size += b->size;
+    p->next = b->next;
+    if (b->next) b->next->prev = p;
+    p->event = b->event;
+    p->event_pending = b->event_pending;
+    delete b;
+    b = p;
+  }
+  Block* n = b->next;
+  if (n && n->free && (n->stream == b->stream || fence_done(d, n))) {
+    unindex_free(d, n);
+    give_event(d, n->event);
+    b->size += n->size;
+    b->next = n->next;
+    if (n->next) n->next->prev = b;
+    delete n;
+  }
+  if (b->prev == nullptr) b->chunk->head = b;
+  index_free(d, b);
+}
+
+}  // namespace alloc
+}  // namespace pd
+
+using namespace pd::alloc;
+
+extern "C" {
+
+// CUDAPluggableAllocator entry points
+void* pd_alloc_malloc(size_t size, int device, hipStream_t stream) { return do_alloc(size, device, stream); }
+
+void pd_alloc_free(void* ptr, size_t /*size*/, int device, hipStream_t stream) { do_free(ptr, device, stream); }
+
+void pd_alloc_configure(uint64_t chunk_bytes, uint64_t limit_bytes) {
+  std::lock_guard<std::mutex> lk(g_cfg_mu);
+  if (chunk_bytes) g_chunk_bytes = round_up(chunk_bytes, size_t(2) << 20);
+  g_limit_bytes = limit_bytes;
+}
+
+// out[0..9] = allocated, reserved, peak_allocated, peak_reserved, num_allocs, num_frees, num_chunks,
+//             num_grow, num_oom_retries, cross_stream_reuse
+void pd_alloc_stats(int device, uint64_t* out) {
+  if (device < 0 || device >= kMaxDevices) return;
+  Device& d = g_dev[device];
+  std::lock_guard<std::mutex> lk(d.mu);
+  const Stats& s = d.st;
+  uint64_t v[10] = {s.allocated, s.reserved, s.peak_allocated, s.peak_reserved, s.num_allocs,
+                    s.num_frees, s.num_chunks, s.num_grow, s.num_oom_retries, s.cross_stream_reuse};
+  std::memcpy(out, v, sizeof(v));
+}
+
+void pd_alloc_reset_peak(int device) {
+  if (device < 0 || device >= kMaxDevices) return;
+  Device& d = g_dev[device];
+  std::lock_guard<std::mutex> lk(d.mu);
+  d.st.peak_allocated = d.st.allocated;
+  d.st.peak_reserved = d.st.reserved;
+}
+
+uint64_t pd_alloc_empty_cache(int device) {
+  if (device < 0 || device >= kMaxDevices) return 0;
+  Device& d = g_dev[device];
+  std::lock_guard<std::mutex> lk(d.mu);
+  uint64_t r = release_free_chunks(d, device);
+  for (hipEvent_t e : d.event_pool) hipEventDestroy(e);
+  d.event_pool.clear();
+  return r;
+}
+
+// largest free block and number of free blocks (fragmentation diagnostics)
+void pd_alloc_fragmentation(int device, uint64_t* out) {
+  if (device < 0 || device >= kMaxDevices) return;
+  Device& d = g_dev[device];
+  std::lock_guard<std::mutex> lk(d.mu);
+  out[0] = d.free_index.empty() ? 0 : d.free_index.rbegin()->first;
+  out[1] = d.free_index.size();
+}
+
+}  // extern "C"

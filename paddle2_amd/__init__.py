@@ -10,6 +10,10 @@ from __future__ import annotations
 
 import torch as _torch  # noqa: F401  (brings up the HIP runtime before our extension loads)
 
+from .device import allocator as _allocator
+
+_allocator._maybe_enable_from_env()  # FLAGS_use_native_allocator: must precede the first device allocation
+
 from .framework import dtype as _dtype_mod
 from .framework.dtype import (bfloat16, bool_ as bool, complex64, complex128, float8_e4m3fn, float8_e5m2,  # noqa: F401,A001
                               float16, float32, float64, get_default_dtype, int8, int16, int32, int64,

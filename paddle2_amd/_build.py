@@ -143,6 +143,46 @@ def build_runtime(verbose=False):
     return out
 
 
+def alloc_target_path():
+    return os.path.join(ROOT, "paddle2_amd", "_pd_alloc.so")
+
+
+def build_allocator(verbose=False):
+    """Native auto-growth device allocator (csrc/alloc/auto_growth.cpp): a plain C-ABI shared library loaded by
+    torch's CUDAPluggableAllocator and by ctypes (stats).  Host code against the HIP runtime."""
+    src = os.path.join(CSRC, "alloc", "auto_growth.cpp")
+    flags = ["-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include"]
+    key = _hash(src, " ".join(flags))
+    out = alloc_target_path()
+    stamp = out + ".stamp"
+    if os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key:
+        return out
+    tmp = out + ".tmp"
+    cmd = ["g++"] + flags + [src, "-o", tmp, "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    _run(cmd)
+    os.replace(tmp, out)
+    with open(stamp, "w") as f:
+        f.write(key)
+    return out
+
+
+def build_alloc_stress(kind="address", verbose=False):
+    """The allocator's bookkeeping + the multi-threaded stress driver, against the fake HIP header (host memory,
+    asynchronous events), under ``kind`` = "address" (ASan+UBSan) or "thread" (TSan).  CPU-only."""
+    adir = os.path.join(CSRC, "alloc")
+    os.makedirs(BUILD, exist_ok=True)
+    out = os.path.join(BUILD, f"alloc_stress_{kind}")
+    cmd = (["g++", "-O1", "-g", "-std=c++17", "-I", os.path.join(adir, "test", "fake_hip")] + _SAN_FLAGS[kind]
+           + [os.path.join(adir, "auto_growth.cpp"), os.path.join(adir, "test", "alloc_stress.cpp"), "-o", out,
+              "-lpthread"])
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    _run(cmd)
+    return out
+
+
 _SAN_FLAGS = {
     "thread": ["-fsanitize=thread"],
     "address": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
@@ -166,7 +206,7 @@ def build_sanitized(kind="thread", verbose=False):
 
 
 def build_all(verbose=False):
-    return build(verbose=verbose), build_runtime(verbose=verbose)
+    return build(verbose=verbose), build_runtime(verbose=verbose), build_allocator(verbose=verbose)
 
 
 if __name__ == "__main__":

@@ -9,6 +9,8 @@ import contextlib
 
 import torch
 
+from . import allocator, context  # noqa: F401
+from .context import DeviceContextPool, GPUContext, get_context  # noqa: F401
 from ..framework.place import (CPUPlace, CUDAPlace, get_device, is_compiled_with_cinn,  # noqa: F401
                                is_compiled_with_cuda, is_compiled_with_custom_device, is_compiled_with_distribute,
                                is_compiled_with_rocm, is_compiled_with_xpu, set_device)
@@ -109,6 +111,12 @@ def stream_guard(stream):
         yield
 
 
+def _dev(device):
+    from .context import _device_index
+
+    return _device_index(device)
+
+
 class cuda:
     """paddle.device.cuda namespace."""
 
@@ -125,27 +133,40 @@ class cuda:
     @staticmethod
     def empty_cache():
         if torch.cuda.is_available():
-            torch.cuda.empty_cache()
+            if allocator.is_active():
+                allocator.empty_cache(_dev(None))
+            else:
+                torch.cuda.empty_cache()
 
     @staticmethod
     def max_memory_allocated(device=None):
+        if allocator.is_active():
+            return allocator.stats(_dev(device))["peak_allocated"]
         return torch.cuda.max_memory_allocated(device) if torch.cuda.is_available() else 0
 
     @staticmethod
     def max_memory_reserved(device=None):
+        if allocator.is_active():
+            return allocator.stats(_dev(device))["peak_reserved"]
         return torch.cuda.max_memory_reserved(device) if torch.cuda.is_available() else 0
 
     @staticmethod
     def memory_allocated(device=None):
+        if allocator.is_active():
+            return allocator.stats(_dev(device))["allocated"]
         return torch.cuda.memory_allocated(device) if torch.cuda.is_available() else 0
 
     @staticmethod
     def memory_reserved(device=None):
+        if allocator.is_active():
+            return allocator.stats(_dev(device))["reserved"]
         return torch.cuda.memory_reserved(device) if torch.cuda.is_available() else 0
 
     @staticmethod
     def reset_max_memory_allocated(device=None):
-        if torch.cuda.is_available():
+        if allocator.is_active():
+            allocator.reset_peak(_dev(device))
+        elif torch.cuda.is_available():
             torch.cuda.reset_peak_memory_stats(device)
 
     @staticmethod

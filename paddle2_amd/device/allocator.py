@@ -1,0 +1,115 @@
+"""Native device allocator front-end (reference: paddle/phi/core/memory/allocation/allocator_facade.cc +
+auto_growth_best_fit_allocator.cc / stream_safe_cuda_allocator.cc; strategy flags in paddle/common/flags.cc).
+
+The allocator itself is C++ (csrc/alloc/auto_growth.cpp -> paddle2_amd/_pd_alloc.so).  Two ways in:
+
+* process-wide: ``enable()`` (or ``FLAGS_use_native_allocator=1`` in the environment, applied at import)
+  swaps torch's caching allocator for it through ``CUDAPluggableAllocator`` — must happen before the first
+  device allocation; every framework tensor is then carved from its chunks;
+* scoped: ``mem_pool()`` returns a ``torch.cuda.MemPool`` whose segments come from it (usable any time, e.g.
+  to give one subsystem its own arena).
+
+``stats()`` / ``empty_cache()`` / ``reset_peak()`` read and manage it through ctypes; ``device.cuda``'s memory
+queries consult it when it is the active allocator.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_LIB = None
+_PLUG = None
+_ACTIVE = [False]
+_FIELDS = ("allocated", "reserved", "peak_allocated", "peak_reserved", "num_allocs", "num_frees", "num_chunks",
+           "num_grow", "num_oom_retries", "cross_stream_reuse")
+
+
+def library_path():
+    return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_pd_alloc.so")
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = library_path()
+        if not os.path.exists(path):
+            raise RuntimeError(f"native allocator not built ({path}); run paddle2_amd._build.build_allocator()")
+        L = ctypes.CDLL(path)
+        L.pd_alloc_configure.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.pd_alloc_stats.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+        L.pd_alloc_reset_peak.argtypes = [ctypes.c_int]
+        L.pd_alloc_empty_cache.argtypes = [ctypes.c_int]
+        L.pd_alloc_empty_cache.restype = ctypes.c_uint64
+        L.pd_alloc_fragmentation.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+        _LIB = L
+    return _LIB
+
+
+def configure(chunk_mb=None, limit_bytes=None):
+    """Chunk size (FLAGS_auto_growth_chunk_size_in_mb) and byte cap (0 = none)."""
+    from ..framework import flags
+
+    if chunk_mb is None:
+        chunk_mb = int(flags.flag("FLAGS_auto_growth_chunk_size_in_mb", 0) or 0) or 256
+    if limit_bytes is None:
+        limit_mb = int(flags.flag("FLAGS_gpu_memory_limit_mb", 0) or 0)
+        limit_bytes = limit_mb << 20
+    lib().pd_alloc_configure(int(chunk_mb) << 20, int(limit_bytes))
+
+
+def _pluggable():
+    global _PLUG
+    if _PLUG is None:
+        _PLUG = torch.cuda.memory.CUDAPluggableAllocator(library_path(), "pd_alloc_malloc", "pd_alloc_free")
+    return _PLUG
+
+
+def enable(chunk_mb=None, limit_bytes=None):
+    """Make the native allocator torch's device allocator for this process (before any device allocation)."""
+    if _ACTIVE[0]:
+        return
+    if torch.cuda.is_initialized():
+        raise RuntimeError("the native allocator must be enabled before the first device allocation "
+                           "(set FLAGS_use_native_allocator=1 in the environment or call enable() first)")
+    configure(chunk_mb, limit_bytes)
+    torch.cuda.memory.change_current_allocator(_pluggable())
+    _ACTIVE[0] = True
+
+
+def is_active():
+    return _ACTIVE[0]
+
+
+def mem_pool():
+    """A torch MemPool whose segments are allocated by the native allocator."""
+    lib()
+    return torch.cuda.MemPool(_pluggable().allocator())
+
+
+def stats(device=0):
+    buf = (ctypes.c_uint64 * len(_FIELDS))()
+    lib().pd_alloc_stats(int(device), buf)
+    return dict(zip(_FIELDS, list(buf)))
+
+
+def fragmentation(device=0):
+    buf = (ctypes.c_uint64 * 2)()
+    lib().pd_alloc_fragmentation(int(device), buf)
+    return {"largest_free_block": buf[0], "free_blocks": buf[1]}
+
+
+def reset_peak(device=0):
+    lib().pd_alloc_reset_peak(int(device))
+
+
+def empty_cache(device=0):
+    """Return fully-free chunks to the driver; -> bytes released."""
+    return int(lib().pd_alloc_empty_cache(int(device)))
+
+
+def _maybe_enable_from_env():
+    v = os.environ.get("FLAGS_use_native_allocator", "")
+    if v.lower() in ("1", "true", "yes", "on"):
+        enable()

@@ -47,9 +47,12 @@ class AsyncLoad:
         self._streams = {}
 
     def _stream(self, device):
+        """The device context's H2D copy stream (shared with every other async host->device copy)."""
         s = self._streams.get(device)
         if s is None:
-            s = torch.cuda.Stream(device=device)
+            from ...device.context import get_context
+
+            s = get_context(device).h2d_stream()
             self._streams[device] = s
         return s
 

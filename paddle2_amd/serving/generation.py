@@ -129,7 +129,9 @@ class LlamaGenerator:
         if not self.use_graph:
             return self._decode_body()
         if self._graph is None:
-            s = torch.cuda.Stream()
+            from ..device.context import get_context
+
+            s = get_context().capture_stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
                 for _ in range(2):  # warm up allocations outside the graph

@@ -203,7 +203,9 @@ class Executor:
         if st is None:
             st = _GraphState()
             st.static_in = {k: v.clone() for k, v in env.items()}
-            s = torch.cuda.Stream()
+            from ..device.context import get_context
+
+            s = get_context().capture_stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
                 for _ in range(2):

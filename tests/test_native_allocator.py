@@ -1,0 +1,136 @@
+"""Native auto-growth device allocator (csrc/alloc/auto_growth.cpp) and the per-device GPUContext
+(reference tests: test/cpp/fluid/memory/auto_growth_best_fit_allocator_test.cc,
+stream_safe_cuda_alloc_test.cu, test/legacy_test/test_cuda_max_memory_allocated.py)."""
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+import torch
+
+import paddle2_amd as paddle
+from paddle2_amd import _build
+
+
+@pytest.mark.parametrize("kind", ["address", "thread"])
+def test_allocator_bookkeeping_under_sanitizers(kind):
+    """4 threads / 4 streams x 20k random alloc-free ops with cross-thread hand-offs: no overlap (tag check),
+    no leak, allocs == frees, every chunk returned by empty_cache — under ASan+UBSan and TSan."""
+    exe = _build.build_alloc_stress(kind)
+    r = subprocess.run([exe, "4", "20000"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    assert "errors=0" in r.stdout
+    assert int(r.stdout.split("cross_stream_reuse=")[1].split()[0]) > 0
+
+
+def test_allocator_library_api_on_cpu():
+    from paddle2_amd.device import allocator
+
+    _build.build_allocator()
+    allocator.configure(chunk_mb=64, limit_bytes=0)
+    st = allocator.stats(0)
+    assert set(st) >= {"allocated", "reserved", "peak_allocated", "num_chunks"}
+    assert allocator.fragmentation(0)["free_blocks"] >= 0
+    assert not allocator.is_active()
+
+
+def test_gpu_context_pool_cpu():
+    from paddle2_amd.device.context import DeviceContextPool, _device_index
+
+    pool = DeviceContextPool.instance()
+    assert pool.get(0) is pool.get("gpu:0") is paddle.device.get_context(0)
+    assert _device_index(torch.device("cuda", 3)) == 3
+    assert repr(pool.get(0)).startswith("GPUContext(device=0")
+
+
+@pytest.mark.gpu
+def test_gpu_context_streams():
+    ctx = paddle.device.get_context()
+    assert ctx.comm_stream() is ctx.comm_stream()
+    assert ctx.h2d_stream() is not ctx.comm_stream()
+    x = torch.ones(1 << 20, device="cuda")
+    with torch.cuda.stream(ctx.comm_stream()):
+        ctx.wait(ctx.comm_stream(), ctx.stream())
+        y = x * 2
+    ctx.wait(ctx.stream(), ctx.comm_stream())
+    assert float(y.sum()) == 2.0 * (1 << 20)
+    facts = ctx.properties()
+    assert facts["num_cus"] >= 1 and facts["wavefront_size"] == 64 and "gfx" in facts["arch"]
+
+
+@pytest.mark.gpu
+def test_native_allocator_mem_pool_integrity():
+    from paddle2_amd.device import allocator
+
+    allocator.configure(chunk_mb=64, limit_bytes=0)
+    before = allocator.stats(torch.cuda.current_device())
+    pool = allocator.mem_pool()
+    g = torch.Generator().manual_seed(0)
+    live = []
+    with torch.cuda.use_mem_pool(pool):
+        for i in range(200):
+            n = int(torch.randint(1, 1 << 22, (1,), generator=g))
+            t = torch.full((n,), float(i % 97), device="cuda")
+            live.append((i, t))
+            if i % 3 == 0:
+                live.pop(int(torch.randint(0, len(live), (1,), generator=g)))
+        torch.cuda.synchronize()
+        for i, t in live:
+            assert float(t.min()) == float(i % 97) == float(t.max())
+    after = allocator.stats(torch.cuda.current_device())
+    assert after["num_grow"] > before["num_grow"] and after["reserved"] > 0
+    del live, t
+    torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_native_allocator_process_wide_training():
+    """FLAGS_use_native_allocator=1: a fresh process trains an MLP with a side-stream copy on the native
+    allocator; the loss trajectory equals the caching allocator's and the stats API reports its usage."""
+    script = textwrap.dedent("""
+        import json, os, sys
+        import numpy as np
+        import torch
+        import paddle2_amd as paddle
+        from paddle2_amd.device import allocator
+        paddle.seed(0)
+        net = paddle.nn.Sequential(paddle.nn.Linear(256, 512), paddle.nn.ReLU(), paddle.nn.Linear(512, 10))
+        opt = paddle.optimizer.AdamW(1e-3, parameters=net.parameters())
+        rs = np.random.RandomState(0)
+        losses = []
+        ctx = paddle.device.get_context()
+        for step in range(20):
+            xh = torch.from_numpy(rs.randn(64, 256).astype("float32")).pin_memory()
+            with torch.cuda.stream(ctx.h2d_stream()):
+                xd = xh.to("cuda", non_blocking=True)
+            torch.cuda.current_stream().wait_stream(ctx.h2d_stream())
+            xd.record_stream(torch.cuda.current_stream())
+            x = paddle.Tensor._wrap(xd)
+            y = paddle.to_tensor(rs.randint(0, 10, (64,)).astype("int64")).cuda()
+            loss = paddle.nn.functional.cross_entropy(net(x), y)
+            loss.backward(); opt.step(); opt.clear_grad()
+            losses.append(float(loss))
+        torch.cuda.synchronize()
+        st = allocator.stats(0) if allocator.is_active() else {}
+        print(json.dumps({"active": allocator.is_active(), "losses": losses, "stats": st,
+                          "api_alloc": paddle.device.cuda.memory_allocated(),
+                          "api_peak": paddle.device.cuda.max_memory_allocated()}))
+    """)
+    import json
+
+    res = {}
+    for mode in ("native", "caching"):
+        env = dict(os.environ)
+        env.pop("FLAGS_use_native_allocator", None)
+        if mode == "native":
+            env["FLAGS_use_native_allocator"] = "1"
+        r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res[mode] = json.loads(r.stdout.strip().splitlines()[-1])
+    nat, cach = res["native"], res["caching"]
+    assert nat["active"] and not cach["active"]
+    assert nat["losses"] == pytest.approx(cach["losses"], rel=1e-5, abs=1e-6)
+    st = nat["stats"]
+    assert st["num_allocs"] > 100 and st["reserved"] >= st["peak_allocated"] > 0
+    assert nat["api_peak"] == st["peak_allocated"] and nat["api_alloc"] == st["allocated"]
