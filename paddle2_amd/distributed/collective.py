@@ -291,14 +291,46 @@ def _all_reduce_torch(t: torch.Tensor, op=ReduceOp.SUM, group=None, sync_op=True
     return _Task(w)
 
 
+def _is_symbolic(tensor):
+    from ..static.graph import SymTensor
+
+    return isinstance(getattr(tensor, "_t", None), SymTensor)
+
+
+def _static_collective(name, tensor, body):
+    """Record an in-place collective into the static Program being built (reference: c_allreduce_sum /
+    c_broadcast ops of static data parallelism).  The op declares the comm stream: the executor's stream
+    analyzer runs it on the device context's comm stream with event dependencies on producers/consumers."""
+    def run(x):
+        if x.device.type != "meta":
+            body(x)
+        return x
+
+    run._pd_stream = "comm"
+    run.__name__ = run.__qualname__ = name
+    tensor._t._program._record(run, (tensor._t,), {}, kind="native")
+    return _Task(None)
+
+
 def all_reduce(tensor, op=ReduceOp.SUM, group=None, sync_op=True, use_calc_stream=False):
     from . import watchdog
 
+    if _is_symbolic(tensor):
+        names = {ReduceOp.SUM: "sum", ReduceOp.MAX: "max", ReduceOp.MIN: "min", ReduceOp.PROD: "prod",
+                 ReduceOp.AVG: "avg"}
+        return _static_collective(f"c_allreduce_{names.get(op, op)}", tensor,
+                                  lambda x: _all_reduce_torch(x, op, group, True))
     with watchdog.track("all_reduce", group, tensor):
         return _all_reduce_torch(tensor._t, op, group, sync_op)
 
 
 def broadcast(tensor, src=0, group=None, sync_op=True):
+    if _is_symbolic(tensor):
+        def body(x):
+            g, pg = _pg(group)
+            if not _single(g):
+                dist.broadcast(x, src=src, group=pg)
+        return _static_collective("c_broadcast", tensor, body)
     g, pg = _pg(group)
     if _single(g):
         return _Task(None)

@@ -10,6 +10,8 @@ feeds into the graph's static input buffers and replay the whole step as one gra
 """
 from __future__ import annotations
 
+import weakref
+
 import numpy as np
 import torch
 from torch.utils import _pytree as pytree
@@ -93,9 +95,22 @@ class Executor:
         self._graphs.clear()
 
     # ---------------------------------------------------------------- core replay
-    def _replay(self, program, env, grad=None):
+    def _replay(self, program, env, grad=None, keep=None):
+        """Run ``program`` over ``env`` (vid -> tensor).  With ``keep`` (the fetch targets) the plan's garbage
+        collection drops every value after its last use, and ops the stream analyzer placed on the comm /
+        copy streams run there with event dependencies on their producers and consumers."""
         needs_grad = any(o.kind in ("backward", "grad") for o in program.ops) or bool(grad)
         ctx = torch.enable_grad() if needs_grad else torch.no_grad()
+        plan = _plan(program, keep) if keep is not None else None
+        streams = plan is not None and plan.multi_stream and torch.cuda.is_available() and \
+            self._device.type == "cuda"
+        if streams:
+            from ..device.context import get_context
+
+            gctx = get_context(self._device)
+            side = {"comm": gctx.comm_stream, "h2d": gctx.h2d_stream, "d2h": gctx.d2h_stream}
+            compute = torch.cuda.current_stream(self._device)
+            ready = {}   # vid -> event recorded right after its producer (only for cross-stream values)
 
         def res(x):
             if isinstance(x, VarRef):
@@ -105,15 +120,32 @@ class Executor:
             return x
 
         with ctx:
-            for op in program.ops:
+            for i, op in enumerate(program.ops):
                 if op.kind in ("torch", "native"):
                     args = pytree.tree_map(res, op.args)
                     kw = pytree.tree_map(res, op.kwargs)
-                    out = op.fn(*args, **kw)
+                    if streams and (plan.stream_of[i] != "compute" or plan.waits_on[i]):
+                        st = side[plan.stream_of[i]]() if plan.stream_of[i] != "compute" else compute
+                        for v in plan.waits_on[i]:
+                            st.wait_event(ready[v])
+                            if st is not compute:
+                                env[v].record_stream(st)   # allocator: the side stream still reads it
+                        with torch.cuda.stream(st):
+                            out = op.fn(*args, **kw)
+                    else:
+                        out = op.fn(*args, **kw)
                     leaves = pytree.tree_leaves(out)
                     for vid, val in zip(op.outs, leaves):
                         if vid is not None:
                             env[vid] = val
+                            if streams and vid in plan.cross:
+                                e = torch.cuda.Event()
+                                e.record(side[plan.stream_of[i]]() if plan.stream_of[i] != "compute" else compute)
+                                ready[vid] = e
+                    if plan is not None:
+                        for v in plan.free_after[i]:
+                            env.pop(v, None)
+                    continue
                 elif op.kind == "backward":
                     loss = env[op.attrs["loss"]]
                     loss.backward()
@@ -132,6 +164,13 @@ class Executor:
                     with torch.no_grad():
                         opt.step()
                     opt.clear_grad(set_to_zero=False)
+                if plan is not None:
+                    for v in plan.free_after[i]:
+                        env.pop(v, None)
+        if streams and plan.cross:
+            # values produced on a side stream and fetched / left in env: the caller reads them on compute
+            for v, e in ready.items():
+                compute.wait_event(e)
         return env
 
     def run(self, program=None, feed=None, fetch_list=None, feed_var_name="feed", fetch_var_name="fetch", scope=None,
@@ -176,7 +215,7 @@ class Executor:
         if strategy is not None and strategy.enable_cuda_graph and self._device.type == "cuda":
             outs = self._run_graph(program, env, fetch_ids)
         else:
-            env = self._replay(program, env, _grad)
+            env = self._replay(program, env, _grad, keep=set(fetch_ids))
             outs = [env[i] for i in fetch_ids]
         if return_numpy:
             return [o.detach().float().cpu().numpy() if o.dtype == torch.bfloat16 else o.detach().cpu().numpy()
@@ -220,3 +259,78 @@ class Executor:
             st.static_in[k].copy_(v)
         st.graph.replay()
         return [o.clone() for o in st.static_out]
+
+
+# ==================================================================================== execution plan
+class _Plan:
+    """Per-(program, fetch set) analysis (reference: new_executor/interpreter/dependency_builder.cc,
+    stream_analyzer.cc, garbage collection in interpreter_util):
+
+    * ``free_after[i]`` — values whose last reader is op i (dropped right after it unless fetched), so peak
+      memory follows the live set instead of the whole program;
+    * ``stream_of[i]`` — "compute", or the stream class a function declares via ``_pd_stream`` ("comm" for
+      collectives, "h2d" / "d2h" for copies); ``waits_on[i]`` — inputs produced on another stream (op i's
+      stream waits on their ready events); ``cross`` — values that need such an event.
+    """
+
+    def __init__(self, program, keep):
+        ops = program.ops
+        n = len(ops)
+        last = {}
+        producer = {}
+        self.stream_of = []
+        self.waits_on = [[] for _ in range(n)]
+        self.cross = set()
+        for i, op in enumerate(ops):
+            klass = (op.attrs.get("stream") or getattr(op.fn, "_pd_stream", None) or "compute") \
+                if op.kind in ("torch", "native") else "compute"
+            self.stream_of.append(klass)
+            for v in _op_reads(op):
+                last[v] = i
+                if v in producer and self.stream_of[producer[v]] != klass:
+                    self.waits_on[i].append(v)
+                    self.cross.add(v)
+            for v in _op_writes(op):
+                producer[v] = i
+        keep = set(keep or ())
+        self.free_after = [[] for _ in range(n)]
+        for v, i in last.items():
+            if v not in keep:
+                self.free_after[i].append(v)
+        self.multi_stream = any(k != "compute" for k in self.stream_of)
+
+
+def _op_reads(op):
+    vids = [x.vid for x in pytree.tree_leaves((op.args, op.kwargs)) if isinstance(x, VarRef)]
+    a = op.attrs
+    if "loss" in a:
+        vids.append(a["loss"])
+    for k in ("targets", "inputs"):
+        vids.extend(v for v in a.get(k, ()) if isinstance(v, int))
+    return vids
+
+
+def _op_writes(op):
+    out = [v for v in op.outs if v is not None]
+    a = op.attrs
+    if "out" in a:
+        out.append(a["out"])
+    out.extend(a.get("outs", ()))
+    return out
+
+
+_PLANS = weakref.WeakKeyDictionary()   # program -> {(num ops, fetch set): plan}
+
+
+def _plan(program, keep):
+    from ..framework import flags
+
+    if float(flags.flag("FLAGS_eager_delete_tensor_gb", 0.0)) < 0:
+        keep = None   # garbage collection disabled: keep everything
+    per = _PLANS.setdefault(program, {})
+    key = (len(program.ops), frozenset(keep) if keep is not None else None)
+    p = per.get(key)
+    if p is None:
+        p = _Plan(program, keep if keep is not None else {v for op in program.ops for v in _op_reads(op)})
+        per[key] = p
+    return p

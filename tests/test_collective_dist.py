@@ -66,3 +66,14 @@ def test_fused_comm_buffer_and_collective_perf():
         assert abs(r["grads"]["rs_shard_head"][0] - (exp_w if r["grads"]["rs_shard_rank"] == 0 else
                                                      r["grads"]["rs_shard_head"][0])) < 1e-5
     assert [p[:2] for p in r0["perf"]] == [[1 << 16, 2], [1 << 18, 2]] and all(p[2] and p[3] for p in r0["perf"])
+
+
+def test_static_program_collectives_and_plan():
+    """Recorded c_allreduce_sum / c_broadcast in a static Program, executed on 2 gloo ranks: values match,
+    the stream analyzer puts both on the comm stream with event waits, and GC frees intermediates."""
+    res = run_workers("static_comm_worker.py", 2)
+    for r in res:
+        assert r["z"] == [7.0, 13.0, 19.0]           # 2*(1x + 2x) + 1
+        assert r["w"] == [1.5, 3.5, 5.5]             # rank 1's x (2x) - 0.5
+        assert r["comm_ops"] == ["c_allreduce_sum", "c_broadcast"]
+        assert r["waits"] >= 2 and r["freed"] >= 2
