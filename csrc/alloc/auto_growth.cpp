@@ -40,6 +40,7 @@ struct Chunk;
 struct Block {
   char* ptr;
   size_t size;
+  size_t req;            // bytes the caller asked for (guard / canary bookkeeping)
   bool free;
   hipStream_t stream;
   hipEvent_t event;      // recorded at free time when more than one stream is in use
@@ -76,6 +77,16 @@ struct Device {
 
 static Device g_dev[kMaxDevices];
 static size_t g_chunk_bytes = size_t(256) << 20;
+// debug: every block gets g_guard extra bytes past the request; with g_canary the slack is filled with a
+// pattern at allocation and verified at free, so a kernel writing past its tensor is reported (pointer,
+// size, first bad offset) instead of silently corrupting the neighbour
+static size_t g_guard = 0;
+static bool g_canary = false;
+constexpr unsigned char kCanary = 0xA5;
+struct Violation {
+  uint64_t ptr, req, offset;
+};
+static std::vector<Violation> g_violations;
 static uint64_t g_limit_bytes = 0;   // 0 = unlimited
 static std::mutex g_cfg_mu;
 
@@ -141,7 +152,7 @@ static Block* carve(Device& d, Block* b, size_t size, hipStream_t stream) {
   b->event_pending = false;
   if (b->size - size >= kMinSplit) {
     // the remainder stays "freed on b's stream" and keeps its fence for other streams
-    Block* rest = new Block{b->ptr + size, b->size - size, true, b->stream, ev, pending, b->chunk, b, b->next, {}};
+    Block* rest = new Block{b->ptr + size, b->size - size, 0, true, b->stream, ev, pending, b->chunk, b, b->next, {}};
     ev = nullptr;
     if (b->next) b->next->prev = rest;
     b->next = rest;
@@ -170,7 +181,7 @@ static bool grow(Device& d, int dev, size_t size, hipStream_t stream) {
     return false;
   }
   Chunk* c = new Chunk{static_cast<char*>(p), bytes, nullptr};
-  Block* b = new Block{c->base, bytes, true, stream, nullptr, false, c, nullptr, nullptr, {}};
+  Block* b = new Block{c->base, bytes, 0, true, stream, nullptr, false, c, nullptr, nullptr, {}};
   c->head = b;
   d.chunks.push_back(c);
   index_free(d, b);
@@ -260,7 +271,7 @@ static void* do_alloc(size_t size, int dev, hipStream_t stream) {
     d.multi_stream = true;
     hipDeviceSynchronize();
   }
-  size_t need = round_up(size ? size : 1, kAlign);
+  size_t need = round_up((size ? size : 1) + g_guard, kAlign);
   Block* b = find_fit(d, need, stream);
   if (!b) {
     coalesce_settled(d);
@@ -276,6 +287,8 @@ static void* do_alloc(size_t size, int dev, hipStream_t stream) {
     if (!b) return nullptr;
   }
   b = carve(d, b, need, stream);
+  b->req = size;
+  if (g_canary && b->size > size) hipMemsetAsync(b->ptr + size, kCanary, b->size - size, stream);
   d.live.emplace(b->ptr, b);
   d.st.allocated += b->size;
   d.st.num_allocs++;
@@ -294,6 +307,21 @@ static void do_free(void* ptr, int dev, hipStream_t stream) {
   }
   Block* b = it->second;
   d.live.erase(it);
+  if (g_canary && b->size > b->req) {
+    size_t n = b->size - b->req;
+    std::vector<unsigned char> host(n);
+    hipStreamSynchronize(stream);
+    if (hipMemcpy(host.data(), b->ptr + b->req, n, hipMemcpyDeviceToHost) == hipSuccess) {
+      for (size_t i = 0; i < n; ++i) {
+        if (host[i] != kCanary) {
+          g_violations.push_back({reinterpret_cast<uint64_t>(b->ptr), b->req, i});
+          std::fprintf(stderr, "[pd_alloc] write past the end of a %zu-byte block at %p: +%zu bytes\n", b->req,
+                       (void*)b->ptr, i);
+          break;
+        }
+      }
+    }
+  }
   d.st.allocated -= b->size;
   d.st.num_frees++;
   b->stream = stream;
@@ -345,6 +373,25 @@ extern "C" {
 void* pd_alloc_malloc(size_t size, int device, hipStream_t stream) { return do_alloc(size, device, stream); }
 
 void pd_alloc_free(void* ptr, size_t /*size*/, int device, hipStream_t stream) { do_free(ptr, device, stream); }
+
+void pd_alloc_debug(uint64_t guard_bytes, int canary) {
+  std::lock_guard<std::mutex> lk(g_cfg_mu);
+  g_guard = round_up(guard_bytes, kAlign);
+  g_canary = canary != 0;
+}
+
+// violations recorded by the canary check: out[3*i .. 3*i+2] = (ptr, requested bytes, first bad offset)
+uint64_t pd_alloc_violations(uint64_t* out, uint64_t max_n) {
+  uint64_t n = 0;
+  for (auto& v : g_violations) {
+    if (n >= max_n) break;
+    out[3 * n] = v.ptr;
+    out[3 * n + 1] = v.req;
+    out[3 * n + 2] = v.offset;
+    ++n;
+  }
+  return g_violations.size();
+}
 
 void pd_alloc_configure(uint64_t chunk_bytes, uint64_t limit_bytes) {
   std::lock_guard<std::mutex> lk(g_cfg_mu);

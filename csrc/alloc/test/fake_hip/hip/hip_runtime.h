@@ -6,6 +6,7 @@
 #include <atomic>
 #include <cstddef>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <set>
 
@@ -37,6 +38,9 @@ inline hipError_t hipFree(void* p) { std::free(p); return hipSuccess; }  // byte
 inline hipError_t hipGetDevice(int* d) { *d = fakehip::cur_dev; return hipSuccess; }
 inline hipError_t hipSetDevice(int d) { fakehip::cur_dev = d; return hipSuccess; }
 inline hipError_t hipGetLastError() { return hipSuccess; }
+enum { hipMemcpyDeviceToHost = 2 };
+inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { std::memset(p, v, n); return hipSuccess; }
+inline hipError_t hipMemcpy(void* d, const void* s, size_t n, int) { std::memcpy(d, s, n); return hipSuccess; }
 inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) {
   *e = new FakeEvent();
   std::lock_guard<std::mutex> lk(fakehip::mu());

@@ -155,6 +155,42 @@ PYBIND11_MODULE(_runtime, m) {
   m.def("watchdog_timed_out", &watchdog_timed_out);
   m.def("watchdog_inflight", &watchdog_inflight);
 
+  py::class_<FleetTask>(m, "FleetTask")
+      .def(py::init<>())
+      .def_readwrite("id", &FleetTask::id)
+      .def_readwrite("rank", &FleetTask::rank)
+      .def_readwrite("role", &FleetTask::role)
+      .def_readwrite("max_run_times", &FleetTask::max_run_times)
+      .def_readwrite("run_per_steps", &FleetTask::run_per_steps)
+      .def_readwrite("run_at_offset", &FleetTask::run_at_offset)
+      .def_readwrite("upstream", &FleetTask::upstream)
+      .def_readwrite("downstream", &FleetTask::downstream);
+
+  py::class_<FleetCarrier>(m, "FleetCarrier")
+      .def(py::init<int, int>(), py::arg("rank"), py::arg("num_threads") = 2)
+      .def("add_task", &FleetCarrier::add_task)
+      .def("add_remote_task", &FleetCarrier::add_remote_task)
+      .def("set_compute",
+           [](FleetCarrier& c, py::function fn) {
+             // the callback runs on a loop thread: take the GIL, surface Python errors as C++ exceptions
+             auto holder = std::make_shared<py::function>(std::move(fn));
+             c.set_compute([holder](int64_t task, int64_t step) {
+               py::gil_scoped_acquire g;
+               try {
+                 (*holder)(task, step);
+               } catch (py::error_already_set& e) {
+                 throw std::runtime_error(e.what());
+               }
+             });
+           })
+      .def("listen", &FleetCarrier::listen, py::arg("host") = "127.0.0.1")
+      .def("set_peer", &FleetCarrier::set_peer)
+      .def("start", &FleetCarrier::start)
+      .def("wait", &FleetCarrier::wait, py::arg("timeout_s") = -1.0, py::call_guard<py::gil_scoped_release>())
+      .def("trace", &FleetCarrier::trace)
+      .def("clear_trace", &FleetCarrier::clear_trace)
+      .def("shutdown", &FleetCarrier::shutdown, py::call_guard<py::gil_scoped_release>());
+
   py::class_<BlockingQueue>(m, "BlockingQueue")
       .def(py::init<size_t>(), py::arg("capacity"))
       .def("push", &BlockingQueue::push, py::arg("obj"), py::arg("timeout") = -1.0)

@@ -2,7 +2,9 @@
 // host event tracer, and the bounded blocking queue used by the data loader.
 #pragma once
 
+#include <array>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -74,5 +76,39 @@ std::vector<int64_t> watchdog_take_finished();
 void watchdog_end(int64_t id);
 std::vector<std::string> watchdog_timed_out();
 int64_t watchdog_inflight();
+
+// ------------------------------------------------------------------ FleetExecutor (fleet_executor.cpp)
+struct FleetTask {
+  enum Role : int { kCompute = 0, kAmplifier = 1, kSource = 2, kSink = 3 };
+  int64_t id = 0;
+  int rank = 0;
+  int role = kCompute;
+  int64_t max_run_times = 1;
+  int64_t run_per_steps = 1;
+  int64_t run_at_offset = 0;
+  std::vector<std::pair<int64_t, int64_t>> upstream;    // (task id, buffer size)
+  std::vector<std::pair<int64_t, int64_t>> downstream;  // (task id, buffer size)
+};
+
+class FleetCarrier {
+ public:
+  using ComputeFn = std::function<void(int64_t task, int64_t step)>;
+  FleetCarrier(int rank, int num_threads);
+  ~FleetCarrier();
+  void add_task(const FleetTask& t);           // every task of the job; only this rank's get interceptors
+  void add_remote_task(int64_t id, int rank);
+  void set_compute(ComputeFn fn);
+  int listen(const std::string& host);          // message-bus listener; returns the port
+  void set_peer(int rank, const std::string& host, int port);
+  void start();
+  bool wait(double timeout_s);                  // true when every local task finished; throws on error
+  std::vector<std::array<int64_t, 3>> trace();  // (task, step, sequence) of compute callbacks
+  void clear_trace();
+  void shutdown();
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
+};
 
 }  // namespace pdrt

@@ -1,4 +1,5 @@
-// Concurrency stress driver for the host runtime (tcp_store.cpp, watchdog.cpp, tracer.cpp), built with
+// Concurrency stress driver for the host runtime (tcp_store.cpp, watchdog.cpp, tracer.cpp,
+// fleet_executor.cpp), built with
 // -fsanitize=thread (data races) or -fsanitize=address,undefined (memory errors / UB) by
 // paddle2_amd/_build.py build_sanitized(); tests/test_sanitizers.py runs both.  Reference role: SURVEY §5.2
 // (race detection / sanitizer builds of the native runtime).  CPU only: watchdog entries carry no HIP event,
@@ -70,6 +71,50 @@ int main() {
   (void)watchdog_take_finished();
   watchdog_stop();
   tracer_enable(false);
+
+  // ---- FleetExecutor: a 3-stage pipeline split over two carriers (message bus over TCP), 4 loop threads
+  // each, 200 micro-steps; every stage must see every step exactly once and in order
+  {
+    constexpr int64_t kSteps = 200;
+    FleetCarrier c0(0, 4), c1(1, 4);
+    std::vector<FleetTask> tasks(5);
+    int64_t ids[5] = {1, 2, 3, 4, 5};
+    int ranks[5] = {0, 0, 1, 1, 1};
+    int roles[5] = {FleetTask::kSource, FleetTask::kCompute, FleetTask::kCompute, FleetTask::kCompute,
+                    FleetTask::kSink};
+    for (int i = 0; i < 5; ++i) {
+      tasks[i].id = ids[i];
+      tasks[i].rank = ranks[i];
+      tasks[i].role = roles[i];
+      tasks[i].max_run_times = kSteps;
+      if (i > 0) tasks[i].upstream = {{ids[i - 1], 2}};
+      if (i < 4) tasks[i].downstream = {{ids[i + 1], 2}};
+    }
+    std::atomic<int64_t> next[6];
+    for (auto& n : next) n = 0;
+    std::atomic<int> order_errors{0};
+    auto fn = [&](int64_t task, int64_t step) {
+      if (next[task].fetch_add(1) != step) order_errors++;
+    };
+    for (auto& t : tasks) {
+      c0.add_task(t);
+      c1.add_task(t);
+    }
+    c0.set_compute(fn);
+    c1.set_compute(fn);
+    int p0 = c0.listen("127.0.0.1"), p1 = c1.listen("127.0.0.1");
+    c0.set_peer(1, "127.0.0.1", p1);
+    c1.set_peer(0, "127.0.0.1", p0);
+    c1.start();
+    c0.start();
+    if (!c0.wait(60.0) || !c1.wait(60.0)) return fail("fleet executor timed out");
+    if (order_errors.load()) return fail("fleet executor step order");
+    for (int t = 2; t <= 4; ++t)
+      if (next[t].load() != kSteps) return fail("fleet executor lost steps");
+    if (c0.trace().size() + c1.trace().size() != 3 * kSteps) return fail("fleet executor trace");
+    c0.shutdown();
+    c1.shutdown();
+  }
 
   TCPStoreClient c("127.0.0.1", port, 30.0);
   if (c.add("counter", 0) != kThreads * kIters) return fail("store counter");

@@ -194,7 +194,7 @@ def build_sanitized(kind="thread", verbose=False):
     csrc/runtime/stress/runtime_stress.cpp: ``kind`` "thread" (TSan, data races) or "address" (ASan + UBSan).
     Host code only — GPU sanitizers are not used on this hardware.  Returns the executable path."""
     rdir = os.path.join(CSRC, "runtime")
-    srcs = [os.path.join(rdir, f) for f in ("tcp_store.cpp", "watchdog.cpp", "tracer.cpp")]
+    srcs = [os.path.join(rdir, f) for f in ("tcp_store.cpp", "watchdog.cpp", "tracer.cpp", "fleet_executor.cpp")]
     srcs.append(os.path.join(rdir, "stress", "runtime_stress.cpp"))
     os.makedirs(BUILD, exist_ok=True)
     out = os.path.join(BUILD, f"runtime_stress_{kind}")

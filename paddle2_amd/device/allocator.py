@@ -43,6 +43,9 @@ def lib():
         L.pd_alloc_empty_cache.argtypes = [ctypes.c_int]
         L.pd_alloc_empty_cache.restype = ctypes.c_uint64
         L.pd_alloc_fragmentation.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+        L.pd_alloc_debug.argtypes = [ctypes.c_uint64, ctypes.c_int]
+        L.pd_alloc_violations.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64]
+        L.pd_alloc_violations.restype = ctypes.c_uint64
         _LIB = L
     return _LIB
 
@@ -109,7 +112,23 @@ def empty_cache(device=0):
     return int(lib().pd_alloc_empty_cache(int(device)))
 
 
+def debug(guard_bytes=4096, canary=True):
+    """Out-of-bounds-write detector: pad every block by ``guard_bytes`` and verify a canary pattern in the
+    slack at free time (host sync per free: a debugging mode)."""
+    lib().pd_alloc_debug(int(guard_bytes), 1 if canary else 0)
+
+
+def violations(max_n=64):
+    """[(ptr, requested_bytes, first_bad_offset)] recorded by the canary check."""
+    buf = (ctypes.c_uint64 * (3 * max_n))()
+    n = int(lib().pd_alloc_violations(buf, max_n))
+    return [(buf[3 * i], buf[3 * i + 1], buf[3 * i + 2]) for i in range(min(n, max_n))]
+
+
 def _maybe_enable_from_env():
     v = os.environ.get("FLAGS_use_native_allocator", "")
     if v.lower() in ("1", "true", "yes", "on"):
+        guard = int(os.environ.get("PD_ALLOC_GUARD_BYTES", "0") or 0)
+        if guard or os.environ.get("PD_ALLOC_CANARY"):
+            debug(guard or 4096, bool(os.environ.get("PD_ALLOC_CANARY")))
         enable()
