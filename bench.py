@@ -191,7 +191,8 @@ def main():
                        "parallelism": par, "layers": cfg.num_hidden_layers},
             "mfu_vs_2.5PF_dense": round(mfu, 4),
             "final_loss": round(final_loss, 4),
-            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if torch.cuda.is_available() else None,
+            "peak_mem_gb": round(paddle.device.cuda.max_memory_allocated() / 2**30, 1) if torch.cuda.is_available()
+            else None,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

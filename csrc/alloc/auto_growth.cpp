@@ -34,6 +34,7 @@ constexpr size_t kAlign = 256;          // HBM transaction / LDS-DMA friendly al
 constexpr size_t kMinSplit = 1024;      // do not leave slivers smaller than this
 constexpr int kMaxDevices = 64;
 constexpr int kMaxScan = 64;            // candidates examined for a cross-stream reusable block
+constexpr size_t kTailGuard = size_t(2) << 20;  // unused slack mapped after every chunk
 
 struct Chunk;
 
@@ -174,7 +175,10 @@ static bool grow(Device& d, int dev, size_t size, hipStream_t stream) {
   hipGetDevice(&prev_dev);
   if (prev_dev != dev) hipSetDevice(dev);
   void* p = nullptr;
-  hipError_t err = hipMalloc(&p, bytes);
+  // every chunk carries kTailGuard mapped-but-never-handed-out bytes: a kernel whose vector / tile loads run
+  // a little past the end of the last tensor of a chunk reads guard memory instead of faulting on unmapped VA
+  // (the caching allocator's rounding gives the same slack; tight packing exposed it on the 7B step)
+  hipError_t err = hipMalloc(&p, bytes + kTailGuard);
   if (prev_dev != dev) hipSetDevice(prev_dev);
   if (err != hipSuccess || !p) {
     (void)hipGetLastError();
@@ -185,7 +189,7 @@ static bool grow(Device& d, int dev, size_t size, hipStream_t stream) {
   c->head = b;
   d.chunks.push_back(c);
   index_free(d, b);
-  d.st.reserved += bytes;
+  d.st.reserved += bytes + kTailGuard;
   d.st.num_chunks++;
   d.st.num_grow++;
   if (d.st.reserved > d.st.peak_reserved) d.st.peak_reserved = d.st.reserved;
@@ -242,8 +246,8 @@ static uint64_t release_free_chunks(Device& d, int dev) {
       b = n;
     }
     hipFree(c->base);
-    released += c->size;
-    d.st.reserved -= c->size;
+    released += c->size + kTailGuard;
+    d.st.reserved -= c->size + kTailGuard;
     d.st.num_chunks--;
     delete c;
   }
