@@ -134,11 +134,24 @@ def is_initialized():
     return _initialized and dist.is_initialized()
 
 
+def _shutdown_at_exit():
+    """Orderly teardown of the default process group at interpreter exit: communicator threads that are
+    still running while the process exits can abort it ("terminate called without an active exception")."""
+    try:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    except Exception:
+        pass
+
+
 def init_parallel_env(backend=None, timeout_s=None):
     """Rendezvous (TCPStore on the master) + default RCCL/gloo process group (parallel.py:978)."""
     global _default_group, _initialized
     if _initialized:
         return _default_group
+    import atexit
+
+    atexit.register(_shutdown_at_exit)
     rank = _env_int("RANK", "PADDLE_TRAINER_ID", default=0)
     world = _env_int("WORLD_SIZE", "PADDLE_TRAINERS_NUM", default=1)
     backend = backend or _backend_for_device()
