@@ -1,5 +1,5 @@
 """paddle.vision (reference: python/paddle/vision/)."""
-from . import datasets, models, transforms  # noqa: F401
+from . import datasets, models, ops, transforms  # noqa: F401
 from .models import *  # noqa: F401,F403
 
 
