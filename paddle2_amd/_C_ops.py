@@ -303,4 +303,10 @@ def __getattr__(name):
             if callable(fn):
                 register_op(name, fn, inplace=base != name)
                 return fn
+    from .ops.op_schema import NATIVE, resolve
+
+    fn = resolve(name)   # reference op names whose public API is spelled differently (ops/op_schema.py)
+    if fn is not None:
+        register_op(name, fn, native_kernel=NATIVE.get(name), inplace=name.endswith("_"))
+        return fn
     raise AttributeError(f"paddle2_amd._C_ops has no op '{name}'")

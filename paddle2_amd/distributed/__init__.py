@@ -4,7 +4,8 @@ from .collective import (Group, P2POp, ParallelEnv, ReduceOp, all_gather, all_ga
                          all_gather_object, all_reduce, alltoall, alltoall_single, barrier, batch_isend_irecv,
                          broadcast, broadcast_object_list, destroy_process_group, gather, get_backend, get_group,
                          get_rank, get_world_size, init_parallel_env, irecv, is_available, is_initialized, isend,
-                         new_group, recv, reduce, reduce_scatter, scatter, scatter_object_list, send, stream, wait)
+                         new_group, partial_allgather, partial_recv, partial_send, recv, reduce, reduce_scatter,
+                         scatter, scatter_object_list, send, stream, wait)
 from .parallel import DataParallel, sync_params_buffers  # noqa: F401
 
 

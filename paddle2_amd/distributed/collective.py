@@ -542,6 +542,46 @@ def recv(tensor, src=0, group=None, sync_op=True):
     return _Task(w)
 
 
+def _slice(t, num, id):
+    flat = t.view(-1)
+    if flat.numel() % num:
+        raise ValueError(f"partial p2p: numel {flat.numel()} is not divisible by num={num}")
+    n = flat.numel() // num
+    return flat[id * n:(id + 1) * n]
+
+
+def partial_send(tensor, dst=0, num=1, id=0, group=None, sync_op=True):
+    """Send the ``id``-th of ``num`` equal slices of ``tensor`` (reference partial_send: the pipeline sends
+    only this mp rank's share of an activation; the peer stage re-assembles it with partial_allgather)."""
+    from ..framework.tensor import Tensor
+
+    return send(Tensor._wrap(_slice(tensor._t.contiguous(), num, id)), dst, group, sync_op)
+
+
+def partial_recv(tensor, src=0, num=1, id=0, group=None, sync_op=True):
+    """Receive into the ``id``-th of ``num`` slices of ``tensor`` (in place)."""
+    from ..framework.tensor import Tensor
+
+    part = _slice(tensor._t, num, id)
+    buf = torch.empty_like(part)
+    task = recv(Tensor._wrap(buf), src, group, sync_op=True)
+    part.copy_(buf)
+    return task
+
+
+def partial_allgather(tensor, num, id, group=None, sync_op=True):
+    """Every rank holds slice ``id`` (its rank in ``group``) of ``tensor`` valid; afterwards all ``num``
+    slices are valid everywhere (reference partial_allgather)."""
+    g, pg = _pg(group)
+    if _single(g):
+        return _Task(None)
+    flat = tensor._t.view(-1)
+    out = torch.empty_like(flat)
+    dist.all_gather_into_tensor(out, _slice(flat, num, id).contiguous(), group=pg)
+    flat.copy_(out)
+    return _Task(None)
+
+
 def isend(tensor, dst, group=None):
     return send(tensor, dst, group, sync_op=False)
 

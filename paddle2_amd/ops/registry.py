@@ -50,6 +50,13 @@ def select(name) -> OpEntry:
     """``SelectKernelOrThrowError`` for a single backend: lookup or a typed error."""
     e = _TABLE.get(name)
     if e is None:
+        from .op_schema import NATIVE, resolve
+
+        fn = resolve(name)
+        if fn is not None:
+            register_op(name, fn, native_kernel=NATIVE.get(name), inplace=name.endswith("_"))
+            e = _TABLE[name]
+    if e is None:
         raise NotImplementedError(f"op '{name}' is not registered in the paddle2_amd op table "
                                   f"({len(_TABLE)} ops registered)")
     return e
@@ -65,7 +72,13 @@ def has_op(name) -> bool:
     return name in _TABLE
 
 
-def list_ops():
+def list_ops(populate=True):
+    """Registered op names; by default the whole resolvable reference inventory (ops/op_schema.py)."""
+    if populate:
+        from .op_schema import _POPULATED, populate as _populate
+
+        if not _POPULATED[0]:
+            _populate()
     return sorted(_TABLE)
 
 

@@ -20,6 +20,8 @@ def test_collectives_and_dataparallel():
     assert r0["scatter"] == [1.0, 1.0] and r1["scatter"] == [2.0, 2.0]
     assert r1["p2p"] == [42.0]
     assert r0["batch_p2p"] == [1.0] and r1["batch_p2p"] == [0.0]
+    assert r1["partial_p2p"] == [100.0, 101.0, 102.0, 103.0, 4.0, 5.0, 6.0, 7.0]
+    assert r0["partial_allgather"] == r1["partial_allgather"] == [0.0, 1.0, 2.0, 3.0]
 
 
 def test_collectives_over_native_store():

@@ -94,4 +94,15 @@ out["dp_diff"] = float(max(np.abs(a.numpy() - b.numpy()).max() for a, b in zip(n
 with dp.no_sync():
     ((dp(paddle.ones([2, 6]))) ** 2).mean().backward()
 out["no_sync_ok"] = True
+# partial p2p / allgather: rank 0 sends its second half, rank 1 receives it into its second half;
+# then each rank holds its own quarter valid and partial_allgather completes the tensor
+buf = paddle.to_tensor(np.arange(8, dtype="float32") + 100 * r)
+if r == 0:
+    dist.partial_send(buf, dst=1, num=2, id=1)
+else:
+    dist.partial_recv(buf, src=0, num=2, id=1)
+out["partial_p2p"] = buf.numpy().tolist()
+pa = paddle.to_tensor(np.where(np.arange(4) // 2 == r, np.arange(4, dtype="float32"), -1.0).astype("float32"))
+dist.partial_allgather(pa, num=2, id=r)
+out["partial_allgather"] = pa.numpy().tolist()
 write_result(out)
