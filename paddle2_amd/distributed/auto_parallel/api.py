@@ -443,15 +443,28 @@ class Strategy:
 
 
 class DistModel:
-    """Dygraph stand-in for the reference's static DistModel: ``__call__(inputs, labels)`` runs one
-    train step (forward, loss, backward, optimizer step) in train mode, or forward+loss in eval mode."""
+    """Static-graph training engine behind ``dist.to_static`` (reference: auto_parallel/api.py DistModel +
+    static/engine.py).  The first call records the train step (forward, loss, backward, optimizer) into a
+    Program for the micro-batch shape; the strategy's pipeline / gradient-merge settings become a job plan
+    (distributed/passes: FThenB, 1F1B, Eager1F1B, VPP, ZBH1) that ``PlanExecutor`` runs over the micro-batches,
+    averaging gradients over data-parallel ranks once per step.  ``strategy.amp`` records the step under
+    auto_cast.  eval() records forward + loss, predict() forward only."""
 
-    def __init__(self, layer, loader=None, loss=None, optimizer=None, strategy=None, metrics=None):
+    def __init__(self, layer, loader=None, loss=None, optimizer=None, strategy=None, metrics=None, input_spec=None):
         self._layer = layer
         self._loss = loss
         self._opt = optimizer
+        self._strategy = strategy or Strategy()
         self._mode = "train" if optimizer is not None else ("eval" if loss is not None else "predict")
         self.dist_loader = loader
+        pp = self._strategy.pipeline
+        gm = self._strategy.gradient_merge
+        self._micro = int(pp.get("accumulate_steps") or 0) if pp.get("enable") else 0
+        if not self._micro and gm.get("enable"):
+            self._micro = int(gm.get("k_steps") or 1)
+        self._micro = max(self._micro, 1)
+        self._schedule = pp.get("schedule_mode") or "1F1B"
+        self._cache = {}
 
     def train(self):
         self._mode = "train"
@@ -465,17 +478,69 @@ class DistModel:
         self._mode = "predict"
         self._layer.eval()
 
+    # ---------------------------------------------------------------- recording
+    def _record(self, mode, inputs, labels):
+        from ... import static
+        from ...amp import auto_cast
+        from ...static import graph as g
+
+        prog = static.Program()
+        was = g._state.static
+        g._state.static = True
+        amp = self._strategy.amp
+        try:
+            with static.program_guard(prog, static.Program()):
+                xs = [static.data(f"input_{i}", list(t.shape), t.dtype) for i, t in enumerate(inputs)]
+                ys = [static.data(f"label_{i}", list(t.shape), t.dtype) for i, t in enumerate(labels)]
+                ctx = auto_cast(True, level=amp.get("level", "O1").upper(), dtype=amp.get("dtype", "bfloat16")) \
+                    if amp.get("enable") else _null()
+                with ctx:
+                    out = self._layer(*xs)
+                    loss = self._loss(out, *ys) if (mode != "predict" and self._loss is not None) else None
+                if mode == "train":
+                    self._opt.minimize(loss)
+        finally:
+            g._state.static = was
+        feeds = [f"input_{i}" for i in range(len(inputs))] + [f"label_{i}" for i in range(len(labels))]
+        return prog, feeds, out, loss
+
+    def _split(self, tensors):
+        n = self._micro
+        outs = []
+        for t in tensors:
+            if t.shape[0] % n:
+                raise ValueError(f"batch {t.shape[0]} is not divisible into {n} micro-batches")
+            outs.append(t.split(n) if isinstance(t, Tensor) else None)   # n equal sections
+        return outs
+
+    # ---------------------------------------------------------------- step
     def __call__(self, *args):
+        from ..passes import PlanExecutor, create_job_list, split_program
+        from ..passes.pipeline_scheduler_pass import FORWARD, Job, Plan
+
+        args = [a if isinstance(a, Tensor) else Tensor._wrap(torch.as_tensor(a)) for a in args]
         if self._mode == "predict":
-            return self._layer(*args)
-        inputs, labels = args[:-1], args[-1]
-        out = self._layer(*inputs)
-        loss = self._loss(out, labels)
+            inputs, labels = args, []
+        else:
+            inputs, labels = args[:-1], args[-1:]
+        n = self._micro if self._mode == "train" else 1
+        parts = self._split(list(inputs) + list(labels)) if n > 1 else [[a] for a in list(inputs) + list(labels)]
+        micro = [[p[i] for p in parts] for i in range(n)]
+        key = (self._mode, tuple((tuple(t.shape), str(t.dtype)) for t in micro[0]))
+        if key not in self._cache:
+            self._cache[key] = self._record(self._mode, micro[0][:len(inputs)], micro[0][len(inputs):])
+        prog, feeds, out, loss = self._cache[key]
+        micro_feeds = [dict(zip(feeds, m)) for m in micro]
         if self._mode == "train":
-            loss.backward()
-            self._opt.step()
-            self._opt.clear_grad()
-        return loss
+            pp = self._strategy.pipeline
+            plan = Plan(create_job_list(self._schedule, n, int(pp.get("pp_stage") or 0),
+                                        int(pp.get("pp_degree") or 1), int(pp.get("vpp_degree") or 1)),
+                        split_program(prog))
+            res = PlanExecutor().run(prog, plan, micro_feeds, [loss])
+            return Tensor._wrap(torch.stack([r[0].detach() for r in res]).mean())
+        plan = Plan([Job(FORWARD, 0)], split_program(prog))
+        res = PlanExecutor().run(prog, plan, micro_feeds, [loss] if self._mode == "eval" else [out])
+        return Tensor._wrap(res[0][0].detach())
 
     def state_dict(self, mode="all"):
         sd = dict(self._layer.state_dict())
@@ -487,5 +552,13 @@ class DistModel:
         self._layer.set_state_dict(sd)
 
 
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 def to_static(layer, loader=None, loss=None, optimizer=None, strategy=None, input_spec=None):
-    return DistModel(layer, loader, loss, optimizer, strategy)
+    return DistModel(layer, loader, loss, optimizer, strategy, input_spec=input_spec)
