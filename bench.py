@@ -196,7 +196,13 @@ def main():
         }
         print(json.dumps(out), flush=True)
     if world > 1:
+        # every rank is past its last collective before any tears down; then leave without running C++ static
+        # destructors (a library thread still joinable there turns a finished run into SIGABRT at exit)
+        C.barrier()
         C.destroy_process_group()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":
