@@ -36,11 +36,63 @@ def estimate_memory_gb(model_cfg, cfg):
     pw = 2 * P / (mp * pp) / (sh if stage >= 3 else 1)
     gr = 2 * P / (mp * pp) / (sh if stage >= 2 else 1)
     opt = 12 * P / (mp * pp) / (sh if stage >= 1 else 1)
-    per_layer = (2 * s * b * h) if cfg.get("use_recompute", False) else s * b * h * 34 / mp
-    inflight = pp if pp > 1 else 1
-    act = per_layer * L * inflight
+    per_layer = layer_activation_bytes(s, b, h, mp, cfg)
+    act = per_layer * L * inflight_micro_batches(pp, cfg.get("vpp_degree", 1) or 1)
     logits = 2 * s * b * model_cfg.get("vocab_size", 32000) * 4 / mp  # fp32 logits + grad
     return (pw + gr + opt + act + logits) / 2**30
+
+
+# per-layer activation bytes (bf16) with flash attention, by recompute granularity: the attention block
+# (qkv / rope / flash out / o-proj inputs) accounts for ~11 sbh of the 34 sbh/mp, core attention (flash
+# output + softmax lse) for ~2 sbh; a recomputed block keeps only its input (2 sbh, not split by mp)
+_ATTN_BLOCK, _CORE_ATTN = 11.0, 2.0
+
+
+def layer_activation_bytes(s, b, h, mp, cfg):
+    if not cfg.get("use_recompute", False):
+        return s * b * h * 34 / mp
+    gran = cfg.get("recompute_granularity") or "full"
+    if gran == "full":
+        return 2 * s * b * h
+    if gran == "full_attn":
+        return s * b * h * (34 - _ATTN_BLOCK) / mp + 2 * s * b * h
+    return s * b * h * (34 - _CORE_ATTN) / mp
+
+
+def inflight_micro_batches(pp, vpp=1):
+    """Micro-batches whose activations the first 1F1B stage holds (interleaving adds (pp-1)/(pp*vpp))."""
+    if pp <= 1:
+        return 1
+    return pp * (1 + (pp - 1) / (pp * vpp)) if vpp > 1 else pp
+
+
+def get_mem(total_cards, parallel_cfg, l, h, a, V, s, gbs):
+    """Peak GiB per GPU of a decoder-only model (reference cost_model.get_mem signature)."""
+    m = {"num_layers": l, "hidden_size": h, "num_attention_heads": a, "vocab_size": V, "seq_length": s,
+         "global_batch_size": gbs}
+    return estimate_memory_gb(m, parallel_cfg)
+
+
+def get_not_oom_cfgs(cfgs, tuner_cfg):
+    """Structurally valid configs annotated with ``memory_cost`` (GiB), dropping those above
+    ``per_card_memory`` (default: 288 GB HBM3E)."""
+    m = tuner_cfg["model_cfg"]
+    total = tuner_cfg.get("search_algo", {}).get("estimated_num_gpus", tuner_cfg.get("num_gpus"))
+    cap = tuner_cfg.get("per_card_memory", HBM_GB)
+    L, h, a, V, gbs = m["num_layers"], m["hidden_size"], m["num_attention_heads"], m["vocab_size"], \
+        m["global_batch_size"]
+    out = []
+    for c in cfgs:
+        mp, sh, mbs, pp, vpp, dp = (c["mp_degree"], c["sharding_degree"], c["micro_batch_size"], c["pp_degree"],
+                                    c.get("vpp_degree", 1), c["dp_degree"])
+        if mp * sh * pp * dp != total or gbs % (sh * dp * mbs) or L % (pp * vpp) or (vpp != 1 and pp <= 2):
+            continue
+        if a % mp or V % mp or h % mp:
+            continue
+        c = dict(c, memory_cost=get_mem(total, c, L, h, a, V, m.get("seq_length", 4096), gbs))
+        if c["memory_cost"] <= cap:
+            out.append(c)
+    return out
 
 
 def estimate_step_time(model_cfg, cfg, global_batch):

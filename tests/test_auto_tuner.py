@@ -1,20 +1,130 @@
-"""Auto tuner (reference tests: test/auto_tuner/ — prune rules, search, recorder) incl. the
+"""Auto tuner (reference tests: test/auto_tuner/ — candidates, search_all, prune rules incl. the history
+rules, dp-estimation / gbs / customize search, recorder best-with-buffer, log parsing, resume) and the
 launcher integration with a real trial script."""
+import copy
 import json
 import os
 import subprocess
 import sys
 
+import pytest
+
 from paddle2_amd.distributed.auto_tuner import AutoTuner, HistoryRecorder, estimate_memory_gb
-from paddle2_amd.distributed.auto_tuner.launch import read_metric_log, run
+from paddle2_amd.distributed.auto_tuner import prune as P
+from paddle2_amd.distributed.auto_tuner import utils as U
+from paddle2_amd.distributed.auto_tuner.launch import run
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLAMA7B = {"hidden_size": 4096, "num_layers": 32, "num_attention_heads": 32, "vocab_size": 32000,
            "seq_length": 4096, "global_batch_size": 64, "intermediate_size": 11008}
+AUTO = {k: "auto" for k in ("dp_degree", "mp_degree", "pp_degree", "sharding_degree", "micro_batch_size",
+                            "sharding_stage")}
 
 
-def test_prune_and_order():
-    cfg = {"num_gpus": 8, "gpus_per_node": 8, "model_cfg": dict(LLAMA7B, num_attention_heads=12)}
+def _cfg(**kw):
+    base = {"num_gpus": 8, "nodes": 1, "gpus_per_node": 8, "model_cfg": dict(LLAMA7B)}
+    base.update(AUTO)
+    base.update(kw)
+    return base
+
+
+def test_param2range_and_candidates():
+    assert U.param2range(None, 8, "x") == [1]
+    assert U.param2range("auto", 4, "x") == [1, 2, 3, 4]
+    assert U.param2range({"min": 2, "max": 4}, 8, "x") == [2, 3, 4]
+    assert U.param2range(3, 8, "x") == [3]
+    with pytest.raises(ValueError):
+        U.param2range("all", 8, "x")
+    assert U.divisor(12) == [1, 2, 3, 4, 6, 12] and U.divisor(1) == [1]
+    c = U.default_candidates(_cfg(model_cfg=dict(LLAMA7B, num_attention_heads=12)))
+    assert c["mp_degree"] == [4, 2, 1]           # memory-first: large mp first; 8 does not divide 12 heads
+    assert c["sharding_stage"] == [3, 2, 1] and c["dp_degree"][0] == 1
+    c = U.default_candidates(_cfg(schedule_mode="performance"))
+    assert c["mp_degree"][0] == 1 and c["micro_batch_size"][0] == 64 and c["sharding_stage"] == [1, 2, 3]
+    # unset dimension pinned to 1
+    cfg = _cfg()
+    del cfg["pp_degree"]
+    assert U.default_candidates(cfg)["pp_degree"] == [1]
+
+
+def test_search_all_is_valid_and_pruned():
+    cfg = _cfg(use_recompute="auto", recompute_granularity="auto", vpp_degree="auto")
+    cfg["candidates"] = U.default_candidates(cfg)
+    cfgs = U.search_all(cfg)
+    before, after = cfg["search_space_size"]
+    assert after == len(cfgs) and before > after > 0
+    for c in cfgs:
+        assert c["dp_degree"] * c["mp_degree"] * c["pp_degree"] * c["sharding_degree"] == 8
+        assert 64 % (c["micro_batch_size"] * c["dp_degree"] * c["sharding_degree"]) == 0
+        assert 32 % (c["pp_degree"] * c["vpp_degree"]) == 0
+        assert not (c["pp_degree"] <= 2 and c["vpp_degree"] > 1)
+        assert not (c["pp_degree"] > 1 and c["sharding_stage"] > 1 and c["sharding_degree"] > 1)
+        assert c["use_recompute"] or c["recompute_granularity"] in (None, "full")
+    # one stage kept when sharding is off
+    no_shard = [c for c in cfgs if c["sharding_degree"] == 1]
+    keys = {json.dumps({k: v for k, v in c.items() if k not in ("sharding_stage", "estimated_memory_gb")},
+                       sort_keys=True) for c in no_shard}
+    assert len(keys) == len(no_shard)
+
+
+def test_schedule_prior_and_invalid_strategy():
+    cfg = _cfg(schedule_prior=["mp4"], invalid_strategy=["pp8"])
+    cfg["candidates"] = U.default_candidates(cfg)
+    cfgs = U.search_all(cfg)
+    assert cfgs[0]["mp_degree"] == 4 and all(c["pp_degree"] != 8 for c in cfgs)
+    assert U._matched({"sharding_degree": 2, "sharding_stage": 3}, "sharding*_stage3")
+    assert not U._matched({"sharding_degree": 1, "sharding_stage": 3}, "sharding*")
+    assert U._matched({"use_recompute": True, "recompute_granularity": "full_attn"}, "recompute1_granularity1")
+
+
+def test_prune_rules():
+    cfg = _cfg()
+    cfg["candidates"] = U.default_candidates(cfg)
+    base = {"dp_degree": 1, "mp_degree": 2, "pp_degree": 4, "sharding_degree": 1, "sharding_stage": 1,
+            "micro_batch_size": 1, "vpp_degree": 1, "use_recompute": False, "recompute_granularity": None}
+    assert not P.prune_by_mp(cfg, base)
+    assert P.prune_by_mp(dict(cfg, model_cfg=dict(LLAMA7B, num_key_value_heads=3)), base)   # GQA split
+    assert P.prune_by_mp(dict(cfg, mp_degree=[16]), dict(base, mp_degree=16))            # beyond xGMI node
+    assert P.prune_by_vpp(cfg, dict(base, pp_degree=2, vpp_degree=2))
+    assert P.prune_by_mbs(cfg, dict(base, micro_batch_size=32))        # 2 micro-batches < pp 4
+    assert P.prune_by_sharding(cfg, dict(base, sharding_degree=2, sharding_stage=2))
+    assert P.prune_by_recompute(cfg, dict(base, recompute_granularity="core_attn"))
+    assert P.prune_by_num_gpus(cfg, dict(base, dp_degree=2))
+    assert P.prune_by_memory_estimation(dict(cfg, max_mem_usage=10), base)
+    assert not P.prune_by_memory_estimation(cfg, base) and base["estimated_memory_gb"] < 288
+    rr = dict(cfg, refined_recompute=["flash_attn"])
+    assert P.prune_by_refined_recompute(rr, dict(base, flash_attn=2))          # no full recompute
+    assert not P.prune_by_refined_recompute(rr, dict(base, use_recompute=True, recompute_granularity="full",
+                                                     flash_attn=8))
+    assert P.prune_by_refined_recompute(rr, dict(base, use_recompute=True, recompute_granularity="full",
+                                                 flash_attn=9))          # > 32 / pp layers
+
+
+def test_history_prune_rules():
+    cfg = _cfg()
+    cfg["candidates"] = U.default_candidates(cfg)
+    base = {"dp_degree": 1, "mp_degree": 2, "pp_degree": 1, "sharding_degree": 4, "sharding_stage": 1,
+            "micro_batch_size": 2, "vpp_degree": 1, "use_recompute": False, "recompute_granularity": None}
+    ran_big = dict(base, micro_batch_size=4, time=1.0)
+    cur = dict(base)
+    assert P.prune_by_mbs_history(cfg, cur, [ran_big], []) and cur["time"] == 1.0
+    oom_small = dict(base, micro_batch_size=1, max_mem_usage="OOM")
+    cur = dict(base)
+    assert P.prune_by_mbs_history(cfg, cur, [oom_small], []) and cur["max_mem_usage"] == "OOM"
+    assert not P.prune_by_mbs_history(cfg, dict(base), [dict(base, micro_batch_size=1, time=1.0)], [])
+    # sharding: a lower stage that ran makes a higher one redundant; a higher one that OOM'd dooms a lower
+    assert P.prune_by_sharding_history(cfg, dict(base, sharding_stage=3), [dict(base, time=2.0)], [])
+    assert P.prune_by_sharding_history(cfg, dict(base), [dict(base, sharding_stage=2, max_mem_usage="OOM")], [])
+    # recompute: no-recompute ran -> full recompute redundant
+    assert P.prune_by_recompute_history(cfg, dict(base, use_recompute=True, recompute_granularity="full"),
+                                        [dict(base, time=3.0)], [])
+    # mp/pp: a larger mp with the same mp*pp OOM'd -> smaller mp OOMs too
+    assert P.prune_by_mp_pp_history(cfg, dict(base, mp_degree=1, pp_degree=2),
+                                    [dict(base, mp_degree=2, pp_degree=1, max_mem_usage="OOM")], [])
+
+
+def test_grid_search_order_and_history_skip():
+    cfg = _cfg(model_cfg=dict(LLAMA7B, num_attention_heads=12))
     t = AutoTuner(cfg)
     for c in t.algo.all_tasks:
         assert c["dp_degree"] * c["mp_degree"] * c["pp_degree"] * c["sharding_degree"] == 8
@@ -22,39 +132,158 @@ def test_prune_and_order():
         assert c["estimated_memory_gb"] <= 288 * 0.92
     est = [c["estimated_step_time_s"] for c in t.algo.all_tasks]
     assert est == sorted(est)
-    # stage 3 sharding needs less memory than stage 1 which needs less than pure dp
+    # after a run with micro-batch b, the same layout with a smaller micro-batch is skipped
+    first = t.search_once()
+    t.add_cfg(dict(first, time=1.0))
+    nxt = []
+    while (c := t.search_once()) is not None:
+        nxt.append(c)
+    same = [c for c in nxt if all(c[k] == first[k] for k in ("dp_degree", "mp_degree", "pp_degree",
+                                                            "sharding_degree", "sharding_stage"))]
+    assert all(c["micro_batch_size"] > first["micro_batch_size"] for c in same)
+
+
+def test_memory_model():
     m = LLAMA7B
     assert estimate_memory_gb(m, {"sharding_degree": 8, "sharding_stage": 3}) < \
         estimate_memory_gb(m, {"sharding_degree": 8, "sharding_stage": 1}) < estimate_memory_gb(m, {})
     # calibrated against the measured 7B single-GPU step: 8 x 4096 tokens, 241 GB peak
     assert abs(estimate_memory_gb(m, {"micro_batch_size": 8}) - 241) < 15
+    full = {"micro_batch_size": 8, "use_recompute": True, "recompute_granularity": "full"}
+    attn = dict(full, recompute_granularity="full_attn")
+    core = dict(full, recompute_granularity="core_attn")
+    assert estimate_memory_gb(m, full) < estimate_memory_gb(m, attn) < estimate_memory_gb(m, core) \
+        < estimate_memory_gb(m, {"micro_batch_size": 8})
+    pp4 = {"pp_degree": 4, "micro_batch_size": 1}
+    assert estimate_memory_gb(m, pp4) < estimate_memory_gb(m, dict(pp4, vpp_degree=2))
 
 
-def test_trials_record_best(tmp_path):
+def test_memory_estimation_tool(tmp_path):
+    tool = os.path.join(ROOT, "paddle2_amd", "distributed", "auto_tuner", "memory_cost_model.py")
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-m", "paddle2_amd.distributed.auto_tuner.memory_cost_model",
+                        "--dp_degree", "1", "--mp_degree", "1", "--pp_degree", "1", "--vpp_degree", "1",
+                        "--sharding_degree", "1", "--sharding_stage", "1", "--micro_batch_size", "8",
+                        "--use_recompute", "False", "--hidden_size", "4096", "--num_layers", "32",
+                        "--num_attention_heads", "32", "--vocab_size", "32000", "--intermediate_size", "11008"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert abs(float(r.stdout) / 1024 - 241) < 15
+    # as a prune tool: a shim that calls the module (the rule runs the tool as a script)
+    shim = tmp_path / "mem.py"
+    shim.write_text(f"import sys; sys.path.insert(0, {ROOT!r})\n"
+                    "from paddle2_amd.distributed.auto_tuner.memory_cost_model import *\n"
+                    "print(get_model_memory_usage(parse_arguments()))\n")
+    cfg = _cfg(memory_estimation_tool=str(shim), max_mem_usage=100)
+    cfg["candidates"] = U.default_candidates(cfg)
+    big = {"dp_degree": 8, "mp_degree": 1, "pp_degree": 1, "vpp_degree": 1, "sharding_degree": 1,
+           "sharding_stage": 1, "micro_batch_size": 8, "use_recompute": False, "recompute_granularity": None}
+    assert P.prune_by_memory_estimation(cfg, big) and big["estimated_memory_usage"] > 100 * 1024
+    assert tool  # the module path exists for users who point at it directly
+
+
+def test_dp_estimation_and_gbs_search():
+    cfg = _cfg(nodes=2, gpus_per_node=8, num_gpus=16,
+               search_algo={"name": "dp_estimation", "estimated_num_gpus": 16, "sharding_overlap": True},
+               metric_cfg={"name": "tokens_per_sec", "OptimizationDirection": "Maximize"})
+    t = AutoTuner(cfg)
+    single = [c for c in t.algo.all_tasks if "sharding_overlap" not in c]
+    assert single and all(c["dp_degree"] == 1 and c["sharding_degree"] == 1 for c in single)
+    for c in single:
+        assert c["num_gpus"] == c["mp_degree"] * c["pp_degree"]
+        assert c["global_batch_size"] == 64 // c["estimated_dp_degree"]
+    pairs = [c for c in t.algo.all_tasks if "sharding_overlap" in c]
+    assert pairs and {c["sharding_overlap"] for c in pairs} == {False, True}
+    g = AutoTuner({"num_gpus": 8, "nodes": 1, "model_cfg": dict(LLAMA7B, global_batch_size="auto"),
+                   "search_algo": {"name": "gbs"}})
+    assert g.tuner_cfg["candidates"]["mp_degree"] == [2] and g.tuner_cfg["candidates"]["pp_degree"] == [2]
+    c = g.search_once()
+    assert c["global_batch_size"] == c["pp_degree"] * c["sharding_degree"] * c["micro_batch_size"]
+    assert g.tuner_cfg["model_cfg"]["global_batch_size"] == c["global_batch_size"]
+
+
+def test_customize_from_csv(tmp_path):
+    p = tmp_path / "cfgs.csv"
+    p.write_text("dp_degree,mp_degree,pp_degree,vpp_degree,micro_batch_size,sharding_degree,sharding_stage,"
+                 "use_recompute,recompute_granularity\n1,2,2,1,1,2,1,true,full\n8,1,1,1,2,1,1,false,\n")
+    t = AutoTuner({"num_gpus": 8, "model_cfg": LLAMA7B, "search_algo": {"name": "customize"},
+                   "configs_csv": str(p)})
+    a, b = t.search_once(), t.search_once()
+    assert a["mp_degree"] == 2 and a["use_recompute"] is True and a["recompute_granularity"] == "full"
+    assert b["dp_degree"] == 8 and b["recompute_granularity"] is None and t.search_once() is None
+
+
+def test_log_parsing(tmp_path):
+    d = tmp_path / "trial"
+    d.mkdir()
+    (d / "workerlog.0").write_text("".join(f"step {i} interval_runtime: {i}.0\n" for i in range(1, 25)) +
+                                   json.dumps({"peak_mem_gb": 12.5}) + "\n")
+    v, err = U.read_metric_log(str(d), "workerlog.0", "interval_runtime")
+    assert err == 0 and v == sum(range(15, 25)) / 10            # mean of the last 10
+    (d / "workerlog.0").write_text("".join(f"{i}.5 step/s\n" for i in range(12)))
+    assert U.read_metric_log(str(d), "workerlog.0", "step/s") == (round(sum(i + .5 for i in range(9, 12)) / 3, 5), 0)
+    metric, mem, err = U.read_log(str(d), target_metric="step/s")
+    assert err & 4   # no memory reading in this log
+    (d / "workerlog.1").write_text("RuntimeError: HIP out of memory. Tried to allocate\n")
+    metric, mem, err = U.read_log(str(d), target_metric="step/s")
+    assert err & 2 and "Out of memory" in U.find_error_from_log(str(d))
+    (d / "0.gpu.log").write_text("index,utilization_gpu,memory_total,memory_used,a,b\n0,90,288000,1234,0,0\n"
+                                 "0,95,288000,2345,0,0\n")
+    assert U.read_memory_log(str(d), "0.gpu.log") == (2345.0, False)
+
+
+def test_recorder_best_with_buffer(tmp_path):
+    r = HistoryRecorder({"metric_cfg": {"name": "tps"}})
+    r.add_cfg(mp_degree=1, tps=300.0, time=300.0, max_mem_usage=270000.0)
+    r.add_cfg(mp_degree=2, tps=250.0, time=250.0, max_mem_usage=150000.0)
+    r.add_cfg(mp_degree=4, tps=None, time=-1, max_mem_usage="OOM")
+    best, err = r.get_best("tps", "Maximize")
+    assert not err and best["mp_degree"] == 1
+    best, err = r.get_best("tps", "Maximize", buffer=50000, max_mem_usage=288000)
+    assert best["mp_degree"] == 2          # the fastest one with 50 GB headroom
+    r.store_history(str(tmp_path / "h.csv"))
+    head = (tmp_path / "h.csv").read_text().splitlines()[0].split(",")
+    assert head[0] == "job_id" and "time" not in head
+    hist, err = HistoryRecorder().load_history(str(tmp_path / "h.csv"))
+    assert not err and len(hist) == 3 and hist[2]["max_mem_usage"] == "OOM"
+
+
+def test_gen_new_args():
+    tc = {"run_cmd": {"micro_batch_size": ["--micro_batch", 1], "mp_degree": ["--tp", 1]},
+          "args_template": {"use_recompute": "--recompute"}}
+    out = U.gen_new_args(["--micro_batch", "1", "--steps", "5"], {"micro_batch_size": 4, "mp_degree": 2,
+                                                                 "use_recompute": True}, tc)
+    assert out == ["--micro_batch", "4", "--steps", "5", "--tp", "2", "--recompute", "1"]
+
+
+def test_trials_record_best_and_resume(tmp_path):
     cfg = {"num_gpus": 4, "model_cfg": dict(LLAMA7B, num_layers=8, global_batch_size=8), "task_limit": 6,
-           "metric_cfg": {"name": "tokens_per_sec", "OptimizationDirection": "Maximize"}}
+           "metric_cfg": {"name": "tokens_per_sec", "OptimizationDirection": "Maximize"}, "sort_by_estimate": False,
+           **AUTO}
+    calls = []
 
     def fake_runner(c, env, argv, log_dir):
+        calls.append(c)
         os.makedirs(log_dir, exist_ok=True)
         tps = 1000 * c["micro_batch_size"] / c["mp_degree"] / c["pp_degree"]
         with open(os.path.join(log_dir, "workerlog.0"), "w") as f:
-            f.write(json.dumps({"tokens_per_sec": tps}) + "\n")
+            f.write(json.dumps({"tokens_per_sec": tps, "peak_mem_gb": 10 * c["micro_batch_size"]}) + "\n")
+        assert json.loads(env["PADDLE_AUTO_TUNER_CFG"])["mp_degree"] == c["mp_degree"]
         return 0
 
-    best, tuner = run(cfg, [], "train.py", [], log_root=str(tmp_path), runner=fake_runner)
-    assert best["tokens_per_sec"] == max(h["tokens_per_sec"] for h in tuner.recorder.history)
+    best, tuner = run(copy.deepcopy(cfg), [], "train.py", [], log_root=str(tmp_path), runner=fake_runner)
+    measured = [h["tokens_per_sec"] for h in tuner.recorder.history if h["tokens_per_sec"] is not None]
+    assert best["tokens_per_sec"] == max(measured)
+    assert all(isinstance(h["max_mem_usage"], float) for h in tuner.recorder.history)
     assert os.path.exists(tmp_path / "history.csv") and os.path.exists(tmp_path / "best_cfg.json")
-    rec = HistoryRecorder()
-    hist, err = rec.load_history(str(tmp_path / "history.csv"))
-    assert not err and len(hist) == 6
-
-
-def test_read_metric_log(tmp_path):
-    p = tmp_path / "log"
-    p.write_text("step 1 interval_runtime: 2.0\nstep 2 interval_runtime: 1.5\n")
-    assert read_metric_log(str(p), "interval_runtime") == (1.5, None)
-    p.write_text("RuntimeError: HIP out of memory\n")
-    assert read_metric_log(str(p), "interval_runtime")[1] == "OOM"
+    n = len(calls)
+    hist, err = HistoryRecorder().load_history(str(tmp_path / "history.csv"))
+    assert not err and len(hist) == n
+    # resume: the stored trials are not re-run
+    best2, tuner2 = run(dict(copy.deepcopy(cfg), resume=True), [], "train.py", [], log_root=str(tmp_path),
+                        runner=fake_runner)
+    assert len(calls) == n and best2["tokens_per_sec"] == best["tokens_per_sec"]
+    assert all(h.get("resumed") for h in tuner2.recorder.history)
 
 
 def test_launch_auto_tuner_end_to_end(tmp_path):
