@@ -21,7 +21,7 @@ int pd_norm_bwd(int, int, int, const void*, const void*, const void*, const floa
                 float*, float*, void*, void*, int, int, int, void*);
 int pd_swiglu_fwd(int, const void*, const void*, void*, long, int, long, long, void*);
 int pd_gemm(int, int, const void*, long, const void*, long, void*, long, void*, long, const void*, int, int, int, float,
-            int, int, int, void*);
+            int, int, int, void*, long, void*);
 int pd_gemm_grouped(int, int, const void*, long, const void*, long, long, void*, long, long, void*, long, const void*,
                     long, const int*, int, int, int, int, int, int, float, int, int, void*);
 int pd_transpose16(const void*, void*, long, long, long, long, void*);
@@ -117,9 +117,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("gemm", [](int layout, int epi, uintptr_t a, long lda, uintptr_t b, long ldb, uintptr_t c, long ldc,
                    uintptr_t c2, long ldc2, uintptr_t bias, int M, int N, int K, float beta, int H, int group_m,
-                   int variant, uintptr_t st) {
+                   int variant, uintptr_t ws, long ws_bytes, uintptr_t st) {
     check(pd_gemm(layout, epi, P<const void*>(a), lda, P<const void*>(b), ldb, P<void*>(c), ldc, P<void*>(c2), ldc2,
-                  P<const void*>(bias), M, N, K, beta, H, group_m, variant, P<void*>(st)),
+                  P<const void*>(bias), M, N, K, beta, H, group_m, variant, P<void*>(ws), ws_bytes, P<void*>(st)),
           "gemm");
   });
   m.def("gemm_grouped", [](int layout, int epi, uintptr_t a, long lda, uintptr_t b, long ldb, long gsb, uintptr_t c,

@@ -33,6 +33,7 @@
 //    up columns; it writes the pre-activation gu for the backward and silu(g)*u).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <utility>
 
 #include "common.h"
@@ -76,7 +77,36 @@ struct Params {
   const int* goff;
   int ngroups, gmode;
   long gsb, gsc, gsbias;
+  // tail split-K (v2 kernel, not grouped): each XCD runs its full waves of tiles whole, and its last partial
+  // wave's tiles as ksplit K-slices of kchunk K-tiles into fp32 slabs `part` ([8][tail_cap][ksplit][BM*BN]);
+  // splitk_reduce_kernel sums the slices in order into C.  cpx = CUs (= workgroup slots) per XCD.
+  float* part;
+  int ksplit, kchunk, tail_cap, cpx;
 };
+
+// Tiles [t0, t0 + n) of the grouped order belong to XCD x (the chunking xcd_remap uses); the first `full`
+// of them fill whole waves of the XCD's cpx CUs, the last `tail` run in its final, partial wave.
+struct XPlan {
+  int t0, n, full, tail;
+};
+__host__ __device__ __forceinline__ XPlan xcd_plan(int nwg, int x, int cpx) {
+  const int q = nwg / 8, r = nwg % 8;
+  XPlan o;
+  o.n = q + (x < r ? 1 : 0);
+  o.t0 = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  o.tail = o.n % cpx;
+  o.full = o.n - o.tail;
+  return o;
+}
+
+// grouped tile order: group_m row-tiles sweep the column tiles together (L2 reuse within an XCD)
+__device__ __forceinline__ void tile_of(const Params& p, int bid, int& tm, int& tn) {
+  const int per_group = p.group_m * p.tiles_n;
+  const int first_m = (bid / per_group) * p.group_m;
+  const int gsz = min(p.tiles_m - first_m, p.group_m);
+  tm = first_m + (bid % per_group) % gsz;
+  tn = (bid % per_group) / gsz;
+}
 
 // Grouped-GEMM set-up: rebase `p` onto this workgroup's group; returns false if the workgroup has no tile.
 // `bx` is the block index the tile decode below uses (gmode 1 strips the group part off it).
@@ -353,15 +383,28 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(Params p) {
   int bx = blockIdx.x;
   if (p.goff) group_setup<EPI>(p, bx);
   const int nwg = p.tiles_m * p.tiles_n;
-  const int bid = xcd_remap(bx, nwg);
-  // grouped order: group_m row-tiles sweep the column tiles together (L2 reuse within an XCD)
-  const int per_group = p.group_m * p.tiles_n;
-  const int gid = bid / per_group;
-  const int first_m = gid * p.group_m;
-  const int gsz = min(p.tiles_m - first_m, p.group_m);
-  int tm = first_m + (bid % per_group) % gsz;
-  const int tn = (bid % per_group) / gsz;
+  int bid, kpart = -1, slab = 0;
+  if (p.ksplit > 1) {
+    const int x = bx % 8, local = bx / 8;
+    const XPlan xp = xcd_plan(nwg, x, p.cpx);
+    if (local >= xp.full + xp.tail * p.ksplit) return;  // whole workgroup: this XCD has fewer blocks
+    if (local < xp.full) {
+      bid = xp.t0 + local;
+    } else {
+      const int r = local - xp.full;
+      bid = xp.t0 + xp.full + r / p.ksplit;
+      kpart = r % p.ksplit;
+      slab = (x * p.tail_cap + r / p.ksplit) * p.ksplit + kpart;
+    }
+  } else {
+    bid = xcd_remap(bx, nwg);
+  }
+  int tm, tn;
+  tile_of(p, bid, tm, tn);
   if (p.goff && p.gmode == 0 && !group_rows<EPI>(p, tm)) return;  // whole workgroup: no tile of any group
+  // a K-slice of a tail tile: rebase K so the loop below sees a problem of kchunk K-tiles
+  const int kt0 = kpart >= 0 ? kpart * p.kchunk : 0;
+  if (kpart >= 0) p.K = min(p.K - kt0 * BK, p.kchunk * BK);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -382,11 +425,11 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(Params p) {
   const Ld LB = lane_setup<BKM, true, EPI>(p.ldb, Ncols, tn, p.H, wave, lane);
   // tile base pointers (element units) at k0 = 0; per K-tile they advance by a_step / b_step elements
   const int tma = DBG == 6 ? 0 : tm, tnb = DBG == 6 ? 0 : tn;  // (ablation 6: every tile loads tile (0,0))
-  const unsigned short* a_t0 = AK ? p.A + (long)tma * BM * p.lda : p.A + (long)tma * BM;
-  const unsigned short* b_t0 =
-      BKM ? p.B + (long)tnb * BN * p.ldb : (EPI == kEpiSwiGLU ? p.B : p.B + (long)tnb * BN);
   const long a_step = AK ? BK : (long)BK * p.lda;
   const long b_step = BKM ? BK : (long)BK * p.ldb;
+  const unsigned short* a_t0 = (AK ? p.A + (long)tma * BM * p.lda : p.A + (long)tma * BM) + a_step * kt0;
+  const unsigned short* b_t0 =
+      (BKM ? p.B + (long)tnb * BN * p.ldb : (EPI == kEpiSwiGLU ? p.B : p.B + (long)tnb * BN)) + b_step * kt0;
   const unsigned a_is = (unsigned)(AK ? 64 * p.lda * 2 : 16 * p.lda * 2);
   const unsigned b_is = (unsigned)(BKM ? 64 * p.ldb * 2 : 16 * p.ldb * 2);
   const bool a_rows_full = !AK || (tm + 1) * BM <= p.M;
@@ -505,7 +548,52 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(Params p) {
     ktile(C1{}, t + 1);
   }
 
+  if constexpr (EPI != kEpiSwiGLU) {
+    if (kpart >= 0) {  // K-slice of a tail tile: the raw fp32 partial into its slab (tile-local, unmasked)
+      float* sp = p.part + (long)slab * (BM * BN);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            sp[(arow + 16 * i + 4 * (lane >> 4) + e) * BN + bcolw + 16 * j + (lane & 15)] = acc[i][j][e];
+      return;
+    }
+  }
   epilogue<EPI>(p, acc, tm, tn, arow, bcolw, wn, lane);
+}
+
+// Sum the K-slices of every tail tile in slice order (deterministic) and apply the epilogue: fp32 main grad
+// C = sum + beta*C, or bf16 C = sum (+ bias).  grid (BM*BN/1024, 8*tail_cap), 256 threads x 4 elements.
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(Params p) {
+  const int x = blockIdx.y / p.tail_cap, j = blockIdx.y % p.tail_cap;
+  const XPlan xp = xcd_plan(p.tiles_m * p.tiles_n, x, p.cpx);
+  if (j >= xp.tail) return;
+  int tm, tn;
+  tile_of(p, xp.t0 + xp.full + j, tm, tn);
+  const int e0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  const int r = tm * BM + e0 / BN, c = tn * BN + e0 % BN;
+  if (r >= p.M) return;
+  const float* sp = p.part + (long)(x * p.tail_cap + j) * p.ksplit * (BM * BN) + e0;
+  float4 s = *(const float4*)sp;
+  for (int k = 1; k < p.ksplit; ++k) {
+    const float4 v = *(const float4*)(sp + (long)k * (BM * BN));
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  const float sv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (c + q >= p.N) break;
+    if constexpr (EPI == kEpiF32) {
+      float* cp = (float*)p.C + (long)r * p.ldc + c + q;
+      *cp = p.beta != 0.f ? sv[q] + p.beta * *cp : sv[q];
+    } else {
+      const float bv = p.bias ? bf2f(p.bias[c + q]) : 0.f;
+      ((unsigned short*)p.C)[(long)r * p.ldc + c + q] = f2bf(sv[q] + bv);
+    }
+  }
 }
 
 // ================================================================================================
@@ -778,9 +866,49 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Params p) {
 }  // namespace pd
 
 // layout: bit0 = A K-major, bit1 = B K-major.  epi: 0 bf16 (+bias), 1 fp32 main grad (beta), 2 swiglu.
+// CUs per XCD of the current device (workgroup slots of the 128 KiB-LDS kernel), cached per device
+static int cus_per_xcd() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 32;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 8) n = 256;
+    cache[dev] = n / 8;
+  }
+  return cache[dev];
+}
+
+// Tail split-K plan: when an XCD's last wave would run at most half full, its tail tiles are cut into
+// ksplit K-slices (at least 8 K-tiles each) so that wave finishes ~ksplit times sooner.  Returns the grid
+// size (0 = no split).  Workspace: 8 * tail_cap * ksplit slabs of BM*BN fp32 (<= 8 * cpx * 256 KiB).
+static int plan_splitk(pd::gm::Params& p, long ws_bytes) {
+  using namespace pd::gm;
+  const int nwg = p.tiles_m * p.tiles_n, cpx = p.cpx;
+  int maxtail = 0;
+  for (int x = 0; x < 8; ++x) maxtail = std::max(maxtail, xcd_plan(nwg, x, cpx).tail);
+  const int ktiles = (p.K + BK - 1) / BK;
+  if (maxtail == 0 || 2 * maxtail > cpx) return 0;
+  int s = std::min(4, cpx / maxtail);
+  while (s > 1 && ktiles / s < 8) --s;
+  if (s < 2) return 0;
+  const int kchunk = (((ktiles + s - 1) / s) + 1) & ~1;  // even: the loop body is two K-tiles
+  s = (ktiles + kchunk - 1) / kchunk;
+  if (s < 2 || 8L * maxtail * s * BM * BN * 4 > ws_bytes) return 0;
+  p.ksplit = s;
+  p.kchunk = kchunk;
+  p.tail_cap = maxtail;
+  int blocks = 0;
+  for (int x = 0; x < 8; ++x) {
+    const XPlan xp = xcd_plan(nwg, x, cpx);
+    blocks = std::max(blocks, xp.full + xp.tail * s);
+  }
+  return 8 * blocks;
+}
+
 extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
                        void* C2, long ldc2, const void* bias, int M, int N, int K, float beta, int H, int group_m,
-                       int variant, void* stream) {
+                       int variant, void* ws, long ws_bytes, void* stream) {
   using namespace pd::gm;
   if (M <= 0 || N <= 0 || K <= 0) return -1;
   if ((layout & 3) && K % 8) return -1;   // K-major operands move 16-B chunks along k
@@ -794,6 +922,7 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   p.M = M; p.N = N; p.K = K; p.beta = beta; p.H = H;
   p.zero = bias;  // ablation 7 only: the caller passes a zeroed buffer in `bias`
   p.goff = nullptr; p.ngroups = 0; p.gmode = 0; p.gsb = p.gsc = p.gsbias = 0;
+  p.part = (float*)ws; p.ksplit = 1; p.kchunk = 0; p.tail_cap = 0; p.cpx = cus_per_xcd();
   p.tiles_m = (M + BM - 1) / BM;
   p.tiles_n = epi == kEpiSwiGLU ? (H + 127) / 128 : (N + BN - 1) / BN;
   p.group_m = group_m > 0 ? group_m : 8;
@@ -803,11 +932,17 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   if (epi == kEpiSwiGLU && (bk || H % 32)) return -3;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(p.tiles_m * p.tiles_n);
-#define PD_GEMM_LAUNCH(AKV, BKV, EPIV)                              \
-  if (variant == 1) {                                                \
-    gemm_pp_kernel<AKV, BKV, EPIV><<<grid, NTHR, 0, st>>>(p);       \
-  } else {                                                           \
-    gemm_kernel<AKV, BKV, EPIV><<<grid, NTHR, 0, st>>>(p);          \
+  if (ws && variant == 0 && epi != kEpiSwiGLU) {
+    const int g = plan_splitk(p, ws_bytes);
+    if (g) grid = dim3(g);
+  }
+  const dim3 rgrid(BM * BN / 1024, 8 * p.tail_cap);
+#define PD_GEMM_LAUNCH(AKV, BKV, EPIV)                                          \
+  if (variant == 1) {                                                            \
+    gemm_pp_kernel<AKV, BKV, EPIV><<<grid, NTHR, 0, st>>>(p);                   \
+  } else {                                                                       \
+    gemm_kernel<AKV, BKV, EPIV><<<grid, NTHR, 0, st>>>(p);                      \
+    if (p.ksplit > 1) splitk_reduce_kernel<EPIV><<<rgrid, 256, 0, st>>>(p);     \
   }
   switch (epi * 4 + layout) {
     case 0 * 4 + 0: PD_GEMM_LAUNCH(false, false, kEpiBF16); break;
@@ -854,6 +989,7 @@ extern "C" int pd_gemm_grouped(int layout, int epi, const void* A, long lda, con
   p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldc2 = ldc2;
   p.N = N; p.beta = beta; p.H = H; p.zero = nullptr;
   p.goff = goff; p.ngroups = ngroups; p.gmode = gmode; p.gsb = gsb; p.gsc = gsc; p.gsbias = gsbias;
+  p.part = nullptr; p.ksplit = 1; p.kchunk = 0; p.tail_cap = 0; p.cpx = 32;
   p.group_m = group_m > 0 ? group_m : 8;
   p.tiles_n = epi == kEpiSwiGLU ? (H + 127) / 128 : (N + BN - 1) / BN;
   const bool ak = layout & 1, bk = (layout >> 1) & 1;

@@ -53,9 +53,28 @@ def supported_wgrad(x2, dy2):
     return x2.shape[1] % 8 == 0 and dy2.shape[1] % 8 == 0 and _ok2d(x2, x2.shape[1]) and _ok2d(dy2, dy2.shape[1])
 
 
+# tail split-K workspace (fp32 K-slice slabs of the last, partial wave's tiles; <= 8 XCDs x 32 CUs x 256 KiB),
+# one per (device, stream) so GEMMs on concurrent streams never share slabs; "0" disables the split
+SPLITK = os.environ.get("PADDLE2_AMD_GEMM_SPLITK", "1") != "0"
+_WS_BYTES = 64 << 20
+_WS = {}
+
+
+def _workspace(t):
+    if not SPLITK:
+        return 0, 0
+    st = torch.cuda.current_stream(t.device)
+    key = (t.device.index, st.cuda_stream)
+    ws = _WS.get(key)
+    if ws is None:
+        ws = _WS[key] = torch.empty(_WS_BYTES, dtype=torch.uint8, device=t.device)
+    return ws.data_ptr(), _WS_BYTES
+
+
 def _launch(layout, epi, a, lda, b, ldb, c, ldc, c2, ldc2, bias, M, Nn, K, beta=0.0, H=0):
+    ws, ws_bytes = _workspace(a) if epi != EPI_SWIGLU and VARIANT == 0 else (0, 0)
     N.native().gemm(layout, epi, a.data_ptr(), lda, b.data_ptr(), ldb, c.data_ptr(), ldc, N.ptr(c2), ldc2,
-                    N.ptr(bias), M, Nn, K, float(beta), H, GROUP_M, VARIANT, N.stream())
+                    N.ptr(bias), M, Nn, K, float(beta), H, GROUP_M, VARIANT, ws, ws_bytes, N.stream())
 
 
 def mm_fwd(x2, w, bias=None, out=None):
