@@ -121,7 +121,28 @@ class _NullCtx:
 
 
 name_scope = _NullCtx
-device_guard = _NullCtx
+
+
+class device_guard:
+    """paddle.static.device_guard (reference base/framework.py device_guard): ops recorded inside carry
+    ``op_device`` ("gpu:<pipeline stage>", "gpu:all"; "cpu" / bare "gpu" are accepted and recorded as
+    given) — HybridParallelInferenceHelper splits a program into pipeline stages by it."""
+
+    def __init__(self, device=None):
+        if device is not None and not (device in ("cpu", "gpu") or device.startswith("gpu:")):
+            raise ValueError(f"device_guard: expected 'cpu', 'gpu', 'gpu:<n>' or 'gpu:all', got {device!r}")
+        self.device = device
+
+    def __enter__(self):
+        self._prev = _g._state.op_device
+        _g._state.op_device = self.device
+        return self
+
+    def __exit__(self, *a):
+        _g._state.op_device = self._prev
+        return False
+
+
 scope_guard = _NullCtx
 ipu_shard_guard = _NullCtx
 

@@ -34,6 +34,7 @@ _ids = itertools.count(1)
 class _State:
     static = False          # paddle.enable_static()
     recording_off = 0       # >0 while computing meta shapes inside a recorded op
+    op_device = None        # static.device_guard: "gpu:<stage>" / "gpu:all" stamped on recorded ops
 
 
 _state = _State()
@@ -193,7 +194,8 @@ class Program:
 
         res = pytree.tree_map(wrap, out)
         if any(o is not None for o in outs):  # pure metadata queries (dim, shape, ...) are not ops
-            self.ops.append(Op(kind, fn, rargs, rkw, outs))
+            self.ops.append(Op(kind, fn, rargs, rkw, outs,
+                               {"op_device": _state.op_device} if _state.op_device else None))
         return res
 
     def append_special(self, kind, **attrs):

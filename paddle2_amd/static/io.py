@@ -71,7 +71,7 @@ def _prune(program, fetch_ids):
     for op in reversed(program.ops):
         if op.kind not in ("torch", "native"):
             continue
-        if any(o in need for o in op.outs if o is not None):
+        if op.attrs.get("side_effect") or any(o in need for o in op.outs if o is not None):
             keep.append(op)
             for x in pytree.tree_leaves((op.args, op.kwargs)):
                 if isinstance(x, VarRef):
