@@ -879,18 +879,24 @@ static int cus_per_xcd() {
   return cache[dev];
 }
 
-// Tail split-K plan: when an XCD's last wave would run at most half full, its tail tiles are cut into
-// ksplit K-slices (at least 8 K-tiles each) so that wave finishes ~ksplit times sooner.  Returns the grid
-// size (0 = no split).  Workspace: 8 * tail_cap * ksplit slabs of BM*BN fp32 (<= 8 * cpx * 256 KiB).
+// Tail split-K plan: an XCD's last, partial wave of `tail` tiles takes one full tile time; cut into s
+// K-slices (at least 8 K-tiles each) it takes ceil(tail*s / cpx) / s of one.  The smallest s (2..4) with the
+// shortest tail time wins if it saves at least 1/8 of a tile time and its slabs fit the workspace (8 *
+// tail_cap * s slabs of BM*BN fp32).  Returns the grid size (0 = no split).
 static int plan_splitk(pd::gm::Params& p, long ws_bytes) {
   using namespace pd::gm;
   const int nwg = p.tiles_m * p.tiles_n, cpx = p.cpx;
   int maxtail = 0;
   for (int x = 0; x < 8; ++x) maxtail = std::max(maxtail, xcd_plan(nwg, x, cpx).tail);
   const int ktiles = (p.K + BK - 1) / BK;
-  if (maxtail == 0 || 2 * maxtail > cpx) return 0;
-  int s = std::min(4, cpx / maxtail);
-  while (s > 1 && ktiles / s < 8) --s;
+  if (maxtail == 0) return 0;
+  int s = 1;
+  double best = 1.0;
+  for (int c = 2; c <= 4; ++c) {
+    if (ktiles / c < 8 || 8L * maxtail * c * BM * BN * 4 > ws_bytes) continue;
+    const double t = (double)((maxtail * c + cpx - 1) / cpx) / c;
+    if (t < best - 0.125) { best = t; s = c; }
+  }
   if (s < 2) return 0;
   const int kchunk = (((ktiles + s - 1) / s) + 1) & ~1;  // even: the loop body is two K-tiles
   s = (ktiles + kchunk - 1) / kchunk;

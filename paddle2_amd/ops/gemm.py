@@ -53,10 +53,11 @@ def supported_wgrad(x2, dy2):
     return x2.shape[1] % 8 == 0 and dy2.shape[1] % 8 == 0 and _ok2d(x2, x2.shape[1]) and _ok2d(dy2, dy2.shape[1])
 
 
-# tail split-K workspace (fp32 K-slice slabs of the last, partial wave's tiles; <= 8 XCDs x 32 CUs x 256 KiB),
-# one per (device, stream) so GEMMs on concurrent streams never share slabs; "0" disables the split
+# tail split-K workspace (fp32 K-slice slabs of the last, partial wave's tiles: 8 XCDs x tail x slices x 256 KiB;
+# 192 MiB covers a 24-tile tail in 4 slices), one per (device, stream) so GEMMs on concurrent streams never share
+# slabs; "0" disables the split
 SPLITK = os.environ.get("PADDLE2_AMD_GEMM_SPLITK", "1") != "0"
-_WS_BYTES = 64 << 20
+_WS_BYTES = 192 << 20
 _WS = {}
 
 
