@@ -62,7 +62,14 @@ class Group:
 
     @property
     def process_group(self):
-        return self.pg
+        """The reference's bound ProcessGroup surface (all_reduce / *_on_calc_stream / *_partial / ...)."""
+        if self.pg is None:
+            return None
+        if getattr(self, "_pg_obj", None) is None:
+            from .process_group import wrap
+
+            self._pg_obj = wrap(self.pg, gid=self.id)
+        return self._pg_obj
 
     @property
     def backend(self):
