@@ -69,6 +69,15 @@ def _find_units(model: Layer):
                 visit(child, inside_unit)
 
     visit(model, False)
+    # parameters the model also reads outside their own layer (tied input/output embeddings: GPT's logits use
+    # word_embeddings.weight) cannot be released after that layer's forward: their layers join the root unit,
+    # which stays gathered for the whole step
+    shared = getattr(model, "_sharding_root_params", None)
+    shared = shared() if callable(shared) else (shared or [])
+    if shared:
+        sid = {id(p) for p in shared}
+        units = [u for u in units if not any(id(p) in sid for p in u.parameters())]
+        claimed = {id(p) for u in units for p in u.parameters()}
     # anything still unclaimed (e.g. params registered on a container) forms a root unit
     rest = [p for p in model.parameters() if id(p) not in claimed]
     return units, rest

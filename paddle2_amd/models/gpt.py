@@ -239,6 +239,10 @@ class GPTForCausalLM(nn.Layer):
         if config.dtype in ("bfloat16", "float16"):
             self.to(dtype=config.dtype)
 
+    def _sharding_root_params(self):
+        """Stage-3 sharding: the tied word embedding is read again by the logits, outside its own layer."""
+        return [self.gpt.word_embeddings.weight] if self.lm_head is None else []
+
     def _logits(self, h):
         cfg = self.config
         if cfg.tensor_parallel_degree > 1:

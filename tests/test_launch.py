@@ -110,3 +110,17 @@ def test_bench_single_runs_sharding3_and_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"] + args, env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_bench_gpt_tied_embedding_under_stage3():
+    """GPT ties the logits to the word embedding: under stage-3 sharding that layer stays in the root unit
+    (gathered all step) instead of being released after the embedding forward."""
+    env = _env()
+    env.pop("WORLD_SIZE", None)
+    args = ["--model", "gpt3-1.3b", "--layers", "2", "--seq-len", "32", "--micro-batch", "1", "--steps", "1",
+            "--warmup", "1"]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _bench_json(r.stdout)
+    assert out["config"]["parallelism"] == "sharding3x1" and out["final_loss"] > 0
