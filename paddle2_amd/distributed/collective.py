@@ -63,12 +63,15 @@ class Group:
     @property
     def process_group(self):
         """The reference's bound ProcessGroup surface (all_reduce / *_on_calc_stream / *_partial / ...)."""
-        if self.pg is None:
+        pg = self.pg
+        if pg is None and dist.is_initialized() and self.nranks == dist.get_world_size():
+            pg = dist.group.WORLD   # the default group rides the world communicator
+        if pg is None:
             return None
         if getattr(self, "_pg_obj", None) is None:
             from .process_group import wrap
 
-            self._pg_obj = wrap(self.pg, gid=self.id)
+            self._pg_obj = wrap(pg, gid=self.id)
         return self._pg_obj
 
     @property
