@@ -20,10 +20,13 @@ from .stat import *  # noqa: F401,F403
 from ._helpers import ut
 from . import array  # noqa: E402
 from .array import *  # noqa: F401,F403
+from . import extra  # noqa: E402
+from .extra import *  # noqa: F401,F403
 from . import creation, linalg, logic, manipulation, math, random, search, stat  # noqa: F811 (re-bind after star imports)
 
 __all__ = sorted(set(creation.__all__ + linalg.__all__ + logic.__all__ + manipulation.__all__ + math.__all__ +
-                     random.__all__ + search.__all__ + stat.__all__ + array.__all__ + ["to_tensor", "Tensor"]))
+                     random.__all__ + search.__all__ + stat.__all__ + array.__all__ + extra.__all__ +
+                     ["to_tensor", "Tensor"]))
 
 _wrap = Tensor._wrap
 
@@ -34,10 +37,10 @@ _NOT_METHODS = {
     "gaussian", "randperm", "standard_normal", "create_tensor", "fill_constant", "complex", "polar",
     "einsum", "concat", "stack", "hstack", "vstack", "dstack", "column_stack", "row_stack",
     "broadcast_tensors", "broadcast_shape", "add_n", "multiplex", "cartesian_prod", "is_tensor",
-    "scatter_nd", "multi_dot", "where", "meshgrid", "shape", "rank", "tolist",
+    "scatter_nd", "multi_dot", "where", "meshgrid", "shape", "rank", "tolist", "block_diag", "log_normal",
 }
 
-_METHOD_SOURCES = (math, manipulation, linalg, logic, search, stat, random, creation)
+_METHOD_SOURCES = (math, manipulation, linalg, logic, search, stat, random, creation, extra)
 
 
 def _install_methods():
