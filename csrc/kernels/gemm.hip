@@ -862,6 +862,181 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Params p) {
   epilogue<EPI>(p, acc, tm, tn, wm * 128, wn * 64, wn, lane);
 }
 
+// ------------------------------------------------------------------------------------------------
+// v3: 4 waves (2 x 2), one wave per SIMD, 128x128 wave tiles (8 x 8 accumulators, 256 acc registers);
+// operands staged global -> VGPR -> LDS (buffer_load_dwordx4 one K-tile ahead, ds_write_b128) instead of
+// LDS-DMA.  Same 256x256x64 tile, the same swizzled LDS images (each lane stores the 16 B the DMA lane
+// of `lane_setup` would have landed, lane-linearly) and the same epilogues.  Rationale
+// (profiles/r2_gemm_native.md): v2 spends ~56 SIMD-cycles per 1-KiB LDS-DMA piece; a ds_write_b128 costs
+// ~13, and a 128x128 wave tile reads 1/3 less LDS per MFMA than 128x64.  Fragment reads are builtins (no
+// LDS-DMA is in flight, so the compiler's waitcnt tracking is exact); one barrier per K-tile.
+constexpr int NTHR3 = 256;
+#ifndef V3_NOSTAGE
+#define V3_NOSTAGE 0
+#endif
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4v lds_u32x4;
+typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8;
+
+template <bool KMAJ, int I>
+__device__ __forceinline__ u32x4v gld(const __amdgpu_buffer_rsrc_t& rs, const Ld& L, unsigned istride, bool full,
+                                      int krem) {
+  const bool ok = full || (KMAJ ? (((L.rmask >> I) & 1) && L.kl < krem) : (L.kl + 16 * I < krem));
+  const unsigned voff = (L.voff + I * istride) | ((unsigned)(!ok) << 31);
+  return __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
+}
+
+template <bool KMAJ, int U, int S>
+__device__ __forceinline__ bf16x8 frag3(lds_char* smem, const RdB<KMAJ>& r, unsigned soff) {
+  // soff: byte offset of the stage (runtime, wave-uniform), added once per read base
+  if constexpr (KMAJ) {
+    return *(const lds_bf16x8*)(smem + (r.b[S] + soff) + U * 16 * 128);
+  } else {
+    const unsigned a = r.b[0] + soff + (((unsigned)(r.f + U) ^ r.b[1]) << 5) + S * 16384;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + a));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + a + 2048));
+    return cat(lo, hi);
+  }
+}
+
+template <bool AK, bool BKM, int EPI>
+__global__ __launch_bounds__(NTHR3, 1) void gemm_v3_kernel(Params p) {
+  __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
+  lds_char* smem = (lds_char*)smem_raw;
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  int tm, tn;
+  tile_of(p, bid, tm, tn);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int Ncols = (EPI == kEpiSwiGLU) ? 2 * p.H : p.N;
+  const int nt = (((p.K + BK - 1) / BK) + 1) & ~1;
+
+  f32x4v acc[2][8][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  // each wave stages the pieces of DMA "waves" vw = wave and wave + 4
+  const Ld LA0 = lane_setup<AK, false, EPI>(p.lda, p.M, tm, p.H, wave, lane);
+  const Ld LA1 = lane_setup<AK, false, EPI>(p.lda, p.M, tm, p.H, wave + 4, lane);
+  const Ld LB0 = lane_setup<BKM, true, EPI>(p.ldb, Ncols, tn, p.H, wave, lane);
+  const Ld LB1 = lane_setup<BKM, true, EPI>(p.ldb, Ncols, tn, p.H, wave + 4, lane);
+  const long a_step = AK ? BK : (long)BK * p.lda;
+  const long b_step = BKM ? BK : (long)BK * p.ldb;
+  const unsigned short* a_t0 = AK ? p.A + (long)tm * BM * p.lda : p.A + (long)tm * BM;
+  const unsigned short* b_t0 = BKM ? p.B + (long)tn * BN * p.ldb : (EPI == kEpiSwiGLU ? p.B : p.B + (long)tn * BN);
+  const unsigned a_is = (unsigned)(AK ? 64 * p.lda * 2 : 16 * p.lda * 2);
+  const unsigned b_is = (unsigned)(BKM ? 64 * p.ldb * 2 : 16 * p.ldb * 2);
+  const bool a_rows_full = !AK || (tm + 1) * BM <= p.M;
+  const bool b_rows_full = !BKM || (tn + 1) * BN <= Ncols;
+
+  const int arow = wm * 128, bcolw = wn * 128;
+  const RdB<AK> ra = rd_setup<AK>(0, arow, lane);
+  const RdB<BKM> rb = rd_setup<BKM>(B_OFF, bcolw, lane);
+
+  u32x4v sa[8], sb[8];  // staged pieces: [I + 4*h] = instruction I of virtual wave wave + 4h
+  // piece k (0..15): operand k>>3 (A, B), virtual-wave half (k>>2)&1, instruction k&3
+  auto load1 = [&](auto Kc, const __amdgpu_buffer_rsrc_t& rsa, const __amdgpu_buffer_rsrc_t& rsb, bool fa, bool fb,
+                   int krem) {
+    constexpr int k = decltype(Kc)::value, i = k & 3, h = (k >> 2) & 1;
+    if constexpr (k < 8) sa[i + 4 * h] = gld<AK, i>(rsa, h ? LA1 : LA0, a_is, fa, krem);
+    else sb[i + 4 * h] = gld<BKM, i>(rsb, h ? LB1 : LB0, b_is, fb, krem);
+  };
+  auto store1 = [&](auto Kc, int st) {
+    constexpr int k = decltype(Kc)::value, i = k & 3, h = (k >> 2) & 1;
+    const int off = (k < 8 ? 0 : B_OFF) + st * TILE_BYTES + (8 * i + wave + 4 * h) * 1024 + lane * 16;
+    *(lds_u32x4*)(smem + off) = k < 8 ? sa[i + 4 * h] : sb[i + 4 * h];
+  };
+  struct TileSrc {
+    __amdgpu_buffer_rsrc_t ra, rb;
+    bool fa, fb;
+    int krem;
+  };
+  auto src = [&](int t) {
+    TileSrc o;
+    o.krem = p.K - t * BK;
+    o.ra = make_rsrc(a_t0 + a_step * t);
+    o.rb = make_rsrc(b_t0 + b_step * t);
+    o.fa = a_rows_full && o.krem >= BK;
+    o.fb = b_rows_full && o.krem >= BK;
+    return o;
+  };
+  auto sync = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+  // fragment sets: x = k32 step 0, y = step 1 (fixed names, never copied).  A fragment of the next set is
+  // read only once the register it replaces is dead (A row i dies after MFMA 8i+7, the B set after the
+  // step), so about one set plus a row is live, not two sets.
+  bf16x8 xa[8], xb[8], ya[8], yb[8];
+  auto rdA = [&](unsigned so, auto S, auto U, bf16x8 (&fa)[8]) {
+    fa[decltype(U)::value] = frag3<AK, decltype(U)::value, decltype(S)::value>(smem, ra, so);
+  };
+  auto rdB = [&](unsigned so, auto S, auto U, bf16x8 (&fb)[8]) {
+    fb[decltype(U)::value] = frag3<BKM, decltype(U)::value, decltype(S)::value>(smem, rb, so);
+  };
+  auto mm = [&](auto Q, const bf16x8 (&fa)[8], const bf16x8 (&fb)[8]) {
+    constexpr int q = decltype(Q)::value, i = q / 8, j = q % 8;
+    acc[j >> 2][i][j & 3] = mfma(fa[i], fb[j], acc[j >> 2][i][j & 3]);
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+
+  // prologue: tile 0 in stage 0 and its step-0 fragments (but xa[7]) read, tile 1 staged in registers
+  {
+    const TileSrc s0 = src(0);
+    sfor<16>([&](auto K) { load1(K, s0.ra, s0.rb, s0.fa, s0.fb, s0.krem); });
+    sfor<16>([&](auto K) { store1(K, 0); });
+    const TileSrc s1 = src(1);
+    sfor<16>([&](auto K) { load1(K, s1.ra, s1.rb, s1.fa, s1.fb, s1.krem); });
+    sync();
+    sfor<7>([&](auto U) { rdA(0u, C0{}, U, xa); });
+    sfor<8>([&](auto U) { rdB(0u, C0{}, U, xb); });
+  }
+
+  // One K-tile from stage ST.  Step 0 (set x): slot 0 reads xa[7]; slot 8i+8 reads ya[i] (i < 7); slots
+  // 56-63 read yb.  Step 1 (set y): slot 0 reads ya[7]; slots 1-16 store tile t+1 (staged a tile ago) into
+  // the other stage; 17-32 load tile t+2 into the staging registers; slot 40 syncs (stores landed, every
+  // read of this stage retired); 41-45, 48, 56 read tile t+1's xa[0..6]; 56-63 its xb.  Past K the range
+  // check turns loads into zeros, so the loop has no branches.
+  for (int t = 0; t < nt; ++t) {
+    const int st = t & 1;
+    const unsigned so = st * TILE_BYTES, sn_off = (st ^ 1) * TILE_BYTES;
+    sfor<64>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      mm(Q, xa, xb);
+      if constexpr (q == 0) rdA(so, C0{}, std::integral_constant<int, 7>{}, xa);
+      if constexpr (q >= 8 && q < 57 && q % 8 == 0) rdA(so, C1{}, std::integral_constant<int, q / 8 - 1>{}, ya);
+      if constexpr (q >= 56) rdB(so, C1{}, std::integral_constant<int, q - 56>{}, yb);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    const TileSrc sn = src(t + 2);
+    sfor<64>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      mm(Q, ya, yb);
+      if constexpr (q == 0) rdA(so, C1{}, std::integral_constant<int, 7>{}, ya);
+      if constexpr (q >= 1 && q <= 16 && !V3_NOSTAGE) store1(std::integral_constant<int, q - 1>{}, st ^ 1);
+      if constexpr (q >= 17 && q <= 32 && !V3_NOSTAGE)
+        load1(std::integral_constant<int, q - 17>{}, sn.ra, sn.rb, sn.fa, sn.fb, sn.krem);
+      if constexpr (q == 40) sync();
+      if constexpr (q >= 41 && q <= 45) rdA(sn_off, C0{}, std::integral_constant<int, q - 41>{}, xa);
+      if constexpr (q == 48) rdA(sn_off, C0{}, std::integral_constant<int, 5>{}, xa);
+      if constexpr (q == 56) rdA(sn_off, C0{}, std::integral_constant<int, 6>{}, xa);
+      if constexpr (q >= 56) rdB(sn_off, C0{}, std::integral_constant<int, q - 56>{}, xb);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+
+#pragma unroll
+  for (int h = 0; h < 2; ++h) epilogue<EPI>(p, acc[h], tm, tn, arow, bcolw + 64 * h, 2 * wn + h, lane);
+}
+
 }  // namespace gm
 }  // namespace pd
 
@@ -946,6 +1121,8 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
 #define PD_GEMM_LAUNCH(AKV, BKV, EPIV)                                          \
   if (variant == 1) {                                                            \
     gemm_pp_kernel<AKV, BKV, EPIV><<<grid, NTHR, 0, st>>>(p);                   \
+  } else if (variant == 3) {                                                     \
+    gemm_v3_kernel<AKV, BKV, EPIV><<<grid, NTHR3, 0, st>>>(p);                  \
   } else {                                                                       \
     gemm_kernel<AKV, BKV, EPIV><<<grid, NTHR, 0, st>>>(p);                      \
     if (p.ksplit > 1) splitk_reduce_kernel<EPIV><<<rgrid, 256, 0, st>>>(p);     \
