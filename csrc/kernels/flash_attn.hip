@@ -139,6 +139,7 @@ struct Ext {
   unsigned drop_seed;   // DROP: per-call seed (Paddle's seed/offset pair folded on the host)
   unsigned drop_thresh; // DROP: element dropped iff hash < p * 2^32
   float drop_rscale;    // DROP: 1 / (1 - p)
+  int dq_atomic;        // dense bwd: dQ partials fp32-atomically added into ONE zeroed slab (pslab = 0)
 };
 
 // Counter-based dropout mask: a stateless 32-bit hash of (seed, batch*head, query, key), so the backward
@@ -772,16 +773,25 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16*
         const int hqd4 = Hq * D * 4;
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(dQs + (long)q0 * Hq * D + (long)hq * D, BMQ * hqd4);
         const int vo = 4 * h * hqd4 + (dsl * 32 + r) * 4;
+        if (ex.dq_atomic) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dq[i] * scale), rs, vo,
-                                                ((i & 3) + 8 * (i >> 2)) * hqd4, 2);
+          for (int i = 0; i < 16; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dq[i] * scale, rs, vo, ((i & 3) + 8 * (i >> 2)) * hqd4, 0);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dq[i] * scale), rs, vo,
+                                                  ((i & 3) + 8 * (i >> 2)) * hqd4, 2);
+        }
       } else {
         float* dqh = dQs + (long)hq * D + dsl * 32 + r;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int q = q0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (q < Sq) __builtin_nontemporal_store(dq[i] * scale, dqh + (long)q * Hq * D);
+          if (q < Sq) {
+            if (ex.dq_atomic) unsafeAtomicAdd(dqh + (long)q * Hq * D, dq[i] * scale);
+            else __builtin_nontemporal_store(dq[i] * scale, dqh + (long)q * Hq * D);
+          }
         }
       }
     }
@@ -923,6 +933,15 @@ int check_args(int dt, int D, int Hq, int Hk, int mode, int drop, float pdrop, c
 
 }  // namespace
 
+// Dense backward dQ accumulation: fp32 atomics into one slab (default; the reference's flash bwd is likewise
+// not bit-reproducible) or, with PADDLE2_AMD_FA_DQ_ATOMIC=0 (set by FLAGS_cudnn_deterministic), per-key-block
+// slabs summed in a fixed order.  Read per call: the Python side sizes the workspace by the same rule.
+static bool fa_dq_atomic() {
+  const char* e = getenv("PADDLE2_AMD_FA_DQ_ATOMIC");
+  return e ? atoi(e) != 0 : true;
+}
+extern "C" int pd_flash_dq_atomic() { return fa_dq_atomic() ? 1 : 0; }
+
 // Key-block width of the backward (rows of the dQ partial slabs): 256 keys for D <= 128, 128 for D = 256.
 extern "C" int pd_flash_bwd_block(int D) { return D > 128 ? 128 : 256; }
 
@@ -958,7 +977,7 @@ extern "C" int pd_flash_fwd(int dt, const void* q, const void* k, const void* v,
 }
 
 // dqp: fp32 workspace of nkb * rows*Hq*D floats (nkb = ceil(Sk / pd_flash_bwd_block(D)), rows = B*Sq, or total_q
-// for varlen) for per-key-block dQ partials (need not be zeroed); delta a [B, Hq, Sq] ([Hq, total_q] varlen) fp32
+// for varlen) for per-key-block dQ partials (need not be zeroed; ONE slab for dense mode when pd_flash_dq_atomic()); delta a [B, Hq, Sq] ([Hq, total_q] varlen) fp32
 // workspace.  q/k/v/o/dout and dq/dk/dv may all be row-strided views ([B, S, H, D] with token strides), e.g. slices
 // of one fused QKV / dQKV buffer.
 extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void* v, const void* o, const void* dout,
@@ -982,10 +1001,15 @@ extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void
     fa::bwd_delta_kernel<false><<<dgrid, 256, 0, st>>>((const bf16*)o, (const bf16*)dout, delta, dB, dS, Hq, D, so);
   const int BNK = pd_flash_bwd_block(D);
   const int nkb = (Sk + BNK - 1) / BNK;
-  const long pslab = nrows * Hq * D;
+  // dense mode, atomic dQ: every key block adds into one zeroed fp32 slab (one slab of workspace, a convert
+  // pass instead of the slab reduce: 0.27 ms less per B8 S4096 H32 D128 layer)
+  const bool atomic = mode == 0 && fa_dq_atomic();
+  const long pslab = atomic ? 0 : nrows * Hq * D;
+  if (atomic) hipMemsetAsync(dqp, 0, nrows * Hq * D * sizeof(float), st);
   dim3 grid(nkb * Hk * B);
   fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm, seed,
-             drop ? (unsigned)fminf(pdrop * 4294967296.f, 4294967040.f) : 0u, drop ? 1.f / (1.f - pdrop) : 1.f};
+             drop ? (unsigned)fminf(pdrop * 4294967296.f, 4294967040.f) : 0u, drop ? 1.f / (1.f - pdrop) : 1.f,
+             atomic ? 1 : 0};
 #define PD_BWD(DD, FF)                                                                                              \
   launch_bwd<DD, FF>(grid, st, q, k, v, dout, lse, delta, dqp, dk, dv, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, sdk, sdv, \
                      pslab, scale, causal, mode, drop, ex)
@@ -997,8 +1021,8 @@ extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void
   long g = (work + 255) / 256;
   if (g > 8192) g = 8192;
 #define PD_DQR(MM, FF)                                                                                             \
-  fa::dq_reduce_kernel<MM, FF><<<(int)g, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, D, nkb, pslab, sdq, causal, \
-                                                       Sk - Sq, BNK, ex)
+  fa::dq_reduce_kernel<MM, FF><<<(int)g, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, D, atomic ? 1 : nkb, pslab, sdq, \
+                                                       atomic ? 0 : causal, Sk - Sq, BNK, ex)
   if (mode == 2) { if (f16) PD_DQR(fa::kMask, true); else PD_DQR(fa::kMask, false); }
   else if (mode == 1) { if (f16) PD_DQR(fa::kVarlen, true); else PD_DQR(fa::kVarlen, false); }
   else { if (f16) PD_DQR(fa::kDense, true); else PD_DQR(fa::kDense, false); }

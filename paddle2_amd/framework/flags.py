@@ -5,7 +5,8 @@ Every reference flag name is registered with its reference default (``_flag_tabl
 framework's own.  The ones with an effect here:
 
   FLAGS_check_nan_inf / _level          NaN/Inf checker at Layer boundaries (framework/nan_inf.py)
-  FLAGS_cudnn_deterministic             deterministic MIOpen + torch deterministic algorithms (warn-only)
+  FLAGS_cudnn_deterministic             deterministic MIOpen + torch deterministic algorithms (warn-only);
+                                        flash-attention bwd sums dQ slabs in order (no fp32 atomics)
   FLAGS_embedding_deterministic         embedding backward through a sorted, atomics-free reduction
   FLAGS_fraction_of_gpu_memory_to_use   per-process cap of the caching allocator (set at device init)
   FLAGS_gpu_memory_limit_mb             absolute cap (MiB), wins over the fraction
@@ -106,6 +107,8 @@ def _alloc_conf():
 
 
 _alloc_conf()
+if _flags.get("FLAGS_cudnn_deterministic"):
+    os.environ.setdefault("PADDLE2_AMD_FA_DQ_ATOMIC", "0")
 if _flags.get("FLAGS_check_nan_inf"):
     from . import nan_inf as _ni  # noqa: E402
 
@@ -147,6 +150,7 @@ def _on_change(key):
         import torch
 
         on = bool(_flags[key])
+        os.environ["PADDLE2_AMD_FA_DQ_ATOMIC"] = "0" if on else "1"  # flash bwd: ordered dQ slab sum
         torch.backends.cudnn.deterministic = on
         torch.backends.cudnn.benchmark = False if on else torch.backends.cudnn.benchmark
         torch.use_deterministic_algorithms(on, warn_only=True)

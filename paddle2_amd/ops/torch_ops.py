@@ -879,13 +879,22 @@ def _flash_fwd_native(q, k, v, causal, scale):
     return out, lse
 
 
+def dq_atomic():
+    """Dense flash backward accumulates dQ with fp32 atomics into one slab unless PADDLE2_AMD_FA_DQ_ATOMIC=0
+    (FLAGS_cudnn_deterministic sets it): the workspace is sized by this rule, the kernel reads the same env."""
+    e = _os.environ.get("PADDLE2_AMD_FA_DQ_ATOMIC")
+    return True if e is None else int(e) != 0
+
+
 def _flash_bwd_native(q, k, v, out, do, lse, dq, dk, dv, scale, causal):
     """dq/dk/dv may be token-strided views (e.g. slices of a dQKV buffer)."""
     B, Sq, Hq, D = q.shape
     Sk, Hk = k.shape[1], k.shape[2]
     bnk = _bwd_block(D)
     nkb = (Sk + bnk - 1) // bnk
-    dq32 = torch.empty(nkb * B * Sq * Hq * D, dtype=torch.float32, device=q.device)  # per-key-block dQ partials
+    # per-key-block dQ partials, or one atomically accumulated slab (same rule as fa_dq_atomic in flash_attn.hip)
+    slabs = 1 if dq_atomic() else nkb
+    dq32 = torch.empty(slabs * B * Sq * Hq * D, dtype=torch.float32, device=q.device)
     delta = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
     N.native().flash_bwd(_ATTN_DT[q.dtype], q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), do.data_ptr(), lse.data_ptr(),
                          delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dq32.data_ptr(), B, Sq, Sk,
@@ -1095,7 +1104,8 @@ class _FlashExtFn(torch.autograd.Function):
         nrows = q.shape[0] if mode == _MODE_VARLEN else B * Sq
         bnk = _bwd_block(D)
         nkb = (Sk + bnk - 1) // bnk
-        dq32 = torch.empty(nkb * nrows * Hq * D, dtype=torch.float32, device=q.device)
+        slabs = 1 if (mode == _MODE_DENSE and dq_atomic()) else nkb  # the kernel's fa_dq_atomic rule
+        dq32 = torch.empty(slabs * nrows * Hq * D, dtype=torch.float32, device=q.device)
         delta = torch.empty_like(lse)
         N.native().flash_bwd_ext(_ATTN_DT[q.dtype], q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), do.data_ptr(),
                                  lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
