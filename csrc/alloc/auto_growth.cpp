@@ -14,6 +14,11 @@
 //     stream itself.  Once a second stream has been seen, every free also records a HIP event, and a block is
 //     handed to a different stream only after its event completed (hipEventQuery) — no host sync, no
 //     cross-stream hazard;
+//   * record_stream (stream_safe_cuda_allocator.cc RecordStream): a live block can be marked as used by other
+//     streams (torch's Tensor.record_stream reaches pd_alloc_record_stream through the pluggable allocator's
+//     record-stream hook).  Freeing such a block records an event on every one of those streams and on the
+//     freeing stream and parks the block on a deferred list; it re-enters the free index only once all of its
+//     events completed (polled, never waited for, at the next allocation);
 //   * limit: an optional byte cap (FLAGS_fraction_of_gpu_memory_to_use / FLAGS_gpu_memory_limit_mb); on a
 //     failed growth the cache of fully-free chunks is released and the growth retried once.
 // Thread-safe (one mutex per device).  C ABI for ctypes; no Python dependency, loads on CPU-only machines.
@@ -50,6 +55,14 @@ struct Block {
   Block* prev;
   Block* next;
   std::multimap<size_t, Block*>::iterator pos;  // position in the free index (valid when free)
+  std::vector<hipStream_t> uses;                 // other streams recorded on the live block (record_stream)
+};
+
+// a freed block still in use by recorded streams: re-indexed once every event completed
+struct Deferred {
+  Block* b;
+  hipStream_t stream;             // freeing stream
+  std::vector<hipEvent_t> events;
 };
 
 struct Chunk {
@@ -62,6 +75,7 @@ struct Stats {
   uint64_t allocated = 0, reserved = 0, peak_allocated = 0, peak_reserved = 0;
   uint64_t num_allocs = 0, num_frees = 0, num_chunks = 0, num_grow = 0, num_oom_retries = 0;
   uint64_t cross_stream_reuse = 0;
+  uint64_t record_stream = 0, deferred_frees = 0;
 };
 
 struct Device {
@@ -70,6 +84,7 @@ struct Device {
   std::unordered_map<void*, Block*> live;
   std::vector<Chunk*> chunks;
   std::vector<hipEvent_t> event_pool;
+  std::vector<Deferred> deferred;
   hipStream_t first_stream = nullptr;
   bool seen_stream = false;
   bool multi_stream = false;
@@ -92,6 +107,8 @@ static uint64_t g_limit_bytes = 0;   // 0 = unlimited
 static std::mutex g_cfg_mu;
 
 static inline size_t round_up(size_t n, size_t a) { return (n + a - 1) / a * a; }
+
+static void process_deferred(Device& d);
 
 static hipEvent_t take_event(Device& d) {
   if (!d.event_pool.empty()) {
@@ -153,7 +170,7 @@ static Block* carve(Device& d, Block* b, size_t size, hipStream_t stream) {
   b->event_pending = false;
   if (b->size - size >= kMinSplit) {
     // the remainder stays "freed on b's stream" and keeps its fence for other streams
-    Block* rest = new Block{b->ptr + size, b->size - size, 0, true, b->stream, ev, pending, b->chunk, b, b->next, {}};
+    Block* rest = new Block{b->ptr + size, b->size - size, 0, true, b->stream, ev, pending, b->chunk, b, b->next, {}, {}};
     ev = nullptr;
     if (b->next) b->next->prev = rest;
     b->next = rest;
@@ -185,7 +202,7 @@ static bool grow(Device& d, int dev, size_t size, hipStream_t stream) {
     return false;
   }
   Chunk* c = new Chunk{static_cast<char*>(p), bytes, nullptr};
-  Block* b = new Block{c->base, bytes, 0, true, stream, nullptr, false, c, nullptr, nullptr, {}};
+  Block* b = new Block{c->base, bytes, 0, true, stream, nullptr, false, c, nullptr, nullptr, {}, {}};
   c->head = b;
   d.chunks.push_back(c);
   index_free(d, b);
@@ -221,6 +238,14 @@ static void coalesce_settled(Device& d) {
 // return every chunk whose blocks are all free to the driver; caller holds the lock
 static uint64_t release_free_chunks(Device& d, int dev) {
   uint64_t released = 0;
+  if (!d.deferred.empty()) {  // settle deferred frees first (their streams' work is done after a device sync)
+    int prev = -1;
+    hipGetDevice(&prev);
+    if (prev != dev) hipSetDevice(dev);
+    hipDeviceSynchronize();
+    if (prev != dev) hipSetDevice(prev);
+    process_deferred(d);
+  }
   std::vector<Chunk*> keep;
   bool synced = false;
   for (Chunk* c : d.chunks) {
@@ -275,6 +300,7 @@ static void* do_alloc(size_t size, int dev, hipStream_t stream) {
     d.multi_stream = true;
     hipDeviceSynchronize();
   }
+  if (!d.deferred.empty()) process_deferred(d);
   size_t need = round_up((size ? size : 1) + g_guard, kAlign);
   Block* b = find_fit(d, need, stream);
   if (!b) {
@@ -298,6 +324,66 @@ static void* do_alloc(size_t size, int dev, hipStream_t stream) {
   d.st.num_allocs++;
   if (d.st.allocated > d.st.peak_allocated) d.st.peak_allocated = d.st.allocated;
   return b->ptr;
+}
+
+// b (no longer live) becomes a free block freed on `stream`; `settled`: every use of it has completed (a deferred
+// free whose events all fired), so it needs no fence.  Coalesces with free neighbours; caller holds the lock.
+static void finish_free(Device& d, Block* b, hipStream_t stream, bool settled) {
+  b->stream = stream;
+  b->uses.clear();
+  if (d.multi_stream && !settled) {
+    b->event = take_event(d);
+    if (b->event && hipEventRecord(b->event, stream) == hipSuccess) {
+      b->event_pending = true;
+    } else {
+      give_event(d, b->event);
+      b->event = nullptr;
+      hipStreamSynchronize(stream);  // could not fence: make the block safe the slow way
+    }
+  }
+  // coalesce with free neighbours that are either from the same stream (b's newer fence covers their earlier
+  // work) or already fenced complete (safe for anyone): the merged block carries b's stream and fence
+  Block* p = b->prev;
+  if (p && p->free && (p->stream == b->stream || fence_done(d, p)) && (!settled || fence_done(d, p))) {
+    unindex_free(d, p);
+    give_event(d, p->event);
+    p->size += b->size;
+    p->next = b->next;
+    if (b->next) b->next->prev = p;
+    p->event = b->event;
+    p->event_pending = b->event_pending;
+    delete b;
+    b = p;
+  }
+  Block* n = b->next;
+  if (n && n->free && (n->stream == b->stream || fence_done(d, n)) && (!settled || fence_done(d, n))) {
+    unindex_free(d, n);
+    give_event(d, n->event);
+    b->size += n->size;
+    b->next = n->next;
+    if (n->next) n->next->prev = b;
+    delete n;
+  }
+  if (b->prev == nullptr) b->chunk->head = b;
+  index_free(d, b);
+}
+
+// re-index deferred frees whose recorded-stream events have all completed; caller holds the lock
+static void process_deferred(Device& d) {
+  size_t keep = 0;
+  for (size_t i = 0; i < d.deferred.size(); ++i) {
+    Deferred& f = d.deferred[i];
+    bool done = true;
+    for (hipEvent_t e : f.events) done = done && hipEventQuery(e) == hipSuccess;
+    if (!done) {
+      if (keep != i) d.deferred[keep] = std::move(f);
+      ++keep;
+      continue;
+    }
+    for (hipEvent_t e : f.events) give_event(d, e);
+    finish_free(d, f.b, f.stream, /*settled=*/true);
+  }
+  d.deferred.resize(keep);
 }
 
 static void do_free(void* ptr, int dev, hipStream_t stream) {
@@ -328,42 +414,54 @@ static void do_free(void* ptr, int dev, hipStream_t stream) {
   }
   d.st.allocated -= b->size;
   d.st.num_frees++;
-  b->stream = stream;
-  if (d.multi_stream) {
-    b->event = take_event(d);
-    if (b->event && hipEventRecord(b->event, stream) == hipSuccess) {
-      b->event_pending = true;
-    } else {
-      give_event(d, b->event);
-      b->event = nullptr;
-      hipStreamSynchronize(stream);  // could not fence: make the block safe the slow way
+  if (!b->uses.empty()) {
+    // used by other streams: fence every one of them (and the freeing stream), re-index when all have passed
+    Deferred f{b, stream, {}};
+    bool ok = true;
+    for (size_t i = 0; i <= b->uses.size() && ok; ++i) {
+      hipStream_t s = i < b->uses.size() ? b->uses[i] : stream;
+      hipEvent_t e = take_event(d);
+      if (!e || hipEventRecord(e, s) != hipSuccess) {
+        give_event(d, e);
+        ok = false;
+        break;
+      }
+      f.events.push_back(e);
     }
+    if (ok) {
+      d.st.deferred_frees++;
+      d.deferred.push_back(std::move(f));
+      return;
+    }
+    for (hipEvent_t e : f.events) give_event(d, e);  // could not fence: settle the slow way
+    for (hipStream_t s : b->uses) hipStreamSynchronize(s);
+    hipStreamSynchronize(stream);
+    finish_free(d, b, stream, /*settled=*/true);
+    return;
   }
-  // coalesce with free neighbours that are either from the same stream (b's newer fence covers their earlier
-  // work) or already fenced complete (safe for anyone): the merged block carries b's stream and fence
-  Block* p = b->prev;
-  if (p && p->free && (p->stream == b->stream || fence_done(d, p))) {
-    unindex_free(d, p);
-    give_event(d, p->event);
-    p->size += b->size;
-    p->next = b->next;
-    if (b->next) b->next->prev = p;
-    p->event = b->event;
-    p->event_pending = b->event_pending;
-    delete b;
-    b = p;
+  finish_free(d, b, stream, /*settled=*/false);
+}
+
+// Tensor.record_stream: the live block holding `ptr` is also used by `stream`
+static void do_record_stream(void* ptr, hipStream_t stream) {
+  for (int dev = 0; dev < kMaxDevices; ++dev) {
+    Device& d = g_dev[dev];
+    if (!d.seen_stream) continue;
+    std::lock_guard<std::mutex> lk(d.mu);
+    auto it = d.live.find(ptr);
+    if (it == d.live.end()) continue;
+    Block* b = it->second;
+    if (stream == b->stream) return;
+    for (hipStream_t s : b->uses)
+      if (s == stream) return;
+    b->uses.push_back(stream);
+    d.st.record_stream++;
+    if (!d.multi_stream) {  // blocks freed so far carry no fence: settle once (as for a second allocating stream)
+      d.multi_stream = true;
+      hipDeviceSynchronize();
+    }
+    return;
   }
-  Block* n = b->next;
-  if (n && n->free && (n->stream == b->stream || fence_done(d, n))) {
-    unindex_free(d, n);
-    give_event(d, n->event);
-    b->size += n->size;
-    b->next = n->next;
-    if (n->next) n->next->prev = b;
-    delete n;
-  }
-  if (b->prev == nullptr) b->chunk->head = b;
-  index_free(d, b);
 }
 
 }  // namespace alloc
@@ -377,6 +475,8 @@ extern "C" {
 void* pd_alloc_malloc(size_t size, int device, hipStream_t stream) { return do_alloc(size, device, stream); }
 
 void pd_alloc_free(void* ptr, size_t /*size*/, int device, hipStream_t stream) { do_free(ptr, device, stream); }
+
+void pd_alloc_record_stream(void* ptr, hipStream_t stream) { do_record_stream(ptr, stream); }
 
 void pd_alloc_debug(uint64_t guard_bytes, int canary) {
   std::lock_guard<std::mutex> lk(g_cfg_mu);
@@ -403,15 +503,16 @@ void pd_alloc_configure(uint64_t chunk_bytes, uint64_t limit_bytes) {
   g_limit_bytes = limit_bytes;
 }
 
-// out[0..9] = allocated, reserved, peak_allocated, peak_reserved, num_allocs, num_frees, num_chunks,
-//             num_grow, num_oom_retries, cross_stream_reuse
+// out[0..12] = allocated, reserved, peak_allocated, peak_reserved, num_allocs, num_frees, num_chunks,
+//              num_grow, num_oom_retries, cross_stream_reuse, record_stream, deferred_frees, deferred_pending
 void pd_alloc_stats(int device, uint64_t* out) {
   if (device < 0 || device >= kMaxDevices) return;
   Device& d = g_dev[device];
   std::lock_guard<std::mutex> lk(d.mu);
   const Stats& s = d.st;
-  uint64_t v[10] = {s.allocated, s.reserved, s.peak_allocated, s.peak_reserved, s.num_allocs,
-                    s.num_frees, s.num_chunks, s.num_grow, s.num_oom_retries, s.cross_stream_reuse};
+  uint64_t v[13] = {s.allocated, s.reserved, s.peak_allocated, s.peak_reserved, s.num_allocs,
+                    s.num_frees, s.num_chunks, s.num_grow, s.num_oom_retries, s.cross_stream_reuse,
+                    s.record_stream, s.deferred_frees, (uint64_t)d.deferred.size()};
   std::memcpy(out, v, sizeof(v));
 }
 

@@ -16,6 +16,7 @@ typedef struct FakeStream* hipStream_t;
 extern "C" {
 void* pd_alloc_malloc(size_t size, int device, hipStream_t stream);
 void pd_alloc_free(void* ptr, size_t size, int device, hipStream_t stream);
+void pd_alloc_record_stream(void* ptr, hipStream_t stream);
 void pd_alloc_configure(uint64_t chunk_bytes, uint64_t limit_bytes);
 void pd_alloc_stats(int device, uint64_t* out);
 uint64_t pd_alloc_empty_cache(int device);
@@ -53,6 +54,8 @@ static void worker(int tid, int iters) {
       if (reinterpret_cast<uintptr_t>(p) % 256 != 0) { g_errors++; std::fprintf(stderr, "misaligned\n"); }
       unsigned char tag = static_cast<unsigned char>(1 + rng() % 250);
       std::memset(p, tag, n);
+      if (rng() % 8 == 0)  // also "used" on another thread's stream: its free is deferred behind that stream
+        pd_alloc_record_stream(p, reinterpret_cast<hipStream_t>(uintptr_t(0x1000 + ((tid + 1) % 4) * 0x10)));
       live.push_back({p, n, tag, stream});
     } else if (op < 9) {
       size_t k = rng() % live.size();
@@ -95,7 +98,7 @@ int main(int argc, char** argv) {
     if (!check(l)) g_errors++;
     pd_alloc_free(l.p, l.n, 0, l.s);
   }
-  uint64_t st[10];
+  uint64_t st[13];
   pd_alloc_stats(0, st);
   if (st[0] != 0) { std::fprintf(stderr, "leaked %llu bytes\n", (unsigned long long)st[0]); g_errors++; }
   if (st[4] != st[5]) { std::fprintf(stderr, "allocs %llu != frees %llu\n", (unsigned long long)st[4],
@@ -104,7 +107,8 @@ int main(int argc, char** argv) {
   pd_alloc_stats(0, st);
   if (st[1] != 0 || released == 0) { std::fprintf(stderr, "empty_cache left %llu reserved\n",
                                                   (unsigned long long)st[1]); g_errors++; }
-  std::printf("allocs=%llu chunks_peak_reserved=%llu cross_stream_reuse=%llu errors=%d\n",
-              (unsigned long long)st[4], (unsigned long long)st[3], (unsigned long long)st[9], g_errors.load());
+  std::printf("allocs=%llu chunks_peak_reserved=%llu cross_stream_reuse=%llu record_stream=%llu deferred=%llu errors=%d\n",
+              (unsigned long long)st[4], (unsigned long long)st[3], (unsigned long long)st[9],
+              (unsigned long long)st[10], (unsigned long long)st[11], g_errors.load());
   return g_errors.load() ? 1 : 0;
 }

@@ -82,6 +82,9 @@ struct Params {
   // splitk_reduce_kernel sums the slices in order into C.  cpx = CUs (= workgroup slots) per XCD.
   float* part;
   int ksplit, kchunk, tail_cap, cpx;
+  // one past the last byte of each operand (v4: the buffer descriptors' num_records), null = unbounded
+  const void* a_end;
+  const void* b_end;
 };
 
 // Tiles [t0, t0 + n) of the grouped order belong to XCD x (the chunking xcd_remap uses); the first `full`
@@ -157,6 +160,11 @@ __device__ __forceinline__ int hsw(int k) { return (k & 3) | (((k >> 3) & 1) << 
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, kRecords, 0x00020000);
+}
+// descriptor whose range check stops at `nbytes` past `base` (clamped to [0, 2^31 - 1]; 0 = every load is 0)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_n(const void* base, long nbytes) {
+  const int n = (int)(nbytes < 0 ? 0L : (nbytes > (long)kRecords ? (long)kRecords : nbytes));
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, n, 0x00020000);
 }
 
 // Column remap of the B operand for the SwiGLU epilogue: tile column c (0..255) of output tile tn
@@ -263,6 +271,11 @@ __device__ __forceinline__ void sync_frags() {
 
 __device__ __forceinline__ f32x4v mfma(bf16x8 a, bf16x8 b, f32x4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// D = A.B + D with D pinned to AGPRs (v4); see the note at its use
+__device__ __forceinline__ void mfma_agpr(f32x4v& c, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
@@ -596,318 +609,54 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(Params p) {
   }
 }
 
-// ================================================================================================
-// Ping-pong variant.  The two wave groups (G0 = waves 0-3, A rows 0-127; G1 = waves 4-7, rows
-// 128-255) run one barrier apart: G1 executes one extra s_barrier first (G0 one at the end), so while
-// one group runs a 16-MFMA cluster (C slot) the other issues its LDS-DMA pieces and fragment reads
-// (M slot) — on every SIMD, which hosts one wave of each group, the MFMA pipe is fed by one wave while
-// the other pays the LDS-DMA issue cost (~60 cycles per 1-KiB piece).
-//   per K-tile and wave: 4 quadrants Q1 (A0,B0) Q2 (A0,B1) Q3 (A1,B1) Q4 (A1,B0), each = M slot
-//   [vmcnt(6); 2 DMA pieces; reads for Q] barrier, C slot [lgkmcnt(0); 16 MFMA] barrier.
-// LDS: each stage is split into 4 x 16 KiB "parts" (A0 = the A0 rows of both groups, A1, B0, B1), laid
-// out part-major [A0s0 A0s1 A1s0 A1s1 B0s0 B0s1 B1s0 B1s1] so every read address is a base VGPR + a
-// 16-bit immediate.  A part is refilled with tile t+2 as soon as both groups have read it in tile t:
-//   G0 M slots: Q1 B1(t+1)  Q2 A1(t+1)  Q3 A0(t+2)  Q4 B0(t+2)      (its 8 of each part's 16 pieces)
-//   G1 M slots: Q1 A1(t+1)  Q2 A0(t+2)  Q3 B0(t+2)  Q4 B1(t+2)
-// so every piece has 4 own M slots (8 slots ~ one K-tile of MFMA time) to land: vmcnt(6) at each M slot
-// retires the pieces issued 4 M slots earlier, one barrier before any group reads them.
-// Part images: K-major [128 part rows][64 k] (128-B rows, chunk ^ ((r>>1)&7)); MN-major [64 k][128 part
-// columns] (256-B rows, 32-B pair ^ hsw(k)) — both conflict-free for the fragment reads.
-namespace ppk {
-constexpr int PART = 16384;
-constexpr int B_REG = 4 * PART;  // B parts start at 64 KiB
-
-__device__ __forceinline__ constexpr int poff(int part, int st) { return (part * 2 + st) * PART; }
-
-// part-local index (0..127) of an operand part -> tile row (A) / tile column (B) (0..255)
-__device__ __forceinline__ int a_part_row(int part, int pr) { return (pr & 63) + (pr >> 6) * 128 + part * 64; }
-__device__ __forceinline__ int b_part_col(int part, int pc) { return (pc >> 5) * 64 + (pc & 31) + part * 32; }
-
-// Per-lane DMA source offsets of one operand: [part 0/1][piece parity e].  Group g issues pieces
-// j = 8g + 2w + e (w = wave in group) of every part; a piece is 8 part rows (K-major) or 4 k rows (MN).
-struct Ldp {
-  unsigned voff[2][2];
-  int kl[2];  // K-major: lane's first k (per parity); MN-major: lane's k (per parity)
-};
-
-template <bool KMAJ, bool ISB, int EPI>
-__device__ __forceinline__ Ldp lane_setup(long ld, int R, int t0, int H, int g, int w, int lane) {
-  Ldp o;
-#pragma unroll
-  for (int part = 0; part < 2; ++part)
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int j = 8 * g + 2 * w + e;
-      if constexpr (KMAJ) {
-        const int pr = 8 * j + (lane >> 3);
-        const int lc = (lane & 7) ^ ((pr >> 1) & 7);
-        const int tr = ISB ? b_part_col(part, pr) : a_part_row(part, pr);   // tile row / col
-        const int gr = ISB ? bcol<EPI>(t0, tr, H) : t0 * BM + tr;
-        const int r0 = ISB ? (EPI == kEpiSwiGLU ? 0 : t0 * BN) : t0 * BM;
-        o.kl[e] = lc * 8;
-        o.voff[part][e] = (unsigned)(((long)(gr - r0) * ld + lc * 8) * 2) | ((unsigned)(gr >= R) << 31);
-      } else {
-        const int k = 4 * j + (lane >> 4);
-        const int pch = lane & 15;
-        const int lch = (((pch >> 1) ^ hsw(k)) << 1) | (pch & 1);
-        const int pc = lch * 8;  // first part column of the 16-B chunk
-        const int tc = ISB ? b_part_col(part, pc) : a_part_row(part, pc);
-        const int gc = ISB ? bcol<EPI>(t0, tc, H) : t0 * BM + tc;
-        const int c0 = ISB ? (EPI == kEpiSwiGLU ? 0 : t0 * BN) : t0 * BM;
-        o.kl[e] = k;
-        o.voff[part][e] = (unsigned)(((long)k * ld + (gc - c0)) * 2) | ((unsigned)(gc >= R) << 31);
-      }
-    }
-  return o;
-}
-
-// Per-lane fragment-read bases (region-relative, stage 0, part 0) of one operand
-//  K-major: b[s] (k32 step s) for part row first + (lane&15); tile u of the wave adds u*16*128.
-//  MN-major: b[0] = x (row/offset part), b[1] = h (pair swizzle); pair = (T ^ h) for 16-col tile T.
-struct Rdp {
-  unsigned b[2];
-  int f;  // MN-major: first 16-column tile (part-local) of the wave
-};
-
-template <bool KMAJ>
-__device__ __forceinline__ Rdp rd_setup(unsigned region, int first, int lane) {
-  Rdp o;
-  if constexpr (KMAJ) {
-    const int rl = lane & 15;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int ch = (4 * s + (lane >> 4)) ^ ((rl >> 1) & 7);
-      o.b[s] = region + (first + rl) * 128 + ch * 16;
-    }
-    o.f = 0;
-  } else {
-    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-    o.b[0] = region + (8 * g + q) * 256 + (pp >> 1) * 16 + (pp & 1) * 8;
-    o.b[1] = q | ((g & 1) << 2);
-    o.f = first >> 4;
-  }
-  return o;
-}
-
-template <bool KMAJ, int U, int S, int PART_, int ST>
-__device__ __forceinline__ bf16x8 read_frag(const Rdp& r) {
-  constexpr int base = poff(PART_, ST);
-  if constexpr (KMAJ) {
-    return rd128<base + U * 16 * 128>(r.b[S]);
-  } else {
-    unsigned h = r.b[1];
-    asm volatile("" : "+v"(h));  // keep the per-read XOR in the loop (no hoisted per-tile bases)
-    const unsigned a = r.b[0] + (((unsigned)(r.f + U) ^ h) << 5);
-    return cat(rdtr<base + S * 8192>(a), rdtr<base + S * 8192 + 1024>(a));
-  }
-}
-}  // namespace ppk
+// ------------------------------------------------------------------------------------------------
+// v4: 4 waves (2 x 2), one wave per SIMD (512-register budget: the 8x8 accumulator grid of a 128x128
+// wave tile lives in the 256 AGPRs), LDS-DMA staging, and a K-tile's COMPLETE fragment set held in
+// VGPRs (2 k32 steps x (8 A + 8 B) fragments = 128 VGPRs) so a stage is released a quarter of the way
+// into the tile.  Per K-tile and wave:
+//   step 0 (64 MFMAs): the step-1 fragments are read behind MFMAs 0-15; after MFMA 23 lgkmcnt(0) +
+//     barrier (every wave has its reads of this stage) and the 16 LDS-DMA pieces of tile t+2 are
+//     streamed into the freed stage one per 5 MFMAs (MFMAs 24-99: a piece's ~60-cycle issue cost hides
+//     under 80 MFMA cycles instead of stalling a dense DMA burst);
+//   step 1 (64 MFMAs): after MFMA 111 vmcnt(16) (this wave's pieces of tile t+1 landed; tile t+2's 16
+//     stay in flight) + barrier (everyone's), then tile t+1's step-0 fragments are read behind the
+//     last 16 MFMAs.
+// LDS images, swizzles, range checks and epilogues are v2's (the DMA lane mapping of v2's 8 waves is
+// kept: wave w issues the pieces of v2 waves w and w + 4).  Per CU and K-tile the piece count and LDS
+// bytes equal v2's; what changes is that the MFMA pipe of each SIMD is fed by one wave that issues its
+// DMA spread out, and B fragments are shared by 128 rows instead of 64 (1/3 fewer LDS reads per MFMA).
+constexpr int NTHR4 = 256;
 
 template <bool AK, bool BKM, int EPI>
-__global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Params p) {
-  using namespace ppk;
+__global__ __launch_bounds__(NTHR4, 1) void gemm_v4_kernel(Params p) {
   __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
   const unsigned sbase = (unsigned)(size_t)smem;
 
+  int bx = blockIdx.x;
+  if (p.goff) group_setup<EPI>(p, bx);
   const int nwg = p.tiles_m * p.tiles_n;
-  const int bid = xcd_remap(blockIdx.x, nwg);
-  const int per_group = p.group_m * p.tiles_n;
-  const int gid = bid / per_group;
-  const int first_m = gid * p.group_m;
-  const int gsz = min(p.tiles_m - first_m, p.group_m);
-  const int tm = first_m + (bid % per_group) % gsz;
-  const int tn = (bid % per_group) / gsz;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;  // wm = group
-  const int Ncols = (EPI == kEpiSwiGLU) ? 2 * p.H : p.N;
-  const int nt = (((p.K + BK - 1) / BK) + 1) & ~1;
-
-  f32x4v acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-
-  const Ldp LA = ppk::lane_setup<AK, false, EPI>(p.lda, p.M, tm, p.H, wm, wn, lane);
-  const Ldp LB = ppk::lane_setup<BKM, true, EPI>(p.ldb, Ncols, tn, p.H, wm, wn, lane);
-  const unsigned short* a_t0 = AK ? p.A + (long)tm * BM * p.lda : p.A + (long)tm * BM;
-  const unsigned short* b_t0 =
-      BKM ? p.B + (long)tn * BN * p.ldb : (EPI == kEpiSwiGLU ? p.B : p.B + (long)tn * BN);
-  const long a_step = AK ? BK : (long)BK * p.lda;
-  const long b_step = BKM ? BK : (long)BK * p.ldb;
-
-  // DMA: this wave's 2 pieces (parity e = 0, 1) of operand part `part` of tile t into stage t & 1
-  auto dmaPart = [&](bool isB, int part, int t) {
-    const unsigned short* base = isB ? b_t0 + b_step * t : a_t0 + a_step * t;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base);
-    const Ldp& L = isB ? LB : LA;
-    const bool kmaj = isB ? BKM : AK;
-    const int krem = p.K - t * BK;
-    const int st = t & 1;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int j = 8 * wm + 2 * wn + e;
-      const bool ok = krem >= BK || (kmaj ? L.kl[e] < krem : L.kl[e] < krem);
-      const unsigned voff = L.voff[part][e] | ((unsigned)(!ok) << 31);
-      lds_char* dst = smem + (isB ? B_REG : 0) + poff(part, st) + j * 1024;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, 0);
-    }
-  };
-
-  // prologue: tiles 0 and 1 completely, drained
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int part = 0; part < 2; ++part) {
-      dmaPart(false, part, t);
-      dmaPart(true, part, t);
-    }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (wm == 1) __builtin_amdgcn_s_barrier();  // the stagger: G1 runs one slot behind G0
-
-  const Rdp ra = ppk::rd_setup<AK>(sbase, AK ? wm * 64 : wm * 64, lane);
-  const Rdp rb = ppk::rd_setup<BKM>(sbase + B_REG, wn * 32, lane);
-
-  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];  // A half (4 m16 x 2 k32), B0 / B1 (2 n16 x 2 k32)
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, 1>;
-
-  auto readA = [&](auto PART_, auto ST) {
-    sfor<4>([&](auto U) {
-      sfor<2>([&](auto S) {
-        fa[U][S] = read_frag<AK, decltype(U)::value, decltype(S)::value, decltype(PART_)::value,
-                             decltype(ST)::value>(ra);
-      });
-    });
-  };
-  auto readB = [&](bf16x8 (&dst)[2][2], auto PART_, auto ST) {
-    sfor<2>([&](auto U) {
-      sfor<2>([&](auto S) {
-        dst[U][S] = read_frag<BKM, decltype(U)::value, decltype(S)::value, decltype(PART_)::value,
-                              decltype(ST)::value>(rb);
-      });
-    });
-  };
-  auto cslot = [&](auto MI, const bf16x8 (&b)[2][2], auto NI) {
-    constexpr int mi = decltype(MI)::value, ni = decltype(NI)::value;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 * mi + i][2 * ni + j] = mfma(fa[i][s], b[j][s], acc[4 * mi + i][2 * ni + j]);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-  };
-  // vmcnt(6) retires the pieces issued 4 own M slots earlier only while every M slot issues its 2; in
-  // the last two K-tiles slots issue fewer, so there every M slot drains (vmcnt(0)).
-  auto mslot_begin = [&](bool steady) {
-    if (steady) {
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  int bid, kpart = -1, slab = 0;
+  if (p.ksplit > 1) {
+    const int x = bx % 8, local = bx / 8;
+    const XPlan xp = xcd_plan(nwg, x, p.cpx);
+    if (local >= xp.full + xp.tail * p.ksplit) return;
+    if (local < xp.full) {
+      bid = xp.t0 + local;
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int r = local - xp.full;
+      bid = xp.t0 + xp.full + r / p.ksplit;
+      kpart = r % p.ksplit;
+      slab = (x * p.tail_cap + r / p.ksplit) * p.ksplit + kpart;
     }
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto mslot_end = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-  };
-
-  auto ktile = [&](auto ST, int t) {
-    const bool n1 = t >= 1 && t + 1 < nt;  // tile t+1 parts not covered by the prologue
-    const bool n2 = t + 2 < nt;
-    // Q1: (A0, B0)
-    mslot_begin(n2);
-    if (wm == 0) { if (n1) dmaPart(true, 1, t + 1); } else { if (n1) dmaPart(false, 1, t + 1); }
-    readA(C0{}, ST);
-    readB(fb0, C0{}, ST);
-    mslot_end();
-    cslot(C0{}, fb0, C0{});
-    // Q2: (A0, B1)
-    mslot_begin(n2);
-    if (wm == 0) { if (n1) dmaPart(false, 1, t + 1); } else { if (n2) dmaPart(false, 0, t + 2); }
-    readB(fb1, C1{}, ST);
-    mslot_end();
-    cslot(C0{}, fb1, C1{});
-    // Q3: (A1, B1)
-    mslot_begin(n2);
-    if (wm == 0) { if (n2) dmaPart(false, 0, t + 2); } else { if (n2) dmaPart(true, 0, t + 2); }
-    readA(C1{}, ST);
-    mslot_end();
-    cslot(C1{}, fb1, C1{});
-    // Q4: (A1, B0)
-    mslot_begin(n2);
-    if (wm == 0) { if (n2) dmaPart(true, 0, t + 2); } else { if (n2) dmaPart(true, 1, t + 2); }
-    mslot_end();
-    cslot(C1{}, fb0, C0{});
-  };
-
-  for (int t = 0; t < nt; t += 2) {
-    ktile(C0{}, t);
-    ktile(C1{}, t + 1);
-  }
-  if (wm == 0) __builtin_amdgcn_s_barrier();  // balance G1's extra barrier
-
-  epilogue<EPI>(p, acc, tm, tn, wm * 128, wn * 64, wn, lane);
-}
-
-// ------------------------------------------------------------------------------------------------
-// v3: 4 waves (2 x 2), one wave per SIMD, 128x128 wave tiles (8 x 8 accumulators, 256 acc registers);
-// operands staged global -> VGPR -> LDS (buffer_load_dwordx4 one K-tile ahead, ds_write_b128) instead of
-// LDS-DMA.  Same 256x256x64 tile, the same swizzled LDS images (each lane stores the 16 B the DMA lane
-// of `lane_setup` would have landed, lane-linearly) and the same epilogues.  Rationale
-// (profiles/r2_gemm_native.md): v2 spends ~56 SIMD-cycles per 1-KiB LDS-DMA piece; a ds_write_b128 costs
-// ~13, and a 128x128 wave tile reads 1/3 less LDS per MFMA than 128x64.  Fragment reads are builtins (no
-// LDS-DMA is in flight, so the compiler's waitcnt tracking is exact); one barrier per K-tile.
-constexpr int NTHR3 = 256;
-#ifndef V3_NOSTAGE
-#define V3_NOSTAGE 0
-#endif
-typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) u32x4v lds_u32x4;
-typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8;
-
-template <bool KMAJ, int I>
-__device__ __forceinline__ u32x4v gld(const __amdgpu_buffer_rsrc_t& rs, const Ld& L, unsigned istride, bool full,
-                                      int krem) {
-  const bool ok = full || (KMAJ ? (((L.rmask >> I) & 1) && L.kl < krem) : (L.kl + 16 * I < krem));
-  const unsigned voff = (L.voff + I * istride) | ((unsigned)(!ok) << 31);
-  return __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
-}
-
-template <bool KMAJ, int U, int S>
-__device__ __forceinline__ bf16x8 frag3(lds_char* smem, const RdB<KMAJ>& r, unsigned soff) {
-  // soff: byte offset of the stage (runtime, wave-uniform), added once per read base
-  if constexpr (KMAJ) {
-    return *(const lds_bf16x8*)(smem + (r.b[S] + soff) + U * 16 * 128);
   } else {
-    const unsigned a = r.b[0] + soff + (((unsigned)(r.f + U) ^ r.b[1]) << 5) + S * 16384;
-    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + a));
-    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + a + 2048));
-    return cat(lo, hi);
+    bid = xcd_remap(bx, nwg);
   }
-}
-
-template <bool AK, bool BKM, int EPI>
-__global__ __launch_bounds__(NTHR3, 1) void gemm_v3_kernel(Params p) {
-  __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
-  lds_char* smem = (lds_char*)smem_raw;
-
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int bid = xcd_remap(blockIdx.x, nwg);
   int tm, tn;
   tile_of(p, bid, tm, tn);
+  if (p.goff && p.gmode == 0 && !group_rows<EPI>(p, tm)) return;
+  const int kt0 = kpart >= 0 ? kpart * p.kchunk : 0;
+  if (kpart >= 0) p.K = min(p.K - kt0 * BK, p.kchunk * BK);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -916,7 +665,7 @@ __global__ __launch_bounds__(NTHR3, 1) void gemm_v3_kernel(Params p) {
   const int Ncols = (EPI == kEpiSwiGLU) ? 2 * p.H : p.N;
   const int nt = (((p.K + BK - 1) / BK) + 1) & ~1;
 
-  f32x4v acc[2][8][4];
+  f32x4v acc[2][8][4];  // [column half h][row tile i][column tile j]: column tile 4h + j of the wave
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -924,115 +673,128 @@ __global__ __launch_bounds__(NTHR3, 1) void gemm_v3_kernel(Params p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
-  // each wave stages the pieces of DMA "waves" vw = wave and wave + 4
   const Ld LA0 = lane_setup<AK, false, EPI>(p.lda, p.M, tm, p.H, wave, lane);
   const Ld LA1 = lane_setup<AK, false, EPI>(p.lda, p.M, tm, p.H, wave + 4, lane);
   const Ld LB0 = lane_setup<BKM, true, EPI>(p.ldb, Ncols, tn, p.H, wave, lane);
   const Ld LB1 = lane_setup<BKM, true, EPI>(p.ldb, Ncols, tn, p.H, wave + 4, lane);
   const long a_step = AK ? BK : (long)BK * p.lda;
   const long b_step = BKM ? BK : (long)BK * p.ldb;
-  const unsigned short* a_t0 = AK ? p.A + (long)tm * BM * p.lda : p.A + (long)tm * BM;
-  const unsigned short* b_t0 = BKM ? p.B + (long)tn * BN * p.ldb : (EPI == kEpiSwiGLU ? p.B : p.B + (long)tn * BN);
+  const unsigned short* a_t0 = (AK ? p.A + (long)tm * BM * p.lda : p.A + (long)tm * BM) + a_step * kt0;
+  const unsigned short* b_t0 =
+      (BKM ? p.B + (long)tn * BN * p.ldb : (EPI == kEpiSwiGLU ? p.B : p.B + (long)tn * BN)) + b_step * kt0;
   const unsigned a_is = (unsigned)(AK ? 64 * p.lda * 2 : 16 * p.lda * 2);
   const unsigned b_is = (unsigned)(BKM ? 64 * p.ldb * 2 : 16 * p.ldb * 2);
   const bool a_rows_full = !AK || (tm + 1) * BM <= p.M;
   const bool b_rows_full = !BKM || (tn + 1) * BN <= Ncols;
+  // byte extent of each operand from its tile-0 base: the buffer descriptors' num_records, so the hardware
+  // range check bounds every DMA to the operand (rows / k past the matrix are additionally masked in software)
+  const long a_bytes = p.a_end ? (long)((const char*)p.a_end - (const char*)a_t0) : (long)kRecords;
+  const long b_bytes = p.b_end ? (long)((const char*)p.b_end - (const char*)b_t0) : (long)kRecords;
 
   const int arow = wm * 128, bcolw = wn * 128;
-  const RdB<AK> ra = rd_setup<AK>(0, arow, lane);
-  const RdB<BKM> rb = rd_setup<BKM>(B_OFF, bcolw, lane);
+  const RdB<AK> ra = rd_setup<AK>(sbase, arow, lane);
+  const RdB<BKM> rb = rd_setup<BKM>(sbase + B_OFF, bcolw, lane);
 
-  u32x4v sa[8], sb[8];  // staged pieces: [I + 4*h] = instruction I of virtual wave wave + 4h
-  // piece k (0..15): operand k>>3 (A, B), virtual-wave half (k>>2)&1, instruction k&3
-  auto load1 = [&](auto Kc, const __amdgpu_buffer_rsrc_t& rsa, const __amdgpu_buffer_rsrc_t& rsb, bool fa, bool fb,
-                   int krem) {
-    constexpr int k = decltype(Kc)::value, i = k & 3, h = (k >> 2) & 1;
-    if constexpr (k < 8) sa[i + 4 * h] = gld<AK, i>(rsa, h ? LA1 : LA0, a_is, fa, krem);
-    else sb[i + 4 * h] = gld<BKM, i>(rsb, h ? LB1 : LB0, b_is, fb, krem);
+  // DMA piece k (0..15) of tile t into stage st: operand k >> 3, v2 wave (wave + 4 * ((k >> 2) & 1)),
+  // instruction k & 3
+  auto piece = [&](auto Kc, int t, int st) {
+    constexpr int k = decltype(Kc)::value, I = k & 3, h = (k >> 2) & 1;
+    const int krem = p.K - t * BK;
+    if constexpr (k < 8) {
+      const long off = a_step * t;
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc_n(a_t0 + off, a_bytes - 2 * off);
+      dma<AK, I>(rs, h ? LA1 : LA0, a_is, smem + st * TILE_BYTES, wave + 4 * h, a_rows_full && krem >= BK, krem);
+    } else {
+      const long off = b_step * t;
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc_n(b_t0 + off, b_bytes - 2 * off);
+      dma<BKM, I>(rs, h ? LB1 : LB0, b_is, smem + B_OFF + st * TILE_BYTES, wave + 4 * h, b_rows_full && krem >= BK,
+                  krem);
+    }
   };
-  auto store1 = [&](auto Kc, int st) {
-    constexpr int k = decltype(Kc)::value, i = k & 3, h = (k >> 2) & 1;
-    const int off = (k < 8 ? 0 : B_OFF) + st * TILE_BYTES + (8 * i + wave + 4 * h) * 1024 + lane * 16;
-    *(lds_u32x4*)(smem + off) = k < 8 ? sa[i + 4 * h] : sb[i + 4 * h];
-  };
-  struct TileSrc {
-    __amdgpu_buffer_rsrc_t ra, rb;
-    bool fa, fb;
-    int krem;
-  };
-  auto src = [&](int t) {
-    TileSrc o;
-    o.krem = p.K - t * BK;
-    o.ra = make_rsrc(a_t0 + a_step * t);
-    o.rb = make_rsrc(b_t0 + b_step * t);
-    o.fa = a_rows_full && o.krem >= BK;
-    o.fb = b_rows_full && o.krem >= BK;
-    return o;
-  };
-  auto sync = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
 
-  // fragment sets: x = k32 step 0, y = step 1 (fixed names, never copied).  A fragment of the next set is
-  // read only once the register it replaces is dead (A row i dies after MFMA 8i+7, the B set after the
-  // step), so about one set plus a row is live, not two sets.
-  bf16x8 xa[8], xb[8], ya[8], yb[8];
-  auto rdA = [&](unsigned so, auto S, auto U, bf16x8 (&fa)[8]) {
-    fa[decltype(U)::value] = frag3<AK, decltype(U)::value, decltype(S)::value>(smem, ra, so);
-  };
-  auto rdB = [&](unsigned so, auto S, auto U, bf16x8 (&fb)[8]) {
-    fb[decltype(U)::value] = frag3<BKM, decltype(U)::value, decltype(S)::value>(smem, rb, so);
-  };
-  auto mm = [&](auto Q, const bf16x8 (&fa)[8], const bf16x8 (&fb)[8]) {
-    constexpr int q = decltype(Q)::value, i = q / 8, j = q % 8;
-    acc[j >> 2][i][j & 3] = mfma(fa[i], fb[j], acc[j >> 2][i][j & 3]);
-  };
+  bf16x8 xa[8], xb[8], ya[8], yb[8];  // k32 step 0 / step 1 fragment sets of the current K-tile
   using C0 = std::integral_constant<int, 0>;
   using C1 = std::integral_constant<int, 1>;
 
-  // prologue: tile 0 in stage 0 and its step-0 fragments (but xa[7]) read, tile 1 staged in registers
-  {
-    const TileSrc s0 = src(0);
-    sfor<16>([&](auto K) { load1(K, s0.ra, s0.rb, s0.fa, s0.fb, s0.krem); });
-    sfor<16>([&](auto K) { store1(K, 0); });
-    const TileSrc s1 = src(1);
-    sfor<16>([&](auto K) { load1(K, s1.ra, s1.rb, s1.fa, s1.fb, s1.krem); });
-    sync();
-    sfor<7>([&](auto U) { rdA(0u, C0{}, U, xa); });
-    sfor<8>([&](auto U) { rdB(0u, C0{}, U, xb); });
-  }
+  // prologue: tiles 0 and 1 in flight, wait for tile 0 (everyone's), read its step-0 fragments
+  sfor<16>([&](auto K) { piece(K, 0, 0); });
+  sfor<16>([&](auto K) { piece(K, 1, 1); });
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  sfor<8>([&](auto U) {
+    xa[U] = read_frag<AK, decltype(U)::value, 0, 0>(ra);
+    xb[U] = read_frag<BKM, decltype(U)::value, 0, 0>(rb);
+  });
 
-  // One K-tile from stage ST.  Step 0 (set x): slot 0 reads xa[7]; slot 8i+8 reads ya[i] (i < 7); slots
-  // 56-63 read yb.  Step 1 (set y): slot 0 reads ya[7]; slots 1-16 store tile t+1 (staged a tile ago) into
-  // the other stage; 17-32 load tile t+2 into the staging registers; slot 40 syncs (stores landed, every
-  // read of this stage retired); 41-45, 48, 56 read tile t+1's xa[0..6]; 56-63 its xb.  Past K the range
-  // check turns loads into zeros, so the loop has no branches.
-  for (int t = 0; t < nt; ++t) {
-    const int st = t & 1;
-    const unsigned so = st * TILE_BYTES, sn_off = (st ^ 1) * TILE_BYTES;
+  auto mm = [&](auto Q, const bf16x8 (&fa)[8], const bf16x8 (&fb)[8]) {
+    constexpr int q = decltype(Q)::value, i = q / 8, j = q % 8;
+    mfma_agpr(acc[j >> 2][i][j & 3], fa[i], fb[j]);
+  };
+
+  // The loop has no branches: past K every piece is range-masked to zeros (no memory traffic), so tiles
+  // nt and nt+1 are "streamed" into stages nobody reads again, and vmcnt(16) always retires tile t+1.
+  auto ktile = [&](auto ST, int t) {
+    constexpr int st = decltype(ST)::value;
+    sync_frags();
+    __builtin_amdgcn_s_setprio(1);
     sfor<64>([&](auto Q) {
       constexpr int q = decltype(Q)::value;
       mm(Q, xa, xb);
-      if constexpr (q == 0) rdA(so, C0{}, std::integral_constant<int, 7>{}, xa);
-      if constexpr (q >= 8 && q < 57 && q % 8 == 0) rdA(so, C1{}, std::integral_constant<int, q / 8 - 1>{}, ya);
-      if constexpr (q >= 56) rdB(so, C1{}, std::integral_constant<int, q - 56>{}, yb);
+      if constexpr (q < 8) ya[q] = read_frag<AK, q, 1, st>(ra);
+      if constexpr (q >= 8 && q < 16) yb[q - 8] = read_frag<BKM, q - 8, 1, st>(rb);
+      if constexpr (q == 23) {
+        // every wave holds all its fragments of this stage: release it
+        __builtin_amdgcn_s_setprio(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+      }
+      if constexpr (q >= 24 && (q - 24) % 5 == 0) piece(std::integral_constant<int, (q - 24) / 5>{}, t + 2, st);
       __builtin_amdgcn_sched_barrier(0);
     });
-    const TileSrc sn = src(t + 2);
     sfor<64>([&](auto Q) {
       constexpr int q = decltype(Q)::value;
       mm(Q, ya, yb);
-      if constexpr (q == 0) rdA(so, C1{}, std::integral_constant<int, 7>{}, ya);
-      if constexpr (q >= 1 && q <= 16 && !V3_NOSTAGE) store1(std::integral_constant<int, q - 1>{}, st ^ 1);
-      if constexpr (q >= 17 && q <= 32 && !V3_NOSTAGE)
-        load1(std::integral_constant<int, q - 17>{}, sn.ra, sn.rb, sn.fa, sn.fb, sn.krem);
-      if constexpr (q == 40) sync();
-      if constexpr (q >= 41 && q <= 45) rdA(sn_off, C0{}, std::integral_constant<int, q - 41>{}, xa);
-      if constexpr (q == 48) rdA(sn_off, C0{}, std::integral_constant<int, 5>{}, xa);
-      if constexpr (q == 56) rdA(sn_off, C0{}, std::integral_constant<int, 6>{}, xa);
-      if constexpr (q >= 56) rdB(sn_off, C0{}, std::integral_constant<int, q - 56>{}, xb);
+      if constexpr (q + 64 >= 24 && (q + 64 - 24) % 5 == 0 && (q + 64 - 24) / 5 < 16)
+        piece(std::integral_constant<int, (q + 64 - 24) / 5>{}, t + 2, st);
+      if constexpr (q == 47) {
+        // tile t+1 landed (own pieces, then everyone's)
+        __builtin_amdgcn_s_setprio(0);
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+      }
+      if constexpr (q >= 48 && q < 56) xa[q - 48] = read_frag<AK, q - 48, 0, st ^ 1>(ra);
+      if constexpr (q >= 56) xb[q - 56] = read_frag<BKM, q - 56, 0, st ^ 1>(rb);
       __builtin_amdgcn_sched_barrier(0);
     });
-  }
+    __builtin_amdgcn_s_setprio(0);
+  };
 
+  for (int t = 0; t < nt; t += 2) {
+    ktile(C0{}, t);
+    ktile(C1{}, t + 1);
+  }
+  // drain the masked tail pieces and the last (unused) fragment reads before the workgroup's LDS goes away;
+  // the s_nops cover the MFMA-write -> accumulator-read wait states of the last MFMAs
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 7" ::: "memory");
+
+  if constexpr (EPI != kEpiSwiGLU) {
+    if (kpart >= 0) {
+      float* sp = p.part + (long)slab * (BM * BN);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              sp[(arow + 16 * i + 4 * (lane >> 4) + e) * BN + bcolw + 64 * h + 16 * j + (lane & 15)] = acc[h][i][j][e];
+      return;
+    }
+  }
 #pragma unroll
   for (int h = 0; h < 2; ++h) epilogue<EPI>(p, acc[h], tm, tn, arow, bcolw + 64 * h, 2 * wn + h, lane);
 }
@@ -1104,6 +866,15 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   p.zero = bias;  // ablation 7 only: the caller passes a zeroed buffer in `bias`
   p.goff = nullptr; p.ngroups = 0; p.gmode = 0; p.gsb = p.gsc = p.gsbias = 0;
   p.part = (float*)ws; p.ksplit = 1; p.kchunk = 0; p.tail_cap = 0; p.cpx = cus_per_xcd();
+  {
+    // operand extents: K-major [rows][ld] with K valid per row, MN-major [k][ld] with rows / cols valid per k
+    const bool ak = layout & 1, bk = (layout >> 1) & 1;
+    const long ncols = epi == kEpiSwiGLU ? 2L * H : (long)N;
+    const long a_el = ak ? (long)(M - 1) * lda + K : (long)(K - 1) * lda + M;
+    const long b_el = bk ? (ncols - 1) * ldb + K : (long)(K - 1) * ldb + ncols;
+    p.a_end = (const unsigned short*)A + a_el;
+    p.b_end = (const unsigned short*)B + b_el;
+  }
   p.tiles_m = (M + BM - 1) / BM;
   p.tiles_n = epi == kEpiSwiGLU ? (H + 127) / 128 : (N + BN - 1) / BN;
   p.group_m = group_m > 0 ? group_m : 8;
@@ -1113,16 +884,15 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   if (epi == kEpiSwiGLU && (bk || H % 32)) return -3;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(p.tiles_m * p.tiles_n);
-  if (ws && variant == 0 && epi != kEpiSwiGLU) {
+  if (ws && (variant == 0 || variant == 4) && epi != kEpiSwiGLU) {
     const int g = plan_splitk(p, ws_bytes);
     if (g) grid = dim3(g);
   }
   const dim3 rgrid(BM * BN / 1024, 8 * p.tail_cap);
 #define PD_GEMM_LAUNCH(AKV, BKV, EPIV)                                          \
-  if (variant == 1) {                                                            \
-    gemm_pp_kernel<AKV, BKV, EPIV><<<grid, NTHR, 0, st>>>(p);                   \
-  } else if (variant == 3) {                                                     \
-    gemm_v3_kernel<AKV, BKV, EPIV><<<grid, NTHR3, 0, st>>>(p);                  \
+  if (variant == 4) {                                                     \
+    gemm_v4_kernel<AKV, BKV, EPIV><<<grid, NTHR4, 0, st>>>(p);                  \
+    if (p.ksplit > 1) splitk_reduce_kernel<EPIV><<<rgrid, 256, 0, st>>>(p);     \
   } else {                                                                       \
     gemm_kernel<AKV, BKV, EPIV><<<grid, NTHR, 0, st>>>(p);                      \
     if (p.ksplit > 1) splitk_reduce_kernel<EPIV><<<rgrid, 256, 0, st>>>(p);     \
@@ -1173,6 +943,7 @@ extern "C" int pd_gemm_grouped(int layout, int epi, const void* A, long lda, con
   p.N = N; p.beta = beta; p.H = H; p.zero = nullptr;
   p.goff = goff; p.ngroups = ngroups; p.gmode = gmode; p.gsb = gsb; p.gsc = gsc; p.gsbias = gsbias;
   p.part = nullptr; p.ksplit = 1; p.kchunk = 0; p.tail_cap = 0; p.cpx = 32;
+  p.a_end = nullptr; p.b_end = nullptr;
   p.group_m = group_m > 0 ? group_m : 8;
   p.tiles_n = epi == kEpiSwiGLU ? (H + 127) / 128 : (N + BN - 1) / BN;
   const bool ak = layout & 1, bk = (layout >> 1) & 1;

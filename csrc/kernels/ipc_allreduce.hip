@@ -40,8 +40,13 @@ __device__ __forceinline__ unsigned* flag(unsigned* sig, int phase, int blk, int
 }
 
 // Block barrier across ranks for phase `ph`: thread p < nranks signals peer p and waits for peer p's signal.
+// The release store of lane p covers only lane p's own writes, so first EVERY thread retires its memory
+// operations system-wide (its data stores visible to peers, its peer reads complete) and the block meets:
+// only then may a peer read what this block wrote, or overwrite what it was reading.
 __device__ __forceinline__ void xbarrier(const Peers& P, int rank, int nranks, int ph, unsigned epoch, unsigned* err,
                                          long long budget) {
+  __threadfence_system();
+  __syncthreads();
   const int p = threadIdx.x;
   if (p < nranks) {
     __hip_atomic_store(flag(P.sig[p], ph, blockIdx.x, rank), epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

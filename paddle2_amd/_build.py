@@ -168,6 +168,41 @@ def build_allocator(verbose=False):
     return out
 
 
+def alloc_torch_target_path():
+    return os.path.join(ROOT, "paddle2_amd", "_pd_alloc_torch.so")
+
+
+def build_alloc_torch(verbose=False):
+    """The torch-side installer of the native allocator (csrc/alloc/torch_hook.cpp): builds torch's pluggable
+    allocator in C++ with the record-stream hook wired to pd_alloc_record_stream.  Links libtorch_hip and resolves
+    the pd_alloc_* symbols from _pd_alloc.so (loaded RTLD_GLOBAL first)."""
+    import torch
+
+    src = os.path.join(CSRC, "alloc", "torch_hook.cpp")
+    tdir = os.path.dirname(torch.__file__)
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    flags = ["-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
+             f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-I", "/opt/rocm/include", "-I", os.path.join(tdir, "include"),
+             "-I", os.path.join(tdir, "include", "torch", "csrc", "api", "include")]
+    key = _hash(src, " ".join(flags))
+    out = alloc_torch_target_path()
+    stamp = out + ".stamp"
+    if os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key:
+        return out
+    tmp = out + ".tmp"
+    lib = os.path.join(tdir, "lib")
+    cmd = ["g++"] + flags + [src, "-o", tmp, "-L" + lib, "-ltorch_hip", "-lc10_hip", "-lc10", "-ltorch_cpu",
+                             "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath," + lib, "-Wl,-rpath,/opt/rocm/lib",
+                             "-Wl,--allow-shlib-undefined"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    _run(cmd)
+    os.replace(tmp, out)
+    with open(stamp, "w") as f:
+        f.write(key)
+    return out
+
+
 def build_alloc_stress(kind="address", verbose=False):
     """The allocator's bookkeeping + the multi-threaded stress driver, against the fake HIP header (host memory,
     asynchronous events), under ``kind`` = "address" (ASan+UBSan) or "thread" (TSan).  CPU-only."""
@@ -206,7 +241,9 @@ def build_sanitized(kind="thread", verbose=False):
 
 
 def build_all(verbose=False):
-    return build(verbose=verbose), build_runtime(verbose=verbose), build_allocator(verbose=verbose)
+    alloc = build_allocator(verbose=verbose)
+    build_alloc_torch(verbose=verbose)
+    return build(verbose=verbose), build_runtime(verbose=verbose), alloc
 
 
 if __name__ == "__main__":

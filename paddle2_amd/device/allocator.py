@@ -22,8 +22,9 @@ import torch
 _LIB = None
 _PLUG = None
 _ACTIVE = [False]
+_HOOKED = [False]
 _FIELDS = ("allocated", "reserved", "peak_allocated", "peak_reserved", "num_allocs", "num_frees", "num_chunks",
-           "num_grow", "num_oom_retries", "cross_stream_reuse")
+           "num_grow", "num_oom_retries", "cross_stream_reuse", "record_stream", "deferred_frees", "deferred_pending")
 
 
 def library_path():
@@ -36,7 +37,7 @@ def lib():
         path = library_path()
         if not os.path.exists(path):
             raise RuntimeError(f"native allocator not built ({path}); run paddle2_amd._build.build_allocator()")
-        L = ctypes.CDLL(path)
+        L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)  # the torch hook resolves pd_alloc_* from it
         L.pd_alloc_configure.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
         L.pd_alloc_stats.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
         L.pd_alloc_reset_peak.argtypes = [ctypes.c_int]
@@ -77,8 +78,22 @@ def enable(chunk_mb=None, limit_bytes=None):
         raise RuntimeError("the native allocator must be enabled before the first device allocation "
                            "(set FLAGS_use_native_allocator=1 in the environment or call enable() first)")
     configure(chunk_mb, limit_bytes)
-    torch.cuda.memory.change_current_allocator(_pluggable())
+    hook = os.path.join(os.path.dirname(library_path()), "_pd_alloc_torch.so")
+    if os.path.exists(hook):
+        # C++ install with Tensor.record_stream -> pd_alloc_record_stream (cross-stream lifetime fencing)
+        lib()
+        H = ctypes.CDLL(hook)
+        if H.pd_alloc_install_torch() != 0:
+            raise RuntimeError("native allocator: torch did not create a pluggable allocator")
+        _HOOKED[0] = True
+    else:  # no record-stream hook: side-stream users must keep their tensors alive themselves
+        torch.cuda.memory.change_current_allocator(_pluggable())
     _ACTIVE[0] = True
+
+
+def has_record_stream():
+    """True when Tensor.record_stream reaches the native allocator (C++ install through _pd_alloc_torch.so)."""
+    return _HOOKED[0]
 
 
 def is_active():

@@ -27,6 +27,24 @@ _OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp
         "avg": dist.ReduceOp.SUM}
 
 
+class _PostTask:
+    """Async task of a collective whose result still needs a scale (gloo AVG / PreMulSum): wait() completes the
+    collective, then applies the scale exactly once."""
+
+    def __init__(self, work, fn):
+        self._work, self._fn, self._done = work, fn, False
+
+    def wait(self, timeout=None):
+        if not self._done:
+            self._work.wait()
+            self._fn()
+            self._done = True
+        return True
+
+    def is_completed(self):
+        return self._done or self._work.is_completed()
+
+
 class PreMulSum:
     """``RedOpCreatePreMulSum``: sum of ``scalar * x`` over ranks (the gradient-averaging reduction)."""
 
@@ -71,26 +89,36 @@ class CommContext:
             return None
         return work
 
-    def _reduce_op(self, op, tensors):
-        """-> c10d op, applying a PreMulSum scale / AVG divide around a SUM."""
+    def _reduce_op(self, op):
+        """-> (c10d op, post scale).  RCCL: AVG is ncclAvg and PreMulSum is ncclRedOpCreatePreMulSum, both inside
+        the collective (nccl_comm_context.cc:79-248); gloo has neither, so SUM plus a scale applied to the
+        RESULT once the work completes (never to the caller's input)."""
         if isinstance(op, PreMulSum):
-            for t in tensors:
-                t.mul_(op.scalar)
-            return dist.ReduceOp.SUM, None
+            if self.backend == "nccl" and hasattr(dist, "_make_nccl_premul_sum"):
+                return dist._make_nccl_premul_sum(float(op.scalar)), None
+            return dist.ReduceOp.SUM, float(op.scalar)
         if _is_avg(op):
+            if self.backend == "nccl":
+                return dist.ReduceOp.AVG, None
             return dist.ReduceOp.SUM, 1.0 / self.size
         return _redop(op), None
 
+    def _post(self, work, sync_op, fn):
+        """Finish ``work`` then run ``fn`` (a result scale): now if sync_op, else on the returned task's wait()."""
+        if sync_op:
+            work.wait()
+            fn()
+            return None
+        return _PostTask(work, fn)
+
     # ---------------------------------------------------------------- collectives
     def all_reduce(self, tensor, op="sum", sync_op=True):
-        rop, post = self._reduce_op(op, [tensor])
+        rop, post = self._reduce_op(op)
         o = dist.AllreduceOptions()
         o.reduceOp = rop
         w = self.pg.allreduce([tensor], o)
         if post is not None:
-            w.wait()
-            tensor.mul_(post)
-            return None
+            return self._post(w, sync_op, lambda: tensor.mul_(post))
         return self._done(w, sync_op)
 
     def broadcast(self, tensor, root, sync_op=True):
@@ -99,16 +127,19 @@ class CommContext:
         return self._done(self.pg.broadcast([tensor], o), sync_op)
 
     def reduce(self, tensor, root, op="sum", sync_op=True):
-        rop, post = self._reduce_op(op, [tensor])
+        rop, post = self._reduce_op(op)
         o = dist.ReduceOptions()
         o.rootRank, o.rootTensor, o.reduceOp = int(root), 0, rop
-        w = self.pg.reduce([tensor], o)
-        if post is not None:
-            w.wait()
-            if self.rank == root:
-                tensor.mul_(post)
-            return None
-        return self._done(w, sync_op)
+        if post is None:
+            return self._done(self.pg.reduce([tensor], o), sync_op)
+        # gloo post scale: reduce a copy so a non-root rank's send buffer stays untouched, scale on the root only
+        buf = tensor.clone()
+        w = self.pg.reduce([buf], o)
+
+        def fin():
+            if self.rank == int(root):
+                tensor.copy_(buf.mul_(post))
+        return self._post(w, sync_op, fin)
 
     def all_gather(self, out, tensor, sync_op=True):
         """``out``: a [size * n, ...] tensor (rank-major) or a list of ``size`` tensors."""
@@ -124,8 +155,8 @@ class CommContext:
 
     def reduce_scatter(self, out, tensor, op="sum", sync_op=True):
         """``out`` (n rows) = this rank's slice of the reduction of ``tensor`` ([size * n, ...])."""
-        t = tensor.clone() if isinstance(op, PreMulSum) else tensor
-        rop, post = self._reduce_op(op, [t])
+        t = tensor
+        rop, post = self._reduce_op(op)
         if self.backend == "nccl":
             o = dist.ReduceScatterOptions()
             o.reduceOp = rop
@@ -262,8 +293,8 @@ class CommContextManager:
 
     def _create(self, kind, store, unique_comm_key, rank, size, **kw):
         key = str(unique_comm_key)
-        if key in self._ctx:
-            raise KeyError(f"communicator {key!r} already exists")
+        if key in self._ctx:  # the reference returns the existing communicator (comm_context_manager.cc:70)
+            return self._ctx[key]
         store = store if store is not None else self._store
         if store is None:
             raise ValueError("no store: pass one or call CommContextManager.set_store first")

@@ -98,6 +98,10 @@ class IpcAllReduce:
                 self.data_ptrs.append(pd_)
                 self.sig_ptrs.append(ps_)
         self._err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        # asynchronous error checks: after every call the error word is copied to pinned host memory behind an
+        # event; completed copies are inspected at the next call, so a timed-out call raises at the latest one
+        # call later instead of silently summing stale peer buffers
+        self._pending = []
         self.epoch = 0
 
     def _exchange(self, mine):
@@ -121,17 +125,43 @@ class IpcAllReduce:
         st = N.stream()
         C.memcpy_d2d(self._data, t.data_ptr(), nbytes, st)
         self.epoch += 1
+        self.poll()
         C.ar_allreduce(mode, _ELT[t.dtype][0], self.data_ptrs, self.sig_ptrs, self.rank, t.data_ptr(), 0, nbytes,
                        self.capacity, self.epoch, self._err.data_ptr(), self.blocks, self.timeout_ms, st)
         if check:
             self.raise_on_timeout()
+        else:
+            host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            host.copy_(self._err, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._pending.append((ev, host))
         return t
 
+    def _fail(self, e):
+        self._err.zero_()
+        self._pending.clear()
+        raise RuntimeError(f"IpcAllReduce: peers {[p for p in range(self.world) if e >> p & 1]} did not arrive "
+                           f"within {self.timeout_ms} ms (the result of that all-reduce is invalid)")
+
+    def poll(self, block=False):
+        """Inspect the error words of finished calls (all pending ones if block); raise on a timeout."""
+        while self._pending:
+            ev, host = self._pending[0]
+            if block:
+                ev.synchronize()
+            elif not ev.query():
+                break
+            self._pending.pop(0)
+            e = int(host[0])
+            if e:
+                self._fail(e)
+
     def raise_on_timeout(self):
+        self.poll(block=True)
         e = int(self._err.item())
         if e:
-            raise RuntimeError(f"IpcAllReduce: peers {[p for p in range(self.world) if e >> p & 1]} did not arrive "
-                               f"within {self.timeout_ms} ms")
+            self._fail(e)
 
     def close(self):
         C = self._C

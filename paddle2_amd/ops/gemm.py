@@ -73,7 +73,7 @@ def _workspace(t):
 
 
 def _launch(layout, epi, a, lda, b, ldb, c, ldc, c2, ldc2, bias, M, Nn, K, beta=0.0, H=0):
-    ws, ws_bytes = _workspace(a) if epi != EPI_SWIGLU and VARIANT == 0 else (0, 0)
+    ws, ws_bytes = _workspace(a) if epi != EPI_SWIGLU and VARIANT in (0, 4) else (0, 0)
     N.native().gemm(layout, epi, a.data_ptr(), lda, b.data_ptr(), ldb, c.data_ptr(), ldc, N.ptr(c2), ldc2,
                     N.ptr(bias), M, Nn, K, float(beta), H, GROUP_M, VARIANT, ws, ws_bytes, N.stream())
 

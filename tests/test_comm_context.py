@@ -39,6 +39,13 @@ def _worker(rank, port, out_dir):
     t = torch.full((2,), float(rank + 1))
     ctx.all_reduce(t, op="avg")
     res["avg"] = t.tolist()
+    t = torch.full((2,), float(rank + 1))
+    task = ctx.all_reduce(t, op="avg", sync_op=False)  # async AVG: the task finishes the scale on wait()
+    task.wait()
+    res["avg_async"] = t.tolist()
+    t = torch.full((2,), float(rank + 1))
+    ctx.reduce(t, root=0, op=ctx.red_op_create_pre_mul_sum(2.0))  # non-root send buffer must stay untouched
+    res["reduce_premul"] = t.tolist()
     t = torch.arange(3.0) + 10 * rank
     ctx.broadcast(t, root=1)
     res["bcast"] = t.tolist()
@@ -66,11 +73,9 @@ def _worker(rank, port, out_dir):
     t = torch.ones(1) * (rank + 3)
     ctx2.all_reduce(t)
     res["ctx2"] = t.tolist()
-    try:
-        CommContextManager.create_gloo_comm_context(store, "ring_7", rank, 2)
-        res["dup"] = "no error"
-    except KeyError:
-        res["dup"] = "KeyError"
+    # re-creating an existing key returns the existing communicator (reference comm_context_manager.cc:70)
+    again = CommContextManager.create_gloo_comm_context(store, "ring_7", rank, 2)
+    res["dup"] = "same" if again is ctx else "different"
     ctx.barrier()
     mgr.release()
     torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
@@ -88,5 +93,5 @@ def test_comm_context_manager_gloo(tmp_path):
         assert res["rs"] == ([0.0, 3.0] if rank == 0 else [6.0, 9.0])
         assert res["a2a"] == ([0.0, 1.0, 100.0, 101.0] if rank == 0 else [2.0, 3.0, 102.0, 103.0])
         assert res["p2p"] == [float((1 - rank) + 5)] * 3
-        assert res["ctx2"] == [7.0] and res["dup"] == "KeyError"
+        assert res["ctx2"] == [7.0] and res["dup"] == "same"
     assert r[0]["reduce"] == [3.0, 3.0]

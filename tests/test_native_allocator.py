@@ -22,6 +22,7 @@ def test_allocator_bookkeeping_under_sanitizers(kind):
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
     assert "errors=0" in r.stdout
     assert int(r.stdout.split("cross_stream_reuse=")[1].split()[0]) > 0
+    assert int(r.stdout.split("deferred=")[1].split()[0]) > 0  # record_stream frees went through the deferral
 
 
 def test_allocator_library_api_on_cpu():
@@ -134,3 +135,41 @@ def test_native_allocator_process_wide_training():
     st = nat["stats"]
     assert st["num_allocs"] > 100 and st["reserved"] >= st["peak_allocated"] > 0
     assert nat["api_peak"] == st["peak_allocated"] and nat["api_alloc"] == st["allocated"]
+
+
+@pytest.mark.gpu
+def test_native_allocator_record_stream_fences_side_stream_reader():
+    """Tensor.record_stream reaches the native allocator (C++ install): a tensor freed on the main stream while a
+    slow side stream still reads it must not be handed to the next main-stream allocation before that read."""
+    script = textwrap.dedent("""
+        import json
+        import torch
+        import paddle2_amd as paddle
+        from paddle2_amd.device import allocator
+        assert allocator.is_active() and allocator.has_record_stream()
+        main = torch.cuda.current_stream()
+        side = torch.cuda.Stream()
+        bad = 0
+        for it in range(20):
+            a = torch.full((1 << 20,), float(it + 1), device="cuda")
+            out = torch.empty_like(a)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                torch.cuda._sleep(20_000_000)    # the side stream reads `a` only after ~10 ms
+                out.copy_(a)
+            a.record_stream(side)
+            del a                                # freed on the main stream while the side read is pending
+            b = torch.full((1 << 20,), -7.0, device="cuda")   # would reuse a's block without the fence
+            torch.cuda.synchronize()
+            bad += int((out != float(it + 1)).sum())
+            del b, out
+        st = allocator.stats(0)
+        print(json.dumps({"bad": bad, "record_stream": st["record_stream"], "deferred": st["deferred_frees"]}))
+    """)
+    import json
+
+    env = dict(os.environ, FLAGS_use_native_allocator="1")
+    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["bad"] == 0 and res["record_stream"] >= 20 and res["deferred"] >= 20, res
