@@ -15,6 +15,10 @@
 // Interceptors on other ranks are reached through the MessageBus: one TCP listener per carrier, lazily opened
 // connections, fixed 32-byte frames.  The compute callback is user code (Python through the binding); an
 // exception stops the carrier and is re-raised by wait().
+// Runs are epochs: start() bumps the carrier's run id and every frame carries the run it belongs to.  A node
+// meeting a frame of a newer run resets its own counters on its own loop thread before handling it (a faster
+// rank's next run may reach us before our start()), and frames of older runs (the last DATA_IS_USELESS of the
+// previous run, still in flight) are dropped, so no counter is ever touched by two runs or two threads.
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -39,7 +43,7 @@ namespace {
 enum MsgType : int64_t { kReady = 0, kUseless = 1, kStart = 2, kStop = 3 };
 
 struct Msg {
-  int64_t src, dst, type, step;
+  int64_t src, dst, type, step, run;
 };
 
 bool send_frame(int fd, const Msg& m) {
@@ -77,6 +81,9 @@ struct FleetCarrier::Impl {
     std::map<int64_t, int64_t> cap;       // downstream id -> buffer size
     int64_t step = 0;                     // steps run (compute / amplifier / source) or received (sink)
     bool started = false;
+    int64_t run = 0;                      // run (epoch) the counters belong to; touched by the loop thread only
+    int64_t finished_run = 0;             // last run this node completed (guarded by done_mu)
+    bool counted = false;                 // sink, or a task with max_run_times > 0: wait() waits for it
   };
 
   struct Loop {
@@ -94,8 +101,7 @@ struct FleetCarrier::Impl {
   std::atomic<bool> running{false};
   std::mutex done_mu;
   std::condition_variable done_cv;
-  int64_t sinks_left = 0;
-  int64_t tasks_left = 0;                 // local non-sink tasks not yet at max_run_times
+  std::atomic<int64_t> epoch{0};          // current run id of this carrier (bumped by start())
   std::string error;                      // guarded by done_mu
   std::atomic<bool> failed{false};        // lock-free view of !error.empty() for the loop threads
   std::vector<std::array<int64_t, 3>> trace;  // (task, step, sequence) of compute callbacks
@@ -174,11 +180,26 @@ struct FleetCarrier::Impl {
     done_cv.notify_all();
   }
 
-  void finish_one(bool sink) {
+  void finish_one(Node& n) {
     std::lock_guard<std::mutex> lk(done_mu);
-    if (sink) --sinks_left;
-    else --tasks_left;
+    n.finished_run = n.run;
     done_cv.notify_all();
+  }
+
+  // every counted node has completed run r (caller holds done_mu)
+  bool all_finished(int64_t r) {
+    for (auto& kv : nodes)
+      if (kv.second.counted && kv.second.finished_run < r) return false;
+    return true;
+  }
+
+  // fresh counters for run r, on the node's loop thread
+  static void reset(Node& n, int64_t r) {
+    n.run = r;
+    n.step = 0;
+    n.started = false;
+    for (auto& kv : n.ready) kv.second = 0;
+    for (auto& kv : n.used) kv.second = 0;
   }
 
   bool can_run(Node& n) {
@@ -210,26 +231,30 @@ struct FleetCarrier::Impl {
     n.step++;
     for (auto& kv : n.ready) {
       kv.second--;
-      post({n.spec.id, kv.first, kUseless, s});
+      post({n.spec.id, kv.first, kUseless, s, n.run});
     }
     for (auto& kv : n.used) {
       kv.second++;
-      post({n.spec.id, kv.first, kReady, s});
+      post({n.spec.id, kv.first, kReady, s, n.run});
     }
-    if (n.step == n.spec.max_run_times) finish_one(false);
+    if (n.step == n.spec.max_run_times) finish_one(n);
   }
 
   void handle(Node& n, const Msg& m) {
     if (failed.load()) return;
+    if (m.run < n.run) return;          // a frame of a finished run
+    if (m.run > n.run) reset(n, m.run);  // the first frame of a newer run (possibly before our start())
     switch (m.type) {
       case kStart:
-        n.started = true;
+        // roots (sources, and nodes without upstream such as an lr Amplifier) start on their own
+        n.started = n.spec.role == FleetTask::kSource || n.spec.upstream.empty();
+        if (!n.started) return;
         break;
       case kReady:
         if (n.spec.role == FleetTask::kSink) {
           n.step++;
-          post({n.spec.id, m.src, kUseless, m.step});
-          if (n.step == n.spec.max_run_times) finish_one(true);
+          post({n.spec.id, m.src, kUseless, m.step, n.run});
+          if (n.step == n.spec.max_run_times) finish_one(n);
           return;
         }
         n.ready[m.src]++;
@@ -250,9 +275,9 @@ struct FleetCarrier::Impl {
         int64_t s = n.step++;
         for (auto& kv : n.used) {
           kv.second++;
-          post({n.spec.id, kv.first, kReady, s});
+          post({n.spec.id, kv.first, kReady, s, n.run});
         }
-        if (n.step == n.spec.max_run_times) finish_one(false);
+        if (n.step == n.spec.max_run_times) finish_one(n);
       }
       return;
     }
@@ -307,6 +332,7 @@ void FleetCarrier::add_task(const FleetTask& t) {
   Impl::Node n;
   n.spec = t;
   n.loop = int(impl_->nodes.size() % impl_->loops.size());
+  n.counted = t.role == FleetTask::kSink || t.max_run_times > 0;
   for (auto& u : t.upstream) n.ready[u.first] = 0;
   for (auto& d : t.downstream) {
     n.used[d.first] = 0;
@@ -347,30 +373,19 @@ void FleetCarrier::start() {
     I.error.clear();
     I.failed = false;
   }
-  I.sinks_left = 0;
-  I.tasks_left = 0;
-  for (auto& kv : I.nodes) {
-    Impl::Node& n = kv.second;
-    n.step = 0;
-    n.started = false;
-    for (auto& r : n.ready) r.second = 0;
-    for (auto& u : n.used) u.second = 0;
-    if (n.spec.role == FleetTask::kSink) I.sinks_left++;
-    else if (n.spec.max_run_times > 0) I.tasks_left++;
-  }
+  // a new run: every node learns it from its kStart (or from an earlier frame of the run) on its loop thread
+  const int64_t r = ++I.epoch;
   I.running = true;
   for (auto& L : I.loops)
     if (!L->th.joinable()) L->th = std::thread([&I, Lp = L.get()] { I.loop_main(Lp); });
-  // sources and every other root (no upstream, e.g. an lr Amplifier) start on their own
-  for (auto& kv : I.nodes)
-    if (kv.second.spec.role == FleetTask::kSource || kv.second.spec.upstream.empty())
-      I.post({-1, kv.first, kStart, 0});
+  for (auto& kv : I.nodes) I.post({-1, kv.first, kStart, 0, r});
 }
 
 bool FleetCarrier::wait(double timeout_s) {
   Impl& I = *impl_;
   std::unique_lock<std::mutex> lk(I.done_mu);
-  auto pred = [&] { return !I.error.empty() || (I.sinks_left <= 0 && I.tasks_left <= 0); };
+  const int64_t r = I.epoch.load();
+  auto pred = [&] { return !I.error.empty() || I.all_finished(r); };
   // system_clock deadline: wait_until maps to pthread_cond_timedwait (steady-clock waits use
   // pthread_cond_clockwait, which GCC 11's TSan runtime does not intercept)
   bool ok = true;

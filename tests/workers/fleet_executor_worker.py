@@ -45,8 +45,17 @@ b.add_downstream_task(4, 2)
 sink.add_upstream_task(3, 2)
 fe = FleetExecutor([src, a, b, sink], rank=r, num_threads=2)
 trace = fe.run(timeout_s=60)
+first_trace = [list(t) for t in trace]
+# repeated runs with rank 1 lagging: rank 0's next-run DATA_IS_READY reaches rank 1 before its start(); run
+# epochs keep the runs apart (no wiped credits, no stale DATA_IS_USELESS from the previous run)
+import time  # noqa: E402
+
+for rep in range(4):
+    if r == 1:
+        time.sleep(0.05 * (rep % 2))
+    fe.run(timeout_s=60)
 for w, _ in pending:
     w.wait()
 dist.barrier()
 fe.release()
-write_result({"results": results, "trace": [list(t) for t in trace]})
+write_result({"results": results, "trace": first_trace})
