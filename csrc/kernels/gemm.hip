@@ -124,6 +124,9 @@ __device__ __forceinline__ bool group_setup(Params& p, int& bx) {
     p.A += (long)r0 * p.lda;
     p.B += (long)r0 * p.ldb;
     p.C = (char*)p.C + g * p.gsc * (EPI == kEpiF32 ? 4 : 2);
+    // this group's token rows only (both operands MN-major): k past the group reads zeros (v4 range check)
+    p.a_end = p.A + (p.K > 0 ? (long)(p.K - 1) * p.lda + p.M : 0);
+    p.b_end = p.B + (p.K > 0 ? (long)(p.K - 1) * p.ldb + p.N : 0);
     return true;
   }
   return true;  // gmode 0 is resolved after the tile decode (it needs the row tile)
@@ -147,6 +150,9 @@ __device__ __forceinline__ bool group_rows(Params& p, int& tm) {
   if (EPI == kEpiSwiGLU) p.C2 += (long)r0 * p.ldc2;
   p.B += g * p.gsb;
   if (p.bias) p.bias += g * p.gsbias;
+  // this group's rows / this expert's weight only: rows past the group read zeros (v4 range check)
+  p.a_end = p.A + (p.M > 0 ? (long)(p.M - 1) * p.lda + p.K : 0);
+  p.b_end = p.B + p.gsb;
   return true;
 }
 
@@ -161,10 +167,14 @@ __device__ __forceinline__ int hsw(int k) { return (k & 3) | (((k >> 3) & 1) << 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, kRecords, 0x00020000);
 }
-// descriptor whose range check stops at `nbytes` past `base` (clamped to [0, 2^31 - 1]; 0 = every load is 0)
+// descriptor whose range check stops at `nbytes` past `base` (clamped to [0, 2^31 - 1]; 0 = every load is 0).
+// The inputs go through readfirstlane: they are wave-uniform, and hipcc otherwise keeps a descriptor built from
+// a select in VGPRs and wraps every buffer op in a waterfall loop (cdna_hip_programming.md T20).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_n(const void* base, long nbytes) {
-  const int n = (int)(nbytes < 0 ? 0L : (nbytes > (long)kRecords ? (long)kRecords : nbytes));
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, n, 0x00020000);
+  const int n = __builtin_amdgcn_readfirstlane((int)(nbytes < 0 ? 0L : (nbytes > (long)kRecords ? (long)kRecords : nbytes)));
+  const unsigned long long a = (unsigned long long)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, n, 0x00020000);
 }
 
 // Column remap of the B operand for the SwiGLU epilogue: tile column c (0..255) of output tile tn
@@ -614,7 +624,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(Params p) {
 // wave tile lives in the 256 AGPRs), LDS-DMA staging, and a K-tile's COMPLETE fragment set held in
 // VGPRs (2 k32 steps x (8 A + 8 B) fragments = 128 VGPRs) so a stage is released a quarter of the way
 // into the tile.  Per K-tile and wave:
-//   step 0 (64 MFMAs): the step-1 fragments are read behind MFMAs 0-15; after MFMA 23 lgkmcnt(0) +
+//   step 0 (64 MFMAs, j-major: B fragment j outer, A fragment i inner, so MFMAs 0-7 need 9 of the 16 x reads
+//     and each later group of 8 one more — counted lgkmcnt waits, no drain at the tile start): the step-1
+//     fragments are read behind MFMAs 0-15; after MFMA 23 lgkmcnt(0) +
 //     barrier (every wave has its reads of this stage) and the 16 LDS-DMA pieces of tile t+2 are
 //     streamed into the freed stage one per 5 MFMAs (MFMAs 24-99: a piece's ~60-cycle issue cost hides
 //     under 80 MFMA cycles instead of stalling a dense DMA burst);
@@ -625,9 +637,162 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(Params p) {
 // kept: wave w issues the pieces of v2 waves w and w + 4).  Per CU and K-tile the piece count and LDS
 // bytes equal v2's; what changes is that the MFMA pipe of each SIMD is fed by one wave that issues its
 // DMA spread out, and B fragments are shared by 128 rows instead of 64 (1/3 fewer LDS reads per MFMA).
+// Epilogue of the transposed accumulator layout (v4): acc[i][j][e] = C[row 16i + (lane & 15)][col 16j + 4 * (lane
+// >> 4) + e] relative to (arow, bcolw) of tile (tm, tn).  One 8-B (bf16) / 16-B (fp32) access per (i, j) when the
+// 4 columns are in range and aligned, element-wise at the ragged right edge.  SwiGLU: gate = columns j in {0, 1},
+// up = j + 2 at the same lane position (the B column remap of bcol<>).
+template <int EPI>
+__device__ __forceinline__ void epilogue_t(const Params& p, f32x4v (&acc)[8][4], int tm, int tn, int arow, int bcolw,
+                                           int lane) {
+  const int row0 = tm * BM + arow + (lane & 15);
+  const int cq = 4 * (lane >> 4);
+  if constexpr (EPI == kEpiSwiGLU) {
+    const int wn = bcolw >> 6;  // 64-column half of the tile: 32 gate + 32 up columns
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int gc = tn * 128 + wn * 32 + 16 * j + cq;  // first of the lane's 4 gate (== output) columns
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = row0 + 16 * i;
+        if (r >= p.M) continue;
+        unsigned short g[4], u[4], o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          g[e] = f2bf(acc[i][j][e]);
+          u[e] = f2bf(acc[i][2 + j][e]);
+          o[e] = f2bf(silu(bf2f(g[e])) * bf2f(u[e]));
+        }
+        unsigned short* gp = p.C2 + (long)r * p.ldc2 + gc;
+        unsigned short* op = (unsigned short*)p.C + (long)r * p.ldc + gc;
+        if (gc + 3 < p.H) {
+          *(uint2*)gp = make_uint2(g[0] | (unsigned)g[1] << 16, g[2] | (unsigned)g[3] << 16);
+          *(uint2*)(gp + p.H) = make_uint2(u[0] | (unsigned)u[1] << 16, u[2] | (unsigned)u[3] << 16);
+          *(uint2*)op = make_uint2(o[0] | (unsigned)o[1] << 16, o[2] | (unsigned)o[3] << 16);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (gc + e < p.H) {
+              gp[e] = g[e];
+              gp[p.H + e] = u[e];
+              op[e] = o[e];
+            }
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = tn * BN + bcolw + 16 * j + cq;
+      if (c >= p.N) continue;
+      const bool vec = c + 3 < p.N;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == kEpiBF16) {
+        if (p.bias) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bv[e] = c + e < p.N ? bf2f(p.bias[c + e]) : 0.f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = row0 + 16 * i;
+        if (r >= p.M) continue;
+        if constexpr (EPI == kEpiBF16) {
+          unsigned short* cp = (unsigned short*)p.C + (long)r * p.ldc + c;
+          unsigned short o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[i][j][e] + bv[e]);
+          if (vec) {
+            *(uint2*)cp = make_uint2(o[0] | (unsigned)o[1] << 16, o[2] | (unsigned)o[3] << 16);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (c + e < p.N) cp[e] = o[e];
+          }
+        } else {
+          float* cp = (float*)p.C + (long)r * p.ldc + c;
+          if (vec) {
+            float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+            if (p.beta != 0.f) {
+              const float4 o = *(const float4*)cp;
+              v.x += p.beta * o.x; v.y += p.beta * o.y; v.z += p.beta * o.z; v.w += p.beta * o.w;
+            }
+            *(float4*)cp = v;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (c + e < p.N) cp[e] = p.beta != 0.f ? acc[i][j][e] + p.beta * cp[e] : acc[i][j][e];
+          }
+        }
+      }
+    }
+  }
+}
+
 constexpr int NTHR4 = 256;
 
-template <bool AK, bool BKM, int EPI>
+// Per-lane fragment-read bases (stage 0, k32 step 0).  K-major: one base per k32 step, fragment u at an
+// immediate +u*2048.  MN-major: one base per 16-column tile u with the pair swizzle folded in (512 registers
+// leave room for 8 bases), step / stage / the second 4-row half as immediates — no VALU per read.
+template <bool KMAJ>
+struct Rd4 {
+  unsigned b[KMAJ ? 2 : 8];
+};
+
+template <bool KMAJ>
+__device__ __forceinline__ Rd4<KMAJ> rd4_setup(unsigned img, int first, int lane) {
+  Rd4<KMAJ> o;
+  if constexpr (KMAJ) {
+    const int rl = lane & 15;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = (4 * s + (lane >> 4)) ^ ((rl >> 1) & 7);
+      o.b[s] = img + (first + rl) * 128 + ch * 16;
+    }
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const unsigned x = img + (8 * g + q) * 512 + (pp >> 1) * 16 + (pp & 1) * 8;
+    const unsigned h = q | ((g & 1) << 2);
+    const int f = first >> 4;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) o.b[u] = x + (((unsigned)(f + u) ^ h) << 5);
+  }
+  return o;
+}
+
+template <bool KMAJ, int U, int S, int ST>
+__device__ __forceinline__ bf16x8 frag4(const Rd4<KMAJ>& r) {
+  if constexpr (KMAJ) {
+    return rd128<ST * TILE_BYTES + U * 16 * 128>(r.b[S]);
+  } else {
+    return cat(rdtr<ST * TILE_BYTES + S * 16384>(r.b[U]), rdtr<ST * TILE_BYTES + S * 16384 + 2048>(r.b[U]));
+  }
+}
+
+// Per-lane DMA source offsets of this wave's 8 pieces of one operand (piece 4h + I = instruction I of v2 wave
+// wave + 4h), column bound folded in as bit 31 (MN-major); kl[h]: K-major lane's first k in the tile (masked
+// mode only).
+struct Pc4 {
+  unsigned v[8];
+  int kl[2];
+};
+
+template <bool KMAJ, bool ISB, int EPI>
+__device__ __forceinline__ Pc4 pc4_setup(long ld, int R, int t0, int H, int wave, int lane, unsigned istride) {
+  Pc4 o;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const Ld L = lane_setup<KMAJ, ISB, EPI>(ld, R, t0, H, wave + 4 * h, lane);
+    o.kl[h] = L.kl;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o.v[4 * h + i] = L.voff + i * istride;
+  }
+  return o;
+}
+
+// FAST: no per-lane k masks — every operand is bounded by the hardware range check alone (exact extents, and
+// descriptors of tiles past K carry num_records 0); otherwise a K-major operand's last, partial K-tile masks the
+// lanes whose 16-B chunk starts at or past K (K % 64 != 0).
+template <bool AK, bool BKM, int EPI, bool FAST>
 __global__ __launch_bounds__(NTHR4, 1) void gemm_v4_kernel(Params p) {
   __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
@@ -663,7 +828,8 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v4_kernel(Params p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int Ncols = (EPI == kEpiSwiGLU) ? 2 * p.H : p.N;
-  const int nt = (((p.K + BK - 1) / BK) + 1) & ~1;
+  const int ktiles = (p.K + BK - 1) / BK;
+  const int nt = (ktiles + 1) & ~1;
 
   f32x4v acc[2][8][4];  // [column half h][row tile i][column tile j]: column tile 4h + j of the wave
 #pragma unroll
@@ -673,10 +839,6 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v4_kernel(Params p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
-  const Ld LA0 = lane_setup<AK, false, EPI>(p.lda, p.M, tm, p.H, wave, lane);
-  const Ld LA1 = lane_setup<AK, false, EPI>(p.lda, p.M, tm, p.H, wave + 4, lane);
-  const Ld LB0 = lane_setup<BKM, true, EPI>(p.ldb, Ncols, tn, p.H, wave, lane);
-  const Ld LB1 = lane_setup<BKM, true, EPI>(p.ldb, Ncols, tn, p.H, wave + 4, lane);
   const long a_step = AK ? BK : (long)BK * p.lda;
   const long b_step = BKM ? BK : (long)BK * p.ldb;
   const unsigned short* a_t0 = (AK ? p.A + (long)tm * BM * p.lda : p.A + (long)tm * BM) + a_step * kt0;
@@ -684,32 +846,35 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v4_kernel(Params p) {
       (BKM ? p.B + (long)tn * BN * p.ldb : (EPI == kEpiSwiGLU ? p.B : p.B + (long)tn * BN)) + b_step * kt0;
   const unsigned a_is = (unsigned)(AK ? 64 * p.lda * 2 : 16 * p.lda * 2);
   const unsigned b_is = (unsigned)(BKM ? 64 * p.ldb * 2 : 16 * p.ldb * 2);
-  const bool a_rows_full = !AK || (tm + 1) * BM <= p.M;
-  const bool b_rows_full = !BKM || (tn + 1) * BN <= Ncols;
-  // byte extent of each operand from its tile-0 base: the buffer descriptors' num_records, so the hardware
-  // range check bounds every DMA to the operand (rows / k past the matrix are additionally masked in software)
-  const long a_bytes = p.a_end ? (long)((const char*)p.a_end - (const char*)a_t0) : (long)kRecords;
-  const long b_bytes = p.b_end ? (long)((const char*)p.b_end - (const char*)b_t0) : (long)kRecords;
+  const Pc4 PA = pc4_setup<AK, false, EPI>(p.lda, p.M, tm, p.H, wave, lane, a_is);
+  const Pc4 PB = pc4_setup<BKM, true, EPI>(p.ldb, Ncols, tn, p.H, wave, lane, b_is);
+  // byte extent of each operand from its tile-0 base: the descriptors' num_records, so the hardware range check
+  // bounds every DMA to the operand (rows past M / N and k past K read as zero)
+  const long a_bytes = (long)((const char*)p.a_end - (const char*)a_t0);
+  const long b_bytes = (long)((const char*)p.b_end - (const char*)b_t0);
+  auto desc = [&](const unsigned short* t0, long step, long bytes, int t) {
+    const long off = step * t;
+    return make_rsrc_n(t0 + off, t < ktiles ? bytes - 2 * off : 0L);
+  };
 
   const int arow = wm * 128, bcolw = wn * 128;
-  const RdB<AK> ra = rd_setup<AK>(sbase, arow, lane);
-  const RdB<BKM> rb = rd_setup<BKM>(sbase + B_OFF, bcolw, lane);
+  const Rd4<AK> ra = rd4_setup<AK>(sbase, arow, lane);
+  const Rd4<BKM> rb = rd4_setup<BKM>(sbase + B_OFF, bcolw, lane);
+  const unsigned wdst = sbase + wave * 1024;  // this wave's first LDS-DMA piece slot
 
   // DMA piece k (0..15) of tile t into stage st: operand k >> 3, v2 wave (wave + 4 * ((k >> 2) & 1)),
-  // instruction k & 3
-  auto piece = [&](auto Kc, int t, int st) {
-    constexpr int k = decltype(Kc)::value, I = k & 3, h = (k >> 2) & 1;
-    const int krem = p.K - t * BK;
-    if constexpr (k < 8) {
-      const long off = a_step * t;
-      const __amdgpu_buffer_rsrc_t rs = make_rsrc_n(a_t0 + off, a_bytes - 2 * off);
-      dma<AK, I>(rs, h ? LA1 : LA0, a_is, smem + st * TILE_BYTES, wave + 4 * h, a_rows_full && krem >= BK, krem);
-    } else {
-      const long off = b_step * t;
-      const __amdgpu_buffer_rsrc_t rs = make_rsrc_n(b_t0 + off, b_bytes - 2 * off);
-      dma<BKM, I>(rs, h ? LB1 : LB0, b_is, smem + B_OFF + st * TILE_BYTES, wave + 4 * h, b_rows_full && krem >= BK,
-                  krem);
-    }
+  // instruction k & 3; `wb` is the opaque per-tile copy of wdst (the 32 slot addresses are one s_add each
+  // instead of 32 loop-invariant SGPRs)
+  auto piece = [&](auto Kc, int st, const __amdgpu_buffer_rsrc_t& rsa, const __amdgpu_buffer_rsrc_t& rsb,
+                   unsigned wb, int krem) {
+    constexpr int k = decltype(Kc)::value, I = k & 3, h = (k >> 2) & 1, j = 4 * h + I;
+    constexpr bool isB = k >= 8;
+    constexpr bool kmaj = isB ? BKM : AK;
+    const unsigned dst = wb + st * TILE_BYTES + (8 * I + 4 * h) * 1024 + (isB ? B_OFF : 0);
+    unsigned v = isB ? PB.v[j] : PA.v[j];
+    if constexpr (!FAST && kmaj) v |= (unsigned)((isB ? PB.kl[h] : PA.kl[h]) >= krem) << 31;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(isB ? rsb : rsa, (__attribute__((address_space(3))) void*)(size_t)dst,
+                                             16, v, 0, 0, 0);
   };
 
   bf16x8 xa[8], xb[8], ya[8], yb[8];  // k32 step 0 / step 1 fragment sets of the current K-tile
@@ -717,32 +882,66 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v4_kernel(Params p) {
   using C1 = std::integral_constant<int, 1>;
 
   // prologue: tiles 0 and 1 in flight, wait for tile 0 (everyone's), read its step-0 fragments
-  sfor<16>([&](auto K) { piece(K, 0, 0); });
-  sfor<16>([&](auto K) { piece(K, 1, 1); });
+  {
+    const __amdgpu_buffer_rsrc_t a0 = desc(a_t0, a_step, a_bytes, 0), b0 = desc(b_t0, b_step, b_bytes, 0);
+    const __amdgpu_buffer_rsrc_t a1 = desc(a_t0, a_step, a_bytes, 1), b1 = desc(b_t0, b_step, b_bytes, 1);
+    sfor<16>([&](auto K) { piece(K, 0, a0, b0, wdst, p.K); });
+    sfor<16>([&](auto K) { piece(K, 1, a1, b1, wdst, p.K - BK); });
+  }
   asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
-  sfor<8>([&](auto U) {
-    xa[U] = read_frag<AK, decltype(U)::value, 0, 0>(ra);
-    xb[U] = read_frag<BKM, decltype(U)::value, 0, 0>(rb);
-  });
+  // fragment-set read order R = [b0, a0..a7, b1..b7]: the j-major MFMA order (B tile j outer, A tile i inner)
+  // can start after 9 reads and needs one more read per 8 MFMAs (counted lgkmcnt, not a full drain)
+  auto rd_set = [&](auto Q, auto S, auto ST, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
+    constexpr int q = decltype(Q)::value, s_ = decltype(S)::value, st_ = decltype(ST)::value;
+    if constexpr (q == 0) fb[0] = frag4<BKM, 0, s_, st_>(rb);
+    else if constexpr (q <= 8) fa[q - 1] = frag4<AK, q - 1, s_, st_>(ra);
+    else fb[q - 8] = frag4<BKM, q - 8, s_, st_>(rb);
+  };
+  sfor<16>([&](auto Q) { rd_set(Q, C0{}, C0{}, xa, xb); });
 
+  // MFMAs as asm on "+a" accumulators: with builtins hipcc re-shuffles the 256 accumulator registers between
+  // AGPRs and VGPRs at the loop header (hundreds of v_accvgpr moves per K-tile pair); pinned to AGPRs they stay
+  // put.  Hazards hipcc no longer sees: the fragments come straight from asm ds_reads (waited by lgkmcnt, no
+  // VALU writes in between) and the accumulators are read only after the s_nop at the end of the loop.
+  // Operands swapped (B fragment as src0): the MFMA computes the TRANSPOSED 16x16 tile, so each lane holds 4
+  // consecutive COLUMNS of one row (row 16i + (lane & 15), columns 16j + 4 * (lane >> 4) + e): the epilogue
+  // stores 8 B (bf16) / 16 B (fp32) per lane instead of 2 / 4 B.
   auto mm = [&](auto Q, const bf16x8 (&fa)[8], const bf16x8 (&fb)[8]) {
-    constexpr int q = decltype(Q)::value, i = q / 8, j = q % 8;
-    mfma_agpr(acc[j >> 2][i][j & 3], fa[i], fb[j]);
+    constexpr int q = decltype(Q)::value, j = q / 8, i = q % 8;
+    mfma_agpr(acc[j >> 2][i][j & 3], fb[j], fa[i]);
   };
 
-  // The loop has no branches: past K every piece is range-masked to zeros (no memory traffic), so tiles
-  // nt and nt+1 are "streamed" into stages nobody reads again, and vmcnt(16) always retires tile t+1.
+  // The loop has no branches: past K every piece reads zeros through a num_records-0 descriptor (no memory
+  // traffic), so tiles nt and nt+1 are "streamed" into stages nobody reads again, and vmcnt(16) always retires
+  // tile t+1.
   auto ktile = [&](auto ST, int t) {
     constexpr int st = decltype(ST)::value;
-    sync_frags();
+    const __amdgpu_buffer_rsrc_t rsa = desc(a_t0, a_step, a_bytes, t + 2), rsb = desc(b_t0, b_step, b_bytes, t + 2);
+    const int krem = p.K - (t + 2) * BK;
+    unsigned wb = wdst;
+    asm volatile("" : "+s"(wb));
     __builtin_amdgcn_s_setprio(1);
     sfor<64>([&](auto Q) {
       constexpr int q = decltype(Q)::value;
+      // x set (read order R, issued behind the previous tile's last 16 MFMAs): MFMAs 0-7 need R[0..8],
+      // MFMAs 8-15 R[9] (outstanding then: R[10..15] + the 8 y reads issued so far); from MFMA 16 on at most 15
+      // LDS ops can be outstanding, so R[10+] are retired by the time each is needed
+      if constexpr (q == 0) {
+        asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (q == 8) {
+        asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (q >= 16 && q < 24 && q % 8 == 0) {
+        asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
       mm(Q, xa, xb);
-      if constexpr (q < 8) ya[q] = read_frag<AK, q, 1, st>(ra);
-      if constexpr (q >= 8 && q < 16) yb[q - 8] = read_frag<BKM, q - 8, 1, st>(rb);
+      if constexpr (q < 16) rd_set(Q, C1{}, ST, ya, yb);
       if constexpr (q == 23) {
         // every wave holds all its fragments of this stage: release it
         __builtin_amdgcn_s_setprio(0);
@@ -750,14 +949,15 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v4_kernel(Params p) {
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_s_setprio(1);
       }
-      if constexpr (q >= 24 && (q - 24) % 5 == 0) piece(std::integral_constant<int, (q - 24) / 5>{}, t + 2, st);
+      if constexpr (q >= 24 && (q - 24) % 5 == 0)
+        piece(std::integral_constant<int, (q - 24) / 5>{}, st, rsa, rsb, wb, krem);
       __builtin_amdgcn_sched_barrier(0);
     });
     sfor<64>([&](auto Q) {
       constexpr int q = decltype(Q)::value;
       mm(Q, ya, yb);
       if constexpr (q + 64 >= 24 && (q + 64 - 24) % 5 == 0 && (q + 64 - 24) / 5 < 16)
-        piece(std::integral_constant<int, (q + 64 - 24) / 5>{}, t + 2, st);
+        piece(std::integral_constant<int, (q + 64 - 24) / 5>{}, st, rsa, rsb, wb, krem);
       if constexpr (q == 47) {
         // tile t+1 landed (own pieces, then everyone's)
         __builtin_amdgcn_s_setprio(0);
@@ -765,8 +965,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v4_kernel(Params p) {
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_s_setprio(1);
       }
-      if constexpr (q >= 48 && q < 56) xa[q - 48] = read_frag<AK, q - 48, 0, st ^ 1>(ra);
-      if constexpr (q >= 56) xb[q - 56] = read_frag<BKM, q - 56, 0, st ^ 1>(rb);
+      if constexpr (q >= 48) rd_set(std::integral_constant<int, q - 48>{}, C0{}, std::integral_constant<int, st ^ 1>{}, xa, xb);
       __builtin_amdgcn_sched_barrier(0);
     });
     __builtin_amdgcn_s_setprio(0);
@@ -791,12 +990,206 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v4_kernel(Params p) {
           for (int i = 0; i < 8; ++i)
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              sp[(arow + 16 * i + 4 * (lane >> 4) + e) * BN + bcolw + 64 * h + 16 * j + (lane & 15)] = acc[h][i][j][e];
+              sp[(arow + 16 * i + (lane & 15)) * BN + bcolw + 64 * h + 16 * j + 4 * (lane >> 4) + e] = acc[h][i][j][e];
       return;
     }
   }
 #pragma unroll
-  for (int h = 0; h < 2; ++h) epilogue<EPI>(p, acc[h], tm, tn, arow, bcolw + 64 * h, 2 * wn + h, lane);
+  for (int h = 0; h < 2; ++h) epilogue_t<EPI>(p, acc[h], tm, tn, arow, bcolw + 64 * h, lane);
+}
+
+// ------------------------------------------------------------------------------------------------
+// v6: v4's K-loop made persistent.  grid = min(tiles, CUs); workgroup w takes tiles slot(w), slot(w) + G, ...
+// (slot = the XCD-chunked remap, so the G tiles in flight at any time are the grouped-order block each XCD's
+// L2 shares, as in a one-wave launch).  The K-tile stream of all its tiles is one pipeline: the LDS-DMA two
+// K-tiles ahead runs across tile boundaries, so the next tile's first K-tiles land while the previous tile's
+// epilogue stores (no per-tile prologue bubble), and the workgroup's LDS / register setup happens once.
+// No tail split-K: the last round may be partial.  (A dynamically scheduled form — per-XCD atomic tile queues
+// with stealing — measured 3-8 % slower than this static one: it loses the grouped L2 block per XCD.)
+template <bool AK, bool BKM, int EPI, bool FAST>
+__global__ __launch_bounds__(NTHR4, 1) void gemm_v6_kernel(Params p) {
+  __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
+  const unsigned sbase = (unsigned)(size_t)(lds_char*)smem_raw;
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int G = gridDim.x;
+  const int slot = xcd_remap(blockIdx.x, G);
+  const int ntile = slot < nwg ? (nwg - slot + G - 1) / G : 0;
+  if (ntile == 0) return;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ktiles = (p.K + BK - 1) / BK;
+  const int nt = (ktiles + 1) & ~1;
+
+  f32x4v acc[2][8][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  const long a_step = AK ? BK : (long)BK * p.lda;
+  const long b_step = BKM ? BK : (long)BK * p.ldb;
+  const unsigned a_is = (unsigned)(AK ? 64 * p.lda * 2 : 16 * p.lda * 2);
+  const unsigned b_is = (unsigned)(BKM ? 64 * p.ldb * 2 : 16 * p.ldb * 2);
+  // lane offsets relative to the tile base: tile-independent (no per-tile column flags — with exact operand
+  // extents the rows / columns past M / N of an edge tile read either zeros or bytes of the operand that only
+  // feed output rows / columns the epilogue never stores)
+  const Pc4 PA = pc4_setup<AK, false, EPI>(p.lda, 1 << 30, 0, p.H, wave, lane, a_is);
+  const Pc4 PB = pc4_setup<BKM, true, EPI>(p.ldb, 1 << 30, 0, p.H, wave, lane, b_is);
+  const char* a_end = (const char*)p.a_end;
+  const char* b_end = (const char*)p.b_end;
+  auto a_base = [&](int tm) { return AK ? p.A + (long)tm * BM * p.lda : p.A + (long)tm * BM; };
+  auto b_base = [&](int tn) {
+    return BKM ? p.B + (long)tn * BN * p.ldb : (EPI == kEpiSwiGLU ? p.B + (long)tn * 128 : p.B + (long)tn * BN);
+  };
+
+  const int arow = wm * 128, bcolw = wn * 128;
+  const Rd4<AK> ra = rd4_setup<AK>(sbase, arow, lane);
+  const Rd4<BKM> rb = rd4_setup<BKM>(sbase + B_OFF, bcolw, lane);
+  const unsigned wdst = sbase + wave * 1024;
+
+  // prefetch cursor: tile (sequence index pu) and K-tile pk of the next K-tile to stream; descriptors of tiles
+  // past this workgroup's last carry num_records 0
+  int pu = 0, pk = 0, ptm = 0, ptn = 0;
+  const unsigned short* pa0 = nullptr;
+  const unsigned short* pb0 = nullptr;
+  auto set_tile = [&](int u) {
+    const int L = slot + u * G;
+    if (u < ntile) tile_of(p, L, ptm, ptn);
+    pa0 = a_base(ptm);
+    pb0 = b_base(ptn);
+  };
+  set_tile(0);
+  auto next_desc = [&](__amdgpu_buffer_rsrc_t& rsa, __amdgpu_buffer_rsrc_t& rsb, int& krem) {
+    const bool live = pu < ntile && pk < ktiles;
+    const long ao = a_step * pk, bo = b_step * pk;
+    rsa = make_rsrc_n(pa0 + ao, live ? (long)(a_end - (const char*)(pa0 + ao)) : 0L);
+    rsb = make_rsrc_n(pb0 + bo, live ? (long)(b_end - (const char*)(pb0 + bo)) : 0L);
+    krem = p.K - pk * BK;
+    if (++pk == nt) {
+      pk = 0;
+      ++pu;
+      set_tile(pu);
+    }
+  };
+
+  auto piece = [&](auto Kc, int st, const __amdgpu_buffer_rsrc_t& rsa, const __amdgpu_buffer_rsrc_t& rsb,
+                   unsigned wb, int krem) {
+    constexpr int k = decltype(Kc)::value, I = k & 3, h = (k >> 2) & 1, j = 4 * h + I;
+    constexpr bool isB = k >= 8;
+    constexpr bool kmaj = isB ? BKM : AK;
+    const unsigned dst = wb + st * TILE_BYTES + (8 * I + 4 * h) * 1024 + (isB ? B_OFF : 0);
+    unsigned v = isB ? PB.v[j] : PA.v[j];
+    if constexpr (!FAST && kmaj) v |= (unsigned)((isB ? PB.kl[h] : PA.kl[h]) >= krem) << 31;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(isB ? rsb : rsa, (__attribute__((address_space(3))) void*)(size_t)dst,
+                                             16, v, 0, 0, 0);
+  };
+
+  bf16x8 xa[8], xb[8], ya[8], yb[8];
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  auto rd_set = [&](auto Q, auto S, auto ST, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
+    constexpr int q = decltype(Q)::value, s_ = decltype(S)::value, st_ = decltype(ST)::value;
+    if constexpr (q == 0) fb[0] = frag4<BKM, 0, s_, st_>(rb);
+    else if constexpr (q <= 8) fa[q - 1] = frag4<AK, q - 1, s_, st_>(ra);
+    else fb[q - 8] = frag4<BKM, q - 8, s_, st_>(rb);
+  };
+
+  // prologue: the first two K-tiles of the first tile
+  {
+    __amdgpu_buffer_rsrc_t rsa, rsb;
+    int krem;
+    next_desc(rsa, rsb, krem);
+    sfor<16>([&](auto K) { piece(K, 0, rsa, rsb, wdst, krem); });
+    next_desc(rsa, rsb, krem);
+    sfor<16>([&](auto K) { piece(K, 1, rsa, rsb, wdst, krem); });
+  }
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  sfor<16>([&](auto Q) { rd_set(Q, C0{}, C0{}, xa, xb); });
+
+  auto mm = [&](auto Q, const bf16x8 (&fa)[8], const bf16x8 (&fb)[8]) {
+    constexpr int q = decltype(Q)::value, j = q / 8, i = q % 8;
+    mfma_agpr(acc[j >> 2][i][j & 3], fb[j], fa[i]);
+  };
+
+  auto ktile = [&](auto ST) {
+    constexpr int st = decltype(ST)::value;
+    __amdgpu_buffer_rsrc_t rsa, rsb;
+    int krem;
+    next_desc(rsa, rsb, krem);
+    unsigned wb = wdst;
+    asm volatile("" : "+s"(wb));
+    __builtin_amdgcn_s_setprio(1);
+    sfor<64>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      if constexpr (q == 0) {
+        asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (q == 8) {
+        asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (q >= 16 && q < 24 && q % 8 == 0) {
+        asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      mm(Q, xa, xb);
+      if constexpr (q < 16) rd_set(Q, C1{}, ST, ya, yb);
+      if constexpr (q == 23) {
+        __builtin_amdgcn_s_setprio(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+      }
+      if constexpr (q >= 24 && (q - 24) % 5 == 0) piece(std::integral_constant<int, (q - 24) / 5>{}, st, rsa, rsb, wb, krem);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    sfor<64>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      mm(Q, ya, yb);
+      if constexpr (q + 64 >= 24 && (q + 64 - 24) % 5 == 0 && (q + 64 - 24) / 5 < 16)
+        piece(std::integral_constant<int, (q + 64 - 24) / 5>{}, st, rsa, rsb, wb, krem);
+      if constexpr (q == 47) {
+        __builtin_amdgcn_s_setprio(0);
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+      }
+      if constexpr (q >= 48) rd_set(std::integral_constant<int, q - 48>{}, C0{}, std::integral_constant<int, st ^ 1>{}, xa, xb);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  int ctm, ctn;
+  tile_of(p, slot, ctm, ctn);
+  for (int u = 0; u < ntile; ++u) {
+    for (int t = 0; t < nt; t += 2) {
+      ktile(C0{});
+      ktile(C1{});
+    }
+    // tile done: its accumulators out (the next tile's first K-tiles are already streaming / being read)
+    asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+#pragma unroll
+    for (int h = 0; h < 2; ++h) epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_nop 4" ::: "memory");
+    if (u + 1 < ntile) tile_of(p, slot + (u + 1) * G, ctm, ctn);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
 }  // namespace gm
@@ -883,16 +1276,28 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   if (!bk && (ldb % 8 || (epi == kEpiSwiGLU ? (2 * H) % 8 : N % 8))) return -2;
   if (epi == kEpiSwiGLU && (bk || H % 32)) return -3;
   hipStream_t st = (hipStream_t)stream;
+  // v4+ store 4 consecutive output columns per lane (8-B bf16 / 16-B fp32 accesses): rows must keep that alignment
+  if (variant >= 4 && (ldc % 4 || (size_t)C % 16 || (C2 && (ldc2 % 4 || (size_t)C2 % 16)))) variant = 0;
   dim3 grid(p.tiles_m * p.tiles_n);
   if (ws && (variant == 0 || variant == 4) && epi != kEpiSwiGLU) {
     const int g = plan_splitk(p, ws_bytes);
     if (g) grid = dim3(g);
   }
   const dim3 rgrid(BM * BN / 1024, 8 * p.tail_cap);
+  const bool fast = !(ak || bk) || K % BK == 0;  // v4: no K-major operand has a partial last K-tile
+  const dim3 pgrid(std::min(p.tiles_m * p.tiles_n, 8 * p.cpx));  // v6: one persistent workgroup per CU
 #define PD_GEMM_LAUNCH(AKV, BKV, EPIV)                                          \
-  if (variant == 4) {                                                     \
-    gemm_v4_kernel<AKV, BKV, EPIV><<<grid, NTHR4, 0, st>>>(p);                  \
+  if (variant == 4) {                                                            \
+    if (fast)                                                                    \
+      gemm_v4_kernel<AKV, BKV, EPIV, true><<<grid, NTHR4, 0, st>>>(p);          \
+    else                                                                         \
+      gemm_v4_kernel<AKV, BKV, EPIV, false><<<grid, NTHR4, 0, st>>>(p);         \
     if (p.ksplit > 1) splitk_reduce_kernel<EPIV><<<rgrid, 256, 0, st>>>(p);     \
+  } else if (variant == 6) {                                                     \
+    if (fast)                                                                    \
+      gemm_v6_kernel<AKV, BKV, EPIV, true><<<pgrid, NTHR4, 0, st>>>(p);         \
+    else                                                                         \
+      gemm_v6_kernel<AKV, BKV, EPIV, false><<<pgrid, NTHR4, 0, st>>>(p);        \
   } else {                                                                       \
     gemm_kernel<AKV, BKV, EPIV><<<grid, NTHR, 0, st>>>(p);                      \
     if (p.ksplit > 1) splitk_reduce_kernel<EPIV><<<rgrid, 256, 0, st>>>(p);     \
