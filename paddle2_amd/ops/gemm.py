@@ -24,8 +24,19 @@ from . import _native as N
 LAYOUT_AK, LAYOUT_BK = 1, 2
 EPI_BF16, EPI_F32, EPI_SWIGLU = 0, 1, 2
 GROUP_M = int(os.environ.get("PADDLE2_AMD_GEMM_GROUP_M", "8"))
-# kernel schedule: 0 = v2 (8 sub-phases, all waves stage), 1 = ping-pong (wave groups one barrier apart)
-VARIANT = int(os.environ.get("PADDLE2_AMD_GEMM_VARIANT", "0"))
+# kernel schedule (csrc/kernels/gemm.hip): 0 = v2 (8 waves, 2 per SIMD, 128x64 wave tiles), 4 = v4 (4 waves,
+# 128x128 wave tiles on AGPR accumulators, spread LDS-DMA, 8/16-B epilogue stores), 6 = v6 (v4 persistent: one
+# workgroup per CU, the DMA pipeline running across tile boundaries).  Per pass, from the measured table in
+# profiles/r3_gemm_v4.md: forward / dgrad (bf16 out, K = 4096..32000) v6, wgrad into the fp32 main grad v4 (its
+# long token reduction leaves persistence little to win, and v6's fp32 read-modify-write epilogue spills),
+# the SwiGLU-epilogue forward v4.  PADDLE2_AMD_GEMM_VARIANT forces one schedule for every pass.
+_FORCE = os.environ.get("PADDLE2_AMD_GEMM_VARIANT")
+VARIANT = int(_FORCE) if _FORCE is not None else None
+PASS_VARIANT = {"fwd": 6, "dgrad": 6, "wgrad": 4, "wgrad_bf16": 4, "swiglu": 4}
+
+
+def _variant(name):
+    return VARIANT if VARIANT is not None else PASS_VARIANT[name]
 # "native" (default on the MI355X) | "blas": route the Linear GEMMs through hipBLASLt instead
 BACKEND = os.environ.get("PADDLE2_AMD_GEMM", "native")
 
@@ -72,10 +83,11 @@ def _workspace(t):
     return ws.data_ptr(), _WS_BYTES
 
 
-def _launch(layout, epi, a, lda, b, ldb, c, ldc, c2, ldc2, bias, M, Nn, K, beta=0.0, H=0):
-    ws, ws_bytes = _workspace(a) if epi != EPI_SWIGLU and VARIANT in (0, 4) else (0, 0)
+def _launch(layout, epi, a, lda, b, ldb, c, ldc, c2, ldc2, bias, M, Nn, K, beta=0.0, H=0, name="fwd"):
+    v = _variant(name)
+    ws, ws_bytes = _workspace(a) if epi != EPI_SWIGLU and v in (0, 4) else (0, 0)
     N.native().gemm(layout, epi, a.data_ptr(), lda, b.data_ptr(), ldb, c.data_ptr(), ldc, N.ptr(c2), ldc2,
-                    N.ptr(bias), M, Nn, K, float(beta), H, GROUP_M, VARIANT, ws, ws_bytes, N.stream())
+                    N.ptr(bias), M, Nn, K, float(beta), H, GROUP_M, v, ws, ws_bytes, N.stream())
 
 
 def mm_fwd(x2, w, bias=None, out=None):
@@ -95,7 +107,7 @@ def mm_dgrad(dy2, w, out=None):
     if out is None:
         out = torch.empty(M, K, dtype=dy2.dtype, device=dy2.device)
     _launch(LAYOUT_AK | LAYOUT_BK, EPI_BF16, dy2, dy2.stride(0), w, w.stride(0), out, out.stride(0), None, 0, None,
-            M, K, Nn)
+            M, K, Nn, name="dgrad")
     return out
 
 
@@ -104,7 +116,8 @@ def mm_wgrad(x2, dy2, out, beta=0.0):
     M, K = x2.shape
     Nn = dy2.shape[1]
     assert out.dtype == torch.float32 and out.shape == (K, Nn) and out.stride(1) == 1
-    _launch(0, EPI_F32, x2, x2.stride(0), dy2, dy2.stride(0), out, out.stride(0), None, 0, None, K, Nn, M, beta)
+    _launch(0, EPI_F32, x2, x2.stride(0), dy2, dy2.stride(0), out, out.stride(0), None, 0, None, K, Nn, M, beta,
+            name="wgrad")
     return out
 
 
@@ -114,7 +127,8 @@ def mm_wgrad_bf16(x2, dy2, out=None):
     Nn = dy2.shape[1]
     if out is None:
         out = torch.empty(K, Nn, dtype=x2.dtype, device=x2.device)
-    _launch(0, EPI_BF16, x2, x2.stride(0), dy2, dy2.stride(0), out, out.stride(0), None, 0, None, K, Nn, M)
+    _launch(0, EPI_BF16, x2, x2.stride(0), dy2, dy2.stride(0), out, out.stride(0), None, 0, None, K, Nn, M,
+            name="wgrad_bf16")
     return out
 
 
@@ -125,7 +139,7 @@ def mm_swiglu(x2, w):
     gu = torch.empty(M, 2 * H, dtype=x2.dtype, device=x2.device)
     a = torch.empty(M, H, dtype=x2.dtype, device=x2.device)
     _launch(LAYOUT_AK, EPI_SWIGLU, x2, x2.stride(0), w, w.stride(0), a, a.stride(0), gu, gu.stride(0), None, M,
-            2 * H, K, 0.0, H)
+            2 * H, K, 0.0, H, name="swiglu")
     return a, gu
 
 

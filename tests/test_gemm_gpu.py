@@ -13,6 +13,13 @@ pytestmark = pytest.mark.gpu
 dev = "cuda"
 
 
+@pytest.fixture(params=[None, 0, 4, 6], ids=["per-pass", "v2", "v4", "v6"], autouse=True)
+def schedule(request, monkeypatch):
+    """Every test runs on each kernel schedule (None = the per-pass default routing)."""
+    monkeypatch.setattr(G, "VARIANT", request.param)
+    return request.param
+
+
 def _rand(*shape, scale=1.0, seed=0):
     g = torch.Generator(device=dev).manual_seed(seed)
     return (torch.randn(*shape, generator=g, device=dev) * scale).to(torch.bfloat16)
@@ -161,19 +168,22 @@ def test_swiglu_linear_node(mode, monkeypatch):
 
 
 @pytest.mark.parametrize("M,N,K", [(2048, 4096, 4096), (300, 520, 72), (4096, 22016, 4096)])
-def test_schedule_variants_bitwise_equal(M, N, K, monkeypatch):
-    """v2 (all waves stage) and ping-pong schedules accumulate the same products in the same order:
-    their outputs must agree bit for bit (a staging race shows up here first)."""
+def test_schedule_variants_bitwise_equal(M, N, K, monkeypatch, schedule):
+    """v2 (8 waves), v4 (4 waves, AGPR accumulators) and v6 (persistent) accumulate the same products in the
+    same order: their outputs must agree bit for bit (a staging race shows up here first)."""
+    if schedule is not None:
+        pytest.skip("compares the schedules itself")
     x, w, dy = _rand(M, K, seed=30), _rand(K, N, seed=31, scale=0.05), _rand(M, N, seed=32)
-    monkeypatch.setattr(G, "SPLITK", False)   # tail split-K sums K-slices in another order (v2 only)
+    monkeypatch.setattr(G, "SPLITK", False)   # tail split-K sums K-slices in another order (v2 / v4)
     outs = []
-    for v in (0, 1):
+    for v in (0, 4, 6):
         monkeypatch.setattr(G, "VARIANT", v)
         o32 = torch.zeros(K, N, device=dev)
         G.mm_wgrad(x, dy, o32)
         outs.append((G.mm_fwd(x, w), G.mm_dgrad(dy, w), o32))
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 22016, 32768), (11008, 4096, 32768), (1024, 1024, 8192),
