@@ -198,6 +198,13 @@ class _Unit:
     # written directly by their weight-gradient GEMM (fp32 accumulate, ops.torch_ops._main_grad_accumulate);
     # the rest (norm weights, embeddings) arrive through autograd and are copied in by the grad hook.
     # The same SUM + fp32 1/N scale runs on RCCL and gloo (the scale is folded into the optimizer).
+    def _flat(self):
+        """This unit's fp32 flat gradient buffer for the running backward (N > 1), from the model's bounded pool."""
+        if self.flat32 is None:
+            self.flat32 = self.model._acquire_flat(self) if self.model is not None else \
+                torch.empty(self.padded, dtype=torch.float32, device=self.device)
+        return self.flat32
+
     def grad_target(self, i):
         """-> (fp32 view of param i's gradient slot, beta): beta 0 = overwrite, 1 = accumulate."""
         o, n, shp = self.offsets[i], self.numels[i], self.shapes[i]
@@ -205,9 +212,7 @@ class _Unit:
             buf = self.grad_shard
             beta = 0 if (self.grad_clean and i not in self.written) else 1
         else:
-            if self.flat32 is None:
-                self.flat32 = torch.empty(self.padded, dtype=torch.float32, device=self.device)
-            buf = self.flat32
+            buf = self._flat()
             beta = 0 if i not in self.written else 1
         return buf[o:o + n].view(shp), beta
 
@@ -245,32 +250,43 @@ class _Unit:
                 self._zero_unwritten(self.grad_shard)
                 self.grad_clean = False
         else:
-            if self.flat32 is None:
-                self.flat32 = torch.empty(self.padded, dtype=torch.float32, device=self.device)
-            self._zero_unwritten(self.flat32)
+            flat = self._flat()
+            self._zero_unwritten(flat)
             if self.grad_clean:
                 out, self.rs_add = self.grad_shard, False
             else:
                 out, self.rs_add = torch.empty(self.S, dtype=torch.float32, device=self.device), True
-            self.rs_work = dist.reduce_scatter_tensor(out, self.flat32, op=dist.ReduceOp.SUM, group=self.group.pg,
+            self.rs_work = dist.reduce_scatter_tensor(out, flat, op=dist.ReduceOp.SUM, group=self.group.pg,
                                                       async_op=True)
             self.rs_buf = out
-            self.flat_grad = self.flat32  # keep alive until the collective completes
+            self.flat_grad = flat  # keep alive until the collective completes (then back to the pool)
             self.flat32 = None
             self.grad_clean = False
+            if self.model is not None:
+                self.model._rs_issued(self)
         self.written = set()
         self.release()
 
-    def finish_grads(self):
-        if self.written:
-            self.reduce_grads()
+    def retire_rs(self):
+        """Complete this unit's reduce-scatter: fold an accumulation step's partial into the owned fp32 shard and
+        hand the flat buffer back; -> the freed flat buffer (or None)."""
+        flat = None
         if self.rs_work is not None:
             self.rs_work.wait()
             if self.rs_add:
                 self.grad_shard.add_(self.rs_buf)
             self.rs_work = None
             self.rs_buf = None
-            self.flat_grad = None
+            flat, self.flat_grad = self.flat_grad, None
+        return flat
+
+    def finish_grads(self):
+        if self.written:
+            self.reduce_grads()
+        if self.model is not None:
+            self.model._retire_all()
+        else:
+            self.retire_rs()
         self.bw_gathered = False
 
     # ------------------------------------------------------------ after the optimizer
@@ -311,9 +327,19 @@ class GroupShardedModel(Layer):
             ps = [p for p in layer.parameters() if id(p) in excluded]
             self._units.append(_Unit(len(self._units), None, ps, group, 2, decay_fn, lr_fn))
         self._order = []       # unit call order in forward
+        self._order_done = False  # a full forward has recorded _order (the last unit stays gathered for backward)
         self._by_layer = {id(u.layer): u for u in self._units if u.layer is not None}
         self._cb_queued = False
         self._hooks = []
+        # stage-3 N > 1 gradient buffers: at most MAX_LIVE_FLAT fp32 flat unit buffers exist at a time (the ones
+        # being written + the ones whose reduce-scatter is in flight); acquiring one more first retires the oldest
+        # reduce-scatter (group_sharded_stage3.py:743-805 keeps one full fp32 grad per PARAM alive instead)
+        self.max_live_flat = 2
+        self._rs_queue = []       # units with a reduce-scatter in flight, oldest first
+        self._flat_pool = {}      # numel -> [free fp32 buffers]
+        self._live_flat = 0
+        self.peak_live_flat = 0
+        self.prefetch_depth = 2
         for u in self._units:
             if u.layer is not None:
                 self._hooks.append(u.layer.register_forward_pre_hook(self._make_pre(u)))
@@ -323,6 +349,36 @@ class GroupShardedModel(Layer):
                 if not p.stop_gradient:
                     self._hooks.append(p._t.register_post_accumulate_grad_hook(self._make_grad_hook(u, i)))
 
+    # ------------------------------------------------------------ bounded fp32 grad buffers (N > 1)
+    def _acquire_flat(self, unit):
+        while self._live_flat >= self.max_live_flat and self._rs_queue:
+            self._retire_oldest()
+        pool = self._flat_pool.get(unit.padded)
+        buf = pool.pop() if pool else torch.empty(unit.padded, dtype=torch.float32, device=unit.device)
+        self._live_flat += 1
+        self.peak_live_flat = max(self.peak_live_flat, self._live_flat)
+        return buf
+
+    def _release_flat(self, buf):
+        if buf is not None:
+            self._flat_pool.setdefault(buf.numel(), []).append(buf)
+            self._live_flat -= 1
+
+    def _rs_issued(self, unit):
+        self._rs_queue.append(unit)
+
+    def _retire_oldest(self):
+        u = self._rs_queue.pop(0)
+        self._release_flat(u.retire_rs())
+
+    def _retire_all(self):
+        while self._rs_queue:
+            self._retire_oldest()
+
+    def release_grad_pool(self):
+        """Free the recycled fp32 flat buffers (they are kept across steps by default)."""
+        self._flat_pool.clear()
+
     # ------------------------------------------------------------ hooks
     def _make_pre(self, u):
         def pre(layer, inputs):
@@ -331,9 +387,11 @@ class GroupShardedModel(Layer):
                 if u.idx not in self._order_set():
                     self._order.append(u.idx)
                 if self._prefetch:
-                    nxt = self._next_in_order(u.idx, +1)
-                    if nxt is not None:
-                        nxt.gather(async_op=True)
+                    # prefetch depth 2: the next two units' all-gathers are in flight while this one computes
+                    for d in range(1, self.prefetch_depth + 1):
+                        nxt = self._next_in_order(u.idx, +d)
+                        if nxt is not None:
+                            nxt.gather(async_op=True)
             return None
 
         return pre
@@ -359,7 +417,9 @@ class GroupShardedModel(Layer):
                     if isinstance(t, torch.Tensor) and t.requires_grad:
                         t.register_hook(self._make_bw_pre(u))
                         hooked = True
-                if hooked:
+                # the last unit of the forward is the first of the backward: keep it gathered across the turn
+                last = self._order_done and self._order and u.idx == self._order[-1]
+                if hooked and not last:
                     u.release()
             elif self._stage == 3:
                 u.release()
@@ -374,9 +434,10 @@ class GroupShardedModel(Layer):
                 self._queue_cb()
                 u.wait()
                 if self._prefetch:
-                    prv = self._next_in_order(u.idx, -1)
-                    if prv is not None and not prv.bw_gathered:
-                        prv.gather(async_op=True)
+                    for d in range(1, self.prefetch_depth + 1):
+                        prv = self._next_in_order(u.idx, -d)
+                        if prv is not None and not prv.bw_gathered:
+                            prv.gather(async_op=True)
             return None
 
         return hook
@@ -399,6 +460,8 @@ class GroupShardedModel(Layer):
             u.finish_grads()
             if self._stage == 3:
                 u.release()
+        self._retire_all()
+        self._order_done = True
 
     # ------------------------------------------------------------ module API
     def forward(self, *args, **kwargs):

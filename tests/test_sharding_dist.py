@@ -37,3 +37,35 @@ def test_stage3_checkpoint_resumes_at_other_degree(tmp_path):
     res = run_workers("sharding_ckpt_worker.py", 2, ["resume", "plain", ck])
     for r in res:
         _close(r["losses"], r["ref"])
+
+
+def test_stage3_grad_buffers_bounded_4ranks():
+    """4 gloo ranks, 6 decoder layers, stage 3: at most 2 fp32 flat unit-gradient buffers are ever alive (the one
+    being written + one reduce-scatter in flight), buffers are recycled, and losses / parameters still match the
+    single-process run (reference keeps a full fp32 grad per parameter alive: group_sharded_stage3.py:743-805)."""
+    res = run_workers("sharding_worker.py", 4, ["p_g_os"], extra_env={"PD_TEST_LAYERS": "6"})
+    for r in res:
+        for a, b in zip(r["losses"], r["ref"]):
+            assert abs(a - b) < 1e-3 * max(1.0, abs(b)), (r["losses"], r["ref"])
+        assert abs(r["csum"] - r["csum_ref"]) < 1e-2 * max(1.0, abs(r["csum_ref"]))
+        assert r["peak_live_flat"] is not None and r["peak_live_flat"] <= 2, r["peak_live_flat"]
+        # recycled per unit size (6 equal decoder layers share their buffers), not re-allocated per unit
+        assert r["pool_bufs"] <= 2 * r["unit_sizes"] < 12, (r["pool_bufs"], r["unit_sizes"])
+
+
+def test_stage3_comm_model_llama7b():
+    """Bytes per rank per step of stage 3 at N = 8 for Llama-2-7B: all-gathers of the bf16 flat units (forward and
+    backward, the last unit kept across the turn) and one fp32 reduce-scatter per unit."""
+    from paddle2_amd.distributed.sharding import comm_model as CM
+
+    units, root = CM.llama_units()
+    assert units[0] == 202_383_360 and len(units) == 32          # 7B decoder layer parameters
+    b = CM.stage3_bytes_per_step(units, 8, root_numel=root)
+    layer_ag = 202_383_360 * 2 * 7 / 8
+    assert abs(b["max_unit_ag"] - layer_ag) < 16
+    assert abs(b["ag_bwd"] - 31 * layer_ag) < 1e3
+    assert abs(b["rs"] / b["ag_bwd"] - 2 * (32 * 202_383_360 + root) / (31 * 202_383_360)) < 1e-6
+    assert 40e9 < b["total"] < 50e9                               # ~45 GB per rank per step
+    b16 = CM.stage3_bytes_per_step(units, 8, grad_bytes=2, root_numel=root)
+    assert abs((b["total"] - b16["total"]) - b["rs"] / 2) < 1e3   # bf16 reduce-scatter saves half the RS bytes
+    assert CM.stage3_bytes_per_step(units, 1)["total"] == 0

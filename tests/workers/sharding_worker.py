@@ -18,7 +18,7 @@ level = sys.argv[1]
 steps = 3
 C.init_parallel_env()
 rank, world = C.get_rank(), C.get_world_size()
-cfg = LlamaConfig.tiny(dtype="float32", num_hidden_layers=2)
+cfg = LlamaConfig.tiny(dtype="float32", num_hidden_layers=int(os.environ.get("PD_TEST_LAYERS", "2")))
 
 
 def make():
@@ -45,6 +45,9 @@ for s in range(steps):
     t = loss._t.detach().clone()
     C._all_reduce_torch(t)
     losses.append(float(t) / world)
+peak_live = getattr(m, "peak_live_flat", None)
+pool_bufs = sum(len(v) for v in getattr(m, "_flat_pool", {}).values())
+sizes = len({u.padded for u in getattr(m, "_units", [])})
 sd = m.state_dict()
 csum = float(sum(v._t.double().sum() for v in sd.values()))
 
@@ -59,5 +62,6 @@ for s in range(steps):
     o2.clear_grad()
     ref.append(float(loss))
 csum_ref = float(sum(v._t.double().sum() for v in m2.state_dict().values()))
-write_result({"losses": losses, "ref": ref, "csum": csum, "csum_ref": csum_ref})
+write_result({"losses": losses, "ref": ref, "csum": csum, "csum_ref": csum_ref, "peak_live_flat": peak_live,
+              "pool_bufs": pool_bufs, "unit_sizes": sizes})
 C.destroy_process_group()
