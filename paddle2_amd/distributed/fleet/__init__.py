@@ -4,7 +4,7 @@ from __future__ import annotations
 
 from ... import distributed as _dist  # noqa: F401
 from .. import collective as C
-from .base.distributed_strategy import DistributedStrategy  # noqa: F401
+from .base.distributed_strategy import DistributedStrategy, validate_hybrid_configs  # noqa: F401
 from .base.topology import CommunicateTopology, HybridCommunicateGroup, ParallelMode  # noqa: F401
 
 _state = {"strategy": None, "hcg": None, "initialized": False, "is_collective": True}
@@ -24,6 +24,7 @@ def init(role_maker=None, is_collective=True, strategy=None, log_level="INFO"):
     if not isinstance(strategy, DistributedStrategy):
         raise TypeError("fleet.init: strategy must be a fleet.DistributedStrategy")
     _state["strategy"] = strategy
+    validate_hybrid_configs(strategy)
     C.init_parallel_env()
     world = C.get_world_size()
     hc = strategy.hybrid_configs

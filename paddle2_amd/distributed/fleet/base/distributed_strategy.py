@@ -15,7 +15,9 @@ lists, O2 for ``use_pure_fp16`` / ``use_pure_bf16``), ``recompute`` + ``recomput
 (those sublayers re-run their forward in backward), ``hybrid_configs.sharding_configs.comm_buffer_size_MB``
 (bucket size of the fused gradient collectives), ``pipeline_configs`` (micro-batching, schedule,
 ``enable_partial_send_recv``), ``gradient_merge`` (k-step accumulation in the hybrid optimizer) and
-``find_unused_parameters``.
+``find_unused_parameters``.  Every ``hybrid_configs`` sub-key (mp_configs / pp_configs / sharding_configs) is
+classified in ``KEY_SEMANTICS`` at the bottom of this file: honoured (where) or numerically neutral (why);
+``fleet.init`` rejects non-default values of anything unimplemented (``validate_hybrid_configs``).
 """
 from __future__ import annotations
 
@@ -281,6 +283,9 @@ class DistributedStrategy:
     def __init__(self):
         object.__setattr__(self, "_top", StrategyConfig("DistributedStrategy", _TOP))
         object.__setattr__(self, "_cfg", {k: StrategyConfig(k, s) for k, s in _CONFIGS.items()})
+        # replicated (non-distributed) parameters whose name contains one of these are kept in sync over the mp
+        # group by mp_configs.sync_param / sync_grad / sync_moment (reference distributed_strategy.py:330)
+        object.__setattr__(self, "sync_param_name", ["embedding", "layer_norm", ".b_"])
 
     # attribute access: top-level switches and *_configs messages
     def __getattr__(self, k):
@@ -293,9 +298,14 @@ class DistributedStrategy:
         raise AttributeError(f"DistributedStrategy has no attribute {k!r}")
 
     def __setattr__(self, k, v):
-        if k in _CONFIGS:
+        if k == "sync_param_name":
+            object.__setattr__(self, k, [str(x) for x in v])
+        elif k in _CONFIGS:
             if not isinstance(v, dict):
                 raise TypeError(f"{k} must be assigned a dict")
+            if k == "hybrid_configs" and isinstance(v.get("mp_configs"), dict) and "sync_param_name" in v["mp_configs"]:
+                v = dict(v, mp_configs=dict(v["mp_configs"]))   # reference :1940 pops it out of mp_configs
+                object.__setattr__(self, "sync_param_name", [str(x) for x in v["mp_configs"].pop("sync_param_name")])
             self._cfg[k].update(v)  # the reference merges assigned dicts into the proto message
         elif k in _TOP:
             self._top[k] = v
@@ -306,6 +316,7 @@ class DistributedStrategy:
         out = DistributedStrategy()
         object.__setattr__(out, "_top", copy.deepcopy(self._top, memo))
         object.__setattr__(out, "_cfg", {k: copy.deepcopy(v, memo) for k, v in self._cfg.items()})
+        object.__setattr__(out, "sync_param_name", list(self.sync_param_name))
         return out
 
     # ------------------------------------------------------------ prototxt (reference :382 / :404)
@@ -362,3 +373,59 @@ class DistributedStrategy:
     def __repr__(self):
         on = [k for k, (t, d) in _TOP.items() if t is _B and self._top[k] and not d]
         return f"DistributedStrategy(enabled={on}, hybrid_configs={dict(self.hybrid_configs)})"
+
+
+# What each hybrid_configs sub-key does here.  "honoured": implemented with the reference's numerics (where);
+# "perf": a scheduling / memory knob whose numerics are unchanged — the MI355X path either always does the
+# optimisation or does not need it (why).  fleet.init rejects a non-default value of any key listed in
+# _UNSUPPORTED; tests/test_distributed_strategy.py checks that every schema key is classified here.
+KEY_SEMANTICS = {
+    "mp_configs": {
+        "sync_param": ("honoured", "HybridParallelOptimizer: sync_param_name params broadcast/averaged over mp after step"),
+        "sync_grad": ("honoured", "HybridParallelOptimizer: sync_param_name grads synced over mp before step"),
+        "sync_moment": ("honoured", "HybridParallelOptimizer: Adam moments of sync_param_name params synced after step"),
+        "sync_mode": ("honoured", "broadcast (from mp rank 0) or average, for the three syncs above"),
+        "mp_async_allreduce": ("perf", "column-parallel dX all-reduce is issued before the dW GEMM in backward anyway"),
+        "mp_skip_c_identity": ("perf", "the identity op is a no-op autograd Function here; nothing to skip"),
+        "mp_fused_linear_param_grad_add": ("perf", "wgrad GEMM always accumulates into the fp32 main grad in its "
+                                                   "epilogue (csrc/kernels/gemm.hip)"),
+        "need_broadcast_data": ("honoured", "TensorParallel broadcasts the inputs from mp rank 0 before forward"),
+        "recompute_allgather": ("perf", "sequence-parallel all-gather outputs are recomputed, not stored, in "
+                                        "recompute; same values"),
+        "sp_async_reduce_scatter": ("perf", "sequence-parallel reduce-scatter runs on the comm stream; same values"),
+    },
+    "pp_configs": {
+        "dp_comm_overlap": ("honoured", "HybridParallelOptimizer: FusedCommBuffer all-reduce from gradient hooks"),
+        "delay_scale_loss": ("honoured", "PipelineParallel: micro-batch losses unscaled, grads scaled by "
+                                         "1/accumulate_steps before the step"),
+        "enable_timer": ("perf", "timers only; see paddle2_amd.profiler"),
+        "sharding_comm_overlap": ("honoured", "DygraphShardingOptimizerV2 reduce-scatter from gradient hooks"),
+        "profiling": ("perf", "timers only"),
+        "release_gradients": ("perf", "gradient buffers are views into persistent comm buffers"),
+        "overlap_p2p_comm": ("perf", "pipeline p2p is always asynchronous (isend/irecv) here"),
+        "clear_every_step_cache": ("perf", "no p2p shape cache is kept between steps"),
+        "use_batch_p2p_comm": ("perf", "p2p ops of one schedule slot are always batched"),
+        "best_unbalanced_scheduler": ("perf", "schedule order only; same gradients"),
+    },
+    "sharding_configs": {
+        "tensor_fusion": ("perf", "V1 always reduces through one flat buffer per dtype"),
+        "accumulate_steps": ("honoured", "V2 / dp hooks communicate after this many backward passes"),
+        "comm_overlap": ("honoured", "V2 reduce-scatter from gradient hooks (V1: raises)"),
+        "split_param": ("honoured", "DygraphShardingOptimizerV2"),
+        "fuse_optimizer": ("perf", "the optimizers use multi-tensor updates anyway"),
+        "use_reduce_avg": ("honoured", "V2 / dp hooks: AVG reduce on RCCL, SUM + scale otherwise"),
+        "comm_buffer_size_MB": ("honoured", "V2 / dp-hook bucket size"),
+        "release_gradients": ("perf", "gradient buffers are views into persistent comm buffers"),
+        "free_grads_in_comm": ("perf", "gradient buffers are views into persistent comm buffers"),
+    },
+}
+_UNSUPPORTED = {}   # (section, key) -> reason; empty: every key above is honoured or numerically neutral
+
+
+def validate_hybrid_configs(strategy):
+    """Raise NotImplementedError for a non-default value of a key that is not implemented (none today)."""
+    hc = strategy.hybrid_configs
+    for (sec, key), why in _UNSUPPORTED.items():
+        dflt = _HYBRID[sec][0][key][1]
+        if hc[sec][key] != dflt:
+            raise NotImplementedError(f"hybrid_configs.{sec}.{key}={hc[sec][key]!r}: {why}")

@@ -18,10 +18,13 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from .....framework.param import Parameter
 from .....framework.tensor import Tensor
 from .....nn.clip import ClipGradByGlobalNorm
 from ...utils.hybrid_parallel_util import _grad_tensor, fused_allreduce_gradients, \
     fused_allreduce_gradients_with_group
+from ...base.topology import ParallelMode
+from ...utils.tensor_fusion_helper import HOOK_ACTION, FusedCommBuffer, _aligned_numel, assign_group_by_size
 
 _wrap = Tensor._wrap
 
@@ -186,19 +189,200 @@ class DygraphShardingOptimizer:
         return getattr(self._inner_opt, name)
 
 
+_DONE = object()   # marker: the bucket's reduction already completed synchronously
+
+
+class _SplitParamBuffer:
+    """One fused buffer of DygraphShardingOptimizerV2 (reference tensor_fusion_helper.py:384 FusedCommBuffer with
+    split parameters): the parameters of a <= comm_buffer_size_MB bucket live in ONE flat param buffer and their
+    gradients in ONE flat grad buffer (both views, 256-B aligned slots, padded to a multiple of the group size).
+    Rank r owns elements [r*S, (r+1)*S) of both: one reduce-scatter gives it the averaged gradient of exactly
+    what it updates, one all-gather redistributes the updated parameters.  ``slices`` are the optimizer-facing
+    Parameters: one per (parameter x owned range) overlap, a view into the param buffer whose .grad is a view into
+    the owned reduced-gradient shard — a parameter may be split between two ranks."""
+
+    def __init__(self, params, group, acc_steps, overlap, use_reduce_avg):
+        self.params = list(params)
+        self.group = group
+        self.N, self.rank = group.nranks, group.rank
+        ts = [p._t for p in self.params]
+        self.dtype, self.device = ts[0].dtype, ts[0].device
+        self.offs, total = [], 0
+        for t in ts:
+            self.offs.append(total)
+            total += _aligned_numel(t.numel(), self.dtype)
+        unit = _aligned_numel(1, self.dtype)
+        total = -(-total // (self.N * unit)) * (self.N * unit)
+        self.total, self.S = total, total // self.N
+        self.pbuf = torch.zeros(total, dtype=self.dtype, device=self.device)
+        self.gbuf = torch.zeros(total, dtype=self.dtype, device=self.device)
+        self.gshard = torch.zeros(self.S, dtype=self.dtype, device=self.device)
+        with torch.no_grad():
+            for t, o in zip(ts, self.offs):
+                self.pbuf[o:o + t.numel()].copy_(t.detach().reshape(-1))
+                t.data = self.pbuf[o:o + t.numel()].view(t.shape)
+        self.bind_grads()
+        lo, hi = self.rank * self.S, (self.rank + 1) * self.S
+        self.slices = []
+        for p, t, o in zip(self.params, ts, self.offs):
+            a, b = max(o, lo), min(o + t.numel(), hi)
+            if a >= b:
+                continue
+            sp = Parameter(self.pbuf[a:b], name=p.name, trainable=not p.stop_gradient,
+                           optimize_attr=dict(getattr(p, "optimize_attr", {"learning_rate": 1.0})),
+                           regularizer=getattr(p, "regularizer", None), need_clip=getattr(p, "need_clip", True),
+                           is_distributed=getattr(p, "is_distributed", False))
+            sp._t.data = self.pbuf[a:b]          # share storage with the full parameter's slot
+            sp._t.grad = self.gshard[a - lo:b - lo]
+            sp._origin = p
+            self.slices.append(sp)
+        self.acc_steps = max(1, int(acc_steps))
+        self.use_avg = use_reduce_avg
+        self._hits = {}
+        self._ready = 0
+        self._task = None
+        self._reduced = False
+        self._scale = False
+        if overlap:
+            for p, o in zip(self.params, self.offs):
+                if not p.stop_gradient:
+                    p._t.register_post_accumulate_grad_hook(self._make_hook(p, o))
+
+    def bind_grads(self):
+        """Every parameter's .grad is its slot of the flat grad buffer (autograd accumulates in place); a
+        gradient that was replaced meanwhile (set to None and recreated) is first added into the slot."""
+        for p, o in zip(self.params, self.offs):
+            self._bind(p._t, o)
+
+    def _bind(self, t, o):
+        slot = self.gbuf[o:o + t.numel()]
+        g = t.grad
+        if g is None or g.data_ptr() != slot.data_ptr():
+            if g is not None:
+                slot.add_(g.reshape(-1).to(slot.dtype))
+            t.grad = slot.view(t.shape)
+
+    def _make_hook(self, p, o):
+        key = id(p)
+        n_train = sum(1 for q in self.params if not q.stop_gradient)
+
+        def hook(t):
+            self._bind(t, o)
+            c = self._hits.get(key, 0) + 1
+            self._hits[key] = c
+            if c == self.acc_steps:
+                self._ready += 1
+                if self._ready == n_train:   # the bucket's last gradient of the last micro-step: communicate now
+                    self.reduce_scatter(async_op=True)
+        return hook
+
+    def reduce_scatter(self, async_op=False):
+        if self._task is not None or self._reduced:
+            return
+        self.bind_grads()
+        if self.N == 1:
+            self.gshard.copy_(self.gbuf)
+            self._task = _DONE
+            return
+        avg = self.use_avg and self.group.backend == "nccl"
+        self._scale = not avg
+        self._task = dist.reduce_scatter_tensor(self.gshard, self.gbuf, op=dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM,
+                                                group=self.group.pg, async_op=True)
+        if not async_op:
+            self.wait()
+
+    def wait(self):
+        if self._task is not None:
+            if self._task is not _DONE:
+                self._task.wait()
+            self._task = None
+            if self._scale:
+                self.gshard.div_(self.N)
+                self._scale = False
+
+    def all_gather_params(self):
+        if self.N == 1:
+            return
+        mine = self.pbuf[self.rank * self.S:(self.rank + 1) * self.S].clone()
+        dist.all_gather_into_tensor(self.pbuf, mine, group=self.group.pg)
+
+    def zero_grad(self):
+        self.wait()
+        self.gbuf.zero_()
+        self.gshard.zero_()
+        self._hits.clear()
+        self._ready = 0
+        self._reduced = False
+        for p, o in zip(self.params, self.offs):
+            p._t.grad = self.gbuf[o:o + p._t.numel()].view(p._t.shape)
+
+
+class DygraphShardingOptimizerV2:
+    """ZeRO stage 1 with split parameters (reference dygraph_sharding_optimizer.py:586 DygraphShardingOptimizerV2,
+    strategy ``sharding_configs.split_param``).  Parameters go, in reverse model order (the order their gradients
+    arrive), into buckets of at most ``comm_buffer_size_MB``; each bucket is a _SplitParamBuffer.  The wrapped
+    optimizer steps only this rank's slices; with ``comm_overlap`` a bucket's reduce-scatter is issued by the
+    gradient hook of its last parameter in the last of ``accumulate_steps`` backward passes (overlapping the rest
+    of the backward), otherwise at step time.  After the step one all-gather per bucket refreshes the params."""
+
+    def __init__(self, optimizer, hcg, comm_buffer_size_MB=256, comm_overlap=False, accumulate_steps=1,
+                 use_reduce_avg=True):
+        self._inner_opt = optimizer
+        self._hcg = hcg
+        self._group = hcg.get_sharding_parallel_group()
+        self._nranks, self._rank = self._group.nranks, self._group.rank
+        self._all_params = list(optimizer._parameter_list)
+        train = [p for p in self._all_params if not p.stop_gradient]
+        groups = assign_group_by_size(list(reversed(train)), int(float(comm_buffer_size_MB) * (1 << 20)))
+        self._buffers = [_SplitParamBuffer(ps, self._group, accumulate_steps, comm_overlap, use_reduce_avg)
+                         for _, ps in sorted(groups.items())]
+        # the inner optimizer now owns the slices, grouped like their source parameters (weight decay, lr ratio)
+        gid = {id(p): i for i, g in enumerate(optimizer._param_groups) for p in g["params"]}
+        new_groups = [dict(g, params=[]) for g in optimizer._param_groups]
+        for b in self._buffers:
+            for sp in b.slices:
+                new_groups[gid.get(id(sp._origin), 0)]["params"].append(sp)
+        optimizer._param_groups = new_groups
+        optimizer._parameter_list = [p for g in new_groups for p in g["params"]]
+        optimizer._mt_cache = None
+        self._rank2params = {self._rank: list(optimizer._parameter_list)}
+
+    def reduce_gradients(self, parameter_list=None, hcg=None):
+        for b in self._buffers:
+            if not b._reduced:
+                b.reduce_scatter(async_op=True)   # no-op for buckets the overlap hooks already launched
+        for b in self._buffers:
+            b.wait()
+            b._reduced = True
+
+    def owned_grads(self):
+        return [b.gshard for b in self._buffers]
+
+    @torch.no_grad()
+    def step(self):
+        self._inner_opt.step()
+        for b in self._buffers:
+            b.all_gather_params()
+
+    def clear_grad(self, set_to_zero=True):
+        for b in self._buffers:
+            b.zero_grad()
+
+    clear_gradients = clear_grad
+
+    def __getattr__(self, name):
+        return getattr(self._inner_opt, name)
+
+
 class HybridParallelOptimizer:
     def __init__(self, optimizer, hcg, strategy):
         self._hcg = hcg
         self._strategy = strategy
         self._sharding = hcg.get_sharding_parallel_world_size() > 1
-        self._inner_opt = DygraphShardingOptimizer(optimizer, hcg) if self._sharding else optimizer
-        self._base_opt = optimizer
-        clip = optimizer._grad_clip
-        if isinstance(clip, ClipGradByGlobalNorm) and not isinstance(clip, HybridParallelClipGrad):
-            optimizer._grad_clip = HybridParallelClipGrad(clip, hcg, sharded=self._sharding)
-        self._all_params = list(self._inner_opt._all_params) if self._sharding else list(optimizer._parameter_list)
-        self._dp_enable = hcg.get_data_parallel_world_size() > 1
-        self._sep_enable = hcg.get_sep_parallel_world_size() > 1
+        hc = strategy.hybrid_configs if strategy is not None else None
+        sc = dict(hc["sharding_configs"]) if hc is not None else {}
+        pc = dict(hc["pp_configs"]) if hc is not None else {}
+        mpc = dict(hc["mp_configs"]) if hc is not None else {}
         # strategy knobs: fused dp all-reduce bucket (fuse_grad_size_in_MB), gradient merge (k-step
         # accumulation; avg divides the merged grads by k)
         self._dp_bucket_mb = int(getattr(strategy, "fuse_grad_size_in_MB", 32)) if strategy is not None else 32
@@ -206,6 +390,90 @@ class HybridParallelOptimizer:
         self._gm_k = int(strategy.gradient_merge_configs["k_steps"]) if gm else 1
         self._gm_avg = bool(strategy.gradient_merge_configs["avg"]) if gm else True
         self._gm_count = 0
+        # backward passes per optimizer step: the gradient hooks communicate after the last of them
+        pipe_acc = int(strategy.pipeline_configs["accumulate_steps"]) if (
+            strategy is not None and hcg.get_pipe_parallel_world_size() > 1) else 1
+        acc = max(pipe_acc, int(sc.get("accumulate_steps", 1))) * self._gm_k
+        self._delay_scale = pipe_acc if bool(pc.get("delay_scale_loss", False)) else 1
+        # sharding_configs: split_param -> V2 (flat split-parameter buffers of comm_buffer_size_MB), comm_overlap
+        # (or pp_configs.sharding_comm_overlap) -> reduce-scatter from gradient hooks, use_reduce_avg
+        self._split = self._sharding and bool(sc.get("split_param", False))
+        if self._split:
+            overlap = bool(sc.get("comm_overlap", False)) or bool(pc.get("sharding_comm_overlap", False))
+            self._inner_opt = DygraphShardingOptimizerV2(optimizer, hcg, float(sc.get("comm_buffer_size_MB", 256)),
+                                                         overlap, acc, bool(sc.get("use_reduce_avg", True)))
+        elif self._sharding:
+            if bool(sc.get("comm_overlap", False)) or bool(pc.get("sharding_comm_overlap", False)):
+                raise NotImplementedError("sharding comm_overlap needs sharding_configs.split_param=True "
+                                          "(DygraphShardingOptimizerV2); stage-1 V1 reduces at step time")
+            self._inner_opt = DygraphShardingOptimizer(optimizer, hcg)
+        else:
+            self._inner_opt = optimizer
+        self._base_opt = optimizer
+        # mp_configs sync_grad / sync_param / sync_moment with sync_mode broadcast | average (reference
+        # hybrid_parallel_optimizer.py:399 _step): replicated params named like strategy.sync_param_name
+        self._mp_cfg = {k: mpc.get(k, d) for k, d in (("sync_grad", False), ("sync_param", True),
+                                                      ("sync_moment", False), ("sync_mode", "broadcast"))}
+        if self._mp_cfg["sync_mode"] not in ("broadcast", "average"):
+            raise ValueError(f"mp_configs.sync_mode must be 'broadcast' or 'average', got {self._mp_cfg['sync_mode']!r}")
+        self._sync_names = list(getattr(strategy, "sync_param_name", ["embedding", "layer_norm", ".b_"])) \
+            if strategy is not None else []
+        clip = optimizer._grad_clip
+        if isinstance(clip, ClipGradByGlobalNorm) and not isinstance(clip, HybridParallelClipGrad):
+            optimizer._grad_clip = HybridParallelClipGrad(clip, hcg, sharded=self._sharding)
+        self._all_params = list(self._inner_opt._all_params) if self._sharding else list(optimizer._parameter_list)
+        # pure data parallelism: the DataParallel wrapper's reducer already all-reduces in backward (reference
+        # hybrid_parallel_optimizer.py: _dp_enable = not use_dp_mode and need_dp) — never reduce twice
+        self._dp_enable = (hcg.get_data_parallel_world_size() > 1
+                           and hcg.get_parallel_mode() != ParallelMode.DATA_PARALLEL)
+        self._sep_enable = hcg.get_sep_parallel_world_size() > 1
+        # pp_configs.dp_comm_overlap: data-parallel gradient buckets all-reduced from gradient hooks during the last
+        # micro-batch's backward (reference pipeline_parallel.py:305-312 / :466-544 FusedCommBuffer hooks)
+        self._dp_buffers = []
+        if bool(pc.get("dp_comm_overlap", False)) and self._dp_enable and not self._sharding:
+            dpg = hcg.get_data_parallel_group()
+            mb = float(sc.get("comm_buffer_size_MB", 256))
+            params = [p for p in self._all_params if not p.stop_gradient]
+            for gi, ps in sorted(assign_group_by_size(list(reversed(params)), int(mb * (1 << 20))).items()):
+                buf = FusedCommBuffer(gi, ps, dpg, acc_steps=acc, act=HOOK_ACTION.ALL_REDUCE, use_main_grad=False,
+                                      scale_after_comm=True, use_reduce_avg=bool(sc.get("use_reduce_avg", True)))
+                for p in ps:
+                    p._t.register_post_accumulate_grad_hook(lambda t, b=buf, p=p: b.add_grad(p))
+                self._dp_buffers.append(buf)
+
+    def _mp_sync_params(self):
+        if self._hcg.get_model_parallel_world_size() <= 1 or not self._sync_names:
+            return []
+        ps = [p for p in self._all_params if not getattr(p, "is_distributed", False)
+              and any(n in p.name for n in self._sync_names)]
+        return sorted(ps, key=lambda p: p.name)
+
+    def _mp_sync(self, t):
+        mp = self._hcg.get_model_parallel_group()
+        if self._mp_cfg["sync_mode"] == "broadcast":
+            dist.broadcast(t, src=self._hcg.get_model_parallel_group_src_rank(), group=mp.pg)
+        else:
+            dist.all_reduce(t, group=mp.pg)
+            t.div_(mp.nranks)
+
+    def _mp_sync_after_step(self):
+        ps = self._mp_sync_params()
+        if not ps:
+            return
+        opt = self._base_opt
+        with torch.no_grad():
+            for p in ps:
+                if self._mp_cfg["sync_param"]:
+                    self._mp_sync(p._t.data)
+                    mw = getattr(opt, "_master_weights", {}).get(p.name)
+                    if mw is not None:
+                        self._mp_sync(mw)
+                if self._mp_cfg["sync_moment"]:
+                    accs = getattr(opt, "_accumulators", {})
+                    for acc in ("moment1", "moment2"):
+                        m = accs.get(acc, {}).get(p.name)
+                        if m is not None:
+                            self._mp_sync(m)
 
     def _sp_params(self):
         return [p for p in self._all_params if getattr(p, "sequence_parallel", False)]
@@ -220,11 +488,33 @@ class HybridParallelOptimizer:
             for g in grads:
                 if g is not None:
                     dist.all_reduce(g, group=mp.pg)
+        if self._mp_cfg["sync_grad"]:
+            for p in self._mp_sync_params():
+                g = _grad_tensor(p)
+                if g is not None:
+                    self._mp_sync(g)
         if self._sharding:
             self._inner_opt.reduce_gradients(self._all_params, hcg)
             if self._dp_enable or self._sep_enable:
-                owned = self._inner_opt._rank2params[self._inner_opt._rank]
-                fused_allreduce_gradients(owned, hcg, self._dp_bucket_mb)
+                if self._split:
+                    # the owned reduced shards are flat: one dp(+sep) all-reduce per bucket
+                    grp = hcg.get_data_sep_parallel_group() if self._sep_enable else hcg.get_data_parallel_group()
+                    for g in self._inner_opt.owned_grads():
+                        dist.all_reduce(g, group=grp.pg)
+                        g.div_(grp.nranks)
+                else:
+                    owned = self._inner_opt._rank2params[self._inner_opt._rank]
+                    fused_allreduce_gradients(owned, hcg, self._dp_bucket_mb)
+        elif self._dp_buffers:
+            for b in self._dp_buffers:
+                if b._task is None and not b._all_params_checked_in():
+                    # the hooks did not launch it (a parameter got no gradient this step): communicate now
+                    for i, p in enumerate(b._params):
+                        g = p._t.grad
+                        if g is not None and g.data_ptr() != b._slot(i).data_ptr():
+                            b.add_grad(p, use_comm=False)
+                    b._comm_grads()
+                b.scale_grads()
         elif self._dp_enable or self._sep_enable:
             fused_allreduce_gradients(self._all_params, hcg, self._dp_bucket_mb)
 
@@ -235,13 +525,17 @@ class HybridParallelOptimizer:
             self._gm_count += 1
             if self._gm_count % self._gm_k:
                 return
-            if self._gm_avg:
-                for p in self._all_params:
-                    g = _grad_tensor(p)
-                    if g is not None:
-                        g.div_(self._gm_k)
         self._hybrid_sync_grad()
+        # gradient-merge average and pipeline delay_scale_loss; linear, so scaling the reduced grads == scaling
+        # before the reduce (and it cannot race a reduction the gradient hooks launched)
+        div = (self._gm_k if self._gm_avg else 1) * self._delay_scale
+        if div > 1:
+            grads = self._inner_opt.owned_grads() if self._split else [_grad_tensor(p) for p in self._all_params]
+            for g in grads:
+                if g is not None:
+                    g.div_(div)
         self._inner_opt.step()
+        self._mp_sync_after_step()
 
     def minimize(self, loss, startup_program=None, parameters=None, no_grad_set=None):
         self.step()
@@ -251,6 +545,8 @@ class HybridParallelOptimizer:
         if self._gm_k > 1 and self._gm_count % self._gm_k:
             return  # still merging gradients
         self._inner_opt.clear_grad(set_to_zero)
+        for b in self._dp_buffers:
+            b._clear_grad_storage()
 
     clear_gradients = clear_grad
 

@@ -202,6 +202,10 @@ class PipelineParallel(MetaParallelBase):
         pc = dict(strategy.pipeline_configs) if strategy is not None else {}
         self.accumulate_steps = int(pc.get("accumulate_steps", 1))
         self.micro_batch_size = int(pc.get("micro_batch_size", 1))
+        # pp_configs.delay_scale_loss: backward the raw micro-batch losses; the optimizer scales the reduced
+        # gradients by 1/accumulate_steps once (HybridParallelOptimizer)
+        ppc = strategy.hybrid_configs["pp_configs"] if strategy is not None else {}
+        self._delay_scale_loss = bool(ppc.get("delay_scale_loss", False))
         self.num_stages = hcg.get_pipe_parallel_world_size()
         self.stage_id = hcg.get_stage_id()
         self.pp_group = hcg.get_pipe_parallel_group()
@@ -393,7 +397,7 @@ class PipelineParallel(MetaParallelBase):
                                 loss_t = loss._t if isinstance(loss, Tensor) else loss
                                 losses.append(loss_t.detach().float())
                                 if not forward_only:
-                                    act_out[(vs, mb)] = (loss_t / M,)
+                                    act_out[(vs, mb)] = (loss_t if self._delay_scale_loss else loss_t / M,)
                             else:
                                 outputs.append(y)
                                 if not forward_only:

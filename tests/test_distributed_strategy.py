@@ -161,3 +161,23 @@ def test_reference_flags_registered_and_effects():
     finally:
         paddle.set_flags({"FLAGS_benchmark_nccl": False})
     assert C.comm_benchmark_stats().get("barrier", [0])[0] >= 1
+
+
+def test_every_hybrid_subconfig_key_is_classified():
+    """honour-or-reject: each mp/pp/sharding sub-key is either implemented or documented as numerically neutral."""
+    from paddle2_amd.distributed.fleet.base import distributed_strategy as ds
+
+    for sec, schema in (("mp_configs", ds._MP), ("pp_configs", ds._PP), ("sharding_configs", ds._DYSHARD)):
+        table = ds.KEY_SEMANTICS[sec]
+        assert set(table) == set(schema), (sec, set(schema) ^ set(table))
+        for k, (kind, why) in table.items():
+            assert kind in ("honoured", "perf") and why, (sec, k)
+
+
+def test_sync_param_name_popped_from_mp_configs():
+    from paddle2_amd.distributed.fleet import DistributedStrategy
+
+    s = DistributedStrategy()
+    assert s.sync_param_name == ["embedding", "layer_norm", ".b_"]
+    s.hybrid_configs = {"mp_configs": {"sync_param_name": ["norm"], "sync_grad": True}}
+    assert s.sync_param_name == ["norm"] and s.hybrid_configs["mp_configs"]["sync_grad"] is True

@@ -29,6 +29,35 @@ def test_fleet_sharding_stage1_matches_single():
         assert abs(r["csum"] - r["csum_ref"]) < 1e-2 * max(1.0, abs(r["csum_ref"]))
 
 
+@pytest.mark.parametrize("variant", ["v1", "v2", "v2ov", "dp2sh2", "dpgm"])
+def test_sharding_v2_and_comm_overlap_match_single(variant):
+    """Sharding V2 (split_param buckets, reduce-scatter from gradient hooks, gradient merge) and the dp hook
+    all-reduce == one process accumulating the global batch (4 gloo ranks)."""
+    res = run_workers("hybrid_worker.py", 4, ["shv2", variant])
+    _close(res)
+    for r in res:
+        assert abs(r["csum"] - r["csum_ref"]) < 1e-3 * max(1.0, abs(r["csum_ref"])), r
+        assert r["v2"] == (variant in ("v2", "v2ov", "dp2sh2")), r
+        if variant not in ("v1", "dpgm"):
+            assert r["buckets"] > 1, r   # several buckets: parameters split over buckets and ranks
+
+
+@pytest.mark.parametrize("kind", ["dp", "sh", "dly"])
+def test_pipeline_grad_comm_overlap_matches_accumulation(kind):
+    """pp 2 x dp 2 (dp_comm_overlap; dly: + delay_scale_loss) and pp 2 x sharding 2 (V2 + sharding_comm_overlap)
+    == grad accumulation."""
+    _close(run_workers("hybrid_worker.py", 4, ["pp_hybrid", kind]), 1e-4)
+
+
+@pytest.mark.parametrize("sync_mode", ["broadcast", "average"])
+def test_mp_sync_param_grad_moment(sync_mode):
+    for r in run_workers("hybrid_worker.py", 2, ["mpsync", sync_mode]):
+        assert r["w_equal"] and r["m_equal"] and r["u_differ"], r
+        assert r["bcast_input"] == 1.0, r
+        if sync_mode == "average":
+            assert r["w_ref_diff"] < 1e-5, r
+
+
 def test_moe_expert_parallel_matches_single():
     for r in run_workers("hybrid_worker.py", 2, ["moe"]):
         assert r["out_diff"] < 1e-5 and r["xg_diff"] < 1e-5 and r["eg"] < 1e-4, r

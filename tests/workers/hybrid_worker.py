@@ -373,6 +373,203 @@ def run_gpt_sp():
     write_result({"losses": sp, "ref": ref})
 
 
+def _llama_ref_run(cfg, data, k, make):
+    """single process: every step accumulates k micro-batches of the GLOBAL batch (loss / k)"""
+    m, o = make()
+    ref = []
+    for s in range(len(data)):
+        tot = 0.0
+        for j in range(k):
+            ids = paddle.Tensor._wrap(data[s][j])
+            loss = m(ids[:, :-1], labels=ids[:, 1:]) / k
+            loss.backward()
+            tot += float(loss)
+        o.step()
+        o.clear_grad()
+        ref.append(tot)
+    return ref, m
+
+
+def run_shv2(variant):
+    """Sharding V2 (split_param) / dp gradient-hook overlap vs. a single process (4 ranks).
+    v2:     sharding 4, split_param, 64 KiB buckets (parameters split across ranks), reduce at step
+    v2ov:   + comm_overlap (reduce-scatter from gradient hooks) and gradient merge k=2
+    dp2sh2: dp 2 x sharding 2, split_param + comm_overlap (owned shards all-reduced over dp)
+    dpgm:   dp 4 (DataParallel reducer only), gradient merge k=2
+    v1:     sharding 4, V1 (whole-parameter ownership) — the V2 == V1 anchor"""
+    from paddle2_amd.models import LlamaConfig, LlamaForCausalLM
+
+    dp = {"v2": 1, "v2ov": 1, "dp2sh2": 2, "dpgm": 4, "v1": 1}[variant]
+    sh = world // dp
+    k = 2 if variant in ("v2ov", "dpgm") else 1
+    strategy = fleet.DistributedStrategy()
+    strategy.hybrid_configs = {
+        "dp_degree": dp, "mp_degree": 1, "pp_degree": 1, "sharding_degree": sh,
+        "sharding_configs": {"split_param": variant != "v1", "comm_buffer_size_MB": 1,
+                             "comm_overlap": variant in ("v2ov", "dp2sh2")},
+        "pp_configs": {"dp_comm_overlap": variant == "dpgm"}}   # ignored without pp: the reducer overlaps
+    if k > 1:
+        strategy.gradient_merge = True
+        strategy.gradient_merge_configs = {"k_steps": k, "avg": True}
+    fleet.init(is_collective=True, strategy=strategy)
+    cfg = LlamaConfig.tiny(dtype="float32", num_hidden_layers=2)
+
+    def make():
+        paddle.seed(7)
+        m = LlamaForCausalLM(cfg)
+        o = paddle.optimizer.AdamW(1e-2, parameters=m.parameters(), weight_decay=0.01,
+                                   grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
+        return m, o
+
+    g = torch.Generator().manual_seed(99)
+    # data[s][j]: global micro-batch j of step s; rank r (data-parallel index over dp x sharding) takes rows 2r:2r+2
+    data = [[torch.randint(0, cfg.vocab_size, (world * 2, 33), generator=g) for _ in range(k)] for _ in range(steps)]
+    m, o = make()
+    m = fleet.distributed_model(m)
+    o = fleet.distributed_optimizer(o)
+    from paddle2_amd.distributed.fleet.meta_optimizers.dygraph_optimizer.hybrid_parallel_optimizer import \
+        DygraphShardingOptimizerV2
+    info = {"v2": isinstance(o._inner_opt, DygraphShardingOptimizerV2),
+            "buckets": len(getattr(o._inner_opt, "_buffers", [])) or len(o._dp_buffers)}
+    losses = []
+    for s in range(steps):
+        tot = 0.0
+        for j in range(k):
+            ids = paddle.Tensor._wrap(data[s][j][rank * 2:(rank + 1) * 2])
+            loss = m(ids[:, :-1], labels=ids[:, 1:])
+            loss.backward()
+            o.step()
+            o.clear_grad()
+            t = loss._t.detach().clone()
+            C._all_reduce_torch(t)
+            tot += float(t) / world / k
+        losses.append(tot)
+    csum = float(sum(p._t.double().sum() for p in m.parameters()))
+    ref, m2 = _llama_ref_run(cfg, data, k, make)
+    csum_ref = float(sum(p._t.double().sum() for p in m2.parameters()))
+    write_result({"losses": losses, "ref": ref, "csum": csum, "csum_ref": csum_ref, **info})
+
+
+def run_pp_hybrid(kind):
+    """pp 2 x (dp 2 with dp_comm_overlap | sharding 2 V2 with sharding_comm_overlap): the pipeline's per-micro-batch
+    backward fires the gradient hooks; communication happens after the last micro-batch == grad accumulation"""
+    from paddle2_amd.distributed.fleet.meta_parallel import LayerDesc, PipelineLayer
+
+    M, MB = 4, 2
+    strategy = fleet.DistributedStrategy()
+    hc = {"dp_degree": 1, "mp_degree": 1, "pp_degree": 2, "sharding_degree": 1,
+          "pp_configs": {"dp_comm_overlap": kind in ("dp", "dly"), "sharding_comm_overlap": kind == "sh",
+                         "delay_scale_loss": kind == "dly"}}
+    if kind in ("dp", "dly"):
+        hc["dp_degree"] = 2
+    else:
+        hc["sharding_degree"] = 2
+        hc["sharding_configs"] = {"split_param": True, "comm_buffer_size_MB": 1}
+    strategy.hybrid_configs = hc
+    strategy.pipeline_configs = {"accumulate_steps": M, "micro_batch_size": MB}
+    fleet.init(is_collective=True, strategy=strategy)
+    hcg = fleet.get_hybrid_communicate_group()
+    didx = hcg.get_data_parallel_rank() if kind in ("dp", "dly") else hcg.get_sharding_parallel_rank()
+    H, Cn, L = 16, 5, 4
+    loss_fn = lambda out, lab: paddle.nn.functional.cross_entropy(out, lab)  # noqa: E731
+    descs = [LayerDesc(Blk, H) for _ in range(L)] + [LayerDesc(Head, H, Cn)]
+    paddle.seed(11)
+    ref_layers = [Blk(H) for _ in range(L)] + [Head(H, Cn)]
+    ref_sd = [l.state_dict() for l in ref_layers]
+    pl = PipelineLayer(descs, loss_fn=loss_fn, seg_method="uniform")
+    for c, vs in enumerate(pl._chunk_vstages):
+        lo = pl.segment_parts[vs]
+        for i, item in enumerate(pl._model_chunks[c]._items):
+            item.set_state_dict(ref_sd[lo + i])
+    model = fleet.distributed_model(pl)
+    opt = fleet.distributed_optimizer(paddle.optimizer.AdamW(0.05, parameters=model.parameters()))
+    g = torch.Generator().manual_seed(2)
+    D = 2
+    xs = [torch.randn(D * M * MB, 3, H, generator=g) for _ in range(steps)]
+    ys = [torch.randint(0, Cn, (D * M * MB, 3), generator=g) for _ in range(steps)]
+    lo, hi = didx * M * MB, (didx + 1) * M * MB
+    losses = []
+    for s in range(steps):
+        loss = model.train_batch([paddle.Tensor._wrap(xs[s][lo:hi]), paddle.Tensor._wrap(ys[s][lo:hi])], opt)
+        t = loss._t.detach().clone().reshape(1)
+        C._all_reduce_torch(t)
+        losses.append(float(t) / world)
+    seq = paddle.nn.Sequential(*ref_layers)
+    ro = paddle.optimizer.AdamW(0.05, parameters=seq.parameters())
+    ref = []
+    for s in range(steps):
+        tot = 0.0
+        for mb in range(D * M):
+            x = paddle.Tensor._wrap(xs[s][mb * MB:(mb + 1) * MB])
+            y = paddle.Tensor._wrap(ys[s][mb * MB:(mb + 1) * MB])
+            l = loss_fn(seq(x), y) / (D * M)
+            l.backward()
+            tot += float(l)
+        ro.step()
+        ro.clear_grad()
+        ref.append(tot)
+    write_result({"losses": losses, "ref": ref})
+
+
+def run_mpsync(sync_mode):
+    """mp_configs sync_grad / sync_param / sync_moment (+ sync_mode) on a replicated parameter whose gradient
+    differs per mp rank, and need_broadcast_data (inputs replaced by mp rank 0's)."""
+    strategy = fleet.DistributedStrategy()
+    strategy.hybrid_configs = {"dp_degree": 1, "mp_degree": world, "pp_degree": 1,
+                               "mp_configs": {"sync_grad": True, "sync_param": True, "sync_moment": True,
+                                              "sync_mode": sync_mode, "need_broadcast_data": False}}
+    strategy.sync_param_name = ["layer_norm"]
+    fleet.init(is_collective=True, strategy=strategy)
+
+    class M(paddle.nn.Layer):
+        def __init__(self):
+            super().__init__()
+            self.w = paddle.create_parameter([8], "float32", name="layer_norm_0.w_0")
+            self.u = paddle.create_parameter([8], "float32", name="other_0.w_0")   # not in sync_param_name
+
+        def forward(self, x):
+            return ((x * self.w).sum() ** 2 + (x * self.u).sum() ** 2)
+
+    paddle.seed(1)
+    m = M()
+    model = fleet.distributed_model(m)
+    opt = fleet.distributed_optimizer(paddle.optimizer.AdamW(0.1, parameters=model.parameters()))
+    xs = [torch.randn(world, 8, generator=torch.Generator().manual_seed(s)) for s in range(2)]
+    for x in xs:
+        loss = model(paddle.Tensor._wrap(x[rank].clone()))
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+    w = m.w._t.detach().clone()
+    u = m.u._t.detach().clone()
+    m1 = opt._base_opt._accumulators["moment1"][m.w.name].clone()
+    ws = [torch.empty_like(w) for _ in range(world)]
+    us = [torch.empty_like(u) for _ in range(world)]
+    ms = [torch.empty_like(m1) for _ in range(world)]
+    dist.all_gather(ws, w)
+    dist.all_gather(us, u)
+    dist.all_gather(ms, m1)
+    out = {"w_equal": all(torch.equal(ws[0], t) for t in ws), "m_equal": all(torch.equal(ms[0], t) for t in ms),
+           "u_differ": not all(torch.equal(us[0], t) for t in us)}
+    if sync_mode == "average":
+        # single process: the replicated param sees the mp-averaged gradient
+        paddle.seed(1)
+        r = M()
+        ro = paddle.optimizer.AdamW(0.1, parameters=[r.w])
+        for x in xs:
+            loss = sum(((x[k] * r.w._t).sum() ** 2) for k in range(world)) / world
+            loss.backward()
+            ro.step()
+            ro.clear_grad()
+        out["w_ref_diff"] = float((r.w._t.detach() - w).abs().max())
+    # need_broadcast_data: a TensorParallel forward sees mp rank 0's input
+    model._need_broadcast_data = True
+    x = torch.full((8,), float(rank + 1))
+    model(paddle.Tensor._wrap(x))
+    out["bcast_input"] = float(x[0])
+    write_result(out)
+
+
 if mode == "tp":
     run_tp()
 elif mode == "pp":
@@ -383,5 +580,11 @@ elif mode == "moe":
     run_moe()
 elif mode == "gpt_sp":
     run_gpt_sp()
+elif mode == "shv2":
+    run_shv2(sys.argv[2])
+elif mode == "mpsync":
+    run_mpsync(sys.argv[2])
+elif mode == "pp_hybrid":
+    run_pp_hybrid(sys.argv[2])
 elif mode == "pp_llama":
     run_pp_llama(int(sys.argv[2]))
