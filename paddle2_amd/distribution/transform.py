@@ -239,27 +239,33 @@ class ChainTransform(Transform):
             shape = t._inverse_shape(shape)
         return shape
 
+    def _event_ranks(self):
+        """(input, output) event rank of the chain.  Stage i is defined on ``dom_i`` event dims and changes the
+        rank by ``shift_i``; at the chain input it therefore needs ``dom_i - (shifts before i)`` dims, and the
+        last stage's output needs ``cod_last - (all shifts)``.  The chain takes the largest requirement; the
+        output rank is the input rank plus every shift."""
+        shifts = [t._codomain.event_rank - t._domain.event_rank for t in self.transforms]
+        needs, acc = [], 0
+        for t, sh in zip(self.transforms, shifts):
+            needs.append(t._domain.event_rank - acc)
+            acc += sh
+        needs.append(self.transforms[-1]._codomain.event_rank - acc)
+        r_in = max(needs)
+        return r_in, r_in + acc
+
     @property
     def _domain(self):
         if not self.transforms:
             return variable.Real()
-        domain = self.transforms[0]._domain
-        event_rank = self.transforms[-1]._codomain.event_rank
-        for t in reversed(self.transforms):
-            event_rank -= t._codomain.event_rank - t._domain.event_rank
-            event_rank = max(event_rank, t._domain.event_rank)
-        return variable.Independent(domain, event_rank - domain.event_rank)
+        base = self.transforms[0]._domain
+        return variable.Independent(base, self._event_ranks()[0] - base.event_rank)
 
     @property
     def _codomain(self):
         if not self.transforms:
             return variable.Real()
-        codomain = self.transforms[-1]._codomain
-        event_rank = self.transforms[0]._domain.event_rank
-        for t in self.transforms:
-            event_rank += t._codomain.event_rank - t._domain.event_rank
-            event_rank = max(event_rank, t._codomain.event_rank)
-        return variable.Independent(codomain, event_rank - codomain.event_rank)
+        base = self.transforms[-1]._codomain
+        return variable.Independent(base, self._event_ranks()[1] - base.event_rank)
 
 
 class ExpTransform(Transform):

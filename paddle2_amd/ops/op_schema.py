@@ -112,9 +112,9 @@ ALIASES = {
     "broadcast": ("distributed.broadcast", {}),
     "reduce": ("distributed.reduce", {}),
     "reduce_scatter": ("distributed.reduce_scatter", {}),
-    "c_sync_calc_stream": ("device.synchronize", {}),
-    "c_sync_comm_stream": ("device.synchronize", {}),
-    "sync_calc_stream": ("device.synchronize", {}),
+    "c_sync_calc_stream": ("ops.op_schema._c_sync_calc_stream", {}),
+    "c_sync_comm_stream": ("ops.op_schema._c_sync_comm_stream", {}),
+    "sync_calc_stream": ("ops.op_schema._c_sync_calc_stream", {}),
     # detection / vision
     "yolo_box": ("vision.ops.yolo_box", {}),
     "yolo_loss": ("vision.ops.yolo_loss", {}),
@@ -308,6 +308,31 @@ def _pool3d(x, kernel_size, strides=None, paddings=0, ceil_mode=False, exclusive
         return F.max_pool3d(x, kernel_size, strides, paddings, ceil_mode=ceil_mode, data_format=data_format)
     return F.avg_pool3d(x, kernel_size, strides, paddings, ceil_mode=ceil_mode, exclusive=exclusive,
                         data_format=data_format)
+
+
+def _c_sync_calc_stream(x=None):
+    """c_sync_calc_stream: the host waits for the CALCULATION stream of the tensor's device only (not the
+    whole device: comm / copy streams keep running)."""
+    import torch
+
+    t = _raw(x) if x is not None else None
+    if torch.cuda.is_available():
+        dev = t.device if isinstance(t, torch.Tensor) and t.is_cuda else torch.cuda.current_device()
+        torch.cuda.current_stream(dev).synchronize()
+    return x
+
+
+def _c_sync_comm_stream(x=None, ring_id=0):
+    """c_sync_comm_stream: the host waits for the device's COMMUNICATION stream (GPUContext.comm_stream)."""
+    import torch
+
+    t = _raw(x) if x is not None else None
+    if torch.cuda.is_available():
+        from ..device.context import get_context
+
+        dev = t.device.index if isinstance(t, torch.Tensor) and t.is_cuda else torch.cuda.current_device()
+        get_context(dev).comm_stream().synchronize()
+    return x
 
 
 def _l1_norm(x):

@@ -12,7 +12,7 @@ from .graph import Program, SymTensor, default_main_program, default_startup_pro
 from .graph import program_guard  # noqa: F401
 from .io import (deserialize_persistables, deserialize_program, load, load_inference_model, load_program_state,  # noqa
                  save, save_inference_model, serialize_persistables, serialize_program, set_program_state)
-from .program import InputSpec  # noqa: F401
+from .input import InputSpec  # noqa: F401
 
 Variable = Tensor  # a static Variable is a Tensor whose storage is a SymTensor
 
