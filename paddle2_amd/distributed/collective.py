@@ -314,6 +314,21 @@ def _all_reduce_torch(t: torch.Tensor, op=ReduceOp.SUM, group=None, sync_op=True
     return _Task(w)
 
 
+def ring_all_reduce(t: torch.Tensor, ring_id=-1):
+    """Sum-all-reduce ``t`` in place over the communicator ``ring_id`` (the tensor-parallel ring of the fused
+    inference ops, reference fused_attention_utils.h:28-64 AllReduce).  ring_id < 0: no-op.  An unknown ring id
+    raises instead of silently computing a partial sum."""
+    if ring_id is None or int(ring_id) < 0:
+        return t
+    g = get_group(int(ring_id))
+    if g is None:
+        if int(ring_id) == 0 and not dist.is_initialized():
+            return t   # single process: ring 0 is the trivial world
+        raise ValueError(f"ring_id {ring_id}: no communicator with that id (create it with new_group)")
+    _all_reduce_torch(t, ReduceOp.SUM, g, True)
+    return t
+
+
 def _is_symbolic(tensor):
     from ..static.graph import SymTensor
 

@@ -11,6 +11,7 @@ import torch
 
 from ....framework.tensor import Tensor
 from ....ops import torch_ops as T
+from ....distributed.collective import ring_all_reduce
 
 _wrap = Tensor._wrap
 
@@ -146,7 +147,13 @@ def fused_feedforward(x, linear1_weight, linear2_weight, linear1_bias=None, line
     h = FU.bias_act(h, _u(linear1_bias), activation)
     if training and dropout1_rate:
         h = torch.nn.functional.dropout(h, dropout1_rate)
-    o = T.linear(h, linear2_weight._t, _u(linear2_bias))
+    if ring_id is not None and int(ring_id) >= 0:
+        o = T.linear(h, linear2_weight._t)
+        ring_all_reduce(o, ring_id)   # tensor parallel: linear1 column / linear2 row shards -> partial sums
+        if linear2_bias is not None:
+            o = o + linear2_bias._t
+    else:
+        o = T.linear(h, linear2_weight._t, _u(linear2_bias))
     if training and dropout2_rate and mode == "upscale_in_train" and add_residual:
         o = FU.dropout_add(o, res, dropout2_rate)
     else:
@@ -183,6 +190,7 @@ def fused_multi_head_attention(x, qkv_weight, linear_weight, pre_layer_norm=Fals
             sc = sc + attn_mask._t.float()
         o = torch.einsum("bnqk,bknd->bqnd", torch.softmax(sc, -1), v.float()).to(t.dtype)
     o = torch.matmul(o.reshape(b, s, nh * hd), linear_weight._t)
+    ring_all_reduce(o, ring_id)   # tensor parallel: this rank's heads only -> out-projection partial sum
     if linear_bias is not None:
         o = o + linear_bias._t
     if add_residual:

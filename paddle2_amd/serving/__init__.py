@@ -23,6 +23,7 @@ import torch
 from ..framework.tensor import Tensor
 from ..ops import _native as N
 from ..ops import torch_ops as T
+from ..distributed.collective import ring_all_reduce
 
 _wrap = Tensor._wrap
 
@@ -280,6 +281,11 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
                             use_neox_rotary_style=False, gqa_group_size=-1, name=None):
     """Stack of pre-LN decoder layers for inference (reference fused_transformer.py:1053).
 
+    Tensor parallel (``ring_id`` >= 0): every rank holds its head slice of qkv / out-projection and its column
+    slice of ffn1 / row slice of ffn2; the two partial sums per layer are all-reduced over communicator
+    ``ring_id`` (reference fused_multi_transformer_kernel.cu:474) before the replicated bias — decode-sized
+    messages take the xGMI one-shot path when that is enabled (distributed/ipc_allreduce.py).
+
     x [b, s, d]; qkv_weights[i]: [3, nh, hd, d] (trans_qkvw) or [d, 3*nh*hd]; cache_kvs[i]:
     [2, b, nh, max_s, hd].  time_step None -> context phase (causal flash attention over the
     prompt, cache filled at [0, s)); else decode phase at position ``time_step`` (s == 1)."""
@@ -334,6 +340,7 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
             o = decode_attention(q[:, 0], ck[0], ck[1], lens, layout="bhsd")[:, None]
         o = o.reshape(b, s, nh * hd)
         a = torch.matmul(o, _u(linear_weights[i]))
+        ring_all_reduce(a, ring_id)   # tensor parallel: heads are sharded, the out-projection partial sums add
         if linear_biases is not None and linear_biases[i] is not None:
             a = a + _u(linear_biases[i])
         w2 = _u(ffn_ln_scales[i])
@@ -352,6 +359,7 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
         else:
             f = torch.nn.functional.gelu(f, approximate="tanh" if activation == "gelu_tanh" else "none")
         f = torch.matmul(f, _u(ffn2_weights[i]))
+        ring_all_reduce(f, ring_id)   # FFN hidden sharded: partial sums add before the (replicated) bias
         if ffn2_biases is not None and ffn2_biases[i] is not None:
             f = f + _u(ffn2_biases[i])
         h = h + f

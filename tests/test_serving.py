@@ -138,3 +138,13 @@ def test_fused_multi_transformer_decode_matches_context():
     ctx, _ = layer(x[:, : s - 1], caches=caches2)
     last, _ = layer(x[:, s - 1:], caches=caches2, time_step=s - 1)
     torch.testing.assert_close(last._t[:, 0], full._t[:, -1], atol=1e-4, rtol=1e-4)
+
+
+def test_tensor_parallel_fused_inference_ops_match_single_rank():
+    """ring_id all-reduce in fused_multi_transformer (context + decode), fused_feedforward and
+    fused_multi_head_attention: 2 gloo ranks with head / ffn shards == 1 rank with the full weights."""
+    from _dist import run_workers
+
+    for r in run_workers("tp_infer_worker.py", 2):
+        assert r["fmt_diff"] < 1e-4 and r["ffn_diff"] < 1e-4 and r["mha_diff"] < 1e-4, r
+        assert r["bad_ring"] == "raised", r
