@@ -59,7 +59,7 @@ int pd_cast_from_f32(int, const float*, void*, long, void*);
 int pd_fp8_cast(int, int, const void*, void*, void*, long, long, const float*, float*, void*);
 int pd_fp8_update_scale(float*, int, float*, float*, float*, float, float, void*);
 int pd_decode_attn(const void*, long, long, const void*, const void*, long, long, long, const int*, int, int,
-                   const int*, int, float*, float*, void*, long, long, int, int, int, int, int, float, void*);
+                   const int*, int, float*, float*, void*, long, long, int, int, int, int, int, float, int, void*);
 int pd_cache_write(const void*, const void*, long, long, void*, void*, long, long, long, const int*, int, int,
                    const int*, const int*, int, int, int, void*);
 long pd_bn_workspace(int, long, int);
@@ -275,11 +275,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("decode_attn", [](uintptr_t q, long sq_b, long sq_h, uintptr_t kc, uintptr_t vc, long s_blk, long s_tok,
                           long s_head, uintptr_t table, int max_blocks, int block_size, uintptr_t seq_lens, int max_len,
                           uintptr_t part_o, uintptr_t part_ml, uintptr_t out, long so_b, long so_h, int B, int Hq,
-                          int Hk, int HD, int splits, float scale, uintptr_t st) {
+                          int Hk, int HD, int splits, float scale, int impl, uintptr_t st) {
     check(pd_decode_attn(P<const void*>(q), sq_b, sq_h, P<const void*>(kc), P<const void*>(vc), s_blk, s_tok, s_head,
                          P<const int*>(table), max_blocks, block_size, P<const int*>(seq_lens), max_len,
                          P<float*>(part_o), P<float*>(part_ml), P<void*>(out), so_b, so_h, B, Hq, Hk, HD, splits,
-                         scale, P<void*>(st)),
+                         scale, impl, P<void*>(st)),
           "decode_attn");
   });
   m.def("cache_write", [](uintptr_t k, uintptr_t v, long sk, long sv, uintptr_t kc, uintptr_t vc, long s_blk,

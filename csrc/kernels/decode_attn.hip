@@ -116,6 +116,192 @@ __global__ __launch_bounds__(256) void decode_kernel(const bf16* __restrict__ q,
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// MFMA decode (HD = 128): the G query heads of a kv group are the 16 (padded) rows of v_mfma_f32_16x16x32_bf16.
+//  * each wave owns every 4th 32-key tile of the workgroup's chunk; a lane loads 16 B of K and of V per
+//    (key, 32-wide d chunk): lane l -> key 16u + (l&15), d = 32c + 8(l>>4) (u = 0,1; c = 0..3) — exactly the
+//    A-operand map of K for S^T = K.Q^T (rows = keys, k = d), so K never touches LDS; Q^T is the B operand,
+//    loaded once;
+//  * S^T's accumulator holds, per lane, 4 keys of column g = l&15: the online softmax runs per lane column
+//    (tile max: 8 in-lane values + 2 cross-group shuffles), and the bf16 P fragment of the P.V MFMA is built in
+//    place — its k order (keys 4h..4h+3, 16+4h..16+4h+3 for lane group h) is matched by the V operand, read from
+//    a per-wave row-major LDS image with ds_read_b64_tr_b16 (T10, XOR-swizzled 256-B rows, conflict-free);
+//  * the next tile's 16 loads are in flight while the current one computes (16 KiB per wave);
+//  * the 4 waves' (m, l, O) are merged through LDS; split partials go to the same merge kernel as the vector path.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) char lds_char;
+
+__device__ __forceinline__ int voff(int row, int ch) {   // 16-B chunk ch of row `row` in a [32][128 bf16] image
+  return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+constexpr int kMfmaLds = 4 * 32 * 256;                   // 4 waves x one 32-key V tile
+
+template <int G>
+__global__ __launch_bounds__(256, 2) void decode_mfma_kernel(const bf16* __restrict__ q, long sq_b, long sq_h,
+                                                             const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+                                                             long s_blk, long s_tok, long s_head,
+                                                             const int* __restrict__ block_table, int max_blocks,
+                                                             int block_size, const int* __restrict__ seq_lens,
+                                                             float* __restrict__ part_o, float* __restrict__ part_ml,
+                                                             bf16* __restrict__ out, long so_b, long so_h, int Hq,
+                                                             int splits, int chunk, float scale) {
+  constexpr int HD = 128;
+  __shared__ __attribute__((aligned(16))) char lds[kMfmaLds + 4 * 16 * 2 * 4];
+  const int b = blockIdx.x, hk = blockIdx.y, sp = blockIdx.z;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, h = l >> 4, c16 = l & 15;
+  const int len = seq_lens[b];
+  const int k_begin = sp * chunk, k_end = min(len, k_begin + chunk);
+  const float sl2 = scale * 1.4426950408889634f;
+
+  bf16x8 qf[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (c16 < G) qf[c] = *reinterpret_cast<const bf16x8*>(q + (long)b * sq_b + (long)(hk * G + c16) * sq_h + 32 * c + 8 * h);
+    else qf[c] = bf16x8{};
+  }
+  f32x4 o[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -1e30f, lsum = 0.f;
+  char* vl = lds + w * (32 * 256);
+  const int ntile = k_end > k_begin ? (k_end - k_begin + 31) / 32 : 0;
+
+  auto row_addr = [&](int key) -> long {
+    key = min(key, len - 1);   // keys past the sequence are masked; keep their loads inside valid blocks
+    long blk = b;
+    int off = key;
+    if (block_table) {
+      blk = block_table[(long)b * max_blocks + key / block_size];
+      off = key % block_size;
+    }
+    return blk * s_blk + (long)off * s_tok + (long)hk * s_head + 8 * h;
+  };
+  bf16x8 kr[2][4], vr[2][4];
+  auto load = [&](int t, bf16x8 (&kk)[2][4], bf16x8 (&vv)[2][4]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long a = row_addr(k_begin + 32 * t + 16 * u + c16);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        kk[u][c] = *reinterpret_cast<const bf16x8*>(kc + a + 32 * c);
+        vv[u][c] = *reinterpret_cast<const bf16x8*>(vc + a + 32 * c);
+      }
+    }
+  };
+  // transposed-read offsets of this lane (tile-independent): rows 4h+q (lo) and 16+4h+q (hi), chunk 2t+(p>>1)
+  const int qq = c16 >> 2, pp = c16 & 3;
+  int t = w;
+  if (t < ntile) load(t, kr, vr);
+  for (; t < ntile; t += 4) {
+    bf16x8 kn[2][4], vn[2][4];
+    if (t + 4 < ntile) load(t + 4, kn, vn);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) *reinterpret_cast<bf16x8*>(vl + voff(16 * u + c16, 4 * c + h)) = vr[u][c];
+    f32x4 s[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      s[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr[u][c], qf[c], s[u], 0, 0, 0);
+    }
+    const int k0 = k_begin + 32 * t;
+    float mt = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = (k0 + 16 * u + 4 * h + e < k_end) ? s[u][e] * sl2 : -INFINITY;
+        s[u][e] = v;
+        mt = fmaxf(mt, v);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    bf16x8 pf;
+    float ps = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pv = exp2f(s[u][e] - mn);
+        ps += pv;
+        pf[4 * u + e] = (__bf16)pv;
+      }
+    lsum = lsum * alpha + ps;
+    float ar[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ar[e] = __shfl(alpha, 4 * h + e, 64);   // O row g = 4h+e lives in lane column g
+#pragma unroll
+    for (int tt = 0; tt < 8; ++tt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[tt][e] *= ar[e];
+#pragma unroll
+    for (int tt = 0; tt < 8; ++tt) {
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4*)((lds_char*)vl + voff(4 * h + qq, 2 * tt + (pp >> 1)) + 8 * (pp & 1)));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4*)((lds_char*)vl + voff(16 + 4 * h + qq, 2 * tt + (pp >> 1)) + 8 * (pp & 1)));
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
+      const s16x8 vv8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      o[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vv8), o[tt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        kr[u][c] = kn[u][c];
+        vr[u][c] = vn[u][c];
+      }
+  }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  __syncthreads();   // every wave is done with its V image: reuse the LDS for the merge
+  float* ow = reinterpret_cast<float*>(lds);                 // [4][16][HD]
+  float* ml = reinterpret_cast<float*>(lds + kMfmaLds);      // [4][16][2]
+  if (h == 0) {
+    ml[(w * 16 + c16) * 2] = m;
+    ml[(w * 16 + c16) * 2 + 1] = lsum;
+  }
+#pragma unroll
+  for (int tt = 0; tt < 8; ++tt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (4 * h + e < G) ow[(w * 16 + 4 * h + e) * HD + 16 * tt + c16] = o[tt][e];
+  __syncthreads();
+  for (int i = tid; i < G * HD; i += 256) {
+    const int g = i / HD, d = i % HD;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, ml[(ww * 16 + g) * 2]);
+    float Lsum = 0.f, acc = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float wt = exp2f(ml[(ww * 16 + g) * 2] - M);
+      Lsum += ml[(ww * 16 + g) * 2 + 1] * wt;
+      acc += ow[(ww * 16 + g) * HD + d] * wt;
+    }
+    const int hq = hk * G + g;
+    if (splits == 1) {
+      out[(long)b * so_b + (long)hq * so_h + d].x = f2bf(Lsum > 0.f ? acc / Lsum : 0.f);
+    } else {
+      const long pi = (((long)b * Hq + hq) * splits + sp);
+      part_o[pi * HD + d] = acc;
+      if (d == 0) {
+        part_ml[pi * 2] = M;
+        part_ml[pi * 2 + 1] = Lsum;
+      }
+    }
+  }
+}
+
 template <int HD>
 __global__ __launch_bounds__(HD) void merge_kernel(const float* __restrict__ part_o,
                                                    const float* __restrict__ part_ml, bf16* __restrict__ out,
@@ -165,16 +351,43 @@ __global__ __launch_bounds__(256) void cache_write_kernel(const bf16* __restrict
 
 using namespace pd;
 
+// impl: 0 = auto (MFMA for HD 128 and G <= 16), 1 = vector path, 2 = MFMA path
 extern "C" int pd_decode_attn(const void* q, long sq_b, long sq_h, const void* kc, const void* vc, long s_blk,
                               long s_tok, long s_head, const int* block_table, int max_blocks, int block_size,
                               const int* seq_lens, int max_len, float* part_o, float* part_ml, void* out, long so_b,
-                              long so_h, int B, int Hq, int Hk, int HD, int splits, float scale, void* stream) {
+                              long so_h, int B, int Hq, int Hk, int HD, int splits, float scale, int impl,
+                              void* stream) {
   if ((HD != 64 && HD != 128) || Hq % Hk) return -1;
   const int G = Hq / Hk;
   hipStream_t st = (hipStream_t)stream;
   if (splits < 1) splits = 1;
   const int chunk = (max_len + splits - 1) / splits;
   dim3 grid(B, Hk, splits);
+  const bool mfma_ok = HD == 128 && G <= 16 && ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(kc) |
+                                                  reinterpret_cast<uintptr_t>(vc)) & 15) == 0 && (sq_h % 8) == 0 && (s_tok % 8) == 0 && (s_head % 8) == 0 &&
+                       (s_blk % 8) == 0 && (sq_b % 8) == 0;
+  if (impl == 2 && !mfma_ok) return -3;
+  if (impl != 1 && mfma_ok) {
+#define PD_DECM(GV)                                                                                                \
+  dec::decode_mfma_kernel<GV><<<grid, 256, 0, st>>>((const bf16*)q, sq_b, sq_h, (const bf16*)kc, (const bf16*)vc,   \
+                                                    s_blk, s_tok, s_head, block_table, max_blocks, block_size,        \
+                                                    seq_lens, part_o, part_ml, (bf16*)out, so_b, so_h, Hq, splits,    \
+                                                    chunk, scale)
+    switch (G) {
+      case 1: PD_DECM(1); break;
+      case 2: PD_DECM(2); break;
+      case 4: PD_DECM(4); break;
+      case 8: PD_DECM(8); break;
+      case 16: PD_DECM(16); break;
+      default: return -2;
+    }
+#undef PD_DECM
+    if (splits > 1) {
+      dim3 mg(B, Hq);
+      dec::merge_kernel<128><<<mg, 128, 0, st>>>(part_o, part_ml, (bf16*)out, so_b, so_h, Hq, splits);
+    }
+    return (int)hipGetLastError();
+  }
 #define PD_DEC(HDV, GV)                                                                                           \
   dec::decode_kernel<HDV, GV><<<grid, 256, 0, st>>>((const bf16*)q, sq_b, sq_h, (const bf16*)kc, (const bf16*)vc, \
                                                     s_blk, s_tok, s_head, block_table, max_blocks, block_size,       \

@@ -17,6 +17,7 @@ MI355X design:
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -33,6 +34,10 @@ def _u(x):
 
 
 # ============================================================================ core attention ops
+# 0 auto (MFMA kernel for D = 128 and <= 16 q heads per kv head), 1 vector kernel, 2 MFMA kernel (raises if unusable)
+_DECODE_IMPL = {"auto": 0, "vec": 1, "mfma": 2}[os.environ.get("PADDLE2_AMD_DECODE_KERNEL", "auto")]
+
+
 def decode_attention(q, k_cache, v_cache, seq_lens, block_table=None, block_size=None, layout="paged",
                      scale=None, splits=None, out=None):
     """One query token per sequence.
@@ -72,7 +77,8 @@ def decode_attention(q, k_cache, v_cache, seq_lens, block_table=None, block_size
         N.native().decode_attn(q.data_ptr(), q.stride(0), q.stride(1), k_cache.data_ptr(), v_cache.data_ptr(),
                                s_blk, s_tok, s_head, N.ptr(bt), 0 if bt is None else bt.shape[1], bs,
                                lens.data_ptr(), max_len, N.ptr(part_o), N.ptr(part_ml), out.data_ptr(),
-                               out.stride(0), out.stride(1), B, Hq, Hk, D, splits, float(scale), N.stream())
+                               out.stride(0), out.stride(1), B, Hq, Hk, D, splits, float(scale), _DECODE_IMPL,
+                               N.stream())
         return out
     # reference path (CPU / other dtypes)
     G = Hq // Hk

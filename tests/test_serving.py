@@ -148,3 +148,12 @@ def test_tensor_parallel_fused_inference_ops_match_single_rank():
     for r in run_workers("tp_infer_worker.py", 2):
         assert r["fmt_diff"] < 1e-4 and r["ffn_diff"] < 1e-4 and r["mha_diff"] < 1e-4, r
         assert r["bad_ring"] == "raised", r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("impl", [1, 2])
+@pytest.mark.parametrize("D,Hq,Hk", [(128, 32, 32), (128, 32, 8), (128, 8, 1), (128, 32, 2)])
+def test_decode_attention_kernels_gpu(impl, D, Hq, Hk, monkeypatch):
+    """vector (1) and MFMA (2) decode kernels, forced, vs fp32 (lens straddle the 32-key tiles and the splits)."""
+    monkeypatch.setattr(serving, "_DECODE_IMPL", impl)
+    _decode_case("cuda", torch.bfloat16, D, Hq, Hk, [1, 31, 33, 300, 4097])
