@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256) void decode_kernel(const bf16* __restrict__ q,
                                                      int splits, int chunk, float scale) {
   constexpr int L = HD / 8;             // lanes per key slot
   constexpr int SLOTS = 256 / L;        // keys processed per iteration
-  const int b = blockIdx.x, hk = blockIdx.y, sp = blockIdx.z;
+  const int hk = blockIdx.x, b = blockIdx.y, sp = blockIdx.z;   // kv heads fastest: a sequence's heads run together
   const int tid = threadIdx.x, slot = tid / L, ln = tid % L;
   const int len = seq_lens[b];
   const int k_begin = sp * chunk, k_end = min(len, k_begin + chunk);
@@ -126,7 +126,8 @@ __global__ __launch_bounds__(256) void decode_kernel(const bf16* __restrict__ q,
 //    (tile max: 8 in-lane values + 2 cross-group shuffles), and the bf16 P fragment of the P.V MFMA is built in
 //    place — its k order (keys 4h..4h+3, 16+4h..16+4h+3 for lane group h) is matched by the V operand, read from
 //    a per-wave row-major LDS image with ds_read_b64_tr_b16 (T10, XOR-swizzled 256-B rows, conflict-free);
-//  * the next tile's 16 loads are in flight while the current one computes (16 KiB per wave);
+//  * the next tile's 16 loads are in flight while the current one computes (16 KiB per wave), and the row
+//    addresses (paged block-table reads) run one more tile ahead;
 //  * the 4 waves' (m, l, O) are merged through LDS; split partials go to the same merge kernel as the vector path.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -140,19 +141,20 @@ __device__ __forceinline__ int voff(int row, int ch) {   // 16-B chunk ch of row
 
 constexpr int kMfmaLds = 4 * 32 * 256;                   // 4 waves x one 32-key V tile
 
-template <int G>
+template <int G, bool PAGED>
 __global__ __launch_bounds__(256, 2) void decode_mfma_kernel(const bf16* __restrict__ q, long sq_b, long sq_h,
                                                              const bf16* __restrict__ kc, const bf16* __restrict__ vc,
                                                              long s_blk, long s_tok, long s_head,
                                                              const int* __restrict__ block_table, int max_blocks,
-                                                             int block_size, const int* __restrict__ seq_lens,
+                                                             int bs_shift, const int* __restrict__ seq_lens,
                                                              float* __restrict__ part_o, float* __restrict__ part_ml,
                                                              bf16* __restrict__ out, long so_b, long so_h, int Hq,
                                                              int splits, int chunk, float scale) {
   constexpr int HD = 128;
   __shared__ __attribute__((aligned(16))) char lds[kMfmaLds + 4 * 16 * 2 * 4];
-  const int b = blockIdx.x, hk = blockIdx.y, sp = blockIdx.z;
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, h = l >> 4, c16 = l & 15;
+  const int hk = blockIdx.x, b = blockIdx.y, sp = blockIdx.z;   // kv heads fastest: a sequence's heads run together
+  const int tid = threadIdx.x, l = tid & 63, h = l >> 4, c16 = l & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: tile loops branch on SGPRs
   const int len = seq_lens[b];
   const int k_begin = sp * chunk, k_end = min(len, k_begin + chunk);
   const float sl2 = scale * 1.4426950408889634f;
@@ -170,21 +172,22 @@ __global__ __launch_bounds__(256, 2) void decode_mfma_kernel(const bf16* __restr
   char* vl = lds + w * (32 * 256);
   const int ntile = k_end > k_begin ? (k_end - k_begin + 31) / 32 : 0;
 
-  auto row_addr = [&](int key) -> long {
-    key = min(key, len - 1);   // keys past the sequence are masked; keep their loads inside valid blocks
-    long blk = b;
-    int off = key;
-    if (block_table) {
-      blk = block_table[(long)b * max_blocks + key / block_size];
-      off = key % block_size;
-    }
-    return blk * s_blk + (long)off * s_tok + (long)hk * s_head + 8 * h;
-  };
-  bf16x8 kr[2][4], vr[2][4];
-  auto load = [&](int t, bf16x8 (&kk)[2][4], bf16x8 (&vv)[2][4]) {
+  // block of this lane's keys (u = 0, 1) in tile t; keys past the sequence are clamped so their (masked)
+  // loads stay inside valid blocks
+  auto blocks = [&](int t, int (&bk)[2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const long a = row_addr(k_begin + 32 * t + 16 * u + c16);
+      const int key = min(k_begin + 32 * t + 16 * u + c16, len - 1);
+      bk[u] = PAGED ? block_table[(long)b * max_blocks + (key >> bs_shift)] : b;
+    }
+  };
+  bf16x8 kr[2][4], vr[2][4];
+  auto load = [&](int t, const int (&bk)[2], bf16x8 (&kk)[2][4], bf16x8 (&vv)[2][4]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int key = min(k_begin + 32 * t + 16 * u + c16, len - 1);
+      const int off = PAGED ? (key & ((1 << bs_shift) - 1)) : key;
+      const long a = (long)bk[u] * s_blk + (long)off * s_tok + (long)hk * s_head + 8 * h;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         kk[u][c] = *reinterpret_cast<const bf16x8*>(kc + a + 32 * c);
@@ -192,74 +195,90 @@ __global__ __launch_bounds__(256, 2) void decode_mfma_kernel(const bf16* __restr
       }
     }
   };
-  // transposed-read offsets of this lane (tile-independent): rows 4h+q (lo) and 16+4h+q (hi), chunk 2t+(p>>1)
-  const int qq = c16 >> 2, pp = c16 & 3;
-  int t = w;
-  if (t < ntile) load(t, kr, vr);
-  for (; t < ntile; t += 4) {
-    bf16x8 kn[2][4], vn[2][4];
-    if (t + 4 < ntile) load(t + 4, kn, vn);
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) *reinterpret_cast<bf16x8*>(vl + voff(16 * u + c16, 4 * c + h)) = vr[u][c];
-    f32x4 s[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      s[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) s[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr[u][c], qf[c], s[u], 0, 0, 0);
+  // Issue order per iteration: block-table reads of tile t+8, then the K/V loads of tile t+4 (whose blocks were
+  // read one iteration earlier, ahead of tile t's loads), then tile t's math — every wait is a counted vmcnt that
+  // leaves the newer loads in flight; a table read placed right in front of its loads cost 20 % on paged caches.
+  const int qq = c16 >> 2, pp = c16 & 3;   // transposed-read lane roles: row 4h+qq / 16+4h+qq, column group pp
+  // one tile's math on the register set (kc_, vc_); the other set's loads stay in flight meanwhile
+  auto compute = [&](int t, const bf16x8 (&kc_)[2][4], const bf16x8 (&vc_)[2][4]) {
+  #pragma unroll
+      for (int u = 0; u < 2; ++u)
+  #pragma unroll
+        for (int c = 0; c < 4; ++c) *reinterpret_cast<bf16x8*>(vl + voff(16 * u + c16, 4 * c + h)) = vc_[u][c];
+      f32x4 s[2];
+  #pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        s[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+        for (int c = 0; c < 4; ++c) s[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kc_[u][c], qf[c], s[u], 0, 0, 0);
+      }
+      const int k0 = k_begin + 32 * t;
+      float mt = -INFINITY;
+  #pragma unroll
+      for (int u = 0; u < 2; ++u)
+  #pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = (k0 + 16 * u + 4 * h + e < k_end) ? s[u][e] * sl2 : -INFINITY;
+          s[u][e] = v;
+          mt = fmaxf(mt, v);
+        }
+      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m, mt);
+      const float alpha = exp2f(m - mn);
+      m = mn;
+      bf16x8 pf;
+      float ps = 0.f;
+  #pragma unroll
+      for (int u = 0; u < 2; ++u)
+  #pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float pv = exp2f(s[u][e] - mn);
+          ps += pv;
+          pf[4 * u + e] = (__bf16)pv;
+        }
+      lsum = lsum * alpha + ps;
+      float ar[4];
+  #pragma unroll
+      for (int e = 0; e < 4; ++e) ar[e] = __shfl(alpha, 4 * h + e, 64);   // O row g = 4h+e lives in lane column g
+  #pragma unroll
+      for (int tt = 0; tt < 8; ++tt)
+  #pragma unroll
+        for (int e = 0; e < 4; ++e) o[tt][e] *= ar[e];
+  #pragma unroll
+      for (int tt = 0; tt < 8; ++tt) {
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)((lds_char*)vl + voff(4 * h + qq, 2 * tt + (pp >> 1)) + 8 * (pp & 1)));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)((lds_char*)vl + voff(16 + 4 * h + qq, 2 * tt + (pp >> 1)) + 8 * (pp & 1)));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 vv8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vv8), o[tt], 0, 0, 0);
+      }
+  };
+  // Two register sets in ping-pong, two tiles per trip and no exit between them: a copy at the loop end would
+  // wait for the prefetch, a conditionally issued load makes the wait counting assume the worst at the join,
+  // and with an exit between the halves the compiler sinks the second set's loads past it (behind the first
+  // half's math).  So loads and table reads are unconditional, clamped to the wave's last tile (a re-read of
+  // a tile just loaded hits L2), and an odd tile count ends with one fully masked tile (alpha = 1, p = 0).
+  bf16x8 k2[2][4], v2[2][4];
+  if (w < ntile) {
+    const int last = w + 4 * ((ntile - 1 - w) / 4);
+    int bn[2], b0[2];
+    blocks(w, b0);
+    blocks(min(w + 4, last), bn);
+    load(w, b0, kr, vr);
+    for (int t = w; t <= last; t += 8) {
+      int bnn[2];
+      blocks(min(t + 8, last), bnn);
+      load(min(t + 4, last), bn, k2, v2);
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the math
+      compute(t, kr, vr);
+      blocks(min(t + 12, last), bn);
+      load(min(t + 8, last), bnn, kr, vr);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(t + 4, k2, v2);
     }
-    const int k0 = k_begin + 32 * t;
-    float mt = -INFINITY;
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = (k0 + 16 * u + 4 * h + e < k_end) ? s[u][e] * sl2 : -INFINITY;
-        s[u][e] = v;
-        mt = fmaxf(mt, v);
-      }
-    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mn = fmaxf(m, mt);
-    const float alpha = exp2f(m - mn);
-    m = mn;
-    bf16x8 pf;
-    float ps = 0.f;
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float pv = exp2f(s[u][e] - mn);
-        ps += pv;
-        pf[4 * u + e] = (__bf16)pv;
-      }
-    lsum = lsum * alpha + ps;
-    float ar[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) ar[e] = __shfl(alpha, 4 * h + e, 64);   // O row g = 4h+e lives in lane column g
-#pragma unroll
-    for (int tt = 0; tt < 8; ++tt)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[tt][e] *= ar[e];
-#pragma unroll
-    for (int tt = 0; tt < 8; ++tt) {
-      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (lds_s16x4*)((lds_char*)vl + voff(4 * h + qq, 2 * tt + (pp >> 1)) + 8 * (pp & 1)));
-      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (lds_s16x4*)((lds_char*)vl + voff(16 + 4 * h + qq, 2 * tt + (pp >> 1)) + 8 * (pp & 1)));
-      typedef short s16x8 __attribute__((ext_vector_type(8)));
-      const s16x8 vv8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      o[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vv8), o[tt], 0, 0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        kr[u][c] = kn[u][c];
-        vr[u][c] = vn[u][c];
-      }
   }
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
@@ -351,7 +370,7 @@ __global__ __launch_bounds__(256) void cache_write_kernel(const bf16* __restrict
 
 using namespace pd;
 
-// impl: 0 = auto (MFMA for HD 128 and G <= 16), 1 = vector path, 2 = MFMA path
+// impl: 0 = auto (MFMA for HD 128 and 2 <= G <= 16), 1 = vector path, 2 = MFMA path
 extern "C" int pd_decode_attn(const void* q, long sq_b, long sq_h, const void* kc, const void* vc, long s_blk,
                               long s_tok, long s_head, const int* block_table, int max_blocks, int block_size,
                               const int* seq_lens, int max_len, float* part_o, float* part_ml, void* out, long so_b,
@@ -362,17 +381,28 @@ extern "C" int pd_decode_attn(const void* q, long sq_b, long sq_h, const void* k
   hipStream_t st = (hipStream_t)stream;
   if (splits < 1) splits = 1;
   const int chunk = (max_len + splits - 1) / splits;
-  dim3 grid(B, Hk, splits);
-  const bool mfma_ok = HD == 128 && G <= 16 && ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(kc) |
+  dim3 grid(Hk, B, splits);   // the Hk workgroups of one token row (paged: adjacent 256-B pieces) are co-resident
+  const bool mfma_shape = HD == 128 && G <= 16 && ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(kc) |
                                                   reinterpret_cast<uintptr_t>(vc)) & 15) == 0 && (sq_h % 8) == 0 && (s_tok % 8) == 0 && (s_head % 8) == 0 &&
                        (s_blk % 8) == 0 && (sq_b % 8) == 0;
+  int bs_shift = 0;
+  while (block_table && (1 << bs_shift) < block_size) ++bs_shift;
+  const bool mfma_ok = mfma_shape && (!block_table || (1 << bs_shift) == block_size);   // paged: pow-2 blocks
   if (impl == 2 && !mfma_ok) return -3;
-  if (impl != 1 && mfma_ok) {
-#define PD_DECM(GV)                                                                                                \
-  dec::decode_mfma_kernel<GV><<<grid, 256, 0, st>>>((const bf16*)q, sq_b, sq_h, (const bf16*)kc, (const bf16*)vc,   \
-                                                    s_blk, s_tok, s_head, block_table, max_blocks, block_size,        \
-                                                    seq_lens, part_o, part_ml, (bf16*)out, so_b, so_h, Hq, splits,    \
-                                                    chunk, scale)
+  // auto: the MFMA kernel for grouped-query attention (2.0-2.9x the vector kernel at G = 4..16); MHA (G = 1)
+  // stays on the vector kernel, which streams 256-B rows at a higher occupancy (5.37 vs 5.11 TB/s, paged
+  // B64 L1088; profiles/r3_decode_attention.md)
+  if (impl == 2 || (impl == 0 && mfma_ok && G >= 2)) {
+#define PD_DECM2(GV, PG)                                                                                           \
+  dec::decode_mfma_kernel<GV, PG><<<grid, 256, 0, st>>>((const bf16*)q, sq_b, sq_h, (const bf16*)kc,                \
+                                                        (const bf16*)vc, s_blk, s_tok, s_head, block_table,           \
+                                                        max_blocks, bs_shift, seq_lens, part_o, part_ml, (bf16*)out,  \
+                                                        so_b, so_h, Hq, splits, chunk, scale)
+#define PD_DECM(GV)          \
+  if (block_table)           \
+    PD_DECM2(GV, true);      \
+  else                       \
+    PD_DECM2(GV, false)
     switch (G) {
       case 1: PD_DECM(1); break;
       case 2: PD_DECM(2); break;
@@ -382,6 +412,7 @@ extern "C" int pd_decode_attn(const void* q, long sq_b, long sq_h, const void* k
       default: return -2;
     }
 #undef PD_DECM
+#undef PD_DECM2
     if (splits > 1) {
       dim3 mg(B, Hq);
       dec::merge_kernel<128><<<mg, 128, 0, st>>>(part_o, part_ml, (bf16*)out, so_b, so_h, Hq, splits);

@@ -34,7 +34,8 @@ def _u(x):
 
 
 # ============================================================================ core attention ops
-# 0 auto (MFMA kernel for D = 128 and <= 16 q heads per kv head), 1 vector kernel, 2 MFMA kernel (raises if unusable)
+# 0 auto (MFMA kernel for D = 128 and 2..16 q heads per kv head, vector kernel for MHA), 1 vector kernel,
+# 2 MFMA kernel (raises if unusable)
 _DECODE_IMPL = {"auto": 0, "vec": 1, "mfma": 2}[os.environ.get("PADDLE2_AMD_DECODE_KERNEL", "auto")]
 
 
@@ -60,8 +61,9 @@ def decode_attention(q, k_cache, v_cache, seq_lens, block_table=None, block_size
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     if out is None:
         out = torch.empty(B, Hq, D, dtype=q.dtype, device=q.device)
+    G = Hq // Hk
     native = (q.device.type == "cuda" and N.use_native(q) and q.dtype == torch.bfloat16 and D in (64, 128)
-              and (Hq // Hk) in (1, 2, 4, 8))
+              and (G in (1, 2, 4, 8) or (D == 128 and G == 16 and _DECODE_IMPL != 1)))
     if native:
         max_len = int(k_cache.shape[0] * bs) if block_table is not None else int(bs)
         if splits is None:
