@@ -466,13 +466,17 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(Params p) {
   // stream DMA instruction I (0..3) of tile t's A / B into stage `st`
   constexpr bool GL = DBG == 7;
   auto dmaA = [&](int t, int st, auto I) {
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(a_t0 + a_step * t);
+    const auto* pa = a_t0 + a_step * t;   // range check ends at the operand's last byte (p.a_end), not 2 GiB on
+    const __amdgpu_buffer_rsrc_t rs =      // (a stray read past the tensor returns 0 instead of touching memory)
+        p.a_end ? make_rsrc_n(pa, (long)((const char*)p.a_end - (const char*)pa)) : make_rsrc(pa);
     const int krem = p.K - t * BK;
     dma<AK, decltype(I)::value, GL>(rs, LA, a_is, smem + st * TILE_BYTES, wave, a_rows_full && krem >= BK, krem,
                                     (const char*)(a_t0 + a_step * t), (const char*)p.zero);
   };
   auto dmaB = [&](int t, int st, auto I) {
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(b_t0 + b_step * t);
+    const auto* pb = b_t0 + b_step * t;
+    const __amdgpu_buffer_rsrc_t rs =
+        p.b_end ? make_rsrc_n(pb, (long)((const char*)p.b_end - (const char*)pb)) : make_rsrc(pb);
     const int krem = p.K - t * BK;
     dma<BKM, decltype(I)::value, GL>(rs, LB, b_is, smem + B_OFF + st * TILE_BYTES, wave,
                                      b_rows_full && krem >= BK, krem, (const char*)(b_t0 + b_step * t),
