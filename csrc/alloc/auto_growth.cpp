@@ -24,8 +24,14 @@
 // Thread-safe (one mutex per device).  C ABI for ctypes; no Python dependency, loads on CPU-only machines.
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -288,7 +294,39 @@ static Block* find_fit(Device& d, size_t size, hipStream_t stream) {
   return nullptr;
 }
 
+// PD_ALLOC_TRACE=<file>: every allocation / free appended as one line ("A <ptr> <bytes> <stream>" /
+// "F <ptr>") with an unbuffered write, so the file is complete up to the instant a GPU fault aborts the process:
+// replaying it gives the live-block map at the fault (scripts/alloc_fault_map.py maps the faulting address to
+// the block it falls in or lies next to).
+static int trace_fd() {
+  static int fd = [] {
+    const char* p = std::getenv("PD_ALLOC_TRACE");
+    return (p && *p) ? ::open(p, O_WRONLY | O_CREAT | O_APPEND | O_TRUNC, 0644) : -1;
+  }();
+  return fd;
+}
+
+static void trace(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+static void trace(const char* fmt, ...) {
+  const int fd = trace_fd();
+  if (fd < 0) return;
+  char buf[128];
+  va_list ap;
+  va_start(ap, fmt);
+  const int n = std::vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (n > 0) (void)!::write(fd, buf, (size_t)std::min(n, (int)sizeof(buf) - 1));
+}
+
+static void* do_alloc_impl(size_t size, int dev, hipStream_t stream);
+
 static void* do_alloc(size_t size, int dev, hipStream_t stream) {
+  void* p = do_alloc_impl(size, dev, stream);
+  trace("A %p %zu %p\n", p, size, (void*)stream);
+  return p;
+}
+
+static void* do_alloc_impl(size_t size, int dev, hipStream_t stream) {
   if (dev < 0 || dev >= kMaxDevices) return nullptr;
   Device& d = g_dev[dev];
   std::lock_guard<std::mutex> lk(d.mu);
@@ -388,6 +426,7 @@ static void process_deferred(Device& d) {
 
 static void do_free(void* ptr, int dev, hipStream_t stream) {
   if (!ptr || dev < 0 || dev >= kMaxDevices) return;
+  trace("F %p\n", ptr);
   Device& d = g_dev[dev];
   std::lock_guard<std::mutex> lk(d.mu);
   auto it = d.live.find(ptr);
