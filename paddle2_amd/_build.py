@@ -143,6 +143,34 @@ def build_runtime(verbose=False):
     return out
 
 
+def rccl_target_path():
+    return os.path.join(ROOT, "paddle2_amd", "_rccl" + _ext_suffix())
+
+
+def build_rccl(verbose=False):
+    """ProcessGroupRCCL core (csrc/comm/rccl_group.cpp): host C++ against the HIP runtime and librccl, pybind11."""
+    import pybind11
+
+    src = os.path.join(CSRC, "comm", "rccl_group.cpp")
+    flags = ["-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include",
+             "-I", sysconfig.get_paths()["include"], "-I", pybind11.get_include()]
+    libs = ["-L/opt/rocm/lib", "-lrccl", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+    key = _hash(src, " ".join(flags + libs))
+    out = rccl_target_path()
+    stamp = out + ".stamp"
+    if os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key:
+        return out
+    tmp = out + ".tmp"
+    cmd = ["g++"] + flags + [src, "-o", tmp] + libs
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    _run(cmd)
+    os.replace(tmp, out)
+    with open(stamp, "w") as f:
+        f.write(key)
+    return out
+
+
 def alloc_target_path():
     return os.path.join(ROOT, "paddle2_amd", "_pd_alloc.so")
 
@@ -243,6 +271,7 @@ def build_sanitized(kind="thread", verbose=False):
 def build_all(verbose=False):
     alloc = build_allocator(verbose=verbose)
     build_alloc_torch(verbose=verbose)
+    build_rccl(verbose=verbose)
     return build(verbose=verbose), build_runtime(verbose=verbose), alloc
 
 

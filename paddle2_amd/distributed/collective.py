@@ -165,6 +165,11 @@ def init_parallel_env(backend=None, timeout_s=None):
     rank = _env_int("RANK", "PADDLE_TRAINER_ID", default=0)
     world = _env_int("WORLD_SIZE", "PADDLE_TRAINERS_NUM", default=1)
     backend = backend or _backend_for_device()
+    native_pg = False
+    if backend in ("nccl", "rccl") and torch.cuda.is_available():
+        from . import rccl_pg  # the framework's own RCCL process group (PADDLE2_AMD_PG=rccl)
+
+        native_pg = rccl_pg.enabled()
     if backend == "nccl" and torch.cuda.is_available():
         local = _env_int("LOCAL_RANK", "PADDLE_LOCAL_RANK", default=rank % max(torch.cuda.device_count(), 1))
         torch.cuda.set_device(local)
@@ -181,7 +186,9 @@ def init_parallel_env(backend=None, timeout_s=None):
         if not dist.is_initialized():
             tout = datetime.timedelta(seconds=timeout_s or int(os.environ.get("FLAGS_comm_timeout_s", "1800")))
             kw = {}
-            if backend == "nccl" and torch.cuda.is_available():
+            if native_pg:
+                backend = rccl_pg.register()
+            elif backend == "nccl" and torch.cuda.is_available():
                 kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
             if os.environ.get("PADDLE2_AMD_NATIVE_STORE", "0") == "1":
                 # rendezvous through the native C++ TCPStore (csrc/runtime/tcp_store.cpp)
@@ -630,7 +637,9 @@ def batch_isend_irecv(p2p_op_list):
         ops.append(dist.P2POp(fn, p.tensor._t, peer, group=pg))
     if not ops:
         return []
-    works = dist.batch_isend_irecv(ops)
+    from .rccl_pg import batch_isend_irecv as _batch
+
+    works = _batch(ops)
     return [_Task(w) for w in works]
 
 

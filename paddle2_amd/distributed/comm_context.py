@@ -113,6 +113,11 @@ class CommContext:
 
     # ---------------------------------------------------------------- collectives
     def all_reduce(self, tensor, op="sum", sync_op=True):
+        from .rccl_pg import ProcessGroupRCCL
+
+        if isinstance(self.pg, ProcessGroupRCCL) and isinstance(op, PreMulSum):
+            # the framework's RCCL group takes the factor directly (ncclRedOpCreatePreMulSum)
+            return self._done(self.pg.all_reduce_native(tensor, premul=float(op.scalar)), sync_op)
         rop, post = self._reduce_op(op)
         o = dist.AllreduceOptions()
         o.reduceOp = rop

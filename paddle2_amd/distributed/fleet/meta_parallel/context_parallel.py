@@ -26,6 +26,7 @@ import torch.distributed as dist
 
 from ....framework.tensor import Tensor
 from ....ops import torch_ops as T
+from ...rccl_pg import batch_isend_irecv as _batch_p2p
 
 __all__ = ["ulysses_attention", "ring_flash_attention", "zigzag_shard", "zigzag_unshard", "context_positions",
            "shard_sequence", "SEP_MODES"]
@@ -136,7 +137,7 @@ class _Ring:
         recv = torch.empty_like(send)
         ops = [dist.P2POp(dist.isend, send, self.nxt, self.pg, tag),
                dist.P2POp(dist.irecv, recv, self.prv, self.pg, tag)]
-        return recv, dist.batch_isend_irecv(ops)
+        return recv, _batch_p2p(ops)
 
 
 def _wait(works):

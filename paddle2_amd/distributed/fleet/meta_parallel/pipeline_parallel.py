@@ -37,6 +37,7 @@ import torch.distributed as dist
 
 from ....framework.tensor import Tensor
 from ...collective import ReduceOp
+from ...rccl_pg import batch_isend_irecv as _batch_p2p
 from ..utils.hybrid_parallel_util import broadcast_dp_parameters, broadcast_mp_parameters, \
     broadcast_sep_parameters, broadcast_sharding_parameters
 from ....ops.torch_ops import WeightGradStore
@@ -314,7 +315,7 @@ class PipelineParallel(MetaParallelBase):
             seen[k] = tag + 1
             p2p.append(dist.P2POp(dist.isend if s else dist.irecv, t, self._peer(st), group=self.pp_group.pg,
                                   tag=(tick % 4096) * 64 + tag))
-        works = dist.batch_isend_irecv(p2p)
+        works = _batch_p2p(p2p)
         if wait:
             for w in works:
                 w.wait()
