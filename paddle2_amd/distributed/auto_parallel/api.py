@@ -4,11 +4,12 @@ python/paddle/distributed/auto_parallel/api.py — ``shard_tensor`` :206, ``dten
 ``shard_dataloader`` :3208, ``to_static``/``DistModel`` :2110/:2693, ``unshard_dtensor`` :2854;
 process_mesh.py; placement_type.py).
 
-MI355X design: a Paddle DistTensor is our Tensor whose storage is a torch ``DTensor`` over a
-``DeviceMesh`` built from the ProcessMesh's rank grid (RCCL sub-communicators per mesh dim).
-Operator-level sharding propagation (the reference's SPMD rules + reshard functions s->r, p->r,
-p->s, s->s) is torch's DTensor dispatcher; ``reshard`` is ``redistribute`` (all-gather /
-reduce-scatter / all-to-all over the mesh dim's communicator).
+MI355X design: a Paddle DistTensor is our Tensor whose storage is a torch ``DTensor`` (local shard +
+``DeviceMesh`` built from the ProcessMesh's rank grid + placements).  The framework's hot ops (norms, linear,
+RoPE, flash attention, SwiGLU, embedding) dispatch DistTensor arguments at op entry through the SPMD rules of
+``spmd_rules.py`` and the framework's own reshard engine (``dist_ops.py`` / ``reshard.py``), running the native
+kernels on the local shards; ``reshard`` below uses the same engine.  Other ops (views, pointwise) keep
+torch's DTensor propagation.
 """
 from __future__ import annotations
 
@@ -260,9 +261,16 @@ def dtensor_from_fn(fn, mesh, placements, *args, **kwargs):
 
 
 def reshard(dist_tensor, mesh, placements):
+    """Same mesh: the framework's reshard engine (reshard.py: s->r all-gather, p->r all-reduce, p->s
+    reduce-scatter, s->s all-to-all, r->s slice; differentiable).  A different mesh: torch's redistribute."""
     t = dist_tensor._t
     assert isinstance(t, _dt.DTensor), "reshard expects a DistTensor"
-    return _attach(_wrap(t.redistribute(mesh._device_mesh(), _torch_placements(mesh, placements))), mesh)
+    dm = mesh._device_mesh()
+    if dm == t.device_mesh:
+        from .reshard import reshard as _own
+
+        return _attach(_wrap(_own(t, _torch_placements(mesh, placements))), mesh)
+    return _attach(_wrap(t.redistribute(dm, _torch_placements(mesh, placements))), mesh)
 
 
 def unshard_dtensor(dist_tensor):

@@ -1,0 +1,173 @@
+"""Reshard engine for DistTensors on the framework's own collective calls (reference:
+paddle/phi/core/distributed/auto_parallel/reshard/ — s_to_r_reshard_function.cc:45 (all-gather),
+p_to_r :66 (all-reduce), p_to_s :70 (reduce-scatter), s_to_s :101 (all-to-all), r_to_s (local slice),
+r_to_p (keep on one rank), nd_mesh_reshard_function.cc (one mesh dim at a time)).
+
+A DistTensor's storage is a torch ``DTensor`` (local shard + mesh + placements); the data movement between two
+placements is done here, per mesh dimension, with c10d collectives on that dimension's process group
+(``DeviceMesh.get_group(dim)`` — RCCL, or the framework's ProcessGroupRCCL when ``PADDLE2_AMD_PG=rccl``), not
+with ``DTensor.redistribute``.  Order per mesh dim follows the reference's nd-mesh function: partial dims are
+resolved first (p->r / p->s), then shard moves (s->s / s->r), then new shards (r->s) — so a reduction is never
+applied to data that was already replicated by a gather.
+
+``reshard(dt, placements)`` is differentiable: the backward reshards the gradient from the target placements
+back to the source placements with the same engine; a replicated gradient flowing back into a partial source
+stays replicated (converting it to partial would only force a later reduction — torch's ``is_backward`` rule).
+
+Shards must divide evenly (the LLM shapes do); an uneven shard raises instead of silently padding.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+from torch.distributed import tensor as _dt
+from torch.distributed.tensor.placement_types import Partial as _TPartial
+from torch.distributed.tensor.placement_types import Replicate as _TReplicate
+from torch.distributed.tensor.placement_types import Shard as _TShard
+
+_RED = {"sum": dist.ReduceOp.SUM, "avg": dist.ReduceOp.AVG, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+COMM_LOG = []   # (kind, mesh_dim) of every collective issued (tests assert the expected plan)
+
+
+def _group(mesh, dim):
+    return mesh.get_group(dim) if mesh.ndim > 1 else mesh.get_group()
+
+
+def _coord(mesh, dim):
+    return mesh.get_local_rank(dim)
+
+
+def _all_gather(x, axis, mesh, dim):
+    g = _group(mesh, dim)
+    n = dist.get_world_size(g)
+    xm = x.movedim(axis, 0).contiguous()
+    out = torch.empty((n * xm.shape[0],) + tuple(xm.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, xm, group=g)
+    COMM_LOG.append(("all_gather", dim))
+    return out.movedim(0, axis).contiguous()
+
+
+def _all_reduce(x, op, mesh, dim):
+    g = _group(mesh, dim)
+    y = x.contiguous().clone()
+    if op == "avg" and dist.get_backend(g) == "gloo":
+        dist.all_reduce(y, op=dist.ReduceOp.SUM, group=g)
+        y.div_(dist.get_world_size(g))
+    else:
+        dist.all_reduce(y, op=_RED[op], group=g)
+    COMM_LOG.append(("all_reduce", dim))
+    return y
+
+
+def _reduce_scatter(x, axis, op, mesh, dim):
+    g = _group(mesh, dim)
+    n = dist.get_world_size(g)
+    xm = x.movedim(axis, 0).contiguous()
+    if xm.shape[0] % n:
+        raise ValueError(f"reshard p->s: axis {axis} of size {xm.shape[0]} does not split over {n} ranks")
+    out = torch.empty((xm.shape[0] // n,) + tuple(xm.shape[1:]), dtype=x.dtype, device=x.device)
+    avg_gloo = op == "avg" and dist.get_backend(g) == "gloo"
+    dist.reduce_scatter_tensor(out, xm, op=dist.ReduceOp.SUM if avg_gloo else _RED[op], group=g)
+    if avg_gloo:
+        out.div_(n)
+    COMM_LOG.append(("reduce_scatter", dim))
+    return out.movedim(0, axis).contiguous()
+
+
+def _all_to_all(x, src_axis, dst_axis, mesh, dim):
+    """Shard(src_axis) -> Shard(dst_axis) over one mesh dim: split dst_axis into n blocks, exchange, concatenate
+    the received blocks along src_axis."""
+    g = _group(mesh, dim)
+    n = dist.get_world_size(g)
+    if x.shape[dst_axis] % n:
+        raise ValueError(f"reshard s->s: axis {dst_axis} of size {x.shape[dst_axis]} does not split over {n}")
+    blocks = [b.contiguous() for b in x.chunk(n, dim=dst_axis)]
+    inp = torch.stack(blocks)                       # [n, ...block]
+    out = torch.empty_like(inp)
+    dist.all_to_all_single(out, inp, group=g)
+    COMM_LOG.append(("all_to_all", dim))
+    return torch.cat(list(out.unbind(0)), dim=src_axis)
+
+
+def _slice(x, axis, mesh, dim):
+    n = mesh.size(dim)
+    if x.shape[axis] % n:
+        raise ValueError(f"reshard r->s: axis {axis} of size {x.shape[axis]} does not split over {n} ranks")
+    return x.chunk(n, dim=axis)[_coord(mesh, dim)].contiguous()
+
+
+def _to_partial(x, mesh, dim):
+    """r -> p(sum): the value lives on coordinate 0 of the mesh dim, zeros elsewhere."""
+    return x.clone() if _coord(mesh, dim) == 0 else torch.zeros_like(x)
+
+
+def _red_name(p):
+    return getattr(p, "reduce_op", "sum")
+
+
+def reshard_local(local, mesh, src, dst, backward=False):
+    """Move ``local`` (this rank's piece under placements ``src``) to placements ``dst`` (tuples of torch
+    placements, one per mesh dim)."""
+    cur = list(src)
+    x = local
+    nd = mesh.ndim
+    # 1. partial dims: reduce (to replicate or straight into a shard)
+    for d in range(nd):
+        s, t = cur[d], dst[d]
+        if isinstance(s, _TPartial) and not isinstance(t, _TPartial):
+            if isinstance(t, _TShard) and not any(isinstance(c, _TShard) and c.dim == t.dim for c in cur):
+                x = _reduce_scatter(x, t.dim, _red_name(s), mesh, d)
+                cur[d] = t
+            else:
+                x = _all_reduce(x, _red_name(s), mesh, d)
+                cur[d] = _TReplicate()
+    # 2. shard moves: s->s (all-to-all) when the target axis is free, else s->r (all-gather)
+    for d in range(nd):
+        s, t = cur[d], dst[d]
+        if isinstance(s, _TShard) and s != t:
+            if isinstance(t, _TShard) and not any(isinstance(c, _TShard) and c.dim == t.dim
+                                                  for i, c in enumerate(cur) if i != d):
+                x = _all_to_all(x, s.dim, t.dim, mesh, d)
+                cur[d] = t
+            else:
+                x = _all_gather(x, s.dim, mesh, d)
+                cur[d] = _TReplicate()
+    # 3. new shards / partials from replicated data (no communication)
+    for d in range(nd):
+        s, t = cur[d], dst[d]
+        if isinstance(s, _TReplicate) and isinstance(t, _TShard):
+            x = _slice(x, t.dim, mesh, d)
+            cur[d] = t
+        elif isinstance(s, _TReplicate) and isinstance(t, _TPartial):
+            if not backward:   # backward: keep a replicated gradient replicated (see module doc)
+                x = _to_partial(x, mesh, d)
+            cur[d] = t
+    return x
+
+
+class _Reshard(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, dt, mesh, src, dst):
+        ctx.mesh, ctx.src, ctx.dst = mesh, src, dst
+        local = reshard_local(dt._local_tensor, mesh, src, dst)
+        return _dt.DTensor.from_local(local, mesh, dst, run_check=False, shape=dt.shape, stride=dt.stride())
+
+    @staticmethod
+    def backward(ctx, g):
+        if not isinstance(g, _dt.DTensor):
+            return None, None, None, None
+        gsrc = tuple(g.placements)
+        tgt = tuple(_TReplicate() if isinstance(p, _TPartial) and isinstance(q, _TReplicate) else p
+                    for p, q in zip(ctx.src, gsrc))
+        local = reshard_local(g._local_tensor, ctx.mesh, gsrc, tgt, backward=True)
+        out = _dt.DTensor.from_local(local, ctx.mesh, tgt, run_check=False, shape=g.shape, stride=g.stride())
+        return out, None, None, None
+
+
+def reshard(dt, placements):
+    """Differentiable reshard of a torch DTensor to ``placements`` (torch placement objects)."""
+    dst = tuple(placements)
+    src = tuple(dt.placements)
+    if src == dst:
+        return dt
+    return _Reshard.apply(dt, dt.device_mesh, src, dst)

@@ -380,6 +380,150 @@ def replicated_forward(*xs):
     return [_attr([-1] * len(x.shape), mesh) for x in xs], [_attr([-1] * len(xs[0].shape), mesh)]
 
 
+# -------------------------------------------------------------------------------------------- LLM op rules
+def _empty(spec):
+    return spec is None or not list(getattr(spec, "shape", []) or [])
+
+
+def rms_norm_forward(x, scale, epsilon=1e-6):
+    """Normalisation over the last axis: that axis is replicated, every leading axis keeps its sharding; scale
+    is replicated; outputs (y, inverse rms [leading axes])."""
+    nd = len(x.shape)
+    dm = _replicate_axes(x, [nd - 1])
+    mesh = _mesh([x, scale])
+    return [_attr(dm, mesh), _attr([-1], mesh)], [_attr(dm, mesh), _attr(dm[:-1], mesh)]
+
+
+def rms_norm_backward(x, scale, invvar, out_grad, epsilon=1e-6):
+    """The output gradient's leading-axis sharding drives; x and out_grad align, d_scale is PARTIAL on the mesh
+    dims that shard the leading (summed-over) axes."""
+    nd = len(x.shape)
+    nota = "".join(_letters(nd))
+    amap = merge_axes([nota, nota[:-1], nota], [x.dims_mapping, invvar.dims_mapping, out_grad.dims_mapping])
+    amap[nota[-1]] = -1
+    mesh = _mesh([x, scale, invvar, out_grad])
+    dm = _map(nota, amap)
+    return ([_attr(dm, mesh), _attr([-1], mesh), _attr(dm[:-1], mesh), _attr(dm, mesh)],
+            [_attr(dm, mesh), _attr([-1], mesh, {m for m in dm[:-1] if m != -1})])
+
+
+def swiglu_forward(x, y=None):
+    """swiglu(x, y) = silu(x) * y: elementwise.  Without y, x = [gate | up] on its last axis: a last-axis
+    sharding is accepted as the per-shard [gate_r | up_r] packing of a column-parallel gate_up projection."""
+    if _empty(y):
+        mesh = _mesh([x])
+        return [_attr(x.dims_mapping, mesh), None], [_attr(x.dims_mapping, mesh)]
+    return elementwise_forward(x, y)
+
+
+def swiglu_backward(x, y, out_grad):
+    if _empty(y):
+        nd = len(x.shape)
+        nota = "".join(_letters(nd))
+        amap = merge_axes([nota, nota], [out_grad.dims_mapping, x.dims_mapping])
+        mesh = _mesh([x, out_grad])
+        dm = _map(nota, amap)
+        return [_attr(dm, mesh), None, _attr(dm, mesh)], [_attr(dm, mesh), None]
+    ins, outs = elementwise_backward(x, y, out_grad)
+    return [ins[0], ins[1], outs[0]], outs[1:]
+
+
+def fused_rope_forward(q, k=None, v=None, sin=None, cos=None, position_ids=None, use_neox_rotary_style=True,
+                       time_major=False, rotary_emb_base=10000.0):
+    """q/k/v [b, s, h, d] (time_major: [s, b, h, d]) share one notation; head_dim is replicated; the sequence
+    axis may stay sharded only when sin/cos are given and position_ids are not (each shard then rotates its own
+    positions); a head sharding that does not divide k/v's head count is dropped.  sin/cos follow the
+    sequence sharding, position_ids take q's batch / sequence mapping with the sequence replicated."""
+    nota = "abcd"
+    seq = 0 if time_major else 1
+    specs = [q] + [t for t in (k, v) if not _empty(t)]
+    notas = [nota] * len(specs)
+    dms = [t.dims_mapping for t in specs]
+    ids_nota = "ba" if time_major else "ab"
+    if not _empty(position_ids):
+        notas.append(ids_nota)
+        dms.append(position_ids.dims_mapping)
+    amap = merge_axes(notas, dms)
+    mesh = _mesh(specs)
+    dm = _map(nota, amap)
+    seq_parallel = not _empty(sin) and not _empty(cos) and _empty(position_ids) and dm[seq] != -1
+    dm[3] = -1
+    if not seq_parallel:
+        dm[seq] = -1
+    if dm[2] != -1 and mesh is not None and getattr(mesh, "shape", None) is not None:
+        n = mesh.shape[dm[2]]
+        for t in specs[1:]:
+            if t.shape[2] != q.shape[2] and t.shape[2] % n:
+                dm[2] = -1
+    qa = _attr(dm, mesh)
+    ka = _attr(dm, mesh) if not _empty(k) else None
+    va = _attr(dm, mesh) if not _empty(v) else None
+    sc = None
+    if not _empty(sin):
+        snd = len(sin.shape)
+        sdm = [-1] * snd
+        if seq_parallel:
+            sdm[0 if snd == 2 else 1] = dm[seq]
+        sc = _attr(sdm, mesh)
+    pa = None
+    if not _empty(position_ids):
+        pdm = _map(ids_nota, amap)
+        pdm[1] = -1
+        pa = _attr(pdm, mesh)
+    return [qa, ka, va, sc, sc, pa], [qa, ka, va]
+
+
+def c_embedding_forward(weight, x, start_index=0, vocab_size=-1):
+    """Vocab-parallel embedding: weight [V, H] rows sharded -> output PARTIAL on that mesh dim (rows outside a
+    shard's vocab range contribute zero); ids keep their sharding and give the output's leading axes."""
+    nx = len(x.shape)
+    xn = "".join(_letters(nx, "jk"))
+    amap = merge_axes([xn, "jk"], [x.dims_mapping, weight.dims_mapping])
+    mesh = _mesh([weight, x])
+    row = weight.dims_mapping[0]
+    out = _attr(_map(xn + "k", amap), mesh, {row} if row > -1 else set())
+    return [_attr(_map("jk", amap), mesh), _attr(_map(xn, amap), mesh)], [out]
+
+
+def c_embedding_backward(weight, x, out_grad, start_index=0, vocab_size=-1):
+    """d_weight keeps the weight's row sharding; ids and out_grad align on the leading axes (a batch-sharded
+    gradient makes d_weight PARTIAL there, which the optimizer-side reduction resolves)."""
+    nx = len(x.shape)
+    xn = "".join(_letters(nx, "jk"))
+    amap = merge_axes([xn, xn + "k"], [x.dims_mapping, out_grad.dims_mapping])
+    amap["k"] = -1
+    mesh = _mesh([weight, x, out_grad])
+    wdm = [weight.dims_mapping[0], -1]
+    xdm = _map(xn, amap)
+    return ([_attr(wdm, mesh), _attr(xdm, mesh), _attr(_map(xn + "k", amap), mesh)],
+            [_attr(wdm, mesh, {m for m in xdm if m != -1})])
+
+
+def moe_gate_dispatch_forward(x, gate_logits, k=2, capacity=0, use_pad=True):
+    """x [S, H], gate_logits [S, E] -> y [E, C, H] (per-expert capacity slots), combine_weights [S, K],
+    scatter_index [K, S], expert_offset [E], expert_id [S, K]; the top-k axis is never sharded."""
+    amap = merge_axes(["sh", "se"], [x.dims_mapping, gate_logits.dims_mapping])
+    amap["k"] = -1
+    amap.setdefault("c", -1)
+    mesh = _mesh([x, gate_logits])
+    ins = [_attr(_map("sh", amap), mesh), _attr(_map("se", amap), mesh)]
+    outs = [_attr(_map(n, amap), mesh) for n in ("esh", "sk", "ks", "e", "sk")]
+    return ins, outs
+
+
+def moe_combine_forward(x, combine_weights, scatter_index):
+    """y[s, h] = sum_k x[scatter_index[s, k], h] * combine_weights[s, k]: a sharded k makes y PARTIAL (and then
+    h may not be sharded as well)."""
+    amap = merge_axes(["sh", "sk", "sk"], [x.dims_mapping, combine_weights.dims_mapping,
+                                           scatter_index.dims_mapping])
+    kd = amap.get("k", -1)
+    if kd != -1:
+        amap["h"] = -1
+    mesh = _mesh([x, combine_weights, scatter_index])
+    ins = [_attr(_map("sh", amap), mesh), _attr(_map("sk", amap), mesh), _attr(_map("sk", amap), mesh)]
+    return ins, [_attr(_map("sh", amap), mesh, {kd} if kd != -1 else set())]
+
+
 _RULES = {
     "matmul": SpmdRule("matmul", matmul_forward, matmul_backward),
     "matmul_v2": SpmdRule("matmul_v2", matmul_forward, matmul_backward),
@@ -398,8 +542,15 @@ _RULES = {
     "c_softmax_with_cross_entropy": SpmdRule("c_softmax_with_cross_entropy", c_softmax_with_cross_entropy_forward),
     "default_data_parallel": SpmdRule("default_data_parallel", default_data_parallel_forward),
     "replicated": SpmdRule("replicated", replicated_forward),
+    "rms_norm": SpmdRule("rms_norm", rms_norm_forward, rms_norm_backward),
+    "swiglu": SpmdRule("swiglu", swiglu_forward, swiglu_backward),
+    "fused_rotary_position_embedding": SpmdRule("fused_rotary_position_embedding", fused_rope_forward),
+    "fused_rope": SpmdRule("fused_rope", fused_rope_forward),
+    "c_embedding": SpmdRule("c_embedding", c_embedding_forward, c_embedding_backward),
+    "moe_gate_dispatch": SpmdRule("moe_gate_dispatch", moe_gate_dispatch_forward),
+    "moe_combine": SpmdRule("moe_combine", moe_combine_forward),
 }
-for _n in ("add", "subtract", "multiply", "divide", "maximum", "minimum", "relu", "gelu", "silu", "swiglu", "cast",
+for _n in ("add", "subtract", "multiply", "divide", "maximum", "minimum", "relu", "gelu", "silu", "cast",
            "scale", "where", "dropout", "fused_dropout_add", "pow", "exp", "sqrt", "tanh", "sigmoid"):
     _RULES[_n] = _RULES["elementwise"]
 for _n in ("sum", "mean", "max", "min", "prod", "reduce_sum", "reduce_mean", "reduce_max"):

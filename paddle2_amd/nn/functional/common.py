@@ -21,6 +21,9 @@ def linear(x, weight, bias=None, name=None):
     w = weight._t
     from ...ops import torch_ops as T
 
+    if isinstance(t, T._DTensor) or isinstance(w, T._DTensor):   # DistTensor: SPMD dispatch (matmul rule)
+        return _wrap(T.linear(t, w, None if bias is None else bias._t))
+
     if (t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and w.dim() == 2) or \
             getattr(w, "_p2_gt", None) is not None or T.WeightGradStore.route:  # main grad / zero-bubble split
         return _wrap(T.linear(t, w, None if bias is None else bias._t))

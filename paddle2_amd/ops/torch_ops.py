@@ -16,6 +16,18 @@ from . import _native as N
 
 _DT = N.DT_CODE
 
+try:   # DistTensor arguments take the SPMD dispatch at op entry (distributed/auto_parallel/dist_ops.py)
+    from torch.distributed.tensor import DTensor as _DTensor
+except Exception:  # noqa: BLE001
+    class _DTensor:  # noqa: D101
+        pass
+
+
+def _dist_ops():
+    from ..distributed.auto_parallel import dist_ops
+
+    return dist_ops
+
 
 def _rows(x: torch.Tensor):
     n = x.shape[-1]
@@ -113,11 +125,15 @@ class _NormFn(torch.autograd.Function):
 
 
 def rms_norm(x, w, eps=1e-6, residual=None):
+    if isinstance(x, _DTensor) or isinstance(residual, _DTensor):   # DistTensor: SPMD dispatch at op entry
+        return _dist_ops().rms_norm(x, w, eps, residual)
     y, h = _NormFn.apply(x, w, None, residual, eps, False)
     return (y, h) if residual is not None else y
 
 
 def layer_norm(x, w, b, eps=1e-5, residual=None):
+    if isinstance(x, _DTensor) or isinstance(residual, _DTensor):
+        return _dist_ops().rms_norm(x, w, eps, residual, layer=True, b=b)
     y, h = _NormFn.apply(x, w, b, residual, eps, True)
     return (y, h) if residual is not None else y
 
@@ -194,6 +210,8 @@ class _SwiGLUFn(torch.autograd.Function):
 
 
 def swiglu(x, y=None):
+    if isinstance(x, _DTensor) or isinstance(y, _DTensor):
+        return _dist_ops().swiglu(x, y)
     return _SwiGLUFn.apply(x, y)
 
 
@@ -285,6 +303,8 @@ def _rope_apply(x, cos, sin, pos, style, time_major, bwd, out=None):
 
 def rope(x, cos, sin, pos=None, style=0, time_major=False):
     """Apply rotary embedding. style 0 = rotate-half, 1 = rotate-every-two (interleaved)."""
+    if isinstance(x, _DTensor):
+        return _dist_ops().rope(x, cos, sin, pos, style, time_major)
     cos = cos.reshape(-1, x.shape[-1]).float().contiguous()
     sin = sin.reshape(-1, x.shape[-1]).float().contiguous()
     if pos is not None:
@@ -509,6 +529,8 @@ def _main_grad_accumulate(gt, x2, dy2):
 def linear(x, w, b=None):
     """Paddle-layout linear on bf16/fp16 GPU tensors through the layout-aware GEMM node (and on any device
     when the weight's gradient goes to an fp32 main-grad buffer); plain matmul otherwise."""
+    if isinstance(x, _DTensor) or isinstance(w, _DTensor):
+        return _dist_ops().linear(x, w, b)
     if (x.device.type == "cuda" and x.dtype in (torch.bfloat16, torch.float16) and w.dtype == x.dtype
             and w.dim() == 2 and x.shape[-1] == w.shape[0] and N.use_native(x)) or \
             (getattr(w, "_p2_gt", None) is not None and w.dim() == 2 and x.shape[-1] == w.shape[0]) or \
@@ -757,6 +779,8 @@ class _EmbFn(torch.autograd.Function):
 
 
 def embedding(ids, w, padding_idx=None, start=0):
+    if isinstance(w, _DTensor) or isinstance(ids, _DTensor):
+        return _dist_ops().embedding(ids, w, padding_idx, start)
     if padding_idx is not None and padding_idx < 0:
         padding_idx = padding_idx + w.shape[0]
     return _EmbFn.apply(ids, w, padding_idx, start)
@@ -863,6 +887,8 @@ class _FlashFn(torch.autograd.Function):
 
 def flash_attention(q, k, v, causal=False, scale=None):
     """q [B, Sq, Hq, D], k/v [B, Sk, Hk, D] -> (out [B, Sq, Hq, D], lse [B, Hq, Sq] fp32)."""
+    if isinstance(q, _DTensor) or isinstance(k, _DTensor):
+        return _dist_ops().flash_attention(q, k, v, causal, scale)
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
     return _FlashFn.apply(q, k, v, bool(causal), float(scale))

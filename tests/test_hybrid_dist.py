@@ -115,3 +115,15 @@ def test_weight_grad_store_splits_backward():
     import torch
 
     torch.testing.assert_close(lin.weight.grad._t, x._t.detach().t() @ torch.ones(5, 4))
+
+
+def test_semi_auto_llama_tensor_parallel_matches_single():
+    """2-rank semi-auto Llama (vocab-sharded embedding, column / row projections) through the SPMD dispatch at
+    op entry and the framework's reshard engine == one process, loss and every weight gradient."""
+    for r in run_workers("semi_auto_llama_worker.py", 2):
+        assert abs(r["loss"] - r["ref_loss"]) < 1e-5 * max(1.0, abs(r["ref_loss"])), r
+        assert r["out_diff"] < 1e-4, r
+        for n, d in r["grad_diff"].items():
+            assert d is not None and d < 1e-4, (n, d, r["trace"])
+        assert {"c_embedding", "rms_norm", "matmul", "rope", "flash_attention", "swiglu"} <= set(r["ops"]), r
+        assert {"all_reduce"} <= set(r["comms"]), r

@@ -81,3 +81,81 @@ def test_transpose_reshape_split_concat():
     assert ins == [[0, -1, -1]] and [o[0] for o in outs] == [[0, -1, -1]] * 2
     ins, outs = fwd("concat", [spec([64, 32], [0, -1]), spec([64, 32], [-1, 1])], axis=0)
     assert outs == [([-1, 1], set())]
+
+
+get_spmd_rule = get_phi_spmd_rule
+MESH24 = _Mesh([2, 4])
+
+
+def _spec(shape, dm):
+    return DistTensorSpec(shape, TensorDistAttr(dm, MESH24))
+
+
+def test_c_embedding_rule_reference_cases():
+    """test/auto_parallel/spmd_rules/test_c_embedding_rule.py: data parallel, vocab(row)-parallel, backward."""
+    r = get_spmd_rule("c_embedding")
+    table, x = _spec([512, 768], [-1, -1]), _spec([4, 1024], [1, -1])
+    ins, outs = r.infer_forward(table, x, 0, -1)
+    assert [a.dims_mapping for a in ins] == [[-1, -1], [1, -1]] and outs[0].dims_mapping == [1, -1, -1]
+    table.set_dims_mapping([1, -1])
+    x.set_dims_mapping([-1, -1])
+    ins, outs = r.infer_forward(table, x, 0, -1)
+    assert [a.dims_mapping for a in ins] == [[1, -1], [-1, -1]]
+    assert outs[0].dims_mapping == [-1, -1, -1] and outs[0]._is_partial() and outs[0]._partial_dims() == {1}
+    out = _spec([4, 1024, 768], [-1, -1, -1])
+    ins, outs = r.infer_backward(table, x, out, 0, -1)
+    assert [a.dims_mapping for a in ins] == [[1, -1], [-1, -1], [-1, -1, -1]] and outs[0].dims_mapping == [1, -1]
+    x.set_dims_mapping([0, -1])
+    out.set_dims_mapping([0, -1, -1])
+    ins, outs = r.infer_backward(table, x, out, 0, -1)
+    assert [a.dims_mapping for a in ins] == [[1, -1], [0, -1], [0, -1, -1]] and outs[0].dims_mapping == [1, -1]
+    assert outs[0]._partial_dims() == {0}   # batch-sharded ids: the table gradient is a partial sum
+
+
+def test_rms_norm_rule():
+    r = get_spmd_rule("rms_norm")
+    x, w = _spec([4, 16, 64], [0, 1, 1]), _spec([64], [0])
+    ins, outs = r.infer_forward(x, w, 1e-6)
+    assert ins[0].dims_mapping == [0, 1, -1] and ins[1].dims_mapping == [-1]
+    assert outs[0].dims_mapping == [0, 1, -1] and outs[1].dims_mapping == [0, 1]
+    og = _spec([4, 16, 64], [0, -1, -1])
+    ins, outs = r.infer_backward(x, w, _spec([4, 16], [0, 1]), og, 1e-6)
+    assert outs[0].dims_mapping == [0, 1, -1] and outs[1].dims_mapping == [-1] and outs[1]._partial_dims() == {0, 1}
+
+
+def test_swiglu_rule():
+    r = get_spmd_rule("swiglu")
+    ins, outs = r.infer_forward(_spec([8, 32], [0, 1]), None)   # packed [gate | up]: per-shard halves allowed
+    assert ins[0].dims_mapping == [0, 1] and outs[0].dims_mapping == [0, 1]
+    ins, outs = r.infer_forward(_spec([8, 32], [0, -1]), _spec([8, 32], [-1, 1]))
+    assert ins[0].dims_mapping == [0, 1] and ins[1].dims_mapping == [0, 1] and outs[0].dims_mapping == [0, 1]
+
+
+def test_fused_rope_rule():
+    r = get_spmd_rule("fused_rotary_position_embedding")
+    q = _spec([2, 64, 8, 32], [0, 1, -1, 1])
+    k = _spec([2, 64, 8, 32], [0, -1, 1, -1])
+    ins, outs = r.infer_forward(q, k, None, None, None, None)
+    # no sin/cos: the sequence axis cannot stay sharded; head_dim never is; heads take the free mesh dim
+    assert outs[0].dims_mapping == [0, -1, -1, -1] or outs[0].dims_mapping == [0, -1, 1, -1]
+    assert outs[0].dims_mapping[3] == -1 and outs[0].dims_mapping[1] == -1
+    sin = _spec([64, 32], [-1, -1])
+    q2 = _spec([2, 64, 8, 32], [0, 1, -1, -1])
+    ins, outs = r.infer_forward(q2, None, None, sin, sin, None)
+    assert outs[0].dims_mapping == [0, 1, -1, -1] and ins[3].dims_mapping == [1, -1]   # sequence parallel
+    ids = _spec([2, 64], [0, -1])
+    ins, outs = r.infer_forward(q2, None, None, sin, sin, ids)
+    assert outs[0].dims_mapping == [0, -1, -1, -1] and ins[5].dims_mapping == [0, -1]
+
+
+def test_moe_gate_dispatch_and_combine_rules():
+    ins, outs = get_spmd_rule("moe_gate_dispatch").infer_forward(_spec([64, 32], [0, -1]), _spec([64, 8], [0, 1]),
+                                                                 2, 16, True)
+    assert [a.dims_mapping for a in ins] == [[0, -1], [0, 1]]
+    assert [a.dims_mapping for a in outs] == [[1, 0, -1], [0, -1], [-1, 0], [1], [0, -1]]
+    ins, outs = get_spmd_rule("moe_combine").infer_forward(_spec([64, 32], [-1, -1]), _spec([64, 2], [-1, 1]),
+                                                           _spec([64, 2], [-1, 1]))
+    assert outs[0].dims_mapping == [-1, -1] and outs[0]._partial_dims() == {1}   # sharded k -> partial
+    ins, outs = get_spmd_rule("moe_combine").infer_forward(_spec([64, 32], [0, 1]), _spec([64, 2], [0, -1]),
+                                                           _spec([64, 2], [0, -1]))
+    assert outs[0].dims_mapping == [0, 1] and not outs[0]._partial_dims()
