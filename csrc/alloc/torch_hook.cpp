@@ -1,29 +1,156 @@
-// Installs the native allocator (auto_growth.cpp) as PyTorch-ROCm's device allocator WITH its record-stream hook.
+// Installs the native allocator (auto_growth.cpp) as PyTorch-ROCm's device allocator WITH its record-stream hook
+// and hipGraph private-pool support.
 //
 // torch.cuda.memory.CUDAPluggableAllocator only takes malloc/free, so Tensor.record_stream (used by the executor's
-// stream analyzer, AsyncLoad, the stage-3 prefetch stream and c10d's ProcessGroupNCCL for async collectives) was
+// stream analyzer, AsyncLoad, the stage-3 prefetch stream and the process groups for async collectives) was
 // a no-op under it: a tensor still read on a side stream could be re-handed out on its allocating stream.  This
 // shim builds the pluggable allocator in C++ and sets record_stream_fn -> pd_alloc_record_stream, the
 // reference's StreamSafeCUDAAllocator::RecordStream (stream_safe_cuda_allocator.cc) equivalent.
+//
+// Graph capture (torch.cuda.graph / CUDAGraph: the serving decode step, the static executor's replay) asks the
+// allocator for a private pool: begin_allocate_to_pool(device, pool, filter) routes every allocation whose
+// stream passes `filter` (the capturing stream) to that pool until end_allocate_to_pool.  Pool blocks are
+// dedicated hipMalloc allocations: memory freed inside the pool is reused only by the same pool (a replay
+// rewrites exactly the addresses the capture recorded), no events are recorded or queried while a capture is
+// underway (both would become graph nodes or invalidate the capture), and release_pool returns the pool's free
+// blocks to the driver (blocks still referenced are freed when their tensor dies).
 #include <hip/hip_runtime.h>
 #include <torch/csrc/cuda/CUDAPluggableAllocator.h>
 
+#include <functional>
+#include <map>
 #include <memory>
+#include <mutex>
+#include <unordered_map>
+#include <utility>
+#include <vector>
 
 extern "C" {
 void* pd_alloc_malloc(size_t size, int device, hipStream_t stream);
 void pd_alloc_free(void* ptr, size_t size, int device, hipStream_t stream);
 void pd_alloc_record_stream(void* ptr, hipStream_t stream);
+}
 
-// 0 on success, 1 if the created allocator is not a CUDAPluggableAllocator (no record-stream hook possible)
+namespace {
+
+using PoolId = std::pair<unsigned long long, unsigned long long>;
+
+struct Router {
+  std::mutex mu;
+  struct Active {
+    int device;
+    PoolId pool;
+    std::function<bool(hipStream_t)> filter;
+  };
+  std::vector<Active> active;                                   // pools currently capturing
+  std::unordered_map<void*, std::pair<PoolId, size_t>> live;    // pool block -> (pool, bytes)
+  std::map<PoolId, std::multimap<size_t, void*>> free_blocks;   // per pool: freed blocks by size
+  std::map<PoolId, bool> released;
+
+  void* malloc(size_t size, int device, hipStream_t stream) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (auto& a : active) {
+        if (a.device != device || !a.filter(stream)) continue;
+        auto& fl = free_blocks[a.pool];
+        auto it = fl.lower_bound(size);
+        if (it != fl.end() && it->first <= 2 * size + (1 << 20)) {   // best fit, bounded waste
+          void* p = it->second;
+          live[p] = {a.pool, it->first};
+          fl.erase(it);
+          return p;
+        }
+        const size_t bytes = (size + 511) & ~size_t(511);
+        void* p = nullptr;
+        int prev = 0;
+        hipGetDevice(&prev);
+        if (prev != device) hipSetDevice(device);
+        const hipError_t e = hipMalloc(&p, bytes ? bytes : 512);
+        if (prev != device) hipSetDevice(prev);
+        if (e != hipSuccess) return nullptr;
+        live[p] = {a.pool, bytes};
+        return p;
+      }
+    }
+    return pd_alloc_malloc(size, device, stream);
+  }
+
+  void free(void* ptr, size_t size, int device, hipStream_t stream) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto it = live.find(ptr);
+      if (it != live.end()) {
+        const PoolId pool = it->second.first;
+        const size_t bytes = it->second.second;
+        live.erase(it);
+        if (released[pool]) hipFree(ptr);
+        else free_blocks[pool].emplace(bytes, ptr);
+        return;
+      }
+    }
+    pd_alloc_free(ptr, size, device, stream);
+  }
+
+  void begin(int device, PoolId pool, std::function<bool(hipStream_t)> filter) {
+    std::lock_guard<std::mutex> lk(mu);
+    released[pool] = false;
+    active.push_back({device, pool, std::move(filter)});
+  }
+
+  void end(int device, PoolId pool) {
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto it = active.begin(); it != active.end(); ++it) {
+      if (it->device == device && it->pool == pool) {
+        active.erase(it);
+        break;
+      }
+    }
+  }
+
+  void release(int device, PoolId pool) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto fit = free_blocks.find(pool);
+    if (fit != free_blocks.end()) {
+      hipDeviceSynchronize();   // a replay still in flight may use the blocks
+      for (auto& kv : fit->second) hipFree(kv.second);
+      free_blocks.erase(fit);
+    }
+    released[pool] = true;      // blocks still live are freed by their own free()
+  }
+};
+
+Router& router() {
+  static Router* r = new Router();   // never destroyed: frees may arrive during interpreter teardown
+  return *r;
+}
+
+PoolId key(const c10::hip::MempoolId_t& id) { return {(unsigned long long)id.first, (unsigned long long)id.second}; }
+
+}  // namespace
+
+extern "C" {
+
+// 0 on success, 1 if the created allocator is not a CUDAPluggableAllocator (no hooks possible)
 int pd_alloc_install_torch() {
   namespace P = torch::cuda::CUDAPluggableAllocator;
   auto a = P::createCustomAllocator(
-      [](size_t size, int device, hipStream_t stream) { return pd_alloc_malloc(size, device, stream); },
-      [](void* ptr, size_t size, int device, hipStream_t stream) { pd_alloc_free(ptr, size, device, stream); });
+      [](size_t size, int device, hipStream_t stream) { return router().malloc(size, device, stream); },
+      [](void* ptr, size_t size, int device, hipStream_t stream) { router().free(ptr, size, device, stream); });
   auto pa = std::dynamic_pointer_cast<P::CUDAPluggableAllocator>(a);
   if (!pa) return 1;
-  pa->set_record_stream_fn([](void* ptr, hipStream_t stream) { pd_alloc_record_stream(ptr, stream); });
+  pa->set_record_stream_fn([](void* ptr, hipStream_t stream) {
+    {
+      std::lock_guard<std::mutex> lk(router().mu);
+      if (router().live.count(ptr)) return;   // pool blocks: ordered by the captured stream
+    }
+    pd_alloc_record_stream(ptr, stream);
+  });
+  pa->set_begin_allocate_to_pool(
+      [](int device, c10::hip::MempoolId_t id, std::function<bool(hipStream_t)> filter) {
+        router().begin(device, key(id), std::move(filter));
+      });
+  pa->set_end_allocate_to_pool_fn([](int device, c10::hip::MempoolId_t id) { router().end(device, key(id)); });
+  pa->set_release_pool([](int device, c10::hip::MempoolId_t id) { router().release(device, key(id)); });
   P::changeCurrentAllocator(a);
   return 0;
 }

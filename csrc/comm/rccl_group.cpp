@@ -26,6 +26,7 @@
 #include <pybind11/stl.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -40,6 +41,10 @@
 namespace py = pybind11;
 
 namespace {
+
+// set by shutdown() (Python atexit / destroy_process_group): later destructors must not touch the HIP runtime or
+// RCCL, which may already be torn down when the interpreter finalises the last Python references
+std::atomic<bool> g_shutdown{false};
 
 void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("[rccl_group] ") + what + ": " + hipGetErrorString(e));
@@ -87,9 +92,14 @@ struct Comm {
   hipStream_t stream = nullptr;
   int device = 0, rank = 0, nranks = 1;
   bool aborted = false;
-  ~Comm() {
+  void release() {
     if (comm && !aborted) ncclCommDestroy(comm);
     if (stream) hipStreamDestroy(stream);
+    comm = nullptr;
+    stream = nullptr;
+  }
+  ~Comm() {
+    if (!g_shutdown) release();
   }
 };
 
@@ -110,8 +120,13 @@ class EventPool {
     std::lock_guard<std::mutex> lk(mu_);
     free_.push_back(e);
   }
-  ~EventPool() {
+  void release() {
+    std::lock_guard<std::mutex> lk(mu_);
     for (hipEvent_t e : free_) hipEventDestroy(e);
+    free_.clear();
+  }
+  ~EventPool() {
+    if (!g_shutdown) release();
   }
 
  private:
@@ -151,6 +166,7 @@ class Task {
        int timeout_ms)
       : comms_(std::move(comms)), ends_(std::move(ends)), pool_(std::move(pool)), timeout_ms_(timeout_ms) {}
   ~Task() {
+    if (g_shutdown) return;
     for (hipEvent_t e : ends_) {
       // an event still pending on a live stream may be reused only after it completes
       if (hipEventQuery(e) == hipSuccess) pool_->put(e);
@@ -361,6 +377,15 @@ class RcclGroup {
     return py::cast(t);
   }
 
+  // finish outstanding work, destroy communicators, streams and pooled events while the runtime is alive
+  void shutdown() {
+    if (g_shutdown) return;
+    hipDeviceSynchronize();
+    for (auto& kv : comms_) kv.second->release();
+    pool_->release();
+    g_shutdown = true;
+  }
+
   void abort() {
     for (auto& kv : comms_) {
       if (!kv.second->aborted) {
@@ -522,5 +547,6 @@ PYBIND11_MODULE(_rccl, m) {
       .def("group_start", &RcclGroup::group_start)
       .def("group_end", &RcclGroup::group_end)
       .def("barrier", &RcclGroup::barrier)
-      .def("abort", &RcclGroup::abort);
+      .def("abort", &RcclGroup::abort)
+      .def("shutdown", &RcclGroup::shutdown);
 }

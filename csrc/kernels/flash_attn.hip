@@ -29,11 +29,12 @@
 //    from its one LDS image both by rows (S) and by columns (dQ), keeping the wave under 256 VGPRs;
 //  * the workgroup sweeps every query head of its GQA group x every 32-row query tile, so dK/dV
 //    are complete in registers and written once (no cross-workgroup sum for dK/dV);
-//  * dS goes through LDS once for dQ = dS.K (4 waves split D).  dQ is NOT summed with float atomics:
-//    at the ≈1.3 TB/s chip-wide atomic rate the 2.2 GB/layer of fp32 adds (B2 S4096 H32) was the
-//    floor of the whole kernel; each key block instead writes its dQ tile with plain non-temporal
-//    stores into its own fp32 slab and dq_reduce_kernel sums the slabs a row actually received
-//    (plain stores run ≈4-5x the atomic rate, and the sum is bitwise reproducible);
+//  * dS goes through LDS once for dQ = dS.K (4 waves split D).  Dense mode (default): every key block
+//    adds its dQ tile into ONE zeroed fp32 slab with buffer fp32 atomics (fa_dq_atomic; the slab is then
+//    converted by dq_reduce_kernel) — at B8 S4096 the per-key-block slabs cost more HBM than the atomics;
+//    deterministic mode (FLAGS_cudnn_deterministic / PADDLE2_AMD_FA_DQ_ATOMIC=0) and the varlen / FlashMask
+//    modes write per-key-block slabs with plain stores, summed in a fixed order by dq_reduce_kernel
+//    (bitwise reproducible);
 //  * the next (head, q-tile) step's Q / dO / lse / delta are prefetched into registers while the
 //    current step computes (T14 issue-early / write-late).
 #include "common.h"

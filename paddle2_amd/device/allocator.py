@@ -141,9 +141,28 @@ def violations(max_n=64):
 
 
 def _maybe_enable_from_env():
-    v = os.environ.get("FLAGS_use_native_allocator", "")
-    if v.lower() in ("1", "true", "yes", "on"):
-        guard = int(os.environ.get("PD_ALLOC_GUARD_BYTES", "0") or 0)
-        if guard or os.environ.get("PD_ALLOC_CANARY"):
-            debug(guard or 4096, bool(os.environ.get("PD_ALLOC_CANARY")))
+    """The native allocator is the process default on a GPU machine (reference: allocator_facade.cc picks
+    auto_growth); ``FLAGS_use_native_allocator=0`` keeps torch's caching allocator.  Enabled at import, before
+    the first device allocation; if torch already allocated on the device (paddle2_amd imported late) the
+    default quietly stays torch's, while an explicit ``=1`` raises."""
+    v = os.environ.get("FLAGS_use_native_allocator", "").strip().lower()
+    if v in ("0", "false", "no", "off"):
+        return
+    explicit = v in ("1", "true", "yes", "on")
+    if not explicit:
+        hook = os.path.join(os.path.dirname(library_path()), "_pd_alloc_torch.so")
+        if not (os.path.exists(library_path()) and os.path.exists(hook)):
+            return
+        try:
+            if torch.cuda.device_count() == 0 or torch.cuda.is_initialized():
+                return
+        except Exception:  # noqa: BLE001
+            return
+    guard = int(os.environ.get("PD_ALLOC_GUARD_BYTES", "0") or 0)
+    if guard or os.environ.get("PD_ALLOC_CANARY"):
+        debug(guard or 4096, bool(os.environ.get("PD_ALLOC_CANARY")))
+    try:
         enable()
+    except RuntimeError:
+        if explicit:
+            raise

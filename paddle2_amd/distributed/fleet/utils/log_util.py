@@ -84,10 +84,12 @@ def check_memory_usage(msg=""):
     GB = float(1 << 30)
     out = {}
     if torch.cuda.is_available():
-        out["max_memory_allocated_size"] = torch.cuda.max_memory_allocated() / GB
-        out["max_memory_reserved_size"] = torch.cuda.max_memory_reserved() / GB
-        out["memory_allocated_size"] = torch.cuda.memory_allocated() / GB
-        out["memory_reserved_size"] = torch.cuda.memory_reserved() / GB
+        from ....device import cuda as _dc   # native-allocator stats when it is the device allocator
+
+        out["max_memory_allocated_size"] = _dc.max_memory_allocated() / GB
+        out["max_memory_reserved_size"] = _dc.max_memory_reserved() / GB
+        out["memory_allocated_size"] = _dc.memory_allocated() / GB
+        out["memory_reserved_size"] = _dc.memory_reserved() / GB
     try:
         import psutil
 

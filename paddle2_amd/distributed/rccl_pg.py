@@ -111,6 +111,7 @@ class ProcessGroupRCCL(dist.ProcessGroup):
         self._g = _native().RcclGroup(store, prefix, rank, size, self._dev, tms)
         self._ext = {}
         self._scratch = None
+        _LIVE.append(self._g)
 
     # ------------------------------------------------------------------ plumbing
     def getBackendName(self):
@@ -345,6 +346,19 @@ class ProcessGroupRCCL(dist.ProcessGroup):
         post = self._copyback([(t, c) for s, c, t, _ in conts if not s and c is not t])
         w = _Work(task, [c for _, c, _, _ in conts], post)
         return [w] * len(ops)
+
+
+_LIVE = []   # every native group: torn down at interpreter exit, before the HIP runtime's own atexit teardown
+
+
+def shutdown_all():
+    while _LIVE:
+        _LIVE.pop().shutdown()
+
+
+import atexit as _atexit  # noqa: E402
+
+_atexit.register(shutdown_all)
 
 
 def _create(store, rank, size, timeout):

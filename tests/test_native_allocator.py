@@ -62,27 +62,77 @@ def test_gpu_context_streams():
 
 @pytest.mark.gpu
 def test_native_allocator_mem_pool_integrity():
-    from paddle2_amd.device import allocator
-
-    allocator.configure(chunk_mb=64, limit_bytes=0)
-    before = allocator.stats(torch.cuda.current_device())
-    pool = allocator.mem_pool()
-    g = torch.Generator().manual_seed(0)
-    live = []
-    with torch.cuda.use_mem_pool(pool):
-        for i in range(200):
-            n = int(torch.randint(1, 1 << 22, (1,), generator=g))
-            t = torch.full((n,), float(i % 97), device="cuda")
-            live.append((i, t))
-            if i % 3 == 0:
-                live.pop(int(torch.randint(0, len(live), (1,), generator=g)))
+    """A torch MemPool backed by the native allocator inside a caching-allocator process (FLAGS=0): random
+    sized live tensors keep their contents and the native chunk pool grows."""
+    script = textwrap.dedent("""
+        import torch
+        from paddle2_amd.device import allocator
+        allocator.configure(chunk_mb=64, limit_bytes=0)
+        before = allocator.stats(torch.cuda.current_device())
+        pool = allocator.mem_pool()
+        g = torch.Generator().manual_seed(0)
+        live = []
+        with torch.cuda.use_mem_pool(pool):
+            for i in range(200):
+                n = int(torch.randint(1, 1 << 22, (1,), generator=g))
+                t = torch.full((n,), float(i % 97), device="cuda")
+                live.append((i, t))
+                if i % 3 == 0:
+                    live.pop(int(torch.randint(0, len(live), (1,), generator=g)))
+            torch.cuda.synchronize()
+            for i, t in live:
+                assert float(t.min()) == float(i % 97) == float(t.max())
+        after = allocator.stats(torch.cuda.current_device())
+        assert after["num_grow"] > before["num_grow"] and after["reserved"] > 0
+        del live, t
         torch.cuda.synchronize()
-        for i, t in live:
-            assert float(t.min()) == float(i % 97) == float(t.max())
-    after = allocator.stats(torch.cuda.current_device())
-    assert after["num_grow"] > before["num_grow"] and after["reserved"] > 0
-    del live, t
-    torch.cuda.synchronize()
+        print("OK")
+    """)
+    env = dict(os.environ, FLAGS_use_native_allocator="0")
+    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stderr[-3000:]
+
+
+@pytest.mark.gpu
+def test_native_allocator_is_default_and_supports_graph_capture():
+    """The native allocator is the process default on the GPU (FLAGS unset), and hipGraph capture gets a
+    private pool from it: a captured step replays correctly after other allocations reuse freed memory."""
+    script = textwrap.dedent("""
+        import json, torch
+        import paddle2_amd as paddle
+        from paddle2_amd.device import allocator
+        x = torch.randn(1024, 1024, device="cuda")
+        w = torch.randn(1024, 1024, device="cuda")
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                y = torch.relu(x @ w) + 1.0
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            y = torch.relu(x @ w) + 1.0
+            z = y * 2.0
+        junk = [torch.randn(512, 512, device="cuda") for _ in range(20)]   # reuse of freed general memory
+        del junk
+        x.copy_(torch.randn(1024, 1024, device="cuda"))
+        g.replay()
+        torch.cuda.synchronize()
+        ref = (torch.relu(x @ w) + 1.0) * 2.0
+        ok = bool(torch.allclose(z, ref, atol=1e-3, rtol=1e-3))
+        del g
+        torch.cuda.synchronize()
+        print(json.dumps({"active": allocator.is_active(), "hooked": allocator.has_record_stream(), "ok": ok,
+                          "peak": paddle.device.cuda.max_memory_allocated()}))
+    """)
+    env = dict(os.environ)
+    env.pop("FLAGS_use_native_allocator", None)
+    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["active"] and res["hooked"] and res["ok"] and res["peak"] > 0, res
 
 
 @pytest.mark.gpu
@@ -123,9 +173,7 @@ def test_native_allocator_process_wide_training():
     res = {}
     for mode in ("native", "caching"):
         env = dict(os.environ)
-        env.pop("FLAGS_use_native_allocator", None)
-        if mode == "native":
-            env["FLAGS_use_native_allocator"] = "1"
+        env["FLAGS_use_native_allocator"] = "1" if mode == "native" else "0"
         r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300, env=env)
         assert r.returncode == 0, r.stderr[-3000:]
         res[mode] = json.loads(r.stdout.strip().splitlines()[-1])
