@@ -97,7 +97,9 @@ struct Device {
   Stats st;
 };
 
-static Device g_dev[kMaxDevices];
+// Immortal: torch frees the last tensors (MemPools, module globals) during interpreter teardown, after static
+// destructors would have run — the per-device state must outlive every free.
+static Device* const g_dev = new Device[kMaxDevices];
 static size_t g_chunk_bytes = size_t(256) << 20;
 // debug: every block gets g_guard extra bytes past the request; with g_canary the slack is filled with a
 // pattern at allocation and verified at free, so a kernel writing past its tensor is reported (pointer,
@@ -108,9 +110,9 @@ constexpr unsigned char kCanary = 0xA5;
 struct Violation {
   uint64_t ptr, req, offset;
 };
-static std::vector<Violation> g_violations;
+static std::vector<Violation>& g_violations = *new std::vector<Violation>();
 static uint64_t g_limit_bytes = 0;   // 0 = unlimited
-static std::mutex g_cfg_mu;
+static std::mutex& g_cfg_mu = *new std::mutex();
 
 static inline size_t round_up(size_t n, size_t a) { return (n + a - 1) / a * a; }
 
