@@ -84,8 +84,9 @@ def test_native_allocator_mem_pool_integrity():
                 assert float(t.min()) == float(i % 97) == float(t.max())
         after = allocator.stats(torch.cuda.current_device())
         assert after["num_grow"] > before["num_grow"] and after["reserved"] > 0
-        del live, t
+        del live, t, pool          # release the pool's segments while the HIP runtime is alive
         torch.cuda.synchronize()
+        torch.cuda.empty_cache()
         print("OK")
     """)
     env = dict(os.environ, FLAGS_use_native_allocator="0")
