@@ -65,7 +65,12 @@ struct Router {
         int prev = 0;
         hipGetDevice(&prev);
         if (prev != device) hipSetDevice(device);
+        // a malloc inside a global-mode capture invalidates it: relax this thread's capture mode around it
+        // (the capture records new VA; replays do not allocate again)
+        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+        hipThreadExchangeStreamCaptureMode(&mode);
         const hipError_t e = hipMalloc(&p, bytes ? bytes : 512);
+        hipThreadExchangeStreamCaptureMode(&mode);
         if (prev != device) hipSetDevice(prev);
         if (e != hipSuccess) return nullptr;
         live[p] = {a.pool, bytes};
