@@ -377,12 +377,12 @@ class RcclGroup {
     return py::cast(t);
   }
 
-  // finish outstanding work, destroy communicators, streams and pooled events while the runtime is alive
+  // interpreter exit: finish outstanding work, then leave communicators / streams / events to process teardown.
+  // Tensors freed later in finalisation may still carry record_stream marks on a comm stream (the allocator
+  // fences their reuse with events on it), so the streams must stay valid; destructors become no-ops.
   void shutdown() {
     if (g_shutdown) return;
     hipDeviceSynchronize();
-    for (auto& kv : comms_) kv.second->release();
-    pool_->release();
     g_shutdown = true;
   }
 
