@@ -1,0 +1,324 @@
+// v7: the TN MFMA GEMM — both operands K-major.  dgrad dx = dy . W^T reads W as [N, K] rows in place; the
+// forward y = x . W runs on W^T (one HBM-speed transpose of the weight per forward, ops/gemm.py), so every
+// fragment read is a conflict-free ds_read_b128 and no transposed LDS read is needed.
+//
+// Reference parity: paddle/phi/kernels/impl/matmul_kernel_impl.h:108 (matmul / matmul_grad) and
+// paddle/phi/kernels/funcs/fused_gemm_epilogue.h:397 (bias epilogue); the SwiGLU epilogue fuses the
+// reference's separate swiglu op (paddle/phi/kernels/fusion/gpu/swiglu_kernel.cu) into the gate|up GEMM.
+//
+// Tile, LDS images and ring are v4's (gemm.hip): 256x256x64 tile, 4 waves x 128x128 wave tiles with the
+// accumulators pinned in AGPRs, a 2-stage LDS-DMA ring (tile t+2 streamed into the stage of tile t once every
+// wave holds its fragments), persistent static schedule as v6 (grid = min(tiles, CUs), XCD-chunked tile slots).
+// What v7 changes is the instruction schedule of a K-tile (128 MFMAs per wave):
+//  * the next K-tile's buffer descriptors are a handful of SALU ops placed between MFMAs (records = end - base
+//    in 32 bits: operand extents are < 2 GiB, host-checked) instead of a serial 64-bit clamp block in front of
+//    the K-tile's first MFMA;
+//  * each LDS-DMA piece is one asm statement `s_add m0 / v_mfma / buffer_load ... lds`: the MFMA covers the
+//    M0 -> LDS-DMA hazard, where the compiler's form puts an s_nop in front of every piece;
+//  * fragment reads go one per two MFMAs (v4 issued them one per MFMA in 16-read bursts), and the MFMA order is
+//    A-fragment-major so a K-tile can start after 9 of its 16 step-0 reads;
+//  * SCHED bit 0: per-operand barriers (4 per K-tile: B's stage is released after B's step-1 reads and A's after
+//    A's; tile t+1's B is waited for before its A) instead of 2;  bit 1: s_setprio 1 around the MFMA stream.
+#include "gemm_core.h"
+
+namespace pd {
+namespace gm {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64;
+
+// Per-lane source offsets of this wave's 8 LDS-DMA pieces of a K-major operand (v4's image): piece j fills LDS
+// block 8(j&3) + 4(j>>2) + wave = rows 64(j&3) + 8(wave + 4(j>>2)) + (lane>>3), 16-B chunk (lane&7) ^ ((row>>1)&7).
+// SwiGLU: tile row r of the packed gate|up weight (read as [2H, K] rows) is gate row (r>>6)*32 + (r&31) or the
+// matching up row H + ... (bit 5), relative to the tile's first gate row.
+template <bool SWI>
+__device__ __forceinline__ void kk_offsets(unsigned (&v)[8], long ld, int H, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int r = 64 * (j & 3) + 8 * (wave + 4 * (j >> 2)) + (lane >> 3);
+    const int lc = (lane & 7) ^ ((r >> 1) & 7);
+    const long row = SWI ? (long)((r >> 6) * 32 + (r & 31) + ((r & 32) ? H : 0)) : (long)r;
+    v[j] = (unsigned)((row * ld + lc * 8) * 2);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// one MFMA with an LDS-DMA piece behind it: M0 (LDS destination = wb + IMM) is written before the MFMA, which
+// covers the M0 -> buffer_load ... lds hazard
+template <int IMM>
+__device__ __forceinline__ void mfma_dma(f32x4v& c, const bf16x8& a, const bf16x8& b, unsigned wb, unsigned voff,
+                                         const i32x4& srd) {
+  asm volatile(
+      "s_add_u32 m0, %1, %2\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %3, %4, %0\n\t"
+      "buffer_load_dwordx4 %5, %6, 0 offen lds"
+      : "+a"(c)
+      : "s"(wb), "i"(IMM), "v"(a), "v"(b), "v"(voff), "s"(srd)
+      : "memory");
+}
+template <int IMM>
+__device__ __forceinline__ void dma_only(unsigned wb, unsigned voff, const i32x4& srd) {
+  asm volatile(
+      "s_add_u32 m0, %0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, 0 offen lds"
+      :
+      : "s"(wb), "i"(IMM), "v"(voff), "s"(srd)
+      : "memory");
+}
+
+// LDS byte offset (from the wave's piece base) of piece j of operand B? in stage ST
+template <bool ISB, int ST, int J>
+constexpr int piece_dst() {
+  return ST * TILE_BYTES + (8 * (J & 3) + 4 * (J >> 2)) * 1024 + (ISB ? B_OFF : 0);
+}
+
+template <int EPI, int SCHED>
+__global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
+  constexpr bool BAR4 = SCHED & 1, PRIO = (SCHED & 2) != 0;
+  constexpr bool SWI = EPI == kEpiSwiGLU;
+  __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
+  const unsigned sbase = (unsigned)(size_t)(lds_char*)smem_raw;
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int G = gridDim.x;
+  const int slot = xcd_remap(blockIdx.x, G);
+  const int ntile = slot < nwg ? (nwg - slot + G - 1) / G : 0;
+  if (ntile == 0) return;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nt = p.K / BK;  // even, K % 128 == 0 (host-checked)
+
+  f32x4v acc[2][8][4];
+  // zero the accumulators of a tile; the zeros are pinned (asm operands) in front of an s_nop so the VALU writes
+  // keep their wait states before the first MFMA reads them as src C (the compiler would otherwise re-place the
+  // zeroing at the tile-loop head, right in front of the asm MFMAs whose operands it cannot see)
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[h][i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+          asm volatile("" : "+a"(acc[h][i][j]));
+        }
+    asm volatile("s_nop 4" ::: "memory");
+  };
+
+  unsigned va[8], vb[8];
+  kk_offsets<false>(va, p.lda, 0, wave, lane);
+  kk_offsets<SWI>(vb, p.ldb, p.H, wave, lane);
+  const int arow = wm * 128, bcolw = wn * 128;
+  const Rd4<true> ra = rd4_setup<true>(sbase, arow, lane);
+  const Rd4<true> rb = rd4_setup<true>(sbase + B_OFF, bcolw, lane);
+  const unsigned wdst = __builtin_amdgcn_readfirstlane(sbase + wave * 1024);
+
+  // stream state: bases of the current tile (c*) and of this workgroup's next tile (n*, live if nlive)
+  const unsigned a_end = (unsigned)(size_t)p.a_end, b_end = (unsigned)(size_t)p.b_end;
+  auto a_base = [&](int tm) { return (u64)(size_t)(p.A + (long)tm * BM * p.lda); };
+  auto b_base = [&](int tn) { return (u64)(size_t)(p.B + (long)tn * (SWI ? 128 : BN) * p.ldb); };
+  int ctm, ctn;
+  tile_of(p, slot, ctm, ctn);
+  u64 ca = a_base(ctm), cb = b_base(ctn), na = ca, nb = cb;
+  bool nlive = false;
+  auto set_next = [&](int u) {
+    nlive = u + 1 < ntile;
+    if (nlive) {
+      int tm, tn;
+      tile_of(p, slot + (u + 1) * G, tm, tn);
+      na = a_base(tm);
+      nb = b_base(tn);
+    }
+  };
+  set_next(0);
+  // descriptors of stream K-tile kk (0 <= kk < nt + 2; kk >= nt: the next tile's K-tile kk - nt)
+  // (bases are < 2^48: the descriptor's high word is the address's high 16 bits, stride 0)
+  auto desc = [&](int kk, u64 cur, u64 nxt, unsigned end) {
+    const bool nx = kk >= nt;
+    const unsigned off = (unsigned)(nx ? kk - nt : kk) << 7;  // * BK * 2 bytes
+    const u64 b = (nx ? nxt : cur) + off;
+    const bool live = !nx || nlive;
+    return i32x4{(int)(unsigned)b, (int)(unsigned)(b >> 32), live ? (int)(end - (unsigned)b) : 0, 0x00020000};
+  };
+  auto descs = [&](int kk, i32x4& sa, i32x4& sb) {
+    sa = desc(kk, ca, na, a_end);
+    sb = desc(kk, cb, nb, b_end);
+  };
+
+  bf16x8 xa[8], xb[8], ya[8], yb[8];  // k32 step 0 / step 1 fragments of the current K-tile
+
+  // prologue: K-tiles 0 and 1 of the first tile in flight, wait for K-tile 0 (everyone's), read its step 0
+  {
+    i32x4 sa, sb;
+    descs(0, sa, sb);
+    sfor<8>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      dma_only<piece_dst<true, 0, j>()>(wdst, vb[j], sb);
+    });
+    sfor<8>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      dma_only<piece_dst<false, 0, j>()>(wdst, va[j], sa);
+    });
+    descs(1, sa, sb);
+    sfor<8>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      dma_only<piece_dst<true, 1, j>()>(wdst, vb[j], sb);
+    });
+    sfor<8>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      dma_only<piece_dst<false, 1, j>()>(wdst, va[j], sa);
+    });
+  }
+  wait_vm<16>();
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  sfor<8>([&](auto U) { xb[decltype(U)::value] = frag4<true, decltype(U)::value, 0, 0>(rb); });
+  sfor<8>([&](auto U) { xa[decltype(U)::value] = frag4<true, decltype(U)::value, 0, 0>(ra); });
+
+  // slot positions (MFMA index q of the K-tile, 0..127)
+  constexpr int REL_B = BAR4 ? 16 : 32, REL_A = 32;        // stage release barriers (before MFMA q)
+  constexpr int DMA_B = REL_B + 1, DMA_A = BAR4 ? 33 : 49;  // first piece slots (then every 2 MFMAs)
+  constexpr int LND_B = BAR4 ? 80 : 96, LND_A = 96;        // tile t+1 landed barriers
+  constexpr int XRD_B = LND_B, XRD_A = BAR4 ? 96 : 112;    // first x-read slots (then every 2 MFMAs)
+
+  auto ktile = [&](auto ST, int k) {
+    constexpr int st = decltype(ST)::value;
+    i32x4 sa, sb;
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+    sfor<128>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      constexpr int qq = q & 63, i = qq >> 3, j = qq & 7;
+      // ---- waits / barriers in front of MFMA q
+      if constexpr (q < 64 && q % 8 == 0 && q != REL_B && q != REL_A) {
+        // step-0 read order [b0..b7, a0..a7]: MFMAs 8i.. need b0..b7 and a_i; y reads issued so far: ceil(q/2)
+        constexpr int ny = q / 2 < 16 ? q / 2 : 16;
+        constexpr int n = 7 - i + ny;
+        wait_lgkm<(n > 15 ? 15 : n)>();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (q == REL_B || q == REL_A) {
+        // every wave holds its step-1 fragments of this stage (B at REL_B, A at REL_A): release it
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+        wait_lgkm<0>();
+        __builtin_amdgcn_s_barrier();
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (q == LND_B || q == LND_A) {
+        // K-tile t+1 landed: B alone (its A + t+2's 16 pieces may stay in flight) or everything of t+1
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+        if constexpr (q == LND_B && BAR4) wait_vm<24>();
+        else wait_vm<16>();
+        __builtin_amdgcn_s_barrier();
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // ---- MFMA q (A-fragment-major; B fragment as src0: the transposed tile, 4 columns per lane)
+      const bf16x8(&fa)[8] = q < 64 ? xa : ya;
+      const bf16x8(&fb)[8] = q < 64 ? xb : yb;
+      f32x4v& c = acc[j >> 2][i][j & 3];
+      constexpr bool pb_ = q >= DMA_B && q < DMA_B + 16 && (q - DMA_B) % 2 == 0;
+      constexpr bool pa_ = q >= DMA_A && q < DMA_A + 16 && (q - DMA_A) % 2 == 0;
+      if constexpr (pb_) {
+        constexpr int pj = (q - DMA_B) / 2;
+        mfma_dma<piece_dst<true, st, pj>()>(c, fb[j], fa[i], wdst, vb[pj], sb);
+      } else if constexpr (pa_) {
+        constexpr int pj = (q - DMA_A) / 2;
+        mfma_dma<piece_dst<false, st, pj>()>(c, fb[j], fa[i], wdst, va[pj], sa);
+      } else {
+        mfma_agpr(c, fb[j], fa[i]);
+      }
+      // ---- work behind MFMA q
+      if constexpr (q == 1 || q == 3) {
+        // K-tile t+2's descriptors (B behind MFMA 1, A behind MFMA 3): SALU between MFMAs — kk made opaque
+        // here so none of it is hoisted into a serial block at the loop head, and the result pinned after
+        int kk = k + 2;
+        asm volatile("" : "+s"(kk));
+        if constexpr (q == 1) {
+          sb = desc(kk, cb, nb, b_end);
+          asm volatile("" : "+s"(sb));
+        } else {
+          sa = desc(kk, ca, na, a_end);
+          asm volatile("" : "+s"(sa));
+        }
+      }
+      if constexpr (q <= 30 && q % 2 == 0) {
+        // step-1 fragments of this stage
+        constexpr int r = q / 2;
+        if constexpr (r < 8) yb[r] = frag4<true, r, 1, st>(rb);
+        else ya[r - 8] = frag4<true, r - 8, 1, st>(ra);
+      }
+      if constexpr (q >= XRD_B && q < XRD_B + 16 && (q - XRD_B) % 2 == 0) {
+        constexpr int r = (q - XRD_B) / 2;
+        xb[r] = frag4<true, r, 0, st ^ 1>(rb);  // K-tile t+1's step-0 fragments
+      }
+      if constexpr (q >= XRD_A && q < XRD_A + 16 && (q - XRD_A) % 2 == 0) {
+        constexpr int r = (q - XRD_A) / 2;
+        xa[r] = frag4<true, r, 0, st ^ 1>(ra);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+
+  for (int u = 0; u < ntile; ++u) {
+    zero_acc();
+    for (int k = 0; k < nt; k += 2) {
+      ktile(std::integral_constant<int, 0>{}, k);
+      ktile(std::integral_constant<int, 1>{}, k + 1);
+    }
+    // tile done: accumulators out while the next tile's first K-tiles stream / sit in LDS
+    asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+#pragma unroll
+    for (int h = 0; h < 2; ++h) epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+    if (u + 1 < ntile) {
+      tile_of(p, slot + (u + 1) * G, ctm, ctn);
+      ca = na;
+      cb = nb;
+      set_next(u + 1);
+    }
+  }
+  // the dead prefetches past the last tile (num_records 0) must land before the workgroup's LDS goes away
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
+}  // namespace gm
+}  // namespace pd
+
+// Launch v7 (called by pd_gemm for variants 7..10 = SCHED 0..3).  Returns false if the problem is outside v7's
+// domain (the caller then runs v6): both operands K-major, bf16 (+bias) or SwiGLU epilogue, K % 128 == 0, every
+// operand extent < 2 GiB, 8-B-aligned output rows.
+bool pd_gemm_v7(const pd::gm::Params& p, int layout, int epi, int sched, int cus, hipStream_t st) {
+  using namespace pd::gm;
+  if (layout != 3 || (epi != kEpiBF16 && epi != kEpiSwiGLU) || p.K % 128) return false;
+  const long a_bytes = (long)((const char*)p.a_end - (const char*)p.A);
+  const long b_bytes = (long)((const char*)p.b_end - (const char*)p.B);
+  if (a_bytes <= 0 || b_bytes <= 0 || a_bytes >= 0x7fffffffL || b_bytes >= 0x7fffffffL) return false;
+  if (p.ldc % 4 || (size_t)p.C % 16 || (p.C2 && (p.ldc2 % 4 || (size_t)p.C2 % 16))) return false;
+  const dim3 grid(std::min(p.tiles_m * p.tiles_n, cus));
+#define PD_V7(E)                                                                        \
+  switch (sched & 3) {                                                                  \
+    case 0: gemm_v7_kernel<E, 0><<<grid, NTHR4, 0, st>>>(p); break;                     \
+    case 1: gemm_v7_kernel<E, 1><<<grid, NTHR4, 0, st>>>(p); break;                     \
+    case 2: gemm_v7_kernel<E, 2><<<grid, NTHR4, 0, st>>>(p); break;                     \
+    default: gemm_v7_kernel<E, 3><<<grid, NTHR4, 0, st>>>(p); break;                    \
+  }
+  if (epi == kEpiBF16) {
+    PD_V7(kEpiBF16)
+  } else {
+    PD_V7(kEpiSwiGLU)
+  }
+#undef PD_V7
+  return true;
+}

@@ -30,6 +30,9 @@ GROUP_M = int(os.environ.get("PADDLE2_AMD_GEMM_GROUP_M", "8"))
 # profiles/r3_gemm_v4.md: forward / dgrad (bf16 out, K = 4096..32000) v6, wgrad into the fp32 main grad v4 (its
 # long token reduction leaves persistence little to win, and v6's fp32 read-modify-write epilogue spills),
 # the SwiGLU-epilogue forward v4.  PADDLE2_AMD_GEMM_VARIANT forces one schedule for every pass.
+# 7..10 = v7 (gemm7.hip, SCHED 0..3): the TN schedule with both operands K-major — dgrad in place, the forward and
+# the SwiGLU forward on W^T (one transpose of the weight per forward); problems outside its domain (K % 128,
+# >= 2 GiB operands) run v6.
 _FORCE = os.environ.get("PADDLE2_AMD_GEMM_VARIANT")
 VARIANT = int(_FORCE) if _FORCE is not None else None
 PASS_VARIANT = {"fwd": 6, "dgrad": 6, "wgrad": 4, "wgrad_bf16": 4, "swiglu": 4}
@@ -90,12 +93,29 @@ def _launch(layout, epi, a, lda, b, ldb, c, ldc, c2, ldc2, bias, M, Nn, K, beta=
                     N.ptr(bias), M, Nn, K, float(beta), H, GROUP_M, v, ws, ws_bytes, N.stream())
 
 
+def _v7(name, K):
+    """The pass runs the TN schedule (v7) on this reduction length."""
+    return 7 <= _variant(name) <= 10 and K % 128 == 0
+
+
+def _wt(w):
+    """W [K, N] -> contiguous W^T [N, K] (HBM-speed HIP transpose) for the TN schedule."""
+    from .torch_ops import transpose2d
+
+    return transpose2d(w)
+
+
 def mm_fwd(x2, w, bias=None, out=None):
     """y[M, N] = x2[M, K] @ w[K, N] (+ bias[N]), bf16."""
     M, K = x2.shape
     Nn = w.shape[1]
     if out is None:
         out = torch.empty(M, Nn, dtype=x2.dtype, device=x2.device)
+    if _v7("fwd", K):
+        wt = _wt(w)
+        _launch(LAYOUT_AK | LAYOUT_BK, EPI_BF16, x2, x2.stride(0), wt, wt.stride(0), out, out.stride(0), None, 0,
+                bias, M, Nn, K)
+        return out
     _launch(LAYOUT_AK, EPI_BF16, x2, x2.stride(0), w, w.stride(0), out, out.stride(0), None, 0, bias, M, Nn, K)
     return out
 
@@ -138,6 +158,11 @@ def mm_swiglu(x2, w):
     H = w.shape[1] // 2
     gu = torch.empty(M, 2 * H, dtype=x2.dtype, device=x2.device)
     a = torch.empty(M, H, dtype=x2.dtype, device=x2.device)
+    if _v7("swiglu", K):
+        wt = _wt(w)
+        _launch(LAYOUT_AK | LAYOUT_BK, EPI_SWIGLU, x2, x2.stride(0), wt, wt.stride(0), a, a.stride(0), gu,
+                gu.stride(0), None, M, 2 * H, K, 0.0, H, name="swiglu")
+        return a, gu
     _launch(LAYOUT_AK, EPI_SWIGLU, x2, x2.stride(0), w, w.stride(0), a, a.stride(0), gu, gu.stride(0), None, M,
             2 * H, K, 0.0, H, name="swiglu")
     return a, gu

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 dev = "cuda"
 
 
-@pytest.fixture(params=[None, 0, 4, 6], ids=["per-pass", "v2", "v4", "v6"], autouse=True)
+@pytest.fixture(params=[None, 0, 4, 6, 7, 8], ids=["per-pass", "v2", "v4", "v6", "v7", "v7b4"], autouse=True)
 def schedule(request, monkeypatch):
     """Every test runs on each kernel schedule (None = the per-pass default routing)."""
     monkeypatch.setattr(G, "VARIANT", request.param)
@@ -169,18 +169,19 @@ def test_swiglu_linear_node(mode, monkeypatch):
 
 @pytest.mark.parametrize("M,N,K", [(2048, 4096, 4096), (300, 520, 72), (4096, 22016, 4096)])
 def test_schedule_variants_bitwise_equal(M, N, K, monkeypatch, schedule):
-    """v2 (8 waves), v4 (4 waves, AGPR accumulators) and v6 (persistent) accumulate the same products in the
-    same order: their outputs must agree bit for bit (a staging race shows up here first)."""
+    """v2 (8 waves), v4 (4 waves, AGPR accumulators), v6 (persistent) and v7 (TN schedule) accumulate the same
+    products in the same order: their outputs must agree bit for bit (a staging race shows up here first)."""
     if schedule is not None:
         pytest.skip("compares the schedules itself")
     x, w, dy = _rand(M, K, seed=30), _rand(K, N, seed=31, scale=0.05), _rand(M, N, seed=32)
     monkeypatch.setattr(G, "SPLITK", False)   # tail split-K sums K-slices in another order (v2 / v4)
     outs = []
-    for v in (0, 4, 6):
+    swi = (N // 2) % 32 == 0
+    for v in (0, 4, 6, 7, 8, 9, 10):  # 7..10: the TN schedule (v7) on W^T for the forward passes
         monkeypatch.setattr(G, "VARIANT", v)
         o32 = torch.zeros(K, N, device=dev)
         G.mm_wgrad(x, dy, o32)
-        outs.append((G.mm_fwd(x, w), G.mm_dgrad(dy, w), o32))
+        outs.append((G.mm_fwd(x, w), G.mm_dgrad(dy, w), o32) + (G.mm_swiglu(x, w) if swi else ()))
     for other in outs[1:]:
         for a, b in zip(outs[0], other):
             assert torch.equal(a, b)
