@@ -191,6 +191,25 @@ PYBIND11_MODULE(_runtime, m) {
       .def("clear_trace", &FleetCarrier::clear_trace)
       .def("shutdown", &FleetCarrier::shutdown, py::call_guard<py::gil_scoped_release>());
 
+  py::class_<InterpPlan>(m, "InterpPlan")
+      .def_readonly("n", &InterpPlan::n)
+      .def_readonly("num_edges_raw", &InterpPlan::num_edges_raw)
+      .def_readonly("downstream", &InterpPlan::downstream)
+      .def_readonly("dep_count", &InterpPlan::dep_count)
+      .def_readonly("order", &InterpPlan::order)
+      .def_readonly("waits", &InterpPlan::waits)
+      .def_property_readonly("record", [](const InterpPlan& p) { return std::vector<int>(p.record.begin(), p.record.end()); })
+      .def_readonly("free_after", &InterpPlan::free_after)
+      .def_readonly("reader_count", &InterpPlan::reader_count);
+  m.def("build_interp_plan", &build_interp_plan, py::arg("reads"), py::arg("writes"), py::arg("stream"),
+        py::arg("barrier"), py::arg("keep"));
+  py::class_<ReadyQueue>(m, "ReadyQueue")
+      .def(py::init<const InterpPlan&>())
+      .def("start", &ReadyQueue::start)
+      .def("pop", &ReadyQueue::pop, py::arg("timeout_s") = -1.0, py::call_guard<py::gil_scoped_release>())
+      .def("done", &ReadyQueue::done)
+      .def("fail", &ReadyQueue::fail)
+      .def("finished", &ReadyQueue::finished);
   py::class_<BlockingQueue>(m, "BlockingQueue")
       .def(py::init<size_t>(), py::arg("capacity"))
       .def("push", &BlockingQueue::push, py::arg("obj"), py::arg("timeout") = -1.0)

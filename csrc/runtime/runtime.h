@@ -8,6 +8,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 namespace pdrt {
@@ -105,6 +106,41 @@ class FleetCarrier {
   std::vector<std::array<int64_t, 3>> trace();  // (task, step, sequence) of compute callbacks
   void clear_trace();
   void shutdown();
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
+};
+
+// ------------------------------------------------------------------ static-graph interpreter (interpreter.cpp)
+struct InterpPlan {
+  int n = 0;
+  int64_t num_edges_raw = 0;                       // RAW + WAR + WAW + barrier edges before the reduction
+  std::vector<std::vector<int>> downstream;        // transitively reduced successors
+  std::vector<int> dep_count;                      // predecessors per instruction
+  std::vector<int> order;                          // issue order (topological; side streams first when ready)
+  std::vector<std::vector<int>> waits;             // producers on another stream (wait on their events)
+  std::vector<char> record;                        // record an event after this instruction
+  std::vector<std::vector<int64_t>> free_after;    // sequential issue: variables dead after this instruction
+  std::unordered_map<int64_t, int> reader_count;   // async queue: readers per (non-kept) variable
+  std::vector<std::vector<int64_t>> reads;         // per instruction, de-duplicated
+};
+
+InterpPlan build_interp_plan(const std::vector<std::vector<int64_t>>& reads,
+                             const std::vector<std::vector<int64_t>>& writes, const std::vector<int>& stream,
+                             const std::vector<int>& barrier, const std::vector<int64_t>& keep);
+
+// Dependency-counting ready queue over a plan: worker threads pop() ready instructions, run them, and report
+// done(i), which releases successors and returns the variables whose last reader just finished.
+class ReadyQueue {
+ public:
+  explicit ReadyQueue(const InterpPlan& plan);
+  ~ReadyQueue();
+  void start();
+  int pop(double timeout_s);          // instruction id; -1 = finished or aborted; -2 = timed out
+  std::vector<int64_t> done(int i);
+  void fail();                        // abort: every waiting pop() returns -1
+  bool finished();
 
  private:
   struct Impl;

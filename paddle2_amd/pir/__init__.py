@@ -288,4 +288,6 @@ def run(program, feeds, device=None):
     return [out[i] for i in sorted(out)]
 
 
-from . import passes  # noqa: E402,F401
+from . import dialect, drr, passes, serialize  # noqa: E402,F401
+from .dialect import IrContext, VerifyError, verify  # noqa: E402,F401
+from .serialize import load, save  # noqa: E402,F401

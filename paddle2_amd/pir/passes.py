@@ -134,7 +134,16 @@ def fused_gemm_epilogue_pass(program):
     return n
 
 
-_PASSES = {"dead_code_elimination_pass": dead_code_elimination_pass,
+def drr_rewrite_pass(program):
+    """The built-in declarative rules (pir/drr.py: GEMM + bias (+ relu / gelu) -> fused_gemm_epilogue, inverse
+    transpose pairs cancelled, scale chains folded), applied greedily."""
+    from . import drr
+
+    return sum(drr.apply_patterns_greedily(program, drr.default_patterns()).values())
+
+
+_PASSES = {"drr_rewrite_pass": drr_rewrite_pass,
+           "dead_code_elimination_pass": dead_code_elimination_pass,
            "common_subexpression_elimination_pass": common_subexpression_elimination_pass,
            "constant_folding_pass": constant_folding_pass,
            "fused_gemm_epilogue_pass": fused_gemm_epilogue_pass}

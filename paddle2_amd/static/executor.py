@@ -55,9 +55,10 @@ class ExecutionStrategy:
 
 
 class CompiledProgram:
-    def __init__(self, program_or_graph, build_strategy=None):
+    def __init__(self, program_or_graph, build_strategy=None, exec_strategy=None):
         self._program = program_or_graph
         self._build_strategy = build_strategy or BuildStrategy()
+        self._exec_strategy = exec_strategy or ExecutionStrategy()
 
     def with_data_parallel(self, *a, **k):
         return self
@@ -84,6 +85,8 @@ class _GraphState:
 
 
 class Executor:
+    _num_threads = 1   # host worker threads of the async interpreter (ExecutionStrategy.num_threads)
+
     def __init__(self, place=None):
         from ..framework.place import _parse_device, current_torch_device
 
@@ -95,22 +98,43 @@ class Executor:
         self._graphs.clear()
 
     # ---------------------------------------------------------------- core replay
-    def _replay(self, program, env, grad=None, keep=None):
-        """Run ``program`` over ``env`` (vid -> tensor).  With ``keep`` (the fetch targets) the plan's garbage
-        collection drops every value after its last use, and ops the stream analyzer placed on the comm /
-        copy streams run there with event dependencies on their producers and consumers."""
-        needs_grad = any(o.kind in ("backward", "grad") for o in program.ops) or bool(grad)
-        ctx = torch.enable_grad() if needs_grad else torch.no_grad()
-        plan = _plan(program, keep) if keep is not None else None
-        streams = plan is not None and plan.multi_stream and torch.cuda.is_available() and \
-            self._device.type == "cuda"
-        if streams:
-            from ..device.context import get_context
+    def _run_op(self, op, env, res):
+        """Run one recorded instruction over ``env`` (outputs bound in place)."""
+        if op.kind in ("torch", "native"):
+            out = op.fn(*pytree.tree_map(res, op.args), **pytree.tree_map(res, op.kwargs))
+            for vid, val in zip(op.outs, pytree.tree_leaves(out)):
+                if vid is not None:
+                    env[vid] = val
+        elif op.kind == "backward":
+            env[op.attrs["loss"]].backward()
+        elif op.kind == "grad":
+            tgts = [env[v] for v in op.attrs["targets"]]
+            ins = [env[v] if isinstance(v, int) else v for v in op.attrs["inputs"]]
+            gs = torch.autograd.grad(tgts, ins, allow_unused=True, retain_graph=True)
+            for vid, g in zip(op.attrs["outs"], gs):
+                env[vid] = g if g is not None else torch.zeros_like(ins[0])
+        elif op.kind == "param_grad":
+            p = op.attrs["param"]
+            g = p._t.grad
+            env[op.attrs["out"]] = g if g is not None else torch.zeros_like(p._t)
+        elif op.kind == "optimize":
+            opt = op.attrs["optimizer"]
+            with torch.no_grad():
+                opt.step()
+            opt.clear_grad(set_to_zero=False)
 
-            gctx = get_context(self._device)
-            side = {"comm": gctx.comm_stream, "h2d": gctx.h2d_stream, "d2h": gctx.d2h_stream}
-            compute = torch.cuda.current_stream(self._device)
-            ready = {}   # vid -> event recorded right after its producer (only for cross-stream values)
+    def _replay(self, program, env, grad=None, keep=None):
+        """Run ``program`` over ``env`` (vid -> tensor) through its interpreter plan (csrc/runtime/interpreter.cpp).
+
+        With ``keep`` (the fetch targets) values are dropped after their last reader.  Device programs issue the
+        instructions in the plan's order (kernels are asynchronous on their streams; instructions the stream
+        analyzer put on the comm / copy streams run there, and only cross-stream dependency edges get events).
+        Host programs with ``ExecutionStrategy.num_threads`` > 1 run on the dependency-counting ready queue: N
+        worker threads execute independent instructions concurrently (reference pir_interpreter.cc async work
+        queue / RunNextInstructions)."""
+        needs_grad = any(o.kind in ("backward", "grad") for o in program.ops) or bool(grad)
+        plan = _plan(program, keep if keep is not None else _ALL)
+        gc = keep is not None
 
         def res(x):
             if isinstance(x, VarRef):
@@ -119,65 +143,87 @@ class Executor:
                 return env[x.vid]
             return x
 
+        on_gpu = torch.cuda.is_available() and self._device.type == "cuda"
+        if not on_gpu and self._num_threads > 1 and plan.n > 1:
+            return self._replay_async(program, env, plan, needs_grad, gc, res)
+        streams = plan.multi_stream and on_gpu
+        if streams:
+            from ..device.context import get_context
+
+            gctx = get_context(self._device)
+            side = {"comm": gctx.comm_stream, "h2d": gctx.h2d_stream, "d2h": gctx.d2h_stream}
+            compute = torch.cuda.current_stream(self._device)
+            done_ev = {}   # instruction -> event recorded right after it (only producers of cross-stream edges)
+        ctx = torch.enable_grad() if needs_grad else torch.no_grad()
         with ctx:
-            for i, op in enumerate(program.ops):
-                if op.kind in ("torch", "native"):
-                    args = pytree.tree_map(res, op.args)
-                    kw = pytree.tree_map(res, op.kwargs)
-                    if streams and (plan.stream_of[i] != "compute" or plan.waits_on[i]):
-                        st = side[plan.stream_of[i]]() if plan.stream_of[i] != "compute" else compute
-                        for v in plan.waits_on[i]:
-                            st.wait_event(ready[v])
-                            if st is not compute:
+            for i in plan.order:
+                op = program.ops[i]
+                if streams and (plan.stream_of[i] != "compute" or plan.waits[i]):
+                    st = side[plan.stream_of[i]]() if plan.stream_of[i] != "compute" else compute
+                    for pi in plan.waits[i]:
+                        st.wait_event(done_ev[pi])
+                    if st is not compute:
+                        for v in plan.reads[i]:
+                            if v in env and isinstance(env[v], torch.Tensor) and env[v].is_cuda:
                                 env[v].record_stream(st)   # allocator: the side stream still reads it
-                        with torch.cuda.stream(st):
-                            out = op.fn(*args, **kw)
-                    else:
-                        out = op.fn(*args, **kw)
-                    leaves = pytree.tree_leaves(out)
-                    for vid, val in zip(op.outs, leaves):
-                        if vid is not None:
-                            env[vid] = val
-                            if streams and vid in plan.cross:
-                                e = torch.cuda.Event()
-                                e.record(side[plan.stream_of[i]]() if plan.stream_of[i] != "compute" else compute)
-                                ready[vid] = e
-                    if plan is not None:
-                        for v in plan.free_after[i]:
-                            env.pop(v, None)
-                    continue
-                elif op.kind == "backward":
-                    loss = env[op.attrs["loss"]]
-                    loss.backward()
-                elif op.kind == "grad":
-                    tgts = [env[v] for v in op.attrs["targets"]]
-                    ins = [env[v] if isinstance(v, int) else v for v in op.attrs["inputs"]]
-                    gs = torch.autograd.grad(tgts, ins, allow_unused=True, retain_graph=True)
-                    for vid, g in zip(op.attrs["outs"], gs):
-                        env[vid] = g if g is not None else torch.zeros_like(ins[0])
-                elif op.kind == "param_grad":
-                    p = op.attrs["param"]
-                    g = p._t.grad
-                    env[op.attrs["out"]] = g if g is not None else torch.zeros_like(p._t)
-                elif op.kind == "optimize":
-                    opt = op.attrs["optimizer"]
-                    with torch.no_grad():
-                        opt.step()
-                    opt.clear_grad(set_to_zero=False)
-                if plan is not None:
+                    with torch.cuda.stream(st):
+                        self._run_op(op, env, res)
+                else:
+                    self._run_op(op, env, res)
+                if streams and plan.record[i]:
+                    e = torch.cuda.Event()
+                    e.record(side[plan.stream_of[i]]() if plan.stream_of[i] != "compute" else compute)
+                    done_ev[i] = e
+                if gc:
                     for v in plan.free_after[i]:
                         env.pop(v, None)
-        if streams and plan.cross:
+        if streams:
             # values produced on a side stream and fetched / left in env: the caller reads them on compute
-            for v, e in ready.items():
-                compute.wait_event(e)
+            for i, e in done_ev.items():
+                if plan.stream_of[i] != "compute":
+                    compute.wait_event(e)
+        return env
+
+    def _replay_async(self, program, env, plan, needs_grad, gc, res):
+        import threading
+
+        q = plan.queue()
+        q.start()
+        errors = []
+
+        def worker():
+            with (torch.enable_grad() if needs_grad else torch.no_grad()):  # grad mode is thread-local
+                while True:
+                    i = q.pop(-1.0)
+                    if i < 0:
+                        return
+                    try:
+                        self._run_op(program.ops[i], env, res)
+                    except BaseException as e:  # noqa: BLE001 - re-raised on the calling thread
+                        errors.append(e)
+                        q.fail()
+                        return
+                    dead = q.done(i)
+                    if gc:
+                        for v in dead:
+                            env.pop(v, None)
+
+        ts = [threading.Thread(target=worker, daemon=True) for _ in range(min(self._num_threads, plan.n))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errors:
+            raise errors[0]
         return env
 
     def run(self, program=None, feed=None, fetch_list=None, feed_var_name="feed", fetch_var_name="fetch", scope=None,
             return_numpy=True, use_program_cache=False, use_prune=False, _grad=None):
         strategy = None
+        self._num_threads = 1
         if isinstance(program, CompiledProgram):
             strategy = program._build_strategy
+            self._num_threads = max(1, int(program._exec_strategy.num_threads))
             program = program._program
         program = program or default_main_program()
         from .pdmodel import PdProgram
@@ -262,42 +308,50 @@ class Executor:
 
 
 # ==================================================================================== execution plan
-class _Plan:
-    """Per-(program, fetch set) analysis (reference: new_executor/interpreter/dependency_builder.cc,
-    stream_analyzer.cc, garbage collection in interpreter_util):
+_STREAM_IDS = {"compute": 0, "comm": 1, "h2d": 2, "d2h": 3}
+_ALL = object()   # keep every value (no garbage collection)
 
-    * ``free_after[i]`` — values whose last reader is op i (dropped right after it unless fetched), so peak
-      memory follows the live set instead of the whole program;
+
+class _Plan:
+    """Per-(program, fetch set) interpreter plan, built natively (csrc/runtime/interpreter.cpp; reference
+    new_executor/interpreter/dependency_builder.cc, stream_analyzer.cc, pir_interpreter.cc:804):
+
+    * a dependency graph over the instructions from their variable reads / writes (RAW, WAR, WAW), with
+      backward / optimizer / in-place instructions as barriers (hidden side effects), transitively reduced;
+    * ``order`` — the issue order (topological; communication / copy instructions issued as soon as ready);
     * ``stream_of[i]`` — "compute", or the stream class a function declares via ``_pd_stream`` ("comm" for
-      collectives, "h2d" / "d2h" for copies); ``waits_on[i]`` — inputs produced on another stream (op i's
-      stream waits on their ready events); ``cross`` — values that need such an event.
+      collectives, "h2d" / "d2h" for copies); ``waits[i]`` — producers on another stream whose events op i's
+      stream waits on; ``record[i]`` — op i records such an event;
+    * ``free_after[i]`` — values whose last reader (in issue order) is op i, dropped right after it unless
+      fetched; the async queue frees a value when its reader count drains instead.
     """
 
     def __init__(self, program, keep):
+        from .. import _rt
+
         ops = program.ops
-        n = len(ops)
-        last = {}
-        producer = {}
-        self.stream_of = []
-        self.waits_on = [[] for _ in range(n)]
-        self.cross = set()
-        for i, op in enumerate(ops):
-            klass = (op.attrs.get("stream") or getattr(op.fn, "_pd_stream", None) or "compute") \
-                if op.kind in ("torch", "native") else "compute"
-            self.stream_of.append(klass)
-            for v in _op_reads(op):
-                last[v] = i
-                if v in producer and self.stream_of[producer[v]] != klass:
-                    self.waits_on[i].append(v)
-                    self.cross.add(v)
-            for v in _op_writes(op):
-                producer[v] = i
-        keep = set(keep or ())
-        self.free_after = [[] for _ in range(n)]
-        for v, i in last.items():
-            if v not in keep:
-                self.free_after[i].append(v)
+        self.n = len(ops)
+        self.reads = [_op_reads(op) for op in ops]
+        writes = [_op_writes(op) for op in ops]
+        self.stream_of = [((op.attrs.get("stream") or getattr(op.fn, "_pd_stream", None) or "compute")
+                           if op.kind in ("torch", "native") else "compute") for op in ops]
+        barrier = [int(op.kind not in ("torch", "native") or bool(set(w) & set(r)))
+                   for op, r, w in zip(ops, self.reads, writes)]
+        keep_ids = sorted({v for r in self.reads for v in r} | {v for w in writes for v in w}) if keep is _ALL \
+            else sorted(keep)
+        self.native = _rt.get().build_interp_plan(self.reads, writes,
+                                                      [_STREAM_IDS.get(c, 0) for c in self.stream_of], barrier,
+                                                      keep_ids)
+        self.order = list(self.native.order)
+        self.waits = self.native.waits
+        self.record = self.native.record
+        self.free_after = self.native.free_after
         self.multi_stream = any(k != "compute" for k in self.stream_of)
+
+    def queue(self):
+        from .. import _rt
+
+        return _rt.get().ReadyQueue(self.native)
 
 
 def _op_reads(op):
@@ -326,11 +380,10 @@ def _plan(program, keep):
     from ..framework import flags
 
     if float(flags.flag("FLAGS_eager_delete_tensor_gb", 0.0)) < 0:
-        keep = None   # garbage collection disabled: keep everything
+        keep = _ALL   # garbage collection disabled: keep everything
     per = _PLANS.setdefault(program, {})
-    key = (len(program.ops), frozenset(keep) if keep is not None else None)
+    key = (len(program.ops), keep if keep is _ALL else frozenset(keep))
     p = per.get(key)
     if p is None:
-        p = _Plan(program, keep if keep is not None else {v for op in program.ops for v in _op_reads(op)})
-        per[key] = p
+        p = per[key] = _Plan(program, keep)
     return p

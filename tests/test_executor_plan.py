@@ -75,8 +75,9 @@ def test_stream_analyzer_plan():
     plan = _plan(main, {c._t._vid})
     assert plan.multi_stream and plan.stream_of.count("comm") == 1
     i = plan.stream_of.index("comm")
-    assert len(plan.waits_on[i]) == 1          # waits for `a` produced on compute
-    assert any(plan.waits_on[j] for j in range(i + 1, len(main.ops)))   # consumer of `b` waits on comm
+    assert len(plan.waits[i]) == 1             # waits for `a`'s producer on compute
+    assert any(i in plan.waits[j] for j in range(i + 1, len(main.ops)))   # consumer of `b` waits on comm
+    assert plan.record[i] and plan.order.index(i) < plan.order.index(i + 1)
     res = paddle.static.Executor().run(main, feed={"x": np.ones((1024, 1024), "float32")}, fetch_list=[c])
     np.testing.assert_allclose(res[0], 14.0)
 
@@ -91,3 +92,127 @@ def test_comm_stream_op_runs_on_context_stream_and_is_fenced():
     out = exe.run(main, feed={"x": xv}, fetch_list=[c])[0]
     np.testing.assert_allclose(out, (xv + 1) * 3 * 2 + (xv + 1), rtol=1e-5)
     assert seen and seen[0] == paddle.device.get_context().comm_stream()
+
+
+# ------------------------------------------------------------------ native interpreter core (csrc/runtime/interpreter.cpp)
+def _native_plan(reads, writes, stream=None, barrier=None, keep=()):
+    from paddle2_amd import _rt
+
+    n = len(reads)
+    return _rt.get().build_interp_plan(reads, writes, stream or [0] * n, barrier or [0] * n, list(keep))
+
+
+def test_dependency_edges_raw_war_waw_and_reduction():
+    # op0: a=f(x)  op1: b=g(x)  op2: c=h(a,b)  op3: a<-k(a) in place  op4: d=m(c)
+    p = _native_plan([[0], [0], [1, 2], [1], [3]], [[1], [2], [3], [1], [4]], keep=[4])
+    down = [sorted(d) for d in p.downstream]
+    assert down[0] == [2] and down[1] == [2]        # RAW a, b (op0 -> op3 WAW is implied through op2)
+    assert 3 in down[2] and 4 in down[2]            # WAR on a (op2 reads a, op3 rewrites it), RAW c
+    assert p.num_edges_raw == 5 and sum(map(len, down)) == 4   # 0 -> 3 (RAW + WAW on a) is implied via op2
+    assert list(p.dep_count) == [0, 0, 2, 1, 1]
+    assert sorted(p.order) == list(range(5)) and p.order.index(2) > max(p.order.index(0), p.order.index(1))
+    freed = {v: i for i, f in enumerate(p.free_after) for v in f}
+    assert 4 not in freed and freed[3] == 4 and freed[2] == 2
+
+
+def test_barrier_orders_everything_and_side_streams_issue_first():
+    # op1 is a barrier (optimizer-like): independent op0 / op2 still order around it; op2 on the comm stream
+    p = _native_plan([[0], [], [5], [0]], [[1], [], [6], [7]], stream=[0, 0, 1, 0], barrier=[0, 1, 0, 0])
+    assert 1 in p.downstream[0] and 2 in p.downstream[1] and 3 in p.downstream[1]
+    p2 = _native_plan([[0], [5], [0]], [[1], [6], [7]], stream=[0, 1, 0])
+    assert p2.order[0] == 1      # the ready comm instruction is issued first
+    assert list(p2.record) == [0, 0, 0] and not any(p2.waits)
+
+
+def test_ready_queue_runs_every_instruction_once_in_dependency_order():
+    import threading
+
+    from paddle2_amd import _rt
+
+    n = 40   # a layered DAG: op i reads the outputs of ops i-3 and i-7
+    reads = [[100 + j for j in (i - 3, i - 7) if j >= 0] for i in range(n)]
+    writes = [[100 + i] for i in range(n)]
+    p = _native_plan(reads, writes, keep=[100 + n - 1])
+    q = _rt.get().ReadyQueue(p)
+    q.start()
+    done, lock, freed = [], threading.Lock(), []
+
+    def work():
+        while True:
+            i = q.pop(5.0)
+            if i < 0:
+                return
+            with lock:
+                for v in reads[i]:
+                    assert v - 100 in done
+                done.append(i)
+            freed.extend(q.done(i))
+
+    ts = [threading.Thread(target=work) for _ in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert sorted(done) == list(range(n)) and q.finished()
+    assert sorted(freed) == sorted({v for r in reads for v in r})   # every non-kept value freed exactly once
+
+
+def _two_branch_program(delay):
+    import time
+
+    def slow(t):
+        if t.device.type != "meta":
+            time.sleep(delay)
+        return t + 1.0
+
+    main = paddle.static.Program()
+    paddle.enable_static()
+    try:
+        with paddle.static.program_guard(main, paddle.static.Program()):
+            x = paddle.static.data("x", [16, 16], "float32")
+            a = paddle.Tensor._wrap(main._record(slow, (x._t * 2.0,), {}, kind="native"))
+            b = paddle.Tensor._wrap(main._record(slow, (x._t - 1.0,), {}, kind="native"))
+            c = a * b
+    finally:
+        paddle.disable_static()
+    return main, c
+
+
+def test_async_host_interpreter_runs_independent_branches_concurrently():
+    import time
+
+    main, c = _two_branch_program(0.4)
+    xv = np.random.RandomState(0).randn(16, 16).astype("float32")
+    exe = paddle.static.Executor("cpu")
+    ref = exe.run(main, feed={"x": xv}, fetch_list=[c])[0]
+    es = paddle.static.ExecutionStrategy()
+    es.num_threads = 4
+    prog = paddle.static.CompiledProgram(main, exec_strategy=es)
+    exe.run(prog, feed={"x": xv}, fetch_list=[c])     # warm the plan
+    t0 = time.perf_counter()
+    out = exe.run(prog, feed={"x": xv}, fetch_list=[c])[0]
+    dt = time.perf_counter() - t0
+    np.testing.assert_allclose(out, ref)
+    np.testing.assert_allclose(out, (xv * 2 + 1) * (xv - 1 + 1), rtol=1e-6)
+    assert dt < 0.7, dt     # the two 0.4 s branches overlapped (sequential would take >= 0.8 s)
+
+
+def test_async_host_interpreter_propagates_errors():
+    def boom(t):
+        if t.device.type != "meta":
+            raise ValueError("instruction failed")
+        return t
+
+    main = paddle.static.Program()
+    paddle.enable_static()
+    try:
+        with paddle.static.program_guard(main, paddle.static.Program()):
+            x = paddle.static.data("x", [4], "float32")
+            y = paddle.Tensor._wrap(main._record(boom, (x._t + 1.0,), {}, kind="native")) * 2.0
+    finally:
+        paddle.disable_static()
+    es = paddle.static.ExecutionStrategy()
+    es.num_threads = 3
+    with pytest.raises(ValueError, match="instruction failed"):
+        paddle.static.Executor("cpu").run(paddle.static.CompiledProgram(main, exec_strategy=es),
+                                          feed={"x": np.ones(4, "float32")}, fetch_list=[y])

@@ -2,6 +2,7 @@
 constant folding, fused_gemm_epilogue) and primitive decomposition — every rewritten program must compute
 what the eager model computes (reference: paddle/pir, fluid/pir/transforms, primitive composite rules)."""
 import numpy as np
+import pytest
 import torch
 
 import paddle2_amd as paddle
@@ -87,3 +88,98 @@ def test_decomposition_to_primitives():
     assert decomposition.decompose(prog2, whitelist={"pd_op.softmax"}) == 1
     assert "pd_op.gelu" in prog2.op_names()
     np.testing.assert_allclose(pir.run(prog2, [x])[0].detach().numpy(), ref.detach().numpy(), rtol=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------------------------ dialect registry / verifier, DRR, serialization
+def test_verify_registered_program_and_catches_breakage():
+    prog = _record(_mlp(), [3, 6])
+    assert pir.verify(prog) == prog.num_ops()
+    info = pir.IrContext.instance().op_info("pd_op.matmul")
+    assert info.has_trait("Pure") and pir.dialect.has_trait(prog.global_block().ops[-1], "SideEffect")
+    # an operand used before its definition
+    ops = prog.global_block().ops
+    i = next(k for k, o in enumerate(ops) if o.name() == "pd_op.matmul")
+    ops.insert(0, ops.pop(i))
+    try:
+        pir.verify(prog)
+        raise AssertionError("verify accepted a use before definition")
+    except pir.VerifyError as e:
+        assert "before its definition" in str(e)
+
+
+def test_verify_rejects_bad_arity_attrs_and_unknown_dialect():
+    p = pir.Program()
+    d = p.global_block().append(pir.Operation("pd_op.data", [], [([4, 4], torch.float32)], {"name": "x", "col": 0}))
+    x = d.result(0)
+    p.global_block().append(pir.Operation("pd_op.matmul", [x], [([4, 4], torch.float32)]))
+    with pytest.raises(pir.VerifyError, match="operands"):
+        pir.verify(p)
+    p2 = pir.Program()
+    d2 = p2.global_block().append(pir.Operation("pd_op.data", [], [([4, 4], torch.float32)], {"name": "x", "col": 0}))
+    p2.global_block().append(pir.Operation("pd_op.softmax", [d2.result(0)], [([4, 4], torch.float32)], {"axis": "1"}))
+    with pytest.raises(pir.VerifyError, match="attribute 'axis'"):
+        pir.verify(p2)
+    p3 = pir.Program()
+    p3.global_block().append(pir.Operation("mydialect.op", [], [([1], torch.float32)]))
+    with pytest.raises(pir.VerifyError, match="dialect"):
+        pir.verify(p3)
+
+
+def test_drr_rewrites_match_the_handwritten_fusion_pass():
+    net = _mlp()
+    x = torch.randn(3, 6)
+    ref = net(paddle.to_tensor(x))._t
+    a, b = _record(net, [3, 6]), _record(net, [3, 6])
+    passes.apply(a, ["fused_gemm_epilogue_pass"])
+    stats = passes.apply(b, ["drr_rewrite_pass"])
+    assert stats["drr_rewrite_pass"] == 3
+    assert sorted(a.op_names()) == sorted(b.op_names())
+    acts = sorted(o.attrs()["activation"] for o in b.global_block().ops if o.name() == "pd_op.fused_gemm_epilogue")
+    assert acts == ["gelu", "identity", "relu"]
+    pir.verify(b)
+    torch.testing.assert_close(pir.run(b, [x])[0], ref, rtol=1e-5, atol=1e-6)
+
+
+def _chain_program():
+    from paddle2_amd.pir import drr  # noqa: F401
+
+    p = pir.Program()
+    blk = p.global_block()
+    x = blk.append(pir.Operation("pd_op.data", [], [([2, 3, 4], torch.float32)], {"name": "x", "col": 0})).result(0)
+    s1 = blk.append(pir.Operation("pd_op.scale", [x], [([2, 3, 4], torch.float32)],
+                                  {"scale": 2.0, "bias": 1.0, "bias_after_scale": True})).result(0)
+    s2 = blk.append(pir.Operation("pd_op.scale", [s1], [([2, 3, 4], torch.float32)],
+                                  {"scale": 3.0, "bias": -0.5, "bias_after_scale": True})).result(0)
+    t1 = blk.append(pir.Operation("pd_op.transpose", [s2], [([3, 4, 2], torch.float32)], {"axis": [1, 2, 0]})).result(0)
+    t2 = blk.append(pir.Operation("pd_op.transpose", [t1], [([2, 3, 4], torch.float32)], {"axis": [2, 0, 1]})).result(0)
+    blk.append(pir.Operation("pd_op.fetch", [t2], [([2, 3, 4], torch.float32)], {"name": "y", "col": 0}))
+    return p
+
+
+def test_drr_cancels_inverse_transposes_and_folds_scales():
+    from paddle2_amd.pir import drr
+
+    x = torch.randn(2, 3, 4)
+    p = _chain_program()
+    stats = drr.apply_patterns_greedily(p, drr.default_patterns())
+    assert stats["cancel_transpose_pair"] == 1 and stats["fold_scale_pair"] == 1
+    assert p.op_names() == ["pd_op.data", "pd_op.scale", "pd_op.fetch"]
+    sc = p.global_block().ops[1].attrs()
+    assert sc["scale"] == 6.0 and sc["bias"] == 2.5
+    pir.verify(p)
+    torch.testing.assert_close(pir.run(p, [x])[0], (x * 2 + 1) * 3 - 0.5)
+
+
+def test_serialize_round_trip(tmp_path):
+    net = _mlp()
+    x = torch.randn(3, 6)
+    prog = _record(net, [3, 6])
+    passes.apply(prog, ["drr_rewrite_pass"])
+    path = str(tmp_path / "m.pir.json")
+    pir.save(prog, path)
+    back = pir.load(path)
+    assert back.op_names() == prog.op_names()
+    for a, b in zip(prog.global_block().ops, back.global_block().ops):
+        assert a.attrs() == b.attrs() and [r.shape for r in a.results()] == [r.shape for r in b.results()]
+    pir.verify(back)
+    torch.testing.assert_close(pir.run(back, [x])[0], pir.run(prog, [x])[0])

@@ -38,6 +38,6 @@ write_result({
     "z": z_out.tolist(), "w": w_out.tolist(),
     "comm_ops": [n for n, s in zip(names, plan.stream_of) if s == "comm"],
     "freed": sum(len(f) for f in plan.free_after),
-    "waits": sum(len(w_) for w_ in plan.waits_on),
+    "waits": sum(len(w_) for w_ in plan.waits),
 })
 dist.barrier()
