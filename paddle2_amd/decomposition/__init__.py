@@ -1,18 +1,21 @@
 """Primitive decomposition of composite ops on PIR programs (reference: paddle/fluid/primitive/ composite rules
 and python/paddle/decomposition/decomp.py ``decompose``).
 
-Composite ops are rewritten into a small primitive set — exp, erf, rsqrt, sigmoid, max / sum reductions
-(keepdim), add / subtract / multiply / divide and scale — which compiler-style passes (and the interpreter)
-handle uniformly.  Rules: softmax, log_softmax, gelu (erf and tanh forms), silu, layer_norm (when its
-Mean / Variance side outputs are unused), mean."""
+Composite ops are rewritten into a small primitive set — exp, log, erf, tanh, rsqrt, sigmoid, max / sum
+reductions (keepdim), add / subtract / multiply / divide / maximum / minimum and scale (``scale(x, 0, c)`` is the
+constant-like-x primitive) — which compiler-style passes (and the interpreter) handle uniformly.  Rules:
+softmax, log_softmax, gelu (erf and tanh forms), silu / swish, mish, softplus, relu, relu6, leaky_relu, elu,
+hardswish, hardsigmoid, square, reciprocal, swiglu, rms_norm, layer_norm (when its Mean / Variance side outputs
+are unused), mean and logsumexp."""
 from __future__ import annotations
 
 import math
 
 from ..pir import Operation
 
-PRIMITIVES = {"pd_op.exp", "pd_op.erf", "pd_op.rsqrt", "pd_op.sigmoid", "pd_op.max", "pd_op.sum", "pd_op.add",
-              "pd_op.subtract", "pd_op.multiply", "pd_op.divide", "pd_op.scale", "pd_op.tanh"}
+PRIMITIVES = {"pd_op.exp", "pd_op.log", "pd_op.erf", "pd_op.rsqrt", "pd_op.sigmoid", "pd_op.max", "pd_op.sum",
+              "pd_op.add", "pd_op.subtract", "pd_op.multiply", "pd_op.divide", "pd_op.maximum", "pd_op.minimum",
+              "pd_op.scale", "pd_op.tanh"}
 
 
 class _Builder:
@@ -43,7 +46,141 @@ def _softmax(b, op, log=False):
     s = b.op("pd_op.subtract", [x, m], x)
     e = b.op("pd_op.exp", [s], x)
     z = b.reduce("pd_op.sum", e, ax)
+    if log:
+        return b.op("pd_op.subtract", [s, b.op("pd_op.log", [z], z)], x)
     return b.op("pd_op.divide", [e, z], x)
+
+
+def _const(b, like, c):
+    """A tensor shaped like ``like`` filled with c: scale(like, 0, c)."""
+    return b.op("pd_op.scale", [like], like, scale=0.0, bias=float(c))
+
+
+def _relu(b, op):
+    x = op.operand_source(0)
+    return b.op("pd_op.maximum", [x, _const(b, x, 0.0)], x)
+
+
+def _relu6(b, op):
+    x = op.operand_source(0)
+    r = b.op("pd_op.maximum", [x, _const(b, x, 0.0)], x)
+    return b.op("pd_op.minimum", [r, _const(b, x, op.attrs().get("threshold", 6.0))], x)
+
+
+def _leaky_relu(b, op):
+    x = op.operand_source(0)
+    a = float(op.attrs().get("alpha", 0.02))
+    ax = b.op("pd_op.scale", [x], x, scale=a, bias=0.0)
+    return b.op("pd_op.maximum" if a <= 1.0 else "pd_op.minimum", [x, ax], x)
+
+
+def _elu(b, op):
+    x = op.operand_source(0)
+    a = float(op.attrs().get("alpha", 1.0))
+    zero = _const(b, x, 0.0)
+    neg = b.op("pd_op.scale", [b.op("pd_op.exp", [b.op("pd_op.minimum", [x, zero], x)], x)], x, scale=a, bias=-a)
+    return b.op("pd_op.add", [b.op("pd_op.maximum", [x, zero], x), neg], x)
+
+
+def _softplus_of(b, x, beta=1.0, threshold=20.0):
+    # log(1 + exp(beta x)) / beta, computed stably as max(bx, 0) + log(1 + exp(-|bx|))
+    bx = b.op("pd_op.scale", [x], x, scale=beta, bias=0.0)
+    zero = _const(b, x, 0.0)
+    pos = b.op("pd_op.maximum", [bx, zero], x)
+    nabs = b.op("pd_op.minimum", [bx, b.op("pd_op.scale", [bx], x, scale=-1.0, bias=0.0)], x)
+    l1p = b.op("pd_op.log", [b.op("pd_op.scale", [b.op("pd_op.exp", [nabs], x)], x, scale=1.0, bias=1.0)], x)
+    sp = b.op("pd_op.add", [pos, l1p], x)
+    return sp if beta == 1.0 else b.op("pd_op.scale", [sp], x, scale=1.0 / beta, bias=0.0)
+
+
+def _softplus(b, op):
+    return _softplus_of(b, op.operand_source(0), float(op.attrs().get("beta", 1.0)))
+
+
+def _mish(b, op):
+    x = op.operand_source(0)
+    return b.op("pd_op.multiply", [x, b.op("pd_op.tanh", [_softplus_of(b, x)], x)], x)
+
+
+def _hardsigmoid_of(b, x, slope, offset):
+    y = b.op("pd_op.scale", [x], x, scale=slope, bias=offset)
+    return b.op("pd_op.minimum", [b.op("pd_op.maximum", [y, _const(b, x, 0.0)], x), _const(b, x, 1.0)], x)
+
+
+def _hardsigmoid(b, op):
+    at = op.attrs()
+    return _hardsigmoid_of(b, op.operand_source(0), float(at.get("slope", 0.1666667)), float(at.get("offset", 0.5)))
+
+
+def _hardswish(b, op):
+    x = op.operand_source(0)
+    return b.op("pd_op.multiply", [x, _hardsigmoid_of(b, x, 1.0 / 6.0, 0.5)], x)
+
+
+def _square(b, op):
+    x = op.operand_source(0)
+    return b.op("pd_op.multiply", [x, x], x)
+
+
+def _reciprocal(b, op):
+    x = op.operand_source(0)
+    return b.op("pd_op.divide", [_const(b, x, 1.0), x], x)
+
+
+def _swiglu(b, op):
+    # swiglu(x, y) = silu(x) * y; single-operand form splits the last axis in halves (not decomposed here)
+    if op.num_operands() != 2:
+        return None
+    x, y = op.operand_source(0), op.operand_source(1)
+    return b.op("pd_op.multiply", [b.op("pd_op.multiply", [x, b.op("pd_op.sigmoid", [x], x)], x), y], x)
+
+
+def _rms_norm(b, op):
+    if any(not r.use_empty() for r in op.results()[1:]):
+        return None
+    x = op.operand_source(0)
+    axes = [len(x.shape) - 1]
+    n = x.shape[-1]
+    ms = b.op("pd_op.scale", [b.reduce("pd_op.sum", b.op("pd_op.multiply", [x, x], x), axes)],
+              b.reduce("pd_op.sum", x, axes), scale=1.0 / n, bias=float(op.attrs().get("epsilon", 1e-6)))
+    y = b.op("pd_op.multiply", [x, b.op("pd_op.rsqrt", [ms], ms)], x)
+    if op.num_operands() > 1:
+        y = b.op("pd_op.multiply", [y, op.operand_source(1)], x)
+    return y
+
+
+def _reduce_axes(op, x):
+    at = op.attrs()
+    nd = len(x.shape)
+    if at.get("reduce_all") or not at.get("dim", at.get("axis")):
+        return list(range(nd))
+    ax = at.get("dim", at.get("axis"))
+    ax = ax if isinstance(ax, (list, tuple)) else [ax]
+    return sorted(a % nd for a in ax)
+
+
+def _mean(b, op):
+    x = op.operand_source(0)
+    if op.num_operands() != 1 or x.shape is None or any(s is None or s < 0 for s in x.shape):
+        return None
+    axes = _reduce_axes(op, x)
+    if not op.attrs().get("keep_dim", op.attrs().get("keepdim", False)) and len(axes) != len(x.shape):
+        return None   # the primitive reductions keep dims; a squeeze would be needed
+    n = 1
+    for a in axes:
+        n *= x.shape[a]
+    s = b.reduce("pd_op.sum", x, axes)
+    return b.op("pd_op.scale", [s], s, scale=1.0 / n, bias=0.0)
+
+
+def _logsumexp(b, op):
+    x = op.operand_source(0)
+    axes = _reduce_axes(op, x)
+    if not op.attrs().get("keepdim", False):
+        return None
+    m = b.reduce("pd_op.max", x, axes)
+    z = b.reduce("pd_op.sum", b.op("pd_op.exp", [b.op("pd_op.subtract", [x, m], x)], x), axes)
+    return b.op("pd_op.add", [m, b.op("pd_op.log", [z], z)], m)
 
 
 def _gelu(b, op):
@@ -89,7 +226,12 @@ def _layer_norm(b, op):
     return y
 
 
-_RULES = {"pd_op.softmax": _softmax, "pd_op.gelu": _gelu, "pd_op.silu": _silu, "pd_op.layer_norm": _layer_norm}
+_RULES = {"pd_op.softmax": _softmax, "pd_op.log_softmax": lambda b, op: _softmax(b, op, log=True),
+          "pd_op.gelu": _gelu, "pd_op.silu": _silu, "pd_op.swish": _silu, "pd_op.layer_norm": _layer_norm,
+          "pd_op.relu": _relu, "pd_op.relu6": _relu6, "pd_op.leaky_relu": _leaky_relu, "pd_op.elu": _elu,
+          "pd_op.softplus": _softplus, "pd_op.mish": _mish, "pd_op.hardsigmoid": _hardsigmoid,
+          "pd_op.hardswish": _hardswish, "pd_op.square": _square, "pd_op.reciprocal": _reciprocal,
+          "pd_op.swiglu": _swiglu, "pd_op.rms_norm": _rms_norm, "pd_op.mean": _mean, "pd_op.logsumexp": _logsumexp}
 
 
 def decompose(program, src_vars=None, blacklist=frozenset(), whitelist=frozenset()):

@@ -229,6 +229,8 @@ def _kernels():
     F = torch.nn.functional
     prim = {
         "exp": lambda v, at: [torch.exp(v[0])],
+        "log": lambda v, at: [torch.log(v[0])],
+        "tanh": lambda v, at: [torch.tanh(v[0])],
         "erf": lambda v, at: [torch.erf(v[0])],
         "rsqrt": lambda v, at: [torch.rsqrt(v[0])],
         "sigmoid": lambda v, at: [torch.sigmoid(v[0])],
@@ -247,7 +249,7 @@ def _kernels():
 
 
 _BINARY_PRIM = {"pd_op.subtract": torch.sub, "pd_op.divide": torch.div, "pd_op.multiply": torch.mul,
-                "pd_op.add": torch.add}
+                "pd_op.add": torch.add, "pd_op.maximum": torch.maximum, "pd_op.minimum": torch.minimum}
 
 
 @torch.no_grad()

@@ -80,7 +80,7 @@ def test_decomposition_to_primitives():
     prog = _record(net, [3, 6])
     n = decomposition.decompose(prog)
     names = set(prog.op_names())
-    assert n == 3 and not names & {"pd_op.softmax", "pd_op.gelu", "pd_op.layer_norm"}
+    assert n == 4 and not names & {"pd_op.softmax", "pd_op.gelu", "pd_op.layer_norm", "pd_op.relu"}
     assert {"pd_op.erf", "pd_op.rsqrt", "pd_op.exp"} <= names
     torch.testing.assert_close(pir.run(prog, [x])[0], ref, rtol=1e-5, atol=1e-5)
     # whitelist restricts the rules applied
@@ -183,3 +183,51 @@ def test_serialize_round_trip(tmp_path):
         assert a.attrs() == b.attrs() and [r.shape for r in a.results()] == [r.shape for r in b.results()]
     pir.verify(back)
     torch.testing.assert_close(pir.run(back, [x])[0], pir.run(prog, [x])[0])
+
+
+def _unary_program(name, shape, attrs=None, extra=None):
+    p = pir.Program()
+    blk = p.global_block()
+    x = blk.append(pir.Operation("pd_op.data", [], [(shape, torch.float32)], {"name": "x", "col": 0})).result(0)
+    operands = [x]
+    if extra is not None:
+        operands.append(blk.append(pir.Operation("pd_op.data", [], [(extra, torch.float32)],
+                                                 {"name": "y", "col": 1})).result(0))
+    y = blk.append(pir.Operation(name, operands, [(shape, torch.float32)], attrs or {})).result(0)
+    blk.append(pir.Operation("pd_op.fetch", [y], [(shape, torch.float32)], {"name": "out", "col": 0}))
+    return p
+
+
+@pytest.mark.parametrize("name,attrs,ref", [
+    ("pd_op.relu", {}, torch.relu),
+    ("pd_op.relu6", {"threshold": 6.0}, lambda x: torch.clamp(x, 0, 6)),
+    ("pd_op.leaky_relu", {"alpha": 0.1}, lambda x: torch.nn.functional.leaky_relu(x, 0.1)),
+    ("pd_op.elu", {"alpha": 0.7}, lambda x: torch.nn.functional.elu(x, 0.7)),
+    ("pd_op.softplus", {"beta": 1.0}, torch.nn.functional.softplus),
+    ("pd_op.mish", {}, torch.nn.functional.mish),
+    ("pd_op.hardswish", {}, torch.nn.functional.hardswish),
+    ("pd_op.hardsigmoid", {"slope": 1.0 / 6, "offset": 0.5}, torch.nn.functional.hardsigmoid),
+    ("pd_op.square", {}, torch.square),
+    ("pd_op.reciprocal", {}, torch.reciprocal),
+    ("pd_op.log_softmax", {"axis": -1}, lambda x: torch.log_softmax(x, -1)),
+    ("pd_op.swish", {}, torch.nn.functional.silu),
+    ("pd_op.mean", {"dim": [1], "keep_dim": True}, lambda x: x.mean(1, keepdim=True)),
+    ("pd_op.logsumexp", {"axis": [1], "keepdim": True}, lambda x: torch.logsumexp(x, 1, keepdim=True)),
+])
+def test_decomposition_rules_match_reference(name, attrs, ref):
+    x = torch.randn(5, 7) * 4
+    p = _unary_program(name, [5, 7], attrs)
+    assert decomposition.decompose(p) == 1
+    names = set(p.op_names()) - {"pd_op.data", "pd_op.fetch"}
+    assert names <= decomposition.PRIMITIVES, names - decomposition.PRIMITIVES
+    torch.testing.assert_close(pir.run(p, [x])[0], ref(x), rtol=1e-5, atol=1e-5)
+
+
+def test_decomposition_swiglu_and_rms_norm():
+    x, y = torch.randn(4, 8), torch.randn(4, 8)
+    p = _unary_program("pd_op.swiglu", [4, 8], {}, extra=[4, 8])
+    assert decomposition.decompose(p) == 1
+    torch.testing.assert_close(pir.run(p, [x, y])[0], torch.nn.functional.silu(x) * y)
+    p2 = _unary_program("pd_op.rms_norm", [4, 8], {"epsilon": 1e-6})
+    assert decomposition.decompose(p2) == 1
+    torch.testing.assert_close(pir.run(p2, [x])[0], x * torch.rsqrt((x * x).mean(-1, keepdim=True) + 1e-6))
