@@ -187,14 +187,20 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int r0, int c0, int 
 // =====================================================================================
 //                                       FORWARD
 // =====================================================================================
-template <int D, bool CAUSAL, int MODE, bool DROP, bool F16>
-__global__ __launch_bounds__(256, (D > 128 ? 1 : 2)) void fwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+// NW waves x 32 query rows per workgroup: NW = 4 (two workgroups per CU for D <= 128) or NW = 8 (one 512-thread
+// workgroup per CU: every K/V tile is staged once for 256 query rows, half the global->LDS traffic and staging VALU
+// per MFMA; causal tiles above a wave's last row are skipped by that wave).  NW = 8 excludes FlashMask (its plans
+// are built for 128-row query blocks).
+template <int D, bool CAUSAL, int MODE, bool DROP, bool F16, int NW>
+__global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ Vv, bf16* __restrict__ O,
                                                      float* __restrict__ LSE, int B, int SqMax, int SkMax, int Hq,
                                                      int Hk, long sq, long sk, long sv, long so, float scale, Ext ex) {
-  constexpr int BM = 128, BN = 64, NCH = D / 8, KS = D / 16, DT = D / 32;
+  constexpr int BM = 32 * NW, BN = 64, NCH = D / 8, KS = D / 16, DT = D / 32, NT = NW * 64;
   constexpr int TILE = BN * D * 2;
-  constexpr int NLOAD = BN * NCH / 256;
+  constexpr int NLOAD = BN * NCH / NT;
+  static_assert(NLOAD * NT == BN * NCH, "tile copy must divide over the workgroup");
+  static_assert(NW == 4 || MODE != kMask, "FlashMask plans assume 128-row query blocks");
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][K|V]
   __shared__ int4 fm_s[MODE == kMask ? 2 * BN : 1];              // [buf][key] FlashMask intervals
 
@@ -262,7 +268,7 @@ __global__ __launch_bounds__(256, (D > 128 ? 1 : 2)) void fwd_kernel(const bf16*
   int voff_k[NLOAD], voff_v[NLOAD];
 #pragma unroll
   for (int i = 0; i < NLOAD; ++i) {
-    const int c = tid + 256 * i, row = c / NCH, ch = c % NCH;
+    const int c = tid + NT * i, row = c / NCH, ch = c % NCH;
     voff_k[i] = row * (int)sk * 2 + ch * 16;
     voff_v[i] = row * (int)sv * 2 + ch * 16;
   }
@@ -290,7 +296,7 @@ __global__ __launch_bounds__(256, (D > 128 ? 1 : 2)) void fwd_kernel(const bf16*
     if constexpr (MODE == kMask) reinterpret_cast<int*>(fm_s + buf * BN)[tid] = stm;
 #pragma unroll
     for (int i = 0; i < NLOAD; ++i) {
-      const int c = tid + 256 * i, row = c / NCH, ch = c % NCH;
+      const int c = tid + NT * i, row = c / NCH, ch = c % NCH;
       const int o = row * (D * 2) + swz(row, ch, NCH) * 16;
       *reinterpret_cast<u16x8*>(kt + o) = stk[i];
       *reinterpret_cast<u16x8*>(vt + o) = stv[i];
@@ -315,6 +321,13 @@ __global__ __launch_bounds__(256, (D > 128 ? 1 : 2)) void fwd_kernel(const bf16*
     lstore(0);
   }
   __syncthreads();
+  // static priority for the second-dispatched half of an 8-wave workgroup (MI355X_MICROARCH "Two waves per SIMD"
+  // item 4): it is the arbitration loser on every segment otherwise
+  if constexpr (NW == 8) {
+    if (wv >= 4) __builtin_amdgcn_s_setprio(1);
+  }
+  // causal: the last key this wave's 32 rows can see; tiles past it are all masked for the wave
+  const int wave_last_key = m0 + wv * 32 + 31 + off;
 
   for (int buf = 0; t < ntiles; buf ^= 1) {
     const int n0 = t * BN;
@@ -322,6 +335,15 @@ __global__ __launch_bounds__(256, (D > 128 ? 1 : 2)) void fwd_kernel(const bf16*
     const bool has_next = tn < ntiles;
     const char* kt = smem + buf * 2 * TILE;
     const char* vt = kt + TILE;
+    if (CAUSAL && NW == 8 && n0 > wave_last_key) {  // wave-uniform: only stage the next tile for the others
+      if (has_next) {
+        gload(tn * BN);
+        lstore(buf ^ 1);
+      }
+      __syncthreads();
+      t = tn;
+      continue;
+    }
 
     // ---- S^T = K . Q^T for two 32-key sub-blocks
     f32x16 s[2];
@@ -884,12 +906,21 @@ namespace {
 template <int D, bool F16>
 void launch_fwd(dim3 grid, hipStream_t st, const void* q, const void* k, const void* v, void* o, float* lse, int B,
                 int Sq, int Sk, int Hq, int Hk, long sq, long sk, long sv, long so, float scale, bool causal, int mode,
-                bool drop, const fa::Ext& ex) {
-#define PD_FA_FWD(CC, MM, DR)                                                                                     \
-  fa::fwd_kernel<D, CC, MM, DR, F16><<<grid, 256, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,       \
-                                                           (bf16*)o, lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, ex)
+                bool drop, const fa::Ext& ex, int nw) {
+#define PD_FA_FWD_W(CC, MM, DR, W)                                                                                 \
+  fa::fwd_kernel<D, CC, MM, DR, F16, W><<<grid, W * 64, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, \
+                                                                 (bf16*)o, lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, \
+                                                                 scale, ex)
+#define PD_FA_FWD(CC, MM, DR) PD_FA_FWD_W(CC, MM, DR, 4)
 #define PD_FA_FWD_C(MM, DR) \
   if (causal) PD_FA_FWD(true, MM, DR); else PD_FA_FWD(false, MM, DR);
+  if constexpr (D == 128) {
+    if (nw == 8) {  // dense / varlen without dropout
+      if (mode == 0) { if (causal) PD_FA_FWD_W(true, fa::kDense, false, 8); else PD_FA_FWD_W(false, fa::kDense, false, 8); }
+      else { if (causal) PD_FA_FWD_W(true, fa::kVarlen, false, 8); else PD_FA_FWD_W(false, fa::kVarlen, false, 8); }
+      return;
+    }
+  }
   if (drop) {
     if (mode == 0) { PD_FA_FWD_C(fa::kDense, true) } else { PD_FA_FWD_C(fa::kVarlen, true) }
   } else if (mode == 0) { PD_FA_FWD_C(fa::kDense, false) }
@@ -897,6 +928,7 @@ void launch_fwd(dim3 grid, hipStream_t st, const void* q, const void* k, const v
   else if constexpr (D <= 128) { PD_FA_FWD_C(fa::kMask, false) }
 #undef PD_FA_FWD_C
 #undef PD_FA_FWD
+#undef PD_FA_FWD_W
 }
 
 template <int D, bool F16>
@@ -943,6 +975,19 @@ static bool fa_dq_atomic() {
 }
 extern "C" int pd_flash_dq_atomic() { return fa_dq_atomic() ? 1 : 0; }
 
+// Forward workgroup width.  Measured (profiles/r3_flash_fwd_waves.md, B8 H32 D128): the 8-wave kernel wins on
+// long non-causal rows (S4096: 982 vs 937 TF/s) and loses on causal S4096 (808 vs 821: the per-wave tile skip
+// leaves SIMD partners unbalanced on the diagonal), D = 64 and short sequences.  PADDLE2_AMD_FA_FWD_WAVES = 4 / 8
+// forces one kernel (8 only where it exists: D = 128, dense / varlen, no dropout).
+static int fa_fwd_waves(int D, int Sq, int causal, int mode, int drop) {
+  if (D != 128 || mode == 2 || drop) return 4;
+  if (const char* e = getenv("PADDLE2_AMD_FA_FWD_WAVES")) {
+    const int w = atoi(e);
+    if (w == 4 || w == 8) return w;
+  }
+  return (!causal && Sq >= 2048) ? 8 : 4;
+}
+
 // Key-block width of the backward (rows of the dQ partial slabs): 256 keys for D <= 128, 128 for D = 256.
 extern "C" int pd_flash_bwd_block(int D) { return D > 128 ? 128 : 256; }
 
@@ -956,12 +1001,13 @@ extern "C" int pd_flash_fwd_ext(int dt, const void* q, const void* k, const void
                                 void* stream) {
   if (int e = check_args(dt, D, Hq, Hk, mode, drop, pdrop, cu_q, cu_k, fm, fm_t64, fm_hm)) return e;
   hipStream_t st = (hipStream_t)stream;
-  const int nmb = (Sq + 127) / 128;
+  const int nw = fa_fwd_waves(D, Sq, causal, mode, drop);
+  const int nmb = (Sq + 32 * nw - 1) / (32 * nw);
   dim3 grid(nmb * Hq * B);
   fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm, seed,
              drop ? (unsigned)fminf(pdrop * 4294967296.f, 4294967040.f) : 0u, drop ? 1.f / (1.f - pdrop) : 1.f};
 #define PD_FWD(DD, FF) \
-  launch_fwd<DD, FF>(grid, st, q, k, v, o, lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, causal, mode, drop, ex)
+  launch_fwd<DD, FF>(grid, st, q, k, v, o, lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, causal, mode, drop, ex, nw)
   const bool f16 = dt == kF16;
   if (D == 128) { if (f16) PD_FWD(128, true); else PD_FWD(128, false); }
   else if (D == 64) { if (f16) PD_FWD(64, true); else PD_FWD(64, false); }

@@ -181,3 +181,101 @@ def test_cond_mismatched_structure_raises():
 
     with pytest.raises(ValueError):
         _static_run(build, {"x": np.ones(2, "float32")})
+
+
+# ---------------------------------------------------------------- return / break / continue / for-range passes
+def _early_return(x):
+    if x.mean() > 0:
+        return x * 2.0
+    y = x - 1.0
+    return y * y
+
+
+def _break_loop(x, n):
+    i = paddle.zeros([1], "float32")
+    s = x
+    while i < n:
+        s = s + 1.0
+        if s.sum() > 10.0:
+            break
+        i = i + 1.0
+    return s
+
+
+def _continue_range(x, n):
+    s = x * 0.0
+    for k in range(n):
+        if k % 2 == 1:
+            continue
+        s = s + x * float(k)
+    return s
+
+
+def _range_tensor_bound(x, n):
+    acc = x
+    for _ in range(n):
+        acc = acc * 0.5 + x
+    return acc
+
+
+def _return_in_loop(x, n):
+    i = paddle.zeros([1], "float32")
+    while i < n:
+        x = x + 1.0
+        if x.sum() > 6.0:
+            return x * 10.0
+        i = i + 1.0
+    return x
+
+
+def test_prepasses_keep_eager_semantics():
+    from paddle2_amd.jit.dy2static import convert_function
+
+    for fn, cases in ((_early_return, [([1.0, 2.0],), ([-3.0, 1.0],)]),
+                      (_break_loop, [([1.0, 2.0], 10.0), ([0.0, 0.0], 2.0), ([5.0, 6.0], 3.0)]),
+                      (_return_in_loop, [([1.0, 1.0], 5.0), ([0.0, 0.0], 1.0)])):
+        g = convert_function(fn)
+        assert g is not fn
+        for c in cases:
+            args = [paddle.to_tensor(np.array(c[0], "float32"))]
+            if len(c) > 1:
+                args.append(paddle.to_tensor(np.array([c[1]], "float32")))
+            np.testing.assert_allclose(_np(g(*args)), _np(fn(*args)), rtol=1e-6)
+    g = convert_function(_continue_range)
+    x = paddle.to_tensor(np.array([1.0, 2.0], "float32"))
+    for n in (0, 1, 4, 7):
+        np.testing.assert_allclose(_np(g(x, n)), _np(_continue_range(x, n)))
+
+
+def test_to_static_early_return_symbolic():
+    sf = paddle.jit.to_static(_early_return)
+    for v in ([1.0, 2.0], [-3.0, 1.0]):
+        x = paddle.to_tensor(np.array(v, "float32"))
+        np.testing.assert_allclose(_np(sf(x)), _np(_early_return(x)), rtol=1e-6)
+    assert len(sf._cache) == 1  # one program serves both return paths
+
+
+def test_to_static_break_in_tensor_while():
+    sf = paddle.jit.to_static(_break_loop)
+    for xv, n in (([1.0, 2.0], 10.0), ([0.0, 0.0], 2.0), ([5.0, 6.0], 3.0)):
+        x = paddle.to_tensor(np.array(xv, "float32"))
+        nt = paddle.to_tensor(np.array([n], "float32"))
+        np.testing.assert_allclose(_np(sf(x, nt)), _np(_break_loop(x, nt)), rtol=1e-6)
+    assert len(sf._cache) == 1
+
+
+def test_to_static_return_inside_tensor_while():
+    sf = paddle.jit.to_static(_return_in_loop)
+    for xv, n in (([1.0, 1.0], 5.0), ([0.0, 0.0], 1.0), ([3.0, 3.0], 4.0)):
+        x = paddle.to_tensor(np.array(xv, "float32"))
+        nt = paddle.to_tensor(np.array([n], "float32"))
+        np.testing.assert_allclose(_np(sf(x, nt)), _np(_return_in_loop(x, nt)), rtol=1e-6)
+
+
+def test_to_static_for_range_over_tensor_bound():
+    sf = paddle.jit.to_static(_range_tensor_bound)
+    x = paddle.to_tensor(np.array([1.0, -2.0], "float32"))
+    for n in (0, 1, 3):
+        nt = paddle.to_tensor(np.array([n], "int64"))
+        np.testing.assert_allclose(_np(sf(x, nt)), _np(_range_tensor_bound(x, n)), rtol=1e-6)
+    assert len(sf._cache) == 1

@@ -74,3 +74,24 @@ def test_flash_varlen_fp16_and_d256():
             a, b = int(cu[i]), int(cu[i + 1])
             ref, _ = T.flash_attention(q[a:b].float()[None], k[a:b].float()[None], v[a:b].float()[None], True)
             assert _err(o[a:b], ref[0]) < 2e-2
+
+
+@pytest.mark.parametrize("causal,Sq,Sk,Hq,Hk", [(False, 2304, 2304, 4, 4), (True, 1000, 1000, 4, 2),
+                                                (True, 512, 1536, 2, 2), (False, 300, 700, 4, 1)])
+def test_fwd_8wave_matches_4wave_and_fp32(monkeypatch, causal, Sq, Sk, Hq, Hk):
+    """The 8-wave forward (256 query rows per workgroup, per-wave causal tile skip) against the 4-wave kernel
+    (bit for bit: same per-row accumulation order) and the fp32 math reference; ragged Sq, Sk > Sq (bottom-right
+    causal alignment) and GQA included."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    q = torch.randn(2, Sq, Hq, 128, generator=g, device=DEV).to(torch.bfloat16)
+    k = torch.randn(2, Sk, Hk, 128, generator=g, device=DEV).to(torch.bfloat16)
+    v = torch.randn(2, Sk, Hk, 128, generator=g, device=DEV).to(torch.bfloat16)
+    outs = {}
+    for w in ("4", "8"):
+        monkeypatch.setenv("PADDLE2_AMD_FA_FWD_WAVES", w)
+        o, lse = T.flash_attention(q, k, v, causal)
+        torch.cuda.synchronize()
+        outs[w] = (o, lse)
+    assert torch.equal(outs["4"][0], outs["8"][0]) and torch.equal(outs["4"][1], outs["8"][1])
+    orf, _ = T.flash_attention(q.float(), k.float(), v.float(), causal)
+    assert _err(outs["8"][0], orf) < 2e-2
