@@ -133,10 +133,29 @@ class StaticFunction:
         return next(iter(self._cache.values()))[0]
 
 
-def to_static(function=None, input_spec=None, build_strategy=None, backend=None, full_graph=True, **kwargs):
+def to_static(function=None, input_spec=None, build_strategy=None, backend=None, full_graph=None, **kwargs):
+    """full_graph=True: AST mode (dy2static conversion, one Program per input signature; an unconvertible
+    construct raises).  full_graph=False: SOT mode (jit/sot.py — guarded Program cache, graph breaks fall back to
+    dygraph at Layer granularity).  Unset: ENABLE_FALL_BACK (reference jit/api.py:109) picks; this framework's
+    default is AST mode, whose conversion already captures tensor-dependent control flow."""
+    if full_graph is None:
+        from .sot import enabled_by_env
+
+        full_graph = not enabled_by_env()
+
     def deco(fn):
         from ..nn.layer.layers import Layer
 
+        if not full_graph:
+            from .sot import SymbolicTranslator, _BoundForward
+
+            if isinstance(fn, Layer):
+                fn._dygraph_forward = fn.forward
+                fn._input_spec = input_spec
+                fn.forward = _BoundForward(SymbolicTranslator(type(fn).forward, layer=fn,
+                                                              build_strategy=build_strategy))
+                return fn
+            return SymbolicTranslator(fn, build_strategy=build_strategy)
         if isinstance(fn, Layer):
             sf = StaticFunction(type(fn).forward, input_spec, build_strategy, layer=fn)
             fn._static_forward = sf
