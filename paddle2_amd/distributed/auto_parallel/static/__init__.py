@@ -1,0 +1,6 @@
+"""Static-graph auto-parallel engine: completion (SPMD-rule propagation over a recorded Program), partitioner
+with reshard insertion (per-rank SPMD execution on the framework's reshard engine), MI355X cost model and a
+placement planner (reference python/paddle/distributed/auto_parallel/static/)."""
+from .completion import Completer, DistAttr, DistContext, attr_from_placements  # noqa: F401
+from .cost_model import ClusterSpec, CostModel, Planner, reshard_steps  # noqa: F401
+from .partitioner import DistributedProgram, parallelize_program  # noqa: F401
