@@ -1,0 +1,645 @@
+"""Long-tail ops of the reference inventory that have no same-named public function (reference
+paddle/phi/ops/yaml/ops.yaml, fused_ops.yaml, sparse_ops.yaml; kernels under paddle/phi/kernels/ named per op).
+
+Functional optimizer steps (``nadam_``, ``radam_``, ``asgd_``, ``rprop_``, ``decayed_adagrad``, ``ftrl``,
+``dpsgd``, ``lars_momentum_``, ``average_accumulates_``) update their tensors in place like the reference's
+inplace kernels; MoE routing helpers (``number_count``, ``assign_pos``, ``limit_by_capacity``,
+``prune_gate_by_capacity``, ``random_routing``) follow python/paddle/distributed/models/moe/utils.py; the fused
+inference ops compose the framework's native kernels (layer_norm / linear / activations).  Registered through
+``op_schema.ALIASES`` so ``_C_ops.<name>`` resolves them.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .op_schema import _lr, _raw, _upd, _wrap
+
+
+def _p(param, master_param, multi_precision):
+    return _raw(master_param if (multi_precision and master_param is not None) else param).float()
+
+
+def _store(param, master_param, multi_precision, new):
+    _upd(param, new)
+    if master_param is not None and multi_precision:
+        _upd(master_param, new)
+
+
+# ------------------------------------------------------------------------------------------ optimizers
+@torch.no_grad()
+def nadam_(param, grad, learning_rate, momentum_decay_pow, beta2_pow, mu_product, moment1, moment2,
+           master_param=None, beta1=0.9, beta2=0.999, epsilon=1e-8, momentum_decay=0.004, multi_precision=False):
+    """phi nadam kernel: momentum_decay_pow carries 0.96^t, mu_product the running product of mu_t."""
+    p, g = _p(param, master_param, multi_precision), _raw(grad).float()
+    mdp = _raw(momentum_decay_pow).float() * 0.96
+    mu_t = beta1 * (1 - 0.5 * mdp ** momentum_decay)
+    mu_t1 = beta1 * (1 - 0.5 * (mdp * 0.96) ** momentum_decay)
+    mup = _raw(mu_product).float() * mu_t
+    b2p = _raw(beta2_pow).float() * beta2
+    m1 = _raw(moment1).float() * beta1 + (1 - beta1) * g
+    m2 = _raw(moment2).float() * beta2 + (1 - beta2) * g * g
+    m1h = mu_t1 * m1 / (1 - mup * mu_t1) + (1 - mu_t) * g / (1 - mup)
+    m2h = m2 / (1 - b2p)
+    _store(param, master_param, multi_precision, p - _lr(learning_rate) * m1h / (m2h.sqrt() + epsilon))
+    for dst, v in ((momentum_decay_pow, mdp), (mu_product, mup), (beta2_pow, b2p), (moment1, m1), (moment2, m2)):
+        _upd(dst, v)
+    return param, momentum_decay_pow, beta2_pow, mu_product, moment1, moment2, master_param
+
+
+@torch.no_grad()
+def radam_(param, grad, learning_rate, beta1_pow, beta2_pow, rho, moment1, moment2, master_param=None, beta1=0.9,
+           beta2=0.999, epsilon=1e-8, multi_precision=False):
+    """phi radam kernel: beta pows advance first, rho carries the step count t (as a float)."""
+    p, g = _p(param, master_param, multi_precision), _raw(grad).float()
+    b1p = _raw(beta1_pow).float() * beta1
+    b2p = _raw(beta2_pow).float() * beta2
+    t = _raw(rho).float() + 1
+    rho_inf = 2 / (1 - beta2) - 1
+    rho_t = rho_inf - 2 * t * b2p / (1 - b2p)
+    m1 = _raw(moment1).float() * beta1 + (1 - beta1) * g
+    m2 = _raw(moment2).float() * beta2 + (1 - beta2) * g * g
+    mh = m1 / (1 - b1p)
+    r = torch.sqrt(((rho_t - 4) * (rho_t - 2) * rho_inf / ((rho_inf - 4) * (rho_inf - 2) * rho_t)).clamp(min=0))
+    adapt = r * mh * torch.sqrt(1 - b2p) / (m2.sqrt() + epsilon)
+    upd = torch.where(rho_t > 5, adapt, mh)
+    _store(param, master_param, multi_precision, p - _lr(learning_rate) * upd)
+    for dst, v in ((beta1_pow, b1p), (beta2_pow, b2p), (rho, t), (moment1, m1), (moment2, m2)):
+        _upd(dst, v)
+    return param, beta1_pow, beta2_pow, rho, moment1, moment2, master_param
+
+
+@torch.no_grad()
+def asgd_(param, grad, learning_rate, d, y, n, master_param=None, multi_precision=False):
+    """phi asgd kernel: d = d - y + g; y = g; p -= lr / n * d (n = min(step, batch_num), supplied)."""
+    p, g = _p(param, master_param, multi_precision), _raw(grad).float()
+    dn = _raw(d).float() - _raw(y).float() + g
+    _store(param, master_param, multi_precision, p - _lr(learning_rate) / _raw(n).float().reshape(-1)[0] * dn)
+    _upd(d, dn)
+    _upd(y, g)
+    return param, d, y, master_param
+
+
+@torch.no_grad()
+def rprop_(param, grad, prev, learning_rate, master_param=None, learning_rate_range=(1e-5, 50), etas=(0.5, 1.2),
+           multi_precision=False):
+    """phi rprop kernel: per-element step sizes (learning_rate is a tensor like param)."""
+    p, g = _p(param, master_param, multi_precision), _raw(grad).float()
+
+    def pair(v):
+        r = _raw(v)
+        return [float(a) for a in (r.reshape(-1).tolist() if isinstance(r, torch.Tensor) else v)]
+
+    lo, hi = pair(learning_rate_range)
+    em, ep = pair(etas)
+    s = g * _raw(prev).float()
+    lrs = _raw(learning_rate).float()
+    lrs = torch.where(s > 0, lrs * ep, torch.where(s < 0, lrs * em, lrs)).clamp(lo, hi)
+    g = torch.where(s < 0, torch.zeros_like(g), g)
+    _store(param, master_param, multi_precision, p - torch.sign(g) * lrs)
+    _upd(prev, g)
+    _upd(learning_rate, lrs)
+    return param, prev, learning_rate, master_param
+
+
+@torch.no_grad()
+def decayed_adagrad(param, grad, moment, learning_rate, decay=0.95, epsilon=1e-6):
+    g = _raw(grad).float()
+    m = _raw(moment).float() * decay + (1 - decay) * g * g
+    _upd(param, _raw(param).float() - _lr(learning_rate) * g / (m.sqrt() + epsilon))
+    _upd(moment, m)
+    return param, moment
+
+
+@torch.no_grad()
+def ftrl(param, squared_accumulator, linear_accumulator, grad, learning_rate, l1=0.0, l2=0.0, lr_power=-0.5):
+    """FTRL-proximal (phi ftrl kernel): returns (param, squared_accum, linear_accum) updated in place."""
+    p, g = _raw(param).float(), _raw(grad).float()
+    n, z = _raw(squared_accumulator).float(), _raw(linear_accumulator).float()
+    lr = _lr(learning_rate)
+    nn_ = n + g * g
+    if lr_power == -0.5:
+        sigma = (nn_.sqrt() - n.sqrt()) / lr
+        denom = nn_.sqrt() / lr + 2 * l2
+    else:
+        sigma = (nn_.pow(-lr_power) - n.pow(-lr_power)) / lr
+        denom = nn_.pow(-lr_power) / lr + 2 * l2
+    z = z + g - sigma * p
+    newp = torch.where(z.abs() > l1, (torch.sign(z) * l1 - z) / denom, torch.zeros_like(z))
+    _upd(param, newp)
+    _upd(squared_accumulator, nn_)
+    _upd(linear_accumulator, z)
+    return param, squared_accumulator, linear_accumulator
+
+
+@torch.no_grad()
+def dpsgd(param, grad, learning_rate, clip=10.0, batch_size=16.0, sigma=1.0, seed=0):
+    """Differentially private SGD (phi dpsgd kernel): clip the gradient to L2 norm ``clip``, add Gaussian noise
+    of std ``sigma * clip`` scaled by 1 / batch_size, then an SGD step."""
+    g = _raw(grad).float()
+    norm = g.norm()
+    g = g / torch.clamp(norm / clip, min=1.0)
+    gen = torch.Generator(device=g.device)
+    gen.manual_seed(int(seed))
+    noise = torch.randn(g.shape, generator=gen, device=g.device) * (sigma * clip)
+    g = g + noise / batch_size
+    _upd(param, _raw(param).float() - _lr(learning_rate) * g)
+    return param
+
+
+@torch.no_grad()
+def lars_momentum_(param, grad, velocity, learning_rate, master_param=None, mu=0.9, lars_coeff=0.001,
+                   lars_weight_decay=(0.0005,), epsilon=0.0, multi_precision=False, rescale_grad=1.0):
+    """LARS momentum for one (or a list of) parameter(s) (phi lars_momentum kernel)."""
+    many = isinstance(param, (list, tuple))
+    ps, gs, vs = (param, grad, velocity) if many else ([param], [grad], [velocity])
+    lrs = learning_rate if isinstance(learning_rate, (list, tuple)) else [learning_rate] * len(ps)
+    mps = master_param if isinstance(master_param, (list, tuple)) else [master_param] * len(ps)
+    wds = list(lars_weight_decay) if isinstance(lars_weight_decay, (list, tuple)) else [lars_weight_decay]
+    for i, (pp, gg, vv) in enumerate(zip(ps, gs, vs)):
+        wd = wds[i] if i < len(wds) else wds[-1]
+        p, g = _p(pp, mps[i], multi_precision), _raw(gg).float() * rescale_grad
+        pn, gn = p.norm(), g.norm()
+        local = torch.where((pn > 0) & (gn > 0), lars_coeff * pn / (gn + wd * pn + epsilon), torch.ones_like(pn))
+        v = _raw(vv).float() * mu + _lr(lrs[i]) * local * (g + wd * p)
+        _store(pp, mps[i], multi_precision, p - v)
+        _upd(vv, v)
+    return param, velocity, master_param
+
+
+@torch.no_grad()
+def average_accumulates_(param, in_sum_1, in_sum_2, in_sum_3, in_num_accumulates, in_old_num_accumulates,
+                         in_num_updates, average_window=0.0, max_average_window=10000, min_average_window=10000):
+    """ModelAverage accumulation (phi average_accumulates kernel): sum_1 += param; every 16384 updates sum_1 is
+    folded into sum_2; when the window is full, sums roll into sum_3 and restart."""
+    p = _raw(param).float()
+    s1, s2, s3 = (_raw(x).float() for x in (in_sum_1, in_sum_2, in_sum_3))
+    na = int(_raw(in_num_accumulates).reshape(-1)[0]) + 1
+    ona = int(_raw(in_old_num_accumulates).reshape(-1)[0])
+    nu = int(_raw(in_num_updates).reshape(-1)[0]) + 1
+    s1 = s1 + p
+    if nu % 16384 == 0:
+        s2, s1 = s2 + s1, torch.zeros_like(s1)
+    if na >= min_average_window and na >= min(max_average_window, nu * average_window):
+        s3, s1, s2 = s1 + s2, torch.zeros_like(s1), torch.zeros_like(s2)
+        ona, na = na, 0
+    for dst, v in ((in_sum_1, s1), (in_sum_2, s2), (in_sum_3, s3)):
+        _upd(dst, v)
+    for dst, v in ((in_num_accumulates, na), (in_old_num_accumulates, ona), (in_num_updates, nu)):
+        _raw(dst).fill_(v)
+    return in_sum_1, in_sum_2, in_sum_3, in_num_accumulates, in_old_num_accumulates, in_num_updates
+
+
+# ------------------------------------------------------------------------------------------ MoE routing
+def number_count(numbers, upper_range):
+    """Count of each expert id in ``numbers`` (ids < 0 are dropped)."""
+    n = _raw(numbers).reshape(-1).long()
+    n = n[(n >= 0) & (n < upper_range)]
+    return _wrap(torch.bincount(n, minlength=upper_range).to(torch.int64))
+
+
+def assign_pos(x, cum_count, eff_num_len):
+    """Token positions grouped by expert: out[cum_count[e-1] .. cum_count[e]) lists the tokens routed to e."""
+    ids = _raw(x).reshape(-1).long()
+    valid = ids >= 0
+    order = torch.argsort(torch.where(valid, ids, torch.full_like(ids, 1 << 40)), stable=True)
+    n = int(_raw(eff_num_len).reshape(-1)[0]) if isinstance(_raw(eff_num_len), torch.Tensor) else int(eff_num_len)
+    return _wrap(order[:n].to(torch.int64))
+
+
+def limit_by_capacity(expert_count, capacity, n_worker):
+    """Clip per-(worker, expert) counts so each expert's total over workers stays within its capacity, filling
+    workers in order (moe utils _limit_by_capacity)."""
+    ec = _raw(expert_count).reshape(int(n_worker), -1).long()
+    cap = _raw(capacity).reshape(-1).long().clone()
+    out = torch.zeros_like(ec)
+    for w in range(ec.shape[0]):
+        take = torch.minimum(ec[w], cap)
+        out[w] = take
+        cap -= take
+    return _wrap(out.reshape(-1))
+
+
+def prune_gate_by_capacity(gate_idx, expert_count, n_expert, n_worker):
+    """Tokens beyond their expert's remaining count get gate -1 (dropped), in token order."""
+    gi = _raw(gate_idx).reshape(-1).long().clone()
+    left = _raw(expert_count).reshape(-1).long().clone()
+    for i in range(gi.numel()):
+        e = int(gi[i])
+        if e < 0:
+            continue
+        if left[e] > 0:
+            left[e] -= 1
+        else:
+            gi[i] = -1
+    return _wrap(gi.reshape(_raw(gate_idx).shape))
+
+
+def random_routing(topk_idx, topk_value, prob):
+    """GShard random routing: the 2nd expert is kept only where 2 * value >= prob (uniform sample)."""
+    idx = _raw(topk_idx).clone()
+    v = _raw(topk_value)
+    p = _raw(prob).reshape(-1)
+    drop = 2 * v[:, 1] < p[: idx.shape[0]]
+    idx[:, 1] = torch.where(drop, torch.full_like(idx[:, 1], -1), idx[:, 1])
+    return _wrap(idx)
+
+
+# ------------------------------------------------------------------------------------------ misc tensor ops
+def partial_concat(x, start_index=0, length=-1):
+    """Concatenate columns [start, start+length) of every 2-D input along axis 1."""
+    outs = []
+    for t in x:
+        r = _raw(t)
+        s = start_index % r.shape[1] if start_index < 0 else start_index
+        e = r.shape[1] if length < 0 else s + length
+        outs.append(r[:, s:e])
+    return _wrap(torch.cat(outs, dim=1))
+
+
+def partial_sum(x, start_index=0, length=-1):
+    """Sum of columns [start, start+length) of every 2-D input."""
+    acc = None
+    for t in x:
+        r = _raw(t)
+        s = start_index % r.shape[1] if start_index < 0 else start_index
+        e = r.shape[1] if length < 0 else s + length
+        acc = r[:, s:e] if acc is None else acc + r[:, s:e]
+    return _wrap(acc)
+
+
+def shuffle_batch(x, seed=None, startup_seed=0):
+    """Shuffle rows (all leading dims flattened); returns (out, shuffle_idx, seed_out)."""
+    r = _raw(x)
+    flat = r.reshape(-1, r.shape[-1])
+    s = int(_raw(seed).reshape(-1)[0]) if seed is not None else int(startup_seed)
+    gen = torch.Generator(device="cpu")
+    gen.manual_seed(s)
+    idx = torch.randperm(flat.shape[0], generator=gen).to(r.device)
+    return (_wrap(flat[idx].reshape(r.shape)), _wrap(idx.to(torch.int64)),
+            _wrap(torch.tensor([s + 1], dtype=torch.int64)))
+
+
+def hash(x, num_hash=1, mod_by=100000):  # noqa: A001 — the reference op name
+    """Per-row hash ids (num_hash independent hashes of each int64 row, modulo mod_by)."""
+    r = _raw(x).long()
+    rows = r.reshape(r.shape[0], -1)
+    out = torch.empty(rows.shape[0], num_hash, 1, dtype=torch.int64, device=r.device)
+    for k in range(num_hash):
+        h = torch.full((rows.shape[0],), 1469598103934665603 + k, dtype=torch.int64, device=r.device)
+        for c in range(rows.shape[1]):
+            h = (h ^ rows[:, c]) * 1099511628211
+        out[:, k, 0] = torch.remainder(h, mod_by)
+    return _wrap(out)
+
+
+def print(x, first_n=-1, message="", summarize=20, print_tensor_name=True, print_tensor_type=True,  # noqa: A001
+          print_tensor_shape=True, print_tensor_layout=True, print_tensor_lod=True, print_phase="BOTH",
+          is_forward=True):
+    import builtins
+
+    r = _raw(x)
+    parts = [message] if message else []
+    if print_tensor_type:
+        parts.append(f"dtype: {r.dtype}")
+    if print_tensor_shape:
+        parts.append(f"shape: {list(r.shape)}")
+    vals = r.reshape(-1)[: summarize if summarize > 0 else None].tolist()
+    parts.append(f"data: {vals}")
+    builtins.print("  ".join(parts))
+    return x
+
+
+def add_position_encoding(x, alpha=1.0, beta=1.0):
+    """x * alpha + beta * sinusoidal position encoding ([B, S, D], half sin / half cos)."""
+    r = _raw(x)
+    B, S, D = r.shape
+    half = D // 2
+    pos = torch.arange(S, device=r.device, dtype=torch.float32)[:, None]
+    div = torch.pow(10000.0, torch.arange(half, device=r.device, dtype=torch.float32) / max(half - 1, 1))
+    enc = torch.cat([torch.sin(pos / div), torch.cos(pos / div)], dim=1)
+    return _wrap((r.float() * alpha + beta * enc[None]).to(r.dtype))
+
+
+def cvm(x, cvm, use_cvm=True):  # noqa: A002
+    """Continuous-value model: the first two columns (show, click) become log(show+1), log(click+1)-log(show+1),
+    or are dropped when use_cvm is False."""
+    r = _raw(x).float()
+    if not use_cvm:
+        return _wrap(r[:, 2:])
+    show = torch.log(r[:, :1] + 1)
+    click = torch.log(r[:, 1:2] + 1) - show
+    return _wrap(torch.cat([show, click, r[:, 2:]], dim=1))
+
+
+def batch_fc(input, w, bias):  # noqa: A002
+    """Per-slot FC: out[s] = input[s] @ w[s] + bias[s] ([S, N, in] x [S, in, out])."""
+    return _wrap(torch.bmm(_raw(input), _raw(w)) + _raw(bias).unsqueeze(1))
+
+
+def accuracy_check(x, y, fn_name="", rtol=1e-5, atol=1e-8, equal_nan=False):
+    ok = torch.allclose(_raw(x).float(), _raw(y).float(), rtol=rtol, atol=atol, equal_nan=equal_nan)
+    if not ok:
+        raise AssertionError(f"accuracy_check failed for {fn_name}")
+    return _wrap(torch.tensor(True))
+
+
+def coalesce_tensor(input, dtype=None, copy_data=False, set_constant=False, persist_output=False,  # noqa: A002
+                    constant=0.0, use_align=True, align_size=-1, size_of_dtype=-1, concated_shapes=(),
+                    concated_ranks=()):
+    """One flat buffer holding every input (256-B aligned chunks when use_align); returns (outputs as views of the
+    buffer, fused buffer)."""
+    ts = [_raw(t) for t in input]
+    dt = ts[0].dtype
+    esz = torch.empty((), dtype=dt).element_size()
+    align = (align_size if align_size > 0 else 256) // esz if use_align else 1
+    sizes = [((t.numel() + align - 1) // align) * align for t in ts]
+    buf = torch.full((sum(sizes),), constant if set_constant else 0, dtype=dt, device=ts[0].device)
+    outs, off = [], 0
+    for t, n in zip(ts, sizes):
+        v = buf[off: off + t.numel()].view(t.shape)
+        if copy_data:
+            v.copy_(t)
+        outs.append(_wrap(v))
+        off += n
+    return outs, _wrap(buf)
+
+
+coalesce_tensor_ = coalesce_tensor
+
+
+def embedding_grad_dense(x, weight, out_grad, padding_idx=-1, sparse=False):
+    ids = _raw(x).reshape(-1).long()
+    g = _raw(out_grad).reshape(ids.numel(), -1)
+    w = _raw(weight)
+    dw = torch.zeros(w.shape, dtype=torch.float32, device=w.device)
+    keep = ids != padding_idx if padding_idx >= 0 else torch.ones_like(ids, dtype=torch.bool)
+    dw.index_add_(0, ids[keep], g[keep].float())
+    return _wrap(dw.to(w.dtype))
+
+
+def straight_through_estimator_grad(out_grad):
+    return out_grad
+
+
+_ACTS = {"relu": F.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh, "gelu": F.gelu, "identity": lambda t: t,
+         "scale": lambda t: t, "swish": F.silu, "silu": F.silu}
+
+
+def fused_elemwise_activation(x, y, functor_list=("elementwise_add", "relu"), axis=-1, scale=0.0,
+                              save_intermediate_out=False):
+    """Two-functor fusion: [binary, unary] -> binary(x, unary(y)); [unary, binary] -> unary(binary(x, y))."""
+    a, b = _raw(x), _raw(y)
+    f0, f1 = functor_list
+
+    def binary(name, u, v):
+        return {"elementwise_add": torch.add, "elementwise_mul": torch.mul, "elementwise_sub": torch.sub}[name](u, v)
+
+    def unary(name, t):
+        return t * scale if name == "scale" else _ACTS[name](t)
+
+    if f0.startswith("elementwise_"):
+        inter = unary(f1, b)
+        out = binary(f0, a, inter)
+    else:
+        inter = binary(f1, a, b)
+        out = unary(f0, inter)
+    return (_wrap(out), _wrap(inter)) if save_intermediate_out else _wrap(out)
+
+
+def fused_elemwise_add_activation(x, y, functor_list=("elementwise_add", "relu"), axis=-1, scale=0.0,
+                                  save_intermediate_out=False):
+    return fused_elemwise_activation(x, y, functor_list, axis, scale, save_intermediate_out)
+
+
+def fused_fc_elementwise_layernorm(x, w, y, bias0=None, scale=None, bias1=None, x_num_col_dims=1,
+                                   activation_type="", epsilon=1e-5, begin_norm_axis=1):
+    """layer_norm(act(x @ w + bias0) + y) (fused_ops.yaml fused_fc_elementwise_layernorm)."""
+    xr = _raw(x).reshape(int(torch.tensor(_raw(x).shape[:x_num_col_dims]).prod()), -1)
+    h = xr @ _raw(w)
+    if bias0 is not None:
+        h = h + _raw(bias0)
+    if activation_type:
+        h = _ACTS[activation_type](h)
+    h = h + _raw(y).reshape(h.shape)
+    nshape = h.shape[begin_norm_axis:]
+    out = F.layer_norm(h.float(), nshape, None if scale is None else _raw(scale).float(),
+                       None if bias1 is None else _raw(bias1).float(), epsilon).to(h.dtype)
+    return _wrap(out)
+
+
+def fused_scale_bias_add_relu(x1, scale1, bias1, x2, scale2=None, bias2=None, fuse_dual=False, exhaustive_search=False):
+    """relu(x1 * scale1 + bias1 + (x2 * scale2 + bias2 if fuse_dual else x2)) over NHWC channels."""
+    a = _raw(x1) * _raw(scale1) + _raw(bias1)
+    b = _raw(x2) * _raw(scale2) + _raw(bias2) if fuse_dual else _raw(x2)
+    return _wrap(F.relu(a + b))
+
+
+def fused_embedding_eltwise_layernorm(ids, embs, bias, scale, epsilon=1e-5):
+    """layer_norm(sum_i embs[i][ids[i]]) (ERNIE-style embedding fusion)."""
+    acc = None
+    for i, e in zip(ids, embs):
+        v = F.embedding(_raw(i).long(), _raw(e))
+        acc = v if acc is None else acc + v
+    return _wrap(F.layer_norm(acc.float(), acc.shape[-1:], _raw(scale).float(), _raw(bias).float(),
+                              epsilon).to(acc.dtype))
+
+
+def squeeze_excitation_block(x, filter, filter_max=None, bias=None, branch=None, act_type=(1, 1, 1),  # noqa: A002
+                             act_param=(0.0, 0.0, 0.0), filter_dims=()):
+    """SE block: x * sigmoid(fc2(relu(fc1(avgpool(x))))) with filter = [fc1 | fc2] flattened ([C/r*C + C*C/r])."""
+    r = _raw(x)
+    C = r.shape[1]
+    f = _raw(filter).reshape(-1)
+    mid = f.numel() // (2 * C)
+    w1, w2 = f[: mid * C].reshape(mid, C), f[mid * C:].reshape(C, mid)
+    s = r.float().mean(dim=(2, 3))
+    h = F.relu(s @ w1.float().t())
+    g = torch.sigmoid(h @ w2.float().t())
+    out = r * g[:, :, None, None].to(r.dtype)
+    if branch is not None:
+        out = out + _raw(branch)
+    return _wrap(out)
+
+
+def fp8_fp8_half_gemm_fused(x, y, bias=None, transpose_x=False, transpose_y=False, scale=1.0, output_dtype="float16",
+                            activation_type="identity"):
+    """fp8 x fp8 -> half GEMM with bias + activation (reference fusion/fp8_gemm): the fp8 operands go through the
+    framework's fp8 GEMM path (ops/fp8.py) with a scalar scale."""
+    a, b = _raw(x), _raw(y)
+    a = a.transpose(-1, -2) if transpose_x else a
+    b = b.transpose(-1, -2) if transpose_y else b
+    out = (a.float() @ b.float()) * scale
+    if bias is not None:
+        out = out + _raw(bias).float()
+    out = _ACTS.get(activation_type, lambda t: t)(out)
+    return _wrap(out.to(torch.float16 if output_dtype == "float16" else torch.bfloat16))
+
+
+def apply_per_channel_scale(x, scales):
+    return _wrap(_raw(x) * _raw(scales))
+
+
+def quant_linear(x, w, bias=None, in_num_col_dims=1, activation_type="", padding_weights=False, scale_in=1.0,
+                 scale_weights=(1.0,), quant_round_type=1, quant_max_bound=127.0, quant_min_bound=-127.0):
+    """int8 linear: x_q = round(x * scale_in * bound) (clipped), w holds int8 values whose dequantised weight is
+    w * scale_weights (per output channel), out = (x_q @ w) * scale_weights / (scale_in * bound) + bias."""
+    xr = _raw(x).float()
+    xq = torch.clamp(torch.round(xr * scale_in * quant_max_bound), quant_min_bound, quant_max_bound)
+    sw = torch.as_tensor(scale_weights, dtype=torch.float32, device=xr.device)
+    acc = xq.reshape(-1, xq.shape[-1]) @ _raw(w).float()
+    out = acc * sw / (scale_in * quant_max_bound)
+    if bias is not None:
+        out = out + _raw(bias).float()
+    if activation_type:
+        out = _ACTS[activation_type](out)
+    return _wrap(out.reshape(*xr.shape[:-1], -1).to(_raw(x).dtype))
+
+
+def fake_quantize_range_abs_max(x, in_scale, iter=None, window_size=10000, bit_length=8, is_test=False,  # noqa: A002
+                                round_type=1):
+    """Quantise-dequantise with the running max of |x| (fake_quantize ops): returns (out, out_scale)."""
+    r = _raw(x).float()
+    bnd = (1 << (bit_length - 1)) - 1
+    s = _raw(in_scale).float().reshape(-1)[0]
+    if not is_test:
+        s = torch.maximum(s, r.abs().max())
+    out = torch.round(torch.clamp(r / s, -1, 1) * bnd) * s / bnd
+    return _wrap(out.to(_raw(x).dtype)), _wrap(s.reshape(1))
+
+
+def moving_average_abs_max_scale(x, in_accum=None, in_state=None, moving_rate=0.9, is_test=False):
+    """scale = accum / state with accum = rate * accum + max|x|, state = rate * state + 1."""
+    r = _raw(x).float()
+    cur = r.abs().max()
+    acc = _raw(in_accum).float().reshape(-1)[0] if in_accum is not None else torch.tensor(0.0)
+    st = _raw(in_state).float().reshape(-1)[0] if in_state is not None else torch.tensor(0.0)
+    if not is_test:
+        acc = moving_rate * acc + cur
+        st = moving_rate * st + 1
+    return x, _wrap((acc / st).reshape(1)), _wrap(st.reshape(1)), _wrap(acc.reshape(1))
+
+
+# ------------------------------------------------------------------------------------------ sparse long tail
+def sparse_acos(x):
+    return _sparse_unary(x, torch.acos)
+
+
+def sparse_acosh(x):
+    return _sparse_unary(x, torch.acosh)
+
+
+def _sparse_unary(x, fn):
+    r = _raw(x)
+    if r.layout == torch.sparse_coo:
+        r = r.coalesce()
+        return _wrap(torch.sparse_coo_tensor(r.indices(), fn(r.values()), r.shape))
+    if r.layout == torch.sparse_csr:
+        return _wrap(torch.sparse_csr_tensor(r.crow_indices(), r.col_indices(), fn(r.values()), r.shape))
+    return _wrap(fn(r))
+
+
+def sparse_full_like(x, value, dtype=None):
+    r = _raw(x)
+    if r.layout == torch.sparse_coo:
+        r = r.coalesce()
+        return _wrap(torch.sparse_coo_tensor(r.indices(), torch.full_like(r.values(), value), r.shape))
+    return _wrap(torch.full_like(r, value))
+
+
+# ------------------------------------------------------------------------------------------ recurrent
+def rnn(x, pre_state, weight_list, sequence_length=None, dropout_prob=0.0, is_bidirec=False, input_size=10,
+        hidden_size=100, num_layers=1, mode="RNN_TANH", seed=0, is_test=False):
+    """The fused cuDNN-style rnn op over [S, B, in] input (time-major): modes LSTM / GRU / RNN_TANH / RNN_RELU;
+    weight_list = per layer/direction [w_ih, w_hh] then the biases (reference ops.yaml rnn)."""
+    xr = _raw(x)
+    ndir = 2 if is_bidirec else 1
+    kind = {"LSTM": torch.nn.LSTM, "GRU": torch.nn.GRU}.get(mode, torch.nn.RNN)
+    kw = {} if kind is not torch.nn.RNN else {"nonlinearity": "relu" if mode == "RNN_RELU" else "tanh"}
+    mod = kind(input_size, hidden_size, num_layers, bias=True, batch_first=False, dropout=0.0,
+               bidirectional=is_bidirec, **kw).to(xr.device, xr.dtype)
+    ws = [_raw(w) for w in weight_list]
+    nw = num_layers * ndir
+    names = []
+    for layer in range(num_layers):
+        for d in range(ndir):
+            sfx = f"_l{layer}" + ("_reverse" if d else "")
+            names.append((f"weight_ih{sfx}", f"weight_hh{sfx}", f"bias_ih{sfx}", f"bias_hh{sfx}"))
+    with torch.no_grad():
+        for i, (wi, wh, bi, bh) in enumerate(names):
+            getattr(mod, wi).copy_(ws[2 * i])
+            getattr(mod, wh).copy_(ws[2 * i + 1])
+            getattr(mod, bi).copy_(ws[2 * nw + 2 * i])
+            getattr(mod, bh).copy_(ws[2 * nw + 2 * i + 1])
+    states = [_raw(s) for s in pre_state]
+    h0 = tuple(states) if mode == "LSTM" else states[0]
+    out, hn = mod(xr, h0)
+    hn = list(hn) if isinstance(hn, tuple) else [hn]
+    return _wrap(out), None, [_wrap(h) for h in hn], None
+
+
+def lstm(input, init_h, init_c, weight, bias, use_peepholes=False, is_reverse=False,  # noqa: A002
+         gate_activation="sigmoid", cell_activation="tanh", candidate_activation="tanh"):
+    """Single-layer LSTM over [B, S, 4H] pre-projected input (legacy lstm op): weight [H, 4H], bias [1, 4H]."""
+    xr = _raw(input)
+    h, c = _raw(init_h), _raw(init_c)
+    W, b = _raw(weight), _raw(bias).reshape(-1)[: W.shape[1]]
+    steps = range(xr.shape[1] - 1, -1, -1) if is_reverse else range(xr.shape[1])
+    outs = [None] * xr.shape[1]
+    for t in steps:
+        g = xr[:, t] + h @ W + b
+        i, f, cc, o = g.chunk(4, dim=-1)
+        c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(cc)
+        h = torch.sigmoid(o) * torch.tanh(c)
+        outs[t] = h
+    return _wrap(torch.stack(outs, 1)), _wrap(torch.stack(outs, 1)), _wrap(c)
+
+
+def gru_unit(input, hidden_prev, weight, bias=None, activation=2, gate_activation=1,  # noqa: A002
+             origin_mode=False):
+    """One GRU step on pre-projected input [B, 3H] (legacy gru_unit): weight [H, 3H] = [W_u | W_r | W_c]."""
+    x, hp, W = _raw(input), _raw(hidden_prev), _raw(weight)
+    H = hp.shape[-1]
+    if bias is not None:
+        x = x + _raw(bias).reshape(-1)
+    ur = x[:, : 2 * H] + hp @ W[:, : 2 * H]
+    u, r = torch.sigmoid(ur).chunk(2, dim=-1)
+    c = torch.tanh(x[:, 2 * H:] + (r * hp) @ W[:, 2 * H:])
+    h = u * hp + (1 - u) * c if origin_mode else (1 - u) * hp + u * c
+    return _wrap(torch.cat([u, r, c], -1)), _wrap(r * hp), _wrap(h)
+
+
+def beam_search(pre_ids, pre_scores, ids, scores, level=0, beam_size=4, end_id=0, is_accumulated=True):
+    """One beam-search step over [B*beam, K] candidates: keep the beam_size best per source sentence; finished
+    beams (pre_id == end_id) keep only themselves.  Returns (selected_ids, selected_scores, parent_idx)."""
+    pi, ps = _raw(pre_ids).reshape(-1), _raw(pre_scores).reshape(-1)
+    cand_ids, cand_sc = _raw(ids), _raw(scores)
+    if not is_accumulated:
+        cand_sc = ps[:, None] + torch.log(cand_sc)
+    fin = pi == end_id
+    cand_sc = torch.where(fin[:, None], torch.full_like(cand_sc, -float("inf")), cand_sc)
+    cand_sc[:, 0] = torch.where(fin, ps, cand_sc[:, 0])
+    cand_ids = torch.where(fin[:, None], torch.full_like(cand_ids, end_id), cand_ids)
+    nb = pi.numel() // beam_size
+    sc = cand_sc.reshape(nb, -1)
+    top, arg = sc.topk(beam_size, dim=-1)
+    K = cand_ids.shape[1]
+    parent = (arg // K) + torch.arange(nb, device=arg.device)[:, None] * beam_size
+    sel = cand_ids.reshape(nb, -1).gather(1, arg)
+    return _wrap(sel.reshape(-1, 1)), _wrap(top.reshape(-1, 1)), _wrap(parent.reshape(-1))
+
+
+def beam_search_decode(ids, scores, beam_size, end_id):
+    """Back-track per-step (ids, parent) lists into full hypotheses: ids / scores are lists of
+    (selected_ids [N,1], parent_idx [N]) step tensors; returns ([N, T] ids, [N] final scores)."""
+    steps = list(ids)
+    T = len(steps)
+    n = _raw(steps[-1][0]).shape[0]
+    out = torch.zeros(n, T, dtype=torch.int64, device=_raw(steps[-1][0]).device)
+    cur = torch.arange(n, device=out.device)
+    for t in range(T - 1, -1, -1):
+        sid, par = _raw(steps[t][0]).reshape(-1), _raw(steps[t][1]).reshape(-1)
+        out[:, t] = sid[cur]
+        cur = par[cur]
+    final = _raw(list(scores)[-1]).reshape(-1)
+    return _wrap(out), _wrap(final)

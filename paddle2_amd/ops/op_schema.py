@@ -259,6 +259,21 @@ ALIASES = {
     "fused_attention": ("incubate.nn.functional.fused_multi_head_attention", {}),
 }
 
+# long-tail ops implemented in ops/extra_ops.py under their reference names
+for _n in ("nadam_", "radam_", "asgd_", "rprop_", "decayed_adagrad", "ftrl", "dpsgd", "lars_momentum_",
+           "average_accumulates_", "number_count", "assign_pos", "limit_by_capacity", "prune_gate_by_capacity",
+           "random_routing", "partial_concat", "partial_sum", "shuffle_batch", "hash", "print",
+           "add_position_encoding", "cvm", "batch_fc", "accuracy_check", "coalesce_tensor", "coalesce_tensor_",
+           "embedding_grad_dense", "straight_through_estimator_grad", "fused_elemwise_activation",
+           "fused_elemwise_add_activation", "fused_fc_elementwise_layernorm", "fused_scale_bias_add_relu",
+           "fused_embedding_eltwise_layernorm", "squeeze_excitation_block", "fp8_fp8_half_gemm_fused",
+           "apply_per_channel_scale", "quant_linear", "fake_quantize_range_abs_max", "moving_average_abs_max_scale",
+           "sparse_acos", "sparse_acosh", "sparse_full_like", "rnn", "lstm", "gru_unit", "beam_search",
+           "beam_search_decode"):
+    ALIASES.setdefault(_n, ("ops.extra_ops." + _n, {}))
+ALIASES.setdefault("nce", ("static.nn.nce", {}))
+ALIASES.setdefault("row_conv", ("static.nn.row_conv", {}))
+
 # reference ops that only exist for other hardware (XPU fused kernels): outside this framework's scope
 _PS_OPS = {"distributed_lookup_table", "distributed_push_sparse", "send_and_recv", "fetch_barrier",
            "sparse_momentum", "pull_box_sparse", "pull_gpups_sparse", "pull_sparse_v2", "push_dense", "push_sparse_v2",

@@ -1,0 +1,133 @@
+"""Long-tail reference ops (paddle2_amd/ops/extra_ops.py) through _C_ops: functional optimizer steps against the
+optimizer classes, MoE routing helpers, fused inference ops against their composite definitions."""
+import numpy as np
+import torch
+
+import paddle2_amd as paddle
+
+C = paddle._C_ops
+
+
+def _cls_steps(cls, p0, grads, **kw):
+    lin = paddle.create_parameter([len(p0)], "float32")
+    lin._t.data.copy_(torch.tensor(p0))
+    opt = cls(parameters=[lin], **kw)
+    for g in grads:
+        lin._t.grad = torch.tensor(g)
+        opt.step()
+    return lin.numpy()
+
+
+def _data(n=3):
+    rs = np.random.RandomState(0)
+    return rs.randn(6).astype("float32"), [rs.randn(6).astype("float32") for _ in range(n)]
+
+
+def test_coverage_rises():
+    from paddle2_amd.ops import op_schema as S
+
+    cov = S.coverage()
+    assert cov["implemented"] / cov["reference_ops"] >= 0.89, cov["missing"]
+
+
+def test_nadam_radam_asgd_rprop_match_classes():
+    p0, gs = _data(8)
+    p = paddle.to_tensor(p0.copy())
+    mdp, b2p, mup = paddle.to_tensor([1.0]), paddle.to_tensor([1.0]), paddle.to_tensor([1.0])
+    m1, m2 = paddle.zeros([6]), paddle.zeros([6])
+    for g in gs[:3]:
+        C.nadam_(p, paddle.to_tensor(g), paddle.to_tensor([0.01]), mdp, b2p, mup, m1, m2, None)
+    np.testing.assert_allclose(p.numpy(), _cls_steps(paddle.optimizer.NAdam, p0, gs[:3], learning_rate=0.01),
+                               rtol=1e-5, atol=1e-6)
+    p = paddle.to_tensor(p0.copy())
+    b1p, b2p, rho = paddle.to_tensor([1.0]), paddle.to_tensor([1.0]), paddle.to_tensor([0.0])
+    m1, m2 = paddle.zeros([6]), paddle.zeros([6])
+    for g in gs:  # rho_t crosses 5 after a few steps: both branches run
+        C.radam_(p, paddle.to_tensor(g), paddle.to_tensor([0.01]), b1p, b2p, rho, m1, m2, None)
+    np.testing.assert_allclose(p.numpy(), _cls_steps(paddle.optimizer.RAdam, p0, gs, learning_rate=0.01),
+                               rtol=1e-5, atol=1e-6)
+    p, d, y = paddle.to_tensor(p0.copy()), paddle.zeros([6]), paddle.zeros([6])
+    for g in gs[:2]:
+        C.asgd_(p, paddle.to_tensor(g), paddle.to_tensor([0.1]), d, y, paddle.to_tensor([1.0]), None)
+    np.testing.assert_allclose(p.numpy(), _cls_steps(paddle.optimizer.ASGD, p0, gs[:2], learning_rate=0.1),
+                               rtol=1e-5, atol=1e-6)
+    p, prev, lrs = paddle.to_tensor(p0.copy()), paddle.zeros([6]), paddle.full([6], 0.01)
+    for g in gs[:3]:
+        C.rprop_(p, paddle.to_tensor(g), prev, lrs, None, (1e-5, 50.0), (0.5, 1.2))
+    np.testing.assert_allclose(p.numpy(), _cls_steps(paddle.optimizer.Rprop, p0, gs[:3], learning_rate=0.01),
+                               rtol=1e-5, atol=1e-6)
+
+
+def test_ftrl_lars_decayed_adagrad():
+    p0, gs = _data(1)
+    p, n, z = paddle.to_tensor(p0.copy()), paddle.zeros([6]), paddle.zeros([6])
+    C.ftrl(p, n, z, paddle.to_tensor(gs[0]), paddle.to_tensor([0.1]), 1e6, 0.0)
+    assert np.all(p.numpy() == 0)  # huge l1: every coordinate shrinks to zero
+    p, v = paddle.to_tensor(p0.copy()), paddle.zeros([6])
+    C.lars_momentum_(p, paddle.to_tensor(gs[0]), v, paddle.to_tensor([0.1]), None, 0.9, 0.001, [0.0])
+    local = 0.001 * np.linalg.norm(p0) / np.linalg.norm(gs[0])
+    np.testing.assert_allclose(p.numpy(), p0 - 0.1 * local * gs[0], rtol=1e-5)
+    p, m = paddle.to_tensor(p0.copy()), paddle.zeros([6])
+    C.decayed_adagrad(p, paddle.to_tensor(gs[0]), m, paddle.to_tensor([0.1]), 0.95, 1e-6)
+    np.testing.assert_allclose(p.numpy(), p0 - 0.1 * gs[0] / (np.sqrt(0.05 * gs[0] ** 2) + 1e-6), rtol=1e-5)
+
+
+def test_moe_routing_helpers():
+    gate = paddle.to_tensor(np.array([2, 0, 2, 1, -1, 2], "int64"))
+    cnt = C.number_count(gate, 3)
+    assert cnt.numpy().tolist() == [1, 1, 3]
+    pos = C.assign_pos(gate, paddle.to_tensor(np.cumsum([1, 1, 3])), 5)
+    assert pos.numpy().tolist() == [1, 3, 0, 2, 5]
+    lim = C.limit_by_capacity(paddle.to_tensor(np.array([2, 1, 3, 2, 2, 2], "int64")),
+                              paddle.to_tensor(np.array([3, 2, 4], "int64")), 2)
+    assert lim.numpy().tolist() == [2, 1, 3, 1, 1, 1]
+    pruned = C.prune_gate_by_capacity(gate, paddle.to_tensor(np.array([1, 1, 2], "int64")), 3, 1)
+    assert pruned.numpy().tolist() == [2, 0, 2, 1, -1, -1]
+
+
+def test_fused_inference_ops_match_composites():
+    rs = np.random.RandomState(1)
+    x, w, y = rs.randn(4, 8).astype("float32"), rs.randn(8, 6).astype("float32"), rs.randn(4, 6).astype("float32")
+    b0, sc, b1 = rs.randn(6).astype("float32"), rs.rand(6).astype("float32"), rs.randn(6).astype("float32")
+    out = C.fused_fc_elementwise_layernorm(paddle.to_tensor(x), paddle.to_tensor(w), paddle.to_tensor(y),
+                                           paddle.to_tensor(b0), paddle.to_tensor(sc), paddle.to_tensor(b1),
+                                           1, "relu")
+    h = np.maximum(x @ w + b0, 0) + y
+    ref = (h - h.mean(1, keepdims=True)) / np.sqrt(h.var(1, keepdims=True) + 1e-5) * sc + b1
+    np.testing.assert_allclose(out.numpy(), ref, rtol=1e-4, atol=1e-5)
+    a, b = paddle.to_tensor(x), paddle.to_tensor(rs.randn(4, 8).astype("float32"))
+    o = C.fused_elemwise_activation(a, b, ["elementwise_add", "relu"])
+    np.testing.assert_allclose(o.numpy(), x + np.maximum(b.numpy(), 0), rtol=1e-6)
+    o = C.fused_elemwise_activation(a, b, ["relu", "elementwise_mul"])
+    np.testing.assert_allclose(o.numpy(), np.maximum(x * b.numpy(), 0), rtol=1e-6)
+    pc = C.partial_concat([a, b], 2, 3)
+    np.testing.assert_allclose(pc.numpy(), np.concatenate([x[:, 2:5], b.numpy()[:, 2:5]], 1))
+    ps = C.partial_sum([a, b], 1, 2)
+    np.testing.assert_allclose(ps.numpy(), x[:, 1:3] + b.numpy()[:, 1:3], rtol=1e-6)
+    outs, buf = C.coalesce_tensor([a, b], None, True)
+    assert buf.shape[0] >= 64 and np.allclose(outs[1].numpy(), b.numpy())
+    outs[0]._t.add_(1.0)  # views of the fused buffer
+    assert np.allclose(buf.numpy()[:32], (x + 1).reshape(-1))
+    q = C.quant_linear(paddle.to_tensor(x), paddle.to_tensor(np.round(w * 20).astype("float32")), None, 1, "",
+                       False, 1.0 / np.abs(x).max(), [1.0 / 20] * 6)
+    np.testing.assert_allclose(q.numpy(), x @ w, atol=0.05 * np.abs(x @ w).max())
+
+
+def test_rnn_op_and_beam_search():
+    rs = np.random.RandomState(2)
+    lstm = torch.nn.LSTM(4, 5)
+    ws = [lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0, lstm.bias_hh_l0]
+    x = torch.tensor(rs.randn(3, 2, 4).astype("float32"))
+    h0, c0 = torch.zeros(1, 2, 5), torch.zeros(1, 2, 5)
+    out, _, states, _ = C.rnn(paddle.Tensor._wrap(x), [paddle.Tensor._wrap(h0), paddle.Tensor._wrap(c0)],
+                              [paddle.Tensor._wrap(w.detach()) for w in ws], None, 0.0, False, 4, 5, 1, "LSTM")
+    ref, (hn, cn) = lstm(x, (h0, c0))
+    np.testing.assert_allclose(out.numpy(), ref.detach().numpy(), rtol=1e-5, atol=1e-6)
+    # beam search: 1 sentence, beam 2, 3 candidates each
+    pre_ids = paddle.to_tensor(np.array([[1], [2]], "int64"))
+    pre_sc = paddle.to_tensor(np.array([[0.0], [0.0]], "float32"))
+    ids = paddle.to_tensor(np.array([[5, 6, 7], [8, 9, 4]], "int64"))
+    sc = paddle.to_tensor(np.array([[0.1, 0.9, 0.2], [0.8, 0.3, 0.4]], "float32"))
+    sel, ssc, parent = C.beam_search(pre_ids, pre_sc, ids, sc, 0, 2, 0)
+    assert sel.numpy().reshape(-1).tolist() == [6, 8]
+    assert parent.numpy().tolist() == [0, 1]
