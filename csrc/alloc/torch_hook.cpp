@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <torch/csrc/cuda/CUDAPluggableAllocator.h>
 
+#include <algorithm>
 #include <functional>
 #include <map>
 #include <memory>
@@ -29,6 +30,8 @@ extern "C" {
 void* pd_alloc_malloc(size_t size, int device, hipStream_t stream);
 void pd_alloc_free(void* ptr, size_t size, int device, hipStream_t stream);
 void pd_alloc_record_stream(void* ptr, hipStream_t stream);
+void pd_alloc_stats(int device, uint64_t* out);
+void pd_alloc_reset_peak(int device);
 }
 
 namespace {
@@ -131,18 +134,64 @@ Router& router() {
 
 PoolId key(const c10::hip::MempoolId_t& id) { return {(unsigned long long)id.first, (unsigned long long)id.second}; }
 
+namespace P = torch::cuda::CUDAPluggableAllocator;
+
+// The pluggable allocator base throws from cacheInfo / getDeviceStats.  ATen's MIOpen convolution sizes its
+// workspace from cacheInfo (the largest block it could get): with the throwing base the workspace bound is 0 and
+// MIOpen falls back to its naive direct kernels (ResNet50 ran `naive_conv_ab_nonpacked_*` at ~200 ms per call);
+// torch.cuda.max_memory_allocated() raised.  Both answer from the native allocator here.
+struct PdTorchAllocator : P::CUDAPluggableAllocator {
+  using P::CUDAPluggableAllocator::CUDAPluggableAllocator;
+
+  void cacheInfo(c10::DeviceIndex device, size_t* largestBlock) override {
+    uint64_t st[13] = {};
+    pd_alloc_stats(device, st);
+    size_t free_b = 0, total_b = 0;
+    int prev = 0;
+    hipGetDevice(&prev);
+    if (prev != device) hipSetDevice(device);
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+    if (prev != device) hipSetDevice(prev);
+    // a workspace can come from the pool's free bytes or from new device memory
+    const size_t pool_free = st[1] > st[0] ? (size_t)(st[1] - st[0]) : 0;
+    *largestBlock = std::max(pool_free, free_b);
+  }
+
+  c10::CachingDeviceAllocator::DeviceStats getDeviceStats(c10::DeviceIndex device) override {
+    uint64_t st[13] = {};
+    pd_alloc_stats(device, st);
+    c10::CachingDeviceAllocator::DeviceStats d;
+    const size_t agg = static_cast<size_t>(c10::CachingDeviceAllocator::StatType::AGGREGATE);
+    auto set = [&](c10::CachingDeviceAllocator::StatArray& a, uint64_t cur, uint64_t peak) {
+      a[agg].current = (int64_t)cur;
+      a[agg].peak = (int64_t)peak;
+    };
+    set(d.allocated_bytes, st[0], st[2]);
+    set(d.active_bytes, st[0], st[2]);
+    set(d.requested_bytes, st[0], st[2]);
+    set(d.reserved_bytes, st[1], st[3]);
+    d.allocation[agg].allocated = (int64_t)st[4];
+    d.allocation[agg].freed = (int64_t)st[5];
+    d.allocation[agg].current = (int64_t)(st[4] - st[5]);
+    d.segment[agg].current = (int64_t)st[6];
+    d.num_alloc_retries = (int64_t)st[8];
+    return d;
+  }
+
+  void resetPeakStats(c10::DeviceIndex device) override { pd_alloc_reset_peak(device); }
+  void resetAccumulatedStats(c10::DeviceIndex) override {}
+};
+
 }  // namespace
 
 extern "C" {
 
 // 0 on success, 1 if the created allocator is not a CUDAPluggableAllocator (no hooks possible)
 int pd_alloc_install_torch() {
-  namespace P = torch::cuda::CUDAPluggableAllocator;
-  auto a = P::createCustomAllocator(
+  auto pa = std::make_shared<PdTorchAllocator>(
       [](size_t size, int device, hipStream_t stream) { return router().malloc(size, device, stream); },
       [](void* ptr, size_t size, int device, hipStream_t stream) { router().free(ptr, size, device, stream); });
-  auto pa = std::dynamic_pointer_cast<P::CUDAPluggableAllocator>(a);
-  if (!pa) return 1;
+  std::shared_ptr<c10::hip::HIPCachingAllocator::HIPAllocator> a = pa;
   pa->set_record_stream_fn([](void* ptr, hipStream_t stream) {
     {
       std::lock_guard<std::mutex> lk(router().mu);

@@ -222,3 +222,43 @@ def test_native_allocator_record_stream_fences_side_stream_reader():
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["bad"] == 0 and res["record_stream"] >= 20 and res["deferred"] >= 20, res
+
+
+@pytest.mark.gpu
+def test_native_allocator_torch_stats_and_miopen_workspace():
+    """torch.cuda memory stats answer from the native allocator, and MIOpen convolutions get a workspace bound
+    from its cacheInfo (a throwing cacheInfo bounded the workspace at 0 and MIOpen fell back to its naive direct
+    kernels, ~100x slower): a ResNet-sized bf16 NHWC 3x3 conv must run at GEMM speed."""
+    script = textwrap.dedent("""
+        import json, time, torch
+        import paddle2_amd  # noqa: F401  (installs the native allocator)
+        from paddle2_amd.device import allocator
+        torch.cuda.reset_peak_memory_stats()
+        x = torch.randn(256, 64, 56, 56, device="cuda", dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+        w = torch.randn(64, 64, 3, 3, device="cuda", dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+        x.requires_grad_(True)
+        w.requires_grad_(True)
+        for _ in range(3):
+            y = torch.nn.functional.conv2d(x, w, padding=1)
+            y.backward(torch.ones_like(y))
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(5):
+            y = torch.nn.functional.conv2d(x, w, padding=1)
+            y.backward(torch.ones_like(y))
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t) / 5 * 1e3
+        st = torch.cuda.memory_stats()
+        print(json.dumps({"active": allocator.is_active(), "ms": ms, "peak": torch.cuda.max_memory_allocated(),
+                          "reserved": torch.cuda.memory_reserved(), "cur": st.get("allocated_bytes.all.current", 0)}))
+    """)
+    env = dict(os.environ)
+    env.pop("FLAGS_use_native_allocator", None)
+    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    # fwd + dgrad + wgrad = 3 x 2*256*56*56*64*64*9 = 44 GFLOP: 30 ms is < 1.5 TF/s (naive kernels take seconds)
+    assert res["active"] and res["peak"] > 0 and res["reserved"] >= res["cur"] > 0, res
+    assert res["ms"] < 30.0, res
