@@ -49,6 +49,8 @@ def parse(argv=None):
     ap.add_argument("--sharding-stage", type=int, default=3, choices=[0, 1, 2, 3],
                     help="0 = no sharding wrapper (DEBUG: not the metric's code path)")
     ap.add_argument("--recompute", action="store_true")
+    ap.add_argument("--accumulate-steps", type=int, default=1,
+                    help="micro-batches per optimizer step (gradient accumulation into the fp32 main grads)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--gemm-autotune", default="auto", choices=["auto", "tune", "off"],
                     help="hipBLASLt solution cache (tuning/gemm_gfx950.csv): auto = use it if present")
@@ -128,13 +130,15 @@ def main():
     b, s = args.micro_batch, args.seq_len
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     # a fresh batch per step (pre-generated, outside the timed region); 8 x 4097 int64 = 262 KB each
+    acc = max(1, args.accumulate_steps)
     batches = [torch.randint(0, cfg.vocab_size, (b, s + 1), generator=gen, device=dev)
-               for _ in range(args.warmup + args.steps)]
+               for _ in range((args.warmup + args.steps) * acc)]
 
     def step(i):
-        ids = paddle.Tensor._wrap(batches[i])
-        loss = model(ids[:, :-1], labels=ids[:, 1:])
-        loss.backward()
+        for j in range(acc):
+            ids = paddle.Tensor._wrap(batches[i * acc + j])
+            loss = model(ids[:, :-1], labels=ids[:, 1:])
+            (loss / acc if acc > 1 else loss).backward()
         opt.step()
         opt.clear_grad()
         return loss
@@ -165,7 +169,7 @@ def main():
     elapsed = float(el.item())
     final_loss = float(loss)
 
-    tokens = b * s * args.steps * world
+    tokens = b * s * acc * args.steps * world
     tps = tokens / elapsed
     ms = elapsed / args.steps * 1000.0
     fpt = gpt_flops_per_token(cfg, s) if is_gpt else llama_flops_per_token(cfg, s)
@@ -187,7 +191,8 @@ def main():
             "dtype": "fp8(e4m3/e5m2)+bf16" if (is_gpt and args.fp8) else "bf16",
             "data": "synthetic (fresh uniform random token ids per step), random-init weights",
             "config": {"model": args.model if not args.layers else f"{args.model}-L{args.layers}(debug)",
-                       "global_batch": b * world, "seq_len": s, "micro_batch_per_gpu": b,
+                       "global_batch": b * acc * world, "seq_len": s, "micro_batch_per_gpu": b,
+                       "accumulate_steps": acc,
                        "parallelism": par, "layers": cfg.num_hidden_layers},
             "mfu_vs_2.5PF_dense": round(mfu, 4),
             "final_loss": round(final_loss, 4),

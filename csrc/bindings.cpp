@@ -17,6 +17,8 @@ extern "C" {
 int pd_norm_fwd(int, int, int, const void*, const void*, const void*, const void*, void*, void*, float*, float*, int,
                 int, float, void*);
 int pd_norm_bwd_blocks(int);
+int pd_bias_grad_chunks(int, int);
+int pd_bias_grad(int, int, const void*, float*, void*, int, int, void*);
 int pd_norm_bwd(int, int, int, const void*, const void*, const void*, const float*, const float*, const void*, void*,
                 float*, float*, void*, void*, int, int, int, void*);
 int pd_swiglu_fwd(int, const void*, const void*, void*, long, int, long, long, void*);
@@ -107,6 +109,10 @@ PYBIND11_MODULE(_C, m) {
           "norm_fwd");
   });
   m.def("norm_bwd_blocks", &pd_norm_bwd_blocks);
+  m.def("bias_grad_chunks", &pd_bias_grad_chunks);
+  m.def("bias_grad", [](int dt, int odt, uintptr_t dy, uintptr_t part, uintptr_t db, int M, int N, uintptr_t st) {
+    check(pd_bias_grad(dt, odt, P<const void*>(dy), P<float*>(part), P<void*>(db), M, N, P<void*>(st)), "bias_grad");
+  });
   m.def("norm_bwd", [](int ln, int dt, int wdt, uintptr_t dy, uintptr_t x, uintptr_t w, uintptr_t mean, uintptr_t rstd,
                        uintptr_t dres, uintptr_t dx, uintptr_t dw_part, uintptr_t db_part, uintptr_t dw, uintptr_t db,
                        int M, int N, int nblocks, uintptr_t st) {

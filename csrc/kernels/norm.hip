@@ -283,7 +283,74 @@ static void bwd_launch(const void* dy, const void* x, const void* w, const float
   if (db_part) colsum_kernel<WT><<<g2, 256, 0, st>>>(db_part, (WT*)db, P, N);
 }
 
+// Bias gradient db[n] = sum_m dy[m, n] (reference: the bias-grad reduction of fused_gemm_epilogue_grad /
+// matmul_with_bias backward).  Pass 1: workgroup (column block of 512, row chunk) — each wave streams every 4th
+// row of the chunk with one 16-B load per lane (a wave reads 1 KiB of a row: full cachelines), fp32 sums, one LDS
+// reduction over the 4 waves, fp32 partial row [chunk, N].  Pass 2: colsum_kernel over the chunks (fixed order:
+// deterministic).  Grid = ceil(N/512) x chunks with chunks sized so the launch is >= 1024 workgroups.
+template <typename T>
+__global__ __launch_bounds__(256) void bias_grad_part_kernel(const T* __restrict__ dy, float* __restrict__ part, int M,
+                                                             int N, int rows_per_chunk) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * 512 + lane * 8;
+  const int r0 = blockIdx.y * rows_per_chunk;
+  const int r1 = min(M, r0 + rows_per_chunk);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c0 < N) {
+    for (int r = r0 + w; r < r1; r += 4) {
+      float v[8];
+      if constexpr (sizeof(T) == 4) {
+        float a[4], b[4];
+        load_vec<T, 4>(dy + (long)r * N + c0, a);
+        load_vec<T, 4>(dy + (long)r * N + c0 + 4, b);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+      } else {
+        load_vec<T, 8>(dy + (long)r * N + c0, v);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[w][lane * 8 + j] = acc[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int c = blockIdx.x * 512 + i;
+    if (c < N) part[(long)blockIdx.y * N + c] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  }
+}
+
 }  // namespace pd
+
+// db [N] (dtype odt) = column sums of dy [M, N] (dtype dt); part: fp32 workspace of pd_bias_grad_chunks(M, N) * N.
+extern "C" int pd_bias_grad_chunks(int M, int N) {
+  const int cb = (N + 511) / 512;
+  int chunks = (1024 + cb - 1) / cb;
+  chunks = chunks < 1 ? 1 : chunks;
+  const int min_rows = 64;  // keep >= 16 rows per wave
+  if (chunks * min_rows > M) chunks = (M + min_rows - 1) / min_rows;
+  return chunks < 1 ? 1 : chunks;
+}
+
+extern "C" int pd_bias_grad(int dt, int odt, const void* dy, float* part, void* db, int M, int N, void* stream) {
+  using namespace pd;
+  if (N % 8 != 0 || M <= 0) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  const int chunks = pd_bias_grad_chunks(M, N);
+  const int rpc = (M + chunks - 1) / chunks;
+  dim3 g1((N + 511) / 512, chunks);
+  if (dt == kBF16) bias_grad_part_kernel<bf16><<<g1, 256, 0, st>>>((const bf16*)dy, part, M, N, rpc);
+  else if (dt == kF16) bias_grad_part_kernel<half16><<<g1, 256, 0, st>>>((const half16*)dy, part, M, N, rpc);
+  else if (dt == kF32) bias_grad_part_kernel<float><<<g1, 256, 0, st>>>((const float*)dy, part, M, N, rpc);
+  else return -2;
+  dim3 g2(ceil_div(N, 64));
+  if (odt == kBF16) colsum_kernel<bf16><<<g2, 256, 0, st>>>(part, (bf16*)db, chunks, N);
+  else if (odt == kF16) colsum_kernel<half16><<<g2, 256, 0, st>>>(part, (half16*)db, chunks, N);
+  else colsum_kernel<float><<<g2, 256, 0, st>>>(part, (float*)db, chunks, N);
+  return (int)hipGetLastError();
+}
 
 // C ABI entry points (bound in bindings.cpp). dtype codes: 0 f32, 1 bf16, 2 f16.
 // Weight dtype may be the activation dtype or f32.

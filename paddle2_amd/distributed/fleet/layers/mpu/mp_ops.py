@@ -168,7 +168,7 @@ class _ColumnLinear(torch.autograd.Function):
         dx = T.mm_t(dy2, w).view(ctx.xshape)
         work = _allreduce_(dx, ctx.group, async_op=True)
         dw = T.weight_grad(x2, dy2, ctx.gt) if ctx.needs_input_grad[1] else None
-        db = dy2.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        db = T.bias_grad(dy2) if ctx.has_b and ctx.needs_input_grad[2] else None
         if work is not None:
             work.wait()
         return dx, dw, db, None
@@ -196,7 +196,7 @@ class _SeqColumnLinear(torch.autograd.Function):
         dxf = T.mm_t(dy2, w).view(ctx.xfshape)
         dx, work = _reduce_scatter_dim0(dxf, ctx.group, async_op=True)
         dw = T.weight_grad(x2, dy2, ctx.gt) if ctx.needs_input_grad[1] else None
-        db = dy2.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        db = T.bias_grad(dy2) if ctx.has_b and ctx.needs_input_grad[2] else None
         if work is not None:
             work.wait()
         return dx, dw, db, None

@@ -439,8 +439,24 @@ class _LinearFn(torch.autograd.Function):
             else:
                 dw = torch.matmul(x2.t(), dy2)
         if has_b and ctx.needs_input_grad[2]:
-            db = dy2.sum(0)
+            db = bias_grad(dy2)
         return dx, dw, db
+
+
+def bias_grad(dy2):
+    """db = dy2.sum(0) for a [M, N] gradient: the native two-pass column sum (csrc/kernels/norm.hip
+    bias_grad_part_kernel + colsum, fp32 accumulation, deterministic) — torch's bf16 dim-0 reduce ran 5-30x slower
+    on the GPT-3 13B step (24.9 ms / 160 calls)."""
+    M, Nn = dy2.shape
+    if (N.use_native(dy2) and dy2.dtype in _DT and Nn % 8 == 0 and dy2.is_contiguous() and M > 0
+            and dy2.data_ptr() % 16 == 0):
+        C = N.native()
+        part = torch.empty(C.bias_grad_chunks(M, Nn) * Nn, dtype=torch.float32, device=dy2.device)
+        db = torch.empty(Nn, dtype=dy2.dtype, device=dy2.device)
+        C.bias_grad(_DT[dy2.dtype], _DT[dy2.dtype], dy2.data_ptr(), part.data_ptr(), db.data_ptr(), M, Nn,
+                    N.stream())
+        return db
+    return dy2.sum(0)
 
 
 def _pass_native(name, t, other=None):

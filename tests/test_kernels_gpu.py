@@ -298,3 +298,20 @@ def test_swiglu_linear_fused(M):
     _close(a, ac, 3e-2, 1e-2)
     _close(xg.grad, xc.grad, 5e-2, 1e-2)
     _close(wg.grad, wc.grad, 5e-1, 1e-2)
+
+
+@pytest.mark.parametrize("M,N,dt", [(4096, 15360, torch.bfloat16), (333, 520, torch.bfloat16), (64, 8, torch.float16),
+                                    (2048, 1000, torch.float32), (8192, 22016, torch.bfloat16)])
+def test_bias_grad_colsum_matches_fp32(M, N, dt):
+    """Native bias-gradient column sum (norm.hip bias_grad_part_kernel + colsum) vs an fp32 sum; ragged column
+    blocks and row chunks, and bitwise reproducible run to run."""
+    from paddle2_amd.ops import torch_ops as T
+
+    g = torch.Generator(device="cuda").manual_seed(7)
+    dy = torch.randn(M, N, generator=g, device="cuda").to(dt)
+    db = T.bias_grad(dy)
+    ref = dy.float().sum(0)
+    assert db.dtype == dt and db.shape == (N,)
+    tol = 1e-4 if dt == torch.float32 else 1e-2
+    assert (db.float() - ref).abs().max().item() <= tol * max(1.0, ref.abs().max().item())
+    assert torch.equal(db, T.bias_grad(dy))
