@@ -766,6 +766,10 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16*
         dkacc[dt] = mfma<F16>(cat4(lds_tr(qimg, oa), lds_tr(qimg, ob)), db, dkacc[dt]);
       }
     }
+    if (MODE == kDense && ex.dq_atomic == 3) {  // ablation: no dQ phase
+      step = step_next;
+      continue;
+    }
     // dS -> LDS image [32 q][BNK keys] (bf16) for dQ: row qi = (i&3) + 8(i>>2) + 4h, column lkey
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -792,6 +796,7 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16*
       // accumulator: row q = (i&3)+8(i>>2)+4h, col d = wv*32 + r -> two 128-B row segments per store.
       // Full 32-row tiles: non-temporal buffer stores, the per-row offset in the scalar soffset (no VALU);
       // the tile that crosses Sq keeps the checked stores
+      if (MODE == kDense && ex.dq_atomic == 2) continue;  // ablation: dQ computed, not stored
       if (q0 + BMQ <= Sq) {
         const int hqd4 = Hq * D * 4;
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(dQs + (long)q0 * Hq * D + (long)hq * D, BMQ * hqd4);
@@ -1057,6 +1062,12 @@ extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void
   fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm, seed,
              drop ? (unsigned)fminf(pdrop * 4294967296.f, 4294967040.f) : 0u, drop ? 1.f / (1.f - pdrop) : 1.f,
              atomic ? 1 : 0};
+  // bench-only ablation (scripts/bench_flash_bwd.py; results are WRONG): 2 = compute dQ but skip its stores,
+  // 3 = skip the whole dQ phase (dS image, barrier, dQ MFMAs, stores) — prices the dQ path in isolation
+  if (const char* e = getenv("PADDLE2_AMD_FA_DEBUG_DQ_ABLATE")) {
+    const int m = atoi(e);
+    if (atomic && (m == 2 || m == 3)) ex.dq_atomic = m;
+  }
 #define PD_BWD(DD, FF)                                                                                              \
   launch_bwd<DD, FF>(grid, st, q, k, v, dout, lse, delta, dqp, dk, dv, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, sdk, sdv, \
                      pslab, scale, causal, mode, drop, ex)
