@@ -141,6 +141,7 @@ struct Ext {
   unsigned drop_thresh; // DROP: element dropped iff hash < p * 2^32
   float drop_rscale;    // DROP: 1 / (1 - p)
   int dq_atomic;        // dense bwd: dQ partials fp32-atomically added into ONE zeroed slab (pslab = 0)
+  int wave_skip;        // fwd, causal: a wave skips the key tiles that lie wholly above its last row
 };
 
 // Counter-based dropout mask: a stateless 32-bit hash of (seed, batch*head, query, key), so the backward
@@ -335,7 +336,7 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
     const bool has_next = tn < ntiles;
     const char* kt = smem + buf * 2 * TILE;
     const char* vt = kt + TILE;
-    if (CAUSAL && NW == 8 && n0 > wave_last_key) {  // wave-uniform: only stage the next tile for the others
+    if (CAUSAL && (NW == 8 || ex.wave_skip) && n0 > wave_last_key) {  // wave-uniform: only stage the next tile for the others
       if (has_next) {
         gload(tn * BN);
         lstore(buf ^ 1);
@@ -1011,6 +1012,7 @@ extern "C" int pd_flash_fwd_ext(int dt, const void* q, const void* k, const void
   dim3 grid(nmb * Hq * B);
   fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm, seed,
              drop ? (unsigned)fminf(pdrop * 4294967296.f, 4294967040.f) : 0u, drop ? 1.f / (1.f - pdrop) : 1.f};
+  if (const char* e = getenv("PADDLE2_AMD_FA_FWD_WAVE_SKIP")) ex.wave_skip = atoi(e) != 0;
 #define PD_FWD(DD, FF) \
   launch_fwd<DD, FF>(grid, st, q, k, v, o, lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, causal, mode, drop, ex, nw)
   const bool f16 = dt == kF16;

@@ -643,3 +643,249 @@ def beam_search_decode(ids, scores, beam_size, end_id):
         cur = par[cur]
     final = _raw(list(scores)[-1]).reshape(-1)
     return _wrap(out), _wrap(final)
+
+
+# ------------------------------------------------------------------------------------------ detection / sequence
+def ctc_align(input, input_length=None, blank=0, merge_repeated=True, padding_value=0):  # noqa: A002
+    """CTC greedy-decode alignment: merge repeats, drop blanks, left-pack each row (padded with padding_value);
+    returns (output [B, T], output_length [B, 1])."""
+    x = _raw(input).long()
+    B, T = x.shape[0], x.shape[1]
+    lens = _raw(input_length).reshape(-1).long() if input_length is not None else torch.full((B,), T)
+    out = torch.full((B, T), padding_value, dtype=x.dtype, device=x.device)
+    olen = torch.zeros(B, 1, dtype=torch.int64, device=x.device)
+    for b in range(B):
+        prev, k = None, 0
+        for t in range(int(lens[b])):
+            tok = int(x[b, t])
+            if tok != blank and not (merge_repeated and tok == prev):
+                out[b, k] = tok
+                k += 1
+            prev = tok
+        olen[b, 0] = k
+    return _wrap(out), _wrap(olen)
+
+
+def crf_decoding(emission, transition, label=None, length=None):
+    """Viterbi decode of a linear-chain CRF: transition [(n+2), n] with the start / stop rows first (reference
+    crf_decoding op layout); emission [B, T, n]; returns the best path [B, T] (or, with label, 1 where the path
+    matches the label)."""
+    e = _raw(emission).float()
+    tr = _raw(transition).float()
+    start, stop, trans = tr[0], tr[1], tr[2:]
+    B, T, n = e.shape
+    lens = _raw(length).reshape(-1).long() if length is not None else torch.full((B,), T, dtype=torch.long)
+    path = torch.zeros(B, T, dtype=torch.int64, device=e.device)
+    for b in range(B):
+        L = int(lens[b])
+        if L == 0:
+            continue
+        score = start + e[b, 0]
+        back = []
+        for t in range(1, L):
+            cand = score[:, None] + trans
+            score, idx = cand.max(0)
+            score = score + e[b, t]
+            back.append(idx)
+        score = score + stop
+        best = int(score.argmax())
+        path[b, L - 1] = best
+        for t in range(L - 2, -1, -1):
+            best = int(back[t][best])
+            path[b, t] = best
+    if label is not None:
+        return _wrap((path == _raw(label).reshape(B, T).long()).to(torch.int64))
+    return _wrap(path)
+
+
+def chunk_eval(inference, label, chunk_scheme="IOB", num_chunk_types=1, excluded_chunk_types=(), seq_length=None):
+    """Chunk precision / recall / F1 for IOB / IOE / IOBES tagging (reference chunk_eval op): tag = type * K + pos."""
+    scheme = {"IOB": ("B", "I"), "IOE": ("I", "E"), "IOBES": ("B", "I", "E", "S"), "plain": ("I",)}[chunk_scheme]
+    K = len(scheme)
+
+    def chunks(seq):
+        out, start, ctype, prev_end = set(), None, None, False
+        for i, tag in enumerate(list(seq) + [-1]):
+            if tag < 0 or tag >= num_chunk_types * K:
+                if start is not None:
+                    out.add((start, i - 1, ctype))
+                start = None
+                continue
+            t, pos = tag // K, scheme[tag % K]
+            begins = pos in ("B", "S") or start is None or t != ctype or (chunk_scheme == "IOE" and prev_end)
+            if begins:
+                if start is not None:
+                    out.add((start, i - 1, ctype))
+                start, ctype = i, t
+            prev_end = pos in ("E", "S")
+            if pos in ("E", "S"):
+                out.add((start, i, ctype))
+                start = None
+        return {c for c in out if c[2] not in excluded_chunk_types}
+
+    inf, lab = _raw(inference).reshape(_raw(inference).shape[0], -1), _raw(label).reshape(_raw(label).shape[0], -1)
+    lens = _raw(seq_length).reshape(-1).tolist() if seq_length is not None else [inf.shape[1]] * inf.shape[0]
+    ni = nl = nc = 0
+    for b in range(inf.shape[0]):
+        ci, cl = chunks(inf[b, : int(lens[b])].tolist()), chunks(lab[b, : int(lens[b])].tolist())
+        ni, nl, nc = ni + len(ci), nl + len(cl), nc + len(ci & cl)
+    p = nc / ni if ni else 0.0
+    r = nc / nl if nl else 0.0
+    f = 2 * p * r / (p + r) if nc else 0.0
+    t = lambda v, dt=torch.float32: _wrap(torch.tensor([v], dtype=dt))  # noqa: E731
+    return t(p), t(r), t(f), t(ni, torch.int64), t(nl, torch.int64), t(nc, torch.int64)
+
+
+def auc(x, label, stat_pos, stat_neg, ins_tag_weight=None, curve="ROC", num_thresholds=4095, slide_steps=1):
+    """Streaming AUC (reference auc op): bucket the positive-class probability into num_thresholds+1 bins,
+    accumulate positive / negative histograms into stat_pos / stat_neg, return (auc, stat_pos, stat_neg)."""
+    p = _raw(x)
+    p = p[:, -1] if p.dim() == 2 else p.reshape(-1)
+    y = _raw(label).reshape(-1).long()
+    bins = torch.clamp((p.float() * num_thresholds).long(), 0, num_thresholds)
+    sp, sn = _raw(stat_pos).reshape(-1), _raw(stat_neg).reshape(-1)
+    sp += torch.bincount(bins[y == 1], minlength=num_thresholds + 1)[: sp.numel()].to(sp.dtype)
+    sn += torch.bincount(bins[y == 0], minlength=num_thresholds + 1)[: sn.numel()].to(sn.dtype)
+    tp = torch.flip(sp.double(), [0]).cumsum(0)
+    fp = torch.flip(sn.double(), [0]).cumsum(0)
+    tpr = torch.cat([torch.zeros(1, dtype=torch.float64), tp / max(tp[-1].item(), 1)])
+    fpr = torch.cat([torch.zeros(1, dtype=torch.float64), fp / max(fp[-1].item(), 1)])
+    area = torch.trapz(tpr, fpr).item() if tp[-1] > 0 and fp[-1] > 0 else 0.0
+    return _wrap(torch.tensor([area], dtype=torch.float64)), stat_pos, stat_neg
+
+
+def bipartite_match(dist_matrix, match_type="bipartite", dist_threshold=0.5):
+    """Greedy bipartite matching of a [R, C] similarity matrix (reference bipartite_match op): repeatedly take the
+    global max; with match_type 'per_prediction' unmatched columns take their best row above dist_threshold.
+    Returns (col -> row index [1, C] or -1, matched distance [1, C])."""
+    d = _raw(dist_matrix).float().clone()
+    R, Cn = d.shape
+    idx = torch.full((Cn,), -1, dtype=torch.int64)
+    dist = torch.zeros(Cn)
+    work = d.clone()
+    for _ in range(min(R, Cn)):
+        v, flat = work.reshape(-1).max(0)
+        if v.item() <= 0 and not torch.isfinite(v):
+            break
+        r, c = divmod(int(flat), Cn)
+        if work[r, c] == -float("inf"):
+            break
+        idx[c], dist[c] = r, d[r, c]
+        work[r, :] = -float("inf")
+        work[:, c] = -float("inf")
+    if match_type == "per_prediction":
+        for c in range(Cn):
+            if idx[c] < 0:
+                v, r = d[:, c].max(0)
+                if v >= dist_threshold:
+                    idx[c], dist[c] = int(r), v
+    return _wrap(idx[None]), _wrap(dist[None])
+
+
+def anchor_generator(input, anchor_sizes=(64, 128, 256, 512), aspect_ratios=(0.5, 1.0, 2.0),  # noqa: A002
+                     variances=(0.1, 0.1, 0.2, 0.2), stride=(16.0, 16.0), offset=0.5):
+    """Faster-RCNN anchors over an NCHW feature map: (anchors [H, W, A, 4] in x1y1x2y2, variances like it)."""
+    H, W = _raw(input).shape[2], _raw(input).shape[3]
+    sw, sh = stride
+    base = []
+    for r in aspect_ratios:
+        for s in anchor_sizes:
+            area = sw * sh
+            bw = round((area / r) ** 0.5)
+            bh = round(bw * r)
+            scale_w, scale_h = s / sw, s / sh
+            aw, ah = scale_w * bw, scale_h * bh
+            base.append((-(aw - 1) / 2, -(ah - 1) / 2, (aw - 1) / 2, (ah - 1) / 2))
+    base = torch.tensor(base)
+    cx = (torch.arange(W) * sw + offset * (sw - 1)).float()
+    cy = (torch.arange(H) * sh + offset * (sh - 1)).float()
+    ctr = torch.stack(torch.meshgrid(cy, cx, indexing="ij"), -1)  # [H, W, 2] (y, x)
+    shift = torch.stack([ctr[..., 1], ctr[..., 0], ctr[..., 1], ctr[..., 0]], -1)[:, :, None, :]
+    anchors = shift + base[None, None]
+    var = torch.tensor(variances, dtype=torch.float32).expand_as(anchors).clone()
+    return _wrap(anchors), _wrap(var)
+
+
+def _nms(boxes, scores, thr, normalized=True):
+    order = scores.argsort(descending=True)
+    keep = []
+    off = 0.0 if normalized else 1.0
+    area = (boxes[:, 2] - boxes[:, 0] + off) * (boxes[:, 3] - boxes[:, 1] + off)
+    while order.numel():
+        i = int(order[0])
+        keep.append(i)
+        if order.numel() == 1:
+            break
+        rest = order[1:]
+        xx1 = torch.maximum(boxes[i, 0], boxes[rest, 0])
+        yy1 = torch.maximum(boxes[i, 1], boxes[rest, 1])
+        xx2 = torch.minimum(boxes[i, 2], boxes[rest, 2])
+        yy2 = torch.minimum(boxes[i, 3], boxes[rest, 3])
+        inter = (xx2 - xx1 + off).clamp(min=0) * (yy2 - yy1 + off).clamp(min=0)
+        iou = inter / (area[i] + area[rest] - inter)
+        order = rest[iou <= thr]
+    return torch.tensor(keep, dtype=torch.int64)
+
+
+def multiclass_nms3(bboxes, scores, rois_num=None, score_threshold=0.05, nms_top_k=1000, keep_top_k=100,
+                    nms_threshold=0.3, normalized=True, nms_eta=1.0, background_label=0):
+    """Per-class NMS then a cross-class keep_top_k (reference multiclass_nms3): bboxes [N, M, 4], scores
+    [N, C, M]; returns (out [K, 6] = label, score, box; index [K, 1]; per-image counts [N])."""
+    bx, sc = _raw(bboxes).float(), _raw(scores).float()
+    outs, idxs, counts = [], [], []
+    M = bx.shape[1]
+    for n in range(bx.shape[0]):
+        dets = []
+        for c in range(sc.shape[1]):
+            if c == background_label:
+                continue
+            s = sc[n, c]
+            cand = (s > score_threshold).nonzero().reshape(-1)
+            if cand.numel() == 0:
+                continue
+            if nms_top_k > -1 and cand.numel() > nms_top_k:
+                cand = cand[s[cand].argsort(descending=True)[:nms_top_k]]
+            keep = cand[_nms(bx[n, cand], s[cand], nms_threshold, normalized)]
+            for k in keep.tolist():
+                dets.append((float(s[k]), c, k))
+        dets.sort(key=lambda t: -t[0])
+        if keep_top_k > -1:
+            dets = dets[:keep_top_k]
+        for score, c, k in dets:
+            outs.append([float(c), score] + bx[n, k].tolist())
+            idxs.append([n * M + k])
+        counts.append(len(dets))
+    out = torch.tensor(outs, dtype=torch.float32).reshape(-1, 6)
+    return _wrap(out), _wrap(torch.tensor(idxs, dtype=torch.int64).reshape(-1, 1)), \
+        _wrap(torch.tensor(counts, dtype=torch.int32))
+
+
+def multiclass_nms(bboxes, scores, score_threshold=0.05, nms_top_k=1000, keep_top_k=100, nms_threshold=0.3,
+                   normalized=True, nms_eta=1.0, background_label=0):
+    return multiclass_nms3(bboxes, scores, None, score_threshold, nms_top_k, keep_top_k, nms_threshold, normalized,
+                           nms_eta, background_label)[0]
+
+
+def im2sequence(x, y=None, kernels=(1, 1), strides=(1, 1), paddings=(0, 0, 0, 0), out_stride=(1, 1)):
+    """Image patches as a sequence (reference im2sequence): [N, C, H, W] -> [N * oh * ow, C * kh * kw]."""
+    r = _raw(x)
+    pt, pl, pb, pr = paddings
+    r = F.pad(r, (pl, pr, pt, pb))
+    cols = F.unfold(r, tuple(kernels), stride=tuple(strides))  # [N, C*kh*kw, L]
+    return _wrap(cols.transpose(1, 2).reshape(-1, cols.shape[1]))
+
+
+def correlation(input1, input2, pad_size=4, kernel_size=1, max_displacement=4, stride1=1, stride2=1,
+                corr_type_multiply=1):
+    """FlowNet correlation: for every displacement (dy, dx) in [-d, d]^2 (step stride2), the channel-mean of
+    input1 * shifted input2 -> [N, (2d/s2+1)^2, H, W] (kernel_size 1, stride1 1)."""
+    a, b = _raw(input1).float(), _raw(input2).float()
+    N, C, H, W = a.shape
+    bp = F.pad(b, (pad_size, pad_size, pad_size, pad_size))
+    outs = []
+    rng = range(-max_displacement, max_displacement + 1, stride2)
+    for dy in rng:
+        for dx in rng:
+            sh = bp[:, :, pad_size + dy: pad_size + dy + H, pad_size + dx: pad_size + dx + W]
+            outs.append((a * sh).sum(1) / C)
+    return _wrap(torch.stack(outs, 1).to(_raw(input1).dtype))

@@ -269,10 +269,12 @@ for _n in ("nadam_", "radam_", "asgd_", "rprop_", "decayed_adagrad", "ftrl", "dp
            "fused_embedding_eltwise_layernorm", "squeeze_excitation_block", "fp8_fp8_half_gemm_fused",
            "apply_per_channel_scale", "quant_linear", "fake_quantize_range_abs_max", "moving_average_abs_max_scale",
            "sparse_acos", "sparse_acosh", "sparse_full_like", "rnn", "lstm", "gru_unit", "beam_search",
-           "beam_search_decode"):
+           "beam_search_decode", "ctc_align", "crf_decoding", "chunk_eval", "auc", "bipartite_match",
+           "anchor_generator", "multiclass_nms", "multiclass_nms3", "im2sequence", "correlation"):
     ALIASES.setdefault(_n, ("ops.extra_ops." + _n, {}))
 ALIASES.setdefault("nce", ("static.nn.nce", {}))
 ALIASES.setdefault("row_conv", ("static.nn.row_conv", {}))
+ALIASES.setdefault("graph_sample_neighbors", ("geometric.sample_neighbors", {}))
 
 # reference ops that only exist for other hardware (XPU fused kernels): outside this framework's scope
 _PS_OPS = {"distributed_lookup_table", "distributed_push_sparse", "send_and_recv", "fetch_barrier",

@@ -41,19 +41,22 @@ def main():
         v = torch.randn(B, S, HK, D, device=dev, dtype=torch.bfloat16, generator=g)
         flops = 4 * B * H * D * S * S * (0.5 if causal else 1.0)
         outs = {}
-        for w in ("4", "8"):
+        for w, skip in (("4", "0"), ("4", "1"), ("8", "0")):
             os.environ["PADDLE2_AMD_FA_FWD_WAVES"] = w
+            os.environ["PADDLE2_AMD_FA_FWD_WAVE_SKIP"] = skip
             fn = lambda: T.flash_attention(q, k, v, causal)  # noqa: E731
             ms = timeit(fn)
             o, lse = fn()[:2]
-            outs[w] = (o.clone(), lse.clone())
-            print(json.dumps({"case": name, "waves": int(w), "fwd_ms": round(ms, 4),
+            outs[(w, skip)] = (o.clone(), lse.clone())
+            print(json.dumps({"case": name, "waves": int(w), "wave_skip": int(skip), "fwd_ms": round(ms, 4),
                               "TFs": round(flops / ms / 1e9, 1)}), flush=True)
-        same_o = torch.equal(outs["4"][0], outs["8"][0])
-        same_l = torch.equal(outs["4"][1], outs["8"][1])
-        print(json.dumps({"case": name, "bitwise_equal_o": same_o, "bitwise_equal_lse": same_l}), flush=True)
-        if not (same_o and same_l):
-            sys.exit(1)
+        base = outs[("4", "0")]
+        for key, (o, lse) in outs.items():
+            same = torch.equal(base[0], o) and torch.equal(base[1], lse)
+            if not same:
+                print(json.dumps({"case": name, "variant": key, "bitwise_equal": False}), flush=True)
+                sys.exit(1)
+        print(json.dumps({"case": name, "bitwise_equal_all": True}), flush=True)
 
 
 if __name__ == "__main__":

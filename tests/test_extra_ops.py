@@ -131,3 +131,50 @@ def test_rnn_op_and_beam_search():
     sel, ssc, parent = C.beam_search(pre_ids, pre_sc, ids, sc, 0, 2, 0)
     assert sel.numpy().reshape(-1).tolist() == [6, 8]
     assert parent.numpy().tolist() == [0, 1]
+
+
+def test_sequence_and_detection_ops():
+    out, olen = C.ctc_align(paddle.to_tensor(np.array([[0, 1, 1, 0, 2, 2, 3, 0]], "int64")),
+                            paddle.to_tensor(np.array([8], "int64")), 0)
+    assert olen.numpy().tolist() == [[3]] and out.numpy()[0, :3].tolist() == [1, 2, 3]
+    # CRF Viterbi vs brute force over all 3^4 paths
+    rs = np.random.RandomState(3)
+    em, tr = rs.randn(1, 4, 3).astype("float32"), rs.randn(5, 3).astype("float32")
+    path = C.crf_decoding(paddle.to_tensor(em), paddle.to_tensor(tr)).numpy()[0].tolist()
+    import itertools
+
+    def score(p):
+        s = tr[0, p[0]] + em[0, 0, p[0]] + tr[1, p[-1]]
+        for t in range(1, 4):
+            s += tr[2 + p[t - 1], p[t]] + em[0, t, p[t]]
+        return s
+
+    best = max(itertools.product(range(3), repeat=4), key=score)
+    assert path == list(best)
+    # IOB chunks: tags type*2 + (0=B, 1=I); label has chunks (0,1,t0) and (3,3,t1)
+    lab = np.array([[0, 1, 4, 2, 4]], "int64")
+    inf = np.array([[0, 1, 4, 2, 3]], "int64")
+    p, r, f, ni, nl, nc = C.chunk_eval(paddle.to_tensor(inf), paddle.to_tensor(lab), "IOB", 2)
+    assert int(nl.numpy()[0]) == 2 and int(ni.numpy()[0]) == 2 and int(nc.numpy()[0]) == 1
+    # AUC of a perfect ranking
+    sp, sn = paddle.zeros([4096], "int64"), paddle.zeros([4096], "int64")
+    a, _, _ = C.auc(paddle.to_tensor(np.array([0.9, 0.8, 0.2, 0.1], "float32")),
+                    paddle.to_tensor(np.array([1, 1, 0, 0], "int64")), sp, sn)
+    assert abs(float(a.numpy()[0]) - 1.0) < 1e-6
+    idx, dist = C.bipartite_match(paddle.to_tensor(np.array([[0.9, 0.2], [0.8, 0.7]], "float32")))
+    assert idx.numpy().tolist() == [[0, 1]]
+    anchors, var = C.anchor_generator(paddle.zeros([1, 8, 2, 3]), [32.0], [1.0], [0.1, 0.1, 0.2, 0.2], [16.0, 16.0])
+    assert list(anchors.shape) == [2, 3, 1, 4]
+    a0 = anchors.numpy()[0, 0, 0]
+    assert abs((a0[2] - a0[0]) - 31.0) < 1e-4  # 32-px square anchor (x2 - x1 = w - 1)
+    boxes = np.array([[[0, 0, 10, 10], [1, 1, 10, 10], [20, 20, 30, 30]]], "float32")
+    scores = np.array([[[0.0, 0.0, 0.0], [0.9, 0.8, 0.7]]], "float32")
+    out, index, cnt = C.multiclass_nms3(paddle.to_tensor(boxes), paddle.to_tensor(scores), None, 0.1, 10, 10, 0.5,
+                                        False)
+    assert cnt.numpy().tolist() == [2] and out.numpy()[:, 1].tolist() == [np.float32(0.9), np.float32(0.7)]
+    seq = C.im2sequence(paddle.ones([2, 3, 4, 4]), None, [2, 2], [2, 2])
+    assert list(seq.shape) == [8, 12]
+    x = paddle.to_tensor(rs.randn(1, 2, 5, 5).astype("float32"))
+    corr = C.correlation(x, x, 1, 1, 1)
+    assert list(corr.shape) == [1, 9, 5, 5]
+    np.testing.assert_allclose(corr.numpy()[0, 4], (x.numpy()[0] ** 2).mean(0), rtol=1e-5)
