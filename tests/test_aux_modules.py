@@ -206,14 +206,8 @@ def test_hub_local(tmp_path):
         paddle.hub.load("someone/repo:main", "x", source="github")
 
 
-def test_onnx_export_requires_onnx(tmp_path):
-    try:
-        import onnx  # noqa: F401
-    except ImportError:
-        with pytest.raises(ImportError):
-            paddle.onnx.export(paddle.nn.Linear(2, 2), str(tmp_path / "m"),
-                               input_spec=[paddle.static.InputSpec([None, 2], "float32")])
-        return
+def test_onnx_export_without_onnx_package(tmp_path):
+    """The exporter writes ModelProto bytes itself (onnx/exporter.py): no onnx package needed."""
     paddle.onnx.export(paddle.nn.Linear(2, 2), str(tmp_path / "m"),
                        input_spec=[paddle.static.InputSpec([None, 2], "float32")])
     assert os.path.exists(tmp_path / "m.onnx")
