@@ -141,8 +141,7 @@ class GPTAttention(nn.Layer):
         else:
             b, s = qkv.shape[0], qkv.shape[1]
         qkv = qkv.reshape(b, s, 3 * self.nh, self.d)
-        q, k, v = qkv[:, :, :self.nh], qkv[:, :, self.nh:2 * self.nh], qkv[:, :, 2 * self.nh:]
-        o, _ = T.flash_attention(q, k, v, causal=True)
+        o = T.qkv_attention(qkv, self.nh, self.nh, causal=True)
         o = o.reshape(b, s, self.nh * self.d)
         if cfg.sequence_parallel and cfg.tensor_parallel_degree > 1:
             o = o.transpose(0, 1).contiguous()

@@ -95,3 +95,18 @@ def test_fwd_8wave_matches_4wave_and_fp32(monkeypatch, causal, Sq, Sk, Hq, Hk):
     assert torch.equal(outs["4"][0], outs["8"][0]) and torch.equal(outs["4"][1], outs["8"][1])
     orf, _ = T.flash_attention(q.float(), k.float(), v.float(), causal)
     assert _err(outs["8"][0], orf) < 2e-2
+
+
+@pytest.mark.parametrize("nh,nkv", [(4, 4), (8, 2)])
+def test_qkv_packed_attention_matches_sliced(nh, nkv):
+    """qkv_attention (GPT path: dQ/dK/dV written straight into one dQKV buffer) equals flash_attention on the
+    sliced views, forward and gradients, bit for bit (same kernels, same accumulation)."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    qkv = torch.randn(2, 300, nh + 2 * nkv, 128, generator=g, device=DEV).to(torch.bfloat16).requires_grad_()
+    o = T.qkv_attention(qkv, nh, nkv, causal=True)
+    go = torch.randn(o.shape, generator=g, device=DEV).to(torch.bfloat16)
+    o.backward(go)
+    ref_in = qkv.detach().clone().requires_grad_()
+    o2, _ = T.flash_attention(ref_in[:, :, :nh], ref_in[:, :, nh:nh + nkv], ref_in[:, :, nh + nkv:], True)
+    o2.backward(go)
+    assert torch.equal(o, o2) and torch.equal(qkv.grad, ref_in.grad)
