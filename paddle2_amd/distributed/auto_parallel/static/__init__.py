@@ -4,3 +4,4 @@ placement planner (reference python/paddle/distributed/auto_parallel/static/).""
 from .completion import Completer, DistAttr, DistContext, attr_from_placements  # noqa: F401
 from .cost_model import ClusterSpec, CostModel, Planner, reshard_steps  # noqa: F401
 from .partitioner import DistributedProgram, parallelize_program  # noqa: F401
+from .engine import Engine  # noqa: F401

@@ -96,3 +96,12 @@ def test_partitioned_tp_and_dp_match_serial():
         # DP forward: the loss mean over the sharded batch is reduced once
         assert r["dp"]["fwd_comm"] == ["all_reduce"], r["dp"]
         assert "grad_all_reduce" in r["dp"]["all_comm"]
+
+
+def test_engine_trains_tp_plan_like_serial():
+    res = run_workers("static_autoparallel_worker.py", 2)
+    for r in res:
+        e = r["engine"]
+        np.testing.assert_allclose(e["losses"], e["ref"], rtol=1e-5, atol=1e-6)
+        assert e["w1_local_shape"] == [8, 8]      # fc1.weight [8, 16] column-sharded over 2 ranks
+        assert e["pred_shape"] == []               # the MLP's forward returns the scalar loss-like mean

@@ -87,4 +87,30 @@ check("tp", {net.fc1.weight: [dist.Shard(1)], net.fc1.bias: [dist.Shard(0)], net
       {"fc1.weight": 1, "fc1.bias": 0, "fc2.weight": 0})
 # data parallel: the batch is sharded, every parameter replicated
 check("dp", {"x": [dist.Shard(0)]}, {})
+
+
+# Engine: the same MLP trained 3 steps under the TP plan (parameters hold local shards, user's SGD steps them)
+from paddle2_amd.distributed.auto_parallel.static import Engine  # noqa: E402
+
+paddle.seed(0)
+net2 = MLP()
+ref2 = MLP()
+ref2.set_state_dict(net2.state_dict())
+eng = Engine(net2, loss=lambda out, label: out, optimizer=paddle.optimizer.SGD(0.1, parameters=net2.parameters()), mesh=mesh,
+             annotations={net2.fc1.weight: [dist.Shard(1)], net2.fc1.bias: [dist.Shard(0)],
+                          net2.fc2.weight: [dist.Shard(0)]})
+opt_ref = paddle.optimizer.SGD(0.1, parameters=ref2.parameters())
+losses, ref_losses = [], []
+dummy = np.zeros([4], "float32")
+for i in range(3):
+    xi = np.random.RandomState(10 + i).randn(4, 8).astype("float32")
+    losses.append(float(eng.run([xi], [dummy], "train").numpy()))
+    lr_ = ref2(paddle.to_tensor(xi))
+    lr_.backward()
+    opt_ref.step()
+    opt_ref.clear_grad()
+    ref_losses.append(float(lr_.numpy()))
+out["engine"] = {"losses": losses, "ref": ref_losses,
+                 "w1_local_shape": list(net2.fc1.weight._t.shape),
+                 "pred_shape": list(eng.run([np.ones([4, 8], "float32")], None, "predict").shape)}
 write_result(out)
