@@ -126,10 +126,11 @@ def _try_bind(host, port):
 def _worker_env(args, local_rank, node_rank, nnodes, world, offset, eps, devices, torch_master):
     grank = offset + local_rank
     env = dict(os.environ)
-    dev = devices[local_rank] if devices else str(local_rank)
+    # more ranks than devices (e.g. gloo ranks sharing one GPU): ranks wrap around the device list
+    dev = devices[local_rank % len(devices)] if devices else str(local_rank)
     env.update({
         "RANK": str(grank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(local_rank),
-        "LOCAL_WORLD_SIZE": str(len(devices) if devices else 1), "GROUP_RANK": str(node_rank),
+        "LOCAL_WORLD_SIZE": str(args.nproc_per_node or (len(devices) if devices else 1)), "GROUP_RANK": str(node_rank),
         "MASTER_ADDR": torch_master[0], "MASTER_PORT": str(torch_master[1]),
         "PADDLE_TRAINER_ID": str(grank), "PADDLE_GLOBAL_RANK": str(grank), "PADDLE_LOCAL_RANK": str(local_rank),
         "PADDLE_TRAINERS_NUM": str(world), "PADDLE_GLOBAL_SIZE": str(world), "PADDLE_NNODES": str(nnodes),
@@ -137,8 +138,8 @@ def _worker_env(args, local_rank, node_rank, nnodes, world, offset, eps, devices
         "PADDLE_MASTER": f"{torch_master[0]}:{torch_master[1]}", "PADDLE_JOB_ID": args.job_id,
         "FLAGS_selected_gpus": dev, "FLAGS_selected_accelerators": dev,
     })
-    if devices:
-        env.setdefault("PADDLE_DISTRI_BACKEND", "nccl")
+    if devices and (args.nproc_per_node or len(devices)) <= len(devices):
+        env.setdefault("PADDLE_DISTRI_BACKEND", "nccl")   # RCCL needs one device per rank
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return env
 
