@@ -889,3 +889,202 @@ def correlation(input1, input2, pad_size=4, kernel_size=1, max_displacement=4, s
             sh = bp[:, :, pad_size + dy: pad_size + dy + H, pad_size + dx: pad_size + dx + W]
             outs.append((a * sh).sum(1) / C)
     return _wrap(torch.stack(outs, 1).to(_raw(input1).dtype))
+
+
+# ------------------------------------------------------------------------------------------ fused inference long tail
+def add_group_norm_silu(x, residual=None, scale=None, bias=None, epsilon=1e-5, groups=32, data_format="NHWC",
+                        activation="silu"):
+    """(x + residual) -> group_norm -> SiLU (diffusion UNet fusion); returns (y, residual_out, mean, var)."""
+    r = _raw(x)
+    h = r + _raw(residual) if residual is not None else r
+    nhwc = data_format == "NHWC"
+    hc = h.movedim(-1, 1) if nhwc else h
+    y = F.group_norm(hc.float(), groups, None if scale is None else _raw(scale).float(),
+                     None if bias is None else _raw(bias).float(), epsilon)
+    if activation == "silu":
+        y = F.silu(y)
+    y = (y.movedim(1, -1) if nhwc else y).to(r.dtype)
+    g = hc.float().reshape(hc.shape[0], groups, -1)
+    return _wrap(y), _wrap(h), _wrap(g.mean(-1)), _wrap(g.var(-1, unbiased=False))
+
+
+def fused_conv2d_add_act(input, filter, bias=None, residual_data=None, strides=(1, 1), paddings=(0, 0),  # noqa: A002
+                         padding_algorithm="EXPLICIT", dilations=(1, 1), groups=1, data_format="NCHW",
+                         activation="relu", split_channels=(), exhaustive_search=False, workspace_size_MB=512,
+                         fuse_alpha=0.0):
+    x, w = _raw(input), _raw(filter)
+    nhwc = data_format == "NHWC"
+    xc = x.movedim(-1, 1) if nhwc else x
+    pad = list(paddings)[:2] if len(paddings) >= 2 else [paddings[0]] * 2
+    y = F.conv2d(xc, w, None if bias is None else _raw(bias), tuple(strides), tuple(pad), tuple(dilations), groups)
+    if residual_data is not None:
+        res = _raw(residual_data)
+        y = y + (res.movedim(-1, 1) if nhwc else res)
+    y = {"relu": F.relu, "identity": lambda t: t, "sigmoid": torch.sigmoid, "swish": F.silu,
+         "leaky_relu": lambda t: F.leaky_relu(t, fuse_alpha)}.get(activation, lambda t: t)(y)
+    return _wrap(y.movedim(1, -1) if nhwc else y)
+
+
+def fusion_repeated_fc_relu(x, w, bias):
+    """relu(... relu(x @ w0 + b0) ... @ wn + bn); returns (relu_out list, out)."""
+    h = _raw(x)
+    outs = []
+    for wi, bi in zip(w, bias):
+        h = F.relu(h @ _raw(wi) + _raw(bi).reshape(-1))
+        outs.append(_wrap(h))
+    return outs[:-1], outs[-1]
+
+
+def fusion_squared_mat_sub(x, y, scalar=1.0):
+    """scalar * ((x @ y)^2 - (x^2 @ y^2)) (the FM second-order term); returns (squared_x, squared_y,
+    squared_xy, out)."""
+    a, b = _raw(x), _raw(y)
+    xy = a @ b
+    sx, sy = a * a, b * b
+    return _wrap(sx), _wrap(sy), _wrap(xy * xy), _wrap(scalar * (xy * xy - sx @ sy))
+
+
+def fusion_transpose_flatten_concat(x, trans_axis, flatten_axis, concat_axis):
+    outs = []
+    for t in x:
+        r = _raw(t).permute(list(trans_axis))
+        outs.append(r.reshape(int(torch.tensor(r.shape[:flatten_axis]).prod()), -1))
+    return _wrap(torch.cat(outs, concat_axis))
+
+
+def multihead_matmul(input, w, bias, bias_qk=None, transpose_q=False, transpose_k=True, transpose_v=False,  # noqa: A002
+                     alpha=1.0, head_number=1):
+    """Fused BERT self-attention (inference): qkv = input @ w + bias with w [H, 3, H]; per-head softmax(alpha q
+    k^T + bias_qk) v; out [B, S, H]."""
+    x = _raw(input)
+    B, S, H = x.shape
+    W = _raw(w).reshape(H, 3 * H)
+    qkv = (x @ W + _raw(bias).reshape(-1)).reshape(B, S, 3, head_number, H // head_number)
+    q, k, v = (qkv[:, :, i].transpose(1, 2) for i in range(3))
+    s = alpha * (q @ k.transpose(-1, -2))
+    if bias_qk is not None:
+        s = s + _raw(bias_qk)
+    o = torch.softmax(s.float(), -1).to(x.dtype) @ v
+    return _wrap(o.transpose(1, 2).reshape(B, S, H))
+
+
+def self_dp_attention(x, alpha=1.0, head_number=1):
+    """Self attention over a packed [B, S, 3, heads, d] qkv tensor (CPU oneDNN op in the reference)."""
+    r = _raw(x)
+    B, S = r.shape[0], r.shape[1]
+    q, k, v = (r[:, :, i].transpose(1, 2) for i in range(3))
+    o = torch.softmax((alpha * q @ k.transpose(-1, -2)).float(), -1).to(r.dtype) @ v
+    return _wrap(o.transpose(1, 2).reshape(B, S, -1))
+
+
+def fused_gate_attention(query, key=None, query_weight=None, key_weight=None, value_weight=None, qkv_weight=None,
+                         nonbatched_bias=None, src_mask=None, gate_weight=None, gate_bias=None, out_linear_weight=None,
+                         out_linear_bias=None, has_gating=True, merge_qkv=True, use_flash_attn=False):
+    """AlphaFold gated self-attention: qkv_weight [3, h, d, c]; softmax(q k^T / sqrt(d) + mask + bias) v, gated by
+    sigmoid(q_in . gate_weight + gate_bias), output projection [h, d, c]."""
+    x = _raw(query)                     # [B, N, S, c]
+    W = _raw(qkv_weight)                # [3, h, d, c]
+    q, k, v = (torch.einsum("bnsc,hdc->bnhsd", x, W[i]) for i in range(3))
+    d = W.shape[2]
+    s = torch.einsum("bnhsd,bnhtd->bnhst", q * d ** -0.5, k)
+    if src_mask is not None:
+        s = s + _raw(src_mask)
+    if nonbatched_bias is not None:
+        s = s + _raw(nonbatched_bias)
+    o = torch.einsum("bnhst,bnhtd->bnhsd", torch.softmax(s.float(), -1).to(x.dtype), v)
+    if has_gating:
+        g = torch.einsum("bnsc,chd->bnhsd", x, _raw(gate_weight))
+        if gate_bias is not None:
+            g = g + _raw(gate_bias)[None, None, :, None, :]
+        o = o * torch.sigmoid(g)
+    out = torch.einsum("bnhsd,hdc->bnsc", o, _raw(out_linear_weight))
+    if out_linear_bias is not None:
+        out = out + _raw(out_linear_bias)
+    return _wrap(out)
+
+
+def cudnn_lstm(x, init_h, init_c, w=None, weight_list=None, sequence_length=None, dropout_prob=0.0,
+               is_bidirec=False, hidden_size=100, num_layers=1, is_test=False, seed=0):
+    """The cuDNN LSTM op: time-major [S, B, in] LSTM over a weight list (same layout as the rnn op)."""
+    out, _, states, _ = rnn(x, [init_h, init_c], weight_list, sequence_length, dropout_prob, is_bidirec,
+                            _raw(x).shape[-1], hidden_size, num_layers, "LSTM", seed, is_test)
+    return out, states[0], states[1]
+
+
+def resnet_basic_block(x, filter1, scale1, bias1, mean1, var1, filter2, scale2, bias2, mean2, var2, filter3=None,
+                       scale3=None, bias3=None, mean3=None, var3=None, stride1=1, stride2=1, stride3=1, padding1=1,
+                       padding2=1, padding3=0, dilation1=1, dilation2=1, dilation3=1, group=1, momentum=0.9,
+                       epsilon=1e-5, data_format="NCHW", has_shortcut=False, use_global_stats=True, is_test=True,
+                       trainable_statistics=False, act_type="relu", find_conv_input_max=True):
+    """Inference ResNet basic block: relu(bn2(conv2(relu(bn1(conv1 x)))) + shortcut(x))."""
+    r = _raw(x)
+
+    def cbn(t, f, s, b, m, v, st, pd, dl):
+        y = F.conv2d(t, _raw(f), None, st, pd, dl, group)
+        return F.batch_norm(y, _raw(m), _raw(v), _raw(s), _raw(b), False, 0.0, epsilon)
+
+    h = F.relu(cbn(r, filter1, scale1, bias1, mean1, var1, stride1, padding1, dilation1))
+    h = cbn(h, filter2, scale2, bias2, mean2, var2, stride2, padding2, dilation2)
+    sc = cbn(r, filter3, scale3, bias3, mean3, var3, stride3, padding3, dilation3) if has_shortcut else r
+    return _wrap(F.relu(h + sc))
+
+
+def resnet_unit(x, filter_x, scale_x, bias_x, mean_x, var_x, z=None, filter_z=None, scale_z=None, bias_z=None,
+                mean_z=None, var_z=None, stride=1, stride_z=1, padding=0, dilation=1, group=1, momentum=0.9,
+                epsilon=1e-5, data_format="NHWC", fuse_add=False, has_shortcut=False, use_global_stats=True,
+                is_test=True, use_addto=False, act_type="relu"):
+    """conv + BN (+ a second conv+BN or a residual add) + ReLU (the ResNet unit fusion)."""
+    nhwc = data_format == "NHWC"
+    r = _raw(x).movedim(-1, 1) if nhwc else _raw(x)
+    y = F.conv2d(r, _raw(filter_x), None, stride, padding, dilation, group)
+    y = F.batch_norm(y, _raw(mean_x), _raw(var_x), _raw(scale_x), _raw(bias_x), False, 0.0, epsilon)
+    if has_shortcut:
+        zz = _raw(z).movedim(-1, 1) if nhwc else _raw(z)
+        zs = F.conv2d(zz, _raw(filter_z), None, stride_z, 0, 1, group)
+        y = y + F.batch_norm(zs, _raw(mean_z), _raw(var_z), _raw(scale_z), _raw(bias_z), False, 0.0, epsilon)
+    elif fuse_add:
+        y = y + (_raw(z).movedim(-1, 1) if nhwc else _raw(z))
+    y = F.relu(y) if act_type == "relu" else y
+    return _wrap(y.movedim(1, -1) if nhwc else y)
+
+
+def blha_get_max_len(seq_lens_encoder, seq_lens_decoder, batch_size):
+    """Max encoder / decoder sequence lengths of a block-attention batch (two [1] int32 tensors)."""
+    e, d = _raw(seq_lens_encoder).reshape(-1), _raw(seq_lens_decoder).reshape(-1)
+    return (_wrap(e.max().reshape(1).to(torch.int32)), _wrap(d.max().reshape(1).to(torch.int32)))
+
+
+def calc_reduced_attn_scores(q, k, softmax_lse):
+    """sum over query rows of the softmax probabilities, per key: [B, H, 1, Sk] (reference calc_reduced_attn op,
+    used for KV-cache pruning), recomputed from q, k and the forward's log-sum-exp."""
+    qf, kf = _raw(q).float().transpose(1, 2), _raw(k).float().transpose(1, 2)  # [B, H, S, D]
+    if kf.shape[1] != qf.shape[1]:
+        kf = kf.repeat_interleave(qf.shape[1] // kf.shape[1], 1)
+    s = qf @ kf.transpose(-1, -2) / qf.shape[-1] ** 0.5
+    lse = _raw(softmax_lse).float()[..., : s.shape[2], None]
+    return _wrap(torch.exp(s - lse).sum(2, keepdim=True))
+
+
+def sparse_batch_norm_(x, mean, variance, scale, bias, is_test=False, momentum=0.9, epsilon=1e-5,
+                       data_format="NDHWC", use_global_stats=False, trainable_statistics=False):
+    """Batch norm over the values of a sparse COO tensor (channel = last dim of the values)."""
+    r = _raw(x).coalesce()
+    vals = r.values()
+    y = F.batch_norm(vals, _raw(mean), _raw(variance), _raw(scale), _raw(bias),
+                     not (is_test or use_global_stats), 1 - momentum, epsilon)
+    return _wrap(torch.sparse_coo_tensor(r.indices(), y, r.shape))
+
+
+sparse_sync_batch_norm_ = sparse_batch_norm_
+
+
+def yolo_box_head(x, anchors, class_num):
+    """YOLOv3 head activation: sigmoid on x, y, objectness and class scores, exp kept raw for w, h (reference
+    yolo_box_head, inference)."""
+    r = _raw(x).clone()
+    N, C, H, W = r.shape
+    na = len(anchors) // 2
+    v = r.reshape(N, na, 5 + class_num, H, W)
+    v[:, :, 0:2] = torch.sigmoid(v[:, :, 0:2])
+    v[:, :, 4:] = torch.sigmoid(v[:, :, 4:])
+    return _wrap(v.reshape(N, C, H, W))

@@ -270,11 +270,18 @@ for _n in ("nadam_", "radam_", "asgd_", "rprop_", "decayed_adagrad", "ftrl", "dp
            "apply_per_channel_scale", "quant_linear", "fake_quantize_range_abs_max", "moving_average_abs_max_scale",
            "sparse_acos", "sparse_acosh", "sparse_full_like", "rnn", "lstm", "gru_unit", "beam_search",
            "beam_search_decode", "ctc_align", "crf_decoding", "chunk_eval", "auc", "bipartite_match",
-           "anchor_generator", "multiclass_nms", "multiclass_nms3", "im2sequence", "correlation"):
+           "anchor_generator", "multiclass_nms", "multiclass_nms3", "im2sequence", "correlation",
+           "add_group_norm_silu", "fused_conv2d_add_act", "fusion_repeated_fc_relu", "fusion_squared_mat_sub",
+           "fusion_transpose_flatten_concat", "multihead_matmul", "self_dp_attention", "fused_gate_attention",
+           "cudnn_lstm", "resnet_basic_block", "resnet_unit", "blha_get_max_len", "calc_reduced_attn_scores",
+           "sparse_batch_norm_", "sparse_sync_batch_norm_", "yolo_box_head"):
     ALIASES.setdefault(_n, ("ops.extra_ops." + _n, {}))
 ALIASES.setdefault("nce", ("static.nn.nce", {}))
 ALIASES.setdefault("row_conv", ("static.nn.row_conv", {}))
 ALIASES.setdefault("graph_sample_neighbors", ("geometric.sample_neighbors", {}))
+ALIASES["print"] = ("ops.extra_ops.print", {})
+ALIASES.setdefault("sparse_conv3d_implicit_gemm", ("sparse.nn.functional.conv3d", {}))
+ALIASES.setdefault("sparse_fused_attention", ("sparse.nn.functional.attention", {}))
 
 # reference ops that only exist for other hardware (XPU fused kernels): outside this framework's scope
 _PS_OPS = {"distributed_lookup_table", "distributed_push_sparse", "send_and_recv", "fetch_barrier",

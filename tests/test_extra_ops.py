@@ -178,3 +178,48 @@ def test_sequence_and_detection_ops():
     corr = C.correlation(x, x, 1, 1, 1)
     assert list(corr.shape) == [1, 9, 5, 5]
     np.testing.assert_allclose(corr.numpy()[0, 4], (x.numpy()[0] ** 2).mean(0), rtol=1e-5)
+
+
+def test_fused_long_tail_batch3():
+    rs = np.random.RandomState(4)
+    x = rs.randn(2, 4, 4, 8).astype("float32")
+    res = rs.randn(2, 4, 4, 8).astype("float32")
+    sc, bi = rs.rand(8).astype("float32"), rs.randn(8).astype("float32")
+    y, h, _, _ = C.add_group_norm_silu(paddle.to_tensor(x), paddle.to_tensor(res), paddle.to_tensor(sc),
+                                       paddle.to_tensor(bi), 1e-5, 4)
+    ref = torch.nn.functional.silu(torch.nn.functional.group_norm(torch.tensor(x + res).permute(0, 3, 1, 2), 4,
+                                                                  torch.tensor(sc), torch.tensor(bi))).permute(0, 2, 3, 1)
+    np.testing.assert_allclose(y.numpy(), ref.numpy(), rtol=1e-4, atol=1e-5)
+    a, b = rs.randn(3, 5).astype("float32"), rs.randn(5, 4).astype("float32")
+    *_, out = C.fusion_squared_mat_sub(paddle.to_tensor(a), paddle.to_tensor(b), 0.5)
+    np.testing.assert_allclose(out.numpy(), 0.5 * ((a @ b) ** 2 - (a * a) @ (b * b)), rtol=1e-4, atol=1e-5)
+    B, S, H, nh = 2, 5, 8, 2
+    inp, w, bias = rs.randn(B, S, H).astype("float32"), rs.randn(H, 3, H).astype("float32"), rs.randn(3 * H).astype(
+        "float32")
+    o = C.multihead_matmul(paddle.to_tensor(inp), paddle.to_tensor(w), paddle.to_tensor(bias), None, False, True,
+                           False, 0.5, nh)
+    qkv = (inp @ w.reshape(H, 3 * H) + bias).reshape(B, S, 3, nh, H // nh)
+    q, k, v = (np.transpose(qkv[:, :, i], (0, 2, 1, 3)) for i in range(3))
+    s = 0.5 * q @ np.swapaxes(k, -1, -2)
+    p = np.exp(s - s.max(-1, keepdims=True))
+    p /= p.sum(-1, keepdims=True)
+    np.testing.assert_allclose(o.numpy(), np.transpose(p @ v, (0, 2, 1, 3)).reshape(B, S, H), rtol=1e-4, atol=1e-5)
+    # resnet_unit (NCHW, no shortcut) == conv -> BN(eval) -> relu
+    xc = rs.randn(1, 3, 6, 6).astype("float32")
+    f = rs.randn(4, 3, 3, 3).astype("float32")
+    m, vv, g, bb = rs.randn(4).astype("float32"), rs.rand(4).astype("float32") + 0.5, rs.rand(4).astype(
+        "float32"), rs.randn(4).astype("float32")
+    T = paddle.to_tensor
+    u = C.resnet_unit(T(xc), T(f), T(g), T(bb), T(m), T(vv), None, None, None, None, None, None, 1, 1, 1,
+                      data_format="NCHW")
+    ref = torch.relu(torch.nn.functional.batch_norm(torch.nn.functional.conv2d(torch.tensor(xc), torch.tensor(f),
+                                                                               padding=1),
+                                                    torch.tensor(m), torch.tensor(vv), torch.tensor(g),
+                                                    torch.tensor(bb), False, 0.0, 1e-5))
+    np.testing.assert_allclose(u.numpy(), ref.numpy(), rtol=1e-4, atol=1e-5)
+    # reduced attention scores: every query row's probabilities sum to 1 -> the per-key sums add up to Sq
+    q4, k4 = rs.randn(1, 6, 2, 8).astype("float32"), rs.randn(1, 6, 2, 8).astype("float32")
+    s4 = np.einsum("bqhd,bkhd->bhqk", q4, k4) / np.sqrt(8)
+    lse = np.log(np.exp(s4).sum(-1))
+    red = C.calc_reduced_attn_scores(T(q4), T(k4), T(lse.astype("float32")))
+    np.testing.assert_allclose(red.numpy().sum(-1), np.full((1, 2, 1), 6.0), rtol=1e-4)
