@@ -65,7 +65,7 @@ ALIASES = {
     "fft_c2r": ("fft.irfftn", {}),
     # attention / fusions
     "flash_attn": ("nn.functional.flash_attention", {}),
-    "memory_efficient_attention": ("incubate.nn.functional.variable_length_memory_efficient_attention", {}),
+    "memory_efficient_attention": ("incubate.nn.memory_efficient_attention_op", {}),
     "fused_softmax_mask": ("incubate.softmax_mask_fuse", {}),
     "fused_softmax_mask_upper_triangle": ("incubate.softmax_mask_fuse_upper_triangle", {}),
     "fused_batch_norm_act": ("nn.functional.batch_norm", {}),
