@@ -534,6 +534,11 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16*
   // compose with its base
   constexpr int KOFF = (2 * QTILE + STILE + 2 * BMQ * 4 + 255) / 256 * 256;
   __shared__ __attribute__((aligned(16))) char smem[KOFF + KTILE];
+  // deferred dQ atomics (dense atomic mode): a step's dQ tile is parked here ([slice][16][64 lanes], conflict-free
+  // b32 accesses) and added at the NEXT step's head, after that step's staging wait.  CDNA counts atomics in
+  // vmcnt, so atomics issued at a step's end made the next head's wait for its prefetched Q/dO (vmcnt(0)) wait
+  // out the atomic round trips: 0.94 ms of the 4.63 ms layer (profiles/r3_flash_bwd_dq_ablation.md)
+  __shared__ float dq_stash[MODE == kDense ? DT * 16 * 64 : 1];
   char* qimg = smem;
   char* doimg = qimg + QTILE;
   char* simg = doimg + QTILE;
@@ -676,6 +681,23 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16*
   int o_srow = r * (BNK * 2) + (((h ^ msk(r)) & (SNCH - 1)) << 4);
   int o_scol = 4 * h * (BNK * 2) + ((((lkey >> 3) ^ h) & (SNCH - 1)) << 4) + ((lkey & 7) << 1);
 
+  int pend_hq = -1, pend_q0 = 0;  // deferred dQ tile (wave-uniform); pend_hq < 0: none
+  auto flush_dq = [&]() {
+    if constexpr (MODE == kDense) {
+      if (pend_hq < 0) return;
+      const int hqd4 = Hq * D * 4;
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(dQs + (long)pend_q0 * Hq * D + (long)pend_hq * D, BMQ * hqd4);
+#pragma unroll
+      for (int dsl = wv; dsl < DT; dsl += NW) {
+        const int vo = 4 * h * hqd4 + (dsl * 32 + r) * 4;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dq_stash[(dsl * 16 + i) * 64 + lane], rs, vo,
+                                                         ((i & 3) + 8 * (i >> 2)) * hqd4, 0);
+      }
+      pend_hq = -1;
+    }
+  };
   while (step < ntot) {
     const int hq = hk * group + step / nqt;
     const int q0 = q_begin + (step % nqt) * BMQ;
@@ -711,6 +733,7 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16*
       }
     }
     __syncthreads();
+    flush_dq();  // the previous step's dQ atomics: issued after this step's staging wait, before the next prefetch
     const int step_next = next_step(step + 1);
     if (step_next < ntot) gload(step_next);  // lands while this step computes
 
@@ -798,6 +821,13 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16*
       // Full 32-row tiles: non-temporal buffer stores, the per-row offset in the scalar soffset (no VALU);
       // the tile that crosses Sq keeps the checked stores
       if (MODE == kDense && ex.dq_atomic == 2) continue;  // ablation: dQ computed, not stored
+      if (MODE == kDense && ex.dq_atomic == 1 && q0 + BMQ <= Sq) {  // park for the next step's head
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dq_stash[(dsl * 16 + i) * 64 + lane] = dq[i] * scale;
+        pend_hq = hq;
+        pend_q0 = q0;
+        continue;
+      }
       if (q0 + BMQ <= Sq) {
         const int hqd4 = Hq * D * 4;
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(dQs + (long)q0 * Hq * D + (long)hq * D, BMQ * hqd4);
@@ -826,6 +856,7 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16*
     }
     step = step_next;
   }
+  flush_dq();
   // write dK (scaled) and dV for this lane's key: accumulator row = d, column = key
   if (mykey < Sk) {
     bf16* dkr = dK + (kt0 + mykey) * sdk + hk * D;

@@ -262,7 +262,9 @@ def dtensor_from_fn(fn, mesh, placements, *args, **kwargs):
 
 def reshard(dist_tensor, mesh, placements):
     """Same mesh: the framework's reshard engine (reshard.py: s->r all-gather, p->r all-reduce, p->s
-    reduce-scatter, s->s all-to-all, r->s slice; differentiable).  A different mesh: torch's redistribute."""
+    reduce-scatter, s->s all-to-all, r->s slice; differentiable).  A different mesh: the cross-mesh path
+    (reshard.reshard_cross_mesh: p2p for same-status meshes, else replicate -> send -> slice); ranks outside the
+    destination mesh hold no local data."""
     t = dist_tensor._t
     assert isinstance(t, _dt.DTensor), "reshard expects a DistTensor"
     dm = mesh._device_mesh()
@@ -270,7 +272,9 @@ def reshard(dist_tensor, mesh, placements):
         from .reshard import reshard as _own
 
         return _attach(_wrap(_own(t, _torch_placements(mesh, placements))), mesh)
-    return _attach(_wrap(t.redistribute(dm, _torch_placements(mesh, placements))), mesh)
+    from .reshard import reshard_cross_mesh
+
+    return _attach(_wrap(reshard_cross_mesh(t, dm, _torch_placements(mesh, placements))), mesh)
 
 
 def unshard_dtensor(dist_tensor):

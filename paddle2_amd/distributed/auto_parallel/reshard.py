@@ -171,3 +171,76 @@ def reshard(dt, placements):
     if src == dst:
         return dt
     return _Reshard.apply(dt, dt.device_mesh, src, dst)
+
+
+# ------------------------------------------------------------------------------------------- cross-mesh
+def _local_shape(shape, mesh_shape, placements):
+    out = list(shape)
+    for d, p in enumerate(placements):
+        if isinstance(p, _TShard):
+            if out[p.dim] % mesh_shape[d]:
+                raise ValueError(f"cross-mesh reshard: axis {p.dim} of size {out[p.dim]} does not split over "
+                                 f"{mesh_shape[d]} ranks")
+            out[p.dim] //= mesh_shape[d]
+    return out
+
+
+def reshard_cross_mesh(dt, dst_mesh, dst_placements):
+    """DTensor on one process mesh -> DTensor on another (reference reshard/same_status_reshard_function.cc and
+    the cross-mesh path of nd_mesh_reshard_function.cc).
+
+    * same status (meshes of one shape, identical placements): every source coordinate sends its local shard to
+      the destination rank at the same coordinate (point-to-point, no collective);
+    * otherwise: the source mesh first resolves its placements to Replicate with the same-mesh engine
+      (all-reduce / all-gather), source rank k % |src| sends the full tensor to destination rank k, and each
+      destination rank slices (or makes partial) its piece.
+
+    Every rank of both meshes must call it.  Ranks outside the destination mesh get a DistTensor without local
+    data.  Forward only (a
+    pipeline-stage hand-off differentiates through its own send / recv pair)."""
+    src_dm = dt.device_mesh
+    src_ranks = src_dm.mesh.flatten().tolist()
+    dst_ranks = dst_mesh.mesh.flatten().tolist()
+    me = dist.get_rank()
+    shape, dtype = tuple(dt.shape), dt.dtype
+    dst_placements = tuple(dst_placements)
+    dev = dt._local_tensor.device if me in src_ranks else (
+        torch.device("cuda", torch.cuda.current_device()) if dst_mesh.device_type == "cuda" else torch.device("cpu"))
+    same = tuple(src_dm.mesh.shape) == tuple(dst_mesh.mesh.shape) and tuple(dt.placements) == dst_placements
+    local = None
+    if same:
+        if me in src_ranks:
+            peer = dst_ranks[src_ranks.index(me)]
+            if peer == me:
+                local = dt._local_tensor
+            else:
+                dist.send(dt._local_tensor.contiguous(), peer)
+                COMM_LOG.append(("send", -1))
+        if me in dst_ranks and local is None:
+            peer = src_ranks[dst_ranks.index(me)]
+            local = torch.empty(_local_shape(shape, list(dst_mesh.mesh.shape), dst_placements), dtype=dtype,
+                                device=dev)
+            dist.recv(local, peer)
+            COMM_LOG.append(("recv", -1))
+    else:
+        full = None
+        if me in src_ranks:
+            full = reshard_local(dt._local_tensor, src_dm, tuple(dt.placements),
+                                 tuple(_TReplicate() for _ in range(src_dm.ndim))).contiguous()
+        for j, d in enumerate(dst_ranks):
+            s = src_ranks[j % len(src_ranks)]
+            if s == d:
+                continue
+            if me == s:
+                dist.send(full, d)
+                COMM_LOG.append(("send", -1))
+            elif me == d:
+                full = torch.empty(shape, dtype=dtype, device=dev)
+                dist.recv(full, s)
+                COMM_LOG.append(("recv", -1))
+        if me in dst_ranks:
+            local = reshard_local(full, dst_mesh, tuple(_TReplicate() for _ in range(dst_mesh.ndim)), dst_placements)
+    if me not in dst_ranks:  # a non-member holds the DistTensor's metadata with no local data (as in torch)
+        local = torch.empty(0, dtype=dtype, device=dev)
+    return _dt.DTensor.from_local(local, dst_mesh, dst_placements, run_check=False, shape=torch.Size(shape),
+                                  stride=torch.empty(shape, device="meta").stride())

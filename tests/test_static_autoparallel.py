@@ -105,3 +105,18 @@ def test_engine_trains_tp_plan_like_serial():
         np.testing.assert_allclose(e["losses"], e["ref"], rtol=1e-5, atol=1e-6)
         assert e["w1_local_shape"] == [8, 8]      # fc1.weight [8, 16] column-sharded over 2 ranks
         assert e["pred_shape"] == []               # the MLP's forward returns the scalar loss-like mean
+
+
+def test_cross_mesh_reshard_four_ranks():
+    res = run_workers("cross_mesh_worker.py", 4)
+    g = np.arange(24, dtype="float32").reshape(4, 6)
+    for r, o in enumerate(res):
+        if r in (2, 3):   # mesh B
+            assert o["same_status"]["local"] == g[2 * (r - 2): 2 * (r - 2) + 2].tolist()
+            assert o["same_status"]["comm"] == ["recv"]
+            assert o["general"]["local"] == g[:, 3 * (r - 2): 3 * (r - 2) + 3].tolist()
+            assert o["back"] == []
+        else:             # mesh A
+            assert o["same_status"]["local"] == [] and o["same_status"]["comm"] == ["send"]
+            assert "all_gather" in o["general"]["comm"]
+            assert o["back"] == g.tolist()
