@@ -12,7 +12,7 @@ import torch  # noqa: E402
 
 import paddle2_amd as paddle  # noqa: E402
 import paddle2_amd.distributed as dist  # noqa: E402
-from paddle2_amd.distributed.auto_parallel import dist_ops, reshard as RS  # noqa: E402
+from paddle2_amd.distributed.auto_parallel import _reshard_engine as RS, dist_ops  # noqa: E402
 from paddle2_amd.models import LlamaConfig  # noqa: E402
 from paddle2_amd.models.llama import LlamaModel  # noqa: E402
 from _dist import write_result  # noqa: E402
