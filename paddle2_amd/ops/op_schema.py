@@ -280,6 +280,8 @@ ALIASES.setdefault("nce", ("static.nn.nce", {}))
 ALIASES.setdefault("row_conv", ("static.nn.row_conv", {}))
 ALIASES.setdefault("graph_sample_neighbors", ("geometric.sample_neighbors", {}))
 ALIASES["print"] = ("ops.extra_ops.print", {})
+for _n in ("sequence_pool", "sequence_softmax", "sequence_expand", "sequence_conv", "lod_reset"):
+    ALIASES.setdefault(_n, ("static.sequence." + _n, {}))
 ALIASES.setdefault("sparse_conv3d_implicit_gemm", ("sparse.nn.functional.conv3d", {}))
 ALIASES.setdefault("sparse_fused_attention", ("sparse.nn.functional.attention", {}))
 

@@ -152,3 +152,6 @@ def py_func(func, x, out, backward_func=None, skip_vars_in_backward_input=None):
 
 
 from . import nn  # noqa: E402,F401
+from .extras import (ExponentialMovingAverage, IpuCompiledProgram, IpuStrategy, Print,  # noqa: E402,F401
+                     WeightNormParamAttr, accuracy, auc, ctr_metric_bundle, load_from_file, normalize_program,
+                     save_to_file, set_ipu_shard, xpu_places)

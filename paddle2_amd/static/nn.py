@@ -461,3 +461,7 @@ def switch_case(branch_index, branch_fns, default=None, name=None):
         items, (_, default) = items[:-1], items[-1]
     pairs = [(branch_index == i, f) for i, f in items]
     return case(pairs, default) if pairs else default()
+
+
+from .sequence import (lod_reset, sequence_conv, sequence_expand, sequence_first_step,  # noqa: E402,F401
+                       sequence_last_step, sequence_pool, sequence_softmax)
