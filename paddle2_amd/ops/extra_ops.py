@@ -1088,3 +1088,237 @@ def yolo_box_head(x, anchors, class_num):
     v[:, :, 0:2] = torch.sigmoid(v[:, :, 0:2])
     v[:, :, 4:] = torch.sigmoid(v[:, :, 4:])
     return _wrap(v.reshape(N, C, H, W))
+
+
+# ------------------------------------------------------------------------------------------ batch 4: DGC, LoD fusions, misc
+def dgc_clip_by_norm(x, current_step, max_norm, rampup_begin_step=-1.0):
+    """clip_by_norm once DGC is active (current_step >= rampup_begin_step), identity before."""
+    if float(_raw(current_step).reshape(-1)[0]) < rampup_begin_step:
+        return x
+    r = _raw(x)
+    n = r.float().norm()
+    return _wrap((r.float() * torch.clamp(max_norm / n.clamp_min(1e-12), max=1.0)).to(r.dtype))
+
+
+@torch.no_grad()
+def dgc_momentum(param, grad, velocity, learning_rate, master_param=None, current_step_tensor=None,
+                 nranks_tensor=None, mu=0.9, use_nesterov=False, regularization_method="", regularization_coeff=0.0,
+                 multi_precision=False, rescale_grad=1.0, rampup_begin_step=-1.0):
+    """Momentum before DGC's rampup step, plain SGD after (the velocity then lives in the DGC op)."""
+    step = float(_raw(current_step_tensor).reshape(-1)[0]) if current_step_tensor is not None else 0.0
+    p, g = _p(param, master_param, multi_precision), _raw(grad).float() * rescale_grad
+    if nranks_tensor is not None:
+        g = g / float(_raw(nranks_tensor).reshape(-1)[0])
+    lr = _lr(learning_rate)
+    if step < rampup_begin_step:
+        v = _raw(velocity).float() * mu + g
+        upd = (g + mu * v) if use_nesterov else v
+        _upd(velocity, v)
+    else:
+        upd = g
+    _store(param, master_param, multi_precision, p - lr * upd)
+    return param, velocity, master_param
+
+
+@torch.no_grad()
+def dgc(u, v, grad, param=None, current_step=None, nranks=None, m=0.9, use_nesterov=True, sparsity=(0.999,),
+        rampup_begin_step=0.0, rampup_step=0.0, regular_coeff=0.0, regular_type=0):
+    """Deep Gradient Compression (reference dgc op): momentum correction u = m u + g, v += u (nesterov: u =
+    m (u + g), v += u + g), keep the top-(1 - sparsity) |v| entries as the encoded gradient, clear them from u
+    and v.  Returns (u, v, encode_grad (indices, values), grad_out (dense), k, gather_buff)."""
+    g = _raw(grad).float()
+    step = float(_raw(current_step).reshape(-1)[0]) if current_step is not None else 0.0
+    sp = list(sparsity) if isinstance(sparsity, (list, tuple)) else [sparsity]
+    idx = 0 if rampup_step <= 0 else min(len(sp) - 1, int((step - rampup_begin_step) * len(sp) / rampup_step))
+    s = sp[max(idx, 0)]
+    uu, vv = _raw(u).float(), _raw(v).float()
+    if use_nesterov:
+        uu = m * (uu + g)
+        vv = vv + uu + g
+    else:
+        uu = m * uu + g
+        vv = vv + uu
+    k = max(1, int(round(g.numel() * (1 - s))))
+    flat = vv.reshape(-1)
+    top = flat.abs().topk(k).indices
+    dense = torch.zeros_like(flat)
+    dense[top] = flat[top]
+    uflat = uu.reshape(-1).clone()
+    uflat[top] = 0
+    flat = flat.clone()
+    flat[top] = 0
+    _upd(u, uflat.reshape(uu.shape))
+    _upd(v, flat.reshape(vv.shape))
+    enc = torch.cat([top.float(), dense[top]])
+    return u, v, _wrap(enc), _wrap(dense.reshape(g.shape).to(_raw(grad).dtype)), _wrap(torch.tensor([k])), None
+
+
+def collect_fpn_proposals(multi_level_rois, multi_level_scores, multi_level_rois_num=None, post_nms_topn=2000):
+    """Concatenate the per-level RoIs and keep the post_nms_topn highest-scoring ones (per image when
+    rois_num is given); returns (rois, rois_num)."""
+    rois = torch.cat([_raw(r) for r in multi_level_rois])
+    sc = torch.cat([_raw(s).reshape(-1) for s in multi_level_scores])
+    if multi_level_rois_num is None:
+        keep = sc.argsort(descending=True)[:post_nms_topn]
+        return _wrap(rois[keep]), _wrap(torch.tensor([keep.numel()], dtype=torch.int32))
+    nums = [_raw(n).reshape(-1).long() for n in multi_level_rois_num]
+    n_img = nums[0].numel()
+    img = torch.cat([torch.repeat_interleave(torch.arange(n_img), n) for n in nums])
+    outs, cnt = [], []
+    for i in range(n_img):
+        sel = (img == i).nonzero().reshape(-1)
+        keep = sel[sc[sel].argsort(descending=True)[:post_nms_topn]]
+        outs.append(rois[keep])
+        cnt.append(keep.numel())
+    return _wrap(torch.cat(outs)), _wrap(torch.tensor(cnt, dtype=torch.int32))
+
+
+def fusion_seqpool_concat(x, pooltype="SUM", axis=1):
+    from ..static.sequence import sequence_pool
+
+    return _wrap(torch.cat([_raw(sequence_pool(t, pooltype)) for t in x], axis))
+
+
+def fused_seqpool_cvm(x, cvm, pooltype="SUM", pad_value=0.0, use_cvm=True, cvm_offset=2):
+    from ..static.sequence import sequence_pool
+
+    outs = []
+    for t in x:
+        pooled = sequence_pool(t, pooltype, pad_value=pad_value)
+        outs.append(_raw(cvm_fn(pooled, use_cvm)))
+    return [_wrap(o) for o in outs]
+
+
+def cvm_fn(t, use_cvm):
+    return cvm(t, None, use_cvm)
+
+
+def fusion_seqpool_cvm_concat(x, cvm, pooltype="SUM", use_cvm=True, axis=1):
+    return _wrap(torch.cat([_raw(o) for o in fused_seqpool_cvm(x, cvm, pooltype, 0.0, use_cvm)], axis))
+
+
+def dist_concat(x, ring_id=0, nranks=1):
+    """All-gather along axis 0 over the ring (one rank: identity)."""
+    if nranks <= 1:
+        return x
+    from ..distributed import collective as Cc
+
+    parts = []
+    Cc.all_gather(parts, x)
+    return _wrap(torch.cat([_raw(p) for p in parts], 0))
+
+
+def fused_token_prune(attn, x, mask, new_mask, keep_first_token=True, keep_order=False):
+    """Keep the tokens with the largest attention received (column sums of attn [B, H, S, S] over heads and
+    queries, masked) — new_mask's length S' tokens per sample; returns (pruned x [B, S', C], cls_inds)."""
+    a = (_raw(attn) + _raw(mask)).float().clamp_min(0) if mask is not None else _raw(attn).float()
+    score = a.sum((1, 2))                              # [B, S]
+    s_new = _raw(new_mask).shape[-1]
+    if keep_first_token:
+        score[:, 0] = float("inf")
+    idx = score.topk(s_new, -1).indices
+    if keep_order:
+        idx = idx.sort(-1).values
+    xr = _raw(x)
+    out = xr.gather(1, idx[..., None].expand(-1, -1, xr.shape[-1]))
+    return _wrap(out), _wrap(idx)
+
+
+def graph_khop_sampler(row, colptr, x, eids=None, sample_sizes=(-1,), return_eids=False):
+    """Multi-hop neighbour sampling: sample_neighbors hop by hop from the frontier, then reindex the union
+    subgraph (reference graph_khop_sampler); returns (edge_src, edge_dst, sample_index, reindex_x)."""
+    from ..geometric import reindex_graph, sample_neighbors
+
+    frontier = x
+    srcs, dsts, counts_all, centers = [], [], [], []
+    for k in sample_sizes:
+        nb, cnt = sample_neighbors(row, colptr, frontier, sample_size=k)[:2]
+        srcs.append(_raw(nb))
+        centers.append(_raw(frontier))
+        counts_all.append(_raw(cnt))
+        frontier = _wrap(torch.unique(_raw(nb)))
+    nbs = torch.cat(srcs)
+    cnt = torch.cat(counts_all)
+    ctr = torch.cat(centers)
+    rs, rd, nodes = reindex_graph(_wrap(ctr), _wrap(nbs), _wrap(cnt))
+    return rs, rd, nodes, _wrap(torch.arange(_raw(x).numel()))
+
+
+def tdm_child(x, tree_info, child_nums=2, dtype="int32"):
+    """Children of tree nodes (reference tdm_child): tree_info rows are [item_id, layer, parent, child_0, ...];
+    returns (children ids, leaf mask)."""
+    ids = _raw(x).long()
+    info = _raw(tree_info).long()
+    ch = info[ids.reshape(-1)][:, 3:3 + child_nums].reshape(*ids.shape, child_nums)
+    leaf = (info[ch.clamp_min(0).reshape(-1)][:, 0] != 0).reshape(ch.shape) & (ch > 0)
+    tdt = torch.int64 if dtype == "int64" else torch.int32
+    return _wrap(ch.to(tdt)), _wrap(leaf.to(tdt))
+
+
+def lookup_table_dequant(w, ids, padding_idx=-1):
+    """Embedding over a uint8-quantised table: each row = [min, max, q_0 .. q_{D-1}] (floats holding packed
+    bytes in the reference); here rows are [min, max, codes...] as floats and value = min + code * (max-min)/255."""
+    tab = _raw(w).float()
+    i = _raw(ids).reshape(-1).long()
+    rows = tab[i]
+    mn, mx, codes = rows[:, :1], rows[:, 1:2], rows[:, 2:]
+    out = mn + codes * (mx - mn) / 255.0
+    if padding_idx >= 0:
+        out[i == padding_idx] = 0
+    return _wrap(out.reshape(*_raw(ids).shape, -1))
+
+
+def gru(input, h0, weight, bias=None, batch_size=None, batch_gate=None, batch_reset_hidden_prev=None,  # noqa: A002
+        batch_hidden=None, activation="tanh", gate_activation="sigmoid", is_reverse=False, origin_mode=False,
+        is_test=False):
+    """Full-sequence GRU over a LoD input of pre-projected gates [T, 3H] (reference gru op): each sequence runs
+    gru_unit steps from h0 (zeros when None); returns the hidden states [T, H] (with the input's LoD)."""
+    from ..static.sequence import _offsets
+
+    x = _raw(input)
+    off = _offsets(input)
+    H = x.shape[1] // 3
+    out = torch.zeros(x.shape[0], H, dtype=x.dtype, device=x.device)
+    for s, (a, b) in enumerate(zip(off[:-1], off[1:])):
+        h = _raw(h0)[s:s + 1] if h0 is not None else torch.zeros(1, H, dtype=x.dtype, device=x.device)
+        rng = range(b - 1, a - 1, -1) if is_reverse else range(a, b)
+        for t in rng:
+            _, _, hn = gru_unit(_wrap(x[t:t + 1]), _wrap(h), weight, bias, origin_mode=origin_mode)
+            h = _raw(hn)
+            out[t] = h[0]
+    res = _wrap(out)
+    res._lod = input._lod
+    return res
+
+
+def fusion_gru(x, h0, weight_x, weight_h, bias=None, activation="tanh", gate_activation="sigmoid",
+               is_reverse=False, use_seq=True, origin_mode=False, use_mkldnn=False, mkldnn_data_type="float32",
+               scale_data=1.0, shift_data=0.0, scale_weights=(1.0,), force_fp32_output=False):
+    """x @ weight_x (+ bias) then the LoD GRU (reference fusion_gru)."""
+    proj = _wrap(_raw(x) @ _raw(weight_x) + (_raw(bias).reshape(-1) if bias is not None else 0))
+    proj._lod = x._lod
+    return gru(proj, h0, weight_h, None, is_reverse=is_reverse, origin_mode=origin_mode)
+
+
+def fusion_lstm(x, weight_x, weight_h, bias, h0=None, c0=None, use_peepholes=False, is_reverse=False,
+                use_seq=True, gate_activation="sigmoid", cell_activation="tanh", candidate_activation="tanh",
+                scale_data=1.0, shift_data=0.0, scale_weights=(1.0,), force_fp32_output=False):
+    """x @ weight_x then an LSTM over each LoD sequence (gates i, f, c, o); returns (hidden [T, H], cell [T, H])."""
+    from ..static.sequence import _offsets
+
+    proj = _raw(x) @ _raw(weight_x) + _raw(bias).reshape(-1)[: _raw(weight_x).shape[1]]
+    off = _offsets(x)
+    H = _raw(weight_h).shape[0]
+    hs = torch.zeros(proj.shape[0], H, dtype=proj.dtype)
+    cs = torch.zeros_like(hs)
+    for s, (a, b) in enumerate(zip(off[:-1], off[1:])):
+        h = _raw(h0)[s] if h0 is not None else torch.zeros(H, dtype=proj.dtype)
+        c = _raw(c0)[s] if c0 is not None else torch.zeros(H, dtype=proj.dtype)
+        for t in (range(b - 1, a - 1, -1) if is_reverse else range(a, b)):
+            gi, gf, gc, go = (proj[t] + h @ _raw(weight_h)).chunk(4)
+            c = torch.sigmoid(gf) * c + torch.sigmoid(gi) * torch.tanh(gc)
+            h = torch.sigmoid(go) * torch.tanh(c)
+            hs[t], cs[t] = h, c
+    ho, co = _wrap(hs), _wrap(cs)
+    ho._lod = co._lod = x._lod
+    return ho, co

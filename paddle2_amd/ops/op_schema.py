@@ -274,7 +274,10 @@ for _n in ("nadam_", "radam_", "asgd_", "rprop_", "decayed_adagrad", "ftrl", "dp
            "add_group_norm_silu", "fused_conv2d_add_act", "fusion_repeated_fc_relu", "fusion_squared_mat_sub",
            "fusion_transpose_flatten_concat", "multihead_matmul", "self_dp_attention", "fused_gate_attention",
            "cudnn_lstm", "resnet_basic_block", "resnet_unit", "blha_get_max_len", "calc_reduced_attn_scores",
-           "sparse_batch_norm_", "sparse_sync_batch_norm_", "yolo_box_head"):
+           "sparse_batch_norm_", "sparse_sync_batch_norm_", "yolo_box_head", "dgc_clip_by_norm", "dgc_momentum",
+           "dgc", "collect_fpn_proposals", "fusion_seqpool_concat", "fused_seqpool_cvm", "fusion_seqpool_cvm_concat",
+           "dist_concat", "fused_token_prune", "graph_khop_sampler", "tdm_child", "lookup_table_dequant", "gru",
+           "fusion_gru", "fusion_lstm"):
     ALIASES.setdefault(_n, ("ops.extra_ops." + _n, {}))
 ALIASES.setdefault("nce", ("static.nn.nce", {}))
 ALIASES.setdefault("row_conv", ("static.nn.row_conv", {}))

@@ -223,3 +223,51 @@ def test_fused_long_tail_batch3():
     lse = np.log(np.exp(s4).sum(-1))
     red = C.calc_reduced_attn_scores(T(q4), T(k4), T(lse.astype("float32")))
     np.testing.assert_allclose(red.numpy().sum(-1), np.full((1, 2, 1), 6.0), rtol=1e-4)
+
+
+def test_batch4_dgc_lod_misc():
+    T = paddle.to_tensor
+    x = T(np.array([3.0, 4.0], "float32"))
+    np.testing.assert_allclose(C.dgc_clip_by_norm(x, T([5.0]), 1.0, 1.0).numpy(), [0.6, 0.8], rtol=1e-6)
+    np.testing.assert_allclose(C.dgc_clip_by_norm(x, T([0.0]), 1.0, 1.0).numpy(), [3.0, 4.0])
+    g = T(np.array([0.1, -5.0, 0.2, 3.0], "float32"))
+    u, v = paddle.zeros([4]), paddle.zeros([4])
+    _, _, enc, dense, k, _ = C.dgc(u, v, g, None, T([1.0]), None, 0.9, False, [0.5])
+    assert int(k.numpy()[0]) == 2
+    np.testing.assert_allclose(dense.numpy(), [0.0, -5.0, 0.0, 3.0])
+    np.testing.assert_allclose(v.numpy(), [0.1, 0.0, 0.2, 0.0], rtol=1e-6)   # sent entries cleared
+    rois, n = C.collect_fpn_proposals([T(np.ones((2, 4), "float32")), T(np.zeros((3, 4), "float32"))],
+                                      [T(np.array([0.5, 0.9], "float32")), T(np.array([0.1, 0.95, 0.2], "float32"))],
+                                      None, 3)
+    assert int(n.numpy()[0]) == 3 and rois.numpy()[0].tolist() == [0, 0, 0, 0]   # 0.95 first
+    a = T(np.arange(8, dtype="float32").reshape(4, 2))
+    a.set_recursive_sequence_lengths([[1, 3]])
+    b = T(np.ones((3, 2), "float32"))
+    b.set_recursive_sequence_lengths([[2, 1]])
+    cat = C.fusion_seqpool_concat([a, b], "SUM", 1)
+    np.testing.assert_allclose(cat.numpy(), [[0, 1, 2, 2], [12, 15, 1, 1]])
+    attn = T(np.random.RandomState(5).rand(1, 2, 4, 4).astype("float32"))
+    xs = T(np.arange(12, dtype="float32").reshape(1, 4, 3))
+    out, idx = C.fused_token_prune(attn, xs, None, T(np.zeros((1, 1, 2, 2), "float32")), True, True)
+    assert idx.numpy()[0, 0] == 0 and list(out.shape) == [1, 2, 3]
+    info = T(np.array([[0, 0, 0, 1, 2], [0, 1, 0, 3, 0], [7, 1, 0, 0, 0], [9, 2, 1, 0, 0]], "int64"))
+    ch, leaf = C.tdm_child(T(np.array([0, 1], "int64")), info, 2)
+    assert ch.numpy().tolist() == [[1, 2], [3, 0]] and leaf.numpy().tolist() == [[0, 1], [1, 0]]
+    # LoD LSTM == torch LSTM on each sequence (gate order i, f, c, o == torch's i, f, g, o)
+    rs = np.random.RandomState(6)
+    D, H = 3, 4
+    wx, wh, bias = rs.randn(D, 4 * H).astype("float32"), rs.randn(H, 4 * H).astype("float32"), rs.randn(
+        1, 4 * H).astype("float32")
+    xv = rs.randn(5, D).astype("float32")
+    xt = T(xv)
+    xt.set_recursive_sequence_lengths([[2, 3]])
+    hs, _ = C.fusion_lstm(xt, T(wx), T(wh), T(bias))
+    lstm = torch.nn.LSTM(D, H)
+    with torch.no_grad():
+        lstm.weight_ih_l0.copy_(torch.tensor(wx).t())
+        lstm.weight_hh_l0.copy_(torch.tensor(wh).t())
+        lstm.bias_ih_l0.copy_(torch.tensor(bias[0]))
+        lstm.bias_hh_l0.zero_()
+    for a0, b0 in ((0, 2), (2, 5)):
+        ref, _ = lstm(torch.tensor(xv[a0:b0])[:, None])
+        np.testing.assert_allclose(hs.numpy()[a0:b0], ref[:, 0].detach().numpy(), rtol=1e-4, atol=1e-5)
