@@ -280,7 +280,7 @@ def shuffle_batch(x, seed=None, startup_seed=0):
             _wrap(torch.tensor([s + 1], dtype=torch.int64)))
 
 
-def hash(x, num_hash=1, mod_by=100000):  # noqa: A001 — the reference op name
+def hash_op(x, num_hash=1, mod_by=100000):
     """Per-row hash ids (num_hash independent hashes of each int64 row, modulo mod_by)."""
     r = _raw(x).long()
     rows = r.reshape(r.shape[0], -1)
@@ -293,11 +293,9 @@ def hash(x, num_hash=1, mod_by=100000):  # noqa: A001 — the reference op name
     return _wrap(out)
 
 
-def print(x, first_n=-1, message="", summarize=20, print_tensor_name=True, print_tensor_type=True,  # noqa: A001
+def print_op(x, first_n=-1, message="", summarize=20, print_tensor_name=True, print_tensor_type=True,
           print_tensor_shape=True, print_tensor_layout=True, print_tensor_lod=True, print_phase="BOTH",
           is_forward=True):
-    import builtins
-
     r = _raw(x)
     parts = [message] if message else []
     if print_tensor_type:
@@ -306,7 +304,7 @@ def print(x, first_n=-1, message="", summarize=20, print_tensor_name=True, print
         parts.append(f"shape: {list(r.shape)}")
     vals = r.reshape(-1)[: summarize if summarize > 0 else None].tolist()
     parts.append(f"data: {vals}")
-    builtins.print("  ".join(parts))
+    print("  ".join(parts))
     return x
 
 

@@ -262,7 +262,7 @@ ALIASES = {
 # long-tail ops implemented in ops/extra_ops.py under their reference names
 for _n in ("nadam_", "radam_", "asgd_", "rprop_", "decayed_adagrad", "ftrl", "dpsgd", "lars_momentum_",
            "average_accumulates_", "number_count", "assign_pos", "limit_by_capacity", "prune_gate_by_capacity",
-           "random_routing", "partial_concat", "partial_sum", "shuffle_batch", "hash", "print",
+           "random_routing", "partial_concat", "partial_sum", "shuffle_batch",
            "add_position_encoding", "cvm", "batch_fc", "accuracy_check", "coalesce_tensor", "coalesce_tensor_",
            "embedding_grad_dense", "straight_through_estimator_grad", "fused_elemwise_activation",
            "fused_elemwise_add_activation", "fused_fc_elementwise_layernorm", "fused_scale_bias_add_relu",
@@ -282,7 +282,8 @@ for _n in ("nadam_", "radam_", "asgd_", "rprop_", "decayed_adagrad", "ftrl", "dp
 ALIASES.setdefault("nce", ("static.nn.nce", {}))
 ALIASES.setdefault("row_conv", ("static.nn.row_conv", {}))
 ALIASES.setdefault("graph_sample_neighbors", ("geometric.sample_neighbors", {}))
-ALIASES["print"] = ("ops.extra_ops.print", {})
+ALIASES["print"] = ("ops.extra_ops.print_op", {})
+ALIASES.setdefault("hash", ("ops.extra_ops.hash_op", {}))
 for _n in ("sequence_pool", "sequence_softmax", "sequence_expand", "sequence_conv", "lod_reset"):
     ALIASES.setdefault(_n, ("static.sequence." + _n, {}))
 ALIASES.setdefault("sparse_conv3d_implicit_gemm", ("sparse.nn.functional.conv3d", {}))

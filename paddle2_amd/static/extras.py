@@ -11,7 +11,7 @@ from ..framework.tensor import Tensor
 
 def Print(input, first_n=-1, message=None, summarize=20, print_tensor_name=True, print_tensor_type=True,  # noqa: A002,N802
           print_tensor_shape=True, print_tensor_lod=True, print_phase="both"):
-    from ..ops.extra_ops import print as _p
+    from ..ops.extra_ops import print_op as _p
 
     return _p(input, first_n, message or "", summarize, print_tensor_name, print_tensor_type, print_tensor_shape)
 
