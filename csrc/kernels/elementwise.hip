@@ -19,10 +19,9 @@ __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ x
                                                          T* __restrict__ out, long rows, int H, long sx, long sy) {
   constexpr int V = 16 / sizeof(T);
   const int hv = H / V;
-  const long total = rows * hv;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long r = i / hv;
-    const int c = (int)(i - r * hv) * V;
+  for (long r = blockIdx.y; r < rows; r += gridDim.y)
+  for (int vi = blockIdx.x * 256 + threadIdx.x; vi < hv; vi += gridDim.x * 256) {
+    const int c = vi * V;
     float a[V], b[V], o[V];
     load_vec<T, V>(x + r * sx + c, a);
     load_vec<T, V>(y + r * sy + c, b);
@@ -39,10 +38,9 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ x
                                                          long sdx, long sdy) {
   constexpr int V = 16 / sizeof(T);
   const int hv = H / V;
-  const long total = rows * hv;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long r = i / hv;
-    const int c = (int)(i - r * hv) * V;
+  for (long r = blockIdx.y; r < rows; r += gridDim.y)
+  for (int vi = blockIdx.x * 256 + threadIdx.x; vi < hv; vi += gridDim.x * 256) {
+    const int c = vi * V;
     float a[V], b[V], g[V], da[V], db[V];
     load_vec<T, V>(x + r * sx + c, a);
     load_vec<T, V>(y + r * sy + c, b);
@@ -240,7 +238,7 @@ extern "C" int pd_swiglu_fwd(int dt, const void* x, const void* y, void* out, lo
   const int V = dt == kF32 ? 4 : 8;
   if (H % V) return -1;
   hipStream_t st = (hipStream_t)stream;
-  const int g = ew_grid(rows * (H / V));
+  const dim3 g = rowcol_grid(rows, H / V);
   PD_DISPATCH_FLOAT(dt, T, swiglu_fwd_kernel<T><<<g, 256, 0, st>>>((const T*)x, (const T*)y, (T*)out, rows, H, sx, sy));
   return (int)hipGetLastError();
 }
@@ -250,7 +248,7 @@ extern "C" int pd_swiglu_bwd(int dt, const void* x, const void* y, const void* d
   const int V = dt == kF32 ? 4 : 8;
   if (H % V) return -1;
   hipStream_t st = (hipStream_t)stream;
-  const int g = ew_grid(rows * (H / V));
+  const dim3 g = rowcol_grid(rows, H / V);
   PD_DISPATCH_FLOAT(dt, T, swiglu_bwd_kernel<T><<<g, 256, 0, st>>>((const T*)x, (const T*)y, (const T*)dout, (T*)dx,
                                                                     (T*)dy, rows, H, sx, sy, sdx, sdy));
   return (int)hipGetLastError();

@@ -66,10 +66,9 @@ __global__ __launch_bounds__(256) void bias_act_fwd(const T* __restrict__ x, con
                                                     T* __restrict__ out, long rows, int H, long sx, long so, int act) {
   constexpr int E = 16 / sizeof(T);
   const int cv = H / E;
-  const long total = rows * cv;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long r = i / cv;
-    const int c = (int)(i - r * cv) * E;
+  for (long r = blockIdx.y; r < rows; r += gridDim.y)
+  for (int vi = blockIdx.x * 256 + threadIdx.x; vi < cv; vi += gridDim.x * 256) {
+    const int c = vi * E;
     float a[E];
     ld8<T>(x + r * sx + c, a);
     if (b) {
@@ -104,10 +103,9 @@ __global__ __launch_bounds__(256) void bias_act_bwd(const T* __restrict__ x, con
                                                     long sx, long sd, int act) {
   constexpr int E = 16 / sizeof(T);
   const int cv = H / E;
-  const long total = rows * cv;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long r = i / cv;
-    const int c = (int)(i - r * cv) * E;
+  for (long r = blockIdx.y; r < rows; r += gridDim.y)
+  for (int vi = blockIdx.x * 256 + threadIdx.x; vi < cv; vi += gridDim.x * 256) {
+    const int c = vi * E;
     float a[E], d[E];
     ld8<T>(x + r * sx + c, a);
     ld8<T>(dout + r * sd + c, d);
@@ -190,7 +188,7 @@ extern "C" int pd_bias_act(int dt, int gated, int act, const void* x, const void
   const int E = dt == kF32 ? 4 : 8;
   if (H % E || sx % E || so % E) return -1;
   hipStream_t st = (hipStream_t)stream;
-  const int g = fa2::grid_for(rows * (H / E));
+  const dim3 g = rowcol_grid(rows, H / E);
 #define PD_BA(T)                                                                                                     \
   if (gated) fa2::bias_act_fwd<T, true><<<g, 256, 0, st>>>((const T*)x, (const T*)b, (T*)out, rows, H, sx, so, act); \
   else fa2::bias_act_fwd<T, false><<<g, 256, 0, st>>>((const T*)x, (const T*)b, (T*)out, rows, H, sx, so, act);
@@ -205,7 +203,7 @@ extern "C" int pd_bias_act_bwd(int dt, int gated, int act, const void* x, const 
   const int E = dt == kF32 ? 4 : 8;
   if (H % E || sx % E || sd % E) return -1;
   hipStream_t st = (hipStream_t)stream;
-  const int g = fa2::grid_for(rows * (H / E));
+  const dim3 g = rowcol_grid(rows, H / E);
 #define PD_BAB(T)                                                                                                  \
   if (gated)                                                                                                       \
     fa2::bias_act_bwd<T, true><<<g, 256, 0, st>>>((const T*)x, (const T*)b, (const T*)dout, (T*)dx, rows, H, sx, \
