@@ -19,15 +19,27 @@ __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ x
                                                          T* __restrict__ out, long rows, int H, long sx, long sy) {
   constexpr int V = 16 / sizeof(T);
   const int hv = H / V;
-  for (long r = blockIdx.y; r < rows; r += gridDim.y)
-  for (int vi = blockIdx.x * 256 + threadIdx.x; vi < hv; vi += gridDim.x * 256) {
-    const int c = vi * V;
-    float a[V], b[V], o[V];
-    load_vec<T, V>(x + r * sx + c, a);
-    load_vec<T, V>(y + r * sy + c, b);
+  // two rows per iteration: four independent 16-B loads in flight per lane before the first use
+  for (long r = 2L * blockIdx.y; r < rows; r += 2L * gridDim.y) {
+    const bool two = r + 1 < rows;
+    for (int vi = blockIdx.x * 256 + threadIdx.x; vi < hv; vi += gridDim.x * 256) {
+      const int c = vi * V;
+      float a[V], b[V], a2[V], b2[V], o[V];
+      load_vec<T, V>(x + r * sx + c, a);
+      load_vec<T, V>(y + r * sy + c, b);
+      if (two) {
+        load_vec<T, V>(x + (r + 1) * sx + c, a2);
+        load_vec<T, V>(y + (r + 1) * sy + c, b2);
+      }
 #pragma unroll
-    for (int j = 0; j < V; ++j) o[j] = a[j] * sigmoidf_(a[j]) * b[j];
-    store_vec<T, V>(out + r * H + c, o);
+      for (int j = 0; j < V; ++j) o[j] = a[j] * sigmoidf_(a[j]) * b[j];
+      store_vec<T, V>(out + r * H + c, o);
+      if (two) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] = a2[j] * sigmoidf_(a2[j]) * b2[j];
+        store_vec<T, V>(out + (r + 1) * H + c, o);
+      }
+    }
   }
 }
 
@@ -38,22 +50,38 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ x
                                                          long sdx, long sdy) {
   constexpr int V = 16 / sizeof(T);
   const int hv = H / V;
-  for (long r = blockIdx.y; r < rows; r += gridDim.y)
-  for (int vi = blockIdx.x * 256 + threadIdx.x; vi < hv; vi += gridDim.x * 256) {
-    const int c = vi * V;
-    float a[V], b[V], g[V], da[V], db[V];
-    load_vec<T, V>(x + r * sx + c, a);
-    load_vec<T, V>(y + r * sy + c, b);
-    load_vec<T, V>(dout + r * H + c, g);
+  // two rows per iteration: six independent 16-B loads in flight per lane before the first use
+  for (long r0 = 2L * blockIdx.y; r0 < rows; r0 += 2L * gridDim.y) {
+    const int nr = r0 + 1 < rows ? 2 : 1;
+    for (int vi = blockIdx.x * 256 + threadIdx.x; vi < hv; vi += gridDim.x * 256) {
+      const int c = vi * V;
+      float a[2][V], b[2][V], g[2][V];
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-      const float s = sigmoidf_(a[j]);
-      const float silu = a[j] * s;
-      db[j] = g[j] * silu;
-      da[j] = g[j] * b[j] * s * (1.f + a[j] * (1.f - s));
+      for (int k = 0; k < 2; ++k) {
+        if (k < nr) {
+          const long r = r0 + k;
+          load_vec<T, V>(x + r * sx + c, a[k]);
+          load_vec<T, V>(y + r * sy + c, b[k]);
+          load_vec<T, V>(dout + r * H + c, g[k]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (k < nr) {
+          const long r = r0 + k;
+          float da[V], db[V];
+#pragma unroll
+          for (int j = 0; j < V; ++j) {
+            const float s = sigmoidf_(a[k][j]);
+            const float silu = a[k][j] * s;
+            db[j] = g[k][j] * silu;
+            da[j] = g[k][j] * b[k][j] * s * (1.f + a[k][j] * (1.f - s));
+          }
+          store_vec<T, V>(dx + r * sdx + c, da);
+          store_vec<T, V>(dy + r * sdy + c, db);
+        }
+      }
     }
-    store_vec<T, V>(dx + r * sdx + c, da);
-    store_vec<T, V>(dy + r * sdy + c, db);
   }
 }
 
@@ -104,17 +132,20 @@ __global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, T* _
                                                    int time_major, long sx, long so) {
   // sx / so: elements between consecutive tokens of x / out (heads are D apart), so q/k can be
   // read straight out of a fused QKV projection and gradients written straight into dQKV.
+  // one workgroup per token (grid-strided): threads cover its (head, 8-pair chunk) items, so the only integer
+  // divisions are one 32-bit token split per token and one small head / chunk split per item (the flat 64-bit
+  // `i % chunks`, `/ Hn`, `/ S` chain cost more VALU than the rotation itself)
   const int half = D / 2;
   const int chunks = (half + 7) / 8;
-  const long total = (long)B * S * Hn * chunks;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int ch = (int)(i % chunks);
-    long t = i / chunks;
-    const int h = (int)(t % Hn);
-    t /= Hn;  // token index in storage order
+  const int per_tok = Hn * chunks;
+  const unsigned ntok = (unsigned)B * (unsigned)S;
+  for (unsigned tt = blockIdx.x; tt < ntok; tt += gridDim.x)
+  for (int j = threadIdx.x; j < per_tok; j += 256) {
+    const int h = j / chunks, ch = j - h * chunks;
+    const long t = tt;  // token index in storage order
     int b, s;
-    if (time_major) { s = (int)(t / B); b = (int)(t % B); }
-    else { b = (int)(t / S); s = (int)(t % S); }
+    if (time_major) { s = (int)(tt / (unsigned)B); b = (int)(tt - (unsigned)s * (unsigned)B); }
+    else { b = (int)(tt / (unsigned)S); s = (int)(tt - (unsigned)b * (unsigned)S); }
     const int p = pos ? (int)pos[(long)b * S + s] : s;
     const T* xr = x + t * sx + (long)h * D;
     T* orow = out + t * so + (long)h * D;
@@ -269,8 +300,9 @@ extern "C" int pd_rope(int dt, int style, int bwd, const void* x, void* out, con
                        void* stream) {
   if (D % 2) return -1;
   hipStream_t st = (hipStream_t)stream;
-  const long work = (long)B * S * Hn * ((D / 2 + 7) / 8);
-  const int g = ew_grid(work);
+  const long ntok = (long)B * S;
+  if (ntok >= (1L << 32)) return -1;
+  const int g = (int)(ntok < 65536 ? (ntok < 1 ? 1 : ntok) : 65536);
   const int es = dt == kF32 ? 4 : 2;
   const bool vec = (D % 16) == 0 && ((sx * es) % 16) == 0 && ((so * es) % 16) == 0;
 #define PD_ROPE1(T, SY, BW, VE) rope_kernel<T, SY, BW, VE><<<g, 256, 0, st>>>((const T*)x, (T*)out, cosv, sinv, pos, B, S, Hn, D, time_major, sx, so)
