@@ -1,6 +1,6 @@
 """paddle.distributed (reference: python/paddle/distributed/__init__.py, 65 public names)."""
 from . import collective, watchdog  # noqa: F401
-from .process_group import ProcessGroup, ProcessGroupGloo, ProcessGroupNCCL  # noqa: F401
+from .process_group import ProcessGroup, ProcessGroupGloo, ProcessGroupMPI, ProcessGroupNCCL  # noqa: F401
 from .comm_context import CommContextManager, GlooCommContext, NCCLCommContext  # noqa: F401
 from .collective import (Group, P2POp, ParallelEnv, ReduceOp, all_gather, all_gather_into_tensor,  # noqa: F401
                          all_gather_object, all_reduce, alltoall, alltoall_single, barrier, batch_isend_irecv,

@@ -103,10 +103,31 @@ def _env_int(*names, default=None):
     return default
 
 
+# rank / world-size / local-rank variables exported by MPI launchers (Open MPI, MPICH / Intel MPI PMI, MVAPICH2,
+# Slurm srun).  The reference's ProcessGroupMPI (paddle/fluid/distributed/collective/process_group_mpi.cc) takes its
+# rank from MPI_Comm_rank; here an ``mpirun``-launched job is recognised from these and runs its collectives on
+# gloo (CPU tensors) or RCCL (GPU tensors) -- the PyTorch-ROCm build has no MPI backend and xGMI is RCCL's anyway.
+_MPI_RANK = ("OMPI_COMM_WORLD_RANK", "PMI_RANK", "PMIX_RANK", "MV2_COMM_WORLD_RANK", "SLURM_PROCID")
+_MPI_SIZE = ("OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "MV2_COMM_WORLD_SIZE", "SLURM_NTASKS")
+_MPI_LOCAL = ("OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "MV2_COMM_WORLD_LOCAL_RANK", "SLURM_LOCALID")
+
+
+def _rank_env(default=0):
+    return _env_int("RANK", "PADDLE_TRAINER_ID", *_MPI_RANK, default=default)
+
+
+def _world_env(default=1):
+    return _env_int("WORLD_SIZE", "PADDLE_TRAINERS_NUM", *_MPI_SIZE, default=default)
+
+
+def _local_env(default=0):
+    return _env_int("LOCAL_RANK", "PADDLE_LOCAL_RANK", *_MPI_LOCAL, default=default)
+
+
 def _backend_for_device():
     if os.environ.get("PADDLE_DISTRI_BACKEND"):
         b = os.environ["PADDLE_DISTRI_BACKEND"].lower()
-        return "nccl" if b in ("nccl", "rccl", "xccl") else b
+        return "nccl" if b in ("nccl", "rccl", "xccl") else ("gloo" if b == "mpi" else b)
     return "nccl" if torch.cuda.is_available() else "gloo"
 
 
@@ -127,7 +148,7 @@ class ParallelEnv:
 
     @property
     def device_id(self):
-        return _env_int("LOCAL_RANK", "PADDLE_LOCAL_RANK", default=0)
+        return _local_env(0)
 
     dev_id = device_id
 
@@ -162,16 +183,18 @@ def init_parallel_env(backend=None, timeout_s=None):
     import atexit
 
     atexit.register(_shutdown_at_exit)
-    rank = _env_int("RANK", "PADDLE_TRAINER_ID", default=0)
-    world = _env_int("WORLD_SIZE", "PADDLE_TRAINERS_NUM", default=1)
+    rank = _rank_env(0)
+    world = _world_env(1)
     backend = backend or _backend_for_device()
+    if backend == "mpi":  # ProcessGroupMPI semantics: MPI-launched ranks, collectives on gloo
+        backend = "gloo"
     native_pg = False
     if backend in ("nccl", "rccl") and torch.cuda.is_available():
         from . import rccl_pg  # the framework's own RCCL process group (PADDLE2_AMD_PG=rccl)
 
         native_pg = rccl_pg.enabled()
     if backend == "nccl" and torch.cuda.is_available():
-        local = _env_int("LOCAL_RANK", "PADDLE_LOCAL_RANK", default=rank % max(torch.cuda.device_count(), 1))
+        local = _local_env(rank % max(torch.cuda.device_count(), 1))
         torch.cuda.set_device(local)
         from ..framework.place import set_device
 
@@ -212,7 +235,7 @@ def get_rank(group=None):
         return group.rank
     if dist.is_initialized():
         return dist.get_rank()
-    return _env_int("RANK", "PADDLE_TRAINER_ID", default=0)
+    return _rank_env(0)
 
 
 def get_world_size(group=None):
@@ -220,7 +243,7 @@ def get_world_size(group=None):
         return group.nranks
     if dist.is_initialized():
         return dist.get_world_size()
-    return _env_int("WORLD_SIZE", "PADDLE_TRAINERS_NUM", default=1)
+    return _world_env(1)
 
 
 def _get_default_group():
@@ -244,7 +267,8 @@ def new_group(ranks=None, backend=None, timeout=None, nccl_comm_init_option=0):
         kw = {}
         if timeout is not None:
             kw["timeout"] = timeout if isinstance(timeout, datetime.timedelta) else datetime.timedelta(seconds=timeout)
-        pg = dist.new_group(ranks=ranks, backend=backend if backend not in (None, "rccl") else None, **kw)
+        bk = "gloo" if backend == "mpi" else backend
+        pg = dist.new_group(ranks=ranks, backend=bk if bk not in (None, "rccl") else None, **kw)
     me = get_rank()
     g = Group(ranks.index(me) if me in ranks else -1, gid, ranks, pg)
     _groups[gid] = g

@@ -336,6 +336,31 @@ class ProcessGroupGloo(ProcessGroup):
     _backend_name = "gloo"
 
 
+class ProcessGroupMPI(ProcessGroup):
+    """``core.ProcessGroupMPI`` (reference paddle/fluid/distributed/collective/process_group_mpi.cc): an
+    MPI-launched group.  ``create`` takes rank / size from the MPI launcher's environment when not given and runs
+    the collectives on gloo (the ROCm PyTorch build has no MPI transport; GPU traffic belongs on RCCL)."""
+
+    _backend_name = "gloo"
+
+    @classmethod
+    def create(cls, store=None, rank=None, world_size=None, group_id=0, timeout=None):
+        from . import collective as C
+
+        rank = C._rank_env(0) if rank is None else rank
+        world_size = C._world_env(1) if world_size is None else world_size
+        if store is None:
+            import os
+
+            host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+            port = int(os.environ.get("MASTER_PORT", "29500"))
+            store = dist.TCPStore(host, port, world_size, rank == 0)
+        return super().create.__func__(cls, store, rank, world_size, group_id, timeout)
+
+    def name(self):
+        return self._name or "MPI"
+
+
 def wrap(pg, name=None, gid=0):
     """ProcessGroup object for a registered c10d group."""
     backend = dist.get_backend(pg)

@@ -22,3 +22,18 @@ def test_process_group_methods_three_ranks():
     assert res[0]["reduce_root"] == float(total)
     assert res[1]["recv"] == [1.0, 2.0, 3.0, 4.0]
     assert res[1]["recv_partial"] == [0.0, 0.0, 7.0, 8.0]
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("flavour", ["ompi", "pmi"])
+def test_mpi_launch_env_and_process_group_mpi(flavour):
+    """mpirun-launched ranks (reference ProcessGroupMPI, process_group_mpi.cc): rank / size / local rank from the
+    MPI launcher's variables, backend "mpi" -> collectives on gloo; ProcessGroupMPI.create() without arguments."""
+    w = 2
+    res = run_workers("mpi_pg_worker.py", w, args=(flavour,))
+    for r, x in enumerate(res):
+        assert (x["env_rank"], x["env_world"], x["dev"]) == (r, w, r)
+        assert x["all_reduce"] == [3.0] * 3
+        assert (x["pg_name"], x["pg_rank"], x["pg_size"], x["pg_sum"]) == ("MPI", r, w, 1.0)
