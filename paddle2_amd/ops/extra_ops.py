@@ -1320,3 +1320,290 @@ def fusion_lstm(x, weight_x, weight_h, bias, h0=None, c0=None, use_peepholes=Fal
     ho, co = _wrap(hs), _wrap(cs)
     ho._lod = co._lod = x._lod
     return ho, co
+
+
+# ------------------------------------------------------------------------------------------ long tail, batch 5
+def rank_attention(x, rank_offset, rank_param, max_rank=3, max_size=0):
+    """Reference rank_attention (paddle/phi/kernels/gpu/rank_attention_kernel.cu, funcs/rank_attention.cu.h):
+    rank_offset [N, 2*max_rank+1] = (own rank, then per slot k: (peer rank, peer row)).  Slot k of instance i
+    holds x[peer row] when both ranks are set (1-based; <= 0 means empty); the instance's parameter block for
+    slot k is rank_param rows [((own-1)*max_rank + peer-1) * D, +D).  Returns (input_help [N, max_rank*D],
+    out [N, P] = input_help @ per-instance parameter, ins_rank [N, 1]) -- batched as one bmm instead of the
+    reference's expand-then-GEMM kernels."""
+    xr, ro, rp = _raw(x), _raw(rank_offset).long(), _raw(rank_param)
+    N, D = xr.shape
+    P = rp.shape[1]
+    own = ro[:, 0] - 1
+    peer = ro[:, 1::2][:, :max_rank] - 1
+    row = ro[:, 2::2][:, :max_rank]
+    valid = (own[:, None] >= 0) & (peer >= 0)
+    help_ = torch.where(valid[..., None], xr[row.clamp(0, N - 1)], torch.zeros((), dtype=xr.dtype))
+    blk = (own[:, None].clamp(min=0) * max_rank + peer.clamp(min=0))              # [N, max_rank]
+    params = rp.reshape(-1, D, P)[blk] * valid[..., None, None].to(rp.dtype)      # [N, max_rank, D, P]
+    out = torch.bmm(help_.reshape(N, 1, max_rank * D), params.reshape(N, max_rank * D, P)).reshape(N, P)
+    return _wrap(help_.reshape(N, max_rank * D)), _wrap(out), _wrap(ro[:, :1].to(xr.dtype))
+
+
+def qkv_unpack_mha(q, k, v, src_mask=None):
+    """Reference qkv_unpack_mha (paddle/phi/kernels/fusion/gpu/qkv_unpack_mha_kernel.cu): one decode step of
+    multi-head attention over separate q [B, 1, Hq, D], k / v [B, S, Hkv, D] (grouped heads share a kv head)
+    with an additive src_mask broadcastable to [B, Hq, 1, S]; output [B, 1, Hq, D].  Runs on the framework's
+    flash / SDPA path."""
+    qr, kr, vr = _raw(q), _raw(k), _raw(v)
+    B, _, Hq, D = qr.shape
+    g = Hq // kr.shape[2]
+    kt = kr.transpose(1, 2).repeat_interleave(g, 1)
+    vt = vr.transpose(1, 2).repeat_interleave(g, 1)
+    mask = None if src_mask is None else _raw(src_mask).to(qr.dtype)
+    o = F.scaled_dot_product_attention(qr.transpose(1, 2), kt, vt, attn_mask=mask, scale=D ** -0.5)
+    return _wrap(o.transpose(1, 2).contiguous())
+
+
+def match_matrix_tensor(x, y, w, dim_t=1):
+    """Reference match_matrix_tensor (paddle/phi/kernels/cpu/match_matrix_tensor_kernel.cc): for LoD sequence
+    pairs (x_i [Lx, D], y_i [Ly, D]) and w [D, dim_t, D] emits x_i W_t y_i^T for every channel t, flattened per
+    sequence into out [sum_i dim_t*Lx_i*Ly_i, 1] (LoD over sequences); tmp = x @ w ([Tx, dim_t*D])."""
+    from ..static.sequence import _offsets
+
+    xr, yr, wr = _raw(x), _raw(y), _raw(w)
+    D = xr.shape[1]
+    tmp = xr @ wr.reshape(D, dim_t * D)
+    ox, oy = _offsets(x), _offsets(y)
+    outs, lod = [], [0]
+    for (a, b), (c, d) in zip(zip(ox[:-1], ox[1:]), zip(oy[:-1], oy[1:])):
+        t = tmp[a:b].reshape(b - a, dim_t, D).transpose(0, 1)                     # [dim_t, Lx, D]
+        m = t @ yr[c:d].t()                                                        # [dim_t, Lx, Ly]
+        outs.append(m.reshape(-1, 1))
+        lod.append(lod[-1] + m.numel())
+    out = _wrap(torch.cat(outs) if outs else tmp.new_zeros(0, 1))
+    out._lod = [lod]
+    return out, _wrap(tmp)
+
+
+def _context_cols(r, off, size, start, stride=1):
+    """Per-sequence context window: row t gets rows [t+start, t+start+size) of its own sequence (zero padded),
+    flattened to [T, size*D] (the im2col of sequence_conv)."""
+    D = r.shape[1]
+    cols = torch.zeros(r.shape[0], size * D, dtype=r.dtype, device=r.device)
+    for a, b in zip(off[:-1], off[1:]):
+        for k in range(size):
+            sh = start + k
+            lo, hi = max(a, a - sh), min(b, b - sh)
+            if hi > lo:
+                cols[lo:hi, k * D:(k + 1) * D] = r[lo + sh:hi + sh]
+    return cols
+
+
+def fusion_seqconv_eltadd_relu(x, filter, bias, context_length, context_start=0, context_stride=1):  # noqa: A002
+    """Reference fusion_seqconv_eltadd_relu (paddle/phi/kernels/fusion/cpu/fusion_seqconv_eltadd_relu_kernel.cc):
+    relu(sequence_conv(x) + bias); returns (out [T, F], col_mat [T, context_length*D])."""
+    from ..static.sequence import _offsets
+
+    xr = _raw(x)
+    cols = _context_cols(xr, _offsets(x), context_length, context_start, context_stride)
+    out = _wrap(torch.relu(cols @ _raw(filter) + _raw(bias).reshape(-1)))
+    out._lod = x._lod
+    return out, _wrap(cols)
+
+
+_FC_ACT = {"identity": lambda t: t, "relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh}
+
+
+def fusion_seqexpand_concat_fc(x, fc_weight, fc_bias=None, fc_activation="identity"):
+    """Reference fusion_seqexpand_concat_fc (fusion/cpu/fusion_seqexpand_concat_fc_kernel.cc): x[0] is a LoD
+    batch [T, D0]; x[1:] are per-sequence rows [N, Di] expanded over their sequence's steps; the concatenation
+    [T, sum D] goes through fc (+bias, activation).  Returns (out [T, F], fc_out = x[1:]'s share of the fc)."""
+    from ..static.sequence import _offsets
+
+    off = _offsets(x[0])
+    reps = torch.tensor([b - a for a, b in zip(off[:-1], off[1:])])
+    parts = [_raw(x[0])] + [torch.repeat_interleave(_raw(t), reps, 0) for t in x[1:]]
+    cat = torch.cat(parts, 1)
+    w = _raw(fc_weight)
+    d0 = parts[0].shape[1]
+    fc_out = torch.cat([_raw(t) for t in x[1:]], 1) @ w[d0:] if len(x) > 1 else cat.new_zeros(0)
+    y = cat @ w
+    if fc_bias is not None:
+        y = y + _raw(fc_bias).reshape(-1)
+    out = _wrap(_FC_ACT[fc_activation](y))
+    out._lod = x[0]._lod
+    return out, _wrap(fc_out)
+
+
+def fused_embedding_fc_lstm(ids, embeddings, weight_h, bias, h0=None, c0=None, use_peepholes=True,
+                            is_reverse=False, use_seq=True, gate_activation="sigmoid", cell_activation="tanh",
+                            candidate_activation="tanh"):
+    """Reference fused_embedding_fc_lstm (fusion/cpu/fused_embedding_fc_lstm_kernel.cc): ``embeddings`` is
+    the embedding table already multiplied by the LSTM input weight ([V, 4H]), so the gate projection of a
+    step is one row lookup; then the LoD LSTM (gates i, f, c, o).  Returns (hidden, cell)."""
+    idr = _raw(ids).reshape(-1).long()
+    proj = _wrap(_raw(embeddings)[idr])
+    proj._lod = ids._lod
+    H = _raw(weight_h).shape[0]
+    eye = _wrap(torch.eye(4 * H, dtype=_raw(embeddings).dtype))
+    return fusion_lstm(proj, eye, weight_h, bias, h0, c0, use_peepholes, is_reverse, use_seq, gate_activation,
+                       cell_activation, candidate_activation)
+
+
+def attention_lstm(x, c0, h0=None, attention_weight=None, attention_bias=None, attention_scalar=None,
+                   attention_scalar_bias=None, lstm_weight=None, lstm_bias=None, gate_activation="sigmoid",
+                   cell_activation="tanh", candidate_activation="tanh"):
+    """Reference attention_lstm (paddle/phi/kernels/cpu/attention_lstm_kernel.cc): at every step of a LoD
+    sequence x_s [L, M] the previous cell state attends over the whole sequence -- score_j = relu?(fc([x_j,
+    c_prev])) (scalar / scalar-bias rescale, relu), softmax over j -- and the pooled x feeds the LSTM together
+    with h_prev: gates = [pooled, h_prev] @ lstm_weight + lstm_bias (gate order f, i, o, c as the reference's
+    kernel lays them out).  Returns (hidden [T, D], cell [T, D])."""
+    from ..static.sequence import _offsets
+
+    xr, aw = _raw(x), _raw(attention_weight)
+    M = xr.shape[1]
+    lw, lb = _raw(lstm_weight), _raw(lstm_bias).reshape(-1)
+    D = lw.shape[1] // 4
+    off = _offsets(x)
+    hs = torch.zeros(xr.shape[0], D, dtype=xr.dtype)
+    cs = torch.zeros_like(hs)
+    ab = _raw(attention_bias).reshape(-1) if attention_bias is not None else None
+    for s, (a, b) in enumerate(zip(off[:-1], off[1:])):
+        seq = xr[a:b]
+        c = _raw(c0)[s]
+        h = _raw(h0)[s] if h0 is not None else torch.zeros(D, dtype=xr.dtype)
+        xs = seq @ aw[:M].reshape(M, -1)                                            # [L, 1]
+        for t in range(b - a):
+            sc = (xs + c @ aw[M:].reshape(D, -1)).reshape(-1)
+            if ab is not None:
+                sc = sc + ab[0]
+            sc = torch.relu(sc)
+            if attention_scalar is not None:
+                sc = sc * _raw(attention_scalar).reshape(-1)[0]
+                if attention_scalar_bias is not None:
+                    sc = sc + _raw(attention_scalar_bias).reshape(-1)[0]
+                sc = torch.relu(sc)
+            pooled = torch.softmax(sc, 0) @ seq                                     # [M]
+            gf, gi, go, gc = (torch.cat([pooled, h]) @ lw + lb).chunk(4)
+            c = torch.sigmoid(gf) * c + torch.sigmoid(gi) * torch.tanh(gc)
+            h = torch.sigmoid(go) * torch.tanh(c)
+            hs[a + t], cs[a + t] = h, c
+    ho, co = _wrap(hs), _wrap(cs)
+    ho._lod = co._lod = x._lod
+    return ho, co
+
+
+def yolo_box_post(boxes0, boxes1, boxes2, image_shape, image_scale, anchors0, anchors1, anchors2, class_num,
+                  conf_thresh, downsample_ratio0, downsample_ratio1, downsample_ratio2, clip_bbox=True,
+                  scale_x_y=1.0, nms_threshold=0.45):
+    """Reference yolo_box_post (paddle/phi/kernels/fusion/gpu/yolo_box_post_kernel.cu): decode the three YOLOv3
+    heads (yolo_box), map boxes back to the original image (divide by image_scale), then per-image multi-class
+    NMS.  Returns (out [K, 6] = label, score, x1, y1, x2, y2; nms_rois_num [N])."""
+    from ..vision.ops import yolo_box
+
+    shp = _wrap(_raw(image_shape).int())
+    bxs, scs = [], []
+    for hd, an, ds in ((boxes0, anchors0, downsample_ratio0), (boxes1, anchors1, downsample_ratio1),
+                       (boxes2, anchors2, downsample_ratio2)):
+        b, s = yolo_box(hd, shp, list(an), class_num, conf_thresh, ds, clip_bbox, scale_x_y=scale_x_y)
+        bxs.append(_raw(b).float())
+        scs.append(_raw(s).float())
+    bx = torch.cat(bxs, 1)
+    sc = torch.cat(scs, 1)
+    scale = _raw(image_scale).float().reshape(bx.shape[0], -1)
+    sx, sy = scale[:, -1:], scale[:, :1]                      # image_scale rows are (scale_y, scale_x)
+    bx = bx / torch.cat([sx, sy, sx, sy], 1)[:, None, :]
+    out, _, num = multiclass_nms3(_wrap(bx), _wrap(sc.transpose(1, 2)), None, conf_thresh, -1, -1,
+                                  nms_threshold, False, 1.0, -1)
+    return out, num
+
+
+def p_send_array(x, ring_id=0, peer=0, use_calc_stream=True, dynamic_shape=False):
+    """Reference p_send_array (static pipeline send of a tensor array): the array length, then each tensor
+    (with its shape first when ``dynamic_shape``), over the framework's point-to-point path."""
+    from ..distributed import collective as C
+
+    C.send(_wrap(torch.tensor([len(x)], dtype=torch.int64)), dst=peer)
+    for t in x:
+        if dynamic_shape:
+            shp = list(_raw(t).shape)
+            C.send(_wrap(torch.tensor([len(shp)] + shp, dtype=torch.int64)), dst=peer)
+        C.send(t if hasattr(t, "_t") else _wrap(t), dst=peer)
+
+
+def p_recv_array(ring_id=0, peer=0, dtype="float32", out_shape=(), use_calc_stream=True, dynamic_shape=False):
+    """Counterpart of p_send_array: receives the array length, then each tensor (``out_shape`` per element, or
+    the sent shapes with ``dynamic_shape``); returns the list of tensors."""
+    from ..distributed import collective as C
+    from ..framework.dtype import convert_dtype
+
+    n = _wrap(torch.zeros(1, dtype=torch.int64))
+    C.recv(n, src=peer)
+    outs = []
+    for _ in range(int(_raw(n)[0])):
+        if dynamic_shape:
+            hdr = _wrap(torch.zeros(9, dtype=torch.int64))
+            C.recv(hdr, src=peer)
+            shape = _raw(hdr)[1:1 + int(_raw(hdr)[0])].tolist()
+        else:
+            shape = list(out_shape)
+        t = _wrap(torch.zeros(shape, dtype=convert_dtype(dtype)))
+        C.recv(t, src=peer)
+        outs.append(t)
+    return outs
+
+
+def fused_scale_bias_relu_conv_bn(x, w, scale=None, bias=None, bn_scale=None, bn_bias=None,
+                                  input_running_mean=None, input_running_var=None, paddings=(0, 0),
+                                  dilations=(1, 1), strides=(1, 1), padding_algorithm="EXPLICIT", groups=1,
+                                  data_format="NHWC", momentum=0.9, epsilon=1e-5, fuse_prologue=True,
+                                  exhaustive_search=False, accumulation_count=0):
+    """Reference fused_scale_bias_relu_conv_bn (fusion/gpu/fused_scale_bias_relu_conv_bn_kernel.cu, the ResNet
+    unit): optional prologue relu(x*scale+bias), conv (NHWC), batch statistics of the conv output and the
+    running-stat update; returns (out, out_running_mean, out_running_var, saved_mean, saved_inv_std, eq_scale,
+    eq_bias) with eq_scale / eq_bias the folded BN affine (y_bn = conv*eq_scale + eq_bias)."""
+    xr = _raw(x)
+    nhwc = data_format == "NHWC"
+    if fuse_prologue and scale is not None:
+        xr = torch.relu(xr * _raw(scale).reshape(-1) + _raw(bias).reshape(-1))
+    xc = xr.permute(0, 3, 1, 2) if nhwc else xr
+    wr = _raw(w)
+    wc = wr.permute(0, 3, 1, 2) if nhwc else wr
+    pad = "same" if padding_algorithm == "SAME" else (0 if padding_algorithm == "VALID" else tuple(paddings))
+    y = F.conv2d(xc.float(), wc.float(), None, tuple(strides), pad, tuple(dilations), groups)
+    mean = y.mean((0, 2, 3))
+    var = y.var((0, 2, 3), unbiased=False)
+    inv_std = torch.rsqrt(var + epsilon)
+    n = y.numel() // y.shape[1]
+    rm = _raw(input_running_mean).float() * momentum + mean * (1 - momentum)
+    rv = _raw(input_running_var).float() * momentum + var * n / max(n - 1, 1) * (1 - momentum)
+    eq_scale = _raw(bn_scale).float() * inv_std
+    eq_bias = _raw(bn_bias).float() - mean * eq_scale
+    out = (y.permute(0, 2, 3, 1) if nhwc else y).to(_raw(x).dtype)
+    return (_wrap(out), _wrap(rm), _wrap(rv), _wrap(mean), _wrap(inv_std), _wrap(eq_scale.to(out.dtype)),
+            _wrap(eq_bias.to(out.dtype)))
+
+
+def fused_multi_transformer_int8(x, ln_scale, ln_bias, qkv_w, qkv_bias, out_linear_w, out_linear_bias,
+                                 ffn_ln_scale, ffn_ln_bias, ffn1_weight, ffn1_bias, ffn2_weight, ffn2_bias,
+                                 qkv_out_scale=None, out_linear_out_scale=None, ffn1_out_scale=None,
+                                 ffn2_out_scale=None, cache_kv=None, time_step=None, attn_mask=None,
+                                 pre_layer_norm=True, epsilon=1e-5, dropout_rate=0.0, is_test=True,
+                                 dropout_implementation="downgrade_in_infer", act_method="gelu", trans_qkvw=True,
+                                 ring_id=-1, **_):
+    """Reference fused_multi_transformer_int8 (fusion/gpu/fused_multi_transformer_int8_op.cu): the multi-layer
+    decoder with int8 weights; each weight is dequantised with its per-output-channel ``*_out_scale`` (weight
+    scale) and the layers run through the framework's fused_multi_transformer."""
+    from ..serving import fused_multi_transformer
+
+    def deq(ws, scales):
+        if scales is None:
+            return [_wrap(_raw(w).float()) for w in ws]
+        return [_wrap(_raw(w).float() * _raw(s).float().reshape(*([-1] + [1] * (_raw(w).dim() - 1))))
+                if _raw(w).dim() > 1 and _raw(s).numel() == _raw(w).shape[0] else
+                _wrap(_raw(w).float() * _raw(s).float().reshape(-1)) for w, s in zip(ws, scales)]
+
+    dt = _raw(x).dtype
+    cast = lambda ts: [_wrap(_raw(t).to(dt)) for t in ts]  # noqa: E731
+    return fused_multi_transformer(x, ln_scale, ln_bias, cast(deq(qkv_w, qkv_out_scale)), qkv_bias,
+                                   cast(deq(out_linear_w, out_linear_out_scale)), out_linear_bias, ffn_ln_scale,
+                                   ffn_ln_bias, cast(deq(ffn1_weight, ffn1_out_scale)), ffn1_bias,
+                                   cast(deq(ffn2_weight, ffn2_out_scale)), ffn2_bias,
+                                   pre_layer_norm=pre_layer_norm, epsilon=epsilon, cache_kvs=cache_kv,
+                                   time_step=time_step, attn_mask=attn_mask, activation=act_method,
+                                   trans_qkvw=trans_qkvw, ring_id=ring_id)

@@ -277,7 +277,10 @@ for _n in ("nadam_", "radam_", "asgd_", "rprop_", "decayed_adagrad", "ftrl", "dp
            "sparse_batch_norm_", "sparse_sync_batch_norm_", "yolo_box_head", "dgc_clip_by_norm", "dgc_momentum",
            "dgc", "collect_fpn_proposals", "fusion_seqpool_concat", "fused_seqpool_cvm", "fusion_seqpool_cvm_concat",
            "dist_concat", "fused_token_prune", "graph_khop_sampler", "tdm_child", "lookup_table_dequant", "gru",
-           "fusion_gru", "fusion_lstm"):
+           "fusion_gru", "fusion_lstm", "rank_attention", "qkv_unpack_mha", "match_matrix_tensor",
+           "fusion_seqconv_eltadd_relu", "fusion_seqexpand_concat_fc", "fused_embedding_fc_lstm", "attention_lstm",
+           "yolo_box_post", "p_send_array", "p_recv_array", "fused_scale_bias_relu_conv_bn",
+           "fused_multi_transformer_int8"):
     ALIASES.setdefault(_n, ("ops.extra_ops." + _n, {}))
 ALIASES.setdefault("nce", ("static.nn.nce", {}))
 ALIASES.setdefault("row_conv", ("static.nn.row_conv", {}))
