@@ -1607,3 +1607,415 @@ def fused_multi_transformer_int8(x, ln_scale, ln_bias, qkv_w, qkv_bias, out_line
                                    pre_layer_norm=pre_layer_norm, epsilon=epsilon, cache_kvs=cache_kv,
                                    time_step=time_step, attn_mask=attn_mask, activation=act_method,
                                    trans_qkvw=trans_qkvw, ring_id=ring_id)
+
+
+# ------------------------------------------------------------------------------------------ long tail, batch 6
+def tdm_sampler(x, travel, layer, output_positive=True, neg_samples_num_list=(), layer_offset_lod=(), seed=0,
+                dtype=2):
+    """Reference tdm_sampler (paddle/phi/kernels/cpu/tdm_sampler_kernel.cc): for every input item walk its
+    tree path (travel[item] = one positive node per layer, 0 = padding) and per layer emit the positive
+    (label 1) then ``neg_samples_num_list[l]`` distinct uniform negatives of that layer (label 0) that are not
+    the positive; padding layers emit zeros with mask 0.  Returns (out, labels, mask), each [N, sum(neg+pos)]."""
+    import numpy as np
+
+    ids = _raw(x).reshape(-1).long().tolist()
+    tr, ly = _raw(travel).long(), _raw(layer).reshape(-1).long()
+    L = len(neg_samples_num_list)
+    width = sum(n + int(output_positive) for n in neg_samples_num_list)
+    out = torch.zeros(len(ids), width, dtype=torch.int64)
+    lab, msk = torch.zeros_like(out), torch.zeros_like(out)
+    rng = np.random.default_rng(seed if seed else None)
+    for i, item in enumerate(ids):
+        off = 0
+        for l in range(L):
+            n = neg_samples_num_list[l]
+            lo, hi = layer_offset_lod[l], layer_offset_lod[l + 1]
+            pos = int(tr[item, l])
+            if pos == 0:
+                off += n + int(output_positive)
+                continue
+            if output_positive:
+                out[i, off], lab[i, off], msk[i, off] = pos, 1, 1
+                off += 1
+            cand = [j for j in range(hi - lo) if int(ly[lo + j]) != pos]
+            pick = rng.choice(len(cand), size=n, replace=False) if n else []
+            for p in pick:
+                out[i, off], msk[i, off] = int(ly[lo + cand[int(p)]]), 1
+                off += 1
+    cast = torch.int32 if dtype == 2 else torch.int64
+    return _wrap(out.to(cast)), _wrap(lab.to(cast)), _wrap(msk.to(cast))
+
+
+def _iou(a, b):
+    iw = max(min(a[2], b[2]) - max(a[0], b[0]), 0.0)
+    ih = max(min(a[3], b[3]) - max(a[1], b[1]), 0.0)
+    inter = iw * ih
+    union = (a[2] - a[0]) * (a[3] - a[1]) + (b[2] - b[0]) * (b[3] - b[1]) - inter
+    return inter / union if union > 0 else 0.0
+
+
+def detection_map(detect_res, label, has_state=None, pos_count=None, true_pos=None, false_pos=None, class_num=1,
+                  background_label=0, overlap_threshold=0.5, evaluate_difficult=True, ap_type="integral"):
+    """Reference detection_map (paddle/phi/kernels/cpu/detection_map_kernel.cc): LoD detections [M, 6] (label,
+    score, box) against LoD ground truth [N, 6] (label, difficult, box) or [N, 5]; greedy score-ordered matching
+    at IoU > overlap_threshold per class, then integral or VOC 11-point AP averaged over the classes with
+    positives.  State (accumulated over batches when has_state != 0): pos_count [C, 1] and per-class (score,
+    flag) lists true_pos / false_pos [K, 2] with a class LoD.  Returns (accum_pos_count, accum_true_pos,
+    accum_false_pos, m_ap)."""
+    from ..static.sequence import _offsets
+
+    det, gt = _raw(detect_res).double(), _raw(label).double()
+    dof, gof = _offsets(detect_res), _offsets(label)
+    pc = {c: 0 for c in range(class_num)}
+    tp = {c: [] for c in range(class_num)}
+    fp = {c: [] for c in range(class_num)}
+    if has_state is not None and int(_raw(has_state).reshape(-1)[0]) != 0:
+        for c, v in enumerate(_raw(pos_count).reshape(-1).tolist()):
+            pc[c] = int(v)
+        for store, t in ((tp, true_pos), (fp, false_pos)):
+            off = _offsets(t)
+            rows = _raw(t).double()
+            for c in range(len(off) - 1):
+                store[c] += [(float(rows[k, 0]), int(rows[k, 1])) for k in range(off[c], off[c + 1])]
+    wide = gt.shape[1] == 6
+    for n in range(len(gof) - 1):
+        gts = {}
+        for i in range(gof[n], gof[n + 1]):
+            c = int(gt[i, 0])
+            diff = bool(gt[i, 1] != 0) if wide else False
+            gts.setdefault(c, []).append((gt[i, 2:6].tolist() if wide else gt[i, 1:5].tolist(), diff))
+            if evaluate_difficult or not diff:
+                pc[c] = pc.get(c, 0) + 1
+        dets = {}
+        for i in range(dof[n], dof[n + 1]):
+            dets.setdefault(int(det[i, 0]), []).append((float(det[i, 1]), [min(max(v, 0.0), 1.0)
+                                                                           for v in det[i, 2:6].tolist()]))
+        for c, preds in dets.items():
+            tp.setdefault(c, []), fp.setdefault(c, [])
+            if c not in gts:
+                tp[c] += [(s, 0) for s, _ in preds]
+                fp[c] += [(s, 1) for s, _ in preds]
+                continue
+            seen = [False] * len(gts[c])
+            for s, box in sorted(preds, key=lambda t: -t[0]):
+                ious = [_iou(box, g) for g, _ in gts[c]]
+                j = max(range(len(ious)), key=lambda k: ious[k])
+                if ious[j] > overlap_threshold:
+                    if evaluate_difficult or not gts[c][j][1]:
+                        hit = not seen[j]
+                        seen[j] = True
+                        tp[c].append((s, int(hit)))
+                        fp[c].append((s, int(not hit)))
+                else:
+                    tp[c].append((s, 0))
+                    fp[c].append((s, 1))
+    m_ap, count = 0.0, 0
+    for c, npos in pc.items():
+        if npos == background_label:   # the reference compares the positive count (sic) with background_label
+            continue
+        if not tp.get(c):
+            count += 1
+            continue
+        t_sorted = [f for _, f in sorted(tp[c], key=lambda t: -t[0])]
+        f_sorted = [f for _, f in sorted(fp[c], key=lambda t: -t[0])]
+        ct = torch.tensor(t_sorted, dtype=torch.float64).cumsum(0)
+        cf = torch.tensor(f_sorted, dtype=torch.float64).cumsum(0)
+        prec = (ct / (ct + cf)).tolist()
+        rec = (ct / npos).tolist()
+        if ap_type == "11point":
+            mp = [0.0] * 11
+            start = len(rec) - 1
+            for j in range(10, -1, -1):
+                for i in range(start, -1, -1):
+                    if rec[i] < j / 10.0:
+                        start = i
+                        if j > 0:
+                            mp[j - 1] = mp[j]
+                        break
+                    mp[j] = max(mp[j], prec[i])
+            m_ap += sum(mp) / 11
+        else:
+            ap, prev = 0.0, 0.0
+            for p, r in zip(prec, rec):
+                if abs(r - prev) > 1e-6:
+                    ap += p * abs(r - prev)
+                prev = r
+            m_ap += ap
+        count += 1
+    m_ap = m_ap / count if count else 0.0
+
+    def pack(store):
+        rows, lod = [], [0]
+        for c in range(class_num):
+            rows += [[s, float(f)] for s, f in store.get(c, [])]
+            lod.append(len(rows))
+        t = _wrap(torch.tensor(rows, dtype=torch.float32).reshape(-1, 2))
+        t._lod = [lod]
+        return t
+
+    apc = _wrap(torch.tensor([[pc.get(c, 0)] for c in range(class_num)], dtype=torch.int32))
+    return apc, pack(tp), pack(fp), _wrap(torch.tensor([m_ap], dtype=torch.float32))
+
+
+def faster_tokenizer(vocab, text, text_pair=None, do_lower_case=False, is_split_into_words=False, max_seq_len=0,
+                     pad_to_max_seq_len=False):
+    """Reference faster_tokenizer (paddle/fluid/operators/string/faster_tokenizer_op.cc): BERT tokenisation --
+    basic split (whitespace, punctuation, CJK chars as words, optional lower-casing / accent stripping), greedy
+    longest-match WordPiece with ``##`` continuations, ``[CLS] a [SEP] (b [SEP])``, pair truncation of the
+    longer side to ``max_seq_len``, [PAD] padding.  ``vocab``: dict token -> id (the reference's Vocab
+    tensor); ``text`` / ``text_pair``: lists of strings.  Returns (input_ids, segment_ids) int64 [B, L]."""
+    import unicodedata
+
+    voc = dict(vocab)
+    unk, cls, sep, pad = (voc.get(t, 0) for t in ("[UNK]", "[CLS]", "[SEP]", "[PAD]"))
+
+    def basic(s):
+        if do_lower_case:
+            s = "".join(ch for ch in unicodedata.normalize("NFD", s.lower()) if unicodedata.category(ch) != "Mn")
+        toks, cur = [], ""
+        for ch in s:
+            cp = ord(ch)
+            punct = unicodedata.category(ch).startswith("P") or (33 <= cp <= 47 or 58 <= cp <= 64 or
+                                                                 91 <= cp <= 96 or 123 <= cp <= 126)
+            cjk = 0x4E00 <= cp <= 0x9FFF or 0x3400 <= cp <= 0x4DBF or 0xF900 <= cp <= 0xFAFF
+            if ch.isspace():
+                if cur:
+                    toks.append(cur)
+                cur = ""
+            elif punct or cjk:
+                if cur:
+                    toks.append(cur)
+                toks.append(ch)
+                cur = ""
+            else:
+                cur += ch
+        if cur:
+            toks.append(cur)
+        return toks
+
+    def wordpiece(w):
+        if len(w) > 100:
+            return [unk]
+        ids, start = [], 0
+        while start < len(w):
+            end = len(w)
+            while end > start:
+                piece = ("##" if start else "") + w[start:end]
+                if piece in voc:
+                    ids.append(voc[piece])
+                    break
+                end -= 1
+            if end == start:
+                return [unk]
+            start = end
+        return ids
+
+    def encode(s):
+        words = s if is_split_into_words else basic(s)
+        return [i for w in words for i in wordpiece(w)]
+
+    texts = [text] if isinstance(text, str) else list(text)
+    pairs = None if text_pair is None else ([text_pair] if isinstance(text_pair, str) else list(text_pair))
+    rows, segs = [], []
+    for k, s in enumerate(texts):
+        a = encode(s)
+        b = encode(pairs[k]) if pairs else None
+        if max_seq_len > 0:
+            budget = max_seq_len - (3 if b is not None else 2)
+            if b is None:
+                a = a[:max(budget, 0)]
+            else:
+                while len(a) + len(b) > budget:
+                    if len(a) >= len(b):
+                        a = a[:-1]
+                    else:
+                        b = b[:-1]
+        ids = [cls] + a + [sep]
+        sg = [0] * len(ids)
+        if b is not None:
+            ids += b + [sep]
+            sg += [1] * (len(b) + 1)
+        rows.append(ids)
+        segs.append(sg)
+    L = max(len(r) for r in rows)
+    if pad_to_max_seq_len and max_seq_len > 0:
+        L = max(L, max_seq_len)
+    ids_t = torch.full((len(rows), L), pad, dtype=torch.int64)
+    seg_t = torch.zeros(len(rows), L, dtype=torch.int64)
+    for i, (r, sg) in enumerate(zip(rows, segs)):
+        ids_t[i, :len(r)] = torch.tensor(r)
+        seg_t[i, :len(sg)] = torch.tensor(sg)
+    return _wrap(ids_t), _wrap(seg_t)
+
+
+_FUSION_GROUPS = {}
+
+
+def register_fusion_group(func_name, fn):
+    """Register the body of a fusion_group subgraph (the reference's fusion_group pass generates device code
+    for an elementwise subgraph and names it ``func_name``; here the body is a Python callable over torch
+    tensors, executed as one fused region -- on the GPU the elementwise chain is HBM-bound either way)."""
+    _FUSION_GROUPS[func_name] = fn
+
+
+def fusion_group(inputs, outs_dtype=(), inputs_dtype=(), func_name="", type=0):  # noqa: A002
+    """Reference fusion_group (paddle/phi/kernels/fusion/gpu/fusion_group_kernel.cu): run the registered
+    subgraph ``func_name`` over ``inputs``; outputs are cast to ``outs_dtype`` (0 = fp32, 1 = fp16, 2 = bf16,
+    as the pass encodes them)."""
+    if func_name not in _FUSION_GROUPS:
+        raise KeyError(f"fusion_group: no subgraph registered under {func_name!r} (register_fusion_group)")
+    outs = _FUSION_GROUPS[func_name](*[_raw(t) for t in inputs])
+    outs = list(outs) if isinstance(outs, (list, tuple)) else [outs]
+    code = {0: torch.float32, 1: torch.float16, 2: torch.bfloat16}
+    return [_wrap(o.to(code[outs_dtype[i]]) if i < len(outs_dtype) else o) for i, o in enumerate(outs)]
+
+
+def pyramid_hash(x, w, white_list=None, black_list=None, num_emb=0, space_len=0, pyramid_layer=2, rand_len=0,
+                 drop_out_percent=0.0, is_training=0, use_filter=True, white_list_len=0, black_list_len=0, seed=0,
+                 lr=0.0, distribute_update_vars=""):
+    """Reference pyramid_hash (paddle/phi/kernels/cpu/pyramid_hash_kernel.cc): every n-gram (2 <= n <=
+    pyramid_layer) of a LoD int32 sequence is hashed into the [space_len + rand_len] table ``w``; its num_emb
+    embedding is num_emb / rand_len chunks, chunk j (at column j) = w[h_j : h_j + rand_len] with
+    h_j = XXH32(n-gram int32 bytes, seed = j + seed) % space_len.  Black-listed n-grams (exact id sequences) are dropped;
+    with use_filter and a white list only listed ones are kept.  Returns (out [#ngrams, num_emb] with the
+    n-gram LoD, drop_pos, x_temp_out).  Hash-function parity with the reference's bloom-filter path is
+    unpinned (no reference binary runs here)."""
+    import xxhash
+
+    xr = _raw(x).reshape(-1).to(torch.int32)
+    wr = _raw(w).reshape(-1)
+    from ..static.sequence import _offsets
+
+    off = _offsets(x)
+
+    def _set(t):
+        if t is None:
+            return set()
+        return {tuple(r) for r in _raw(t).long().reshape(_raw(t).shape[0], -1).tolist()}
+
+    wl, bl = _set(white_list), _set(black_list)
+    rows, lod, drop = [], [0], []
+    for a, b in zip(off[:-1], off[1:]):
+        seq = xr[a:b]
+        n_rows = 0
+        for n in range(2, pyramid_layer + 1):
+            for s in range(0, (b - a) - n + 1):
+                g = seq[s:s + n]
+                key = tuple(g.tolist())
+                if key in bl or (use_filter and wl and key not in wl):
+                    continue
+                byts = g.numpy().tobytes()
+                emb = []
+                for j in range(0, num_emb, rand_len):
+                    h = xxhash.xxh32_intdigest(byts, seed=j + seed) % space_len
+                    emb.append(wr[h:h + rand_len])
+                rows.append(torch.cat(emb)[:num_emb])
+                n_rows += 1
+                drop.append(1)
+        if n_rows == 0:   # the reference emits one zero row for a sequence without n-grams
+            rows.append(torch.zeros(num_emb, dtype=wr.dtype))
+            drop.append(0)
+            n_rows = 1
+        lod.append(lod[-1] + n_rows)
+    out = _wrap(torch.stack(rows))
+    out._lod = [lod]
+    return out, _wrap(torch.tensor(drop, dtype=torch.int32)), _wrap(xr.clone())
+
+
+def distributed_fused_lamb_init(param, grad, beta1=0.9, beta2=0.999, apply_weight_decay=(), alignment=128, rank=0,
+                                nranks=1):
+    """Reference distributed_fused_lamb_init (fusion/gpu/distributed_fused_lamb_init_kernel.cu): pack the fp32
+    and 16-bit parameters (and grads) into aligned flat buffers, zero moments, beta-power scalars, per-param
+    offsets and this rank's shard offsets; param_out / master_param_out / grad_out are views into the flat
+    buffers (the parameters then live in them).  Returns the 18 outputs in the reference's order."""
+    ps, gs = [_raw(p) for p in param], [_raw(g) for g in grad]
+    fp32 = [i for i, p in enumerate(ps) if p.dtype == torch.float32]
+    half = [i for i, p in enumerate(ps) if p.dtype != torch.float32]
+
+    def layout(idx):
+        offs, n = [0], 0
+        for i in idx:
+            n += (ps[i].numel() + alignment - 1) // alignment * alignment
+            offs.append(n)
+        return offs
+
+    o32, o16 = layout(fp32), layout(half)
+    n32, n16 = o32[-1], o16[-1]
+    shard = lambda n: (n + nranks - 1) // nranks  # noqa: E731
+    fp32_param = torch.zeros(n32 + n16)               # masters of the 16-bit params follow the fp32 ones
+    fp32_grad = torch.zeros(n32)
+    fp16_param = torch.zeros(n16, dtype=ps[half[0]].dtype if half else torch.float16)
+    fp16_grad = torch.zeros_like(fp16_param)
+    param_out, master_out, grad_out = [None] * len(ps), [None] * len(ps), [None] * len(ps)
+    for k, i in enumerate(fp32):
+        a, m = o32[k], ps[i].numel()
+        fp32_param[a:a + m] = ps[i].reshape(-1)
+        fp32_grad[a:a + m] = gs[i].reshape(-1).float()
+        param_out[i] = master_out[i] = fp32_param[a:a + m].view(ps[i].shape)
+        grad_out[i] = fp32_grad[a:a + m].view(ps[i].shape)
+    for k, i in enumerate(half):
+        a, m = o16[k], ps[i].numel()
+        fp16_param[a:a + m] = ps[i].reshape(-1)
+        fp16_grad[a:a + m] = gs[i].reshape(-1).to(fp16_grad.dtype)
+        fp32_param[n32 + a:n32 + a + m] = ps[i].reshape(-1).float()
+        param_out[i] = fp16_param[a:a + m].view(ps[i].shape)
+        master_out[i] = fp32_param[n32 + a:n32 + a + m].view(ps[i].shape)
+        grad_out[i] = fp16_grad[a:a + m].view(ps[i].shape)
+    s32, s16 = shard(n32), shard(n16)
+    moment1 = torch.zeros(s32 + s16)
+    moment2 = torch.zeros(s32 + s16)
+    wd = [int(v) for v in (list(apply_weight_decay) or [1] * len(ps))]
+    info = torch.tensor([s32, s16, len(fp32), len(half), rank, nranks] + wd, dtype=torch.int32)
+    order = torch.tensor(fp32 + half, dtype=torch.int32)
+    offs = torch.tensor(o32 + [n32 + v for v in o16[1:]], dtype=torch.int32)
+    return tuple(_wrap(t) if not isinstance(t, list) else [_wrap(v) for v in t] for t in (
+        fp32_param, fp32_grad, fp16_param, fp16_grad, moment1, moment2, torch.tensor([beta1]),
+        torch.tensor([beta2]), offs, torch.tensor([rank * s32, min((rank + 1) * s32, n32)], dtype=torch.int32),
+        torch.tensor([rank * s16, min((rank + 1) * s16, n16)], dtype=torch.int32), info, order, param_out,
+        master_out, grad_out, torch.tensor([1.0]), torch.tensor([0], dtype=torch.int64)))
+
+
+def fused_dconv_drelu_dbn(grad_output, weight, grad_output_add=None, residual_input=None, bn1_eqscale=None,
+                          bn1_eqbias=None, conv_input=None, bn1_mean=None, bn1_inv_std=None, bn1_gamma=None,
+                          bn1_beta=None, bn1_input=None, bn2_mean=None, bn2_inv_std=None, bn2_gamma=None,
+                          bn2_beta=None, bn2_input=None, paddings=(0, 0), dilations=(1, 1), strides=(1, 1),
+                          padding_algorithm="EXPLICIT", groups=1, data_format="NHWC", fuse_shortcut=False,
+                          fuse_dual=False, fuse_add=False, exhaustive_search=False):
+    """Reference fused_dconv_drelu_dbn (fusion/gpu/fused_dconv_drelu_dbn_kernel.cu), the backward of the ResNet
+    unit: the conv's input was relu(bn1(bn1_input)) (+ bn2(bn2_input) with fuse_dual, + residual_input with
+    fuse_shortcut); given dL/d(conv out) returns (grad_weight, grad_bn1_input, grad_bn1_gamma, grad_bn1_beta,
+    grad_bn2_input, grad_bn2_gamma, grad_bn2_beta).  ``grad_output_add`` (fuse_add) is added to the gradient
+    arriving at the relu output.  Computed by autograd over the composed forward (NHWC)."""
+    nhwc = data_format == "NHWC"
+    f32 = lambda t: None if t is None else _raw(t).float()  # noqa: E731
+
+    def bn(inp, mean, inv, g, b):
+        return (inp - mean) * inv * g + b
+
+    x1 = f32(bn1_input).requires_grad_(True)
+    g1, b1 = f32(bn1_gamma).requires_grad_(True), f32(bn1_beta).requires_grad_(True)
+    pre = bn(x1, f32(bn1_mean), f32(bn1_inv_std), g1, b1)
+    x2 = g2 = b2 = None
+    if fuse_dual:
+        x2 = f32(bn2_input).requires_grad_(True)
+        g2, b2 = f32(bn2_gamma).requires_grad_(True), f32(bn2_beta).requires_grad_(True)
+        pre = pre + bn(x2, f32(bn2_mean), f32(bn2_inv_std), g2, b2)
+    elif fuse_shortcut and residual_input is not None:
+        pre = pre + f32(residual_input)
+    act = torch.relu(pre)
+    w = f32(weight).requires_grad_(True)
+    xc = act.permute(0, 3, 1, 2) if nhwc else act
+    wc = w.permute(0, 3, 1, 2) if nhwc else w
+    pad = "same" if padding_algorithm == "SAME" else (0 if padding_algorithm == "VALID" else tuple(paddings))
+    y = F.conv2d(xc, wc, None, tuple(strides), pad, tuple(dilations), groups)
+    dy = f32(grad_output)
+    dy = dy.permute(0, 3, 1, 2) if nhwc else dy
+    extra = f32(grad_output_add) if fuse_add and grad_output_add is not None else None
+    objs = [y] + ([act] if extra is not None else [])
+    grads = [dy] + ([extra] if extra is not None else [])
+    wrt = [w, x1, g1, b1] + ([x2, g2, b2] if fuse_dual else [])
+    gr = torch.autograd.grad(objs, wrt, grads)
+    dt = _raw(bn1_input).dtype
+    outs = [gr[0].to(_raw(weight).dtype), gr[1].to(dt), gr[2], gr[3]]
+    outs += [gr[4].to(dt), gr[5], gr[6]] if fuse_dual else [None, None, None]
+    return tuple(None if o is None else _wrap(o) for o in outs)

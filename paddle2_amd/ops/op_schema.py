@@ -280,7 +280,8 @@ for _n in ("nadam_", "radam_", "asgd_", "rprop_", "decayed_adagrad", "ftrl", "dp
            "fusion_gru", "fusion_lstm", "rank_attention", "qkv_unpack_mha", "match_matrix_tensor",
            "fusion_seqconv_eltadd_relu", "fusion_seqexpand_concat_fc", "fused_embedding_fc_lstm", "attention_lstm",
            "yolo_box_post", "p_send_array", "p_recv_array", "fused_scale_bias_relu_conv_bn",
-           "fused_multi_transformer_int8"):
+           "fused_multi_transformer_int8", "tdm_sampler", "detection_map", "faster_tokenizer", "fusion_group",
+           "pyramid_hash", "distributed_fused_lamb_init", "fused_dconv_drelu_dbn"):
     ALIASES.setdefault(_n, ("ops.extra_ops." + _n, {}))
 ALIASES.setdefault("nce", ("static.nn.nce", {}))
 ALIASES.setdefault("row_conv", ("static.nn.row_conv", {}))

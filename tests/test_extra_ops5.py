@@ -155,3 +155,81 @@ def test_p_send_recv_array_two_ranks():
     res = run_workers("p2p_array_worker.py", 2)
     assert res[1]["a"] == [[[0.0, 1.0, 2.0], [3.0, 4.0, 5.0]], [[1.0] * 3] * 2]
     assert res[1]["b_shapes"] == [[4], [2, 2, 2]] and res[1]["b_sum"] == [6.0, 24.0]
+
+
+def test_tdm_sampler_structure():
+    # tree: layer 1 nodes 1..2, layer 2 nodes 3..6; travel rows are per-item positive paths
+    travel = torch.tensor([[1, 3], [2, 6], [1, 0]])
+    layer = torch.tensor([1, 2, 3, 4, 5, 6])
+    out, lab, msk = E.tdm_sampler(paddle.to_tensor(torch.tensor([0, 1, 2])), paddle.to_tensor(travel),
+                                  paddle.to_tensor(layer), True, [1, 2], [0, 2, 6], seed=3)
+    o, l, m = out._t.tolist(), lab._t.tolist(), msk._t.tolist()
+    assert o[0][0] == 1 and l[0][:2] == [1, 0] and o[0][1] == 2
+    assert o[0][2] == 3 and set(o[0][3:]) <= {4, 5, 6} and len(set(o[0][3:])) == 2
+    assert o[2][2:] == [0, 0, 0] and m[2][2:] == [0, 0, 0] and m[1] == [1] * 5
+
+
+def test_detection_map_perfect_and_half():
+    gt = _lod(torch.tensor([[1, 0, .1, .1, .4, .4], [1, 0, .5, .5, .9, .9]]), [2])
+    det = _lod(torch.tensor([[1, .9, .1, .1, .4, .4], [1, .8, .5, .5, .9, .9]]), [2])
+    *_, m = E.detection_map(det, gt, class_num=2)
+    assert abs(float(m._t[0]) - 1.0) < 1e-6
+    det2 = _lod(torch.tensor([[1, .9, .1, .1, .4, .4], [1, .8, .0, .6, .1, .7]]), [2])
+    pc, tp, fp, m2 = E.detection_map(det2, gt, class_num=2)
+    assert abs(float(m2._t[0]) - 0.5) < 1e-6 and pc._t.reshape(-1).tolist() == [0, 2]
+    # accumulated state: the second batch equals the first -> same AP
+    *_, m3 = E.detection_map(det2, gt, paddle.to_tensor([1]), pc, tp, fp, class_num=2)
+    assert abs(float(m3._t[0]) - 0.5) < 1e-6
+    *_, m4 = E.detection_map(det2, gt, class_num=2, ap_type="11point")
+    assert abs(float(m4._t[0]) - 6 / 11) < 1e-6
+
+
+def test_faster_tokenizer_wordpiece():
+    voc = {t: i for i, t in enumerate(["[PAD]", "[UNK]", "[CLS]", "[SEP]", "hello", "world", "un", "##aff",
+                                       "##able", ",", "!"])}
+    ids, seg = E.faster_tokenizer(voc, ["Hello, unaffable world!"], ["hello"], do_lower_case=True,
+                                  max_seq_len=12, pad_to_max_seq_len=True)
+    assert ids._t.tolist()[0] == [2, 4, 9, 6, 7, 8, 5, 10, 3, 4, 3, 0]
+    assert seg._t.tolist()[0] == [0] * 9 + [1, 1, 0]
+    ids2, _ = E.faster_tokenizer(voc, ["xyz hello"])
+    assert ids2._t.tolist()[0] == [2, 1, 4, 3]
+
+
+def test_fusion_group_and_pyramid_hash_and_lamb_init():
+    E.register_fusion_group("fg_axpy", lambda a, b: (a * 2 + b, torch.relu(a - b)))
+    a, b = torch.randn(4), torch.randn(4)
+    o1, o2 = E.fusion_group([paddle.to_tensor(a), paddle.to_tensor(b)], [0, 2], func_name="fg_axpy")
+    assert torch.allclose(o1._t, a * 2 + b) and o2._t.dtype == torch.bfloat16
+    x = _lod(torch.tensor([[3], [5], [7], [1]], dtype=torch.int32), [3, 1])
+    w = torch.randn(64 + 4)
+    out, drop, _ = E.pyramid_hash(x, paddle.to_tensor(w), num_emb=8, space_len=64, pyramid_layer=3, rand_len=4,
+                                  use_filter=False)
+    assert out._t.shape == (4, 8) and out._lod == [[0, 3, 4]] and drop._t.tolist() == [1, 1, 1, 0]
+    out2, *_ = E.pyramid_hash(x, paddle.to_tensor(w), num_emb=8, space_len=64, pyramid_layer=3, rand_len=4,
+                              use_filter=False)
+    assert torch.equal(out._t, out2._t)   # deterministic hashing
+    ps = [paddle.to_tensor(torch.randn(3, 5)), paddle.to_tensor(torch.randn(7).half())]
+    gs = [paddle.to_tensor(torch.randn(3, 5)), paddle.to_tensor(torch.randn(7).half())]
+    res = E.distributed_fused_lamb_init(ps, gs, alignment=8, rank=0, nranks=2)
+    assert len(res) == 18 and torch.equal(res[13][0]._t, ps[0]._t) and torch.equal(res[14][1]._t, ps[1]._t.float())
+    assert res[0]._t.numel() == 16 + 8 and res[4]._t.numel() == 8 + 4
+
+
+def test_fused_dconv_drelu_dbn_matches_autograd_reference():
+    torch.manual_seed(8)
+    x = torch.randn(2, 4, 4, 3)
+    mean, var = x.mean((0, 1, 2)), x.var((0, 1, 2), unbiased=False)
+    inv = torch.rsqrt(var + 1e-5)
+    g, b = torch.rand(3) + 0.5, torch.randn(3)
+    w = torch.randn(5, 3, 3, 3)
+    dy = torch.randn(2, 4, 4, 5)
+    outs = E.fused_dconv_drelu_dbn(*(paddle.to_tensor(t) for t in (dy, w)), bn1_mean=paddle.to_tensor(mean),
+                                   bn1_inv_std=paddle.to_tensor(inv), bn1_gamma=paddle.to_tensor(g),
+                                   bn1_beta=paddle.to_tensor(b), bn1_input=paddle.to_tensor(x), paddings=(1, 1))
+    xr, wr, gr, br = (t.clone().requires_grad_(True) for t in (x, w, g, b))
+    a = torch.relu((xr - mean) * inv * gr + br)
+    y = torch.nn.functional.conv2d(a.permute(0, 3, 1, 2), wr.permute(0, 3, 1, 2), padding=1)
+    y.backward(dy.permute(0, 3, 1, 2))
+    for o, r in zip(outs[:4], (wr.grad, xr.grad, gr.grad, br.grad)):
+        assert torch.allclose(o._t, r, atol=1e-4)
+    assert outs[4] is None
