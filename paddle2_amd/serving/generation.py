@@ -7,6 +7,11 @@ processes one token per sequence with the flash-decoding kernel.  The decode ste
 shapes (fixed batch, device-side positions / sequence lengths / block tables, no host syncs),
 so it is captured once with ``torch.cuda.CUDAGraph`` (a hipGraph on ROCm) and replayed: one
 graph launch instead of ~10 kernel launches per layer per token.
+
+Weights are static during generation, so every projection keeps a one-time transposed [N, K] copy
+(``weight_layout="nk"``, the default on the GPU): hipBLASLt streams that layout ~1.5x faster at decode
+shapes (M = batch; qkv 2.8 -> 4.0 TB/s, down_proj 1.1 -> 2.7 TB/s, profiles/r3_decode_gemm_layouts.jsonl)
+for 13.5 GB of extra HBM on a 288 GB part.
 """
 from __future__ import annotations
 
@@ -35,7 +40,8 @@ def sample_logits(logits, temperature=1.0, top_k=0, top_p=1.0, generator=None):
 
 
 class LlamaGenerator:
-    def __init__(self, model, max_batch=8, max_seq_len=4096, block_size=64, num_blocks=None, use_graph=True):
+    def __init__(self, model, max_batch=8, max_seq_len=4096, block_size=64, num_blocks=None, use_graph=True,
+                 weight_layout=None):
         self.model = model
         cfg = model.config
         self.cfg = cfg
@@ -58,6 +64,24 @@ class LlamaGenerator:
         self._pos = torch.zeros(max_batch, dtype=torch.int32, device=dev)
         self._lens = torch.zeros(max_batch, dtype=torch.int32, device=dev)
         self._logits = None
+        import os
+
+        self.weight_layout = (weight_layout or os.environ.get("PADDLE2_AMD_SERVING_LAYOUT")
+                              or ("nk" if dev.type == "cuda" else "kn"))
+        self._wt = {}
+
+    def _mm(self, x, param):
+        """x @ W for a Paddle-layout W [K, N]; with the "nk" layout through a cached contiguous W^T (rebuilt
+        if the parameter's storage or version changes)."""
+        w = param._t
+        if self.weight_layout != "nk":
+            return torch.matmul(x, w)
+        key = id(param)
+        ent = self._wt.get(key)
+        if ent is None or ent[0] != w.data_ptr() or ent[1] != w._version:
+            ent = (w.data_ptr(), w._version, T.transpose2d(w))
+            self._wt[key] = ent
+        return torch.matmul(x, ent[2].t())
 
     # ------------------------------------------------------------------ layer pieces
     def _layer_qkv(self, layer, x, residual):
@@ -66,18 +90,18 @@ class LlamaGenerator:
             h = T.rms_norm(x, layer.input_layernorm.weight._t, self.cfg.rms_norm_eps)
         else:
             h, residual = T.rms_norm(x, layer.input_layernorm.weight._t, self.cfg.rms_norm_eps, residual)
-        qkv = torch.matmul(h, layer.self_attn.qkv_proj.weight._t)
+        qkv = self._mm(h, layer.self_attn.qkv_proj.weight)
         return qkv, residual
 
     def _layer_out(self, layer, o, residual):
-        a = torch.matmul(o, layer.self_attn.o_proj.weight._t)
+        a = self._mm(o, layer.self_attn.o_proj.weight)
         h, residual = T.rms_norm(a, layer.post_attention_layernorm.weight._t, self.cfg.rms_norm_eps, residual)
-        f = T.swiglu(torch.matmul(h, layer.mlp.gate_up_fused_proj.weight._t))
-        return torch.matmul(f, layer.mlp.down_proj.weight._t), residual
+        f = T.swiglu(self._mm(h, layer.mlp.gate_up_fused_proj.weight))
+        return self._mm(f, layer.mlp.down_proj.weight), residual
 
     def _logits_of(self, h, residual):
         out, _ = T.rms_norm(h, self.model.llama.norm.weight._t, self.cfg.rms_norm_eps, residual)
-        return torch.matmul(out, self.model.lm_head.weight._t)
+        return self._mm(out, self.model.lm_head.weight)
 
     # ------------------------------------------------------------------ prefill
     @torch.no_grad()

@@ -109,6 +109,24 @@ def test_generation_matches_full_recompute_cpu():
         assert o == greedy_reference(m, p, 6)
 
 
+def test_generation_transposed_weight_layout_cpu():
+    """weight_layout="nk" (the GPU default: cached W^T per projection) generates the same tokens, and the
+    cache follows in-place weight updates (version bump)."""
+    from paddle2_amd.serving.generation import LlamaGenerator, greedy_reference
+
+    m = _tiny_llama("cpu")
+    gen = LlamaGenerator(m, max_batch=2, max_seq_len=64, block_size=8, use_graph=False, weight_layout="nk")
+    prompts = [[1, 5, 9, 3], [7, 2]]
+    assert gen.generate(prompts, max_new_tokens=6) == [greedy_reference(m, p, 6) for p in prompts]
+    assert len(gen._wt) > 0
+    w = m.lm_head.weight
+    with torch.no_grad():
+        w._t.mul_(-1.0)
+    gen2 = LlamaGenerator(m, max_batch=2, max_seq_len=64, block_size=8, use_graph=False, weight_layout="nk")
+    gen2._wt = gen._wt
+    assert gen2.generate(prompts[:1], max_new_tokens=4) == [greedy_reference(m, prompts[0], 4)]
+
+
 @pytest.mark.gpu
 def test_generation_hip_graph_gpu():
     from paddle2_amd.serving.generation import LlamaGenerator, greedy_reference
