@@ -764,8 +764,9 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   if (epi == kEpiSwiGLU && H % 32) return -3;
   hipStream_t st = (hipStream_t)stream;
   // v7 (gemm7.hip): the TN schedule, variants 7..10 = its SCHED 0..3; problems outside its domain run v6
-  if (variant >= 7 && variant <= 10) {
-    if (pd_gemm_v7(p, layout, epi, variant - 7, 8 * p.cpx, st)) return (int)hipGetLastError();
+  if ((variant >= 7 && variant <= 10) || variant >= 64) {
+    if (pd_gemm_v7(p, layout, epi, variant >= 64 ? variant - 64 : variant - 7, 8 * p.cpx, st))
+      return (int)hipGetLastError();
     variant = 6;
   }
   if (epi == kEpiSwiGLU && bk) return -3;  // K-major gate|up weight: v7 only

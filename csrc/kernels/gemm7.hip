@@ -52,28 +52,41 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 // one MFMA with an LDS-DMA piece behind it: M0 (LDS destination = wb + IMM) is written before the MFMA, which
-// covers the M0 -> buffer_load ... lds hazard
-template <int IMM>
+// covers the M0 -> buffer_load ... lds hazard.  POL = the load's cache policy (SCHED bits 2-3 for A, 4-5 for B):
+// 0 default, 1 sc0 sc1 (L1 bypass), 2 nt (streaming), 3 sc1.
+#define PD_V7_MFMA_DMA(POLSTR)                                        \
+  asm volatile(                                                      \
+      "s_add_u32 m0, %1, %2\n\t"                                     \
+      "v_mfma_f32_16x16x32_bf16 %0, %3, %4, %0\n\t"                  \
+      "buffer_load_dwordx4 %5, %6, 0 offen" POLSTR " lds"             \
+      : "+a"(c)                                                      \
+      : "s"(wb), "i"(IMM), "v"(a), "v"(b), "v"(voff), "s"(srd)       \
+      : "memory")
+#define PD_V7_DMA_ONLY(POLSTR)                                        \
+  asm volatile(                                                      \
+      "s_add_u32 m0, %0, %1\n\t"                                     \
+      "s_nop 0\n\t"                                                  \
+      "buffer_load_dwordx4 %2, %3, 0 offen" POLSTR " lds"             \
+      :                                                              \
+      : "s"(wb), "i"(IMM), "v"(voff), "s"(srd)                       \
+      : "memory")
+template <int IMM, int POL = 0>
 __device__ __forceinline__ void mfma_dma(f32x4v& c, const bf16x8& a, const bf16x8& b, unsigned wb, unsigned voff,
                                          const i32x4& srd) {
-  asm volatile(
-      "s_add_u32 m0, %1, %2\n\t"
-      "v_mfma_f32_16x16x32_bf16 %0, %3, %4, %0\n\t"
-      "buffer_load_dwordx4 %5, %6, 0 offen lds"
-      : "+a"(c)
-      : "s"(wb), "i"(IMM), "v"(a), "v"(b), "v"(voff), "s"(srd)
-      : "memory");
+  if constexpr (POL == 1) PD_V7_MFMA_DMA(" sc0 sc1");
+  else if constexpr (POL == 2) PD_V7_MFMA_DMA(" nt");
+  else if constexpr (POL == 3) PD_V7_MFMA_DMA(" sc1");
+  else PD_V7_MFMA_DMA("");
 }
-template <int IMM>
+template <int IMM, int POL = 0>
 __device__ __forceinline__ void dma_only(unsigned wb, unsigned voff, const i32x4& srd) {
-  asm volatile(
-      "s_add_u32 m0, %0, %1\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %2, %3, 0 offen lds"
-      :
-      : "s"(wb), "i"(IMM), "v"(voff), "s"(srd)
-      : "memory");
+  if constexpr (POL == 1) PD_V7_DMA_ONLY(" sc0 sc1");
+  else if constexpr (POL == 2) PD_V7_DMA_ONLY(" nt");
+  else if constexpr (POL == 3) PD_V7_DMA_ONLY(" sc1");
+  else PD_V7_DMA_ONLY("");
 }
+#undef PD_V7_MFMA_DMA
+#undef PD_V7_DMA_ONLY
 
 // LDS byte offset (from the wave's piece base) of piece j of operand B? in stage ST
 template <bool ISB, int ST, int J>
@@ -84,6 +97,8 @@ constexpr int piece_dst() {
 template <int EPI, int SCHED>
 __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   constexpr bool BAR4 = SCHED & 1, PRIO = (SCHED & 2) != 0;
+  constexpr int PA = (SCHED >> 2) & 3, PB = (SCHED >> 4) & 3;  // LDS-DMA cache policy of A / B (see mfma_dma)
+  constexpr int PLVL = (SCHED & 64) ? 3 : 1;                    // s_setprio level around the MFMA stream
   constexpr bool SWI = EPI == kEpiSwiGLU;
   __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
   const unsigned sbase = (unsigned)(size_t)(lds_char*)smem_raw;
@@ -164,20 +179,20 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
     descs(0, sa, sb);
     sfor<8>([&](auto J) {
       constexpr int j = decltype(J)::value;
-      dma_only<piece_dst<true, 0, j>()>(wdst, vb[j], sb);
+      dma_only<piece_dst<true, 0, j>(), PB>(wdst, vb[j], sb);
     });
     sfor<8>([&](auto J) {
       constexpr int j = decltype(J)::value;
-      dma_only<piece_dst<false, 0, j>()>(wdst, va[j], sa);
+      dma_only<piece_dst<false, 0, j>(), PA>(wdst, va[j], sa);
     });
     descs(1, sa, sb);
     sfor<8>([&](auto J) {
       constexpr int j = decltype(J)::value;
-      dma_only<piece_dst<true, 1, j>()>(wdst, vb[j], sb);
+      dma_only<piece_dst<true, 1, j>(), PB>(wdst, vb[j], sb);
     });
     sfor<8>([&](auto J) {
       constexpr int j = decltype(J)::value;
-      dma_only<piece_dst<false, 1, j>()>(wdst, va[j], sa);
+      dma_only<piece_dst<false, 1, j>(), PA>(wdst, va[j], sa);
     });
   }
   wait_vm<16>();
@@ -195,7 +210,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   auto ktile = [&](auto ST, int k) {
     constexpr int st = decltype(ST)::value;
     i32x4 sa, sb;
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(PLVL);
     sfor<128>([&](auto Q) {
       constexpr int q = decltype(Q)::value;
       constexpr int qq = q & 63, i = qq >> 3, j = qq & 7;
@@ -212,7 +227,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
         if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
         wait_lgkm<0>();
         __builtin_amdgcn_s_barrier();
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(PLVL);
         __builtin_amdgcn_sched_barrier(0);
       }
       if constexpr (q == LND_B || q == LND_A) {
@@ -221,7 +236,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
         if constexpr (q == LND_B && BAR4) wait_vm<24>();
         else wait_vm<16>();
         __builtin_amdgcn_s_barrier();
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(PLVL);
         __builtin_amdgcn_sched_barrier(0);
       }
       // ---- MFMA q (A-fragment-major; B fragment as src0: the transposed tile, 4 columns per lane)
@@ -232,10 +247,10 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
       constexpr bool pa_ = q >= DMA_A && q < DMA_A + 16 && (q - DMA_A) % 2 == 0;
       if constexpr (pb_) {
         constexpr int pj = (q - DMA_B) / 2;
-        mfma_dma<piece_dst<true, st, pj>()>(c, fb[j], fa[i], wdst, vb[pj], sb);
+        mfma_dma<piece_dst<true, st, pj>(), PB>(c, fb[j], fa[i], wdst, vb[pj], sb);
       } else if constexpr (pa_) {
         constexpr int pj = (q - DMA_A) / 2;
-        mfma_dma<piece_dst<false, st, pj>()>(c, fb[j], fa[i], wdst, va[pj], sa);
+        mfma_dma<piece_dst<false, st, pj>(), PA>(c, fb[j], fa[i], wdst, va[pj], sa);
       } else {
         mfma_agpr(c, fb[j], fa[i]);
       }
@@ -307,18 +322,30 @@ bool pd_gemm_v7(const pd::gm::Params& p, int layout, int epi, int sched, int cus
   if (a_bytes <= 0 || b_bytes <= 0 || a_bytes >= 0x7fffffffL || b_bytes >= 0x7fffffffL) return false;
   if (p.ldc % 4 || (size_t)p.C % 16 || (p.C2 && (p.ldc2 % 4 || (size_t)p.C2 % 16))) return false;
   const dim3 grid(std::min(p.tiles_m * p.tiles_n, cus));
-#define PD_V7(E)                                                                        \
-  switch (sched & 3) {                                                                  \
-    case 0: gemm_v7_kernel<E, 0><<<grid, NTHR4, 0, st>>>(p); break;                     \
-    case 1: gemm_v7_kernel<E, 1><<<grid, NTHR4, 0, st>>>(p); break;                     \
-    case 2: gemm_v7_kernel<E, 2><<<grid, NTHR4, 0, st>>>(p); break;                     \
-    default: gemm_v7_kernel<E, 3><<<grid, NTHR4, 0, st>>>(p); break;                    \
+  // SCHED 0..3 = variants 7..10; the experiment configurations (cache policy / priority level, variant 64 + cfg)
+  // are instantiated for the bf16 epilogue only
+#define PD_V7_CASE(E, S) \
+  case S: gemm_v7_kernel<E, S><<<grid, NTHR4, 0, st>>>(p); break;
+#define PD_V7(E)                                                        \
+  switch (sched) {                                                      \
+    PD_V7_CASE(E, 0) PD_V7_CASE(E, 1) PD_V7_CASE(E, 2) PD_V7_CASE(E, 3) \
+    default: return false;                                              \
+  }
+  if (epi == kEpiBF16 && sched > 3) {
+    switch (sched) {
+      PD_V7_CASE(kEpiBF16, 6) PD_V7_CASE(kEpiBF16, 18) PD_V7_CASE(kEpiBF16, 22) PD_V7_CASE(kEpiBF16, 10)
+      PD_V7_CASE(kEpiBF16, 42) PD_V7_CASE(kEpiBF16, 66) PD_V7_CASE(kEpiBF16, 86) PD_V7_CASE(kEpiBF16, 20)
+      PD_V7_CASE(kEpiBF16, 14)
+      default: return false;
+    }
+    return true;
   }
   if (epi == kEpiBF16) {
     PD_V7(kEpiBF16)
   } else {
     PD_V7(kEpiSwiGLU)
   }
+#undef PD_V7_CASE
 #undef PD_V7
   return true;
 }

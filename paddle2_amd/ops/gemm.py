@@ -95,7 +95,8 @@ def _launch(layout, epi, a, lda, b, ldb, c, ldc, c2, ldc2, bias, M, Nn, K, beta=
 
 def _v7(name, K):
     """The pass runs the TN schedule (v7) on this reduction length."""
-    return 7 <= _variant(name) <= 10 and K % 128 == 0
+    v = _variant(name)
+    return (7 <= v <= 10 or v >= 64) and K % 128 == 0
 
 
 def _wt(w):
