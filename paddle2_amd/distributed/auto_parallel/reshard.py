@@ -121,8 +121,10 @@ def reshard_local(local, mesh, src, dst, backward=False):
             else:
                 x = _all_reduce(x, _red_name(s), mesh, d)
                 cur[d] = _TReplicate()
-    # 2. shard moves: s->s (all-to-all) when the target axis is free, else s->r (all-gather)
-    for d in range(nd):
+    # 2. shard moves: s->s (all-to-all) when the target axis is free, else s->r (all-gather).  Innermost mesh dim
+    #    first (reference nd_mesh_reshard_function.cc:149): a tensor axis sharded over several mesh dims was split
+    #    outer dim first, so it must be gathered inner dim first or the pieces come back interleaved.
+    for d in reversed(range(nd)):
         s, t = cur[d], dst[d]
         if isinstance(s, _TShard) and s != t:
             if isinstance(t, _TShard) and not any(isinstance(c, _TShard) and c.dim == t.dim

@@ -279,21 +279,29 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     return _wrap(out.reshape(tok, Hq * D)), qkv, key_cache, value_cache
 
 
-_WT_CACHE = {}
-
-
 def _static_mm(x, w):
-    """x @ W for a static inference weight W [K, N]: on the GPU through a cached contiguous W^T, the layout
-    hipBLASLt streams fastest at decode shapes (profiles/r3_decode_gemm_layouts.jsonl).  The entry keeps W
-    alive and is rebuilt when W's storage or version changes."""
+    """x @ W for a static inference weight W [K, N]: on the GPU through a contiguous W^T, the layout hipBLASLt
+    streams fastest at decode shapes (profiles/r3_decode_gemm_layouts.jsonl).  The transposed copy is attached to
+    W itself (attribute ``_pd_wt``), so it lives exactly as long as W does — nothing global holds W — and it is
+    re-transposed in place when W's version changes (``clear_static_weight_cache`` drops it)."""
     if not w.is_cuda or w.dim() != 2:
         return torch.matmul(x, w)
-    key = (w.data_ptr(), tuple(w.shape), w.dtype)
-    ent = _WT_CACHE.get(key)
-    if ent is None or ent[0] is not w or ent[1] != w._version:
-        ent = (w, w._version, T.transpose2d(w))
-        _WT_CACHE[key] = ent
-    return torch.matmul(x, ent[2].t())
+    ent = getattr(w, "_pd_wt", None)
+    if ent is None or ent[1].shape != (w.shape[1], w.shape[0]):
+        ent = [w._version, T.transpose2d(w)]
+        w._pd_wt = ent
+    elif ent[0] != w._version:
+        ent[1].copy_(w.t())
+        ent[0] = w._version
+    return torch.matmul(x, ent[1].t())
+
+
+def clear_static_weight_cache(*weights):
+    """Drop the transposed copies that ``_static_mm`` attached to ``weights`` (paddle or torch tensors)."""
+    for w in weights:
+        t = getattr(w, "_t", w)
+        if hasattr(t, "_pd_wt"):
+            del t._pd_wt
 
 
 @torch.no_grad()

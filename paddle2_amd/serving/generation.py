@@ -71,17 +71,42 @@ class LlamaGenerator:
         self._wt = {}
 
     def _mm(self, x, param):
-        """x @ W for a Paddle-layout W [K, N]; with the "nk" layout through a cached contiguous W^T (rebuilt
-        if the parameter's storage or version changes)."""
+        """x @ W for a Paddle-layout W [K, N]; with the "nk" layout through a cached contiguous W^T.
+
+        A parameter whose storage or version changed (set_state_dict, an in-place update) is re-transposed INTO
+        the cached buffer, so a captured decode graph that reads that buffer stays valid and sees the new
+        weights; only a shape change replaces the buffer, and then the graph is dropped and re-captured."""
         w = param._t
         if self.weight_layout != "nk":
             return torch.matmul(x, w)
         key = id(param)
         ent = self._wt.get(key)
-        if ent is None or ent[0] != w.data_ptr() or ent[1] != w._version:
-            ent = (w.data_ptr(), w._version, T.transpose2d(w))
-            self._wt[key] = ent
+        if ent is None:
+            if not self._wt and not self._nk_fits():
+                self.weight_layout = "kn"  # no room for a transposed copy of every projection
+                return torch.matmul(x, w)
+            ent = self._wt[key] = [w.data_ptr(), w._version, T.transpose2d(w)]
+        elif ent[0] != w.data_ptr() or ent[1] != w._version:
+            if ent[2].shape == (w.shape[1], w.shape[0]) and ent[2].dtype == w.dtype:
+                ent[2].copy_(w.t())
+            else:
+                ent[2] = T.transpose2d(w)
+                self._graph = None
+            ent[0], ent[1] = w.data_ptr(), w._version
         return torch.matmul(x, ent[2].t())
+
+    def _nk_fits(self):
+        """The transposed copies (one per projection weight) fit in free device memory with a 10 % margin."""
+        if self.dev.type != "cuda":
+            return True
+        need = 0
+        for layer in self.model.llama.layers:
+            for lin in (layer.self_attn.qkv_proj, layer.self_attn.o_proj, layer.mlp.gate_up_fused_proj,
+                        layer.mlp.down_proj):
+                need += lin.weight._t.numel() * lin.weight._t.element_size()
+        need += self.model.lm_head.weight._t.numel() * self.model.lm_head.weight._t.element_size()
+        free, _ = torch.cuda.mem_get_info(self.dev)
+        return need * 1.1 < free
 
     # ------------------------------------------------------------------ layer pieces
     def _layer_qkv(self, layer, x, residual):

@@ -143,6 +143,83 @@ def test_generation_hip_graph_gpu():
         assert o[:3] == ref[:3], (o, ref)
 
 
+@pytest.mark.gpu
+def test_generation_graph_follows_weight_update_gpu():
+    """A captured decode graph reads the cached W^T buffers; an in-place weight update between two generate()
+    calls is re-transposed into those same buffers, so the replayed graph uses the new weights (no stale /
+    freed W^T)."""
+    from paddle2_amd.serving.generation import LlamaGenerator, greedy_reference
+
+    paddle.set_device("gpu:0")
+    m = _tiny_llama("cuda")
+    prompts = [[1, 5, 9, 3, 11, 4], [7, 2, 8]]
+    gen = LlamaGenerator(m, max_batch=2, max_seq_len=128, block_size=16, use_graph=True, weight_layout="nk")
+    gen.generate(prompts, 6)
+    assert gen._graph is not None
+    bufs = {k: v[2].data_ptr() for k, v in gen._wt.items()}
+    with torch.no_grad():
+        m.lm_head.weight._t.mul_(-1.0)
+        m.llama.layers[0].mlp.down_proj.weight._t.mul_(0.5)
+    out = gen.generate(prompts, 6)
+    assert {k: v[2].data_ptr() for k, v in gen._wt.items()} == bufs   # updated in place, same addresses
+    eager = LlamaGenerator(m, max_batch=2, max_seq_len=128, block_size=16, use_graph=False,
+                           weight_layout="kn").generate(prompts, 6)
+    assert out == eager
+    for p, o in zip(prompts, out):
+        assert o[:3] == greedy_reference(m, p, 6)[:3]
+
+
+def test_static_mm_cache_lives_on_the_weight():
+    """fused_multi_transformer's W^T copies hang off the weight tensor (no module-global cache pinning weights)
+    and follow in-place updates; clear_static_weight_cache drops them."""
+    import gc
+    import weakref
+
+    from paddle2_amd.serving import _static_mm, clear_static_weight_cache
+
+    if not torch.cuda.is_available():
+        w = torch.randn(8, 4)
+        x = torch.randn(3, 8)
+        torch.testing.assert_close(_static_mm(x, w), x @ w)   # CPU: plain matmul, nothing attached
+        assert not hasattr(w, "_pd_wt")
+        return
+    w = torch.randn(64, 32, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(5, 64, device="cuda", dtype=torch.bfloat16)
+    torch.testing.assert_close(_static_mm(x, w).float(), (x.float() @ w.float()), atol=5e-2, rtol=2e-2)
+    buf = w._pd_wt[1].data_ptr()
+    with torch.no_grad():
+        w.mul_(2.0)
+    torch.testing.assert_close(_static_mm(x, w).float(), (x.float() @ w.float()), atol=1e-1, rtol=2e-2)
+    assert w._pd_wt[1].data_ptr() == buf
+    ref = weakref.ref(w)
+    del w
+    gc.collect()
+    assert ref() is None   # nothing global kept the weight alive
+    w2 = torch.randn(64, 32, device="cuda", dtype=torch.bfloat16)
+    _static_mm(x, w2)
+    clear_static_weight_cache(w2)
+    assert not hasattr(w2, "_pd_wt")
+
+
+@pytest.mark.gpu
+def test_fused_multi_transformer_gpu_matches_cpu():
+    """The GPU fused_multi_transformer (cached W^T projections, native decode kernels) matches the CPU op."""
+    from paddle2_amd.incubate.nn import FusedMultiTransformer
+
+    paddle.seed(0)
+    layer = FusedMultiTransformer(128, 4, 256, num_layers=2, activation="gelu")
+    b, s, nh, hd = 2, 6, 4, 32
+    x = paddle.randn([b, s, 128])
+    caches = [paddle.zeros([2, b, nh, 16, hd]) for _ in range(2)]
+    ref, _ = layer(x, caches=caches)
+    paddle.set_device("gpu:0")
+    layer.to(device="gpu:0")
+    xg = paddle.to_tensor(x._t.cuda())
+    cg = [paddle.zeros([2, b, nh, 16, hd]) for _ in range(2)]
+    out, _ = layer(xg, caches=cg)
+    torch.testing.assert_close(out._t.float().cpu(), ref._t.float(), atol=2e-3, rtol=2e-3)
+
+
 def test_fused_multi_transformer_decode_matches_context():
     from paddle2_amd.incubate.nn import FusedMultiTransformer
 

@@ -120,3 +120,13 @@ def test_cross_mesh_reshard_four_ranks():
             assert o["same_status"]["local"] == [] and o["same_status"]["comm"] == ["send"]
             assert "all_gather" in o["general"]["comm"]
             assert o["back"] == g.tolist()
+
+
+def test_nested_same_axis_shard_to_replicate_four_ranks():
+    """[Shard(0), Shard(0)] on a 2x2 mesh -> replicated keeps the row order (the advisor's interleave case)."""
+    res = run_workers("nested_shard_worker.py", 4)
+    g = np.arange(48, dtype="float32").reshape(8, 6)
+    for r, o in enumerate(res):
+        assert o["local"] == g[2 * r: 2 * r + 2].tolist()   # rank (i, j) = chunk j of chunk i = rows 2(2i+j)..
+        assert o["full"] == g.tolist()
+        assert o["again"] == o["local"]
