@@ -94,11 +94,53 @@ constexpr int piece_dst() {
   return ST * TILE_BYTES + (8 * (J & 3) + 4 * (J >> 2)) * 1024 + (ISB ? B_OFF : 0);
 }
 
+// bf16 epilogue of an interior tile with 16-B stores (SCHED bit 8).  A lane holds 4 consecutive columns of one row
+// per 16x16 accumulator (transposed MFMA tile: row = lane & 15, columns 4 (lane >> 4) ..); packing two row blocks
+// (2q, 2q + 1) and swapping lanes 16-31 / 48-63 of the first with lanes 0-15 / 32-47 of the second
+// (v_permlane16_swap) gives every lane 8 consecutive columns of one row: lanes 0-15 block 2q columns 0-7, 16-31
+// block 2q+1 columns 0-7, 32-47 block 2q columns 8-15, 48-63 block 2q+1 columns 8-15 — one dwordx4 store per pair
+// of row blocks and column tile instead of two dwordx2 (cdna_hip_programming.md T21, with the 16-lane swap that
+// matches the 16x16 layout).  Bias is added before the packing.
+__device__ __forceinline__ unsigned pack_bf2(float a, float b) {
+  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+}
+__device__ __forceinline__ void epilogue_v7_x4(const Params& p, f32x4v (&acc)[8][4], int tm, int tn, int arow,
+                                               int bcolw, int lane) {
+  unsigned short* C = (unsigned short*)p.C;
+  const int sub = (lane >> 4) & 1;                // which block of the pair this lane stores
+  const int r = lane & 15;
+  const int ch = 8 * (lane >> 5);                 // column half of the 16-column tile
+  const long row_base = (long)tm * BM + arow + r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c0 = tn * BN + bcolw + 16 * j;      // first column of tile j
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias) {
+      const int cb = c0 + 4 * (lane >> 4);        // this lane's 4 columns before the swap
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[e] = bf2f(p.bias[cb + e]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4v& a = acc[2 * q][j];
+      const f32x4v& b = acc[2 * q + 1][j];
+      unsigned x0 = pack_bf2(a[0] + bv[0], a[1] + bv[1]), x1 = pack_bf2(a[2] + bv[2], a[3] + bv[3]);
+      unsigned y0 = pack_bf2(b[0] + bv[0], b[1] + bv[1]), y1 = pack_bf2(b[2] + bv[2], b[3] + bv[3]);
+      auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+      auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+      const long row = row_base + 16 * (2 * q + sub);
+      *(uint4*)(C + row * p.ldc + c0 + ch) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    }
+  }
+}
+
 template <int EPI, int SCHED>
 __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   constexpr bool BAR4 = SCHED & 1, PRIO = (SCHED & 2) != 0;
   constexpr int PA = (SCHED >> 2) & 3, PB = (SCHED >> 4) & 3;  // LDS-DMA cache policy of A / B (see mfma_dma)
   constexpr int PLVL = (SCHED & 64) ? 3 : 1;                    // s_setprio level around the MFMA stream
+  constexpr bool VS = (SCHED & 128) != 0;                        // the three-barrier spread schedule (ktile_v)
+  constexpr bool X4 = (SCHED & 256) != 0;                        // 16-B epilogue stores on interior tiles
   constexpr bool SWI = EPI == kEpiSwiGLU;
   __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
   const unsigned sbase = (unsigned)(size_t)(lds_char*)smem_raw;
@@ -200,6 +242,10 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   __builtin_amdgcn_sched_barrier(0);
   sfor<8>([&](auto U) { xb[decltype(U)::value] = frag4<true, decltype(U)::value, 0, 0>(rb); });
   sfor<8>([&](auto U) { xa[decltype(U)::value] = frag4<true, decltype(U)::value, 0, 0>(ra); });
+  if constexpr (VS) {
+    wait_lgkm<0>();
+    __builtin_amdgcn_sched_barrier(0);
+  }
 
   // slot positions (MFMA index q of the K-tile, 0..127)
   constexpr int REL_B = BAR4 ? 16 : 32, REL_A = 32;        // stage release barriers (before MFMA q)
@@ -287,16 +333,111 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
+  // SCHED bit 7: the spread schedule — per K-tile (MFMA index n = 0..127, B-fragment-major order, "before MFMA n"):
+  //   step-1 A fragments at n = 1, 3, .., 15; lgkmcnt(0) + barrier at 21 (A's half of the stage released);
+  //   A pieces 0-4 of tile t+2 at 23, 26, .., 35 beside the step-1 B fragments (25 .. 43); lgkmcnt(0) + barrier at
+  //   51 (B released); A pieces 5-7 at 53, 56, 59, B pieces 0-4 at 62, 65, 86, 88, 90; vmcnt(13) + barrier at 92
+  //   (tile t+1 landed: only this tile's 13 pieces stay in flight); tile t+1's step-0 fragments from 94 (A) and
+  //   106 (B) with B pieces 5-7 at 97, 101, 125 in between; lgkmcnt(0) at 127.  Three barriers, no counted
+  //   lgkmcnt waits: every fragment is read at least 8 MFMAs (~128 cycles) before its first use, and the 16
+  //   LDS-DMA pieces are spread over 100 MFMAs instead of one burst.
+  auto ktile_v = [&](auto ST, int k) {
+    constexpr int st = decltype(ST)::value;
+    i32x4 sa, sb;
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(PLVL);
+    sfor<128>([&](auto Q) {
+      constexpr int n = decltype(Q)::value;
+      constexpr int RA1[8] = {1, 3, 5, 7, 9, 11, 13, 15};
+      constexpr int RB1[8] = {25, 28, 31, 34, 37, 39, 41, 43};
+      constexpr int PA_[8] = {23, 26, 29, 32, 35, 53, 56, 59};
+      constexpr int PB_[8] = {62, 65, 86, 88, 90, 97, 101, 125};
+      constexpr int XA[8] = {94, 95, 96, 98, 99, 103, 104, 105};
+      constexpr int XB[8] = {106, 107, 110, 113, 115, 118, 121, 124};
+      auto idx = [](const int (&t)[8], int v) constexpr {
+        int r = -1;
+        for (int i = 0; i < 8; ++i)
+          if (t[i] == v) r = i;
+        return r;
+      };
+      constexpr int ra1 = idx(RA1, n), rb1 = idx(RB1, n), pa = idx(PA_, n), pb = idx(PB_, n), xa_ = idx(XA, n),
+                    xb_ = idx(XB, n);
+      // ---- in front of MFMA n
+      if constexpr (n == 21 || n == 51) {
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+        wait_lgkm<0>();
+        __builtin_amdgcn_s_barrier();
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(PLVL);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (n == 92) {
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+        wait_vm<13>();
+        __builtin_amdgcn_s_barrier();
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(PLVL);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (n == 127) {
+        wait_lgkm<0>();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (ra1 >= 0) ya[ra1] = frag4<true, (ra1 < 0 ? 0 : ra1), 1, st>(ra);
+      if constexpr (rb1 >= 0) yb[rb1] = frag4<true, (rb1 < 0 ? 0 : rb1), 1, st>(rb);
+      if constexpr (xa_ >= 0) xa[xa_] = frag4<true, (xa_ < 0 ? 0 : xa_), 0, st ^ 1>(ra);
+      if constexpr (xb_ >= 0) xb[xb_] = frag4<true, (xb_ < 0 ? 0 : xb_), 0, st ^ 1>(rb);
+      // ---- MFMA n (B fragment outer, A inner; B as src0: the transposed tile, 4 columns per lane)
+      constexpr int nn = n & 63, j = nn >> 3, i = nn & 7;
+      const bf16x8(&fa)[8] = n < 64 ? xa : ya;
+      const bf16x8(&fb)[8] = n < 64 ? xb : yb;
+      f32x4v& c = acc[j >> 2][i][j & 3];
+      if constexpr (pa >= 0) {
+        mfma_dma<piece_dst<false, st, (pa < 0 ? 0 : pa)>(), PA>(c, fb[j], fa[i], wdst, va[pa < 0 ? 0 : pa], sa);
+      } else if constexpr (pb >= 0) {
+        mfma_dma<piece_dst<true, st, (pb < 0 ? 0 : pb)>(), PB>(c, fb[j], fa[i], wdst, vb[pb < 0 ? 0 : pb], sb);
+      } else {
+        mfma_agpr(c, fb[j], fa[i]);
+      }
+      // ---- behind MFMA n: tile t+2's descriptors (SALU between MFMAs), A before its first piece at 23
+      if constexpr (n == 2 || n == 10) {
+        int kk = k + 2;
+        asm volatile("" : "+s"(kk));
+        if constexpr (n == 2) {
+          sa = desc(kk, ca, na, a_end);
+          asm volatile("" : "+s"(sa));
+        } else {
+          sb = desc(kk, cb, nb, b_end);
+          asm volatile("" : "+s"(sb));
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+
   for (int u = 0; u < ntile; ++u) {
     zero_acc();
     for (int k = 0; k < nt; k += 2) {
-      ktile(std::integral_constant<int, 0>{}, k);
-      ktile(std::integral_constant<int, 1>{}, k + 1);
+      if constexpr (VS) {
+        ktile_v(std::integral_constant<int, 0>{}, k);
+        ktile_v(std::integral_constant<int, 1>{}, k + 1);
+      } else {
+        ktile(std::integral_constant<int, 0>{}, k);
+        ktile(std::integral_constant<int, 1>{}, k + 1);
+      }
     }
     // tile done: accumulators out while the next tile's first K-tiles stream / sit in LDS
     asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
 #pragma unroll
-    for (int h = 0; h < 2; ++h) epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+    for (int h = 0; h < 2; ++h) {
+      if constexpr (X4 && EPI == kEpiBF16) {
+        // interior tile, 16-B aligned rows: the widened stores; otherwise the element-checked epilogue
+        if ((ctm + 1) * BM <= p.M && (ctn + 1) * BN <= p.N && (p.ldc & 7) == 0 && ((size_t)p.C & 15) == 0)
+          epilogue_v7_x4(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+        else
+          epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+      } else {
+        epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+      }
+    }
     if (u + 1 < ntile) {
       tile_of(p, slot + (u + 1) * G, ctm, ctn);
       ca = na;
@@ -335,7 +476,8 @@ bool pd_gemm_v7(const pd::gm::Params& p, int layout, int epi, int sched, int cus
     switch (sched) {
       PD_V7_CASE(kEpiBF16, 6) PD_V7_CASE(kEpiBF16, 18) PD_V7_CASE(kEpiBF16, 22) PD_V7_CASE(kEpiBF16, 10)
       PD_V7_CASE(kEpiBF16, 42) PD_V7_CASE(kEpiBF16, 66) PD_V7_CASE(kEpiBF16, 86) PD_V7_CASE(kEpiBF16, 20)
-      PD_V7_CASE(kEpiBF16, 14)
+      PD_V7_CASE(kEpiBF16, 14) PD_V7_CASE(kEpiBF16, 128) PD_V7_CASE(kEpiBF16, 130) PD_V7_CASE(kEpiBF16, 194)
+      PD_V7_CASE(kEpiBF16, 384)
       default: return false;
     }
     return true;

@@ -155,7 +155,7 @@ def build_rccl(verbose=False):
     flags = ["-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include",
              "-I", sysconfig.get_paths()["include"], "-I", pybind11.get_include()]
     libs = ["-L/opt/rocm/lib", "-lrccl", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
-    key = _hash(src, " ".join(flags + libs))
+    key = _hash(src, " ".join(flags + libs) + open(os.path.join(CSRC, "comm", "rccl_core.h")).read())
     out = rccl_target_path()
     stamp = out + ".stamp"
     if os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key:
@@ -262,6 +262,21 @@ def build_sanitized(kind="thread", verbose=False):
     os.makedirs(BUILD, exist_ok=True)
     out = os.path.join(BUILD, f"runtime_stress_{kind}")
     cmd = ["g++", "-O1", "-g", "-std=c++17", "-I", rdir] + _SAN_FLAGS[kind] + srcs + ["-o", out, "-lpthread", "-ldl"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    _run(cmd)
+    return out
+
+
+def build_rccl_stress(kind="thread", verbose=False):
+    """The ProcessGroupRCCL core (csrc/comm/rccl_core.h) + its 4-rank stress driver (csrc/comm/test/rccl_stress.cpp)
+    against the threaded fake RCCL / HIP (csrc/comm/test/fake/), under ``kind`` = "thread" (TSan) or "address"
+    (ASan + UBSan).  CPU-only; returns the executable path."""
+    cdir = os.path.join(CSRC, "comm")
+    os.makedirs(BUILD, exist_ok=True)
+    out = os.path.join(BUILD, f"rccl_stress_{kind}")
+    cmd = (["g++", "-O1", "-g", "-std=c++17", "-I", os.path.join(cdir, "test", "fake")] + _SAN_FLAGS[kind]
+           + [os.path.join(cdir, "test", "rccl_stress.cpp"), "-o", out, "-lpthread"])
     if verbose:
         print(" ".join(cmd), flush=True)
     _run(cmd)

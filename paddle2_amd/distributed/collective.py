@@ -175,6 +175,40 @@ def _shutdown_at_exit():
         pass
 
 
+_PG_STATUS = {"backend": None, "canary": None, "ipc": None}
+
+
+def _check_native_pg(store, rank, world, tout):
+    """Validate the default ProcessGroupRCCL on the devices (rccl_pg.canary); if any rank's check fails, every
+    rank drops it and re-creates the default group as torch's ProcessGroupNCCL on the same store (unless the user
+    asked for the own group explicitly: then raise).  The xGMI IPC all-reduce is then enabled for latency-bound
+    messages if it reproduces RCCL's result bit for bit on every rank (ipc_allreduce.auto_enable)."""
+    from . import ipc_allreduce, rccl_pg
+
+    ok, verdicts = rccl_pg.canary(store, rank, world)
+    _PG_STATUS["canary"] = verdicts
+    if not ok:
+        if rccl_pg.requested():
+            raise RuntimeError(f"ProcessGroupRCCL start-up check failed: {verdicts}")
+        import warnings
+
+        warnings.warn(f"ProcessGroupRCCL start-up check failed ({verdicts}); falling back to torch's "
+                      "ProcessGroupNCCL", RuntimeWarning)
+        dist.destroy_process_group()
+        dist.init_process_group(backend="nccl", rank=rank, world_size=world, timeout=tout,
+                                store=dist.PrefixStore("c10d_fallback", store),
+                                device_id=torch.device("cuda", torch.cuda.current_device()))
+        _PG_STATUS["backend"] = "c10d"
+        return
+    _PG_STATUS["backend"] = rccl_pg.BACKEND
+    _PG_STATUS["ipc"] = ipc_allreduce.auto_enable(store, rank, world)
+
+
+def pg_status():
+    """Which process group the job runs on and what its start-up checks found."""
+    return dict(_PG_STATUS)
+
+
 def init_parallel_env(backend=None, timeout_s=None):
     """Rendezvous (TCPStore on the master) + default RCCL/gloo process group (parallel.py:978)."""
     global _default_group, _initialized
@@ -190,9 +224,10 @@ def init_parallel_env(backend=None, timeout_s=None):
         backend = "gloo"
     native_pg = False
     if backend in ("nccl", "rccl") and torch.cuda.is_available():
-        from . import rccl_pg  # the framework's own RCCL process group (PADDLE2_AMD_PG=rccl)
+        from . import rccl_pg  # the framework's own RCCL process group (default; PADDLE2_AMD_PG=c10d opts out)
 
         native_pg = rccl_pg.enabled()
+        backend = "nccl"
     if backend == "nccl" and torch.cuda.is_available():
         local = _local_env(rank % max(torch.cuda.device_count(), 1))
         torch.cuda.set_device(local)
@@ -219,7 +254,13 @@ def init_parallel_env(backend=None, timeout_s=None):
 
                 st = create_or_get_global_tcp_store(rank, world, timeout=tout.total_seconds())
                 kw["store"] = TorchStore(st)
+            elif native_pg:
+                # an explicit store: the start-up check below may have to re-create the default group on it
+                kw["store"] = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
+                                            rank == 0, timeout=tout)
             dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=tout, **kw)
+            if native_pg:
+                _check_native_pg(kw["store"], rank, world, tout)
     _default_group = Group(rank, 0, list(range(world)), dist.group.WORLD if dist.is_initialized() else None,
                            name="_default_pg")
     _groups[0] = _default_group

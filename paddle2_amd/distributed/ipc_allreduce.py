@@ -198,17 +198,75 @@ def local_allreduce(tensors, mode=0, blocks=8, timeout_ms=5000):
 
 
 _COMM = {}
+# auto mode (the default on single-node GPU jobs): the start-up check of collective.init_parallel_env enables the
+# one-shot path for SUM messages of at most AUTO_MAX_BYTES on the default group once it has reproduced RCCL's
+# result on every rank; PADDLE2_AMD_IPC_ALLREDUCE=1 forces it on for every group (up to 32 MiB, no check), =0 off
+AUTO_MAX_BYTES = 1 << 20
+_AUTO = {"comm": None, "group": None}
+
+
+def _mode():
+    v = os.environ.get("PADDLE2_AMD_IPC_ALLREDUCE", "auto").lower()
+    return "on" if v == "1" else ("off" if v in ("0", "off") else "auto")
+
+
+def auto_enable(store, rank, world):
+    """Start-up check for the auto mode: a one-shot IPC all-reduce of integer-valued fp32 / bf16 tensors (exact in
+    any summation order) must equal the RCCL all-reduce on every rank and finish without a flag timeout.  All ranks
+    agree through the store; returns a status string ("on" when enabled)."""
+    import torch.distributed as dist
+
+    from .rccl_pg import _agree
+
+    if _mode() != "auto":
+        return _mode()
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("PADDLE_LOCAL_SIZE", world)))
+    if world < 2 or world > MAX_RANKS or local != world:
+        return "off: not a single-node group of 2..8 ranks"
+    status = "ok"
+    comm = None
+    try:
+        comm = IpcAllReduce(None, capacity=AUTO_MAX_BYTES, oneshot_max=AUTO_MAX_BYTES, timeout_ms=10000)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        for dt, n in ((torch.float32, 4096), (torch.bfloat16, 2048), (torch.float32, AUTO_MAX_BYTES // 4)):
+            x = ((torch.arange(n, device=dev) % 7) + rank).to(dt)
+            ref = x.clone()
+            dist.all_reduce(ref)
+            comm.all_reduce(x, check=True)
+            if not torch.equal(x, ref):
+                status = f"mismatch:{dt}:{n}"
+                break
+        torch.cuda.synchronize()
+    except Exception as e:  # noqa: BLE001
+        status = f"error:{type(e).__name__}:{str(e)[:200]}"
+    verdicts = _agree(store, "ipc_canary", rank, world, status)
+    if all(v == "ok" for v in verdicts):
+        _AUTO["comm"] = comm
+        _AUTO["group"] = dist.group.WORLD
+        return "on"
+    if comm is not None:
+        comm.close()
+    return f"off: {verdicts}"
 
 
 def maybe_all_reduce(t, group=None):
-    """collective.all_reduce hook: IPC path for small SUM messages when PADDLE2_AMD_IPC_ALLREDUCE=1 (opt-in);
-    returns True if it handled the tensor."""
-    if os.environ.get("PADDLE2_AMD_IPC_ALLREDUCE") != "1" or not t.is_cuda:
+    """collective.all_reduce hook: the IPC path for small SUM messages — forced on (PADDLE2_AMD_IPC_ALLREDUCE=1,
+    any group up to 32 MiB) or, in auto mode, on the default group for messages <= AUTO_MAX_BYTES once the start-up
+    check passed.  Returns True if it handled the tensor."""
+    if not t.is_cuda:
         return False
-    key = id(group)
-    comm = _COMM.get(key)
-    if comm is None:
-        comm = _COMM[key] = IpcAllReduce(group)
+    mode = _mode()
+    if mode == "auto":
+        comm = _AUTO["comm"]
+        if comm is None or (group is not None and group is not _AUTO["group"]):
+            return False
+    elif mode == "on":
+        key = id(group)
+        comm = _COMM.get(key)
+        if comm is None:
+            comm = _COMM[key] = IpcAllReduce(group)
+    else:
+        return False
     if not comm.supports(t):
         return False
     comm.all_reduce(t)

@@ -378,7 +378,93 @@ def register():
 
 
 def enabled():
+    """The own process group is the default for GPU jobs; ``PADDLE2_AMD_PG=c10d`` (or torch / nccl) selects torch's
+    ProcessGroupNCCL instead."""
+    v = os.environ.get("PADDLE2_AMD_PG", "").lower()
+    if v in ("c10d", "torch", "nccl", "0", "off"):
+        return False
+    return True
+
+
+def requested():
+    """The user asked for this group explicitly (no fallback to c10d if its start-up check fails)."""
     return os.environ.get("PADDLE2_AMD_PG", "").lower() in ("rccl", "native", BACKEND)
+
+
+def _agree(store, key, rank, world, mine, timeout_s=300.0):
+    """Every rank publishes ``mine`` (str) under key/<rank>; returns the list of all ranks' values."""
+    import time
+
+    store.set(f"{key}/{rank}", mine)
+    out = []
+    t0 = time.time()
+    for r in range(world):
+        while True:
+            try:
+                out.append(store.get(f"{key}/{r}").decode())
+                break
+            except Exception:
+                if time.time() - t0 > timeout_s:
+                    out.append("missing")
+                    break
+                time.sleep(0.05)
+    return out
+
+
+def canary(store, rank, world, timeout_ms=120_000):
+    """Start-up check of the default ProcessGroupRCCL on the real devices: all-reduce (sum, avg), all-gather,
+    reduce-scatter and a ring of pair-communicator send / recv (one coalesced group), each host-synchronised
+    with a bounded wait (a hang aborts the communicator instead of blocking) and checked exactly.  Every rank
+    publishes its verdict through the store; returns (all_ok, verdicts)."""
+    status = "ok"
+    try:
+        pg = dist.distributed_c10d._get_default_group()
+        if isinstance(pg, dist.ProcessGroup) and not isinstance(pg, ProcessGroupRCCL):
+            try:
+                pg = pg._get_backend(torch.device("cuda"))
+            except Exception:
+                pass
+        if not isinstance(pg, ProcessGroupRCCL):
+            raise RuntimeError(f"default group is {type(pg).__name__}, not ProcessGroupRCCL")
+        old = pg._g.timeout_ms
+        pg._g.timeout_ms = timeout_ms
+        try:
+            dev = torch.device("cuda", torch.cuda.current_device())
+            tri = world * (world + 1) / 2
+            t = torch.full((1024,), float(rank + 1), device=dev)
+            pg.all_reduce_native(t, 0).synchronize()
+            a = torch.full((256,), float(rank + 1), device=dev, dtype=torch.bfloat16)
+            pg.all_reduce_native(a, 4).synchronize()
+            ag = torch.empty(world * 8, device=dev)
+            pg._allgather_base(ag, torch.full((8,), float(rank), device=dev)).synchronize()
+            rs = torch.empty(8, device=dev)
+            pg.reduce_scatter_native(rs, torch.arange(world * 8, device=dev, dtype=torch.float32)).synchronize()
+            nxt, prv = (rank + 1) % world, (rank - 1) % world
+            recv = torch.zeros(16, device=dev)
+            works = pg.batch_p2p([(True, torch.full((16,), float(rank), device=dev), nxt), (False, recv, prv)])
+            works[0].synchronize()
+            torch.cuda.synchronize()
+            exp_ag = torch.arange(world, device=dev, dtype=torch.float32).repeat_interleave(8)
+            exp_rs = world * torch.arange(rank * 8, rank * 8 + 8, device=dev, dtype=torch.float32)
+            bad = []
+            if not bool((t == tri).all()):
+                bad.append("all_reduce")
+            if not bool((a.float() == tri / world).all()):
+                bad.append("avg")
+            if not torch.equal(ag, exp_ag):
+                bad.append("all_gather")
+            if not torch.equal(rs, exp_rs):
+                bad.append("reduce_scatter")
+            if not bool((recv == float(prv)).all()):
+                bad.append("p2p")
+            if bad:
+                status = "mismatch:" + ",".join(bad)
+        finally:
+            pg._g.timeout_ms = old
+    except Exception as e:   # noqa: BLE001 - any failure means: do not use this group
+        status = f"error:{type(e).__name__}:{str(e)[:200]}"
+    verdicts = _agree(store, "pdrccl_canary", rank, world, status)
+    return all(v == "ok" for v in verdicts), verdicts
 
 
 def batch_isend_irecv(p2p_ops):

@@ -10,6 +10,13 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def pypath(root):
+    """PYTHONPATH for a child process: ``root`` first, then the caller's entries (an interposer some harnesses put
+    there, e.g. a loaded-library recorder, must survive into the children)."""
+    old = os.environ.get("PYTHONPATH", "")
+    return root if not old else root + os.pathsep + old
+
+
 def free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -27,7 +34,7 @@ def run_workers(script, nprocs, args=(), timeout=300, extra_env=None):
         env = dict(os.environ)
         env.update({"RANK": str(r), "WORLD_SIZE": str(nprocs), "LOCAL_RANK": str(r), "MASTER_ADDR": "127.0.0.1",
                     "MASTER_PORT": str(port), "PADDLE_TRAINER_ID": str(r), "PADDLE_TRAINERS_NUM": str(nprocs),
-                    "PD_TEST_OUT": os.path.join(out_dir, f"rank{r}.json"), "PYTHONPATH": ROOT,
+                    "PD_TEST_OUT": os.path.join(out_dir, f"rank{r}.json"), "PYTHONPATH": pypath(ROOT),
                     "PADDLE2_AMD_DEVICE": "cpu", "OMP_NUM_THREADS": "1", "PADDLE_DISTRI_BACKEND": "gloo"})
         if extra_env:
             env.update(extra_env)

@@ -4,6 +4,8 @@ launcher integration with a real trial script."""
 import copy
 import json
 import os
+
+from _dist import pypath as _pypath  # noqa: E402
 import subprocess
 import sys
 
@@ -160,7 +162,7 @@ def test_memory_model():
 
 def test_memory_estimation_tool(tmp_path):
     tool = os.path.join(ROOT, "paddle2_amd", "distributed", "auto_tuner", "memory_cost_model.py")
-    env = dict(os.environ, PYTHONPATH=ROOT)
+    env = dict(os.environ, PYTHONPATH=_pypath(ROOT))
     r = subprocess.run([sys.executable, "-m", "paddle2_amd.distributed.auto_tuner.memory_cost_model",
                         "--dp_degree", "1", "--mp_degree", "1", "--pp_degree", "1", "--vpp_degree", "1",
                         "--sharding_degree", "1", "--sharding_stage", "1", "--micro_batch_size", "8",
@@ -297,7 +299,7 @@ def test_launch_auto_tuner_end_to_end(tmp_path):
            "metric_cfg": {"name": "step_time", "OptimizationDirection": "Minimize"}}
     cj = tmp_path / "tuner.json"
     cj.write_text(json.dumps(cfg))
-    env = dict(os.environ, PYTHONPATH=ROOT)
+    env = dict(os.environ, PYTHONPATH=_pypath(ROOT))
     r = subprocess.run([sys.executable, "-m", "paddle2_amd.distributed.launch", "--auto_tuner_json", str(cj),
                         "--log_dir", str(tmp_path / "logs"), str(script)], env=env, cwd=ROOT, capture_output=True,
                        text=True, timeout=300)

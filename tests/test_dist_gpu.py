@@ -3,6 +3,8 @@ place two ranks on one device), so stage-3 all-gather / reduce-scatter / barrier
 device tensors end to end (tiny Llama, bench.py self-launch)."""
 import json
 import os
+
+from _dist import pypath as _pypath  # noqa: E402
 import subprocess
 import sys
 
@@ -14,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.gpu
 def test_bench_two_ranks_share_one_gpu():
     env = dict(os.environ)
-    env.update({"PADDLE_DISTRI_BACKEND": "gloo", "PADDLE2_AMD_DEVICE": "gpu:0", "PYTHONPATH": ROOT})
+    env.update({"PADDLE_DISTRI_BACKEND": "gloo", "PADDLE2_AMD_DEVICE": "gpu:0", "PYTHONPATH": _pypath(ROOT)})
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "tiny",
                         "--seq-len", "512", "--micro-batch", "2", "--steps", "3", "--warmup", "1"],
                        capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)

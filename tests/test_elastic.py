@@ -3,6 +3,8 @@ launch elastic controller): two launcher 'nodes' with --nnodes 1:2 rendezvous ov
 TCPStore; when one node dies the survivor detects the missing heartbeat, re-rendezvouses and
 restarts its worker with world size 1."""
 import os
+
+from _dist import pypath as _pypath  # noqa: E402
 import signal
 import socket
 import subprocess
@@ -34,7 +36,7 @@ def _wait(pred, timeout):
 @pytest.mark.timeout(240)
 def test_elastic_scale_in(tmp_path):
     port = _port()
-    env = dict(os.environ, PYTHONPATH=ROOT, PADDLE_DISTRI_BACKEND="gloo")
+    env = dict(os.environ, PYTHONPATH=_pypath(ROOT), PADDLE_DISTRI_BACKEND="gloo")
     env.pop("CUDA_VISIBLE_DEVICES", None)
     base = [sys.executable, "-m", "paddle2_amd.distributed.launch", "--master", f"127.0.0.1:{port}", "--nnodes",
             "1:2", "--nproc_per_node", "1", "--elastic_ttl", "2", "--host", "127.0.0.1", "--job_id", "el"]

@@ -1,5 +1,7 @@
 """Launcher / spawn (reference tests: test/legacy_test/test_launch_coverage.py, test_spawn_and_init_parallel_env.py)."""
 import os
+
+from _dist import pypath as _pypath  # noqa: E402
 import subprocess
 import sys
 
@@ -23,7 +25,7 @@ print("OK rank", dist.get_rank(), flush=True)
 
 
 def _env():
-    env = dict(os.environ, PYTHONPATH=ROOT, PADDLE2_AMD_DEVICE="cpu", PADDLE_DISTRI_BACKEND="gloo")
+    env = dict(os.environ, PYTHONPATH=_pypath(ROOT), PADDLE2_AMD_DEVICE="cpu", PADDLE_DISTRI_BACKEND="gloo")
     return env
 
 

@@ -3,6 +3,8 @@ MI355X: every collective of the torch ProcessGroup surface, AVG / PreMulSum nati
 group, stream ordering of an async collective behind a long GEMM, non-contiguous outputs."""
 import json
 import os
+
+from _dist import pypath as _pypath  # noqa: E402
 import subprocess
 import sys
 
@@ -16,7 +18,7 @@ def test_native_rccl_process_group(tmp_path):
     from _dist import free_port
 
     out = tmp_path / "r.json"
-    env = dict(os.environ, MASTER_PORT=str(free_port()), PYTHONPATH=ROOT, PD_TEST_OUT=str(out))
+    env = dict(os.environ, MASTER_PORT=str(free_port()), PYTHONPATH=_pypath(ROOT), PD_TEST_OUT=str(out))
     env.pop("PADDLE2_AMD_DEVICE", None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "workers", "native_pg_worker.py")], env=env,
                        capture_output=True, text=True, timeout=180)
@@ -34,6 +36,7 @@ def test_native_rccl_process_group(tmp_path):
     assert res["coalesced"] == [10.0, 21.0]
     assert res["p2p_self"] == [float(i) for i in range(6)]
     assert res["num_comms"] == 0 or res["num_comms"] >= 1
+    assert res["canary"] == [True, ["ok"]], res["canary"]
 
 
 def test_native_rccl_module_builds_and_loads():

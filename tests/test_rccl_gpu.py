@@ -2,6 +2,8 @@
 one-rank RCCL world (the collectives run through RCCL kernels, not the gloo fallbacks)."""
 import json
 import os
+
+from _dist import pypath as _pypath  # noqa: E402
 import subprocess
 import sys
 
@@ -16,7 +18,7 @@ def test_process_group_on_rccl(tmp_path):
 
     out = tmp_path / "r.json"
     env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-               MASTER_PORT=str(free_port()), PYTHONPATH=ROOT, PD_TEST_OUT=str(out))
+               MASTER_PORT=str(free_port()), PYTHONPATH=_pypath(ROOT), PD_TEST_OUT=str(out))
     env.pop("PADDLE_DISTRI_BACKEND", None)
     env.pop("PADDLE2_AMD_DEVICE", None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "workers", "rccl_pg_worker.py")], env=env,

@@ -111,6 +111,10 @@ dist.barrier()
 torch.cuda.synchronize()
 res["num_comms"] = pg._g.num_comms()
 print("ok num_comms", flush=True)
+# the start-up check init_parallel_env runs on a default ProcessGroupRCCL (1 rank: p2p to self)
+ok, verdicts = rccl_pg.canary(dist.distributed_c10d._get_default_store(), 0, 1)
+res["canary"] = [ok, verdicts]
+print("ok canary", verdicts, flush=True)
 dist.destroy_process_group()
 with open(os.environ["PD_TEST_OUT"], "w") as f:
     json.dump(res, f)
