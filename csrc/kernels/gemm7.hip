@@ -472,6 +472,13 @@ bool pd_gemm_v7(const pd::gm::Params& p, int layout, int epi, int sched, int cus
     PD_V7_CASE(E, 0) PD_V7_CASE(E, 1) PD_V7_CASE(E, 2) PD_V7_CASE(E, 3) \
     default: return false;                                              \
   }
+  if (epi == kEpiSwiGLU && sched > 3) {   // the spread schedule with the SwiGLU epilogue
+    switch (sched) {
+      PD_V7_CASE(kEpiSwiGLU, 128) PD_V7_CASE(kEpiSwiGLU, 384)
+      default: return false;
+    }
+    return true;
+  }
   if (epi == kEpiBF16 && sched > 3) {
     switch (sched) {
       PD_V7_CASE(kEpiBF16, 6) PD_V7_CASE(kEpiBF16, 18) PD_V7_CASE(kEpiBF16, 22) PD_V7_CASE(kEpiBF16, 10)

@@ -86,10 +86,12 @@ class SymbolicTranslator:
         self._layer = layer
         self._build_strategy = build_strategy
         self._training = training
-        self._programs = {}      # guard -> StaticFunction holding that guard's Program
+        self._programs = {}      # guard -> StaticFunction holding that guard's Program (Program-level mode)
+        self._traces = {}        # guard -> [opcode_executor.Trace] (bytecode mode)
         self._eager = {}         # guard -> break reason
         self._children_done = False
-        self.stats = {"compiled": 0, "guard_hits": 0, "graph_breaks": 0, "eager_calls": 0, "breaks": []}
+        self.stats = {"compiled": 0, "guard_hits": 0, "graph_breaks": 0, "eager_calls": 0, "breaks": [],
+                      "simulations": 0, "trace_misses": 0}
         try:
             self._sig = inspect.signature(fn)
         except (TypeError, ValueError):
@@ -143,6 +145,10 @@ class SymbolicTranslator:
             # called while an enclosing translator records: inline into that Program
             return self._fn(*args, **kwargs) if self._layer is None else self._fn(self._layer, *args, **kwargs)
         args, kwargs = self._positional(args, kwargs)
+        from . import opcode_executor as oe
+
+        if oe.enabled() and not kwargs:
+            return self._call_bytecode(args)
         if kwargs or not _is_static_capable(args):
             return self._run_eager(args, kwargs)
         key = self._guard(args)
@@ -164,6 +170,48 @@ class SymbolicTranslator:
         else:
             self.stats["guard_hits"] += 1
         return sf(*args)
+
+    # ------------------------------------------------------------------ bytecode mode (jit/opcode_executor.py)
+    MAX_TRACES = 8
+
+    def _call_bytecode(self, args):
+        """Replay a recorded trace of this guard if one applies; otherwise simulate the bytecode (sub-graphs split
+        at the graph breaks) and keep the new trace."""
+        from . import opcode_executor as oe
+
+        key = self._guard(args)
+        if key in self._eager:
+            return self._run_eager(args, {})
+        full = ((self._layer,) + tuple(args)) if self._layer is not None else tuple(args)
+        for tr in self._traces.get(key, ()):
+            try:
+                out = oe.replay(tr, full)
+            except oe.TraceMiss:
+                self.stats["trace_misses"] += 1
+                continue
+            self.stats["guard_hits"] += 1
+            return out
+        try:
+            res, tr = oe.translate_call(self._fn, full, None, self._build_strategy)
+        except oe.Unsupported as e:
+            reason = f"Unsupported: {e}"[:300]
+            self._eager[key] = reason
+            self.stats["breaks"].append(reason)
+            return self._run_eager(args, {})
+        self.stats["simulations"] += 1
+        self.stats["compiled"] += tr.n_graphs
+        self.stats["graph_breaks"] += tr.n_breaks
+        if tr.n_breaks:
+            self.stats["breaks"].append(f"{tr.n_breaks} break(s) in {self._fn.__qualname__}")
+        if tr.replayable:
+            lst = self._traces.setdefault(key, [])
+            if len(lst) < self.MAX_TRACES:
+                lst.append(tr)
+        return res
+
+    @property
+    def traces(self):
+        return [t for ts in self._traces.values() for t in ts]
 
     def __get__(self, obj, objtype=None):
         if obj is None or self._layer is not None:

@@ -1,6 +1,9 @@
-"""SOT mode (to_static(full_graph=False), jit/sot.py): guarded Program cache, graph-break fallback with
-sub-layer translation (reference tests: test/sot/test_guard*.py, test_break_graph.py, test_simulate_initialize)."""
+"""SOT mode (to_static(full_graph=False)): the bytecode translator (jit/opcode_executor.py — CPython 3.10 opcodes
+simulated into sub-graphs, graph breaks mid-function, trace replay under guards) and the Program-level mode
+(jit/sot.py with PADDLE2_AMD_SOT_BYTECODE=0: guarded Program cache, Layer-granularity fallback).  Reference tests:
+test/sot/test_guard*.py, test_break_graph.py, test_simulate_initialize.py, test_04_list.py, test_11_jumps.py."""
 import numpy as np
+import pytest
 
 import paddle2_amd as paddle
 from paddle2_amd.jit import sot
@@ -43,7 +46,12 @@ def _needs_value(x):
     return x * float(n)
 
 
-def test_graph_break_falls_back_to_eager():
+@pytest.fixture
+def program_mode(monkeypatch):
+    monkeypatch.setenv("PADDLE2_AMD_SOT_BYTECODE", "0")
+
+
+def test_graph_break_falls_back_to_eager(program_mode):
     f = paddle.jit.to_static(_needs_value, full_graph=False)
     x = paddle.to_tensor(np.array([1.0, 2.0], "float32"))
     np.testing.assert_allclose(_np(f(x)), [3.0, 6.0])
@@ -74,7 +82,7 @@ class _Outer(paddle.nn.Layer):
         return self.b(h)
 
 
-def test_layer_break_pushes_translation_to_sublayers_and_trains():
+def test_layer_break_pushes_translation_to_sublayers_and_trains(program_mode):
     paddle.seed(0)
     net = _Outer()
     x = paddle.to_tensor(np.random.RandomState(0).randn(3, 4).astype("float32"))
@@ -93,7 +101,7 @@ def test_layer_break_pushes_translation_to_sublayers_and_trains():
     assert s["compiled"] >= 2 and s["graph_breaks"] >= 1
 
 
-def test_tensor_control_flow_compiles_without_break():
+def test_tensor_control_flow_compiles_without_break(program_mode):
     def f(x):
         if x.mean() > 0:
             return x + 1.0
@@ -126,3 +134,113 @@ def test_env_selects_sot(monkeypatch):
     assert isinstance(f, sot.SymbolicTranslator)
     monkeypatch.setenv("ENABLE_FALL_BACK", "0")
     assert not isinstance(paddle.jit.to_static(_scaled), sot.SymbolicTranslator)
+
+
+# ------------------------------------------------------------------------------------ bytecode translator
+def _branchy(x, y):
+    z = x + y
+    if z.sum() > 0:          # tensor-dependent jump: graph break in the middle of the function
+        z = z * 2
+    else:
+        z = z - 1
+    return z * 3
+
+
+def test_bytecode_break_mid_function_and_trace_replay():
+    f = paddle.jit.to_static(_branchy, full_graph=False)
+    x = paddle.to_tensor(np.ones([2, 3], "float32"))
+    y = paddle.to_tensor(np.ones([2, 3], "float32"))
+    np.testing.assert_allclose(_np(f(x, y)), _np(_branchy(x, y)))
+    assert f.stats["compiled"] == 2 and f.stats["graph_breaks"] == 1 and f.stats["simulations"] == 1
+    (tr,) = f.traces
+    assert [s[0] for s in tr.steps] == ["graph", "branch", "graph", "return"]
+    np.testing.assert_allclose(_np(f(x * 2, y)), _np(_branchy(x * 2, y)))   # same branch: replayed, no simulation
+    assert f.stats["guard_hits"] == 1 and f.stats["simulations"] == 1
+    xn = paddle.to_tensor(np.full([2, 3], -5.0, "float32"))
+    np.testing.assert_allclose(_np(f(xn, y)), _np(_branchy(xn, y)))         # other branch: miss, new trace
+    assert f.stats["trace_misses"] == 1 and f.stats["simulations"] == 2 and len(f.traces) == 2
+    np.testing.assert_allclose(_np(f(xn, y)), _np(_branchy(xn, y)))         # both outcomes now replay
+    np.testing.assert_allclose(_np(f(x, y)), _np(_branchy(x, y)))
+    assert f.stats["simulations"] == 2
+
+
+def _valued(x):
+    n = int(x.max())         # a concrete Python value: break at the call, value guarded on replay
+    h = x * n
+    return h + 1, n
+
+
+def test_bytecode_value_break_is_guarded():
+    f = paddle.jit.to_static(_valued, full_graph=False)
+    x = paddle.to_tensor(np.array([1.0, 2.0], "float32"))
+    out, n = f(x)
+    assert n == 2
+    np.testing.assert_allclose(_np(out), [3.0, 5.0])
+    (tr,) = f.traces
+    assert [s[0] for s in tr.steps] == ["graph", "call", "graph", "return"]
+    out, n = f(paddle.to_tensor(np.array([0.5, 2.0], "float32")))      # same max: replay
+    np.testing.assert_allclose(_np(out), [2.0, 5.0])
+    assert f.stats["guard_hits"] == 1
+    out, n = f(paddle.to_tensor(np.array([1.0, 3.0], "float32")))      # max changed: guard miss, re-simulated
+    assert n == 3
+    np.testing.assert_allclose(_np(out), [4.0, 10.0])
+    assert f.stats["trace_misses"] == 1 and f.stats["simulations"] == 2
+
+
+def _helper(z, k):
+    if z.mean() > k:          # the break is inside the inlined callee
+        return z * 0.5
+    return z
+
+
+def _uses_closures(xs, k):
+    ys = [x * 2 for x in xs]          # list comprehension: MAKE_FUNCTION, simulated inline
+    s = ys[0] + ys[1]
+    acc = 0
+    for i in range(3):
+        acc = acc + i
+    s = _helper(s, k)
+    scale = lambda v: v + acc          # noqa: E731 - a closure over a simulated cell
+    return scale(s)
+
+
+def test_bytecode_inlines_user_functions_comprehensions_and_closures():
+    f = paddle.jit.to_static(_uses_closures, full_graph=False)
+    xs = [paddle.to_tensor(np.ones([2], "float32")), paddle.to_tensor(np.full([2], 3.0, "float32"))]
+    np.testing.assert_allclose(_np(f(xs, 1.0)), _np(_uses_closures(xs, 1.0)))
+    assert f.stats["graph_breaks"] == 1 and f.stats["compiled"] == 2
+    np.testing.assert_allclose(_np(f(xs, 100.0)), _np(_uses_closures(xs, 100.0)))   # new scalar: new guard
+
+
+def test_bytecode_layer_break_trains_like_eager():
+    paddle.seed(0)
+    net = _Outer()
+    x = paddle.to_tensor(np.random.RandomState(0).randn(3, 4).astype("float32"))
+    ref = net.b(net.a(x))
+    ref.sum().backward()
+    g_ref = net.a.fc.weight.grad.numpy().copy()
+    net.clear_gradients()
+    paddle.jit.to_static(net, full_graph=False)
+    for _ in range(2):   # simulate, then replay
+        net.clear_gradients()
+        out = net(x)
+        np.testing.assert_allclose(_np(out), _np(ref), rtol=1e-6)
+        out.sum().backward()
+        np.testing.assert_allclose(net.a.fc.weight.grad.numpy(), g_ref, rtol=1e-6)
+    st = net.forward.translator.stats
+    assert st["graph_breaks"] == 1 and st["guard_hits"] == 1 and st["simulations"] == 1
+
+
+def _with_try(x):
+    try:
+        return x + 1
+    finally:
+        pass
+
+
+def test_bytecode_unsupported_construct_runs_eagerly():
+    f = paddle.jit.to_static(_with_try, full_graph=False)
+    x = paddle.to_tensor(np.ones([2], "float32"))
+    np.testing.assert_allclose(_np(f(x)), [2.0, 2.0])
+    np.testing.assert_allclose(_np(f(x)), [2.0, 2.0])
+    assert f.stats["eager_calls"] == 2 and "Unsupported" in f.stats["breaks"][0]
