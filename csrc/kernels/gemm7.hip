@@ -134,6 +134,57 @@ __device__ __forceinline__ void epilogue_v7_x4(const Params& p, f32x4v (&acc)[8]
   }
 }
 
+// SwiGLU epilogue of an interior tile with 16-B stores (SCHED bit 8): the same row-block pairing + v_permlane16_swap
+// as epilogue_v7_x4, applied to the gate, up and silu(gate) * up values (gate / up = column tiles j and j + 2 of
+// the wave's 64-column half: bcol<kEpiSwiGLU>).  Rounding as epilogue_t: the activation uses the bf16-rounded gate
+// and up, exactly what the backward reads back from gu.
+__device__ __forceinline__ void epilogue_v7_swi_x4(const Params& p, f32x4v (&acc)[8][4], int tm, int tn, int arow,
+                                                   int bcolw, int lane) {
+  const int wsub = bcolw >> 6;                    // 64-column half of the tile: 32 gate + 32 up columns
+  const int sub = (lane >> 4) & 1;
+  const int r = lane & 15;
+  const int ch = 8 * (lane >> 5);
+  const long row_base = (long)tm * BM + arow + r;
+  unsigned short* out = (unsigned short*)p.C;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int gc0 = tn * 128 + wsub * 32 + 16 * j;   // first gate (== output) column of this 16-column tile
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      unsigned g2[2][2], u2[2][2], o2[2][2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const f32x4v& ga = acc[2 * q + b][j];
+        const f32x4v& ua = acc[2 * q + b][2 + j];
+        float gv[4], uv[4], ov[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          gv[e] = bf2f(f2bf(ga[e]));
+          uv[e] = bf2f(f2bf(ua[e]));
+          ov[e] = silu(gv[e]) * uv[e];
+        }
+        g2[b][0] = pack_bf2(gv[0], gv[1]);
+        g2[b][1] = pack_bf2(gv[2], gv[3]);
+        u2[b][0] = pack_bf2(uv[0], uv[1]);
+        u2[b][1] = pack_bf2(uv[2], uv[3]);
+        o2[b][0] = pack_bf2(ov[0], ov[1]);
+        o2[b][1] = pack_bf2(ov[2], ov[3]);
+      }
+      auto g0 = __builtin_amdgcn_permlane16_swap(g2[0][0], g2[1][0], false, false);
+      auto g1 = __builtin_amdgcn_permlane16_swap(g2[0][1], g2[1][1], false, false);
+      auto u0 = __builtin_amdgcn_permlane16_swap(u2[0][0], u2[1][0], false, false);
+      auto u1 = __builtin_amdgcn_permlane16_swap(u2[0][1], u2[1][1], false, false);
+      auto o0 = __builtin_amdgcn_permlane16_swap(o2[0][0], o2[1][0], false, false);
+      auto o1 = __builtin_amdgcn_permlane16_swap(o2[0][1], o2[1][1], false, false);
+      const long row = row_base + 16 * (2 * q + sub);
+      const int c = gc0 + ch;
+      *(uint4*)(p.C2 + row * p.ldc2 + c) = make_uint4(g0[0], g1[0], g0[1], g1[1]);
+      *(uint4*)(p.C2 + row * p.ldc2 + p.H + c) = make_uint4(u0[0], u1[0], u0[1], u1[1]);
+      *(uint4*)(out + row * p.ldc + c) = make_uint4(o0[0], o1[0], o0[1], o1[1]);
+    }
+  }
+}
+
 template <int EPI, int SCHED>
 __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   constexpr bool BAR4 = SCHED & 1, PRIO = (SCHED & 2) != 0;
@@ -432,6 +483,12 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
         // interior tile, 16-B aligned rows: the widened stores; otherwise the element-checked epilogue
         if ((ctm + 1) * BM <= p.M && (ctn + 1) * BN <= p.N && (p.ldc & 7) == 0 && ((size_t)p.C & 15) == 0)
           epilogue_v7_x4(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+        else
+          epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+      } else if constexpr (X4 && EPI == kEpiSwiGLU) {
+        if ((ctm + 1) * BM <= p.M && (ctn + 1) * 128 <= p.H && (p.ldc & 7) == 0 && (p.ldc2 & 7) == 0 &&
+            (p.H & 7) == 0 && ((size_t)p.C & 15) == 0 && ((size_t)p.C2 & 15) == 0)
+          epilogue_v7_swi_x4(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
         else
           epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
       } else {

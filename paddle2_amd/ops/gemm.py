@@ -24,6 +24,7 @@ from . import _native as N
 LAYOUT_AK, LAYOUT_BK = 1, 2
 EPI_BF16, EPI_F32, EPI_SWIGLU = 0, 1, 2
 GROUP_M = int(os.environ.get("PADDLE2_AMD_GEMM_GROUP_M", "8"))
+_GROUP_FORCED = "PADDLE2_AMD_GEMM_GROUP_M" in os.environ
 # kernel schedule (csrc/kernels/gemm.hip): 0 = v2 (8 waves, 2 per SIMD, 128x64 wave tiles), 4 = v4 (4 waves,
 # 128x128 wave tiles on AGPR accumulators, spread LDS-DMA, 8/16-B epilogue stores), 6 = v6 (v4 persistent: one
 # workgroup per CU, the DMA pipeline running across tile boundaries).  Per pass, from the measured table in
@@ -33,9 +34,16 @@ GROUP_M = int(os.environ.get("PADDLE2_AMD_GEMM_GROUP_M", "8"))
 # 7..10 = v7 (gemm7.hip, SCHED 0..3): the TN schedule with both operands K-major — dgrad in place, the forward and
 # the SwiGLU forward on W^T (one transpose of the weight per forward); problems outside its domain (K % 128,
 # >= 2 GiB operands) run v6.
+# 64 + cfg = v7 with SCHED cfg (gemm7.hip); V7_SPREAD = SCHED 384: the spread three-barrier K-tile schedule
+# (LDS-DMA pieces spread over 100 MFMAs, every fragment read >= 8 MFMAs before use, 3 barriers) + 16-B epilogue
+# stores (v_permlane16_swap pairing) — profiles/r4_gemm_spread.md: the forward / dgrad / SwiGLU default.
+V7_SPREAD = 64 + 384
 _FORCE = os.environ.get("PADDLE2_AMD_GEMM_VARIANT")
 VARIANT = int(_FORCE) if _FORCE is not None else None
-PASS_VARIANT = {"fwd": 6, "dgrad": 6, "wgrad": 4, "wgrad_bf16": 4, "swiglu": 4}
+PASS_VARIANT = {"fwd": V7_SPREAD, "dgrad": V7_SPREAD, "wgrad": 4, "wgrad_bf16": 4, "swiglu": V7_SPREAD}
+# grouped tile order per pass (row tiles that sweep the column tiles together): 4 for the spread TN schedule
+# (forward +2..7 %, dgrad +0..2 % over 8 at M = 32768; profiles/r4_gemm_spread.md), 8 for the wgrad kernels
+PASS_GROUP_M = {"fwd": 4, "dgrad": 4, "swiglu": 4, "wgrad": 8, "wgrad_bf16": 8}
 
 
 def _variant(name):
@@ -89,8 +97,9 @@ def _workspace(t):
 def _launch(layout, epi, a, lda, b, ldb, c, ldc, c2, ldc2, bias, M, Nn, K, beta=0.0, H=0, name="fwd"):
     v = _variant(name)
     ws, ws_bytes = _workspace(a) if epi != EPI_SWIGLU and v in (0, 4) else (0, 0)
+    gm = GROUP_M if _GROUP_FORCED else PASS_GROUP_M.get(name, GROUP_M)
     N.native().gemm(layout, epi, a.data_ptr(), lda, b.data_ptr(), ldb, c.data_ptr(), ldc, N.ptr(c2), ldc2,
-                    N.ptr(bias), M, Nn, K, float(beta), H, GROUP_M, v, ws, ws_bytes, N.stream())
+                    N.ptr(bias), M, Nn, K, float(beta), H, gm, v, ws, ws_bytes, N.stream())
 
 
 def _v7(name, K):

@@ -476,8 +476,8 @@ def _pass_native(name, t, other=None):
     return _GEMM_PASS.get("wgrad" if name == "wgrad32" else name, "native") == "native"
 
 
-_GEMM_PASS = {"fwd": _os.environ.get("PADDLE2_AMD_GEMM_FWD", "blas"),
-              "dgrad": _os.environ.get("PADDLE2_AMD_GEMM_DGRAD", "blas"),
+_GEMM_PASS = {"fwd": _os.environ.get("PADDLE2_AMD_GEMM_FWD", "native"),
+              "dgrad": _os.environ.get("PADDLE2_AMD_GEMM_DGRAD", "native"),
               "wgrad": _os.environ.get("PADDLE2_AMD_GEMM_WGRAD", "native")}
 
 

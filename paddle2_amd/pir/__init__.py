@@ -101,7 +101,7 @@ class Operation:
 
         res = ", ".join(repr(r) for r in self._results)
         ops = ", ".join(repr(o) for o in self._operands)
-        attrs = ",".join(f"{k}:{fmt(v)}" for k, v in self.attrs_.items() if k != "value")
+        attrs = ",".join(f"{k}:{fmt(v)}" for k, v in self.attrs_.items() if k != "value" and not k.startswith("__"))
         tin = ", ".join(o.type_str() for o in self._operands)
         tout = ", ".join(r.type_str() for r in self._results)
         return f"({res}) = \"{self._name}\" ({ops}) {{{attrs}}} : ({tin}) -> {tout}"

@@ -246,18 +246,7 @@ class Executor:
             if sym is None:
                 raise KeyError(f"feed '{name}' is not a data variable of this program")
             env[sym._vid] = _feed_tensor(v, sym, self._device)
-        if not any(o.kind in ("backward", "grad", "optimize", "param_grad") for o in program.ops):
-            # inference: run only the ops the fetch targets depend on (reference use_prune)
-            key = (id(program), len(program.ops), tuple(fetch_ids))
-            pruned = self._pruned.get(key)
-            if pruned is None:
-                from .io import _prune
-
-                pruned = Program()
-                pruned.ops = _prune(program, fetch_ids)
-                pruned.feeds, pruned.vars = program.feeds, program.vars
-                self._pruned[key] = pruned
-            program = pruned
+        program = self._executable(program, fetch_ids)
         if strategy is not None and strategy.enable_cuda_graph and self._device.type == "cuda":
             outs = self._run_graph(program, env, fetch_ids)
         else:
@@ -267,6 +256,36 @@ class Executor:
             return [o.detach().float().cpu().numpy() if o.dtype == torch.bfloat16 else o.detach().cpu().numpy()
                     for o in outs]
         return [Tensor._wrap(o if _grad else o.detach()) for o in outs]
+
+    def _executable(self, program, fetch_ids):
+        """What runs: the Program translated to PIR, optimised by the pass pipeline (DCE against the fetch targets
+        and the side effects, CSE, fused_gemm_epilogue) and lowered back to instructions (pir/lowering.py; reference
+        pir_interpreter.cc runs the PIR program after the passes).  FLAGS_enable_pir_in_executor=0 runs the
+        recorded instructions as they are (inference programs still pruned to the fetch targets)."""
+        from ..framework import flags
+
+        key = (id(program), len(program.ops), tuple(fetch_ids))
+        hit = self._pruned.get(key)
+        if hit is not None:
+            return hit[0]
+        train = any(o.kind in ("backward", "grad", "optimize", "param_grad") for o in program.ops)
+        if str(flags.flag("FLAGS_enable_pir_in_executor", True)).lower() not in ("0", "false"):
+            from ..pir import lowering
+
+            exe_prog, pir_prog, stats = lowering.optimize(program, fetch_ids)
+            self._pruned[key] = (exe_prog, program)   # the source program stays alive while its key is cached
+            self.last_pir = pir_prog
+            self.last_pass_stats = stats
+            return exe_prog
+        if train:
+            return program
+        from .io import _prune
+
+        pruned = Program()
+        pruned.ops = _prune(program, fetch_ids)
+        pruned.feeds, pruned.vars = program.feeds, program.vars
+        self._pruned[key] = (pruned, program)
+        return pruned
 
     @staticmethod
     def _fetch_id(program, f):
