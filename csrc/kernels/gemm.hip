@@ -277,7 +277,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(Params p) {
 //     stay in flight) + barrier (everyone's), then tile t+1's step-0 fragments are read behind the
 //     last 16 MFMAs.
 // lanes whose 16-B chunk starts at or past K (K % 64 != 0).
-template <bool AK, bool BKM, int EPI, bool FAST>
+// SP: the spread three-barrier K-tile schedule of v7 (gemm7.hip ktile_v) on any operand layout — fragments of an
+// MN-major operand are two ds_read_b64_tr_b16 each; used for the wgrad (both operands MN-major, fp32 main grad).
+template <bool AK, bool BKM, int EPI, bool FAST, bool SP = false>
 __global__ __launch_bounds__(NTHR4, 1) void gemm_v4_kernel(Params p) {
   __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
@@ -456,9 +458,69 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v4_kernel(Params p) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  for (int t = 0; t < nt; t += 2) {
-    ktile(C0{}, t);
-    ktile(C1{}, t + 1);
+  // the spread schedule (SP): see gemm7.hip ktile_v for the per-MFMA positions
+  auto ktile_sp = [&](auto ST, int t) {
+    constexpr int st = decltype(ST)::value;
+    const __amdgpu_buffer_rsrc_t rsa = desc(a_t0, a_step, a_bytes, t + 2), rsb = desc(b_t0, b_step, b_bytes, t + 2);
+    const int krem = p.K - (t + 2) * BK;
+    unsigned wb = wdst;
+    asm volatile("" : "+s"(wb));
+    sfor<128>([&](auto Q) {
+      constexpr int n = decltype(Q)::value;
+      constexpr int RA1[8] = {1, 3, 5, 7, 9, 11, 13, 15};
+      constexpr int RB1[8] = {25, 28, 31, 34, 37, 39, 41, 43};
+      constexpr int PA_[8] = {23, 26, 29, 32, 35, 53, 56, 59};
+      constexpr int PB_[8] = {62, 65, 86, 88, 90, 97, 101, 125};
+      constexpr int XA[8] = {94, 95, 96, 98, 99, 103, 104, 105};
+      constexpr int XB[8] = {106, 107, 110, 113, 115, 118, 121, 124};
+      auto idx = [](const int (&tb)[8], int v) constexpr {
+        int r = -1;
+        for (int i = 0; i < 8; ++i)
+          if (tb[i] == v) r = i;
+        return r;
+      };
+      constexpr int ra1 = idx(RA1, n), rb1 = idx(RB1, n), pa = idx(PA_, n), pb = idx(PB_, n), xa_ = idx(XA, n),
+                    xb_ = idx(XB, n);
+      if constexpr (n == 21 || n == 51) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (n == 92) {
+        asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (n == 127) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (ra1 >= 0) ya[ra1] = frag4<AK, (ra1 < 0 ? 0 : ra1), 1, st>(ra);
+      if constexpr (rb1 >= 0) yb[rb1] = frag4<BKM, (rb1 < 0 ? 0 : rb1), 1, st>(rb);
+      if constexpr (xa_ >= 0) xa[xa_] = frag4<AK, (xa_ < 0 ? 0 : xa_), 0, st ^ 1>(ra);
+      if constexpr (xb_ >= 0) xb[xb_] = frag4<BKM, (xb_ < 0 ? 0 : xb_), 0, st ^ 1>(rb);
+      constexpr int nn = n & 63;
+      if constexpr (n < 64) mm(std::integral_constant<int, nn>{}, xa, xb);
+      else mm(std::integral_constant<int, nn>{}, ya, yb);
+      // pieces behind the MFMA (a buffer_load ... lds after an MFMA: the compiler covers the M0 hazard itself)
+      if constexpr (pa >= 0) piece(std::integral_constant<int, (pa < 0 ? 0 : pa)>{}, st, rsa, rsb, wb, krem);
+      if constexpr (pb >= 0) piece(std::integral_constant<int, 8 + (pb < 0 ? 0 : pb)>{}, st, rsa, rsb, wb, krem);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+
+  if constexpr (SP) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the prologue's step-0 reads (no counted waits in SP)
+    __builtin_amdgcn_sched_barrier(0);
+    for (int t = 0; t < nt; t += 2) {
+      ktile_sp(C0{}, t);
+      ktile_sp(C1{}, t + 1);
+    }
+  } else {
+    for (int t = 0; t < nt; t += 2) {
+      ktile(C0{}, t);
+      ktile(C1{}, t + 1);
+    }
   }
   // drain the masked tail pieces and the last (unused) fragment reads before the workgroup's LDS goes away;
   // the s_nops cover the MFMA-write -> accumulator-read wait states of the last MFMAs
@@ -773,7 +835,7 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   // v4+ store 4 consecutive output columns per lane (8-B bf16 / 16-B fp32 accesses): rows must keep that alignment
   if (variant >= 4 && (ldc % 4 || (size_t)C % 16 || (C2 && (ldc2 % 4 || (size_t)C2 % 16)))) variant = 0;
   dim3 grid(p.tiles_m * p.tiles_n);
-  if (ws && (variant == 0 || variant == 4) && epi != kEpiSwiGLU) {
+  if (ws && (variant == 0 || variant == 4 || variant == 5) && epi != kEpiSwiGLU) {
     const int g = plan_splitk(p, ws_bytes);
     if (g) grid = dim3(g);
   }
@@ -781,7 +843,13 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   const bool fast = !(ak || bk) || K % BK == 0;  // v4: no K-major operand has a partial last K-tile
   const dim3 pgrid(std::min(p.tiles_m * p.tiles_n, 8 * p.cpx));  // v6: one persistent workgroup per CU
 #define PD_GEMM_LAUNCH(AKV, BKV, EPIV)                                          \
-  if (variant == 4) {                                                            \
+  if (variant == 5) {                                                            \
+    if (fast)                                                                    \
+      gemm_v4_kernel<AKV, BKV, EPIV, true, true><<<grid, NTHR4, 0, st>>>(p);    \
+    else                                                                         \
+      gemm_v4_kernel<AKV, BKV, EPIV, false, true><<<grid, NTHR4, 0, st>>>(p);   \
+    if (p.ksplit > 1) splitk_reduce_kernel<EPIV><<<rgrid, 256, 0, st>>>(p);     \
+  } else if (variant == 4) {                                                     \
     if (fast)                                                                    \
       gemm_v4_kernel<AKV, BKV, EPIV, true><<<grid, NTHR4, 0, st>>>(p);          \
     else                                                                         \

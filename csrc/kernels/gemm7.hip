@@ -104,6 +104,14 @@ constexpr int piece_dst() {
 __device__ __forceinline__ unsigned pack_bf2(float a, float b) {
   return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
 }
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ void st16(void* ptr, unsigned a, unsigned b, unsigned c, unsigned d) {
+  const u32x4v v = {a, b, c, d};
+  if constexpr (NT) __builtin_nontemporal_store(v, (u32x4v*)ptr);
+  else *(u32x4v*)ptr = v;
+}
+template <bool NT = false>
 __device__ __forceinline__ void epilogue_v7_x4(const Params& p, f32x4v (&acc)[8][4], int tm, int tn, int arow,
                                                int bcolw, int lane) {
   unsigned short* C = (unsigned short*)p.C;
@@ -129,7 +137,7 @@ __device__ __forceinline__ void epilogue_v7_x4(const Params& p, f32x4v (&acc)[8]
       auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
       auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
       const long row = row_base + 16 * (2 * q + sub);
-      *(uint4*)(C + row * p.ldc + c0 + ch) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      st16<NT>(C + row * p.ldc + c0 + ch, s0[0], s1[0], s0[1], s1[1]);
     }
   }
 }
@@ -138,6 +146,7 @@ __device__ __forceinline__ void epilogue_v7_x4(const Params& p, f32x4v (&acc)[8]
 // as epilogue_v7_x4, applied to the gate, up and silu(gate) * up values (gate / up = column tiles j and j + 2 of
 // the wave's 64-column half: bcol<kEpiSwiGLU>).  Rounding as epilogue_t: the activation uses the bf16-rounded gate
 // and up, exactly what the backward reads back from gu.
+template <bool NT = false>
 __device__ __forceinline__ void epilogue_v7_swi_x4(const Params& p, f32x4v (&acc)[8][4], int tm, int tn, int arow,
                                                    int bcolw, int lane) {
   const int wsub = bcolw >> 6;                    // 64-column half of the tile: 32 gate + 32 up columns
@@ -178,9 +187,9 @@ __device__ __forceinline__ void epilogue_v7_swi_x4(const Params& p, f32x4v (&acc
       auto o1 = __builtin_amdgcn_permlane16_swap(o2[0][1], o2[1][1], false, false);
       const long row = row_base + 16 * (2 * q + sub);
       const int c = gc0 + ch;
-      *(uint4*)(p.C2 + row * p.ldc2 + c) = make_uint4(g0[0], g1[0], g0[1], g1[1]);
-      *(uint4*)(p.C2 + row * p.ldc2 + p.H + c) = make_uint4(u0[0], u1[0], u0[1], u1[1]);
-      *(uint4*)(out + row * p.ldc + c) = make_uint4(o0[0], o1[0], o0[1], o1[1]);
+      st16<NT>(p.C2 + row * p.ldc2 + c, g0[0], g1[0], g0[1], g1[1]);
+      st16<NT>(p.C2 + row * p.ldc2 + p.H + c, u0[0], u1[0], u0[1], u1[1]);
+      st16<NT>(out + row * p.ldc + c, o0[0], o1[0], o0[1], o1[1]);
     }
   }
 }
@@ -192,6 +201,8 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   constexpr int PLVL = (SCHED & 64) ? 3 : 1;                    // s_setprio level around the MFMA stream
   constexpr bool VS = (SCHED & 128) != 0;                        // the three-barrier spread schedule (ktile_v)
   constexpr bool X4 = (SCHED & 256) != 0;                        // 16-B epilogue stores on interior tiles
+  constexpr bool ROT = (SCHED & 512) != 0;                       // odd slots start their K loop half way
+  constexpr bool NTS = (SCHED & 1024) != 0;                      // non-temporal epilogue stores (X4 path)
   constexpr bool SWI = EPI == kEpiSwiGLU;
   __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
   const unsigned sbase = (unsigned)(size_t)(lds_char*)smem_raw;
@@ -252,9 +263,15 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   set_next(0);
   // descriptors of stream K-tile kk (0 <= kk < nt + 2; kk >= nt: the next tile's K-tile kk - nt)
   // (bases are < 2^48: the descriptor's high word is the address's high 16 bits, stride 0)
+  // SCHED bit 9: every workgroup of an odd slot runs its K-tiles rotated by nt / 2 (same products, another
+  // summation order), so the persistent grid's tiles end — and their epilogue stores burst — in two interleaved
+  // phases instead of all 256 CUs at once
+  const int rot = (ROT && (slot & 1)) ? nt / 2 : 0;
   auto desc = [&](int kk, u64 cur, u64 nxt, unsigned end) {
     const bool nx = kk >= nt;
-    const unsigned off = (unsigned)(nx ? kk - nt : kk) << 7;  // * BK * 2 bytes
+    int kt = nx ? kk - nt : kk;
+    if constexpr (ROT) kt = kt + rot >= nt ? kt + rot - nt : kt + rot;
+    const unsigned off = (unsigned)kt << 7;  // * BK * 2 bytes
     const u64 b = (nx ? nxt : cur) + off;
     const bool live = !nx || nlive;
     return i32x4{(int)(unsigned)b, (int)(unsigned)(b >> 32), live ? (int)(end - (unsigned)b) : 0, 0x00020000};
@@ -482,13 +499,13 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
       if constexpr (X4 && EPI == kEpiBF16) {
         // interior tile, 16-B aligned rows: the widened stores; otherwise the element-checked epilogue
         if ((ctm + 1) * BM <= p.M && (ctn + 1) * BN <= p.N && (p.ldc & 7) == 0 && ((size_t)p.C & 15) == 0)
-          epilogue_v7_x4(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+          epilogue_v7_x4<NTS>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
         else
           epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
       } else if constexpr (X4 && EPI == kEpiSwiGLU) {
         if ((ctm + 1) * BM <= p.M && (ctn + 1) * 128 <= p.H && (p.ldc & 7) == 0 && (p.ldc2 & 7) == 0 &&
             (p.H & 7) == 0 && ((size_t)p.C & 15) == 0 && ((size_t)p.C2 & 15) == 0)
-          epilogue_v7_swi_x4(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+          epilogue_v7_swi_x4<NTS>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
         else
           epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
       } else {
@@ -531,7 +548,8 @@ bool pd_gemm_v7(const pd::gm::Params& p, int layout, int epi, int sched, int cus
   }
   if (epi == kEpiSwiGLU && sched > 3) {   // the spread schedule with the SwiGLU epilogue
     switch (sched) {
-      PD_V7_CASE(kEpiSwiGLU, 128) PD_V7_CASE(kEpiSwiGLU, 384)
+      PD_V7_CASE(kEpiSwiGLU, 128) PD_V7_CASE(kEpiSwiGLU, 384) PD_V7_CASE(kEpiSwiGLU, 896)
+      PD_V7_CASE(kEpiSwiGLU, 1408) PD_V7_CASE(kEpiSwiGLU, 1920)
       default: return false;
     }
     return true;
@@ -541,7 +559,7 @@ bool pd_gemm_v7(const pd::gm::Params& p, int layout, int epi, int sched, int cus
       PD_V7_CASE(kEpiBF16, 6) PD_V7_CASE(kEpiBF16, 18) PD_V7_CASE(kEpiBF16, 22) PD_V7_CASE(kEpiBF16, 10)
       PD_V7_CASE(kEpiBF16, 42) PD_V7_CASE(kEpiBF16, 66) PD_V7_CASE(kEpiBF16, 86) PD_V7_CASE(kEpiBF16, 20)
       PD_V7_CASE(kEpiBF16, 14) PD_V7_CASE(kEpiBF16, 128) PD_V7_CASE(kEpiBF16, 130) PD_V7_CASE(kEpiBF16, 194)
-      PD_V7_CASE(kEpiBF16, 384)
+      PD_V7_CASE(kEpiBF16, 384) PD_V7_CASE(kEpiBF16, 896) PD_V7_CASE(kEpiBF16, 1408) PD_V7_CASE(kEpiBF16, 1920)
       default: return false;
     }
     return true;

@@ -96,7 +96,7 @@ def _workspace(t):
 
 def _launch(layout, epi, a, lda, b, ldb, c, ldc, c2, ldc2, bias, M, Nn, K, beta=0.0, H=0, name="fwd"):
     v = _variant(name)
-    ws, ws_bytes = _workspace(a) if epi != EPI_SWIGLU and v in (0, 4) else (0, 0)
+    ws, ws_bytes = _workspace(a) if epi != EPI_SWIGLU and v in (0, 4, 5) else (0, 0)
     gm = GROUP_M if _GROUP_FORCED else PASS_GROUP_M.get(name, GROUP_M)
     N.native().gemm(layout, epi, a.data_ptr(), lda, b.data_ptr(), ldb, c.data_ptr(), ldc, N.ptr(c2), ldc2,
                     N.ptr(bias), M, Nn, K, float(beta), H, gm, v, ws, ws_bytes, N.stream())

@@ -56,15 +56,30 @@ def _pd_name(op):
     return f"rec.{op.kind}.{q or n}"
 
 
+def _known_pure_fn(fn):
+    """torch operators and the framework's kernel entry points (ops/, pir/kernels.py) compute their outputs from
+    their inputs; any other recorded callable (a send / recv, a user hook, ...) may act outside the program."""
+    mod = getattr(fn, "__module__", None)
+    if mod is None:   # builtin methods of torch._C.TensorBase / VariableFunctions
+        owner = getattr(fn, "__objclass__", None) or getattr(fn, "__self__", None)
+        mod = getattr(owner, "__module__", None) or type(owner).__module__
+    mod = str(mod or "")
+    return mod.startswith("torch") or mod.startswith("paddle2_amd.ops") or mod.startswith("paddle2_amd.pir")
+
+
 def _side_effect(op, reads):
     if op.kind not in ("torch", "native"):
+        return True
+    if not _known_pure_fn(op.fn):
         return True
     n = _fn_name(op)
     if n.endswith("_") and not n.endswith("__"):   # in-place torch method (add_, copy_, ...)
         return True
-    outs = [v for v in op.outs if v is not None]
-    if any(v in reads for v in outs):              # an instruction writing a variable it reads
+    if n in ("__iadd__", "__isub__", "__imul__", "__itruediv__", "__ifloordiv__", "__ipow__", "__iand__",
+             "__ior__", "__ixor__", "__setitem__", "__delitem__") or "out" in op.kwargs or op.kwargs.get("inplace"):
         return True
+    # an op returning its input unchanged (x.long() on an int64 x, a no-op view) keeps the variable id: an alias,
+    # not a write
     if op.attrs.get("stream") or getattr(op.fn, "_pd_stream", None):   # collectives / copies on side streams
         return True
     return False

@@ -81,7 +81,7 @@ for name, K, Nn in SHAPES:
     if name == "gate_up":
         ra, rgu = with_variant(4, lambda: G.mm_swiglu(x, w))
         emit(name, "swiglu", "v4", timeit(lambda: with_variant(4, lambda: G.mm_swiglu(x, w))), flop)
-        for v in [v for v in VARS if v <= 10 or v in (192, 448)]:   # configurations with a SwiGLU instance
+        for v in [v for v in VARS if v <= 10 or v in (192, 448, 960, 1472, 1984)]:   # with a SwiGLU instance
             a, gu = with_variant(v, lambda: G.mm_swiglu(x, w))
             same = bool(torch.equal(a, ra) and torch.equal(gu, rgu))
             emit(name, "swiglu", f"v{v}+T", timeit(lambda: with_variant(v, lambda: G.mm_swiglu(x, w))), flop,

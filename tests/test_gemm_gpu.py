@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 dev = "cuda"
 
 
-@pytest.fixture(params=[None, 0, 4, 6, 7, 8, G.V7_SPREAD], ids=["per-pass", "v2", "v4", "v6", "v7", "v7b4", "v7spread"],
+@pytest.fixture(params=[None, 0, 4, 5, 6, 7, 8, G.V7_SPREAD], ids=["per-pass", "v2", "v4", "v4spread", "v6", "v7", "v7b4", "v7spread"],
                 autouse=True)
 def schedule(request, monkeypatch):
     """Every test runs on each kernel schedule (None = the per-pass default routing)."""
@@ -178,7 +178,7 @@ def test_schedule_variants_bitwise_equal(M, N, K, monkeypatch, schedule):
     monkeypatch.setattr(G, "SPLITK", False)   # tail split-K sums K-slices in another order (v2 / v4)
     outs = []
     swi = (N // 2) % 32 == 0
-    for v in (0, 4, 6, 7, 8, 9, 10, G.V7_SPREAD, 64 + 128):  # v7 (TN, on W^T for the forward) incl. spread
+    for v in (0, 4, 5, 6, 7, 8, 9, 10, G.V7_SPREAD, 64 + 128):  # v5: v4 spread; v7 (TN) incl. spread
         monkeypatch.setattr(G, "VARIANT", v)
         o32 = torch.zeros(K, N, device=dev)
         G.mm_wgrad(x, dy, o32)
