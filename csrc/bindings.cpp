@@ -27,6 +27,8 @@ int pd_gemm(int, int, const void*, long, const void*, long, void*, long, void*, 
 int pd_gemm_grouped(int, int, const void*, long, const void*, long, long, void*, long, long, void*, long, const void*,
                     long, const int*, int, int, int, int, int, int, float, int, int, void*);
 int pd_transpose16(const void*, void*, long, long, long, long, void*);
+int pd_gemm_f8(int, int, int, const void*, long, const void*, long, void*, long, const void*, const float*,
+               const float*, int, int, int, float, int, int, void*);
 long pd_ar_sig_bytes();
 int pd_bias_act(int, int, int, const void*, const void*, void*, long, int, long, long, void*);
 int pd_bias_act_bwd(int, int, int, const void*, const void*, const void*, void*, long, int, long, long, void*);
@@ -127,6 +129,13 @@ PYBIND11_MODULE(_C, m) {
     check(pd_gemm(layout, epi, P<const void*>(a), lda, P<const void*>(b), ldb, P<void*>(c), ldc, P<void*>(c2), ldc2,
                   P<const void*>(bias), M, N, K, beta, H, group_m, variant, P<void*>(ws), ws_bytes, P<void*>(st)),
           "gemm");
+  });
+  m.def("gemm_f8", [](int fa, int fb, int epi, uintptr_t a, long lda, uintptr_t b, long ldb, uintptr_t c, long ldc,
+                      uintptr_t bias, uintptr_t sa, uintptr_t sb, int M, int N, int K, float beta, int group_m, int cus,
+                      uintptr_t st) {
+    return pd_gemm_f8(fa, fb, epi, P<const void*>(a), lda, P<const void*>(b), ldb, P<void*>(c), ldc,
+                      P<const void*>(bias), P<const float*>(sa), P<const float*>(sb), M, N, K, beta, group_m, cus,
+                      P<void*>(st));
   });
   m.def("gemm_grouped", [](int layout, int epi, uintptr_t a, long lda, uintptr_t b, long ldb, long gsb, uintptr_t c,
                            long ldc, long gsc, uintptr_t c2, long ldc2, uintptr_t bias, long gsbias, uintptr_t goff,

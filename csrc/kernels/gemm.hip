@@ -824,6 +824,7 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   if (!ak && (lda % 8 || M % 8)) return -2;   // MN-major operands move whole 16-B column chunks
   if (!bk && (ldb % 8 || (epi == kEpiSwiGLU ? (2 * H) % 8 : N % 8))) return -2;
   if (epi == kEpiSwiGLU && H % 32) return -3;
+  if ((epi == kEpiGeLU || epi == kEpiDGeLU) && (!C2 || ldc2 < N)) return -3;   // the pre-activation operand
   hipStream_t st = (hipStream_t)stream;
   // v7 (gemm7.hip): the TN schedule, variants 7..10 = its SCHED 0..3; problems outside its domain run v6
   if ((variant >= 7 && variant <= 10) || variant >= 64) {
@@ -835,7 +836,7 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   // v4+ store 4 consecutive output columns per lane (8-B bf16 / 16-B fp32 accesses): rows must keep that alignment
   if (variant >= 4 && (ldc % 4 || (size_t)C % 16 || (C2 && (ldc2 % 4 || (size_t)C2 % 16)))) variant = 0;
   dim3 grid(p.tiles_m * p.tiles_n);
-  if (ws && (variant == 0 || variant == 4 || variant == 5) && epi != kEpiSwiGLU) {
+  if (ws && (variant == 0 || variant == 4 || variant == 5) && (epi == kEpiBF16 || epi == kEpiF32)) {
     const int g = plan_splitk(p, ws_bytes);
     if (g) grid = dim3(g);
   }
@@ -872,6 +873,9 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
     case 1 * 4 + 1: PD_GEMM_LAUNCH(true, false, kEpiF32); break;
     case 1 * 4 + 3: PD_GEMM_LAUNCH(true, true, kEpiF32); break;
     case 2 * 4 + 1: PD_GEMM_LAUNCH(true, false, kEpiSwiGLU); break;
+    case 3 * 4 + 1: PD_GEMM_LAUNCH(true, false, kEpiGeLU); break;
+    case 3 * 4 + 3: PD_GEMM_LAUNCH(true, true, kEpiGeLU); break;
+    case 4 * 4 + 3: PD_GEMM_LAUNCH(true, true, kEpiDGeLU); break;
 #ifdef PD_GEMM_DEBUG_VARIANTS
     // timing-only ablations (WRONG results): 16+: no vmcnt at the barrier, 20+: no lgkm syncs, 24+: no barrier
     case 16 + 3: gemm_kernel<true, true, kEpiBF16, 1><<<grid, NTHR, 0, st>>>(p); break;

@@ -24,7 +24,10 @@ constexpr int LDS_BYTES = 4 * TILE_BYTES;       // 2-stage ring, 128 KiB (stage 
 constexpr unsigned kOOB = 0x80000000u;          // voffset beyond num_records -> the load returns 0
 constexpr int kRecords = 0x7fffffff;
 
-enum Epi : int { kEpiBF16 = 0, kEpiF32 = 1, kEpiSwiGLU = 2 };
+// kEpiGeLU: C = gelu(acc + bias), C2 = acc + bias (the pre-activation the backward reads); kEpiDGeLU: C = acc *
+// gelu'(C2) with C2 = that saved pre-activation (reference funcs/fused_gemm_epilogue.h:382 GELU_AUX_BIAS forward,
+// :580 the gelu_grad backward).  Both: p.H = 1 for the tanh approximation, 0 for erf.
+enum Epi : int { kEpiBF16 = 0, kEpiF32 = 1, kEpiSwiGLU = 2, kEpiGeLU = 3, kEpiDGeLU = 4 };
 
 struct Params {
   const unsigned short* A;
@@ -36,7 +39,7 @@ struct Params {
   int M, N, K;
   int tiles_m, tiles_n, group_m;
   float beta;
-  int H;                        // swiglu: gate/up split (columns of the packed weight)
+  int H;                        // swiglu: gate/up split (columns of the packed weight); gelu: 1 = tanh form
   const void* zero;             // (ablation 7) 16 zero bytes for out-of-range global_load_lds lanes
   // grouped GEMM (MoE experts): goff [ngroups + 1] device offsets, never read back by the host.
   //  gmode 0 (fwd / dgrad): group g owns rows [goff[g], goff[g+1]) of A and C; B (and bias) advance by gsb
@@ -55,6 +58,9 @@ struct Params {
   // one past the last byte of each operand (v4: the buffer descriptors' num_records), null = unbounded
   const void* a_end;
   const void* b_end;
+  // fp8 GEMM (gemm8.hip): device dequant factors of A and B (the product is scaled by *sa * *sb), null = 1
+  const float* sa;
+  const float* sb;
 };
 
 // Tiles [t0, t0 + n) of the grouped order belong to XCD x (the chunking xcd_remap uses); the first `full`
@@ -260,6 +266,33 @@ __device__ __forceinline__ void mfma_agpr(f32x4v& c, const bf16x8& a, const bf16
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
+// GELU and its derivative in fp32 (torch's two forms: erf, and tanh with approximate = True)
+__device__ __forceinline__ float gelu_f(float x, int tanh_form) {
+  if (tanh_form) return 0.5f * x * (1.f + tanhf(0.7978845608f * (x + 0.044715f * x * x * x)));
+  return 0.5f * x * (1.f + erff(x * 0.70710678118f));
+}
+__device__ __forceinline__ float dgelu_f(float x, int tanh_form) {
+  if (tanh_form) {
+    const float x2 = x * x, t = tanhf(0.7978845608f * (x + 0.044715f * x2 * x));
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.7978845608f * (1.f + 0.134145f * x2);
+  }
+  return 0.5f * (1.f + erff(x * 0.70710678118f)) + x * 0.3989422804f * __expf(-0.5f * x * x);
+}
+
+// bf16 output value of the bf16-producing epilogues from the fp32 accumulator: the plain / bias value, gelu of the
+// (bf16-rounded, stored) pre-activation, or acc * gelu'(saved pre-activation `aux`)
+template <int EPI>
+__device__ __forceinline__ unsigned short epi_out(float acc, float bv, unsigned short aux, int tanh_form,
+                                                  unsigned short& pre) {
+  if constexpr (EPI == kEpiDGeLU) {
+    return f2bf(acc * dgelu_f(bf2f(aux), tanh_form));
+  } else {
+    pre = f2bf(acc + bv);
+    if constexpr (EPI == kEpiGeLU) return f2bf(gelu_f(bf2f(pre), tanh_form));
+    return pre;
+  }
+}
+
 template <int N, typename F, int... Is>
 __device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, Is...>) {
   (f(std::integral_constant<int, Is>{}), ...);
@@ -346,7 +379,7 @@ __device__ __forceinline__ void epilogue(const Params& p, f32x4v (&acc)[8][4], i
       const int c = tn * BN + bcolw + 16 * j + (lane & 15);
       if (c >= p.N) continue;
       float bv = 0.f;
-      if constexpr (EPI == kEpiBF16) {
+      if constexpr (EPI == kEpiBF16 || EPI == kEpiGeLU) {
         if (p.bias) bv = bf2f(p.bias[c]);
       }
 #pragma unroll
@@ -355,8 +388,11 @@ __device__ __forceinline__ void epilogue(const Params& p, f32x4v (&acc)[8][4], i
         for (int e = 0; e < 4; ++e) {
           const int r = row0 + 16 * i + e;
           if (r < p.M) {
-            if constexpr (EPI == kEpiBF16) {
-              ((unsigned short*)p.C)[(long)r * p.ldc + c] = f2bf(acc[i][j][e] + bv);
+            if constexpr (EPI != kEpiF32) {
+              unsigned short pre;
+              const unsigned short aux = EPI == kEpiDGeLU ? p.C2[(long)r * p.ldc2 + c] : 0;
+              ((unsigned short*)p.C)[(long)r * p.ldc + c] = epi_out<EPI>(acc[i][j][e], bv, aux, p.H, pre);
+              if constexpr (EPI == kEpiGeLU) p.C2[(long)r * p.ldc2 + c] = pre;
             } else {
               float* cp = (float*)p.C + (long)r * p.ldc + c;
               *cp = p.beta != 0.f ? acc[i][j][e] + p.beta * *cp : acc[i][j][e];
@@ -420,7 +456,7 @@ __device__ __forceinline__ void epilogue_t(const Params& p, f32x4v (&acc)[8][4],
       if (c >= p.N) continue;
       const bool vec = c + 3 < p.N;
       float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (EPI == kEpiBF16) {
+      if constexpr (EPI == kEpiBF16 || EPI == kEpiGeLU) {
         if (p.bias) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) bv[e] = c + e < p.N ? bf2f(p.bias[c + e]) : 0.f;
@@ -430,17 +466,32 @@ __device__ __forceinline__ void epilogue_t(const Params& p, f32x4v (&acc)[8][4],
       for (int i = 0; i < 8; ++i) {
         const int r = row0 + 16 * i;
         if (r >= p.M) continue;
-        if constexpr (EPI == kEpiBF16) {
+        if constexpr (EPI != kEpiF32) {
           unsigned short* cp = (unsigned short*)p.C + (long)r * p.ldc + c;
-          unsigned short o[4];
+          unsigned short* ap = EPI == kEpiBF16 ? nullptr : p.C2 + (long)r * p.ldc2 + c;
+          unsigned short o[4], pre[4], aux[4] = {0, 0, 0, 0};
+          if constexpr (EPI == kEpiDGeLU) {
+            if (vec) {
+              const uint2 a2 = *(const uint2*)ap;
+              aux[0] = a2.x & 0xffff; aux[1] = a2.x >> 16; aux[2] = a2.y & 0xffff; aux[3] = a2.y >> 16;
+            } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[i][j][e] + bv[e]);
+              for (int e = 0; e < 4; ++e) aux[e] = c + e < p.N ? ap[e] : 0;
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = epi_out<EPI>(acc[i][j][e], bv[e], aux[e], p.H, pre[e]);
           if (vec) {
             *(uint2*)cp = make_uint2(o[0] | (unsigned)o[1] << 16, o[2] | (unsigned)o[3] << 16);
+            if constexpr (EPI == kEpiGeLU)
+              *(uint2*)ap = make_uint2(pre[0] | (unsigned)pre[1] << 16, pre[2] | (unsigned)pre[3] << 16);
           } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              if (c + e < p.N) cp[e] = o[e];
+              if (c + e < p.N) {
+                cp[e] = o[e];
+                if constexpr (EPI == kEpiGeLU) ap[e] = pre[e];
+              }
           }
         } else {
           float* cp = (float*)p.C + (long)r * p.ldc + c;

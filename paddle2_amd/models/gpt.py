@@ -155,6 +155,14 @@ class GPTMLP(nn.Layer):
         self.fc2 = _proj(config, config.intermediate_size, config.hidden_size, "row")
 
     def forward(self, x):
+        f1, f2 = self.fc1, self.fc2
+        if (type(f1) is nn.Linear and type(f2) is nn.Linear and not (f1._forward_pre_hooks or f1._forward_post_hooks
+                                                                     or f2._forward_pre_hooks or f2._forward_post_hooks)):
+            args = (x._t, f1.weight._t, None if f1.bias is None else f1.bias._t, f2.weight._t,
+                    None if f2.bias is None else f2.bias._t)
+            if T.gelu_mlp_ok(*args):
+                # one autograd node with GELU in the GEMM epilogues (forward GELU_AUX_BIAS, backward dGELU)
+                return _wrap(T._GeluMLPFn.apply(*args, True))
         return self.fc2(F.gelu(self.fc1(x), approximate=True))
 
 

@@ -8,11 +8,14 @@ Recipe (HYBRID format): forward operands x, W in e4m3fn; the output gradient in 
 tensor role keeps an amax history on the device; the scale used for a cast is derived from the
 history BEFORE the cast (delayed scaling), and the cast kernel (csrc/kernels/fp8.hip) records the
 tensor's amax in the same pass, so quantization is one fused read of the bf16 tensor — plus the
-transposed copy the column-major B operand needs.  The GEMMs are plain library fp8 GEMMs
-(hipBLASLt through ``torch._scaled_mm``) with the inverse scales as dequant factors and bf16 out.
+transposed copy the column-major B operand needs.  The GEMMs run on the hand-written K=128 fp8 MFMA kernel
+(csrc/kernels/gemm8.hip, both operands K-major, the inverse scales as device dequant factors, bf16 out);
+shapes outside its domain (K % 256) go to hipBLASLt through ``torch._scaled_mm``.
 A CPU emulation (quantize -> dequantize -> fp32 matmul) keeps the recipe testable without a GPU.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -89,9 +92,53 @@ def cast(x2, meta: FP8TensorMeta, transpose=False, keep_rowmajor=True):
     return (q if (keep_rowmajor or not transpose) else None), (q.t().contiguous() if transpose else None)
 
 
+# "native" (default): the hand-written K=128 fp8 MFMA GEMM (csrc/kernels/gemm8.hip) for every shape in its domain;
+# "blas": hipBLASLt through torch._scaled_mm
+GEMM = os.environ.get("PADDLE2_AMD_FP8_GEMM", "native")
+_CUS = {}
+_FMT = {E4M3: 0, E5M2: 1}
+# (A format, B format, output) pairs the kernel is instantiated for: forward e4m3 x e4m3, dgrad e5m2 x e4m3,
+# wgrad e4m3 x e5m2 (bf16 or fp32 dW)
+_NATIVE_CASES = {(0, 0, torch.bfloat16), (1, 0, torch.bfloat16), (0, 1, torch.bfloat16), (0, 1, torch.float32)}
+
+
+def _cus(dev):
+    c = _CUS.get(dev.index)
+    if c is None:
+        c = _CUS[dev.index] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return c
+
+
+def mm_native(a, bT, inv_a, inv_b, out_dtype, bias=None):
+    """C[M, N] = (a[M, K] . bT[N, K]^T) * inv_a * inv_b (+ bias) on the native fp8 GEMM (both operands K-major
+    fp8, dequant factors as device scalars).  None when the problem is outside the kernel's domain."""
+    fa, fb = _FMT.get(a.dtype), _FMT.get(bT.dtype)
+    if (fa, fb, out_dtype) not in _NATIVE_CASES or a.stride(1) != 1 or bT.stride(1) != 1:
+        return None
+    if bias is not None and (out_dtype != torch.bfloat16 or bias.dtype != torch.bfloat16 or not bias.is_contiguous()):
+        return None
+    M, K = a.shape
+    Nn = bT.shape[0]
+    c = torch.empty(M, Nn, dtype=out_dtype, device=a.device)
+    rc = N.native().gemm_f8(fa, fb, 0 if out_dtype == torch.bfloat16 else 1, a.data_ptr(), a.stride(0),
+                            bT.data_ptr(), bT.stride(0), c.data_ptr(), c.stride(0), N.ptr(bias),
+                            inv_a.data_ptr(), inv_b.data_ptr(), M, Nn, K, 0.0, 4, _cus(a.device), N.stream())
+    if rc == -1:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"native fp8 GEMM failed: {rc}")
+    return c
+
+
 def _mm(a, b_colmajor, inv_a, inv_b, out_dtype, bias=None):
     """(a * inv_a) @ (b * inv_b) with a row-major [M, K] fp8 and b a column-major [K, N] fp8 view."""
     if a.device.type == "cuda":
+        if GEMM == "native" and N.use_native(a):
+            inv_a = inv_a.float().reshape(1).contiguous()
+            inv_b = inv_b.float().reshape(1).contiguous()
+            c = mm_native(a, b_colmajor.t(), inv_a, inv_b, out_dtype, bias)
+            if c is not None:
+                return c
         return torch._scaled_mm(a, b_colmajor, scale_a=inv_a, scale_b=inv_b, bias=bias, out_dtype=out_dtype)
     y = (a.float() * inv_a) @ (b_colmajor.float() * inv_b)
     if bias is not None:

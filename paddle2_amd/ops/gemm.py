@@ -22,7 +22,7 @@ import torch
 from . import _native as N
 
 LAYOUT_AK, LAYOUT_BK = 1, 2
-EPI_BF16, EPI_F32, EPI_SWIGLU = 0, 1, 2
+EPI_BF16, EPI_F32, EPI_SWIGLU, EPI_GELU, EPI_DGELU = 0, 1, 2, 3, 4
 GROUP_M = int(os.environ.get("PADDLE2_AMD_GEMM_GROUP_M", "8"))
 _GROUP_FORCED = "PADDLE2_AMD_GEMM_GROUP_M" in os.environ
 # kernel schedule (csrc/kernels/gemm.hip): 0 = v2 (8 waves, 2 per SIMD, 128x64 wave tiles), 4 = v4 (4 waves,
@@ -96,7 +96,7 @@ def _workspace(t):
 
 def _launch(layout, epi, a, lda, b, ldb, c, ldc, c2, ldc2, bias, M, Nn, K, beta=0.0, H=0, name="fwd"):
     v = _variant(name)
-    ws, ws_bytes = _workspace(a) if epi != EPI_SWIGLU and v in (0, 4, 5) else (0, 0)
+    ws, ws_bytes = _workspace(a) if epi in (EPI_BF16, EPI_F32) and v in (0, 4, 5) else (0, 0)
     gm = GROUP_M if _GROUP_FORCED else PASS_GROUP_M.get(name, GROUP_M)
     N.native().gemm(layout, epi, a.data_ptr(), lda, b.data_ptr(), ldb, c.data_ptr(), ldc, N.ptr(c2), ldc2,
                     N.ptr(bias), M, Nn, K, float(beta), H, gm, v, ws, ws_bytes, N.stream())
@@ -159,6 +159,35 @@ def mm_wgrad_bf16(x2, dy2, out=None):
         out = torch.empty(K, Nn, dtype=x2.dtype, device=x2.device)
     _launch(0, EPI_BF16, x2, x2.stride(0), dy2, dy2.stride(0), out, out.stride(0), None, 0, None, K, Nn, M,
             name="wgrad_bf16")
+    return out
+
+
+def mm_gelu(x2, w, bias=None, approximate=True):
+    """a[M, N] = gelu(x2 @ w + bias), h[M, N] = x2 @ w + bias (the pre-activation, kept for the backward) from ONE
+    GEMM (GELU_AUX_BIAS epilogue, reference funcs/fused_gemm_epilogue.h:382).  -> (a, h)."""
+    M, K = x2.shape
+    Nn = w.shape[1]
+    a = torch.empty(M, Nn, dtype=x2.dtype, device=x2.device)
+    h = torch.empty(M, Nn, dtype=x2.dtype, device=x2.device)
+    if _v7("fwd", K):
+        wt = _wt(w)
+        _launch(LAYOUT_AK | LAYOUT_BK, EPI_GELU, x2, x2.stride(0), wt, wt.stride(0), a, a.stride(0), h, h.stride(0),
+                bias, M, Nn, K, 0.0, int(bool(approximate)))
+        return a, h
+    _launch(LAYOUT_AK, EPI_GELU, x2, x2.stride(0), w, w.stride(0), a, a.stride(0), h, h.stride(0), bias, M, Nn, K,
+            0.0, int(bool(approximate)))
+    return a, h
+
+
+def mm_dgrad_dgelu(dy2, w, h, approximate=True):
+    """dh[M, K] = (dy2[M, N] @ w[K, N]^T) * gelu'(h[M, K]): the next linear's input gradient with the GELU backward
+    in its epilogue (reference funcs/fused_gemm_epilogue.h:580) — the product is never rounded before the scale."""
+    M, Nn = dy2.shape
+    K = w.shape[0]
+    assert h.shape == (M, K) and h.stride(1) == 1 and h.dtype == dy2.dtype
+    out = torch.empty(M, K, dtype=dy2.dtype, device=dy2.device)
+    _launch(LAYOUT_AK | LAYOUT_BK, EPI_DGELU, dy2, dy2.stride(0), w, w.stride(0), out, out.stride(0), h, h.stride(0),
+            None, M, K, Nn, 0.0, int(bool(approximate)), name="dgrad")
     return out
 
 

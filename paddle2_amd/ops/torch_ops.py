@@ -556,6 +556,77 @@ def linear(x, w, b=None):
     return y + b if b is not None else y
 
 
+class _GeluMLPFn(torch.autograd.Function):
+    """y = gelu(x @ W1 + b1) @ W2 + b2 (the GPT MLP) as one autograd node, so the GELU rides on the GEMM epilogues in
+    both directions (reference funcs/fused_gemm_epilogue.h:382 GELU_AUX_BIAS forward, :580 gelu_grad backward;
+    incubate fused_feedforward):
+      forward   a, h = gelu(x W1 + b1), x W1 + b1       one GEMM, two outputs (h is what the backward needs)
+                y = a W2 + b2                            bias epilogue
+      backward  dh = (dy W2^T) * gelu'(h)               the dgrad GEMM with the dGELU epilogue
+                dW2 = a^T dy, dW1 = x^T dh (fp32 main grads when the weights have them), db = column sums
+                dx = dh W1^T"""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, approximate):
+        from . import gemm as G
+
+        K = w1.shape[0]
+        x2 = x.reshape(-1, K)
+        a, h = G.mm_gelu(x2, w1, None if b1 is None else b1.contiguous(), approximate)
+        y = G.mm_fwd(a, w2, bias=None if b2 is None else b2.contiguous())
+        ctx.save_for_backward(x2, w1, w2, a, h)
+        ctx.meta = (x.shape, b1 is not None, b2 is not None, approximate)
+        ctx.gt = (getattr(w1, "_p2_gt", None), getattr(w2, "_p2_gt", None))
+        return y.view(*x.shape[:-1], w2.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import gemm as G
+
+        x2, w1, w2, a, h = ctx.saved_tensors
+        xshape, has_b1, has_b2, approximate = ctx.meta
+        gt1, gt2 = ctx.gt
+        dy2 = dy.reshape(-1, w2.shape[1])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dh = G.mm_dgrad_dgelu(dy2, w2, h, approximate)
+        need = ctx.needs_input_grad
+        dw2 = weight_grad(a, dy2, gt2) if need[3] else None
+        db2 = bias_grad(dy2) if has_b2 and need[4] else None
+        dw1 = weight_grad(x2, dh, gt1) if need[1] else None
+        db1 = bias_grad(dh) if has_b1 and need[2] else None
+        dx = G.mm_dgrad(dh, w1).view(xshape) if need[0] else None
+        return dx, dw1, db1, dw2, db2, None
+
+
+_FUSED_GELU_MLP = _os.environ.get("PADDLE2_AMD_FUSED_GELU_MLP", "1") != "0"
+
+
+def gelu_mlp_ok(x, w1, b1, w2, b2):
+    """The fused GELU-MLP node applies: bf16 GPU tensors of one dtype, native GEMM shapes, no distributed or
+    zero-bubble weight-gradient routing."""
+    from . import gemm as G
+
+    def _bias_ok(b, n):
+        return b is None or (b.dtype == x.dtype and tuple(b.shape) == (n,))
+
+    return (_FUSED_GELU_MLP and not any(isinstance(t, _DTensor) for t in (x, w1, w2)) and not WeightGradStore.route
+            and w1.dim() == 2 and w2.dim() == 2 and w1.dtype == x.dtype == w2.dtype
+            and x.shape[-1] == w1.shape[0] and w1.shape[1] == w2.shape[0] and G.enabled(x)
+            and _bias_ok(b1, w1.shape[1]) and _bias_ok(b2, w2.shape[1]) and x.is_contiguous()
+            and G.supported_fwd(x.reshape(-1, w1.shape[0]), w1) and w2.shape[1] % 8 == 0
+            and _pass_native("fwd", x) and _pass_native("dgrad", x))
+
+
+def gelu_mlp(x, w1, b1, w2, b2, approximate=True):
+    """gelu(x @ W1 + b1) @ W2 + b2 with Paddle-layout weights: the fused node when gelu_mlp_ok, the plain
+    composition otherwise."""
+    if gelu_mlp_ok(x, w1, b1, w2, b2):
+        return _GeluMLPFn.apply(x, w1, b1, w2, b2, bool(approximate))
+    t = linear(x, w1, b1)
+    return linear(torch.nn.functional.gelu(t, approximate="tanh" if approximate else "none"), w2, b2)
+
+
 class _SwiGLULinearFn(torch.autograd.Function):
     """a = swiglu(x @ W) for the packed gate|up projection W [K, 2H] (Llama MLP up half), one node:
     forward through W^T (fast hipBLASLt layout); backward's SwiGLU kernel also writes dY^T, so the weight

@@ -91,6 +91,52 @@ def test_swiglu_epilogue(M, K, H):
     assert _rel(a, a_ref) < 8e-3
 
 
+GELU_SHAPES = [(256, 256, 128), (300, 520, 72), (1000, 264, 1032), (2048, 5120, 5120)]
+
+
+@pytest.mark.parametrize("M,N,K", GELU_SHAPES)
+@pytest.mark.parametrize("approx", [True, False])
+def test_gelu_epilogue(M, N, K, approx):
+    """gelu(x @ W + b) and the stored pre-activation from one GEMM vs the fp32 reference."""
+    x, w, b = _rand(M, K, seed=20), _rand(K, N, seed=21, scale=K ** -0.5), _rand(N, seed=22)
+    a, h = G.mm_gelu(x, w, b, approximate=approx)
+    h_ref = x.float() @ w.float() + b.float()
+    assert _rel(h, h_ref) < 8e-3
+    a_ref = torch.nn.functional.gelu(h.float(), approximate="tanh" if approx else "none")  # from the stored h
+    assert _rel(a, a_ref) < 8e-3
+
+
+@pytest.mark.parametrize("M,N,K", GELU_SHAPES)
+@pytest.mark.parametrize("approx", [True, False])
+def test_dgelu_epilogue(M, N, K, approx):
+    """dh = (dy @ W^T) * gelu'(h) vs autograd through an fp32 gelu."""
+    dy, w, h = _rand(M, N, seed=23), _rand(K, N, seed=24, scale=N ** -0.5), _rand(M, K, seed=25)
+    hr = h.float().requires_grad_()
+    torch.nn.functional.gelu(hr, approximate="tanh" if approx else "none").backward(dy.float() @ w.float().t())
+    assert _rel(G.mm_dgrad_dgelu(dy, w, h, approximate=approx), hr.grad) < 8e-3
+
+
+def test_gelu_mlp_node_matches_fp32():
+    """The fused GPT MLP node (torch_ops._GeluMLPFn): output and every gradient vs the fp32 composition."""
+    from paddle2_amd.ops import torch_ops as T
+
+    M, H, F4 = 1024, 512, 2048
+    x = _rand(M, H, seed=26)
+    w1, b1 = _rand(H, F4, seed=27, scale=H ** -0.5), _rand(F4, seed=28, scale=0.1)
+    w2, b2 = _rand(F4, H, seed=29, scale=F4 ** -0.5), _rand(H, seed=30, scale=0.1)
+    dy = _rand(M, H, seed=31)
+    ts = [t.clone().requires_grad_() for t in (x, w1, b1, w2, b2)]
+    assert T.gelu_mlp_ok(*ts)
+    y = T._GeluMLPFn.apply(*ts, True)
+    y.backward(dy)
+    rs = [t.float().requires_grad_() for t in (x, w1, b1, w2, b2)]
+    yr = torch.nn.functional.gelu(rs[0] @ rs[1] + rs[2], approximate="tanh") @ rs[3] + rs[4]
+    yr.backward(dy.float())
+    assert _rel(y, yr) < 1e-2
+    for t, r in zip(ts, rs):
+        assert _rel(t.grad, r.grad) < 1.5e-2
+
+
 @pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 4096), (4096, 11008)])
 def test_llama7b_shapes_m32768(N, K):
     """bench shapes at M = 32768 tokens: fwd, dgrad, fp32 wgrad vs fp32 references (row-sampled)."""
