@@ -6,7 +6,10 @@ reductions (keepdim), add / subtract / multiply / divide / maximum / minimum and
 constant-like-x primitive) — which compiler-style passes (and the interpreter) handle uniformly.  Rules:
 softmax, log_softmax, gelu (erf and tanh forms), silu / swish, mish, softplus, relu, relu6, leaky_relu, elu,
 hardswish, hardsigmoid, square, reciprocal, swiglu, rms_norm, layer_norm (when its Mean / Variance side outputs
-are unused), mean and logsumexp."""
+are unused), mean and logsumexp here; the rest of the reference's composite set (norms, losses, shape ops,
+embedding, dropout, more activations) in ``decomposition.rules``.  ``decomposition.vjp.append_backward`` then
+differentiates a decomposed program through per-primitive VJP rules (reference
+paddle/fluid/primitive/rule/vjp/details.h)."""
 from __future__ import annotations
 
 import math
@@ -24,6 +27,11 @@ class _Builder:
 
     def op(self, name, operands, like, **attrs):
         o = Operation(name, operands, [(list(like.shape) if like.shape is not None else None, like.dtype)], attrs)
+        self.p.block.insert_before(self.anchor, o)
+        return o.result(0)
+
+    def op2(self, name, operands, rshape, rdtype, **attrs):
+        o = Operation(name, operands, [(None if rshape is None else list(rshape), rdtype)], attrs)
         self.p.block.insert_before(self.anchor, o)
         return o.result(0)
 
@@ -232,6 +240,16 @@ _RULES = {"pd_op.softmax": _softmax, "pd_op.log_softmax": lambda b, op: _softmax
           "pd_op.softplus": _softplus, "pd_op.mish": _mish, "pd_op.hardsigmoid": _hardsigmoid,
           "pd_op.hardswish": _hardswish, "pd_op.square": _square, "pd_op.reciprocal": _reciprocal,
           "pd_op.swiglu": _swiglu, "pd_op.rms_norm": _rms_norm, "pd_op.mean": _mean, "pd_op.logsumexp": _logsumexp}
+
+
+from .rules import EXTRA_PRIMITIVES as _EXTRA, RULES as _MORE  # noqa: E402
+
+_RULES.update(_MORE)
+PRIMITIVES = PRIMITIVES | _EXTRA
+
+
+def has_rule(name):
+    return name in _RULES
 
 
 def decompose(program, src_vars=None, blacklist=frozenset(), whitelist=frozenset()):

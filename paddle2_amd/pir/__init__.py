@@ -209,7 +209,7 @@ def translate_to_pir(program, feed_vars, fetch_vars):
 
 
 # ============================================================================================ interpreter
-def _kernels():
+def _kernels(device=None):
     from ..ops import fused as FU
     from ..ops import torch_ops as T
     from ..static.pdmodel import PdProgram
@@ -237,7 +237,37 @@ def _kernels():
         "max": lambda v, at: [torch.amax(v[0], dim=at["axis"], keepdim=at.get("keepdim", True))],
         "sum": lambda v, at: [torch.sum(v[0], dim=at["axis"], keepdim=at.get("keepdim", True))]
         if "axis" in at else None,
-        "full": lambda v, at: [torch.full(at["shape"], at["value"], dtype=at.get("dtype", torch.float32))],
+        "full": lambda v, at: [torch.full(at["shape"], at["value"], dtype=at.get("dtype", torch.float32),
+                                          device=device)],
+        # primitives of decomposition.rules / decomposition.vjp
+        "sqrt": lambda v, at: [torch.sqrt(v[0])],
+        "abs": lambda v, at: [torch.abs(v[0])],
+        "sign": lambda v, at: [torch.sign(v[0])],
+        "floor": lambda v, at: [torch.floor(v[0])],
+        "pow": lambda v, at: [torch.pow(v[0], at["y"])],
+        "reshape": lambda v, at: [v[0].reshape(at["shape"])],
+        "concat": lambda v, at: [torch.cat(v, dim=at["axis"])],
+        "gather": lambda v, at: [torch.index_select(v[0], at["axis"], v[1].reshape(-1).long())],
+        "take_along_axis": lambda v, at: [torch.take_along_dim(v[0], v[1].long(), dim=at["axis"])],
+        "matmul": lambda v, at: [torch.matmul(v[0].mT if at.get("transpose_x") else v[0],
+                                              v[1].mT if at.get("transpose_y") else v[1])],
+        "cast": lambda v, at: [v[0].to(at["dtype"])],
+        "where": lambda v, at: [torch.where(v[0], v[1], v[2])],
+        "greater_than": lambda v, at: [torch.gt(v[0], v[1])],
+        "greater_equal": lambda v, at: [torch.ge(v[0], v[1])],
+        "less_than": lambda v, at: [torch.lt(v[0], v[1])],
+        "less_equal": lambda v, at: [torch.le(v[0], v[1])],
+        "equal": lambda v, at: [torch.eq(v[0], v[1])],
+        "not_equal": lambda v, at: [torch.ne(v[0], v[1])],
+        "arange": lambda v, at: [torch.arange(at["start"], at["end"], at["step"], dtype=at.get("dtype"),
+                                              device=device)],
+        "uniform": lambda v, at: [_uniform(at, device)],
+        "expand": lambda v, at: [v[0].expand(at["shape"]).contiguous()],
+        "transpose": lambda v, at: [v[0].permute(at["perm"])],
+        "slice": lambda v, at: [v[0].narrow(at["axis"], at["start"], at["end"] - at["start"])],
+        "index_add": lambda v, at: [torch.index_add(v[0], at["axis"], v[1].reshape(-1).long(), v[2])],
+        "scatter_add_along": lambda v, at: [torch.scatter_add(v[0], at["axis"], v[1].long(), v[2])],
+        "min": lambda v, at: [torch.amin(v[0], dim=at["axis"], keepdim=at.get("keepdim", True))],
     }
 
     def fused_gemm_epilogue(op, vals, at):
@@ -248,6 +278,13 @@ def _kernels():
     return via_desc, prim, fused_gemm_epilogue
 
 
+def _uniform(at, device):
+    g = None
+    if at.get("seed"):
+        g = torch.Generator(device=device or "cpu").manual_seed(int(at["seed"]))
+    return torch.rand(at["shape"], generator=g, device=device) * (at["max"] - at["min"]) + at["min"]
+
+
 _BINARY_PRIM = {"pd_op.subtract": torch.sub, "pd_op.divide": torch.div, "pd_op.multiply": torch.mul,
                 "pd_op.add": torch.add, "pd_op.maximum": torch.maximum, "pd_op.minimum": torch.minimum}
 
@@ -256,7 +293,13 @@ _BINARY_PRIM = {"pd_op.subtract": torch.sub, "pd_op.divide": torch.div, "pd_op.m
 def run(program, feeds, device=None):
     """Execute a PIR Program: feeds in pd_op.data column order -> fetch values in pd_op.fetch column order
     (inference: no autograd graph)."""
-    via_desc, prim, fge = _kernels()
+    if device is None:
+        for f in feeds:
+            t = f._t if hasattr(f, "_t") else f
+            if isinstance(t, torch.Tensor):
+                device = t.device
+                break
+    via_desc, prim, fge = _kernels(device)
     env = {}
     out = {}
     for op in program.block.ops:
