@@ -27,6 +27,8 @@ int pd_gemm(int, int, const void*, long, const void*, long, void*, long, void*, 
 int pd_gemm_grouped(int, int, const void*, long, const void*, long, long, void*, long, long, void*, long, const void*,
                     long, const int*, int, int, int, int, int, int, float, int, int, void*);
 int pd_transpose16(const void*, void*, long, long, long, long, void*);
+int pd_gemm_conv(const void*, long, const void*, const void*, const void*, long, void*, long, int, int, int, int,
+                 int, int, int, int, int, int, int, int, void*);
 int pd_gemm_f8(int, int, int, const void*, long, const void*, long, void*, long, const void*, const float*,
                const float*, int, int, int, float, int, int, void*);
 long pd_ar_sig_bytes();
@@ -129,6 +131,13 @@ PYBIND11_MODULE(_C, m) {
     check(pd_gemm(layout, epi, P<const void*>(a), lda, P<const void*>(b), ldb, P<void*>(c), ldc, P<void*>(c2), ldc2,
                   P<const void*>(bias), M, N, K, beta, H, group_m, variant, P<void*>(ws), ws_bytes, P<void*>(st)),
           "gemm");
+  });
+  m.def("gemm_conv", [](uintptr_t a, long lda, uintptr_t a_lo, uintptr_t a_hi, uintptr_t b, long ldb, uintptr_t c,
+                        long ldc, int M, int N, int K, int taps, int kw, int pitch, int pad_h, int pad_w, int sign,
+                        int kpb_log2, int group_m, int cus, uintptr_t st) {
+    return pd_gemm_conv(P<const void*>(a), lda, P<const void*>(a_lo), P<const void*>(a_hi), P<const void*>(b), ldb,
+                        P<void*>(c), ldc, M, N, K, taps, kw, pitch, pad_h, pad_w, sign, kpb_log2, group_m, cus,
+                        P<void*>(st));
   });
   m.def("gemm_f8", [](int fa, int fb, int epi, uintptr_t a, long lda, uintptr_t b, long ldb, uintptr_t c, long ldc,
                       uintptr_t bias, uintptr_t sa, uintptr_t sb, int M, int N, int K, float beta, int group_m, int cus,

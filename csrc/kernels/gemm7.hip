@@ -85,6 +85,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   constexpr bool X4 = (SCHED & 256) != 0;                        // 16-B epilogue stores on interior tiles
   constexpr bool ROT = (SCHED & 512) != 0;                       // odd slots start their K loop half way
   constexpr bool NTS = (SCHED & 1024) != 0;                      // non-temporal epilogue stores (X4 path)
+  constexpr bool CONV = (SCHED & 2048) != 0;                     // implicit-GEMM convolution (row-shifted A taps)
   constexpr bool SWI = EPI == kEpiSwiGLU;
   __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
   const unsigned sbase = (unsigned)(size_t)(lds_char*)smem_raw;
@@ -158,8 +159,30 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
     const bool live = !nx || nlive;
     return i32x4{(int)(unsigned)b, (int)(unsigned)(b >> 32), live ? (int)(end - (unsigned)b) : 0, 0x00020000};
   };
+  // SCHED bit 11, implicit-GEMM convolution over a zero-bordered NHWC input (ops/conv_gemm.py): K = taps x C, and
+  // K-tile kt of tap t = kt >> cv_kpb_log2 reads the A rows shifted by sign * ((kh - pad_h) * pitch + kw - pad_w)
+  // pixels — only the descriptor base moves, per lane nothing changes (taps past cv_taps read the centre rows and
+  // meet zero weight columns).
+  auto desc_a = [&](int kk) {
+    if constexpr (!CONV) {
+      return desc(kk, ca, na, a_end);
+    } else {
+      const bool nx = kk >= nt;
+      const int kt = nx ? kk - nt : kk;
+      const int tap = kt >> p.cv_kpb_log2;
+      const int kc = kt & ((1 << p.cv_kpb_log2) - 1);
+      int rows = 0;
+      if (tap < p.cv_taps) {
+        const int kh = tap / p.cv_kw, kw = tap - kh * p.cv_kw;
+        rows = p.cv_sign * ((kh - p.cv_pad_h) * p.cv_pitch + (kw - p.cv_pad_w));
+      }
+      const u64 b = (nx ? na : ca) + (u64)((long)rows * p.lda * 2 + ((long)kc << 7));
+      const bool live = !nx || nlive;
+      return i32x4{(int)(unsigned)b, (int)(unsigned)(b >> 32), live ? (int)(a_end - (unsigned)b) : 0, 0x00020000};
+    }
+  };
   auto descs = [&](int kk, i32x4& sa, i32x4& sb) {
-    sa = desc(kk, ca, na, a_end);
+    sa = desc_a(kk);
     sb = desc(kk, cb, nb, b_end);
   };
 
@@ -260,7 +283,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
           sb = desc(kk, cb, nb, b_end);
           asm volatile("" : "+s"(sb));
         } else {
-          sa = desc(kk, ca, na, a_end);
+          sa = desc_a(kk);
           asm volatile("" : "+s"(sa));
         }
       }
@@ -351,7 +374,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
         int kk = k + 2;
         asm volatile("" : "+s"(kk));
         if constexpr (n == 2) {
-          sa = desc(kk, ca, na, a_end);
+          sa = desc_a(kk);
           asm volatile("" : "+s"(sa));
         } else {
           sb = desc(kk, cb, nb, b_end);
@@ -462,4 +485,52 @@ bool pd_gemm_v7(const pd::gm::Params& p, int layout, int epi, int sched, int cus
 #undef PD_V7_CASE
 #undef PD_V7
   return true;
+}
+
+// Implicit-GEMM convolution on the spread TN schedule (ops/conv_gemm.py): C[M, N] = sum over taps t of
+// A[r + shift_t, :] . B[:, t*Cin : (t+1)*Cin]^T with A the zero-bordered NHWC input flattened to [pixels, lda]
+// (A points at padded pixel 0; [a_lo, a_hi) is the allocation, guard rows included) and B the tap-major weight
+// [N, K] (K = taps x Cin rounded up to an even number of 64-wide K-tiles, zero columns past the taps).
+// Returns -1 outside the kernel's domain.
+extern "C" int pd_gemm_conv(const void* A, long lda, const void* a_lo, const void* a_hi, const void* B, long ldb,
+                            void* C, long ldc, int M, int N, int K, int taps, int kw, int pitch, int pad_h, int pad_w,
+                            int sign, int kpb_log2, int group_m, int cus, void* stream) {
+  using namespace pd::gm;
+  if (M <= 0 || N <= 0 || K % 128 || lda % 8 || ldb % 8 || ldc % 4 || (size_t)C % 16) return -1;
+  if ((64L << kpb_log2) != lda) return -1;   // one tap = one row of channels = 2^kpb_log2 K-tiles
+  // every tap's shifted rows must stay inside [a_lo, a_hi)
+  long lo_rows = 0, hi_rows = 0;
+  for (int t = 0; t < taps; ++t) {
+    const int kh = t / kw, kx = t - kh * kw;
+    const long r = (long)sign * ((long)(kh - pad_h) * pitch + (kx - pad_w));
+    lo_rows = std::min(lo_rows, r);
+    hi_rows = std::max(hi_rows, r);
+  }
+  const char* a = (const char*)A;
+  if (a + lo_rows * lda * 2 < (const char*)a_lo) return -1;
+  if (a + (long)(M + hi_rows) * lda * 2 > (const char*)a_hi) return -1;
+  const long a_bytes = (const char*)a_hi - a, b_bytes = ((long)(N - 1) * ldb + K) * 2;
+  if (a_bytes >= 0x7fffffffL || b_bytes >= 0x7fffffffL || (const char*)a_lo < a - 0x3fffffffL) return -1;
+  Params p;
+  p.A = (const unsigned short*)A;
+  p.B = (const unsigned short*)B;
+  p.C = C;
+  p.C2 = nullptr;
+  p.bias = nullptr;
+  p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldc2 = 0;
+  p.M = M; p.N = N; p.K = K; p.beta = 0.f; p.H = 0;
+  p.zero = nullptr;
+  p.goff = nullptr; p.ngroups = 0; p.gmode = 0; p.gsb = p.gsc = p.gsbias = 0;
+  p.part = nullptr; p.ksplit = 1; p.kchunk = 0; p.tail_cap = 0; p.cpx = cus / 8;
+  p.a_end = a_hi;
+  p.b_end = (const char*)B + b_bytes;
+  p.sa = p.sb = nullptr;
+  p.cv_kpb_log2 = kpb_log2; p.cv_kw = kw; p.cv_taps = taps; p.cv_pitch = pitch; p.cv_pad_h = pad_h;
+  p.cv_pad_w = pad_w; p.cv_sign = sign;
+  p.tiles_m = (M + BM - 1) / BM;
+  p.tiles_n = (N + BN - 1) / BN;
+  p.group_m = group_m > 0 ? group_m : 4;
+  const dim3 grid(std::min(p.tiles_m * p.tiles_n, cus));
+  gemm_v7_kernel<kEpiBF16, 384 | 2048><<<grid, NTHR4, 0, (hipStream_t)stream>>>(p);
+  return (int)hipGetLastError();
 }

@@ -61,6 +61,9 @@ struct Params {
   // fp8 GEMM (gemm8.hip): device dequant factors of A and B (the product is scaled by *sa * *sb), null = 1
   const float* sa;
   const float* sb;
+  // implicit-GEMM convolution (gemm7.hip SCHED bit 11): K-tiles per tap (log2), taps, kernel width, padded row pitch,
+  // padding and the shift's sign (+1 forward, -1 input gradient)
+  int cv_kpb_log2, cv_taps, cv_kw, cv_pitch, cv_pad_h, cv_pad_w, cv_sign;
 };
 
 // Tiles [t0, t0 + n) of the grouped order belong to XCD x (the chunking xcd_remap uses); the first `full`

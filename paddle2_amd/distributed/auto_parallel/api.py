@@ -4,12 +4,12 @@ python/paddle/distributed/auto_parallel/api.py — ``shard_tensor`` :206, ``dten
 ``shard_dataloader`` :3208, ``to_static``/``DistModel`` :2110/:2693, ``unshard_dtensor`` :2854;
 process_mesh.py; placement_type.py).
 
-MI355X design: a Paddle DistTensor is our Tensor whose storage is a torch ``DTensor`` (local shard +
-``DeviceMesh`` built from the ProcessMesh's rank grid + placements).  The framework's hot ops (norms, linear,
-RoPE, flash attention, SwiGLU, embedding) dispatch DistTensor arguments at op entry through the SPMD rules of
-``spmd_rules.py`` and the framework's own reshard engine (``dist_ops.py`` / ``reshard.py``), running the native
-kernels on the local shards; ``reshard`` below uses the same engine.  Other ops (views, pointwise) keep
-torch's DTensor propagation.
+MI355X design: a Paddle DistTensor is our Tensor whose storage is the framework's own ``DistTensor``
+(dist_tensor.py: local shard + the ProcessMesh's communicators + placements).  The framework's hot ops (norms,
+linear, RoPE, flash attention, SwiGLU, embedding) dispatch DistTensor arguments at op entry through the SPMD rules
+of ``spmd_rules.py`` and the reshard engine (``dist_ops.py`` / ``reshard.py``), running the native kernels on the
+local shards; every other op goes through DistTensor's aten-level SPMD dispatch; ``reshard`` below uses the same
+engine.
 """
 from __future__ import annotations
 
@@ -17,7 +17,6 @@ import copy
 
 import numpy as np
 import torch
-from torch.distributed import tensor as _dt
 
 from ...framework.tensor import Tensor
 from ...framework.place import current_torch_device
@@ -26,88 +25,8 @@ _wrap = Tensor._wrap
 
 
 # ----------------------------------------------------------------------------- placements
-class Placement:
-    def is_shard(self, dim=None):
-        return False
-
-    def is_replicated(self):
-        return False
-
-    def is_partial(self):
-        return False
-
-
-class Shard(Placement):
-    def __init__(self, dim, **kw):
-        self.dim = int(dim)
-
-    def get_dim(self):
-        return self.dim
-
-    def is_shard(self, dim=None):
-        return dim is None or dim == self.dim
-
-    def _torch(self):
-        return _dt.Shard(self.dim)
-
-    def __eq__(self, o):
-        return isinstance(o, Shard) and o.dim == self.dim
-
-    def __hash__(self):
-        return hash(("S", self.dim))
-
-    def __repr__(self):
-        return f"Shard(dim={self.dim})"
-
-
-class Replicate(Placement):
-    def is_replicated(self):
-        return True
-
-    def _torch(self):
-        return _dt.Replicate()
-
-    def __eq__(self, o):
-        return isinstance(o, Replicate)
-
-    def __hash__(self):
-        return hash("R")
-
-    def __repr__(self):
-        return "Replicate()"
-
-
-class Partial(Placement):
-    def __init__(self, reduce_type=None):
-        from ..collective import ReduceOp
-
-        self.reduce_type = ReduceOp.SUM if reduce_type is None else reduce_type
-
-    def is_partial(self):
-        return True
-
-    def _torch(self):
-        from ..collective import ReduceOp
-
-        op = {ReduceOp.SUM: "sum", ReduceOp.AVG: "avg", ReduceOp.MAX: "max", ReduceOp.MIN: "min"}[self.reduce_type]
-        return _dt.Partial(op)
-
-    def __eq__(self, o):
-        return isinstance(o, Partial) and o.reduce_type == self.reduce_type
-
-    def __hash__(self):
-        return hash(("P", self.reduce_type))
-
-    def __repr__(self):
-        return f"Partial(reduce_type={self.reduce_type})"
-
-
-def _from_torch_placement(p):
-    if isinstance(p, _dt.Shard):
-        return Shard(p.dim)
-    if isinstance(p, _dt.Replicate):
-        return Replicate()
-    return Partial()
+from .placement import MeshGroups, Partial, Placement, Replicate, Shard  # noqa: E402,F401
+from .dist_tensor import DistTensor, distribute_tensor  # noqa: E402
 
 
 # ----------------------------------------------------------------------------- ProcessMesh
@@ -180,15 +99,14 @@ class ProcessMesh:
         return f"ProcessMesh(shape={self.shape}, process_ids={self.process_ids}, dim_names={self._dim_names})"
 
     def _device_mesh(self):
-        """torch DeviceMesh for this rank grid (collective: every rank must call it in the same order)."""
+        """The mesh's communicators (placement.MeshGroups; collective: every rank builds them in the same order)."""
         key = hash(self)
         dm = _MESH_CACHE.get(key)
         if dm is None:
             from .. import collective as C
 
             C.init_parallel_env()
-            dev = current_torch_device().type
-            dm = _dt.DeviceMesh(dev, torch.tensor(self._mesh), mesh_dim_names=tuple(self._dim_names))
+            dm = MeshGroups(self._mesh, self._dim_names, current_torch_device().type)
             _MESH_CACHE[key] = dm
         return dm
 
@@ -206,15 +124,15 @@ def get_mesh():
 
 
 # ----------------------------------------------------------------------------- DistTensor API
-def _torch_placements(mesh, placements):
-    out = [p._torch() if isinstance(p, Placement) else p for p in placements]
+def _placements(mesh, placements):
+    out = list(placements)
     while len(out) < mesh.ndim:
-        out.append(_dt.Replicate())
-    return out
+        out.append(Replicate())
+    return tuple(out)
 
 
 def is_dist_tensor(t):
-    return isinstance(getattr(t, "_t", None), _dt.DTensor)
+    return isinstance(getattr(t, "_t", None), DistTensor)
 
 
 def _attach(w, mesh):
@@ -225,6 +143,7 @@ def _attach(w, mesh):
 def shard_tensor(data, mesh, placements, dtype=None, place=None, stop_gradient=None):
     """Distribute a (replicated, identical on every rank) global tensor by ``placements``."""
     from ...framework.tensor import to_tensor
+    from .reshard import reshard as _own
 
     t = data if isinstance(data, Tensor) else to_tensor(data, dtype=dtype)
     src = t._t
@@ -233,12 +152,11 @@ def shard_tensor(data, mesh, placements, dtype=None, place=None, stop_gradient=N
 
         src = src.to(convert_dtype(dtype))
     dm = mesh._device_mesh()
-    src = src.to(dm.device_type if dm.device_type == "cpu" else current_torch_device())
-    if isinstance(src, _dt.DTensor):
-        out = src.redistribute(dm, _torch_placements(mesh, placements))
+    if isinstance(src, DistTensor):
+        out = _own(src, _placements(mesh, placements))
     else:
-        leaf = src.detach()
-        out = _dt.distribute_tensor(leaf, dm, _torch_placements(mesh, placements))
+        src = src.to("cpu" if dm.device_type == "cpu" else current_torch_device())
+        out = distribute_tensor(src.detach(), dm, _placements(mesh, placements))
     sg = t.stop_gradient if stop_gradient is None else stop_gradient
     if isinstance(t, Tensor) and hasattr(t, "trainable") and type(t).__name__ in ("Parameter", "EagerParamBase"):
         from ...framework.param import Parameter
@@ -252,7 +170,7 @@ def shard_tensor(data, mesh, placements, dtype=None, place=None, stop_gradient=N
 
 def dtensor_from_local(local_tensor, mesh, placements):
     lt = local_tensor._t if isinstance(local_tensor, Tensor) else local_tensor
-    out = _dt.DTensor.from_local(lt, mesh._device_mesh(), _torch_placements(mesh, placements), run_check=False)
+    out = DistTensor.from_local(lt, mesh._device_mesh(), _placements(mesh, placements))
     return _attach(_wrap(out), mesh)
 
 
@@ -266,32 +184,32 @@ def reshard(dist_tensor, mesh, placements):
     (reshard.reshard_cross_mesh: p2p for same-status meshes, else replicate -> send -> slice); ranks outside the
     destination mesh hold no local data."""
     t = dist_tensor._t
-    assert isinstance(t, _dt.DTensor), "reshard expects a DistTensor"
+    assert isinstance(t, DistTensor), "reshard expects a DistTensor"
     dm = mesh._device_mesh()
     if dm == t.device_mesh:
         from .reshard import reshard as _own
 
-        return _attach(_wrap(_own(t, _torch_placements(mesh, placements))), mesh)
+        return _attach(_wrap(_own(t, _placements(mesh, placements))), mesh)
     from .reshard import reshard_cross_mesh
 
-    return _attach(_wrap(reshard_cross_mesh(t, dm, _torch_placements(mesh, placements))), mesh)
+    return _attach(_wrap(reshard_cross_mesh(t, dm, _placements(mesh, placements))), mesh)
 
 
 def unshard_dtensor(dist_tensor):
     t = dist_tensor._t
-    if isinstance(t, _dt.DTensor):
+    if isinstance(t, DistTensor):
         return _wrap(t.full_tensor())
     return dist_tensor
 
 
 def local_tensor(dist_tensor):
     t = dist_tensor._t
-    return _wrap(t.to_local()) if isinstance(t, _dt.DTensor) else dist_tensor
+    return _wrap(t.to_local()) if isinstance(t, DistTensor) else dist_tensor
 
 
 def placements_of(dist_tensor):
     t = dist_tensor._t
-    return [_from_torch_placement(p) for p in t.placements] if isinstance(t, _dt.DTensor) else None
+    return list(t.placements) if isinstance(t, DistTensor) else None
 
 
 def shard_layer(layer, process_mesh, shard_fn=None, input_fn=None, output_fn=None):
@@ -306,8 +224,7 @@ def shard_layer(layer, process_mesh, shard_fn=None, input_fn=None, output_fn=Non
         for pname, p in list(sub._parameters.items()):
             if p is None or is_dist_tensor(p):
                 continue
-            d = _dt.distribute_tensor(p._t.detach(), process_mesh._device_mesh(),
-                                      _torch_placements(process_mesh, [Replicate()]))
+            d = distribute_tensor(p._t.detach(), process_mesh._device_mesh(), _placements(process_mesh, []))
             np_ = Parameter(d, name=p.name)
             np_.stop_gradient = p.stop_gradient
             np_.process_mesh = process_mesh
@@ -330,13 +247,13 @@ class _ShardingStageBase:
         """Optimizer-state placements: param's own placements with the sharding dim set to Shard(0)."""
         t = param._t
         mesh = getattr(param, "process_mesh", self._mesh)
-        if isinstance(t, _dt.DTensor):
+        if isinstance(t, DistTensor):
             pl = list(t.placements)
         else:
-            pl = [_dt.Replicate()] * mesh.ndim
+            pl = [Replicate()] * mesh.ndim
         ax = mesh.dim_names.index(self._dim) if isinstance(self._dim, str) else int(self._dim)
-        if isinstance(pl[ax], _dt.Replicate) and t.shape[0] % mesh.shape[ax] == 0:
-            pl[ax] = _dt.Shard(0)
+        if isinstance(pl[ax], Replicate) and t.shape[0] % mesh.shape[ax] == 0:
+            pl[ax] = Shard(0)
         return mesh, pl
 
 
@@ -365,10 +282,10 @@ class _ShardOptimizer:
             def sharded_acc(name, p, like=None, dtype=torch.float32, fill=0.0, _orig=orig_acc):
                 d = optimizer._accumulators[name]
                 t = d.get(p.name)
-                if t is None and isinstance(p._t, _dt.DTensor):
+                if t is None and isinstance(p._t, DistTensor):
                     mesh, pl = shard_fn._placements_for(p)
-                    full = torch.full(tuple(p._t.shape), fill, dtype=dtype, device=p._t.to_local().device)
-                    t = _dt.distribute_tensor(full, mesh._device_mesh(), pl)
+                    full = torch.full(tuple(p._t.shape), fill, dtype=dtype, device=p._t._local_tensor.device)
+                    t = distribute_tensor(full, mesh._device_mesh(), pl)
                     d[p.name] = t
                     return t
                 return _orig(name, p, like, dtype, fill)

@@ -14,20 +14,20 @@ DistTensor arguments at entry (``ops/torch_ops.py``, ``nn/functional``) and come
      sharded letter makes that input's gradient PARTIAL);
   5. wrap the local outputs as DistTensors with the rule's output placements.
 
-Ops without a hook keep torch's DTensor dispatch (sharding propagation for view / pointwise ops).
+Ops without a hook go through DistTensor's aten-level SPMD dispatch (dist_tensor.py).
 """
 from __future__ import annotations
 
 import torch
-from torch.distributed import tensor as _dt
-from torch.distributed.tensor.placement_types import Partial as _TPartial
-from torch.distributed.tensor.placement_types import Replicate as _TReplicate
-from torch.distributed.tensor.placement_types import Shard as _TShard
 
 from . import spmd_rules as R
+from .dist_tensor import DistTensor
+from .placement import Partial as _TPartial
+from .placement import Replicate as _TReplicate
+from .placement import Shard as _TShard
 from .reshard import reshard
 
-DTensor = _dt.DTensor
+DTensor = DistTensor
 TRACE = []   # (op, [input dims_mapping], [output dims_mapping]) of every dispatched op (tests inspect it)
 
 
@@ -81,7 +81,7 @@ def _as_dist(t, dm):
     """plain tensors join the computation replicated over the mesh"""
     if t is None or isinstance(t, DTensor):
         return t
-    return DTensor.from_local(t, dm, [_TReplicate()] * dm.ndim, run_check=False)
+    return DistTensor.from_local(t, dm, [_TReplicate()] * dm.ndim)
 
 
 def _local(t, dm, attr, grad_partial=()):
@@ -97,12 +97,7 @@ def _local(t, dm, attr, grad_partial=()):
 
 
 def _wrap(local, dm, attr, shape=None):
-    pl = _placements(attr, dm.ndim)
-    kw = {}
-    if shape is not None:
-        kw["shape"] = torch.Size(shape)
-        kw["stride"] = torch.empty(shape, device="meta").stride()
-    return DTensor.from_local(local, dm, pl, run_check=False, **kw)
+    return DistTensor.from_local(local, dm, _placements(attr, dm.ndim), shape=None if shape is None else tuple(shape))
 
 
 def _sharded_dims(dms):

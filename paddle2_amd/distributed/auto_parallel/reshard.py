@@ -3,10 +3,9 @@ paddle/phi/core/distributed/auto_parallel/reshard/ — s_to_r_reshard_function.c
 p_to_r :66 (all-reduce), p_to_s :70 (reduce-scatter), s_to_s :101 (all-to-all), r_to_s (local slice),
 r_to_p (keep on one rank), nd_mesh_reshard_function.cc (one mesh dim at a time)).
 
-A DistTensor's storage is a torch ``DTensor`` (local shard + mesh + placements); the data movement between two
-placements is done here, per mesh dimension, with c10d collectives on that dimension's process group
-(``DeviceMesh.get_group(dim)`` — RCCL, or the framework's ProcessGroupRCCL when ``PADDLE2_AMD_PG=rccl``), not
-with ``DTensor.redistribute``.  Order per mesh dim follows the reference's nd-mesh function: partial dims are
+A DistTensor (dist_tensor.py: local shard + MeshGroups + placements) moves between two placements here, per mesh
+dimension, with collectives on that dimension's process group (``MeshGroups.get_group(dim)`` — the framework's
+ProcessGroupRCCL over xGMI on the GPU, gloo on the CPU).  Order per mesh dim follows the reference's nd-mesh function: partial dims are
 resolved first (p->r / p->s), then shard moves (s->s / s->r), then new shards (r->s) — so a reduction is never
 applied to data that was already replicated by a gather.
 
@@ -20,17 +19,17 @@ from __future__ import annotations
 
 import torch
 import torch.distributed as dist
-from torch.distributed import tensor as _dt
-from torch.distributed.tensor.placement_types import Partial as _TPartial
-from torch.distributed.tensor.placement_types import Replicate as _TReplicate
-from torch.distributed.tensor.placement_types import Shard as _TShard
+
+from .placement import Partial as _TPartial
+from .placement import Replicate as _TReplicate
+from .placement import Shard as _TShard
 
 _RED = {"sum": dist.ReduceOp.SUM, "avg": dist.ReduceOp.AVG, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
 COMM_LOG = []   # (kind, mesh_dim) of every collective issued (tests assert the expected plan)
 
 
 def _group(mesh, dim):
-    return mesh.get_group(dim) if mesh.ndim > 1 else mesh.get_group()
+    return mesh.get_group(dim)
 
 
 def _coord(mesh, dim):
@@ -102,7 +101,7 @@ def _to_partial(x, mesh, dim):
 
 
 def _red_name(p):
-    return getattr(p, "reduce_op", "sum")
+    return p.reduce_op
 
 
 def reshard_local(local, mesh, src, dst, backward=False):
@@ -150,24 +149,27 @@ def reshard_local(local, mesh, src, dst, backward=False):
 class _Reshard(torch.autograd.Function):
     @staticmethod
     def forward(ctx, dt, mesh, src, dst):
+        from .dist_tensor import DistTensor
+
         ctx.mesh, ctx.src, ctx.dst = mesh, src, dst
         local = reshard_local(dt._local_tensor, mesh, src, dst)
-        return _dt.DTensor.from_local(local, mesh, dst, run_check=False, shape=dt.shape, stride=dt.stride())
+        return DistTensor(local, mesh, dst, dt.shape)
 
     @staticmethod
     def backward(ctx, g):
-        if not isinstance(g, _dt.DTensor):
+        from .dist_tensor import DistTensor
+
+        if not isinstance(g, DistTensor):
             return None, None, None, None
         gsrc = tuple(g.placements)
         tgt = tuple(_TReplicate() if isinstance(p, _TPartial) and isinstance(q, _TReplicate) else p
                     for p, q in zip(ctx.src, gsrc))
         local = reshard_local(g._local_tensor, ctx.mesh, gsrc, tgt, backward=True)
-        out = _dt.DTensor.from_local(local, ctx.mesh, tgt, run_check=False, shape=g.shape, stride=g.stride())
-        return out, None, None, None
+        return DistTensor(local, ctx.mesh, tgt, g.shape), None, None, None
 
 
 def reshard(dt, placements):
-    """Differentiable reshard of a torch DTensor to ``placements`` (torch placement objects)."""
+    """Differentiable reshard of a DistTensor to ``placements`` (one per mesh dim)."""
     dst = tuple(placements)
     src = tuple(dt.placements)
     if src == dst:
@@ -188,7 +190,7 @@ def _local_shape(shape, mesh_shape, placements):
 
 
 def reshard_cross_mesh(dt, dst_mesh, dst_placements):
-    """DTensor on one process mesh -> DTensor on another (reference reshard/same_status_reshard_function.cc and
+    """DistTensor on one process mesh -> DistTensor on another (reference reshard/same_status_reshard_function.cc and
     the cross-mesh path of nd_mesh_reshard_function.cc).
 
     * same status (meshes of one shape, identical placements): every source coordinate sends its local shard to
@@ -242,7 +244,8 @@ def reshard_cross_mesh(dt, dst_mesh, dst_placements):
                 COMM_LOG.append(("recv", -1))
         if me in dst_ranks:
             local = reshard_local(full, dst_mesh, tuple(_TReplicate() for _ in range(dst_mesh.ndim)), dst_placements)
-    if me not in dst_ranks:  # a non-member holds the DistTensor's metadata with no local data (as in torch)
+    if me not in dst_ranks:  # a non-member holds the DistTensor's metadata with no local data
         local = torch.empty(0, dtype=dtype, device=dev)
-    return _dt.DTensor.from_local(local, dst_mesh, dst_placements, run_check=False, shape=torch.Size(shape),
-                                  stride=torch.empty(shape, device="meta").stride())
+    from .dist_tensor import DistTensor
+
+    return DistTensor(local, dst_mesh, dst_placements, shape)

@@ -40,10 +40,10 @@ class DistAttr:
         self.reduce = reduce
 
     def placements(self, ndim_mesh):
-        """torch placements per mesh dim (for the reshard engine)."""
-        from torch.distributed.tensor.placement_types import Partial as TP
-        from torch.distributed.tensor.placement_types import Replicate as TR
-        from torch.distributed.tensor.placement_types import Shard as TS
+        """placements per mesh dim (for the reshard engine)."""
+        from ..placement import Partial as TP
+        from ..placement import Replicate as TR
+        from ..placement import Shard as TS
 
         out = []
         for d in range(ndim_mesh):
@@ -72,7 +72,7 @@ def attr_from_placements(placements, ndim):
             dm[p.get_dim() if hasattr(p, "get_dim") else p.dim] = d
         elif isinstance(p, Partial):
             partial.add(d)
-            red = p._torch().reduce_op
+            red = p.reduce_op
     return DistAttr(dm, partial, red)
 
 

@@ -39,14 +39,14 @@ class _LocalReshard(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        from torch.distributed.tensor.placement_types import Partial as TP
-        from torch.distributed.tensor.placement_types import Replicate as TR
+        from ..placement import Partial as TP
+        from ..placement import Replicate as TR
 
         tgt = tuple(TR() if isinstance(p, TP) else p for p in ctx.src)
         gsrc = tuple(TR() if isinstance(p, TP) else p for p in ctx.dst)
         out = reshard_local(g.contiguous(), ctx.mesh, gsrc, tgt, backward=True)
         for d, p in enumerate(ctx.src):
-            if isinstance(p, TP) and getattr(p, "reduce_op", "sum") == "avg":
+            if isinstance(p, TP) and p.reduce_op == "avg":
                 out = out / ctx.mesh.size(d)
         return out, None, None, None
 

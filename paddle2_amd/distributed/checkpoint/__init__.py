@@ -57,13 +57,17 @@ def _dtype_name(t):
 def _local_chunk(v):
     """-> (local torch tensor, global_offset tuple, global_shape tuple, replicated?)."""
     t = v._t if isinstance(v, Tensor) else v
-    from torch.distributed.tensor import DTensor
-    from torch.distributed.tensor._utils import compute_local_shape_and_global_offset
+    from ..auto_parallel.dist_tensor import DistTensor
+    from ..auto_parallel.placement import local_shape_and_offset
 
-    if isinstance(t, DTensor):
-        shape, off = compute_local_shape_and_global_offset(t.shape, t.device_mesh, t.placements)
+    if isinstance(t, DistTensor):
+        from ..auto_parallel.reshard import reshard
+
+        if any(p.is_partial() for p in t.placements):   # a partial value is saved reduced
+            t = reshard(t, tuple(p if not p.is_partial() else _rep() for p in t.placements))
+        shape, off = local_shape_and_offset(t.shape, t.device_mesh, t.placements)
         replicated = all(not p.is_shard() for p in t.placements)
-        return t.to_local(), tuple(int(o) for o in off), tuple(int(s) for s in t.shape), replicated
+        return t._local_tensor, tuple(int(o) for o in off), tuple(int(s) for s in t.shape), replicated
     # TP-sharded parameter (fleet mpu layers): offset from the mp rank along split_axis
     if isinstance(v, Tensor) and getattr(v, "is_distributed", False) and hasattr(v, "split_axis"):
         from ..fleet import get_hybrid_communicate_group
@@ -77,6 +81,12 @@ def _local_chunk(v):
             off[ax] = r * t.shape[ax]
             return t, tuple(off), tuple(gshape), False
     return t, tuple([0] * t.dim()), tuple(t.shape), True
+
+
+def _rep():
+    from ..auto_parallel.placement import Replicate
+
+    return Replicate()
 
 
 def flatten_state_dict(state_dict, prefix=""):

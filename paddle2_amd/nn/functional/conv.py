@@ -72,66 +72,16 @@ def _resolve_padding(padding, n, spatial, k, s, d):
     return int(padding), None
 
 
-import os as _os
-
-_CONV1X1 = _os.environ.get("PADDLE2_AMD_CONV1X1", "native")   # native | miopen
-
-
-class _Conv1x1Fn(torch.autograd.Function):
-    """Channels-last 1x1 convolution as the GEMM it is, on the hand-written MFMA kernels (reference
-    paddle/phi/kernels/gpudnn/conv_kernel.cu:305 runs it through cuDNN / MIOpen):
-
-      forward  y[P, Co]  = x[P, Ci] . W[Co, Ci]^T    both operands K-major: the TN kernel, no transpose
-      dgrad    dx[P, Ci] = dy[P, Co] . W[Co, Ci]     the forward GEMM node (W read as [K, N])
-      wgrad    dW[Co, Ci] = dy^T . x                 the wgrad kernel (both operands token-major)
-
-    P = N*H*W pixels (stride-2 1x1 convs subsample the input first); bias in the forward epilogue."""
-
-    calls = 0
-
-    @staticmethod
-    def forward(ctx, x, w, b):
-        from ...ops import gemm as G
-
-        _Conv1x1Fn.calls += 1
-        Nb, H, W_, Ci = x.shape
-        Co = w.shape[0]
-        x2 = x.reshape(-1, Ci)
-        w2 = w.reshape(Co, Ci)
-        y = torch.empty(x2.shape[0], Co, dtype=x.dtype, device=x.device)
-        G._launch(G.LAYOUT_AK | G.LAYOUT_BK, G.EPI_BF16, x2, Ci, w2, Ci, y, Co, None, 0,
-                  None if b is None else b.contiguous(), x2.shape[0], Co, Ci, name="fwd")
-        ctx.save_for_backward(x2, w2)
-        ctx.meta = (x.shape, w.shape, b is not None)
-        return y.view(Nb, H, W_, Co)
-
-    @staticmethod
-    def backward(ctx, dy):
-        from ...ops import gemm as G
-        from ...ops.torch_ops import bias_grad
-
-        x2, w2 = ctx.saved_tensors
-        xshape, wshape, has_b = ctx.meta
-        dy2 = dy.reshape(-1, w2.shape[0])
-        if not dy2.is_contiguous():
-            dy2 = dy2.contiguous()
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = G.mm_fwd(dy2, w2).view(xshape)
-        if ctx.needs_input_grad[1]:
-            dw = G.mm_wgrad_bf16(dy2, x2).view(wshape)
-        if has_b and ctx.needs_input_grad[2]:
-            db = bias_grad(dy2)
-        return dx, dw, db
+from ...ops import conv_gemm as _CG  # noqa: E402
 
 
 def _conv1x1_native(t_nhwc, weight, bias, stride, groups, dilation):
-    """The native path applies: GPU bf16, NHWC, a 1x1 kernel without padding or groups, channel counts the
+    """The native 1x1 path applies: GPU bf16, NHWC, a 1x1 kernel without padding or groups, channel counts the
     GEMM's 16-B chunks take (multiples of 8)."""
     from ...ops import _native as N
 
     w = weight._t
-    return (_CONV1X1 == "native" and t_nhwc.is_cuda and t_nhwc.dtype == torch.bfloat16
+    return (_CG.MODE == "native" and t_nhwc.is_cuda and t_nhwc.dtype == torch.bfloat16
             and w.dtype == t_nhwc.dtype and groups == 1 and tuple(w.shape[2:]) == (1, 1)
             and all(dd == 1 for dd in dilation) and w.shape[1] % 8 == 0 and w.shape[0] % 8 == 0
             and (bias is None or bias._t.dtype == t_nhwc.dtype) and N.use_native(t_nhwc))
@@ -147,7 +97,17 @@ def _conv(x, weight, bias, stride, padding, dilation, groups, data_format, n):
                 t = t[:, ::s2[0], ::s2[1], :]
             if not t.is_contiguous():
                 t = t.contiguous()
-            return _wrap(_Conv1x1Fn.apply(t, weight._t, None if bias is None else bias._t))
+            return _wrap(_CG.Conv1x1Fn.apply(t, weight._t, None if bias is None else bias._t))
+    if cl and n == 2:
+        s2, d2 = _ntuple(stride, 2), _ntuple(dilation, 2)
+        pad = padding if isinstance(padding, str) else _ntuple(padding, 2)
+        if isinstance(pad, str):
+            pad = [1, 1] if pad.upper() == "SAME" and s2 == [1, 1] else None
+        if pad is not None and _CG.eligible_3x3(t, weight._t, s2, pad, d2, groups):
+            y = _CG.Conv3x3Fn.apply(t.contiguous(), weight._t)
+            if bias is not None:
+                y = y + bias._t
+            return _wrap(y)
     if cl:
         t = t.movedim(-1, 1)
     k = list(weight._t.shape[2:])

@@ -17,7 +17,7 @@ from . import _native as N
 _DT = N.DT_CODE
 
 try:   # DistTensor arguments take the SPMD dispatch at op entry (distributed/auto_parallel/dist_ops.py)
-    from torch.distributed.tensor import DTensor as _DTensor
+    from ..distributed.auto_parallel.dist_tensor import DistTensor as _DTensor
 except Exception:  # noqa: BLE001
     class _DTensor:  # noqa: D101
         pass

@@ -1,13 +1,13 @@
 """Channels-last 1x1 convolutions on the native MFMA GEMM (nn/functional/conv.py `_Conv1x1Fn`) against an fp32
 PyTorch conv2d of the same op: forward, dx, dW and db, stride 1 and 2, channel counts off the 128/256 tiles,
-the ResNet-50 bottleneck widths; plus the routing (3x3 / padded / NCHW convs stay on MIOpen).
+the ResNet-50 bottleneck widths; plus the routing (padded / NCHW 1x1 convs do not take it).
 """
 import pytest
 import torch
 import torch.nn.functional as F
 
 import paddle2_amd as paddle
-from paddle2_amd.nn.functional import conv as C
+from paddle2_amd.ops import conv_gemm as CG
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
@@ -40,9 +40,9 @@ def test_conv1x1_native_matches_fp32(N, H, W, Ci, Co, stride, bias):
     px = paddle.to_tensor(x, stop_gradient=False)
     pw = paddle.to_tensor(w, stop_gradient=False)
     pb = paddle.to_tensor(b, stop_gradient=False) if bias else None
-    before = C._Conv1x1Fn.calls
+    before = CG.calls["1x1"]
     y = paddle.nn.functional.conv2d(px, pw, pb, stride=stride, data_format="NHWC")
-    assert C._Conv1x1Fn.calls == before + 1, "the 1x1 conv did not take the native GEMM path"
+    assert CG.calls["1x1"] == before + 1, "the 1x1 conv did not take the native GEMM path"
     y.backward(paddle.to_tensor(dy))
     assert tuple(y.shape) == tuple(yr.shape)
     assert _rel(y._t, yr) < 8e-3
@@ -56,9 +56,9 @@ def test_other_convs_stay_on_miopen():
     x = paddle.to_tensor(torch.randn(2, 8, 8, 64, device=dev).to(torch.bfloat16))
     w3 = paddle.to_tensor(torch.randn(64, 64, 3, 3, device=dev).to(torch.bfloat16))
     w1 = paddle.to_tensor(torch.randn(64, 64, 1, 1, device=dev).to(torch.bfloat16))
-    before = C._Conv1x1Fn.calls
+    before = CG.calls["1x1"]
     paddle.nn.functional.conv2d(x, w3, padding=1, data_format="NHWC")
     paddle.nn.functional.conv2d(x, w1, padding=1, data_format="NHWC")
     xn = paddle.to_tensor(x._t.permute(0, 3, 1, 2).contiguous())
     paddle.nn.functional.conv2d(xn, w1)
-    assert C._Conv1x1Fn.calls == before
+    assert CG.calls["1x1"] == before
