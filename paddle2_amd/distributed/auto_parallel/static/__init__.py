@@ -5,3 +5,4 @@ from .completion import Completer, DistAttr, DistContext, attr_from_placements  
 from .cost_model import ClusterSpec, CostModel, Planner, reshard_steps  # noqa: F401
 from .partitioner import DistributedProgram, parallelize_program  # noqa: F401
 from .engine import Engine  # noqa: F401
+from .resharder import DistMainProgram, Resharder, build_dist_main_program, comm_kinds  # noqa: F401,E402

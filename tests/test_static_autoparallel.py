@@ -146,3 +146,22 @@ def test_own_dist_tensor_aten_dispatch(nprocs):
         assert o["row_out"][-1].startswith("Partial")
         assert o["col_out"][-1] == "Shard(dim=1)"
         assert {"all_reduce", "all_gather"} <= set(o["comm"])
+
+
+@pytest.mark.parametrize("mode", ["tp", "dp"])
+def test_resharder_dist_main_program_trains_like_serial(mode):
+    """The explicit dist_main_program (communication ops inserted by the Resharder) trains 3 SGD steps through the
+    static Executor exactly like the serial run; the TP plan's program carries the row-parallel all-reduce, the
+    partial-bias op and the column-parallel input's gradient all-reduce, the DP plan's the feed split and the
+    weight-gradient all-reduces."""
+    res = run_workers("static_dist_program_worker.py", 2, args=(mode,))
+    for o in res:
+        np.testing.assert_allclose(o["losses"], o["ref"], rtol=1e-5, atol=1e-6)
+        assert o["param_err"] < 1e-5, o["param_err"]
+        ops = set(o["comm_ops"])
+        if mode == "tp":
+            assert o["w1_local"] == [8, 8]
+            assert {"c_allreduce_sum", "c_partial", "c_identity"} <= ops, ops
+        else:
+            assert "c_identity" in ops and any(k.startswith("c_allreduce") for k in ops), ops
+        assert "c_allreduce_sum" in o["program"] or "c_allreduce_avg" in o["program"]
