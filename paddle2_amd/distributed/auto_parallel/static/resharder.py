@@ -93,6 +93,7 @@ def _grad_allreduce_fn(mesh, dims):
 
     fn.__name__ = fn.__qualname__ = "c_identity"
     fn.comm = True
+    fn.dims = tuple(dims)
     return fn
 
 

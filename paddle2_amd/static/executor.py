@@ -122,6 +122,9 @@ class Executor:
             with torch.no_grad():
                 opt.step()
             opt.clear_grad(set_to_zero=False)
+        elif op.kind == "call":
+            # a host instruction a pass inserted (fused gradient all-reduce, gradient merge, sharded step, ...)
+            op.attrs["fn"](env)
 
     def _replay(self, program, env, grad=None, keep=None):
         """Run ``program`` over ``env`` (vid -> tensor) through its interpreter plan (csrc/runtime/interpreter.cpp).

@@ -165,3 +165,23 @@ def test_resharder_dist_main_program_trains_like_serial(mode):
         else:
             assert "c_identity" in ops and any(k.startswith("c_allreduce") for k in ops), ops
         assert "c_allreduce_sum" in o["program"] or "c_allreduce_avg" in o["program"]
+
+
+@pytest.mark.parametrize("passes", ["fuse", "merge", "recompute", "sharding", "fuse,sharding", "amp"])
+def test_static_passes_train_like_serial(passes):
+    """Passes over the dist_main_program of a data-parallel plan (2 ranks, Adam): fused + bucketed gradient
+    all-reduce, gradient merge (k = 2), recompute of an op range, sharding stage 1 (each rank holds the optimizer
+    state of its own parameters only), AMP (bf16 white-list ops) — the trained parameters match the serial run."""
+    res = run_workers("static_passes_worker.py", 2, args=(passes,))
+    for o in res:
+        tol = 5e-2 if passes == "amp" else 1e-5
+        np.testing.assert_allclose(o["losses"], o["ref"], rtol=tol, atol=tol)
+        assert o["param_err"] < (5e-2 if passes == "amp" else 1e-5), o["param_err"]
+        if "fuse" in passes:
+            assert o["buckets"] >= 1 and o["fused_calls"] == 4
+        if passes == "recompute":
+            assert len(o["recompute_ops"]) == 1
+        if "sharding" in passes:
+            assert 0 < o["my_acc"] < o["n_params"]
+        if passes == "amp":
+            assert o["amp_ops"] >= 2

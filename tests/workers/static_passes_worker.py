@@ -1,0 +1,81 @@
+"""Rank worker: static auto-parallel passes on a dist_main_program (DP plan over 2 ranks) — fused gradient
+all-reduce, gradient merge, recompute, sharding stage 1 and AMP — each trained against the serial run."""
+import os
+import sys
+
+sys.path.insert(0, os.environ.get("PYTHONPATH", "."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+
+import numpy as np  # noqa: E402
+
+import paddle2_amd as paddle  # noqa: E402
+import paddle2_amd.distributed as dist  # noqa: E402
+from paddle2_amd.distributed.auto_parallel.static import (amp_pass, build_dist_main_program,  # noqa: E402
+                                                           fuse_allreduce_pass, gradient_merge_pass,
+                                                           parallelize_program, recompute_pass, sharding_pass)
+from _dist import write_result  # noqa: E402
+
+dist.init_parallel_env()
+mesh = dist.ProcessMesh([0, 1], dim_names=["dp"])
+passes = sys.argv[1].split(",")
+out = {}
+
+
+class MLP(paddle.nn.Layer):
+    def __init__(self):
+        super().__init__()
+        self.fc1 = paddle.nn.Linear(8, 16)
+        self.fc2 = paddle.nn.Linear(16, 4)
+
+    def forward(self, x):
+        return self.fc2(paddle.nn.functional.gelu(self.fc1(x))).pow(2).mean()
+
+
+paddle.seed(0)
+net, ref = MLP(), MLP()
+ref.set_state_dict(net.state_dict())
+main = paddle.static.Program()
+paddle.enable_static()
+opt = paddle.optimizer.Adam(0.05, parameters=net.parameters())
+with paddle.static.program_guard(main, paddle.static.Program()):
+    xs = paddle.static.data("x", [8, 8], "float32")
+    loss = net(xs)
+    opt.minimize(loss)
+paddle.disable_static()
+dmp = build_dist_main_program(parallelize_program(main, mesh, {"x": [dist.Shard(0)]}), [loss])
+k = 1
+if "fuse" in passes:
+    fused = fuse_allreduce_pass(dmp, bucket_mb=1)
+    out["buckets"] = len(fused.buckets())
+if "merge" in passes:
+    k = 2
+    gradient_merge_pass(dmp, k)
+if "recompute" in passes:
+    first = [i for i, o in enumerate(dmp.program.ops) if o.kind == "torch"]
+    recompute_pass(dmp, [(first[1], first[4])])
+    out["recompute_ops"] = [o.name for o in dmp.program.ops if getattr(o.fn, "recompute", False)]
+if "sharding" in passes:
+    owners = sharding_pass(dmp, 0)
+if "amp" in passes:
+    out["amp_ops"] = amp_pass(dmp)
+exe = paddle.static.Executor()
+ropt = paddle.optimizer.Adam(0.05, parameters=ref.parameters())
+losses, ref_losses = [], []
+for i in range(4):
+    xi = np.random.RandomState(30 + i).randn(8, 8).astype("float32")
+    (lv,) = exe.run(dmp.program, feed=dmp.local_feed({"x": xi}), fetch_list=[dmp.fetch(loss)])
+    losses.append(float(lv))
+    rl = ref(paddle.to_tensor(xi))
+    (rl / k).backward()
+    if (i + 1) % k == 0:
+        ropt.step()
+        ropt.clear_grad()
+    ref_losses.append(float(rl.numpy()))
+out["losses"], out["ref"] = losses, ref_losses
+out["param_err"] = max(float(np.abs(a.numpy() - b.numpy()).max()) for a, b in zip(net.parameters(), ref.parameters()))
+if "sharding" in passes:
+    out["my_acc"] = len(opt._accumulators.get("moment1", {}))
+    out["n_params"] = len(opt._parameter_list)
+if "fuse" in passes:
+    out["fused_calls"] = fused.calls
+write_result(out)
