@@ -61,7 +61,7 @@ def test_random_scaled(fa, fb, od, M, N, K):
     sb = torch.full((1,), 3.0, device=dev)
     c = F8.mm_native(a8, b8, sa, sb, od)
     ref = (a8.float() @ b8.float().t()) * 0.75
-    assert _rel(c, ref) < (1e-5 if od == torch.float32 else 8e-3)
+    assert _rel(c, ref) < (1e-4 if od == torch.float32 else 8e-3)
 
 
 def test_bias_epilogue():
