@@ -70,6 +70,8 @@ int pd_cache_write(const void*, const void*, long, long, void*, void*, long, lon
                    const int*, const int*, int, int, int, void*);
 long pd_bn_workspace(int, long, int);
 int pd_wo_splits(int, int, int, int);
+int pd_dec_splits(int, int, int);
+int pd_dec_gemm(const void*, const void*, const void*, void*, float*, int, int, int, int, void*);
 long pd_wo_workspace(int, int, int);
 int pd_wo_gemm(int, const void*, const void*, const float*, const float*, int, const void*, void*, float*, int, int, int,
                int, void*);
@@ -390,6 +392,13 @@ PYBIND11_MODULE(_C, m) {
                     P<const float*>(invstd), P<const float*>(g), P<void*>(dx), P<void*>(dz), P<float*>(dg),
                     P<float*>(db), M, C, P<float*>(ws), relu, P<void*>(st)),
           "bn_bwd");
+  });
+  m.def("dec_splits", &pd_dec_splits);
+  m.def("dec_gemm", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t out, uintptr_t ws, int M, int N, int K,
+                       int S, uintptr_t st) {
+    check(pd_dec_gemm(P<const void*>(x), P<const void*>(w), P<const void*>(bias), P<void*>(out), P<float*>(ws), M, N,
+                      K, S, P<void*>(st)),
+          "dec_gemm");
   });
   m.def("wo_splits", &pd_wo_splits);
   m.def("wo_workspace", &pd_wo_workspace);

@@ -189,6 +189,104 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(const unsigned short* __re
   }
 }
 
+// bf16 weights (the serving decode GEMM on the cached [N, K] projection weights): the same schedule with each lane
+// streaming 32 contiguous K-bytes of its channel per 64-wide K step (two 16-B loads = the two MFMA fragments), no
+// conversion.  Y[M, N] = X[M, K] . W^T, M <= 64, fp32 split-K partials into ws (summed by wo_reduce_kernel).
+template <int MT, int RT>
+__global__ __launch_bounds__(256) void dec_gemm_kernel(const unsigned short* __restrict__ X,
+                                                       const unsigned short* __restrict__ W, float* __restrict__ ws,
+                                                       int M, int N, int K, int kmax) {
+  extern __shared__ unsigned short xs[];  // [M][kmax + kWoPad]
+  const int pitch = kmax + kWoPad;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int U = K / 64, S = gridDim.y;
+  const int k0 = (int)((long)U * blockIdx.y / S) * 64;
+  const int Kblk = (int)((long)U * (blockIdx.y + 1) / S) * 64 - k0;
+  const int vpr = Kblk / 8;
+  for (int i = tid; i < M * vpr; i += 256) {
+    const int r = i / vpr, c = (i % vpr) * 8;
+    *reinterpret_cast<uint4*>(xs + r * pitch + c) = *reinterpret_cast<const uint4*>(X + (long)r * K + k0 + c);
+  }
+  __syncthreads();
+
+  const int g = lane >> 4;
+  const int nbase = blockIdx.x * kWoRows * RT + wave * 16;
+  const unsigned short* wrow[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) wrow[r] = W + (long)(nbase + r * kWoRows + (lane & 15)) * K + k0 + 16 * g;
+  wo_f32x4 acc[RT][MT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[r][t] = wo_f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nsteps = Kblk / 64;
+  constexpr int D = RT == 1 ? 4 : 2;
+  uint4 wb[RT][D][2];
+  auto ld = [&](int r, int s, uint4 (&o)[2]) {
+    if (s < nsteps) {
+      const uint4* p = reinterpret_cast<const uint4*>(wrow[r] + s * 64);
+      o[0] = p[0];
+      o[1] = p[1];
+    } else {
+      o[0] = o[1] = make_uint4(0, 0, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int d = 0; d < D; ++d) ld(r, d, wb[r][d]);
+  for (int c = 0; c < nsteps; c += D) {
+    uint4 nb[RT][D][2];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int d = 0; d < D; ++d) ld(r, c + D + d, nb[r][d]);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int s = c + d;
+      if (s >= nsteps) break;
+      const int kk = s * 64 + 16 * g;
+      wo_bf16x8 b0[MT], b1[MT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int m = t * 16 + (lane & 15);
+        const unsigned short* xr = xs + m * pitch + kk;
+        const wo_bf16x8 z = {};
+        b0[t] = m < M ? *reinterpret_cast<const wo_bf16x8*>(xr) : z;
+        b1[t] = m < M ? *reinterpret_cast<const wo_bf16x8*>(xr + 8) : z;
+      }
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const wo_bf16x8 a0 = __builtin_bit_cast(wo_bf16x8, wb[r][d][0]);
+        const wo_bf16x8 a1 = __builtin_bit_cast(wo_bf16x8, wb[r][d][1]);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0[t], acc[r][t], 0, 0, 0);
+          acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[t], acc[r][t], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        wb[r][d][0] = nb[r][d][0];
+        wb[r][d][1] = nb[r][d][1];
+      }
+  }
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    const int nb = nbase + r * kWoRows + (lane >> 4) * 4;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int m = t * 16 + (lane & 15);
+      if (m < M)
+        *reinterpret_cast<float4*>(ws + ((long)blockIdx.y * M + m) * N + nb) =
+            make_float4(acc[r][t][0], acc[r][t][1], acc[r][t][2], acc[r][t][3]);
+    }
+  }
+}
+
 // out[m, n] = (sum_s ws[s, m, n]) * cscale[n] + bias[n]   (bf16 out / bias)
 __global__ __launch_bounds__(256) void wo_reduce_kernel(const float* __restrict__ ws, int S, int M, int N,
                                                         const float* __restrict__ cscale,
@@ -281,5 +379,33 @@ extern "C" int pd_wo_gemm(int int4, const void* X, const void* W, const float* c
   const long total = (long)M * N;
   wo_reduce_kernel<<<(int)((total / 4 + 255) / 256), 256, 0, st>>>(ws, S, M, N, group > 0 ? nullptr : cscale,
                                                                  (const unsigned short*)bias, (unsigned short*)out);
+  return (int)hipGetLastError();
+}
+
+// Decode GEMM on bf16 weights: out[M, N] = X[M, K] . W[N, K]^T (+ bias), M <= 64, split-K S (pd_dec_splits).
+extern "C" int pd_dec_splits(int M, int N, int K) { return pd_wo_splits(M, N, K, 0); }
+
+extern "C" int pd_dec_gemm(const void* X, const void* W, const void* bias, void* out, float* ws, int M, int N, int K,
+                           int S, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (M < 1 || M > 64 || N % kWoRows || K % 64 || S < 1 || S > K / 64) return -1;
+  const int kmax = ((K / 64 + S - 1) / S) * 64;
+  const int MT = wo_mt(M), RT = wo_rt(M, N);
+  const size_t lds = (size_t)M * (kmax + kWoPad) * 2;
+  if (lds > 160 * 1024) return -3;
+  dim3 grid(N / (kWoRows * RT), S);
+  auto launch = [&](auto kern) {
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    kern<<<grid, 256, lds, st>>>((const unsigned short*)X, (const unsigned short*)W, ws, M, N, K, kmax);
+  };
+#define PD_DEC_R(MT_)                                                                         \
+  if (RT == 1) launch(dec_gemm_kernel<MT_, 1>);                                              \
+  else if (RT == 2) launch(dec_gemm_kernel<MT_, 2>);                                         \
+  else launch(dec_gemm_kernel<MT_, 4>);
+  if (MT == 1) { PD_DEC_R(1) } else if (MT == 2) { PD_DEC_R(2) } else { PD_DEC_R(4) }
+#undef PD_DEC_R
+  const long total = (long)M * N;
+  wo_reduce_kernel<<<(int)((total / 4 + 255) / 256), 256, 0, st>>>(ws, S, M, N, nullptr, (const unsigned short*)bias,
+                                                                 (unsigned short*)out);
   return (int)hipGetLastError();
 }

@@ -58,3 +58,37 @@ def weight_only_matmul(x, w, scale, weight_dtype="int8", group_size=-1, bias=Non
     if bias is not None:
         y = y + bias.to(y.dtype)
     return y.to(x.dtype)
+
+
+# ---------------------------------------------------------------------------------------------- bf16 decode GEMM
+# "native": the split-K MFMA stream kernel (csrc/kernels/weight_only.hip dec_gemm_kernel) for decode-sized token
+# counts on the cached [N, K] weights; "blas": hipBLASLt through torch.matmul
+import os as _os  # noqa: E402
+
+DECODE_GEMM = _os.environ.get("PADDLE2_AMD_DECODE_GEMM", "native")
+
+
+def decode_ok(x, wt):
+    M, K = x.shape
+    return (x.device.type == "cuda" and x.dtype == torch.bfloat16 and wt.dtype == torch.bfloat16 and 1 <= M <= 64
+            and K % 64 == 0 and wt.shape[1] == K and wt.shape[0] % 64 == 0 and wt.is_contiguous()
+            and N.use_native(x))
+
+
+def decode_matmul(x, wt, bias=None):
+    """y[M, N] = x[M, K] @ wt[N, K]^T (+ bias) for M <= 64 on the native stream kernel (weights read once, split-K
+    over the 256 CUs, fp32 partials summed in a second pass); torch.matmul otherwise."""
+    x = x.contiguous()
+    if DECODE_GEMM != "native" or not decode_ok(x, wt):
+        y = torch.matmul(x, wt.t())
+        return y if bias is None else y + bias
+    M, K = x.shape
+    Nn = wt.shape[0]
+    C = N.native()
+    S = C.dec_splits(M, Nn, K)
+    ws = torch.empty(S * M * Nn, dtype=torch.float32, device=x.device)
+    out = torch.empty(M, Nn, dtype=x.dtype, device=x.device)
+    if bias is not None:
+        bias = bias.to(torch.bfloat16).contiguous()
+    C.dec_gemm(x.data_ptr(), wt.data_ptr(), N.ptr(bias), out.data_ptr(), ws.data_ptr(), M, Nn, K, S, N.stream())
+    return out

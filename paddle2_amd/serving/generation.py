@@ -93,6 +93,10 @@ class LlamaGenerator:
                 ent[2] = T.transpose2d(w)
                 self._graph = None
             ent[0], ent[1] = w.data_ptr(), w._version
+        if x.dim() == 2 and x.shape[0] <= 64:
+            from ..ops import weight_only as WO
+
+            return WO.decode_matmul(x, ent[2])   # decode: the native weight-streaming kernel
         return torch.matmul(x, ent[2].t())
 
     def _nk_fits(self):
