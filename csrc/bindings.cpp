@@ -29,6 +29,7 @@ int pd_gemm_grouped(int, int, const void*, long, const void*, long, long, void*,
 int pd_transpose16(const void*, void*, long, long, long, long, void*);
 int pd_gemm_conv(const void*, long, const void*, const void*, const void*, long, void*, long, int, int, int, int,
                  int, int, int, int, int, int, int, int, void*);
+void pd_gemm_set_rope(const float*, const float*, int, int);
 int pd_gemm_f8(int, int, int, const void*, long, const void*, long, void*, long, const void*, const float*,
                const float*, int, int, int, float, int, int, void*);
 long pd_ar_sig_bytes();
@@ -140,6 +141,9 @@ PYBIND11_MODULE(_C, m) {
     return pd_gemm_conv(P<const void*>(a), lda, P<const void*>(a_lo), P<const void*>(a_hi), P<const void*>(b), ldb,
                         P<void*>(c), ldc, M, N, K, taps, kw, pitch, pad_h, pad_w, sign, kpb_log2, group_m, cus,
                         P<void*>(st));
+  });
+  m.def("gemm_set_rope", [](uintptr_t cos, uintptr_t sin, int cols, int seq) {
+    pd_gemm_set_rope(P<const float*>(cos), P<const float*>(sin), cols, seq);
   });
   m.def("gemm_f8", [](int fa, int fb, int epi, uintptr_t a, long lda, uintptr_t b, long ldb, uintptr_t c, long ldc,
                       uintptr_t bias, uintptr_t sa, uintptr_t sb, int M, int N, int K, float beta, int group_m, int cus,

@@ -791,11 +791,20 @@ static int plan_splitk(pd::gm::Params& p, long ws_bytes) {
   return 8 * blocks;
 }
 
+// RoPE-epilogue tables of the next pd_gemm call on this thread (pd_gemm_set_rope; consumed by the call)
+static thread_local const float* t_rope_cos = nullptr;
+static thread_local const float* t_rope_sin = nullptr;
+static thread_local int t_rope_cols = 0, t_rope_seq = 0;
+extern "C" void pd_gemm_set_rope(const float* cos, const float* sin, int cols, int seq) {
+  t_rope_cos = cos; t_rope_sin = sin; t_rope_cols = cols; t_rope_seq = seq;
+}
+
 extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
                        void* C2, long ldc2, const void* bias, int M, int N, int K, float beta, int H, int group_m,
                        int variant, void* ws, long ws_bytes, void* stream) {
   using namespace pd::gm;
   if (M <= 0 || N <= 0 || K <= 0) return -1;
+  if (epi == kEpiRope && (layout != 3 || !t_rope_cos)) return -3;   // RoPE: TN layout, tables set first
   if ((layout & 3) && K % 8) return -1;   // K-major operands move 16-B chunks along k
   Params p;
   p.A = (const unsigned short*)A;
@@ -808,6 +817,8 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   p.zero = bias;  // ablation 7 only: the caller passes a zeroed buffer in `bias`
   p.goff = nullptr; p.ngroups = 0; p.gmode = 0; p.gsb = p.gsc = p.gsbias = 0;
   p.part = (float*)ws; p.ksplit = 1; p.kchunk = 0; p.tail_cap = 0; p.cpx = cus_per_xcd();
+  p.rope_cos = t_rope_cos; p.rope_sin = t_rope_sin; p.rope_cols = t_rope_cols; p.rope_seq = t_rope_seq;
+  t_rope_cos = t_rope_sin = nullptr;
   {
     // operand extents: K-major [rows][ld] with K valid per row, MN-major [k][ld] with rows / cols valid per k
     const bool ak = layout & 1, bk = (layout >> 1) & 1;
@@ -832,6 +843,7 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
       return (int)hipGetLastError();
     variant = 6;
   }
+  if (epi == kEpiRope) return -3;   // only the spread TN schedule has the RoPE epilogue
   if (epi == kEpiSwiGLU && bk) return -3;  // K-major gate|up weight: v7 only
   // v4+ store 4 consecutive output columns per lane (8-B bf16 / 16-B fp32 accesses): rows must keep that alignment
   if (variant >= 4 && (ldc % 4 || (size_t)C % 16 || (C2 && (ldc2 % 4 || (size_t)C2 % 16)))) variant = 0;

@@ -76,6 +76,36 @@ __device__ __forceinline__ void epilogue_v7_swi_x4(const Params& p, f32x4v (&acc
   }
 }
 
+// RoPE epilogue (kEpiRope): the wave's 128 columns are one head when they lie below rope_cols, and its two 64-column
+// halves h = 0 / 1 hold head dims d and d + 64 at the same lane position — every rotate-half pair is in one lane, so
+// the rotation runs on the fp32 accumulators (x1 cos - x2 sin, x2 cos + x1 sin; cos / sin[d + 64] = [d] for the
+// rotate-half tables) before the usual bf16 stores.
+__device__ __forceinline__ void rope_rotate(const Params& p, f32x4v (&acc)[2][8][4], int tm, int tn, int arow,
+                                            int bcolw, int lane) {
+  if (tn * BN + bcolw >= p.rope_cols) return;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = tm * BM + arow + 16 * i + (lane & 15);
+    const int pos = (r < p.M ? r : 0) % p.rope_seq;
+    const float* cr = p.rope_cos + (long)pos * 128;
+    const float* sr = p.rope_sin + (long)pos * 128;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int d = 16 * j + 4 * g;
+      const float4 c = *(const float4*)(cr + d);
+      const float4 sn = *(const float4*)(sr + d);
+      const float cv[4] = {c.x, c.y, c.z, c.w}, sv[4] = {sn.x, sn.y, sn.z, sn.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x1 = acc[0][i][j][e], x2 = acc[1][i][j][e];
+        acc[0][i][j][e] = x1 * cv[e] - x2 * sv[e];
+        acc[1][i][j][e] = x2 * cv[e] + x1 * sv[e];
+      }
+    }
+  }
+}
+
 template <int EPI, int SCHED>
 __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   constexpr bool BAR4 = SCHED & 1, PRIO = (SCHED & 2) != 0;
@@ -399,14 +429,15 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
     }
     // tile done: accumulators out while the next tile's first K-tiles stream / sit in LDS
     asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+    if constexpr (EPI == kEpiRope) rope_rotate(p, acc, ctm, ctn, arow, bcolw, lane);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      if constexpr (X4 && EPI == kEpiBF16) {
+      if constexpr (X4 && (EPI == kEpiBF16 || EPI == kEpiRope)) {
         // interior tile, 16-B aligned rows: the widened stores; otherwise the element-checked epilogue
         if ((ctm + 1) * BM <= p.M && (ctn + 1) * BN <= p.N && (p.ldc & 7) == 0 && ((size_t)p.C & 15) == 0)
           epilogue_v7_x4<NTS>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
         else
-          epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+          epilogue_t<kEpiBF16>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
       } else if constexpr (X4 && EPI == kEpiSwiGLU) {
         if ((ctm + 1) * BM <= p.M && (ctn + 1) * 128 <= p.H && (p.ldc & 7) == 0 && (p.ldc2 & 7) == 0 &&
             (p.H & 7) == 0 && ((size_t)p.C & 15) == 0 && ((size_t)p.C2 & 15) == 0)
@@ -457,6 +488,11 @@ bool pd_gemm_v7(const pd::gm::Params& p, int layout, int epi, int sched, int cus
       PD_V7_CASE(kEpiSwiGLU, 1408) PD_V7_CASE(kEpiSwiGLU, 1920)
       default: return false;
     }
+    return true;
+  }
+  if (epi == kEpiRope) {   // RoPE epilogue: the spread schedule only, bias-free
+    if (sched != 384 || p.bias || !p.rope_cos || !p.rope_sin || p.rope_seq <= 0 || p.rope_cols % 128) return false;
+    gemm_v7_kernel<kEpiRope, 384><<<grid, NTHR4, 0, st>>>(p);
     return true;
   }
   if (epi == kEpiGeLU || epi == kEpiDGeLU) {   // the GELU epilogues: the spread schedule only

@@ -27,7 +27,9 @@ constexpr int kRecords = 0x7fffffff;
 // kEpiGeLU: C = gelu(acc + bias), C2 = acc + bias (the pre-activation the backward reads); kEpiDGeLU: C = acc *
 // gelu'(C2) with C2 = that saved pre-activation (reference funcs/fused_gemm_epilogue.h:382 GELU_AUX_BIAS forward,
 // :580 the gelu_grad backward).  Both: p.H = 1 for the tanh approximation, 0 for erf.
-enum Epi : int { kEpiBF16 = 0, kEpiF32 = 1, kEpiSwiGLU = 2, kEpiGeLU = 3, kEpiDGeLU = 4 };
+// kEpiRope (v7 only): bf16 out with rotate-half RoPE applied to the 128-wide heads of columns < rope_cols
+// (position = row % rope_seq; fp32 cos / sin tables [rope_seq, 128]) — the QKV projection's q / k heads.
+enum Epi : int { kEpiBF16 = 0, kEpiF32 = 1, kEpiSwiGLU = 2, kEpiGeLU = 3, kEpiDGeLU = 4, kEpiRope = 5 };
 
 struct Params {
   const unsigned short* A;
@@ -64,6 +66,10 @@ struct Params {
   // implicit-GEMM convolution (gemm7.hip SCHED bit 11): K-tiles per tap (log2), taps, kernel width, padded row pitch,
   // padding and the shift's sign (+1 forward, -1 input gradient)
   int cv_kpb_log2, cv_taps, cv_kw, cv_pitch, cv_pad_h, cv_pad_w, cv_sign;
+  // RoPE epilogue (kEpiRope)
+  const float* rope_cos;
+  const float* rope_sin;
+  int rope_cols, rope_seq;
 };
 
 // Tiles [t0, t0 + n) of the grouped order belong to XCD x (the chunking xcd_remap uses); the first `full`

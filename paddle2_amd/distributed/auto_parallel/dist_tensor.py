@@ -460,6 +460,8 @@ def _rule(func, name, args, kwargs, dts, nd_mesh, mesh):
         out_shape = list(shapes[0]) if shapes else list(args[1])
         ins, outp = _view_rule(x, out_shape)
         lx = _reshard_to(x, ins)
+        if not lx.is_contiguous():   # the global view is of a contiguous tensor; the local shard may be strided
+            lx = lx.contiguous()
         return (lx, _local_view_shape(out_shape, outp, mesh)) + tuple(args[2:]), kwargs, [tuple(outp)], shapes
     if name in ("unsqueeze", "squeeze", "expand", "slice", "select", "split", "split_with_sizes", "unbind", "cat",
                 "stack", "index_select", "gather", "scatter_add", "index_add", "index_put", "nonzero", "sort",

@@ -172,6 +172,17 @@ class LlamaAttention(nn.Layer):
             attn = CP.ring_flash_attention if self.config.context_parallel == "ring" else CP.ulysses_attention
             o = attn(q, k, v, self._sep_group(), causal=True)
             return self.o_proj(_wrap(o.reshape(b, s, nh * d)))
+        if self.config.fuse_attention_qkv and type(self.qkv_proj) is nn.Linear and not (
+                self.qkv_proj._forward_pre_hooks or self.qkv_proj._forward_post_hooks):
+            w = self.qkv_proj.weight._t
+            bias = None if self.qkv_proj.bias is None else self.qkv_proj.bias._t
+            if T.qkv_rope_linear_ok(x._t, w, bias, d, pos):
+                # RoPE in the QKV GEMM epilogue, attention on the rotated qkv in place
+                c128 = cos.reshape(-1, d)[:s].float().contiguous()
+                s128 = sin.reshape(-1, d)[:s].float().contiguous()
+                qkv = T._QKVRopeLinearFn.apply(x._t, w, c128, s128, nh + nkv, s).view(b, s, nh + 2 * nkv, d)
+                o = T.qkv_attention(qkv, nh, nkv, causal=True)
+                return self.o_proj(_wrap(o.reshape(b, s, nh * d)))
         if self.config.fuse_attention_qkv:
             # one autograd node: strided q/k/v views -> RoPE -> flash attention; backward fills one dQKV
             qkv = self.qkv_proj(x)._t.view(b, s, nh + 2 * nkv, d)

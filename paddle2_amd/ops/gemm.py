@@ -22,7 +22,7 @@ import torch
 from . import _native as N
 
 LAYOUT_AK, LAYOUT_BK = 1, 2
-EPI_BF16, EPI_F32, EPI_SWIGLU, EPI_GELU, EPI_DGELU = 0, 1, 2, 3, 4
+EPI_BF16, EPI_F32, EPI_SWIGLU, EPI_GELU, EPI_DGELU, EPI_ROPE = 0, 1, 2, 3, 4, 5
 GROUP_M = int(os.environ.get("PADDLE2_AMD_GEMM_GROUP_M", "8"))
 _GROUP_FORCED = "PADDLE2_AMD_GEMM_GROUP_M" in os.environ
 # kernel schedule (csrc/kernels/gemm.hip): 0 = v2 (8 waves, 2 per SIMD, 128x64 wave tiles), 4 = v4 (4 waves,
@@ -40,10 +40,11 @@ _GROUP_FORCED = "PADDLE2_AMD_GEMM_GROUP_M" in os.environ
 V7_SPREAD = 64 + 384
 _FORCE = os.environ.get("PADDLE2_AMD_GEMM_VARIANT")
 VARIANT = int(_FORCE) if _FORCE is not None else None
-PASS_VARIANT = {"fwd": V7_SPREAD, "dgrad": V7_SPREAD, "wgrad": 4, "wgrad_bf16": 4, "swiglu": V7_SPREAD}
+PASS_VARIANT = {"fwd": V7_SPREAD, "dgrad": V7_SPREAD, "wgrad": 4, "wgrad_bf16": 4, "swiglu": V7_SPREAD,
+                "rope": V7_SPREAD}
 # grouped tile order per pass (row tiles that sweep the column tiles together): 4 for the spread TN schedule
 # (forward +2..7 %, dgrad +0..2 % over 8 at M = 32768; profiles/r4_gemm_spread.md), 8 for the wgrad kernels
-PASS_GROUP_M = {"fwd": 4, "dgrad": 4, "swiglu": 4, "wgrad": 8, "wgrad_bf16": 8}
+PASS_GROUP_M = {"fwd": 4, "dgrad": 4, "swiglu": 4, "wgrad": 8, "wgrad_bf16": 8, "rope": 4}
 
 
 def _variant(name):
@@ -188,6 +189,23 @@ def mm_dgrad_dgelu(dy2, w, h, approximate=True):
     out = torch.empty(M, K, dtype=dy2.dtype, device=dy2.device)
     _launch(LAYOUT_AK | LAYOUT_BK, EPI_DGELU, dy2, dy2.stride(0), w, w.stride(0), out, out.stride(0), h, h.stride(0),
             None, M, K, Nn, 0.0, int(bool(approximate)), name="dgrad")
+    return out
+
+
+def mm_fwd_rope(x2, w, cos, sin, rope_cols, seq):
+    """y[M, N] = x2 @ w with rotate-half RoPE applied in the epilogue to the 128-wide heads of columns < rope_cols
+    (row r at position r % seq; fp32 cos / sin [seq, 128]) — the QKV projection with its q / k rotation fused.
+    None when the spread TN schedule is not the one selected (the caller then runs GEMM + RoPE)."""
+    M, K = x2.shape
+    Nn = w.shape[1]
+    if _variant("rope") != V7_SPREAD or K % 128 or rope_cols % 128 or Nn % 8:
+        return None
+    assert cos.dtype == sin.dtype == torch.float32 and cos.shape == sin.shape == (seq, 128)
+    out = torch.empty(M, Nn, dtype=x2.dtype, device=x2.device)
+    wt = _wt(w)
+    N.native().gemm_set_rope(cos.data_ptr(), sin.data_ptr(), int(rope_cols), int(seq))
+    _launch(LAYOUT_AK | LAYOUT_BK, EPI_ROPE, x2, x2.stride(0), wt, wt.stride(0), out, out.stride(0), None, 0, None,
+            M, Nn, K, name="rope")
     return out
 
 

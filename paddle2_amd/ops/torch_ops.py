@@ -16,11 +16,25 @@ from . import _native as N
 
 _DT = N.DT_CODE
 
-try:   # DistTensor arguments take the SPMD dispatch at op entry (distributed/auto_parallel/dist_ops.py)
-    from ..distributed.auto_parallel.dist_tensor import DistTensor as _DTensor
-except Exception:  # noqa: BLE001
-    class _DTensor:  # noqa: D101
-        pass
+_DT_CLS = []
+
+
+class _DTensorMeta(type):
+    """``isinstance(x, _DTensor)`` is the framework's DistTensor, resolved on first use (the distributed package
+    imports this module, so it cannot be imported here)."""
+
+    def __instancecheck__(cls, obj):
+        if type(obj) is torch.Tensor or not isinstance(obj, torch.Tensor):
+            return False
+        if not _DT_CLS:
+            from ..distributed.auto_parallel.dist_tensor import DistTensor
+
+            _DT_CLS.append(DistTensor)
+        return isinstance(obj, _DT_CLS[0])
+
+
+class _DTensor(metaclass=_DTensorMeta):
+    """DistTensor arguments take the SPMD dispatch at op entry (distributed/auto_parallel/dist_ops.py)."""
 
 
 def _dist_ops():
@@ -1445,6 +1459,62 @@ class _QKVRopeAttnFn(torch.autograd.Function):
         _rope_apply(dq, cos, sin, pos, 0, False, True, out=dqkv[:, :, :nh])
         _rope_apply(dk, cos, sin, pos, 0, False, True, out=dqkv[:, :, nh:nh + nkv])
         return dqkv, None, None, None, None, None, None, None
+
+
+class _QKVRopeLinearFn(torch.autograd.Function):
+    """qkv = RoPE_{q,k}(x @ W) for the fused QKV projection (W [K, (Hq+2Hk) * 128]): the rotation of the q / k heads
+    runs in the GEMM epilogue on the fp32 accumulators (gemm7.hip kEpiRope), so neither a RoPE kernel nor rotated
+    q / k copies exist in the forward; the attention then reads the rotated qkv in place (_QKVAttnFn).  Backward:
+    RoPE^T on the q / k columns of the incoming gradient, then the projection's dgrad / wgrad."""
+
+    @staticmethod
+    def forward(ctx, x, w, cos, sin, nq_heads, seq):
+        from . import gemm as G
+
+        K = w.shape[0]
+        x2 = x.reshape(-1, K)
+        rope_cols = nq_heads * 128
+        y = G.mm_fwd_rope(x2, w, cos, sin, rope_cols, seq)
+        if y is None:   # another GEMM schedule selected: GEMM, then RoPE on the q / k heads
+            y = G.mm_fwd(x2, w)
+            y4 = y.view(-1, seq, w.shape[1] // 128, 128)
+            y4[:, :, :nq_heads].copy_(_rope_apply(y4[:, :, :nq_heads], cos, sin, None, 0, False, False))
+        ctx.save_for_backward(x2, w, cos, sin)
+        ctx.meta = (x.shape, nq_heads, seq)
+        ctx.gt = getattr(w, "_p2_gt", None)
+        return y.view(*x.shape[:-1], w.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import gemm as G
+
+        x2, w, cos, sin = ctx.saved_tensors
+        xshape, nq, seq = ctx.meta
+        Nn = w.shape[1]
+        dy4 = dy.reshape(-1, seq, Nn // 128, 128)
+        dpre = torch.empty(dy4.shape, dtype=dy.dtype, device=dy.device)
+        _rope_apply(dy4[:, :, :nq], cos, sin, None, 0, False, True, out=dpre[:, :, :nq])
+        dpre[:, :, nq:].copy_(dy4[:, :, nq:])
+        d2 = dpre.view(-1, Nn)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = G.mm_dgrad(d2, w).view(xshape)
+        if ctx.needs_input_grad[1]:
+            dw = weight_grad(x2, d2, ctx.gt)
+        return dx, dw, None, None, None, None
+
+
+def qkv_rope_linear_ok(x, w, bias, head_dim, pos):
+    from . import gemm as G
+
+    return (head_dim == 128 and bias is None and pos is None and not isinstance(x, _DTensor)
+            and not isinstance(w, _DTensor) and not WeightGradStore.route and w.dim() == 2
+            and w.dtype == x.dtype and x.shape[-1] == w.shape[0] and G.enabled(x) and x.is_contiguous()
+            and G.supported_fwd(x.reshape(-1, w.shape[0]), w) and w.shape[1] % 128 == 0
+            and _pass_native("fwd", x) and _pass_native("dgrad", x) and _ROPE_IN_GEMM)
+
+
+_ROPE_IN_GEMM = _os.environ.get("PADDLE2_AMD_ROPE_IN_GEMM", "1") != "0"
 
 
 class _QKVAttnFn(torch.autograd.Function):

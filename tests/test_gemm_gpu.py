@@ -258,3 +258,31 @@ def test_tail_splitk_wgrad_and_fwd(M, N, K, beta, monkeypatch):
     a, w, b = _rand(M, K, seed=42), _rand(K, N, seed=43, scale=0.02), _rand(N, seed=44)
     rows = torch.arange(0, M, 53, device=dev)
     assert _rel(G.mm_fwd(a, w, bias=b)[rows], a[rows].float() @ w.float() + b.float()) < 8e-3
+
+
+@pytest.mark.parametrize("B,S,nq,nkv", [(2, 256, 4, 2), (1, 512, 8, 8)])
+def test_qkv_rope_linear_node(B, S, nq, nkv):
+    """The QKV projection with RoPE in the GEMM epilogue (torch_ops._QKVRopeLinearFn): rotated q / k heads and the
+    unrotated v vs the fp32 GEMM + rotate-half reference, and the input / weight gradients through RoPE^T."""
+    from paddle2_amd.ops import torch_ops as T
+
+    K, D = 512, 128
+    Nn = (nq + 2 * nkv) * D
+    x = _rand(B, S, K, seed=40)
+    w = _rand(K, Nn, seed=41, scale=K ** -0.5)
+    cos, sin = T.rope_tables(S, D, interleaved=False, device=dev)
+    dy = _rand(B, S, Nn, seed=42)
+    xi, wi = x.clone().requires_grad_(), w.clone().requires_grad_()
+    y = T._QKVRopeLinearFn.apply(xi, wi, cos.contiguous(), sin.contiguous(), nq + nkv, S)
+    y.backward(dy)
+    xr, wr = x.float().requires_grad_(), w.float().requires_grad_()
+    h = (xr @ wr).view(B, S, nq + 2 * nkv, D)
+    c, s_ = cos[None, :, None, :], sin[None, :, None, :]
+    qk = h[:, :, :nq + nkv]
+    x1, x2 = qk[..., :D // 2], qk[..., D // 2:]
+    rot = torch.cat([x1 * c[..., :D // 2] - x2 * s_[..., :D // 2], x2 * c[..., D // 2:] + x1 * s_[..., D // 2:]], -1)
+    yr = torch.cat([rot, h[:, :, nq + nkv:]], 2).view(B, S, Nn)
+    yr.backward(dy.float())
+    assert _rel(y, yr) < 8e-3
+    assert _rel(xi.grad, xr.grad) < 1e-2
+    assert _rel(wi.grad, wr.grad) < 1e-2
