@@ -605,4 +605,41 @@ def _unsqueeze_like(func, name, args, kwargs, dts, nd_mesh, mesh, shapes):
                 ins_g.append(Replicate()); ins_i.append(Replicate()); outp.append(Replicate())
         la, lk = _apply(args, kwargs, {id(g): ins_g, id(ids): ins_i})
         return la, lk, [tuple(outp)], shapes
+    if name in ("slice", "select", "split", "split_with_sizes", "unbind", "flip", "roll", "cumsum") \
+            and x is not None:
+        nd = x.dim()
+        if name in ("slice", "select", "cumsum"):
+            axis = args[1] if len(args) > 1 else kwargs.get("dim", 0)
+        elif name in ("split", "split_with_sizes"):   # (self, split_size(s), dim=0)
+            axis = args[2] if len(args) > 2 else kwargs.get("dim", 0)
+        elif name == "unbind":
+            axis = args[1] if len(args) > 1 else kwargs.get("dim", 0)
+        elif name == "flip":
+            axis = list(args[1])
+        else:   # roll(x, shifts, dims)
+            axis = list(args[2]) if len(args) > 2 and args[2] else list(range(nd))
+        axes = {a % nd for a in (axis if isinstance(axis, (list, tuple)) else [axis])}
+        ins = []
+        for p in x._placements:
+            ins.append(Replicate() if (isinstance(p, Shard) and p.dim % nd in axes) else p)
+        if name in ("select", "unbind"):
+            a = next(iter(axes))
+            outp = [Shard(p.dim - (1 if p.dim > a else 0)) if isinstance(p, Shard) else p for p in ins]
+        else:
+            outp = ins
+        la, lk = _apply(args, kwargs, {id(x): ins})
+        return la, lk, [tuple(outp)], shapes
+    if name in ("cat", "stack"):
+        ts = [t for t in args[0]]
+        dim = args[1] if len(args) > 1 else kwargs.get("dim", 0)
+        ref = next(t for t in ts if isinstance(t, DistTensor))
+        nd = ref.dim()
+        a = dim % (nd + (1 if name == "stack" else 0))
+        base = [Replicate() if (isinstance(p, Shard) and p.dim == a and name == "cat") or isinstance(p, Partial)
+                else p for p in ref._placements]
+        want = {id(t): base for t in ts if isinstance(t, DistTensor)}
+        la, lk = _apply(args, kwargs, want)
+        outp = base if name == "cat" else [Shard(p.dim + (1 if p.dim >= a else 0)) if isinstance(p, Shard) else p
+                                           for p in base]
+        return la, lk, [tuple(outp)], shapes
     raise _Fallback()

@@ -76,6 +76,14 @@ ids = torch.tensor([[1, 3], [0, 2]])
 E = torch.randn(5, 6, generator=gen)
 check("embedding_col", torch.nn.functional.embedding(ids, dist_(E, R(), S(1))), torch.nn.functional.embedding(ids, E))
 
+# ---- shape ops: slicing / selecting / splitting along a replicated axis keeps the other axis' shards
+xs_ = dist_(A, S(0), S(1))
+check("slice", xs_[:, 1:5], A[:, 1:5])
+check("select", xs_[:, 2], A[:, 2])
+check("split", torch.cat(torch.split(xs_, 2, dim=1), 0), torch.cat(torch.split(A, 2, dim=1), 0))
+check("cat", torch.cat([xs_, xs_ * 2], 1), torch.cat([A, A * 2], 1))
+check("stack", torch.stack([xs_, xs_], 0), torch.stack([A, A], 0))
+
 # ---- autograd through a tensor-parallel MLP (col -> gelu -> row), data-parallel input rows
 W1 = torch.randn(6, 8, generator=gen) * 0.3
 W2 = torch.randn(8, 6, generator=gen) * 0.3
