@@ -14,8 +14,12 @@ the current sub-graph is closed (its live tensors — every symbolic value in th
 all simulated frames — are fetched by running it through the Executor), the jump / call runs on the concrete
 values, and a new sub-graph starts from the instruction after it.  Calls of plain user Python functions (and the
 ``forward`` of hook-free user Layers) are simulated inline in a child frame, so a break inside them is a break at
-that instruction too.  Opcodes outside the supported set (``with``, ``try``, generators, closures being created)
-abandon the translation for the whole call (``Unsupported``: the caller runs it eagerly).
+that instruction too.  A ``with`` block breaks the graph at its ``__enter__`` and at its ``__exit__`` (both run
+concretely and are recorded as calls, so the sub-graph of the body runs INSIDE the context: ``with paddle.no_grad():``
+records and replays a no-grad segment); a manager the replay cannot re-enter (a ``contextlib`` generator, one whose
+constructor already changed state) makes the trace simulation-only.  Opcodes outside the supported set (``try``,
+``async with``, generators) abandon the translation for the whole call (``Unsupported``: the caller runs it eagerly);
+an abandoned translation leaves the contexts it entered first.
 
 The simulation also records a ``Trace`` — the flat sequence of sub-graphs, branch outcomes, eager calls and the
 return spec, over *slots* (every tensor that enters the frame: arguments, sub-graph outputs, eager-call results).
@@ -167,6 +171,7 @@ class OpcodeExecutor:
         self.slot_val = {}     # slot -> Tensor (keeps it alive: ids stay unique)
         self.graph = None      # current sub-graph state
         self._steps = 0
+        self._exits = []       # bound __exit__ of the ``with`` blocks entered and not yet left (innermost last)
 
     # ----------------------------------------------------------------------------------- slots & specs
     def _new_slot(self, t):
@@ -287,14 +292,19 @@ class OpcodeExecutor:
         self._suspend()
         self.graph = None
         outs, seen = [], {}
+        # a lifted input still live unchanged maps back to its slot's tensor (fetching it would detach it when the
+        # sub-graph runs under no_grad, and copies it for nothing otherwise)
+        fed = {id(s): self.slot_val[k] for k, s in gs["lifted"].items()}
 
         def collect(t):
-            if _is_sym_tensor(t) and id(t) not in seen:
+            if _is_sym_tensor(t) and id(t) not in seen and id(t) not in fed:
                 seen[id(t)] = len(outs)
                 outs.append(t)
             return t
 
         self._map_state(collect)
+        if fed:
+            self._map_state(lambda t: fed.get(id(t), t))
         if not outs:
             return
         prog = gs["prog"]
@@ -331,9 +341,11 @@ class OpcodeExecutor:
         self._start_graph()
         try:
             ret = self._execute(fr)
-        except BaseException:
+        except BaseException as e:
             self._suspend()
             self.graph = None
+            while self._exits:   # leave the contexts the simulation entered before the call is re-run eagerly
+                self._exits.pop()(type(e), e, e.__traceback__)
             raise
         return ret
 
@@ -417,6 +429,21 @@ class OpcodeExecutor:
         r = f(*args, **kwargs)
         rspec = self._bind(r)
         self.trace.steps.append(("call", fspec, aspec, kspec, rspec))
+        self.trace.n_breaks += 1
+        self._start_graph()
+        return r
+
+    def _ctx_call(self, f, args, mgr):
+        """Graph break at a context manager's ``__enter__`` / ``__exit__``: the sub-graph so far runs before it (a
+        body's graph runs inside the context), the call runs concretely and is recorded for replay."""
+        fr = self.frames[-1]
+        fr.stack.append(list(args))
+        self._end_graph()
+        args = fr.stack.pop()
+        aspec = self._spec(list(args))
+        r = f(*args)
+        rspec = ("const", r) if r is mgr or r is None else self._bind(r)
+        self.trace.steps.append(("call", ("const", f), aspec, ("dict", ()), rspec))
         self.trace.n_breaks += 1
         self._start_graph()
         return r
@@ -569,7 +596,26 @@ class OpcodeExecutor:
         args = fr.stack[len(fr.stack) - n:] if n else []
         del fr.stack[len(fr.stack) - n:]
         f = fr.stack.pop()
+        if self._exits and n == 3 and any(f is e for e in self._exits):   # the normal exit of a ``with`` block
+            self._exits = [e for e in self._exits if e is not f]
+            fr.stack.append(self._ctx_call(f, args, f.__self__))
+            return
         fr.stack.append(self._call(fr, f, args, {}))
+
+    def op_SETUP_WITH(self, fr, ins):
+        mgr = fr.stack.pop()
+        if isinstance(mgr, Tensor):
+            raise Unsupported("with over a tensor")
+        cls = type(mgr)
+        enter, exit_ = cls.__enter__.__get__(mgr, cls), cls.__exit__.__get__(mgr, cls)
+        if not _reusable_ctx(mgr):
+            self.trace.replayable = False   # the replay would re-enter a spent / pre-applied manager
+        fr.stack.append(exit_)
+        self._exits.append(exit_)
+        fr.stack.append(self._ctx_call(enter, (), mgr))
+
+    def op_POP_BLOCK(self, fr, ins):
+        pass   # the simulator keeps no block stack: exceptions leave the simulation (see run())
 
     def op_CALL_FUNCTION_KW(self, fr, ins):
         names = fr.stack.pop()
@@ -788,6 +834,16 @@ class OpcodeExecutor:
                 else annotations
         f.__module__ = fr.glb.get("__name__")
         fr.stack.append(f)
+
+
+def _reusable_ctx(mgr):
+    """Managers whose ``__enter__`` holds all their effect and that can be entered again (the replay re-runs the
+    recorded ``__enter__`` / ``__exit__`` on the same object)."""
+    from ..framework import grad_mode
+
+    if getattr(mgr, "_sot_reusable", False):
+        return True
+    return type(mgr) in (grad_mode.no_grad, grad_mode.enable_grad, torch.no_grad, torch.enable_grad)
 
 
 # ------------------------------------------------------------------------------------------- replay

@@ -244,3 +244,53 @@ def test_bytecode_unsupported_construct_runs_eagerly():
     np.testing.assert_allclose(_np(f(x)), [2.0, 2.0])
     np.testing.assert_allclose(_np(f(x)), [2.0, 2.0])
     assert f.stats["eager_calls"] == 2 and "Unsupported" in f.stats["breaks"][0]
+
+
+def _with_no_grad(x, w):
+    h = x * w
+    with paddle.no_grad():
+        d = (h * 2).detach() + w   # recorded inside the context: no graph to w from this term
+    return h.sum() + d.sum()
+
+
+def test_bytecode_with_block_breaks_and_replays_inside_context():
+    f = paddle.jit.to_static(_with_no_grad, full_graph=False)
+    x = paddle.to_tensor(np.arange(6, dtype="float32").reshape(2, 3))
+    for step in range(2):
+        w = paddle.to_tensor(np.full([2, 3], 0.5, "float32"), stop_gradient=False)
+        out = f(x, w)
+        np.testing.assert_allclose(float(out), float((x * 0.5).sum() + (x * 1.0 + 0.5).sum()), rtol=1e-6)
+        out.backward()
+        np.testing.assert_allclose(_np(w.grad), _np(x))        # only h.sum() carries gradient
+        assert paddle.is_grad_enabled()
+    assert f.stats["simulations"] == 1 and f.stats["guard_hits"] == 1
+    (tr,) = f.traces
+    assert [s[0] for s in tr.steps] == ["graph", "call", "graph", "call", "graph", "return"]
+
+
+def _with_generator_ctx(x):
+    with paddle.amp.auto_cast(enable=False):
+        y = x + 1
+    return y * 2
+
+
+def test_bytecode_with_single_use_manager_simulates_each_call():
+    f = paddle.jit.to_static(_with_generator_ctx, full_graph=False)
+    x = paddle.to_tensor(np.ones([3], "float32"))
+    for _ in range(2):
+        np.testing.assert_allclose(_np(f(x)), [4.0, 4.0, 4.0])
+    assert f.stats["simulations"] == 2 and f.stats["guard_hits"] == 0 and not f.traces
+
+
+def _with_raise(x):
+    with paddle.no_grad():
+        if x.shape[0] > 1:
+            raise ValueError("boom")
+    return x
+
+
+def test_bytecode_with_block_left_when_translation_is_abandoned():
+    f = paddle.jit.to_static(_with_raise, full_graph=False)
+    with pytest.raises(ValueError):
+        f(paddle.to_tensor(np.ones([3], "float32")))
+    assert paddle.is_grad_enabled()
