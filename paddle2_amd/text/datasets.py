@@ -3,8 +3,7 @@ conll05,wmt14,wmt16}.py).
 
 There is no network here: every dataset reads a local copy of the official archive via
 ``data_file=`` (the reference's download cache path) and raises a clear error when it is missing.
-UCIHousing, Imdb, Imikolov and Movielens parse their archives; Conll05st / WMT14 / WMT16 read the
-pre-tokenised archives' line formats.
+Every dataset parses its official archive layout (dictionaries, tab-separated pairs, gzipped CoNLL columns).
 """
 from __future__ import annotations
 
@@ -169,40 +168,239 @@ class Movielens(Dataset):
         return len(self.data)
 
 
-class _LineCorpus(Dataset):
-    """Parallel / labelled line corpora stored as tab-separated text inside an archive."""
+_S, _E, _U = "<s>", "<e>", "<unk>"
 
-    def __init__(self, data_file, name, member_pattern):
-        _need(data_file, name)
-        self.data = []
-        opener = zipfile.ZipFile if data_file.endswith(".zip") else tarfile.open
-        with opener(data_file) as a:
-            members = a.namelist() if isinstance(a, zipfile.ZipFile) else [m.name for m in a.getmembers()]
-            for m in members:
-                if re.search(member_pattern, m):
-                    raw = a.read(m) if isinstance(a, zipfile.ZipFile) else a.extractfile(m).read()
-                    for ln in raw.decode("utf-8", "ignore").splitlines():
-                        if ln.strip():
-                            self.data.append(ln.split("\t"))
 
+def _tar_lines(tf, name):
+    for ln in tf.extractfile(name):
+        yield ln.decode("utf-8", "ignore")
+
+
+def _pairs_to_ids(lines, src_dict, trg_dict, src_col, unk, max_len=None):
+    """Tab-separated sentence pairs -> (src, trg, trg_next) id lists with <s>/<e> framing."""
+    src_ids, trg_ids, trg_next = [], [], []
+    s_id, e_id = src_dict[_S], src_dict[_E]
+    for ln in lines:
+        cols = ln.strip().split("\t")
+        if len(cols) != 2:
+            continue
+        src = [s_id] + [src_dict.get(w, unk) for w in cols[src_col].split()] + [e_id]
+        trg = [trg_dict.get(w, unk) for w in cols[1 - src_col].split()]
+        if max_len is not None and (len(src) > max_len or len(trg) > max_len):
+            continue
+        src_ids.append(src)
+        trg_ids.append([trg_dict.get(_S, s_id)] + trg)
+        trg_next.append(trg + [trg_dict.get(_E, e_id)])
+    return src_ids, trg_ids, trg_next
+
+
+class _Seq2Seq(Dataset):
     def __getitem__(self, idx):
-        return tuple(self.data[idx])
+        return np.array(self.src_ids[idx]), np.array(self.trg_ids[idx]), np.array(self.trg_ids_next[idx])
 
     def __len__(self):
-        return len(self.data)
+        return len(self.src_ids)
 
 
-class Conll05st(_LineCorpus):
+class WMT14(_Seq2Seq):
+    """WMT14 en-fr (reference text/datasets/wmt14.py:113-215): the archive's ``src.dict`` / ``trg.dict`` give the
+    first ``dict_size`` words their line numbers; ``{mode}/{mode}`` holds tab-separated pairs; pairs longer than 80
+    ids are dropped.  Items: (src ids with <s>..<e>, <s> + trg ids, trg ids + <e>)."""
+
+    def __init__(self, data_file=None, mode="train", dict_size=-1, download=True):
+        mode = mode.lower()
+        if mode not in ("train", "test", "gen"):
+            raise ValueError(f"mode should be 'train', 'test' or 'gen', but got {mode}")
+        _need(data_file, "WMT14")
+        if dict_size <= 0:
+            raise ValueError("dict_size should be set as positive number")
+        self.mode, self.data_file, self.dict_size = mode, data_file, dict_size
+        with tarfile.open(data_file) as tf:
+            names = [m.name for m in tf.getmembers()]
+
+            def read_dict(suffix):
+                (name,) = [n for n in names if n.endswith(suffix)]
+                out = {}
+                for i, ln in enumerate(_tar_lines(tf, name)):
+                    if i >= dict_size:
+                        break
+                    out[ln.strip()] = i
+                return out
+
+            self.src_dict, self.trg_dict = read_dict("src.dict"), read_dict("trg.dict")
+            self.src_ids, self.trg_ids, self.trg_ids_next = [], [], []
+            for name in (n for n in names if n.endswith(f"{mode}/{mode}")):
+                a, b, c = _pairs_to_ids(_tar_lines(tf, name), self.src_dict, self.trg_dict, 0, 2, max_len=80)
+                self.src_ids += a
+                self.trg_ids += b
+                self.trg_ids_next += c
+
+    def get_dict(self, reverse=False):
+        if reverse:
+            return {v: k for k, v in self.src_dict.items()}, {v: k for k, v in self.trg_dict.items()}
+        return self.src_dict, self.trg_dict
+
+
+class WMT16(_Seq2Seq):
+    """WMT16 en-de (reference text/datasets/wmt16.py:130-339): word dictionaries are built from ``wmt16/train``
+    by descending frequency after the three marks (<s>, <e>, <unk>), ``dict_size`` entries in total; ``lang``
+    picks the source column.  Dictionaries are kept in memory (and cached per archive / size in this process)."""
+
+    TOTAL_EN_WORDS, TOTAL_DE_WORDS = 11250, 19220
+    _dict_cache = {}
+
+    def __init__(self, data_file=None, mode="train", src_dict_size=-1, trg_dict_size=-1, lang="en", download=True):
+        mode = mode.lower()
+        if mode not in ("train", "test", "val"):
+            raise ValueError(f"mode should be 'train', 'test' or 'val', but got {mode}")
+        if lang not in ("en", "de"):
+            raise ValueError(f"lang should be 'en' or 'de', but got {lang}")
+        _need(data_file, "WMT16")
+        if src_dict_size <= 0 or trg_dict_size <= 0:
+            raise ValueError("dict_size should be set as positive number")
+        self.mode, self.data_file, self.lang = mode, data_file, lang
+        other = "de" if lang == "en" else "en"
+        total = {"en": self.TOTAL_EN_WORDS, "de": self.TOTAL_DE_WORDS}
+        self.src_dict_size = min(src_dict_size, total[lang])
+        self.trg_dict_size = min(trg_dict_size, total[other])
+        self.src_dict = self._load_dict(lang, src_dict_size)
+        self.trg_dict = self._load_dict(other, trg_dict_size)
+        with tarfile.open(data_file) as tf:
+            self.src_ids, self.trg_ids, self.trg_ids_next = _pairs_to_ids(
+                _tar_lines(tf, f"wmt16/{mode}"), self.src_dict, self.trg_dict, 0 if lang == "en" else 1,
+                self.src_dict[_U])
+
+    def _load_dict(self, lang, dict_size, reverse=False):
+        key = (os.path.abspath(self.data_file), lang, dict_size)
+        d = self._dict_cache.get(key)
+        if d is None:
+            counts = collections.Counter()
+            col = 0 if lang == "en" else 1
+            with tarfile.open(self.data_file) as tf:
+                for ln in _tar_lines(tf, "wmt16/train"):
+                    cols = ln.strip().split("\t")
+                    if len(cols) == 2:
+                        counts.update(cols[col].split())
+            words = [_S, _E, _U] + [w for w, _ in sorted(counts.items(), key=lambda x: -x[1])][:max(dict_size - 3, 0)]
+            d = self._dict_cache[key] = {w: i for i, w in enumerate(words)}
+        return {i: w for w, i in d.items()} if reverse else dict(d)
+
+    def get_dict(self, lang, reverse=False):
+        size = self.src_dict_size if lang == self.lang else self.trg_dict_size
+        return self._load_dict(lang, size, reverse)
+
+
+class Conll05st(Dataset):
+    """CoNLL-2005 semantic role labelling, WSJ test split (reference text/datasets/conll05.py:125-397).
+
+    ``test.wsj.words.gz`` / ``test.wsj.props.gz`` inside the archive are read in lock-step; a blank props line ends
+    a sentence, whose first props column marks the predicates and every further column is one predicate's bracketed
+    argument spans, turned into B-/I-/O tags.  Items are the nine id sequences of the reference's SRL model: words,
+    the five-word context window around the verb (each repeated over the sentence), the predicate, the window mark,
+    and the tag ids.  The label dictionary orders its tags by name (the reference iterates a set, whose order is
+    not fixed across interpreter runs)."""
+
+    UNK_IDX = 0
+
     def __init__(self, data_file=None, word_dict_file=None, verb_dict_file=None, target_dict_file=None,
                  emb_file=None, download=True):
-        super().__init__(data_file, "Conll05st", r"test\.wsj.*words|props")
+        for f, n in ((data_file, "Conll05st data_file"), (word_dict_file, "Conll05st word_dict_file"),
+                     (verb_dict_file, "Conll05st verb_dict_file"), (target_dict_file, "Conll05st target_dict_file")):
+            _need(f, n)
+        self.data_file, self.emb_file = data_file, emb_file
+        self.word_dict_file, self.verb_dict_file, self.target_dict_file = word_dict_file, verb_dict_file, \
+            target_dict_file
+        self.word_dict = self._load_dict(word_dict_file)
+        self.predicate_dict = self._load_dict(verb_dict_file)
+        self.label_dict = self._load_label_dict(target_dict_file)
+        self._load_anno()
 
+    @staticmethod
+    def _load_dict(filename):
+        with open(filename) as f:
+            return {ln.strip(): i for i, ln in enumerate(f)}
 
-class WMT14(_LineCorpus):
-    def __init__(self, data_file=None, mode="train", dict_size=-1, download=True):
-        super().__init__(data_file, "WMT14", rf"{mode}/{mode}")
+    @staticmethod
+    def _load_label_dict(filename):
+        tags = set()
+        with open(filename) as f:
+            for ln in f:
+                ln = ln.strip()
+                if ln[:2] in ("B-", "I-"):
+                    tags.add(ln[2:])
+        d = {}
+        for t in sorted(tags):
+            d["B-" + t] = len(d)
+            d["I-" + t] = len(d)
+        d["O"] = len(d)
+        return d
 
+    @staticmethod
+    def _bio(column):
+        """One predicate's props column (``(A0*``, ``*``, ``*)``, ``(V*)``) -> B-/I-/O tags."""
+        out, tag, open_ = [], "O", False
+        for tok in column:
+            if tok == "*":
+                out.append("I-" + tag if open_ else "O")
+            elif tok == "*)":
+                out.append("I-" + tag)
+                open_ = False
+            elif "(" in tok:
+                tag = tok[1:tok.index("*")]
+                out.append("B-" + tag)
+                open_ = ")" not in tok
+            else:
+                raise RuntimeError(f"Unexpected label: {tok}")
+        return out
 
-class WMT16(_LineCorpus):
-    def __init__(self, data_file=None, mode="train", src_dict_size=-1, trg_dict_size=-1, lang="en", download=True):
-        super().__init__(data_file, "WMT16", rf"wmt16/{mode}")
+    def _load_anno(self):
+        import gzip
+
+        self.sentences, self.predicates, self.labels = [], [], []
+        base = "conll05st-release/test.wsj"
+        with tarfile.open(self.data_file) as tf, \
+                gzip.GzipFile(fileobj=tf.extractfile(f"{base}/words/test.wsj.words.gz")) as wf, \
+                gzip.GzipFile(fileobj=tf.extractfile(f"{base}/props/test.wsj.props.gz")) as pf:
+            words, rows = [], []
+            for w, p in zip(wf, pf):
+                w, cols = w.decode().strip(), p.decode().split()
+                if cols:
+                    words.append(w)
+                    rows.append(cols)
+                    continue
+                if rows:
+                    columns = list(zip(*rows))
+                    verbs = [x for x in columns[0] if x != "-"]
+                    for k, col in enumerate(columns[1:]):
+                        self.sentences.append(words)
+                        self.predicates.append(verbs[k])
+                        self.labels.append(self._bio(col))
+                words, rows = [], []
+
+    def __getitem__(self, idx):
+        sent, pred, labels = self.sentences[idx], self.predicates[idx], self.labels[idx]
+        n = len(sent)
+        v = labels.index("B-V")
+        mark = [0] * n
+        ctx = []
+        for off in (-2, -1, 0, 1, 2):
+            j = v + off
+            if 0 <= j < n:
+                mark[j] = 1
+                ctx.append(sent[j])
+            else:
+                ctx.append("bos" if off < 0 else "eos")
+        wd = self.word_dict
+        out = [[wd.get(w, self.UNK_IDX) for w in sent]]
+        out += [[wd.get(c, self.UNK_IDX)] * n for c in ctx]
+        out += [[self.predicate_dict.get(pred)] * n, mark, [self.label_dict.get(t) for t in labels]]
+        return tuple(np.array(x) for x in out)
+
+    def __len__(self):
+        return len(self.sentences)
+
+    def get_dict(self):
+        return self.word_dict, self.predicate_dict, self.label_dict
+
+    def get_embedding(self):
+        return self.emb_file
