@@ -91,6 +91,7 @@ int pd_flash_bwd_ext(int, const void*, const void*, const void*, const void*, co
 int pd_flash_fwd(int, const void*, const void*, const void*, void*, float*, int, int, int, int, int, int, long, long,
                  long, long, float, int, void*);
 int pd_flash_bwd_block(int);
+void pd_flash_bwd_set_rope(const float*, const float*);
 int pd_flash_bwd(int, const void*, const void*, const void*, const void*, const void*, const float*, float*, void*,
                  void*, void*, float*, int, int, int, int, int, int, long, long, long, long, long, long, long, float,
                  int, void*);
@@ -324,6 +325,9 @@ PYBIND11_MODULE(_C, m) {
     check(pd_cast_from_f32(dt, P<const float*>(src), P<void*>(dst), n, P<void*>(st)), "cast_from_f32");
   });
   m.def("flash_bwd_block", [](int D) { return pd_flash_bwd_block(D); });
+  m.def("flash_bwd_set_rope", [](uintptr_t cos, uintptr_t sin) {
+    pd_flash_bwd_set_rope(P<const float*>(cos), P<const float*>(sin));
+  });
   m.def("flash_fwd", [](int dt, uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t lse, int B, int Sq,
                         int Sk, int Hq, int Hk, int D, long sq_row, long sk_row, long sv_row, long so_row, float scale,
                         int causal, uintptr_t st) {

@@ -142,6 +142,11 @@ struct Ext {
   float drop_rscale;    // DROP: 1 / (1 - p)
   int dq_atomic;        // dense bwd: dQ partials fp32-atomically added into ONE zeroed slab (pslab = 0)
   int wave_skip;        // fwd, causal: a wave skips the key tiles that lie wholly above its last row
+  // dense bwd, D = 128: q / k were rotate-half RoPE'd in the producing GEMM's epilogue; dK (bwd epilogue) and dQ
+  // (dq_reduce) leave as RoPE^T of their gradients, i.e. gradients of the PRE-rotation q / k.  fp32 [S, 128]
+  // tables (first 64 columns used), position = token index within its sequence.
+  const float* rope_cos;
+  const float* rope_sin;
 };
 
 // Counter-based dropout mask: a stateless 32-bit hash of (seed, batch*head, query, key), so the backward
@@ -861,6 +866,33 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16*
   if (mykey < Sk) {
     bf16* dkr = dK + (kt0 + mykey) * sdk + hk * D;
     bf16* dvr = dV + (kt0 + mykey) * sdv + hk * D;
+    bool rope_t = false;
+    if constexpr (D == 128 && MODE == kDense) rope_t = ex.rope_cos != nullptr;
+    if (rope_t) {
+      // RoPE^T on dK: columns d and d + 64 of this lane's key sit in slices dt and dt + 2; each rotated pair is
+      // stored at once (short live ranges: the epilogue runs with the whole dK / dV accumulator set live)
+      const float* cr = ex.rope_cos + (long)mykey * 128;
+      const float* sr = ex.rope_sin + (long)mykey * 128;
+#pragma unroll
+      for (int dt = 0; dt < DT / 2; ++dt) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int d = dt * 32 + 8 * c + 4 * h;
+          const float4 cv = *reinterpret_cast<const float4*>(cr + d);
+          const float4 sv = *reinterpret_cast<const float4*>(sr + d);
+          const float cc[4] = {cv.x, cv.y, cv.z, cv.w}, sn[4] = {sv.x, sv.y, sv.z, sv.w};
+          unsigned short lo16[4], hi16[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float lo = dkacc[dt][4 * c + e] * scale, hi = dkacc[dt + DT / 2][4 * c + e] * scale;
+            lo16[e] = cvt16<F16>(lo * cc[e] + hi * sn[e]);
+            hi16[e] = cvt16<F16>(hi * cc[e] - lo * sn[e]);
+          }
+          *reinterpret_cast<ushort4*>(dkr + d) = ushort4{lo16[0], lo16[1], lo16[2], lo16[3]};
+          *reinterpret_cast<ushort4*>(dkr + d + D / 2) = ushort4{hi16[0], hi16[1], hi16[2], hi16[3]};
+        }
+      }
+    }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
 #pragma unroll
@@ -871,7 +903,7 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16*
         kv.z = cvt16<F16>(dkacc[dt][4 * c + 2] * scale); kv.w = cvt16<F16>(dkacc[dt][4 * c + 3] * scale);
         vv.x = cvt16<F16>(dvacc[dt][4 * c + 0]); vv.y = cvt16<F16>(dvacc[dt][4 * c + 1]);
         vv.z = cvt16<F16>(dvacc[dt][4 * c + 2]); vv.w = cvt16<F16>(dvacc[dt][4 * c + 3]);
-        *reinterpret_cast<ushort4*>(dkr + d) = kv;
+        if (!rope_t) *reinterpret_cast<ushort4*>(dkr + d) = kv;
         *reinterpret_cast<ushort4*>(dvr + d) = vv;
       }
     }
@@ -880,6 +912,58 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16*
 
 // dQ[b, q, h, :] = sum over the key blocks that wrote row q of their partial slabs; bf16 out with row
 // stride sdq.  Causal: key block kb wrote rows q >= qbegin(kb) = floor(max(0, kb*BNK - off) / BMQ) * BMQ.
+// RoPE^T variant (dense, D = 128, Ext::rope_cos set): a thread takes 8 columns of a head's low half and the
+// matching 8 of its high half, sums both over the slabs and rotates them back before the bf16 store.
+template <bool F16>
+__global__ __launch_bounds__(256) void dq_reduce_rope_kernel(const float* __restrict__ P, bf16* __restrict__ dq,
+                                                             int B, int Sq, int Hq, int nkb, long pslab, long sdq,
+                                                             int causal, int off, int bnk, Ext ex) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  const long per_row = (long)Hq * 8;  // (head, 8-column chunk of the low half) per thread
+  const long total = (long)B * Sq * per_row;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long row = i / per_row;
+    const int j = (int)(i - row * per_row);
+    const int d0 = (j & 7) * 8;
+    const long e = (long)(j >> 3) * 128 + d0;
+    const int q = (int)(row % Sq);
+    int kb_end = nkb;
+    if (causal) {
+      const int lim = q + off;
+      kb_end = lim < 0 ? 0 : min(nkb, lim / bnk + 1);
+      while (kb_end < nkb && (max(0, kb_end * bnk - off) / 32) * 32 <= q) ++kb_end;
+    }
+    float lo[8] = {0, 0, 0, 0, 0, 0, 0, 0}, hi[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const float* src = P + row * (long)Hq * 128 + e;
+    for (int kb = 0; kb < kb_end; ++kb) {
+      const float* sp = src + kb * pslab;
+      const f32x4 a0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sp));
+      const f32x4 a1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sp + 4));
+      const f32x4 b0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sp + 64));
+      const f32x4 b1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sp + 68));
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { lo[t] += a0[t]; lo[4 + t] += a1[t]; hi[t] += b0[t]; hi[4 + t] += b1[t]; }
+    }
+    const float* cr = ex.rope_cos + (long)q * 128 + d0;
+    const float* sr = ex.rope_sin + (long)q * 128 + d0;
+    float olo[8], ohi[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float c = cr[t], sn = sr[t];
+      olo[t] = lo[t] * c + hi[t] * sn;
+      ohi[t] = hi[t] * c - lo[t] * sn;
+    }
+    bf16* out = dq + row * sdq + e;
+    if constexpr (F16) {
+      store_vec<half16, 8>(reinterpret_cast<half16*>(out), olo);
+      store_vec<half16, 8>(reinterpret_cast<half16*>(out + 64), ohi);
+    } else {
+      store_vec<bf16, 8>(out, olo);
+      store_vec<bf16, 8>(out + 64, ohi);
+    }
+  }
+}
+
 template <int MODE, bool F16>
 __global__ __launch_bounds__(256) void dq_reduce_kernel(const float* __restrict__ P, bf16* __restrict__ dq, int B,
                                                         int Sq, int Hq, int D, int nkb, long pslab, long sdq,
@@ -1068,13 +1152,28 @@ extern "C" int pd_flash_fwd(int dt, const void* q, const void* k, const void* v,
 // for varlen) for per-key-block dQ partials (need not be zeroed; ONE slab for dense mode when pd_flash_dq_atomic()); delta a [B, Hq, Sq] ([Hq, total_q] varlen) fp32
 // workspace.  q/k/v/o/dout and dq/dk/dv may all be row-strided views ([B, S, H, D] with token strides), e.g. slices
 // of one fused QKV / dQKV buffer.
+// RoPE^T tables for the next pd_flash_bwd_ext call on this thread (consumed by it; dense mode, D = 128 only)
+static thread_local const float* t_bwd_rope_cos = nullptr;
+static thread_local const float* t_bwd_rope_sin = nullptr;
+extern "C" void pd_flash_bwd_set_rope(const float* cos, const float* sin) {
+  t_bwd_rope_cos = cos;
+  t_bwd_rope_sin = sin;
+}
+
 extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void* v, const void* o, const void* dout,
                                 const float* lse, float* delta, void* dq, void* dk, void* dv, float* dqp, int B,
                                 int Sq, int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, long sdq,
                                 long sdk, long sdv, float scale, int causal, int mode, const int* cu_q, const int* cu_k,
                                 int total_q, const int* fm, const int* fm_t64, const int* fm_t256, int fm_hm,
                                 int drop, unsigned seed, float pdrop, void* stream) {
-  if (int e = check_args(dt, D, Hq, Hk, mode, drop, pdrop, cu_q, cu_k, fm, fm_t256, fm_hm)) return e;
+  if (int e = check_args(dt, D, Hq, Hk, mode, drop, pdrop, cu_q, cu_k, fm, fm_t256, fm_hm)) {
+    t_bwd_rope_cos = t_bwd_rope_sin = nullptr;
+    return e;
+  }
+  if (t_bwd_rope_cos && (mode != 0 || D != 128 || !t_bwd_rope_sin)) {
+    t_bwd_rope_cos = t_bwd_rope_sin = nullptr;
+    return -4;
+  }
   hipStream_t st = (hipStream_t)stream;
   const bool f16 = dt == kF16;
   const long nrows = mode == 1 ? (long)total_q : (long)B * Sq;  // query tokens
@@ -1098,6 +1197,9 @@ extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void
   fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm, seed,
              drop ? (unsigned)fminf(pdrop * 4294967296.f, 4294967040.f) : 0u, drop ? 1.f / (1.f - pdrop) : 1.f,
              atomic ? 1 : 0};
+  ex.rope_cos = t_bwd_rope_cos;
+  ex.rope_sin = t_bwd_rope_sin;
+  t_bwd_rope_cos = t_bwd_rope_sin = nullptr;
   // bench-only ablation (scripts/bench_flash_bwd.py; results are WRONG): 2 = compute dQ but skip its stores,
   // 3 = skip the whole dQ phase (dS image, barrier, dQ MFMAs, stores) — prices the dQ path in isolation
   if (const char* e = getenv("PADDLE2_AMD_FA_DEBUG_DQ_ABLATE")) {
@@ -1117,7 +1219,16 @@ extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void
 #define PD_DQR(MM, FF)                                                                                             \
   fa::dq_reduce_kernel<MM, FF><<<(int)g, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, D, atomic ? 1 : nkb, pslab, sdq, \
                                                        atomic ? 0 : causal, Sk - Sq, BNK, ex)
-  if (mode == 2) { if (f16) PD_DQR(fa::kMask, true); else PD_DQR(fa::kMask, false); }
+  if (ex.rope_cos) {
+    long gr = (nrows * Hq * 8 + 255) / 256;
+    if (gr > 8192) gr = 8192;
+    if (f16)
+      fa::dq_reduce_rope_kernel<true><<<(int)gr, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, atomic ? 1 : nkb, pslab, sdq,
+                                                               atomic ? 0 : causal, Sk - Sq, BNK, ex);
+    else
+      fa::dq_reduce_rope_kernel<false><<<(int)gr, 256, 0, st>>>(dqp, (bf16*)dq, B, Sq, Hq, atomic ? 1 : nkb, pslab,
+                                                                sdq, atomic ? 0 : causal, Sk - Sq, BNK, ex);
+  } else if (mode == 2) { if (f16) PD_DQR(fa::kMask, true); else PD_DQR(fa::kMask, false); }
   else if (mode == 1) { if (f16) PD_DQR(fa::kVarlen, true); else PD_DQR(fa::kVarlen, false); }
   else { if (f16) PD_DQR(fa::kDense, true); else PD_DQR(fa::kDense, false); }
 #undef PD_DQR

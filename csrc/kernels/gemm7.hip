@@ -206,7 +206,11 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
         const int kh = tap / p.cv_kw, kw = tap - kh * p.cv_kw;
         rows = p.cv_sign * ((kh - p.cv_pad_h) * p.cv_pitch + (kw - p.cv_pad_w));
       }
-      const u64 b = (nx ? na : ca) + (u64)((long)rows * p.lda * 2 + ((long)kc << 7));
+      // channel offset as a 32-bit add (a 64-bit (long)kc << 7 was lowered to an s_lshl_b64 whose high source
+      // register still held a partial product of the row offset: K-tile 1 read the wrong rows on gfx950)
+      const long roff = (long)rows * (p.lda * 2);
+      const unsigned coff = (unsigned)kc << 7;
+      const u64 b = (nx ? na : ca) + (u64)roff + (u64)coff;
       const bool live = !nx || nlive;
       return i32x4{(int)(unsigned)b, (int)(unsigned)(b >> 32), live ? (int)(a_end - (unsigned)b) : 0, 0x00020000};
     }

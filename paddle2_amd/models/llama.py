@@ -180,8 +180,12 @@ class LlamaAttention(nn.Layer):
                 # RoPE in the QKV GEMM epilogue, attention on the rotated qkv in place
                 c128 = cos.reshape(-1, d)[:s].float().contiguous()
                 s128 = sin.reshape(-1, d)[:s].float().contiguous()
-                qkv = T._QKVRopeLinearFn.apply(x._t, w, c128, s128, nh + nkv, s).view(b, s, nh + 2 * nkv, d)
-                o = T.qkv_attention(qkv, nh, nkv, causal=True)
+                if T._ROPE_BWD_IN_FLASH:
+                    # one node: backward un-rotates dQ / dK inside the flash backward
+                    o = T.qkv_proj_rope_attention(x._t, w, c128, s128, nh, nkv, s)
+                else:
+                    qkv = T._QKVRopeLinearFn.apply(x._t, w, c128, s128, nh + nkv, s).view(b, s, nh + 2 * nkv, d)
+                    o = T.qkv_attention(qkv, nh, nkv, causal=True)
                 return self.o_proj(_wrap(o.reshape(b, s, nh * d)))
         if self.config.fuse_attention_qkv:
             # one autograd node: strided q/k/v views -> RoPE -> flash attention; backward fills one dQKV

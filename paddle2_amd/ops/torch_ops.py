@@ -1013,8 +1013,10 @@ def dq_atomic():
     return True if e is None else int(e) != 0
 
 
-def _flash_bwd_native(q, k, v, out, do, lse, dq, dk, dv, scale, causal):
-    """dq/dk/dv may be token-strided views (e.g. slices of a dQKV buffer)."""
+def _flash_bwd_native(q, k, v, out, do, lse, dq, dk, dv, scale, causal, rope=None):
+    """dq/dk/dv may be token-strided views (e.g. slices of a dQKV buffer).  ``rope`` = (cos, sin) fp32 [>= S, 128]
+    tables: q / k were rotate-half RoPE'd by their producer, and dq / dk come out as the gradients of the
+    PRE-rotation q / k (RoPE^T folded into the dK epilogue and the dQ reduce; dense, D = 128)."""
     B, Sq, Hq, D = q.shape
     Sk, Hk = k.shape[1], k.shape[2]
     bnk = _bwd_block(D)
@@ -1023,6 +1025,11 @@ def _flash_bwd_native(q, k, v, out, do, lse, dq, dk, dv, scale, causal):
     slabs = 1 if dq_atomic() else nkb
     dq32 = torch.empty(slabs * B * Sq * Hq * D, dtype=torch.float32, device=q.device)
     delta = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
+    if rope is not None:
+        cos, sin = rope
+        assert D == 128 and cos.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous() and \
+            cos.shape[-1] == 128 and cos.shape[0] >= max(Sq, Sk), "RoPE^T fold: fp32 [S, 128] tables, D = 128"
+        N.native().flash_bwd_set_rope(cos.data_ptr(), sin.data_ptr())
     N.native().flash_bwd(_ATTN_DT[q.dtype], q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), do.data_ptr(), lse.data_ptr(),
                          delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dq32.data_ptr(), B, Sq, Sk,
                          Hq, Hk, D, q.stride(1), k.stride(1), v.stride(1), do.stride(1), dq.stride(1), dk.stride(1),
@@ -1453,12 +1460,74 @@ class _QKVRopeAttnFn(torch.autograd.Function):
         nh, nkv, causal, scale = ctx.meta
         v = qkv[:, :, nh + nkv:]
         dqkv = torch.empty_like(qkv)
+        if pos is None and q.shape[-1] == 128 and _ROPE_BWD_IN_FLASH:
+            # RoPE^T inside the flash backward: dQ / dK land in dQKV already un-rotated (no RoPE passes)
+            _flash_bwd_native(q, k, v, out, dout.contiguous(), lse, dqkv[:, :, :nh], dqkv[:, :, nh:nh + nkv],
+                              dqkv[:, :, nh + nkv:], scale, causal, rope=(cos, sin))
+            return dqkv, None, None, None, None, None, None, None
         dq = torch.empty_like(q)
         dk = torch.empty_like(k)
         _flash_bwd_native(q, k, v, out, dout.contiguous(), lse, dq, dk, dqkv[:, :, nh + nkv:], scale, causal)
         _rope_apply(dq, cos, sin, pos, 0, False, True, out=dqkv[:, :, :nh])
         _rope_apply(dk, cos, sin, pos, 0, False, True, out=dqkv[:, :, nh:nh + nkv])
         return dqkv, None, None, None, None, None, None, None
+
+
+# PADDLE2_AMD_ROPE_BWD_IN_FLASH=0: RoPE^T as separate passes after the flash backward (A/B switch)
+_ROPE_BWD_IN_FLASH = _os.environ.get("PADDLE2_AMD_ROPE_BWD_IN_FLASH", "1") != "0"
+
+
+class _QKVProjRopeAttnFn(torch.autograd.Function):
+    """x -> qkv = RoPE_{q,k}(x @ W) -> causal flash attention as ONE autograd node (Llama's fused QKV path).
+
+    Forward: the rotation runs in the QKV GEMM epilogue (gemm7.hip kEpiRope) and the attention reads the rotated
+    qkv in place.  Backward: the flash backward writes dV and the gradients of the PRE-rotation q / k straight into
+    one dQKV buffer (RoPE^T folded into its dK epilogue and dQ reduce), which feeds the projection's dgrad / wgrad
+    directly — no RoPE kernel and no rotated copies in either direction."""
+
+    @staticmethod
+    def forward(ctx, x, w, cos, sin, nh, nkv, seq, scale):
+        from . import gemm as G
+
+        K = w.shape[0]
+        x2 = x.reshape(-1, K)
+        y = G.mm_fwd_rope(x2, w, cos, sin, (nh + nkv) * 128, seq)
+        if y is None:
+            y = G.mm_fwd(x2, w)
+            y4 = y.view(-1, seq, w.shape[1] // 128, 128)
+            y4[:, :, :nh + nkv].copy_(_rope_apply(y4[:, :, :nh + nkv], cos, sin, None, 0, False, False))
+        qkv = y.view(-1, seq, nh + 2 * nkv, 128)
+        out, lse = _flash_fwd_native(qkv[:, :, :nh], qkv[:, :, nh:nh + nkv], qkv[:, :, nh + nkv:], True, scale)
+        ctx.save_for_backward(x2, w, cos, sin, qkv, out, lse)
+        ctx.meta = (x.shape, nh, nkv, scale)
+        ctx.gt = getattr(w, "_p2_gt", None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from . import gemm as G
+
+        x2, w, cos, sin, qkv, out, lse = ctx.saved_tensors
+        xshape, nh, nkv, scale = ctx.meta
+        dqkv = torch.empty_like(qkv)
+        _flash_bwd_native(qkv[:, :, :nh], qkv[:, :, nh:nh + nkv], qkv[:, :, nh + nkv:], out, dout.contiguous(), lse,
+                          dqkv[:, :, :nh], dqkv[:, :, nh:nh + nkv], dqkv[:, :, nh + nkv:], scale, True,
+                          rope=(cos, sin))
+        d2 = dqkv.view(-1, w.shape[1])
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = G.mm_dgrad(d2, w).view(xshape)
+        if ctx.needs_input_grad[1]:
+            dw = weight_grad(x2, d2, ctx.gt)
+        return dx, dw, None, None, None, None, None, None
+
+
+def qkv_proj_rope_attention(x, w, cos, sin, nh, nkv, seq, scale=None):
+    """Fused QKV projection + RoPE + causal attention (see _QKVProjRopeAttnFn); x [B, S, K] -> [B, S, nh, 128].
+    Callers check qkv_rope_linear_ok first; cos / sin are fp32 [seq, 128]."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(128)
+    return _QKVProjRopeAttnFn.apply(x, w, cos, sin, nh, nkv, seq, float(scale))
 
 
 class _QKVRopeLinearFn(torch.autograd.Function):

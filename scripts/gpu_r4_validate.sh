@@ -8,6 +8,8 @@ timeout -k 10 300 python3 -u -m pytest tests/test_fp8_gemm_gpu.py tests/test_fp8
 rc=$?; echo "fp8 tests rc=$rc"; tail -4 $O/fp8_tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python3 -u -m pytest tests/test_conv1x1_gpu.py tests/test_conv3x3_gpu.py -x -q --timeout 120 --timeout-method thread > $O/conv_tests.log 2>&1
 rc=$?; echo "conv tests rc=$rc"; tail -4 $O/conv_tests.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python3 -u -m pytest tests/test_rope_fold_gpu.py tests/test_flash_gpu.py -x -q --timeout 120 --timeout-method thread > $O/flash_tests.log 2>&1
+rc=$?; echo "flash tests rc=$rc"; tail -4 $O/flash_tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python3 -u -m pytest tests/test_decode_gemm_gpu.py -x -q --timeout 120 --timeout-method thread > $O/dec_tests.log 2>&1
 rc=$?; echo "decode gemm tests rc=$rc"; tail -4 $O/dec_tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python3 -u -m pytest tests/test_gemm_gpu.py -x -q --timeout 300 --timeout-method thread > $O/gemm_tests.log 2>&1
