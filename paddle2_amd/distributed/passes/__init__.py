@@ -1,7 +1,7 @@
 """Distributed program passes (reference: python/paddle/distributed/passes/): pipeline scheduler passes
 (FThenB / 1F1B / Eager1F1B / VPP / ZBH1) producing job plans for static programs."""
-from .pipeline_scheduler_pass import (BACKWARD, FORWARD, OPT, Job, Plan, PlanExecutor, apply_pass,  # noqa: F401
-                                      create_job_list, split_program)
+from .pipeline_scheduler_pass import (BACKWARD, FORWARD, OPT, Job, Plan, PlanExecutor, StagePlanExecutor,  # noqa: F401
+                                      apply_pass, create_job_list, split_program)
 
 
 def new_pass(name, attrs=None):

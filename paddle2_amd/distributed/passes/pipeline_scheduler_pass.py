@@ -267,3 +267,176 @@ class PlanExecutor:
                 if tdist.get_backend() == "gloo":
                     g.div_(tdist.get_world_size())
 
+
+
+# ------------------------------------------------------------------------------------------ stage execution
+def _op_stage(op):
+    """-> pipeline stage of a recorded op from its ``op_device`` ("gpu:<k>"), "all" for "gpu:all", None when
+    unannotated."""
+    d = op.attrs.get("op_device") if op.attrs else None
+    if not d or ":" not in d:
+        return None
+    tail = d.split(":")[-1]
+    return "all" if tail == "all" else int(tail)
+
+
+class StagePlanExecutor:
+    """Runs a Plan on ONE stage of a pipeline group: the multi-rank form of ``PlanExecutor`` (reference: the
+    pipeline passes give each pp rank the ops of its stage plus send_v2 / recv_v2 at the stage boundaries, and the
+    StandaloneExecutor runs that rank's job list; python/paddle/distributed/passes/pipeline_scheduler_pass/
+    pipeline_pass_base.py, pass_utils.py ``_split_program_into_forward_backward_optimize``).
+
+    The forward program's ops are assigned to stages by their ``paddle.static.device_guard("gpu:<k>")`` annotation
+    (unannotated ops stay on the stage of the op before them; "gpu:all" ops run on every stage).  A value produced
+    on stage p and read on stage q crosses p -> q directly (xGMI links every GPU pair) with a shape header, so
+    micro-batches of any size need no shape patching.  Per job of this stage's list:
+
+    * forward(i): receive the micro-batch's boundary inputs (as leaves that require grad), replay this stage's ops
+      with autograd on, send the boundary outputs (isend, drained at the end of the step);
+    * backward(i): on the loss stage back-propagate loss_i / num_micro_batches, elsewhere receive the gradients of
+      the sent outputs (summed over consumers) and back-propagate them; then send the received inputs' gradients
+      back to their producers — parameter gradients accumulate in ``.grad`` over the micro-batches;
+    * optimizer: average the accumulated gradients over ``dp_group`` (if any) and step — parameters of other
+      stages have no gradient and are skipped by the optimizer.
+
+    Receives block in job order and sends are asynchronous; every schedule of ``create_job_list`` orders each
+    stage's jobs so that a receive only waits on jobs its peer has already issued, hence no deadlock.
+    """
+
+    def __init__(self, program, plan, pp_ranks=None, executor=None, dp_group=None):
+        import torch.distributed as tdist
+
+        from ...static import Executor
+        from ...static.graph import Program
+        from ..fleet.utils.hybrid_parallel_inference import _Comm, _in_vids
+
+        self._exe = executor or Executor()
+        self._dp_group = dp_group
+        rank = tdist.get_rank() if tdist.is_initialized() else 0
+        self.pp_ranks = list(pp_ranks) if pp_ranks is not None else list(
+            range(tdist.get_world_size() if tdist.is_initialized() else 1))
+        if rank not in self.pp_ranks:
+            raise ValueError(f"rank {rank} is not in the pipeline group {self.pp_ranks}")
+        self.stage = self.pp_ranks.index(rank)
+        self.program, self.plan = program, plan
+        fwd = plan.program(FORWARD)
+        stages, cur = [], 0
+        for op in fwd.ops:
+            s = _op_stage(op)
+            if s is None:
+                s = cur
+            elif s != "all":
+                if s >= len(self.pp_ranks):
+                    raise ValueError(f"op placed on stage {s} but the pipeline has {len(self.pp_ranks)} stages")
+                cur = s
+            stages.append(s)
+        producer, pidx, consumers = {}, {}, {}
+        for i, (op, s) in enumerate(zip(fwd.ops, stages)):
+            for v in _in_vids(op):
+                consumers.setdefault(v, set()).update(range(len(self.pp_ranks)) if s == "all" else {s})
+            for v in op.outs:
+                if v is not None:
+                    producer[v], pidx[v] = s, i
+        me = self.stage
+        local = Program()
+        local.feeds, local.vars = fwd.feeds, fwd.vars
+        local.ops = [op for op, s in zip(fwd.ops, stages) if s == me or s == "all"]
+        self._local = local
+        reads = {v for op in local.ops for v in _in_vids(op)}
+        # boundary values in producer-op order on both sides of every pair (the message order of a channel)
+        self._recv = sorted(((v, producer[v]) for v in reads if producer.get(v) not in (None, me, "all")),
+                            key=lambda e: pidx[e[0]])
+        self._send = sorted(((v, sorted(consumers.get(v, set()) - {me})) for v, s in producer.items()
+                             if s == me and consumers.get(v, set()) - {me}), key=lambda e: pidx[e[0]])
+        bwd = plan.program(BACKWARD)
+        self._loss = next((op.attrs["loss"] for op in bwd.ops if op.kind == "backward"), None)
+        self._loss_local = self._loss is not None and producer.get(self._loss) in (me, "all")
+        self._comm = _Comm(None)
+        self._optimizers = [op.attrs["optimizer"] for op in plan.program(OPT).ops]
+
+    def _dtype(self, vid):
+        v = self.program.vars.get(vid)
+        return v.dtype if isinstance(v, torch.Tensor) else torch.float32
+
+    def run(self, micro_feeds, fetch_list=()):
+        """-> per micro-batch list of the fetch values this stage holds (None for values of other stages)."""
+        from ...static.executor import _feed_tensor
+
+        exe, m = self._exe, len(micro_feeds)
+        dev = exe._device
+        fetch_ids = [exe._fetch_id(self.program, f) for f in fetch_list]
+        envs, recvd, fetched = [None] * m, [None] * m, [None] * m
+        rank_of = self.pp_ranks.__getitem__
+        for job in self.plan.job_list():
+            t, i = _base_type(job.type()), job.micro_batch_id()
+            if t == FORWARD:
+                env, got = {}, {}
+                for name, v in micro_feeds[i].items():
+                    sym = self.program.feeds[name]
+                    env[sym._vid] = _feed_tensor(v, sym, dev)
+                for vid, src in self._recv:
+                    x = self._comm.recv(rank_of(src), self._dtype(vid), dev)
+                    if x.is_floating_point():
+                        x.requires_grad_(True)
+                    env[vid] = got[vid] = x
+                with torch.enable_grad():
+                    envs[i] = exe._replay(self._local, env, grad=True)
+                recvd[i] = got
+                for vid, dsts in self._send:
+                    for q in dsts:
+                        self._comm.send(envs[i][vid].detach(), rank_of(q))
+                fetched[i] = [envs[i].get(f) for f in fetch_ids]
+            elif t == BACKWARD:
+                if job.type().startswith(BACKWARD + "_w"):
+                    continue   # weight-grad half: autograd produces it together with the input gradient
+                env = envs[i]
+                outs, grads = [], []
+                if self._loss_local:
+                    outs.append(env[self._loss] / m)
+                    grads.append(None)
+                for vid, dsts in self._send:
+                    gsum = None
+                    for q in dsts:
+                        if not self._dtype(vid).is_floating_point:
+                            continue
+                        g = self._comm.recv(rank_of(q), self._dtype(vid), dev)
+                        gsum = g if gsum is None else gsum + g
+                    x = env[vid]
+                    if gsum is not None and isinstance(x, torch.Tensor) and x.requires_grad:
+                        outs.append(x)
+                        grads.append(gsum)
+                if outs:
+                    torch.autograd.backward(outs, [g if g is not None else torch.ones_like(o)
+                                                   for o, g in zip(outs, grads)])
+                for vid, src in self._recv:
+                    x = recvd[i][vid]
+                    if not x.is_floating_point():
+                        continue
+                    g = x.grad if x.grad is not None else torch.zeros_like(x)
+                    self._comm.send(g, rank_of(src))
+                envs[i] = {k: v for k, v in env.items() if k in fetch_ids}   # free the activations
+                recvd[i] = None
+            elif t == OPT:
+                self._comm.drain()
+                self._average_grads()
+                with torch.no_grad():
+                    for opt in self._optimizers:
+                        opt.step()
+                        opt.clear_grad(set_to_zero=False)
+        self._comm.drain()
+        return fetched
+
+    def _average_grads(self):
+        import torch.distributed as tdist
+
+        if self._dp_group is None or not tdist.is_initialized():
+            return
+        n = tdist.get_world_size(self._dp_group)
+        if n == 1:
+            return
+        for opt in self._optimizers:
+            for p in opt._parameter_list:
+                g = p._t.grad
+                if g is not None:
+                    tdist.all_reduce(g, group=self._dp_group)
+                    g.div_(n)

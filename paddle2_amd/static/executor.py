@@ -238,6 +238,11 @@ class Executor:
             return [o.detach().cpu().numpy() if return_numpy else Tensor._wrap(o) for o in outs]
         if not isinstance(program, Program):
             raise TypeError("Executor.run expects a static Program")
+        if getattr(program, "_pipeline_opt", None):
+            # minimized by incubate.optimizer.PipelineOptimizer: this rank's pipeline stage over micro-batches
+            from ..incubate.optimizer import _run_pipeline
+
+            return _run_pipeline(self, program, feed, fetch_list, return_numpy)
         feed = feed or {}
         fetch_list = fetch_list or []
         if not program.ops and not fetch_list:
