@@ -76,34 +76,66 @@ __device__ __forceinline__ void epilogue_v7_swi_x4(const Params& p, f32x4v (&acc
   }
 }
 
-// RoPE epilogue (kEpiRope): the wave's 128 columns are one head when they lie below rope_cols, and its two 64-column
-// halves h = 0 / 1 hold head dims d and d + 64 at the same lane position — every rotate-half pair is in one lane, so
-// the rotation runs on the fp32 accumulators (x1 cos - x2 sin, x2 cos + x1 sin; cos / sin[d + 64] = [d] for the
-// rotate-half tables) before the usual bf16 stores.
-__device__ __forceinline__ void rope_rotate(const Params& p, f32x4v (&acc)[2][8][4], int tm, int tn, int arow,
-                                            int bcolw, int lane) {
-  if (tn * BN + bcolw >= p.rope_cols) return;
-  const int g = lane >> 4;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int r = tm * BM + arow + 16 * i + (lane & 15);
-    const int pos = (r < p.M ? r : 0) % p.rope_seq;
-    const float* cr = p.rope_cos + (long)pos * 128;
-    const float* sr = p.rope_sin + (long)pos * 128;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int d = 16 * j + 4 * g;
-      const float4 c = *(const float4*)(cr + d);
-      const float4 sn = *(const float4*)(sr + d);
-      const float cv[4] = {c.x, c.y, c.z, c.w}, sv[4] = {sn.x, sn.y, sn.z, sn.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float x1 = acc[0][i][j][e], x2 = acc[1][i][j][e];
-        acc[0][i][j][e] = x1 * cv[e] - x2 * sv[e];
-        acc[1][i][j][e] = x2 * cv[e] + x1 * sv[e];
-      }
-    }
-  }
+// RoPE epilogue (kEpiRope, whole 256 x 256 tiles): the wave's 128 columns are one head when they lie below
+// rope_cols, and its two 64-column halves h = 0 / 1 hold head dims d and d + 64 at the same lane position, so every
+// rotate-half pair is in one lane: out_0 = x_0 cos - x_1 sin, out_1 = x_1 cos + x_0 sin on the fp32 accumulators
+// (cos / sin[d + 64] = [d] for rotate-half tables), fused into the 16-B-store epilogue.  Each half's pass reads
+// its partner half's accumulators in place — the pass structure of the plain epilogue; rotating the accumulator
+// set first (or both halves per group) kept hundreds of extra values alive next to the next tile's prefetched
+// fragments and spilled 468-780 B/lane to scratch, this form leaves ~100 B/lane outside the MFMA loop.
+template <bool NT>
+__device__ __forceinline__ void epilogue_v7_rope_x4(const Params& p, f32x4v (&acc)[2][8][4], int tm, int tn,
+                                                    int arow, int bcolw, int lane) {
+  unsigned short* C = (unsigned short*)p.C;
+  const int sub = (lane >> 4) & 1;
+  const int r = lane & 15;
+  const int ch = 8 * (lane >> 5);
+  const long row_base = (long)tm * BM + arow + r;
+  const float sgn_lo = tn * BN + bcolw < p.rope_cols ? 1.f : 0.f;   // 0: v heads, stored unrotated
+  // token position of row block i: one 32-bit remainder, then p0 + 16 i with one conditional wrap (the host
+  // requires rope_seq >= 128 > 16 * 7)
+  const unsigned seq = (unsigned)p.rope_seq;
+  const unsigned p0 = (unsigned)row_base % seq;
+  auto pos = [&](int i) -> long {
+    const unsigned t = p0 + 16u * i;
+    return (long)(t >= seq ? t - seq : t);
+  };
+  // the same pass structure as the plain 16-B epilogue (half h outer): out_h = x_h cos + (h ? x_0 : -x_1) sin,
+  // reading the partner half's accumulators in place; tables are L1 hits on the second half's pass
+  sfor<2>([&](auto H) {
+    constexpr int h = decltype(H)::value;
+    sfor<4>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      const int d = 16 * j + 4 * (lane >> 4);
+      sfor<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const f32x4v& a = acc[h][2 * q][j];
+        const f32x4v& b = acc[h][2 * q + 1][j];
+        const f32x4v& pa = acc[1 - h][2 * q][j];
+        const f32x4v& pb = acc[1 - h][2 * q + 1][j];
+        const float4 ca = *(const float4*)(p.rope_cos + pos(2 * q) * 128 + d);
+        const float4 sa = *(const float4*)(p.rope_sin + pos(2 * q) * 128 + d);
+        const float4 cb = *(const float4*)(p.rope_cos + pos(2 * q + 1) * 128 + d);
+        const float4 sb = *(const float4*)(p.rope_sin + pos(2 * q + 1) * 128 + d);
+        const float sg = (h ? 1.f : -1.f) * sgn_lo;
+        // rotated (or, for v heads, cos = 1 / sin = 0 equivalent) values of this half
+        const float c0 = sgn_lo ? ca.x : 1.f, c1 = sgn_lo ? ca.y : 1.f, c2 = sgn_lo ? ca.z : 1.f,
+                    c3 = sgn_lo ? ca.w : 1.f;
+        const float d0 = sgn_lo ? cb.x : 1.f, d1 = sgn_lo ? cb.y : 1.f, d2 = sgn_lo ? cb.z : 1.f,
+                    d3 = sgn_lo ? cb.w : 1.f;
+        const float x0 = a[0] * c0 + sg * pa[0] * sa.x, x1 = a[1] * c1 + sg * pa[1] * sa.y;
+        const float x2 = a[2] * c2 + sg * pa[2] * sa.z, x3 = a[3] * c3 + sg * pa[3] * sa.w;
+        const float y0 = b[0] * d0 + sg * pb[0] * sb.x, y1 = b[1] * d1 + sg * pb[1] * sb.y;
+        const float y2 = b[2] * d2 + sg * pb[2] * sb.z, y3 = b[3] * d3 + sg * pb[3] * sb.w;
+        unsigned u0 = pack_bf2(x0, x1), u1 = pack_bf2(x2, x3);
+        unsigned w0 = pack_bf2(y0, y1), w1 = pack_bf2(y2, y3);
+        auto s0 = __builtin_amdgcn_permlane16_swap(u0, w0, false, false);
+        auto s1 = __builtin_amdgcn_permlane16_swap(u1, w1, false, false);
+        const long row = row_base + 16 * (2 * q + sub);
+        st16<NT>(C + row * p.ldc + tn * BN + bcolw + 64 * h + 16 * j + ch, s0[0], s1[0], s0[1], s1[1]);
+      });
+    });
+  });
 }
 
 template <int EPI, int SCHED>
@@ -190,9 +222,11 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
     return i32x4{(int)(unsigned)b, (int)(unsigned)(b >> 32), live ? (int)(end - (unsigned)b) : 0, 0x00020000};
   };
   // SCHED bit 11, implicit-GEMM convolution over a zero-bordered NHWC input (ops/conv_gemm.py): K = taps x C, and
-  // K-tile kt of tap t = kt >> cv_kpb_log2 reads the A rows shifted by sign * ((kh - pad_h) * pitch + kw - pad_w)
-  // pixels — only the descriptor base moves, per lane nothing changes (taps past cv_taps read the centre rows and
-  // meet zero weight columns).
+  // K-tile kt of tap t = kt >> cv_kpb_log2 reads the A rows shifted by the tap's host-computed byte offset
+  // cv_off[t] — only the descriptor base moves, per lane nothing changes (taps past cv_taps read the centre rows
+  // and meet zero weight columns).  The offset is picked by a select chain over the kernarg table: scalar ops only
+  // (an indexed kernarg array would be copied to scratch; an in-kernel tap / kw division put VALU + a branch into
+  // the descriptor code, and that build lost K-tile 1's contribution on gfx950)
   auto desc_a = [&](int kk) {
     if constexpr (!CONV) {
       return desc(kk, ca, na, a_end);
@@ -200,16 +234,10 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
       const bool nx = kk >= nt;
       const int kt = nx ? kk - nt : kk;
       const int tap = kt >> p.cv_kpb_log2;
-      const int kc = kt & ((1 << p.cv_kpb_log2) - 1);
-      int rows = 0;
-      if (tap < p.cv_taps) {
-        const int kh = tap / p.cv_kw, kw = tap - kh * p.cv_kw;
-        rows = p.cv_sign * ((kh - p.cv_pad_h) * p.cv_pitch + (kw - p.cv_pad_w));
-      }
-      // channel offset as a 32-bit add (a 64-bit (long)kc << 7 was lowered to an s_lshl_b64 whose high source
-      // register still held a partial product of the row offset: K-tile 1 read the wrong rows on gfx950)
-      const long roff = (long)rows * (p.lda * 2);
-      const unsigned coff = (unsigned)kc << 7;
+      const unsigned coff = (unsigned)(kt & ((1 << p.cv_kpb_log2) - 1)) << 7;
+      long roff = 0;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) roff = tap == t ? p.cv_off[t] : roff;
       const u64 b = (nx ? na : ca) + (u64)roff + (u64)coff;
       const bool live = !nx || nlive;
       return i32x4{(int)(unsigned)b, (int)(unsigned)(b >> 32), live ? (int)(a_end - (unsigned)b) : 0, 0x00020000};
@@ -433,23 +461,32 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
     }
     // tile done: accumulators out while the next tile's first K-tiles stream / sit in LDS
     asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
-    if constexpr (EPI == kEpiRope) rope_rotate(p, acc, ctm, ctn, arow, bcolw, lane);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if constexpr (X4 && (EPI == kEpiBF16 || EPI == kEpiRope)) {
-        // interior tile, 16-B aligned rows: the widened stores; otherwise the element-checked epilogue
-        if ((ctm + 1) * BM <= p.M && (ctn + 1) * BN <= p.N && (p.ldc & 7) == 0 && ((size_t)p.C & 15) == 0)
-          epilogue_v7_x4<NTS>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
-        else
-          epilogue_t<kEpiBF16>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
-      } else if constexpr (X4 && EPI == kEpiSwiGLU) {
-        if ((ctm + 1) * BM <= p.M && (ctn + 1) * 128 <= p.H && (p.ldc & 7) == 0 && (p.ldc2 & 7) == 0 &&
-            (p.H & 7) == 0 && ((size_t)p.C & 15) == 0 && ((size_t)p.C2 & 15) == 0)
-          epilogue_v7_swi_x4<NTS>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
-        else
-          epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
-      } else {
+    if constexpr (EPI == kEpiRope) epilogue_v7_rope_x4<NTS>(p, acc, ctm, ctn, arow, bcolw, lane);   // whole tiles
+    if constexpr (EPI == kEpiGeLU || EPI == kEpiDGeLU) {
+      // compile-time halves (sfor): with a runtime h — the unroller gives up on the large GELU / dGELU bodies —
+      // acc[h] was indexed dynamically and all 256 accumulators were demoted to scratch (1040 B/lane)
+      sfor<2>([&](auto H) {
+        constexpr int h = decltype(H)::value;
         epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+      });
+    } else if constexpr (EPI != kEpiRope) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if constexpr (X4 && EPI == kEpiBF16) {
+          // interior tile, 16-B aligned rows: the widened stores; otherwise the element-checked epilogue
+          if ((ctm + 1) * BM <= p.M && (ctn + 1) * BN <= p.N && (p.ldc & 7) == 0 && ((size_t)p.C & 15) == 0)
+            epilogue_v7_x4<NTS>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+          else
+            epilogue_t<kEpiBF16>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+        } else if constexpr (X4 && EPI == kEpiSwiGLU) {
+          if ((ctm + 1) * BM <= p.M && (ctn + 1) * 128 <= p.H && (p.ldc & 7) == 0 && (p.ldc2 & 7) == 0 &&
+              (p.H & 7) == 0 && ((size_t)p.C & 15) == 0 && ((size_t)p.C2 & 15) == 0)
+            epilogue_v7_swi_x4<NTS>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+          else
+            epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+        } else {
+          epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+        }
       }
     }
     if (u + 1 < ntile) {
@@ -495,7 +532,10 @@ bool pd_gemm_v7(const pd::gm::Params& p, int layout, int epi, int sched, int cus
     return true;
   }
   if (epi == kEpiRope) {   // RoPE epilogue: the spread schedule only, bias-free
-    if (sched != 384 || p.bias || !p.rope_cos || !p.rope_sin || p.rope_seq <= 0 || p.rope_cols % 128) return false;
+    // whole tiles only (M, N multiples of 256, 16-B rows): the kernel carries just the streaming 16-B-store form
+    if (sched != 384 || p.bias || !p.rope_cos || !p.rope_sin || p.rope_seq < 128 || p.rope_cols % 128 ||
+        p.M % BM || p.N % BN || (p.ldc & 7) || ((size_t)p.C & 15))
+      return false;
     gemm_v7_kernel<kEpiRope, 384><<<grid, NTHR4, 0, st>>>(p);
     return true;
   }
@@ -538,6 +578,7 @@ extern "C" int pd_gemm_conv(const void* A, long lda, const void* a_lo, const voi
   using namespace pd::gm;
   if (M <= 0 || N <= 0 || K % 128 || lda % 8 || ldb % 8 || ldc % 4 || (size_t)C % 16) return -1;
   if ((64L << kpb_log2) != lda) return -1;   // one tap = one row of channels = 2^kpb_log2 K-tiles
+  if (taps < 1 || taps > 16 || kw < 1) return -1;
   // every tap's shifted rows must stay inside [a_lo, a_hi)
   long lo_rows = 0, hi_rows = 0;
   for (int t = 0; t < taps; ++t) {
@@ -565,8 +606,11 @@ extern "C" int pd_gemm_conv(const void* A, long lda, const void* a_lo, const voi
   p.a_end = a_hi;
   p.b_end = (const char*)B + b_bytes;
   p.sa = p.sb = nullptr;
-  p.cv_kpb_log2 = kpb_log2; p.cv_kw = kw; p.cv_taps = taps; p.cv_pitch = pitch; p.cv_pad_h = pad_h;
-  p.cv_pad_w = pad_w; p.cv_sign = sign;
+  p.cv_kpb_log2 = kpb_log2; p.cv_taps = taps;
+  for (int t = 0; t < 16; ++t) {
+    const int kh = t / kw, kx = t - kh * kw;
+    p.cv_off[t] = t < taps ? (long)sign * ((long)(kh - pad_h) * pitch + (kx - pad_w)) * lda * 2 : 0;
+  }
   p.tiles_m = (M + BM - 1) / BM;
   p.tiles_n = (N + BN - 1) / BN;
   p.group_m = group_m > 0 ? group_m : 4;

@@ -65,7 +65,8 @@ struct Params {
   const float* sb;
   // implicit-GEMM convolution (gemm7.hip SCHED bit 11): K-tiles per tap (log2), taps, kernel width, padded row pitch,
   // padding and the shift's sign (+1 forward, -1 input gradient)
-  int cv_kpb_log2, cv_taps, cv_kw, cv_pitch, cv_pad_h, cv_pad_w, cv_sign;
+  int cv_kpb_log2, cv_taps;
+  long cv_off[16];   // implicit-GEMM conv: byte offset of tap t's A rows (host-computed)
   // RoPE epilogue (kEpiRope)
   const float* rope_cos;
   const float* rope_sin;

@@ -198,7 +198,8 @@ def mm_fwd_rope(x2, w, cos, sin, rope_cols, seq):
     None when the spread TN schedule is not the one selected (the caller then runs GEMM + RoPE)."""
     M, K = x2.shape
     Nn = w.shape[1]
-    if _variant("rope") != V7_SPREAD or K % 128 or rope_cols % 128 or Nn % 8:
+    # whole 256 x 256 tiles and seq >= 128 (the kernel's fused epilogue carries no edge-tile form)
+    if _variant("rope") != V7_SPREAD or K % 128 or rope_cols % 128 or Nn % 256 or M % 256 or seq < 128:
         return None
     assert cos.dtype == sin.dtype == torch.float32 and cos.shape == sin.shape == (seq, 128)
     out = torch.empty(M, Nn, dtype=x2.dtype, device=x2.device)

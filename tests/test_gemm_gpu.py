@@ -260,7 +260,7 @@ def test_tail_splitk_wgrad_and_fwd(M, N, K, beta, monkeypatch):
     assert _rel(G.mm_fwd(a, w, bias=b)[rows], a[rows].float() @ w.float() + b.float()) < 8e-3
 
 
-@pytest.mark.parametrize("B,S,nq,nkv", [(2, 256, 4, 2), (1, 512, 8, 8)])
+@pytest.mark.parametrize("B,S,nq,nkv", [(2, 256, 4, 2), (1, 512, 8, 8), (1, 200, 2, 1)])
 def test_qkv_rope_linear_node(B, S, nq, nkv):
     """The QKV projection with RoPE in the GEMM epilogue (torch_ops._QKVRopeLinearFn): rotated q / k heads and the
     unrotated v vs the fp32 GEMM + rotate-half reference, and the input / weight gradients through RoPE^T."""
