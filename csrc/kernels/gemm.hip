@@ -541,8 +541,17 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v4_kernel(Params p) {
       return;
     }
   }
+  if constexpr (EPI == kEpiGeLU || EPI == kEpiDGeLU) {
+    // compile-time halves: a runtime h (the unroller gives up on the GELU bodies) indexed acc[h]
+    // dynamically, which demoted every accumulator to scratch -- inside the MFMA loop
+    sfor<2>([&](auto H) {
+      constexpr int h = decltype(H)::value;
+      epilogue_t<EPI>(p, acc[h], tm, tn, arow, bcolw + 64 * h, lane);
+    });
+  } else {
 #pragma unroll
-  for (int h = 0; h < 2; ++h) epilogue_t<EPI>(p, acc[h], tm, tn, arow, bcolw + 64 * h, lane);
+    for (int h = 0; h < 2; ++h) epilogue_t<EPI>(p, acc[h], tm, tn, arow, bcolw + 64 * h, lane);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -725,8 +734,17 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v6_kernel(Params p) {
     }
     // tile done: its accumulators out (the next tile's first K-tiles are already streaming / being read)
     asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+    if constexpr (EPI == kEpiGeLU || EPI == kEpiDGeLU) {
+      // compile-time halves: a runtime h (the unroller gives up on the GELU bodies) indexed acc[h]
+      // dynamically, which demoted every accumulator to scratch -- inside the MFMA loop
+      sfor<2>([&](auto H) {
+        constexpr int h = decltype(H)::value;
+        epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+      });
+    } else {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+      for (int h = 0; h < 2; ++h) epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
