@@ -23,6 +23,7 @@ def softmax_mask_fuse_upper_triangle(x, name=None):
 def __getattr__(name):
     import importlib
 
-    if name in ("distributed", "autograd", "optimizer", "asp", "tensor", "fp8", "autotune"):
+    if name in ("distributed", "autograd", "optimizer", "asp", "tensor", "fp8", "autotune", "jit", "layers",
+                "operators", "multiprocessing", "checkpoint", "framework"):
         return importlib.import_module(f".{name}", __name__)
     raise AttributeError(name)

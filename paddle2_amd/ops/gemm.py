@@ -40,7 +40,7 @@ _GROUP_FORCED = "PADDLE2_AMD_GEMM_GROUP_M" in os.environ
 V7_SPREAD = 64 + 384
 _FORCE = os.environ.get("PADDLE2_AMD_GEMM_VARIANT")
 VARIANT = int(_FORCE) if _FORCE is not None else None
-PASS_VARIANT = {"fwd": V7_SPREAD, "dgrad": V7_SPREAD, "wgrad": 4, "wgrad_bf16": 4, "swiglu": V7_SPREAD,
+PASS_VARIANT = {"fwd": V7_SPREAD, "dgrad": V7_SPREAD, "wgrad": 5, "wgrad_bf16": 5, "swiglu": V7_SPREAD,
                 "rope": V7_SPREAD}
 # grouped tile order per pass (row tiles that sweep the column tiles together): 4 for the spread TN schedule
 # (forward +2..7 %, dgrad +0..2 % over 8 at M = 32768; profiles/r4_gemm_spread.md), 8 for the wgrad kernels

@@ -65,21 +65,30 @@ def weight_only_matmul(x, w, scale, weight_dtype="int8", group_size=-1, bias=Non
 # counts on the cached [N, K] weights; "blas": hipBLASLt through torch.matmul
 import os as _os  # noqa: E402
 
-DECODE_GEMM = _os.environ.get("PADDLE2_AMD_DECODE_GEMM", "native")
+DECODE_GEMM = _os.environ.get("PADDLE2_AMD_DECODE_GEMM", "auto")   # auto | native | blas
 
 
 def decode_ok(x, wt):
+    """The native stream kernel is taken where it measured faster than hipBLASLt's skinny GEMM
+    (profiles/r4_decode_gemm.md): M <= 16 with N <= 8192 (the o / down projections: 2.6-4.0 vs 1.9-3.4 TB/s);
+    the wide projections and M = 64 stay on the library kernel.  PADDLE2_AMD_DECODE_GEMM=native forces it for
+    every M <= 64."""
     M, K = x.shape
-    return (x.device.type == "cuda" and x.dtype == torch.bfloat16 and wt.dtype == torch.bfloat16 and 1 <= M <= 64
-            and K % 64 == 0 and wt.shape[1] == K and wt.shape[0] % 64 == 0 and wt.is_contiguous()
-            and N.use_native(x))
+    Nn = wt.shape[0]
+    ok = (x.device.type == "cuda" and x.dtype == torch.bfloat16 and wt.dtype == torch.bfloat16 and 1 <= M <= 64
+          and K % 64 == 0 and wt.shape[1] == K and Nn % 64 == 0 and wt.is_contiguous() and N.use_native(x))
+    if not ok:
+        return False
+    if DECODE_GEMM == "blas":
+        return False
+    return DECODE_GEMM == "native" or (M <= 16 and Nn <= 8192)
 
 
 def decode_matmul(x, wt, bias=None):
     """y[M, N] = x[M, K] @ wt[N, K]^T (+ bias) for M <= 64 on the native stream kernel (weights read once, split-K
     over the 256 CUs, fp32 partials summed in a second pass); torch.matmul otherwise."""
     x = x.contiguous()
-    if DECODE_GEMM != "native" or not decode_ok(x, wt):
+    if not decode_ok(x, wt):
         y = torch.matmul(x, wt.t())
         return y if bias is None else y + bias
     M, K = x.shape
