@@ -104,7 +104,7 @@ def test_incubate_layers_and_operators():
     inp = paddle.to_tensor(np.random.RandomState(1).randn(2, 6, 6, 8).astype("float32"))
     out = unit(inp, inp)
     assert out.shape == [2, 6, 6, 8] and float(out.min()) >= 0.0
-    g = paddle.to_tensor(np.random.RandomState(2).rand(1, 8, 4, 8, 8).astype("float32"))
+    g = paddle.to_tensor(np.random.RandomState(2).rand(1, 6, 4, 8, 8).astype("float32"))   # 2 out x 3 in
     img = paddle.to_tensor(np.random.RandomState(3).rand(1, 3, 16, 16).astype("float32"))
     guide = paddle.to_tensor(np.random.RandomState(4).rand(1, 16, 16).astype("float32"))
     assert L.bilateral_slice(img, guide, g, has_offset=False).shape == [1, 2, 16, 16]
