@@ -854,6 +854,7 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   if (!bk && (ldb % 8 || (epi == kEpiSwiGLU ? (2 * H) % 8 : N % 8))) return -2;
   if (epi == kEpiSwiGLU && H % 32) return -3;
   if ((epi == kEpiGeLU || epi == kEpiDGeLU) && (!C2 || ldc2 < N)) return -3;   // the pre-activation operand
+  if (epi == kEpiDSwiGLU && (!C2 || H != N || ldc2 < 2L * N || ldc < 2L * N)) return -3;   // gate | up, 2N wide
   hipStream_t st = (hipStream_t)stream;
   // v7 (gemm7.hip): the TN schedule, variants 7..10 = its SCHED 0..3; problems outside its domain run v6
   if ((variant >= 7 && variant <= 10) || variant >= 64) {
@@ -861,7 +862,7 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
       return (int)hipGetLastError();
     variant = 6;
   }
-  if (epi == kEpiRope) return -3;   // only the spread TN schedule has the RoPE epilogue
+  if (epi == kEpiRope || epi == kEpiDSwiGLU) return -3;   // the spread TN schedule only (RoPE / SwiGLU backward)
   if (epi == kEpiSwiGLU && bk) return -3;  // K-major gate|up weight: v7 only
   // v4+ store 4 consecutive output columns per lane (8-B bf16 / 16-B fp32 accesses): rows must keep that alignment
   if (variant >= 4 && (ldc % 4 || (size_t)C % 16 || (C2 && (ldc2 % 4 || (size_t)C2 % 16)))) variant = 0;

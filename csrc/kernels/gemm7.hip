@@ -462,7 +462,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
     // tile done: accumulators out while the next tile's first K-tiles stream / sit in LDS
     asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
     if constexpr (EPI == kEpiRope) epilogue_v7_rope_x4<NTS>(p, acc, ctm, ctn, arow, bcolw, lane);   // whole tiles
-    if constexpr (EPI == kEpiGeLU || EPI == kEpiDGeLU) {
+    if constexpr (EPI == kEpiGeLU || EPI == kEpiDGeLU || EPI == kEpiDSwiGLU) {
       // compile-time halves (sfor): with a runtime h — the unroller gives up on the large GELU / dGELU bodies —
       // acc[h] was indexed dynamically and all 256 accumulators were demoted to scratch (1040 B/lane)
       sfor<2>([&](auto H) {
@@ -537,6 +537,11 @@ bool pd_gemm_v7(const pd::gm::Params& p, int layout, int epi, int sched, int cus
         p.M % BM || p.N % BN || (p.ldc & 7) || ((size_t)p.C & 15))
       return false;
     gemm_v7_kernel<kEpiRope, 384><<<grid, NTHR4, 0, st>>>(p);
+    return true;
+  }
+  if (epi == kEpiDSwiGLU) {   // SwiGLU backward in the down projection's dgrad: the spread schedule only
+    if (sched != 384 || p.bias || !p.C2 || p.H != p.N) return false;
+    gemm_v7_kernel<kEpiDSwiGLU, 384><<<grid, NTHR4, 0, st>>>(p);
     return true;
   }
   if (epi == kEpiGeLU || epi == kEpiDGeLU) {   // the GELU epilogues: the spread schedule only

@@ -29,7 +29,12 @@ constexpr int kRecords = 0x7fffffff;
 // :580 the gelu_grad backward).  Both: p.H = 1 for the tanh approximation, 0 for erf.
 // kEpiRope (v7 only): bf16 out with rotate-half RoPE applied to the 128-wide heads of columns < rope_cols
 // (position = row % rope_seq; fp32 cos / sin tables [rope_seq, 128]) — the QKV projection's q / k heads.
-enum Epi : int { kEpiBF16 = 0, kEpiF32 = 1, kEpiSwiGLU = 2, kEpiGeLU = 3, kEpiDGeLU = 4, kEpiRope = 5 };
+// kEpiDSwiGLU: the down projection's input gradient d_a = acc is never stored: with gate = C2[r, c], up =
+// C2[r, H + c] (the SwiGLU forward's saved pre-activations) the epilogue writes C[r, c] = d_a * up * silu'(gate)
+// and C[r, H + c] = d_a * silu(gate) — the SwiGLU backward (C may alias C2: every element is read, then written,
+// by the same lane).
+enum Epi : int { kEpiBF16 = 0, kEpiF32 = 1, kEpiSwiGLU = 2, kEpiGeLU = 3, kEpiDGeLU = 4, kEpiRope = 5,
+                 kEpiDSwiGLU = 6 };
 
 struct Params {
   const unsigned short* A;
@@ -455,6 +460,50 @@ __device__ __forceinline__ void epilogue_t(const Params& p, f32x4v (&acc)[8][4],
               gp[e] = g[e];
               gp[p.H + e] = u[e];
               op[e] = o[e];
+            }
+        }
+      }
+    }
+  } else if constexpr (EPI == kEpiDSwiGLU) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = tn * BN + bcolw + 16 * j + cq;   // d_a column = gate column; up at c + H
+      if (c >= p.N) continue;
+      const bool vec = c + 3 < p.N;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = row0 + 16 * i;
+        if (r >= p.M) continue;
+        const unsigned short* gp = p.C2 + (long)r * p.ldc2 + c;
+        unsigned short* dp = (unsigned short*)p.C + (long)r * p.ldc + c;
+        unsigned short g[4], u[4], dg[4], du[4];
+        if (vec) {
+          const uint2 g2 = *(const uint2*)gp, u2 = *(const uint2*)(gp + p.H);
+          g[0] = g2.x & 0xffff; g[1] = g2.x >> 16; g[2] = g2.y & 0xffff; g[3] = g2.y >> 16;
+          u[0] = u2.x & 0xffff; u[1] = u2.x >> 16; u[2] = u2.y & 0xffff; u[3] = u2.y >> 16;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            g[e] = c + e < p.N ? gp[e] : 0;
+            u[e] = c + e < p.N ? gp[p.H + e] : 0;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float gv = bf2f(g[e]), uv = bf2f(u[e]), da = acc[i][j][e];
+          const float sg = 1.f / (1.f + __expf(-gv));
+          dg[e] = f2bf(da * uv * sg * (1.f + gv * (1.f - sg)));
+          du[e] = f2bf(da * gv * sg);
+        }
+        if (vec) {
+          *(uint2*)dp = make_uint2(dg[0] | (unsigned)dg[1] << 16, dg[2] | (unsigned)dg[3] << 16);
+          *(uint2*)(dp + p.H) = make_uint2(du[0] | (unsigned)du[1] << 16, du[2] | (unsigned)du[3] << 16);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (c + e < p.N) {
+              dp[e] = dg[e];
+              dp[p.H + e] = du[e];
             }
         }
       }

@@ -22,7 +22,7 @@ import torch
 from . import _native as N
 
 LAYOUT_AK, LAYOUT_BK = 1, 2
-EPI_BF16, EPI_F32, EPI_SWIGLU, EPI_GELU, EPI_DGELU, EPI_ROPE = 0, 1, 2, 3, 4, 5
+EPI_BF16, EPI_F32, EPI_SWIGLU, EPI_GELU, EPI_DGELU, EPI_ROPE, EPI_DSWIGLU = 0, 1, 2, 3, 4, 5, 6
 GROUP_M = int(os.environ.get("PADDLE2_AMD_GEMM_GROUP_M", "8"))
 _GROUP_FORCED = "PADDLE2_AMD_GEMM_GROUP_M" in os.environ
 # kernel schedule (csrc/kernels/gemm.hip): 0 = v2 (8 waves, 2 per SIMD, 128x64 wave tiles), 4 = v4 (4 waves,
@@ -189,6 +189,21 @@ def mm_dgrad_dgelu(dy2, w, h, approximate=True):
     out = torch.empty(M, K, dtype=dy2.dtype, device=dy2.device)
     _launch(LAYOUT_AK | LAYOUT_BK, EPI_DGELU, dy2, dy2.stride(0), w, w.stride(0), out, out.stride(0), h, h.stride(0),
             None, M, K, Nn, 0.0, int(bool(approximate)), name="dgrad")
+    return out
+
+
+def mm_dgrad_dswiglu(dy2, w, gu, out=None):
+    """d_gu[M, 2H] from the down projection's output gradient: d_a = dy2[M, N] @ w[H, N]^T stays in fp32 in the
+    epilogue, which writes d_gate = d_a * up * silu'(gate) and d_up = d_a * silu(gate) (gu = [gate | up] the SwiGLU
+    forward saved).  ``out`` may be ``gu`` itself (in place).  None unless the spread TN schedule is selected."""
+    M, Nn = dy2.shape
+    H = w.shape[0]
+    if _variant("dgrad") != V7_SPREAD or Nn % 128 or gu.shape != (M, 2 * H) or gu.stride(1) != 1 or H % 8:
+        return None
+    if out is None:
+        out = torch.empty_like(gu)
+    _launch(LAYOUT_AK | LAYOUT_BK, EPI_DSWIGLU, dy2, dy2.stride(0), w, w.stride(0), out, out.stride(0), gu,
+            gu.stride(0), None, M, H, Nn, 0.0, H, name="dgrad")
     return out
 
 

@@ -1583,7 +1583,10 @@ def qkv_rope_linear_ok(x, w, bias, head_dim, pos):
             and _pass_native("fwd", x) and _pass_native("dgrad", x) and _ROPE_IN_GEMM)
 
 
-_ROPE_IN_GEMM = _os.environ.get("PADDLE2_AMD_ROPE_IN_GEMM", "1") != "0"
+# RoPE in the QKV GEMM epilogue: opt-in.  Measured in the Llama-2-7B step (profiles/r4_rope_fusion.md) the rotating
+# epilogue costs the QKV GEMM 0.73 ms per layer (1.45 -> 1.10 PF/s) against 0.2 ms for the separate RoPE pass:
+# 27,221 vs 27,521 tokens/s.  The backward's RoPE^T stays folded into the flash backward either way.
+_ROPE_IN_GEMM = _os.environ.get("PADDLE2_AMD_ROPE_IN_GEMM", "0") != "0"
 
 
 class _QKVAttnFn(torch.autograd.Function):

@@ -60,7 +60,8 @@ def test_qkv_rope_attention_fold_matches_unfused(monkeypatch, B, S, nh, nkv):
     assert _rel(grads[True][1], xr.grad) < 2e-2
 
 
-def test_qkv_proj_rope_attention_node():
+def test_qkv_proj_rope_attention_node(monkeypatch):
+    monkeypatch.setattr(T, "_ROPE_IN_GEMM", True)    # opt-in route (profiles/r4_rope_fusion.md)
     B, S, K, nh, nkv = 2, 512, 1024, 8, 8
     g = torch.Generator(device=dev).manual_seed(1)
     x = torch.randn(B, S, K, generator=g, device=dev).to(torch.bfloat16)
