@@ -216,6 +216,12 @@ class LlamaMLP(nn.Layer):
 
     def forward(self, x):
         if self.config.fuse_attention_ffn and type(self.gate_up_fused_proj) is nn.Linear:
+            gu, dn = self.gate_up_fused_proj, self.down_proj
+            if (type(dn) is nn.Linear and gu.bias is None and dn.bias is None and not (
+                    gu._forward_pre_hooks or gu._forward_post_hooks or dn._forward_pre_hooks
+                    or dn._forward_post_hooks) and T.swiglu_mlp_ok(x._t, gu.weight._t, dn.weight._t)):
+                # one node: the SwiGLU backward runs in the down projection's dgrad epilogue
+                return _wrap(T.swiglu_mlp(x._t, gu.weight._t, dn.weight._t))
             a = T.swiglu_linear(x._t, self.gate_up_fused_proj.weight._t)  # one node: GEMM + SwiGLU (+dY^T)
         elif self.config.fuse_attention_ffn:
             a = T.swiglu(self.gate_up_fused_proj(x)._t)  # per-rank [gate_r | up_r]

@@ -697,6 +697,68 @@ class _SwiGLULinearFn(torch.autograd.Function):
         return dx, dw
 
 
+class _SwiGLUMLPFn(torch.autograd.Function):
+    """y = swiglu(x @ W_gu) @ W_down (Llama MLP, W_gu [K, 2H] packed gate | up) as ONE autograd node so the SwiGLU
+    backward runs in the down projection's dgrad epilogue: d_a = dy @ W_down^T never leaves the fp32 accumulators,
+    the epilogue reads gate / up from the saved pre-activations and writes d_gate / d_up (gemm kEpiDSwiGLU) — no
+    d_a round trip and no separate SwiGLU-backward pass."""
+
+    @staticmethod
+    def forward(ctx, x, w_gu, w_down):
+        from . import gemm as G
+
+        K = w_gu.shape[0]
+        x2 = x.reshape(-1, K)
+        a, gu = G.mm_swiglu(x2, w_gu)
+        y = G.mm_fwd(a, w_down)
+        ctx.save_for_backward(x2, w_gu, w_down, a, gu)
+        ctx.gts = (getattr(w_gu, "_p2_gt", None), getattr(w_down, "_p2_gt", None))
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], w_down.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import gemm as G
+
+        x2, w_gu, w_down, a, gu = ctx.saved_tensors
+        gt_gu, gt_down = ctx.gts
+        dy2 = dy.reshape(-1, w_down.shape[1]).contiguous()
+        dgu = G.mm_dgrad_dswiglu(dy2, w_down, gu)
+        if dgu is None:   # another dgrad schedule selected: GEMM, then the SwiGLU backward kernel
+            da = G.mm_dgrad(dy2, w_down)
+            M, H2 = gu.shape
+            H, es = H2 // 2, gu.element_size()
+            dgu = torch.empty_like(gu)
+            N.native().swiglu_bwd(_DT[gu.dtype], gu.data_ptr(), gu.data_ptr() + H * es, da.data_ptr(),
+                                  dgu.data_ptr(), dgu.data_ptr() + H * es, M, H, H2, H2, H2, H2, N.stream())
+        dw_down = weight_grad(a, dy2, gt_down) if ctx.needs_input_grad[2] else None
+        dx = G.mm_dgrad(dgu, w_gu).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dw_gu = weight_grad(x2, dgu, gt_gu) if ctx.needs_input_grad[1] else None
+        return dx, dw_gu, dw_down
+
+
+# PADDLE2_AMD_SWIGLU_MLP_NODE=0: the MLP as two linear nodes (SwiGLU backward as its own pass) — A/B switch
+_SWIGLU_MLP_NODE = _os.environ.get("PADDLE2_AMD_SWIGLU_MLP_NODE", "1") != "0"
+
+
+def swiglu_mlp_ok(x, w_gu, w_down):
+    from . import gemm as G
+
+    K, H2 = w_gu.shape
+    M = x.numel() // K if K else 0
+    return (_SWIGLU_MLP_NODE and x.device.type == "cuda" and x.dtype == torch.bfloat16 and w_gu.dtype == x.dtype
+            and w_down.dtype == x.dtype and N.use_native(x) and not isinstance(x, _DTensor)
+            and not isinstance(w_gu, _DTensor) and not isinstance(w_down, _DTensor) and not WeightGradStore.route
+            and x.shape[-1] == K and w_down.shape[0] == H2 // 2 and (H2 // 2) % 128 == 0 and M >= 4096
+            and M % 8 == 0 and x.is_contiguous() and G.supported_fwd(x.reshape(-1, K), w_gu)
+            and _pass_native("fwd", x) and _pass_native("dgrad", x) and _pass_native("swiglu", x)
+            and G._variant("dgrad") == G.V7_SPREAD and w_down.shape[1] % 128 == 0)
+
+
+def swiglu_mlp(x, w_gu, w_down):
+    return _SwiGLUMLPFn.apply(x, w_gu, w_down)
+
+
 def swiglu_linear(x, w):
     """swiglu(x @ W) with W [K, 2H] packed [gate | up]."""
     K, H2 = w.shape

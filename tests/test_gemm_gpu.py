@@ -286,3 +286,39 @@ def test_qkv_rope_linear_node(B, S, nq, nkv):
     assert _rel(y, yr) < 8e-3
     assert _rel(xi.grad, xr.grad) < 1e-2
     assert _rel(wi.grad, wr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("M,H,N", [(256, 256, 128), (1024, 640, 512), (4096, 1408, 1024)])
+def test_dswiglu_epilogue(M, H, N):
+    """d_gu = SwiGLU backward of (dy @ W^T) with the saved gate | up, from one GEMM epilogue, vs fp32 autograd."""
+    if G._variant("dgrad") != G.V7_SPREAD:
+        pytest.skip("spread TN schedule only")
+    dy, w, gu = _rand(M, N, seed=50), _rand(H, N, seed=51, scale=N ** -0.5), _rand(M, 2 * H, seed=52)
+    out = G.mm_dgrad_dswiglu(dy, w, gu)
+    assert out is not None
+    gr = gu.float().requires_grad_()
+    g, u = gr[:, :H], gr[:, H:]
+    (torch.nn.functional.silu(g) * u).backward(dy.float() @ w.float().t())
+    assert _rel(out, gr.grad) < 1e-2
+
+
+def test_swiglu_mlp_node_matches_fp32():
+    """The one-node Llama MLP (torch_ops._SwiGLUMLPFn): output and the input / weight gradients vs fp32."""
+    from paddle2_amd.ops import torch_ops as T
+
+    M, K, H = 4096, 512, 1408
+    x = _rand(M, K, seed=53)
+    wgu, wd = _rand(K, 2 * H, seed=54, scale=K ** -0.5), _rand(H, K, seed=55, scale=H ** -0.5)
+    dy = _rand(M, K, seed=56)
+    if not T.swiglu_mlp_ok(x, wgu, wd):
+        pytest.skip("MLP node not selected for this schedule")
+    xi, a, b = (t.clone().requires_grad_() for t in (x, wgu, wd))
+    y = T.swiglu_mlp(xi, a, b)
+    y.backward(dy)
+    xr, ar, br = (t.float().requires_grad_() for t in (x, wgu, wd))
+    h = xr @ ar
+    yr = (torch.nn.functional.silu(h[:, :H]) * h[:, H:]) @ br
+    yr.backward(dy.float())
+    assert _rel(y, yr) < 1e-2
+    for got, ref in ((xi.grad, xr.grad), (a.grad, ar.grad), (b.grad, br.grad)):
+        assert _rel(got, ref) < 2e-2
