@@ -737,8 +737,10 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         return dx, dw_gu, dw_down
 
 
-# PADDLE2_AMD_SWIGLU_MLP_NODE=0: the MLP as two linear nodes (SwiGLU backward as its own pass) — A/B switch
-_SWIGLU_MLP_NODE = _os.environ.get("PADDLE2_AMD_SWIGLU_MLP_NODE", "1") != "0"
+# Opt-in (PADDLE2_AMD_SWIGLU_MLP_NODE=1).  Measured in the Llama-2-7B step (profiles/r4_epilogue_fusions.md): the
+# SwiGLU-backward epilogue takes the down dgrad from ~2.0 to 3.2 ms per layer (two reads and two writes per output
+# element in the element-checked epilogue) against 0.65 ms for the separate pass: 27,071 vs 27,408 tokens/s.
+_SWIGLU_MLP_NODE = _os.environ.get("PADDLE2_AMD_SWIGLU_MLP_NODE", "0") != "0"
 
 
 def swiglu_mlp_ok(x, w_gu, w_down):
