@@ -45,6 +45,10 @@ PASS_VARIANT = {"fwd": V7_SPREAD, "dgrad": V7_SPREAD, "wgrad": 5, "wgrad_bf16": 
 # grouped tile order per pass (row tiles that sweep the column tiles together): 4 for the spread TN schedule
 # (forward +2..7 %, dgrad +0..2 % over 8 at M = 32768; profiles/r4_gemm_spread.md), 8 for the wgrad kernels
 PASS_GROUP_M = {"fwd": 4, "dgrad": 4, "swiglu": 4, "wgrad": 8, "wgrad_bf16": 8, "rope": 4}
+for _k in list(PASS_GROUP_M):   # per-pass override: PADDLE2_AMD_GEMM_GROUP_M_FWD=2, ..._DGRAD, ..._SWIGLU, ...
+    _e = os.environ.get("PADDLE2_AMD_GEMM_GROUP_M_" + _k.upper())
+    if _e:
+        PASS_GROUP_M[_k] = int(_e)
 
 
 def _variant(name):
