@@ -264,7 +264,11 @@ def decompose(program, src_vars=None, blacklist=frozenset(), whitelist=frozenset
         new = rule(_Builder(program, op), op)
         if new is None:
             continue
-        op.result(0).replace_all_uses_with(new)
+        if isinstance(new, (list, tuple)):   # multi-output op (unbind / unstack / meshgrid): one value per result
+            for i, v in enumerate(new):
+                op.result(i).replace_all_uses_with(v)
+        else:
+            op.result(0).replace_all_uses_with(new)
         program.block.remove_op(op)
         n += 1
     return n

@@ -284,6 +284,40 @@ def _stack(b, op):
     return b.op2("pd_op.concat", parts, shape, xs[0].dtype, axis=axis)
 
 
+def _unbind(b, op):
+    """unbind / unstack along ``axis``: per index a unit slice reshaped without that axis (multi-output)."""
+    x = op.operand_source(0)
+    if not _static(x):
+        return None
+    nd = len(x.shape)
+    axis = int(_attr(op, "axis", default=0)) % nd
+    n = x.shape[axis]
+    if n != op.num_results():
+        return None
+    out_shape = list(x.shape[:axis]) + list(x.shape[axis + 1:])
+    outs = []
+    for i in range(n):
+        sl_shape = list(x.shape)
+        sl_shape[axis] = 1
+        sl = b.op2("pd_op.slice", [x], sl_shape, x.dtype, axis=axis, start=i, end=i + 1)
+        outs.append(reshape(b, sl, out_shape))
+    return outs
+
+
+def _meshgrid(b, op):
+    """meshgrid of k 1-D inputs (ij indexing): input i reshaped to size n_i on axis i and expanded to the grid."""
+    xs = op.operands()
+    if not xs or not all(_static(x) and len(x.shape) == 1 for x in xs) or op.num_results() != len(xs):
+        return None
+    grid = [x.shape[0] for x in xs]
+    outs = []
+    for i, x in enumerate(xs):
+        shp = [1] * len(xs)
+        shp[i] = grid[i]
+        outs.append(b.op2("pd_op.expand", [reshape(b, x, shp)], grid, x.dtype, shape=grid))
+    return outs
+
+
 def _to_result_shape(b, op):
     """squeeze / unsqueeze / flatten: a reshape to the (static) result shape."""
     x, r = op.operand_source(0), op.result(0)
@@ -553,7 +587,8 @@ RULES = {
     "pd_op.any": _any, "pd_op.mean_all": _mean_all, "pd_op.p_norm": _p_norm, "pd_op.pow": _pow,
     "pd_op.huber_loss": _huber_loss, "pd_op.one_hot": _one_hot, "pd_op.squared_l2_norm": _squared_l2_norm,
     "pd_op.bce_loss": _bce_loss, "pd_op.bmm": _bmm, "pd_op.batch_norm": _batch_norm, "pd_op.batch_norm_": _batch_norm,
-    "pd_op.stack": _stack, "pd_op.squeeze": _to_result_shape, "pd_op.unsqueeze": _to_result_shape,
+    "pd_op.stack": _stack, "pd_op.unbind": _unbind, "pd_op.unstack": _unbind, "pd_op.meshgrid": _meshgrid,
+    "pd_op.squeeze": _to_result_shape, "pd_op.unsqueeze": _to_result_shape,
     "pd_op.squeeze2": _to_result_shape, "pd_op.unsqueeze2": _to_result_shape, "pd_op.flatten": _to_result_shape,
     "pd_op.add_n": _add_n, "pd_op.sum": _add_n, "pd_op.full_like": _full_like, "pd_op.dropout": _dropout, "pd_op.heaviside": _heaviside,
     "pd_op.instance_norm": _instance_norm, "pd_op.clip": _clip, "pd_op.index_select": _index_select,

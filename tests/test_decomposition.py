@@ -127,6 +127,31 @@ def test_shape_ops():
     _check("pd_op.bmm", [_r(2, 3, 4), _r(2, 4, 5)], torch.bmm, {}, [2, 3, 5])
 
 
+def _check_multi(name, inputs, attrs, out_shapes, refs):
+    """Multi-output composite (unbind / unstack / meshgrid): every result fetched and compared."""
+    p = pir.Program()
+    vals = [p.block.append(pir.Operation("pd_op.data", [], [(list(t.shape), t.dtype)],
+                                         {"name": f"x{i}", "col": i})).result(0) for i, t in enumerate(inputs)]
+    op = p.block.append(pir.Operation(name, vals, [(s, torch.float32) for s in out_shapes], attrs))
+    for i, s in enumerate(out_shapes):
+        p.block.append(pir.Operation("pd_op.fetch", [op.result(i)], [(s, torch.float32)], {"name": f"o{i}", "col": i}))
+    assert decomposition.decompose(p) == 1, f"{name} was not decomposed"
+    left = {o.name() for o in p.block.ops} - {"pd_op.data", "pd_op.fetch"}
+    assert left <= decomposition.PRIMITIVES, left - decomposition.PRIMITIVES
+    got = pir.run(p, inputs)
+    assert len(got) == len(refs)
+    for a, b in zip(got, refs):
+        torch.testing.assert_close(a, b)
+
+
+def test_multi_output_ops():
+    x = _r(2, 3, 4)
+    _check_multi("pd_op.unbind", [x], {"axis": 1}, [[2, 4]] * 3, list(torch.unbind(x, 1)))
+    _check_multi("pd_op.unstack", [x], {"axis": -1}, [[2, 3]] * 4, list(torch.unbind(x, -1)))
+    u, v = _r(3), _r(5)
+    _check_multi("pd_op.meshgrid", [u, v], {}, [[3, 5], [3, 5]], list(torch.meshgrid(u, v, indexing="ij")))
+
+
 def test_indexing_ops():
     x = _r(4, 6)
     idx = torch.tensor([3, 0, 3, 1])
