@@ -81,10 +81,11 @@ def _conv1x1_native(t_nhwc, weight, bias, stride, groups, dilation):
     from ...ops import _native as N
 
     w = weight._t
-    return (_CG.MODE == "native" and t_nhwc.is_cuda and t_nhwc.dtype == torch.bfloat16
+    return (_CG.MODE in ("native", "auto") and t_nhwc.is_cuda and t_nhwc.dtype == torch.bfloat16
             and w.dtype == t_nhwc.dtype and groups == 1 and tuple(w.shape[2:]) == (1, 1)
             and all(dd == 1 for dd in dilation) and w.shape[1] % 8 == 0 and w.shape[0] % 8 == 0
-            and (bias is None or bias._t.dtype == t_nhwc.dtype) and N.use_native(t_nhwc))
+            and (bias is None or bias._t.dtype == t_nhwc.dtype) and N.use_native(t_nhwc)
+            and _CG.route("1x1", t_nhwc, w, stride, [0, 0]))
 
 
 def _conv(x, weight, bias, stride, padding, dilation, groups, data_format, n):

@@ -24,7 +24,11 @@ import torch
 from . import _native as N
 from . import gemm as G
 
-MODE = os.environ.get("PADDLE2_AMD_CONV", "native")   # native | miopen
+# auto (default) | native | miopen.  auto: per layer shape the faster of the native kernels and MIOpen, from one
+# timed forward + backward of each (profiles/r4_secondary_configs.md: whole-network native 5,922 vs MIOpen
+# 7,295 images/s on ResNet50 b=256, so the choice is made per shape, not globally)
+MODE = os.environ.get("PADDLE2_AMD_CONV", "auto")
+_ROUTE = {}
 _CUS = {}
 calls = {"1x1": 0, "3x3": 0}
 
@@ -173,10 +177,52 @@ class Conv3x3Fn(torch.autograd.Function):
 
 
 def eligible_3x3(t_nhwc, w, stride, padding, dilation, groups):
-    if MODE != "native" or not t_nhwc.is_cuda or t_nhwc.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+    if MODE not in ("native", "auto") or not t_nhwc.is_cuda or t_nhwc.dtype != torch.bfloat16 \
+            or w.dtype != torch.bfloat16:
         return False
     if not N.use_native(t_nhwc) or groups != 1 or tuple(w.shape[2:]) != (3, 3):
         return False
     if list(stride) != [1, 1] or list(dilation) != [1, 1] or list(padding) != [1, 1]:
         return False
-    return _pow2_64(w.shape[1]) and _pow2_64(w.shape[0])
+    return _pow2_64(w.shape[1]) and _pow2_64(w.shape[0]) and route("3x3", t_nhwc, w, [1, 1], [1, 1])
+
+
+def _time_fwd_bwd(fn, x, w, iters=2):
+    from ..incubate.autotune import _bench
+
+    with torch.enable_grad():
+        xx = x.detach().requires_grad_(x.is_floating_point())
+        ww = w.detach().requires_grad_(True)
+        dy = torch.randn_like(fn(xx, ww))
+
+        def run():
+            torch.autograd.backward(fn(xx, ww), dy)
+            xx.grad = ww.grad = None
+
+        return _bench(run, iters)
+
+
+def route(kind, x, w, stride, padding):
+    """True -> the native kernel runs this NHWC conv.  MODE native: always; auto: timed once per (kind, shapes)
+    against MIOpen (torch conv2d on the channels-last view), forward + backward, and cached."""
+    if MODE == "native":
+        return True
+    key = (kind, tuple(x.shape), tuple(w.shape), tuple(stride))
+    r = _ROUTE.get(key)
+    if r is None:
+        if torch.cuda.is_current_stream_capturing():
+            return True                               # no timing inside a graph capture
+        s = list(stride)
+        if kind == "1x1":
+            def nat(a, b):
+                a = a[:, ::s[0], ::s[1], :] if s != [1, 1] else a
+                return Conv1x1Fn.apply(a.contiguous(), b, None)
+        else:
+            def nat(a, b):
+                return Conv3x3Fn.apply(a.contiguous(), b)
+
+        def lib(a, b):
+            return torch.nn.functional.conv2d(a.movedim(-1, 1), b, None, s, list(padding)).movedim(1, -1)
+
+        r = _ROUTE[key] = _time_fwd_bwd(nat, x, w) <= _time_fwd_bwd(lib, x, w)
+    return r

@@ -92,9 +92,12 @@ def cast(x2, meta: FP8TensorMeta, transpose=False, keep_rowmajor=True):
     return (q if (keep_rowmajor or not transpose) else None), (q.t().contiguous() if transpose else None)
 
 
-# "native" (default): the hand-written K=128 fp8 MFMA GEMM (csrc/kernels/gemm8.hip) for every shape in its domain;
-# "blas": hipBLASLt through torch._scaled_mm
-GEMM = os.environ.get("PADDLE2_AMD_FP8_GEMM", "native")
+# "auto" (default): per (formats, M, N, K) the faster of the native kernel and hipBLASLt, timed on device events the
+# first time the shape is seen (the native kernel has no split-K: at M = 4096 its 256 x 256 tiles leave a partial
+# last wave that hipBLASLt's stream-K does not — profiles/r4_secondary_configs.md); "native": the hand-written
+# K=128 fp8 MFMA GEMM (csrc/kernels/gemm8.hip) for every shape in its domain; "blas": hipBLASLt (torch._scaled_mm)
+GEMM = os.environ.get("PADDLE2_AMD_FP8_GEMM", "auto")
+_ROUTE = {}
 _CUS = {}
 _FMT = {E4M3: 0, E5M2: 1}
 # (A format, B format, output) pairs the kernel is instantiated for: forward e4m3 x e4m3, dgrad e5m2 x e4m3,
@@ -130,15 +133,36 @@ def mm_native(a, bT, inv_a, inv_b, out_dtype, bias=None):
     return c
 
 
+def _native_faster(nat, lib, iters=3):
+    """Time both GEMM routes once on device events (after one untimed call each); False when the native kernel
+    does not cover the problem."""
+    from ..incubate.autotune import _bench
+
+    if nat() is None:
+        return False
+    return _bench(nat, iters) <= _bench(lib, iters)
+
+
 def _mm(a, b_colmajor, inv_a, inv_b, out_dtype, bias=None):
     """(a * inv_a) @ (b * inv_b) with a row-major [M, K] fp8 and b a column-major [K, N] fp8 view."""
     if a.device.type == "cuda":
-        if GEMM == "native" and N.use_native(a):
-            inv_a = inv_a.float().reshape(1).contiguous()
-            inv_b = inv_b.float().reshape(1).contiguous()
-            c = mm_native(a, b_colmajor.t(), inv_a, inv_b, out_dtype, bias)
-            if c is not None:
-                return c
+        if GEMM in ("native", "auto") and N.use_native(a):
+            ia = inv_a.float().reshape(1).contiguous()
+            ib = inv_b.float().reshape(1).contiguous()
+            nat = lambda: mm_native(a, b_colmajor.t(), ia, ib, out_dtype, bias)  # noqa: E731
+            use = True
+            if GEMM == "auto":
+                key = (a.dtype, b_colmajor.dtype, out_dtype, a.shape[0], b_colmajor.shape[1], a.shape[1], bias is None)
+                use = _ROUTE.get(key)
+                if use is None and torch.cuda.is_current_stream_capturing():
+                    use = True                     # no timing inside a graph capture
+                elif use is None:
+                    use = _ROUTE[key] = _native_faster(nat, lambda: torch._scaled_mm(
+                        a, b_colmajor, scale_a=inv_a, scale_b=inv_b, bias=bias, out_dtype=out_dtype))
+            if use:
+                c = nat()
+                if c is not None:
+                    return c
         return torch._scaled_mm(a, b_colmajor, scale_a=inv_a, scale_b=inv_b, bias=bias, out_dtype=out_dtype)
     y = (a.float() * inv_a) @ (b_colmajor.float() * inv_b)
     if bias is not None:

@@ -613,7 +613,7 @@ class _GeluMLPFn(torch.autograd.Function):
         return dx, dw1, db1, dw2, db2, None
 
 
-_FUSED_GELU_MLP = _os.environ.get("PADDLE2_AMD_FUSED_GELU_MLP", "1") != "0"
+_FUSED_GELU_MLP = _os.environ.get("PADDLE2_AMD_FUSED_GELU_MLP", "0") != "0"
 
 
 def gelu_mlp_ok(x, w1, b1, w2, b2):

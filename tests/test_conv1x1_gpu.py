@@ -13,6 +13,12 @@ pytestmark = pytest.mark.gpu
 dev = "cuda"
 
 
+@pytest.fixture(autouse=True)
+def _native_conv(monkeypatch):
+    """These tests pin the native kernels (the default "auto" mode may route a shape to MIOpen)."""
+    monkeypatch.setattr(CG, "MODE", "native")
+
+
 def _rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
 
@@ -62,3 +68,17 @@ def test_other_convs_stay_on_miopen():
     xn = paddle.to_tensor(x._t.permute(0, 3, 1, 2).contiguous())
     paddle.nn.functional.conv2d(xn, w1)
     assert CG.calls["1x1"] == before
+
+
+def test_auto_route_times_once_and_matches(monkeypatch):
+    """MODE auto: the first call of a shape times native vs MIOpen and caches the decision; either route gives
+    the fp32 reference's result."""
+    monkeypatch.setattr(CG, "MODE", "auto")
+    monkeypatch.setattr(CG, "_ROUTE", {})
+    x = torch.randn(4, 14, 14, 64, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(128, 64, 1, 1, device=dev, dtype=torch.bfloat16) * 0.1
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float()).permute(0, 2, 3, 1)
+    for _ in range(2):
+        y = paddle.nn.functional.conv2d(paddle.to_tensor(x), paddle.to_tensor(w), data_format="NHWC")
+        assert _rel(y._t, ref) < 1e-2
+    assert len(CG._ROUTE) == 1

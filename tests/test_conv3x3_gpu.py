@@ -13,6 +13,12 @@ pytestmark = pytest.mark.gpu
 dev = "cuda"
 
 
+@pytest.fixture(autouse=True)
+def _native_conv(monkeypatch):
+    """These tests pin the native kernels (the default "auto" mode may route a shape to MIOpen)."""
+    monkeypatch.setattr(CG, "MODE", "native")
+
+
 def _rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
 

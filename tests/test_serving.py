@@ -206,17 +206,24 @@ def test_fused_multi_transformer_gpu_matches_cpu():
     """The GPU fused_multi_transformer (cached W^T projections, native decode kernels) matches the CPU op."""
     from paddle2_amd.incubate.nn import FusedMultiTransformer
 
-    paddle.seed(0)
-    layer = FusedMultiTransformer(128, 4, 256, num_layers=2, activation="gelu")
-    b, s, nh, hd = 2, 6, 4, 32
-    x = paddle.randn([b, s, 128])
-    caches = [paddle.zeros([2, b, nh, 16, hd]) for _ in range(2)]
-    ref, _ = layer(x, caches=caches)
-    paddle.set_device("gpu:0")
-    layer.to(device="gpu:0")
-    xg = paddle.to_tensor(x._t.cuda())
-    cg = [paddle.zeros([2, b, nh, 16, hd]) for _ in range(2)]
-    out, _ = layer(xg, caches=cg)
+    prev = paddle.get_device()
+    try:
+        paddle.set_device("cpu")    # the reference pass on the CPU op (the default device on a GPU box is gpu:0)
+        paddle.seed(0)
+        layer = FusedMultiTransformer(128, 4, 256, num_layers=2, activation="gelu")
+        b, s, nh, hd = 2, 6, 4, 32
+        x = paddle.randn([b, s, 128])
+        caches = [paddle.zeros([2, b, nh, 16, hd]) for _ in range(2)]
+        ref, _ = layer(x, caches=caches)
+        assert ref._t.device.type == "cpu"
+        paddle.set_device("gpu:0")
+        layer.to(device="gpu:0")
+        xg = paddle.to_tensor(x._t.cuda())
+        cg = [paddle.zeros([2, b, nh, 16, hd]) for _ in range(2)]
+        out, _ = layer(xg, caches=cg)
+        assert out._t.is_cuda
+    finally:
+        paddle.set_device(prev)
     torch.testing.assert_close(out._t.float().cpu(), ref._t.float(), atol=2e-3, rtol=2e-3)
 
 
