@@ -54,10 +54,11 @@ def parse(argv=None):
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--gemm-autotune", default="auto", choices=["auto", "tune", "off"],
                     help="hipBLASLt solution cache (tuning/gemm_gfx950.csv): auto = use it if present")
-    ap.add_argument("--gemm-route", default="auto", choices=["auto", "static", "measure"],
-                    help="bf16 Linear GEMM backend per shape: static = the per-pass table (ops/gemm.py), measure = "
-                         "time native vs hipBLASLt per (pass, M, N, K) once (incubate/autotune.py route), auto = "
-                         "measure for the GPT configs (M = 4096 tokens: partial last waves) and static for Llama")
+    ap.add_argument("--gemm-route", default="static", choices=["static", "measure"],
+                    help="bf16 Linear GEMM backend per shape: static = the per-pass table (ops/gemm.py: the native "
+                         "kernels), measure = time native vs hipBLASLt per (pass, M, N, K) once (incubate/autotune.py "
+                         "route).  GPT-3 13B: static 10,893 vs measure 10,860 tokens/s with the tail split-K "
+                         "(profiles/r4_gemm_tail_splitk.md)")
     return ap.parse_args(argv)
 
 
@@ -94,7 +95,7 @@ def main():
 
         if args.gemm_autotune == "tune" or os.path.exists(autotune.DEFAULT_GEMM_CACHE):
             autotune.enable_gemm_autotune(tuning=args.gemm_autotune == "tune")
-    if args.gemm_route == "measure" or (args.gemm_route == "auto" and args.model.startswith("gpt3")):
+    if args.gemm_route == "measure":
         if torch.cuda.is_available():
             from paddle2_amd.incubate import autotune
 

@@ -31,7 +31,7 @@ int pd_gemm_conv(const void*, long, const void*, const void*, const void*, long,
                  int, int, int, int, int, int, int, int, void*);
 void pd_gemm_set_rope(const float*, const float*, int, int);
 int pd_gemm_f8(int, int, int, const void*, long, const void*, long, void*, long, const void*, const float*,
-               const float*, int, int, int, float, int, int, void*);
+               const float*, int, int, int, float, int, int, void*, long, void*);
 long pd_ar_sig_bytes();
 int pd_bias_act(int, int, int, const void*, const void*, void*, long, int, long, long, void*);
 int pd_bias_act_bwd(int, int, int, const void*, const void*, const void*, void*, long, int, long, long, void*);
@@ -148,10 +148,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("gemm_f8", [](int fa, int fb, int epi, uintptr_t a, long lda, uintptr_t b, long ldb, uintptr_t c, long ldc,
                       uintptr_t bias, uintptr_t sa, uintptr_t sb, int M, int N, int K, float beta, int group_m, int cus,
-                      uintptr_t st) {
+                      uintptr_t ws, long ws_bytes, uintptr_t st) {
     return pd_gemm_f8(fa, fb, epi, P<const void*>(a), lda, P<const void*>(b), ldb, P<void*>(c), ldc,
                       P<const void*>(bias), P<const float*>(sa), P<const float*>(sb), M, N, K, beta, group_m, cus,
-                      P<void*>(st));
+                      P<void*>(ws), ws_bytes, P<void*>(st));
   });
   m.def("gemm_grouped", [](int layout, int epi, uintptr_t a, long lda, uintptr_t b, long ldb, long gsb, uintptr_t c,
                            long ldc, long gsc, uintptr_t c2, long ldc2, uintptr_t bias, long gsbias, uintptr_t goff,

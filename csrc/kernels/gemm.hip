@@ -760,7 +760,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v6_kernel(Params p) {
 }  // namespace gm
 }  // namespace pd
 
-bool pd_gemm_v7(const pd::gm::Params& p, int layout, int epi, int sched, int cus, hipStream_t st);  // gemm7.hip
+bool pd_gemm_v7(const pd::gm::Params& p, int layout, int epi, int sched, int cus, long ws_bytes, hipStream_t st);  // gemm7.hip
 
 // layout: bit0 = A K-major, bit1 = B K-major.  epi: 0 bf16 (+bias), 1 fp32 main grad (beta), 2 swiglu.
 // CUs per XCD of the current device (workgroup slots of the 128 KiB-LDS kernel), cached per device
@@ -858,7 +858,7 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   hipStream_t st = (hipStream_t)stream;
   // v7 (gemm7.hip): the TN schedule, variants 7..10 = its SCHED 0..3; problems outside its domain run v6
   if ((variant >= 7 && variant <= 10) || variant >= 64) {
-    if (pd_gemm_v7(p, layout, epi, variant >= 64 ? variant - 64 : variant - 7, 8 * p.cpx, st))
+    if (pd_gemm_v7(p, layout, epi, variant >= 64 ? variant - 64 : variant - 7, 8 * p.cpx, ws ? ws_bytes : 0, st))
       return (int)hipGetLastError();
     variant = 6;
   }

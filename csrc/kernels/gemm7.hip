@@ -148,6 +148,10 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   constexpr bool ROT = (SCHED & 512) != 0;                       // odd slots start their K loop half way
   constexpr bool NTS = (SCHED & 1024) != 0;                      // non-temporal epilogue stores (X4 path)
   constexpr bool CONV = (SCHED & 2048) != 0;                     // implicit-GEMM convolution (row-shifted A taps)
+  // tail split-K (a launch of its own after the whole tiles' launch, which skips the last tail_cap tiles): the last
+  // partial wave's tail_cap tiles run as ksplit K-slices, one per workgroup (slot = tail tile * ksplit + slice),
+  // into fp32 slabs that v7_tail_reduce_kernel sums (an in-loop tail unit spilled 700 B/lane to scratch)
+  constexpr bool TSK = (SCHED & 4096) != 0;
   constexpr bool SWI = EPI == kEpiSwiGLU;
   __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
   const unsigned sbase = (unsigned)(size_t)(lds_char*)smem_raw;
@@ -155,13 +159,17 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   const int nwg = p.tiles_m * p.tiles_n;
   const int G = gridDim.x;
   const int slot = xcd_remap(blockIdx.x, G);
-  const int ntile = slot < nwg ? (nwg - slot + G - 1) / G : 0;
+  // tail_cap > 0: the whole-tile launch leaves the last tail_cap tiles to the TSK launch (one slice per workgroup)
+  const int whole = nwg - p.tail_cap, nwhole = 0;
+  const int ntile = TSK ? (slot < p.tail_cap * p.ksplit ? 1 : 0) : (slot < whole ? (whole - slot + G - 1) / G : 0);
   if (ntile == 0) return;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int nt = p.K / BK;  // even, K % 128 == 0 (host-checked)
+  const int ntc = TSK ? nt / p.ksplit : nt;   // K-tiles of a tail slice (even, host-checked)
+  int ntu = TSK && nwhole == 0 ? ntc : nt;    // K-tiles of the current unit
 
   f32x4v acc[2][8][4];
   // zero the accumulators of a tile; the zeros are pinned (asm operands) in front of an s_nop so the VALU writes
@@ -192,17 +200,26 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   const unsigned a_end = (unsigned)(size_t)p.a_end, b_end = (unsigned)(size_t)p.b_end;
   auto a_base = [&](int tm) { return (u64)(size_t)(p.A + (long)tm * BM * p.lda); };
   auto b_base = [&](int tn) { return (u64)(size_t)(p.B + (long)tn * (SWI ? 128 : BN) * p.ldb); };
+  // unit u of this workgroup: tile slot + u * G, or (TSK, u == nwhole) its tail slice, whose bases start at the
+  // slice's first K-tile
+  auto unit_tile = [&](int u, int& tm, int& tn) {
+    if (TSK && u == nwhole) tile_of(p, whole + slot / p.ksplit, tm, tn);
+    else tile_of(p, slot + u * G, tm, tn);
+  };
+  auto unit_koff = [&](int u) -> u64 {
+    return (TSK && u == nwhole) ? (u64)(unsigned)((slot % p.ksplit) * ntc) << 7 : 0;
+  };
   int ctm, ctn;
-  tile_of(p, slot, ctm, ctn);
-  u64 ca = a_base(ctm), cb = b_base(ctn), na = ca, nb = cb;
+  unit_tile(0, ctm, ctn);
+  u64 ca = a_base(ctm) + unit_koff(0), cb = b_base(ctn) + unit_koff(0), na = ca, nb = cb;
   bool nlive = false;
   auto set_next = [&](int u) {
     nlive = u + 1 < ntile;
     if (nlive) {
       int tm, tn;
-      tile_of(p, slot + (u + 1) * G, tm, tn);
-      na = a_base(tm);
-      nb = b_base(tn);
+      unit_tile(u + 1, tm, tn);
+      na = a_base(tm) + unit_koff(u + 1);
+      nb = b_base(tn) + unit_koff(u + 1);
     }
   };
   set_next(0);
@@ -213,8 +230,9 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   // phases instead of all 256 CUs at once
   const int rot = (ROT && (slot & 1)) ? nt / 2 : 0;
   auto desc = [&](int kk, u64 cur, u64 nxt, unsigned end) {
-    const bool nx = kk >= nt;
-    int kt = nx ? kk - nt : kk;
+    const int ntx = TSK ? ntu : nt;
+    const bool nx = kk >= ntx;
+    int kt = nx ? kk - ntx : kk;
     if constexpr (ROT) kt = kt + rot >= nt ? kt + rot - nt : kt + rot;
     const unsigned off = (unsigned)kt << 7;  // * BK * 2 bytes
     const u64 b = (nx ? nxt : cur) + off;
@@ -450,7 +468,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
 
   for (int u = 0; u < ntile; ++u) {
     zero_acc();
-    for (int k = 0; k < nt; k += 2) {
+    for (int k = 0; k < (TSK ? ntu : nt); k += 2) {
       if constexpr (VS) {
         ktile_v(std::integral_constant<int, 0>{}, k);
         ktile_v(std::integral_constant<int, 1>{}, k + 1);
@@ -468,6 +486,12 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
       sfor<2>([&](auto H) {
         constexpr int h = decltype(H)::value;
         epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+      });
+    } else if constexpr (TSK) {
+      // tail slice: the fp32 partial into its slab
+      sfor<2>([&](auto H) {
+        constexpr int h = decltype(H)::value;
+        store_partial(p.part + (long)slot * (BM * BN), acc[h], arow, bcolw + 64 * h, lane);
       });
     } else if constexpr (EPI != kEpiRope) {
 #pragma unroll
@@ -490,9 +514,10 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
       }
     }
     if (u + 1 < ntile) {
-      tile_of(p, slot + (u + 1) * G, ctm, ctn);
+      unit_tile(u + 1, ctm, ctn);
       ca = na;
       cb = nb;
+      if constexpr (TSK) ntu = u + 1 == nwhole ? ntc : nt;
       set_next(u + 1);
     }
   }
@@ -506,8 +531,9 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
 // Launch v7 (called by pd_gemm for variants 7..10 = SCHED 0..3).  Returns false if the problem is outside v7's
 // domain (the caller then runs v6): both operands K-major, bf16 (+bias) or SwiGLU epilogue, K % 128 == 0, every
 // operand extent < 2 GiB, 8-B-aligned output rows.
-bool pd_gemm_v7(const pd::gm::Params& p, int layout, int epi, int sched, int cus, hipStream_t st) {
+bool pd_gemm_v7(const pd::gm::Params& p_in, int layout, int epi, int sched, int cus, long ws_bytes, hipStream_t st) {
   using namespace pd::gm;
+  Params p = p_in;
   if (layout != 3 || epi == kEpiF32 || p.K % 128) return false;
   const long a_bytes = (long)((const char*)p.a_end - (const char*)p.A);
   const long b_bytes = (long)((const char*)p.b_end - (const char*)p.B);
@@ -551,6 +577,22 @@ bool pd_gemm_v7(const pd::gm::Params& p, int layout, int epi, int sched, int cus
     else
       gemm_v7_kernel<kEpiDGeLU, 384><<<grid, NTHR4, 0, st>>>(p);
     return true;
+  }
+  if (epi == kEpiBF16 && sched == 384 && p.part && ws_bytes > 0) {
+    // tail split-K plan: with G = cus persistent workgroups the last partial wave holds R = tiles % G tiles; when
+    // R <= G / 2 they run as ks = G / R (<= 8) K-slices of >= 8 K-tiles each (one slice per workgroup) instead
+    // of one whole tile on R CUs while the rest idle — e.g. M = 4096, N = 5120: 320 tiles, 64 of them in 4
+    // slices, 1.25 instead of 2 tile times + a ~64 MiB fp32 fix-up read
+    const int nwg = p.tiles_m * p.tiles_n, G = cus, R = nwg % G;
+    const int ks = tail_plan(nwg, G, p.K / BK, ws_bytes);
+    if (ks >= 2) {
+      p.ksplit = ks;
+      p.tail_cap = R;
+      if (nwg > R) gemm_v7_kernel<kEpiBF16, 384><<<dim3(std::min(nwg - R, G)), NTHR4, 0, st>>>(p);   // whole tiles
+      gemm_v7_kernel<kEpiBF16, 384 | 4096><<<dim3(R * ks), NTHR4, 0, st>>>(p);                     // tail slices
+      tail_reduce_kernel<kEpiBF16><<<dim3(BM * BN / 1024, R), 256, 0, st>>>(p, nwg - R);
+      return true;
+    }
   }
   if (epi == kEpiBF16 && sched > 3) {
     switch (sched) {

@@ -59,7 +59,7 @@ __device__ __forceinline__ void mfma8_dma(f32x4v& c, const i32x8& b, const i32x8
       : "memory");
 }
 
-template <int FA, int FB, int EPI>
+template <int FA, int FB, int EPI, bool TSK = false>
 __global__ __launch_bounds__(NTHR4, 1) void gemm_f8_kernel(Params p) {
   __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
   const unsigned sbase = (unsigned)(size_t)(lds_char*)smem_raw;
@@ -67,13 +67,16 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_f8_kernel(Params p) {
   const int nwg = p.tiles_m * p.tiles_n;
   const int G = gridDim.x;
   const int slot = xcd_remap(blockIdx.x, G);
-  const int ntile = slot < nwg ? (nwg - slot + G - 1) / G : 0;
+  // tail split-K (gemm_tn.h): the whole-tile launch skips the last tail_cap tiles, the TSK launch runs them as
+  // ksplit K-slices (slot = tail tile * ksplit + slice), one per workgroup
+  const int whole = nwg - p.tail_cap;
+  const int ntile = TSK ? (slot < p.tail_cap * p.ksplit ? 1 : 0) : (slot < whole ? (whole - slot + G - 1) / G : 0);
   if (ntile == 0) return;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int nt = p.K / BK;  // K-tiles of 128 fp8 (p.K counts 2-byte units); even, host-checked
+  const int nt = TSK ? p.K / BK / p.ksplit : p.K / BK;  // K-tiles of 128 fp8 (p.K counts 2-byte units); even
   const float scale = (p.sa ? *p.sa : 1.f) * (p.sb ? *p.sb : 1.f);
 
   f32x4v acc[2][8][4];
@@ -103,8 +106,9 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_f8_kernel(Params p) {
   auto a_base = [&](int tm) { return (u64)(size_t)(p.A + (long)tm * BM * p.lda); };
   auto b_base = [&](int tn) { return (u64)(size_t)(p.B + (long)tn * BN * p.ldb); };
   int ctm, ctn;
-  tile_of(p, slot, ctm, ctn);
-  u64 ca = a_base(ctm), cb = b_base(ctn), na = ca, nb = cb;
+  tile_of(p, TSK ? whole + slot / p.ksplit : slot, ctm, ctn);
+  const u64 koff = TSK ? (u64)(unsigned)((slot % p.ksplit) * nt) << 7 : 0;   // the slice's first K-tile
+  u64 ca = a_base(ctm) + koff, cb = b_base(ctn) + koff, na = ca, nb = cb;
   bool nlive = false;
   auto set_next = [&](int u) {
     nlive = u + 1 < ntile;
@@ -213,15 +217,22 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_f8_kernel(Params p) {
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[h][i][j] *= scale;
+    if constexpr (TSK) {
+      sfor<2>([&](auto H) {
+        constexpr int h = decltype(H)::value;
+        store_partial(p.part + (long)slot * (BM * BN), acc[h], arow, bcolw + 64 * h, lane);
+      });
+    } else {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if constexpr (EPI == kEpiBF16) {
-        if ((ctm + 1) * BM <= p.M && (ctn + 1) * BN <= p.N && (p.ldc & 7) == 0 && ((size_t)p.C & 15) == 0)
-          epilogue_v7_x4<false>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
-        else
+      for (int h = 0; h < 2; ++h) {
+        if constexpr (EPI == kEpiBF16) {
+          if ((ctm + 1) * BM <= p.M && (ctn + 1) * BN <= p.N && (p.ldc & 7) == 0 && ((size_t)p.C & 15) == 0)
+            epilogue_v7_x4<false>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+          else
+            epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+        } else {
           epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
-      } else {
-        epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+        }
       }
     }
     if (u + 1 < ntile) {
@@ -243,7 +254,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_f8_kernel(Params p) {
 // domain (K % 256, 16-B rows, operand extents >= 2 GiB, unsupported format pair): the caller takes another path.
 extern "C" int pd_gemm_f8(int fa, int fb, int epi, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
                           const void* bias, const float* sa, const float* sb, int M, int N, int K, float beta,
-                          int group_m, int cus, void* stream) {
+                          int group_m, int cus, void* ws, long ws_bytes, void* stream) {
   using namespace pd::gm;
   if (M <= 0 || N <= 0 || K <= 0 || K % 256 || lda % 16 || ldb % 16 || lda < K || ldb < K) return -1;
   if ((size_t)A % 16 || (size_t)B % 16 || (size_t)C % 16 || ldc % 4 || ldc < N) return -1;
@@ -268,13 +279,26 @@ extern "C" int pd_gemm_f8(int fa, int fb, int epi, const void* A, long lda, cons
   p.tiles_n = (N + BN - 1) / BN;
   p.group_m = group_m > 0 ? group_m : 4;
   hipStream_t st = (hipStream_t)stream;
-  const dim3 grid(std::min(p.tiles_m * p.tiles_n, cus));
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int ks = ws ? tail_plan(nwg, cus, p.K / BK, ws_bytes) : 0;
+  const int R = ks ? nwg % cus : 0;
+  if (ks) {
+    p.part = (float*)ws; p.ksplit = ks; p.tail_cap = R;
+  }
+  const dim3 grid(std::min(nwg - R, cus)), tgrid(R * ks), rgrid(BM * BN / 1024, R);
+#define PD_F8(FA_, FB_, E_)                                                                   \
+  if (nwg > R) gemm_f8_kernel<FA_, FB_, E_><<<grid, NTHR4, 0, st>>>(p);                      \
+  if (ks) {                                                                                   \
+    gemm_f8_kernel<FA_, FB_, E_, true><<<tgrid, NTHR4, 0, st>>>(p);                           \
+    tail_reduce_kernel<E_><<<rgrid, 256, 0, st>>>(p, nwg - R);                               \
+  }
   switch (fa * 100 + fb * 10 + epi) {
-    case 0: gemm_f8_kernel<0, 0, kEpiBF16><<<grid, NTHR4, 0, st>>>(p); break;    // forward
-    case 100: gemm_f8_kernel<1, 0, kEpiBF16><<<grid, NTHR4, 0, st>>>(p); break;  // dgrad
-    case 10: gemm_f8_kernel<0, 1, kEpiBF16><<<grid, NTHR4, 0, st>>>(p); break;   // wgrad, bf16 dW
-    case 11: gemm_f8_kernel<0, 1, kEpiF32><<<grid, NTHR4, 0, st>>>(p); break;    // wgrad, fp32 dW
+    case 0: PD_F8(0, 0, kEpiBF16) break;    // forward
+    case 100: PD_F8(1, 0, kEpiBF16) break;  // dgrad
+    case 10: PD_F8(0, 1, kEpiBF16) break;   // wgrad, bf16 dW
+    case 11: PD_F8(0, 1, kEpiF32) break;    // wgrad, fp32 dW
     default: return -1;
   }
+#undef PD_F8
   return (int)hipGetLastError();
 }

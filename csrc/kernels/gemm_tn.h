@@ -124,5 +124,78 @@ __device__ __forceinline__ void epilogue_v7_x4(const Params& p, f32x4v (&acc)[8]
   }
 }
 
+// ---------------------------------------------------------------------------------------------------- tail split-K
+// Persistent TN GEMMs (v7, fp8) run tiles_m * tiles_n tiles on G workgroups; the last partial wave of R = tiles % G
+// tiles keeps R CUs busy for one whole tile time while the rest idle (M = 4096, N = 5120: 320 tiles, 64 in the
+// tail).  The split: the whole-tile launch skips the last tail_cap = R tiles, a second launch runs each of them
+// as ksplit K-slices (one per workgroup, fp32 partials into slabs of the workspace p.part), and tail_reduce_kernel
+// sums the slabs into C.  The slice count: ks = min(G / R, 8) lowered until the K-tile count nt splits into even
+// slices of >= 8 K-tiles; 0 = no split (R > G / 2, too short a K, or the slabs do not fit the workspace).
+inline int tail_plan(int nwg, int G, int nt, long ws_bytes) {
+  const int R = nwg % G;
+  // >= 8 waves: the tail is <= 1/16 of the run and the second launch's seam costs about what the split saves
+  // (Llama M = 32768 shapes measured 0-1.5 % slower with it, profiles/r4_gemm_tail_splitk.md)
+  if (R == 0 || ws_bytes <= 0 || nwg >= 8 * G) return 0;
+  int ks = std::min(G / R, 8);
+  while (ks > 1 && (nt % (2 * ks) || nt / ks < 8)) --ks;
+  return ks >= 2 && (long)R * ks * BM * BN * 4 <= ws_bytes ? ks : 0;
+}
+
+// The fp32 partial of one K-slice of a tail tile, plain row-major [BM][BN] in its slab (tile-relative rows /
+// columns of epilogue_t's lane mapping)
+__device__ __forceinline__ void store_partial(float* slab, const f32x4v (&acc)[8][4], int arow, int bcolw, int lane) {
+  const int cq = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *(float4*)(slab + (arow + 16 * i + (lane & 15)) * BN + bcolw + 16 * j + cq) =
+          make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+}
+
+// Fix-up: tail tile r's C = the sum of its ksplit fp32 slabs (r * ksplit ..): bf16 (+ bias) or fp32 (+ beta * C).
+// grid (BM * BN / 1024, tail_cap), 256 threads x 4 consecutive columns.
+template <int EPI>
+__global__ __launch_bounds__(256) void tail_reduce_kernel(Params p, int whole) {
+  const int r = blockIdx.y;
+  int tm, tn;
+  tile_of(p, whole + r, tm, tn);
+  const int e0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  const int row = e0 / BN, col = e0 - row * BN;
+  const long gr = (long)tm * BM + row;
+  const int gc = tn * BN + col;
+  if (gr >= p.M || gc >= p.N) return;
+  const float* sp = p.part + (long)r * p.ksplit * (BM * BN) + e0;
+  float4 v = *(const float4*)sp;
+  for (int k = 1; k < p.ksplit; ++k) {
+    const float4 o = *(const float4*)(sp + (long)k * (BM * BN));
+    v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+  }
+  float a[4] = {v.x, v.y, v.z, v.w};
+  const bool vec = gc + 3 < p.N;
+  if constexpr (EPI == kEpiF32) {
+    float* cp = (float*)p.C + gr * p.ldc + gc;
+    for (int e = 0; e < 4; ++e)
+      if (p.beta != 0.f && gc + e < p.N) a[e] += p.beta * cp[e];
+    if (vec) {
+      *(float4*)cp = make_float4(a[0], a[1], a[2], a[3]);
+    } else {
+      for (int e = 0; e < 4; ++e)
+        if (gc + e < p.N) cp[e] = a[e];
+    }
+  } else {
+    unsigned short o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = f2bf(a[e] + (p.bias && gc + e < p.N ? bf2f(p.bias[gc + e]) : 0.f));
+    unsigned short* cp = (unsigned short*)p.C + gr * p.ldc + gc;
+    if (vec) {
+      *(uint2*)cp = make_uint2(o[0] | (unsigned)o[1] << 16, o[2] | (unsigned)o[3] << 16);
+    } else {
+      for (int e = 0; e < 4; ++e)
+        if (gc + e < p.N) cp[e] = o[e];
+    }
+  }
+}
+
 }  // namespace gm
 }  // namespace pd

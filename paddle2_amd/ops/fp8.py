@@ -112,6 +112,19 @@ def _cus(dev):
     return c
 
 
+# tail split-K (gemm_tn.h: a last partial wave of <= CUs / 2 tiles as K-slices + an fp32 fix-up) on the bf16 GEMM's
+# per-stream workspace; "0" disables
+TAILK = os.environ.get("PADDLE2_AMD_FP8_TAILK", "1") != "0"
+
+
+def _ws(t):
+    if not TAILK:
+        return 0, 0
+    from . import gemm as G
+
+    return G._workspace(t) if G.SPLITK else (0, 0)
+
+
 def mm_native(a, bT, inv_a, inv_b, out_dtype, bias=None):
     """C[M, N] = (a[M, K] . bT[N, K]^T) * inv_a * inv_b (+ bias) on the native fp8 GEMM (both operands K-major
     fp8, dequant factors as device scalars).  None when the problem is outside the kernel's domain."""
@@ -125,7 +138,8 @@ def mm_native(a, bT, inv_a, inv_b, out_dtype, bias=None):
     c = torch.empty(M, Nn, dtype=out_dtype, device=a.device)
     rc = N.native().gemm_f8(fa, fb, 0 if out_dtype == torch.bfloat16 else 1, a.data_ptr(), a.stride(0),
                             bT.data_ptr(), bT.stride(0), c.data_ptr(), c.stride(0), N.ptr(bias),
-                            inv_a.data_ptr(), inv_b.data_ptr(), M, Nn, K, 0.0, 4, _cus(a.device), N.stream())
+                            inv_a.data_ptr(), inv_b.data_ptr(), M, Nn, K, 0.0, 4, _cus(a.device), *_ws(a),
+                            N.stream())
     if rc == -1:
         return None
     if rc != 0:

@@ -84,6 +84,9 @@ def supported_wgrad(x2, dy2):
 # 192 MiB covers a 24-tile tail in 4 slices), one per (device, stream) so GEMMs on concurrent streams never share
 # slabs; "0" disables the split
 SPLITK = os.environ.get("PADDLE2_AMD_GEMM_SPLITK", "1") != "0"
+# the spread TN schedule's tail split-K (gemm7.hip SCHED bit 12: a last partial wave of <= CUs / 2 tiles runs as
+# K-slices on every CU + an fp32 fix-up), bf16-output forward / dgrad; "0" disables
+V7_TAILK = os.environ.get("PADDLE2_AMD_GEMM_V7_TAILK", "1") != "0"
 _WS_BYTES = 192 << 20
 _WS = {}
 
@@ -101,7 +104,8 @@ def _workspace(t):
 
 def _launch(layout, epi, a, lda, b, ldb, c, ldc, c2, ldc2, bias, M, Nn, K, beta=0.0, H=0, name="fwd"):
     v = _variant(name)
-    ws, ws_bytes = _workspace(a) if epi in (EPI_BF16, EPI_F32) and v in (0, 4, 5) else (0, 0)
+    tail = (epi in (EPI_BF16, EPI_F32) and v in (0, 4, 5)) or (V7_TAILK and epi == EPI_BF16 and v == V7_SPREAD)
+    ws, ws_bytes = _workspace(a) if tail else (0, 0)
     gm = GROUP_M if _GROUP_FORCED else PASS_GROUP_M.get(name, GROUP_M)
     N.native().gemm(layout, epi, a.data_ptr(), lda, b.data_ptr(), ldb, c.data_ptr(), ldc, N.ptr(c2), ldc2,
                     N.ptr(bias), M, Nn, K, float(beta), H, gm, v, ws, ws_bytes, N.stream())

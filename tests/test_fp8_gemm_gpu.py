@@ -26,7 +26,8 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("fa,fb,od", [(E4, E4, torch.bfloat16), (E5, E4, torch.bfloat16), (E4, E5, torch.bfloat16),
                                       (E4, E5, torch.float32)])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 512), (300, 520, 768)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 512), (300, 520, 768),
+                                   (1024, 1024, 4096), (1000, 1000, 4096)])   # 16 tiles: tail split-K, 4 slices
 def test_exact_integers(fa, fb, od, M, N, K):
     a = _ints((M, K), -4, 5, 1)          # |products| <= 16, sums < 2^24: exact in fp32
     b = _ints((N, K), -4, 5, 2)

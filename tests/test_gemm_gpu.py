@@ -116,10 +116,11 @@ def test_dgelu_epilogue(M, N, K, approx):
     assert _rel(G.mm_dgrad_dgelu(dy, w, h, approximate=approx), hr.grad) < 8e-3
 
 
-def test_gelu_mlp_node_matches_fp32():
-    """The fused GPT MLP node (torch_ops._GeluMLPFn): output and every gradient vs the fp32 composition."""
+def test_gelu_mlp_node_matches_fp32(monkeypatch):
+    """The fused GPT MLP node (torch_ops._GeluMLPFn, opt-in): output and every gradient vs the fp32 composition."""
     from paddle2_amd.ops import torch_ops as T
 
+    monkeypatch.setattr(T, "_FUSED_GELU_MLP", True)
     M, H, F4 = 1024, 512, 2048
     x = _rand(M, H, seed=26)
     w1, b1 = _rand(H, F4, seed=27, scale=H ** -0.5), _rand(F4, seed=28, scale=0.1)
@@ -324,3 +325,20 @@ def test_swiglu_mlp_node_matches_fp32(monkeypatch):
     assert _rel(y, yr) < 1e-2
     for got, ref in ((xi.grad, xr.grad), (a.grad, ar.grad), (b.grad, br.grad)):
         assert _rel(got, ref) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K,bias", [(4096, 5120, 5120, False), (4096, 5120, 5120, True), (1000, 1000, 2048, True),
+                                        (640, 4096, 1024, False)])
+def test_v7_tail_splitk_matches_fp32(M, N, K, bias, monkeypatch):
+    """Spread TN schedule with the tail split-K (a partial last wave of <= CUs / 2 tiles as K-slices + fp32 fix-up;
+    gemm7.hip SCHED bit 12): forward (+ bias) and dgrad vs fp32, and vs the same GEMM without the split."""
+    x, w, dy = _rand(M, K, seed=40), _rand(K, N, seed=41, scale=K ** -0.5), _rand(M, N, seed=42)
+    b = _rand(N, seed=43, scale=0.5) if bias else None
+    ref = x.float() @ w.float() + (b.float() if bias else 0.0)
+    y = G.mm_fwd(x, w, b)
+    assert _rel(y, ref) < 8e-3
+    dx = G.mm_dgrad(dy, w)
+    assert _rel(dx, dy.float() @ w.float().t()) < 8e-3
+    monkeypatch.setattr(G, "V7_TAILK", False)
+    y0 = G.mm_fwd(x, w, b)
+    assert _rel(y, y0) < 8e-3
