@@ -49,9 +49,22 @@ def require():
     return m
 
 
+_SYM = []
+
+
+def _sym_cls():
+    if not _SYM:
+        from ..static.graph import SymTensor
+
+        _SYM.append(SymTensor)
+    return _SYM[0]
+
+
 def use_native(t: torch.Tensor) -> bool:
-    """True when ``t`` lives on the GPU and the kernels must be used."""
-    if t.device.type != "cuda":
+    """True when ``t`` lives on the GPU and the kernels must be used.  Symbolic (static-graph recording) tensors
+    report the device the Program will run on but have no storage: never hand them to a kernel — the caller's
+    composite / graph-op path records them instead."""
+    if t.device.type != "cuda" or isinstance(t, _sym_cls()):
         return False
     if os.environ.get("PADDLE2_AMD_DISABLE_NATIVE") == "1":
         return False

@@ -1789,8 +1789,8 @@ def batch_norm_act(x, running_mean, running_var, weight=None, bias=None, trainin
         raise ValueError(f"fused batch norm supports act in (None, 'relu'), got {act!r}")
     relu = act == "relu"
     Cn = x.shape[-1]
-    ok = (x.device.type == "cuda" and x.dtype in _DT and x.is_contiguous() and Cn % (4 if x.dtype == torch.float32
-                                                                                     else 8) == 0
+    ok = (x.device.type == "cuda" and N.use_native(x) and x.dtype in _DT and x.is_contiguous()
+          and Cn % (4 if x.dtype == torch.float32 else 8) == 0
           and running_mean.dtype == torch.float32 and running_var.dtype == torch.float32
           and running_mean.is_contiguous() and running_var.is_contiguous()
           and (residual is None or (residual.shape == x.shape and residual.dtype == x.dtype)))

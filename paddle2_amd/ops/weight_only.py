@@ -32,8 +32,8 @@ def dequantize(w, scale, weight_dtype="int8", group_size=-1, dtype=torch.float32
 def _native_ok(x, w, weight_dtype, group_size):
     M, K = x.shape
     Nn = w.shape[0] * (2 if weight_dtype == "int4" else 1)
-    return (x.device.type == "cuda" and x.dtype == torch.bfloat16 and M <= 64 and K % 64 == 0 and Nn % 64 == 0
-            and group_size in (-1, 64, 128) and w.is_contiguous())
+    return (x.device.type == "cuda" and N.use_native(x) and x.dtype == torch.bfloat16 and M <= 64 and K % 64 == 0
+            and Nn % 64 == 0 and group_size in (-1, 64, 128) and w.is_contiguous())
 
 
 def weight_only_matmul(x, w, scale, weight_dtype="int8", group_size=-1, bias=None):

@@ -101,6 +101,11 @@ def main():
             "final_loss": round(float(loss), 4),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if torch.cuda.is_available() else None,
         }), flush=True)
+        from paddle2_amd.ops import conv_gemm as CG
+
+        for k, v in sorted(CG._ROUTE.items(), key=str):
+            print("conv routes:", k[0], "x", list(k[1]), "w", list(k[2]), "stride", list(k[3]),
+                  "native" if v else "miopen", file=sys.stderr)
     if world > 1:
         C.destroy_process_group()
 
