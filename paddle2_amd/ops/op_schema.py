@@ -1168,7 +1168,46 @@ def op_schema(name):
         args = []
     info = kernel_info(name)
     impl = getattr(fn, "__module__", "") + "." + getattr(fn, "__qualname__", getattr(fn, "__name__", ""))
-    return {"op": name, "args": args, "inplace": e.inplace, "impl": impl, "native_kernel": info["native_kernel"]}
+    from .registry import has_op
+
+    base = name[:-1] if name.endswith("_") else name
+    inplace_variant = base + "_" if (not name.endswith("_") and has_op(base + "_")) else None
+    return {"op": name, "args": args, "inplace": e.inplace, "inplace_variant": inplace_variant,
+            "inplace_of": base if name.endswith("_") and has_op(base) else None, "impl": impl,
+            "native_kernel": info["native_kernel"], "backward": backward_info(base)}
+
+
+# no gradient flows through these (reference backward.yaml has no *_grad entry for them): comparisons, logical /
+# bitwise ops, index-valued outputs, constants, random sources, shape / metadata queries, optimizer updates
+_NO_GRAD_PREFIX = ("equal", "not_equal", "less", "greater", "logical_", "bitwise_", "is", "arg", "full", "zeros",
+                   "ones", "empty", "arange", "linspace", "logspace", "eye", "randint", "randperm", "uniform",
+                   "gaussian", "bernoulli", "multinomial", "poisson", "shape", "numel", "rank", "accuracy", "auc",
+                   "one_hot", "unique", "nonzero", "histogram", "bincount", "searchsorted", "bucketize", "sign",
+                   "floor", "ceil", "round", "trunc", "c_", "send", "recv", "barrier", "all_", "reduce_scatter",
+                   "broadcast", "fake_", "dequantize", "quantize", "check_", "memcpy", "print", "top_p", "nms",
+                   "sgd_", "momentum_", "adam", "adamw", "lamb_", "rmsprop_", "adagrad_", "adamax_", "adadelta_",
+                   "merged_", "update_loss_scaling", "check_finite")
+
+
+def backward_info(name):
+    """How ``name`` is differentiated here (the reference declares it in backward.yaml as ``<name>_grad``):
+    ``none`` (not differentiable), ``prim_vjp`` (a primitive VJP rule over PIR, decomposition/vjp.py),
+    ``composite`` (decomposed into primitives that carry VJP rules, decomposition/rules.py) or ``autograd``
+    (dygraph autograd through the implementation: a torch.autograd.Function with a hand-written / native
+    backward, or differentiable torch ops)."""
+    from .. import decomposition as D
+    from ..decomposition import vjp as V
+
+    if name.startswith(_NO_GRAD_PREFIX):
+        return {"kind": "none", "grad_op": None}
+    key = "pd_op." + name
+    if key in V.VJP:
+        kind = "none" if V.VJP[key] is V._v_none else "prim_vjp"
+    elif D.has_rule(key):
+        kind = "composite"
+    else:
+        kind = "autograd"
+    return {"kind": kind, "grad_op": None if kind == "none" else name + "_grad"}
 
 
 def _to_meta(x):

@@ -137,3 +137,18 @@ def test_fake_quant_ops():
     assert list(sc.shape) == [4]
     back = paddle._C_ops.fake_channel_wise_dequantize_max_abs(qc, [sc], [8], 0)
     np.testing.assert_allclose(back.numpy(), x.numpy(), atol=float(sc.numpy().max()) / 127)
+
+
+def test_schema_backward_and_inplace_records():
+    """Per-op backward kind (reference backward.yaml <op>_grad) and inplace pairing."""
+    assert S.op_schema("exp")["backward"] == {"kind": "prim_vjp", "grad_op": "exp_grad"}
+    assert S.op_schema("softmax")["backward"]["kind"] == "composite"
+    assert S.op_schema("argmax")["backward"]["kind"] == "none"
+    assert S.op_schema("equal")["backward"]["grad_op"] is None
+    assert S.op_schema("flash_attn")["backward"]["kind"] in ("autograd", "composite")
+    rec = S.op_schema("relu")
+    assert rec["inplace_variant"] in (None, "relu_")
+    if R.has_op("relu_"):
+        assert S.op_schema("relu_")["inplace_of"] == "relu"
+    kinds = {S.op_schema(n)["backward"]["kind"] for n in R.list_ops()[:600:5]}
+    assert {"none", "autograd"} <= kinds
