@@ -63,7 +63,18 @@ def selu(x, scale=1.0507009873554804934193349852946, alpha=1.6732632423543772848
 
 
 def gelu(x, approximate=False, name=None):
-    return _wrap(F.gelu(x._t, approximate="tanh" if approximate else "none"))
+    """GPU bf16 / fp16: the native bias-activation kernel (csrc/kernels/fused_act.hip, erf or tanh form, its own
+    backward) instead of ATen's GeluCUDAKernel / GeluBackward (reference phi/kernels/gpu/gelu_kernel.cu)."""
+    t = x._t
+    if t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and t.dim() >= 1 and t.shape[-1] % 8 == 0:
+        from ...ops import _native as N
+        from ...ops import torch_ops as T
+
+        if not isinstance(t, T._DTensor) and N.use_native(t):
+            from ...ops import fused as FU
+
+            return _wrap(FU.bias_act(t, None, "gelu_tanh" if approximate else "gelu"))
+    return _wrap(F.gelu(t, approximate="tanh" if approximate else "none"))
 
 
 def silu(x, name=None):

@@ -14,13 +14,13 @@ DEVS = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
 def _ref_act(name, t):
     F = torch.nn.functional
     H = t.shape[-1] // 2
-    return {"gelu": F.gelu, "relu": torch.relu, "silu": F.silu, "identity": lambda v: v,
+    return {"gelu": F.gelu, "gelu_tanh": lambda v: F.gelu(v, approximate="tanh"), "relu": torch.relu, "silu": F.silu, "identity": lambda v: v,
             "swiglu": lambda v: F.silu(v[..., :H]) * v[..., H:],
             "geglu": lambda v: F.gelu(v[..., :H]) * v[..., H:]}[name](t)
 
 
 @pytest.mark.parametrize("dev", DEVS)
-@pytest.mark.parametrize("act", ["gelu", "relu", "silu", "identity", "swiglu", "geglu"])
+@pytest.mark.parametrize("act", ["gelu", "gelu_tanh", "relu", "silu", "identity", "swiglu", "geglu"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_bias_act_fwd_bwd(dev, act, dtype):
     g = torch.Generator().manual_seed(0)
@@ -63,3 +63,21 @@ def test_incubate_entry_points():
     vals = set(r._t.unique().tolist())
     assert vals <= {0.0, 2.0}
     assert IF.fused_dropout_add(paddle.ones([2, 8]), paddle.ones([2, 8]), p=0.5, training=False)._t.eq(2).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("approximate", [False, True])
+def test_functional_gelu_native_on_gpu(approximate):
+    """paddle.nn.functional.gelu on a bf16 GPU tensor runs the native kernel: forward and grad vs fp32."""
+    g = torch.Generator().manual_seed(1)
+    x0 = torch.randn(64, 256, generator=g)
+    x = paddle.to_tensor(x0.to("cuda", torch.bfloat16))
+    x.stop_gradient = False
+    y = paddle.nn.functional.gelu(x, approximate=approximate)
+    assert y._t.grad_fn is not None and "BiasAct" in type(y._t.grad_fn).__name__
+    y.sum().backward()
+    xr = x0.to(torch.bfloat16).float().requires_grad_()
+    yr = torch.nn.functional.gelu(xr, approximate="tanh" if approximate else "none")
+    yr.sum().backward()
+    torch.testing.assert_close(y._t.float().cpu(), yr.detach(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(x.grad._t.float().cpu(), xr.grad, rtol=2e-2, atol=2e-2)
