@@ -187,7 +187,7 @@ def eligible_3x3(t_nhwc, w, stride, padding, dilation, groups):
     return _pow2_64(w.shape[1]) and _pow2_64(w.shape[0]) and route("3x3", t_nhwc, w, [1, 1], [1, 1])
 
 
-def _time_fwd_bwd(fn, x, w, iters=2):
+def _time_fwd_bwd(fn, x, w, iters=5):
     from ..incubate.autotune import _bench
 
     with torch.enable_grad():

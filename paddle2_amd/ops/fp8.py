@@ -147,7 +147,7 @@ def mm_native(a, bT, inv_a, inv_b, out_dtype, bias=None):
     return c
 
 
-def _native_faster(nat, lib, iters=3):
+def _native_faster(nat, lib, iters=10):
     """Time both GEMM routes once on device events (after one untimed call each); False when the native kernel
     does not cover the problem."""
     from ..incubate.autotune import _bench
