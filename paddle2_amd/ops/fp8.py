@@ -211,7 +211,14 @@ class _FP8LinearFn(torch.autograd.Function):
         gq, gqT = cast(dy2, mg, transpose=True)                  # dY [M, N] and dY^T [N, M]
         dx = _mm(gq, wq.t(), mg.inv_scale, inv_w, out_dtype)     # [M, N] @ [N, K]
         dw = _mm(xqT, gqT.t(), inv_x, mg.inv_scale, wdt if wdt in (torch.bfloat16, torch.float16) else torch.float32)
-        db = dy2.sum(0, dtype=torch.float32).to(wdt) if has_b else None
+        db = None
+        if has_b:
+            # the native two-pass column sum (torch_ops.bias_grad): ATen's bf16 dim-0 reduce took 24.5 ms / 160
+            # calls of the GPT-3 13B fp8 step (profiles/r4_gpt13b_fp8_step_kernels.txt)
+            from .torch_ops import bias_grad
+
+            db = (bias_grad(dy2.contiguous()) if dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16)
+                  else dy2.sum(0, dtype=torch.float32)).to(wdt)
         mg.update()
         return dx.reshape(xshape), dw.to(wdt), db, None, None, None
 
