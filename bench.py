@@ -35,7 +35,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 
 
 def parse(argv=None):
-    ap = argparse.ArgumentParser()
+    ap = argparse.ArgumentParser(
+        formatter_class=argparse.RawDescriptionHelpFormatter,
+        epilog="""BASELINE.json configs on one 8-GPU node (T = torchrun --nnodes=1 --nproc-per-node 8 \\
+    --master-addr 127.0.0.1 --master-port 29500; or drop T and let --gpus 8 self-launch):
+  3  Llama-2 7B Fleet sharding-3 bf16 (the headline):
+       T bench.py --gpus 8
+  4  Llama-2 13B TP=2 x PP=4 hybrid (1F1B, Column/RowParallelLinear over xGMI):
+       T bench.py --gpus 8 --model llama2-13b --mp 2 --pp 4 --micro-batch 1 --seq-len 4096
+       (4 x pp = 16 micro-batches of 1 x 4096 per step by default: --accumulate-steps)
+  5  GPT-3 13B fp8 MFMA + sequence-parallel + sharding-3 (TP=2 x sharding 4):
+       T bench.py --gpus 8 --model gpt3-13b --fp8 --mp 2 --sp --seq-len 2048 --micro-batch 4
+  2  ResNet50 bf16 DP: scripts/bench_resnet50.py""")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
@@ -43,11 +54,17 @@ def parse(argv=None):
     ap.add_argument("--micro-batch", type=int, default=8,
                     help="sequences per GPU per step (8 x 4096 tokens fits one 288 GB MI355X)")
     ap.add_argument("--model", default="llama2-7b",
-                    choices=["llama2-7b", "llama2-13b", "tiny", "gpt3-13b", "gpt3-6.7b", "gpt3-1.3b"])
+                    choices=["llama2-7b", "llama2-13b", "tiny", "gpt3-13b", "gpt3-6.7b", "gpt3-1.3b", "gpt3-tiny"])
     ap.add_argument("--fp8", action="store_true", help="GPT configs: fp8 (e4m3/e5m2 delayed scaling) linears")
     ap.add_argument("--layers", type=int, default=None, help="DEBUG ONLY: override layer count (invalid for the metric)")
     ap.add_argument("--sharding-stage", type=int, default=3, choices=[0, 1, 2, 3],
                     help="0 = no sharding wrapper (DEBUG: not the metric's code path)")
+    ap.add_argument("--mp", type=int, default=1, help="tensor-parallel degree (Column/RowParallelLinear)")
+    ap.add_argument("--pp", type=int, default=1, help="pipeline-parallel degree (Llama: LlamaForCausalLMPipe)")
+    ap.add_argument("--vpp", type=int, default=1, help="virtual pipeline stages per rank (interleaved 1F1B)")
+    ap.add_argument("--pp-schedule", default="1F1B", choices=["1F1B", "FThenB", "VPP", "ZBH1"])
+    ap.add_argument("--sp", action="store_true", help="sequence parallelism inside the TP group (needs --mp > 1)")
+    ap.add_argument("--dp", type=int, default=1, help="data-parallel degree (the rest of the world is sharding)")
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--accumulate-steps", type=int, default=1,
                     help="micro-batches per optimizer step (gradient accumulation into the fp32 main grads)")
@@ -101,35 +118,65 @@ def main():
 
             autotune.enable_routing_autotune(os.path.join(tempfile.gettempdir(), f"gemm_route_{os.getpid()}.json"))
 
+    mp, pp, vpp, dp = args.mp, args.pp, args.vpp, args.dp
+    if world % (mp * pp * dp):
+        print(f"error: world {world} is not a multiple of mp {mp} x pp {pp} x dp {dp}", file=sys.stderr)
+        sys.exit(2)
+    sh = world // (mp * pp * dp)   # the rest of the world shards the model / optimizer state
+    if args.sp and mp == 1:
+        print("error: --sp needs --mp > 1", file=sys.stderr)
+        sys.exit(2)
+    if pp > 1 and (args.model.startswith("gpt3") or sh > 1):
+        print("error: --pp runs the Llama pipeline form without sharding (mp x pp x dp == world)", file=sys.stderr)
+        sys.exit(2)
+    if dp > 1 and sh > 1 and args.sharding_stage > 0:
+        print("error: --dp > 1 with sharding: use --dp world (pure DP, --sharding-stage 0) or --dp 1", file=sys.stderr)
+        sys.exit(2)
+    acc = max(1, args.accumulate_steps)
+    if pp > 1 and args.accumulate_steps == 1:
+        acc = 4 * pp * vpp   # micro-batches per step: 1F1B bubble (pp-1)/(acc+pp-1) = 16 % at pp 4
     strategy = fleet.DistributedStrategy()
-    strategy.hybrid_configs = {"dp_degree": 1, "mp_degree": 1, "pp_degree": 1, "sharding_degree": world}
+    strategy.hybrid_configs = {"dp_degree": dp, "mp_degree": mp, "pp_degree": pp, "sharding_degree": sh}
+    if pp > 1:
+        strategy.pipeline_configs = {"accumulate_steps": acc, "micro_batch_size": args.micro_batch,
+                                     "schedule_mode": args.pp_schedule if vpp == 1 else "VPP"}
     fleet.init(is_collective=True, strategy=strategy)
     paddle.seed(1234)  # same init on every rank (stage 3 shards one replica)
 
     is_gpt = args.model.startswith("gpt3")
+    extra = {"tensor_parallel_degree": mp, "sequence_parallel": bool(args.sp)}
     if is_gpt:
         from paddle2_amd.models import GPTConfig, GPTForCausalLM, gpt_flops_per_token
 
-        cfg = {"gpt3-13b": GPTConfig.gpt3_13b, "gpt3-6.7b": GPTConfig.gpt3_6_7b,
-               "gpt3-1.3b": GPTConfig.gpt3_1_3b}[args.model](use_fp8=args.fp8)
+        cfg = {"gpt3-13b": GPTConfig.gpt3_13b, "gpt3-6.7b": GPTConfig.gpt3_6_7b, "gpt3-1.3b": GPTConfig.gpt3_1_3b,
+               "gpt3-tiny": GPTConfig.tiny}[args.model](use_fp8=args.fp8, **extra)
     elif args.model == "llama2-7b":
-        cfg = LlamaConfig.llama2_7b()
+        cfg = LlamaConfig.llama2_7b(**extra)
     elif args.model == "llama2-13b":
-        cfg = LlamaConfig.llama2_13b()
+        cfg = LlamaConfig.llama2_13b(**extra)
     else:
-        cfg = LlamaConfig.tiny()
+        cfg = LlamaConfig.tiny(**extra)
     cfg.max_position_embeddings = max(cfg.max_position_embeddings, args.seq_len)
     if args.layers:
         cfg.num_hidden_layers = args.layers
     cfg.recompute = args.recompute
 
-    model = GPTForCausalLM(cfg) if is_gpt else LlamaForCausalLM(cfg)
+    if pp > 1:
+        from paddle2_amd.models import LlamaForCausalLMPipe
+
+        model = LlamaForCausalLMPipe(cfg, num_virtual_pipeline_stages=vpp if vpp > 1 else None)
+    else:
+        model = GPTForCausalLM(cfg) if is_gpt else LlamaForCausalLM(cfg)
     decay = {p.name for n, p in model.named_parameters() if "norm" not in n}
     opt = paddle.optimizer.AdamW(learning_rate=3e-4, beta1=0.9, beta2=0.95, epsilon=1e-8,
                                  parameters=model.parameters(), weight_decay=0.1,
                                  apply_decay_param_fun=lambda n: n in decay,
                                  grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0), multi_precision=True)
-    if args.sharding_stage > 0:
+    if pp > 1 or (mp > 1 and args.sharding_stage == 0) or dp > 1 and args.sharding_stage == 0:
+        # hybrid TP x PP (x DP): the fleet wrappers (PipelineParallel 1F1B / TensorParallel, HybridParallelOptimizer)
+        model = fleet.distributed_model(model)
+        opt = fleet.distributed_optimizer(opt)
+    elif args.sharding_stage > 0:
         from paddle2_amd.distributed.sharding import group_sharded_parallel
 
         level = {1: "os", 2: "os_g", 3: "p_g_os"}[args.sharding_stage]
@@ -138,13 +185,22 @@ def main():
 
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     b, s = args.micro_batch, args.seq_len
-    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    hcg = fleet.get_hybrid_communicate_group()
+    # the data stream: one per data-parallel replica (dp x sharding ranks read different batches; the TP and PP
+    # ranks of one replica read the same one)
+    data_rank = hcg.get_data_parallel_rank() * sh + hcg.get_sharding_parallel_rank()
+    gen = torch.Generator(device=dev).manual_seed(1000 + data_rank)
     # a fresh batch per step (pre-generated, outside the timed region); 8 x 4097 int64 = 262 KB each
-    acc = max(1, args.accumulate_steps)
-    batches = [torch.randint(0, cfg.vocab_size, (b, s + 1), generator=gen, device=dev)
-               for _ in range((args.warmup + args.steps) * acc)]
+    nb = args.warmup + args.steps
+    if pp > 1:
+        batches = [torch.randint(0, cfg.vocab_size, (b * acc, s + 1), generator=gen, device=dev) for _ in range(nb)]
+    else:
+        batches = [torch.randint(0, cfg.vocab_size, (b, s + 1), generator=gen, device=dev) for _ in range(nb * acc)]
 
     def step(i):
+        if pp > 1:   # one pipelined step over acc micro-batches (1F1B), optimizer step and clear inside
+            ids = paddle.Tensor._wrap(batches[i])
+            return model.train_batch([ids[:, :-1], ids[:, 1:]], opt)
         for j in range(acc):
             ids = paddle.Tensor._wrap(batches[i * acc + j])
             loss = model(ids[:, :-1], labels=ids[:, 1:])
@@ -179,16 +235,29 @@ def main():
     elapsed = float(el.item())
     final_loss = float(loss)
 
-    tokens = b * s * acc * args.steps * world
+    replicas = dp * sh   # data-parallel replicas: each trains its own b x acc sequences per step
+    tokens = b * s * acc * args.steps * replicas
     tps = tokens / elapsed
     ms = elapsed / args.steps * 1000.0
     fpt = gpt_flops_per_token(cfg, s) if is_gpt else llama_flops_per_token(cfg, s)
     mfu = tps / world * fpt / 2.5e15
     if rank == 0:
-        par = f"sharding{args.sharding_stage}x{world}" if args.sharding_stage > 0 else f"single(no-sharding,debug)x{world}"
+        parts = ([f"mp{mp}" + ("+sp" if args.sp else "")] if mp > 1 else []) + \
+            ([f"pp{pp}" + (f"v{vpp}" if vpp > 1 else "") + f"({args.pp_schedule if vpp == 1 else 'VPP'})"]
+             if pp > 1 else []) + ([f"dp{dp}"] if dp > 1 else [])
+        if sh > 1 or not parts:
+            parts.append(f"sharding{args.sharding_stage}({sh})" if args.sharding_stage > 0
+                         else f"single(no-sharding,debug)({sh})")
+        par = "x".join(parts)
+        names = {"llama2-7b": "Llama-2-7B", "llama2-13b": "Llama-2-13B", "gpt3-13b": "GPT-3 13B",
+                 "gpt3-6.7b": "GPT-3 6.7B", "gpt3-1.3b": "GPT-3 1.3B", "tiny": "tiny-llama(debug)",
+                 "gpt3-tiny": "tiny-gpt(debug)"}
+        if args.model == "llama2-7b" and mp == pp == dp == 1 and args.sharding_stage == 3:
+            metric = "tokens/sec (whole node) Llama-2-7B Fleet sharding-3 bf16"   # BASELINE.json's headline
+        else:
+            metric = f"tokens/sec (whole node) {names[args.model]} {'fp8' if args.fp8 else 'bf16'} {' x '.join(parts)}"
         out = {
-            "metric": ("tokens/sec (whole node) Llama-2-7B Fleet sharding-3 bf16" if args.model == "llama2-7b"
-                       else f"tokens/sec (whole node) {args.model} {'fp8' if args.fp8 else 'bf16'}"),
+            "metric": metric,
             "value": round(tps, 2),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -201,7 +270,7 @@ def main():
             "dtype": "fp8(e4m3/e5m2)+bf16" if (is_gpt and args.fp8) else "bf16",
             "data": "synthetic (fresh uniform random token ids per step), random-init weights",
             "config": {"model": args.model if not args.layers else f"{args.model}-L{args.layers}(debug)",
-                       "global_batch": b * acc * world, "seq_len": s, "micro_batch_per_gpu": b,
+                       "global_batch": b * acc * replicas, "seq_len": s, "micro_batch_per_gpu": b,
                        "accumulate_steps": acc,
                        "parallelism": par, "layers": cfg.num_hidden_layers},
             "mfu_vs_2.5PF_dense": round(mfu, 4),

@@ -152,6 +152,12 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   // partial wave's tail_cap tiles run as ksplit K-slices, one per workgroup (slot = tail tile * ksplit + slice),
   // into fp32 slabs that v7_tail_reduce_kernel sums (an in-loop tail unit spilled 700 B/lane to scratch)
   constexpr bool TSK = (SCHED & 4096) != 0;
+  // experiment bits (variant 64 + SCHED, bf16 epilogue only): 8192 = epilogue stores ablated (accumulators kept
+  // live, the tile's output never written) — the cost of the store burst; 16384 = XCD-phase stagger: the
+  // workgroups of XCD x sleep x * p.kchunk * ~8k cycles before their first tile, so the XCDs' tile boundaries (and
+  // their epilogue store bursts) fall at different times
+  constexpr bool NOST = (SCHED & 8192) != 0;
+  constexpr bool XDLY = (SCHED & 16384) != 0;
   constexpr bool SWI = EPI == kEpiSwiGLU;
   __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
   const unsigned sbase = (unsigned)(size_t)(lds_char*)smem_raw;
@@ -164,6 +170,10 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   const int ntile = TSK ? (slot < p.tail_cap * p.ksplit ? 1 : 0) : (slot < whole ? (whole - slot + G - 1) / G : 0);
   if (ntile == 0) return;
 
+  if constexpr (XDLY) {
+    const int xs = (blockIdx.x & 7) * p.kchunk;
+    for (int i = 0; i < xs; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -496,7 +506,14 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
     } else if constexpr (EPI != kEpiRope) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        if constexpr (X4 && EPI == kEpiBF16) {
+        if constexpr (NOST) {
+          // never true at run time (ablation): the stores are skipped, the accumulators stay live
+          if (p.beta == -1234.5f) epilogue_v7_x4<NTS>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) asm volatile("" ::"a"(acc[h][i][j]));
+        } else if constexpr (X4 && EPI == kEpiBF16) {
           // interior tile, 16-B aligned rows: the widened stores; otherwise the element-checked epilogue
           if ((ctm + 1) * BM <= p.M && (ctn + 1) * BN <= p.N && (p.ldc & 7) == 0 && ((size_t)p.C & 15) == 0)
             epilogue_v7_x4<NTS>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
@@ -540,6 +557,10 @@ bool pd_gemm_v7(const pd::gm::Params& p_in, int layout, int epi, int sched, int 
   if (a_bytes <= 0 || b_bytes <= 0 || a_bytes >= 0x7fffffffL || b_bytes >= 0x7fffffffL) return false;
   if (p.ldc % 4 || (size_t)p.C % 16 || (p.C2 && (p.ldc2 % 4 || (size_t)p.C2 % 16))) return false;
   const dim3 grid(std::min(p.tiles_m * p.tiles_n, cus));
+  if (sched & 16384) {   // XCD-stagger experiment: the per-XCD delay unit from the environment
+    const char* d = getenv("PD_GEMM_XCD_DELAY");
+    p.kchunk = d ? atoi(d) : 1;
+  }
   // SCHED 0..3 = variants 7..10; the experiment configurations (cache policy / priority level, variant 64 + cfg)
   // are instantiated for the bf16 epilogue only
 #define PD_V7_CASE(E, S) \
@@ -600,6 +621,7 @@ bool pd_gemm_v7(const pd::gm::Params& p_in, int layout, int epi, int sched, int 
       PD_V7_CASE(kEpiBF16, 42) PD_V7_CASE(kEpiBF16, 66) PD_V7_CASE(kEpiBF16, 86) PD_V7_CASE(kEpiBF16, 20)
       PD_V7_CASE(kEpiBF16, 14) PD_V7_CASE(kEpiBF16, 128) PD_V7_CASE(kEpiBF16, 130) PD_V7_CASE(kEpiBF16, 194)
       PD_V7_CASE(kEpiBF16, 384) PD_V7_CASE(kEpiBF16, 896) PD_V7_CASE(kEpiBF16, 1408) PD_V7_CASE(kEpiBF16, 1920)
+      PD_V7_CASE(kEpiBF16, 384 | 8192) PD_V7_CASE(kEpiBF16, 384 | 16384)
       default: return false;
     }
     return true;

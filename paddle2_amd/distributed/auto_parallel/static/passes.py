@@ -138,6 +138,13 @@ def fuse_allreduce_pass(dmp, bucket_mb=256):
     if not params:
         return None
     fused = _FusedAllReduce(params, dmp._dm, tuple(sorted(dims)), bucket_mb << 20)
+    merge = [o for o in prog.ops if o.kind == "call" and "pre_step" in o.attrs]
+    if merge:
+        # gradient merge: the gradients accumulate over k micro-steps, so the sum runs once, at the k-step boundary
+        # just before the optimizer step (reducing the accumulated grad every micro-step would re-add the sums of
+        # earlier micro-steps world-fold)
+        merge[0].attrs["pre_step"].append(fused)
+        return fused
     i = next(k for k, o in enumerate(prog.ops) if o.kind == "backward")
     prog.ops.insert(i + 1, Op("call", None, (), {}, [], {"fn": fused, "name": "fused_allreduce_grads"}))
     return fused
@@ -149,16 +156,21 @@ def gradient_merge_pass(dmp, k_steps, avg=True):
     from ....static.graph import Op
 
     prog = dmp.program
+    # an already-applied fused DP all-reduce moves from behind the backward to the k-step boundary
+    pre = [o.attrs["fn"] for o in prog.ops if o.kind == "call" and o.attrs.get("name") == "fused_allreduce_grads"]
+    prog.ops = [o for o in prog.ops if not (o.kind == "call" and o.attrs.get("name") == "fused_allreduce_grads")]
     for i, op in enumerate(prog.ops):
         if op.kind != "optimize":
             continue
         opt = op.attrs["optimizer"]
         state = {"n": 0}
 
-        def step(env, opt=opt, state=state):
+        def step(env, opt=opt, state=state, pre=pre):
             state["n"] += 1
             if state["n"] % k_steps:
                 return
+            for f in pre:   # gradient sums over the DP groups (fuse_allreduce_pass), once per merged step
+                f(env)
             with torch.no_grad():
                 if avg:
                     for p in opt._parameter_list:
@@ -168,7 +180,7 @@ def gradient_merge_pass(dmp, k_steps, avg=True):
             opt.clear_grad(set_to_zero=False)
 
         prog.ops[i] = Op("call", None, (), {}, [], {"fn": step, "name": f"gradient_merge_k{k_steps}",
-                                                     "optimizer": opt})
+                                                     "optimizer": opt, "pre_step": pre})
     return prog
 
 

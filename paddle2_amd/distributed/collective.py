@@ -209,6 +209,39 @@ def pg_status():
     return dict(_PG_STATUS)
 
 
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rendezvous_store(rank, world, tout):
+    """The default group's rendezvous store (reference paddle/phi/core/distributed/store/store_utils.cc:31-75).
+
+    * Launched by torch.distributed.run / torchrun: the elastic agent already hosts a c10d TCPStore on MASTER_PORT
+      (TORCHELASTIC_USE_AGENT_STORE=True), so every rank — rank 0 included — connects to it as a client, under a
+      key prefix of its own so nothing collides with the agent's keys.
+    * Otherwise the framework's native C++ TCPStore (csrc/runtime/tcp_store.cpp), rank 0 hosting the daemon —
+      the default; PADDLE2_AMD_STORE=torch selects torch's TCPStore instead."""
+    addr, port = os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"])
+    if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
+        _PG_STATUS["store"] = "agent"
+        base = dist.TCPStore(addr, port, world, False, timeout=tout)
+        return dist.PrefixStore("paddle2_amd/default_pg", base)
+    if os.environ.get("PADDLE2_AMD_STORE", "native") == "torch" or os.environ.get("PADDLE2_AMD_NATIVE_STORE") == "0":
+        _PG_STATUS["store"] = "torch"
+        return dist.TCPStore(addr, port, world, rank == 0, timeout=tout)
+    from .store import TorchStore, create_or_get_global_tcp_store
+
+    _PG_STATUS["store"] = "native"
+    return TorchStore(create_or_get_global_tcp_store(rank, world, host=addr, port=port,
+                                                     timeout=tout.total_seconds()))
+
+
 def init_parallel_env(backend=None, timeout_s=None):
     """Rendezvous (TCPStore on the master) + default RCCL/gloo process group (parallel.py:978)."""
     global _default_group, _initialized
@@ -234,12 +267,15 @@ def init_parallel_env(backend=None, timeout_s=None):
         from ..framework.place import set_device
 
         set_device(f"gpu:{local}")
-    if world > 1:
+    # PADDLE2_AMD_STAGE3_FORCE_COMM=1 (sharding.group_sharded.force_comm): a 1-rank job gets a real process group
+    # too, so its sharding collectives run through the communicator
+    solo_pg = world == 1 and os.environ.get("PADDLE2_AMD_STAGE3_FORCE_COMM", "0") == "1"
+    if world > 1 or solo_pg:
         if "MASTER_ADDR" not in os.environ:
             master = os.environ.get("PADDLE_MASTER", "127.0.0.1:29500")
             host, port = master.rsplit(":", 1)
             os.environ["MASTER_ADDR"] = host
-            os.environ["MASTER_PORT"] = port
+            os.environ["MASTER_PORT"] = port if not solo_pg else str(_free_port())
         os.environ.setdefault("MASTER_PORT", "29500")
         if not dist.is_initialized():
             tout = datetime.timedelta(seconds=timeout_s or int(os.environ.get("FLAGS_comm_timeout_s", "1800")))
@@ -248,16 +284,8 @@ def init_parallel_env(backend=None, timeout_s=None):
                 backend = rccl_pg.register()
             elif backend == "nccl" and torch.cuda.is_available():
                 kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
-            if os.environ.get("PADDLE2_AMD_NATIVE_STORE", "0") == "1":
-                # rendezvous through the native C++ TCPStore (csrc/runtime/tcp_store.cpp)
-                from .store import TorchStore, create_or_get_global_tcp_store
-
-                st = create_or_get_global_tcp_store(rank, world, timeout=tout.total_seconds())
-                kw["store"] = TorchStore(st)
-            elif native_pg:
-                # an explicit store: the start-up check below may have to re-create the default group on it
-                kw["store"] = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
-                                            rank == 0, timeout=tout)
+            # an explicit store: the start-up check below may have to re-create the default group on it
+            kw["store"] = _rendezvous_store(rank, world, tout)
             dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=tout, **kw)
             if native_pg:
                 _check_native_pg(kw["store"], rank, world, tout)

@@ -222,6 +222,12 @@ class CommContext:
         if not batch:
             return
         if self.backend == "nccl":  # one RCCL group launch (ncclGroupStart/End) for the whole batch
+            from .rccl_pg import ProcessGroupRCCL
+
+            if isinstance(self.pg, ProcessGroupRCCL):
+                for w in self.pg.batch_p2p([(kind == "send", t, peer) for kind, t, peer in batch]):
+                    w.wait()
+                return
             dev = torch.device(self._device())
             self.pg._start_coalescing(dev)
             for kind, t, peer in batch:
@@ -252,11 +258,17 @@ class CommContext:
 
 
 class NCCLCommContext(CommContext):
-    """RCCL communicator (torch's ProcessGroupNCCL on ROCm): unique id exchanged through the store."""
+    """RCCL communicator: the framework's own ProcessGroupRCCL (csrc/comm/rccl_group.cpp — unique id exchanged
+    through the store, own comm stream and event fences), as the default process group is; PADDLE2_AMD_PG=c10d
+    selects torch's ProcessGroupNCCL for both (reference comm_context_manager.cc:61-122 CreateNCCLCommContext)."""
 
     backend = "nccl"
 
     def _make_pg(self, store, rank, size, timeout):
+        from . import rccl_pg
+
+        if rccl_pg.enabled():
+            return rccl_pg.ProcessGroupRCCL(store, rank, size, timeout, prefix=f"ctx/{self.key}")
         opts = dist.ProcessGroupNCCL.Options()
         opts._timeout = timeout
         return dist.ProcessGroupNCCL(store, rank, size, opts)

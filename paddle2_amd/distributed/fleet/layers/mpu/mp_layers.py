@@ -40,6 +40,36 @@ def _init_ctx(world):
     return contextlib.nullcontext()
 
 
+class _Fp8Local:
+    """fp8 local GEMM of a tensor-parallel linear (``fp8=True`` or a DelayedScaling recipe): the shard's matmul
+    runs as e4m3 forward / e5m2-gradient GEMMs with per-layer delayed scaling (ops/fp8.py fp8_linear, the
+    Float8Linear recipe) while the TP / SP collectives around it stay bf16 — each rank scales its own weight shard
+    and gradient, the gathered activation is the same bytes on every rank (reference: fp8 GEMMs inside
+    ColumnSequenceParallelLinear / RowSequenceParallelLinear, sequence_parallel_utils.py:429,564)."""
+
+    def _init_fp8(self, fp8):
+        self._fp8 = fp8
+        self._fp8_metas = None
+
+    def _fp8_on(self):
+        return bool(getattr(self, "_fp8", None))
+
+    def _fp8_mm(self, x, b):
+        from .....ops import fp8 as F8
+
+        dev = x.device
+        if self._fp8_metas is None or self._fp8_metas[0].amax.device != dev:
+            from .....incubate.fp8 import DelayedScaling
+
+            r = self._fp8 if isinstance(self._fp8, DelayedScaling) else DelayedScaling()
+            bwd = F8.E5M2 if r.fp8_format == "HYBRID" else F8.E4M3
+            self._fp8_metas = (F8.FP8TensorMeta(F8.E4M3, r.amax_history_len, r.margin, dev),
+                               F8.FP8TensorMeta(F8.E4M3, r.amax_history_len, r.margin, dev),
+                               F8.FP8TensorMeta(bwd, r.amax_history_len, r.margin, dev))
+        mx, mw, mg = self._fp8_metas
+        return F8.fp8_linear(x, self.weight._t, b, mx, mw, mg)
+
+
 class VocabParallelEmbedding(nn.Layer):
     def __init__(self, num_embeddings, embedding_dim, weight_attr=None, mp_group=None, name=None):
         super().__init__()
@@ -69,10 +99,11 @@ class VocabParallelEmbedding(nn.Layer):
         return out
 
 
-class ColumnParallelLinear(nn.Layer):
+class ColumnParallelLinear(nn.Layer, _Fp8Local):
     def __init__(self, in_features, out_features, weight_attr=None, has_bias=None, gather_output=True,
-                 fuse_matmul_bias=False, mp_group=None, name=None):
+                 fuse_matmul_bias=False, mp_group=None, name=None, fp8=None):
         super().__init__()
+        self._init_fp8(fp8)
         self.model_parallel_group, self.world_size, self.rank = _mp_info(mp_group)
         self.is_mp = self.world_size > 1
         assert out_features % self.world_size == 0, "out_features must be divisible by mp degree"
@@ -95,7 +126,10 @@ class ColumnParallelLinear(nn.Layer):
 
     def forward(self, x):
         b = None if self.bias is None else self.bias._t
-        if self.is_mp:
+        if self._fp8_on():
+            xt = mp_ops._Identity.apply(x._t, self.model_parallel_group) if self.is_mp else x._t
+            y = self._fp8_mm(xt, b)
+        elif self.is_mp:
             y = mp_ops._ColumnLinear.apply(x._t, self.weight._t, b, self.model_parallel_group)
         else:
             from .....ops import torch_ops as T
@@ -107,10 +141,11 @@ class ColumnParallelLinear(nn.Layer):
         return out
 
 
-class RowParallelLinear(nn.Layer):
+class RowParallelLinear(nn.Layer, _Fp8Local):
     def __init__(self, in_features, out_features, weight_attr=None, has_bias=True, input_is_parallel=False,
-                 fuse_matmul_bias=False, mp_group=None, name=None):
+                 fuse_matmul_bias=False, mp_group=None, name=None, fp8=None):
         super().__init__()
+        self._init_fp8(fp8)
         self.model_parallel_group, self.world_size, self.rank = _mp_info(mp_group)
         self.is_mp = self.world_size > 1
         assert in_features % self.world_size == 0, "in_features must be divisible by mp degree"
@@ -132,7 +167,7 @@ class RowParallelLinear(nn.Layer):
         from .....ops import torch_ops as T
 
         # the Linear node (native GEMMs, fp32 main-grad accumulation) then the mp all-reduce of the partials
-        y = _wrap(T.linear(x._t, self.weight._t))
+        y = _wrap(self._fp8_mm(x._t, None) if self._fp8_on() else T.linear(x._t, self.weight._t))
         if self.is_mp:
             y = mp_ops._mp_allreduce(y, group=self.model_parallel_group)
         if self.bias is not None:

@@ -15,7 +15,7 @@ from .... import nn
 from ....framework.tensor import Tensor
 from ....nn import initializer as I
 from ..layers.mpu import mp_ops
-from ..layers.mpu.mp_layers import _init_ctx, _mp_info
+from ..layers.mpu.mp_layers import _Fp8Local, _init_ctx, _mp_info
 
 _wrap = Tensor._wrap
 
@@ -135,10 +135,11 @@ def register_sequence_parallel_allreduce_hooks(model, accumulation_steps=1, fuse
         p._t.register_post_accumulate_grad_hook(hook)
 
 
-class ColumnSequenceParallelLinear(nn.Layer):
+class ColumnSequenceParallelLinear(nn.Layer, _Fp8Local):
     def __init__(self, in_features, out_features, weight_attr=None, has_bias=None, gather_output=True,
-                 fuse_matmul_bias=False, mp_group=None, name=None):
+                 fuse_matmul_bias=False, mp_group=None, name=None, fp8=None):
         super().__init__()
+        self._init_fp8(fp8)
         self.model_parallel_group, self.world_size, self.rank = _mp_info(mp_group)
         assert not gather_output, "ColumnSequenceParallelLinear requires gather_output=False"
         assert out_features % self.world_size == 0
@@ -161,13 +162,18 @@ class ColumnSequenceParallelLinear(nn.Layer):
 
     def forward(self, x):
         b = None if self.bias is None else self.bias._t
+        if self._fp8_on():
+            # all-gather of the sequence shards (bwd: reduce-scatter of dX), then the fp8 GEMM on the full sequence
+            xf = _AllGather.apply(x._t, self.model_parallel_group) if self.world_size > 1 else x._t
+            return _wrap(self._fp8_mm(xf, b))
         return _wrap(mp_ops._SeqColumnLinear.apply(x._t, self.weight._t, b, self.model_parallel_group))
 
 
-class RowSequenceParallelLinear(nn.Layer):
+class RowSequenceParallelLinear(nn.Layer, _Fp8Local):
     def __init__(self, in_features, out_features, weight_attr=None, has_bias=True, input_is_parallel=True,
-                 fuse_matmul_bias=False, mp_group=None, name=None):
+                 fuse_matmul_bias=False, mp_group=None, name=None, fp8=None):
         super().__init__()
+        self._init_fp8(fp8)
         self.model_parallel_group, self.world_size, self.rank = _mp_info(mp_group)
         assert input_is_parallel, "RowSequenceParallelLinear requires input_is_parallel=True"
         assert in_features % self.world_size == 0
@@ -188,7 +194,12 @@ class RowSequenceParallelLinear(nn.Layer):
             self.bias = None
 
     def forward(self, x):
-        y = mp_ops._SeqRowLinear.apply(x._t, self.weight._t, self.model_parallel_group)
+        if self._fp8_on():
+            # fp8 GEMM of the partial sums, then their reduce-scatter onto the sequence shards (bwd: all-gather)
+            y = self._fp8_mm(x._t, None)
+            y = _ReduceScatter.apply(y, self.model_parallel_group) if self.world_size > 1 else y
+        else:
+            y = mp_ops._SeqRowLinear.apply(x._t, self.weight._t, self.model_parallel_group)
         if self.bias is not None:
             y = y + self.bias._t
         return _wrap(y)

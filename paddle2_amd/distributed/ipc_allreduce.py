@@ -255,6 +255,11 @@ def maybe_all_reduce(t, group=None):
     check passed.  Returns True if it handled the tensor."""
     if not t.is_cuda:
         return False
+    # never inside a HIP-graph capture: the barrier epoch is a host value baked into the captured launch (every
+    # replay after the first would pass the barrier at once and read peers' stale buffers) and poll() would record
+    # event queries into the graph — captured collectives stay on RCCL, which graphs replay correctly
+    if torch.cuda.is_current_stream_capturing():
+        return False
     mode = _mode()
     if mode == "auto":
         comm = _AUTO["comm"]

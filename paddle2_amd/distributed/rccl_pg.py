@@ -20,9 +20,11 @@ The communicators, streams, event fences and tasks are C++ (csrc/comm/rccl_group
 * ``batch_isend_irecv`` (module function) coalesces p2p ops into one RCCL group, which a same-stream
   send-then-recv pair needs to not deadlock.
 
-Selected with ``PADDLE2_AMD_PG=rccl`` (collective.init_parallel_env passes backend "pdrccl" to
-init_process_group); the default stays torch's ProcessGroupNCCL until a multi-GPU run has validated this
-group (only the 1-rank path runs on this project's single-GPU test box).
+This group is the default for GPU jobs: collective.init_parallel_env passes backend "pdrccl" to
+init_process_group, then ``canary`` checks every collective kind on the real devices and, if any rank's check
+fails, every rank falls back to torch's ProcessGroupNCCL on the same store.  ``PADDLE2_AMD_PG=rccl`` demands this
+group (a failed check raises instead of falling back); ``PADDLE2_AMD_PG=c10d`` opts out.  The communicator
+registry (comm_context.NCCLCommContext) creates this group too.
 """
 from __future__ import annotations
 

@@ -39,6 +39,16 @@ from .. import collective as C
 _EMPTY = {}
 
 
+def force_comm():
+    """PADDLE2_AMD_STAGE3_FORCE_COMM=1: a 1-rank sharding group still takes the N > 1 code path — real
+    all_gather_into_tensor / reduce_scatter_tensor on the group's process group (comm stream included), the fp32
+    flat-gradient pool, prefetch and retire_rs — so one GPU exercises what an 8-GPU node runs (collective.py then
+    initialises a 1-rank process group)."""
+    import os
+
+    return os.environ.get("PADDLE2_AMD_STAGE3_FORCE_COMM", "0") == "1"
+
+
 def _empty(dtype, device):
     key = (dtype, device)
     if key not in _EMPTY:
@@ -105,6 +115,8 @@ class _Unit:
         self.stage = stage
         self.N = group.nranks
         self.rank = group.rank
+        # collectives on (N > 1, or forced on a 1-rank group that has a process group): see force_comm
+        self.comm = self.N > 1 or (force_comm() and getattr(group, "pg", None) is not None)
         p0 = self.params[0]._t
         self.dtype, self.device = p0.dtype, p0.device
         self.numels = [p._t.numel() for p in self.params]
@@ -161,7 +173,7 @@ class _Unit:
     def gather(self, async_op=True):
         if self.full is not None or self.work is not None:
             return
-        if self.N == 1:
+        if not self.comm:
             # the single shard IS the full flat buffer: bind the parameters to it, no copy
             self.full = self.shard
             self._bind(self.shard)
@@ -208,7 +220,7 @@ class _Unit:
     def grad_target(self, i):
         """-> (fp32 view of param i's gradient slot, beta): beta 0 = overwrite, 1 = accumulate."""
         o, n, shp = self.offsets[i], self.numels[i], self.shapes[i]
-        if self.N == 1:
+        if not self.comm:
             buf = self.grad_shard
             beta = 0 if (self.grad_clean and i not in self.written) else 1
         else:
@@ -229,6 +241,12 @@ class _Unit:
         g = p._t.grad
         if g is None:
             return
+        spg = self.model._sp_group if self.model is not None else None
+        if spg is not None and getattr(p, "sequence_parallel", False):
+            # a sequence-parallel parameter (norm weights / row-linear bias inside TP + SP) saw only this rank's
+            # sequence shard: its gradient is the sum over the mp group (HybridParallelOptimizer's SP sync, done
+            # here because stage 3 consumes the gradient before any optimizer hook runs)
+            dist.all_reduce(g, group=spg.pg)
         view, beta = self.grad_target(i)
         if beta == 0:
             view.copy_(g.reshape(view.shape))
@@ -245,7 +263,7 @@ class _Unit:
             buf[self.total:].zero_()
 
     def reduce_grads(self):
-        if self.N == 1:
+        if not self.comm:
             if self.grad_clean:
                 self._zero_unwritten(self.grad_shard)
                 self.grad_clean = False
@@ -294,7 +312,7 @@ class _Unit:
         """Stage 1/2: all-gather the updated slices into the replicated parameters."""
         if self.stage == 3:
             return
-        if self.N == 1:
+        if not self.comm:
             self.full[: self.S].copy_(self.shard)
             return
         dist.all_gather_into_tensor(self.full, self.shard, group=self.group.pg)
@@ -326,6 +344,19 @@ class GroupShardedModel(Layer):
             # gradients and optimizer state are still reduce-scattered / sharded (one replicated unit)
             ps = [p for p in layer.parameters() if id(p) in excluded]
             self._units.append(_Unit(len(self._units), None, ps, group, 2, decay_fn, lr_fn))
+        # tensor parallelism inside the sharded model: _mp_group (the clip norm sums the TP-sharded parameters over
+        # it); _sp_group (the same group when sequence-parallel parameters exist: their grads are summed over it)
+        self._mp_group = self._sp_group = None
+        try:
+            from .. import fleet
+
+            hcg = fleet.get_hybrid_communicate_group()
+            if hcg is not None and hcg.get_model_parallel_world_size() > 1:
+                self._mp_group = hcg.get_model_parallel_group()
+                if any(getattr(p, "sequence_parallel", False) for p in layer.parameters()):
+                    self._sp_group = self._mp_group
+        except Exception:   # noqa: BLE001 - no fleet: plain sharding
+            self._mp_group = self._sp_group = None
         self._order = []       # unit call order in forward
         self._order_done = False  # a full forward has recorded _order (the last unit stays gathered for backward)
         self._by_layer = {id(u.layer): u for u in self._units if u.layer is not None}
@@ -569,6 +600,21 @@ class GroupShardedOptimizer:
     def _global_sq_norm(self):
         from ...ops import _native as N
 
+        mpg = self._model._mp_group
+        if mpg is not None:
+            # TP inside: a TP-sharded parameter's norm is the sum over the mp group, a replicated one (norms, SP
+            # parameters after their mp sum) counts once — every mp rank then clips with the same coefficient
+            dev = self._model._units[0].device
+            sq = torch.zeros(2, dtype=torch.float32, device=dev)
+            for u in self._model._units:
+                for (p, o, n, _, _) in u.pieces:
+                    seg = u.grad_shard[o:o + n]
+                    sq[0 if getattr(p, "is_distributed", False) else 1] += torch.dot(seg, seg)
+            if self._model._units[0].comm:
+                dist.all_reduce(sq, group=self._model._group.pg)
+            sd = sq[:1].clone()
+            dist.all_reduce(sd, group=mpg.pg)
+            return sd + sq[1:]
         shards = [u.grad_shard for u in self._model._units]
         if shards[0].is_cuda and N.use_native(shards[0]) and all(g.dtype == shards[0].dtype for g in shards):
             # one multi-tensor launch over every unit's fp32 grad shard (csrc/kernels/optim.hip sqnorm_mt)
@@ -583,7 +629,7 @@ class GroupShardedOptimizer:
             for g in shards:
                 sq += torch.dot(g, g)
         g = self._model._group
-        if g.nranks > 1:
+        if self._model._units[0].comm:
             dist.all_reduce(sq, group=g.pg)
         return sq
 

@@ -3,7 +3,7 @@
 
 ``TCPStore`` wraps the native C++ daemon/client (csrc/runtime/tcp_store.cpp).  ``TorchStore``
 adapts it to ``torch.distributed.Store`` so RCCL/gloo process groups can rendezvous through the
-native store (``init_parallel_env`` does so when ``PADDLE2_AMD_NATIVE_STORE=1``).
+native store (``init_parallel_env``'s default store: collective._rendezvous_store).
 """
 from __future__ import annotations
 
@@ -25,6 +25,7 @@ class TCPStore:
         self.port = self._server.port if self._server is not None else int(port)
         self.host = hostname
         self.world_size = world_size
+        self.timeout = timeout
         self._client = rt.TCPStoreClient(hostname, self.port, float(timeout))
 
     # Paddle API
@@ -67,6 +68,9 @@ class TCPStore:
             self._server = None
 
 
+_LIVE = []
+
+
 class TorchStore(dist.Store):
     """torch.distributed.Store backed by the native TCPStore client."""
 
@@ -74,6 +78,9 @@ class TorchStore(dist.Store):
         super().__init__()
         self._s = store
         self._c = store._client
+        # c10d keeps only the C++ half of a Python-subclassed store alive; once the Python object is collected its
+        # overrides are gone and every call fails ("Not implemented"), so the job holds every instance
+        _LIVE.append(self)
 
     def set(self, key, value):
         self._c.set(key, value.encode() if isinstance(value, str) else bytes(value))
@@ -103,6 +110,29 @@ class TorchStore(dist.Store):
 
     def set_timeout(self, timeout):
         self._c.set_timeout(timeout.total_seconds() if isinstance(timeout, datetime.timedelta) else float(timeout))
+
+    def clone(self):
+        """A second client connection to the same daemon (ProcessGroupGloo clones the store for every group)."""
+        c = TorchStore(TCPStore(self._s.host, self._s.port, False, self._s.world_size, self._s.timeout))
+        return c
+
+    def multi_get(self, keys):
+        return [self._c.get(k) for k in keys]
+
+    def multi_set(self, keys, values):
+        for k, v in zip(keys, values):
+            self.set(k, v)
+
+    def append(self, key, value):
+        v = value.encode() if isinstance(value, str) else bytes(value)
+        while True:   # read-modify-write on compare_set: appends from several clients never lose bytes
+            cur = self._c.get(key) if self._c.check([key]) else b""
+            new = bytes(cur) + v
+            if bytes(self._c.compare_set(key, bytes(cur) if cur else b"", new)) == new:
+                return
+
+    def has_extended_api(self):
+        return False
 
 
 _global_store = None

@@ -81,19 +81,22 @@ def _proj(cfg, fin, fout, kind, bias=True):
     """kind 'col' | 'row'; picks TP / SP / fp8 variants."""
     attr = nn.ParamAttr(initializer=I.Normal(0.0, cfg.initializer_range))
     tp = cfg.tensor_parallel_degree
+    fp8 = True if cfg.use_fp8 else None   # TP / SP linears: fp8 local GEMMs, bf16 collectives
     if tp > 1:
         if cfg.sequence_parallel:
             from ..distributed.fleet.utils.sequence_parallel_utils import (ColumnSequenceParallelLinear,
                                                                            RowSequenceParallelLinear)
 
             if kind == "col":
-                return ColumnSequenceParallelLinear(fin, fout, weight_attr=attr, has_bias=bias, gather_output=False)
-            return RowSequenceParallelLinear(fin, fout, weight_attr=attr, has_bias=bias, input_is_parallel=True)
+                return ColumnSequenceParallelLinear(fin, fout, weight_attr=attr, has_bias=bias, gather_output=False,
+                                                    fp8=fp8)
+            return RowSequenceParallelLinear(fin, fout, weight_attr=attr, has_bias=bias, input_is_parallel=True,
+                                             fp8=fp8)
         from ..distributed.fleet.layers.mpu import ColumnParallelLinear, RowParallelLinear
 
         if kind == "col":
-            return ColumnParallelLinear(fin, fout, weight_attr=attr, has_bias=bias, gather_output=False)
-        return RowParallelLinear(fin, fout, weight_attr=attr, has_bias=bias, input_is_parallel=True)
+            return ColumnParallelLinear(fin, fout, weight_attr=attr, has_bias=bias, gather_output=False, fp8=fp8)
+        return RowParallelLinear(fin, fout, weight_attr=attr, has_bias=bias, input_is_parallel=True, fp8=fp8)
     if cfg.use_fp8:
         from ..incubate.fp8 import Float8Linear
 

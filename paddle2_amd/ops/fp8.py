@@ -217,8 +217,8 @@ class _FP8LinearFn(torch.autograd.Function):
             # calls of the GPT-3 13B fp8 step (profiles/r4_gpt13b_fp8_step_kernels.txt)
             from .torch_ops import bias_grad
 
-            db = (bias_grad(dy2.contiguous()) if dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16)
-                  else dy2.sum(0, dtype=torch.float32)).to(wdt)
+            db = (bias_grad(dy2.contiguous(), out_dtype=wdt) if dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16)
+                  else dy2.sum(0, dtype=torch.float32).to(wdt))
         mg.update()
         return dx.reshape(xshape), dw.to(wdt), db, None, None, None
 

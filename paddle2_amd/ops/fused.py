@@ -41,16 +41,24 @@ class _BiasActFn(torch.autograd.Function):
         else:
             t = x2.float() + (0 if bias is None else bias.float())
             out = (_act_torch(act, t[:, :H]) * t[:, H:] if gated else _act_torch(act, t)).to(x.dtype)
-        ctx.save_for_backward(x2, bias)
+        ctx.save_for_backward(x, bias)   # the input itself: under create_graph it carries the graph back to x
         ctx.meta = (act, gated, shp, H)
         return out.reshape(*shp[:-1], H)
 
     @staticmethod
     def backward(ctx, dout):
-        x2, bias = ctx.saved_tensors
+        x, bias = ctx.saved_tensors
         act, gated, shp, H = ctx.meta
+        x2 = x.reshape(-1, shp[-1]).contiguous()
         d2 = dout.reshape(-1, H).contiguous()
-        if ctx.native:
+        if torch.is_grad_enabled():
+            # create_graph (double backward, incubate.autograd Hessian / jvp): a differentiable backward in torch
+            # ops — the native kernel writes dx through raw pointers, with no graph for the second-order terms
+            t = x2.float() + (0 if bias is None else bias.float())
+            y = _act_torch(act, t[:, :H]) * t[:, H:] if gated else _act_torch(act, t)
+            (dx,) = torch.autograd.grad(y, t, d2.float(), create_graph=True)
+            dx = dx.to(x2.dtype)
+        elif ctx.native:
             b = None if bias is None else bias.contiguous().to(x2.dtype)
             dx = torch.empty_like(x2)
             N.native().bias_act_bwd(N.DT_CODE[x2.dtype], int(gated), ACTS[act], x2.data_ptr(), N.ptr(b),

@@ -457,20 +457,21 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
-def bias_grad(dy2):
+def bias_grad(dy2, out_dtype=None):
     """db = dy2.sum(0) for a [M, N] gradient: the native two-pass column sum (csrc/kernels/norm.hip
     bias_grad_part_kernel + colsum, fp32 accumulation, deterministic) — torch's bf16 dim-0 reduce ran 5-30x slower
-    on the GPT-3 13B step (24.9 ms / 160 calls)."""
+    on the GPT-3 13B step (24.9 ms / 160 calls).  ``out_dtype`` (default dy2's): the fp32 partials are rounded once,
+    straight to it — an fp32 master bias gets the fp32 sum, not a bf16-rounded one."""
     M, Nn = dy2.shape
-    if (N.use_native(dy2) and dy2.dtype in _DT and Nn % 8 == 0 and dy2.is_contiguous() and M > 0
+    odt = out_dtype or dy2.dtype
+    if (N.use_native(dy2) and dy2.dtype in _DT and odt in _DT and Nn % 8 == 0 and dy2.is_contiguous() and M > 0
             and dy2.data_ptr() % 16 == 0):
         C = N.native()
         part = torch.empty(C.bias_grad_chunks(M, Nn) * Nn, dtype=torch.float32, device=dy2.device)
-        db = torch.empty(Nn, dtype=dy2.dtype, device=dy2.device)
-        C.bias_grad(_DT[dy2.dtype], _DT[dy2.dtype], dy2.data_ptr(), part.data_ptr(), db.data_ptr(), M, Nn,
-                    N.stream())
+        db = torch.empty(Nn, dtype=odt, device=dy2.device)
+        C.bias_grad(_DT[dy2.dtype], _DT[odt], dy2.data_ptr(), part.data_ptr(), db.data_ptr(), M, Nn, N.stream())
         return db
-    return dy2.sum(0)
+    return dy2.sum(0, dtype=torch.float32).to(odt)
 
 
 def _pass_native(name, t, other=None):

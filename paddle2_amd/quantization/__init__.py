@@ -403,25 +403,35 @@ class Quantization(metaclass=abc.ABCMeta):
             object.__setattr__(m, k, v) if k in m.__dict__ else None
         return m
 
+    @staticmethod
+    def _replace_children(layer, make, descend):
+        """Post-order rewrite of the layer tree: a child for which ``make(child)`` returns a layer is swapped for
+        it (in place, by name); otherwise the walk enters the child when ``descend(child)`` allows."""
+        swaps = []
+        for name, child in layer.named_children():
+            new = make(child)
+            if new is not None:
+                swaps.append((name, new))
+            elif descend(child):
+                Quantization._replace_children(child, make, descend)
+        for name, new in swaps:
+            layer._sub_layers[name] = new
+
     def _convert_to_quant_layers(self, model, config):
-        repl = {}
-        for name, child in model.named_children():
-            if config._is_quantifiable(child) and type(child) in config.qat_layer_mappings:
-                repl[name] = config._get_qat_layer(child)
-            else:
-                self._convert_to_quant_layers(child, config)
-        for k, v in repl.items():
-            model._sub_layers[k] = v
+        # quantifiable layers with a QAT mapping become their quantized counterparts
+        self._replace_children(
+            model,
+            lambda c: config._get_qat_layer(c) if config._is_quantifiable(c) and type(c) in
+            config.qat_layer_mappings else None,
+            lambda c: True)
 
     def _insert_activation_observers(self, model, config):
-        repl = {}
-        for name, child in model.named_children():
-            if config._need_observe(child):
-                repl[name] = config._get_observe_wrapper(child)
-            elif type(child) not in config.qat_layer_mappings.values():
-                self._insert_activation_observers(child, config)
-        for k, v in repl.items():
-            model._sub_layers[k] = v
+        # observed layers get their observe wrapper; already-quantized layers are leaves
+        qat_types = tuple(config.qat_layer_mappings.values())
+        self._replace_children(
+            model,
+            lambda c: config._get_observe_wrapper(c) if config._need_observe(c) else None,
+            lambda c: type(c) not in qat_types)
 
     def _details(self):
         return self._config.details()

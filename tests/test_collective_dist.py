@@ -79,3 +79,32 @@ def test_static_program_collectives_and_plan():
         assert r["w"] == [1.5, 3.5, 5.5]             # rank 1's x (2x) - 0.5
         assert r["comm_ops"] == ["c_allreduce_sum", "c_broadcast"]
         assert r["waits"] >= 2 and r["freed"] >= 2
+
+
+def test_collectives_under_torchrun_agent_store():
+    """Launched by torch.distributed.run (the bench.py contract for N > 1): the elastic agent hosts the store on
+    MASTER_PORT, so rank 0 must connect to it as a client instead of binding the port again (EADDRINUSE)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    import tempfile
+
+    from _dist import ROOT, free_port, pypath
+
+    out_dir = tempfile.mkdtemp(prefix="pd_trun_")
+    env = dict(os.environ)
+    env.update({"PYTHONPATH": pypath(ROOT), "PADDLE2_AMD_DEVICE": "cpu", "OMP_NUM_THREADS": "1",
+                "PADDLE_DISTRI_BACKEND": "gloo", "PD_TEST_OUT_DIR": out_dir})
+    env.pop("RANK", None)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "tests", "workers", "torchrun_worker.py")]
+    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-4000:]
+    res = []
+    for r in range(2):
+        with open(os.path.join(out_dir, f"rank{r}.json")) as f:
+            res.append(json.load(f))
+    for r in res:
+        assert r["all_reduce"] == [3.0, 3.0] and r["store"] == "agent"

@@ -81,3 +81,34 @@ def test_functional_gelu_native_on_gpu(approximate):
     yr.sum().backward()
     torch.testing.assert_close(y._t.float().cpu(), yr.detach(), rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(x.grad._t.float().cpu(), xr.grad, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("dev", DEVS)
+@pytest.mark.parametrize("act", ["gelu", "gelu_tanh", "silu", "swiglu"])
+def test_bias_act_double_backward(dev, act):
+    """create_graph through the fused bias-act: the second-order terms (d/dx of the input gradient) match torch's
+    own double backward of the same function in fp32 (bf16 inputs on the GPU)."""
+    from paddle2_amd.ops import fused as Fz
+
+    dt = torch.bfloat16 if dev == "cuda" else torch.float32
+    g = torch.Generator().manual_seed(3)
+    W = 64
+    x0 = torch.randn(16, W, generator=g).to(dt)
+    b0 = torch.randn(W, generator=g).to(dt)
+    x = x0.to(dev).requires_grad_(True)
+    b = b0.to(dev).requires_grad_(True)
+    y = Fz.bias_act(x, b, act)
+    (gx,) = torch.autograd.grad(y.float().pow(2).sum(), x, create_graph=True)
+    (hx,) = torch.autograd.grad(gx.float().sum(), x)
+    xr = x0.float().requires_grad_(True)
+    t = xr + b0.float()
+    F = torch.nn.functional
+    if act == "swiglu":
+        yr = F.silu(t[:, :W // 2]) * t[:, W // 2:]
+    else:
+        yr = {"gelu": F.gelu, "gelu_tanh": lambda v: F.gelu(v, approximate="tanh"), "silu": F.silu}[act](t)
+    (gr,) = torch.autograd.grad(yr.pow(2).sum(), xr, create_graph=True)
+    (hr,) = torch.autograd.grad(gr.sum(), xr)
+    tol = 8e-2 if dt == torch.bfloat16 else 1e-4
+    assert hx.abs().sum() > 0
+    torch.testing.assert_close(hx.float().cpu(), hr, rtol=tol, atol=tol * hr.abs().max().item())

@@ -90,6 +90,19 @@ def test_gpt_sequence_parallel_matches_tensor_parallel():
     _close(run_workers("hybrid_worker.py", 2, ["gpt_sp"]), 1e-4)
 
 
+def test_gpt_fp8_sp_sharding3_matches_tp_dp():
+    """BASELINE config 5 in miniature (bench.py --model gpt3-13b --fp8 --mp 2 --sp on 8 GPUs): fp8 TP2 + SP +
+    stage-3 sharding over the other ranks trains like fp8 TP2 x DP2 through the fleet wrappers (same weights, same
+    global batch, global-norm clipping on both sides)."""
+    a = run_workers("hybrid_worker.py", 4, ["gpt_fp8_hybrid", "sh3"])
+    b = run_workers("hybrid_worker.py", 4, ["gpt_fp8_hybrid", "dp"])
+    for r in a + b:
+        assert r["losses"] == a[0]["losses"] if r in a else r["losses"] == b[0]["losses"]
+    assert abs(a[0]["losses"][0] - b[0]["losses"][0]) < 1e-3, (a[0], b[0])
+    for x, y in zip(a[0]["losses"], b[0]["losses"]):
+        assert abs(x - y) < 2e-2 * max(1.0, abs(y)), (a[0]["losses"], b[0]["losses"])
+
+
 def test_weight_grad_store_splits_backward():
     """ZB-H1's B/W split: with defer on, Linear backward leaves weight grads to the queued W pass."""
     import paddle2_amd as paddle

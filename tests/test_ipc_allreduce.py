@@ -122,3 +122,38 @@ def test_two_process_ipc_allreduce_bit_exact():
     for r in res:
         assert r["ok"], r
         assert r["checked"] == 160
+
+
+@pytest.mark.gpu
+def test_ipc_path_declines_inside_graph_capture(monkeypatch):
+    """A captured all_reduce must not take the IPC path (its barrier epoch would be baked into the graph): during
+    capture maybe_all_reduce declines even with the path forced on, outside capture it still takes the tensor."""
+    calls = []
+
+    class _Fake:
+        def supports(self, t):
+            return True
+
+        def all_reduce(self, t):
+            calls.append(t.numel())
+            t.mul_(2)
+
+    monkeypatch.setitem(IA._AUTO, "comm", _Fake())
+    monkeypatch.setitem(IA._AUTO, "group", None)
+    monkeypatch.setenv("PADDLE2_AMD_IPC_ALLREDUCE", "auto")
+    x = torch.ones(256, device="cuda")
+    assert IA.maybe_all_reduce(x) and calls == [256]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    taken = []
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            taken.append(IA.maybe_all_reduce(x))
+            x.add_(1)
+    torch.cuda.current_stream().wait_stream(s)
+    assert taken == [False] and calls == [256]
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.all(x == 5)

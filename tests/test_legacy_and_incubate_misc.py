@@ -110,21 +110,21 @@ def test_incubate_layers_and_operators():
     assert L.bilateral_slice(img, guide, g, has_offset=False).shape == [1, 2, 16, 16]
 
 
-def _child(q):
+def _child(q, done):
     t = q.get()
     t._t.mul_(2)        # shared storage: the parent sees the update
-    q.put("done")
+    done.put("done")
 
 
 def test_incubate_multiprocessing_shares_cpu_tensors():
     M = paddle.incubate.multiprocessing
     ctx = mp.get_context("fork")
-    q = ctx.Queue()
+    q, done = ctx.Queue(), ctx.Queue()   # separate reply queue: the parent must never read back its own put
     t = paddle.to_tensor(np.ones(4, "float32"))
-    p = ctx.Process(target=_child, args=(q,))
+    p = ctx.Process(target=_child, args=(q, done))
     p.start()
     q.put(t)
-    assert q.get(timeout=30) == "done"
+    assert done.get(timeout=30) == "done"
     p.join(30)
     np.testing.assert_allclose(t.numpy(), [2, 2, 2, 2])
     assert callable(M.init_reductions)

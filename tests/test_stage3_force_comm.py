@@ -1,0 +1,50 @@
+"""Stage 3's N > 1 collective path forced on one rank (PADDLE2_AMD_STAGE3_FORCE_COMM=1: real all-gather /
+reduce-scatter on the group's process group, the fp32 flat-gradient pool, prefetch, retire_rs) trains bit for bit
+like the N = 1 short-circuit (reference group_sharded_stage3.py:851-1074).  CPU: gloo; GPU: the framework's RCCL
+group on the comm stream."""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import pytest
+
+from _dist import ROOT, pypath
+
+
+def _run(dev, force, acc=1):
+    out = os.path.join(tempfile.mkdtemp(prefix="pd_fc_"), "r.json")
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "LOCAL_RANK"):
+        env.pop(k, None)
+    env.update({"PYTHONPATH": pypath(ROOT), "PD_TEST_OUT": out, "PD_TEST_DEVICE": dev, "PD_TEST_ACC": str(acc),
+                "PADDLE2_AMD_STAGE3_FORCE_COMM": "1" if force else "0", "OMP_NUM_THREADS": "2"})
+    if dev == "cpu":
+        env.update({"PADDLE2_AMD_DEVICE": "cpu", "PADDLE_DISTRI_BACKEND": "gloo"})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "workers", "force_comm_worker.py")], env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-4000:]
+    with open(out) as f:
+        return json.load(f)
+
+
+def _check(dev, acc):
+    a, b = _run(dev, False, acc), _run(dev, True, acc)
+    assert not any(a["comm"]) and not a["initialized"]
+    assert all(b["comm"]) and b["initialized"] and b["peak_live_flat"] >= 1
+    assert a["losses"] == b["losses"]
+    assert a["digest"] == b["digest"]
+    return b
+
+
+@pytest.mark.parametrize("acc", [1, 2])
+def test_force_comm_matches_short_circuit_cpu(acc):
+    _check("cpu", acc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("acc", [1, 2])
+def test_force_comm_matches_short_circuit_gpu(acc):
+    b = _check("cuda", acc)
+    assert b["pg"] == "pdrccl"

@@ -167,7 +167,8 @@ def test_resharder_dist_main_program_trains_like_serial(mode):
         assert "c_allreduce_sum" in o["program"] or "c_allreduce_avg" in o["program"]
 
 
-@pytest.mark.parametrize("passes", ["fuse", "merge", "recompute", "sharding", "fuse,sharding", "amp"])
+@pytest.mark.parametrize("passes", ["fuse", "merge", "recompute", "sharding", "fuse,sharding", "amp", "fuse,merge",
+                                    "merge,fuse"])
 def test_static_passes_train_like_serial(passes):
     """Passes over the dist_main_program of a data-parallel plan (2 ranks, Adam): fused + bucketed gradient
     all-reduce, gradient merge (k = 2), recompute of an op range, sharding stage 1 (each rank holds the optimizer
@@ -178,7 +179,8 @@ def test_static_passes_train_like_serial(passes):
         np.testing.assert_allclose(o["losses"], o["ref"], rtol=tol, atol=tol)
         assert o["param_err"] < (5e-2 if passes == "amp" else 1e-5), o["param_err"]
         if "fuse" in passes:
-            assert o["buckets"] >= 1 and o["fused_calls"] == 4
+            # with gradient merge (k = 2) the sum runs once per merged step, at the k-step boundary
+            assert o["buckets"] >= 1 and o["fused_calls"] == (2 if "merge" in passes else 4)
         if passes == "recompute":
             assert len(o["recompute_ops"]) == 1
         if "sharding" in passes:

@@ -373,6 +373,48 @@ def run_gpt_sp():
     write_result({"losses": sp, "ref": ref})
 
 
+def run_gpt_fp8_hybrid(kind):
+    """BASELINE config 5 in miniature: GPT fp8 linears with TP 2 (+ SP) inside, on 4 ranks.
+    kind sh3: TP2 + SP + group-sharded stage 3 over the other 2 ranks (bench.py --mp 2 --sp, sharding 2);
+    kind dp:  TP2 (no SP) + 2-way data parallel through the fleet wrappers — the reference configuration.
+    Same init (model-parallel RNG per mp rank), same global batch of 4 sequences per step (2 per replica), global-norm
+    clipping on: the mean losses must agree."""
+    from paddle2_amd.models import GPTConfig, GPTForCausalLM
+
+    sp = kind == "sh3"
+    strategy = fleet.DistributedStrategy()
+    strategy.hybrid_configs = {"dp_degree": 1 if sp else 2, "mp_degree": 2, "pp_degree": 1,
+                               "sharding_degree": 2 if sp else 1}
+    fleet.init(is_collective=True, strategy=strategy)
+    hcg = fleet.get_hybrid_communicate_group()
+    g = torch.Generator().manual_seed(6)
+    data = [torch.randint(0, 512, (4, 33), generator=g) for _ in range(4)]
+    paddle.seed(9)
+    m = GPTForCausalLM(GPTConfig.tiny(dtype="float32", tensor_parallel_degree=2, sequence_parallel=sp,
+                                      use_fp8=True))
+    opt = paddle.optimizer.AdamW(1e-2, parameters=m.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    if sp:
+        from paddle2_amd.distributed.sharding import group_sharded_parallel
+
+        m, opt, _ = group_sharded_parallel(m, opt, "p_g_os", group=hcg.get_sharding_parallel_group())
+        rep = hcg.get_sharding_parallel_rank()
+    else:
+        m = fleet.distributed_model(m)
+        opt = fleet.distributed_optimizer(opt)
+        rep = hcg.get_data_parallel_rank()
+    out = []
+    for ids in data:
+        ids = paddle.Tensor._wrap(ids[2 * rep:2 * rep + 2])
+        loss = m(ids[:, :-1], labels=ids[:, 1:])
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        t = loss._t.detach().float().clone()
+        dist.all_reduce(t)
+        out.append(float(t) / world)
+    write_result({"losses": out})
+
+
 def _llama_ref_run(cfg, data, k, make):
     """single process: every step accumulates k micro-batches of the GLOBAL batch (loss / k)"""
     m, o = make()
@@ -580,6 +622,8 @@ elif mode == "moe":
     run_moe()
 elif mode == "gpt_sp":
     run_gpt_sp()
+elif mode == "gpt_fp8_hybrid":
+    run_gpt_fp8_hybrid(sys.argv[2])
 elif mode == "shv2":
     run_shv2(sys.argv[2])
 elif mode == "mpsync":

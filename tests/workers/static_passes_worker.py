@@ -43,13 +43,13 @@ with paddle.static.program_guard(main, paddle.static.Program()):
     opt.minimize(loss)
 paddle.disable_static()
 dmp = build_dist_main_program(parallelize_program(main, mesh, {"x": [dist.Shard(0)]}), [loss])
-k = 1
-if "fuse" in passes:
-    fused = fuse_allreduce_pass(dmp, bucket_mb=1)
-    out["buckets"] = len(fused.buckets())
-if "merge" in passes:
-    k = 2
-    gradient_merge_pass(dmp, k)
+k = 2 if "merge" in passes else 1
+for name in passes:   # in the order given: fuse-then-merge and merge-then-fuse must both sum once per merged step
+    if name == "fuse":
+        fused = fuse_allreduce_pass(dmp, bucket_mb=1)
+        out["buckets"] = len(fused.buckets())
+    elif name == "merge":
+        gradient_merge_pass(dmp, k)
 if "recompute" in passes:
     first = [i for i, o in enumerate(dmp.program.ops) if o.kind == "torch"]
     recompute_pass(dmp, [(first[1], first[4])])
