@@ -39,6 +39,8 @@
 //    current step computes (T14 issue-early / write-late).
 #include "common.h"
 
+#include <type_traits>
+
 namespace pd {
 namespace fa {
 
@@ -172,6 +174,16 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes > 0 ? bytes : 0, 0x00020000);
 }
+// the same for a base / extent the compiler cannot PROVE wave-uniform although it is (derived from loop state that
+// lives in VGPRs): the inputs go through readfirstlane, so the descriptor sits in SGPRs and each buffer op is one
+// instruction — otherwise hipcc wraps every op in a waterfall loop (cdna_hip_programming.md T20; the dQ atomics of
+// the backward were 32 such loops per step)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_u(const void* p, int bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane(bytes > 0 ? bytes : 0);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, n, 0x00020000);
+}
 __device__ __forceinline__ bool fm_masked(int4 m, int row) {
   return (row >= m.x && row < m.y) || (row >= m.z && row < m.w);
 }
@@ -288,8 +300,8 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
     // VGPR, and keys past Sk fall outside num_records and read as zero — no per-load 64-bit address math,
     // compare or select
     const int nrows = min(Sk - n0, BN);
-    const __amdgpu_buffer_rsrc_t rk = make_rsrc(Kb + (long)n0 * sk, nrows * (int)sk * 2);
-    const __amdgpu_buffer_rsrc_t rv = make_rsrc(Vb + (long)n0 * sv, nrows * (int)sv * 2);
+    const __amdgpu_buffer_rsrc_t rk = make_rsrc_u(Kb + (long)n0 * sk, nrows * (int)sk * 2);
+    const __amdgpu_buffer_rsrc_t rv = make_rsrc_u(Vb + (long)n0 * sv, nrows * (int)sv * 2);
 #pragma unroll
     for (int i = 0; i < NLOAD; ++i) {
       stk[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rk, voff_k[i], 0, 0));
@@ -335,22 +347,34 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
   // causal: the last key this wave's 32 rows can see; tiles past it are all masked for the wave
   const int wave_last_key = m0 + wv * 32 + 31 + off;
 
-  for (int buf = 0; t < ntiles; buf ^= 1) {
-    const int n0 = t * BN;
-    const int tn = next_tile(t + 1);
-    const bool has_next = tn < ntiles;
-    const char* kt = smem + buf * 2 * TILE;
-    const char* vt = kt + TILE;
-    if (CAUSAL && (NW == 8 || ex.wave_skip) && n0 > wave_last_key) {  // wave-uniform: only stage the next tile for the others
-      if (has_next) {
-        gload(tn * BN);
-        lstore(buf ^ 1);
-      }
-      __syncthreads();
-      t = tn;
-      continue;
-    }
+  // Per-lane LDS read bases (D <= 128; cdna guide T20-style address hygiene): every K row read and V^T transposed
+  // read is one precomputed lane base + a compile-time immediate (buffer / key sub-block / 16-row step), so the tile
+  // body carries no per-read swizzle arithmetic.
+  //  K row read (key row kb*32 + r, 16-B chunk 2ks + h): chunk ^ m(r) = (2ks) ^ (h ^ m(r)) -> o_k ^ (ks << 5)
+  //  V^T tr read (rows r0 + 4hh + qq (+8), 16-B chunk 4dt + cbits): -> o_va / o_vb ^ (dt << 6)
+  constexpr bool PRE = D <= 128;
+  int o_k = 0, o_va = 0, o_vb = 0;   // three lane bases; one v_xor per read (all-precomputed spilled: 256 VGPRs)
+  if constexpr (PRE) {
+    auto mm = [](int row) { return ((row & 3) << 2) | ((row >> 2) & 3); };
+    o_k = r * (D * 2) + (((h ^ mm(r)) & (NCH - 1)) << 4);
+    const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3, hh = g >> 1;
+    const int cbits = ((g & 1) << 1) | (pp >> 1);
+    const int ra = 4 * hh + qq, rb = ra + 8;
+    o_va = ra * (D * 2) + (((cbits ^ mm(ra)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
+    o_vb = rb * (D * 2) + (((cbits ^ mm(rb)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
+  }
 
+  // One key tile.  MASKED (compile time): the boundary / causal-diagonal / FlashMask-partial tiles run the element
+  // masks; every other tile runs a body with no mask code at all (a runtime branch inside one body was if-converted
+  // by hipcc: ~100 compares / selects per tile on every tile).  BUF: the LDS stage (a compile-time stage doubled the
+  // bodies and spilled 264 B/lane).
+  auto tile = [&](auto MASKED_, int BUF, int n0, bool has_next, int tn) {
+    constexpr bool MASKED = decltype(MASKED_)::value;
+    const char* kt = smem + BUF * 2 * TILE;
+    const char* vt = kt + TILE;
+    // opaque per tile: the XOR-ed read offsets are recomputed (1 VALU each) instead of hoisted out of the loop as
+    // ~50 live registers (which spilled)
+    if constexpr (PRE) asm volatile("" : "+v"(o_k), "+v"(o_va), "+v"(o_vb));
     // ---- S^T = K . Q^T for two 32-key sub-blocks
     f32x16 s[2];
 #pragma unroll
@@ -359,17 +383,17 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
       const int krow = kb * 32 + r;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        bf16x8 a = lds_b128(kt, krow * (D * 2) + swz(krow, 2 * ks + h, NCH) * 16);
+        bf16x8 a;
+        if constexpr (PRE) a = lds_b128(kt + kb * 32 * (D * 2), o_k ^ (ks << 5));
+        else a = lds_b128(kt, krow * (D * 2) + swz(krow, 2 * ks + h, NCH) * 16);
         s[kb] = mfma<F16>(a, qf[ks], s[kb]);
       }
     }
     // next tile's K/V loads issue after QK^T (T14): softmax + PV cover their flight, lstore waits at the end
     if (has_next) gload(tn * BN);
-    // ---- mask, online softmax (lane owns query qrow; 32 of the 64 keys).  The max is taken on raw
-    // scores and the 1/sqrt(d)*log2(e) scale is folded into one FMA feeding v_exp_f32; masking is
-    // a separate, wave-uniformly skipped pass so the common (unmasked) tile has no branches.
-    const bool need_mask = (n0 + BN > Sk) || (CAUSAL && (n0 + BN - 1 > m0 + off));
-    if (need_mask) {
+    // ---- mask, online softmax (lane owns query qrow; 32 of the 64 keys).  The max is taken on raw scores and the
+    // 1/sqrt(d)*log2(e) scale is folded into one FMA feeding v_exp_f32.
+    if constexpr (MASKED) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
@@ -378,38 +402,47 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
           s[kb][i] = (key >= Sk || (CAUSAL && key > qrow + off)) ? -INFINITY : s[kb][i];
         }
       }
-    }
-    if constexpr (MODE == kMask) {
-      if (plan[2 + t] == 1) {
-        // 4 consecutive keys per group from the LDS image; the sched barrier keeps only one group's
-        // intervals live (the D=128 accumulators leave no room for all 32)
-        const int4* fmt_s = fm_s + buf * BN;
+      if constexpr (MODE == kMask) {
+        if (plan[2 + n0 / BN] == 1) {
+          // 4 consecutive keys per group from the LDS image; the sched barrier keeps only one group's
+          // intervals live (the D=128 accumulators leave no room for all 32)
+          const int4* fmt_s = fm_s + BUF * BN;
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
+          for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
+            for (int g = 0; g < 4; ++g) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int4 m = fmt_s[kb * 32 + 8 * g + 4 * h + j];
-              s[kb][4 * g + j] = fm_masked(m, qrow) ? -INFINITY : s[kb][4 * g + j];
+              for (int j = 0; j < 4; ++j) {
+                const int4 m = fmt_s[kb * 32 + 8 * g + 4 * h + j];
+                s[kb][4 * g + j] = fm_masked(m, qrow) ? -INFINITY : s[kb][4 * g + j];
+              }
+              __builtin_amdgcn_sched_barrier(0);
             }
-            __builtin_amdgcn_sched_barrier(0);
           }
         }
       }
     }
-    float mx = -INFINITY;
+    // row max: four independent max3 chains (one 16-deep chain was a serial latency path), then the lane-half
+    // exchange by v_permlane32_swap (no LDS round trip: ds_bpermute + lgkmcnt wait)
+    float mxa[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[kb][i]);
+      for (int i = 0; i < 16; ++i) mxa[i & 3] = fmaxf(mxa[i & 3], s[kb][i]);
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float mx = fmaxf(fmaxf(mxa[0], mxa[1]), fmaxf(mxa[2], mxa[3]));
+    {
+      const unsigned mu = __builtin_bit_cast(unsigned, mx);
+      const auto sw = __builtin_amdgcn_permlane32_swap(mu, mu, false, false);
+      mx = fmaxf(__builtin_bit_cast(float, (unsigned)sw[0]), __builtin_bit_cast(float, (unsigned)sw[1]));
+    }
     // defer-max (T13): the running base moves only when some row of the wave grew past it by more than
-    // 2^kDefer; otherwise P <= 2^kDefer (exact in fp32 / bf16) and the l / O rescale — DT*16 multiplies
-    // per lane, a quarter of the tile's VALU issue — is skipped (wave-uniform branch)
+    // 2^kDefer; otherwise P <= 2^kDefer (exact in fp32 / bf16) and the l / O rescale is skipped.  The branch is
+    // wave-uniform and kept a real branch (the asm statement cannot be speculated): if-converted, its DT*16
+    // multiplies and copies ran on every tile
     const float m_cand = fmaxf(m_i, mx * sl2);
-    if (__any(m_cand > m_i + kDefer)) {
+    if (__builtin_expect(__any(m_cand > m_i + kDefer), 0)) {
+      asm volatile("" ::: "memory");
       const float alpha = __builtin_amdgcn_exp2f(m_i - (m_cand == -INFINITY ? 0.f : m_cand));
       l_i *= alpha;
 #pragma unroll
@@ -417,17 +450,17 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
       m_i = m_cand;
     }
     const float base = m_i == -INFINITY ? 0.f : m_i;
-    float ls = 0.f;
+    float lsa[4] = {0.f, 0.f, 0.f, 0.f};   // four independent add chains (a 32-deep serial chain before)
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const float p = __builtin_amdgcn_exp2f(fmaf(s[kb][i], sl2, -base));
         s[kb][i] = p;
-        ls += p;
+        lsa[i & 3] += p;
       }
     }
-    l_i += ls;  // per lane-half partial; halves combined at the end
+    l_i += (lsa[0] + lsa[1]) + (lsa[2] + lsa[3]);  // per lane-half partial; halves combined at the end
     if constexpr (DROP) {  // row sums keep the undropped P; only the P.V operand is masked
       const unsigned bh = (unsigned)(b * Hq + hq);
 #pragma unroll
@@ -448,13 +481,40 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
         const bf16x8 pb = pack8<F16>(s[kb], ss);
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-          const bf16x8 a = tr_frag<D, true>(vt, kb * 32 + 16 * ss, dt * 32, lane);
+          bf16x8 a;
+          if constexpr (PRE) {
+            const char* vr = vt + (kb * 32 + 16 * ss) * (D * 2);
+            a = cat4(lds_tr(vr, o_va ^ (dt << 6)), lds_tr(vr, o_vb ^ (dt << 6)));
+          } else {
+            a = tr_frag<D, true>(vt, kb * 32 + 16 * ss, dt * 32, lane);
+          }
           oacc[dt] = mfma<F16>(a, pb, oacc[dt]);
         }
       }
     }
-    if (has_next) lstore(buf ^ 1);  // write late (T14)
+    if (has_next) lstore(BUF ^ 1);  // write late (T14)
     __syncthreads();
+  };
+
+  using FalseT = std::integral_constant<bool, false>;
+  using TrueT = std::integral_constant<bool, true>;
+  for (int buf = 0; t < ntiles; buf ^= 1) {
+    const int n0 = t * BN;
+    const int tn = next_tile(t + 1);
+    const bool has_next = tn < ntiles;
+    if (CAUSAL && (NW == 8 || ex.wave_skip) && n0 > wave_last_key) {  // wave-uniform: only stage the next tile for the others
+      if (has_next) {
+        gload(tn * BN);
+        lstore(buf ^ 1);
+      }
+      __syncthreads();
+      t = tn;
+      continue;
+    }
+    bool masked = (n0 + BN > Sk) || (CAUSAL && (n0 + BN - 1 > m0 + off));
+    if constexpr (MODE == kMask) masked = masked || plan[2 + t] == 1;
+    if (masked) tile(TrueT{}, buf, n0, has_next, tn);
+    else tile(FalseT{}, buf, n0, has_next, tn);
     t = tn;
   }
 
@@ -522,15 +582,18 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const bf16* __restrict__
 template <int D>
 constexpr int bwd_waves() { return D > 128 ? 4 : 8; }
 
-template <int D, bool CAUSAL, int MODE, bool DROP, bool F16>
-__global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+// NWB = 4 at D = 128 (dense, atomic dQ): 128-key blocks, two 256-thread workgroups per CU instead of one 512-thread
+// one — the two workgroups' barriers are independent, so SIMD partners drift apart and one wave's exp / dS VALU runs
+// beside the other's MFMAs instead of colliding with them; every wave takes a dQ slice (4 slices, 4 waves)
+template <int D, bool CAUSAL, int MODE, bool DROP, bool F16, int NWB = bwd_waves<D>()>
+__global__ __launch_bounds__(NWB * 64, (NWB == 4 && D <= 128) ? 2 : 1) void bwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ Vv, const bf16* __restrict__ dO,
                                                      const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                      float* __restrict__ dQP, bf16* __restrict__ dK,
                                                      bf16* __restrict__ dV, int B, int SqMax, int SkMax, int Hq,
                                                      int Hk, long sq, long sk, long sv, long so, long sdk, long sdv,
                                                      long pslab, float scale, Ext ex) {
-  constexpr int NW = bwd_waves<D>(), BNK = NW * 32, BMQ = 32, NCH = D / 8, KS = D / 16, DT = D / 32;
+  constexpr int NW = NWB, BNK = NW * 32, BMQ = 32, NCH = D / 8, KS = D / 16, DT = D / 32;
   constexpr int KTILE = BNK * D * 2;     // K block image: B operand of S (row reads) and of dQ (tr reads)
   constexpr int QTILE = BMQ * D * 2;     // Q / dO tile image
   constexpr int STILE = BMQ * BNK * 2;   // dS tile [32 q][256 keys]
@@ -644,8 +707,8 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16*
     const int hq = hk * group + step / nqt;
     const int q0 = q_begin + (step % nqt) * BMQ;
     const int nrows = min(Sq - q0, BMQ);
-    const __amdgpu_buffer_rsrc_t rq = make_rsrc(Q + (qt0 + q0) * sq + hq * D, nrows * (int)sq * 2);
-    const __amdgpu_buffer_rsrc_t rd = make_rsrc(dO + (qt0 + q0) * so + hq * D, nrows * (int)so * 2);
+    const __amdgpu_buffer_rsrc_t rq = make_rsrc_u(Q + (qt0 + q0) * sq + hq * D, nrows * (int)sq * 2);
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc_u(dO + (qt0 + q0) * so + hq * D, nrows * (int)so * 2);
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int c = tid + NW * 64 * i;
@@ -691,7 +754,7 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16*
     if constexpr (MODE == kDense) {
       if (pend_hq < 0) return;
       const int hqd4 = Hq * D * 4;
-      const __amdgpu_buffer_rsrc_t rs = make_rsrc(dQs + (long)pend_q0 * Hq * D + (long)pend_hq * D, BMQ * hqd4);
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc_u(dQs + (long)pend_q0 * Hq * D + (long)pend_hq * D, BMQ * hqd4);
 #pragma unroll
       for (int dsl = wv; dsl < DT; dsl += NW) {
         const int vo = 4 * h * hqd4 + (dsl * 32 + r) * 4;
@@ -835,7 +898,7 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, 1) void bwd_kernel(const bf16*
       }
       if (q0 + BMQ <= Sq) {
         const int hqd4 = Hq * D * 4;
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(dQs + (long)q0 * Hq * D + (long)hq * D, BMQ * hqd4);
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc_u(dQs + (long)q0 * Hq * D + (long)hq * D, BMQ * hqd4);
         const int vo = 4 * h * hqd4 + (dsl * 32 + r) * 4;
         if (ex.dq_atomic) {
 #pragma unroll
@@ -1056,8 +1119,19 @@ template <int D, bool F16>
 void launch_bwd(dim3 grid, hipStream_t st, const void* q, const void* k, const void* v, const void* dout,
                 const float* lse, const float* delta, float* dqp, void* dk, void* dv, int B, int Sq, int Sk, int Hq,
                 int Hk, long sq, long sk, long sv, long so, long sdk, long sdv, long pslab, float scale, bool causal,
-                int mode, bool drop, const fa::Ext& ex) {
+                int mode, bool drop, const fa::Ext& ex, int nwb) {
   constexpr int NT = fa::bwd_waves<D>() * 64;
+  if constexpr (D == 128) {
+    if (nwb == 4) {   // dense, atomic dQ, no dropout (fa_bwd_waves)
+#define PD_FA_BWD4(CC)                                                                                              \
+  fa::bwd_kernel<D, CC, fa::kDense, false, F16, 4><<<grid, 256, 0, st>>>(                                          \
+      (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, dqp, (bf16*)dk, (bf16*)dv, B, \
+      Sq, Sk, Hq, Hk, sq, sk, sv, so, sdk, sdv, pslab, scale, ex)
+      if (causal) PD_FA_BWD4(true); else PD_FA_BWD4(false);
+#undef PD_FA_BWD4
+      return;
+    }
+  }
 #define PD_FA_BWD(CC, MM, DR)                                                                                    \
   fa::bwd_kernel<D, CC, MM, DR, F16><<<grid, NT, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,       \
                                                           (const bf16*)dout, lse, delta, dqp, (bf16*)dk, (bf16*)dv, \
@@ -1110,7 +1184,19 @@ static int fa_fwd_waves(int D, int Sq, int causal, int mode, int drop) {
 }
 
 // Key-block width of the backward (rows of the dQ partial slabs): 256 keys for D <= 128, 128 for D = 256.
+// (The 4-wave D = 128 kernel's 128-key blocks run only in the dense atomic mode, whose dQ is one slab.)
 extern "C" int pd_flash_bwd_block(int D) { return D > 128 ? 128 : 256; }
+
+// Backward workgroup width at D = 128 for the dense atomic-dQ path: 8 waves (256 keys, one workgroup per CU) or 4
+// (128 keys, two per CU).  PADDLE2_AMD_FA_BWD_WAVES = 4 / 8 forces one.
+static int fa_bwd_waves(int D, int mode, bool atomic, int drop) {
+  if (D != 128 || mode != 0 || !atomic || drop) return D > 128 ? 4 : 8;
+  if (const char* e = getenv("PADDLE2_AMD_FA_BWD_WAVES")) {
+    const int w = atoi(e);
+    if (w == 4 || w == 8) return w;
+  }
+  return 8;
+}
 
 // mode: 0 dense, 1 varlen (B sequences, Sq/Sk = max_seqlen, rows located by cu_q/cu_k, lse [Hq, total_q]),
 // 2 FlashMask (dense layout + fm [B, fm_hm, Sk] int4 intervals with the fm_t64 / fm_t256 fwd / bwd plans).
@@ -1186,11 +1272,12 @@ extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void
     fa::bwd_delta_kernel<true><<<dgrid, 256, 0, st>>>((const bf16*)o, (const bf16*)dout, delta, dB, dS, Hq, D, so);
   else
     fa::bwd_delta_kernel<false><<<dgrid, 256, 0, st>>>((const bf16*)o, (const bf16*)dout, delta, dB, dS, Hq, D, so);
-  const int BNK = pd_flash_bwd_block(D);
-  const int nkb = (Sk + BNK - 1) / BNK;
   // dense mode, atomic dQ: every key block adds into one zeroed fp32 slab (one slab of workspace, a convert
   // pass instead of the slab reduce: 0.27 ms less per B8 S4096 H32 D128 layer)
   const bool atomic = mode == 0 && fa_dq_atomic();
+  const int nwb = fa_bwd_waves(D, mode, atomic, drop);
+  const int BNK = D == 128 && nwb == 4 ? 128 : pd_flash_bwd_block(D);
+  const int nkb = (Sk + BNK - 1) / BNK;
   const long pslab = atomic ? 0 : nrows * Hq * D;
   if (atomic) hipMemsetAsync(dqp, 0, nrows * Hq * D * sizeof(float), st);
   dim3 grid(nkb * Hk * B);
@@ -1208,7 +1295,7 @@ extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void
   }
 #define PD_BWD(DD, FF)                                                                                              \
   launch_bwd<DD, FF>(grid, st, q, k, v, dout, lse, delta, dqp, dk, dv, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, sdk, sdv, \
-                     pslab, scale, causal, mode, drop, ex)
+                     pslab, scale, causal, mode, drop, ex, nwb)
   if (D == 128) { if (f16) PD_BWD(128, true); else PD_BWD(128, false); }
   else if (D == 64) { if (f16) PD_BWD(64, true); else PD_BWD(64, false); }
   else { if (f16) PD_BWD(256, true); else PD_BWD(256, false); }

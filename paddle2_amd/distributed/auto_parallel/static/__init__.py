@@ -6,4 +6,5 @@ from .cost_model import ClusterSpec, CostModel, Planner, reshard_steps  # noqa: 
 from .partitioner import DistributedProgram, parallelize_program  # noqa: F401
 from .engine import Engine  # noqa: F401
 from .resharder import DistMainProgram, Resharder, build_dist_main_program, comm_kinds  # noqa: F401,E402
-from .passes import amp_pass, fuse_allreduce_pass, gradient_merge_pass, recompute_pass, sharding_pass  # noqa: F401,E402
+from .passes import (allreduce_matmul_grad_overlap_pass, amp_pass, fuse_allreduce_pass, gradient_merge_pass,  # noqa: F401,E402
+                     recompute_pass, sequence_parallel_optimization_pass, sharding_pass)

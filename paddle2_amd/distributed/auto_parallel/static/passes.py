@@ -235,19 +235,55 @@ def recompute_pass(dmp, segments):
 
 
 # ------------------------------------------------------------------------------------------------ sharding
-def sharding_pass(dmp, mesh_dim=0):
-    """Stage 1: the optimizer state sharded over ``mesh_dim``.  Parameters are assigned to owners greedily by size;
-    each rank steps its own and broadcasts them (one coalesced broadcast per owner).  -> {param name: owner}."""
+def _row_of(mesh, mesh_dim):
+    n = mesh.size(mesh_dim)
+    ranks = mesh.mesh.movedim(mesh_dim, -1).reshape(-1, n)
+    return next(r for r in ranks.tolist() if dist.get_rank() in r)
+
+
+def _coalesced_broadcast(tensors, src, group):
+    flat = torch.cat([t.reshape(-1) for t in tensors])
+    dist.broadcast(flat, src=src, group=group)
+    off = 0
+    for t in tensors:
+        t.copy_(flat[off:off + t.numel()].view_as(t))
+        off += t.numel()
+
+
+def sharding_pass(dmp, mesh_dim=0, stage=1):
+    """ZeRO over ``mesh_dim`` (reference python/paddle/distributed/passes/auto_parallel_sharding.py:92-740
+    ``ShardingPass``, stages 1 / 2 / 3).  Parameters are assigned to owners greedily by size.
+
+    * stage 1 — optimizer state sharded: each rank steps only its own parameters (accumulators exist only for
+      those) and broadcasts them, one coalesced broadcast per owner;
+    * stage 2 — + gradients sharded: the per-use gradient all-reduces of the replicated parameters over
+      ``mesh_dim`` (the plan's ``c_identity`` ops, or a fused all-reduce from ``fuse_allreduce_pass``) are removed;
+      at the step every owner's gradients are reduced to it in one coalesced ``reduce`` (half the bytes of the
+      all-reduce) and the other ranks drop theirs;
+    * stage 3 — + parameters sharded: after the step a rank keeps only the parameters it owns (the others'
+      storage is released); the program's first op re-materialises them by one coalesced broadcast per owner, so
+      between steps every rank holds 1/n of the replicated parameters.
+    -> {param name: owner}; ``dmp.gather_params()`` materialises every parameter (e.g. before a checkpoint)."""
     from ....static.graph import Op
 
+    assert stage in (1, 2, 3)
     prog = dmp.program
     mesh = dmp._dm
     group = mesh.get_group(mesh_dim)
     n = mesh.size(mesh_dim)
     me = mesh.get_local_rank(mesh_dim)
-    ranks = mesh.mesh.movedim(mesh_dim, -1).reshape(-1, n)
-    row = next(r for r in ranks.tolist() if dist.get_rank() in r)
-    owners = {}
+    row = _row_of(mesh, mesh_dim)
+    if stage >= 2:
+        from .resharder import _grad_allreduce_fn
+
+        for op in prog.ops:
+            fn = op.fn
+            if op.kind == "torch" and getattr(fn, "comm", False) and fn.__name__ == "c_identity" and \
+                    isinstance(op.args[0], torch.Tensor) and op.args[0].requires_grad and mesh_dim in fn.dims:
+                rest = tuple(d for d in fn.dims if d != mesh_dim)
+                op.fn = _grad_allreduce_fn(fn.mesh, rest) if rest else _named(lambda x: x, "identity")
+        prog.ops = [o for o in prog.ops if not (o.kind == "call" and o.attrs.get("name") == "fused_allreduce_grads")]
+    owners, released = {}, []
     for i, op in enumerate(prog.ops):
         if op.kind != "optimize":
             continue
@@ -258,26 +294,261 @@ def sharding_pass(dmp, mesh_dim=0):
             owners[p.name] = o
             load[o] += p._t.numel()
         mine = [p for p in opt._parameter_list if owners[p.name] == me]
+        shapes = {p.name: (tuple(p._t.shape), p._t.dtype, p._t.device) for p in opt._parameter_list}
 
         def step(env, opt=opt, mine=mine):
             full = opt._parameter_list
             with torch.no_grad():
+                if stage >= 2:
+                    for o in range(n):
+                        ps = [p for p in full if owners[p.name] == o]
+                        if not ps:
+                            continue
+                        grads = [p._t.grad if p._t.grad is not None else torch.zeros_like(p._t) for p in ps]
+                        flat = torch.cat([g.reshape(-1) for g in grads])
+                        dist.reduce(flat, dst=row[o], group=group)
+                        off = 0
+                        for p, g in zip(ps, grads):
+                            k = g.numel()
+                            p._t.grad = flat[off:off + k].view_as(g).clone() if o == me else None
+                            off += k
                 opt._parameter_list, opt._mt_cache = mine, None
                 try:
                     opt.step()
                 finally:
                     opt._parameter_list, opt._mt_cache = full, None
-                for o in range(n):
-                    ps = [p._t for p in full if owners[p.name] == o]
-                    if not ps:
-                        continue
-                    flat = torch.cat([t.reshape(-1) for t in ps])
-                    dist.broadcast(flat, src=row[o], group=group)
-                    off = 0
-                    for t in ps:
-                        t.copy_(flat[off:off + t.numel()].view_as(t))
-                        off += t.numel()
+                if stage < 3:
+                    for o in range(n):
+                        ps = [p._t for p in full if owners[p.name] == o]
+                        if ps:
+                            _coalesced_broadcast(ps, row[o], group)
+                else:
+                    for p in full:
+                        if owners[p.name] != me:
+                            p._t.data = torch.empty(0, dtype=p._t.dtype, device=p._t.device)
             opt.clear_grad(set_to_zero=False)
 
-        prog.ops[i] = Op("call", None, (), {}, [], {"fn": step, "name": "sharding_stage1_step", "optimizer": opt})
+        prog.ops[i] = Op("call", None, (), {}, [], {"fn": step, "name": f"sharding_stage{stage}_step",
+                                                     "optimizer": opt})
+        released.append((opt, shapes))
+
+    def gather_params(env=None):
+        """(stage 3) re-materialise every parameter from its owner: one coalesced broadcast per owner."""
+        with torch.no_grad():
+            for opt, shapes in released:
+                for p in opt._parameter_list:
+                    shp, dt, dev = shapes[p.name]
+                    if tuple(p._t.shape) != shp:
+                        p._t.data = torch.empty(shp, dtype=dt, device=dev)
+                for o in range(n):
+                    ps = [p._t for p in opt._parameter_list if owners[p.name] == o]
+                    if ps:
+                        _coalesced_broadcast(ps, row[o], group)
+
+    if stage == 3:
+        prog.ops.insert(0, Op("call", None, (), {}, [], {"fn": gather_params, "name": "sharding_stage3_gather"}))
+        # stage 3 starts from the released state: a rank holds only its own parameters
+        with torch.no_grad():
+            for opt, _ in released:
+                for p in opt._parameter_list:
+                    if owners[p.name] != me:
+                        p._t.data = torch.empty(0, dtype=p._t.dtype, device=p._t.device)
+    dmp.gather_params = gather_params
     return owners
+
+
+# ------------------------------------------------------------------------------------------------ sequence parallel
+# ops whose output row i depends only on input row i of the sequence operand (the other operands are parameters or
+# per-row activations of the same length): the reduce-scatter can move in front of them
+_ROW_LOCAL = {"add", "sub", "mul", "div", "relu", "gelu", "silu", "sigmoid", "tanh", "swish", "addmm", "mm",
+              "matmul", "linear", "scale", "dropout", "rms_norm", "layer_norm", "cast", "pow", "neg", "exp"}
+
+
+def _consumers(prog):
+    from ....static.graph import VarRef
+
+    uses = {}
+    for i, op in enumerate(prog.ops):
+        for x in pytree.tree_leaves((op.args, op.kwargs)):
+            if isinstance(x, VarRef):
+                uses.setdefault(x.vid, []).append(i)
+        if "loss" in op.attrs:
+            uses.setdefault(op.attrs["loss"], []).append(i)
+    return uses
+
+
+def sequence_parallel_optimization_pass(dmp):
+    """Megatron sequence parallelism on the plan (reference python/paddle/distributed/passes/
+    auto_parallel_sequence_parallel_optimization.py:33): a partial sum that is all-reduced, then run through
+    row-local ops (residual add, activation, norm, a linear with replicated weights), then split on the sequence
+    (dim 0) over the same mesh dim is rewritten as ONE reduce-scatter onto the sequence shards followed by the same
+    ops on the shard — the all-reduce's second half and the redundant full-length ops disappear.  Per-row
+    activation operands of the moved ops are split to the shard (their gradient all-gathers back); a replicated
+    parameter operand gets a gradient all-reduce over the mesh dim (it now sees only the local rows).
+    -> number of rewritten chains."""
+    from ....static.graph import Op, VarRef
+    from ..placement import Partial, Replicate, Shard
+    from .resharder import _comm_fn, _grad_allreduce_fn, comm_kinds
+
+    prog = dmp.program
+    uses = _consumers(prog)
+    n_done = 0
+    i = 0
+    while i < len(prog.ops):
+        a = prog.ops[i]
+        fa = a.fn
+        if not (a.kind == "torch" and getattr(fa, "comm", False) and fa.__name__ in ("c_allreduce_sum", "c_allreduce_avg")
+                and hasattr(fa, "src")):
+            i += 1
+            continue
+        dims = [d for d, (s_, t_) in enumerate(zip(fa.src, fa.dst)) if isinstance(s_, Partial) and isinstance(t_, Replicate)]
+        # follow the single-consumer chain
+        chain, cur, b = [], a.outs[0], None
+        while True:
+            us = uses.get(cur, [])
+            if len(us) != 1:
+                break
+            e = prog.ops[us[0]]
+            fe = e.fn
+            if e.kind == "torch" and getattr(fe, "comm", False) and fe.__name__ == "c_split" and hasattr(fe, "dst"):
+                sd = [d for d, (s_, t_) in enumerate(zip(fe.src, fe.dst)) if isinstance(s_, Replicate) and isinstance(t_, Shard)]
+                if sd == dims and all(fe.dst[d].dim == 0 for d in sd):
+                    b = (us[0], e)
+                break
+            if e.kind not in ("torch", "native") or op_key(e) not in _ROW_LOCAL or len(e.outs) != 1:
+                break
+            seq_pos = [k for k, x in enumerate(e.args) if isinstance(x, VarRef) and x.vid == cur]
+            if op_key(e) in ("addmm",) and seq_pos != [1]:
+                break
+            if op_key(e) in ("mm", "matmul", "linear") and seq_pos != [0]:
+                break
+            chain.append((us[0], e))
+            cur = e.outs[0]
+        if b is None or not dims:
+            i += 1
+            continue
+        mesh = fa.mesh
+        nsh = 1
+        for d in dims:
+            nsh *= mesh.size(d)
+        rows = prog.vars[a.outs[0]].shape[0]
+        # the all-reduce becomes the reduce-scatter onto the sequence shards
+        dst = list(fa.src)
+        for d in dims:
+            dst[d] = Shard(0)
+        a.fn = _comm_fn(comm_kinds(fa.src, tuple(dst)), mesh, fa.src, tuple(dst))
+        old_out = a.outs[0]
+        ov = prog.vars[old_out]
+        nv = _new_var(prog, [ov.shape[0] // nsh] + list(ov.shape[1:]), ov.dtype)
+        a.outs = [nv._vid]
+        rename = {old_out: nv._vid}
+        inserts = []   # (before op index, Op)
+        for idx, e in chain:
+            new_args = []
+            for x in e.args:
+                if isinstance(x, VarRef) and x.vid in rename:
+                    new_args.append(VarRef(rename[x.vid]))
+                elif isinstance(x, VarRef) and len(prog.vars[x.vid].shape) > 0 and prog.vars[x.vid].shape[0] == rows:
+                    # a per-row activation operand: split it onto the shard too (backward: all-gather)
+                    xv = prog.vars[x.vid]
+                    sv = _new_var(prog, [rows // nsh] + list(xv.shape[1:]), xv.dtype)
+                    srcp = tuple(Replicate() for _ in fa.src)
+                    inserts.append((idx, Op("torch", _comm_fn(["c_split"], mesh, srcp, tuple(dst)), (x,), {},
+                                            [sv._vid])))
+                    new_args.append(VarRef(sv._vid))
+                elif isinstance(x, torch.Tensor) and x.requires_grad:
+                    # a replicated parameter now applied to the local rows only: its gradient is summed over dims
+                    pv = _new_var(prog, list(x.shape), x.dtype)
+                    inserts.append((idx, Op("torch", _grad_allreduce_fn(mesh, tuple(dims)), (x,), {}, [pv._vid])))
+                    new_args.append(VarRef(pv._vid))
+                else:
+                    new_args.append(x)
+            e.args = tuple(new_args)
+            old = e.outs[0]
+            evr = prog.vars[old]
+            ev = _new_var(prog, [evr.shape[0] // nsh] + list(evr.shape[1:]), evr.dtype)
+            e.outs = [ev._vid]
+            rename[old] = ev._vid
+        bidx, bop = b
+        bop.args = tuple(VarRef(rename[x.vid]) if isinstance(x, VarRef) and x.vid in rename else x for x in bop.args)
+        bop.fn = _named(lambda x: x, "identity")   # the split is already done
+        for idx, op in sorted(inserts, key=lambda t: -t[0]):
+            prog.ops.insert(idx, op)
+        uses = _consumers(prog)
+        n_done += 1
+        i += 1
+    return n_done
+
+
+# ------------------------------------------------------------------------------------------------ comm / compute overlap
+class _OverlapLinear(torch.autograd.Function):
+    """y = x @ w (+ b) whose input gradient is all-reduced over mesh dims: the all-reduce of dX is issued
+    asynchronously right after dX and waited for only after dW / db — the column-parallel pattern of
+    allreduce_matmul_grad_overlapping.py:37."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, mesh, dims):
+        ctx.save_for_backward(x, w)
+        ctx.mesh, ctx.dims, ctx.has_b = mesh, dims, b is not None
+        return torch.addmm(b, x, w) if b is not None else x @ w
+
+    @staticmethod
+    def backward(ctx, g):
+        from ..reshard import COMM_LOG, _group
+
+        x, w = ctx.saved_tensors
+        dx = (g @ w.t()).contiguous()
+        works = []
+        for d in ctx.dims:
+            works.append(dist.all_reduce(dx, op=dist.ReduceOp.SUM, group=_group(ctx.mesh, d), async_op=True))
+            COMM_LOG.append(("grad_all_reduce_overlap", d))
+            if len(ctx.dims) > 1:   # several dims: each sum must finish before the next starts
+                works.pop().wait()
+        dw = x.t() @ g
+        db = g.sum(0) if ctx.has_b else None
+        for wk in works:
+            wk.wait()
+        return dx, dw, db, None, None
+
+
+def allreduce_matmul_grad_overlap_pass(dmp):
+    """(reference python/paddle/distributed/passes/allreduce_matmul_grad_overlapping.py:37) a ``c_identity`` on a
+    linear's activation input (its backward all-reduces dX over the mesh: the column-parallel input) followed by
+    that linear (``addmm`` / ``mm`` / ``matmul``, the activation as the row operand) becomes one op whose backward
+    overlaps the dX all-reduce with the dW / db GEMMs instead of running it after them.  -> fused pairs."""
+    from ....static.graph import Op, VarRef
+
+    prog = dmp.program
+    uses = _consumers(prog)
+    n = 0
+    for i, op in enumerate(prog.ops):
+        f = op.fn
+        if not (op.kind == "torch" and getattr(f, "comm", False) and f.__name__ == "c_identity"
+                and isinstance(op.args[0], VarRef) and hasattr(f, "mesh")):
+            continue
+        us = uses.get(op.outs[0], [])
+        if len(us) != 1:
+            continue
+        mm = prog.ops[us[0]]
+        key = op_key(mm) if mm.kind in ("torch", "native") else ""
+        if key == "addmm" and len(mm.args) == 3 and isinstance(mm.args[1], VarRef) and mm.args[1].vid == op.outs[0] \
+                and not mm.kwargs:
+            b, w = mm.args[0], mm.args[2]
+        elif key in ("mm", "matmul") and len(mm.args) == 2 and isinstance(mm.args[0], VarRef) and \
+                mm.args[0].vid == op.outs[0] and not mm.kwargs:
+            b, w = None, mm.args[1]
+        else:
+            continue
+        if not (isinstance(w, (torch.Tensor, VarRef))) or (isinstance(w, torch.Tensor) and w.dim() != 2):
+            continue
+        mesh, dims = f.mesh, tuple(f.dims)
+
+        def fused(x, w_, b_=None, mesh=mesh, dims=dims):
+            return _OverlapLinear.apply(x, w_, b_, mesh, dims)
+
+        mm.fn = _named(fused, "linear_overlap_dx_allreduce", comm=True)
+        mm.args = (op.args[0], w) + ((b,) if b is not None else ())
+        op.fn = _named(lambda x: x, "identity")   # its all-reduce moved into the fused backward
+        op.fn.comm = False
+        n += 1
+    return n

@@ -71,6 +71,7 @@ def _comm_fn(kinds, mesh, src, dst):
 
     fn.__name__ = fn.__qualname__ = "+".join(kinds) or "identity"
     fn.comm = True
+    fn.mesh, fn.src, fn.dst = mesh, tuple(src), tuple(dst)   # what passes (sequence_parallel_optimization) rewrite
     return fn
 
 
@@ -94,6 +95,7 @@ def _grad_allreduce_fn(mesh, dims):
     fn.__name__ = fn.__qualname__ = "c_identity"
     fn.comm = True
     fn.dims = tuple(dims)
+    fn.mesh = mesh
     return fn
 
 

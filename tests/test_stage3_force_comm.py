@@ -22,6 +22,10 @@ def _run(dev, force, acc=1):
                 "PADDLE2_AMD_STAGE3_FORCE_COMM": "1" if force else "0", "OMP_NUM_THREADS": "2"})
     if dev == "cpu":
         env.update({"PADDLE2_AMD_DEVICE": "cpu", "PADDLE_DISTRI_BACKEND": "gloo"})
+    else:
+        # deterministic flash backward (per-key-block dQ slabs summed in a fixed order): the default fp32-atomic dQ
+        # makes two identical runs differ in the last bits, which would hide what this test compares
+        env["PADDLE2_AMD_FA_DQ_ATOMIC"] = "0"
     p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "workers", "force_comm_worker.py")], env=env,
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-4000:]
@@ -46,5 +50,15 @@ def test_force_comm_matches_short_circuit_cpu(acc):
 @pytest.mark.gpu
 @pytest.mark.parametrize("acc", [1, 2])
 def test_force_comm_matches_short_circuit_gpu(acc):
-    b = _check("cuda", acc)
-    assert b["pg"] == "pdrccl"
+    """On the GPU some backward kernels add with fp32 atomics (embedding gradient, flash dQ), so two runs of the
+    SAME path may differ in the last bits: the forced-comm run must then be as close to the short-circuit as a
+    second short-circuit run is (bitwise equal whenever the short-circuit path repeats bitwise)."""
+    a, a2, b = _run("cuda", False, acc), _run("cuda", False, acc), _run("cuda", True, acc)
+    assert not any(a["comm"]) and all(b["comm"]) and b["initialized"] and b["pg"] == "pdrccl"
+    assert a["losses"][0] == b["losses"][0]   # the first forward reads the same parameters
+    noise = max(abs(x - y) for x, y in zip(a["losses"], a2["losses"]))
+    diff = max(abs(x - y) for x, y in zip(a["losses"], b["losses"]))
+    if noise == 0.0:
+        assert a["losses"] == b["losses"] and a["digest"] == b["digest"], (a, b)
+    else:
+        assert diff <= 4 * noise + 1e-6, (a["losses"], a2["losses"], b["losses"])

@@ -168,7 +168,8 @@ def test_resharder_dist_main_program_trains_like_serial(mode):
 
 
 @pytest.mark.parametrize("passes", ["fuse", "merge", "recompute", "sharding", "fuse,sharding", "amp", "fuse,merge",
-                                    "merge,fuse"])
+                                    "merge,fuse", "sharding2", "fuse,sharding2", "sharding3", "spopt", "overlap",
+                                    "spopt,overlap"])
 def test_static_passes_train_like_serial(passes):
     """Passes over the dist_main_program of a data-parallel plan (2 ranks, Adam): fused + bucketed gradient
     all-reduce, gradient merge (k = 2), recompute of an op range, sharding stage 1 (each rank holds the optimizer
@@ -180,10 +181,21 @@ def test_static_passes_train_like_serial(passes):
         assert o["param_err"] < (5e-2 if passes == "amp" else 1e-5), o["param_err"]
         if "fuse" in passes:
             # with gradient merge (k = 2) the sum runs once per merged step, at the k-step boundary
-            assert o["buckets"] >= 1 and o["fused_calls"] == (2 if "merge" in passes else 4)
+            # (stage 2 replaces the fused all-reduce by its reduce-to-owner: the fused op never runs)
+            calls = 0 if "sharding2" in passes else (2 if "merge" in passes else 4)
+            assert o["buckets"] >= 1 and o["fused_calls"] == calls
         if passes == "recompute":
             assert len(o["recompute_ops"]) == 1
         if "sharding" in passes:
             assert 0 < o["my_acc"] < o["n_params"]
         if passes == "amp":
             assert o["amp_ops"] >= 2
+        if "sharding2" in passes:   # the per-use gradient all-reduces are gone (reduced to owners at the step)
+            assert "c_identity" not in o["comm_after"] and "c_identity" in o["comm_before"], o
+        if passes == "sharding3":   # between steps a rank holds only the parameters it owns
+            assert 0 < o["released"] < o["n_params_total"], o
+        if "spopt" in passes:       # all-reduce -> row-local ops -> split became ONE reduce-scatter
+            assert o["spopt"] >= 1 and "c_reducescatter" in o["comm_after"], o
+            assert "c_allreduce_sum" in o["comm_before"] and "c_allreduce_sum" not in o["comm_after"], o
+        if "overlap" in passes:
+            assert o["overlap"] >= 1 and "linear_overlap_dx_allreduce" in o["comm_after"], o

@@ -10,9 +10,11 @@ import numpy as np  # noqa: E402
 
 import paddle2_amd as paddle  # noqa: E402
 import paddle2_amd.distributed as dist  # noqa: E402
-from paddle2_amd.distributed.auto_parallel.static import (amp_pass, build_dist_main_program,  # noqa: E402
+from paddle2_amd.distributed.auto_parallel.static import (allreduce_matmul_grad_overlap_pass,  # noqa: E402
+                                                           amp_pass, build_dist_main_program,
                                                            fuse_allreduce_pass, gradient_merge_pass,
-                                                           parallelize_program, recompute_pass, sharding_pass)
+                                                           parallelize_program, recompute_pass,
+                                                           sequence_parallel_optimization_pass, sharding_pass)
 from _dist import write_result  # noqa: E402
 
 dist.init_parallel_env()
@@ -31,18 +33,45 @@ class MLP(paddle.nn.Layer):
         return self.fc2(paddle.nn.functional.gelu(self.fc1(x))).pow(2).mean()
 
 
+class TPMLP(paddle.nn.Layer):
+    """column fc1 / row fc2 (Megatron MLP) + residual + an fc3 head whose loss rows are sharded: the plan carries a
+    row-parallel all-reduce -> row-local ops -> sequence split chain and a column-parallel input c_identity"""
+
+    def __init__(self):
+        super().__init__()
+        self.fc1 = paddle.nn.Linear(8, 16)
+        self.fc2 = paddle.nn.Linear(16, 8)
+        self.fc3 = paddle.nn.Linear(8, 4)
+
+    def forward(self, x, y):
+        h = self.fc2(paddle.nn.functional.gelu(self.fc1(x)))
+        h = paddle.nn.functional.relu(h + x)
+        return (self.fc3(h) - y).pow(2).mean()
+
+
+tp = any(p_ in ("spopt", "overlap") for p_ in passes)
 paddle.seed(0)
-net, ref = MLP(), MLP()
+net, ref = (TPMLP(), TPMLP()) if tp else (MLP(), MLP())
 ref.set_state_dict(net.state_dict())
 main = paddle.static.Program()
 paddle.enable_static()
 opt = paddle.optimizer.Adam(0.05, parameters=net.parameters())
 with paddle.static.program_guard(main, paddle.static.Program()):
     xs = paddle.static.data("x", [8, 8], "float32")
-    loss = net(xs)
+    if tp:
+        ys = paddle.static.data("y", [8, 4], "float32")
+        loss = net(xs, ys)
+    else:
+        loss = net(xs)
     opt.minimize(loss)
 paddle.disable_static()
-dmp = build_dist_main_program(parallelize_program(main, mesh, {"x": [dist.Shard(0)]}), [loss])
+if tp:
+    ann = {"y": [dist.Shard(0)], net.fc1.weight: [dist.Shard(1)], net.fc1.bias: [dist.Shard(0)],
+           net.fc2.weight: [dist.Shard(0)]}
+else:
+    ann = {"x": [dist.Shard(0)]}
+dmp = build_dist_main_program(parallelize_program(main, mesh, ann), [loss])
+out["comm_before"] = dmp.comm_ops()
 k = 2 if "merge" in passes else 1
 for name in passes:   # in the order given: fuse-then-merge and merge-then-fuse must both sum once per merged step
     if name == "fuse":
@@ -56,6 +85,14 @@ if "recompute" in passes:
     out["recompute_ops"] = [o.name for o in dmp.program.ops if getattr(o.fn, "recompute", False)]
 if "sharding" in passes:
     owners = sharding_pass(dmp, 0)
+for st in (2, 3):
+    if f"sharding{st}" in passes:
+        owners = sharding_pass(dmp, 0, stage=st)
+if "spopt" in passes:
+    out["spopt"] = sequence_parallel_optimization_pass(dmp)
+if "overlap" in passes:
+    out["overlap"] = allreduce_matmul_grad_overlap_pass(dmp)
+out["comm_after"] = dmp.comm_ops()
 if "amp" in passes:
     out["amp_ops"] = amp_pass(dmp)
 exe = paddle.static.Executor()
@@ -63,17 +100,36 @@ ropt = paddle.optimizer.Adam(0.05, parameters=ref.parameters())
 losses, ref_losses = [], []
 for i in range(4):
     xi = np.random.RandomState(30 + i).randn(8, 8).astype("float32")
-    (lv,) = exe.run(dmp.program, feed=dmp.local_feed({"x": xi}), fetch_list=[dmp.fetch(loss)])
+    yi = np.random.RandomState(60 + i).randn(8, 4).astype("float32")
+    feed = {"x": xi, "y": yi} if tp else {"x": xi}
+    (lv,) = exe.run(dmp.program, feed=dmp.local_feed(feed), fetch_list=[dmp.fetch(loss)])
     losses.append(float(lv))
-    rl = ref(paddle.to_tensor(xi))
+    rl = ref(paddle.to_tensor(xi), paddle.to_tensor(yi)) if tp else ref(paddle.to_tensor(xi))
     (rl / k).backward()
     if (i + 1) % k == 0:
         ropt.step()
         ropt.clear_grad()
     ref_losses.append(float(rl.numpy()))
 out["losses"], out["ref"] = losses, ref_losses
-out["param_err"] = max(float(np.abs(a.numpy() - b.numpy()).max()) for a, b in zip(net.parameters(), ref.parameters()))
-if "sharding" in passes:
+if any(f"sharding{st}" in passes for st in (2, 3)):
+    out["released"] = sum(1 for p in net.parameters() if p._t.numel() == 0)
+    out["n_params_total"] = len(list(net.parameters()))
+    dmp.gather_params()
+if tp:
+    # TP-sharded parameters: compare the local shard with the matching slice of the serial parameter
+    def _local(ref_p, p):
+        r = ref_p.numpy()
+        if tuple(r.shape) == tuple(p._t.shape):
+            return r
+        ax = [d for d in range(r.ndim) if r.shape[d] != p._t.shape[d]][0]
+        k = p._t.shape[ax]
+        return np.take(r, range(dist.get_rank() * k, (dist.get_rank() + 1) * k), axis=ax)
+
+    out["param_err"] = max(float(np.abs(_local(b, a) - a.numpy()).max()) for a, b in zip(net.parameters(),
+                                                                                         ref.parameters()))
+else:
+    out["param_err"] = max(float(np.abs(a.numpy() - b.numpy()).max()) for a, b in zip(net.parameters(), ref.parameters()))
+if any(p_.startswith("sharding") for p_ in passes):
     out["my_acc"] = len(opt._accumulators.get("moment1", {}))
     out["n_params"] = len(opt._parameter_list)
 if "fuse" in passes:
