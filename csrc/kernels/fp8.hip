@@ -7,7 +7,9 @@
 // computes this tensor's amax in the same pass (one read of the bf16 tensor), so quantization
 // is a single fused pass:
 //   * cast_amax:            y = sat(x * scale) -> fp8, amax = max|x|            (row-major)
-//   * cast_transpose_amax:  y = sat(x * scale) and yT = y^T -> fp8, amax       (64x64 LDS tiles)
+//   * cast_transpose_amax:  y = sat(x * scale) and yT = y^T -> fp8, amax       (bf16: in-register 8x8 byte
+//                           transposes, cast_transpose_amax_v2_kernel; other types: 64x64 LDS tiles)
+// amax is kAmaxSlots floats per tensor role (sharded same-address atomics), folded by update_scale.
 // The transposed copy is what the column-major B operand of the fp8 GEMM wants for the weight
 // (forward) and for x / dy (weight-gradient GEMM).  Conversion uses v_cvt_pk_fp8_f32 /
 // v_cvt_pk_bf8_f32 (OCP encodings on gfx950) after saturating to the format's max finite value.
@@ -39,14 +41,75 @@ __device__ __forceinline__ void atomic_max_pos(float* addr, float v) {
   atomicMax(reinterpret_cast<unsigned*>(addr), __float_as_uint(v));
 }
 
-// block-wide max, then ONE atomic per workgroup (grids are capped at ~1k workgroups, so the
-// per-tensor amax costs ~1k same-address atomics instead of one per wave of every tile)
+// A tensor role's amax lives in kAmaxSlots floats: workgroup b adds into slot b % kAmaxSlots (same-address atomics
+// serialise at ~12 ns each — a 1k-workgroup cast spent ~12 us on its ONE amax word); update_scale folds the slots.
+constexpr int kAmaxSlots = 64;
+
+// block-wide max, then ONE atomic per workgroup into its slot
 __device__ __forceinline__ void block_amax(float m, float* amax) {
   __shared__ float red[4];
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0 && amax) atomic_max_pos(amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+  if (threadIdx.x == 0 && amax)
+    atomic_max_pos(amax + (blockIdx.x % kAmaxSlots), fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
+
+// 4 x 4 byte transpose: rows a..d (each 4 fp8 of consecutive columns) -> 4 words, word j = column j's 4 rows
+__device__ __forceinline__ void tr4x4(unsigned a, unsigned b, unsigned c, unsigned d, unsigned (&o)[4]) {
+  const unsigned ab0 = __builtin_amdgcn_perm(b, a, 0x05010400u), ab1 = __builtin_amdgcn_perm(b, a, 0x07030602u);
+  const unsigned cd0 = __builtin_amdgcn_perm(d, c, 0x05010400u), cd1 = __builtin_amdgcn_perm(d, c, 0x07030602u);
+  o[0] = __builtin_amdgcn_perm(cd0, ab0, 0x05040100u);
+  o[1] = __builtin_amdgcn_perm(cd0, ab0, 0x07060302u);
+  o[2] = __builtin_amdgcn_perm(cd1, ab1, 0x05040100u);
+  o[3] = __builtin_amdgcn_perm(cd1, ab1, 0x07060302u);
+}
+
+// x [R, C] bf16 (C % 8 == 0, R % 8 == 0) -> y [R, C] (optional) and yT [C, R], LDS-free: a lane quantises an 8 x 8 block
+// (8 rows x one 16-B load each), writes its 8 row words of y (8 B each) and, after an in-register byte transpose
+// (v_perm), its 8 column words of yT (8 B each: rows 8rb..8rb+7 of one column).  A wave covers 64 rows x 64 columns
+// (lane: rb = lane & 7, cb = lane >> 3 -> the 8 lanes of a row block read one 128-B row segment, the 8 lanes of a
+// column write one 64-B yT segment); a workgroup 64 rows x 256 columns.  Replaces the 64 x 64 fp32 LDS-tile kernel
+// (two barriers per tile, 4-B stores; ~57 us per [4096, 5120] cast in the GPT-3 13B fp8 step).
+template <bool E5M2>
+__global__ __launch_bounds__(256) void cast_transpose_amax_v2_kernel(const unsigned short* __restrict__ x,
+                                                                     uint8_t* __restrict__ y, uint8_t* __restrict__ yT,
+                                                                     int R, int C, const float* __restrict__ scale,
+                                                                     float* __restrict__ amax) {
+  const float s = scale[0];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rb = lane & 7, cb = lane >> 3;
+  const int tilesC = (C + 255) / 256;
+  const int r = (blockIdx.x / tilesC) * 64 + 8 * rb;
+  const int c = (blockIdx.x % tilesC) * 256 + wave * 64 + 8 * cb;
+  float m = 0.f;
+  if (r < R && c < C) {
+    unsigned lo[8], hi[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v[8];
+      load_vec<bf16, 8>(reinterpret_cast<const bf16*>(x) + (long)(r + i) * C + c, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
+      lo[i] = pack4<E5M2>(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
+      hi[i] = pack4<E5M2>(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
+    }
+    if (y) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) *reinterpret_cast<uint2*>(y + (long)(r + i) * C + c) = make_uint2(lo[i], hi[i]);
+    }
+    unsigned t0[4], t1[4], t2[4], t3[4];
+    tr4x4(lo[0], lo[1], lo[2], lo[3], t0);   // columns 0-3, rows 0-3
+    tr4x4(lo[4], lo[5], lo[6], lo[7], t1);   // columns 0-3, rows 4-7
+    tr4x4(hi[0], hi[1], hi[2], hi[3], t2);   // columns 4-7, rows 0-3
+    tr4x4(hi[4], hi[5], hi[6], hi[7], t3);   // columns 4-7, rows 4-7
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      *reinterpret_cast<uint2*>(yT + (long)(c + j) * R + r) = make_uint2(t0[j], t1[j]);
+      *reinterpret_cast<uint2*>(yT + (long)(c + 4 + j) * R + r) = make_uint2(t2[j], t3[j]);
+    }
+  }
+  block_amax(m, amax);
 }
 
 template <typename T, bool E5M2>
@@ -164,15 +227,17 @@ __global__ void update_scale_kernel(float* __restrict__ hist, int len, float* __
                                     float* __restrict__ scale, float* __restrict__ inv_scale, float fp8_max,
                                     float margin_pow2) {
   if (threadIdx.x != 0) return;
+  float a = 0.f;
+  for (int i = 0; i < kAmaxSlots; ++i) a = fmaxf(a, amax[i]);
   for (int i = len - 1; i > 0; --i) hist[i] = hist[i - 1];
-  hist[0] = amax[0];
+  hist[0] = a;
   float m = 0.f;
   for (int i = 0; i < len; ++i) m = fmaxf(m, hist[i]);
   float s = scale[0];
   if (m > 0.f && isfinite(m)) s = fp8_max / m / margin_pow2;
   scale[0] = s;
   inv_scale[0] = 1.f / s;
-  amax[0] = 0.f;
+  for (int i = 0; i < kAmaxSlots; ++i) amax[i] = 0.f;
 }
 
 }  // namespace fp8
@@ -193,6 +258,15 @@ extern "C" int pd_fp8_cast(int dt, int e5m2, const void* x, void* y, void* yT, l
                                                                                amax))
     if (e5m2) { PD_FP8_CAST(true); } else { PD_FP8_CAST(false); }
 #undef PD_FP8_CAST
+  } else if (dt == kBF16 && C % 8 == 0 && R % 8 == 0 && (size_t)x % 16 == 0 && (size_t)yT % 8 == 0 &&
+             (!y || (size_t)y % 8 == 0) && R * C < (1L << 31)) {
+    const long wgs = ((C + 255) / 256) * ((R + 63) / 64);
+    if (e5m2)
+      fp8::cast_transpose_amax_v2_kernel<true><<<(unsigned)wgs, 256, 0, st>>>(
+          (const unsigned short*)x, (uint8_t*)y, (uint8_t*)yT, (int)R, (int)C, scale, amax);
+    else
+      fp8::cast_transpose_amax_v2_kernel<false><<<(unsigned)wgs, 256, 0, st>>>(
+          (const unsigned short*)x, (uint8_t*)y, (uint8_t*)yT, (int)R, (int)C, scale, amax);
   } else {
     long tiles = ((C + 63) / 64) * ((R + 63) / 64);
     dim3 grid((unsigned)(tiles < 1024 ? tiles : 1024));

@@ -59,7 +59,12 @@ __device__ __forceinline__ void mfma8_dma(f32x4v& c, const i32x8& b, const i32x8
       : "memory");
 }
 
-template <int FA, int FB, int EPI, bool TSK = false>
+// SCHED 1 (the late-wait K-tile): the one barrier at n = 0 becomes two — lgkmcnt(0) + barrier at n = 0 (every wave
+// holds tile t's fragments: stage(t) may take tile t+2's pieces) and vmcnt(13) + barrier before MFMA 14 (tile t+1
+// landed; this tile's first 13 pieces stay in flight) — and tile t+1's fragments are read from MFMA 14 on (B_7's
+// second set at 14-15, A at 16-31, B_j at >= 8j + 8: 32-41, 48-49, 56-57).  A piece of tile t+1 then has ~62
+// MFMAs (instead of ~48) between its issue and the wait that needs it.
+template <int FA, int FB, int EPI, bool TSK = false, int SCHED = 0>
 __global__ __launch_bounds__(NTHR4, 1) void gemm_f8_kernel(Params p) {
   __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
   const unsigned sbase = (unsigned)(size_t)(lds_char*)smem_raw;
@@ -158,28 +163,56 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_f8_kernel(Params p) {
     sfor<64>([&](auto Q) {
       constexpr int n = decltype(Q)::value;
       constexpr int j = n >> 3, i = n & 7;
-      if constexpr (n == 0) {
+      if constexpr (SCHED == 1) {
+        if constexpr (n == 0) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (n == 14) {
+          asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (n == 14) bx[7 + nx] = frag4<true, 7, 0, nx>(rb);
+        if constexpr (n == 15) by[7 + nx] = frag4<true, 7, 1, nx>(rb);
+        if constexpr (n >= 16 && n <= 31) {
+          constexpr int r = n - 16, u = r >> 1;
+          if constexpr (r & 1)
+            ay[nx][u] = frag4<true, u, 1, nx>(ra);
+          else
+            ax[nx][u] = frag4<true, u, 0, nx>(ra);
+        }
+        constexpr int bj = (n >= 32 && n <= 41) ? (n - 32) >> 1 : (n == 48 || n == 49) ? 5 : (n == 56 || n == 57) ? 6 : -1;
+        if constexpr (bj >= 0) {
+          if constexpr ((n & 1) == 0)
+            bx[bj < 0 ? 0 : bj] = frag4<true, (bj < 0 ? 0 : bj), 0, nx>(rb);
+          else
+            by[bj < 0 ? 0 : bj] = frag4<true, (bj < 0 ? 0 : bj), 1, nx>(rb);
+        }
+      }
+      if constexpr (SCHED == 0 && n == 0) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
       }
       // ---- tile t+1's fragments (stage nx)
-      if constexpr (n >= 2 && n <= 32 && n % 2 == 0) {
+      if constexpr (SCHED == 0 && n >= 2 && n <= 32 && n % 2 == 0) {
         constexpr int r = (n - 2) / 2, u = r >> 1;
         if constexpr (r & 1)
           ay[nx][u] = frag4<true, u, 1, nx>(ra);
         else
           ax[nx][u] = frag4<true, u, 0, nx>(ra);
       }
-      if constexpr (n >= 8 && n <= 57 && (n % 8) < 2) {
+      if constexpr (SCHED == 0 && n >= 8 && n <= 57 && (n % 8) < 2) {
         constexpr int jb = n / 8 - 1;
         if constexpr (n % 8 == 0)
           bx[jb] = frag4<true, jb, 0, nx>(rb);
         else
           by[jb] = frag4<true, jb, 1, nx>(rb);
       }
-      if constexpr (n == 36) bx[7 + nx] = frag4<true, 7, 0, nx>(rb);
-      if constexpr (n == 37) by[7 + nx] = frag4<true, 7, 1, nx>(rb);
+      if constexpr (SCHED == 0 && n == 36) bx[7 + nx] = frag4<true, 7, 0, nx>(rb);
+      if constexpr (SCHED == 0 && n == 37) by[7 + nx] = frag4<true, 7, 1, nx>(rb);
       // ---- MFMA n, with piece n - 1 of tile t+2 behind it for n = 1..16 (A pieces, then B)
       constexpr int jj = j < 7 ? j : 7 + st;
       f32x4v& c = acc[j >> 2][i][j & 3];
@@ -286,10 +319,17 @@ extern "C" int pd_gemm_f8(int fa, int fb, int epi, const void* A, long lda, cons
     p.part = (float*)ws; p.ksplit = ks; p.tail_cap = R;
   }
   const dim3 grid(std::min(nwg - R, cus)), tgrid(R * ks), rgrid(BM * BN / 1024, R);
+  // K-tile schedule: PADDLE2_AMD_FP8_SCHED (0 = one barrier per K-tile, 1 = the late-wait schedule), read per call
+  const char* se = getenv("PADDLE2_AMD_FP8_SCHED");
+  const int sched = se ? atoi(se) : 0;
 #define PD_F8(FA_, FB_, E_)                                                                   \
-  if (nwg > R) gemm_f8_kernel<FA_, FB_, E_><<<grid, NTHR4, 0, st>>>(p);                      \
+  if (nwg > R) {                                                                              \
+    if (sched == 1) gemm_f8_kernel<FA_, FB_, E_, false, 1><<<grid, NTHR4, 0, st>>>(p);       \
+    else gemm_f8_kernel<FA_, FB_, E_><<<grid, NTHR4, 0, st>>>(p);                             \
+  }                                                                                           \
   if (ks) {                                                                                   \
-    gemm_f8_kernel<FA_, FB_, E_, true><<<tgrid, NTHR4, 0, st>>>(p);                           \
+    if (sched == 1) gemm_f8_kernel<FA_, FB_, E_, true, 1><<<tgrid, NTHR4, 0, st>>>(p);       \
+    else gemm_f8_kernel<FA_, FB_, E_, true><<<tgrid, NTHR4, 0, st>>>(p);                      \
     tail_reduce_kernel<E_><<<rgrid, 256, 0, st>>>(p, nwg - R);                               \
   }
   switch (fa * 100 + fb * 10 + epi) {

@@ -25,6 +25,7 @@ from . import _native as N
 E4M3 = torch.float8_e4m3fn
 E5M2 = torch.float8_e5m2
 _MAX = {E4M3: 448.0, E5M2: 57344.0}
+AMAX_SLOTS = 64   # csrc/kernels/fp8.hip kAmaxSlots
 
 
 class FP8TensorMeta:
@@ -34,7 +35,9 @@ class FP8TensorMeta:
         dev = device or torch.device("cpu")
         self.fmt = fmt
         self.history = torch.zeros(history_len, dtype=torch.float32, device=dev)
-        self.amax = torch.zeros(1, dtype=torch.float32, device=dev)
+        # AMAX_SLOTS floats: the native cast kernels spread their per-workgroup atomicMax over the slots
+        # (csrc/kernels/fp8.hip kAmaxSlots); update() folds them
+        self.amax = torch.zeros(AMAX_SLOTS, dtype=torch.float32, device=dev)
         self.scale = torch.ones(1, dtype=torch.float32, device=dev)
         self.inv_scale = torch.ones(1, dtype=torch.float32, device=dev)
         self.margin = margin
@@ -62,7 +65,7 @@ class FP8TensorMeta:
                                         float(2 ** self.margin), N.stream())
             return
         self.history.copy_(torch.roll(self.history, 1))
-        self.history[0] = self.amax[0]
+        self.history[0] = self.amax.max()
         m = self.history.max()
         if float(m) > 0 and torch.isfinite(m):
             self.scale.fill_(_MAX[self.fmt] / float(m) / 2 ** self.margin)
@@ -87,7 +90,7 @@ def cast(x2, meta: FP8TensorMeta, transpose=False, keep_rowmajor=True):
                             meta.scale.data_ptr(), meta.amax.data_ptr(), N.stream())
         return (None if q is None else q.view(meta.fmt)), (None if qT is None else qT.view(meta.fmt))
     xf = x2.float()
-    meta.amax.copy_(torch.maximum(meta.amax, xf.abs().max().reshape(1)))
+    meta.amax[:1].copy_(torch.maximum(meta.amax[:1], xf.abs().max().reshape(1)))
     q = (xf * meta.scale).clamp(-_MAX[meta.fmt], _MAX[meta.fmt]).to(meta.fmt)
     return (q if (keep_rowmajor or not transpose) else None), (q.t().contiguous() if transpose else None)
 

@@ -66,13 +66,14 @@ def weight_only_matmul(x, w, scale, weight_dtype="int8", group_size=-1, bias=Non
 import os as _os  # noqa: E402
 
 DECODE_GEMM = _os.environ.get("PADDLE2_AMD_DECODE_GEMM", "auto")   # auto | native | blas
+DEC64_WAVES = int(_os.environ.get("PADDLE2_AMD_DEC64_WAVES", "8"))  # waves per workgroup of the M > 16 kernel
 
 
 def decode_ok(x, wt):
     """The native stream kernel is taken where it measured faster than hipBLASLt's skinny GEMM
     (profiles/r4_decode_gemm.md): M <= 16 with N <= 8192 (the o / down projections: 2.6-4.0 vs 1.9-3.4 TB/s);
-    the wide projections and M = 64 stay on the library kernel.  PADDLE2_AMD_DECODE_GEMM=native forces it for
-    every M <= 64."""
+    16 < M <= 64 runs the whole-K stream kernel (dec64_kernel: no split-K partials through HBM).
+    PADDLE2_AMD_DECODE_GEMM=native forces the native kernels for every M <= 64, =blas the library."""
     M, K = x.shape
     Nn = wt.shape[0]
     ok = (x.device.type == "cuda" and x.dtype == torch.bfloat16 and wt.dtype == torch.bfloat16 and 1 <= M <= 64
@@ -81,7 +82,9 @@ def decode_ok(x, wt):
         return False
     if DECODE_GEMM == "blas":
         return False
-    return DECODE_GEMM == "native" or (M <= 16 and Nn <= 8192)
+    if M > 16:
+        return Nn % 16 == 0   # the whole-K MFMA stream kernel (dec64_kernel): the b17-64 serving step
+    return DECODE_GEMM == "native" or Nn <= 8192
 
 
 def decode_matmul(x, wt, bias=None):
@@ -94,6 +97,12 @@ def decode_matmul(x, wt, bias=None):
     M, K = x.shape
     Nn = wt.shape[0]
     C = N.native()
+    if M > 16:
+        out = torch.empty(M, Nn, dtype=x.dtype, device=x.device)
+        if bias is not None:
+            bias = bias.to(torch.bfloat16).contiguous()
+        C.dec64_gemm(x.data_ptr(), wt.data_ptr(), N.ptr(bias), out.data_ptr(), M, Nn, K, DEC64_WAVES, N.stream())
+        return out
     S = C.dec_splits(M, Nn, K)
     ws = torch.empty(S * M * Nn, dtype=torch.float32, device=x.device)
     out = torch.empty(M, Nn, dtype=x.dtype, device=x.device)

@@ -12,8 +12,10 @@ timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 > $O/bench_plain.log 
 r=$?; tail -1 $O/bench_plain.log; [ $r -ne 0 ] && { tail -30 $O/bench_plain.log; exit $r; }
 PADDLE2_AMD_STAGE3_FORCE_COMM=1 timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 > $O/bench_force.log 2>&1
 r=$?; tail -1 $O/bench_force.log; [ $r -ne 0 ] && { tail -30 $O/bench_force.log; exit $r; }
+timeout -k 10 300 python -u scripts/exp_decode64.py > $O/dec64.jsonl 2> $O/dec64.err
+r=$?; cat $O/dec64.jsonl; [ $r -ne 0 ] && { tail -20 $O/dec64.err; exit $r; }
 timeout -k 10 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread -p no:cacheprovider -m gpu \
-  tests/test_stage3_force_comm.py tests/test_ipc_allreduce.py tests/test_fused_act.py tests/test_comm_context_gpu.py \
+  tests/test_decode_gemm_gpu.py tests/test_stage3_force_comm.py tests/test_ipc_allreduce.py tests/test_fused_act.py tests/test_comm_context_gpu.py \
   tests/test_native_pg_gpu.py tests/test_bench_configs.py > $O/tests.log 2>&1
 r=$?; tail -3 $O/tests.log; [ $r -ne 0 ] && { grep -E "^E |FAIL" $O/tests.log | head -30; exit $r; }
 exit 0

@@ -26,3 +26,23 @@ def test_decode_gemm_matches_fp32(M, N, K, monkeypatch):
     ref = x.float() @ wt.float().t() + b.float()
     assert y.shape == (M, N) and y.dtype == torch.bfloat16
     assert _rel(y, ref) < 8e-3
+
+
+@pytest.mark.parametrize("waves", [4, 8])
+@pytest.mark.parametrize("M", [17, 40, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 11008), (12288, 4096), (48, 192)])
+def test_dec64_whole_k_kernel(M, N, K, waves, monkeypatch):
+    """The M > 16 whole-K kernel (dec64_kernel) at both workgroup widths, ragged M, K not a multiple of the wave
+    count's 64-wide steps (11008 = 172 steps), a tiny shape with fewer steps than waves."""
+    monkeypatch.setattr(WO, "DECODE_GEMM", "auto")
+    monkeypatch.setattr(WO, "DEC64_WAVES", waves)
+    g = torch.Generator(device=dev).manual_seed(7 * M + N)
+    x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    wt = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=dev, generator=g).to(torch.bfloat16)
+    assert WO.decode_ok(x, wt)
+    y = WO.decode_matmul(x, wt, b)
+    ref = x.float() @ wt.float().t() + b.float()
+    assert _rel(y, ref) < 8e-3
+    y2 = WO.decode_matmul(x, wt)
+    assert _rel(y2, x.float() @ wt.float().t()) < 8e-3
