@@ -15,10 +15,13 @@
 // Interceptors on other ranks are reached through the MessageBus: one TCP listener per carrier, lazily opened
 // connections, fixed 32-byte frames.  The compute callback is user code (Python through the binding); an
 // exception stops the carrier and is re-raised by wait().
-// Runs are epochs: start() bumps the carrier's run id and every frame carries the run it belongs to.  A node
-// meeting a frame of a newer run resets its own counters on its own loop thread before handling it (a faster
-// rank's next run may reach us before our start()), and frames of older runs (the last DATA_IS_USELESS of the
-// previous run, still in flight) are dropped, so no counter is ever touched by two runs or two threads.
+// Runs are epochs: start() bumps the carrier's run id and every frame carries the run it belongs to.  A frame of a
+// newer run that reaches a node before that run's kStart (a faster rank's next run may reach us while this node
+// still finishes the current one, or before our start()) is stashed on the node and replayed, in arrival order,
+// right after the node resets its counters for that run on its own loop thread; frames of older runs (the last
+// DATA_IS_USELESS of the previous run, still in flight) are dropped.  No counter is touched by two runs or two
+// threads, and no step of the current run is lost to an early frame of the next (resetting on that frame dropped
+// the node's last steps of the current run).
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -84,6 +87,7 @@ struct FleetCarrier::Impl {
     int64_t run = 0;                      // run (epoch) the counters belong to; touched by the loop thread only
     int64_t finished_run = 0;             // last run this node completed (guarded by done_mu)
     bool counted = false;                 // sink, or a task with max_run_times > 0: wait() waits for it
+    std::deque<Msg> stash;                // frames of a newer run that arrived before its kStart (loop thread only)
   };
 
   struct Loop {
@@ -243,7 +247,27 @@ struct FleetCarrier::Impl {
   void handle(Node& n, const Msg& m) {
     if (failed.load()) return;
     if (m.run < n.run) return;          // a frame of a finished run
-    if (m.run > n.run) reset(n, m.run);  // the first frame of a newer run (possibly before our start())
+    if (m.run > n.run) {
+      if (m.type != kStart) {           // a newer run's frame before its start reached this node: keep it
+        n.stash.push_back(m);
+        return;
+      }
+      reset(n, m.run);
+      dispatch(n, m);
+      std::deque<Msg> st;
+      st.swap(n.stash);
+      for (const Msg& f : st) {
+        if (f.run == n.run) dispatch(n, f);
+        else if (f.run > n.run) n.stash.push_back(f);
+      }
+      return;
+    }
+    dispatch(n, m);
+  }
+
+  // a frame of the node's current run
+  void dispatch(Node& n, const Msg& m) {
+    if (failed.load()) return;
     switch (m.type) {
       case kStart:
         // roots (sources, and nodes without upstream such as an lr Amplifier) start on their own
