@@ -249,6 +249,8 @@ def main():
             parts.append(f"sharding{args.sharding_stage}({sh})" if args.sharding_stage > 0
                          else f"single(no-sharding,debug)({sh})")
         par = "x".join(parts)
+        if len(parts) == 1 and sh > 1 or (not (mp > 1 or pp > 1 or dp > 1) and args.sharding_stage > 0):
+            par = f"sharding{args.sharding_stage}x{sh}"   # the headline's label (earlier rounds' records)
         names = {"llama2-7b": "Llama-2-7B", "llama2-13b": "Llama-2-13B", "gpt3-13b": "GPT-3 13B",
                  "gpt3-6.7b": "GPT-3 6.7B", "gpt3-1.3b": "GPT-3 1.3B", "tiny": "tiny-llama(debug)",
                  "gpt3-tiny": "tiny-gpt(debug)"}

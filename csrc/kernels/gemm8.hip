@@ -64,8 +64,30 @@ __device__ __forceinline__ void mfma8_dma(f32x4v& c, const i32x8& b, const i32x8
 // landed; this tile's first 13 pieces stay in flight) — and tile t+1's fragments are read from MFMA 14 on (B_7's
 // second set at 14-15, A at 16-31, B_j at >= 8j + 8: 32-41, 48-49, 56-57).  A piece of tile t+1 then has ~62
 // MFMAs (instead of ~48) between its issue and the wait that needs it.
+// SCHED 2 (spread pieces): SCHED 1's waits and fragment reads, but tile t+2's 16 LDS-DMA pieces go one per two MFMAs
+// (A at n = 1, 5, .., 29, B at n = 3, 7, .., 31) instead of one behind each of MFMAs 1..16: a piece's issue costs
+// tens of cycles beside MFMAs (MI355X_MICROARCH 'LDS-DMA piece issue cost'), so 16 back-to-back pieces starve the
+// matrix pipe for part of the burst; the late wait at n = 14 then leaves the 7 pieces issued before it in flight.
+template <int SCHED>
+__device__ constexpr int f8_piece_a(int n) {   // A piece index issued behind MFMA n, or -1
+  if constexpr (SCHED == 2) return (n >= 1 && n <= 29 && (n - 1) % 4 == 0) ? (n - 1) / 4 : -1;
+  else return (n >= 1 && n <= 8) ? n - 1 : -1;
+}
+template <int SCHED>
+__device__ constexpr int f8_piece_b(int n) {
+  if constexpr (SCHED == 2) return (n >= 3 && n <= 31 && (n - 3) % 4 == 0) ? (n - 3) / 4 : -1;
+  else return (n >= 9 && n <= 16) ? n - 9 : -1;
+}
+template <int SCHED>
+__device__ constexpr int f8_pieces_before(int n) {   // pieces issued behind MFMAs 0 .. n-1 of a K-tile
+  int c = 0;
+  for (int i = 0; i < n; ++i) c += (f8_piece_a<SCHED>(i) >= 0) + (f8_piece_b<SCHED>(i) >= 0);
+  return c;
+}
+
 template <int FA, int FB, int EPI, bool TSK = false, int SCHED = 0>
 __global__ __launch_bounds__(NTHR4, 1) void gemm_f8_kernel(Params p) {
+  constexpr bool LATE = SCHED >= 1;   // SCHED 1 / 2: the late-wait K-tile
   __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
   const unsigned sbase = (unsigned)(size_t)(lds_char*)smem_raw;
 
@@ -163,14 +185,15 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_f8_kernel(Params p) {
     sfor<64>([&](auto Q) {
       constexpr int n = decltype(Q)::value;
       constexpr int j = n >> 3, i = n & 7;
-      if constexpr (SCHED == 1) {
+      if constexpr (LATE) {
         if constexpr (n == 0) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
           __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr (n == 14) {
-          asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+          constexpr int inflight = f8_pieces_before<SCHED>(14);
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(inflight) : "memory");
           __builtin_amdgcn_s_barrier();
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -191,36 +214,37 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_f8_kernel(Params p) {
             by[bj < 0 ? 0 : bj] = frag4<true, (bj < 0 ? 0 : bj), 1, nx>(rb);
         }
       }
-      if constexpr (SCHED == 0 && n == 0) {
+      if constexpr (!LATE && n == 0) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
       }
       // ---- tile t+1's fragments (stage nx)
-      if constexpr (SCHED == 0 && n >= 2 && n <= 32 && n % 2 == 0) {
+      if constexpr (!LATE && n >= 2 && n <= 32 && n % 2 == 0) {
         constexpr int r = (n - 2) / 2, u = r >> 1;
         if constexpr (r & 1)
           ay[nx][u] = frag4<true, u, 1, nx>(ra);
         else
           ax[nx][u] = frag4<true, u, 0, nx>(ra);
       }
-      if constexpr (SCHED == 0 && n >= 8 && n <= 57 && (n % 8) < 2) {
+      if constexpr (!LATE && n >= 8 && n <= 57 && (n % 8) < 2) {
         constexpr int jb = n / 8 - 1;
         if constexpr (n % 8 == 0)
           bx[jb] = frag4<true, jb, 0, nx>(rb);
         else
           by[jb] = frag4<true, jb, 1, nx>(rb);
       }
-      if constexpr (SCHED == 0 && n == 36) bx[7 + nx] = frag4<true, 7, 0, nx>(rb);
-      if constexpr (SCHED == 0 && n == 37) by[7 + nx] = frag4<true, 7, 1, nx>(rb);
+      if constexpr (!LATE && n == 36) bx[7 + nx] = frag4<true, 7, 0, nx>(rb);
+      if constexpr (!LATE && n == 37) by[7 + nx] = frag4<true, 7, 1, nx>(rb);
       // ---- MFMA n, with piece n - 1 of tile t+2 behind it for n = 1..16 (A pieces, then B)
       constexpr int jj = j < 7 ? j : 7 + st;
       f32x4v& c = acc[j >> 2][i][j & 3];
       const i32x8 fb = pair(bx[jj], by[jj]), fa = pair(ax[st][i], ay[st][i]);
-      if constexpr (n >= 1 && n <= 8) {
-        mfma8_dma<piece_dst<false, st, (n - 1) & 7>(), FB, FA>(c, fb, fa, wdst, va[(n - 1) & 7], sa);
-      } else if constexpr (n >= 9 && n <= 16) {
-        mfma8_dma<piece_dst<true, st, (n - 9) & 7>(), FB, FA>(c, fb, fa, wdst, vb[(n - 9) & 7], sb);
+      constexpr int pa = f8_piece_a<SCHED>(n), pb = f8_piece_b<SCHED>(n);
+      if constexpr (pa >= 0) {
+        mfma8_dma<piece_dst<false, st, (pa & 7)>(), FB, FA>(c, fb, fa, wdst, va[pa & 7], sa);
+      } else if constexpr (pb >= 0) {
+        mfma8_dma<piece_dst<true, st, (pb & 7)>(), FB, FA>(c, fb, fa, wdst, vb[pb & 7], sb);
       } else {
         mfma8<FB, FA>(c, fb, fa);
       }
@@ -319,16 +343,19 @@ extern "C" int pd_gemm_f8(int fa, int fb, int epi, const void* A, long lda, cons
     p.part = (float*)ws; p.ksplit = ks; p.tail_cap = R;
   }
   const dim3 grid(std::min(nwg - R, cus)), tgrid(R * ks), rgrid(BM * BN / 1024, R);
-  // K-tile schedule: PADDLE2_AMD_FP8_SCHED (0 = one barrier per K-tile, 1 = the late-wait schedule), read per call
+  // K-tile schedule: PADDLE2_AMD_FP8_SCHED (0 = one barrier per K-tile, 1 = the late-wait schedule, 2 = late wait +
+  // spread pieces), read per call
   const char* se = getenv("PADDLE2_AMD_FP8_SCHED");
   const int sched = se ? atoi(se) : 0;
 #define PD_F8(FA_, FB_, E_)                                                                   \
   if (nwg > R) {                                                                              \
     if (sched == 1) gemm_f8_kernel<FA_, FB_, E_, false, 1><<<grid, NTHR4, 0, st>>>(p);       \
+    else if (sched == 2) gemm_f8_kernel<FA_, FB_, E_, false, 2><<<grid, NTHR4, 0, st>>>(p);  \
     else gemm_f8_kernel<FA_, FB_, E_><<<grid, NTHR4, 0, st>>>(p);                             \
   }                                                                                           \
   if (ks) {                                                                                   \
     if (sched == 1) gemm_f8_kernel<FA_, FB_, E_, true, 1><<<tgrid, NTHR4, 0, st>>>(p);       \
+    else if (sched == 2) gemm_f8_kernel<FA_, FB_, E_, true, 2><<<tgrid, NTHR4, 0, st>>>(p);  \
     else gemm_f8_kernel<FA_, FB_, E_, true><<<tgrid, NTHR4, 0, st>>>(p);                      \
     tail_reduce_kernel<E_><<<rgrid, 256, 0, st>>>(p, nwg - R);                               \
   }

@@ -307,9 +307,14 @@ __global__ __launch_bounds__(64 * KW) void dec64_kernel(const unsigned short* __
   const int U = K / 64;
   const int s0 = U * wave / KW, s1 = U * (wave + 1) / KW;   // this wave's 64-wide K steps
   const int ns = s1 - s0;
-  // buffer descriptors (wave-uniform bases; out-of-range rows / steps read 0)
+  // buffer descriptors (wave-uniform bases) with EXACT extents: W from the wave's first K step of row n0 to the end
+  // of row n0 + 15, X to the end of row M - 1.  Prefetches past the wave's range use the offset kSkip, which is
+  // beyond both extents, so the range check returns zeros (an earlier form bounded W at 0x7fffffff and skipped
+  // with 0x7ffffff0 — INSIDE that range — and the tail prefetches read ~2 GiB past the weight: a GPU fault)
+  constexpr int kSkip = (int)0x7fffff00;
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<unsigned short*>(W + (long)n0 * K + (long)s0 * 64), (short)0, 0x7fffffff, 0x00020000);
+      const_cast<unsigned short*>(W + (long)n0 * K + (long)s0 * 64), (short)0, (int)((16L * K - (long)s0 * 64) * 2),
+      0x00020000);
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<unsigned short*>(X + (long)s0 * 64), (short)0, (int)(((long)M * K - (long)s0 * 64) * 2), 0x00020000);
   const int wvo = (r16 * K + 16 * g) * 2;                      // lane's W byte offset at step 0 (row n0 + r16)
@@ -317,14 +322,14 @@ __global__ __launch_bounds__(64 * KW) void dec64_kernel(const unsigned short* __
 #pragma unroll
   for (int t = 0; t < MT; ++t) xvo[t] = ((t * 16 + r16) * K + 16 * g) * 2;
   auto ldw = [&](int s, uint4 (&o)[2]) {
-    const int v = s < ns ? wvo + s * 128 : 0x7ffffff0;   // past the wave's range: an offset the descriptor drops
+    const int v = s < ns ? wvo + s * 128 : kSkip;   // past the wave's range: an offset beyond the extent
     o[0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, v, 0, 0));
     o[1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, v + 16, 0, 0));
   };
   auto ldx = [&](int s, uint4 (&o)[MT][2]) {
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
-      const int v = s < ns ? xvo[t] + s * 128 : 0x7ffffff0;
+      const int v = s < ns ? xvo[t] + s * 128 : kSkip;
       o[t][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, v, 0, 0));
       o[t][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, v + 16, 0, 0));
     }
@@ -482,7 +487,8 @@ extern "C" int pd_dec64_gemm(const void* X, const void* W, const void* bias, voi
                              void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (M < 1 || M > 64 || N % 16 || K % 64 || (kw != 4 && kw != 8) || (size_t)X % 16 || (size_t)W % 16) return -1;
-  if ((long)N * K * 2 >= 0x7fffffffL || (long)M * K * 2 >= 0x7fffffffL) return -1;
+  // byte offsets (incl. the skip offset kSkip = 0x7fffff00 and its +16) stay below 2^31 and beyond every extent
+  if ((long)N * K * 2 >= 0x7fffff00L || (long)M * K * 2 >= 0x7fffff00L) return -1;
   const dim3 grid(N / 16);
 #define PD_D64(MT_, KW_) \
   dec64_kernel<MT_, KW_, 8><<<grid, 64 * KW_, 0, st>>>((const unsigned short*)X, (const unsigned short*)W, \

@@ -1,8 +1,8 @@
 """``python -m paddle2_amd.distributed.launch`` — collective job launcher.
 
 Reference: python/paddle/distributed/launch/ (main.py, context/args_envs.py, controllers/
-collective.py:91-200 ``_build_pod_with_args`` / ``_build_pod_with_master``, controllers/watcher,
-job/container.py log files ``workerlog.N``), and the legacy fleet/launch.py.
+collective.py:91-200 ``_build_pod_with_args`` / ``_build_pod_with_master``, controllers/watcher.py,
+controllers/master.py HTTPMaster, job/container.py log files ``workerlog.N``), and the legacy fleet/launch.py.
 
 One process per GPU.  Multi-node jobs rendezvous through the native C++ TCPStore
 (csrc/runtime/tcp_store.cpp) hosted by node 0 at ``--master``: every node registers its address
@@ -10,7 +10,10 @@ and process count, node ranks / global rank offsets are derived from the registr
 (or ``--rank``), and each worker gets both Paddle's env contract (PADDLE_TRAINER_ID,
 PADDLE_TRAINERS_NUM, PADDLE_CURRENT_ENDPOINT, PADDLE_TRAINER_ENDPOINTS, PADDLE_MASTER,
 FLAGS_selected_gpus, ...) and torch.distributed's (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
-The watcher restarts the whole pod up to ``--max_restart`` times when a worker fails (fault
+``--master http://host:port`` rendezvouses through the HTTP key-value master instead (launch/master.py, the
+reference's default master).  The GPU watcher (launch/watcher.py, ``--enable_gpu_log``) samples every
+device's utilisation and memory from the amdgpu sysfs into ``<log_dir>/<job_id>.gpu.log``.
+The launcher restarts the whole pod up to ``--max_restart`` times when a worker fails (fault
 tolerance level 1) and otherwise tears the pod down and exits with the failing worker's code.
 
 Elastic mode (``--nnodes MIN:MAX``, reference fleet/elastic): membership is tracked by the
@@ -49,6 +52,9 @@ def _parse(argv=None):
                     help="run the hybrid-parallel auto tuner with this config instead of a single job")
     ap.add_argument("--host", default=None, help="this node's address")
     ap.add_argument("--start_port", type=int, default=None)
+    ap.add_argument("--enable_gpu_log", "--enable-gpu-log", dest="enable_gpu_log", default="True",
+                    help="GPU utilisation / memory log <log_dir>/<job_id>.gpu.log (True / False)")
+    ap.add_argument("--gpu_log_interval", type=float, default=5.0, help="seconds between GPU log samples")
     ap.add_argument("training_script")
     ap.add_argument("training_script_args", nargs=argparse.REMAINDER)
     return ap.parse_args(argv)
@@ -93,6 +99,8 @@ class _Rendezvous:
             ports = [self.args.start_port + i if self.args.start_port else _free_port() for i in range(self.nproc)]
             eps = [f"{self.host}:{p}" for p in ports]
             return 0, 1, self.nproc, 0, eps, None
+        if self.args.master.startswith("http://"):
+            return self._run_http(nnodes)
         from ..store import TCPStore
 
         mhost, mport = self.args.master.rsplit(":", 1)
@@ -110,6 +118,28 @@ class _Rendezvous:
         world = sum(int(i[1]) for i in infos)
         eps = [f"{h}:{p}" for h, _, ps in infos for p in ps.split(",")]
         return node_rank, nnodes, world, offset, eps, store
+
+
+    def _run_http(self, nnodes):
+        """Rendezvous through the HTTP KV master (reference controllers/master.py HTTPMaster.sync_peers)."""
+        from .master import HTTPMaster
+
+        ep = self.args.master[len("http://"):]
+        mhost = ep.rsplit(":", 1)[0]
+        if self.args.rank >= 0:
+            is_main = self.args.rank == 0
+        else:
+            is_main = None if mhost in ("127.0.0.1", "localhost", self.host) else False
+        master = HTTPMaster(ep, is_main=is_main)
+        ports = [_free_port() for _ in range(self.nproc)]
+        val = f"{self.host}|{self.nproc}|{','.join(map(str, ports))}"
+        vals, node_rank = master.sync_peers(f"{self.args.job_id}/nodes", f"{self.host}:{os.getpid()}", val, nnodes,
+                                            self.args.rank)
+        infos = [v.split("|") for v in vals]
+        offset = sum(int(i[1]) for i in infos[:node_rank])
+        world = sum(int(i[1]) for i in infos)
+        eps = [f"{h}:{p}" for h, _, ps in infos for p in ps.split(",")]
+        return node_rank, nnodes, world, offset, eps, master
 
 
 def _try_bind(host, port):
@@ -281,11 +311,27 @@ def launch(argv=None):
         return _launch_elastic(args, nproc, devices, host)
     node_rank, nnodes, world, offset, eps, store = _Rendezvous(args, nproc, host).run()
     if args.master and nnodes > 1:
-        mhost = args.master.rsplit(":", 1)[0]
-        torch_port = int(args.master.rsplit(":", 1)[1]) + 1
+        mep = args.master[len("http://"):] if args.master.startswith("http://") else args.master
+        mhost = mep.rsplit(":", 1)[0]
+        torch_port = int(mep.rsplit(":", 1)[1]) + 1
         torch_master = (mhost, torch_port)
     else:
         torch_master = ("127.0.0.1", _free_port())
+    watcher = None
+    if str(args.enable_gpu_log).lower() in ("1", "true", "yes"):
+        from .watcher import Watcher
+
+        watcher = Watcher(args.log_dir, args.job_id, devices, args.gpu_log_interval)
+    try:
+        return _run_pods(args, nproc, devices, node_rank, nnodes, world, offset, eps, torch_master)
+    finally:
+        if watcher is not None:
+            watcher.stop()
+        if hasattr(store, "stop"):
+            store.stop()
+
+
+def _run_pods(args, nproc, devices, node_rank, nnodes, world, offset, eps, torch_master):
     cmd = [sys.executable, "-u", args.training_script] + list(args.training_script_args)
     restarts = 0
     while True:
