@@ -209,8 +209,13 @@ def main():
         opt.clear_grad()
         return loss
 
+    dbg = os.environ.get("PADDLE2_AMD_BENCH_DEBUG", "0") == "1"   # per-warmup-step sync + memory line (stderr)
     for i in range(args.warmup):
         loss = step(i)
+        if dbg and torch.cuda.is_available():
+            torch.cuda.synchronize()
+            print(f"[bench] warmup step {i} ok: allocated {torch.cuda.memory_allocated() / 2**30:.1f} GiB, "
+                  f"peak {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB", file=sys.stderr, flush=True)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     from paddle2_amd.distributed import collective as C

@@ -262,8 +262,9 @@ class GPTForCausalLM(nn.Layer):
             g = _mp_info(None)[0]
             w = self.gpt.word_embeddings.weight._t.t() if self.lm_head is None else self.lm_head._t
             return _wrap(_ColumnLinear.apply(h._t, w, None, g))
-        w = self.gpt.word_embeddings.weight._t.t() if self.lm_head is None else self.lm_head._t
-        return _wrap(torch.matmul(h._t, w))
+        if self.lm_head is None:   # tied: h @ E^T on the TN GEMM with E as stored
+            return _wrap(T.tied_logits(h._t, self.gpt.word_embeddings.weight._t))
+        return _wrap(T.linear(h._t, self.lm_head._t))
 
     def forward(self, input_ids, labels=None, position_ids=None):
         logits = self._logits(self.gpt(input_ids, position_ids))

@@ -128,9 +128,10 @@ def _ws(t):
     return G._workspace(t) if G.SPLITK else (0, 0)
 
 
-def mm_native(a, bT, inv_a, inv_b, out_dtype, bias=None):
+def mm_native(a, bT, inv_a, inv_b, out_dtype, bias=None, out=None, beta=0.0):
     """C[M, N] = (a[M, K] . bT[N, K]^T) * inv_a * inv_b (+ bias) on the native fp8 GEMM (both operands K-major
-    fp8, dequant factors as device scalars).  None when the problem is outside the kernel's domain."""
+    fp8, dequant factors as device scalars).  ``out``: write into this [M, N] tensor (fp32 output: C = product +
+    beta * C, e.g. a sharding unit's fp32 main-grad slot).  None when the problem is outside the kernel's domain."""
     fa, fb = _FMT.get(a.dtype), _FMT.get(bT.dtype)
     if (fa, fb, out_dtype) not in _NATIVE_CASES or a.stride(1) != 1 or bT.stride(1) != 1:
         return None
@@ -138,10 +139,12 @@ def mm_native(a, bT, inv_a, inv_b, out_dtype, bias=None):
         return None
     M, K = a.shape
     Nn = bT.shape[0]
-    c = torch.empty(M, Nn, dtype=out_dtype, device=a.device)
+    if out is not None and (out.dtype != out_dtype or tuple(out.shape) != (M, Nn) or out.stride(1) != 1):
+        return None
+    c = torch.empty(M, Nn, dtype=out_dtype, device=a.device) if out is None else out
     rc = N.native().gemm_f8(fa, fb, 0 if out_dtype == torch.bfloat16 else 1, a.data_ptr(), a.stride(0),
                             bT.data_ptr(), bT.stride(0), c.data_ptr(), c.stride(0), N.ptr(bias),
-                            inv_a.data_ptr(), inv_b.data_ptr(), M, Nn, K, 0.0, 4, _cus(a.device), *_ws(a),
+                            inv_a.data_ptr(), inv_b.data_ptr(), M, Nn, K, float(beta), 4, _cus(a.device), *_ws(a),
                             N.stream())
     if rc == -1:
         return None
@@ -187,6 +190,27 @@ def _mm(a, b_colmajor, inv_a, inv_b, out_dtype, bias=None):
     return y.to(out_dtype)
 
 
+# The weight gradient of an fp8 linear whose weight has an fp32 main-grad slot (a sharding unit's ``_p2_gt``, as the
+# bf16 linear): the native fp8 GEMM writes the fp32 product straight into the slot (C = dW + beta * C) instead of a
+# bf16 dW that autograd hands to the unit's hook for a bf16 -> fp32 conversion pass.  "0" keeps the bf16 dW.
+WGRAD_MAIN = os.environ.get("PADDLE2_AMD_FP8_WGRAD_MAIN", "0") != "0"
+
+
+def _wgrad_into_main(gt, xqT, gqT, inv_x, inv_g):
+    """dW^T layout note: W is [K, N]; dW = x^T dY = (xqT [K, M]) . (gqT [N, M])^T -> [K, N] written into the
+    unit's fp32 slot.  True when done (the slot is then marked written)."""
+    owner, idx = gt
+    view, beta = owner.grad_target(idx)
+    if view.dtype != torch.float32 or not view.is_contiguous() or not N.use_native(xqT):
+        return False
+    ia = inv_x.float().reshape(1).contiguous()
+    ib = inv_g.float().reshape(1).contiguous()
+    if mm_native(xqT, gqT, ia, ib, torch.float32, out=view, beta=float(beta)) is None:
+        return False
+    owner.param_grad_done(idx)
+    return True
+
+
 class _FP8LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bias, mx, mw, mg):
@@ -203,6 +227,7 @@ class _FP8LinearFn(torch.autograd.Function):
         mx.update()
         mw.update()
         ctx.meta = (mg, x.shape, bias is not None, out_dtype, w.dtype)
+        ctx.gt = getattr(w, "_p2_gt", None) if WGRAD_MAIN and w.is_cuda else None
         return y.reshape(*x.shape[:-1], N_)
 
     @staticmethod
@@ -213,7 +238,11 @@ class _FP8LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, N_)
         gq, gqT = cast(dy2, mg, transpose=True)                  # dY [M, N] and dY^T [N, M]
         dx = _mm(gq, wq.t(), mg.inv_scale, inv_w, out_dtype)     # [M, N] @ [N, K]
-        dw = _mm(xqT, gqT.t(), inv_x, mg.inv_scale, wdt if wdt in (torch.bfloat16, torch.float16) else torch.float32)
+        if ctx.gt is not None and ctx.needs_input_grad[1] and _wgrad_into_main(ctx.gt, xqT, gqT, inv_x, mg.inv_scale):
+            dw = None
+        else:
+            dw = _mm(xqT, gqT.t(), inv_x, mg.inv_scale,
+                     wdt if wdt in (torch.bfloat16, torch.float16) else torch.float32).to(wdt)
         db = None
         if has_b:
             # the native two-pass column sum (torch_ops.bias_grad): ATen's bf16 dim-0 reduce took 24.5 ms / 160
@@ -223,7 +252,7 @@ class _FP8LinearFn(torch.autograd.Function):
             db = (bias_grad(dy2.contiguous(), out_dtype=wdt) if dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16)
                   else dy2.sum(0, dtype=torch.float32).to(wdt))
         mg.update()
-        return dx.reshape(xshape), dw.to(wdt), db, None, None, None
+        return dx.reshape(xshape), dw, db, None, None, None
 
 
 @_graph_op

@@ -571,6 +571,46 @@ def linear(x, w, b=None):
     return y + b if b is not None else y
 
 
+class _TiedLogitsFn(torch.autograd.Function):
+    """logits = h @ E^T for a tied word embedding E [V, H] (GPT's output layer) on the native GEMM: E as stored is
+    the K-major B operand of the TN kernel (no transpose pass); backward dh = dlogits @ E (the forward form) and
+    dE = dlogits^T @ h (the weight-gradient form, bf16, accumulated by autograd with the embedding's own grad).
+    Reference: the tied-embedding matmul of test/auto_parallel/get_gpt_model.py (paddle.matmul(x, w,
+    transpose_y=True))."""
+
+    @staticmethod
+    def forward(ctx, h2, E):
+        from . import gemm as G
+
+        ctx.save_for_backward(h2, E)
+        return G.mm_dgrad(h2, E)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import gemm as G
+
+        h2, E = ctx.saved_tensors
+        dy2 = dy.contiguous()
+        dh = G.mm_fwd(dy2, E) if ctx.needs_input_grad[0] else None
+        dE = G.mm_wgrad_bf16(dy2, h2) if ctx.needs_input_grad[1] else None
+        return dh, dE
+
+
+def tied_logits(h, E):
+    """h [..., H] @ E[V, H]^T: the native TN GEMM for bf16 GPU tensors of native-friendly shapes, torch.matmul
+    otherwise."""
+    from . import gemm as G
+
+    h2 = h.reshape(-1, h.shape[-1])
+    if (h.device.type == "cuda" and G.enabled(h2) and E.dtype == h2.dtype and E.dim() == 2
+            and E.shape[1] == h2.shape[1] and E.shape[0] % 8 == 0 and G.supported_dgrad(h2, E)
+            and _pass_native("dgrad", h2, E)):
+        if not h2.is_contiguous():
+            h2 = h2.contiguous()
+        return _TiedLogitsFn.apply(h2, E).view(*h.shape[:-1], E.shape[0])
+    return torch.matmul(h, E.t())
+
+
 class _GeluMLPFn(torch.autograd.Function):
     """y = gelu(x @ W1 + b1) @ W2 + b2 (the GPT MLP) as one autograd node, so the GELU rides on the GEMM epilogues in
     both directions (reference funcs/fused_gemm_epilogue.h:382 GELU_AUX_BIAS forward, :580 gelu_grad backward;

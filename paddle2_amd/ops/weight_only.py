@@ -77,14 +77,14 @@ def decode_ok(x, wt):
     M, K = x.shape
     Nn = wt.shape[0]
     ok = (x.device.type == "cuda" and x.dtype == torch.bfloat16 and wt.dtype == torch.bfloat16 and 1 <= M <= 64
-          and K % 64 == 0 and wt.shape[1] == K and Nn % 64 == 0 and wt.is_contiguous() and N.use_native(x))
+          and K % 64 == 0 and wt.shape[1] == K and wt.is_contiguous() and N.use_native(x))
     if not ok:
         return False
     if DECODE_GEMM == "blas":
         return False
     if M > 16:
         return Nn % 16 == 0   # the whole-K MFMA stream kernel (dec64_kernel): the b17-64 serving step
-    return DECODE_GEMM == "native" or Nn <= 8192
+    return Nn % 64 == 0 and (DECODE_GEMM == "native" or Nn <= 8192)   # the split-K kernel: 64-row blocks
 
 
 def decode_matmul(x, wt, bias=None):

@@ -8,7 +8,7 @@ export TMPDIR=/tmp PYTHONPATH=$PWD
 timeout -k 10 120 ./scripts/mfma_shape > $O/mfma_shape.jsonl 2> $O/mfma_shape.err
 r=$?; cat $O/mfma_shape.jsonl; [ $r -ne 0 ] && { tail -20 $O/mfma_shape.err; exit $r; }
 PADDLE2_AMD_FP8_SCHED=2 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu \
-  tests/test_fp8_gemm_gpu.py > $O/tests_s2.log 2>&1
+  tests/test_fp8_gemm_gpu.py tests/test_fp8_gpu.py tests/test_decode_gemm_gpu.py > $O/tests_s2.log 2>&1
 r=$?; tail -2 $O/tests_s2.log; [ $r -ne 0 ] && { grep -E "^E |FAIL" $O/tests_s2.log | head -30; exit $r; }
 for sc in 0 1 2; do
   PADDLE2_AMD_FP8_SCHED=$sc timeout -k 10 300 python -u scripts/bench_gemm_fp8.py > $O/fp8_s$sc.jsonl 2> $O/fp8_s$sc.err
@@ -23,12 +23,6 @@ done
 timeout -s KILL 90 rocprofv3 --pmc $CTR -d $O/pmc_native1 -o run --output-format csv -- python3 scripts/prof_fp8.py native 8192 8192 8192 1 \
   > $O/pmc_native1.log 2>&1
 r=$?; echo "pmc native sched1 rc=$r"; [ $r -ne 0 ] && { tail -20 $O/pmc_native1.log; exit $r; }
-timeout -k 10 400 python -u bench.py --model gpt3-13b --fp8 --seq-len 2048 --micro-batch 2 --steps 10 --warmup 3 > $O/fp8_bench.log 2>&1
-r=$?; tail -1 $O/fp8_bench.log; [ $r -ne 0 ] && { tail -30 $O/fp8_bench.log; exit $r; }
-timeout -k 10 420 rocprofv3 --kernel-trace --stats -d $O/prof_fp8 -o run --output-format csv -- python3 bench.py --model gpt3-13b --fp8 --seq-len 2048 --micro-batch 2 --steps 3 --warmup 2 > $O/prof_fp8.log 2>&1
-r=$?; echo "prof rc=$r"; [ $r -ne 0 ] && { tail -20 $O/prof_fp8.log; exit $r; }
-python3 scripts/kernel_table.py $(find $O/prof_fp8 -name "*kernel_trace.csv" | head -1) > $O/kernels_fp8.txt 2>&1; head -45 $O/kernels_fp8.txt
-rm -f $(find $O/prof_fp8 -name "*kernel_trace.csv") 2>/dev/null
 timeout -k 10 300 python -u scripts/exp_decode64.py > $O/dec64.jsonl 2> $O/dec64.err
 r=$?; cat $O/dec64.jsonl; [ $r -ne 0 ] && { tail -20 $O/dec64.err; exit $r; }
 timeout -k 10 300 python -u scripts/bench_serving.py --batch 64 > $O/serving_b64.log 2>&1

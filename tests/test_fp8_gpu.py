@@ -76,3 +76,53 @@ def test_gpt_fp8_trains_on_gpu():
         o.clear_grad()
         losses.append(float(loss))
     assert losses[-1] < losses[0], losses
+
+
+class _Slot:
+    """A stand-in sharding unit: one fp32 main-grad slot per weight (grad_target / param_grad_done)."""
+
+    def __init__(self, shape):
+        self.buf = torch.full(shape, 0.25, device=DEV, dtype=torch.float32)
+        self.done = 0
+
+    def grad_target(self, i):
+        return self.buf, 1   # accumulate onto the existing value (beta 1)
+
+    def param_grad_done(self, i):
+        self.done += 1
+
+
+def test_fp8_wgrad_into_fp32_main_grad_slot(monkeypatch):
+    """PADDLE2_AMD_FP8_WGRAD_MAIN: the native fp8 weight-gradient GEMM writes fp32 straight into the unit's slot
+    (C = dW + 1 * C) — equal, up to the bf16 rounding the other path applies, to the bf16 dW + conversion."""
+    from paddle2_amd.ops import fp8
+
+    torch.manual_seed(0)
+    K, Nn, M = 512, 768, 1024
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(K, Nn, device=DEV) * 0.05).bfloat16()
+    g = torch.randn(M, Nn, device=DEV, dtype=torch.bfloat16)
+    metas = [fp8.FP8TensorMeta(f, device=torch.device(DEV)) for f in (fp8.E4M3, fp8.E4M3, fp8.E5M2)]
+
+    def run(main):
+        monkeypatch.setattr(fp8, "WGRAD_MAIN", main)
+        for m in metas:   # same scales for both runs
+            m.initialized = False
+            m.history.zero_()
+            m.amax.zero_()
+        wl = w.clone().requires_grad_()
+        slot = _Slot((K, Nn))
+        if main:
+            wl._p2_gt = (slot, 0)
+        y = fp8.fp8_linear(x, wl, None, *metas)
+        y.backward(g)
+        return wl.grad, slot
+
+    gw_bf16, _ = run(False)
+    gw_none, slot = run(True)
+    assert gw_none is None and slot.done == 1
+    ref = gw_bf16.float() + 0.25
+    rel = float((slot.buf - ref).norm() / ref.norm())
+    assert rel < 1e-2, rel
+    exact = (x.float().t() @ g.float()) + 0.25
+    assert float((slot.buf - exact).norm() / exact.norm()) < 0.08

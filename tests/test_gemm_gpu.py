@@ -342,3 +342,27 @@ def test_v7_tail_splitk_matches_fp32(M, N, K, bias, monkeypatch):
     monkeypatch.setattr(G, "V7_TAILK", False)
     y0 = G.mm_fwd(x, w, b)
     assert _rel(y, y0) < 8e-3
+
+
+@pytest.mark.parametrize("M,V,H", [(1024, 2048, 512), (777, 4096, 256)])
+def test_tied_logits_native_matches_fp32(M, V, H):
+    """GPT's tied output layer h @ E^T on the native TN GEMM (E as stored): forward and both gradients vs fp32."""
+    from paddle2_amd.ops import torch_ops as T
+
+    torch.manual_seed(0)
+    h = (torch.randn(M, H, device="cuda") * 0.5).bfloat16().requires_grad_()
+    E = (torch.randn(V, H, device="cuda") * 0.5).bfloat16().requires_grad_()
+    y = T.tied_logits(h, E)
+    fn, names = y.grad_fn, []
+    while fn is not None:
+        names.append(type(fn).__name__)
+        fn = fn.next_functions[0][0] if fn.next_functions else None
+    assert any(n.startswith("_TiedLogitsFn") for n in names), names
+    g = torch.randn(M, V, device="cuda").bfloat16()
+    y.backward(g)
+    hf, Ef = h.detach().float().requires_grad_(), E.detach().float().requires_grad_()
+    yf = hf @ Ef.t()
+    yf.backward(g.float())
+    assert _rel(y, yf) < 1e-2
+    assert _rel(h.grad, hf.grad) < 1e-2
+    assert _rel(E.grad, Ef.grad) < 1e-2
