@@ -214,8 +214,21 @@ def main():
         loss = step(i)
         if dbg and torch.cuda.is_available():
             torch.cuda.synchronize()
+            extra = ""
+            try:
+                from paddle2_amd.device import allocator as _al
+
+                if _al.is_active():
+                    st = _al.stats(torch.cuda.current_device())
+                    fr, tot = torch.cuda.mem_get_info()
+                    extra = (f", device free {fr / 2**30:.1f} of {tot / 2**30:.1f} GiB"
+                             f", reserved {st['reserved'] / 2**30:.1f} GiB, chunks {st['num_chunks']}, "
+                             f"oom_retries {st['num_oom_retries']}, cross_stream {st['cross_stream_reuse']}, "
+                             f"record_stream {st['record_stream']}, deferred {st['deferred_frees']}")
+            except Exception as e:  # noqa: BLE001 - diagnostics only
+                extra = f", allocator stats unavailable: {e}"
             print(f"[bench] warmup step {i} ok: allocated {torch.cuda.memory_allocated() / 2**30:.1f} GiB, "
-                  f"peak {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB", file=sys.stderr, flush=True)
+                  f"peak {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB{extra}", file=sys.stderr, flush=True)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     from paddle2_amd.distributed import collective as C

@@ -20,7 +20,11 @@
 //     freeing stream and parks the block on a deferred list; it re-enters the free index only once all of its
 //     events completed (polled, never waited for, at the next allocation);
 //   * limit: an optional byte cap (FLAGS_fraction_of_gpu_memory_to_use / FLAGS_gpu_memory_limit_mb); on a
-//     failed growth the cache of fully-free chunks is released and the growth retried once.
+//     failed growth the cache of fully-free chunks is released and the growth retried once;
+//   * headroom (opt-in, FLAGS_native_allocator_headroom_mb): a growth never leaves less than `g_headroom` bytes of
+//     the device free (hipMemGetInfo at every growth), for the runtime's own later allocations;
+//   * out of memory: one device sync settles every fence, the free index is coalesced and scanned in full, then
+//     fully-free chunks go back to the driver for a last growth (see do_alloc_impl).
 // Thread-safe (one mutex per device).  C ABI for ctypes; no Python dependency, loads on CPU-only machines.
 #include <hip/hip_runtime.h>
 
@@ -112,6 +116,7 @@ struct Violation {
 };
 static std::vector<Violation>& g_violations = *new std::vector<Violation>();
 static uint64_t g_limit_bytes = 0;   // 0 = unlimited
+static uint64_t g_headroom = 0;   // device bytes a growth leaves free for the runtime (0 = off)
 static std::mutex& g_cfg_mu = *new std::mutex();
 
 static inline size_t round_up(size_t n, size_t a) { return (n + a - 1) / a * a; }
@@ -199,6 +204,20 @@ static bool grow(Device& d, int dev, size_t size, hipStream_t stream) {
   int prev_dev = -1;
   hipGetDevice(&prev_dev);
   if (prev_dev != dev) hipSetDevice(dev);
+  if (g_headroom) {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && total_b > 0) {
+      const size_t exact = round_up(size, kAlign);
+      if ((uint64_t)free_b < (uint64_t)bytes + kTailGuard + g_headroom) {
+        // a full chunk would eat into the runtime's headroom: take only what is asked, if even that fits
+        if ((uint64_t)free_b < (uint64_t)exact + kTailGuard + g_headroom) {
+          if (prev_dev != dev) hipSetDevice(prev_dev);
+          return false;
+        }
+        bytes = exact;
+      }
+    }
+  }
   void* p = nullptr;
   // every chunk carries kTailGuard mapped-but-never-handed-out bytes: a kernel whose vector / tile loads run
   // a little past the end of the last tensor of a chunk reads guard memory instead of faulting on unmapped VA
@@ -348,12 +367,41 @@ static void* do_alloc_impl(size_t size, int dev, hipStream_t stream) {
     b = find_fit(d, need, stream);
   }
   if (!b) {
-    if (!grow(d, dev, need, stream)) {
+    if (grow(d, dev, need, stream)) {
+      b = find_fit(d, need, stream);
+    } else {
+      // out of device memory: first settle — one device sync retires every pending fence (deferred record_stream
+      // frees re-enter the index, cross-stream blocks become usable), settled neighbours coalesce, and the whole
+      // free index is scanned (not just the first kMaxScan candidates); only then are fully-free chunks returned
+      // to the driver for one more growth.  If nothing fits the allocation fails (torch.OutOfMemoryError through
+      // the torch hook — a null pointer handed to torch became a GPU memory-access fault).
       d.st.num_oom_retries++;
-      release_free_chunks(d, dev);
-      if (!grow(d, dev, need, stream)) return nullptr;
+      int prev = -1;
+      hipGetDevice(&prev);
+      if (prev != dev) hipSetDevice(dev);
+      hipDeviceSynchronize();
+      if (prev != dev) hipSetDevice(prev);
+      process_deferred(d);
+      for (auto& kv : d.free_index) fence_done(d, kv.second);
+      coalesce_settled(d);
+      for (auto it = d.free_index.lower_bound(need); it != d.free_index.end(); ++it) {
+        if (usable_on(d, it->second, stream)) {
+          b = it->second;
+          break;
+        }
+      }
+      if (!b) {
+        // last resort: return the fully-free chunks to the driver and grow once more (the pool is fragmented:
+        // free bytes exist but no block holds `need`)
+        release_free_chunks(d, dev);
+        if (grow(d, dev, need, stream)) b = find_fit(d, need, stream);
+      }
+      if (!b) {
+        std::fprintf(stderr, "[pd_alloc] out of memory: %zu bytes on device %d (allocated %llu, reserved %llu)\n",
+                     need, dev, (unsigned long long)d.st.allocated, (unsigned long long)d.st.reserved);
+        return nullptr;   // the torch hook turns this into torch.OutOfMemoryError
+      }
     }
-    b = find_fit(d, need, stream);
     if (!b) return nullptr;
   }
   b = carve(d, b, need, stream);
@@ -542,6 +590,12 @@ void pd_alloc_configure(uint64_t chunk_bytes, uint64_t limit_bytes) {
   std::lock_guard<std::mutex> lk(g_cfg_mu);
   if (chunk_bytes) g_chunk_bytes = round_up(chunk_bytes, size_t(2) << 20);
   g_limit_bytes = limit_bytes;
+}
+
+// bytes of device memory every growth leaves free for the HIP runtime / RCCL / driver (0 disables the check)
+void pd_alloc_set_headroom(uint64_t bytes) {
+  std::lock_guard<std::mutex> lk(g_cfg_mu);
+  g_headroom = bytes;
 }
 
 // out[0..12] = allocated, reserved, peak_allocated, peak_reserved, num_allocs, num_frees, num_chunks,

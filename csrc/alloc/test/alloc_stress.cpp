@@ -18,6 +18,7 @@ void* pd_alloc_malloc(size_t size, int device, hipStream_t stream);
 void pd_alloc_free(void* ptr, size_t size, int device, hipStream_t stream);
 void pd_alloc_record_stream(void* ptr, hipStream_t stream);
 void pd_alloc_configure(uint64_t chunk_bytes, uint64_t limit_bytes);
+void pd_alloc_set_headroom(uint64_t bytes);
 void pd_alloc_stats(int device, uint64_t* out);
 uint64_t pd_alloc_empty_cache(int device);
 }
@@ -91,6 +92,22 @@ int main(int argc, char** argv) {
   int threads = argc > 1 ? std::atoi(argv[1]) : 4;
   int iters = argc > 2 ? std::atoi(argv[2]) : 20000;
   pd_alloc_configure(uint64_t(8) << 20, 0);
+  // headroom: the fake device holds 4 GiB; with 3 GiB kept free a 512 MiB request fits, a second 768 MiB one
+  // (which would leave < 3 GiB) must be refused instead of eating the runtime's share
+  {
+    pd_alloc_set_headroom(uint64_t(3) << 30);
+    hipStream_t s0 = reinterpret_cast<hipStream_t>(uintptr_t(0x999));
+    void* a = pd_alloc_malloc(size_t(512) << 20, 0, s0);
+    void* b = a ? pd_alloc_malloc(size_t(768) << 20, 0, s0) : nullptr;
+    if (!a || b) {
+      std::fprintf(stderr, "headroom: a=%p b=%p (want a != null, b == null)\n", a, b);
+      g_errors++;
+    }
+    if (a) pd_alloc_free(a, size_t(512) << 20, 0, s0);
+    if (b) pd_alloc_free(b, size_t(768) << 20, 0, s0);
+    pd_alloc_empty_cache(0);
+    pd_alloc_set_headroom(uint64_t(64) << 20);
+  }
   std::vector<std::thread> ts;
   for (int t = 0; t < threads; ++t) ts.emplace_back(worker, t, iters);
   for (auto& t : ts) t.join();

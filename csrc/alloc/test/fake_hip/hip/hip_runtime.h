@@ -35,6 +35,11 @@ inline hipError_t hipMalloc(void** p, size_t n) {
   return hipSuccess;
 }
 inline hipError_t hipFree(void* p) { std::free(p); return hipSuccess; }  // byte accounting is approximate
+inline hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
+  *total_b = fakehip::cap();
+  *free_b = fakehip::cap() > fakehip::in_use() ? fakehip::cap() - fakehip::in_use() : 0;
+  return hipSuccess;
+}
 inline hipError_t hipGetDevice(int* d) { *d = fakehip::cur_dev; return hipSuccess; }
 inline hipError_t hipSetDevice(int d) { fakehip::cur_dev = d; return hipSuccess; }
 inline hipError_t hipGetLastError() { return hipSuccess; }

@@ -30,6 +30,7 @@ extern "C" {
 void* pd_alloc_malloc(size_t size, int device, hipStream_t stream);
 void pd_alloc_free(void* ptr, size_t size, int device, hipStream_t stream);
 void pd_alloc_record_stream(void* ptr, hipStream_t stream);
+void pd_alloc_fragmentation(int device, uint64_t* out);
 void pd_alloc_stats(int device, uint64_t* out);
 void pd_alloc_reset_peak(int device);
 }
@@ -152,9 +153,11 @@ struct PdTorchAllocator : P::CUDAPluggableAllocator {
     if (prev != device) hipSetDevice(device);
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
     if (prev != device) hipSetDevice(prev);
-    // a workspace can come from the pool's free bytes or from new device memory
-    const size_t pool_free = st[1] > st[0] ? (size_t)(st[1] - st[0]) : 0;
-    *largestBlock = std::max(pool_free, free_b);
+    // a workspace can come from the largest free block of the pool or from new device memory (the pool's free
+    // BYTES are scattered over many blocks: quoting them promised workspaces no single block could hold)
+    uint64_t frag[2] = {0, 0};
+    pd_alloc_fragmentation(device, frag);
+    *largestBlock = std::max((size_t)frag[0], free_b);
   }
 
   c10::CachingDeviceAllocator::DeviceStats getDeviceStats(c10::DeviceIndex device) override {
@@ -189,7 +192,16 @@ extern "C" {
 // 0 on success, 1 if the created allocator is not a CUDAPluggableAllocator (no hooks possible)
 int pd_alloc_install_torch() {
   auto pa = std::make_shared<PdTorchAllocator>(
-      [](size_t size, int device, hipStream_t stream) { return router().malloc(size, device, stream); },
+      [](size_t size, int device, hipStream_t stream) {
+        void* p = router().malloc(size, device, stream);
+        // torch's pluggable allocator wraps whatever pointer comes back: a null one for a non-empty tensor made
+        // the next kernel write to address 0 (an out-of-memory turned into a GPU memory-access fault).  Raise
+        // torch's OutOfMemoryError instead, as its caching allocator does.
+        TORCH_CHECK_WITH(OutOfMemoryError, p != nullptr || size == 0,
+                         "native allocator: out of memory allocating ", size, " bytes on device ", device,
+                         " (FLAGS_use_native_allocator=0 selects torch's caching allocator)");
+        return p;
+      },
       [](void* ptr, size_t size, int device, hipStream_t stream) { router().free(ptr, size, device, stream); });
   std::shared_ptr<c10::hip::HIPCachingAllocator::HIPAllocator> a = pa;
   pa->set_record_stream_fn([](void* ptr, hipStream_t stream) {

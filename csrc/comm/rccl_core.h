@@ -107,10 +107,16 @@ struct Comm {
   }
 };
 
+// Events are never destroyed (or handed out again) while a stream may still signal them: a finished task's end
+// event and a fence event go to `pending_` and return to the free list only once hipEventQuery reports them
+// complete (swept on every get()).  Destroying a still-pending end event — the Task of an async collective is
+// dropped as soon as the caller's stream has been told to wait for it, long before the GPU passed the event —
+// raced with the stream's later signal on the 7B stage-3 comm path (illegal memory access without a per-step sync).
 class EventPool {
  public:
   hipEvent_t get() {
     std::lock_guard<std::mutex> lk(mu_);
+    if (free_.empty()) sweep();
     if (!free_.empty()) {
       hipEvent_t e = free_.back();
       free_.pop_back();
@@ -120,22 +126,37 @@ class EventPool {
     hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
     return e;
   }
-  void put(hipEvent_t e) {
+  // an event that may still be pending on a stream: reusable once it has completed
+  void retire(hipEvent_t e) {
     std::lock_guard<std::mutex> lk(mu_);
-    free_.push_back(e);
+    pending_.push_back(e);
+    if (pending_.size() > 256) sweep();
   }
+  void put(hipEvent_t e) { retire(e); }
   void release() {
     std::lock_guard<std::mutex> lk(mu_);
     for (hipEvent_t e : free_) hipEventDestroy(e);
     free_.clear();
+    for (hipEvent_t e : pending_) hipEventDestroy(e);   // shutdown: the device work is over
+    pending_.clear();
   }
   ~EventPool() {
     if (!g_shutdown) release();
   }
 
  private:
+  // move completed pending events to the free list (caller holds mu_)
+  void sweep() {
+    size_t keep = 0;
+    for (size_t i = 0; i < pending_.size(); ++i) {
+      if (hipEventQuery(pending_[i]) == hipSuccess) free_.push_back(pending_[i]);
+      else pending_[keep++] = pending_[i];
+    }
+    pending_.resize(keep);
+  }
   std::mutex mu_;
   std::vector<hipEvent_t> free_;
+  std::vector<hipEvent_t> pending_;
 };
 
 // IEEE binary16 from binary32, round to nearest even (the PreMulSum scalar of an fp16 reduction)
@@ -180,11 +201,9 @@ class Task {
       : comms_(std::move(comms)), ends_(std::move(ends)), pool_(std::move(pool)), timeout_ms_(timeout_ms) {}
   ~Task() {
     if (g_shutdown) return;
-    for (hipEvent_t e : ends_) {
-      // an event still pending on a live stream may be reused only after it completes
-      if (hipEventQuery(e) == hipSuccess) pool_->put(e);
-      else hipEventDestroy(e);
-    }
+    // an end event may still be pending on the comm stream (the caller's stream only WAITS for it): the pool
+    // recycles it after it completes — never destroyed while the GPU may still signal it
+    for (hipEvent_t e : ends_) pool_->retire(e);
   }
   // the caller's stream waits for the communication (no host block)
   void wait(uintptr_t stream) {
@@ -437,7 +456,7 @@ class RcclGroup {
       hipEvent_t pre = pool_->get();
       hip_check(hipEventRecord(pre, coalescing_ ? (hipStream_t)co_calc_ : cstream), "hipEventRecord");
       hip_check(hipStreamWaitEvent(c->stream, pre, 0), "hipStreamWaitEvent");
-      pool_->put(pre);   // a recorded event may be re-recorded: the wait captured this record already
+      pool_->retire(pre);   // reused only after the calc stream passed it
       if (coalescing_) co_comms_.push_back(c);
     }
     enqueue(c->stream);

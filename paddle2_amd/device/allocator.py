@@ -39,6 +39,7 @@ def lib():
             raise RuntimeError(f"native allocator not built ({path}); run paddle2_amd._build.build_allocator()")
         L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)  # the torch hook resolves pd_alloc_* from it
         L.pd_alloc_configure.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.pd_alloc_set_headroom.argtypes = [ctypes.c_uint64]
         L.pd_alloc_stats.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
         L.pd_alloc_reset_peak.argtypes = [ctypes.c_int]
         L.pd_alloc_empty_cache.argtypes = [ctypes.c_int]
@@ -61,6 +62,9 @@ def configure(chunk_mb=None, limit_bytes=None):
         limit_mb = int(flags.flag("FLAGS_gpu_memory_limit_mb", 0) or 0)
         limit_bytes = limit_mb << 20
     lib().pd_alloc_configure(int(chunk_mb) << 20, int(limit_bytes))
+    # device bytes every growth leaves free for the HIP runtime (kernel scratch), RCCL and the driver
+    headroom_mb = int(flags.flag("FLAGS_native_allocator_headroom_mb", 0) or 0)
+    lib().pd_alloc_set_headroom(int(headroom_mb) << 20)
 
 
 def _pluggable():

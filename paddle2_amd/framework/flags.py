@@ -10,6 +10,8 @@ framework's own.  The ones with an effect here:
   FLAGS_embedding_deterministic         embedding backward through a sorted, atomics-free reduction
   FLAGS_fraction_of_gpu_memory_to_use   per-process cap of the caching allocator (set at device init)
   FLAGS_gpu_memory_limit_mb             absolute cap (MiB), wins over the fraction
+  FLAGS_native_allocator_headroom_mb    device MiB every native-allocator growth leaves free for the HIP
+                                        runtime (kernel scratch), RCCL and the driver (default 0 = off)
   FLAGS_allocator_strategy              auto_growth -> expandable segments; naive_best_fit -> plain caching
   FLAGS_auto_growth_chunk_size_in_mb    allocator rounding granularity
   FLAGS_use_cuda_malloc_async_allocator stream-ordered async allocator backend
@@ -48,6 +50,7 @@ _DEFAULTS.update({
     "FLAGS_allocator_strategy": "auto_growth",
     "FLAGS_fraction_of_gpu_memory_to_use": 0.92,
     "FLAGS_gpu_memory_limit_mb": 0,
+    "FLAGS_native_allocator_headroom_mb": 0,
     "FLAGS_use_autotune": False,
     "FLAGS_cudnn_deterministic": False,
     "FLAGS_embedding_deterministic": 0,

@@ -262,3 +262,23 @@ def test_native_allocator_torch_stats_and_miopen_workspace():
     # fwd + dgrad + wgrad = 3 x 2*256*56*56*64*64*9 = 44 GFLOP: 30 ms is < 1.5 TF/s (naive kernels take seconds)
     assert res["active"] and res["peak"] > 0 and res["reserved"] >= res["cur"] > 0, res
     assert res["ms"] < 30.0, res
+
+
+@pytest.mark.gpu
+def test_native_allocator_oom_raises_torch_error():
+    """An allocation the device cannot hold raises torch.OutOfMemoryError (through the torch hook), never hands torch
+    a null pointer — a null data pointer for a non-empty tensor turned a 7B out-of-memory into a GPU memory-access
+    fault.  torch.empty launches no kernel, so the check itself cannot touch the device."""
+    import torch
+
+    from paddle2_amd.device import allocator
+
+    if not allocator.is_active():
+        pytest.skip("native allocator not active")
+    total = torch.cuda.get_device_properties(0).total_memory
+    before = allocator.stats(0)["num_oom_retries"]
+    with pytest.raises(torch.OutOfMemoryError):
+        torch.empty(int(total * 1.5) // 2, dtype=torch.bfloat16, device="cuda")
+    assert allocator.stats(0)["num_oom_retries"] == before + 1
+    x = torch.ones(1024, device="cuda")   # the allocator still serves after the failure
+    assert float(x.sum()) == 1024.0
