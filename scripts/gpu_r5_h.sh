@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round 5 (h): the GPT-3 13B fp8 step (b2 s2048): default routing, fp8 wgrad into the fp32 main-grad slot, the
-# all-native fp8 GEMM on schedules 1 / 2; then a kernel table of the default step.
+# Round 5 (h): the GPT-3 13B fp8 step (b2 s2048): default routing (fp8 schedule 2 is now the kernel default), fp8
+# wgrad into the fp32 main-grad slot, the all-native fp8 GEMM on schedules 1 / 2; then kernel tables of the default
+# fp8 step and of the default Llama-2-7B bench step.
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r5h
 mkdir -p $O
@@ -16,4 +17,8 @@ timeout -k 10 420 rocprofv3 --kernel-trace --stats -d $O/prof_fp8 -o run --outpu
 r=$?; echo "prof rc=$r"; [ $r -ne 0 ] && { tail -20 $O/prof_fp8.log; exit $r; }
 python3 scripts/kernel_table.py $(find $O/prof_fp8 -name "*kernel_trace.csv" | head -1) > $O/kernels_fp8.txt 2>&1; head -45 $O/kernels_fp8.txt
 rm -f $(find $O/prof_fp8 -name "*kernel_trace.csv") 2>/dev/null
+timeout -k 10 420 rocprofv3 --kernel-trace --stats -d $O/prof_7b -o run --output-format csv -- python3 bench.py --steps 3 --warmup 2 > $O/prof_7b.log 2>&1
+r=$?; echo "prof 7b rc=$r"; tail -1 $O/prof_7b.log | cut -c1-300; [ $r -ne 0 ] && { tail -20 $O/prof_7b.log; exit $r; }
+python3 scripts/kernel_table.py $(find $O/prof_7b -name "*kernel_trace.csv" | head -1) > $O/kernels_7b.txt 2>&1; head -45 $O/kernels_7b.txt
+rm -f $(find $O/prof_7b -name "*kernel_trace.csv") 2>/dev/null
 exit 0
