@@ -73,7 +73,8 @@ long pd_bn_workspace(int, long, int);
 int pd_wo_splits(int, int, int, int);
 int pd_dec_splits(int, int, int);
 int pd_dec_gemm(const void*, const void*, const void*, void*, float*, int, int, int, int, void*);
-int pd_dec64_gemm(const void*, const void*, const void*, void*, int, int, int, int, void*);
+int pd_dec64_gemm(const void*, const void*, const void*, void*, int, int, int, int, int, void*);
+int pd_dec64_rt(int);
 long pd_wo_workspace(int, int, int);
 int pd_wo_gemm(int, const void*, const void*, const float*, const float*, int, const void*, void*, float*, int, int, int,
                int, void*);
@@ -404,11 +405,12 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("dec_splits", &pd_dec_splits);
   m.def("dec64_gemm", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t out, int M, int N, int K, int kw,
-                         uintptr_t st) {
-    check(pd_dec64_gemm(P<const void*>(x), P<const void*>(w), P<const void*>(bias), P<void*>(out), M, N, K, kw,
+                         int rt, uintptr_t st) {
+    check(pd_dec64_gemm(P<const void*>(x), P<const void*>(w), P<const void*>(bias), P<void*>(out), M, N, K, kw, rt,
                         P<void*>(st)),
           "dec64_gemm");
   });
+  m.def("dec64_rt", &pd_dec64_rt);
   m.def("dec_gemm", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t out, uintptr_t ws, int M, int N, int K,
                        int S, uintptr_t st) {
     check(pd_dec_gemm(P<const void*>(x), P<const void*>(w), P<const void*>(bias), P<void*>(out), P<float*>(ws), M, N,

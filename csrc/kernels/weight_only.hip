@@ -288,14 +288,16 @@ __global__ __launch_bounds__(256) void dec_gemm_kernel(const unsigned short* __r
 }
 
 // Decode GEMM for 16 < M <= 64 tokens (the batched serving step): out[M, N] = X[M, K] . W[N, K]^T (+ bias), bf16.
-// One workgroup = 16 output channels (W rows) x the WHOLE K, split over its KW waves (no cross-workgroup split-K:
+// One workgroup = 16 * RT output channels (W rows) x the WHOLE K, split over its KW waves (no cross-workgroup split-K:
 // the split-K kernel above moves S x M x N fp32 partials through HBM, which at M = 64 costs 25-100 % of the weight
-// bytes); the KW wave partials meet once in LDS.  Per 64-wide K step a lane streams 32 contiguous bytes of its
-// channel (two MFMA A fragments) from HBM, DW steps ahead (DW x 32 B in flight per lane), and reads its MT X row
-// fragments (X: 64 x K bf16, L2-resident, shared by every workgroup) one step ahead; v_mfma_f32_16x16x32_bf16 gives
-// D[channel][token] = out^T.  X rows >= M and K past the wave's range read as zeros through the buffer descriptors'
-// range check.  grid = N / 16 workgroups (256 for N = 4096 — one per CU), block = 64 * KW.
-template <int MT, int KW, int DW>
+// bytes); the KW wave partials meet once in LDS.  Per 64-wide K step a lane streams 32 contiguous bytes of each of
+// its RT channels (two MFMA A fragments per channel tile) from HBM, DW steps ahead (DW x RT x 32 B in flight per
+// lane), and reads its MT X row fragments (X: 64 x K bf16, L2-resident, shared by every workgroup) one step ahead;
+// v_mfma_f32_16x16x32_bf16 gives D[channel][token] = out^T.  RT sets the X reuse: every X fragment a wave loads
+// feeds RT channel tiles, so X's L2 -> CU traffic is MT / RT times the weight bytes (RT = 1: 4x at M = 64, which
+// capped the kernel at 1.5-1.7 TB/s of weights; profiles/r5_decode_serving.md).  X rows >= M and K past the wave's
+// range read as zeros through the buffer descriptors' range check.  grid = N / (16 RT) workgroups, block = 64 * KW.
+template <int MT, int KW, int DW, int RT>
 __global__ __launch_bounds__(64 * KW) void dec64_kernel(const unsigned short* __restrict__ X,
                                                         const unsigned short* __restrict__ W,
                                                         const unsigned short* __restrict__ bias,
@@ -303,28 +305,32 @@ __global__ __launch_bounds__(64 * KW) void dec64_kernel(const unsigned short* __
   __shared__ wo_f32x4 red[KW][MT][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int n0 = blockIdx.x * 16;
+  const int n0 = blockIdx.x * 16 * RT;
   const int U = K / 64;
   const int s0 = U * wave / KW, s1 = U * (wave + 1) / KW;   // this wave's 64-wide K steps
   const int ns = s1 - s0;
   // buffer descriptors (wave-uniform bases) with EXACT extents: W from the wave's first K step of row n0 to the end
-  // of row n0 + 15, X to the end of row M - 1.  Prefetches past the wave's range use the offset kSkip, which is
-  // beyond both extents, so the range check returns zeros (an earlier form bounded W at 0x7fffffff and skipped
+  // of row n0 + 16 RT - 1, X to the end of row M - 1.  Prefetches past the wave's range use the offset kSkip, which
+  // is beyond both extents, so the range check returns zeros (an earlier form bounded W at 0x7fffffff and skipped
   // with 0x7ffffff0 — INSIDE that range — and the tail prefetches read ~2 GiB past the weight: a GPU fault)
   constexpr int kSkip = (int)0x7fffff00;
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<unsigned short*>(W + (long)n0 * K + (long)s0 * 64), (short)0, (int)((16L * K - (long)s0 * 64) * 2),
-      0x00020000);
+      const_cast<unsigned short*>(W + (long)n0 * K + (long)s0 * 64), (short)0,
+      (int)((16L * RT * K - (long)s0 * 64) * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<unsigned short*>(X + (long)s0 * 64), (short)0, (int)(((long)M * K - (long)s0 * 64) * 2), 0x00020000);
   const int wvo = (r16 * K + 16 * g) * 2;                      // lane's W byte offset at step 0 (row n0 + r16)
+  const int rstride = 16 * K * 2;                              // bytes between channel tiles
   int xvo[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) xvo[t] = ((t * 16 + r16) * K + 16 * g) * 2;
-  auto ldw = [&](int s, uint4 (&o)[2]) {
-    const int v = s < ns ? wvo + s * 128 : kSkip;   // past the wave's range: an offset beyond the extent
-    o[0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, v, 0, 0));
-    o[1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, v + 16, 0, 0));
+  auto ldw = [&](int s, uint4 (&o)[RT][2]) {
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int v = s < ns ? wvo + r * rstride + s * 128 : kSkip;   // past the wave's range: beyond the extent
+      o[r][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, v, 0, 0));
+      o[r][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, v + 16, 0, 0));
+    }
   };
   auto ldx = [&](int s, uint4 (&o)[MT][2]) {
 #pragma unroll
@@ -334,10 +340,12 @@ __global__ __launch_bounds__(64 * KW) void dec64_kernel(const unsigned short* __
       o[t][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, v + 16, 0, 0));
     }
   };
-  wo_f32x4 acc[MT];
+  wo_f32x4 acc[RT][MT];
 #pragma unroll
-  for (int t = 0; t < MT; ++t) acc[t] = wo_f32x4{0.f, 0.f, 0.f, 0.f};
-  uint4 wb[DW][2], xb[2][MT][2];
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[r][t] = wo_f32x4{0.f, 0.f, 0.f, 0.f};
+  uint4 wb[DW][RT][2], xb[2][MT][2];
 #pragma unroll
   for (int d = 0; d < DW; ++d) ldw(d, wb[d]);
   ldx(0, xb[0]);
@@ -348,40 +356,49 @@ __global__ __launch_bounds__(64 * KW) void dec64_kernel(const unsigned short* __
       const int s = c + d;
       if (s >= ns) break;
       ldx(s + 1, xb[(d + 1) & 1]);
-      const wo_bf16x8 a0 = __builtin_bit_cast(wo_bf16x8, wb[d][0]);
-      const wo_bf16x8 a1 = __builtin_bit_cast(wo_bf16x8, wb[d][1]);
 #pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, __builtin_bit_cast(wo_bf16x8, xb[d & 1][t][0]), acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, __builtin_bit_cast(wo_bf16x8, xb[d & 1][t][1]), acc[t], 0, 0, 0);
+      for (int r = 0; r < RT; ++r) {
+        const wo_bf16x8 a0 = __builtin_bit_cast(wo_bf16x8, wb[d][r][0]);
+        const wo_bf16x8 a1 = __builtin_bit_cast(wo_bf16x8, wb[d][r][1]);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, __builtin_bit_cast(wo_bf16x8, xb[d & 1][t][0]),
+                                                              acc[r][t], 0, 0, 0);
+          acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, __builtin_bit_cast(wo_bf16x8, xb[d & 1][t][1]),
+                                                              acc[r][t], 0, 0, 0);
+        }
       }
       ldw(s + DW, wb[d]);
     }
   }
-  // the KW partials of this workgroup's 16 channels: LDS, then wave t (< MT) sums token tile t
+  // per channel tile: the KW partials through LDS, then wave t (< MT) sums token tile t and stores it
 #pragma unroll
-  for (int t = 0; t < MT; ++t) red[wave][t][lane] = acc[t];
-  __syncthreads();
-  if (wave < MT) {
-    const int t = wave;
-    wo_f32x4 v = red[0][t][lane];
+  for (int r = 0; r < RT; ++r) {
+    if (r) __syncthreads();   // the previous tile's readers are done with red
 #pragma unroll
-    for (int w = 1; w < KW; ++w) {
-      const wo_f32x4 o = red[w][t][lane];
-      v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
-    }
-    // D[channel 4g + e][token 16t + r16] -> out[token][n0 + 4g .. + 3]
-    const int m = t * 16 + r16;
-    const int n = n0 + 4 * g;
-    if (m < M) {
-      float o[4] = {v[0], v[1], v[2], v[3]};
-      if (bias) {
+    for (int t = 0; t < MT; ++t) red[wave][t][lane] = acc[r][t];
+    __syncthreads();
+    if (wave < MT) {
+      const int t = wave;
+      wo_f32x4 v = red[0][t][lane];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] += bf2f(bias[n + e]);
+      for (int w = 1; w < KW; ++w) {
+        const wo_f32x4 o = red[w][t][lane];
+        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
       }
-      const uint2 pk = make_uint2((unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16),
-                                  (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16));
-      *reinterpret_cast<uint2*>(out + (long)m * N + n) = pk;
+      // D[channel 4g + e][token 16t + r16] -> out[token][n0 + 16 r + 4g .. + 3]
+      const int m = t * 16 + r16;
+      const int n = n0 + 16 * r + 4 * g;
+      if (m < M) {
+        float o[4] = {v[0], v[1], v[2], v[3]};
+        if (bias) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] += bf2f(bias[n + e]);
+        }
+        const uint2 pk = make_uint2((unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16),
+                                    (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16));
+        *reinterpret_cast<uint2*>(out + (long)m * N + n) = pk;
+      }
     }
   }
 }
@@ -482,23 +499,34 @@ extern "C" int pd_wo_gemm(int int4, const void* X, const void* W, const float* c
 }
 
 // The whole-K decode GEMM for 16 < M <= 64 (dec64_kernel): N % 16 == 0, K % 64 == 0, 16-B aligned rows.  kw: waves
-// per workgroup (4 or 8).  Returns -1 outside the domain.
+// per workgroup (4 or 8); rt: channel tiles per workgroup (1, 2 or 4; N % (16 rt) == 0), 0 = auto: 4 for the wide
+// projections (N >= 8192: 1.6 -> 2.7-3.5 TB/s at M = 64 even at 128-192 workgroups), 1 below (N = 4096 needs its
+// 256 workgroups; rt 4 there halves the rate).  Measured: profiles/r5_decode_serving.md.  Returns -1 outside the
+// domain.
+extern "C" int pd_dec64_rt(int N) { return (N >= 8192 && N % 64 == 0) ? 4 : 1; }
+
 extern "C" int pd_dec64_gemm(const void* X, const void* W, const void* bias, void* out, int M, int N, int K, int kw,
-                             void* stream) {
+                             int rt, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (rt == 0) rt = pd_dec64_rt(N);
   if (M < 1 || M > 64 || N % 16 || K % 64 || (kw != 4 && kw != 8) || (size_t)X % 16 || (size_t)W % 16) return -1;
+  if ((rt != 1 && rt != 2 && rt != 4) || N % (16 * rt)) return -1;
   // byte offsets (incl. the skip offset kSkip = 0x7fffff00 and its +16) stay below 2^31 and beyond every extent
   if ((long)N * K * 2 >= 0x7fffff00L || (long)M * K * 2 >= 0x7fffff00L) return -1;
-  const dim3 grid(N / 16);
-#define PD_D64(MT_, KW_) \
-  dec64_kernel<MT_, KW_, 8><<<grid, 64 * KW_, 0, st>>>((const unsigned short*)X, (const unsigned short*)W, \
-                                                        (const unsigned short*)bias, (unsigned short*)out, M, N, K)
+  const dim3 grid(N / (16 * rt));
+  // DW x RT = 8: the same 256 B of W in flight per lane at every RT
+#define PD_D64(MT_, KW_, RT_) \
+  dec64_kernel<MT_, KW_, 8 / RT_, RT_><<<grid, 64 * KW_, 0, st>>>((const unsigned short*)X, (const unsigned short*)W, \
+                                                                  (const unsigned short*)bias, (unsigned short*)out, M, N, K)
+#define PD_D64_RT(MT_, KW_) \
+  if (rt == 1) PD_D64(MT_, KW_, 1); else if (rt == 2) PD_D64(MT_, KW_, 2); else PD_D64(MT_, KW_, 4);
   const int mt = (M + 15) / 16;
   if (kw == 8) {
-    if (mt <= 2) PD_D64(2, 8); else PD_D64(4, 8);
+    if (mt <= 2) { PD_D64_RT(2, 8) } else { PD_D64_RT(4, 8) }
   } else {
-    if (mt <= 2) PD_D64(2, 4); else PD_D64(4, 4);
+    if (mt <= 2) { PD_D64_RT(2, 4) } else { PD_D64_RT(4, 4) }
   }
+#undef PD_D64_RT
 #undef PD_D64
   return (int)hipGetLastError();
 }

@@ -192,8 +192,9 @@ def _mm(a, b_colmajor, inv_a, inv_b, out_dtype, bias=None):
 
 # The weight gradient of an fp8 linear whose weight has an fp32 main-grad slot (a sharding unit's ``_p2_gt``, as the
 # bf16 linear): the native fp8 GEMM writes the fp32 product straight into the slot (C = dW + beta * C) instead of a
-# bf16 dW that autograd hands to the unit's hook for a bf16 -> fp32 conversion pass.  "0" keeps the bf16 dW.
-WGRAD_MAIN = os.environ.get("PADDLE2_AMD_FP8_WGRAD_MAIN", "0") != "0"
+# bf16 dW that autograd hands to the unit's hook for a bf16 -> fp32 conversion pass (on by default: GPT-3 13B fp8
+# step 14,686 vs 14,542 tok/s, profiles/r5_gpt13b_fp8_step.md).  "0" keeps the bf16 dW.
+WGRAD_MAIN = os.environ.get("PADDLE2_AMD_FP8_WGRAD_MAIN", "1") != "0"
 
 
 def _wgrad_into_main(gt, xqT, gqT, inv_x, inv_g):

@@ -67,12 +67,15 @@ import os as _os  # noqa: E402
 
 DECODE_GEMM = _os.environ.get("PADDLE2_AMD_DECODE_GEMM", "auto")   # auto | native | blas
 DEC64_WAVES = int(_os.environ.get("PADDLE2_AMD_DEC64_WAVES", "8"))  # waves per workgroup of the M > 16 kernel
+DEC64_RT = int(_os.environ.get("PADDLE2_AMD_DEC64_RT", "0"))        # its channel tiles per workgroup (0 = auto)
 
 
 def decode_ok(x, wt):
     """The native stream kernel is taken where it measured faster than hipBLASLt's skinny GEMM
-    (profiles/r4_decode_gemm.md): M <= 16 with N <= 8192 (the o / down projections: 2.6-4.0 vs 1.9-3.4 TB/s);
-    16 < M <= 64 runs the whole-K stream kernel (dec64_kernel: no split-K partials through HBM).
+    (profiles/r4_decode_gemm.md): M <= 16 with N <= 8192 (the o / down projections: 2.6-4.0 vs 1.9-3.4 TB/s).
+    16 < M <= 64 has the whole-K stream kernel (dec64_kernel: no split-K partials through HBM), which beats the
+    library only on the square 4096 x 4096 projection at M <= 32 (profiles/r5_decode_serving.md: 2.1 vs 1.8 TB/s;
+    1.5-2.8 vs 2.7-4.4 TB/s on the wide ones), so auto routes only that shape to it.
     PADDLE2_AMD_DECODE_GEMM=native forces the native kernels for every M <= 64, =blas the library."""
     M, K = x.shape
     Nn = wt.shape[0]
@@ -82,8 +85,8 @@ def decode_ok(x, wt):
         return False
     if DECODE_GEMM == "blas":
         return False
-    if M > 16:
-        return Nn % 16 == 0   # the whole-K MFMA stream kernel (dec64_kernel): the b17-64 serving step
+    if M > 16:   # the whole-K MFMA stream kernel (dec64_kernel): the b17-64 serving step
+        return Nn % 16 == 0 and (DECODE_GEMM == "native" or (M <= 32 and Nn <= 4096 and K <= 4096))
     return Nn % 64 == 0 and (DECODE_GEMM == "native" or Nn <= 8192)   # the split-K kernel: 64-row blocks
 
 
@@ -101,7 +104,8 @@ def decode_matmul(x, wt, bias=None):
         out = torch.empty(M, Nn, dtype=x.dtype, device=x.device)
         if bias is not None:
             bias = bias.to(torch.bfloat16).contiguous()
-        C.dec64_gemm(x.data_ptr(), wt.data_ptr(), N.ptr(bias), out.data_ptr(), M, Nn, K, DEC64_WAVES, N.stream())
+        C.dec64_gemm(x.data_ptr(), wt.data_ptr(), N.ptr(bias), out.data_ptr(), M, Nn, K, DEC64_WAVES, DEC64_RT,
+                     N.stream())
         return out
     S = C.dec_splits(M, Nn, K)
     ws = torch.empty(S * M * Nn, dtype=torch.float32, device=x.device)

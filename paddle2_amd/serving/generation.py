@@ -93,10 +93,14 @@ class LlamaGenerator:
                 ent[2] = T.transpose2d(w)
                 self._graph = None
             ent[0], ent[1] = w.data_ptr(), w._version
-        if x.dim() == 2 and x.shape[0] <= 64:
+        K = x.shape[-1]
+        if x.numel() <= 64 * K:
+            # decode ([B, 1, K] hidden states, B <= 64): the rows flattened to one [B, K] operand so the native
+            # weight-streaming kernel sees them (ops/weight_only.decode_ok picks it or hipBLASLt per shape)
             from ..ops import weight_only as WO
 
-            return WO.decode_matmul(x, ent[2])   # decode: the native weight-streaming kernel
+            y = WO.decode_matmul(x.reshape(-1, K), ent[2])
+            return y.view(*x.shape[:-1], y.shape[-1])
         return torch.matmul(x, ent[2].t())
 
     def _nk_fits(self):

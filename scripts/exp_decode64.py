@@ -1,4 +1,4 @@
-"""Decode GEMM at 17-64 tokens: the whole-K dec64 kernel (4 / 8 waves) vs hipBLASLt on the Llama-2-7B projections,
+"""Decode GEMM at 17-64 tokens: the whole-K dec64 kernel (8 waves, 1 / 2 / 4 channel tiles per workgroup) vs hipBLASLt on the Llama-2-7B projections,
 weights rotated over copies totalling > 512 MB so every call streams them from HBM (a single weight stays in the
 256 MB Infinity Cache across a loop and reads at cache speed).  TB/s counts the weight bytes."""
 import json
@@ -7,6 +7,8 @@ import torch
 
 from paddle2_amd.ops import _native as N
 from paddle2_amd.ops import weight_only as WO
+
+WO.DECODE_GEMM = "native"   # time the kernel on every shape (auto routes only the ones it wins)
 
 
 def bench(fn, copies, iters=60):
@@ -22,7 +24,7 @@ def bench(fn, copies, iters=60):
     return s.elapsed_time(e) / iters
 
 
-for M in (32, 64):
+for M in (24, 32, 48, 64):
     for name, Nn, K in (("qkv", 12288, 4096), ("o", 4096, 4096), ("gate_up", 22016, 4096), ("down", 4096, 11008),
                         ("lm_head", 32000, 4096)):
         wb = Nn * K * 2
@@ -30,11 +32,15 @@ for M in (32, 64):
         copies = [torch.randn(Nn, K, device="cuda").to(torch.bfloat16) for _ in range(ncp)]
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
         rec = {"M": M, "proj": name, "N": Nn, "K": K, "copies": ncp}
-        for kw in (4, 8):
-            WO.DEC64_WAVES = kw
+        WO.DEC64_WAVES = 8
+        for rt in (1, 2, 4):
+            if Nn % (16 * rt):
+                continue
+            WO.DEC64_RT = rt
             t = bench(lambda w: WO.decode_matmul(x, w), copies)
-            rec[f"dec64_w{kw}_us"] = round(t * 1e3, 1)
-            rec[f"dec64_w{kw}_TBs"] = round(wb / t / 1e9, 2)
+            rec[f"dec64_rt{rt}_us"] = round(t * 1e3, 1)
+            rec[f"dec64_rt{rt}_TBs"] = round(wb / t / 1e9, 2)
+        WO.DEC64_RT = 0
         t = bench(lambda w: torch.matmul(x, w.t()), copies)
         rec["blas_us"], rec["blas_TBs"] = round(t * 1e3, 1), round(wb / t / 1e9, 2)
         y = WO.decode_matmul(x, copies[0])

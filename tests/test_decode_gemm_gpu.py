@@ -28,14 +28,19 @@ def test_decode_gemm_matches_fp32(M, N, K, monkeypatch):
     assert _rel(y, ref) < 8e-3
 
 
+@pytest.mark.parametrize("rt", [0, 1, 2, 4])
 @pytest.mark.parametrize("waves", [4, 8])
 @pytest.mark.parametrize("M", [17, 40, 64])
-@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 11008), (12288, 4096), (48, 192)])
-def test_dec64_whole_k_kernel(M, N, K, waves, monkeypatch):
-    """The M > 16 whole-K kernel (dec64_kernel) at both workgroup widths, ragged M, K not a multiple of the wave
-    count's 64-wide steps (11008 = 172 steps), a tiny shape with fewer steps than waves."""
-    monkeypatch.setattr(WO, "DECODE_GEMM", "auto")
+@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 11008), (12288, 4096), (48, 192), (192, 128)])
+def test_dec64_whole_k_kernel(M, N, K, waves, rt, monkeypatch):
+    """The M > 16 whole-K kernel (dec64_kernel) at both workgroup widths and every channel-tile count (rt, 0 =
+    auto), ragged M, K not a multiple of the wave count's 64-wide steps (11008 = 172 steps), tiny shapes with fewer
+    steps than waves."""
+    if rt and N % (16 * rt):
+        pytest.skip("N not a multiple of the workgroup's channels")
+    monkeypatch.setattr(WO, "DECODE_GEMM", "native")
     monkeypatch.setattr(WO, "DEC64_WAVES", waves)
+    monkeypatch.setattr(WO, "DEC64_RT", rt)
     g = torch.Generator(device=dev).manual_seed(7 * M + N)
     x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
     wt = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)
@@ -46,3 +51,16 @@ def test_dec64_whole_k_kernel(M, N, K, waves, monkeypatch):
     assert _rel(y, ref) < 8e-3
     y2 = WO.decode_matmul(x, wt)
     assert _rel(y2, x.float() @ wt.float().t()) < 8e-3
+
+
+def test_auto_routing(monkeypatch):
+    """auto: native split-K at M <= 16 on N <= 8192, dec64 only on the 4096 x 4096 projection at M <= 32,
+    hipBLASLt elsewhere (profiles/r4_decode_gemm.md, profiles/r5_decode_serving.md)."""
+    monkeypatch.setattr(WO, "DECODE_GEMM", "auto")
+
+    def ok(M, N, K):
+        return WO.decode_ok(torch.empty(M, K, device=dev, dtype=torch.bfloat16),
+                            torch.empty(N, K, device=dev, dtype=torch.bfloat16))
+
+    assert ok(1, 4096, 4096) and ok(16, 4096, 11008) and not ok(1, 12288, 4096)
+    assert ok(32, 4096, 4096) and not ok(64, 4096, 4096) and not ok(32, 4096, 11008) and not ok(32, 12288, 4096)

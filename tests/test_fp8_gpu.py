@@ -38,6 +38,27 @@ def test_fp8_delayed_scaling_update():
     assert float(m.amax.abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("hlen", [1, 4, 16, 64, 70])
+def test_fp8_update_scale_matches_cpu_recipe(hlen):
+    """The one-wave update kernel (slot fold, history roll, history max; serial beyond 64 entries) against the CPU
+    path of FP8TensorMeta.update over several steps, including steps whose amax is zero."""
+    from paddle2_amd.ops import fp8
+
+    g = torch.Generator().manual_seed(hlen)
+    gpu = fp8.FP8TensorMeta(torch.float8_e5m2, history_len=hlen, margin=1, device=torch.device(DEV))
+    cpu = fp8.FP8TensorMeta(torch.float8_e5m2, history_len=hlen, margin=1)
+    for step in range(hlen + 5):
+        a = torch.rand(fp8.AMAX_SLOTS, generator=g) * (0 if step % 3 == 2 else 10.0 ** (step % 4))
+        gpu.amax.copy_(a)
+        cpu.amax.copy_(a)
+        gpu.update()
+        cpu.update()
+        assert torch.equal(gpu.history.cpu(), cpu.history), step
+        assert float(gpu.scale) == pytest.approx(float(cpu.scale), rel=1e-6)
+        assert float(gpu.inv_scale) == pytest.approx(float(cpu.inv_scale), rel=1e-6)
+        assert float(gpu.amax.abs().max()) == 0.0
+
+
 def test_fp8_linear_matches_bf16():
     import paddle2_amd as paddle
     from paddle2_amd.incubate.fp8 import Float8Linear

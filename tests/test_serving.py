@@ -163,10 +163,39 @@ def test_generation_graph_follows_weight_update_gpu():
     out = gen.generate(prompts, 6)
     assert {k: v[2].data_ptr() for k, v in gen._wt.items()} == bufs   # updated in place, same addresses
     eager = LlamaGenerator(m, max_batch=2, max_seq_len=128, block_size=16, use_graph=False,
-                           weight_layout="kn").generate(prompts, 6)
+                           weight_layout="nk").generate(prompts, 6)   # same GEMM kernels, fresh W^T copies
     assert out == eager
     for p, o in zip(prompts, out):
         assert o[:3] == greedy_reference(m, p, 6)[:3]
+
+
+@pytest.mark.gpu
+def test_decode_step_runs_the_native_decode_gemm_gpu(monkeypatch):
+    """The decode step's [B, 1, K] hidden states (and a short prompt's rows) reach the native weight-streaming GEMM
+    flattened to [rows, K], and the tokens match the hipBLASLt ("kn") layout."""
+    from paddle2_amd.ops import weight_only as WO
+    from paddle2_amd.serving.generation import LlamaGenerator
+
+    paddle.set_device("gpu:0")
+    m = _tiny_llama("cuda")
+    prompts = [[1, 5, 9, 3, 11, 4], [7, 2, 8]]
+    monkeypatch.setattr(WO, "DECODE_GEMM", "native")
+    native_calls = []
+    real = WO.decode_matmul
+
+    def counting(x, wt, bias=None):
+        if WO.decode_ok(x, wt):
+            native_calls.append(tuple(x.shape))
+        return real(x, wt, bias)
+
+    monkeypatch.setattr(WO, "decode_matmul", counting)
+    out = LlamaGenerator(m, max_batch=2, max_seq_len=128, block_size=16, use_graph=False,
+                         weight_layout="nk").generate(prompts, 6)
+    assert (2, 256) in native_calls   # the B = 2 decode rows
+    eager = LlamaGenerator(m, max_batch=2, max_seq_len=128, block_size=16, use_graph=False,
+                           weight_layout="kn").generate(prompts, 6)
+    for a, b in zip(out, eager):
+        assert a[:3] == b[:3]
 
 
 def test_static_mm_cache_lives_on_the_weight():

@@ -26,6 +26,7 @@ def _run(dev, force, acc=1):
         # deterministic flash backward (per-key-block dQ slabs summed in a fixed order): the default fp32-atomic dQ
         # makes two identical runs differ in the last bits, which would hide what this test compares
         env["PADDLE2_AMD_FA_DQ_ATOMIC"] = "0"
+        env["FLAGS_embedding_deterministic"] = "1"   # the embedding gradient's fp32 atomics, likewise
     p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "workers", "force_comm_worker.py")], env=env,
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-4000:]
@@ -50,9 +51,11 @@ def test_force_comm_matches_short_circuit_cpu(acc):
 @pytest.mark.gpu
 @pytest.mark.parametrize("acc", [1, 2])
 def test_force_comm_matches_short_circuit_gpu(acc):
-    """On the GPU some backward kernels add with fp32 atomics (embedding gradient, flash dQ), so two runs of the
-    SAME path may differ in the last bits: the forced-comm run must then be as close to the short-circuit as a
-    second short-circuit run is (bitwise equal whenever the short-circuit path repeats bitwise)."""
+    """The runs use the deterministic flash dQ and embedding gradient, so the short-circuit path normally repeats
+    bit for bit and the forced-comm run must then match it bitwise.  Should some other kernel still add with
+    atomics (two short-circuit runs differ), the losses diverge chaotically from the first differing bit over the
+    4 steps, so the bound is a multiple of that run-to-run noise with a floor of 5e-3 (a missing or doubled
+    gradient moves the losses by far more)."""
     a, a2, b = _run("cuda", False, acc), _run("cuda", False, acc), _run("cuda", True, acc)
     assert not any(a["comm"]) and all(b["comm"]) and b["initialized"] and b["pg"] == "pdrccl"
     assert a["losses"][0] == b["losses"][0]   # the first forward reads the same parameters
@@ -61,4 +64,4 @@ def test_force_comm_matches_short_circuit_gpu(acc):
     if noise == 0.0:
         assert a["losses"] == b["losses"] and a["digest"] == b["digest"], (a, b)
     else:
-        assert diff <= 4 * noise + 1e-6, (a["losses"], a2["losses"], b["losses"])
+        assert diff <= max(8 * noise, 5e-3), (a["losses"], a2["losses"], b["losses"])
