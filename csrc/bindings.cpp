@@ -75,6 +75,8 @@ int pd_dec_splits(int, int, int);
 int pd_dec_gemm(const void*, const void*, const void*, void*, float*, int, int, int, int, void*);
 int pd_dec64_gemm(const void*, const void*, const void*, void*, int, int, int, int, int, void*);
 int pd_dec64_rt(int);
+int pd_dec64s_gemm(const void*, const void*, const void*, void*, float*, int, int, int, int, int, int, void*);
+long pd_dec64s_workspace(int, int, int, int, int, int);
 long pd_wo_workspace(int, int, int);
 int pd_wo_gemm(int, const void*, const void*, const float*, const float*, int, const void*, void*, float*, int, int, int,
                int, void*);
@@ -411,6 +413,13 @@ PYBIND11_MODULE(_C, m) {
           "dec64_gemm");
   });
   m.def("dec64_rt", &pd_dec64_rt);
+  m.def("dec64s_gemm", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t out, uintptr_t ws, int M, int N, int K,
+                          int dw, int rt, int S, uintptr_t st) {
+    check(pd_dec64s_gemm(P<const void*>(x), P<const void*>(w), P<const void*>(bias), P<void*>(out), P<float*>(ws), M,
+                         N, K, dw, rt, S, P<void*>(st)),
+          "dec64s_gemm");
+  });
+  m.def("dec64s_workspace", &pd_dec64s_workspace);
   m.def("dec_gemm", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t out, uintptr_t ws, int M, int N, int K,
                        int S, uintptr_t st) {
     check(pd_dec_gemm(P<const void*>(x), P<const void*>(w), P<const void*>(bias), P<void*>(out), P<float*>(ws), M, N,

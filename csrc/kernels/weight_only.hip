@@ -403,6 +403,136 @@ __global__ __launch_bounds__(64 * KW) void dec64_kernel(const unsigned short* __
   }
 }
 
+// Decode GEMM for 16 < M <= 64, X through LDS (dec64s_kernel): the fix for dec64_kernel's limit.  vmcnt retires
+// VMEM loads in issue order, so dec64_kernel's one-step X prefetch made every wait also wait for the W loads issued
+// before it: its 8-step W ring worked like a 1-step one.  Here the waves of a workgroup split the CHANNELS (wave w:
+// channels n0 + 16 RT w ..) and walk the same 64-wide K steps together; each step's X tile [64 tokens][64 k] (8 KiB)
+// arrives by LDS-DMA (buffer_load ... lds, 1 KiB per wave-instruction, 8 / KW per wave) into a DW-slot LDS ring
+// and is read by every wave (ds_read_b128, lgkmcnt), so the only VMEM traffic is the DW - 1 steps of W and X
+// pieces in flight, all issued together per step: one counted `vmcnt` + `s_barrier` per step.
+// LDS image of a step tile: row r (token) at 128 r, 16-B chunk c (k 8c .. 8c + 7) at position c ^ (r & 7) (the
+// swizzle is applied on the DMA source side: lane i of a piece fetches chunk (i & 7) ^ (i >> 3)), so the 16-lane
+// ds_read_b128 groups (same chunk pair, 8 consecutive rows) are conflict-free.
+// Split-K over gridDim.y (S): S == 1 writes bf16 (+ bias) directly; S > 1 writes fp32 partials into ws [S][M][N]
+// for wo_reduce_kernel.  grid = (N / (16 RT KW), S), block = 64 KW.
+// one 16-B-per-lane LDS-DMA piece (1 KiB per wave) at the wave-uniform LDS address dst
+__device__ __forceinline__ void dec_lds_dma16(const __amdgpu_buffer_rsrc_t& rs, unsigned dst, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(size_t)dst, 16, voff, 0, 0, 0);
+}
+
+template <int MT, int KW, int RT, int DW>
+__global__ __launch_bounds__(64 * KW) void dec64s_kernel(const unsigned short* __restrict__ X,
+                                                         const unsigned short* __restrict__ W,
+                                                         const unsigned short* __restrict__ bias,
+                                                         unsigned short* __restrict__ out, float* __restrict__ ws,
+                                                         int M, int N, int K) {
+  constexpr int D = DW - 1;                 // prefetch distance (steps in flight)
+  constexpr int P = 8 / KW;                 // X pieces per wave per step
+  constexpr int C = P + 2 * RT;             // VMEM instructions per wave per step
+  static_assert((D - 1) * C <= 63, "vmcnt immediate");
+  __shared__ __attribute__((aligned(1024))) char xs[DW * 8192];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform: SGPR descriptors
+  const int g = lane >> 4, r16 = lane & 15;
+  const int n0 = (blockIdx.x * KW + wave) * 16 * RT;   // this wave's first channel
+  const int U = K / 64, S = gridDim.y;
+  const int s0 = (int)((long)U * blockIdx.y / S), ns = (int)((long)U * (blockIdx.y + 1) / S) - s0;
+  // Prefetches past the split's last step read whatever the offset lands on (the next row's K, or zeros beyond the
+  // extent through the range check) — never used: the step loop stops at ns.  No select, no branch per issue.
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(W + (long)n0 * K + (long)s0 * 64), (short)0,
+      (int)((16L * RT * K - (long)s0 * 64) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(X + (long)s0 * 64), (short)0, (int)(((long)M * K - (long)s0 * 64) * 2), 0x00020000);
+  const int wvo = (r16 * K + 16 * g) * 2;   // lane's W byte offset at step 0 (channel n0 + r16, k 16 g)
+  const int rstride = 16 * K * 2;
+  // X piece j of this wave: rows 8 (wave + KW j) + (lane >> 3), source chunk (lane & 7) ^ (lane >> 3)
+  int xvo[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const int row = 8 * (wave + KW * j) + (lane >> 3);
+    xvo[j] = (row * K + 8 * ((lane & 7) ^ (lane >> 3))) * 2;
+  }
+  const unsigned xbase = (unsigned)(size_t)(__attribute__((address_space(3))) char*)xs;
+  auto issue = [&](int s, int slot, uint4 (&o)[RT][2]) {
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const unsigned dst = xbase + slot * 8192 + (wave + KW * j) * 1024;
+      dec_lds_dma16(rx, dst, (unsigned)(xvo[j] + s * 128));
+    }
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int v = wvo + r * rstride + s * 128;
+      o[r][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, v, 0, 0));
+      o[r][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, v + 16, 0, 0));
+    }
+  };
+  wo_f32x4 acc[RT][MT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[r][t] = wo_f32x4{0.f, 0.f, 0.f, 0.f};
+  uint4 wb[DW][RT][2];
+#pragma unroll
+  for (int d = 0; d < D; ++d) issue(d, d, wb[d]);
+  // lane's X read offsets inside a slot: token row 16 t + r16, chunks 2g / 2g + 1 at their swizzled positions
+  const int xr0 = r16 * 128 + ((2 * g) ^ (r16 & 7)) * 16, xr1 = r16 * 128 + ((2 * g + 1) ^ (r16 & 7)) * 16;
+  for (int c = 0; c < ns; c += DW) {
+#pragma unroll
+    for (int d = 0; d < DW; ++d) {
+      const int s = c + d;
+      if (s >= ns) break;
+      // step s's pieces (this wave's) landed: D - 1 later steps may stay in flight; then everyone's
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"((D - 1) * C) : "memory");
+      __builtin_amdgcn_s_barrier();
+      // every wave is past step s - 1: its slot (d - 1) takes step s + D
+      issue(s + D, (d + DW - 1) % DW, wb[(d + DW - 1) % DW]);
+      const char* xt = xs + d * 8192;
+      wo_bf16x8 b0[MT], b1[MT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        b0[t] = *reinterpret_cast<const wo_bf16x8*>(xt + t * 16 * 128 + xr0);
+        b1[t] = *reinterpret_cast<const wo_bf16x8*>(xt + t * 16 * 128 + xr1);
+      }
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const wo_bf16x8 a0 = __builtin_bit_cast(wo_bf16x8, wb[d][r][0]);
+        const wo_bf16x8 a1 = __builtin_bit_cast(wo_bf16x8, wb[d][r][1]);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0[t], acc[r][t], 0, 0, 0);
+          acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[t], acc[r][t], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // drain the tail prefetches (zero-filled, past the range) before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // D[channel 4g + e][token 16t + r16]
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    const int n = n0 + 16 * r + 4 * g;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int m = t * 16 + r16;
+      if (m >= M) continue;
+      if (S == 1) {
+        float o[4] = {acc[r][t][0], acc[r][t][1], acc[r][t][2], acc[r][t][3]};
+        if (bias) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] += bf2f(bias[n + e]);
+        }
+        *reinterpret_cast<uint2*>(out + (long)m * N + n) =
+            make_uint2((unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16),
+                       (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16));
+      } else {
+        *reinterpret_cast<float4*>(ws + ((long)blockIdx.y * M + m) * N + n) =
+            make_float4(acc[r][t][0], acc[r][t][1], acc[r][t][2], acc[r][t][3]);
+      }
+    }
+  }
+}
+
 // out[m, n] = (sum_s ws[s, m, n]) * cscale[n] + bias[n]   (bf16 out / bias)
 __global__ __launch_bounds__(256) void wo_reduce_kernel(const float* __restrict__ ws, int S, int M, int N,
                                                         const float* __restrict__ cscale,
@@ -528,6 +658,61 @@ extern "C" int pd_dec64_gemm(const void* X, const void* W, const void* bias, voi
   }
 #undef PD_D64_RT
 #undef PD_D64
+  return (int)hipGetLastError();
+}
+
+// The LDS-X decode GEMM (dec64s_kernel) for 16 < M <= 64: N % (64 rt) == 0, K % 64 == 0, 16-B aligned rows.
+// cfg = (dw, rt, S): dw LDS ring slots (rt 1: 8 / 16, rt 2: 8 / 11); 0 fields = auto (pd_dec64s_cfg).
+// ws: S * M * N floats when S > 1 (fp32 partials summed by wo_reduce_kernel).  Returns -1 outside the domain.
+extern "C" void pd_dec64s_cfg(int M, int N, int K, int* dw, int* rt, int* S) {
+  // ~24 MiB of weight bytes in flight chip-wide (HBM latency x bandwidth) from S x N x (DW - 1) x 128 B, and
+  // enough workgroups to reach most CUs
+  if (*rt == 0) *rt = (N % 128 == 0 && N >= 16384) ? 2 : 1;
+  if (*dw == 0) *dw = *rt == 1 ? 16 : 11;   // the vmcnt immediate caps (DW - 2) x (2 + 2 RT) at 63
+  if (*S == 0) {
+    const long per = (long)N * (*dw - 1) * 128;
+    int s = (int)((24L << 20) / per);
+    const int wgs = N / (64 * *rt);
+    while (s > 1 && wgs * s > 512) --s;
+    if (s < 1) s = 1;
+    if (s > K / 64) s = K / 64;
+    *S = s;
+  }
+}
+
+extern "C" long pd_dec64s_workspace(int M, int N, int K, int dw, int rt, int S) {
+  pd_dec64s_cfg(M, N, K, &dw, &rt, &S);
+  return S > 1 ? (long)S * M * N : 0;
+}
+
+extern "C" int pd_dec64s_gemm(const void* X, const void* W, const void* bias, void* out, float* ws, int M, int N,
+                              int K, int dw, int rt, int S, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  pd_dec64s_cfg(M, N, K, &dw, &rt, &S);
+  if (M < 1 || M > 64 || K % 64 || (size_t)X % 16 || (size_t)W % 16) return -1;
+  const bool dw_ok = rt == 1 ? (dw == 8 || dw == 16) : (dw == 8 || dw == 11);
+  if ((rt != 1 && rt != 2) || !dw_ok || N % (64 * rt) || S < 1 || S > K / 64) return -1;
+  if (S > 1 && ws == nullptr) return -1;
+  if ((long)N * K * 2 >= 0x7fffff00L || (long)M * K * 2 >= 0x7fffff00L) return -1;
+  const dim3 grid(N / (64 * rt), S);
+#define PD_D64S(MT_, RT_, DW_)                                                                                  \
+  dec64s_kernel<MT_, 4, RT_, DW_><<<grid, 256, 0, st>>>((const unsigned short*)X, (const unsigned short*)W,     \
+                                                       (const unsigned short*)bias, (unsigned short*)out, ws, M, \
+                                                       N, K)
+#define PD_D64S_RT(MT_)                                   \
+  if (rt == 1) {                                          \
+    if (dw == 8) PD_D64S(MT_, 1, 8); else PD_D64S(MT_, 1, 16); \
+  } else {                                                \
+    if (dw == 8) PD_D64S(MT_, 2, 8); else PD_D64S(MT_, 2, 11); \
+  }
+  if (M <= 32) { PD_D64S_RT(2) } else { PD_D64S_RT(4) }
+#undef PD_D64S_RT
+#undef PD_D64S
+  if (S > 1) {
+    const long total = (long)M * N;
+    wo_reduce_kernel<<<(int)((total / 4 + 255) / 256), 256, 0, st>>>(ws, S, M, N, nullptr,
+                                                                   (const unsigned short*)bias, (unsigned short*)out);
+  }
   return (int)hipGetLastError();
 }
 

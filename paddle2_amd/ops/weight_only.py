@@ -68,14 +68,20 @@ import os as _os  # noqa: E402
 DECODE_GEMM = _os.environ.get("PADDLE2_AMD_DECODE_GEMM", "auto")   # auto | native | blas
 DEC64_WAVES = int(_os.environ.get("PADDLE2_AMD_DEC64_WAVES", "8"))  # waves per workgroup of the M > 16 kernel
 DEC64_RT = int(_os.environ.get("PADDLE2_AMD_DEC64_RT", "0"))        # its channel tiles per workgroup (0 = auto)
+# M > 16 kernel: "r" = dec64_kernel (X prefetched in registers), "s" = dec64s_kernel (X through an LDS ring, waves
+# split the channels; cfg "dw,rt,S" with 0 = auto), "auto" = r for M <= 32, s above (measured per M:
+# profiles/r5_decode_serving.md)
+DEC64_IMPL = _os.environ.get("PADDLE2_AMD_DEC64_IMPL", "auto")
+DEC64S_CFG = tuple(int(v) for v in _os.environ.get("PADDLE2_AMD_DEC64S_CFG", "0,0,0").split(","))
 
 
 def decode_ok(x, wt):
     """The native stream kernel is taken where it measured faster than hipBLASLt's skinny GEMM
     (profiles/r4_decode_gemm.md): M <= 16 with N <= 8192 (the o / down projections: 2.6-4.0 vs 1.9-3.4 TB/s).
-    16 < M <= 64 has the whole-K stream kernel (dec64_kernel: no split-K partials through HBM), which beats the
-    library only on the square 4096 x 4096 projection at M <= 32 (profiles/r5_decode_serving.md: 2.1 vs 1.8 TB/s;
-    1.5-2.8 vs 2.7-4.4 TB/s on the wide ones), so auto routes only that shape to it.
+    16 < M <= 64 has the whole-K stream kernels (dec64_kernel up to M = 32, the LDS-X dec64s_kernel above), which
+    beat the library only on the square 4096 x 4096 projection (profiles/r5_decode_serving.md: 2.2 vs 1.8 TB/s at
+    M <= 32, 1.86-1.89 vs 1.83-1.84 above; 2.5-3.7 vs 4.0-4.3 TB/s on the wide ones), so auto routes only that
+    shape to them.
     PADDLE2_AMD_DECODE_GEMM=native forces the native kernels for every M <= 64, =blas the library."""
     M, K = x.shape
     Nn = wt.shape[0]
@@ -86,7 +92,7 @@ def decode_ok(x, wt):
     if DECODE_GEMM == "blas":
         return False
     if M > 16:   # the whole-K MFMA stream kernel (dec64_kernel): the b17-64 serving step
-        return Nn % 16 == 0 and (DECODE_GEMM == "native" or (M <= 32 and Nn <= 4096 and K <= 4096))
+        return Nn % 16 == 0 and (DECODE_GEMM == "native" or (Nn <= 4096 and K <= 4096))
     return Nn % 64 == 0 and (DECODE_GEMM == "native" or Nn <= 8192)   # the split-K kernel: 64-row blocks
 
 
@@ -104,6 +110,14 @@ def decode_matmul(x, wt, bias=None):
         out = torch.empty(M, Nn, dtype=x.dtype, device=x.device)
         if bias is not None:
             bias = bias.to(torch.bfloat16).contiguous()
+        impl = DEC64_IMPL if DEC64_IMPL != "auto" else ("r" if M <= 32 else "s")
+        if impl == "s" and Nn % 64 == 0:
+            dw, rt, S = DEC64S_CFG
+            n_ws = C.dec64s_workspace(M, Nn, K, dw, rt, S)
+            ws = torch.empty(max(n_ws, 1), dtype=torch.float32, device=x.device)
+            C.dec64s_gemm(x.data_ptr(), wt.data_ptr(), N.ptr(bias), out.data_ptr(), ws.data_ptr(), M, Nn, K, dw, rt,
+                          S, N.stream())
+            return out
         C.dec64_gemm(x.data_ptr(), wt.data_ptr(), N.ptr(bias), out.data_ptr(), M, Nn, K, DEC64_WAVES, DEC64_RT,
                      N.stream())
         return out

@@ -41,6 +41,16 @@ for M in (24, 32, 48, 64):
             rec[f"dec64_rt{rt}_us"] = round(t * 1e3, 1)
             rec[f"dec64_rt{rt}_TBs"] = round(wb / t / 1e9, 2)
         WO.DEC64_RT = 0
+        WO.DEC64_IMPL = "s"
+        for cfg in ((0, 0, 0), (16, 1, 1), (16, 1, 2), (8, 1, 2), (11, 2, 1), (8, 2, 2)):
+            dw, rt, S = cfg
+            if rt and Nn % (64 * rt):
+                continue
+            WO.DEC64S_CFG = cfg
+            t = bench(lambda w: WO.decode_matmul(x, w), copies)
+            key = "s_auto" if cfg == (0, 0, 0) else f"s{dw}_{rt}_{S}"
+            rec[f"{key}_TBs"] = round(wb / t / 1e9, 2)
+        WO.DEC64_IMPL = "r"
         t = bench(lambda w: torch.matmul(x, w.t()), copies)
         rec["blas_us"], rec["blas_TBs"] = round(t * 1e3, 1), round(wb / t / 1e9, 2)
         y = WO.decode_matmul(x, copies[0])

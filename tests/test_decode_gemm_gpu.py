@@ -41,6 +41,7 @@ def test_dec64_whole_k_kernel(M, N, K, waves, rt, monkeypatch):
     monkeypatch.setattr(WO, "DECODE_GEMM", "native")
     monkeypatch.setattr(WO, "DEC64_WAVES", waves)
     monkeypatch.setattr(WO, "DEC64_RT", rt)
+    monkeypatch.setattr(WO, "DEC64_IMPL", "r")
     g = torch.Generator(device=dev).manual_seed(7 * M + N)
     x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
     wt = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)
@@ -54,7 +55,7 @@ def test_dec64_whole_k_kernel(M, N, K, waves, rt, monkeypatch):
 
 
 def test_auto_routing(monkeypatch):
-    """auto: native split-K at M <= 16 on N <= 8192, dec64 only on the 4096 x 4096 projection at M <= 32,
+    """auto: native split-K at M <= 16 on N <= 8192, the M > 16 kernels only on the 4096 x 4096 projection,
     hipBLASLt elsewhere (profiles/r4_decode_gemm.md, profiles/r5_decode_serving.md)."""
     monkeypatch.setattr(WO, "DECODE_GEMM", "auto")
 
@@ -63,4 +64,27 @@ def test_auto_routing(monkeypatch):
                             torch.empty(N, K, device=dev, dtype=torch.bfloat16))
 
     assert ok(1, 4096, 4096) and ok(16, 4096, 11008) and not ok(1, 12288, 4096)
-    assert ok(32, 4096, 4096) and not ok(64, 4096, 4096) and not ok(32, 4096, 11008) and not ok(32, 12288, 4096)
+    assert ok(32, 4096, 4096) and ok(64, 4096, 4096) and not ok(32, 4096, 11008) and not ok(64, 12288, 4096)
+
+
+@pytest.mark.parametrize("cfg", [(0, 0, 0), (8, 1, 1), (16, 1, 3), (8, 2, 1), (11, 2, 2)])
+@pytest.mark.parametrize("M", [17, 40, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 11008), (12288, 4096), (192, 128), (256, 320)])
+def test_dec64s_lds_x_kernel(M, N, K, cfg, monkeypatch):
+    """The LDS-X M > 16 kernel (dec64s_kernel): ring depths 8 / 11 / 16, one or two channel tiles per wave, split-K
+    1-3 (fp32 partials + reduce), auto; ragged M, tiny K with fewer steps than the ring, K not a multiple of S."""
+    dw, rt, S = cfg
+    if (rt and N % (64 * rt)) or S > K // 64:
+        pytest.skip("outside this configuration's domain")
+    monkeypatch.setattr(WO, "DECODE_GEMM", "native")
+    monkeypatch.setattr(WO, "DEC64_IMPL", "s")
+    monkeypatch.setattr(WO, "DEC64S_CFG", cfg)
+    g = torch.Generator(device=dev).manual_seed(11 * M + N + K)
+    x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    wt = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=dev, generator=g).to(torch.bfloat16)
+    y = WO.decode_matmul(x, wt, b)
+    ref = x.float() @ wt.float().t() + b.float()
+    assert y.shape == (M, N) and _rel(y, ref) < 8e-3
+    y2 = WO.decode_matmul(x, wt)
+    assert _rel(y2, x.float() @ wt.float().t()) < 8e-3
