@@ -7,6 +7,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <tuple>
+#include <vector>
+
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -63,8 +66,10 @@ int pd_ce_bwd(int, const void*, const int64_t*, const float*, const float*, void
 int pd_embed_fwd(int, const int64_t*, const void*, void*, long, int, long, long, void*);
 int pd_embed_bwd(int, const int64_t*, const void*, float*, long, int, long, long, long, void*);
 int pd_cast_from_f32(int, const float*, void*, long, void*);
-int pd_fp8_cast(int, int, const void*, void*, void*, long, long, const float*, float*, void*);
-int pd_fp8_update_scale(float*, int, float*, float*, float*, float, float, void*);
+int pd_fp8_cast(int, int, const void*, void*, void*, long, long, const float*, float*, float*, void*);
+int pd_colsum(int, const float*, void*, int, int, void*);
+int pd_fp8_update_scale(int, float* const*, const int*, float* const*, float* const*, float* const*, float* const*,
+                        const float*, const float*, void*);
 int pd_decode_attn(const void*, long, long, const void*, const void*, long, long, long, const int*, int, int,
                    const int*, int, float*, float*, void*, long, long, int, int, int, int, int, float, int, void*);
 int pd_cache_write(const void*, const void*, long, long, void*, void*, long, long, long, const int*, int, int,
@@ -296,15 +301,39 @@ PYBIND11_MODULE(_C, m) {
           "embed_bwd");
   });
   m.def("fp8_cast", [](int dt, int e5m2, uintptr_t x, uintptr_t y, uintptr_t yT, long R, long C, uintptr_t scale,
-                       uintptr_t amax, uintptr_t st) {
-    check(pd_fp8_cast(dt, e5m2, P<const void*>(x), P<void*>(y), P<void*>(yT), R, C, P<const float*>(scale),
-                      P<float*>(amax), P<void*>(st)),
-          "fp8_cast");
+                       uintptr_t amax, uintptr_t st, uintptr_t colpart) {
+    // colpart requested on a path without it: returns False (nothing launched) so the caller sums dY itself
+    const int rc = pd_fp8_cast(dt, e5m2, P<const void*>(x), P<void*>(y), P<void*>(yT), R, C, P<const float*>(scale),
+                               P<float*>(amax), P<float*>(colpart), P<void*>(st));
+    if (rc == -5) return false;
+    check(rc, "fp8_cast");
+    return true;
+  }, py::arg("dt"), py::arg("e5m2"), py::arg("x"), py::arg("y"), py::arg("yT"), py::arg("R"), py::arg("C"),
+     py::arg("scale"), py::arg("amax"), py::arg("st"), py::arg("colpart") = 0);
+  m.def("colsum", [](int odt, uintptr_t part, uintptr_t db, int Pn, int N, uintptr_t st) {
+    check(pd_colsum(odt, P<const float*>(part), P<void*>(db), Pn, N, P<void*>(st)), "colsum");
   });
-  m.def("fp8_update_scale", [](uintptr_t hist, int len, uintptr_t amax, uintptr_t scale, uintptr_t inv,
-                               float fp8_max, float margin, uintptr_t st) {
-    check(pd_fp8_update_scale(P<float*>(hist), len, P<float*>(amax), P<float*>(scale), P<float*>(inv), fp8_max,
-                              margin, P<void*>(st)),
+  // roles: [(hist, len, amax, scale, inv, snap (0 = none), fp8_max, margin_pow2)], up to 4 in one launch
+  m.def("fp8_update_scale", [](const std::vector<std::tuple<uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
+                                                            float, float>>& roles,
+                               uintptr_t st) {
+    const int n = (int)roles.size();
+    std::vector<float*> hist(n), amax(n), scale(n), inv(n), snap(n);
+    std::vector<int> len(n);
+    std::vector<float> fmax(n), mp2(n);
+    for (int i = 0; i < n; ++i) {
+      const auto& r = roles[i];
+      hist[i] = P<float*>(std::get<0>(r));
+      len[i] = std::get<1>(r);
+      amax[i] = P<float*>(std::get<2>(r));
+      scale[i] = P<float*>(std::get<3>(r));
+      inv[i] = P<float*>(std::get<4>(r));
+      snap[i] = P<float*>(std::get<5>(r));
+      fmax[i] = std::get<6>(r);
+      mp2[i] = std::get<7>(r);
+    }
+    check(pd_fp8_update_scale(n, hist.data(), len.data(), amax.data(), scale.data(), inv.data(), snap.data(),
+                              fmax.data(), mp2.data(), P<void*>(st)),
           "fp8_update_scale");
   });
   m.def("decode_attn", [](uintptr_t q, long sq_b, long sq_h, uintptr_t kc, uintptr_t vc, long s_blk, long s_tok,

@@ -71,11 +71,14 @@ __device__ __forceinline__ void tr4x4(unsigned a, unsigned b, unsigned c, unsign
 // (lane: rb = lane & 7, cb = lane >> 3 -> the 8 lanes of a row block read one 128-B row segment, the 8 lanes of a
 // column write one 64-B yT segment); a workgroup 64 rows x 256 columns.  Replaces the 64 x 64 fp32 LDS-tile kernel
 // (two barriers per tile, 4-B stores; ~57 us per [4096, 5120] cast in the GPT-3 13B fp8 step).
+// colpart (optional, the fp8 linear's dY cast): the unscaled column sums of each 64-row block, fp32 [ceil(R/64), C],
+// for the bias gradient (colsum_kernel folds the row blocks) — the bias-grad pass no longer re-reads dY.
 template <bool E5M2>
 __global__ __launch_bounds__(256) void cast_transpose_amax_v2_kernel(const unsigned short* __restrict__ x,
                                                                      uint8_t* __restrict__ y, uint8_t* __restrict__ yT,
                                                                      int R, int C, const float* __restrict__ scale,
-                                                                     float* __restrict__ amax) {
+                                                                     float* __restrict__ amax,
+                                                                     float* __restrict__ colpart) {
   const float s = scale[0];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int rb = lane & 7, cb = lane >> 3;
@@ -83,6 +86,7 @@ __global__ __launch_bounds__(256) void cast_transpose_amax_v2_kernel(const unsig
   const int r = (blockIdx.x / tilesC) * 64 + 8 * rb;
   const int c = (blockIdx.x % tilesC) * 256 + wave * 64 + 8 * cb;
   float m = 0.f;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (r < R && c < C) {
     unsigned lo[8], hi[8];
 #pragma unroll
@@ -91,6 +95,10 @@ __global__ __launch_bounds__(256) void cast_transpose_amax_v2_kernel(const unsig
       load_vec<bf16, 8>(reinterpret_cast<const bf16*>(x) + (long)(r + i) * C + c, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
+      if (colpart) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cs[j] += v[j];
+      }
       lo[i] = pack4<E5M2>(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
       hi[i] = pack4<E5M2>(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
     }
@@ -107,6 +115,20 @@ __global__ __launch_bounds__(256) void cast_transpose_amax_v2_kernel(const unsig
     for (int j = 0; j < 4; ++j) {
       *reinterpret_cast<uint2*>(yT + (long)(c + j) * R + r) = make_uint2(t0[j], t1[j]);
       *reinterpret_cast<uint2*>(yT + (long)(c + 4 + j) * R + r) = make_uint2(t2[j], t3[j]);
+    }
+  }
+  if (colpart) {
+    // the 8 lanes of a column block (rb = 0..7: consecutive lanes) hold 8 rows each: fold them, lane rb = 0 stores
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      cs[j] += __shfl_xor(cs[j], 1);
+      cs[j] += __shfl_xor(cs[j], 2);
+      cs[j] += __shfl_xor(cs[j], 4);
+    }
+    if (rb == 0 && c < C) {
+      float* dst = colpart + (long)(blockIdx.x / tilesC) * C + c;
+      *reinterpret_cast<float4*>(dst) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
     }
   }
   block_amax(m, amax);
@@ -232,11 +254,27 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-__global__ __launch_bounds__(64) void update_scale_kernel(float* __restrict__ hist, int len, float* __restrict__ amax,
-                                                          float* __restrict__ scale, float* __restrict__ inv_scale,
-                                                          float fp8_max, float margin_pow2) {
+// up to kMaxMetas tensor roles in one launch (workgroup b = role b), e.g. the forward's x and W metas: the
+// dequant factor each cast used is snapshotted into snap[b] (nullable) before the roll — the backward's copy, in
+// the same launch instead of a separate 4-byte device copy per role (320 copyBuffer launches per GPT-3 13B step)
+constexpr int kMaxMetas = 4;
+struct UpdArgs {
+  float* hist[kMaxMetas];
+  float* amax[kMaxMetas];
+  float* scale[kMaxMetas];
+  float* inv[kMaxMetas];
+  float* snap[kMaxMetas];
+  int len[kMaxMetas];
+  float fp8_max[kMaxMetas];
+  float margin_pow2[kMaxMetas];
+};
+
+__global__ __launch_bounds__(64) void update_scale_kernel(UpdArgs u) {
   static_assert(kAmaxSlots == 64, "one amax slot per lane");
-  const int i = threadIdx.x;
+  const int b = blockIdx.x, i = threadIdx.x;
+  float* __restrict__ hist = u.hist[b];
+  float* __restrict__ amax = u.amax[b];
+  const int len = u.len[b];
   const float a = wave_max(amax[i]);
   float m;
   if (len <= 64) {
@@ -254,10 +292,11 @@ __global__ __launch_bounds__(64) void update_scale_kernel(float* __restrict__ hi
   }
   amax[i] = 0.f;
   if (i == 0) {
-    float s = scale[0];
-    if (m > 0.f && isfinite(m)) s = fp8_max / m / margin_pow2;
-    scale[0] = s;
-    inv_scale[0] = 1.f / s;
+    if (u.snap[b]) u.snap[b][0] = u.inv[b][0];
+    float s = u.scale[b][0];
+    if (m > 0.f && isfinite(m)) s = u.fp8_max[b] / m / u.margin_pow2[b];
+    u.scale[b][0] = s;
+    u.inv[b][0] = 1.f / s;
   }
 }
 
@@ -266,9 +305,14 @@ __global__ __launch_bounds__(64) void update_scale_kernel(float* __restrict__ hi
 
 using namespace pd;
 
+// colpart: optional fp32 [ceil(R / 64), C] column sums of x per 64-row block (bf16 x with a transposed copy only:
+// the LDS-free v2 path); -5 when requested on another path (the caller then sums the columns itself).
 extern "C" int pd_fp8_cast(int dt, int e5m2, const void* x, void* y, void* yT, long R, long C, const float* scale,
-                           float* amax, void* stream) {
+                           float* amax, float* colpart, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  const bool v2 = yT != nullptr && dt == kBF16 && C % 8 == 0 && R % 8 == 0 && (size_t)x % 16 == 0 &&
+                  (size_t)yT % 8 == 0 && (!y || (size_t)y % 8 == 0) && R * C < (1L << 31);
+  if (colpart && (!v2 || (size_t)colpart % 16 != 0)) return -5;
   if (yT == nullptr) {
     const long n = R * C;
     long g = (n / 8 + 255) / 256;
@@ -279,15 +323,14 @@ extern "C" int pd_fp8_cast(int dt, int e5m2, const void* x, void* y, void* yT, l
                                                                                amax))
     if (e5m2) { PD_FP8_CAST(true); } else { PD_FP8_CAST(false); }
 #undef PD_FP8_CAST
-  } else if (dt == kBF16 && C % 8 == 0 && R % 8 == 0 && (size_t)x % 16 == 0 && (size_t)yT % 8 == 0 &&
-             (!y || (size_t)y % 8 == 0) && R * C < (1L << 31)) {
+  } else if (v2) {
     const long wgs = ((C + 255) / 256) * ((R + 63) / 64);
     if (e5m2)
       fp8::cast_transpose_amax_v2_kernel<true><<<(unsigned)wgs, 256, 0, st>>>(
-          (const unsigned short*)x, (uint8_t*)y, (uint8_t*)yT, (int)R, (int)C, scale, amax);
+          (const unsigned short*)x, (uint8_t*)y, (uint8_t*)yT, (int)R, (int)C, scale, amax, colpart);
     else
       fp8::cast_transpose_amax_v2_kernel<false><<<(unsigned)wgs, 256, 0, st>>>(
-          (const unsigned short*)x, (uint8_t*)y, (uint8_t*)yT, (int)R, (int)C, scale, amax);
+          (const unsigned short*)x, (uint8_t*)y, (uint8_t*)yT, (int)R, (int)C, scale, amax, colpart);
   } else {
     long tiles = ((C + 63) / 64) * ((R + 63) / 64);
     dim3 grid((unsigned)(tiles < 1024 ? tiles : 1024));
@@ -300,8 +343,21 @@ extern "C" int pd_fp8_cast(int dt, int e5m2, const void* x, void* y, void* yT, l
   return (int)hipGetLastError();
 }
 
-extern "C" int pd_fp8_update_scale(float* hist, int len, float* amax, float* scale, float* inv_scale, float fp8_max,
-                                   float margin_pow2, void* stream) {
-  fp8::update_scale_kernel<<<1, 64, 0, (hipStream_t)stream>>>(hist, len, amax, scale, inv_scale, fp8_max, margin_pow2);
+extern "C" int pd_fp8_update_scale(int n, float* const* hist, const int* len, float* const* amax, float* const* scale,
+                                   float* const* inv_scale, float* const* snap, const float* fp8_max,
+                                   const float* margin_pow2, void* stream) {
+  if (n < 1 || n > fp8::kMaxMetas) return -1;
+  fp8::UpdArgs u{};
+  for (int b = 0; b < n; ++b) {
+    u.hist[b] = hist[b];
+    u.amax[b] = amax[b];
+    u.scale[b] = scale[b];
+    u.inv[b] = inv_scale[b];
+    u.snap[b] = snap[b];
+    u.len[b] = len[b];
+    u.fp8_max[b] = fp8_max[b];
+    u.margin_pow2[b] = margin_pow2[b];
+  }
+  fp8::update_scale_kernel<<<n, 64, 0, (hipStream_t)stream>>>(u);
   return (int)hipGetLastError();
 }

@@ -334,6 +334,19 @@ extern "C" int pd_bias_grad_chunks(int M, int N) {
   return chunks < 1 ? 1 : chunks;
 }
 
+// db[n] = sum_p part[p, n] (fixed order) -> odt: the second pass of the bias gradient on partial row sums some
+// other kernel produced (the fp8 dY cast's per-64-row-block column sums).
+extern "C" int pd_colsum(int odt, const float* part, void* db, int P, int N, void* stream) {
+  using namespace pd;
+  if (N % 4 != 0 || P <= 0) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 g2(ceil_div(N, 64));
+  if (odt == kBF16) colsum_kernel<bf16><<<g2, 256, 0, st>>>(part, (bf16*)db, P, N);
+  else if (odt == kF16) colsum_kernel<half16><<<g2, 256, 0, st>>>(part, (half16*)db, P, N);
+  else colsum_kernel<float><<<g2, 256, 0, st>>>(part, (float*)db, P, N);
+  return (int)hipGetLastError();
+}
+
 extern "C" int pd_bias_grad(int dt, int odt, const void* dy, float* part, void* db, int M, int N, void* stream) {
   using namespace pd;
   if (N % 8 != 0 || M <= 0) return -1;

@@ -57,13 +57,18 @@ class FP8TensorMeta:
             setattr(self, k, getattr(self, k).to(device))
         return self
 
-    def update(self):
-        """Roll the history, recompute scale = fp8_max / max(history) / 2^margin, reset amax."""
-        if self.amax.device.type == "cuda" and N.use_native(self.amax):
-            N.native().fp8_update_scale(self.history.data_ptr(), self.history.numel(), self.amax.data_ptr(),
-                                        self.scale.data_ptr(), self.inv_scale.data_ptr(), _MAX[self.fmt],
-                                        float(2 ** self.margin), N.stream())
-            return
+    def update(self, snap=None):
+        """Roll the history, recompute scale = fp8_max / max(history) / 2^margin, reset amax.  ``snap``: a 1-float
+        tensor that receives the inverse scale in force BEFORE the update (what this step's cast used)."""
+        update_metas([(self, snap)])
+
+    def _native_role(self, snap):
+        return (self.history.data_ptr(), self.history.numel(), self.amax.data_ptr(), self.scale.data_ptr(),
+                self.inv_scale.data_ptr(), N.ptr(snap), _MAX[self.fmt], float(2 ** self.margin))
+
+    def _update_ref(self, snap=None):
+        if snap is not None:
+            snap.copy_(self.inv_scale.reshape(snap.shape))
         self.history.copy_(torch.roll(self.history, 1))
         self.history[0] = self.amax.max()
         m = self.history.max()
@@ -73,12 +78,28 @@ class FP8TensorMeta:
         self.amax.zero_()
 
 
+_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def update_metas(pairs):
+    """[(meta, snap or None)]: every role's delayed-scaling update — on the GPU in ONE launch (up to 4 roles per
+    launch: the forward's x and W roles together), each snap receiving that role's pre-update inverse scale."""
+    gpu = [p for p in pairs if p[0].amax.device.type == "cuda" and N.use_native(p[0].amax)]
+    for i in range(0, len(gpu), 4):
+        N.native().fp8_update_scale([m._native_role(s) for m, s in gpu[i:i + 4]], N.stream())
+    for m, s in pairs:
+        if not (m.amax.device.type == "cuda" and N.use_native(m.amax)):
+            m._update_ref(s)
+
+
 def _dt_code(t):
-    return {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}[t.dtype]
+    return _CODE[t.dtype]
 
 
-def cast(x2, meta: FP8TensorMeta, transpose=False, keep_rowmajor=True):
-    """x2 [R, C] -> (q [R, C] or None, qT [C, R] or None) in meta.fmt, recording amax into meta."""
+def cast(x2, meta: FP8TensorMeta, transpose=False, keep_rowmajor=True, colsum=False):
+    """x2 [R, C] -> (q [R, C] or None, qT [C, R] or None) in meta.fmt, recording amax into meta.  ``colsum``: also
+    return the unscaled fp32 column sums of every 64-row block ([ceil(R/64), C], summed in the same pass over x2 —
+    the fp8 linear's bias gradient), or None where the kernel path has no such output."""
     R, C = x2.shape
     if not meta.initialized:
         meta.init_from(x2)
@@ -86,13 +107,20 @@ def cast(x2, meta: FP8TensorMeta, transpose=False, keep_rowmajor=True):
         x2 = x2.contiguous()
         q = torch.empty(R, C, dtype=torch.uint8, device=x2.device) if (keep_rowmajor or not transpose) else None
         qT = torch.empty(C, R, dtype=torch.uint8, device=x2.device) if transpose else None
-        N.native().fp8_cast(_dt_code(x2), int(meta.fmt == E5M2), x2.data_ptr(), N.ptr(q), N.ptr(qT), R, C,
-                            meta.scale.data_ptr(), meta.amax.data_ptr(), N.stream())
-        return (None if q is None else q.view(meta.fmt)), (None if qT is None else qT.view(meta.fmt))
+        part = torch.empty((R + 63) // 64, C, dtype=torch.float32, device=x2.device) if colsum else None
+        done = N.native().fp8_cast(_dt_code(x2), int(meta.fmt == E5M2), x2.data_ptr(), N.ptr(q), N.ptr(qT), R, C,
+                                   meta.scale.data_ptr(), meta.amax.data_ptr(), N.stream(), N.ptr(part))
+        if not done:   # no fused column sums on this path: plain cast
+            part = None
+            N.native().fp8_cast(_dt_code(x2), int(meta.fmt == E5M2), x2.data_ptr(), N.ptr(q), N.ptr(qT), R, C,
+                                meta.scale.data_ptr(), meta.amax.data_ptr(), N.stream())
+        out = (None if q is None else q.view(meta.fmt)), (None if qT is None else qT.view(meta.fmt))
+        return (*out, part) if colsum else out
     xf = x2.float()
     meta.amax[:1].copy_(torch.maximum(meta.amax[:1], xf.abs().max().reshape(1)))
     q = (xf * meta.scale).clamp(-_MAX[meta.fmt], _MAX[meta.fmt]).to(meta.fmt)
-    return (q if (keep_rowmajor or not transpose) else None), (q.t().contiguous() if transpose else None)
+    out = (q if (keep_rowmajor or not transpose) else None), (q.t().contiguous() if transpose else None)
+    return (*out, None) if colsum else out
 
 
 # "auto" (default): per (formats, M, N, K) the faster of the native kernel and hipBLASLt, timed on device events the
@@ -223,10 +251,10 @@ class _FP8LinearFn(torch.autograd.Function):
         out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) else torch.float32
         y = _mm(xq, wqT.t(), mx.inv_scale, mw.inv_scale, out_dtype,
                 None if bias is None else bias.to(out_dtype))
-        # dequant factors of THIS step's casts (update() below rolls the scales in place)
-        ctx.save_for_backward(xqT, wq, mx.inv_scale.clone(), mw.inv_scale.clone())
-        mx.update()
-        mw.update()
+        # dequant factors of THIS step's casts, snapshotted by the (single) update launch that rolls both scales
+        snap = torch.empty(2, dtype=torch.float32, device=mx.inv_scale.device)
+        update_metas([(mx, snap[0:1]), (mw, snap[1:2])])
+        ctx.save_for_backward(xqT, wq, snap[0:1], snap[1:2])
         ctx.meta = (mg, x.shape, bias is not None, out_dtype, w.dtype)
         ctx.gt = getattr(w, "_p2_gt", None) if WGRAD_MAIN and w.is_cuda else None
         return y.reshape(*x.shape[:-1], N_)
@@ -237,7 +265,11 @@ class _FP8LinearFn(torch.autograd.Function):
         mg, xshape, has_b, out_dtype, wdt = ctx.meta
         N_ = dy.shape[-1]
         dy2 = dy.reshape(-1, N_)
-        gq, gqT = cast(dy2, mg, transpose=True)                  # dY [M, N] and dY^T [N, M]
+        # dY [M, N], dY^T [N, M] and, with a bias, dY's column sums per 64-row block from the same pass
+        if has_b:
+            gq, gqT, dpart = cast(dy2, mg, transpose=True, colsum=True)
+        else:
+            (gq, gqT), dpart = cast(dy2, mg, transpose=True), None
         dx = _mm(gq, wq.t(), mg.inv_scale, inv_w, out_dtype)     # [M, N] @ [N, K]
         if ctx.gt is not None and ctx.needs_input_grad[1] and _wgrad_into_main(ctx.gt, xqT, gqT, inv_x, mg.inv_scale):
             dw = None
@@ -245,7 +277,11 @@ class _FP8LinearFn(torch.autograd.Function):
             dw = _mm(xqT, gqT.t(), inv_x, mg.inv_scale,
                      wdt if wdt in (torch.bfloat16, torch.float16) else torch.float32).to(wdt)
         db = None
-        if has_b:
+        if has_b and dpart is not None and wdt in _CODE:
+            # the cast's per-block column sums folded in a fixed order (no second read of dY)
+            db = torch.empty(N_, dtype=wdt, device=dy2.device)
+            N.native().colsum(_CODE[wdt], dpart.data_ptr(), db.data_ptr(), dpart.shape[0], N_, N.stream())
+        elif has_b:
             # the native two-pass column sum (torch_ops.bias_grad): ATen's bf16 dim-0 reduce took 24.5 ms / 160
             # calls of the GPT-3 13B fp8 step (profiles/r4_gpt13b_fp8_step_kernels.txt)
             from .torch_ops import bias_grad

@@ -38,6 +38,47 @@ def test_fp8_delayed_scaling_update():
     assert float(m.amax.abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("shape", [(64, 128), (136, 264), (1000, 24), (4096, 5120)])
+def test_fp8_cast_fused_column_sums(shape):
+    """cast(..., colsum=True): the dY cast also returns per-64-row-block column sums (the fp8 linear's bias
+    gradient without a second read of dY); the casts are unchanged, and the folded sums match fp32 (incl. R % 64)."""
+    from paddle2_amd.ops import _native as N
+    from paddle2_amd.ops import fp8
+
+    R, C = shape
+    x = torch.randn(shape, device=DEV, dtype=torch.bfloat16) * 3
+    meta = fp8.FP8TensorMeta(torch.float8_e5m2, device=torch.device(DEV))
+    meta.scale.fill_(5.0)
+    meta.initialized = True
+    q, qT, part = fp8.cast(x, meta, transpose=True, colsum=True)
+    ref = (x.float() * 5.0).clamp(-57344.0, 57344.0).to(torch.float8_e5m2)
+    assert torch.equal(q.view(torch.uint8), ref.view(torch.uint8))
+    assert torch.equal(qT.view(torch.uint8), ref.t().contiguous().view(torch.uint8))
+    assert part is not None and part.shape == ((R + 63) // 64, C)
+    blocks = torch.nn.functional.pad(x.float(), (0, 0, 0, part.shape[0] * 64 - R)).reshape(-1, 64, C).sum(1)
+    torch.testing.assert_close(part, blocks, rtol=1e-5, atol=1e-3)
+    db = torch.empty(C, dtype=torch.float32, device=DEV)
+    N.native().colsum(0, part.data_ptr(), db.data_ptr(), part.shape[0], C, N.stream())
+    torch.testing.assert_close(db, x.float().sum(0), rtol=1e-5, atol=1e-2)
+
+
+def test_fp8_linear_bias_grad_from_fused_sums():
+    """The fp8 linear's bias gradient (from the dY cast's column sums) equals dY summed over tokens in fp32."""
+    import paddle2_amd as paddle
+    from paddle2_amd.incubate.fp8 import Float8Linear
+
+    paddle.set_device("gpu:0")
+    paddle.seed(1)
+    lin = Float8Linear(256, 512)
+    lin.to(dtype="bfloat16")
+    x = paddle.randn([3, 48, 256]).astype("bfloat16")   # 144 tokens: a partial 64-row block
+    y = lin(x)
+    g = torch.randn(y.shape, device=DEV, dtype=torch.bfloat16)
+    y._t.backward(g)
+    db = lin.bias.grad._t.float()
+    torch.testing.assert_close(db, g.float().reshape(-1, 512).sum(0), rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("hlen", [1, 4, 16, 64, 70])
 def test_fp8_update_scale_matches_cpu_recipe(hlen):
     """The one-wave update kernel (slot fold, history roll, history max; serial beyond 64 entries) against the CPU
