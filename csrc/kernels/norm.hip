@@ -137,6 +137,7 @@ __global__ __launch_bounds__(kNormBlock) void norm_bwd_kernel(
     const float r = rstd[row];
     const float mu = LAYERNORM ? mean[row] : 0.f;
     float xh[MAXV][V], g[MAXV][V];
+    float dr[HAS_DRES ? MAXV : 1][V];   // the residual-branch gradient, loaded with dy / x (not after the reduction)
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
@@ -145,6 +146,7 @@ __global__ __launch_bounds__(kNormBlock) void norm_bwd_kernel(
         float dyv[V];
         load_vec<T, V>(dy + off + vi * V, dyv);
         load_vec<T, V>(x + off + vi * V, xh[k]);
+        if constexpr (HAS_DRES) load_vec<T, V>(dres + off + vi * V, dr[k]);
 #pragma unroll
         for (int j = 0; j < V; ++j) {
           xh[k][j] = (xh[k][j] - mu) * r;
@@ -173,10 +175,8 @@ __global__ __launch_bounds__(kNormBlock) void norm_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < V; ++j) o[j] = r * (g[k][j] - xh[k][j] * s1 - (LAYERNORM ? s2 : 0.f));
         if constexpr (HAS_DRES) {
-          float d2[V];
-          load_vec<T, V>(dres + off + vi * V, d2);
 #pragma unroll
-          for (int j = 0; j < V; ++j) o[j] += d2[j];
+          for (int j = 0; j < V; ++j) o[j] += dr[k][j];
         }
         store_vec<T, V>(dx + off + vi * V, o);
       }
@@ -391,8 +391,10 @@ extern "C" int pd_norm_fwd(int layernorm, int dt, int wdt, const void* x, const 
   return (int)hipGetLastError();
 }
 
-// Number of blocks the backward uses; caller allocates partials of nblocks x N floats.
-extern "C" int pd_norm_bwd_blocks(int M) { return M < 512 ? M : 512; }
+// Number of blocks the backward uses; caller allocates partials of nblocks x N floats.  Each block keeps ONE row in
+// flight (load -> block reduction -> store), so the rows in flight per CU set the bandwidth: 1024 blocks (4 per CU)
+// instead of 512 (the Llama-2-7B step's [32768, 4096] backward ran latency-bound at 4.7 TB/s with 2 per CU).
+extern "C" int pd_norm_bwd_blocks(int M) { return M < 1024 ? M : 1024; }
 
 extern "C" int pd_norm_bwd(int layernorm, int dt, int wdt, const void* dy, const void* x, const void* w,
                            const float* mean, const float* rstd, const void* dres, void* dx, float* dw_part,
