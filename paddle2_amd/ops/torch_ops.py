@@ -682,6 +682,11 @@ def gelu_mlp(x, w1, b1, w2, b2, approximate=True):
     return linear(torch.nn.functional.gelu(t, approximate="tanh" if approximate else "none"), w2, b2)
 
 
+# The gate|up forward: "fused" = the GEMM's SwiGLU epilogue writes gu AND a (one kernel); "split" = the plain GEMM
+# writes gu and the memory-bound SwiGLU kernel reads it back for a (measured in profiles/r5_swiglu_fwd.md)
+_SWIGLU_FWD = _os.environ.get("PADDLE2_AMD_SWIGLU_FWD", "split")
+
+
 class _SwiGLULinearFn(torch.autograd.Function):
     """a = swiglu(x @ W) for the packed gate|up projection W [K, 2H] (Llama MLP up half), one node:
     forward through W^T (fast hipBLASLt layout); backward's SwiGLU kernel also writes dY^T, so the weight
@@ -695,7 +700,11 @@ class _SwiGLULinearFn(torch.autograd.Function):
         from . import gemm as G
 
         if _pass_native("fwd", x2) and G.supported_fwd(x2, w):
-            a, gu = G.mm_swiglu(x2, w)  # one kernel: GEMM + SwiGLU epilogue (gu kept for the backward)
+            if _SWIGLU_FWD == "split":
+                gu = G.mm_fwd(x2, w)    # plain GEMM (its 16-B bf16 epilogue), then the SwiGLU pass
+                a = swiglu(gu)
+            else:
+                a, gu = G.mm_swiglu(x2, w)  # one kernel: GEMM + SwiGLU epilogue (gu kept for the backward)
         else:
             gu = torch.matmul(x2, transpose2d(w).t())
             a = swiglu(gu)
