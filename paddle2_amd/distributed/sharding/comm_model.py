@@ -5,7 +5,9 @@ Model of this framework's stage 3 (group_sharded.py), not the reference's (group
 reduces every parameter's full gradient and slices it; here ONE reduce-scatter per flat unit moves half of that):
 
   * forward: one all-gather per unit (param dtype), except the root unit (tied / shared parameters) gathered once;
-  * backward: the same all-gathers again, except the last forward unit, kept gathered across the turn;
+  * backward: the same all-gathers again, except the last forward unit, kept gathered across the turn — or none
+    at all with ``keep_gathered`` (every unit stays gathered from its forward to its backward: the MI355X default
+    when the bf16 model is <= 8 % of HBM, group_sharded.GroupShardedModel._keep_gathered_policy);
   * gradients: one reduce-scatter per unit of its flat fp32 gradient (``grad_bytes`` = 4; 2 for a bf16 reduce-
     scatter, which halves the bytes but sums the ranks' partials in bf16);
   * ring algorithms: a rank moves (N-1)/N of each collective's full buffer; time = bytes / bus bandwidth.
@@ -17,7 +19,8 @@ node and pass it in).
 from __future__ import annotations
 
 
-def stage3_bytes_per_step(unit_numels, N, param_bytes=2, grad_bytes=4, root_numel=0, keep_last=True):
+def stage3_bytes_per_step(unit_numels, N, param_bytes=2, grad_bytes=4, root_numel=0, keep_last=True,
+                          keep_gathered=False):
     """-> dict of per-rank bytes per step: ag_fwd, ag_bwd, rs, total (and the per-unit peaks)."""
     if N <= 1:
         return {"ag_fwd": 0, "ag_bwd": 0, "rs": 0, "total": 0, "max_unit_ag": 0, "max_unit_rs": 0}
@@ -27,7 +30,7 @@ def stage3_bytes_per_step(unit_numels, N, param_bytes=2, grad_bytes=4, root_nume
     rs = [p * grad_bytes * f for p in pad]
     root_pad = (-(-root_numel // N)) * N if root_numel else 0
     ag_fwd = sum(ag) + root_pad * param_bytes * f
-    ag_bwd = sum(ag) - (ag[-1] if keep_last and ag else 0)
+    ag_bwd = 0 if keep_gathered else sum(ag) - (ag[-1] if keep_last and ag else 0)
     rs_tot = sum(rs) + root_pad * grad_bytes * f
     return {"ag_fwd": ag_fwd, "ag_bwd": ag_bwd, "rs": rs_tot, "total": ag_fwd + ag_bwd + rs_tot,
             "max_unit_ag": max(ag) if ag else 0, "max_unit_rs": max(rs) if rs else 0}
@@ -48,8 +51,8 @@ def step_comm_time(bytes_per_step, busbw_GBps=350.0):
     return bytes_per_step / (busbw_GBps * 1e9)
 
 
-def llama7b_report(N=8, busbw_GBps=350.0, grad_bytes=4):
+def llama7b_report(N=8, busbw_GBps=350.0, grad_bytes=4, keep_gathered=True):
     units, root = llama_units()
-    b = stage3_bytes_per_step(units, N, grad_bytes=grad_bytes, root_numel=root)
+    b = stage3_bytes_per_step(units, N, grad_bytes=grad_bytes, root_numel=root, keep_gathered=keep_gathered)
     b["seconds"] = step_comm_time(b["total"], busbw_GBps)
     return b

@@ -148,6 +148,7 @@ class _Unit:
         self.model = None
         self.n_trainable = sum(1 for p in self.params if not p.stop_gradient)
         self.bw_gathered = False
+        self.n_gathers = 0   # all-gathers issued (the comm path), for tests and the comm model
         for i, p in enumerate(self.params):
             if not p.stop_gradient and p._t.dim() == 2:
                 p._t._p2_gt = (self, i)  # weight-gradient GEMMs write straight into the fp32 target
@@ -179,6 +180,7 @@ class _Unit:
             self._bind(self.shard)
             return
         buf = torch.empty(self.padded, dtype=self.dtype, device=self.device)
+        self.n_gathers += 1
         self.work = dist.all_gather_into_tensor(buf, self.shard, group=self.group.pg, async_op=async_op)
         self._pending = buf
         if not async_op:
@@ -371,6 +373,7 @@ class GroupShardedModel(Layer):
         self._live_flat = 0
         self.peak_live_flat = 0
         self.prefetch_depth = 2
+        self.keep_gathered = self._keep_gathered_policy()
         for u in self._units:
             if u.layer is not None:
                 self._hooks.append(u.layer.register_forward_pre_hook(self._make_pre(u)))
@@ -379,6 +382,29 @@ class GroupShardedModel(Layer):
             for i, p in enumerate(u.params):
                 if not p.stop_gradient:
                     self._hooks.append(p._t.register_post_accumulate_grad_hook(self._make_grad_hook(u, i)))
+
+    def _keep_gathered_policy(self):
+        """Stage 3 at N > 1 keeps every unit gathered from its forward to its backward (no backward re-gather: one
+        of the step's three collectives per unit) when the whole bf16 model is a small share of HBM — on MI355X
+        the 288 GB card holds Llama-2-7B's 13.5 GB of gathered parameters beside a ~170 GiB per-rank peak at
+        N = 8 (profiles/r5_stage3_force_comm.md).  PADDLE2_AMD_STAGE3_KEEP_GATHERED = auto | 1 | 0."""
+        import os
+
+        mode = os.environ.get("PADDLE2_AMD_STAGE3_KEEP_GATHERED", "auto")
+        if self._stage != 3 or mode == "0":
+            return False
+        comm = [u for u in self._units if u.comm]
+        if not comm:
+            return False
+        if mode == "1":
+            return True
+        if force_comm() or self._group.nranks <= 1:
+            return False   # the 1-GPU rehearsal holds the whole optimizer state: no room for a second copy
+        dev = comm[0].device
+        if dev.type != "cuda":
+            return False
+        full = sum(u.padded * torch.tensor([], dtype=u.dtype).element_size() for u in comm)
+        return full <= 0.08 * torch.cuda.get_device_properties(dev).total_memory
 
     # ------------------------------------------------------------ bounded fp32 grad buffers (N > 1)
     def _acquire_flat(self, unit):
@@ -449,8 +475,9 @@ class GroupShardedModel(Layer):
                         t.register_hook(self._make_bw_pre(u))
                         hooked = True
                 # the last unit of the forward is the first of the backward: keep it gathered across the turn
+                # (every unit, with keep_gathered: the backward then issues no all-gather at all)
                 last = self._order_done and self._order and u.idx == self._order[-1]
-                if hooked and not last:
+                if hooked and not last and not self.keep_gathered:
                     u.release()
             elif self._stage == 3:
                 u.release()

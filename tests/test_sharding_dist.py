@@ -53,6 +53,25 @@ def test_stage3_grad_buffers_bounded_4ranks():
         assert r["pool_bufs"] <= 2 * r["unit_sizes"] < 12, (r["pool_bufs"], r["unit_sizes"])
 
 
+def test_stage3_keep_gathered_skips_backward_gathers():
+    """PADDLE2_AMD_STAGE3_KEEP_GATHERED=1 (the MI355X default when the bf16 model is <= 8 % of HBM): units stay
+    gathered from forward to backward, so the backward issues no all-gather — fewer gathers per step than the
+    re-gathering path, the same losses / parameters as the single-process run."""
+    keep = run_workers("sharding_worker.py", 2, ["p_g_os"],
+                       extra_env={"PD_TEST_LAYERS": "4", "PADDLE2_AMD_STAGE3_KEEP_GATHERED": "1"})
+    regather = run_workers("sharding_worker.py", 2, ["p_g_os"],
+                           extra_env={"PD_TEST_LAYERS": "4", "PADDLE2_AMD_STAGE3_KEEP_GATHERED": "0"})
+    for r in keep + regather:
+        for a, b in zip(r["losses"], r["ref"]):
+            assert abs(a - b) < 1e-3 * max(1.0, abs(b)), (r["losses"], r["ref"])
+        assert abs(r["csum"] - r["csum_ref"]) < 1e-2 * max(1.0, abs(r["csum_ref"]))
+    assert all(r["keep"] for r in keep) and not any(r["keep"] for r in regather)
+    assert keep[0]["losses"] == regather[0]["losses"]
+    # 3 steps x 4 decoder units: the re-gathering path gathers most units twice per step, keep_gathered once
+    assert keep[0]["gathers"] < regather[0]["gathers"], (keep[0]["gathers"], regather[0]["gathers"])
+    assert keep[0]["gathers"] <= 3 * keep[0]["n_units"] + 1
+
+
 def test_stage3_comm_model_llama7b():
     """Bytes per rank per step of stage 3 at N = 8 for Llama-2-7B: all-gathers of the bf16 flat units (forward and
     backward, the last unit kept across the turn) and one fp32 reduce-scatter per unit."""
@@ -69,3 +88,5 @@ def test_stage3_comm_model_llama7b():
     b16 = CM.stage3_bytes_per_step(units, 8, grad_bytes=2, root_numel=root)
     assert abs((b["total"] - b16["total"]) - b["rs"] / 2) < 1e3   # bf16 reduce-scatter saves half the RS bytes
     assert CM.stage3_bytes_per_step(units, 1)["total"] == 0
+    kept = CM.stage3_bytes_per_step(units, 8, root_numel=root, keep_gathered=True)
+    assert kept["ag_bwd"] == 0 and abs((b["total"] - kept["total"]) - b["ag_bwd"]) < 1e3   # ~11 GB less per step

@@ -13,13 +13,14 @@ import pytest
 from _dist import ROOT, pypath
 
 
-def _run(dev, force, acc=1):
+def _run(dev, force, acc=1, keep="auto"):
     out = os.path.join(tempfile.mkdtemp(prefix="pd_fc_"), "r.json")
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "LOCAL_RANK"):
         env.pop(k, None)
     env.update({"PYTHONPATH": pypath(ROOT), "PD_TEST_OUT": out, "PD_TEST_DEVICE": dev, "PD_TEST_ACC": str(acc),
-                "PADDLE2_AMD_STAGE3_FORCE_COMM": "1" if force else "0", "OMP_NUM_THREADS": "2"})
+                "PADDLE2_AMD_STAGE3_FORCE_COMM": "1" if force else "0", "OMP_NUM_THREADS": "2",
+                "PADDLE2_AMD_STAGE3_KEEP_GATHERED": keep})
     if dev == "cpu":
         env.update({"PADDLE2_AMD_DEVICE": "cpu", "PADDLE_DISTRI_BACKEND": "gloo"})
     else:
@@ -65,3 +66,22 @@ def test_force_comm_matches_short_circuit_gpu(acc):
         assert a["losses"] == b["losses"] and a["digest"] == b["digest"], (a, b)
     else:
         assert diff <= max(8 * noise, 5e-3), (a["losses"], a2["losses"], b["losses"])
+
+
+@pytest.mark.gpu
+def test_force_comm_keep_gathered_gpu():
+    """Forced comm with every unit kept gathered from forward to backward (the N > 1 MI355X default): the same
+    training as the N = 1 short-circuit on the GPU comm path."""
+    a, a2, b = _run("cuda", False), _run("cuda", False), _run("cuda", True, keep="1")
+    assert all(b["comm"]) and b["pg"] == "pdrccl"
+    assert a["losses"][0] == b["losses"][0]
+    noise = max(abs(x - y) for x, y in zip(a["losses"], a2["losses"]))
+    if noise == 0.0:
+        assert a["losses"] == b["losses"] and a["digest"] == b["digest"], (a, b)
+    else:
+        assert max(abs(x - y) for x, y in zip(a["losses"], b["losses"])) <= max(8 * noise, 5e-3)
+
+
+def test_force_comm_keep_gathered_cpu():
+    a, b = _run("cpu", False), _run("cpu", True, keep="1")
+    assert all(b["comm"]) and a["losses"] == b["losses"] and a["digest"] == b["digest"]

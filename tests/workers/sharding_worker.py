@@ -48,6 +48,8 @@ for s in range(steps):
 peak_live = getattr(m, "peak_live_flat", None)
 pool_bufs = sum(len(v) for v in getattr(m, "_flat_pool", {}).values())
 sizes = len({u.padded for u in getattr(m, "_units", [])})
+gathers = sum(getattr(u, "n_gathers", 0) for u in getattr(m, "_units", []))
+keep = getattr(m, "keep_gathered", None)
 sd = m.state_dict()
 csum = float(sum(v._t.double().sum() for v in sd.values()))
 
@@ -63,5 +65,6 @@ for s in range(steps):
     ref.append(float(loss))
 csum_ref = float(sum(v._t.double().sum() for v in m2.state_dict().values()))
 write_result({"losses": losses, "ref": ref, "csum": csum, "csum_ref": csum_ref, "peak_live_flat": peak_live,
-              "pool_bufs": pool_bufs, "unit_sizes": sizes})
+              "pool_bufs": pool_bufs, "unit_sizes": sizes, "gathers": gathers, "keep": keep,
+              "n_units": len(getattr(m, "_units", []))})
 C.destroy_process_group()
