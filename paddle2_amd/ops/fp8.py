@@ -143,6 +143,9 @@ def _cus(dev):
     return c
 
 
+# tile-group height of the native fp8 GEMM's tile order (rows of 256 x 256 tiles walked together; 4 by default)
+GROUP_M = int(os.environ.get("PADDLE2_AMD_FP8_GROUP_M", "4"))
+
 # tail split-K (gemm_tn.h: a last partial wave of <= CUs / 2 tiles as K-slices + an fp32 fix-up) on the bf16 GEMM's
 # per-stream workspace; "0" disables
 TAILK = os.environ.get("PADDLE2_AMD_FP8_TAILK", "1") != "0"
@@ -172,8 +175,8 @@ def mm_native(a, bT, inv_a, inv_b, out_dtype, bias=None, out=None, beta=0.0):
     c = torch.empty(M, Nn, dtype=out_dtype, device=a.device) if out is None else out
     rc = N.native().gemm_f8(fa, fb, 0 if out_dtype == torch.bfloat16 else 1, a.data_ptr(), a.stride(0),
                             bT.data_ptr(), bT.stride(0), c.data_ptr(), c.stride(0), N.ptr(bias),
-                            inv_a.data_ptr(), inv_b.data_ptr(), M, Nn, K, float(beta), 4, _cus(a.device), *_ws(a),
-                            N.stream())
+                            inv_a.data_ptr(), inv_b.data_ptr(), M, Nn, K, float(beta), GROUP_M, _cus(a.device),
+                            *_ws(a), N.stream())
     if rc == -1:
         return None
     if rc != 0:
