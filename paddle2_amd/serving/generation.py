@@ -63,6 +63,8 @@ class LlamaGenerator:
         self._tok = torch.zeros(max_batch, dtype=torch.long, device=dev)
         self._pos = torch.zeros(max_batch, dtype=torch.int32, device=dev)
         self._lens = torch.zeros(max_batch, dtype=torch.int32, device=dev)
+        # the KV-cache write's sequence index per decode row: static, so no arange / int32 cast per layer per step
+        self._slots = torch.arange(max_batch, dtype=torch.int32, device=dev)
         self._logits = None
         import os
 
@@ -169,10 +171,12 @@ class LlamaGenerator:
         for li, layer in enumerate(self.model.llama.layers):
             qkv, residual = self._layer_qkv(layer, x, residual)
             qkv = qkv.view(B, 1, nh + 2 * nkv, d)
-            q = T.rope(qkv[:, :, :nh], self.cos, self.sin, pos[:, None], style=0)
-            k = T.rope(qkv[:, :, nh:nh + nkv], self.cos, self.sin, pos[:, None], style=0)
-            write_kv(k[:, 0].contiguous(), qkv[:, 0, nh + nkv:].contiguous(), self.cache.k[li], self.cache.v[li],
-                     torch.arange(B, device=self.dev), self._pos, self.cache.block_table)
+            # q and k are adjacent heads of qkv: one RoPE launch over both
+            qk = T.rope(qkv[:, :, :nh + nkv], self.cos, self.sin, pos[:, None], style=0)
+            q, k = qk[:, :, :nh], qk[:, :, nh:]
+            # k and v stay strided views (the cache write takes row strides): no per-layer copies
+            write_kv(k[:, 0], qkv[:, 0, nh + nkv:], self.cache.k[li], self.cache.v[li],
+                     self._slots[:B], self._pos, self.cache.block_table)
             o = decode_attention(q[:, 0], self.cache.k[li], self.cache.v[li], self._lens, self.cache.block_table)
             x, residual = self._layer_out(layer, o.reshape(B, 1, nh * d), residual)
         return self._logits_of(x, residual)[:, 0]
