@@ -192,7 +192,12 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(const unsigned short* __re
 // bf16 weights (the serving decode GEMM on the cached [N, K] projection weights): the same schedule with each lane
 // streaming 32 contiguous K-bytes of its channel per 64-wide K step (two 16-B loads = the two MFMA fragments), no
 // conversion.  Y[M, N] = X[M, K] . W^T, M <= 64, fp32 split-K partials into ws (summed by wo_reduce_kernel).
-template <int MT, int RT>
+// GLU (the Llama MLP's down projection at decode): X is the gate|up GEMM output gu [M, 2K] and the staged row is
+// silu(gate) * up, rounded to bf16 once like swiglu_fwd_kernel — the SwiGLU pass folds into the X staging (the
+// whole X tile goes through LDS anyway), one launch less per layer.
+__device__ __forceinline__ float dec_sigmoid(float x) { return 1.f / (1.f + __expf(-x)); }   // as swiglu_fwd
+
+template <int MT, int RT, bool GLU = false>
 __global__ __launch_bounds__(256) void dec_gemm_kernel(const unsigned short* __restrict__ X,
                                                        const unsigned short* __restrict__ W, float* __restrict__ ws,
                                                        int M, int N, int K, int kmax) {
@@ -205,7 +210,21 @@ __global__ __launch_bounds__(256) void dec_gemm_kernel(const unsigned short* __r
   const int vpr = Kblk / 8;
   for (int i = tid; i < M * vpr; i += 256) {
     const int r = i / vpr, c = (i % vpr) * 8;
-    *reinterpret_cast<uint4*>(xs + r * pitch + c) = *reinterpret_cast<const uint4*>(X + (long)r * K + k0 + c);
+    if constexpr (GLU) {
+      const uint4 gv = *reinterpret_cast<const uint4*>(X + (long)r * 2 * K + k0 + c);
+      const uint4 uv = *reinterpret_cast<const uint4*>(X + (long)r * 2 * K + K + k0 + c);
+      const unsigned gw[4] = {gv.x, gv.y, gv.z, gv.w}, uw[4] = {uv.x, uv.y, uv.z, uv.w};
+      unsigned ow[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float g0 = __uint_as_float(gw[j] << 16), g1 = __uint_as_float(gw[j] & 0xffff0000u);
+        const float u0 = __uint_as_float(uw[j] << 16), u1 = __uint_as_float(uw[j] & 0xffff0000u);
+        ow[j] = (unsigned)f2bf(g0 * dec_sigmoid(g0) * u0) | ((unsigned)f2bf(g1 * dec_sigmoid(g1) * u1) << 16);
+      }
+      *reinterpret_cast<uint4*>(xs + r * pitch + c) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    } else {
+      *reinterpret_cast<uint4*>(xs + r * pitch + c) = *reinterpret_cast<const uint4*>(X + (long)r * K + k0 + c);
+    }
   }
   __syncthreads();
 
@@ -719,8 +738,9 @@ extern "C" int pd_dec64s_gemm(const void* X, const void* W, const void* bias, vo
 // Decode GEMM on bf16 weights: out[M, N] = X[M, K] . W[N, K]^T (+ bias), M <= 64, split-K S (pd_dec_splits).
 extern "C" int pd_dec_splits(int M, int N, int K) { return pd_wo_splits(M, N, K, 0); }
 
+// glu: X is the gate|up output [M, 2K] and the GEMM runs on silu(gate) * up (the SwiGLU folded into X staging).
 extern "C" int pd_dec_gemm(const void* X, const void* W, const void* bias, void* out, float* ws, int M, int N, int K,
-                           int S, void* stream) {
+                           int S, int glu, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (M < 1 || M > 64 || N % kWoRows || K % 64 || S < 1 || S > K / 64) return -1;
   const int kmax = ((K / 64 + S - 1) / S) * 64;
@@ -732,11 +752,15 @@ extern "C" int pd_dec_gemm(const void* X, const void* W, const void* bias, void*
     if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     kern<<<grid, 256, lds, st>>>((const unsigned short*)X, (const unsigned short*)W, ws, M, N, K, kmax);
   };
-#define PD_DEC_R(MT_)                                                                         \
-  if (RT == 1) launch(dec_gemm_kernel<MT_, 1>);                                              \
-  else if (RT == 2) launch(dec_gemm_kernel<MT_, 2>);                                         \
-  else launch(dec_gemm_kernel<MT_, 4>);
-  if (MT == 1) { PD_DEC_R(1) } else if (MT == 2) { PD_DEC_R(2) } else { PD_DEC_R(4) }
+#define PD_DEC_R(MT_, G_)                                                                     \
+  if (RT == 1) launch(dec_gemm_kernel<MT_, 1, G_>);                                          \
+  else if (RT == 2) launch(dec_gemm_kernel<MT_, 2, G_>);                                     \
+  else launch(dec_gemm_kernel<MT_, 4, G_>);
+  if (glu) {
+    if (MT == 1) { PD_DEC_R(1, true) } else if (MT == 2) { PD_DEC_R(2, true) } else { PD_DEC_R(4, true) }
+  } else {
+    if (MT == 1) { PD_DEC_R(1, false) } else if (MT == 2) { PD_DEC_R(2, false) } else { PD_DEC_R(4, false) }
+  }
 #undef PD_DEC_R
   const long total = (long)M * N;
   wo_reduce_kernel<<<(int)((total / 4 + 255) / 256), 256, 0, st>>>(ws, S, M, N, nullptr, (const unsigned short*)bias,

@@ -96,6 +96,30 @@ def decode_ok(x, wt):
     return Nn % 64 == 0 and (DECODE_GEMM == "native" or Nn <= 8192)   # the split-K kernel: 64-row blocks
 
 
+def decode_glu_ok(gu, wt):
+    """The SwiGLU-staged split-K decode GEMM covers the M <= 16 rows whose plain decode GEMM runs native."""
+    M, K2 = gu.shape
+    K, Nn = K2 // 2, wt.shape[0]
+    return (gu.device.type == "cuda" and gu.dtype == torch.bfloat16 and wt.dtype == torch.bfloat16 and K2 % 2 == 0
+            and 1 <= M <= 16 and K % 64 == 0 and wt.shape[1] == K and wt.is_contiguous() and N.use_native(gu)
+            and DECODE_GEMM != "blas" and Nn % 64 == 0 and (DECODE_GEMM == "native" or Nn <= 8192))
+
+
+def decode_glu_matmul(gu, wt):
+    """y[M, N] = (silu(gate) * up) @ wt[N, K]^T for the gate|up output gu = [gate | up] [M, 2K], M <= 16: the SwiGLU
+    is applied while the split-K kernel stages X in LDS (csrc/kernels/weight_only.hip dec_gemm_kernel<GLU>)."""
+    M, K2 = gu.shape
+    K = K2 // 2
+    Nn = wt.shape[0]
+    gu = gu.contiguous()
+    C = N.native()
+    S = C.dec_splits(M, Nn, K)
+    ws = torch.empty(S * M * Nn, dtype=torch.float32, device=gu.device)
+    out = torch.empty(M, Nn, dtype=gu.dtype, device=gu.device)
+    C.dec_gemm(gu.data_ptr(), wt.data_ptr(), 0, out.data_ptr(), ws.data_ptr(), M, Nn, K, S, N.stream(), 1)
+    return out
+
+
 def decode_matmul(x, wt, bias=None):
     """y[M, N] = x[M, K] @ wt[N, K]^T (+ bias) for M <= 64 on the native stream kernel (weights read once, split-K
     over the 256 CUs, fp32 partials summed in a second pass); torch.matmul otherwise."""

@@ -131,8 +131,27 @@ class LlamaGenerator:
     def _layer_out(self, layer, o, residual):
         a = self._mm(o, layer.self_attn.o_proj.weight)
         h, residual = T.rms_norm(a, layer.post_attention_layernorm.weight._t, self.cfg.rms_norm_eps, residual)
-        f = T.swiglu(self._mm(h, layer.mlp.gate_up_fused_proj.weight))
-        return self._mm(f, layer.mlp.down_proj.weight), residual
+        gu = self._mm(h, layer.mlp.gate_up_fused_proj.weight)
+        down = self._mm_glu(gu, layer.mlp.down_proj.weight)   # decode rows: SwiGLU inside the down GEMM
+        if down is not None:
+            return down, residual
+        return self._mm(T.swiglu(gu), layer.mlp.down_proj.weight), residual
+
+    def _mm_glu(self, gu, param):
+        """swiglu(gu) @ W on the SwiGLU-staged decode GEMM (<= 16 rows, cached W^T), else None."""
+        if self.weight_layout != "nk" or gu.numel() > 16 * gu.shape[-1]:
+            return None
+        from ..ops import weight_only as WO
+
+        w = param._t
+        ent = self._wt.get(id(param))
+        if ent is None or ent[0] != w.data_ptr() or ent[1] != w._version:
+            return None   # let _mm (re)build the cached W^T first
+        gu2 = gu.reshape(-1, gu.shape[-1])
+        if not WO.decode_glu_ok(gu2, ent[2]):
+            return None
+        y = WO.decode_glu_matmul(gu2, ent[2])
+        return y.view(*gu.shape[:-1], y.shape[-1])
 
     def _logits_of(self, h, residual):
         out, _ = T.rms_norm(h, self.model.llama.norm.weight._t, self.cfg.rms_norm_eps, residual)

@@ -88,3 +88,19 @@ def test_dec64s_lds_x_kernel(M, N, K, cfg, monkeypatch):
     assert y.shape == (M, N) and _rel(y, ref) < 8e-3
     y2 = WO.decode_matmul(x, wt)
     assert _rel(y2, x.float() @ wt.float().t()) < 8e-3
+
+
+@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("N,K", [(4096, 11008), (256, 704), (128, 64)])
+def test_decode_glu_matmul_matches_fp32(M, N, K):
+    """The SwiGLU-staged split-K decode GEMM (dec_gemm_kernel<GLU>): (silu(gate) * up, rounded to bf16 like
+    swiglu_fwd) @ W^T against fp32, for the Llama-2-7B down projection and small shapes (K = 64: one K step)."""
+    g = torch.Generator(device=dev).manual_seed(5 * M + N + K)
+    gu = torch.randn(M, 2 * K, device=dev, generator=g).to(torch.bfloat16)
+    wt = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)
+    assert WO.decode_glu_ok(gu, wt)
+    y = WO.decode_glu_matmul(gu, wt)
+    gate, up = gu.float()[:, :K], gu.float()[:, K:]
+    a = (gate * torch.sigmoid(gate) * up).to(torch.bfloat16).float()
+    ref = a @ wt.float().t()
+    assert y.shape == (M, N) and _rel(y, ref) < 8e-3

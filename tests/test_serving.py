@@ -288,3 +288,37 @@ def test_decode_attention_kernels_gpu(impl, D, Hq, Hk, monkeypatch):
     """vector (1) and MFMA (2) decode kernels, forced, vs fp32 (lens straddle the 32-key tiles and the splits)."""
     monkeypatch.setattr(serving, "_DECODE_IMPL", impl)
     _decode_case("cuda", torch.bfloat16, D, Hq, Hk, [1, 31, 33, 300, 4097])
+
+
+@pytest.mark.gpu
+def test_decode_step_folds_swiglu_into_down_gemm_gpu(monkeypatch):
+    """Decode rows (<= 16) run the down projection on the SwiGLU-staged decode GEMM (no separate SwiGLU pass);
+    tokens match the unfused path."""
+    from paddle2_amd.models import LlamaConfig, LlamaForCausalLM
+    from paddle2_amd.ops import weight_only as WO
+    from paddle2_amd.serving.generation import LlamaGenerator
+
+    paddle.set_device("gpu:0")
+    paddle.seed(3)
+    cfg = LlamaConfig.tiny(num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, intermediate_size=704,
+                           dtype="bfloat16")
+    m = LlamaForCausalLM(cfg)
+    m.to(device="gpu:0")
+    m.eval()
+    prompts = [[1, 5, 9, 3, 11, 4], [7, 2, 8]]
+    calls = []
+    real = WO.decode_glu_matmul
+
+    def counting(gu, wt):
+        calls.append(tuple(gu.shape))
+        return real(gu, wt)
+
+    monkeypatch.setattr(WO, "decode_glu_matmul", counting)
+    fused = LlamaGenerator(m, max_batch=2, max_seq_len=128, block_size=16, use_graph=False,
+                           weight_layout="nk").generate(prompts, 6)
+    assert (2, 2 * 704) in calls
+    monkeypatch.setattr(WO, "decode_glu_ok", lambda gu, wt: False)
+    plain = LlamaGenerator(m, max_batch=2, max_seq_len=128, block_size=16, use_graph=False,
+                           weight_layout="nk").generate(prompts, 6)
+    for a, b in zip(fused, plain):
+        assert a[:3] == b[:3]
