@@ -317,6 +317,9 @@ def test_decode_step_folds_swiglu_into_down_gemm_gpu(monkeypatch):
     fused = LlamaGenerator(m, max_batch=2, max_seq_len=128, block_size=16, use_graph=False,
                            weight_layout="nk").generate(prompts, 6)
     assert (2, 2 * 704) in calls
+    graph = LlamaGenerator(m, max_batch=2, max_seq_len=128, block_size=16, use_graph=True,
+                           weight_layout="nk").generate(prompts, 6)
+    assert graph == fused   # the captured decode step replays the fused kernel
     monkeypatch.setattr(WO, "decode_glu_ok", lambda gu, wt: False)
     plain = LlamaGenerator(m, max_batch=2, max_seq_len=128, block_size=16, use_graph=False,
                            weight_layout="nk").generate(prompts, 6)
