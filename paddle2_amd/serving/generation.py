@@ -180,6 +180,40 @@ class LlamaGenerator:
         self.cache.seq_lens[slot] = n
         return self._logits_of(x[:, -1:], residual[:, -1:])[0, 0]
 
+    @torch.no_grad()
+    def prefill_batch(self, slots, prompts):
+        """Run several prompts as ONE packed token batch (the reference's batched encoder pass of
+        block_multihead_attention, seq_lens_encoder): every projection GEMM sees all prompts' tokens — M = the
+        summed lengths instead of one prompt's, so a 1024-token prompt no longer under-fills the 256 CUs — and
+        attention is the varlen flash kernel over cu_seqlens.  Returns the last-token logits [len(prompts), V]."""
+        lens = [len(p) for p in prompts]
+        total = sum(lens)
+        nh, nkv, d = self.nh, self.nkv, self.d
+        for s, n in zip(slots, lens):
+            self.cache.allocate(s, n + 1)
+        ids = torch.as_tensor([int(t) for p in prompts for t in p], dtype=torch.long).to(self.dev)
+        pos = torch.cat([torch.arange(n, dtype=torch.int32) for n in lens]).to(self.dev)
+        tok_batch = torch.cat([torch.full((n,), s, dtype=torch.int32) for s, n in zip(slots, lens)]).to(self.dev)
+        cu = torch.zeros(len(lens) + 1, dtype=torch.int32)
+        cu[1:] = torch.cumsum(torch.as_tensor(lens, dtype=torch.int32), 0)
+        last = (cu[1:] - 1).to(torch.long).to(self.dev)
+        cu = cu.to(self.dev)
+        pos_l = pos.long()[None]
+        x = self.model.llama.embed_tokens.weight._t[ids][None]  # [1, total, h]
+        residual = None
+        for li, layer in enumerate(self.model.llama.layers):
+            qkv, residual = self._layer_qkv(layer, x, residual)
+            qkv = qkv.view(1, total, nh + 2 * nkv, d)
+            qk = T.rope(qkv[:, :, :nh + nkv], self.cos, self.sin, pos_l, style=0)   # per-token positions
+            q, k, v = qk[0, :, :nh], qk[0, :, nh:], qkv[0, :, nh + nkv:]
+            write_kv(k, v, self.cache.k[li], self.cache.v[li], tok_batch, pos, self.cache.block_table)
+            o, _ = T.flash_attention_varlen(q.contiguous(), k.contiguous(), v.contiguous(), cu, cu, max(lens),
+                                            max(lens), causal=True)
+            x, residual = self._layer_out(layer, o.reshape(1, total, nh * d), residual)
+        for s, n in zip(slots, lens):
+            self.cache.seq_lens[s] = n
+        return self._logits_of(x[:, last], residual[:, last])[0]
+
     # ------------------------------------------------------------------ decode
     def _decode_body(self):
         nh, nkv, d = self.nh, self.nkv, self.d
@@ -236,14 +270,15 @@ class LlamaGenerator:
         pos = torch.zeros(B, dtype=torch.int32, device=self.dev)
         outs = [[] for _ in prompts]
         done = [False] * len(prompts)
+        # one packed prefill for all prompts (per-prompt when a single one is given)
+        first = (self.prefill_batch(list(range(len(prompts))), prompts) if len(prompts) > 1 else
+                 self.prefill(0, torch.as_tensor(prompts[0], dtype=torch.long))[None]) if prompts else None
         for i, p in enumerate(prompts):
-            p = torch.as_tensor(p, dtype=torch.long)
-            logits = self.prefill(i, p)
-            t = sample_logits(logits[None], temperature, top_k, top_p, gen)[0]
+            t = sample_logits(first[i:i + 1], temperature, top_k, top_p, gen)[0]
             toks[i] = t
-            pos[i] = p.numel()
+            pos[i] = len(p)
             outs[i].append(int(t))
-            self.cache.allocate(i, p.numel() + max_new_tokens + 1)
+            self.cache.allocate(i, len(p) + max_new_tokens + 1)
         for i in range(len(prompts), B):  # idle slots decode a dummy token at position 0
             self.cache.allocate(i, max_new_tokens + 2)
         for _ in range(max_new_tokens - 1):

@@ -109,6 +109,32 @@ def test_generation_matches_full_recompute_cpu():
         assert o == greedy_reference(m, p, 6)
 
 
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_packed_prefill_matches_per_prompt(dev):
+    """prefill_batch (all prompts as one packed token batch, varlen attention, per-token RoPE positions) gives the
+    per-prompt prefill's last-token logits and fills the same KV cache rows."""
+    from paddle2_amd.serving.generation import LlamaGenerator
+
+    if dev == "cuda":
+        paddle.set_device("gpu:0")
+    m = _tiny_llama(dev)
+    prompts = [[1, 5, 9, 3, 11, 4, 2], [7, 2, 8], [4, 4, 1, 9, 13]]
+    a = LlamaGenerator(m, max_batch=3, max_seq_len=64, block_size=8, use_graph=False)
+    b = LlamaGenerator(m, max_batch=3, max_seq_len=64, block_size=8, use_graph=False)
+    packed = a.prefill_batch([0, 1, 2], prompts)
+    seq = torch.stack([b.prefill(i, torch.as_tensor(p)) for i, p in enumerate(prompts)])
+    tol = dict(atol=2e-2, rtol=2e-2) if dev == "cuda" else dict(atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(packed.float(), seq.float(), **tol)
+    assert torch.equal(a.cache.seq_lens[:3].cpu(), b.cache.seq_lens[:3].cpu())
+    for li in range(len(a.cache.k)):
+        for i, p in enumerate(prompts):
+            for t in range(len(p)):
+                blk_a = a.cache.block_table[i, t // 8]
+                blk_b = b.cache.block_table[i, t // 8]
+                torch.testing.assert_close(a.cache.k[li][blk_a, t % 8].float(), b.cache.k[li][blk_b, t % 8].float(),
+                                           **tol)
+
+
 def test_generation_transposed_weight_layout_cpu():
     """weight_layout="nk" (the GPU default: cached W^T per projection) generates the same tokens, and the
     cache follows in-place weight updates (version bump)."""
