@@ -42,6 +42,10 @@ _FORCE = os.environ.get("PADDLE2_AMD_GEMM_VARIANT")
 VARIANT = int(_FORCE) if _FORCE is not None else None
 PASS_VARIANT = {"fwd": V7_SPREAD, "dgrad": V7_SPREAD, "wgrad": 5, "wgrad_bf16": 5, "swiglu": V7_SPREAD,
                 "rope": V7_SPREAD}
+for _k in list(PASS_VARIANT):   # per-pass override: PADDLE2_AMD_GEMM_VARIANT_FWD=6 (the forward on W as is, no W^T)
+    _e = os.environ.get("PADDLE2_AMD_GEMM_VARIANT_" + _k.upper())
+    if _e:
+        PASS_VARIANT[_k] = int(_e)
 # grouped tile order per pass (row tiles that sweep the column tiles together): 4 for the spread TN schedule
 # (forward +2..7 %, dgrad +0..2 % over 8 at M = 32768; profiles/r4_gemm_spread.md), 8 for the wgrad kernels
 PASS_GROUP_M = {"fwd": 4, "dgrad": 4, "swiglu": 4, "wgrad": 8, "wgrad_bf16": 8, "rope": 4}
