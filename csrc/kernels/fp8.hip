@@ -254,10 +254,10 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// up to kMaxMetas tensor roles in one launch (workgroup b = role b), e.g. the forward's x and W metas: the
-// dequant factor each cast used is snapshotted into snap[b] (nullable) before the roll — the backward's copy, in
-// the same launch instead of a separate 4-byte device copy per role (320 copyBuffer launches per GPT-3 13B step)
-constexpr int kMaxMetas = 4;
+// up to kMaxMetas tensor roles in one launch (workgroup b = role b; ops/fp8.py batches the deferred updates of
+// several linears).  The dequant factor each cast used is snapshotted into snap[b] (nullable) before the roll —
+// the backward's copy, in the same launch instead of a separate 4-byte device copy per role (320 copyBuffer launches per GPT-3 13B step)
+constexpr int kMaxMetas = 16;
 struct UpdArgs {
   float* hist[kMaxMetas];
   float* amax[kMaxMetas];

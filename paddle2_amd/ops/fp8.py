@@ -52,6 +52,25 @@ class FP8TensorMeta:
         self.inv_scale.copy_(1.0 / s)
         self.initialized = True
 
+    # Host-visible reads of a role whose update is still queued (defer_update) launch the queue first.
+    def _settled(name):
+        key = "_" + name
+
+        def get(self):
+            if id(self) in _PENDING_IDS:
+                flush_updates()
+            return self.__dict__[key]
+
+        def put(self, v):
+            self.__dict__[key] = v
+        return property(get, put)
+
+    history = _settled("history")
+    amax = _settled("amax")
+    scale = _settled("scale")
+    inv_scale = _settled("inv_scale")
+    del _settled
+
     def to(self, device):
         for k in ("history", "amax", "scale", "inv_scale"):
             setattr(self, k, getattr(self, k).to(device))
@@ -81,15 +100,53 @@ class FP8TensorMeta:
 _CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 
 
+_MAX_ROLES = 16   # csrc/kernels/fp8.hip kMaxMetas
+# GPU role updates deferred by defer_update(): launched in batches of _MAX_ROLES, or as soon as one of the pending
+# roles is cast again (its next cast must see the rolled scale) — 480 per-role updates of the GPT-3 13B fp8 step
+# become ~30 launches.  Stream order keeps every update after the casts that recorded its amax.
+DEFER_UPDATES = os.environ.get("PADDLE2_AMD_FP8_DEFER", "1") != "0"
+_PENDING = []
+_PENDING_IDS = set()
+
+
 def update_metas(pairs):
-    """[(meta, snap or None)]: every role's delayed-scaling update — on the GPU in ONE launch (up to 4 roles per
-    launch: the forward's x and W roles together), each snap receiving that role's pre-update inverse scale."""
+    """[(meta, snap or None)]: every role's delayed-scaling update, now — on the GPU in as few launches as possible
+    (up to 16 roles each), each snap receiving that role's pre-update inverse scale."""
     gpu = [p for p in pairs if p[0].amax.device.type == "cuda" and N.use_native(p[0].amax)]
-    for i in range(0, len(gpu), 4):
-        N.native().fp8_update_scale([m._native_role(s) for m, s in gpu[i:i + 4]], N.stream())
+    for i in range(0, len(gpu), _MAX_ROLES):
+        N.native().fp8_update_scale([m._native_role(s) for m, s in gpu[i:i + _MAX_ROLES]], N.stream())
     for m, s in pairs:
         if not (m.amax.device.type == "cuda" and N.use_native(m.amax)):
             m._update_ref(s)
+
+
+def defer_update(pairs):
+    """Queue the updates of GPU roles (CPU roles update at once); the snaps are written when the batch launches,
+    which is before anything reads them (the backward of the same linear runs after later casts or a flush)."""
+    if not DEFER_UPDATES:
+        update_metas(pairs)
+        return
+    now = []
+    for m, s in pairs:
+        if m.amax.device.type == "cuda" and N.use_native(m.amax) and id(m) not in _PENDING_IDS:
+            _PENDING.append((m, s))
+            _PENDING_IDS.add(id(m))
+        else:
+            now.append((m, s))
+    if now:
+        flush_updates()
+        update_metas(now)
+    if len(_PENDING) >= _MAX_ROLES:
+        flush_updates()
+
+
+def flush_updates():
+    """Launch every queued role update (call before reading a pending role's scale / history on the host)."""
+    if _PENDING:
+        batch = list(_PENDING)
+        _PENDING.clear()
+        _PENDING_IDS.clear()
+        update_metas(batch)
 
 
 def _dt_code(t):
@@ -101,6 +158,8 @@ def cast(x2, meta: FP8TensorMeta, transpose=False, keep_rowmajor=True, colsum=Fa
     return the unscaled fp32 column sums of every 64-row block ([ceil(R/64), C], summed in the same pass over x2 —
     the fp8 linear's bias gradient), or None where the kernel path has no such output."""
     R, C = x2.shape
+    if id(meta) in _PENDING_IDS:
+        flush_updates()   # this role's previous update must land before its scale is used again
     if not meta.initialized:
         meta.init_from(x2)
     if x2.device.type == "cuda" and N.use_native(x2):
@@ -256,16 +315,18 @@ class _FP8LinearFn(torch.autograd.Function):
                 None if bias is None else bias.to(out_dtype))
         # dequant factors of THIS step's casts, snapshotted by the (single) update launch that rolls both scales
         snap = torch.empty(2, dtype=torch.float32, device=mx.inv_scale.device)
-        update_metas([(mx, snap[0:1]), (mw, snap[1:2])])
+        defer_update([(mx, snap[0:1]), (mw, snap[1:2])])
         ctx.save_for_backward(xqT, wq, snap[0:1], snap[1:2])
-        ctx.meta = (mg, x.shape, bias is not None, out_dtype, w.dtype)
+        ctx.meta = (mg, x.shape, bias is not None, out_dtype, w.dtype, mx, mw)
         ctx.gt = getattr(w, "_p2_gt", None) if WGRAD_MAIN and w.is_cuda else None
         return y.reshape(*x.shape[:-1], N_)
 
     @staticmethod
     def backward(ctx, dy):
         xqT, wq, inv_x, inv_w = ctx.saved_tensors
-        mg, xshape, has_b, out_dtype, wdt = ctx.meta
+        mg, xshape, has_b, out_dtype, wdt, mx, mw = ctx.meta
+        if id(mx) in _PENDING_IDS or id(mw) in _PENDING_IDS:
+            flush_updates()   # the snaps read below are written by that queued launch
         N_ = dy.shape[-1]
         dy2 = dy.reshape(-1, N_)
         # dY [M, N], dY^T [N, M] and, with a bias, dY's column sums per 64-row block from the same pass
@@ -291,7 +352,7 @@ class _FP8LinearFn(torch.autograd.Function):
 
             db = (bias_grad(dy2.contiguous(), out_dtype=wdt) if dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16)
                   else dy2.sum(0, dtype=torch.float32).to(wdt))
-        mg.update()
+        defer_update([(mg, None)])
         return dx.reshape(xshape), dw, db, None, None, None
 
 

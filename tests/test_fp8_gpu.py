@@ -188,3 +188,43 @@ def test_fp8_wgrad_into_fp32_main_grad_slot(monkeypatch):
     assert rel < 1e-2, rel
     exact = (x.float().t() @ g.float()) + 0.25
     assert float((slot.buf - exact).norm() / exact.norm()) < 0.08
+
+
+def test_fp8_deferred_scale_updates_match_immediate(monkeypatch):
+    """PADDLE2_AMD_FP8_DEFER: the per-linear delayed-scaling updates queued and launched 16 roles at a time (or when a
+    queued role is cast again, or its state is read) give bit-identical outputs, gradients and scaling state to one
+    update launch per linear.  8 chained linears = 24 roles per step, so both flush triggers fire."""
+    from paddle2_amd.ops import fp8
+
+    torch.manual_seed(3)
+    L, K, M = 8, 256, 512
+    ws = [(torch.randn(K, K, device=DEV) * 0.06).bfloat16() for _ in range(L)]
+    xs = [torch.randn(M, K, device=DEV, dtype=torch.bfloat16) for _ in range(3)]
+
+    def run(defer):
+        monkeypatch.setattr(fp8, "DEFER_UPDATES", defer)
+        metas = [[fp8.FP8TensorMeta(f, device=torch.device(DEV)) for f in (fp8.E4M3, fp8.E4M3, fp8.E5M2)]
+                 for _ in range(L)]
+        outs, grads = [], []
+        for x in xs:
+            wl = [w.clone().requires_grad_() for w in ws]
+            h = x
+            for w, m in zip(wl, metas):
+                h = fp8.fp8_linear(h, w, None, *m)
+            h.float().square().mean().backward()
+            outs.append(h.detach())
+            grads.append([w.grad for w in wl])
+        fp8.flush_updates()
+        state = [torch.cat([m.history, m.scale, m.inv_scale]) for ms in metas for m in ms]
+        return outs, grads, state
+
+    o1, g1, s1 = run(False)
+    o2, g2, s2 = run(True)
+    assert not fp8._PENDING
+    for a, b in zip(o1, o2):
+        assert torch.equal(a, b)
+    for ga, gb in zip(g1, g2):
+        for a, b in zip(ga, gb):
+            assert torch.equal(a, b)
+    for a, b in zip(s1, s2):
+        assert torch.equal(a, b)
