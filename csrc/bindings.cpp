@@ -21,9 +21,9 @@ int pd_norm_fwd(int, int, int, const void*, const void*, const void*, const void
                 int, float, void*);
 int pd_norm_bwd_blocks(int);
 int pd_bias_grad_chunks(int, int);
-int pd_bias_grad(int, int, const void*, float*, void*, int, int, void*);
+int pd_bias_grad(int, int, const void*, float*, void*, int, int, int, void*);
 int pd_norm_bwd(int, int, int, const void*, const void*, const void*, const float*, const float*, const void*, void*,
-                float*, float*, void*, void*, int, int, int, void*);
+                float*, float*, void*, void*, int, int, int, int, int, int, void*);
 int pd_swiglu_fwd(int, const void*, const void*, void*, long, int, long, long, void*);
 int pd_gemm(int, int, const void*, long, const void*, long, void*, long, void*, long, const void*, int, int, int, float,
             int, int, int, void*, long, void*);
@@ -67,7 +67,7 @@ int pd_embed_fwd(int, const int64_t*, const void*, void*, long, int, long, long,
 int pd_embed_bwd(int, const int64_t*, const void*, float*, long, int, long, long, long, void*);
 int pd_cast_from_f32(int, const float*, void*, long, void*);
 int pd_fp8_cast(int, int, const void*, void*, void*, long, long, const float*, float*, float*, void*);
-int pd_colsum(int, const float*, void*, int, int, void*);
+int pd_colsum(int, const float*, void*, int, int, int, void*);
 int pd_fp8_update_scale(int, float* const*, const int*, float* const*, float* const*, float* const*, float* const*,
                         const float*, const float*, void*);
 int pd_decode_attn(const void*, long, long, const void*, const void*, long, long, long, const int*, int, int,
@@ -127,17 +127,23 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("norm_bwd_blocks", &pd_norm_bwd_blocks);
   m.def("bias_grad_chunks", &pd_bias_grad_chunks);
-  m.def("bias_grad", [](int dt, int odt, uintptr_t dy, uintptr_t part, uintptr_t db, int M, int N, uintptr_t st) {
-    check(pd_bias_grad(dt, odt, P<const void*>(dy), P<float*>(part), P<void*>(db), M, N, P<void*>(st)), "bias_grad");
-  });
+  m.def("bias_grad", [](int dt, int odt, uintptr_t dy, uintptr_t part, uintptr_t db, int M, int N, uintptr_t st,
+                        int acc) {
+    check(pd_bias_grad(dt, odt, P<const void*>(dy), P<float*>(part), P<void*>(db), M, N, acc, P<void*>(st)),
+          "bias_grad");
+  }, py::arg("dt"), py::arg("odt"), py::arg("dy"), py::arg("part"), py::arg("db"), py::arg("M"), py::arg("N"),
+     py::arg("st"), py::arg("acc") = 0);
   m.def("norm_bwd", [](int ln, int dt, int wdt, uintptr_t dy, uintptr_t x, uintptr_t w, uintptr_t mean, uintptr_t rstd,
                        uintptr_t dres, uintptr_t dx, uintptr_t dw_part, uintptr_t db_part, uintptr_t dw, uintptr_t db,
-                       int M, int N, int nblocks, uintptr_t st) {
+                       int M, int N, int nblocks, uintptr_t st, int odt, int acc_w, int acc_b) {
     check(pd_norm_bwd(ln, dt, wdt, P<const void*>(dy), P<const void*>(x), P<const void*>(w), P<const float*>(mean),
                       P<const float*>(rstd), P<const void*>(dres), P<void*>(dx), P<float*>(dw_part),
-                      P<float*>(db_part), P<void*>(dw), P<void*>(db), M, N, nblocks, P<void*>(st)),
+                      P<float*>(db_part), P<void*>(dw), P<void*>(db), M, N, nblocks, odt, acc_w, acc_b, P<void*>(st)),
           "norm_bwd");
-  });
+  }, py::arg("ln"), py::arg("dt"), py::arg("wdt"), py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"),
+     py::arg("rstd"), py::arg("dres"), py::arg("dx"), py::arg("dw_part"), py::arg("db_part"), py::arg("dw"),
+     py::arg("db"), py::arg("M"), py::arg("N"), py::arg("nblocks"), py::arg("st"), py::arg("odt") = -1,
+     py::arg("acc_w") = 0, py::arg("acc_b") = 0);
   m.def("gemm", [](int layout, int epi, uintptr_t a, long lda, uintptr_t b, long ldb, uintptr_t c, long ldc,
                    uintptr_t c2, long ldc2, uintptr_t bias, int M, int N, int K, float beta, int H, int group_m,
                    int variant, uintptr_t ws, long ws_bytes, uintptr_t st) {
@@ -310,10 +316,10 @@ PYBIND11_MODULE(_C, m) {
     return true;
   }, py::arg("dt"), py::arg("e5m2"), py::arg("x"), py::arg("y"), py::arg("yT"), py::arg("R"), py::arg("C"),
      py::arg("scale"), py::arg("amax"), py::arg("st"), py::arg("colpart") = 0);
-  m.def("colsum", [](int odt, uintptr_t part, uintptr_t db, int Pn, int N, uintptr_t st) {
-    check(pd_colsum(odt, P<const float*>(part), P<void*>(db), Pn, N, P<void*>(st)), "colsum");
-  });
-  // roles: [(hist, len, amax, scale, inv, snap (0 = none), fp8_max, margin_pow2)], up to 4 in one launch
+  m.def("colsum", [](int odt, uintptr_t part, uintptr_t db, int Pn, int N, uintptr_t st, int acc) {
+    check(pd_colsum(odt, P<const float*>(part), P<void*>(db), Pn, N, acc, P<void*>(st)), "colsum");
+  }, py::arg("odt"), py::arg("part"), py::arg("db"), py::arg("Pn"), py::arg("N"), py::arg("st"), py::arg("acc") = 0);
+  // roles: [(hist, len, amax, scale, inv, snap (0 = none), fp8_max, margin_pow2)], up to 16 in one launch
   m.def("fp8_update_scale", [](const std::vector<std::tuple<uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
                                                             float, float>>& roles,
                                uintptr_t st) {

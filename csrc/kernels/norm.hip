@@ -205,7 +205,8 @@ __global__ __launch_bounds__(kNormBlock) void norm_bwd_kernel(
 // x 16 row lanes; each lane streams P/16 rows with 16-B loads, then one LDS reduction. Deterministic
 // (fixed summation order) and ~P/16 loads in flight per lane instead of a serial P-long chain.
 template <typename WT>
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, WT* __restrict__ out, int P, int N) {
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, WT* __restrict__ out, int P, int N,
+                                                     int accumulate) {
   __shared__ float4 red[16][16];
   const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
   const int c = (blockIdx.x * 16 + cq) * 4;
@@ -225,6 +226,10 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
     for (int i = 1; i < 16; ++i) {
       const float4 v = red[i][cq];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    if (accumulate) {   // out += sum: a gradient accumulated into its fp32 main-grad slot
+      s.x += Elt<WT>::ld(out + c); s.y += Elt<WT>::ld(out + c + 1);
+      s.z += Elt<WT>::ld(out + c + 2); s.w += Elt<WT>::ld(out + c + 3);
     }
     Elt<WT>::st(out + c, s.x); Elt<WT>::st(out + c + 1, s.y);
     Elt<WT>::st(out + c + 2, s.z); Elt<WT>::st(out + c + 3, s.w);
@@ -259,10 +264,18 @@ static void fwd_launch(const void* x, const void* res, const void* w, const void
 #undef PD_NORM_FWD
 }
 
+// colsum_kernel with the output dtype chosen at run time (a parameter's own dtype, or fp32 for its main-grad slot)
+static void colsum_to(int odt, const float* part, void* out, int P, int N, int acc, hipStream_t st) {
+  dim3 g2(ceil_div(N, 64));
+  if (odt == kBF16) colsum_kernel<bf16><<<g2, 256, 0, st>>>(part, (bf16*)out, P, N, acc);
+  else if (odt == kF16) colsum_kernel<half16><<<g2, 256, 0, st>>>(part, (half16*)out, P, N, acc);
+  else colsum_kernel<float><<<g2, 256, 0, st>>>(part, (float*)out, P, N, acc);
+}
+
 template <typename T, typename WT, bool LN>
 static void bwd_launch(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
                        const void* dres, void* dx, float* dw_part, float* db_part, void* dw, void* db,
-                       int M, int N, int nblocks, hipStream_t st) {
+                       int M, int N, int nblocks, int odt, int acc_w, int acc_b, hipStream_t st) {
   constexpr int V = 16 / sizeof(T);
   const int nv = N / V;
   const int maxv = (nv + kNormBlock - 1) / kNormBlock;
@@ -277,10 +290,8 @@ static void bwd_launch(const void* dy, const void* x, const void* w, const float
   else if (maxv <= 4) { PD_NORM_BWD(4) }
   else { PD_NORM_BWD(4) }
 #undef PD_NORM_BWD
-  const int P = nblocks;
-  dim3 g2(ceil_div(N, 64));
-  colsum_kernel<WT><<<g2, 256, 0, st>>>(dw_part, (WT*)dw, P, N);
-  if (db_part) colsum_kernel<WT><<<g2, 256, 0, st>>>(db_part, (WT*)db, P, N);
+  colsum_to(odt, dw_part, dw, nblocks, N, acc_w, st);
+  if (db_part) colsum_to(odt, db_part, db, nblocks, N, acc_b, st);
 }
 
 // Bias gradient db[n] = sum_m dy[m, n] (reference: the bias-grad reduction of fused_gemm_epilogue_grad /
@@ -336,18 +347,16 @@ extern "C" int pd_bias_grad_chunks(int M, int N) {
 
 // db[n] = sum_p part[p, n] (fixed order) -> odt: the second pass of the bias gradient on partial row sums some
 // other kernel produced (the fp8 dY cast's per-64-row-block column sums).
-extern "C" int pd_colsum(int odt, const float* part, void* db, int P, int N, void* stream) {
+// acc: db += sum (accumulate into an existing fp32 main-grad slot) instead of db = sum.
+extern "C" int pd_colsum(int odt, const float* part, void* db, int P, int N, int acc, void* stream) {
   using namespace pd;
   if (N % 4 != 0 || P <= 0) return -1;
-  hipStream_t st = (hipStream_t)stream;
-  dim3 g2(ceil_div(N, 64));
-  if (odt == kBF16) colsum_kernel<bf16><<<g2, 256, 0, st>>>(part, (bf16*)db, P, N);
-  else if (odt == kF16) colsum_kernel<half16><<<g2, 256, 0, st>>>(part, (half16*)db, P, N);
-  else colsum_kernel<float><<<g2, 256, 0, st>>>(part, (float*)db, P, N);
+  colsum_to(odt, part, db, P, N, acc, (hipStream_t)stream);
   return (int)hipGetLastError();
 }
 
-extern "C" int pd_bias_grad(int dt, int odt, const void* dy, float* part, void* db, int M, int N, void* stream) {
+extern "C" int pd_bias_grad(int dt, int odt, const void* dy, float* part, void* db, int M, int N, int acc,
+                            void* stream) {
   using namespace pd;
   if (N % 8 != 0 || M <= 0) return -1;
   hipStream_t st = (hipStream_t)stream;
@@ -358,10 +367,7 @@ extern "C" int pd_bias_grad(int dt, int odt, const void* dy, float* part, void* 
   else if (dt == kF16) bias_grad_part_kernel<half16><<<g1, 256, 0, st>>>((const half16*)dy, part, M, N, rpc);
   else if (dt == kF32) bias_grad_part_kernel<float><<<g1, 256, 0, st>>>((const float*)dy, part, M, N, rpc);
   else return -2;
-  dim3 g2(ceil_div(N, 64));
-  if (odt == kBF16) colsum_kernel<bf16><<<g2, 256, 0, st>>>(part, (bf16*)db, chunks, N);
-  else if (odt == kF16) colsum_kernel<half16><<<g2, 256, 0, st>>>(part, (half16*)db, chunks, N);
-  else colsum_kernel<float><<<g2, 256, 0, st>>>(part, (float*)db, chunks, N);
+  colsum_to(odt, part, db, chunks, N, acc, st);
   return (int)hipGetLastError();
 }
 
@@ -398,23 +404,26 @@ extern "C" int pd_norm_bwd_blocks(int M) { return M < 1024 ? M : 1024; }
 
 extern "C" int pd_norm_bwd(int layernorm, int dt, int wdt, const void* dy, const void* x, const void* w,
                            const float* mean, const float* rstd, const void* dres, void* dx, float* dw_part,
-                           float* db_part, void* dw, void* db, int M, int N, int nblocks, void* stream) {
+                           float* db_part, void* dw, void* db, int M, int N, int nblocks, int odt, int acc_w,
+                           int acc_b, void* stream) {
   using namespace pd;
   hipStream_t st = (hipStream_t)stream;
+  // dw / db dtype: the weight's compute dtype by default (odt < 0), or fp32 main-grad slots written in place
+  if (odt < 0) odt = (wdt == kF32 || dt == kF32) ? kF32 : dt;
   const int V = dt == kF32 ? 4 : 8;
   if (N % V != 0 || N / V > kNormBlock * 4 || N % 4 != 0) return -1;
 #define PD_BWD_CASE(T)                                                                                           \
   if (wdt == kF32 && dt != kF32) {                                                                               \
-    if (layernorm) bwd_launch<T, float, true>(dy, x, w, mean, rstd, dres, dx, dw_part, db_part, dw, db, M, N, nblocks, st); \
-    else bwd_launch<T, float, false>(dy, x, w, mean, rstd, dres, dx, dw_part, nullptr, dw, nullptr, M, N, nblocks, st);   \
+    if (layernorm) bwd_launch<T, float, true>(dy, x, w, mean, rstd, dres, dx, dw_part, db_part, dw, db, M, N, nblocks, odt, acc_w, acc_b, st); \
+    else bwd_launch<T, float, false>(dy, x, w, mean, rstd, dres, dx, dw_part, nullptr, dw, nullptr, M, N, nblocks, odt, acc_w, acc_b, st);   \
   } else {                                                                                                       \
-    if (layernorm) bwd_launch<T, T, true>(dy, x, w, mean, rstd, dres, dx, dw_part, db_part, dw, db, M, N, nblocks, st);     \
-    else bwd_launch<T, T, false>(dy, x, w, mean, rstd, dres, dx, dw_part, nullptr, dw, nullptr, M, N, nblocks, st);       \
+    if (layernorm) bwd_launch<T, T, true>(dy, x, w, mean, rstd, dres, dx, dw_part, db_part, dw, db, M, N, nblocks, odt, acc_w, acc_b, st);     \
+    else bwd_launch<T, T, false>(dy, x, w, mean, rstd, dres, dx, dw_part, nullptr, dw, nullptr, M, N, nblocks, odt, acc_w, acc_b, st);       \
   }
   if (dt == kF32) {
     using T = float;
-    if (layernorm) bwd_launch<T, T, true>(dy, x, w, mean, rstd, dres, dx, dw_part, db_part, dw, db, M, N, nblocks, st);
-    else bwd_launch<T, T, false>(dy, x, w, mean, rstd, dres, dx, dw_part, nullptr, dw, nullptr, M, N, nblocks, st);
+    if (layernorm) bwd_launch<T, T, true>(dy, x, w, mean, rstd, dres, dx, dw_part, db_part, dw, db, M, N, nblocks, odt, acc_w, acc_b, st);
+    else bwd_launch<T, T, false>(dy, x, w, mean, rstd, dres, dx, dw_part, nullptr, dw, nullptr, M, N, nblocks, odt, acc_w, acc_b, st);
   } else if (dt == kBF16) { PD_BWD_CASE(bf16) }
   else { PD_BWD_CASE(half16) }
 #undef PD_BWD_CASE

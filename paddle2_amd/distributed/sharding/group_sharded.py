@@ -152,6 +152,8 @@ class _Unit:
         for i, p in enumerate(self.params):
             if not p.stop_gradient and p._t.dim() == 2:
                 p._t._p2_gt = (self, i)  # weight-gradient GEMMs write straight into the fp32 target
+            elif not p.stop_gradient and p._t.dim() == 1 and not getattr(p, "sequence_parallel", False):
+                p._t._p2_bt = (self, i)  # bias / norm-weight column sums likewise (ops.torch_ops.main_slot)
         # optimizer pieces: (param, shard offset, length) for every param overlapping my slice
         self.pieces = []
         for p, o, n in zip(self.params, self.offsets, self.numels):

@@ -319,6 +319,7 @@ class _FP8LinearFn(torch.autograd.Function):
         ctx.save_for_backward(xqT, wq, snap[0:1], snap[1:2])
         ctx.meta = (mg, x.shape, bias is not None, out_dtype, w.dtype, mx, mw)
         ctx.gt = getattr(w, "_p2_gt", None) if WGRAD_MAIN and w.is_cuda else None
+        ctx.bt = bias
         return y.reshape(*x.shape[:-1], N_)
 
     @staticmethod
@@ -342,9 +343,19 @@ class _FP8LinearFn(torch.autograd.Function):
                      wdt if wdt in (torch.bfloat16, torch.float16) else torch.float32).to(wdt)
         db = None
         if has_b and dpart is not None and wdt in _CODE:
-            # the cast's per-block column sums folded in a fixed order (no second read of dY)
-            db = torch.empty(N_, dtype=wdt, device=dy2.device)
-            N.native().colsum(_CODE[wdt], dpart.data_ptr(), db.data_ptr(), dpart.shape[0], N_, N.stream())
+            # the cast's per-block column sums folded in a fixed order (no second read of dY) — into the bias's
+            # fp32 main-grad slot when it has one
+            from .torch_ops import BIAS_MAIN, main_slot
+
+            slot = main_slot(ctx.bt) if BIAS_MAIN and ctx.needs_input_grad[2] else None
+            if slot is not None:
+                view, beta, owner, idx = slot
+                N.native().colsum(_CODE[torch.float32], dpart.data_ptr(), view.data_ptr(), dpart.shape[0], N_,
+                                  N.stream(), acc=int(beta != 0))
+                owner.param_grad_done(idx)
+            else:
+                db = torch.empty(N_, dtype=wdt, device=dy2.device)
+                N.native().colsum(_CODE[wdt], dpart.data_ptr(), db.data_ptr(), dpart.shape[0], N_, N.stream())
         elif has_b:
             # the native two-pass column sum (torch_ops.bias_grad): ATen's bf16 dim-0 reduce took 24.5 ms / 160
             # calls of the GPT-3 13B fp8 step (profiles/r4_gpt13b_fp8_step_kernels.txt)

@@ -98,6 +98,7 @@ class _NormFn(torch.autograd.Function):
         ctx.has_b = bc is not None
         ctx.shape = shape
         ctx.wdtype = w.dtype
+        ctx.params = (w, b)
         if res2 is not None:
             return y.reshape(shape), h.reshape(shape)
         return y.reshape(shape), None
@@ -114,11 +115,31 @@ class _NormFn(torch.autograd.Function):
             dx = torch.empty_like(hh)
             dw_part = torch.empty(nb, Nn, dtype=torch.float32, device=hh.device)
             db_part = torch.empty(nb, Nn, dtype=torch.float32, device=hh.device) if ctx.layernorm else None
-            dw = torch.empty(Nn, dtype=wc.dtype, device=hh.device)
-            db = torch.empty(Nn, dtype=wc.dtype, device=hh.device) if ctx.layernorm else None
+            # weight (and bias) gradients straight into their fp32 main-grad slots when every one has a slot
+            wp, bp = ctx.params
+            slots = None
+            if BIAS_MAIN and ctx.needs_input_grad[1] and (not ctx.has_b or ctx.needs_input_grad[2]):
+                slots = [main_slot(wp)] + ([main_slot(bp)] if ctx.has_b else [])
+                if any(sl is None for sl in slots):
+                    slots = None
+            if slots is not None:
+                dw = slots[0][0]
+                db = slots[1][0] if ctx.has_b else (
+                    torch.empty(Nn, dtype=torch.float32, device=hh.device) if ctx.layernorm else None)
+                accs = [int(sl[1] != 0) for sl in slots] + [0]
+                odt = _DT[torch.float32]
+            else:
+                dw = torch.empty(Nn, dtype=wc.dtype, device=hh.device)
+                db = torch.empty(Nn, dtype=wc.dtype, device=hh.device) if ctx.layernorm else None
+                accs, odt = [0, 0], -1
             C.norm_bwd(int(ctx.layernorm), _DT[hh.dtype], _DT[wc.dtype], dy2.data_ptr(), hh.data_ptr(), wc.data_ptr(),
                        N.ptr(mean), rstd.data_ptr(), N.ptr(dh2), dx.data_ptr(), dw_part.data_ptr(), N.ptr(db_part),
-                       dw.data_ptr(), N.ptr(db), M, Nn, nb, N.stream())
+                       dw.data_ptr(), N.ptr(db), M, Nn, nb, N.stream(), odt=odt, acc_w=accs[0], acc_b=accs[1])
+            if slots is not None:
+                for _v, _b, owner, idx in slots:
+                    owner.param_grad_done(idx)
+                dx = dx.reshape(ctx.shape)
+                return dx, None, None, (dx if ctx.has_res else None), None, None
         else:
             hf = hh.float()
             xh = (hf - mean[:, None]) * rstd[:, None] if ctx.layernorm else hf * rstd[:, None]
@@ -414,6 +435,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x2, w)
         ctx.meta = (x.shape, dw_t, b is not None)
         ctx.gt = getattr(w, "_p2_gt", None)
+        ctx.bt = b
         ctx.w_leaf = w if WeightGradStore.route else None
         return y.view(*x.shape[:-1], Nn)
 
@@ -453,25 +475,51 @@ class _LinearFn(torch.autograd.Function):
             else:
                 dw = torch.matmul(x2.t(), dy2)
         if has_b and ctx.needs_input_grad[2]:
-            db = bias_grad(dy2)
+            db = bias_grad(dy2, bt=ctx.bt)
         return dx, dw, db
 
 
-def bias_grad(dy2, out_dtype=None):
+def main_slot(t):
+    """The fp32 main-grad slot of a 1-D parameter (a sharding unit's ``_p2_bt``: biases, norm weights) as
+    (view, beta, owner, index), or None.  Its gradient kernel writes there (beta 1: accumulate) and calls
+    ``owner.param_grad_done(index)``; autograd then gets None, so no bf16 gradient and no fp32 conversion pass."""
+    bt = getattr(t, "_p2_bt", None) if t is not None else None
+    if bt is None:
+        return None
+    owner, idx = bt
+    view, beta = owner.grad_target(idx)
+    if view.dtype != torch.float32 or not view.is_contiguous() or view.data_ptr() % 16 != 0:
+        return None
+    return view, beta, owner, idx
+
+
+def bias_grad(dy2, out_dtype=None, bt=None):
     """db = dy2.sum(0) for a [M, N] gradient: the native two-pass column sum (csrc/kernels/norm.hip
     bias_grad_part_kernel + colsum, fp32 accumulation, deterministic) — torch's bf16 dim-0 reduce ran 5-30x slower
     on the GPT-3 13B step (24.9 ms / 160 calls).  ``out_dtype`` (default dy2's): the fp32 partials are rounded once,
-    straight to it — an fp32 master bias gets the fp32 sum, not a bf16-rounded one."""
+    straight to it — an fp32 master bias gets the fp32 sum, not a bf16-rounded one.  ``bt``: the bias tensor; with
+    an fp32 main-grad slot (main_slot) the sum lands there and None is returned."""
     M, Nn = dy2.shape
     odt = out_dtype or dy2.dtype
     if (N.use_native(dy2) and dy2.dtype in _DT and odt in _DT and Nn % 8 == 0 and dy2.is_contiguous() and M > 0
             and dy2.data_ptr() % 16 == 0):
         C = N.native()
         part = torch.empty(C.bias_grad_chunks(M, Nn) * Nn, dtype=torch.float32, device=dy2.device)
+        slot = main_slot(bt) if bt is not None and BIAS_MAIN else None
+        if slot is not None:
+            view, beta, owner, idx = slot
+            C.bias_grad(_DT[dy2.dtype], _DT[torch.float32], dy2.data_ptr(), part.data_ptr(), view.data_ptr(), M, Nn,
+                        N.stream(), acc=int(beta != 0))
+            owner.param_grad_done(idx)
+            return None
         db = torch.empty(Nn, dtype=odt, device=dy2.device)
         C.bias_grad(_DT[dy2.dtype], _DT[odt], dy2.data_ptr(), part.data_ptr(), db.data_ptr(), M, Nn, N.stream())
         return db
     return dy2.sum(0, dtype=torch.float32).to(odt)
+
+
+# 1-D parameter gradients (biases, norm weights) written straight into their fp32 main-grad slots
+BIAS_MAIN = _os.environ.get("PADDLE2_AMD_BIAS_MAIN", "1") != "0"
 
 
 def _pass_native(name, t, other=None):
