@@ -123,7 +123,10 @@ def update_metas(pairs):
 def defer_update(pairs):
     """Queue the updates of GPU roles (CPU roles update at once); the snaps are written when the batch launches,
     which is before anything reads them (the backward of the same linear runs after later casts or a flush)."""
-    if not DEFER_UPDATES:
+    if not DEFER_UPDATES or (pairs[0][0].amax.is_cuda and torch.cuda.is_current_stream_capturing()):
+        # (a HIP-graph capture must contain its own updates: a queue flushed after the capture ends would run once,
+        # eagerly, and never on replay)
+        flush_updates()
         update_metas(pairs)
         return
     now = []

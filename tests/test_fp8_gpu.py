@@ -228,3 +228,31 @@ def test_fp8_deferred_scale_updates_match_immediate(monkeypatch):
             assert torch.equal(a, b)
     for a, b in zip(s1, s2):
         assert torch.equal(a, b)
+
+
+def test_fp8_scale_updates_captured_in_hip_graph():
+    """Inside a HIP-graph capture the delayed-scaling updates are not queued: they are captured with the linear,
+    so every replay rolls the history (a queue flushed after the capture would run once, eagerly)."""
+    from paddle2_amd.ops import fp8
+
+    torch.manual_seed(4)
+    x = torch.randn(256, 256, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(256, 256, device=DEV) * 0.05).bfloat16()
+    metas = [fp8.FP8TensorMeta(f, device=torch.device(DEV)) for f in (fp8.E4M3, fp8.E4M3, fp8.E5M2)]
+    with torch.no_grad():
+        for _ in range(2):   # warm-up: first-use init and the per-shape GEMM route outside the capture
+            fp8.fp8_linear(x, w, None, *metas)
+        fp8.flush_updates()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            y = fp8.fp8_linear(x, w, None, *metas)
+        assert not fp8._PENDING
+        h = metas[0].history.clone()
+        assert int((h > 0).sum()) == 2
+        for k in range(3):
+            g.replay()
+            torch.cuda.synchronize()
+            assert int((metas[0].history > 0).sum()) == 3 + k
+    ref = x.float() @ w.float()
+    assert float((y.float() - ref).norm() / ref.norm()) < 0.08
