@@ -37,6 +37,9 @@ def _u(x):
 # 0 auto (MFMA kernel for D = 128 and 2..16 q heads per kv head, vector kernel for MHA), 1 vector kernel,
 # 2 MFMA kernel (raises if unusable)
 _DECODE_IMPL = {"auto": 0, "vec": 1, "mfma": 2}[os.environ.get("PADDLE2_AMD_DECODE_KERNEL", "auto")]
+# KV-split sizing: at least WG_TARGET workgroups over the cache's capacity, at least SPLIT_TOKENS keys per split
+_DECODE_WG_TARGET = int(os.environ.get("PADDLE2_AMD_DECODE_WG_TARGET", "2048"))
+_DECODE_SPLIT_TOKENS = int(os.environ.get("PADDLE2_AMD_DECODE_SPLIT_TOKENS", "64"))
 
 
 def decode_attention(q, k_cache, v_cache, seq_lens, block_table=None, block_size=None, layout="paged",
@@ -68,9 +71,9 @@ def decode_attention(q, k_cache, v_cache, seq_lens, block_table=None, block_size
         max_len = int(k_cache.shape[0] * bs) if block_table is not None else int(bs)
         if splits is None:
             # enough workgroups to fill the chip: B * Hk * splits >= ~2 per CU
-            splits = max(1, min(64, (512 + B * Hk - 1) // (B * Hk)))
+            splits = max(1, min(64, (_DECODE_WG_TARGET + B * Hk - 1) // (B * Hk)))
             if block_table is not None:
-                splits = max(1, min(splits, (block_table.shape[1] * bs) // 256 or 1))
+                splits = max(1, min(splits, (block_table.shape[1] * bs) // _DECODE_SPLIT_TOKENS or 1))
         lens = seq_lens.to(torch.int32).contiguous()
         max_len = int(block_table.shape[1] * bs) if block_table is not None else int(bs)
         part_o = torch.empty(B * Hq * splits * D, dtype=torch.float32, device=q.device) if splits > 1 else None
