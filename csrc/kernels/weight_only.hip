@@ -197,10 +197,17 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(const unsigned short* __re
 // whole X tile goes through LDS anyway), one launch less per layer.
 __device__ __forceinline__ float dec_sigmoid(float x) { return 1.f / (1.f + __expf(-x)); }   // as swiglu_fwd
 
+// cnt (optional): one int per column block, zero between calls.  The last of the S split-K workgroups of a column
+// block to finish (atomic arrival count) sums the S partials in split order — bit-identical to wo_reduce_kernel —
+// adds the bias and writes bf16 out, then re-arms its counter.  That drops the reduce launch (~5 us per projection
+// at decode batch 1, where the step is a chain of small kernels).  Nobody waits on the counter, so no workgroup can
+// stall another.
 template <int MT, int RT, bool GLU = false>
 __global__ __launch_bounds__(256) void dec_gemm_kernel(const unsigned short* __restrict__ X,
                                                        const unsigned short* __restrict__ W, float* __restrict__ ws,
-                                                       int M, int N, int K, int kmax) {
+                                                       int M, int N, int K, int kmax, int* __restrict__ cnt,
+                                                       const unsigned short* __restrict__ bias,
+                                                       unsigned short* __restrict__ out) {
   extern __shared__ unsigned short xs[];  // [M][kmax + kWoPad]
   const int pitch = kmax + kWoPad;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -299,10 +306,52 @@ __global__ __launch_bounds__(256) void dec_gemm_kernel(const unsigned short* __r
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const int m = t * 16 + (lane & 15);
-      if (m < M)
-        *reinterpret_cast<float4*>(ws + ((long)blockIdx.y * M + m) * N + nb) =
-            make_float4(acc[r][t][0], acc[r][t][1], acc[r][t][2], acc[r][t][3]);
+      if (m >= M) continue;
+      float* dst = ws + ((long)blockIdx.y * M + m) * N + nb;
+      if (cnt == nullptr) {
+        *reinterpret_cast<float4*>(dst) = make_float4(acc[r][t][0], acc[r][t][1], acc[r][t][2], acc[r][t][3]);
+      } else {
+        // write-through (system-scope) stores: the partials reach memory, not just this XCD's L2, so the reducing
+        // workgroup on any XCD reads them without a whole-L2 writeback / invalidate fence (measured 3x slower)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) __hip_atomic_store(dst + j, acc[r][t][j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
+  }
+  if (cnt == nullptr) return;
+  __shared__ int is_last;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // this wave's stores complete (vmcnt 0)
+  __syncthreads();
+  if (tid == 0) {
+    const int prev = __hip_atomic_fetch_add(cnt + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    is_last = prev == S - 1;
+    if (is_last) __hip_atomic_store(cnt + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);   // re-arm
+  }
+  __syncthreads();
+  if (!is_last) return;
+  const int ncol = kWoRows * RT, n0 = blockIdx.x * ncol, q = ncol / 4;
+  auto ld4 = [&](const float* p) {   // system-scope loads: from memory, past any stale cached line
+    return make_float4(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                       __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                       __hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                       __hip_atomic_load(p + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  };
+  for (int i = tid; i < M * q; i += 256) {
+    const int m = i / q, n = n0 + (i % q) * 4;
+    float4 a = ld4(ws + (long)m * N + n);
+    for (int sp = 1; sp < S; ++sp) {
+      const float4 b = ld4(ws + ((long)sp * M + m) * N + n);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    float v[4] = {a.x, a.y, a.z, a.w};
+    unsigned short o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (bias) v[j] += bf2f(bias[n + j]);
+      o[j] = f2bf(v[j]);
+    }
+    *reinterpret_cast<uint2*>(out + (long)m * N + n) =
+        make_uint2((unsigned)o[0] | ((unsigned)o[1] << 16), (unsigned)o[2] | ((unsigned)o[3] << 16));
   }
 }
 
@@ -739,8 +788,9 @@ extern "C" int pd_dec64s_gemm(const void* X, const void* W, const void* bias, vo
 extern "C" int pd_dec_splits(int M, int N, int K) { return pd_wo_splits(M, N, K, 0); }
 
 // glu: X is the gate|up output [M, 2K] and the GEMM runs on silu(gate) * up (the SwiGLU folded into X staging).
+// cnt: nullable int[N / 64] zeroed counters (the fused last-arriver reduction; nullptr = separate reduce launch).
 extern "C" int pd_dec_gemm(const void* X, const void* W, const void* bias, void* out, float* ws, int M, int N, int K,
-                           int S, int glu, void* stream) {
+                           int S, int glu, int* cnt, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (M < 1 || M > 64 || N % kWoRows || K % 64 || S < 1 || S > K / 64) return -1;
   const int kmax = ((K / 64 + S - 1) / S) * 64;
@@ -750,7 +800,8 @@ extern "C" int pd_dec_gemm(const void* X, const void* W, const void* bias, void*
   dim3 grid(N / (kWoRows * RT), S);
   auto launch = [&](auto kern) {
     if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    kern<<<grid, 256, lds, st>>>((const unsigned short*)X, (const unsigned short*)W, ws, M, N, K, kmax);
+    kern<<<grid, 256, lds, st>>>((const unsigned short*)X, (const unsigned short*)W, ws, M, N, K, kmax, cnt,
+                                 (const unsigned short*)bias, (unsigned short*)out);
   };
 #define PD_DEC_R(MT_, G_)                                                                     \
   if (RT == 1) launch(dec_gemm_kernel<MT_, 1, G_>);                                          \
@@ -762,8 +813,10 @@ extern "C" int pd_dec_gemm(const void* X, const void* W, const void* bias, void*
     if (MT == 1) { PD_DEC_R(1, false) } else if (MT == 2) { PD_DEC_R(2, false) } else { PD_DEC_R(4, false) }
   }
 #undef PD_DEC_R
-  const long total = (long)M * N;
-  wo_reduce_kernel<<<(int)((total / 4 + 255) / 256), 256, 0, st>>>(ws, S, M, N, nullptr, (const unsigned short*)bias,
-                                                                 (unsigned short*)out);
+  if (cnt == nullptr) {
+    const long total = (long)M * N;
+    wo_reduce_kernel<<<(int)((total / 4 + 255) / 256), 256, 0, st>>>(ws, S, M, N, nullptr,
+                                                                   (const unsigned short*)bias, (unsigned short*)out);
+  }
   return (int)hipGetLastError();
 }

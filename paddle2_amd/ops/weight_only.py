@@ -93,7 +93,10 @@ def decode_ok(x, wt):
         return False
     if M > 16:   # the whole-K MFMA stream kernel (dec64_kernel): the b17-64 serving step
         return Nn % 16 == 0 and (DECODE_GEMM == "native" or (Nn <= 4096 and K <= 4096))
-    return Nn % 64 == 0 and (DECODE_GEMM == "native" or Nn <= 8192)   # the split-K kernel: 64-row blocks
+    # the split-K kernel (64-row blocks): every width up to 8 rows — in the HIP-graph decode step it beats hipBLASLt
+    # on the wide qkv / gate|up projections too (b1-b8 3.8-6.6 % faster per step, profiles/r5_decode_serving.md) —
+    # and N <= 8192 for 9-16 rows (b16: the library wins the wide ones by ~1.5 %)
+    return Nn % 64 == 0 and (DECODE_GEMM == "native" or M <= 8 or Nn <= 8192)
 
 
 def decode_glu_ok(gu, wt):
@@ -116,8 +119,26 @@ def decode_glu_matmul(gu, wt):
     S = C.dec_splits(M, Nn, K)
     ws = torch.empty(S * M * Nn, dtype=torch.float32, device=gu.device)
     out = torch.empty(M, Nn, dtype=gu.dtype, device=gu.device)
-    C.dec_gemm(gu.data_ptr(), wt.data_ptr(), 0, out.data_ptr(), ws.data_ptr(), M, Nn, K, S, N.stream(), 1)
+    C.dec_gemm(gu.data_ptr(), wt.data_ptr(), 0, out.data_ptr(), ws.data_ptr(), M, Nn, K, S, N.stream(), 1,
+               _dec_counters(gu.device, Nn))
     return out
+
+
+# The split-K decode GEMM reduces its partials in the last-arriving workgroup of each column block (no reduce launch);
+# its arrival counters: one zeroed int32 buffer per (device, stream), re-armed by the kernel itself.
+DEC_FUSED_REDUCE = _os.environ.get("PADDLE2_AMD_DEC_FUSED_REDUCE", "0") != "0"
+_DEC_CNT = {}
+_DEC_CNT_LEN = 4096   # column blocks: N / 64 <= 4096 (N <= 262,144)
+
+
+def _dec_counters(dev, Nn):
+    if not DEC_FUSED_REDUCE or Nn // 64 > _DEC_CNT_LEN:
+        return 0
+    key = (dev, N.stream())
+    buf = _DEC_CNT.get(key)
+    if buf is None:
+        buf = _DEC_CNT[key] = torch.zeros(_DEC_CNT_LEN, dtype=torch.int32, device=dev)
+    return buf.data_ptr()
 
 
 def decode_matmul(x, wt, bias=None):
@@ -150,5 +171,6 @@ def decode_matmul(x, wt, bias=None):
     out = torch.empty(M, Nn, dtype=x.dtype, device=x.device)
     if bias is not None:
         bias = bias.to(torch.bfloat16).contiguous()
-    C.dec_gemm(x.data_ptr(), wt.data_ptr(), N.ptr(bias), out.data_ptr(), ws.data_ptr(), M, Nn, K, S, N.stream())
+    C.dec_gemm(x.data_ptr(), wt.data_ptr(), N.ptr(bias), out.data_ptr(), ws.data_ptr(), M, Nn, K, S, N.stream(), 0,
+               _dec_counters(x.device, Nn))
     return out

@@ -55,15 +55,16 @@ def test_dec64_whole_k_kernel(M, N, K, waves, rt, monkeypatch):
 
 
 def test_auto_routing(monkeypatch):
-    """auto: native split-K at M <= 16 on N <= 8192, the M > 16 kernels only on the 4096 x 4096 projection,
-    hipBLASLt elsewhere (profiles/r4_decode_gemm.md, profiles/r5_decode_serving.md)."""
+    """auto: native split-K at M <= 8 on every width and at M <= 16 on N <= 8192, the M > 16 kernels only on the
+    4096 x 4096 projection, hipBLASLt elsewhere (profiles/r4_decode_gemm.md, profiles/r5_decode_serving.md)."""
     monkeypatch.setattr(WO, "DECODE_GEMM", "auto")
 
     def ok(M, N, K):
         return WO.decode_ok(torch.empty(M, K, device=dev, dtype=torch.bfloat16),
                             torch.empty(N, K, device=dev, dtype=torch.bfloat16))
 
-    assert ok(1, 4096, 4096) and ok(16, 4096, 11008) and not ok(1, 12288, 4096)
+    assert ok(1, 4096, 4096) and ok(16, 4096, 11008) and ok(1, 12288, 4096) and ok(8, 22016, 4096)
+    assert not ok(9, 12288, 4096) and not ok(16, 22016, 4096)
     assert ok(32, 4096, 4096) and ok(64, 4096, 4096) and not ok(32, 4096, 11008) and not ok(64, 12288, 4096)
 
 
@@ -104,3 +105,44 @@ def test_decode_glu_matmul_matches_fp32(M, N, K):
     a = (gate * torch.sigmoid(gate) * up).to(torch.bfloat16).float()
     ref = a @ wt.float().t()
     assert y.shape == (M, N) and _rel(y, ref) < 8e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,Nn,K,glu,has_bias", [(1, 4096, 4096, False, False), (4, 12288, 4096, False, True),
+                                                 (16, 22016, 4096, False, False), (1, 4096, 11008, True, False),
+                                                 (8, 4096, 11008, True, False), (3, 1024, 512, False, True)])
+def test_dec_gemm_fused_reduce_bit_exact(monkeypatch, M, Nn, K, glu, has_bias):
+    """Split-K partials summed by the last-arriving workgroup of each column block (PADDLE2_AMD_DEC_FUSED_REDUCE)
+    equal the separate wo_reduce launch bit for bit (same split order), over repeated calls and HIP-graph replays
+    (the kernel re-arms its arrival counters)."""
+    from paddle2_amd.ops import weight_only as WO
+
+    torch.manual_seed(M * 7 + K)
+    x = torch.randn(M, 2 * K if glu else K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(Nn, K, device="cuda") * 0.02).bfloat16()
+    b = (torch.randn(Nn, device="cuda") * 0.1).bfloat16() if has_bias else None
+
+    def run():
+        return WO.decode_glu_matmul(x, w) if glu else WO.decode_matmul(x, w, b)
+
+    monkeypatch.setattr(WO, "DECODE_GEMM", "native")   # the split-K kernel for every shape here
+    assert glu or WO.decode_ok(x, w)
+    monkeypatch.setattr(WO, "DEC_FUSED_REDUCE", False)
+    ref = run()
+    exact = x.float() @ w.float().t() if not glu else None
+    if exact is not None:
+        exact = exact + (b.float() if b is not None else 0)
+        assert float((ref.float() - exact).norm() / exact.norm()) < 1e-2
+    monkeypatch.setattr(WO, "DEC_FUSED_REDUCE", True)
+    for _ in range(3):
+        assert torch.equal(run(), ref)
+    y = run()   # warm the counter buffer outside the capture
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y = run()
+    for _ in range(3):
+        y.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(y, ref)
+    assert WO._DEC_CNT and all(int(c.abs().sum()) == 0 for c in WO._DEC_CNT.values())
