@@ -236,6 +236,98 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
   }
 }
 
+// Few rows (the serving decode step, M <= 64): one workgroup per row, its 4 waves splitting the row (vector vi of
+// thread tid: tid + 256 k) with an LDS sum across the waves.  The one-wave-per-row kernel above leaves a single wave
+// walking 8 dependent-issue vectors per lane at M = 1 (9 us per call in the b1 decode trace).
+__device__ __forceinline__ float block_sum4(float v, float* sm) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float t = sm[0] + sm[1] + sm[2] + sm[3];
+  __syncthreads();
+  return t;
+}
+
+template <typename T, typename WT, int MAXV, bool LAYERNORM, bool HAS_RES, bool HAS_BIAS>
+__global__ __launch_bounds__(kNormBlock) void norm_fwd_row_kernel(
+    const T* __restrict__ x, const T* __restrict__ res, const WT* __restrict__ w, const WT* __restrict__ b,
+    T* __restrict__ y, T* __restrict__ res_out, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+    int M, int N, float eps) {
+  constexpr int V = 16 / sizeof(T);
+  __shared__ float sm[4];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int nv = N / V;
+  const long off = (long)row * N;
+  float buf[MAXV][V];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = tid + k * kNormBlock;
+    if (vi < nv) {
+      load_vec<T, V>(x + off + vi * V, buf[k]);
+      if constexpr (HAS_RES) {
+        float r[V];
+        load_vec<T, V>(res + off + vi * V, r);
+#pragma unroll
+        for (int j = 0; j < V; ++j) buf[k][j] += r[j];
+        store_vec<T, V>(res_out + off + vi * V, buf[k]);
+#pragma unroll
+        for (int j = 0; j < V; ++j) buf[k][j] = round_to<T>(buf[k][j]);
+      }
+#pragma unroll
+      for (int j = 0; j < V; ++j) s += LAYERNORM ? buf[k][j] : buf[k][j] * buf[k][j];
+    }
+  }
+  float mu = 0.f, rstd;
+  if constexpr (LAYERNORM) {
+    mu = block_sum4(s, sm) / N;
+    float v2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      if (tid + k * kNormBlock < nv) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) { const float d = buf[k][j] - mu; v2 += d * d; }
+      }
+    }
+    rstd = rsqrtf(block_sum4(v2, sm) / N + eps);
+  } else {
+    rstd = rsqrtf(block_sum4(s, sm) / N + eps);
+  }
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = tid + k * kNormBlock;
+    if (vi < nv) {
+      constexpr int WV = 16 / sizeof(WT);
+      float wv[V], bv[V];
+      if constexpr (WV == V) {
+        load_vec<WT, V>(w + vi * V, wv);
+        if constexpr (HAS_BIAS) load_vec<WT, V>(b + vi * V, bv);
+      } else {
+        float t0[4], t1[4];
+        load_vec<WT, 4>(w + vi * V, t0); load_vec<WT, 4>(w + vi * V + 4, t1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { wv[j] = t0[j]; wv[j + 4] = t1[j]; }
+        if constexpr (HAS_BIAS) {
+          load_vec<WT, 4>(b + vi * V, t0); load_vec<WT, 4>(b + vi * V + 4, t1);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { bv[j] = t0[j]; bv[j + 4] = t1[j]; }
+        }
+      }
+      float o[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        o[j] = (buf[k][j] - mu) * rstd * wv[j];
+        if constexpr (HAS_BIAS) o[j] += bv[j];
+      }
+      store_vec<T, V>(y + off + vi * V, o);
+    }
+  }
+  if (tid == 0) {
+    if (mean_out) mean_out[row] = mu;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
 // ------------------------------------------------------------------------------------ host
 template <typename T, typename WT, bool LN>
 static void fwd_launch(const void* x, const void* res, const void* w, const void* b, void* y, void* res_out,
@@ -256,7 +348,28 @@ static void fwd_launch(const void* x, const void* res, const void* w, const void
     else norm_fwd_kernel<T, WT, MV, LN, false, false><<<grid, block, 0, st>>>((const T*)x, nullptr,         \
              (const WT*)w, (const WT*)b, (T*)y, nullptr, mean, rstd, M, N, eps);                             \
   }
-  if (maxv <= 1) { PD_NORM_FWD(1) }
+  const int maxr = (nv + kNormBlock - 1) / kNormBlock;
+  // few rows: a workgroup per row (PADDLE2_AMD_NORM_ROW_MAXM, default 64; 0 = off)
+  static const int row_maxm = getenv("PADDLE2_AMD_NORM_ROW_MAXM") ? atoi(getenv("PADDLE2_AMD_NORM_ROW_MAXM")) : 64;
+  if (M <= row_maxm && maxr <= 4) {
+    dim3 grow(M);
+#define PD_NORM_FWD_ROW(MV)                                                                                  \
+    if (res) {                                                                                               \
+      if (b) norm_fwd_row_kernel<T, WT, MV, LN, true, true><<<grow, block, 0, st>>>((const T*)x,            \
+               (const T*)res, (const WT*)w, (const WT*)b, (T*)y, (T*)res_out, mean, rstd, M, N, eps);        \
+      else norm_fwd_row_kernel<T, WT, MV, LN, true, false><<<grow, block, 0, st>>>((const T*)x,             \
+               (const T*)res, (const WT*)w, (const WT*)b, (T*)y, (T*)res_out, mean, rstd, M, N, eps);        \
+    } else {                                                                                                 \
+      if (b) norm_fwd_row_kernel<T, WT, MV, LN, false, true><<<grow, block, 0, st>>>((const T*)x, nullptr,  \
+               (const WT*)w, (const WT*)b, (T*)y, nullptr, mean, rstd, M, N, eps);                           \
+      else norm_fwd_row_kernel<T, WT, MV, LN, false, false><<<grow, block, 0, st>>>((const T*)x, nullptr,   \
+               (const WT*)w, (const WT*)b, (T*)y, nullptr, mean, rstd, M, N, eps);                           \
+    }
+    if (maxr <= 1) { PD_NORM_FWD_ROW(1) }
+    else if (maxr <= 2) { PD_NORM_FWD_ROW(2) }
+    else { PD_NORM_FWD_ROW(4) }
+#undef PD_NORM_FWD_ROW
+  } else if (maxv <= 1) { PD_NORM_FWD(1) }
   else if (maxv <= 2) { PD_NORM_FWD(2) }
   else if (maxv <= 4) { PD_NORM_FWD(4) }
   else if (maxv <= 8) { PD_NORM_FWD(8) }
