@@ -609,6 +609,9 @@ __global__ __launch_bounds__(256) void wo_reduce_kernel(const float* __restrict_
   const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i >= (long)M * N) return;
   float4 a = *reinterpret_cast<const float4*>(ws + i);
+  // unrolled so the S partial loads are issued together (same summation order): at decode M = 1 the launch is a few
+  // workgroups and its time is this chain's latency
+#pragma unroll 8
   for (int s = 1; s < S; ++s) {
     const float4 b = *reinterpret_cast<const float4*>(ws + (long)s * M * N + i);
     a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
