@@ -350,7 +350,7 @@ static void* do_alloc(size_t size, int dev, hipStream_t stream) {
 static void* do_alloc_impl(size_t size, int dev, hipStream_t stream) {
   if (dev < 0 || dev >= kMaxDevices) return nullptr;
   Device& d = g_dev[dev];
-  std::lock_guard<std::mutex> lk(d.mu);
+  std::unique_lock<std::mutex> lk(d.mu);
   if (!d.seen_stream) {
     d.seen_stream = true;
     d.first_stream = stream;
@@ -376,11 +376,21 @@ static void* do_alloc_impl(size_t size, int dev, hipStream_t stream) {
       // to the driver for one more growth.  If nothing fits the allocation fails (torch.OutOfMemoryError through
       // the torch hook — a null pointer handed to torch became a GPU memory-access fault).
       d.st.num_oom_retries++;
-      int prev = -1;
-      hipGetDevice(&prev);
-      if (prev != dev) hipSetDevice(dev);
-      hipDeviceSynchronize();
-      if (prev != dev) hipSetDevice(prev);
+      // Under stream capture a device sync is illegal (it would invalidate the capture instead of failing the
+      // allocation): settle only what the fences already show, never return chunks, and fail with OOM.  Outside
+      // capture the sync runs with the allocator lock RELEASED, so other threads' allocations (and RCCL / p2p work
+      // waiting on peers) are not blocked behind the drain; the free index is re-scanned after relocking.
+      hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+      const bool capturing = hipStreamIsCapturing(stream, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
+      if (!capturing) {
+        lk.unlock();
+        int prev = -1;
+        hipGetDevice(&prev);
+        if (prev != dev) hipSetDevice(dev);
+        hipDeviceSynchronize();
+        if (prev != dev) hipSetDevice(prev);
+        lk.lock();
+      }
       process_deferred(d);
       for (auto& kv : d.free_index) fence_done(d, kv.second);
       coalesce_settled(d);
@@ -390,7 +400,7 @@ static void* do_alloc_impl(size_t size, int dev, hipStream_t stream) {
           break;
         }
       }
-      if (!b) {
+      if (!b && !capturing) {
         // last resort: return the fully-free chunks to the driver and grow once more (the pool is fragmented:
         // free bytes exist but no block holds `need`)
         release_free_chunks(d, dev);

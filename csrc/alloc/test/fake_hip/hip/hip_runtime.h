@@ -73,3 +73,8 @@ inline hipError_t hipDeviceSynchronize() {
   return hipSuccess;
 }
 inline hipError_t hipStreamSynchronize(hipStream_t) { return hipDeviceSynchronize(); }
+enum hipStreamCaptureStatus { hipStreamCaptureStatusNone = 0, hipStreamCaptureStatusActive = 1 };
+inline hipError_t hipStreamIsCapturing(hipStream_t, hipStreamCaptureStatus* s) {
+  *s = hipStreamCaptureStatusNone;
+  return hipSuccess;
+}

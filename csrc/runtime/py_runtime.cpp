@@ -129,6 +129,11 @@ PYBIND11_MODULE(_runtime, m) {
              }
              return py::bytes(out);
            })
+      .def("append", [](TCPStoreClient& c, const std::string& k, py::bytes v) {
+             std::string s = v;
+             py::gil_scoped_release rel;
+             return c.append(k, s);
+           })
       .def("set_timeout", &TCPStoreClient::set_timeout)
       .def_property_readonly("timeout", &TCPStoreClient::timeout);
 

@@ -38,6 +38,7 @@ class TCPStoreClient {
   bool remove(const std::string& k);
   int64_t num_keys();
   std::string compare_set(const std::string& k, const std::string& expected, const std::string& desired);
+  int64_t append(const std::string& k, const std::string& v);  // server-side atomic append -> new length
   void set_timeout(double s);
   double timeout() const { return timeout_s_; }
 

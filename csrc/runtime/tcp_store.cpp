@@ -30,7 +30,7 @@
 
 namespace pdrt {
 
-enum Cmd : uint8_t { kSet = 1, kGet = 2, kAdd = 3, kCheck = 4, kWait = 5, kDelete = 6, kNumKeys = 7, kCas = 8 };
+enum Cmd : uint8_t { kSet = 1, kGet = 2, kAdd = 3, kCheck = 4, kWait = 5, kDelete = 6, kNumKeys = 7, kCas = 8, kAppend = 9 };
 
 static void put_u32(std::string& b, uint32_t v) { b.append(reinterpret_cast<const char*>(&v), 4); }
 static void put_str(std::string& b, const std::string& s) { put_u32(b, (uint32_t)s.size()); b += s; }
@@ -149,6 +149,17 @@ struct TCPStoreServer::Impl {
         case kNumKeys: {
           int64_t n = (int64_t)kv.size();
           c.out.append(reinterpret_cast<const char*>(&n), 8);
+          break;
+        }
+        case kAppend: {
+          // atomic on the server (one event loop): concurrent appends of identical bytes both land, which a
+          // client-side read / compare_set loop cannot guarantee (ABA on equal values); returns the new length
+          if (!rd_str(k) || !rd_str(v)) return true;
+          std::string& cur = kv[k];
+          cur += v;
+          const int64_t n = (int64_t)cur.size();
+          c.out.append(reinterpret_cast<const char*>(&n), 8);
+          wake_waiters();
           break;
         }
         case kCas: {
@@ -392,6 +403,17 @@ int64_t TCPStoreClient::num_keys() {
   int64_t v;
   recv_all(reinterpret_cast<char*>(&v), 8);
   return v;
+}
+
+int64_t TCPStoreClient::append(const std::string& k, const std::string& v) {
+  std::lock_guard<std::mutex> g(mu_);
+  std::string b(1, (char)kAppend);
+  put_str(b, k);
+  put_str(b, v);
+  send_all(b);
+  int64_t n;
+  recv_all(reinterpret_cast<char*>(&n), 8);
+  return n;
 }
 
 std::string TCPStoreClient::compare_set(const std::string& k, const std::string& expected, const std::string& desired) {

@@ -192,6 +192,9 @@ class CUDAGraph:
         self._ctx = None
 
     def capture_begin(self):
+        from ..ops import fp8
+
+        fp8.before_capture()   # eager fp8 scale updates land before, not inside, the capture
         self._stream.wait_stream(torch.cuda.current_stream())
         self._ctx = torch.cuda.graph(self._g, pool=self._pool, stream=self._stream)
         self._ctx.__enter__()

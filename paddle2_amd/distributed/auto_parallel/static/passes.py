@@ -377,6 +377,60 @@ def _consumers(prog):
     return uses
 
 
+# operand positions that carry the sequence (row) dimension, by op: every other position is a weight-like operand
+_SP_ROW_POS = {"mm": (0,), "matmul": (0,), "linear": (0,), "addmm": (1,), "rms_norm": (0,), "layer_norm": (0,)}
+
+
+def _sp_operand_roles(prog, e, cur):
+    """Roles of op ``e``'s positional operands for the sequence-parallel rewrite, or None when the op cannot be
+    moved onto the sequence shard.  "row": carries the sequence dim (split onto the shard); "param": a weight-like
+    graph value (its gradient is all-reduced over the mesh dims once the op sees only the local rows); "const":
+    left alone.  The decision comes from the op's operand semantics — for a GEMM only the activation position, for
+    an elementwise op only an operand of the output's rank whose leading dim is the row count — never from a shape
+    coincidence (a [hidden, hidden] weight with hidden == rows stays a weight).  Keyword operands that are graph
+    values or trainable tensors end the chain: they are not rewritten, so moving the op would be wrong."""
+    from ....static.graph import VarRef
+
+    for x in pytree.tree_leaves(e.kwargs):
+        if isinstance(x, VarRef) or (isinstance(x, torch.Tensor) and (x.requires_grad or x.dim() > 0)):
+            return None
+    key = op_key(e)
+    cur_v = prog.vars[cur]
+    rows, nd = cur_v.shape[0], len(cur_v.shape)
+    roles = []
+    for k, x in enumerate(e.args):
+        if key in _SP_ROW_POS:
+            if isinstance(x, VarRef):
+                if k in _SP_ROW_POS[key]:
+                    roles.append("row")
+                elif x.vid == cur:
+                    return None      # the chain value in a weight position (e.g. x^T-shaped use): not row-local
+                else:
+                    roles.append("param")
+            elif k in _SP_ROW_POS[key]:
+                return None          # the row operand is not a graph value
+            else:
+                roles.append("const")
+            continue
+        # elementwise / activation: row-aligned iff same rank as the chain value with the row count leading
+        if isinstance(x, VarRef):
+            xs = prog.vars[x.vid].shape
+            if x.vid == cur or (len(xs) == nd and nd > 0 and xs[0] == rows):
+                roles.append("row")
+            elif len(xs) < nd or (len(xs) == nd and xs[0] == 1):
+                roles.append("param")   # broadcast along the rows
+            else:
+                return None
+        elif isinstance(x, torch.Tensor) and x.dim() == nd and nd > 0 and x.shape[0] == rows and x.shape[0] != 1:
+            return None              # a full-length constant would need its own split
+        else:
+            roles.append("const")
+    if key in _SP_ROW_POS and not any(isinstance(x, VarRef) and x.vid == cur for k, x in enumerate(e.args)
+                                      if k in _SP_ROW_POS[key]):
+        return None
+    return roles
+
+
 def sequence_parallel_optimization_pass(dmp):
     """Megatron sequence parallelism on the plan (reference python/paddle/distributed/passes/
     auto_parallel_sequence_parallel_optimization.py:33): a partial sum that is all-reduced, then run through
@@ -417,12 +471,10 @@ def sequence_parallel_optimization_pass(dmp):
                 break
             if e.kind not in ("torch", "native") or op_key(e) not in _ROW_LOCAL or len(e.outs) != 1:
                 break
-            seq_pos = [k for k, x in enumerate(e.args) if isinstance(x, VarRef) and x.vid == cur]
-            if op_key(e) in ("addmm",) and seq_pos != [1]:
+            roles = _sp_operand_roles(prog, e, cur)
+            if roles is None:
                 break
-            if op_key(e) in ("mm", "matmul", "linear") and seq_pos != [0]:
-                break
-            chain.append((us[0], e))
+            chain.append((us[0], e, roles))
             cur = e.outs[0]
         if b is None or not dims:
             i += 1
@@ -443,12 +495,12 @@ def sequence_parallel_optimization_pass(dmp):
         a.outs = [nv._vid]
         rename = {old_out: nv._vid}
         inserts = []   # (before op index, Op)
-        for idx, e in chain:
+        for idx, e, roles in chain:
             new_args = []
-            for x in e.args:
+            for x, role in zip(e.args, roles):
                 if isinstance(x, VarRef) and x.vid in rename:
                     new_args.append(VarRef(rename[x.vid]))
-                elif isinstance(x, VarRef) and len(prog.vars[x.vid].shape) > 0 and prog.vars[x.vid].shape[0] == rows:
+                elif isinstance(x, VarRef) and role == "row":
                     # a per-row activation operand: split it onto the shard too (backward: all-gather)
                     xv = prog.vars[x.vid]
                     sv = _new_var(prog, [rows // nsh] + list(xv.shape[1:]), xv.dtype)
@@ -456,9 +508,10 @@ def sequence_parallel_optimization_pass(dmp):
                     inserts.append((idx, Op("torch", _comm_fn(["c_split"], mesh, srcp, tuple(dst)), (x,), {},
                                             [sv._vid])))
                     new_args.append(VarRef(sv._vid))
-                elif isinstance(x, torch.Tensor) and x.requires_grad:
+                elif (isinstance(x, torch.Tensor) and x.requires_grad) or (isinstance(x, VarRef) and role == "param"):
                     # a replicated parameter now applied to the local rows only: its gradient is summed over dims
-                    pv = _new_var(prog, list(x.shape), x.dtype)
+                    xm = prog.vars[x.vid] if isinstance(x, VarRef) else x
+                    pv = _new_var(prog, list(xm.shape), xm.dtype)
                     inserts.append((idx, Op("torch", _grad_allreduce_fn(mesh, tuple(dims)), (x,), {}, [pv._vid])))
                     new_args.append(VarRef(pv._vid))
                 else:

@@ -356,6 +356,9 @@ def destroy_process_group(group=None):
         _groups.clear()
         _default_group = None
         _initialized = False
+        from .store import release_clones
+
+        release_clones()   # no group is left to use the per-group store connections
     else:
         dist.destroy_process_group(group.pg)
         _groups.pop(group.id, None)

@@ -376,6 +376,10 @@ class GroupShardedModel(Layer):
         self.peak_live_flat = 0
         self.prefetch_depth = 2
         self.keep_gathered = self._keep_gathered_policy()
+        # units left gathered by a grad-enabled forward for the backward (the turn unit, or all with keep_gathered);
+        # cleared by _finalize_backward — a forward that never gets a backward (eval without no_grad) would
+        # otherwise hold them gathered for good, so the next forward releases whatever is still listed
+        self._kept = set()
         for u in self._units:
             if u.layer is not None:
                 self._hooks.append(u.layer.register_forward_pre_hook(self._make_pre(u)))
@@ -481,6 +485,10 @@ class GroupShardedModel(Layer):
                 last = self._order_done and self._order and u.idx == self._order[-1]
                 if hooked and not last and not self.keep_gathered:
                     u.release()
+                elif hooked:
+                    self._kept.add(u.idx)
+                else:
+                    u.release()   # no output needs a gradient: no backward will come for this unit
             elif self._stage == 3:
                 u.release()
             return None
@@ -516,6 +524,7 @@ class GroupShardedModel(Layer):
 
     def _finalize_backward(self):
         self._cb_queued = False
+        self._kept.clear()
         for u in self._units:
             u.finish_grads()
             if self._stage == 3:
@@ -526,6 +535,11 @@ class GroupShardedModel(Layer):
     # ------------------------------------------------------------ module API
     def forward(self, *args, **kwargs):
         if self._stage == 3:
+            if self._kept:
+                # kept gathered by the previous forward, whose backward never ran: release before re-gathering
+                for i in sorted(self._kept):
+                    self._units[i].release()
+                self._kept.clear()
             for u in self._units:
                 if u.layer is None:
                     u.wait()  # root unit: keep gathered for the whole step

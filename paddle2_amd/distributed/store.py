@@ -71,6 +71,12 @@ class TCPStore:
 _LIVE = []
 
 
+def release_clones():
+    """Drop the per-group clone connections once every process group is gone (destroy_process_group of the
+    world): c10d then holds none of them, and each one's socket closes with its client."""
+    _LIVE[:] = [s for s in _LIVE if not getattr(s, "_is_clone", False)]
+
+
 class TorchStore(dist.Store):
     """torch.distributed.Store backed by the native TCPStore client."""
 
@@ -112,8 +118,10 @@ class TorchStore(dist.Store):
         self._c.set_timeout(timeout.total_seconds() if isinstance(timeout, datetime.timedelta) else float(timeout))
 
     def clone(self):
-        """A second client connection to the same daemon (ProcessGroupGloo clones the store for every group)."""
+        """A second client connection to the same daemon (ProcessGroupGloo clones the store for every group).
+        Clones are held (see _LIVE) until the job's groups are destroyed, then released (release_clones)."""
         c = TorchStore(TCPStore(self._s.host, self._s.port, False, self._s.world_size, self._s.timeout))
+        c._is_clone = True
         return c
 
     def multi_get(self, keys):
@@ -124,12 +132,9 @@ class TorchStore(dist.Store):
             self.set(k, v)
 
     def append(self, key, value):
+        # one server-side command: concurrent appends (identical bytes included) all land, in arrival order
         v = value.encode() if isinstance(value, str) else bytes(value)
-        while True:   # read-modify-write on compare_set: appends from several clients never lose bytes
-            cur = self._c.get(key) if self._c.check([key]) else b""
-            new = bytes(cur) + v
-            if bytes(self._c.compare_set(key, bytes(cur) if cur else b"", new)) == new:
-                return
+        self._c.append(key, v)
 
     def has_extended_api(self):
         return False

@@ -125,7 +125,7 @@ def defer_update(pairs):
     which is before anything reads them (the backward of the same linear runs after later casts or a flush)."""
     if not DEFER_UPDATES or (pairs[0][0].amax.is_cuda and torch.cuda.is_current_stream_capturing()):
         # (a HIP-graph capture must contain its own updates: a queue flushed after the capture ends would run once,
-        # eagerly, and never on replay)
+        # eagerly, and never on replay; a queue left by eager steps raises here instead of entering the graph)
         flush_updates()
         update_metas(pairs)
         return
@@ -146,10 +146,27 @@ def defer_update(pairs):
 def flush_updates():
     """Launch every queued role update (call before reading a pending role's scale / history on the host)."""
     if _PENDING:
+        _check_not_capturing()
         batch = list(_PENDING)
         _PENDING.clear()
         _PENDING_IDS.clear()
         update_metas(batch)
+
+
+def _check_not_capturing():
+    """Updates queued by EAGER steps must never be flushed into a HIP-graph capture: the graph would replay that
+    stale update (one extra history roll per replay) and write pre-update inverse scales into snap tensors that
+    live outside the graph's pool.  Every capture entry of the framework calls before_capture() first; a capture
+    started elsewhere with updates still queued is an error, not a silent corruption."""
+    if _PENDING and torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("fp8: delayed-scaling updates from eager steps are still queued at HIP-graph capture; "
+                           "call paddle2_amd.ops.fp8.before_capture() (or flush_updates()) before capturing")
+
+
+def before_capture():
+    """Settle the eager update queue before a HIP-graph capture begins (executor, device.CUDAGraph, serving decode):
+    inside a capture every update is then recorded by the cast that needs it, once per replay."""
+    flush_updates()
 
 
 def _dt_code(t):
@@ -161,6 +178,8 @@ def cast(x2, meta: FP8TensorMeta, transpose=False, keep_rowmajor=True, colsum=Fa
     return the unscaled fp32 column sums of every 64-row block ([ceil(R/64), C], summed in the same pass over x2 —
     the fp8 linear's bias gradient), or None where the kernel path has no such output."""
     R, C = x2.shape
+    if _PENDING and x2.is_cuda:
+        _check_not_capturing()
     if id(meta) in _PENDING_IDS:
         flush_updates()   # this role's previous update must land before its scale is used again
     if not meta.initialized:

@@ -251,6 +251,9 @@ class LlamaGenerator:
                 for _ in range(2):  # warm up allocations outside the graph
                     self._decode_body()
             torch.cuda.current_stream().wait_stream(s)
+            from ..ops import fp8
+
+            fp8.before_capture()
             self._graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._graph):
                 self._logits = self._decode_body()

@@ -323,6 +323,9 @@ class Executor:
                 for _ in range(2):
                     e2 = self._replay(program, dict(st.static_in))
             torch.cuda.current_stream().wait_stream(s)
+            from ..ops import fp8
+
+            fp8.before_capture()   # the warm-up replays' queued fp8 updates must not enter the graph
             st.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(st.graph):
                 e3 = self._replay(program, dict(st.static_in))

@@ -256,3 +256,43 @@ def test_fp8_scale_updates_captured_in_hip_graph():
             assert int((metas[0].history > 0).sum()) == 3 + k
     ref = x.float() @ w.float()
     assert float((y.float() - ref).norm() / ref.norm()) < 0.08
+
+
+def test_fp8_capture_without_manual_flush_advances_once_per_replay():
+    """eager warm-up steps leave deferred updates queued; paddle's CUDAGraph.capture_begin settles
+    them first, so the captured graph holds only the capture's own update and each replay rolls the history once.
+    A raw torch capture with updates still queued raises instead of recording the stale update."""
+    from paddle2_amd.device import CUDAGraph
+    from paddle2_amd.ops import fp8
+
+    torch.manual_seed(5)
+    x = torch.randn(256, 256, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(256, 256, device=DEV) * 0.05).bfloat16()
+    metas = [fp8.FP8TensorMeta(f, device=torch.device(DEV)) for f in (fp8.E4M3, fp8.E4M3, fp8.E5M2)]
+    with torch.no_grad():
+        for _ in range(2):
+            fp8.fp8_linear(x, w, None, *metas)
+        assert fp8._PENDING, "the eager warm-up should leave its updates queued"
+        g = CUDAGraph()
+        g.capture_begin()
+        y = fp8.fp8_linear(x, w, None, *metas)
+        g.capture_end()
+        assert not fp8._PENDING
+        torch.cuda.synchronize()
+        n0 = int((metas[0].history > 0).sum())
+        assert n0 == 2
+        for k in range(3):
+            g.replay()
+            torch.cuda.synchronize()
+            assert int((metas[0].history > 0).sum()) == n0 + 1 + k
+        # raw capture with a queue left by eager steps: refused
+        fp8.fp8_linear(x, w, None, *metas)
+        assert fp8._PENDING
+        g2 = torch.cuda.CUDAGraph()
+        with pytest.raises(RuntimeError, match="before_capture"):
+            with torch.cuda.graph(g2):
+                fp8.fp8_linear(x, w, None, *metas)
+        fp8._PENDING.clear()
+        fp8._PENDING_IDS.clear()
+    ref = x.float() @ w.float()
+    assert float((y.float() - ref).norm() / ref.norm()) < 0.08

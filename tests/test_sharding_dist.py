@@ -72,6 +72,17 @@ def test_stage3_keep_gathered_skips_backward_gathers():
     assert keep[0]["gathers"] <= 3 * keep[0]["n_units"] + 1
 
 
+def test_stage3_kept_units_released_without_backward():
+    """with keep_gathered, a grad-enabled forward that never gets a backward (eval without no_grad)
+    leaves its units gathered; the next forward releases them instead of holding them for good."""
+    res = run_workers("sharding_worker.py", 2, ["p_g_os"],
+                      extra_env={"PD_TEST_LAYERS": "4", "PADDLE2_AMD_STAGE3_KEEP_GATHERED": "1",
+                                 "PD_TEST_EVAL_NO_BWD": "1"})
+    for r in res:
+        assert r["held_after_eval"] >= 3, r          # kept for a backward that never comes
+        assert r["held_next"] == 0, r                # released by the next (no-grad) forward
+
+
 def test_stage3_comm_model_llama7b():
     """Bytes per rank per step of stage 3 at N = 8 for Llama-2-7B: all-gathers of the bf16 flat units (forward and
     backward, the last unit kept across the turn) and one fp32 reduce-scatter per unit."""

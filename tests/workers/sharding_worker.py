@@ -45,6 +45,15 @@ for s in range(steps):
     t = loss._t.detach().clone()
     C._all_reduce_torch(t)
     losses.append(float(t) / world)
+held_after_eval = held_next = None
+if os.environ.get("PD_TEST_EVAL_NO_BWD") == "1" and level == "p_g_os":
+    # a grad-enabled forward that never gets a backward: its kept units must not stay gathered for good
+    ids = paddle.Tensor._wrap(data[0][rank * 2:(rank + 1) * 2])
+    m(ids[:, :-1], labels=ids[:, 1:])
+    held_after_eval = sum(1 for u in m._units if u.layer is not None and u.full is not None)
+    with paddle.no_grad():
+        m(ids[:, :-1], labels=ids[:, 1:])
+    held_next = sum(1 for u in m._units if u.layer is not None and u.full is not None)
 peak_live = getattr(m, "peak_live_flat", None)
 pool_bufs = sum(len(v) for v in getattr(m, "_flat_pool", {}).values())
 sizes = len({u.padded for u in getattr(m, "_units", [])})
@@ -66,5 +75,6 @@ for s in range(steps):
 csum_ref = float(sum(v._t.double().sum() for v in m2.state_dict().values()))
 write_result({"losses": losses, "ref": ref, "csum": csum, "csum_ref": csum_ref, "peak_live_flat": peak_live,
               "pool_bufs": pool_bufs, "unit_sizes": sizes, "gathers": gathers, "keep": keep,
-              "n_units": len(getattr(m, "_units", []))})
+              "n_units": len(getattr(m, "_units", [])),
+              "held_after_eval": held_after_eval, "held_next": held_next})
 C.destroy_process_group()

@@ -88,12 +88,16 @@ if "sharding" in passes:
 for st in (2, 3):
     if f"sharding{st}" in passes:
         owners = sharding_pass(dmp, 0, stage=st)
+if "amp" in passes and passes.index("amp") < passes.index("spopt") if "spopt" in passes else False:
+    # AMP first: the fc3 weight reaches its matmul as a bf16 cast GRAPH value of shape [8, 4] — its leading dim
+    # equals the row count, the coincidence the sequence-parallel rewrite must not take for an activation
+    out["amp_ops"] = amp_pass(dmp)
 if "spopt" in passes:
     out["spopt"] = sequence_parallel_optimization_pass(dmp)
 if "overlap" in passes:
     out["overlap"] = allreduce_matmul_grad_overlap_pass(dmp)
 out["comm_after"] = dmp.comm_ops()
-if "amp" in passes:
+if "amp" in passes and "amp_ops" not in out:
     out["amp_ops"] = amp_pass(dmp)
 exe = paddle.static.Executor()
 ropt = paddle.optimizer.Adam(0.05, parameters=ref.parameters())
