@@ -71,6 +71,13 @@ def parse(argv=None):
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--gemm-autotune", default="auto", choices=["auto", "tune", "off"],
                     help="hipBLASLt solution cache (tuning/gemm_gfx950.csv): auto = use it if present")
+    ap.add_argument("--expect-pg", default="auto", choices=["auto", "pdrccl", "c10d", "gloo", "any"],
+                    help="process group the run must be on (auto: pdrccl on GPUs unless PADDLE2_AMD_PG opts out, gloo "
+                         "on CPU); a mismatch — e.g. a failed start-up canary that fell back to c10d — exits 3")
+    ap.add_argument("--allow-pg-fallback", action="store_true", help="accept a fallen-back process group (= any)")
+    ap.add_argument("--hang-guard-s", type=float, default=0.0,
+                    help="bound on the timed region (0: max(300 s, 20 x the measured warm-up step time x steps)); "
+                         "past it every rank dumps its last collective per group and exits 124")
     ap.add_argument("--gemm-route", default="static", choices=["static", "measure"],
                     help="bf16 Linear GEMM backend per shape: static = the per-pass table (ops/gemm.py: the native "
                          "kernels), measure = time native vs hipBLASLt per (pass, M, N, K) once (incubate/autotune.py "
@@ -88,6 +95,54 @@ def _self_launch(args) -> int:
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(cmd, env=env, cwd=ROOT)
+
+
+def expected_pg(world, on_gpu, native_enabled, want="auto"):
+    """The process-group backend a run of ``world`` ranks must report (None: no requirement)."""
+    if world <= 1 or want == "any":
+        return None
+    if want != "auto":
+        return want
+    if not on_gpu:
+        return "gloo"
+    return "pdrccl" if native_enabled else "c10d"
+
+
+def pg_problem(status, expect):
+    """Error text when the job's process group is not the expected one (a silent fallback), else None."""
+    if expect is None or status.get("backend") == expect:
+        return None
+    return (f"process group is {status.get('backend')!r}, expected {expect!r} (start-up canary verdicts: "
+            f"{status.get('canary')}); refusing to report a number from a fallen-back communicator "
+            "(--allow-pg-fallback / --expect-pg any to accept)")
+
+
+def _hang_report(guard_s):
+    """Printed by every rank when the timed region outlives its guard: the communicator state and the latest
+    collective of each process group, then a non-zero exit (no re-exec; the launcher tears the job down)."""
+    rep = {"error": "bench timed region exceeded its guard", "guard_s": round(guard_s, 1),
+           "rank": int(os.environ.get("RANK", "0"))}
+    try:
+        from paddle2_amd.distributed import collective as C
+
+        rep["pg"] = C.pg_status()
+    except Exception as e:  # noqa: BLE001 - diagnostics only
+        rep["pg"] = repr(e)
+    try:
+        from paddle2_amd.distributed import rccl_pg
+
+        rep["last_ops"] = rccl_pg.last_ops()
+    except Exception as e:  # noqa: BLE001
+        rep["last_ops"] = repr(e)
+    try:
+        from paddle2_amd.distributed import watchdog
+
+        rep["watchdog_timeouts"] = watchdog.check_once(0.0)
+    except Exception as e:  # noqa: BLE001
+        rep["watchdog_timeouts"] = repr(e)
+    print(json.dumps(rep, default=str), file=sys.stderr, flush=True)
+    sys.stdout.flush()
+    os._exit(124)
 
 
 def main():
@@ -141,6 +196,21 @@ def main():
         strategy.pipeline_configs = {"accumulate_steps": acc, "micro_batch_size": args.micro_batch,
                                      "schedule_mode": args.pp_schedule if vpp == 1 else "VPP"}
     fleet.init(is_collective=True, strategy=strategy)
+    from paddle2_amd.distributed import collective as C
+
+    # what actually runs the collectives: a fallback (failed canary -> c10d, or gloo) must not yield a silent number
+    pgs = C.pg_status()
+    native_on = False
+    if torch.cuda.is_available():
+        from paddle2_amd.distributed import rccl_pg
+
+        native_on = rccl_pg.enabled()
+    want = "any" if args.allow_pg_fallback else args.expect_pg
+    err = pg_problem(pgs, expected_pg(world, torch.cuda.is_available(), native_on, want))
+    if err:
+        print(f"error: {err}", file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(3)
     paddle.seed(1234)  # same init on every rank (stage 3 shards one replica)
 
     is_gpt = args.model.startswith("gpt3")
@@ -210,6 +280,7 @@ def main():
         return loss
 
     dbg = os.environ.get("PADDLE2_AMD_BENCH_DEBUG", "0") == "1"   # per-warmup-step sync + memory line (stderr)
+    tw0 = time.perf_counter()
     for i in range(args.warmup):
         loss = step(i)
         if dbg and torch.cuda.is_available():
@@ -231,7 +302,14 @@ def main():
                   f"peak {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB{extra}", file=sys.stderr, flush=True)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
-    from paddle2_amd.distributed import collective as C
+    warm_step_s = (time.perf_counter() - tw0) / max(1, args.warmup)
+    # bounded-time guard around the timed region (a hung collective must end the run, with a report, not stall it)
+    import threading
+
+    guard_s = args.hang_guard_s or max(300.0, 20.0 * warm_step_s * args.steps)
+    guard = threading.Timer(guard_s, _hang_report, args=(guard_s,))
+    guard.daemon = True
+    guard.start()
 
     if world > 1:
         C.barrier()
@@ -252,6 +330,16 @@ def main():
         torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(el.item())
     final_loss = float(loss)
+    guard.cancel()
+    peak = paddle.device.cuda.max_memory_allocated() / 2**30 if torch.cuda.is_available() else 0.0
+    peaks = [round(peak, 1)]
+    if world > 1:
+        pt = torch.tensor([peak], dtype=torch.float64, device=dev)
+        pl = [torch.zeros_like(pt) for _ in range(world)]
+        torch.distributed.all_gather(pl, pt)
+        peaks = [round(float(x.item()), 1) for x in pl]
+    pgs = C.pg_status()
+    comm_world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
 
     replicas = dp * sh   # data-parallel replicas: each trains its own b x acc sequences per step
     tokens = b * s * acc * args.steps * replicas
@@ -295,8 +383,15 @@ def main():
                        "parallelism": par, "layers": cfg.num_hidden_layers},
             "mfu_vs_2.5PF_dense": round(mfu, 4),
             "final_loss": round(final_loss, 4),
-            "peak_mem_gb": round(paddle.device.cuda.max_memory_allocated() / 2**30, 1) if torch.cuda.is_available()
-            else None,
+            "peak_mem_gb": round(peak, 1) if torch.cuda.is_available() else None,
+            # self-diagnosis of the communicator that produced this number (a fallback would otherwise look valid)
+            "pg_backend": pgs.get("backend"),
+            "canary": pgs.get("canary"),
+            "comm_world_size": comm_world,
+            "ipc_allreduce": pgs.get("ipc"),
+            "peak_mem_gb_per_rank": peaks,
+            "stage3_keep_gathered": getattr(model, "keep_gathered", None),
+            "hang_guard_s": round(guard_s, 1),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -205,7 +205,9 @@ def _check_native_pg(store, rank, world, tout):
 
 
 def pg_status():
-    """Which process group the job runs on and what its start-up checks found."""
+    """Which process group the job runs on and what its start-up checks found: backend ("pdrccl" = the framework's
+    own ProcessGroupRCCL, "c10d" = torch's ProcessGroupNCCL, "gloo", "none" = single process), the per-rank canary
+    verdicts of the native group, whether the xGMI IPC all-reduce is on, and the rendezvous store."""
     return dict(_PG_STATUS)
 
 
@@ -289,6 +291,10 @@ def init_parallel_env(backend=None, timeout_s=None):
             dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=tout, **kw)
             if native_pg:
                 _check_native_pg(kw["store"], rank, world, tout)
+            else:
+                _PG_STATUS["backend"] = "gloo" if backend == "gloo" else "c10d"
+    if _PG_STATUS["backend"] is None:
+        _PG_STATUS["backend"] = "none" if not dist.is_initialized() else str(dist.get_backend())
     _default_group = Group(rank, 0, list(range(world)), dist.group.WORLD if dist.is_initialized() else None,
                            name="_default_pg")
     _groups[0] = _default_group

@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import sys
 
 import torch
 import torch.distributed as dist
@@ -113,7 +114,11 @@ class ProcessGroupRCCL(dist.ProcessGroup):
         self._g = _native().RcclGroup(store, prefix, rank, size, self._dev, tms)
         self._ext = {}
         self._scratch = None
+        self._prefix = prefix
+        self._nops = 0
+        self.last_op = None      # (sequence number, collective, tensor shapes) of the latest launch (hang reports)
         _LIVE.append(self._g)
+        _GROUPS.append(self)
 
     # ------------------------------------------------------------------ plumbing
     def getBackendName(self):
@@ -131,6 +136,8 @@ class ProcessGroupRCCL(dist.ProcessGroup):
     def _launch(self, fn, tensors, outs=(), use_calc=False, comm_stream=None):
         """run native ``fn(calc_stream, use_calc)`` on contiguous tensors; non-contiguous outputs are copied back
         after the op (on the stream that waits for it)."""
+        self._nops += 1
+        self.last_op = (self._nops, sys._getframe(1).f_code.co_name, [tuple(t.shape) for t in tensors[:4]])
         task = fn(self._calc(), use_calc)
         if task is not None:
             cs = self._stream(comm_stream if comm_stream is not None else self._g.comm_stream())
@@ -351,6 +358,17 @@ class ProcessGroupRCCL(dist.ProcessGroup):
 
 
 _LIVE = []   # every native group: torn down at interpreter exit, before the HIP runtime's own atexit teardown
+_GROUPS = []  # the Python groups, for last_ops()
+
+
+def last_ops():
+    """The latest collective launched on every ProcessGroupRCCL of this process: [{group, rank, size, seq, op,
+    shapes}] — what a hang report prints (the reference comm_task_manager's last-started task per group)."""
+    out = []
+    for g in _GROUPS:
+        seq, op, shapes = g.last_op if g.last_op is not None else (0, None, [])
+        out.append({"group": g._prefix, "rank": g.rank(), "size": g.size(), "seq": seq, "op": op, "shapes": shapes})
+    return out
 
 
 def shutdown_all():
