@@ -250,6 +250,232 @@ def _coalesced_broadcast(tensors, src, group):
         off += t.numel()
 
 
+class _Stage3State:
+    """Runtime state of the static stage-3 program: per-unit gathers (forward, one unit of prefetch), re-gathers for
+    the backward through saved-tensor hooks, the asynchronous reduces to the owners, and a live-bytes meter."""
+
+    def __init__(self, units, owners, row, group, me):
+        self.units = units            # [[Parameter, ...]] in forward order
+        self.owners, self.row, self.group, self.me = owners, row, group, me
+        self.prefetched = {}          # unit -> (works, tensors) issued ahead
+        self.bwd_cache = {}           # unit -> re-gathered tensors (backward), dropped by the unit's backward
+        self.pending = []             # (work, grad, param) reduces in flight
+        self.storage = {}             # storage data_ptr -> (unit, index) of live gathered tensors
+        self.live = 0
+        self.peak = 0
+        self.n_gathers = 0
+        self.hooks = None
+
+    # ---- gathers
+    def _issue(self, k):
+        works, outs = [], []
+        for p in self.units[k]:
+            o = self.owners[p.name]
+            full = torch.empty(self.shapes[p.name], dtype=p._t.dtype, device=p._t.device)
+            if o == self.me:
+                full.copy_(p._t.detach())
+            works.append(dist.broadcast(full, src=self.row[o], group=self.group, async_op=True))
+            outs.append(full)
+        self.n_gathers += 1
+        return works, outs
+
+    def _track(self, k, outs):
+        import weakref
+
+        for i, t in enumerate(outs):
+            key = t.untyped_storage().data_ptr()
+            self.storage[key] = (k, i)
+            nb = t.numel() * t.element_size()
+            self.live += nb
+            weakref.finalize(t, self._untrack, key, nb)
+        self.peak = max(self.peak, self.live)
+
+    def _untrack(self, key, nb):
+        self.storage.pop(key, None)
+        self.live -= nb
+
+    def materialize(self, k):
+        works, outs = self.prefetched.pop(k, None) or self._issue(k)
+        for w in works:
+            w.wait()
+        self._track(k, outs)
+        return outs
+
+    def prefetch(self, k):
+        if 0 <= k < len(self.units) and k not in self.prefetched and k not in self.bwd_cache:
+            self.prefetched[k] = self._issue(k)
+
+    # ---- backward re-gather (saved-tensor hooks)
+    def pack(self, t):
+        if not isinstance(t, torch.Tensor) or t.device.type == "meta":
+            return t
+        hit = self.storage.get(t.untyped_storage().data_ptr())
+        if hit is None:
+            return t
+        base = t._base if t._base is not None else t
+        return ("_p2_stage3", hit[0], hit[1], tuple(t.size()), tuple(t.stride()),
+                t.storage_offset() - base.storage_offset(), t.requires_grad)
+
+    def unpack(self, x):
+        if not (isinstance(x, tuple) and x and x[0] == "_p2_stage3"):
+            return x
+        _, k, i, size, stride, off, _rg = x
+        if k not in self.bwd_cache:
+            self.bwd_cache[k] = self.materialize(k)
+            self.prefetch(k - 1)   # one unit ahead in backward order
+        return torch.as_strided(self.bwd_cache[k][i], size, stride, off)
+
+    def release_bwd(self, k):
+        self.bwd_cache.pop(k, None)
+
+    def reduce_async(self, k, grads):
+        for p, g in zip(self.units[k], grads):
+            g = torch.zeros(self.shapes[p.name], dtype=p._t.dtype, device=p._t.device) if g is None else g.contiguous()
+            w = dist.reduce(g, dst=self.row[self.owners[p.name]], group=self.group, async_op=True)
+            self.pending.append((w, g, p))
+
+
+class _GatherUnit(torch.autograd.Function):
+    """Forward: the full parameters of unit k (broadcast from their owners; unit k + 1 is prefetched).  Backward:
+    drops the unit's re-gathered copy and issues the gradient reduce to the owners asynchronously (it overlaps the
+    rest of the backward; the sharded step waits for it) — the parameters themselves get no autograd gradient."""
+
+    @staticmethod
+    def forward(ctx, state, k, *params):
+        ctx.state, ctx.k, ctx.n = state, k, len(params)
+        outs = state.materialize(k)
+        state.prefetch(k + 1)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        ctx.state.release_bwd(ctx.k)
+        ctx.state.reduce_async(ctx.k, grads)
+        return (None, None) + (None,) * ctx.n
+
+
+def _sharding_stage3(dmp, mesh_dim, group, n, me, row):
+    """Stage 3 with per-use parameter gathers (reference auto_parallel_sharding.py:584-700 broadcast-before-use /
+    free-after-use, :761 / :938 fused + overlapped parameter comm, :1192 overlapped gradient comm):
+
+    * parameters are grouped into units by their first forward consumer; ONE gather op per unit is inserted right
+      before that consumer and every forward use reads its output — a rank holds 1/n of the parameters plus the
+      gathered unit(s) in flight (the next unit is prefetched asynchronously), and each gathered copy dies after its
+      last forward reader (the executor drops it; the autograd graph keeps a token, not the tensor);
+    * the backward re-gathers a unit when its first saved tensor is unpacked (one unit of prefetch in backward
+      order) and drops it when the unit's gather node runs, which also issues the gradient reduce to the owners
+      asynchronously — overlapped with the rest of the backward;
+    * the sharded step waits for the reduces, steps the owned parameters and leaves the others released."""
+    from ....static.graph import Op, VarRef
+
+    prog = dmp.program
+    i_bwd = next((i for i, o in enumerate(prog.ops) if o.kind in ("backward", "grad")), len(prog.ops))
+    opt_ops = [(i, o) for i, o in enumerate(prog.ops) if o.kind == "optimize"]
+    owners, shapes, plist = {}, {}, []
+    for _, op in opt_ops:
+        opt = op.attrs["optimizer"]
+        load = [0] * n
+        for p in sorted(opt._parameter_list, key=lambda q: -q._t.numel()):
+            o = min(range(n), key=lambda r: load[r])
+            owners[p.name] = o
+            load[o] += p._t.numel()
+            shapes[p.name] = tuple(p._t.shape)
+            plist.append(p)
+    by_id = {id(p._t): p for p in plist}
+    # units: parameters grouped by their first forward consumer, in program order
+    first, units = {}, []
+    for i in range(i_bwd):
+        op = prog.ops[i]
+        if op.kind not in ("torch", "native"):
+            continue
+        for x in pytree.tree_leaves((op.args, op.kwargs)):
+            p = by_id.get(id(x)) if isinstance(x, torch.Tensor) else None
+            if p is not None and p.name not in first:
+                first[p.name] = i
+    for i in sorted(set(first.values())):
+        units.append((i, [p for p in plist if first.get(p.name) == i]))
+    state = _Stage3State([u for _, u in units], owners, row, group, me)
+    state.shapes = shapes
+    # gather ops (inserted back to front so indices stay valid) and forward uses rewired to their outputs
+    out_of = {}
+    gather_ops = []
+    for k, (i, ps) in enumerate(units):
+        vs = [_new_var(prog, shapes[p.name], p._t.dtype) for p in ps]
+        for p, v in zip(ps, vs):
+            out_of[id(p._t)] = v._vid
+
+        def gather(*params, k=k):
+            return _GatherUnit.apply(state, k, *params)
+
+        gather_ops.append((i, Op("torch", _named(gather, f"stage3_gather[{k}]", comm=True, stage3=True),
+                                 tuple(p._t for p in ps), {}, [v._vid for v in vs])))
+    for i in range(i_bwd):
+        op = prog.ops[i]
+        if op.kind not in ("torch", "native"):
+            continue
+        swap = lambda x: VarRef(out_of[id(x)]) if isinstance(x, torch.Tensor) and id(x) in out_of else x  # noqa: E731
+        op.args = pytree.tree_map(swap, op.args)
+        op.kwargs = pytree.tree_map(swap, op.kwargs)
+
+    def hooks_on(env):
+        state.hooks = torch.autograd.graph.saved_tensors_hooks(state.pack, state.unpack)
+        state.hooks.__enter__()
+
+    def hooks_off(env):
+        if state.hooks is not None:
+            state.hooks.__exit__(None, None, None)
+            state.hooks = None
+
+    for i, op in opt_ops:
+        opt = op.attrs["optimizer"]
+        mine = [p for p in opt._parameter_list if owners[p.name] == me]
+
+        def step(env, opt=opt, mine=mine):
+            full = opt._parameter_list
+            with torch.no_grad():
+                for w, g, p in state.pending:
+                    w.wait()
+                    if owners[p.name] == me:
+                        p._t.grad = g if p._t.grad is None else p._t.grad + g
+                state.pending.clear()
+                state.bwd_cache.clear()
+                state.prefetched.clear()
+                opt._parameter_list, opt._mt_cache = mine, None
+                try:
+                    opt.step()
+                finally:
+                    opt._parameter_list, opt._mt_cache = full, None
+                for p in full:
+                    if owners[p.name] != me and p._t.numel():
+                        p._t.data = torch.empty(0, dtype=p._t.dtype, device=p._t.device)
+            opt.clear_grad(set_to_zero=False)
+
+        prog.ops[i] = Op("call", None, (), {}, [], {"fn": step, "name": "sharding_stage3_step", "optimizer": opt})
+    prog.ops.insert(i_bwd, Op("call", None, (), {}, [], {"fn": hooks_off, "name": "sharding_stage3_hooks_off"}))
+    for i, op in sorted(gather_ops, key=lambda t: -t[0]):
+        prog.ops.insert(i, op)
+    prog.ops.insert(0, Op("call", None, (), {}, [], {"fn": hooks_on, "name": "sharding_stage3_hooks_on"}))
+
+    def gather_params(env=None):
+        """re-materialise every parameter from its owner into the parameters themselves (checkpointing)."""
+        with torch.no_grad():
+            for p in plist:
+                if tuple(p._t.shape) != shapes[p.name]:
+                    p._t.data = torch.empty(shapes[p.name], dtype=p._t.dtype, device=p._t.device)
+            for o in range(n):
+                ps = [p._t for p in plist if owners[p.name] == o]
+                if ps:
+                    _coalesced_broadcast(ps, row[o], group)
+
+    with torch.no_grad():   # stage 3 starts from the released state: a rank holds only its own parameters
+        for p in plist:
+            if owners[p.name] != me:
+                p._t.data = torch.empty(0, dtype=p._t.dtype, device=p._t.device)
+    dmp.gather_params = gather_params
+    dmp.stage3_state = state
+    return owners
+
+
 def sharding_pass(dmp, mesh_dim=0, stage=1):
     """ZeRO over ``mesh_dim`` (reference python/paddle/distributed/passes/auto_parallel_sharding.py:92-740
     ``ShardingPass``, stages 1 / 2 / 3).  Parameters are assigned to owners greedily by size.
@@ -260,9 +486,10 @@ def sharding_pass(dmp, mesh_dim=0, stage=1):
       ``mesh_dim`` (the plan's ``c_identity`` ops, or a fused all-reduce from ``fuse_allreduce_pass``) are removed;
       at the step every owner's gradients are reduced to it in one coalesced ``reduce`` (half the bytes of the
       all-reduce) and the other ranks drop theirs;
-    * stage 3 — + parameters sharded: after the step a rank keeps only the parameters it owns (the others'
-      storage is released); the program's first op re-materialises them by one coalesced broadcast per owner, so
-      between steps every rank holds 1/n of the replicated parameters.
+    * stage 3 — + parameters sharded, gathered per use (_sharding_stage3): one gather op per unit right before
+      its first forward consumer, next unit prefetched, backward re-gathers through saved-tensor hooks, gradient
+      reduces to the owners issued asynchronously from the backward; a rank holds 1/n of the parameters plus the
+      unit(s) in flight, during the step as between steps.
     -> {param name: owner}; ``dmp.gather_params()`` materialises every parameter (e.g. before a checkpoint)."""
     from ....static.graph import Op
 
@@ -283,6 +510,8 @@ def sharding_pass(dmp, mesh_dim=0, stage=1):
                 rest = tuple(d for d in fn.dims if d != mesh_dim)
                 op.fn = _grad_allreduce_fn(fn.mesh, rest) if rest else _named(lambda x: x, "identity")
         prog.ops = [o for o in prog.ops if not (o.kind == "call" and o.attrs.get("name") == "fused_allreduce_grads")]
+    if stage == 3:
+        return _sharding_stage3(dmp, mesh_dim, group, n, me, row)
     owners, released = {}, []
     for i, op in enumerate(prog.ops):
         if op.kind != "optimize":

@@ -169,7 +169,7 @@ def test_resharder_dist_main_program_trains_like_serial(mode):
 
 @pytest.mark.parametrize("passes", ["fuse", "merge", "recompute", "sharding", "fuse,sharding", "amp", "fuse,merge",
                                     "merge,fuse", "sharding2", "fuse,sharding2", "sharding3", "spopt", "overlap",
-                                    "spopt,overlap", "amp,spopt"])
+                                    "spopt,overlap", "amp,spopt", "sharding3,deep"])
 def test_static_passes_train_like_serial(passes):
     """Passes over the dist_main_program of a data-parallel plan (2 ranks, Adam): fused + bucketed gradient
     all-reduce, gradient merge (k = 2), recompute of an op range, sharding stage 1 (each rank holds the optimizer
@@ -194,6 +194,13 @@ def test_static_passes_train_like_serial(passes):
             assert "c_identity" not in o["comm_after"] and "c_identity" in o["comm_before"], o
         if passes == "sharding3":   # between steps a rank holds only the parameters it owns
             assert 0 < o["released"] < o["n_params_total"], o
+        if passes == "sharding3,deep":
+            # per-use gathers: during the step at most the unit in use + one prefetched + one re-gathered in the
+            # backward are live — a small share of the 8-layer model, not the whole of it
+            assert o["stage3_units"] >= 8, o
+            assert o["stage3_peak"] <= 4 * o["unit_bytes"] < o["total_bytes"] / 2, o
+            # each unit gathered once in the forward and once in the backward per step (4 steps)
+            assert o["stage3_gathers"] <= 4 * 2 * o["stage3_units"], o
         if "spopt" in passes:       # all-reduce -> row-local ops -> split became ONE reduce-scatter
             assert o["spopt"] >= 1 and "c_reducescatter" in o["comm_after"], o
             assert "c_allreduce_sum" in o["comm_before"] and "c_allreduce_sum" not in o["comm_after"], o

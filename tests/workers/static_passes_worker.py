@@ -49,9 +49,25 @@ class TPMLP(paddle.nn.Layer):
         return (self.fc3(h) - y).pow(2).mean()
 
 
+class DeepMLP(paddle.nn.Layer):
+    """8 equal layers: stage 3's per-use gathers must keep only a few of them gathered at a time"""
+
+    def __init__(self):
+        super().__init__()
+        self.fcs = paddle.nn.LayerList([paddle.nn.Linear(8, 8) for _ in range(8)])
+
+    def forward(self, x):
+        for fc in self.fcs:
+            x = paddle.nn.functional.gelu(fc(x))
+        return x.pow(2).mean()
+
+
 tp = any(p_ in ("spopt", "overlap") for p_ in passes)
 paddle.seed(0)
-net, ref = (TPMLP(), TPMLP()) if tp else (MLP(), MLP())
+if "deep" in passes:
+    net, ref = DeepMLP(), DeepMLP()
+else:
+    net, ref = (TPMLP(), TPMLP()) if tp else (MLP(), MLP())
 ref.set_state_dict(net.state_dict())
 main = paddle.static.Program()
 paddle.enable_static()
@@ -116,6 +132,15 @@ for i in range(4):
     ref_losses.append(float(rl.numpy()))
 out["losses"], out["ref"] = losses, ref_losses
 if any(f"sharding{st}" in passes for st in (2, 3)):
+    st3 = getattr(dmp, "stage3_state", None)
+    if st3 is not None:
+        nb = lambda p: p._t.numel() * p._t.element_size()  # noqa: E731
+        out["stage3_peak"] = st3.peak
+        out["stage3_gathers"] = st3.n_gathers
+        out["stage3_units"] = len(st3.units)
+        out["own_bytes"] = sum(nb(p) for p in net.parameters() if p._t.numel())
+        out["unit_bytes"] = max(sum(4 * int(np.prod(st3.shapes[p.name])) for p in u) for u in st3.units)
+        out["total_bytes"] = sum(4 * int(np.prod(v)) for v in st3.shapes.values())
     out["released"] = sum(1 for p in net.parameters() if p._t.numel() == 0)
     out["n_params_total"] = len(list(net.parameters()))
     dmp.gather_params()
