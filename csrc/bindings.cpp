@@ -101,6 +101,8 @@ int pd_flash_fwd(int, const void*, const void*, const void*, void*, float*, int,
                  long, long, float, int, void*);
 int pd_flash_bwd_block(int);
 void pd_flash_bwd_set_rope(const float*, const float*);
+long pd_flash_ds_elems(int, int, int, int, int, int);
+void pd_flash_bwd_set_ds(void*);
 int pd_flash_bwd(int, const void*, const void*, const void*, const void*, const void*, const float*, float*, void*,
                  void*, void*, float*, int, int, int, int, int, int, long, long, long, long, long, long, long, float,
                  int, void*);
@@ -364,6 +366,10 @@ PYBIND11_MODULE(_C, m) {
     check(pd_cast_from_f32(dt, P<const float*>(src), P<void*>(dst), n, P<void*>(st)), "cast_from_f32");
   });
   m.def("flash_bwd_block", [](int D) { return pd_flash_bwd_block(D); });
+  m.def("flash_ds_elems", [](int B, int Sq, int Sk, int Hq, int D, int causal) {
+    return pd_flash_ds_elems(B, Sq, Sk, Hq, D, causal);
+  });
+  m.def("flash_bwd_set_ds", [](uintptr_t ds) { pd_flash_bwd_set_ds(P<void*>(ds)); });
   m.def("flash_bwd_set_rope", [](uintptr_t cos, uintptr_t sin) {
     pd_flash_bwd_set_rope(P<const float*>(cos), P<const float*>(sin));
   });

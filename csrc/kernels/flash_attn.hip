@@ -39,6 +39,8 @@
 //    current step computes (T14 issue-early / write-late).
 #include "common.h"
 
+#include <algorithm>
+#include <cstring>
 #include <type_traits>
 
 namespace pd {
@@ -63,6 +65,15 @@ template <int D>
 __device__ __forceinline__ int tile_off(int row, int col) {
   constexpr int NCH = D / 8;
   return row * (D * 2) + swz(row, col >> 3, NCH) * 16 + (col & 7) * 2;
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not its global memory ops.
+// __syncthreads() is a release fence as well, so hipcc puts s_waitcnt vmcnt(0) in front of it — every in-flight
+// global load (prefetch) and store of the wave would drain at each barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 __device__ __forceinline__ bf16x8 lds_b128(const char* base, int off) {
@@ -149,6 +160,15 @@ struct Ext {
   // tables (first 64 columns used), position = token index within its sequence.
   const float* rope_cos;
   const float* rope_sin;
+  // split-dQ mode (dense): the backward stores dS (bf16, unscaled) per (q tile, key block) into this compact
+  // buffer instead of running the dQ phase; dq_gemm_kernel then computes dQ = scale * dS . K.  Layout per
+  // (b, hq): key block kb owns tiles t >= tb(kb) (tb = q_begin / 32), one [BNK/32 key slices][32 q][32 keys] block
+  // each (slice w = wave w's keys, written as 2 KB contiguous), key blocks in order:
+  // elem = (b*Hq + hq) * ds_per_bh + base(kb) + (t - tb(kb)) * 32 * BNK + (key / 32) * 1024 + [fragment order:
+  // ((key % 32) / 16) * 512 + ((key / 8) & 1) * 256 + row * 8 + key % 8]
+  bf16* ds_out;
+  long ds_per_bh;
+  int pair_order;       // bwd: dispatch a (b, kv head) pair's key blocks together on one XCD (needs Hk*B % 8 == 0)
 };
 
 // Counter-based dropout mask: a stateless 32-bit hash of (seed, batch*head, query, key), so the backward
@@ -585,7 +605,7 @@ constexpr int bwd_waves() { return D > 128 ? 4 : 8; }
 // NWB = 4 at D = 128 (dense, atomic dQ): 128-key blocks, two 256-thread workgroups per CU instead of one 512-thread
 // one — the two workgroups' barriers are independent, so SIMD partners drift apart and one wave's exp / dS VALU runs
 // beside the other's MFMAs instead of colliding with them; every wave takes a dQ slice (4 slices, 4 waves)
-template <int D, bool CAUSAL, int MODE, bool DROP, bool F16, int NWB = bwd_waves<D>()>
+template <int D, bool CAUSAL, int MODE, bool DROP, bool F16, int NWB = bwd_waves<D>(), bool DQS = false>
 __global__ __launch_bounds__(NWB * 64, (NWB == 4 && D <= 128) ? 2 : 1) void bwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ Vv, const bf16* __restrict__ dO,
                                                      const float* __restrict__ LSE, const float* __restrict__ DELTA,
@@ -614,9 +634,17 @@ __global__ __launch_bounds__(NWB * 64, (NWB == 4 && D <= 128) ? 2 : 1) void bwd_
   float* del_s = lse_s + BMQ;
   char* kimg = smem + KOFF;
 
-  // heaviest (lowest, under the causal mask) key blocks first, round-robin over the XCDs
-  const int kblk = blockIdx.x / (Hk * B);
-  const int rest = blockIdx.x % (Hk * B);
+  // heaviest (lowest, under the causal mask) key blocks first, round-robin over the XCDs.  Ext::pair_order: the key
+  // blocks of one (b, kv head) pair are dispatched together onto one XCD (pair = (bid / 8 / nkb) * 8 + bid % 8), so
+  // the pair's Q / dO tiles are re-read from that XCD's L2 instead of from HBM by every key block
+  int kblk = blockIdx.x / (Hk * B);
+  int rest = blockIdx.x % (Hk * B);
+  if (ex.pair_order) {
+    const int nkb_all = gridDim.x / (Hk * B);
+    const int j = blockIdx.x / 8;
+    rest = (j / nkb_all) * 8 + blockIdx.x % 8;
+    kblk = j % nkb_all;
+  }
   const int hk = rest % Hk;
   const int b = rest / Hk;
   const int group = Hq / Hk;
@@ -749,6 +777,34 @@ __global__ __launch_bounds__(NWB * 64, (NWB == 4 && D <= 128) ? 2 : 1) void bwd_
   int o_srow = r * (BNK * 2) + (((h ^ msk(r)) & (SNCH - 1)) << 4);
   int o_scol = 4 * h * (BNK * 2) + ((((lkey >> 3) ^ h) & (SNCH - 1)) << 4) + ((lkey & 7) << 1);
 
+  // split-dQ mode: this key block's first dS block within a (b, hq) region (sum over the earlier key blocks)
+  // (a compile-time variant: as a runtime branch the two dQ paths shared one register allocation and one waitcnt
+  // state at the loop head, and the split path's head waited for its own dS stores)
+  static_assert(!DQS || MODE == kDense, "split dQ is a dense-mode path");
+  constexpr bool ds_split = DQS;
+  long ds_kb_base = 0;
+  if constexpr (MODE == kDense) {
+    if (ex.ds_out != nullptr) {
+      const int nqt_all = (Sq + BMQ - 1) / BMQ;
+      for (int k2 = 0; k2 < kblk; ++k2) {
+        const int tb = CAUSAL ? max(0, k2 * BNK - off) / BMQ : 0;
+        ds_kb_base += (long)max(0, nqt_all - tb) * (BMQ * BNK);
+      }
+    }
+  }
+
+  bf16* pend_ds = nullptr;        // split-dQ: this wave's parked dS slice goes here at the next step's head
+  auto flush_ds = [&]() {
+    if (pend_ds == nullptr) return;
+    const char* wimg = simg + wv * (BMQ * 32 * 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = lane + 64 * j;
+      const u16x8 v = *reinterpret_cast<const u16x8*>(wimg + ((c ^ ((c >> 5) & 3)) << 4));
+      __builtin_nontemporal_store(v, reinterpret_cast<u16x8*>(pend_ds + c * 8));
+    }
+    pend_ds = nullptr;
+  };
   int pend_hq = -1, pend_q0 = 0;  // deferred dQ tile (wave-uniform); pend_hq < 0: none
   auto flush_dq = [&]() {
     if constexpr (MODE == kDense) {
@@ -801,6 +857,7 @@ __global__ __launch_bounds__(NWB * 64, (NWB == 4 && D <= 128) ? 2 : 1) void bwd_
       }
     }
     __syncthreads();
+    flush_ds();  // the previous step's dS slice (split-dQ; a step ahead of the next barrier's vmcnt(0) drain)
     flush_dq();  // the previous step's dQ atomics: issued after this step's staging wait, before the next prefetch
     const int step_next = next_step(step + 1);
     if (step_next < ntot) gload(step_next);  // lands while this step computes
@@ -859,6 +916,33 @@ __global__ __launch_bounds__(NWB * 64, (NWB == 4 && D <= 128) ? 2 : 1) void bwd_
       }
     }
     if (MODE == kDense && ex.dq_atomic == 3) {  // ablation: no dQ phase
+      step = step_next;
+      continue;
+    }
+    if (ds_split && ex.dq_atomic == 5) {   // bench-only ablation: dS computed, never stored
+      asm volatile("" ::"v"(dpacc));
+      step = step_next;
+      continue;
+    }
+    if (ds_split) {
+      // split-dQ: the wave transposes its [32 q][32 keys] dS slice through a PRIVATE 2-KB LDS region (its share of
+      // the dS image; no workgroup barrier); the 2 KB leave as 16-B stores at the NEXT step's head, after that
+      // step's staging wait (stores count in vmcnt: issued here, they made the head's wait for the prefetched Q / dO
+      // wait for them too) — no dQ MFMAs and no atomics in this kernel
+      // slice layout (global = LDS up to the swizzle): MFMA-fragment order for dq_gemm_kernel's B operand — 16-B
+      // unit u = (key / 16) * 64 + ((key / 8) & 1) * 32 + q holds keys 8 (u / 32) .. +8 of row q, so each of its
+      // fragment loads is one contiguous 1-KB wave read; in LDS unit u sits at u ^ ((u >> 5) & 3) (the four
+      // units one ds_write_b16 instruction touches land on different banks)
+      char* wimg = simg + wv * (BMQ * 32 * 2);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int q = (i & 3) + 8 * (i >> 2) + 4 * h;
+        const int u = (r >> 4) * 64 + ((r >> 3) & 1) * 32 + q;
+        *reinterpret_cast<unsigned short*>(wimg + ((u ^ ((u >> 5) & 3)) << 4) + (r & 7) * 2) = cvt16<F16>(dpacc[i]);
+      }
+      if (ex.dq_atomic != 4)   // 4: bench-only ablation, LDS transpose without the global stores
+        pend_ds = ex.ds_out + ((long)(b * Hq + hq)) * ex.ds_per_bh + ds_kb_base + (long)(step % nqt) * (BMQ * BNK) +
+                  wv * (BMQ * 32);
       step = step_next;
       continue;
     }
@@ -925,6 +1009,7 @@ __global__ __launch_bounds__(NWB * 64, (NWB == 4 && D <= 128) ? 2 : 1) void bwd_
     step = step_next;
   }
   flush_dq();
+  flush_ds();
   // write dK (scaled) and dV for this lane's key: accumulator row = d, column = key
   if (mykey < Sk) {
     bf16* dkr = dK + (kt0 + mykey) * sdk + hk * D;
@@ -968,6 +1053,194 @@ __global__ __launch_bounds__(NWB * 64, (NWB == 4 && D <= 128) ? 2 : 1) void bwd_
         vv.z = cvt16<F16>(dvacc[dt][4 * c + 2]); vv.w = cvt16<F16>(dvacc[dt][4 * c + 3]);
         if (!rope_t) *reinterpret_cast<ushort4*>(dkr + d) = kv;
         *reinterpret_cast<ushort4*>(dvr + d) = vv;
+      }
+    }
+  }
+}
+
+// Split-dQ second half (dense, D = 128, 256-key backward blocks): dQ = scale * dS . K from the compact dS buffer of
+// the backward, summed over key blocks in registers (fp32, fixed order: bitwise reproducible, no atomics), RoPE^T
+// and the bf16 store fused into the epilogue — no zeroed slab, no reduce pass.  Memory-bound on the dS read.
+// Workgroup: 4 waves x 32 query rows (one 32-row dS tile per wave) of one (b, hq).  Per 64-key step the K tile is
+// staged in LDS (register-staged, double-buffered, the forward's swizzled image, shared by the waves); each wave
+// computes the swapped product dQ^T[d][q] += K^T[d][k] . dS^T[k][q]: K^T fragments by transposed LDS reads (natural
+// k order), dS^T fragments straight from the wave's own dS rows (16 B per lane, one step ahead, buffer loads).
+template <bool F16, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void dq_gemm_kernel(const bf16* __restrict__ dS, const bf16* __restrict__ K,
+                                                        bf16* __restrict__ dQ, int B, int Sq, int Sk, int Hq, int Hk,
+                                                        long sk, long sdq, long per_bh, float scale,
+                                                        const float* __restrict__ rcos,
+                                                        const float* __restrict__ rsin) {
+  constexpr int D = 128, NCH = D / 8, BNK = 256, BN = 64, NT = 256, TILE = BN * D * 2;
+  constexpr int NLOAD = BN * NCH / NT;   // 4 chunks of 16 B per thread per K tile
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE];
+  const int off = Sk - Sq;
+  const int nqt_all = (Sq + 31) / 32;
+  const int nmb = (Sq + 127) / 128;
+  const int total = nmb * Hq * B;
+  const int w_id = xcd_remap(blockIdx.x, total);
+  int mb = w_id % nmb;
+  const int hq = (w_id / nmb) % Hq;
+  const int b = w_id / (nmb * Hq);
+  if (CAUSAL) mb = nmb - 1 - mb;   // heaviest query blocks first
+  const int hk = hq / (Hq / Hk);
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int t = mb * 4 + wv;       // this wave's dS tile (wave-uniform in SGPRs: scalar branches, buffer bases)
+  const int nkb = (Sk + BNK - 1) / BNK;
+  auto tb = [&](int kb) { return CAUSAL ? max(0, kb * BNK - off) / 32 : 0; };
+  // key blocks that wrote tile tt: tb(kb) <= tt (tb is non-decreasing)
+  auto nkb_of = [&](int tt) {
+    int n = 0;
+    for (int kb = 0; kb < nkb; ++kb)
+      if (tb(kb) <= tt) n = kb + 1;
+    return n;
+  };
+  const int my_nkb = t < nqt_all ? nkb_of(t) : 0;
+  const int wg_nkb = nkb_of(min(mb * 4 + 3, nqt_all - 1));
+  const int nsteps = wg_nkb * (BNK / BN);
+
+  const bf16* Kb = K + (long)b * Sk * sk + hk * D;
+  const bf16* dSb = dS + ((long)b * Hq + hq) * per_bh;
+
+  // every load below is issued unconditionally (a dead one gets num_records 0 and reads zeros): loads under a
+  // branch made the waitcnt pass merge states at the join and wait for the prefetch itself
+  int voff_k[NLOAD];
+#pragma unroll
+  for (int i = 0; i < NLOAD; ++i) {
+    const int c = tid + NT * i, row = c / NCH, ch = c % NCH;
+    voff_k[i] = row * (int)sk * 2 + ch * 16;
+  }
+  auto gload = [&](int st, bool live, u16x8 (&stk)[NLOAD]) {
+    const int n0 = st * BN;
+    const int nrows = live ? min(Sk - n0, BN) : 0;
+    const __amdgpu_buffer_rsrc_t rk = make_rsrc_u(Kb + (long)(live ? n0 : 0) * sk, nrows * (int)sk * 2);
+#pragma unroll
+    for (int i = 0; i < NLOAD; ++i)
+      stk[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rk, voff_k[i], 0, 0));
+  };
+  auto lstore = [&](int buf, const u16x8 (&stk)[NLOAD]) {
+    char* kt = smem + buf * TILE;
+#pragma unroll
+    for (int i = 0; i < NLOAD; ++i) {
+      const int c = tid + NT * i, row = c / NCH, ch = c % NCH;
+      *reinterpret_cast<u16x8*>(kt + row * (D * 2) + swz(row, ch, NCH) * 16) = stk[i];
+    }
+  };
+  // dS^T fragments of a step (two 32-key slices of the block, 4 KB contiguous, stored in fragment order by the
+  // backward): k-slice ks of lane l is 16 B at ks * 1 KB + l * 16 — one contiguous 1-KB read per fragment
+  int lkb = 0;
+  long lbase = 0;   // load cursor: key block and its base in the (b, hq) region
+  const int voff_ds = lane * 16;
+  auto load_ds = [&](int st, bool live, bf16x8 (&dst)[4]) {
+    const int kb = st / (BNK / BN);
+    while (lkb < kb) {
+      lbase += (long)max(0, nqt_all - tb(lkb)) * (32 * BNK);
+      ++lkb;
+    }
+    const bool ok = live && kb < my_nkb;
+    const bf16* p = dSb + (ok ? lbase + (long)(t - tb(kb)) * (32 * BNK) + (st % (BNK / BN)) * (BN * 32) : 0);
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc_u(p, ok ? BN * 32 * 2 : 0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      dst[ks] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rd, voff_ds + ks * 1024, 0, 0));
+  };
+  // transposed K^T reads, natural k order: rows 16 ks + 8 hh + qq (+4), 16-B chunk 4 dt + cbits
+  auto mm = [](int row) { return ((row & 3) << 2) | ((row >> 2) & 3); };
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3, hh = g >> 1;
+  const int cbits = ((g & 1) << 1) | (pp >> 1);
+  const int ra = 8 * hh + qq, rb = ra + 4;
+  int o_a = ra * (D * 2) + (((cbits ^ mm(ra)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
+  int o_b = rb * (D * 2) + (((cbits ^ mm(rb)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) acc[dt] = f32x16{};
+  // everything streams two steps ahead: K tiles in two register sets (tile st + 1 goes to LDS at the end of step st,
+  // tile st + 2 is loaded during it), dS fragments in three sets (step st multiplies set st % 3 while st + 1 and
+  // st + 2 are in flight) — named sets, no register copies (a copy would wait for the prefetch)
+  bf16x8 dsa[4], dsb[4], dsc[4];
+  u16x8 ka[NLOAD], kb2[NLOAD];
+  gload(0, nsteps > 0, ka);
+  gload(1, nsteps > 1, kb2);
+  load_ds(0, nsteps > 0, dsa);
+  load_ds(1, nsteps > 1, dsb);
+  lstore(0, ka);
+  lds_barrier();
+  // one 64-key step: K tile st + 2 into `kn`, dS fragments of step st + 2 into `nxt2`, 16 MFMAs on `cur`
+  // (accumulator-major: each K^T fragment is read one MFMA ahead), then K tile st + 1 (`k1`) into the other stage
+  auto body = [&](int st, bf16x8 (&cur)[4], bf16x8 (&nxt2)[4], u16x8 (&k1)[NLOAD], u16x8 (&kn)[NLOAD]) {
+    const int buf = st & 1;
+    gload(st + 2, st + 2 < nsteps, kn);
+    load_ds(st + 2, st + 2 < nsteps, nxt2);
+    asm volatile("" : "+v"(o_a), "+v"(o_b));
+    if (st / (BNK / BN) < my_nkb) {   // wave-uniform: this wave's tile was written by this key block
+      const char* kt = smem + buf * TILE;
+      auto rdA = [&](int dt, int ks) {
+        const char* kr = kt + 16 * ks * (D * 2);
+        return cat4(lds_tr(kr, o_a ^ (dt << 6)), lds_tr(kr, o_b ^ (dt << 6)));
+      };
+      bf16x8 af[2];
+      af[0] = rdA(0, 0);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int dt = j >> 2, ks = j & 3;
+        if (j < 15) af[(j + 1) & 1] = rdA((j + 1) >> 2, (j + 1) & 3);
+        acc[dt] = mfma<F16>(af[j & 1], cur[ks], acc[dt]);
+      }
+    }
+    lstore(buf ^ 1, k1);   // (dead on the last step: zeros into the idle stage)
+    lds_barrier();         // the later K / dS loads stay in flight across it
+  };
+  // K set of step st + 1: ka for odd st + 1, kb2 for even ... (tile t lives in ka if t even, kb2 if t odd)
+  for (int st = 0; st < nsteps; st += 6) {
+    body(st, dsa, dsc, kb2, ka);
+    if (st + 1 < nsteps) body(st + 1, dsb, dsa, ka, kb2);
+    if (st + 2 < nsteps) body(st + 2, dsc, dsb, kb2, ka);
+    if (st + 3 < nsteps) body(st + 3, dsa, dsc, ka, kb2);
+    if (st + 4 < nsteps) body(st + 4, dsb, dsa, kb2, ka);
+    if (st + 5 < nsteps) body(st + 5, dsc, dsb, ka, kb2);
+  }
+
+  // epilogue: lane = query row q, accumulator rows = d (32 dt + 8 c + 4 h + e)
+  const int q = t * 32 + r;
+  if (t >= nqt_all || q >= Sq) return;
+  bf16* orow = dQ + ((long)b * Sq + q) * sdq + hq * D;
+  if (rcos != nullptr) {
+    // RoPE^T: dims d and d + 64 (slices dt and dt + 2) of this lane's row rotate back together
+    const float* cr = rcos + (long)q * 128;
+    const float* sr = rsin + (long)q * 128;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int d = dt * 32 + 8 * c + 4 * h;
+        const float4 cv = *reinterpret_cast<const float4*>(cr + d);
+        const float4 sv = *reinterpret_cast<const float4*>(sr + d);
+        const float cc[4] = {cv.x, cv.y, cv.z, cv.w}, sn[4] = {sv.x, sv.y, sv.z, sv.w};
+        unsigned short lo16[4], hi16[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float lo = acc[dt][4 * c + e] * scale, hi = acc[dt + 2][4 * c + e] * scale;
+          lo16[e] = cvt16<F16>(lo * cc[e] + hi * sn[e]);
+          hi16[e] = cvt16<F16>(hi * cc[e] - lo * sn[e]);
+        }
+        *reinterpret_cast<ushort4*>(orow + d) = ushort4{lo16[0], lo16[1], lo16[2], lo16[3]};
+        *reinterpret_cast<ushort4*>(orow + d + 64) = ushort4{hi16[0], hi16[1], hi16[2], hi16[3]};
+      }
+    }
+  } else {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int d = dt * 32 + 8 * c + 4 * h;
+        ushort4 v;
+        v.x = cvt16<F16>(acc[dt][4 * c + 0] * scale);
+        v.y = cvt16<F16>(acc[dt][4 * c + 1] * scale);
+        v.z = cvt16<F16>(acc[dt][4 * c + 2] * scale);
+        v.w = cvt16<F16>(acc[dt][4 * c + 3] * scale);
+        *reinterpret_cast<ushort4*>(orow + d) = v;
       }
     }
   }
@@ -1122,6 +1395,18 @@ void launch_bwd(dim3 grid, hipStream_t st, const void* q, const void* k, const v
                 int mode, bool drop, const fa::Ext& ex, int nwb) {
   constexpr int NT = fa::bwd_waves<D>() * 64;
   if constexpr (D == 128) {
+    if (ex.ds_out != nullptr) {   // split dQ (dense, 8 waves): dS out, no dQ phase
+#define PD_FA_BWDS(CC, DR)                                                                                         \
+  fa::bwd_kernel<D, CC, fa::kDense, DR, F16, 8, true><<<grid, 512, 0, st>>>(                                      \
+      (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, dqp, (bf16*)dk, (bf16*)dv, B, \
+      Sq, Sk, Hq, Hk, sq, sk, sv, so, sdk, sdv, pslab, scale, ex)
+      if (drop) { if (causal) PD_FA_BWDS(true, true); else PD_FA_BWDS(false, true); }
+      else { if (causal) PD_FA_BWDS(true, false); else PD_FA_BWDS(false, false); }
+#undef PD_FA_BWDS
+      return;
+    }
+  }
+  if constexpr (D == 128) {
     if (nwb == 4) {   // dense, atomic dQ, no dropout (fa_bwd_waves)
 #define PD_FA_BWD4(CC)                                                                                              \
   fa::bwd_kernel<D, CC, fa::kDense, false, F16, 4><<<grid, 256, 0, st>>>(                                          \
@@ -1246,15 +1531,46 @@ extern "C" void pd_flash_bwd_set_rope(const float* cos, const float* sin) {
   t_bwd_rope_sin = sin;
 }
 
+// Split-dQ workspace (dense, D = 128): bf16 elements of the compact dS buffer per (b, hq) — every key block's
+// [32 q][256 keys] blocks for the 32-row query tiles it visits — or 0 where the split path does not apply.
+// Opt-in (PADDLE2_AMD_FA_DQ_SPLIT=1): a deterministic dQ without atomics or fp32 slabs.  At B8 S4096 H32 D128
+// causal it measured 4.5-5.2 ms per layer against 4.4-4.5 for the fused atomic path (profiles/r6_flash_dq_split.md):
+// the 4.6 GB of dS stores cost the main kernel ~0.6 ms of memory traffic and dq_gemm_kernel reads them back in
+// 1.1 ms, more than the atomics (0.8 ms) plus the fused dQ MFMAs (0.75 ms) they replace.
+static long fa_ds_per_bh(int Sq, int Sk, int D, int causal) {
+  if (D != 128) return 0;
+  const int BNK = 256, nqt = (Sq + 31) / 32, nkb = (Sk + BNK - 1) / BNK, off = Sk - Sq;
+  long n = 0;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int tb = causal ? std::max(0, kb * BNK - off) / 32 : 0;
+    n += (long)std::max(0, nqt - tb) * 32 * BNK;
+  }
+  return n;
+}
+extern "C" long pd_flash_ds_elems(int B, int Sq, int Sk, int Hq, int D, int causal) {
+  const char* e = getenv("PADDLE2_AMD_FA_DQ_SPLIT");
+  if (!e || atoi(e) == 0) return 0;
+  return (long)B * Hq * fa_ds_per_bh(Sq, Sk, D, causal);
+}
+// dS workspace for the next pd_flash_bwd_ext call on this thread (consumed by it; dense mode only)
+static thread_local void* t_bwd_ds = nullptr;
+extern "C" void pd_flash_bwd_set_ds(void* ds) { t_bwd_ds = ds; }
+
 extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void* v, const void* o, const void* dout,
                                 const float* lse, float* delta, void* dq, void* dk, void* dv, float* dqp, int B,
                                 int Sq, int Sk, int Hq, int Hk, int D, long sq, long sk, long sv, long so, long sdq,
                                 long sdk, long sdv, float scale, int causal, int mode, const int* cu_q, const int* cu_k,
                                 int total_q, const int* fm, const int* fm_t64, const int* fm_t256, int fm_hm,
                                 int drop, unsigned seed, float pdrop, void* stream) {
+  void* ds = t_bwd_ds;
+  t_bwd_ds = nullptr;
   if (int e = check_args(dt, D, Hq, Hk, mode, drop, pdrop, cu_q, cu_k, fm, fm_t256, fm_hm)) {
     t_bwd_rope_cos = t_bwd_rope_sin = nullptr;
     return e;
+  }
+  if (ds && (mode != 0 || D != 128)) {
+    t_bwd_rope_cos = t_bwd_rope_sin = nullptr;
+    return -5;
   }
   if (t_bwd_rope_cos && (mode != 0 || D != 128 || !t_bwd_rope_sin)) {
     t_bwd_rope_cos = t_bwd_rope_sin = nullptr;
@@ -1274,11 +1590,12 @@ extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void
     fa::bwd_delta_kernel<false><<<dgrid, 256, 0, st>>>((const bf16*)o, (const bf16*)dout, delta, dB, dS, Hq, D, so);
   // dense mode, atomic dQ: every key block adds into one zeroed fp32 slab (one slab of workspace, a convert
   // pass instead of the slab reduce: 0.27 ms less per B8 S4096 H32 D128 layer)
-  const bool atomic = mode == 0 && fa_dq_atomic();
-  const int nwb = fa_bwd_waves(D, mode, atomic, drop);
+  const bool split = ds != nullptr;   // dS out + dq_gemm_kernel (no dQ phase, no slab, no reduce)
+  const bool atomic = !split && mode == 0 && fa_dq_atomic();
+  const int nwb = split ? 8 : fa_bwd_waves(D, mode, atomic, drop);
   const int BNK = D == 128 && nwb == 4 ? 128 : pd_flash_bwd_block(D);
   const int nkb = (Sk + BNK - 1) / BNK;
-  const long pslab = atomic ? 0 : nrows * Hq * D;
+  const long pslab = (atomic || split) ? 0 : nrows * Hq * D;
   if (atomic) hipMemsetAsync(dqp, 0, nrows * Hq * D * sizeof(float), st);
   dim3 grid(nkb * Hk * B);
   fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm, seed,
@@ -1287,11 +1604,20 @@ extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void
   ex.rope_cos = t_bwd_rope_cos;
   ex.rope_sin = t_bwd_rope_sin;
   t_bwd_rope_cos = t_bwd_rope_sin = nullptr;
+  // PADDLE2_AMD_FA_BWD_ORDER = pair: co-dispatch a pair's key blocks (L2 reuse of Q / dO) instead of heaviest first
+  if (const char* e = getenv("PADDLE2_AMD_FA_BWD_ORDER"))
+    ex.pair_order = (strcmp(e, "pair") == 0 && (Hk * B) % 8 == 0) ? 1 : 0;
+  if (split) {
+    ex.ds_out = (bf16*)ds;
+    ex.ds_per_bh = fa_ds_per_bh(Sq, Sk, D, causal);
+    // the dK epilogue applies RoPE^T itself (ex.rope_cos); dQ's RoPE^T moves into dq_gemm_kernel
+  }
   // bench-only ablation (scripts/bench_flash_bwd.py; results are WRONG): 2 = compute dQ but skip its stores,
   // 3 = skip the whole dQ phase (dS image, barrier, dQ MFMAs, stores) — prices the dQ path in isolation
   if (const char* e = getenv("PADDLE2_AMD_FA_DEBUG_DQ_ABLATE")) {
     const int m = atoi(e);
     if (atomic && (m == 2 || m == 3)) ex.dq_atomic = m;
+    if (split && (m == 4 || m == 5)) ex.dq_atomic = m;   // split: 4 = no dS stores, 5 = no dS LDS image either
   }
 #define PD_BWD(DD, FF)                                                                                              \
   launch_bwd<DD, FF>(grid, st, q, k, v, dout, lse, delta, dqp, dk, dv, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, sdk, sdv, \
@@ -1300,6 +1626,17 @@ extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void
   else if (D == 64) { if (f16) PD_BWD(64, true); else PD_BWD(64, false); }
   else { if (f16) PD_BWD(256, true); else PD_BWD(256, false); }
 #undef PD_BWD
+  if (split) {
+    const int nmb = (Sq + 127) / 128;
+    const dim3 g2(nmb * Hq * B);
+#define PD_DQG(FF, CC)                                                                                              \
+  fa::dq_gemm_kernel<FF, CC><<<g2, 256, 0, st>>>((const bf16*)ds, (const bf16*)k, (bf16*)dq, B, Sq, Sk, Hq, Hk, sk, \
+                                                 sdq, ex.ds_per_bh, scale, ex.rope_cos, ex.rope_sin)
+    if (f16) { if (causal) PD_DQG(true, true); else PD_DQG(true, false); }
+    else { if (causal) PD_DQG(false, true); else PD_DQG(false, false); }
+#undef PD_DQG
+    return (int)hipGetLastError();
+  }
   long work = nrows * Hq * D / 8;
   long g = (work + 255) / 256;
   if (g > 8192) g = 8192;

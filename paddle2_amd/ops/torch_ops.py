@@ -1183,15 +1183,26 @@ def _flash_bwd_native(q, k, v, out, do, lse, dq, dk, dv, scale, causal, rope=Non
     Sk, Hk = k.shape[1], k.shape[2]
     bnk = _bwd_block(D)
     nkb = (Sk + bnk - 1) // bnk
-    # per-key-block dQ partials, or one atomically accumulated slab (same rule as fa_dq_atomic in flash_attn.hip)
-    slabs = 1 if dq_atomic() else nkb
-    dq32 = torch.empty(slabs * B * Sq * Hq * D, dtype=torch.float32, device=q.device)
+    # split dQ (opt-in PADDLE2_AMD_FA_DQ_SPLIT=1; dense, D = 128; flash_attn.hip dq_gemm_kernel): the backward
+    # stores dS into a compact bf16 buffer and a second kernel computes dQ = scale * dS . K — deterministic, no fp32
+    # dQ slab, no atomics (slower than the fused atomic default at the Llama shape: profiles/r6_flash_dq_split.md)
+    ds_n = N.native().flash_ds_elems(B, Sq, Sk, Hq, D, int(bool(causal)))
+    if ds_n > 0:
+        ds = torch.empty(ds_n, dtype=q.dtype, device=q.device)
+        dq32 = torch.empty(0, dtype=torch.float32, device=q.device)
+    else:
+        ds = None
+        # per-key-block dQ partials, or one atomically accumulated slab (same rule as fa_dq_atomic in flash_attn.hip)
+        slabs = 1 if dq_atomic() else nkb
+        dq32 = torch.empty(slabs * B * Sq * Hq * D, dtype=torch.float32, device=q.device)
     delta = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
     if rope is not None:
         cos, sin = rope
         assert D == 128 and cos.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous() and \
             cos.shape[-1] == 128 and cos.shape[0] >= max(Sq, Sk), "RoPE^T fold: fp32 [S, 128] tables, D = 128"
         N.native().flash_bwd_set_rope(cos.data_ptr(), sin.data_ptr())
+    if ds is not None:
+        N.native().flash_bwd_set_ds(ds.data_ptr())
     N.native().flash_bwd(_ATTN_DT[q.dtype], q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), do.data_ptr(), lse.data_ptr(),
                          delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dq32.data_ptr(), B, Sq, Sk,
                          Hq, Hk, D, q.stride(1), k.stride(1), v.stride(1), do.stride(1), dq.stride(1), dk.stride(1),

@@ -1,5 +1,6 @@
-"""Flash backward dQ-path ablation at the Llama-2-7B shape (B8 S4096 H32 D128 causal): normal atomic dQ, per-key-
-block slabs (deterministic), dQ computed but not stored, no dQ phase at all.  Prices the dQ traffic."""
+"""Flash backward dQ-path comparison at the Llama-2-7B shape (B8 S4096 H32 D128 causal): split dQ (dS stored,
+dq_gemm_kernel; the default), fused atomic dQ, per-key-block slabs (deterministic fused), and the bench-only
+ablations of the fused kernel (dQ computed but not stored; no dQ phase at all)."""
 import json
 import os
 import sys
@@ -17,10 +18,18 @@ scale = D ** -0.5
 out, lse = T._flash_fwd_native(q, k, v, True, scale)
 dq, dk, dv = (torch.empty_like(q) for _ in range(3))
 flops = 2.5 * 4 * B * H * S * S * D / 2
-for name, env in (("atomic", {}), ("slabs", {"PADDLE2_AMD_FA_DQ_ATOMIC": "0"}),
-                  ("no_dq_store", {"PADDLE2_AMD_FA_DEBUG_DQ_ABLATE": "2"}),
-                  ("no_dq_phase", {"PADDLE2_AMD_FA_DEBUG_DQ_ABLATE": "3"})):
-    for kk in ("PADDLE2_AMD_FA_DQ_ATOMIC", "PADDLE2_AMD_FA_DEBUG_DQ_ABLATE"):
+KEYS = ("PADDLE2_AMD_FA_DQ_ATOMIC", "PADDLE2_AMD_FA_DEBUG_DQ_ABLATE", "PADDLE2_AMD_FA_DQ_SPLIT",
+        "PADDLE2_AMD_FA_BWD_ORDER")
+SPLIT = {"PADDLE2_AMD_FA_DQ_SPLIT": "1"}
+for name, env in (("split", SPLIT), ("atomic", {"PADDLE2_AMD_FA_DQ_SPLIT": "0"}),
+                  ("split_no_ds_store", {**SPLIT, "PADDLE2_AMD_FA_DEBUG_DQ_ABLATE": "4"}),
+                  ("split_no_ds", {**SPLIT, "PADDLE2_AMD_FA_DEBUG_DQ_ABLATE": "5"}),
+                  ("split_pair", {**SPLIT, "PADDLE2_AMD_FA_BWD_ORDER": "pair"}),
+                  ("atomic_pair", {"PADDLE2_AMD_FA_DQ_SPLIT": "0", "PADDLE2_AMD_FA_BWD_ORDER": "pair"}),
+                  ("slabs", {"PADDLE2_AMD_FA_DQ_SPLIT": "0", "PADDLE2_AMD_FA_DQ_ATOMIC": "0"}),
+                  ("no_dq_store", {"PADDLE2_AMD_FA_DQ_SPLIT": "0", "PADDLE2_AMD_FA_DEBUG_DQ_ABLATE": "2"}),
+                  ("no_dq_phase", {"PADDLE2_AMD_FA_DQ_SPLIT": "0", "PADDLE2_AMD_FA_DEBUG_DQ_ABLATE": "3"})):
+    for kk in KEYS:
         os.environ.pop(kk, None)
     os.environ.update(env)
 
