@@ -335,6 +335,64 @@ class _Stage3State:
             self.pending.append((w, g, p))
 
 
+class _Stage2Buckets:
+    """Stage 2's gradient reduces issued FROM the backward: each parameter's post-accumulate hook marks it ready;
+    a bucket (one owner's parameters, in reverse order of first forward use, up to ``cap`` bytes) is flattened and
+    reduced to its owner asynchronously as soon as all its members are ready, so the reduces overlap the rest of
+    the backward; the sharded step waits for them (reference auto_parallel_sharding.py:1192 fused + overlapped
+    gradient comm)."""
+
+    def __init__(self, buckets, owners, row, group, me):
+        self.buckets, self.owners, self.row, self.group, self.me = buckets, owners, row, group, me
+        self.bucket_of = {id(p._t): bi for bi, b in enumerate(buckets) for p in b}
+        self.ready = [set() for _ in buckets]
+        self.pending = []             # (work, flat, bucket index)
+        self.acc = {}                 # owner: parameter name -> reduced gradient summed over backwards
+        self.issued = 0
+        self.from_backward = 0        # reduces launched by the hooks, i.e. while the backward was still running
+
+    def hook(self, t):
+        bi = self.bucket_of.get(id(t))
+        if bi is None:
+            return
+        self.ready[bi].add(id(t))
+        if len(self.ready[bi]) == len(self.buckets[bi]):
+            self._launch(bi)
+
+    def _launch(self, bi):
+        ps = self.buckets[bi]
+        with torch.no_grad():
+            flat = torch.cat([(p._t.grad if p._t.grad is not None else torch.zeros_like(p._t)).reshape(-1)
+                              for p in ps])
+            for p in ps:
+                p._t.grad = None      # consumed: the next backward (gradient merge) accumulates afresh
+        w = dist.reduce(flat, dst=self.row[self.owners[ps[0].name]], group=self.group, async_op=True)
+        self.pending.append((w, flat, bi))
+        self.ready[bi] = set()
+        self.issued += 1
+
+    def settle(self):
+        """Wait for every reduce (launching buckets a backward left partly ready, in bucket order — the same on
+        every rank), then hand the owners their summed gradients."""
+        self.from_backward += len(self.pending)
+        for bi, r in enumerate(self.ready):
+            if r:
+                self._launch(bi)
+        for w, flat, bi in self.pending:
+            w.wait()
+            ps = self.buckets[bi]
+            if self.owners[ps[0].name] == self.me:
+                off = 0
+                for p in ps:
+                    k = p._t.numel()
+                    g = flat[off:off + k].view_as(p._t)
+                    self.acc[p.name] = g if p.name not in self.acc else self.acc[p.name] + g
+                    off += k
+        self.pending.clear()
+        out, self.acc = self.acc, {}
+        return out
+
+
 class _GatherUnit(torch.autograd.Function):
     """Forward: the full parameters of unit k (broadcast from their owners; unit k + 1 is prefetched).  Backward:
     drops the unit's re-gathered copy and issues the gradient reduce to the owners asynchronously (it overlaps the
@@ -352,6 +410,35 @@ class _GatherUnit(torch.autograd.Function):
         ctx.state.release_bwd(ctx.k)
         ctx.state.reduce_async(ctx.k, grads)
         return (None, None) + (None,) * ctx.n
+
+
+def _stage2_buckets(prog, params, owners, row, group, me, cap=16 << 20):
+    """Buckets for _Stage2Buckets: each owner's parameters in reverse order of first forward use (the order the
+    backward finishes them), cut at ``cap`` bytes; hooks registered on every parameter."""
+    first = {}
+    by_id = {id(p._t): p for p in params}
+    for i, op in enumerate(prog.ops):
+        if op.kind not in ("torch", "native"):
+            continue
+        for x in pytree.tree_leaves((op.args, op.kwargs)):
+            p = by_id.get(id(x)) if isinstance(x, torch.Tensor) else None
+            if p is not None and p.name not in first:
+                first[p.name] = i
+    order = sorted(params, key=lambda p: -first.get(p.name, -1))
+    buckets, cur, size = [], {}, {}
+    for p in order:
+        o = owners[p.name]
+        nb = p._t.numel() * p._t.element_size()
+        if o in cur and size[o] + nb > cap:
+            buckets.append(cur.pop(o))
+        cur.setdefault(o, []).append(p)
+        size[o] = (size.get(o, 0) if o in cur and len(cur[o]) > 1 else 0) + nb
+    buckets.extend(cur.values())
+    st = _Stage2Buckets(buckets, owners, row, group, me)
+    for p in params:
+        if not p.stop_gradient:
+            p._t.register_post_accumulate_grad_hook(st.hook)
+    return st
 
 
 def _sharding_stage3(dmp, mesh_dim, group, n, me, row):
@@ -484,8 +571,9 @@ def sharding_pass(dmp, mesh_dim=0, stage=1):
       those) and broadcasts them, one coalesced broadcast per owner;
     * stage 2 — + gradients sharded: the per-use gradient all-reduces of the replicated parameters over
       ``mesh_dim`` (the plan's ``c_identity`` ops, or a fused all-reduce from ``fuse_allreduce_pass``) are removed;
-      at the step every owner's gradients are reduced to it in one coalesced ``reduce`` (half the bytes of the
-      all-reduce) and the other ranks drop theirs;
+      each owner's gradients are reduced to it in buckets issued asynchronously FROM the backward as they become
+      ready (_Stage2Buckets; half the bytes of the all-reduce, overlapped with the rest of the backward) and the
+      other ranks drop theirs;
     * stage 3 — + parameters sharded, gathered per use (_sharding_stage3): one gather op per unit right before
       its first forward consumer, next unit prefetched, backward re-gathers through saved-tensor hooks, gradient
       reduces to the owners issued asynchronously from the backward; a rank holds 1/n of the parameters plus the
@@ -524,23 +612,18 @@ def sharding_pass(dmp, mesh_dim=0, stage=1):
             load[o] += p._t.numel()
         mine = [p for p in opt._parameter_list if owners[p.name] == me]
         shapes = {p.name: (tuple(p._t.shape), p._t.dtype, p._t.device) for p in opt._parameter_list}
+        bk = None
+        if stage == 2:
+            bk = _stage2_buckets(prog, opt._parameter_list, owners, row, group, me)
+            dmp.stage2_buckets = bk
 
-        def step(env, opt=opt, mine=mine):
+        def step(env, opt=opt, mine=mine, bk=bk):
             full = opt._parameter_list
             with torch.no_grad():
-                if stage >= 2:
-                    for o in range(n):
-                        ps = [p for p in full if owners[p.name] == o]
-                        if not ps:
-                            continue
-                        grads = [p._t.grad if p._t.grad is not None else torch.zeros_like(p._t) for p in ps]
-                        flat = torch.cat([g.reshape(-1) for g in grads])
-                        dist.reduce(flat, dst=row[o], group=group)
-                        off = 0
-                        for p, g in zip(ps, grads):
-                            k = g.numel()
-                            p._t.grad = flat[off:off + k].view_as(g).clone() if o == me else None
-                            off += k
+                if bk is not None:
+                    red = bk.settle()
+                    for p in full:
+                        p._t.grad = red.get(p.name) if owners[p.name] == me else None
                 opt._parameter_list, opt._mt_cache = mine, None
                 try:
                     opt.step()

@@ -192,6 +192,8 @@ def test_static_passes_train_like_serial(passes):
             assert o["amp_ops"] >= 2
         if "sharding2" in passes:   # the per-use gradient all-reduces are gone (reduced to owners at the step)
             assert "c_identity" not in o["comm_after"] and "c_identity" in o["comm_before"], o
+            # every bucket's reduce was issued by the backward hooks (overlapped), none left for the step
+            assert o["stage2_from_backward"] == o["stage2_issued"] == 4 * o["stage2_buckets"], o
         if passes == "sharding3":   # between steps a rank holds only the parameters it owns
             assert 0 < o["released"] < o["n_params_total"], o
         if passes == "sharding3,deep":

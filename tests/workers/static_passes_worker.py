@@ -132,6 +132,11 @@ for i in range(4):
     ref_losses.append(float(rl.numpy()))
 out["losses"], out["ref"] = losses, ref_losses
 if any(f"sharding{st}" in passes for st in (2, 3)):
+    bk2 = getattr(dmp, "stage2_buckets", None)
+    if bk2 is not None:
+        out["stage2_buckets"] = len(bk2.buckets)
+        out["stage2_from_backward"] = bk2.from_backward
+        out["stage2_issued"] = bk2.issued
     st3 = getattr(dmp, "stage3_state", None)
     if st3 is not None:
         nb = lambda p: p._t.numel() * p._t.element_size()  # noqa: E731
