@@ -97,13 +97,14 @@ def _self_launch(args) -> int:
     return subprocess.call(cmd, env=env, cwd=ROOT)
 
 
-def expected_pg(world, on_gpu, native_enabled, want="auto"):
-    """The process-group backend a run of ``world`` ranks must report (None: no requirement)."""
+def expected_pg(world, on_gpu, native_enabled, want="auto", requested=None):
+    """The process-group backend a run of ``world`` ranks must report (None: no requirement).  ``requested``: an
+    explicitly chosen backend (PADDLE_DISTRI_BACKEND) — gloo / mpi then run on gloo by the user's choice."""
     if world <= 1 or want == "any":
         return None
     if want != "auto":
         return want
-    if not on_gpu:
+    if not on_gpu or (requested or "").lower() in ("gloo", "mpi"):
         return "gloo"
     return "pdrccl" if native_enabled else "c10d"
 
@@ -206,7 +207,8 @@ def main():
 
         native_on = rccl_pg.enabled()
     want = "any" if args.allow_pg_fallback else args.expect_pg
-    err = pg_problem(pgs, expected_pg(world, torch.cuda.is_available(), native_on, want))
+    err = pg_problem(pgs, expected_pg(world, torch.cuda.is_available(), native_on, want,
+                                      os.environ.get("PADDLE_DISTRI_BACKEND")))
     if err:
         print(f"error: {err}", file=sys.stderr, flush=True)
         sys.stdout.flush()

@@ -93,6 +93,7 @@ def test_bench_pg_check_with_injected_canary_failure():
     assert bench.pg_problem(status, bench.expected_pg(8, True, True, "any")) is None
     assert bench.pg_problem({"backend": "c10d"}, bench.expected_pg(8, True, False)) is None   # explicit opt-out
     assert bench.expected_pg(1, True, True) is None
+    assert bench.expected_pg(2, True, True, requested="gloo") == "gloo"    # explicit gloo on GPUs (shared-GPU tests)
 
 
 def test_bench_hang_guard_exits_with_report():
