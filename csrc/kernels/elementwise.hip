@@ -10,7 +10,7 @@
 
 namespace pd {
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // ------------------------------------------------------------------------------ SwiGLU
 // x, y: [rows, H] with row strides sx, sy (elements) — for the packed form y = x + H.

@@ -23,8 +23,8 @@ __device__ __forceinline__ float act_f(int act, float v) {
       const float u = 0.7978845608028654f * (v + 0.044715f * v * v * v);
       return 0.5f * v * (1.f + tanhf(u));
     }
-    case kSilu: return v / (1.f + __expf(-v));
-    case kSigmoid: return 1.f / (1.f + __expf(-v));
+    case kSilu: return v * __builtin_amdgcn_rcpf(1.f + __expf(-v));
+    case kSigmoid: return __builtin_amdgcn_rcpf(1.f + __expf(-v));
     default: return v;
   }
 }
@@ -44,11 +44,11 @@ __device__ __forceinline__ float act_grad(int act, float v) {
       return 0.5f * (1.f + t) + 0.5f * v * (1.f - t * t) * du;
     }
     case kSilu: {
-      const float s = 1.f / (1.f + __expf(-v));
+      const float s = __builtin_amdgcn_rcpf(1.f + __expf(-v));
       return s * (1.f + v * (1.f - s));
     }
     case kSigmoid: {
-      const float s = 1.f / (1.f + __expf(-v));
+      const float s = __builtin_amdgcn_rcpf(1.f + __expf(-v));
       return s * (1.f - s);
     }
     default: return 1.f;

@@ -279,7 +279,8 @@ __device__ __forceinline__ void mfma_agpr(f32x4v& c, const bf16x8& a, const bf16
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
 
-__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+// v_rcp_f32 (1 ulp) instead of the IEEE divide sequence: the epilogue is exposed VALU time
+__device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // GELU and its derivative in fp32 (torch's two forms: erf, and tanh with approximate = True)
 __device__ __forceinline__ float gelu_f(float x, int tanh_form) {
@@ -491,7 +492,7 @@ __device__ __forceinline__ void epilogue_t(const Params& p, f32x4v (&acc)[8][4],
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float gv = bf2f(g[e]), uv = bf2f(u[e]), da = acc[i][j][e];
-          const float sg = 1.f / (1.f + __expf(-gv));
+          const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-gv));
           dg[e] = f2bf(da * uv * sg * (1.f + gv * (1.f - sg)));
           du[e] = f2bf(da * gv * sg);
         }

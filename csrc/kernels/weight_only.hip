@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(const unsigned short* __re
 // GLU (the Llama MLP's down projection at decode): X is the gate|up GEMM output gu [M, 2K] and the staged row is
 // silu(gate) * up, rounded to bf16 once like swiglu_fwd_kernel — the SwiGLU pass folds into the X staging (the
 // whole X tile goes through LDS anyway), one launch less per layer.
-__device__ __forceinline__ float dec_sigmoid(float x) { return 1.f / (1.f + __expf(-x)); }   // as swiglu_fwd
+__device__ __forceinline__ float dec_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }   // as swiglu_fwd
 
 // cnt (optional): one int per column block, zero between calls.  The last of the S split-K workgroups of a column
 // block to finish (atomic arrival count) sums the S partials in split order — bit-identical to wo_reduce_kernel —
