@@ -55,6 +55,7 @@ typedef __attribute__((address_space(3))) char lds_char;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 constexpr float kDefer = 8.f;  // fwd defer-max threshold (log2 units)
+constexpr float kBig = 32.f;   // two-row-block fwd: base / running-max gap that triggers the exact second pass
 
 __device__ __forceinline__ int swz(int row, int ch, int nch) {
   return ch ^ ((((row & 3) << 2) | ((row >> 2) & 3)) & (nch - 1));
@@ -124,6 +125,24 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
                                                   0);
   else return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+
+// O^T += V^T . P^T with the accumulator pinned to AGPRs (the two-row-block forward: its 128 O registers per lane must
+// live in the accumulator file, which the compiler's own allocation did not find — 270 v_accvgpr copies per tile).
+// NOP: the P operand was just written by VALU (pack8); two wait states before an MFMA reads it (the hazard
+// recognizer does not look inside an asm statement).
+template <bool F16, bool NOP>
+__device__ __forceinline__ void mfma_acc(f32x16& c, bf16x8 a, bf16x8 b) {
+  if constexpr (F16) {
+    if constexpr (NOP) asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+    else asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  } else {
+    if constexpr (NOP) asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+    else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  }
+}
+// wait states between the last asm MFMA writing an AGPR accumulator and a VALU / v_accvgpr read of it (16-pass XDL
+// write -> VALU read: 18)
+__device__ __forceinline__ void mfma_acc_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
 
 // XCD-aware bijective remap of a 1-D block id (cdna guide §5 "XCD swizzle must be bijective").
 __device__ __forceinline__ int xcd_remap(int bid, int n) {
@@ -229,18 +248,27 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int r0, int c0, int 
 // workgroup per CU: every K/V tile is staged once for 256 query rows, half the global->LDS traffic and staging VALU
 // per MFMA; causal tiles above a wave's last row are skipped by that wave).  NW = 8 excludes FlashMask (its plans
 // are built for 128-row query blocks).
-template <int D, bool CAUSAL, int MODE, bool DROP, bool F16, int NW>
-__global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+// RB = 2 (NW = 4, D = 128, dense / varlen, no dropout): every wave owns TWO 32-row query blocks (rows m0 + 32 wv and
+// m0 + 128 + 32 wv of a 256-row workgroup, one workgroup per CU with the whole 512-register file): each K fragment
+// (ds_read_b128) and each V^T fragment (2 x ds_read_b64_tr_b16) feeds two MFMAs instead of one, a K/V tile is staged
+// once for 256 rows, and the two blocks' softmax chains are independent VALU work the scheduler can place beside
+// the other block's MFMAs (one wave per SIMD: no partner wave's MFMAs compete for the matrix pipe).
+template <int D, bool CAUSAL, int MODE, bool DROP, bool F16, int NW, int RB = 1>
+__global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 || RB == 2 ? 1 : 2)) void fwd_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ Vv, bf16* __restrict__ O,
                                                      float* __restrict__ LSE, int B, int SqMax, int SkMax, int Hq,
                                                      int Hk, long sq, long sk, long sv, long so, float scale, Ext ex) {
-  constexpr int BM = 32 * NW, BN = 64, NCH = D / 8, KS = D / 16, DT = D / 32, NT = NW * 64;
+  constexpr int BM = 32 * NW * RB, BN = 64, NCH = D / 8, KS = D / 16, DT = D / 32, NT = NW * 64;
   constexpr int TILE = BN * D * 2;
   constexpr int NLOAD = BN * NCH / NT;
   static_assert(NLOAD * NT == BN * NCH, "tile copy must divide over the workgroup");
   static_assert(NW == 4 || MODE != kMask, "FlashMask plans assume 128-row query blocks");
+  static_assert(RB == 1 || (NW == 4 && D <= 128 && MODE != kMask && !DROP), "two row blocks: 4 waves, no mask / dropout");
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][K|V]
   __shared__ int4 fm_s[MODE == kMask ? 2 * BN : 1];              // [buf][key] FlashMask intervals
+  // RB = 2: the workgroup's 256 Q rows stay in LDS (same swizzled row image as K) and are read per tile — 64 VGPRs of
+  // Q fragments did not fit beside 2 x 32 score and 2 x 64 output registers per lane
+  __shared__ __attribute__((aligned(16))) char qsm[RB == 2 ? BM * D * 2 : 16];
 
   const int nmb = (SqMax + BM - 1) / BM;
   const int total = nmb * Hq * B;
@@ -281,17 +309,34 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
     plan = ex.fm_t64 + (mh * nmb + mb) * (nt_all + 2);
   }
 
-  // Q fragments (B operand of S^T = K.Q^T): lane holds Q[q][16ks + 8h .. +8]
-  const int qrow = m0 + wv * 32 + r;
-  bf16x8 qf[KS];
+  // Q fragments (B operand of S^T = K.Q^T): lane holds Q[q][16ks + 8h .. +8]; row block j = rows m0 + 32 NW j + 32 wv
+  int qrow[RB];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    if (qrow < Sq) qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (long)qrow * sq + ks * 16 + 8 * h);
-    else qf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < RB; ++j) qrow[j] = m0 + j * 32 * NW + wv * 32 + r;
+  constexpr int QF = RB == 1 ? KS : 1;
+  bf16x8 qf[QF];
+  if constexpr (RB == 1) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (qrow[0] < Sq) qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (long)qrow[0] * sq + ks * 16 + 8 * h);
+      else qf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    // settle the Q fragment loads before the loop (see bwd_kernel: keeps vmcnt(0) out of the tile loop)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(qf[ks]));
+  } else {
+    // Q block [BM rows][D] -> LDS image (rows past Sq read as zero through the buffer extent); the first tile's
+    // barrier publishes it
+    const int nq = max(0, min(Sq - m0, BM));
+    const __amdgpu_buffer_rsrc_t rq = make_rsrc_u(Qb + (long)m0 * sq, nq * (int)sq * 2);
+    constexpr int NQL = BM * NCH / NT;
+#pragma unroll
+    for (int i = 0; i < NQL; ++i) {
+      const int c = tid + NT * i, row = c / NCH, ch = c % NCH;
+      const u16x8 v = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rq, row * (int)sq * 2 + ch * 16, 0, 0));
+      *reinterpret_cast<u16x8*>(qsm + row * (D * 2) + swz(row, ch, NCH) * 16) = v;
+    }
   }
-  // settle the Q fragment loads before the loop (see bwd_kernel: keeps vmcnt(0) out of the tile loop)
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(qf[ks]));
 
   int n_end = Sk;
   if (CAUSAL) n_end = min(Sk, m0 + BM + off);
@@ -341,10 +386,30 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
     }
   };
 
-  f32x16 oacc[DT];
+  f32x16 oacc[RB][DT];
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt) oacc[dt] = f32x16{};
-  float m_i = -INFINITY, l_i = 0.f;
+  for (int j = 0; j < RB; ++j)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      oacc[j][dt] = f32x16{};
+      if constexpr (RB == 2) asm volatile("" : "+a"(oacc[j][dt]));
+    }
+  if constexpr (RB == 2) asm volatile("s_nop 4" ::: "memory");
+  float m_i[RB], l_i[RB];
+  // RB = 2: no O rescale inside the loop (a VALU multiply of the AGPR-pinned accumulators made hipcc home them in
+  // VGPRs and copy 128 registers per tile).  m_i is the exponent base, set once at the row's first finite tile (O and l
+  // are still zero there, so no rescale is needed); m_run tracks the true running max.  A row whose max later climbs
+  // more than kBig above its base (P > 2^kBig; the bases are otherwise exact, P only ranges wider than with kDefer)
+  // flags the workgroup, which then repeats the sweep with every base fixed at the row's final maximum (pass 1: no
+  // growth possible) — a rare second pass in place of a per-tile rescale path.
+  float m_run[RB];
+  bool ovf = false;
+#pragma unroll
+  for (int j = 0; j < RB; ++j) {
+    m_i[j] = -INFINITY;
+    l_i[j] = 0.f;
+    m_run[j] = -INFINITY;
+  }
   const float sl2 = scale * kLog2e;
 
   // next key tile >= t that is not fully masked (FlashMask); identity otherwise
@@ -354,6 +419,11 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
     }
     return t;
   };
+  const int t_first = t;
+  __shared__ int wg_ovf;
+  if constexpr (RB == 2) {
+    if (tid == 0) wg_ovf = 0;
+  }
   if (t < ntiles) {
     gload(t * BN);
     lstore(0);
@@ -364,8 +434,8 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
   if constexpr (NW == 8) {
     if (wv >= 4) __builtin_amdgcn_s_setprio(1);
   }
-  // causal: the last key this wave's 32 rows can see; tiles past it are all masked for the wave
-  const int wave_last_key = m0 + wv * 32 + 31 + off;
+  // causal: the last key this wave's rows (its last row block) can see; tiles past it are all masked for the wave
+  const int wave_last_key = m0 + (RB - 1) * 32 * NW + wv * 32 + 31 + off;
 
   // Per-lane LDS read bases (D <= 128; cdna guide T20-style address hygiene): every K row read and V^T transposed
   // read is one precomputed lane base + a compile-time immediate (buffer / key sub-block / 16-row step), so the tile
@@ -388,38 +458,63 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
   // masks; every other tile runs a body with no mask code at all (a runtime branch inside one body was if-converted
   // by hipcc: ~100 compares / selects per tile on every tile).  BUF: the LDS stage (a compile-time stage doubled the
   // bodies and spilled 264 B/lane).
-  auto tile = [&](auto MASKED_, int BUF, int n0, bool has_next, int tn) {
+  auto tile = [&](auto MASKED_, int BUF, int n0, bool has_next, int tn, bool rt_mask) {
     constexpr bool MASKED = decltype(MASKED_)::value;
     const char* kt = smem + BUF * 2 * TILE;
     const char* vt = kt + TILE;
     // opaque per tile: the XOR-ed read offsets are recomputed (1 VALU each) instead of hoisted out of the loop as
     // ~50 live registers (which spilled)
     if constexpr (PRE) asm volatile("" : "+v"(o_k), "+v"(o_va), "+v"(o_vb));
-    // ---- S^T = K . Q^T for two 32-key sub-blocks
-    f32x16 s[2];
+    // ---- S^T = K . Q^T for two 32-key sub-blocks (each K fragment feeds every row block)
+    f32x16 s[RB][2];
+    if constexpr (RB == 1) {
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      s[kb] = f32x16{};
-      const int krow = kb * 32 + r;
+      for (int kb = 0; kb < 2; ++kb) {
+        s[0][kb] = f32x16{};
+        const int krow = kb * 32 + r;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          bf16x8 a;
+          if constexpr (PRE) a = lds_b128(kt + kb * 32 * (D * 2), o_k ^ (ks << 5));
+          else a = lds_b128(kt, krow * (D * 2) + swz(krow, 2 * ks + h, NCH) * 16);
+          s[0][kb] = mfma<F16>(a, qf[ks], s[0][kb]);
+        }
+      }
+    } else {
+      // ks outer: per step one fragment read per row block (Q) and per key sub-block (K), four MFMAs
+#pragma unroll
+      for (int j = 0; j < RB; ++j) s[j][0] = s[j][1] = f32x16{};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        bf16x8 a;
-        if constexpr (PRE) a = lds_b128(kt + kb * 32 * (D * 2), o_k ^ (ks << 5));
-        else a = lds_b128(kt, krow * (D * 2) + swz(krow, 2 * ks + h, NCH) * 16);
-        s[kb] = mfma<F16>(a, qf[ks], s[kb]);
+        bf16x8 bq[RB], a[2];
+#pragma unroll
+        for (int j = 0; j < RB; ++j) bq[j] = lds_b128(qsm + (j * 32 * NW + wv * 32) * (D * 2), o_k ^ (ks << 5));
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) a[kb] = lds_b128(kt + kb * 32 * (D * 2), o_k ^ (ks << 5));
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int j = 0; j < RB; ++j) s[j][kb] = mfma<F16>(a[kb], bq[j], s[j][kb]);
       }
     }
     // next tile's K/V loads issue after QK^T (T14): softmax + PV cover their flight, lstore waits at the end
     if (has_next) gload(tn * BN);
     // ---- mask, online softmax (lane owns query qrow; 32 of the 64 keys).  The max is taken on raw scores and the
     // 1/sqrt(d)*log2(e) scale is folded into one FMA feeding v_exp_f32.
-    if constexpr (MASKED) {
+    auto apply_mask = [&]() {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
+      for (int j = 0; j < RB; ++j) {
+        // key = n0 + 4h + c with the compile-time c = 32kb + (i&3) + 8(i>>2): masked iff c >= lim (key >= Sk, or
+        // key > qrow + off when causal) — one compare against an immediate per score, nothing hoisted per lane
+        int lim = Sk - n0 - 4 * h;
+        if constexpr (CAUSAL) lim = min(lim, qrow[j] + off - n0 - 4 * h + 1);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int key = n0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          s[kb][i] = (key >= Sk || (CAUSAL && key > qrow + off)) ? -INFINITY : s[kb][i];
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int c = kb * 32 + (i & 3) + 8 * (i >> 2);
+            s[j][kb][i] = c >= lim ? -INFINITY : s[j][kb][i];
+          }
         }
       }
       if constexpr (MODE == kMask) {
@@ -432,55 +527,83 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
 #pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                const int4 m = fmt_s[kb * 32 + 8 * g + 4 * h + j];
-                s[kb][4 * g + j] = fm_masked(m, qrow) ? -INFINITY : s[kb][4 * g + j];
+              for (int jj = 0; jj < 4; ++jj) {
+                const int4 m = fmt_s[kb * 32 + 8 * g + 4 * h + jj];
+                s[0][kb][4 * g + jj] = fm_masked(m, qrow[0]) ? -INFINITY : s[0][kb][4 * g + jj];
               }
               __builtin_amdgcn_sched_barrier(0);
             }
           }
         }
       }
+    };
+    if constexpr (MASKED) apply_mask();
+    else if constexpr (RB == 2) {
+      // one body for both tile kinds with two row blocks (two bodies made the register allocator disagree on
+      // the loop-carried accumulators' homes at the join: 600 B/lane of spills); a real branch, not if-converted
+      if (rt_mask) {
+        asm volatile("" ::: "memory");
+        apply_mask();
+      }
     }
     // row max: four independent max3 chains (one 16-deep chain was a serial latency path), then the lane-half
     // exchange by v_permlane32_swap (no LDS round trip: ds_bpermute + lgkmcnt wait)
-    float mxa[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    float m_cand[RB];
+    bool grow = false;
+    (void)m_cand;
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+    for (int j = 0; j < RB; ++j) {
+      float mxa[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) mxa[i & 3] = fmaxf(mxa[i & 3], s[kb][i]);
-    }
-    float mx = fmaxf(fmaxf(mxa[0], mxa[1]), fmaxf(mxa[2], mxa[3]));
-    {
-      const unsigned mu = __builtin_bit_cast(unsigned, mx);
-      const auto sw = __builtin_amdgcn_permlane32_swap(mu, mu, false, false);
-      mx = fmaxf(__builtin_bit_cast(float, (unsigned)sw[0]), __builtin_bit_cast(float, (unsigned)sw[1]));
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mxa[i & 3] = fmaxf(mxa[i & 3], s[j][kb][i]);
+      }
+      float mx = fmaxf(fmaxf(mxa[0], mxa[1]), fmaxf(mxa[2], mxa[3]));
+      {
+        const unsigned mu = __builtin_bit_cast(unsigned, mx);
+        const auto sw = __builtin_amdgcn_permlane32_swap(mu, mu, false, false);
+        mx = fmaxf(__builtin_bit_cast(float, (unsigned)sw[0]), __builtin_bit_cast(float, (unsigned)sw[1]));
+      }
+      if constexpr (RB == 2) {
+        m_run[j] = fmaxf(m_run[j], mx * sl2);
+        m_i[j] = m_i[j] == -INFINITY ? m_run[j] : m_i[j];   // first finite tile: O, l still zero
+        ovf = ovf || (m_run[j] > m_i[j] + kBig);
+      } else {
+        m_cand[j] = fmaxf(m_i[j], mx * sl2);
+        grow = grow || (m_cand[j] > m_i[j] + kDefer);
+      }
     }
     // defer-max (T13): the running base moves only when some row of the wave grew past it by more than
     // 2^kDefer; otherwise P <= 2^kDefer (exact in fp32 / bf16) and the l / O rescale is skipped.  The branch is
     // wave-uniform and kept a real branch (the asm statement cannot be speculated): if-converted, its DT*16
-    // multiplies and copies ran on every tile
-    const float m_cand = fmaxf(m_i, mx * sl2);
-    if (__builtin_expect(__any(m_cand > m_i + kDefer), 0)) {
-      asm volatile("" ::: "memory");
-      const float alpha = __builtin_amdgcn_exp2f(m_i - (m_cand == -INFINITY ? 0.f : m_cand));
-      l_i *= alpha;
+    // multiplies and copies ran on every tile.  With two row blocks one branch moves both bases (moving a base
+    // that did not need it is exact: the defer is only a skip)
+    if constexpr (RB == 1) {
+      if (__builtin_expect(__any(grow), 0)) {
+        asm volatile("" ::: "memory");
+        const float alpha = __builtin_amdgcn_exp2f(m_i[0] - (m_cand[0] == -INFINITY ? 0.f : m_cand[0]));
+        l_i[0] *= alpha;
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) oacc[dt] *= alpha;
-      m_i = m_cand;
-    }
-    const float base = m_i == -INFINITY ? 0.f : m_i;
-    float lsa[4] = {0.f, 0.f, 0.f, 0.f};   // four independent add chains (a 32-deep serial chain before)
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(s[kb][i], sl2, -base));
-        s[kb][i] = p;
-        lsa[i & 3] += p;
+        for (int dt = 0; dt < DT; ++dt) oacc[0][dt] *= alpha;
+        m_i[0] = m_cand[0];
       }
     }
-    l_i += (lsa[0] + lsa[1]) + (lsa[2] + lsa[3]);  // per lane-half partial; halves combined at the end
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const float base = m_i[j] == -INFINITY ? 0.f : m_i[j];
+      float lsa[4] = {0.f, 0.f, 0.f, 0.f};   // four independent add chains (a 32-deep serial chain before)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[j][kb][i], sl2, -base));
+          s[j][kb][i] = p;
+          lsa[i & 3] += p;
+        }
+      }
+      l_i[j] += (lsa[0] + lsa[1]) + (lsa[2] + lsa[3]);  // per lane-half partial; halves combined at the end
+    }
     if constexpr (DROP) {  // row sums keep the undropped P; only the P.V operand is masked
       const unsigned bh = (unsigned)(b * Hq + hq);
 #pragma unroll
@@ -488,17 +611,19 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int key = n0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (!drop_keep(ex, bh, (unsigned)qrow, (unsigned)key)) s[kb][i] = 0.f;
+          if (!drop_keep(ex, bh, (unsigned)qrow[0], (unsigned)key)) s[0][kb][i] = 0.f;
         }
       }
     }
 
-    // ---- O^T += V^T . P^T
+    // ---- O^T += V^T . P^T (each V^T fragment feeds every row block)
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 pb = pack8<F16>(s[kb], ss);
+        bf16x8 pb[RB];
+#pragma unroll
+        for (int j = 0; j < RB; ++j) pb[j] = pack8<F16>(s[j][kb], ss);
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
           bf16x8 a;
@@ -508,7 +633,18 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
           } else {
             a = tr_frag<D, true>(vt, kb * 32 + 16 * ss, dt * 32, lane);
           }
-          oacc[dt] = mfma<F16>(a, pb, oacc[dt]);
+          if constexpr (RB == 2) {
+            // dt = 0: the first reads of this step's VALU-packed P fragments
+            if (dt == 0) {
+              mfma_acc<F16, true>(oacc[0][dt], a, pb[0]);
+              mfma_acc<F16, true>(oacc[RB - 1][dt], a, pb[RB - 1]);
+            } else {
+              mfma_acc<F16, false>(oacc[0][dt], a, pb[0]);
+              mfma_acc<F16, false>(oacc[RB - 1][dt], a, pb[RB - 1]);
+            }
+          } else {
+            oacc[0][dt] = mfma<F16>(a, pb[0], oacc[0][dt]);
+          }
         }
       }
     }
@@ -516,13 +652,122 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
     __syncthreads();
   };
 
+  // RB = 2 tile, software-ordered so each row block's softmax runs beside the other block's MFMAs (one wave per SIMD
+  // has no partner wave to fill the MFMA pipe while it exponentiates):
+  //   QK0 | mask0? | QK1 || softmax0 | mask1? | PV0 || softmax1 | PV1
+  // The rare causal / boundary masks are real (uniform) branches placed where they do not split an overlapped pair.
+  auto tile2 = [&](int BUF, int n0, bool has_next, int tn, bool rt_mask) {
+    const char* kt = smem + BUF * 2 * TILE;
+    const char* vt = kt + TILE;
+    if constexpr (PRE) asm volatile("" : "+v"(o_k), "+v"(o_va), "+v"(o_vb));
+    f32x16 s0[2], s1[2];
+    auto qk = [&](f32x16 (&sb)[2], int j) {
+      sb[0] = sb[1] = f32x16{};
+      const char* qb = qsm + (j * 32 * NW + wv * 32) * (D * 2);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 bq = lds_b128(qb, o_k ^ (ks << 5));
+        const bf16x8 a0 = lds_b128(kt, o_k ^ (ks << 5));
+        const bf16x8 a1 = lds_b128(kt + 32 * (D * 2), o_k ^ (ks << 5));
+        sb[0] = mfma<F16>(a0, bq, sb[0]);
+        sb[1] = mfma<F16>(a1, bq, sb[1]);
+      }
+    };
+    auto mask = [&](f32x16 (&sb)[2], int j) {
+      if (rt_mask) {
+        asm volatile("" ::: "memory");
+        int lim = Sk - n0 - 4 * h;
+        if constexpr (CAUSAL) lim = min(lim, qrow[j] + off - n0 - 4 * h + 1);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int c = kb * 32 + (i & 3) + 8 * (i >> 2);
+            sb[kb][i] = c >= lim ? -INFINITY : sb[kb][i];
+          }
+      }
+    };
+    auto softmax = [&](f32x16 (&sb)[2], int j) {
+      float mxa[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mxa[i & 3] = fmaxf(mxa[i & 3], sb[kb][i]);
+      float mx = fmaxf(fmaxf(mxa[0], mxa[1]), fmaxf(mxa[2], mxa[3]));
+      {
+        const unsigned mu = __builtin_bit_cast(unsigned, mx);
+        const auto sw = __builtin_amdgcn_permlane32_swap(mu, mu, false, false);
+        mx = fmaxf(__builtin_bit_cast(float, (unsigned)sw[0]), __builtin_bit_cast(float, (unsigned)sw[1]));
+      }
+      m_run[j] = fmaxf(m_run[j], mx * sl2);
+      m_i[j] = m_i[j] == -INFINITY ? m_run[j] : m_i[j];
+      ovf = ovf || (m_run[j] > m_i[j] + kBig);
+      const float base = m_i[j] == -INFINITY ? 0.f : m_i[j];
+      float lsa[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float pp = __builtin_amdgcn_exp2f(fmaf(sb[kb][i], sl2, -base));
+          sb[kb][i] = pp;
+          lsa[i & 3] += pp;
+        }
+      l_i[j] += (lsa[0] + lsa[1]) + (lsa[2] + lsa[3]);
+    };
+    auto pv = [&](f32x16 (&sb)[2], int j) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const bf16x8 pb = pack8<F16>(sb[kb], ss);
+          const char* vr = vt + (kb * 32 + 16 * ss) * (D * 2);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            const bf16x8 a = cat4(lds_tr(vr, o_va ^ (dt << 6)), lds_tr(vr, o_vb ^ (dt << 6)));
+            if (dt == 0) mfma_acc<F16, true>(oacc[j][dt], a, pb);
+            else mfma_acc<F16, false>(oacc[j][dt], a, pb);
+          }
+        }
+    };
+    qk(s0, 0);
+    mask(s0, 0);
+    qk(s1, 1);
+    // unconditional (no branch between QK1 and softmax0): past the last tile the buffer extent is 0 and the loads
+    // read zeros into a stage nobody reads
+    gload(tn * BN);
+    softmax(s0, 0);
+    // interleave: per QK1 MFMA up to 2 LDS reads and 6 VALU of softmax0
+#pragma unroll
+    for (int g = 0; g < 2 * KS; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x402, 6, 0);
+    }
+    // pin P0 here: otherwise its exps are sunk past the mask1 branch into PV0's block, out of QK1's MFMA stream
+    asm volatile("" : "+v"(s0[0]), "+v"(s0[1]));
+    mask(s1, 1);
+    softmax(s1, 1);
+    pv(s0, 0);
+#pragma unroll
+    for (int g = 0; g < 2 * DT; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+      __builtin_amdgcn_sched_group_barrier(0x402, 8, 1);
+    }
+    pv(s1, 1);
+    lstore(BUF ^ 1);  // write late (T14)
+    (void)has_next;
+    __syncthreads();
+  };
+
   using FalseT = std::integral_constant<bool, false>;
   using TrueT = std::integral_constant<bool, true>;
+  for (int pass = 0;; ++pass) {
   for (int buf = 0; t < ntiles; buf ^= 1) {
     const int n0 = t * BN;
     const int tn = next_tile(t + 1);
     const bool has_next = tn < ntiles;
-    if (CAUSAL && (NW == 8 || ex.wave_skip) && n0 > wave_last_key) {  // wave-uniform: only stage the next tile for the others
+    if (CAUSAL && (NW == 8 || RB == 2 || ex.wave_skip) && n0 > wave_last_key) {  // wave-uniform: only stage the next tile for the others
       if (has_next) {
         gload(tn * BN);
         lstore(buf ^ 1);
@@ -533,32 +778,80 @@ __global__ __launch_bounds__(NW * 64, (NW == 8 || D > 128 ? 1 : 2)) void fwd_ker
     }
     bool masked = (n0 + BN > Sk) || (CAUSAL && (n0 + BN - 1 > m0 + off));
     if constexpr (MODE == kMask) masked = masked || plan[2 + t] == 1;
-    if (masked) tile(TrueT{}, buf, n0, has_next, tn);
-    else tile(FalseT{}, buf, n0, has_next, tn);
+    if constexpr (RB == 2) tile2(buf, n0, has_next, tn, masked);
+    else if (masked) tile(TrueT{}, buf, n0, has_next, tn, true);
+    else tile(FalseT{}, buf, n0, has_next, tn, false);
     t = tn;
   }
-
-  // ---- epilogue: normalise, store O (row = query, 4 consecutive d per store) and LSE
-  const float l_tot = l_i + __shfl_xor(l_i, 32, 64);
-  float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  if constexpr (DROP) inv *= ex.drop_rscale;
-  if (qrow < Sq) {
-    bf16* orow = O + (qt0 + qrow) * so + hq * D;
+  if constexpr (RB == 1) {
+    break;
+  } else {
+    if (pass == 1) break;
+    if (__any(ovf) && lane == 0) wg_ovf = 1;
+    __syncthreads();
+    if (__builtin_expect(wg_ovf == 0, 1)) break;
+    // rare: repeat the sweep with every row's base at its final maximum (P <= 1, no growth)
+    mfma_acc_drain();
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
+    for (int j = 0; j < RB; ++j) {
+      m_i[j] = m_run[j];
+      l_i[j] = 0.f;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int d = dt * 32 + 8 * c + 4 * h;
-        ushort4 v;
-        v.x = cvt16<F16>(oacc[dt][4 * c + 0] * inv);
-        v.y = cvt16<F16>(oacc[dt][4 * c + 1] * inv);
-        v.z = cvt16<F16>(oacc[dt][4 * c + 2] * inv);
-        v.w = cvt16<F16>(oacc[dt][4 * c + 3] * inv);
-        *reinterpret_cast<ushort4*>(orow + d) = v;
+      for (int dt = 0; dt < DT; ++dt) {
+        oacc[j][dt] = f32x16{};
+        asm volatile("" : "+a"(oacc[j][dt]));
       }
     }
-    if (h == 0) {
-      LSE[lse0 + qrow] = l_tot > 0.f ? (m_i + log2f(l_tot)) * kLn2 : INFINITY;
+    asm volatile("s_nop 4" ::: "memory");
+    t = t_first;
+    if (t < ntiles) {
+      gload(t * BN);
+      lstore(0);
+    }
+    __syncthreads();
+  }
+  }
+
+  // ---- epilogue: normalise, store O and LSE.  A row's 8 consecutive d of a 32-column group sit 4 + 4 in lanes i and
+  // i + 32; one v_permlane32_swap per dword pairs groups (c, c + 1) so each lane stores 16 contiguous bytes (lanes < 32
+  // group c, lanes >= 32 group c + 1): 8 dwordx4 stores per row block instead of 16 dwordx2 (the store tail is
+  // issue-bound: cdna guide T21).  The swaps run with every lane active, before the row-bound check.
+  if constexpr (RB == 2) mfma_acc_drain();
+#pragma unroll
+  for (int j = 0; j < RB; ++j) {
+    const float l_tot = l_i[j] + __shfl_xor(l_i[j], 32, 64);
+    float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+    if constexpr (DROP) inv *= ex.drop_rscale;
+    unsigned pk[DT][4][2];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          pk[dt][c][e] = (unsigned)cvt16<F16>(oacc[j][dt][4 * c + 2 * e] * inv) |
+                         ((unsigned)cvt16<F16>(oacc[j][dt][4 * c + 2 * e + 1] * inv) << 16);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; c += 2)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(pk[dt][c][e], pk[dt][c + 1][e], false, false);
+          pk[dt][c][e] = sw[0];
+          pk[dt][c + 1][e] = sw[1];
+        }
+    if (qrow[j] < Sq) {
+      char* orow = reinterpret_cast<char*>(O + (qt0 + qrow[j]) * so + hq * D) + (h ? 16 : 0);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int c = 0; c < 4; c += 2)
+          *reinterpret_cast<uint4*>(orow + 64 * dt + 16 * c) =
+              make_uint4(pk[dt][c][0], pk[dt][c][1], pk[dt][c + 1][0], pk[dt][c + 1][1]);
+      if (h == 0) {
+        LSE[lse0 + qrow[j]] = l_tot > 0.f ? (m_i[j] + log2f(l_tot)) * kLn2 : INFINITY;
+      }
     }
   }
 }
@@ -1358,12 +1651,22 @@ __global__ __launch_bounds__(256) void dq_reduce_kernel(const float* __restrict_
 
 using namespace pd;
 
+#ifndef PD_FA_DEVICE_ONLY
+namespace pd {
+namespace fa {
+// the two-row-block forward lives in flash_fwd2.hip (its own compile flags)
+void launch_fwd_rb2(bool f16, bool causal, int mode, dim3 grid, hipStream_t st, const void* q, const void* k,
+                    const void* v, void* o, float* lse, int B, int Sq, int Sk, int Hq, int Hk, long sq, long sk, long sv,
+                    long so, float scale, const Ext& ex);
+}  // namespace fa
+}  // namespace pd
+
 namespace {
 
 template <int D, bool F16>
 void launch_fwd(dim3 grid, hipStream_t st, const void* q, const void* k, const void* v, void* o, float* lse, int B,
                 int Sq, int Sk, int Hq, int Hk, long sq, long sk, long sv, long so, float scale, bool causal, int mode,
-                bool drop, const fa::Ext& ex, int nw) {
+                bool drop, const fa::Ext& ex, int nw, int rb) {
 #define PD_FA_FWD_W(CC, MM, DR, W)                                                                                 \
   fa::fwd_kernel<D, CC, MM, DR, F16, W><<<grid, W * 64, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, \
                                                                  (bf16*)o, lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, \
@@ -1372,6 +1675,10 @@ void launch_fwd(dim3 grid, hipStream_t st, const void* q, const void* k, const v
 #define PD_FA_FWD_C(MM, DR) \
   if (causal) PD_FA_FWD(true, MM, DR); else PD_FA_FWD(false, MM, DR);
   if constexpr (D == 128) {
+    if (nw == 4 && rb == 2) {  // two row blocks per wave: dense / varlen without dropout
+      fa::launch_fwd_rb2(F16, causal, mode, grid, st, q, k, v, o, lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, ex);
+      return;
+    }
     if (nw == 8) {  // dense / varlen without dropout
       if (mode == 0) { if (causal) PD_FA_FWD_W(true, fa::kDense, false, 8); else PD_FA_FWD_W(false, fa::kDense, false, 8); }
       else { if (causal) PD_FA_FWD_W(true, fa::kVarlen, false, 8); else PD_FA_FWD_W(false, fa::kVarlen, false, 8); }
@@ -1468,6 +1775,15 @@ static int fa_fwd_waves(int D, int Sq, int causal, int mode, int drop) {
   return (!causal && Sq >= 2048) ? 8 : 4;
 }
 
+// Row blocks per wave of the 4-wave forward (D = 128, dense / varlen, no dropout): 1 = 32 rows per wave, two
+// workgroups per CU; 2 = 64 rows per wave (two 32-row blocks sharing every K / V fragment read), one 256-row
+// workgroup per CU.  PADDLE2_AMD_FA_FWD_RB = 1 / 2 forces one.
+static int fa_fwd_rb(int D, int nw, int mode, int drop) {
+  if (D != 128 || nw != 4 || mode == 2 || drop) return 1;
+  if (const char* e = getenv("PADDLE2_AMD_FA_FWD_RB")) return atoi(e) == 2 ? 2 : 1;
+  return 1;
+}
+
 // Key-block width of the backward (rows of the dQ partial slabs): 256 keys for D <= 128, 128 for D = 256.
 // (The 4-wave D = 128 kernel's 128-key blocks run only in the dense atomic mode, whose dQ is one slab.)
 extern "C" int pd_flash_bwd_block(int D) { return D > 128 ? 128 : 256; }
@@ -1494,7 +1810,8 @@ extern "C" int pd_flash_fwd_ext(int dt, const void* q, const void* k, const void
   if (int e = check_args(dt, D, Hq, Hk, mode, drop, pdrop, cu_q, cu_k, fm, fm_t64, fm_hm)) return e;
   hipStream_t st = (hipStream_t)stream;
   const int nw = fa_fwd_waves(D, Sq, causal, mode, drop);
-  const int nmb = (Sq + 32 * nw - 1) / (32 * nw);
+  const int rb = fa_fwd_rb(D, nw, mode, drop);
+  const int nmb = (Sq + 32 * nw * rb - 1) / (32 * nw * rb);
   dim3 grid(nmb * Hq * B);
   fa::Ext ex{cu_q, cu_k, total_q, (const int4*)fm, fm_t64, fm_t256, fm_hm, seed,
              drop ? (unsigned)fminf(pdrop * 4294967296.f, 4294967040.f) : 0u, drop ? 1.f / (1.f - pdrop) : 1.f};
@@ -1503,7 +1820,7 @@ extern "C" int pd_flash_fwd_ext(int dt, const void* q, const void* k, const void
   ex.wave_skip = 1;
   if (const char* e = getenv("PADDLE2_AMD_FA_FWD_WAVE_SKIP")) ex.wave_skip = atoi(e) != 0;
 #define PD_FWD(DD, FF) \
-  launch_fwd<DD, FF>(grid, st, q, k, v, o, lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, causal, mode, drop, ex, nw)
+  launch_fwd<DD, FF>(grid, st, q, k, v, o, lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, causal, mode, drop, ex, nw, rb)
   const bool f16 = dt == kF16;
   if (D == 128) { if (f16) PD_FWD(128, true); else PD_FWD(128, false); }
   else if (D == 64) { if (f16) PD_FWD(64, true); else PD_FWD(64, false); }
@@ -1667,3 +1984,4 @@ extern "C" int pd_flash_bwd(int dt, const void* q, const void* k, const void* v,
                           sdk, sdv, scale, causal, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr, 1, 0, 0u, 0.f,
                           stream);
 }
+#endif  // PD_FA_DEVICE_ONLY

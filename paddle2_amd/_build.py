@@ -35,10 +35,18 @@ def _sources():
     return hips, os.path.join(CSRC, "bindings.cpp")
 
 
+# per-translation-unit extras: flash_fwd2.hip includes flash_attn.hip and needs the VGPR form of the MFMAs
+_TU_FLAGS = {"flash_fwd2.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+_TU_DEPS = {"flash_fwd2.hip": ["flash_attn.hip"]}
+
+
 def _hash(path, extra=""):
     h = hashlib.sha1()
     with open(path, "rb") as f:
         h.update(f.read())
+    for dep in _TU_DEPS.get(os.path.basename(path), []):
+        with open(os.path.join(os.path.dirname(path), dep), "rb") as f:
+            h.update(f.read())
     # headers affect every translation unit
     kdir = os.path.join(CSRC, "kernels")
     for hf in sorted(os.listdir(kdir)):
@@ -68,7 +76,7 @@ def build(verbose=False, jobs=None):
 
     def compile_one(src):
         is_hip = src.endswith(".hip")
-        flags = hip_flags if is_hip else host_flags
+        flags = (hip_flags + _TU_FLAGS.get(os.path.basename(src), [])) if is_hip else host_flags
         key = _hash(src, " ".join(flags))
         obj = os.path.join(BUILD, os.path.basename(src) + "." + key + ".o")
         if not os.path.exists(obj):

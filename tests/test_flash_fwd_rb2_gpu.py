@@ -1,0 +1,116 @@
+"""Two-row-block flash forward (csrc/kernels/flash_fwd2.hip, fwd_kernel<..., NW = 4, RB = 2>): every wave owns two
+32-row query blocks, the O accumulators stay in AGPRs, and there is no per-tile O rescale — the exponent base is
+fixed at a row's first finite tile, and a workgroup whose row maximum later climbs more than 2^32 above its base
+repeats the sweep with the exact maxima.  Checked against an fp32 reference (O and LSE) for causal / full, ragged
+and offset (Sq != Sk) shapes, GQA, fp16, varlen, and inputs built to trigger the second pass."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def rb_env():
+    old = os.environ.get("PADDLE2_AMD_FA_FWD_RB")
+    yield
+    if old is None:
+        os.environ.pop("PADDLE2_AMD_FA_FWD_RB", None)
+    else:
+        os.environ["PADDLE2_AMD_FA_FWD_RB"] = old
+
+
+def _ref(q, k, v, causal, scale):
+    Sq, Hq = q.shape[1], q.shape[2]
+    Sk, Hk = k.shape[1], k.shape[2]
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
+    kr, vr = kf.repeat_interleave(Hq // Hk, 1), vf.repeat_interleave(Hq // Hk, 1)
+    s = qf @ kr.transpose(-1, -2) * scale
+    if causal:
+        i = torch.arange(Sq, device=s.device)[:, None]
+        j = torch.arange(Sk, device=s.device)[None, :]
+        s = s.masked_fill(j > i + (Sk - Sq), float("-inf"))
+    lse = torch.logsumexp(s, -1)
+    p = torch.nan_to_num(torch.softmax(s, -1), nan=0.0)
+    return (p @ vr).transpose(1, 2), lse
+
+
+def _run(q, k, v, causal, scale, rb):
+    from paddle2_amd.ops import torch_ops as T
+
+    os.environ["PADDLE2_AMD_FA_FWD_RB"] = str(rb)
+    return T._flash_fwd_native(q, k, v, causal, scale)
+
+
+def _check(q, k, v, causal, scale, o_tol=1.2e-2):
+    o2, lse2 = _run(q, k, v, causal, scale, 2)
+    o1, lse1 = _run(q, k, v, causal, scale, 1)
+    ro, rl = _ref(q, k, v, causal, scale)
+    seen = torch.isfinite(rl)                       # rows that see at least one key
+    err2 = (o2.float() - ro).abs().max().item()
+    err1 = (o1.float() - ro).abs().max().item()
+    assert err2 <= max(o_tol, 1.5 * err1), (err2, err1)
+    assert torch.allclose(lse2[seen], rl[seen], atol=2e-3, rtol=1e-4)
+    assert torch.all(o2.float()[(~seen).transpose(1, 2)[..., None].expand_as(o2)] == 0)
+    return err2
+
+
+@pytest.mark.parametrize("B,Sq,Sk,Hq,Hk,causal,dt", [
+    (2, 1024, 1024, 4, 4, True, torch.bfloat16),
+    (2, 1024, 1024, 4, 4, False, torch.bfloat16),
+    (1, 777, 1291, 4, 2, True, torch.bfloat16),     # ragged, bottom-right causal offset, GQA
+    (1, 1291, 777, 4, 4, True, torch.bfloat16),     # more queries than keys: rows that see no key
+    (2, 300, 300, 8, 2, False, torch.float16),
+    (1, 256, 256, 2, 2, True, torch.bfloat16),      # one workgroup row block
+    (1, 100, 5000, 2, 1, False, torch.bfloat16),    # one partial row block, long keys
+])
+def test_rb2_matches_reference(rb_env, B, Sq, Sk, Hq, Hk, causal, dt):
+    from paddle2_amd.ops import _native
+
+    _native.require()
+    D = 128
+    g = torch.Generator(device="cpu").manual_seed(7)
+    q = torch.randn(B, Sq, Hq, D, generator=g).to(dt).cuda()
+    k, v = (torch.randn(B, Sk, Hk, D, generator=g).to(dt).cuda() for _ in range(2))
+    _check(q, k, v, causal, D ** -0.5)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_rb2_second_pass(rb_env, causal):
+    """Scores that grow by far more than 2^32 after the first key tiles: the fixed first-tile base would overflow the
+    P range, so the workgroup must take the exact second pass — and still match the reference."""
+    from paddle2_amd.ops import _native
+
+    _native.require()
+    B, S, H, D = 1, 1024, 2, 128
+    g = torch.Generator(device="cpu").manual_seed(3)
+    q = torch.randn(B, S, H, D, generator=g)
+    k = torch.randn(B, S, H, D, generator=g)
+    v = torch.randn(B, S, H, D, generator=g)
+    q = q.abs() * 0.5
+    k = k.abs() * 0.5
+    k[:, 512:] *= 25.0        # late keys: scores ~43 above the early ones (~62 in log2 units > 32)
+    q, k, v = (t.to(torch.bfloat16).cuda() for t in (q, k, v))
+    _check(q, k, v, causal, D ** -0.5, o_tol=2e-2)
+
+
+def test_rb2_varlen(rb_env):
+    from paddle2_amd.ops import _native
+    from paddle2_amd.ops import torch_ops as T
+
+    _native.require()
+    D, H = 128, 4
+    lens = [300, 1000, 17, 512]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32)
+    tot = int(cu[-1])
+    g = torch.Generator(device="cpu").manual_seed(5)
+    q, k, v = (torch.randn(tot, H, D, generator=g).to(torch.bfloat16).cuda() for _ in range(3))
+    outs = {}
+    for rb in (1, 2):
+        os.environ["PADDLE2_AMD_FA_FWD_RB"] = str(rb)
+        outs[rb] = T.flash_attention_varlen(q, k, v, cu, cu, max(lens), max(lens), causal=True)[0].float()
+    for i, L in enumerate(lens):
+        a, b = int(cu[i]), int(cu[i + 1])
+        ro, _ = _ref(q[None, a:b], k[None, a:b], v[None, a:b], True, D ** -0.5)
+        assert (outs[2][a:b] - ro[0]).abs().max().item() <= max(1.2e-2, 1.5 * (outs[1][a:b] - ro[0]).abs().max().item())
