@@ -78,6 +78,10 @@ def parse(argv=None):
     ap.add_argument("--hang-guard-s", type=float, default=0.0,
                     help="bound on the timed region (0: max(300 s, 20 x the measured warm-up step time x steps)); "
                          "past it every rank dumps its last collective per group and exits 124")
+    ap.add_argument("--comm-probe-mb", type=float, default=-1.0,
+                    help="N > 1: per-rank MB of an all-gather / reduce-scatter / all-reduce probe on the world group "
+                         "after the warm-up (bus bandwidth in the metric line: the communicator's own speed beside the "
+                         "scaling curve); -1 = 32 MB on GPUs, 1 MB on CPU; 0 = off")
     ap.add_argument("--gemm-route", default="static", choices=["static", "measure"],
                     help="bf16 Linear GEMM backend per shape: static = the per-pass table (ops/gemm.py: the native "
                          "kernels), measure = time native vs hipBLASLt per (pass, M, N, K) once (incubate/autotune.py "
@@ -144,6 +148,29 @@ def _hang_report(guard_s):
     print(json.dumps(rep, default=str), file=sys.stderr, flush=True)
     sys.stdout.flush()
     os._exit(124)
+
+
+def comm_probe(world, mb, on_gpu):
+    """{op: bus GB/s} of an all-gather, reduce-scatter and all-reduce of ``mb`` MB per rank (bf16) on the world group
+    (fleet.collective_perf's timing, nccl-tests bus conventions), or None for one rank / mb == 0."""
+    if world <= 1 or mb == 0:
+        return None
+    import torch
+
+    from paddle2_amd.distributed import collective as C
+    from paddle2_amd.distributed.fleet.collective_perf import perf_one
+
+    if mb < 0:
+        mb = 32.0 if on_gpu else 1.0
+    nbytes = int(mb * 2**20)
+    out = {"mb_per_rank": mb}
+    for op in ("allgather", "reduce_scatter", "allreduce"):
+        # all-gather sends its input to every peer; reduce-scatter / all-reduce take the full buffer
+        r = perf_one(op, nbytes if op == "allgather" else nbytes * world, C._get_default_group(),
+                     round=5 if on_gpu else 2, dtype=torch.bfloat16)
+        out[op + "_busbw_GBps"] = round(r["busbw_GBs"], 1)
+        out[op + "_ms"] = round(r["time_ms"], 3)
+    return out
 
 
 def main():
@@ -312,6 +339,8 @@ def main():
     guard = threading.Timer(guard_s, _hang_report, args=(guard_s,))
     guard.daemon = True
     guard.start()
+    # communicator probe (outside the timed region, under the guard): bus bandwidth of the collectives sharding-3 runs
+    probe = comm_probe(world, args.comm_probe_mb, torch.cuda.is_available())
 
     if world > 1:
         C.barrier()
@@ -394,6 +423,7 @@ def main():
             "peak_mem_gb_per_rank": peaks,
             "stage3_keep_gathered": getattr(model, "keep_gathered", None),
             "hang_guard_s": round(guard_s, 1),
+            "comm_probe": probe,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

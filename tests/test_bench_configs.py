@@ -70,6 +70,10 @@ def test_bench_reports_communicator_self_diagnosis():
     assert "canary" in res and "ipc_allreduce" in res
     assert res["stage3_keep_gathered"] is False      # CPU: the keep-gathered policy stays off
     assert res["hang_guard_s"] >= 300
+    cp = res["comm_probe"]                           # the communicator's own bus bandwidth beside the number
+    assert cp["mb_per_rank"] == 1.0
+    for op in ("allgather", "reduce_scatter", "allreduce"):
+        assert cp[op + "_busbw_GBps"] > 0 and cp[op + "_ms"] > 0
 
 
 def test_bench_refuses_fallen_back_process_group():
