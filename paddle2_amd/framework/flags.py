@@ -7,6 +7,9 @@ framework's own.  The ones with an effect here:
   FLAGS_check_nan_inf / _level          NaN/Inf checker at Layer boundaries (framework/nan_inf.py)
   FLAGS_cudnn_deterministic             deterministic MIOpen + torch deterministic algorithms (warn-only);
                                         flash-attention bwd sums dQ slabs in order (no fp32 atomics)
+  FLAGS_cudnn_exhaustive_search         MIOpen Find: convolutions benchmark their solvers per shape once and
+                                        keep the fastest (torch.backends.cudnn.benchmark); off under
+                                        FLAGS_cudnn_deterministic
   FLAGS_embedding_deterministic         embedding backward through a sorted, atomics-free reduction
   FLAGS_fraction_of_gpu_memory_to_use   per-process cap of the caching allocator (set at device init)
   FLAGS_gpu_memory_limit_mb             absolute cap (MiB), wins over the fraction
@@ -112,6 +115,17 @@ def _alloc_conf():
 _alloc_conf()
 if _flags.get("FLAGS_cudnn_deterministic"):
     os.environ.setdefault("PADDLE2_AMD_FA_DQ_ATOMIC", "0")
+
+
+def _apply_conv_search():
+    import torch
+
+    torch.backends.cudnn.benchmark = bool(_flags.get("FLAGS_cudnn_exhaustive_search")) and \
+        not _flags.get("FLAGS_cudnn_deterministic")
+
+
+if _flags.get("FLAGS_cudnn_exhaustive_search"):
+    _apply_conv_search()
 if _flags.get("FLAGS_check_nan_inf"):
     from . import nan_inf as _ni  # noqa: E402
 
@@ -155,8 +169,10 @@ def _on_change(key):
         on = bool(_flags[key])
         os.environ["PADDLE2_AMD_FA_DQ_ATOMIC"] = "0" if on else "1"  # flash bwd: ordered dQ slab sum
         torch.backends.cudnn.deterministic = on
-        torch.backends.cudnn.benchmark = False if on else torch.backends.cudnn.benchmark
+        torch.backends.cudnn.benchmark = False if on else bool(_flags.get("FLAGS_cudnn_exhaustive_search"))
         torch.use_deterministic_algorithms(on, warn_only=True)
+    if key == "FLAGS_cudnn_exhaustive_search":
+        _apply_conv_search()
     if key == "FLAGS_paddle_num_threads":
         import torch
 

@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
     ap.add_argument("--data-format", default="NHWC", choices=["NHWC", "NCHW"])
     ap.add_argument("--dtype", default="bfloat16", choices=["bfloat16", "float32"])
+    ap.add_argument("--exhaustive-search", type=int, default=1, choices=[0, 1],
+                    help="FLAGS_cudnn_exhaustive_search: MIOpen Find per conv shape (the reference's ResNet recipes "
+                         "set it); 0 = MIOpen's immediate-mode heuristic")
     args = ap.parse_args()
 
     import torch
@@ -38,6 +41,7 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    paddle.set_flags({"FLAGS_cudnn_exhaustive_search": bool(args.exhaustive_search)})
     strategy = fleet.DistributedStrategy()
     strategy.hybrid_configs = {"dp_degree": world, "mp_degree": 1, "pp_degree": 1, "sharding_degree": 1}
     fleet.init(is_collective=True, strategy=strategy)
@@ -99,6 +103,7 @@ def main():
             "config": {"model": "resnet50", "global_batch": args.batch * world, "batch_per_gpu": args.batch,
                        "data_format": args.data_format, "parallelism": f"dp{world}"},
             "final_loss": round(float(loss), 4),
+            "exhaustive_search": bool(args.exhaustive_search),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if torch.cuda.is_available() else None,
         }), flush=True)
         from paddle2_amd.ops import conv_gemm as CG

@@ -43,3 +43,24 @@ def test_comm_dynamic_and_static_checks():
         assert r["ok"] == [2.0, 4.0, 6.0]
         assert r["caught"] is True
         assert r["static"] is True
+
+
+def test_conv_exhaustive_search_flag_drives_miopen_find():
+    """FLAGS_cudnn_exhaustive_search (reference: conv algorithm search) switches MIOpen Find on through
+    torch.backends.cudnn.benchmark; FLAGS_cudnn_deterministic keeps it off while set."""
+    import torch
+
+    import paddle2_amd as paddle
+
+    old = paddle.get_flags(["FLAGS_cudnn_exhaustive_search", "FLAGS_cudnn_deterministic"])
+    try:
+        paddle.set_flags({"FLAGS_cudnn_exhaustive_search": True})
+        assert torch.backends.cudnn.benchmark
+        paddle.set_flags({"FLAGS_cudnn_deterministic": True})
+        assert not torch.backends.cudnn.benchmark
+        paddle.set_flags({"FLAGS_cudnn_deterministic": False})
+        assert torch.backends.cudnn.benchmark
+        paddle.set_flags({"FLAGS_cudnn_exhaustive_search": False})
+        assert not torch.backends.cudnn.benchmark
+    finally:
+        paddle.set_flags(old)
