@@ -21,6 +21,34 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _find_db_setup(args):
+    """Point MIOpen's user db at a scratch copy of the seed (before the first convolution initialises MIOpen)."""
+    import shutil
+    import tempfile
+
+    if "MIOPEN_USER_DB_PATH" in os.environ:
+        return
+    db = tempfile.mkdtemp(prefix="miopen_db_")
+    if args.find_db and os.path.isdir(args.find_db):
+        for f in os.listdir(args.find_db):
+            if f.endswith(".txt"):
+                shutil.copy(os.path.join(args.find_db, f), db)
+    os.environ["MIOPEN_USER_DB_PATH"] = db
+
+
+def _find_db_save(dst):
+    import shutil
+
+    os.makedirs(dst, exist_ok=True)
+    src = os.environ["MIOPEN_USER_DB_PATH"]
+    for f in os.listdir(src):
+        if f.endswith(".txt"):
+            shutil.copy(os.path.join(src, f), dst)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
@@ -31,7 +59,13 @@ def main():
     ap.add_argument("--exhaustive-search", type=int, default=1, choices=[0, 1],
                     help="FLAGS_cudnn_exhaustive_search: MIOpen Find per conv shape (the reference's ResNet recipes "
                          "set it); 0 = MIOpen's immediate-mode heuristic")
+    ap.add_argument("--find-db", default=os.path.join(ROOT, "tuning", "miopen"),
+                    help="MIOpen user find-db seed directory (text records of the solver Find chose per shape, made "
+                         "by an earlier --save-find-db run): copied to a scratch MIOPEN_USER_DB_PATH so a fresh box "
+                         "skips the search ('' = search from scratch)")
+    ap.add_argument("--save-find-db", default="", help="copy the user find-db here after the run")
     args = ap.parse_args()
+    _find_db_setup(args)
 
     import torch
 
@@ -71,8 +105,13 @@ def main():
         opt.clear_grad()
         return loss
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
+        tw = time.perf_counter()
         loss = step()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if rank == 0:   # progress (MIOpen Find can spend minutes on the first step's shapes)
+            print(f"[resnet50] warmup step {i}: {time.perf_counter() - tw:.1f} s", file=sys.stderr, flush=True)
     from paddle2_amd.distributed import collective as C
 
     def sync():
@@ -111,6 +150,8 @@ def main():
         for k, v in sorted(CG._ROUTE.items(), key=str):
             print("conv routes:", k[0], "x", list(k[1]), "w", list(k[2]), "stride", list(k[3]),
                   "native" if v else "miopen", file=sys.stderr)
+        if args.save_find_db:
+            _find_db_save(args.save_find_db)
     if world > 1:
         C.destroy_process_group()
 
