@@ -22,7 +22,17 @@ ap.add_argument("--no-graph", action="store_true")
 ap.add_argument("--layers", type=int, default=None)
 ap.add_argument("--prefill", default="batch", choices=["batch", "seq"],
                 help="prefill all prompts as one packed batch (default) or one at a time")
+ap.add_argument("--gemm-autotune", default="auto", choices=["auto", "tune", "off"],
+                help="hipBLASLt selection cache (tuning/gemm_gfx950.csv) for the GEMMs that route to hipBLASLt (the "
+                     "wide b64 decode projections): auto = use it if present; tune = search and extend it (eager "
+                     "steps only: TunableOp does not tune inside a HIP-graph capture, use with --no-graph)")
 args = ap.parse_args()
+
+if args.gemm_autotune != "off":
+    from paddle2_amd.incubate import autotune
+
+    if args.gemm_autotune == "tune" or os.path.exists(autotune.DEFAULT_GEMM_CACHE):
+        autotune.enable_gemm_autotune(tuning=args.gemm_autotune == "tune")
 
 paddle.set_device("gpu:0")
 paddle.seed(0)
