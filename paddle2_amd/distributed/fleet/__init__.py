@@ -171,7 +171,7 @@ def distributed_optimizer(optimizer, strategy=None):
     hcg = _hcg()
     if hcg.get_parallel_mode() == ParallelMode.DATA_PARALLEL and hcg.nranks == 1:
         return optimizer
-    from .meta_optimizers.hybrid_parallel_optimizer import HybridParallelOptimizer
+    from .meta_optimizers import HybridParallelOptimizer
 
     return HybridParallelOptimizer(optimizer, hcg, strategy or _state["strategy"])
 

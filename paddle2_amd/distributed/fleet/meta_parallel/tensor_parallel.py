@@ -1,5 +1,5 @@
-"""TensorParallel / ShardingParallel / SegmentParallel model wrappers (reference:
-fleet/meta_parallel/tensor_parallel.py, sharding_parallel.py, segment_parallel.py:26-40).
+"""TensorParallel model wrapper (reference: fleet/meta_parallel/tensor_parallel.py); ShardingParallel and
+SegmentParallel are in sharding_parallel.py / segment_parallel.py.
 
 At construction they make replicated state identical across the relevant groups: non-distributed
 params over the mp group, everything over the dp / sharding / sep groups.  Gradient reduction
@@ -57,20 +57,6 @@ class TensorParallel(MetaParallelBase):
         return self._layers(*inputs, **kwargs)
 
 
-class ShardingParallel(MetaParallelBase):
-    def _prepare_for_model(self):
-        broadcast_sharding_parameters(self._layers, self._hcg)
-        if self._hcg.get_data_parallel_world_size() > 1:
-            broadcast_dp_parameters(self._layers, self._hcg)
-
-
-class SegmentParallel(MetaParallelBase):
-    def _prepare_for_model(self):
-        hcg = self._hcg
-        broadcast_sep_parameters(self._layers, hcg)
-        if hcg.get_model_parallel_world_size() > 1:
-            broadcast_mp_parameters(self._layers, hcg)
-        if hcg.get_sharding_parallel_world_size() > 1:
-            broadcast_sharding_parameters(self._layers, hcg)
-        if hcg.get_data_parallel_world_size() > 1:
-            broadcast_dp_parameters(self._layers, hcg)
+# the sharding / segment wrappers live in their reference modules; re-exported for existing imports
+from .segment_parallel import SegmentParallel  # noqa: E402,F401
+from .sharding_parallel import ShardingParallel  # noqa: E402,F401

@@ -1,45 +1,11 @@
-"""Random-variable domains and constraints (reference: python/paddle/distribution/variable.py, constraint.py)."""
+"""Random-variable domains (reference: python/paddle/distribution/variable.py); the constraints they check are in
+constraint.py."""
 from __future__ import annotations
 
 import torch
 
+from .constraint import Constraint, Range, _Positive, _Real, _Simplex, positive, real, simplex  # noqa: F401
 from .distribution import _wrap, raw
-
-
-class Constraint:
-    def __call__(self, value):
-        raise NotImplementedError
-
-
-class _Real(Constraint):
-    def __call__(self, value):
-        v = raw(value)
-        return _wrap(v == v)
-
-
-class Range(Constraint):
-    def __init__(self, lower, upper):
-        self._lower, self._upper = lower, upper
-
-    def __call__(self, value):
-        v = raw(value)
-        return _wrap((raw(self._lower) <= v) & (v <= raw(self._upper)))
-
-
-class _Positive(Constraint):
-    def __call__(self, value):
-        return _wrap(raw(value) >= 0.0)
-
-
-class _Simplex(Constraint):
-    def __call__(self, value):
-        v = raw(value)
-        return _wrap(torch.all(v >= 0, dim=-1) & ((v.sum(-1) - 1).abs() < 1e-6))
-
-
-real = _Real()
-positive = _Positive()
-simplex = _Simplex()
 
 
 class Variable:

@@ -221,18 +221,23 @@ def limit_by_capacity(expert_count, capacity, n_worker):
 
 
 def prune_gate_by_capacity(gate_idx, expert_count, n_expert, n_worker):
-    """Tokens beyond their expert's remaining count get gate -1 (dropped), in token order."""
-    gi = _raw(gate_idx).reshape(-1).long().clone()
-    left = _raw(expert_count).reshape(-1).long().clone()
-    for i in range(gi.numel()):
-        e = int(gi[i])
-        if e < 0:
-            continue
-        if left[e] > 0:
-            left[e] -= 1
-        else:
-            gi[i] = -1
-    return _wrap(gi.reshape(_raw(gate_idx).shape))
+    """Tokens beyond their expert's remaining count get gate -1 (dropped), in token order: a token is kept iff its
+    rank among the earlier tokens routed to the same expert is below that expert's count (vectorised: stable sort by
+    expert, rank = position - first position of the expert's run; no per-token host loop)."""
+    g = _raw(gate_idx)
+    gi = g.reshape(-1).long()
+    cnt = _raw(expert_count).reshape(-1).long().to(gi.device)
+    ne = cnt.numel()
+    valid = (gi >= 0) & (gi < ne)
+    key = torch.where(valid, gi, torch.full_like(gi, ne))
+    order = torch.argsort(key, stable=True)
+    sk = key[order]
+    rank_sorted = torch.arange(sk.numel(), device=gi.device) - torch.searchsorted(sk, sk, right=False)
+    rank = torch.empty_like(rank_sorted)
+    rank[order] = rank_sorted
+    cap = torch.cat([cnt, cnt.new_zeros(1)])[key]
+    out = torch.where(valid & (rank < cap), gi, torch.full_like(gi, -1))
+    return _wrap(out.to(g.dtype).reshape(g.shape))
 
 
 def random_routing(topk_idx, topk_value, prob):

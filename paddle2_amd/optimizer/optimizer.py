@@ -23,14 +23,7 @@ from .multi_tensor import MultiTensorTable, aligned16
 _wrap = Tensor._wrap
 
 
-class L2Decay:
-    def __init__(self, coeff=0.0):
-        self._coeff = float(coeff)
-
-
-class L1Decay:
-    def __init__(self, coeff=0.0):
-        self._coeff = float(coeff)
+from ..regularizer import L1Decay, L2Decay, as_regularizer  # noqa: E402,F401  (re-exported by paddle.optimizer)
 
 
 def _grad_of(p):
@@ -195,15 +188,8 @@ class Optimizer:
         return None, pg
 
     def _reg_grad(self, p, g):
-        reg = getattr(p, "regularizer", None) or self.regularization
-        if reg is None:
-            return g
-        coeff = reg._coeff if isinstance(reg, (L2Decay, L1Decay)) else float(reg)
-        if coeff == 0.0:
-            return g
-        if isinstance(reg, L1Decay):
-            return g + coeff * torch.sign(p._t).to(g.dtype)
-        return g + coeff * p._t.to(g.dtype)
+        reg = as_regularizer(getattr(p, "regularizer", None) or self.regularization)
+        return g if reg is None else reg.decay(p._t, g)
 
     def _apply(self, params_grads):
         raise NotImplementedError

@@ -27,211 +27,12 @@ def _t(x):
     return x._t if isinstance(x, Tensor) else x
 
 
-# ----------------------------------------------------------------------------- bases
-class BaseQuanter(Layer, metaclass=abc.ABCMeta):
-    def __init__(self):
-        super().__init__()
-
-    @abc.abstractmethod
-    def forward(self, input):
-        ...
-
-    @abc.abstractmethod
-    def scales(self):
-        ...
-
-    @abc.abstractmethod
-    def zero_points(self):
-        ...
-
-    @abc.abstractmethod
-    def quant_axis(self):
-        ...
-
-    @abc.abstractmethod
-    def bit_length(self):
-        ...
-
-
-class BaseObserver(BaseQuanter, metaclass=abc.ABCMeta):
-    def __init__(self):
-        super().__init__()
-
-    @abc.abstractmethod
-    def cal_thresholds(self):
-        ...
-
-
-class ClassWithArguments(metaclass=abc.ABCMeta):
-    def __init__(self, **kwargs):
-        self._kwargs = kwargs
-
-    @property
-    def args(self):
-        return self._kwargs
-
-    @abc.abstractmethod
-    def _get_class(self):
-        ...
-
-    def __str__(self):
-        args = ",".join(f"{k}={v}" for k, v in self._kwargs.items())
-        return f"{self.__class__.__name__}({args})"
-
-    __repr__ = __str__
-
-
-class QuanterFactory(ClassWithArguments):
-    """Holds constructor arguments; ``_instance(layer)`` builds one quanter per quantized layer."""
-
-    def __init__(self, **kwargs):
-        super().__init__(**kwargs)
-        self.partial_class = None
-
-    def _instance(self, layer):
-        return self._get_class()(layer, **self._kwargs)
-
-
-ObserverFactory = QuanterFactory
-
-
-def quanter(class_name):
-    """Decorator: ``@quanter("MyQuanter")`` on a BaseQuanter subclass ``MyQuanterLayer`` registers a
-    factory class named ``MyQuanter`` in the caller's module."""
-
-    def deco(target):
-        import inspect
-
-        frm = inspect.stack()[1]
-        mod = inspect.getmodule(frm[0])
-        factory = type(class_name, (QuanterFactory,), {
-            "__init__": lambda self, *a, **k: QuanterFactory.__init__(self, **k),
-            "_get_class": lambda self: target})
-        if mod is not None:
-            setattr(mod, class_name, factory)
-        return target
-
-    return deco
-
-
-# ----------------------------------------------------------------------------- observers / quanters
-class AbsmaxObserverLayer(BaseObserver):
-    def __init__(self, layer, quant_bits=8):
-        super().__init__()
-        self._quant_bits = quant_bits
-        self.abs_max_val = torch.tensor(1e-7)
-
-    def forward(self, input):
-        x = _t(input)
-        self.abs_max_val = torch.maximum(self.abs_max_val.to(x.device), x.detach().abs().max().float())
-        return input
-
-    def cal_thresholds(self):
-        self.thresholds = self.abs_max_val
-
-    def bit_length(self):
-        return self._quant_bits
-
-    def quant_axis(self):
-        return -1
-
-    def scales(self):
-        return _w(self.abs_max_val.reshape(()).clone())
-
-    def zero_points(self):
-        return None
-
-
-class AbsmaxObserver(QuanterFactory):
-    def __init__(self, quant_bits=8):
-        super().__init__(quant_bits=quant_bits)
-
-    def _get_class(self):
-        return AbsmaxObserverLayer
-
-
-class GroupWiseWeightObserverLayer(BaseObserver):
-    """Per-(group of input rows, output channel) abs-max for weight-only quantization."""
-
-    def __init__(self, layer, quant_bits=8, group_size=128):
-        super().__init__()
-        self._quant_bits, self.group_size = quant_bits, group_size
-        self._max = None
-
-    def forward(self, input):
-        x = _t(input).detach().float()
-        if x.dim() == 2 and x.shape[0] % self.group_size == 0:
-            m = x.reshape(-1, self.group_size, x.shape[1]).abs().amax(1)
-        else:
-            m = x.abs().amax(0, keepdim=True)
-        self._max = m if self._max is None else torch.maximum(self._max, m)
-        return input
-
-    def cal_thresholds(self):
-        pass
-
-    def bit_length(self):
-        return self._quant_bits
-
-    def quant_axis(self):
-        return -1
-
-    def scales(self):
-        return _w(self._max) if self._max is not None else None
-
-    def zero_points(self):
-        return None
-
-
-class GroupWiseWeightObserver(QuanterFactory):
-    def __init__(self, quant_bits=8, group_size=128):
-        super().__init__(quant_bits=quant_bits, group_size=group_size)
-
-    def _get_class(self):
-        return GroupWiseWeightObserverLayer
-
-
-class FakeQuanterWithAbsMaxObserverLayer(BaseQuanter):
-    """Moving-average abs-max fake quanter: scale = accum/state, accum = rate*accum + max|x|."""
-
-    def __init__(self, layer, name=None, moving_rate=0.9, bit_length=8, dtype="float32"):
-        super().__init__()
-        self._moving_rate, self._bit_length = moving_rate, bit_length
-        self.register_buffer("_scale", _w(torch.full((1,), 1e-3)))
-        self.register_buffer("_state", _w(torch.zeros(1)))
-        self.register_buffer("_accum", _w(torch.zeros(1)))
-
-    def forward(self, input):
-        from ..nn.quant.quant_layers import fake_quant_dequant
-
-        x = _t(input)
-        if self.training:
-            with torch.no_grad():
-                cur = x.detach().abs().max().float().reshape(1).to(self._accum._t.device)
-                self._accum._t.mul_(self._moving_rate).add_(cur)
-                self._state._t.mul_(self._moving_rate).add_(1.0)
-                self._scale._t.copy_(self._accum._t / self._state._t)
-        return _w(fake_quant_dequant(x, self._scale._t.to(x.device).reshape(()), self._bit_length))
-
-    def bit_length(self):
-        return self._bit_length
-
-    def quant_axis(self):
-        return -1
-
-    def scales(self):
-        return self._scale
-
-    def zero_points(self):
-        return None
-
-
-class FakeQuanterWithAbsMaxObserver(QuanterFactory):
-    def __init__(self, moving_rate=0.9, bit_length=8, dtype="float32", name=None):
-        super().__init__(name=name, moving_rate=moving_rate, bit_length=bit_length, dtype=dtype)
-
-    def _get_class(self):
-        return FakeQuanterWithAbsMaxObserverLayer
+from .base_quanter import BaseQuanter  # noqa: E402
+from .base_observer import BaseObserver  # noqa: E402
+from .factory import ClassWithArguments, ObserverFactory, QuanterFactory, quanter  # noqa: E402,F401
+from .observers import (AbsmaxObserver, AbsmaxObserverLayer, GroupWiseWeightObserver,  # noqa: E402,F401
+                        GroupWiseWeightObserverLayer)
+from .quanters import FakeQuanterWithAbsMaxObserver, FakeQuanterWithAbsMaxObserverLayer  # noqa: E402,F401
 
 
 class ObserveWrapper(Layer):

@@ -98,7 +98,7 @@ def test_gradient_merge_in_hybrid_optimizer():
 
     import paddle2_amd as paddle
     from paddle2_amd.distributed import fleet
-    from paddle2_amd.distributed.fleet.meta_optimizers.hybrid_parallel_optimizer import HybridParallelOptimizer
+    from paddle2_amd.distributed.fleet.meta_optimizers import HybridParallelOptimizer
 
     s = fleet.DistributedStrategy()
     s.gradient_merge = True
