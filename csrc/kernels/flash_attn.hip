@@ -1658,10 +1658,20 @@ namespace fa {
 void launch_fwd_rb2(bool f16, bool causal, int mode, dim3 grid, hipStream_t st, const void* q, const void* k,
                     const void* v, void* o, float* lse, int B, int Sq, int Sk, int Hq, int Hk, long sq, long sk, long sv,
                     long so, float scale, const Ext& ex);
+// the 16x16x32-MFMA forward (flash_fwd2.hip; PADDLE2_AMD_FA_FWD_MFMA=16)
+void launch_fwd_m16(bool f16, bool causal, int mode, dim3 grid, hipStream_t st, const void* q, const void* k,
+                    const void* v, void* o, float* lse, int B, int Sq, int Sk, int Hq, int Hk, long sq, long sk, long sv,
+                    long so, float scale, const Ext& ex);
 }  // namespace fa
 }  // namespace pd
 
 namespace {
+
+// PADDLE2_AMD_FA_FWD_MFMA = 16: the forward on v_mfma_f32_16x16x32 (D = 128, dense / varlen, no dropout, 4 waves)
+bool fa_fwd_m16() {
+  const char* e = getenv("PADDLE2_AMD_FA_FWD_MFMA");
+  return e && atoi(e) == 16;
+}
 
 template <int D, bool F16>
 void launch_fwd(dim3 grid, hipStream_t st, const void* q, const void* k, const void* v, void* o, float* lse, int B,
@@ -1675,6 +1685,10 @@ void launch_fwd(dim3 grid, hipStream_t st, const void* q, const void* k, const v
 #define PD_FA_FWD_C(MM, DR) \
   if (causal) PD_FA_FWD(true, MM, DR); else PD_FA_FWD(false, MM, DR);
   if constexpr (D == 128) {
+    if (nw == 4 && rb == 1 && mode != 2 && !drop && fa_fwd_m16()) {  // 16x16x32 MFMAs (opt-in)
+      fa::launch_fwd_m16(F16, causal, mode, grid, st, q, k, v, o, lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, ex);
+      return;
+    }
     if (nw == 4 && rb == 2) {  // two row blocks per wave: dense / varlen without dropout
       fa::launch_fwd_rb2(F16, causal, mode, grid, st, q, k, v, o, lse, B, Sq, Sk, Hq, Hk, sq, sk, sv, so, scale, ex);
       return;

@@ -59,13 +59,14 @@ def main():
         scale = D ** -0.5
         ro = ref_slice(q, k, v, causal, scale)
         for rnd in range(rounds):
-            for rb in ("1", "2"):
+            for rb, mf in (("1", "32"), ("2", "32"), ("1", "16")):
                 os.environ["PADDLE2_AMD_FA_FWD_RB"] = rb
+                os.environ["PADDLE2_AMD_FA_FWD_MFMA"] = mf
                 fn = lambda: T._flash_fwd_native(q, k, v, causal, scale)  # noqa: E731
                 ms = timeit(fn)
                 o = fn()[0]
                 err = (o[:1, :, :2].float() - ro).abs().max().item()
-                print(json.dumps({"case": name, "rb": int(rb), "round": rnd, "fwd_ms": round(ms, 4),
+                print(json.dumps({"case": name, "rb": int(rb), "mfma": int(mf), "round": rnd, "fwd_ms": round(ms, 4),
                                   "TFs": round(flops / ms / 1e9, 1), "max_abs_err": round(err, 5)}), flush=True)
 
 

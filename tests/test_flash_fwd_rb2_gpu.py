@@ -1,4 +1,5 @@
-"""Two-row-block flash forward (csrc/kernels/flash_fwd2.hip, fwd_kernel<..., NW = 4, RB = 2>): every wave owns two
+"""Two-row-block flash forward and the 16x16x32-MFMA forward (csrc/kernels/flash_fwd2.hip: fwd_kernel<..., NW = 4,
+RB = 2>, fwd16_kernel).  RB = 2: every wave owns two
 32-row query blocks, the O accumulators stay in AGPRs, and there is no per-tile O rescale — the exponent base is
 fixed at a row's first finite tile, and a workgroup whose row maximum later climbs more than 2^32 above its base
 repeats the sweep with the exact maxima.  Checked against an fp32 reference (O and LSE) for causal / full, ragged
@@ -11,14 +12,18 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+_KNOBS = ("PADDLE2_AMD_FA_FWD_RB", "PADDLE2_AMD_FA_FWD_MFMA")
+
+
 @pytest.fixture
 def rb_env():
-    old = os.environ.get("PADDLE2_AMD_FA_FWD_RB")
+    old = {k: os.environ.get(k) for k in _KNOBS}
     yield
-    if old is None:
-        os.environ.pop("PADDLE2_AMD_FA_FWD_RB", None)
-    else:
-        os.environ["PADDLE2_AMD_FA_FWD_RB"] = old
+    for k, v in old.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
 
 
 def _ref(q, k, v, causal, scale):
@@ -36,15 +41,16 @@ def _ref(q, k, v, causal, scale):
     return (p @ vr).transpose(1, 2), lse
 
 
-def _run(q, k, v, causal, scale, rb):
+def _run(q, k, v, causal, scale, rb, mfma="32"):
     from paddle2_amd.ops import torch_ops as T
 
     os.environ["PADDLE2_AMD_FA_FWD_RB"] = str(rb)
+    os.environ["PADDLE2_AMD_FA_FWD_MFMA"] = mfma
     return T._flash_fwd_native(q, k, v, causal, scale)
 
 
-def _check(q, k, v, causal, scale, o_tol=1.2e-2):
-    o2, lse2 = _run(q, k, v, causal, scale, 2)
+def _check(q, k, v, causal, scale, o_tol=1.2e-2, variant=(2, "32")):
+    o2, lse2 = _run(q, k, v, causal, scale, *variant)
     o1, lse1 = _run(q, k, v, causal, scale, 1)
     ro, rl = _ref(q, k, v, causal, scale)
     seen = torch.isfinite(rl)                       # rows that see at least one key
@@ -65,7 +71,8 @@ def _check(q, k, v, causal, scale, o_tol=1.2e-2):
     (1, 256, 256, 2, 2, True, torch.bfloat16),      # one workgroup row block
     (1, 100, 5000, 2, 1, False, torch.bfloat16),    # one partial row block, long keys
 ])
-def test_rb2_matches_reference(rb_env, B, Sq, Sk, Hq, Hk, causal, dt):
+@pytest.mark.parametrize("variant", [(2, "32"), (1, "16")], ids=["rb2", "mfma16"])
+def test_rb2_matches_reference(rb_env, B, Sq, Sk, Hq, Hk, causal, dt, variant):
     from paddle2_amd.ops import _native
 
     _native.require()
@@ -73,11 +80,12 @@ def test_rb2_matches_reference(rb_env, B, Sq, Sk, Hq, Hk, causal, dt):
     g = torch.Generator(device="cpu").manual_seed(7)
     q = torch.randn(B, Sq, Hq, D, generator=g).to(dt).cuda()
     k, v = (torch.randn(B, Sk, Hk, D, generator=g).to(dt).cuda() for _ in range(2))
-    _check(q, k, v, causal, D ** -0.5)
+    _check(q, k, v, causal, D ** -0.5, variant=variant)
 
 
 @pytest.mark.parametrize("causal", [True, False])
-def test_rb2_second_pass(rb_env, causal):
+@pytest.mark.parametrize("variant", [(2, "32"), (1, "16")], ids=["rb2", "mfma16"])
+def test_rb2_second_pass(rb_env, causal, variant):
     """Scores that grow by far more than 2^32 after the first key tiles: the fixed first-tile base would overflow the
     P range, so the workgroup must take the exact second pass — and still match the reference."""
     from paddle2_amd.ops import _native
@@ -92,10 +100,11 @@ def test_rb2_second_pass(rb_env, causal):
     k = k.abs() * 0.5
     k[:, 512:] *= 25.0        # late keys: scores ~43 above the early ones (~62 in log2 units > 32)
     q, k, v = (t.to(torch.bfloat16).cuda() for t in (q, k, v))
-    _check(q, k, v, causal, D ** -0.5, o_tol=2e-2)
+    _check(q, k, v, causal, D ** -0.5, o_tol=2e-2, variant=variant)
 
 
-def test_rb2_varlen(rb_env):
+@pytest.mark.parametrize("variant", [(2, "32"), (1, "16")], ids=["rb2", "mfma16"])
+def test_rb2_varlen(rb_env, variant):
     from paddle2_amd.ops import _native
     from paddle2_amd.ops import torch_ops as T
 
@@ -107,9 +116,10 @@ def test_rb2_varlen(rb_env):
     g = torch.Generator(device="cpu").manual_seed(5)
     q, k, v = (torch.randn(tot, H, D, generator=g).to(torch.bfloat16).cuda() for _ in range(3))
     outs = {}
-    for rb in (1, 2):
+    for key, (rb, mf) in ((1, (1, "32")), (2, variant)):
         os.environ["PADDLE2_AMD_FA_FWD_RB"] = str(rb)
-        outs[rb] = T.flash_attention_varlen(q, k, v, cu, cu, max(lens), max(lens), causal=True)[0].float()
+        os.environ["PADDLE2_AMD_FA_FWD_MFMA"] = mf
+        outs[key] = T.flash_attention_varlen(q, k, v, cu, cu, max(lens), max(lens), causal=True)[0].float()
     for i, L in enumerate(lens):
         a, b = int(cu[i]), int(cu[i + 1])
         ro, _ = _ref(q[None, a:b], k[None, a:b], v[None, a:b], True, D ** -0.5)
