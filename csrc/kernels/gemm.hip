@@ -860,7 +860,9 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   if ((variant >= 7 && variant <= 10) || variant >= 64) {
     if (pd_gemm_v7(p, layout, epi, variant >= 64 ? variant - 64 : variant - 7, 8 * p.cpx, ws ? ws_bytes : 0, st))
       return (int)hipGetLastError();
-    variant = 6;
+    // outside the TN kernel's domain: the persistent v6, or for the MN-major weight gradient (SCHED bit 15) v4's
+    // spread schedule, which takes any layout
+    variant = (variant >= 64 && ((variant - 64) & (32768 | 65536))) ? 5 : 6;
   }
   if (epi == kEpiRope || epi == kEpiDSwiGLU) return -3;   // the spread TN schedule only (RoPE / SwiGLU backward)
   if (epi == kEpiSwiGLU && bk) return -3;  // K-major gate|up weight: v7 only

@@ -138,6 +138,71 @@ __device__ __forceinline__ void epilogue_v7_rope_x4(const Params& p, f32x4v (&ac
   });
 }
 
+// SCHED bit 15 (MN): both operands MN-major — the weight gradient dW = X^T . dY with X [tokens, K] and dY [tokens, N] as
+// stored (tokens = the reduction).  Same LDS images as v4's MN-major path (gemm_core.h lane_setup / rd_setup): piece
+// (h, i) of a wave fills k rows 16 i + 2 (wave + 4 h) + (lane >> 5) of the [64 k][256] image, 16-B column chunk
+// (lane & 31) ^ (hsw(k) << 1); fragments are two ds_read_b64_tr_b16 each.  Columns past M / N inside a row are read
+// (unused accumulator columns, never stored); the descriptor extent still bounds the operand's last row.
+__device__ __forceinline__ void mn_offsets(unsigned (&v)[8], long ld, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int h = j >> 2, i = j & 3;
+    const int kk = 2 * (wave + 4 * h) + (lane >> 5);
+    const int lc = (lane & 31) ^ (hsw(kk) << 1);
+    v[j] = (unsigned)((((long)kk + 16 * i) * ld + lc * 8) * 2);
+  }
+}
+
+// fp32 main-grad epilogue of the MN-major weight gradient: C = acc (beta 0, the step's first write of the gradient)
+// or C += acc (beta 1, accumulation) with each accumulator taken straight from its AGPRs (gfx950 memory ops take AGPR
+// data), so no accumulator is copied into the VGPRs that hold the next tile's prefetched fragments — the generic form
+// (epilogue_t) spilled 112-153 VGPRs.  beta 1 adds by no-return fp32 atomics: one add per element, so the result is
+// exactly round(C + acc), the read-modify-write's value.  Rows past M are skipped per lane; N % 8 == 0 (host-checked)
+// keeps every 4-column group whole.  Other beta values are declined by the host (v4's spread kernel runs them).
+__device__ __forceinline__ void st_f4_agpr(float* ptr, const f32x4v& a) {
+  asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(ptr), "a"(a) : "memory");
+}
+__device__ __forceinline__ void add_f4_agpr(float* ptr, const f32x4v& a) {
+  asm volatile("global_atomic_add_f32 %0, %1, off\n\t"
+               "global_atomic_add_f32 %0, %2, off offset:4\n\t"
+               "global_atomic_add_f32 %0, %3, off offset:8\n\t"
+               "global_atomic_add_f32 %0, %4, off offset:12"
+               ::"v"(ptr), "a"(a[0]), "a"(a[1]), "a"(a[2]), "a"(a[3]) : "memory");
+}
+__device__ __forceinline__ void epilogue_v7_f32(const Params& p, f32x4v (&acc)[8][4], int tm, int tn, int arow, int bcolw,
+                                                int lane) {
+  float* C = (float*)p.C;
+  const int row0 = tm * BM + arow + (lane & 15);
+  const int c0 = tn * BN + bcolw + 4 * (lane >> 4);
+  float* base = C + (long)row0 * p.ldc + c0;
+  const bool add = p.beta != 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (c0 + 16 * j >= p.N) continue;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (row0 + 16 * i >= p.M) continue;
+      float* cp = base + (long)(16 * i) * p.ldc + 16 * j;
+      if (add) add_f4_agpr(cp, acc[i][j]);
+      else st_f4_agpr(cp, acc[i][j]);
+    }
+  }
+}
+
+// fragment U of k32 step S from stage ST: K-major one ds_read_b128, MN-major two transposed reads (ds_read_b64_tr_b16)
+// off one of 8 per-lane bases with the pair swizzle folded in — step / stage / half as immediates, no VALU per read
+// (a per-read recomputed swizzle, 2 bases instead of 8, ran the Llama weight gradients 10-14 % slower)
+template <bool MN, int U, int S, int ST>
+__device__ __forceinline__ bf16x8 fragx(const Rd4<!MN>& r) {
+  return frag4<!MN, U, S, ST>(r);
+}
+template <bool MN>
+using RdX = Rd4<!MN>;
+template <bool MN>
+__device__ __forceinline__ RdX<MN> rdx_setup(unsigned img, int first, int lane) {
+  return rd4_setup<!MN>(img, first, lane);
+}
+
 template <int EPI, int SCHED>
 __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   constexpr bool BAR4 = SCHED & 1, PRIO = (SCHED & 2) != 0;
@@ -159,6 +224,9 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   constexpr bool NOST = (SCHED & 8192) != 0;
   constexpr bool XDLY = (SCHED & 16384) != 0;
   constexpr bool SWI = EPI == kEpiSwiGLU;
+  // bits 15 / 16: A / B MN-major (the weight gradient: both; the forward on W as stored: B)
+  constexpr bool MNA = (SCHED & 32768) != 0, MNB = (SCHED & 65536) != 0, MN = MNA || MNB;
+  static_assert(!MN || (VS && !CONV && !ROT && !SWI && EPI != kEpiRope), "MN-major: the spread schedule, plain epilogues");
   __shared__ __attribute__((aligned(1024))) char smem_raw[LDS_BYTES];
   const unsigned sbase = (unsigned)(size_t)(lds_char*)smem_raw;
 
@@ -199,37 +267,43 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   };
 
   unsigned va[8], vb[8];
-  kk_offsets<false>(va, p.lda, 0, wave, lane);
-  kk_offsets<SWI>(vb, p.ldb, p.H, wave, lane);
+  if constexpr (MNA) mn_offsets(va, p.lda, wave, lane);
+  else kk_offsets<false>(va, p.lda, 0, wave, lane);
+  if constexpr (MNB) mn_offsets(vb, p.ldb, wave, lane);
+  else kk_offsets<SWI>(vb, p.ldb, p.H, wave, lane);
   const int arow = wm * 128, bcolw = wn * 128;
-  const Rd4<true> ra = rd4_setup<true>(sbase, arow, lane);
-  const Rd4<true> rb = rd4_setup<true>(sbase + B_OFF, bcolw, lane);
+  const RdX<MNA> ra = rdx_setup<MNA>(sbase, arow, lane);
+  const RdX<MNB> rb = rdx_setup<MNB>(sbase + B_OFF, bcolw, lane);
+  // bytes per K-tile along each operand: 64 k-columns (K-major) or 64 k-rows (MN-major)
+  const unsigned kst_a = MNA ? (unsigned)(p.lda * (BK * 2)) : 128u, kst_b = MNB ? (unsigned)(p.ldb * (BK * 2)) : 128u;
   const unsigned wdst = __builtin_amdgcn_readfirstlane(sbase + wave * 1024);
 
   // stream state: bases of the current tile (c*) and of this workgroup's next tile (n*, live if nlive)
   const unsigned a_end = (unsigned)(size_t)p.a_end, b_end = (unsigned)(size_t)p.b_end;
-  auto a_base = [&](int tm) { return (u64)(size_t)(p.A + (long)tm * BM * p.lda); };
-  auto b_base = [&](int tn) { return (u64)(size_t)(p.B + (long)tn * (SWI ? 128 : BN) * p.ldb); };
+  auto a_base = [&](int tm) { return (u64)(size_t)(p.A + (MNA ? (long)tm * BM : (long)tm * BM * p.lda)); };
+  auto b_base = [&](int tn) {
+    return (u64)(size_t)(p.B + (MNB ? (long)tn * BN : (long)tn * (SWI ? 128 : BN) * p.ldb));
+  };
   // unit u of this workgroup: tile slot + u * G, or (TSK, u == nwhole) its tail slice, whose bases start at the
   // slice's first K-tile
   auto unit_tile = [&](int u, int& tm, int& tn) {
     if (TSK && u == nwhole) tile_of(p, whole + slot / p.ksplit, tm, tn);
     else tile_of(p, slot + u * G, tm, tn);
   };
-  auto unit_koff = [&](int u) -> u64 {
-    return (TSK && u == nwhole) ? (u64)(unsigned)((slot % p.ksplit) * ntc) << 7 : 0;
+  auto unit_koff = [&](int u, unsigned kst) -> u64 {
+    return (TSK && u == nwhole) ? (u64)(unsigned)((slot % p.ksplit) * ntc) * kst : 0;
   };
   int ctm, ctn;
   unit_tile(0, ctm, ctn);
-  u64 ca = a_base(ctm) + unit_koff(0), cb = b_base(ctn) + unit_koff(0), na = ca, nb = cb;
+  u64 ca = a_base(ctm) + unit_koff(0, kst_a), cb = b_base(ctn) + unit_koff(0, kst_b), na = ca, nb = cb;
   bool nlive = false;
   auto set_next = [&](int u) {
     nlive = u + 1 < ntile;
     if (nlive) {
       int tm, tn;
       unit_tile(u + 1, tm, tn);
-      na = a_base(tm) + unit_koff(u + 1);
-      nb = b_base(tn) + unit_koff(u + 1);
+      na = a_base(tm) + unit_koff(u + 1, kst_a);
+      nb = b_base(tn) + unit_koff(u + 1, kst_b);
     }
   };
   set_next(0);
@@ -239,12 +313,12 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   // summation order), so the persistent grid's tiles end — and their epilogue stores burst — in two interleaved
   // phases instead of all 256 CUs at once
   const int rot = (ROT && (slot & 1)) ? nt / 2 : 0;
-  auto desc = [&](int kk, u64 cur, u64 nxt, unsigned end) {
+  auto desc = [&](int kk, u64 cur, u64 nxt, unsigned end, unsigned kst) {
     const int ntx = TSK ? ntu : nt;
     const bool nx = kk >= ntx;
     int kt = nx ? kk - ntx : kk;
     if constexpr (ROT) kt = kt + rot >= nt ? kt + rot - nt : kt + rot;
-    const unsigned off = (unsigned)kt << 7;  // * BK * 2 bytes
+    const unsigned off = MN ? (unsigned)kt * kst : (unsigned)kt << 7;  // K-major: * BK * 2 bytes (kst = 128)
     const u64 b = (nx ? nxt : cur) + off;
     const bool live = !nx || nlive;
     return i32x4{(int)(unsigned)b, (int)(unsigned)(b >> 32), live ? (int)(end - (unsigned)b) : 0, 0x00020000};
@@ -257,7 +331,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   // the descriptor code, and that build lost K-tile 1's contribution on gfx950)
   auto desc_a = [&](int kk) {
     if constexpr (!CONV) {
-      return desc(kk, ca, na, a_end);
+      return desc(kk, ca, na, a_end, kst_a);
     } else {
       const bool nx = kk >= nt;
       const int kt = nx ? kk - nt : kk;
@@ -273,7 +347,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   };
   auto descs = [&](int kk, i32x4& sa, i32x4& sb) {
     sa = desc_a(kk);
-    sb = desc(kk, cb, nb, b_end);
+    sb = desc(kk, cb, nb, b_end, kst_b);
   };
 
   bf16x8 xa[8], xb[8], ya[8], yb[8];  // k32 step 0 / step 1 fragments of the current K-tile
@@ -303,8 +377,8 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
   wait_vm<16>();
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
-  sfor<8>([&](auto U) { xb[decltype(U)::value] = frag4<true, decltype(U)::value, 0, 0>(rb); });
-  sfor<8>([&](auto U) { xa[decltype(U)::value] = frag4<true, decltype(U)::value, 0, 0>(ra); });
+  sfor<8>([&](auto U) { xb[decltype(U)::value] = fragx<MNB, decltype(U)::value, 0, 0>(rb); });
+  sfor<8>([&](auto U) { xa[decltype(U)::value] = fragx<MNA, decltype(U)::value, 0, 0>(ra); });
   if constexpr (VS) {
     wait_lgkm<0>();
     __builtin_amdgcn_sched_barrier(0);
@@ -370,7 +444,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
         int kk = k + 2;
         asm volatile("" : "+s"(kk));
         if constexpr (q == 1) {
-          sb = desc(kk, cb, nb, b_end);
+          sb = desc(kk, cb, nb, b_end, kst_b);
           asm volatile("" : "+s"(sb));
         } else {
           sa = desc_a(kk);
@@ -443,10 +517,10 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
         wait_lgkm<0>();
         __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (ra1 >= 0) ya[ra1] = frag4<true, (ra1 < 0 ? 0 : ra1), 1, st>(ra);
-      if constexpr (rb1 >= 0) yb[rb1] = frag4<true, (rb1 < 0 ? 0 : rb1), 1, st>(rb);
-      if constexpr (xa_ >= 0) xa[xa_] = frag4<true, (xa_ < 0 ? 0 : xa_), 0, st ^ 1>(ra);
-      if constexpr (xb_ >= 0) xb[xb_] = frag4<true, (xb_ < 0 ? 0 : xb_), 0, st ^ 1>(rb);
+      if constexpr (ra1 >= 0) ya[ra1] = fragx<MNA, (ra1 < 0 ? 0 : ra1), 1, st>(ra);
+      if constexpr (rb1 >= 0) yb[rb1] = fragx<MNB, (rb1 < 0 ? 0 : rb1), 1, st>(rb);
+      if constexpr (xa_ >= 0) xa[xa_] = fragx<MNA, (xa_ < 0 ? 0 : xa_), 0, st ^ 1>(ra);
+      if constexpr (xb_ >= 0) xb[xb_] = fragx<MNB, (xb_ < 0 ? 0 : xb_), 0, st ^ 1>(rb);
       // ---- MFMA n (B fragment outer, A inner; B as src0: the transposed tile, 4 columns per lane)
       constexpr int nn = n & 63, j = nn >> 3, i = nn & 7;
       const bf16x8(&fa)[8] = n < 64 ? xa : ya;
@@ -467,7 +541,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
           sa = desc_a(kk);
           asm volatile("" : "+s"(sa));
         } else {
-          sb = desc(kk, cb, nb, b_end);
+          sb = desc(kk, cb, nb, b_end, kst_b);
           asm volatile("" : "+s"(sb));
         }
       }
@@ -525,6 +599,8 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
             epilogue_v7_swi_x4<NTS>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
           else
             epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
+        } else if constexpr (EPI == kEpiF32) {
+          epilogue_v7_f32(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
         } else {
           epilogue_t<EPI>(p, acc[h], ctm, ctn, arow, bcolw + 64 * h, lane);
         }
@@ -551,12 +627,49 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_v7_kernel(Params p) {
 bool pd_gemm_v7(const pd::gm::Params& p_in, int layout, int epi, int sched, int cus, long ws_bytes, hipStream_t st) {
   using namespace pd::gm;
   Params p = p_in;
-  if (layout != 3 || epi == kEpiF32 || p.K % 128) return false;
   const long a_bytes = (long)((const char*)p.a_end - (const char*)p.A);
   const long b_bytes = (long)((const char*)p.b_end - (const char*)p.B);
   if (a_bytes <= 0 || b_bytes <= 0 || a_bytes >= 0x7fffffffL || b_bytes >= 0x7fffffffL) return false;
   if (p.ldc % 4 || (size_t)p.C % 16 || (p.C2 && (p.ldc2 % 4 || (size_t)p.C2 % 16))) return false;
   const dim3 grid(std::min(p.tiles_m * p.tiles_n, cus));
+  if (sched & (32768 | 65536)) {
+    // MN-major operands on the persistent spread schedule (bit 15: A, bit 16: B): the weight gradient (layout 0, fp32
+    // main-grad C = product + beta C with beta 0 / 1, or bf16) and the forward on W as stored (layout 1: x K-major, W
+    // N-major; bf16 + bias); every 64-k-row K-tile stride in 32 bits; tail split-K as the TN forward
+    const bool mna = sched & 32768, mnb = sched & 65536;
+    if ((layout & 1) == mna || ((layout >> 1) & 1) == mnb || p.K % 128 || p.C2) return false;
+    if (epi != kEpiF32 && epi != kEpiBF16) return false;
+    if (epi == kEpiF32 && (p.bias || (p.beta != 0.f && p.beta != 1.f))) return false;
+    if (mna && (p.lda % 8 || p.M % 8 || (long)p.lda * 128 * (p.K / BK) >= 0xffffffffL)) return false;
+    if (mnb && (p.ldb % 8 || p.N % 8 || (long)p.ldb * 128 * (p.K / BK) >= 0xffffffffL)) return false;
+    const int nwg = p.tiles_m * p.tiles_n, G = cus, R = nwg % G;
+    const int ks = p.part && ws_bytes > 0 ? tail_plan(nwg, G, p.K / BK, ws_bytes) : 0;
+    if (ks >= 2) {
+      p.ksplit = ks;
+      p.tail_cap = R;
+    }
+    const dim3 wgrid(ks >= 2 ? std::min(nwg - R, G) : grid.x), tgrid(R * ks);
+    const bool whole = ks < 2 || nwg > R;
+#define PD_V7_MN(E, S)                                                                   \
+  {                                                                                      \
+    if (whole) gemm_v7_kernel<E, S><<<wgrid, NTHR4, 0, st>>>(p);                         \
+    if (ks >= 2) {                                                                       \
+      gemm_v7_kernel<E, S | 4096><<<tgrid, NTHR4, 0, st>>>(p);                           \
+      tail_reduce_kernel<E><<<dim3(BM * BN / 1024, R), 256, 0, st>>>(p, nwg - R);        \
+    }                                                                                    \
+  }
+    if (mna && mnb) {
+      if (epi == kEpiF32) PD_V7_MN(kEpiF32, 384 | 32768 | 65536)
+      else PD_V7_MN(kEpiBF16, 384 | 32768 | 65536)
+    } else if (mnb) {
+      PD_V7_MN(kEpiBF16, 384 | 65536)
+    } else {
+      return false;
+    }
+#undef PD_V7_MN
+    return true;
+  }
+  if (layout != 3 || epi == kEpiF32 || p.K % 128) return false;
   if (sched & 16384) {   // XCD-stagger experiment: the per-XCD delay unit from the environment
     const char* d = getenv("PD_GEMM_XCD_DELAY");
     p.kchunk = d ? atoi(d) : 1;

@@ -38,17 +38,22 @@ _GROUP_FORCED = "PADDLE2_AMD_GEMM_GROUP_M" in os.environ
 # (LDS-DMA pieces spread over 100 MFMAs, every fragment read >= 8 MFMAs before use, 3 barriers) + 16-B epilogue
 # stores (v_permlane16_swap pairing) — profiles/r4_gemm_spread.md: the forward / dgrad / SwiGLU default.
 V7_SPREAD = 64 + 384
+# The spread schedule on the persistent v7 kernel with MN-major operands (gemm7.hip SCHED bits 15 / 16 = A / B):
+# V7_MN both — the weight gradient on X and dY as stored (fp32 main-grad or bf16 epilogue); V7_NNF B only — the
+# forward on W as stored (bf16 + bias).  Tail split-K like the TN forward; outside their domain v4's spread kernel.
+V7_MN = 64 + (384 | 32768 | 65536)
+V7_NNF = 64 + (384 | 65536)
 _FORCE = os.environ.get("PADDLE2_AMD_GEMM_VARIANT")
 VARIANT = int(_FORCE) if _FORCE is not None else None
 PASS_VARIANT = {"fwd": V7_SPREAD, "dgrad": V7_SPREAD, "wgrad": 5, "wgrad_bf16": 5, "swiglu": V7_SPREAD,
-                "rope": V7_SPREAD}
+                "rope": V7_SPREAD, "fwd_nn": 5}
 for _k in list(PASS_VARIANT):   # per-pass override: PADDLE2_AMD_GEMM_VARIANT_FWD=6 (the forward on W as is, no W^T)
     _e = os.environ.get("PADDLE2_AMD_GEMM_VARIANT_" + _k.upper())
     if _e:
         PASS_VARIANT[_k] = int(_e)
 # grouped tile order per pass (row tiles that sweep the column tiles together): 4 for the spread TN schedule
 # (forward +2..7 %, dgrad +0..2 % over 8 at M = 32768; profiles/r4_gemm_spread.md), 8 for the wgrad kernels
-PASS_GROUP_M = {"fwd": 4, "dgrad": 4, "swiglu": 4, "wgrad": 8, "wgrad_bf16": 8, "rope": 4}
+PASS_GROUP_M = {"fwd": 4, "dgrad": 4, "swiglu": 4, "wgrad": 8, "wgrad_bf16": 8, "rope": 4, "fwd_nn": 4}
 for _k in list(PASS_GROUP_M):   # per-pass override: PADDLE2_AMD_GEMM_GROUP_M_FWD=2, ..._DGRAD, ..._SWIGLU, ...
     _e = os.environ.get("PADDLE2_AMD_GEMM_GROUP_M_" + _k.upper())
     if _e:
@@ -108,7 +113,8 @@ def _workspace(t):
 
 def _launch(layout, epi, a, lda, b, ldb, c, ldc, c2, ldc2, bias, M, Nn, K, beta=0.0, H=0, name="fwd"):
     v = _variant(name)
-    tail = (epi in (EPI_BF16, EPI_F32) and v in (0, 4, 5)) or (V7_TAILK and epi == EPI_BF16 and v == V7_SPREAD)
+    tail = ((epi in (EPI_BF16, EPI_F32) and v in (0, 4, 5, V7_MN, V7_NNF))
+            or (V7_TAILK and epi == EPI_BF16 and v == V7_SPREAD))
     ws, ws_bytes = _workspace(a) if tail else (0, 0)
     gm = GROUP_M if _GROUP_FORCED else PASS_GROUP_M.get(name, GROUP_M)
     N.native().gemm(layout, epi, a.data_ptr(), lda, b.data_ptr(), ldb, c.data_ptr(), ldc, N.ptr(c2), ldc2,
@@ -128,12 +134,29 @@ def _wt(w):
     return transpose2d(w)
 
 
+# The TN forward transposes W once per call (one HBM pass over the weight); the spread schedule on W as stored
+# (variant 5: B operand N-major through transposed LDS reads) skips it but runs its MFMA loop ~2 % slower.  The
+# transpose is a fixed cost per weight and the loop cost scales with M, so short token batches take the N-major
+# form: GPT-3 13B bf16 (M = 4096) 11,043 / 11,079 -> 11,169 / 11,149 tok/s, Llama-2-7B (M = 32768) 27,810 -> 27,231
+# on the TN default's side (profiles/r6_fwd_nn_small_m.md).  Rows at or below this use variant 5; "0" disables.
+FWD_NN_MAX_M = int(os.environ.get("PADDLE2_AMD_GEMM_FWD_NN_MAX_M", "8192"))
+
+
+def _fwd_nn(M):
+    return (0 < M <= FWD_NN_MAX_M and VARIANT is None and PASS_VARIANT["fwd"] == V7_SPREAD
+            and "PADDLE2_AMD_GEMM_VARIANT_FWD" not in os.environ)
+
+
 def mm_fwd(x2, w, bias=None, out=None):
     """y[M, N] = x2[M, K] @ w[K, N] (+ bias[N]), bf16."""
     M, K = x2.shape
     Nn = w.shape[1]
     if out is None:
         out = torch.empty(M, Nn, dtype=x2.dtype, device=x2.device)
+    if _fwd_nn(M):
+        _launch(LAYOUT_AK, EPI_BF16, x2, x2.stride(0), w, w.stride(0), out, out.stride(0), None, 0, bias, M, Nn, K,
+                name="fwd_nn")
+        return out
     if _v7("fwd", K):
         wt = _wt(w)
         _launch(LAYOUT_AK | LAYOUT_BK, EPI_BF16, x2, x2.stride(0), wt, wt.stride(0), out, out.stride(0), None, 0,

@@ -327,6 +327,61 @@ def test_swiglu_mlp_node_matches_fp32(monkeypatch):
         assert _rel(got, ref) < 2e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 1536, 4096), (520, 776, 2048), (4096, 5120, 4096), (2048, 256, 8192),
+                                   (256, 4096, 1024)])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_wgrad_v7_mn_matches_v5_and_fp64(M, N, K, beta, schedule, monkeypatch):
+    """The weight gradient on the persistent spread kernel with both operands MN-major (gemm7.hip SCHED bit 15): the
+    same products in the same order as v4's spread wgrad (bit-identical without the tail split-K; beta 1 adds by
+    one fp32 atomic per element = the read-modify-write's rounding), and vs fp64 with the split, incl. ragged tiles
+    (M, N not multiples of 256) and the bf16 epilogue."""
+    if schedule is not None:
+        pytest.skip("compares two fixed schedules")
+    # out[M, N] = x[K, M]^T @ dy[K, N] (K tokens)
+    x, dy = _rand(K, M, seed=60), _rand(K, N, seed=61)
+    out0 = torch.randn(M, N, device=dev)
+    ref = x.double().t() @ dy.double() + (beta * out0.double() if beta else 0)
+    res = {}
+    for split in (False, True):
+        monkeypatch.setattr(G, "SPLITK", split)
+        for v in (5, G.V7_MN):
+            monkeypatch.setattr(G, "VARIANT", v)
+            o = out0.clone()
+            G.mm_wgrad(x, dy, o, beta=beta)
+            res[(split, v)] = o
+    assert torch.equal(res[(False, 5)], res[(False, G.V7_MN)])
+    assert _rel(res[(True, G.V7_MN)], ref) < 1e-5
+    assert _rel(res[(True, G.V7_MN)], res[(False, G.V7_MN)]) < 1e-6
+    monkeypatch.setattr(G, "VARIANT", G.V7_MN)
+    ob = G.mm_wgrad_bf16(x, dy)
+    assert _rel(ob, x.float().t() @ dy.float()) < 8e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 5120, 5120), (1000, 1000, 2048), (256, 15360, 5120), (8192, 4096, 4096)])
+def test_fwd_nn_small_m_matches_tn(M, N, K, schedule, monkeypatch):
+    """Short token batches run the forward on W as stored (spread schedule, B N-major, no W^T pass; v4's kernel or the
+    persistent v7 one): the same products in the same order as the TN route on W^T, so bit-identical without the tail
+    split-K, and vs fp32 with it."""
+    if schedule is not None:
+        pytest.skip("per-pass routing only")
+    x, w, b = _rand(M, K, seed=50), _rand(K, N, seed=51, scale=K ** -0.5), _rand(N, seed=52, scale=0.5)
+    assert G._fwd_nn(M)
+    ref = x.float() @ w.float() + b.float()
+    ys = {}
+    for split in (True, False):
+        monkeypatch.setattr(G, "SPLITK", split)
+        monkeypatch.setattr(G, "V7_TAILK", split)
+        for v in (5, G.V7_NNF):   # v4's spread kernel / the persistent v7 kernel with W N-major
+            monkeypatch.setitem(G.PASS_VARIANT, "fwd_nn", v)
+            ys[(split, v)] = G.mm_fwd(x, w, b)
+            assert _rel(ys[(split, v)], ref) < 8e-3
+    monkeypatch.setattr(G, "FWD_NN_MAX_M", 0)
+    assert not G._fwd_nn(M)
+    y_tn = G.mm_fwd(x, w, b)
+    assert torch.equal(ys[(False, 5)], y_tn)
+    assert torch.equal(ys[(False, G.V7_NNF)], y_tn)
+
+
 @pytest.mark.parametrize("M,N,K,bias", [(4096, 5120, 5120, False), (4096, 5120, 5120, True), (1000, 1000, 2048, True),
                                         (640, 4096, 1024, False)])
 def test_v7_tail_splitk_matches_fp32(M, N, K, bias, monkeypatch):
