@@ -858,11 +858,14 @@ extern "C" int pd_gemm(int layout, int epi, const void* A, long lda, const void*
   hipStream_t st = (hipStream_t)stream;
   // v7 (gemm7.hip): the TN schedule, variants 7..10 = its SCHED 0..3; problems outside its domain run v6
   if ((variant >= 7 && variant <= 10) || variant >= 64) {
-    if (pd_gemm_v7(p, layout, epi, variant >= 64 ? variant - 64 : variant - 7, 8 * p.cpx, ws ? ws_bytes : 0, st))
+    const int sched = variant >= 64 ? variant - 64 : variant - 7;
+    if (pd_gemm_v7(p, layout, epi, sched, 8 * p.cpx, ws ? ws_bytes : 0, st)) return (int)hipGetLastError();
+    const bool mn = variant >= 64 && (sched & (32768 | 65536));
+    // an MN-major schedule asked for a problem whose operands are both K-major: the same schedule on the TN kernel
+    if (mn && layout == 3 && pd_gemm_v7(p, layout, epi, sched & ~(32768 | 65536), 8 * p.cpx, ws ? ws_bytes : 0, st))
       return (int)hipGetLastError();
-    // outside the TN kernel's domain: the persistent v6, or for the MN-major weight gradient (SCHED bit 15) v4's
-    // spread schedule, which takes any layout
-    variant = (variant >= 64 && ((variant - 64) & (32768 | 65536))) ? 5 : 6;
+    // outside the kernel's domain: the persistent v6, or for the MN-major schedules v4's spread kernel (any layout)
+    variant = mn ? 5 : 6;
   }
   if (epi == kEpiRope || epi == kEpiDSwiGLU) return -3;   // the spread TN schedule only (RoPE / SwiGLU backward)
   if (epi == kEpiSwiGLU && bk) return -3;  // K-major gate|up weight: v7 only

@@ -45,15 +45,15 @@ V7_MN = 64 + (384 | 32768 | 65536)
 V7_NNF = 64 + (384 | 65536)
 _FORCE = os.environ.get("PADDLE2_AMD_GEMM_VARIANT")
 VARIANT = int(_FORCE) if _FORCE is not None else None
-PASS_VARIANT = {"fwd": V7_SPREAD, "dgrad": V7_SPREAD, "wgrad": 5, "wgrad_bf16": 5, "swiglu": V7_SPREAD,
-                "rope": V7_SPREAD, "fwd_nn": 5}
+PASS_VARIANT = {"fwd": V7_SPREAD, "dgrad": V7_SPREAD, "wgrad": V7_MN, "wgrad_acc": 5, "wgrad_bf16": V7_MN,
+                "swiglu": V7_SPREAD, "rope": V7_SPREAD, "fwd_nn": V7_NNF}
 for _k in list(PASS_VARIANT):   # per-pass override: PADDLE2_AMD_GEMM_VARIANT_FWD=6 (the forward on W as is, no W^T)
     _e = os.environ.get("PADDLE2_AMD_GEMM_VARIANT_" + _k.upper())
     if _e:
         PASS_VARIANT[_k] = int(_e)
 # grouped tile order per pass (row tiles that sweep the column tiles together): 4 for the spread TN schedule
 # (forward +2..7 %, dgrad +0..2 % over 8 at M = 32768; profiles/r4_gemm_spread.md), 8 for the wgrad kernels
-PASS_GROUP_M = {"fwd": 4, "dgrad": 4, "swiglu": 4, "wgrad": 8, "wgrad_bf16": 8, "rope": 4, "fwd_nn": 4}
+PASS_GROUP_M = {"fwd": 4, "dgrad": 4, "swiglu": 4, "wgrad": 8, "wgrad_acc": 8, "wgrad_bf16": 8, "rope": 4, "fwd_nn": 4}
 for _k in list(PASS_GROUP_M):   # per-pass override: PADDLE2_AMD_GEMM_GROUP_M_FWD=2, ..._DGRAD, ..._SWIGLU, ...
     _e = os.environ.get("PADDLE2_AMD_GEMM_GROUP_M_" + _k.upper())
     if _e:
@@ -134,12 +134,12 @@ def _wt(w):
     return transpose2d(w)
 
 
-# The TN forward transposes W once per call (one HBM pass over the weight); the spread schedule on W as stored
-# (variant 5: B operand N-major through transposed LDS reads) skips it but runs its MFMA loop ~2 % slower.  The
-# transpose is a fixed cost per weight and the loop cost scales with M, so short token batches take the N-major
-# form: GPT-3 13B bf16 (M = 4096) 11,043 / 11,079 -> 11,169 / 11,149 tok/s, Llama-2-7B (M = 32768) 27,810 -> 27,231
-# on the TN default's side (profiles/r6_fwd_nn_small_m.md).  Rows at or below this use variant 5; "0" disables.
-FWD_NN_MAX_M = int(os.environ.get("PADDLE2_AMD_GEMM_FWD_NN_MAX_M", "8192"))
+# The forward on W as stored (B operand N-major through transposed LDS reads) instead of the TN kernel on a per-call
+# W^T: the persistent spread kernel with W N-major (V7_NNF) ties the TN route at M = 32768 (Llama-2-7B 28,036 vs
+# 28,033 tok/s) and wins at M = 4096 (GPT-3 13B 11,563 -> 11,780) — no transpose pass, no transient W^T.  (v4's
+# spread kernel on W, variant 5, lost 2.1 % at M = 32768: profiles/r6_gemm_mn_major.md.)  Rows at or below this take
+# it; "0" keeps every forward on the TN route.
+FWD_NN_MAX_M = int(os.environ.get("PADDLE2_AMD_GEMM_FWD_NN_MAX_M", str(1 << 30)))
 
 
 def _fwd_nn(M):
@@ -182,8 +182,10 @@ def mm_wgrad(x2, dy2, out, beta=0.0):
     M, K = x2.shape
     Nn = dy2.shape[1]
     assert out.dtype == torch.float32 and out.shape == (K, Nn) and out.stride(1) == 1
+    # the step's first write (beta 0) on the persistent MN-major kernel; accumulation (beta != 0) on v4's spread
+    # kernel, whose read-modify-write epilogue beats the persistent kernel's atomic adds (profiles/r6_gemm_mn_major.md)
     _launch(0, EPI_F32, x2, x2.stride(0), dy2, dy2.stride(0), out, out.stride(0), None, 0, None, K, Nn, M, beta,
-            name="wgrad")
+            name="wgrad" if beta == 0 else "wgrad_acc")
     return out
 
 

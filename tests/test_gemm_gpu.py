@@ -225,7 +225,7 @@ def test_schedule_variants_bitwise_equal(M, N, K, monkeypatch, schedule):
     monkeypatch.setattr(G, "SPLITK", False)   # tail split-K sums K-slices in another order (v2 / v4)
     outs = []
     swi = (N // 2) % 32 == 0
-    for v in (0, 4, 5, 6, 7, 8, 9, 10, G.V7_SPREAD, 64 + 128):  # v5: v4 spread; v7 (TN) incl. spread
+    for v in (0, 4, 5, 6, 7, 8, 9, 10, G.V7_SPREAD, 64 + 128, G.V7_MN):  # v5: v4 spread; v7 (TN) incl. spread
         monkeypatch.setattr(G, "VARIANT", v)
         o32 = torch.zeros(K, N, device=dev)
         G.mm_wgrad(x, dy, o32)
