@@ -188,6 +188,10 @@ struct Ext {
   bf16* ds_out;
   long ds_per_bh;
   int pair_order;       // bwd: dispatch a (b, kv head) pair's key blocks together on one XCD (needs Hk*B % 8 == 0)
+  // bwd, 8 waves (PADDLE2_AMD_FA_BWD_OPT): bit 0 = waves 4-7 at s_setprio 1 (the second-dispatched half loses every
+  // arbitration otherwise, MI355X_MICROARCH "Two waves per SIMD" item 4); bit 1 = the dQ slices run on waves 4-7
+  // instead of 0-3 (the half that finishes its S / dP / dV / dK MFMAs later takes the dQ tail)
+  int bwd_opt;
 };
 
 // Counter-based dropout mask: a stateless 32-bit hash of (seed, batch*head, query, key), so the backward
@@ -943,6 +947,10 @@ __global__ __launch_bounds__(NWB * 64, (NWB == 4 && D <= 128) ? 2 : 1) void bwd_
   const int group = Hq / Hk;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
+  // the wave's dQ slice index base (wave-uniform): wv, or with bwd_opt bit 1 and 8 waves wv ^ 4 (waves 4-7 take the
+  // slices; waves 0-3 start at >= DT and skip the dQ loop)
+  const int wq = (NW == 8 && (ex.bwd_opt & 2)) ? (wv ^ 4) : wv;
+  if (NW == 8 && (ex.bwd_opt & 1) && wv >= 4) __builtin_amdgcn_s_setprio(1);
   const int k0 = kblk * BNK;
   int Sq = SqMax, Sk = SkMax;
   long qt0 = (long)b * SqMax, kt0 = (long)b * SkMax;
@@ -1063,8 +1071,8 @@ __global__ __launch_bounds__(NWB * 64, (NWB == 4 && D <= 128) ? 2 : 1) void bwd_
   // transposed K^T reads for dQ (natural k): rows 16ks + 8hh + qq (+4); chunk wv*4 + cb
   const int rqa = 8 * hh + qq, rqb = rqa + 4;
   // (relative to smem: KOFF folded into the lane base, the per-ks step stays an immediate < 64 KiB)
-  int o_kqA = KOFF + rqa * (D * 2) + ((((wv * 4 + cb) ^ msk(rqa)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
-  int o_kqB = KOFF + rqb * (D * 2) + ((((wv * 4 + cb) ^ msk(rqb)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
+  int o_kqA = KOFF + rqa * (D * 2) + ((((wq * 4 + cb) ^ msk(rqa)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
+  int o_kqB = KOFF + rqb * (D * 2) + ((((wq * 4 + cb) ^ msk(rqb)) & (NCH - 1)) << 4) + ((pp & 1) << 3);
   // dS image [32 q][BNK keys]: A-operand row reads and this lane's column writes
   constexpr int SNCH = BNK / 8;
   int o_srow = r * (BNK * 2) + (((h ^ msk(r)) & (SNCH - 1)) << 4);
@@ -1105,7 +1113,7 @@ __global__ __launch_bounds__(NWB * 64, (NWB == 4 && D <= 128) ? 2 : 1) void bwd_
       const int hqd4 = Hq * D * 4;
       const __amdgpu_buffer_rsrc_t rs = make_rsrc_u(dQs + (long)pend_q0 * Hq * D + (long)pend_hq * D, BMQ * hqd4);
 #pragma unroll
-      for (int dsl = wv; dsl < DT; dsl += NW) {
+      for (int dsl = wq; dsl < DT; dsl += NW) {
         const int vo = 4 * h * hqd4 + (dsl * 32 + r) * 4;
 #pragma unroll
         for (int i = 0; i < 16; ++i)
@@ -1252,9 +1260,9 @@ __global__ __launch_bounds__(NWB * 64, (NWB == 4 && D <= 128) ? 2 : 1) void bwd_
     // Slice dsl's K^T chunk is (dsl*4 + cb) ^ m with m < 16: for dsl = wv + NW that is the wave's own
     // chunk + 16 (bit 4 untouched by the XOR), i.e. +256 B on the lane base
 #pragma unroll
-    for (int dsl = wv; dsl < DT; dsl += NW) {
+    for (int dsl = wq; dsl < DT; dsl += NW) {
       f32x16 dq = f32x16{};
-      const int kq_shift = (dsl - wv) * 64;
+      const int kq_shift = (dsl - wq) * 64;
 #pragma unroll
       for (int ks = 0; ks < BNK / 16; ++ks) {
         const bf16x8 a = lds_b128(simg, o_srow ^ (ks << 5));
@@ -1938,6 +1946,7 @@ extern "C" int pd_flash_bwd_ext(int dt, const void* q, const void* k, const void
   // PADDLE2_AMD_FA_BWD_ORDER = pair: co-dispatch a pair's key blocks (L2 reuse of Q / dO) instead of heaviest first
   if (const char* e = getenv("PADDLE2_AMD_FA_BWD_ORDER"))
     ex.pair_order = (strcmp(e, "pair") == 0 && (Hk * B) % 8 == 0) ? 1 : 0;
+  if (const char* e = getenv("PADDLE2_AMD_FA_BWD_OPT")) ex.bwd_opt = atoi(e) & 3;
   if (split) {
     ex.ds_out = (bf16*)ds;
     ex.ds_per_bh = fa_ds_per_bh(Sq, Sk, D, causal);
