@@ -19,6 +19,9 @@
 //    A-fragment-major so a K-tile can start after 9 of its 16 step-0 reads;
 //  * SCHED bit 0: per-operand barriers (4 per K-tile: B's stage is released after B's step-1 reads and A's after
 //    A's; tile t+1's B is waited for before its A) instead of 2;  bit 1: s_setprio 1 around the MFMA stream.
+//  * SCHED bits 15 / 16 (spread schedule only): A / B MN-major — v4's MN-major LDS images and transposed fragment
+//    reads on this persistent kernel: the weight gradient on X and dY as stored (both bits, fp32 main grad stored
+//    from the AGPRs) and the forward on W as stored (bit 16), so no W^T pass (profiles/r6_gemm_mn_major.md).
 #include "gemm_tn.h"
 
 namespace pd {

@@ -46,14 +46,19 @@ V7_NNF = 64 + (384 | 65536)
 _FORCE = os.environ.get("PADDLE2_AMD_GEMM_VARIANT")
 VARIANT = int(_FORCE) if _FORCE is not None else None
 PASS_VARIANT = {"fwd": V7_SPREAD, "dgrad": V7_SPREAD, "wgrad": V7_MN, "wgrad_acc": 5, "wgrad_bf16": V7_MN,
-                "swiglu": V7_SPREAD, "rope": V7_SPREAD, "fwd_nn": V7_NNF}
+                "swiglu": V7_SPREAD, "rope": V7_SPREAD, "fwd_nn": V7_NNF, "fwd_nn_wide": V7_NNF, "wgrad_short": V7_MN}
 for _k in list(PASS_VARIANT):   # per-pass override: PADDLE2_AMD_GEMM_VARIANT_FWD=6 (the forward on W as is, no W^T)
     _e = os.environ.get("PADDLE2_AMD_GEMM_VARIANT_" + _k.upper())
     if _e:
         PASS_VARIANT[_k] = int(_e)
 # grouped tile order per pass (row tiles that sweep the column tiles together): 4 for the spread TN schedule
 # (forward +2..7 %, dgrad +0..2 % over 8 at M = 32768; profiles/r4_gemm_spread.md), 8 for the wgrad kernels
-PASS_GROUP_M = {"fwd": 4, "dgrad": 4, "swiglu": 4, "wgrad": 8, "wgrad_acc": 8, "wgrad_bf16": 8, "rope": 4, "fwd_nn": 4}
+# the N-major forward: 4, but 2 for long outputs wider than 16384 columns (M >= 16384: gate|up 22016 at 32768 tokens
+# 4.24 -> 4.08 ms, 8 / 16 lose 10-22 %; at 4096 tokens 4 stays best); the MN-major wgrad: 8, but 4 for short token
+# reductions into wide outputs (<= 8192 tokens, N >= 2 M: GPT-3 13B qkv / fc1 -4 %) — profiles/r6_gemm_mn_major.md,
+# r6/gemm_groupm_r6w.jsonl, r6/gemm_groupm_r6x.jsonl
+PASS_GROUP_M = {"fwd": 4, "dgrad": 4, "swiglu": 4, "wgrad": 8, "wgrad_acc": 8, "wgrad_bf16": 8, "rope": 4, "fwd_nn": 4,
+                "fwd_nn_wide": 2, "wgrad_short": 4}
 for _k in list(PASS_GROUP_M):   # per-pass override: PADDLE2_AMD_GEMM_GROUP_M_FWD=2, ..._DGRAD, ..._SWIGLU, ...
     _e = os.environ.get("PADDLE2_AMD_GEMM_GROUP_M_" + _k.upper())
     if _e:
@@ -155,7 +160,7 @@ def mm_fwd(x2, w, bias=None, out=None):
         out = torch.empty(M, Nn, dtype=x2.dtype, device=x2.device)
     if _fwd_nn(M):
         _launch(LAYOUT_AK, EPI_BF16, x2, x2.stride(0), w, w.stride(0), out, out.stride(0), None, 0, bias, M, Nn, K,
-                name="fwd_nn")
+                name="fwd_nn_wide" if Nn > 16384 and M >= 16384 else "fwd_nn")
         return out
     if _v7("fwd", K):
         wt = _wt(w)
@@ -184,8 +189,9 @@ def mm_wgrad(x2, dy2, out, beta=0.0):
     assert out.dtype == torch.float32 and out.shape == (K, Nn) and out.stride(1) == 1
     # the step's first write (beta 0) on the persistent MN-major kernel; accumulation (beta != 0) on v4's spread
     # kernel, whose read-modify-write epilogue beats the persistent kernel's atomic adds (profiles/r6_gemm_mn_major.md)
+    name = "wgrad_acc" if beta != 0 else ("wgrad_short" if M <= 8192 and Nn >= 2 * K else "wgrad")
     _launch(0, EPI_F32, x2, x2.stride(0), dy2, dy2.stride(0), out, out.stride(0), None, 0, None, K, Nn, M, beta,
-            name="wgrad" if beta == 0 else "wgrad_acc")
+            name=name)
     return out
 
 

@@ -357,7 +357,8 @@ def test_wgrad_v7_mn_matches_v5_and_fp64(M, N, K, beta, schedule, monkeypatch):
     assert _rel(ob, x.float().t() @ dy.float()) < 8e-3
 
 
-@pytest.mark.parametrize("M,N,K", [(4096, 5120, 5120), (1000, 1000, 2048), (256, 15360, 5120), (8192, 4096, 4096)])
+@pytest.mark.parametrize("M,N,K", [(4096, 5120, 5120), (1000, 1000, 2048), (256, 15360, 5120), (8192, 4096, 4096),
+                                   (512, 22016, 1024)])
 def test_fwd_nn_small_m_matches_tn(M, N, K, schedule, monkeypatch):
     """Short token batches run the forward on W as stored (spread schedule, B N-major, no W^T pass; v4's kernel or the
     persistent v7 one): the same products in the same order as the TN route on W^T, so bit-identical without the tail
@@ -373,6 +374,7 @@ def test_fwd_nn_small_m_matches_tn(M, N, K, schedule, monkeypatch):
         monkeypatch.setattr(G, "V7_TAILK", split)
         for v in (5, G.V7_NNF):   # v4's spread kernel / the persistent v7 kernel with W N-major
             monkeypatch.setitem(G.PASS_VARIANT, "fwd_nn", v)
+            monkeypatch.setitem(G.PASS_VARIANT, "fwd_nn_wide", v)
             ys[(split, v)] = G.mm_fwd(x, w, b)
             assert _rel(ys[(split, v)], ref) < 8e-3
     monkeypatch.setattr(G, "FWD_NN_MAX_M", 0)
