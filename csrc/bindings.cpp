@@ -77,7 +77,9 @@ int pd_cache_write(const void*, const void*, long, long, void*, void*, long, lon
 long pd_bn_workspace(int, long, int);
 int pd_wo_splits(int, int, int, int);
 int pd_dec_splits(int, int, int);
-int pd_dec_gemm(const void*, const void*, const void*, void*, float*, int, int, int, int, int, int*, void*);
+int pd_dec_gemm(const void*, const void*, const void*, void*, float*, int, int, int, int, int, int*, void*, int);
+int pd_dec_reduce(const float*, int, int, int, const void*, void*, void*);
+int pd_norm_fwd_part(int, const float*, int, const void*, const void*, void*, void*, int, int, float, void*);
 int pd_dec64_gemm(const void*, const void*, const void*, void*, int, int, int, int, int, void*);
 int pd_dec64_rt(int);
 int pd_dec64s_gemm(const void*, const void*, const void*, void*, float*, int, int, int, int, int, int, void*);
@@ -462,12 +464,21 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("dec64s_workspace", &pd_dec64s_workspace);
   m.def("dec_gemm", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t out, uintptr_t ws, int M, int N, int K,
-                       int S, uintptr_t st, int glu, uintptr_t cnt) {
+                       int S, uintptr_t st, int glu, uintptr_t cnt, int noreduce) {
     check(pd_dec_gemm(P<const void*>(x), P<const void*>(w), P<const void*>(bias), P<void*>(out), P<float*>(ws), M, N,
-                      K, S, glu, P<int*>(cnt), P<void*>(st)),
+                      K, S, glu, P<int*>(cnt), P<void*>(st), noreduce),
           "dec_gemm");
   }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("out"), py::arg("ws"), py::arg("M"), py::arg("N"),
-     py::arg("K"), py::arg("S"), py::arg("st"), py::arg("glu") = 0, py::arg("cnt") = 0);
+     py::arg("K"), py::arg("S"), py::arg("st"), py::arg("glu") = 0, py::arg("cnt") = 0, py::arg("noreduce") = 0);
+  m.def("dec_reduce", [](uintptr_t ws, int S, int M, int N, uintptr_t bias, uintptr_t out, uintptr_t st) {
+    check(pd_dec_reduce(P<const float*>(ws), S, M, N, P<const void*>(bias), P<void*>(out), P<void*>(st)), "dec_reduce");
+  });
+  m.def("norm_fwd_part", [](int wdt, uintptr_t part, int S, uintptr_t res, uintptr_t w, uintptr_t y, uintptr_t res_out,
+                            int M, int N, float eps, uintptr_t st) {
+    check(pd_norm_fwd_part(wdt, P<const float*>(part), S, P<const void*>(res), P<const void*>(w), P<void*>(y),
+                           P<void*>(res_out), M, N, eps, P<void*>(st)),
+          "norm_fwd_part");
+  });
   m.def("wo_splits", &pd_wo_splits);
   m.def("wo_workspace", &pd_wo_workspace);
   m.def("wo_gemm", [](int int4, uintptr_t x, uintptr_t w, uintptr_t cs, uintptr_t gs, int group, uintptr_t bias,

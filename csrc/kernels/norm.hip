@@ -248,11 +248,14 @@ __device__ __forceinline__ float block_sum4(float v, float* sm) {
   return t;
 }
 
-template <typename T, typename WT, int MAXV, bool LAYERNORM, bool HAS_RES, bool HAS_BIAS>
+// PART (decode, bf16): x is not a tensor but the S fp32 split-K partials [S, M, N] of the decode GEMM that produced it
+// (pd_dec_gemm noreduce): summed here in split order and rounded to T — exactly wo_reduce_kernel's bf16 output, so the
+// reduce launch between the projection and its residual-add + norm disappears
+template <typename T, typename WT, int MAXV, bool LAYERNORM, bool HAS_RES, bool HAS_BIAS, bool PART = false>
 __global__ __launch_bounds__(kNormBlock) void norm_fwd_row_kernel(
     const T* __restrict__ x, const T* __restrict__ res, const WT* __restrict__ w, const WT* __restrict__ b,
     T* __restrict__ y, T* __restrict__ res_out, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-    int M, int N, float eps) {
+    int M, int N, float eps, const float* __restrict__ part = nullptr, int S = 0) {
   constexpr int V = 16 / sizeof(T);
   __shared__ float sm[4];
   const int row = blockIdx.x, tid = threadIdx.x;
@@ -264,7 +267,23 @@ __global__ __launch_bounds__(kNormBlock) void norm_fwd_row_kernel(
   for (int k = 0; k < MAXV; ++k) {
     const int vi = tid + k * kNormBlock;
     if (vi < nv) {
-      load_vec<T, V>(x + off + vi * V, buf[k]);
+      if constexpr (PART) {
+        static_assert(V == 8, "PART: 16-bit rows");
+        const float* p0 = part + off + vi * V;
+        float4 a0 = *reinterpret_cast<const float4*>(p0), a1 = *reinterpret_cast<const float4*>(p0 + 4);
+#pragma unroll 8
+        for (int sp = 1; sp < S; ++sp) {
+          const float* ps = p0 + (long)sp * M * N;
+          const float4 b0 = *reinterpret_cast<const float4*>(ps), b1 = *reinterpret_cast<const float4*>(ps + 4);
+          a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
+          a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
+        }
+        const float t[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) buf[k][j] = round_to<T>(t[j]);
+      } else {
+        load_vec<T, V>(x + off + vi * V, buf[k]);
+      }
       if constexpr (HAS_RES) {
         float r[V];
         load_vec<T, V>(res + off + vi * V, r);
@@ -486,6 +505,29 @@ extern "C" int pd_bias_grad(int dt, int odt, const void* dy, float* part, void* 
 
 // C ABI entry points (bound in bindings.cpp). dtype codes: 0 f32, 1 bf16, 2 f16.
 // Weight dtype may be the activation dtype or f32.
+// RMSNorm with residual of a few decode rows whose input is a decode GEMM's split-K partials (see PART above):
+// res_out = round(sum of the partials) + res, y = norm(res_out) * w.  bf16 rows, bf16 or fp32 weight, M <= 64.
+extern "C" int pd_norm_fwd_part(int wdt, const float* part, int S, const void* res, const void* w, void* y,
+                                void* res_out, int M, int N, float eps, void* stream) {
+  using namespace pd;
+  hipStream_t st = (hipStream_t)stream;
+  constexpr int V = 8;
+  const int nv = N / V;
+  const int maxr = (nv + kNormBlock - 1) / kNormBlock;
+  if (N % V || maxr > 4 || M < 1 || M > 64 || S < 1 || !res || !res_out) return -1;
+  if (wdt != kBF16 && wdt != kF32) return -2;
+  dim3 grow(M), block(kNormBlock);
+#define PD_NORM_PART(WT_, MV)                                                                                     \
+  norm_fwd_row_kernel<bf16, WT_, MV, false, true, false, true><<<grow, block, 0, st>>>(                          \
+      nullptr, (const bf16*)res, (const WT_*)w, nullptr, (bf16*)y, (bf16*)res_out, nullptr, nullptr, M, N, eps, part, S);
+#define PD_NORM_PART_W(WT_)                                                                                       \
+  if (maxr <= 1) { PD_NORM_PART(WT_, 1) } else if (maxr <= 2) { PD_NORM_PART(WT_, 2) } else { PD_NORM_PART(WT_, 4) }
+  if (wdt == kBF16) { PD_NORM_PART_W(bf16) } else { PD_NORM_PART_W(float) }
+#undef PD_NORM_PART_W
+#undef PD_NORM_PART
+  return (int)hipGetLastError();
+}
+
 extern "C" int pd_norm_fwd(int layernorm, int dt, int wdt, const void* x, const void* res, const void* w,
                            const void* b, void* y, void* res_out, float* mean, float* rstd, int M, int N,
                            float eps, void* stream) {

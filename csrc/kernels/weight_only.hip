@@ -792,8 +792,10 @@ extern "C" int pd_dec_splits(int M, int N, int K) { return pd_wo_splits(M, N, K,
 
 // glu: X is the gate|up output [M, 2K] and the GEMM runs on silu(gate) * up (the SwiGLU folded into X staging).
 // cnt: nullable int[N / 64] zeroed counters (the fused last-arriver reduction; nullptr = separate reduce launch).
+// noreduce: leave the S fp32 partials [S, M, N] in ws for the consumer to sum (pd_norm_fwd_part; pd_dec_reduce);
+// `out` / `bias` unused then
 extern "C" int pd_dec_gemm(const void* X, const void* W, const void* bias, void* out, float* ws, int M, int N, int K,
-                           int S, int glu, int* cnt, void* stream) {
+                           int S, int glu, int* cnt, void* stream, int noreduce) {
   hipStream_t st = (hipStream_t)stream;
   if (M < 1 || M > 64 || N % kWoRows || K % 64 || S < 1 || S > K / 64) return -1;
   const int kmax = ((K / 64 + S - 1) / S) * 64;
@@ -816,10 +818,19 @@ extern "C" int pd_dec_gemm(const void* X, const void* W, const void* bias, void*
     if (MT == 1) { PD_DEC_R(1, false) } else if (MT == 2) { PD_DEC_R(2, false) } else { PD_DEC_R(4, false) }
   }
 #undef PD_DEC_R
-  if (cnt == nullptr) {
+  if (cnt == nullptr && !noreduce) {
     const long total = (long)M * N;
     wo_reduce_kernel<<<(int)((total / 4 + 255) / 256), 256, 0, st>>>(ws, S, M, N, nullptr,
                                                                    (const unsigned short*)bias, (unsigned short*)out);
   }
+  return (int)hipGetLastError();
+}
+
+// The reduce of a pd_dec_gemm(noreduce) call on its own: out[M, N] bf16 = sum of the S partials (+ bias)
+extern "C" int pd_dec_reduce(const float* ws, int S, int M, int N, const void* bias, void* out, void* stream) {
+  if (M < 1 || N % 4 || S < 1) return -1;
+  const long total = (long)M * N;
+  wo_reduce_kernel<<<(int)((total / 4 + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      ws, S, M, N, nullptr, (const unsigned short*)bias, (unsigned short*)out);
   return (int)hipGetLastError();
 }

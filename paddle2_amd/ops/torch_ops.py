@@ -166,6 +166,22 @@ def rms_norm(x, w, eps=1e-6, residual=None):
     return (y, h) if residual is not None else y
 
 
+def rms_norm_partials(p, w, eps, residual):
+    """rms_norm(x, w, eps, residual) -> (y, x + residual) where x arrives as a decode GEMM's unreduced split-K partials
+    (ops.weight_only.DecodePartials): the partials are summed and rounded inside the norm kernel, bit-identical to
+    reducing them first.  Falls back to materialising x when the rows are outside the kernel's form."""
+    r2 = residual.reshape(p.M, p.N) if residual.is_contiguous() else None
+    wdt = _DT.get(w.dtype)
+    if (r2 is None or p.dtype != torch.bfloat16 or residual.dtype != torch.bfloat16 or wdt not in (_DT[torch.bfloat16],
+            _DT[torch.float32]) or not w.is_contiguous() or p.N % 8 or p.N > 8192 or not N.use_native(residual)):
+        return rms_norm(p.materialize(), w, eps, residual)
+    y = torch.empty(p.M, p.N, dtype=residual.dtype, device=residual.device)
+    h = torch.empty_like(y)
+    N.native().norm_fwd_part(wdt, p.ws.data_ptr(), p.S, r2.data_ptr(), w.data_ptr(), y.data_ptr(), h.data_ptr(),
+                             p.M, p.N, float(eps), N.stream())
+    return y.view(p.shape), h.view(p.shape)
+
+
 def layer_norm(x, w, b, eps=1e-5, residual=None):
     if isinstance(x, _DTensor) or isinstance(residual, _DTensor):
         return _dist_ops().rms_norm(x, w, eps, residual, layer=True, b=b)

@@ -141,6 +141,63 @@ def _dec_counters(dev, Nn):
     return buf.data_ptr()
 
 
+# Opt-in ("1"): decode rows (M <= 16) on the split-K kernel leave their S fp32 partials to the consumer — the o / down
+# projections' outputs feed a residual-add + RMSNorm that sums them itself (torch_ops.rms_norm_partials,
+# csrc/kernels/norm.hip PART), so the per-projection reduce launch disappears.  Bit-identical, but slower in the
+# graphed decode step (b1 4.46 vs 4.39 ms, b16 6.28 vs 6.22; profiles/r6_decode_partials.md): the norm sums the 16
+# partials of a row on ONE workgroup, where the reduce launch spreads them over several.
+PARTIALS = _os.environ.get("PADDLE2_AMD_DEC_PARTIALS", "0") == "1"
+
+
+class DecodePartials:
+    """The unreduced output of a split-K decode GEMM: ``ws`` [S, M, N] fp32, summed in split order by its consumer
+    (bit-identical to the reduce launch's bf16 output); ``materialize()`` runs that reduce for any other consumer."""
+
+    __slots__ = ("ws", "S", "M", "N", "shape", "dtype")
+
+    def __init__(self, ws, S, M, Nn, shape, dtype):
+        self.ws, self.S, self.M, self.N, self.shape, self.dtype = ws, S, M, Nn, shape, dtype
+
+    def materialize(self):
+        out = torch.empty(self.M, self.N, dtype=self.dtype, device=self.ws.device)
+        N.native().dec_reduce(self.ws.data_ptr(), self.S, self.M, self.N, 0, out.data_ptr(), N.stream())
+        return out.view(self.shape)
+
+
+def _partials_ok(M):
+    return PARTIALS and not DEC_FUSED_REDUCE and 1 <= M <= 16
+
+
+def decode_matmul_partials(x, wt, shape):
+    """x[M, K] @ wt[N, K]^T as DecodePartials (``shape``: the view of the materialised output), or None when these
+    rows do not run the split-K kernel."""
+    x = x.contiguous()
+    M, K = x.shape
+    if not (_partials_ok(M) and decode_ok(x, wt)):
+        return None
+    Nn = wt.shape[0]
+    C = N.native()
+    S = C.dec_splits(M, Nn, K)
+    ws = torch.empty(S * M * Nn, dtype=torch.float32, device=x.device)
+    C.dec_gemm(x.data_ptr(), wt.data_ptr(), 0, 0, ws.data_ptr(), M, Nn, K, S, N.stream(), 0, 0, 1)
+    return DecodePartials(ws, S, M, Nn, shape, x.dtype)
+
+
+def decode_glu_partials(gu, wt, shape):
+    """(silu(gate) * up) @ wt^T (decode_glu_matmul) as DecodePartials, or None outside its route."""
+    M, K2 = gu.shape
+    if not (_partials_ok(M) and decode_glu_ok(gu, wt)):
+        return None
+    K = K2 // 2
+    Nn = wt.shape[0]
+    gu = gu.contiguous()
+    C = N.native()
+    S = C.dec_splits(M, Nn, K)
+    ws = torch.empty(S * M * Nn, dtype=torch.float32, device=gu.device)
+    C.dec_gemm(gu.data_ptr(), wt.data_ptr(), 0, 0, ws.data_ptr(), M, Nn, K, S, N.stream(), 1, 0, 1)
+    return DecodePartials(ws, S, M, Nn, shape, gu.dtype)
+
+
 def decode_matmul(x, wt, bias=None):
     """y[M, N] = x[M, K] @ wt[N, K]^T (+ bias) for M <= 64 on the native stream kernel (weights read once, split-K
     over the 256 CUs, fp32 partials summed in a second pass); torch.matmul otherwise."""

@@ -72,6 +72,53 @@ class LlamaGenerator:
                               or ("nk" if dev.type == "cuda" else "kn"))
         self._wt = {}
 
+    def _mm_part(self, x, param):
+        """x @ W for decode rows that run the split-K kernel, as its unreduced partials (weight_only.DecodePartials,
+        summed by the residual-add + RMSNorm that consumes them: _norm); the plain product otherwise."""
+        if self.weight_layout == "nk" and x.numel() <= 16 * x.shape[-1]:
+            wt = self._wt_of(param)
+            if wt is not None:
+                from ..ops import weight_only as WO
+
+                K = x.shape[-1]
+                p = WO.decode_matmul_partials(x.reshape(-1, K), wt, tuple(x.shape[:-1]) + (wt.shape[0],))
+                if p is not None:
+                    return p
+        return self._mm(x, param)
+
+    def _norm(self, x, weight, residual):
+        """Residual-add + RMSNorm of the layer stream; x may be a decode GEMM's unreduced partials."""
+        from ..ops import weight_only as WO
+
+        if isinstance(x, WO.DecodePartials):
+            if residual is None:
+                x = x.materialize()
+            else:
+                return T.rms_norm_partials(x, weight, self.cfg.rms_norm_eps, residual)
+        if residual is None:
+            return T.rms_norm(x, weight, self.cfg.rms_norm_eps), x
+        return T.rms_norm(x, weight, self.cfg.rms_norm_eps, residual)
+
+    def _wt_of(self, param):
+        """The cached W^T of a projection ("nk" layout), refreshed in place when the parameter changed; None when the
+        transposed copies do not fit (the layout then falls back to "kn")."""
+        w = param._t
+        key = id(param)
+        ent = self._wt.get(key)
+        if ent is None:
+            if not self._wt and not self._nk_fits():
+                self.weight_layout = "kn"
+                return None
+            ent = self._wt[key] = [w.data_ptr(), w._version, T.transpose2d(w)]
+        elif ent[0] != w.data_ptr() or ent[1] != w._version:
+            if ent[2].shape == (w.shape[1], w.shape[0]) and ent[2].dtype == w.dtype:
+                ent[2].copy_(w.t())
+            else:
+                ent[2] = T.transpose2d(w)
+                self._graph = None
+            ent[0], ent[1] = w.data_ptr(), w._version
+        return ent[2]
+
     def _mm(self, x, param):
         """x @ W for a Paddle-layout W [K, N]; with the "nk" layout through a cached contiguous W^T.
 
@@ -120,25 +167,24 @@ class LlamaGenerator:
 
     # ------------------------------------------------------------------ layer pieces
     def _layer_qkv(self, layer, x, residual):
-        if residual is None:
-            residual = x
-            h = T.rms_norm(x, layer.input_layernorm.weight._t, self.cfg.rms_norm_eps)
-        else:
-            h, residual = T.rms_norm(x, layer.input_layernorm.weight._t, self.cfg.rms_norm_eps, residual)
+        h, residual = self._norm(x, layer.input_layernorm.weight._t, residual)
         qkv = self._mm(h, layer.self_attn.qkv_proj.weight)
         return qkv, residual
 
-    def _layer_out(self, layer, o, residual):
-        a = self._mm(o, layer.self_attn.o_proj.weight)
-        h, residual = T.rms_norm(a, layer.post_attention_layernorm.weight._t, self.cfg.rms_norm_eps, residual)
+    def _layer_out(self, layer, o, residual, partials=False):
+        # decode step (``partials``): the o / down projections hand their split-K partials to the next residual-add +
+        # norm, which sums them (no reduce launch); the returned stream x may then be a DecodePartials
+        a = self._mm_part(o, layer.self_attn.o_proj.weight) if partials else self._mm(o, layer.self_attn.o_proj.weight)
+        h, residual = self._norm(a, layer.post_attention_layernorm.weight._t, residual)
         gu = self._mm(h, layer.mlp.gate_up_fused_proj.weight)
-        down = self._mm_glu(gu, layer.mlp.down_proj.weight)   # decode rows: SwiGLU inside the down GEMM
+        down = self._mm_glu(gu, layer.mlp.down_proj.weight, partials=partials)   # SwiGLU inside the down GEMM
         if down is not None:
             return down, residual
         return self._mm(T.swiglu(gu), layer.mlp.down_proj.weight), residual
 
-    def _mm_glu(self, gu, param):
-        """swiglu(gu) @ W on the SwiGLU-staged decode GEMM (<= 16 rows, cached W^T), else None."""
+    def _mm_glu(self, gu, param, partials=False):
+        """swiglu(gu) @ W on the SwiGLU-staged decode GEMM (<= 16 rows, cached W^T), else None; ``partials``: as the
+        unreduced split-K partials (weight_only.DecodePartials) when available."""
         if self.weight_layout != "nk" or gu.numel() > 16 * gu.shape[-1]:
             return None
         from ..ops import weight_only as WO
@@ -150,11 +196,15 @@ class LlamaGenerator:
         gu2 = gu.reshape(-1, gu.shape[-1])
         if not WO.decode_glu_ok(gu2, ent[2]):
             return None
+        if partials:
+            p = WO.decode_glu_partials(gu2, ent[2], tuple(gu.shape[:-1]) + (ent[2].shape[0],))
+            if p is not None:
+                return p
         y = WO.decode_glu_matmul(gu2, ent[2])
         return y.view(*gu.shape[:-1], y.shape[-1])
 
     def _logits_of(self, h, residual):
-        out, _ = T.rms_norm(h, self.model.llama.norm.weight._t, self.cfg.rms_norm_eps, residual)
+        out, _ = self._norm(h, self.model.llama.norm.weight._t, residual)
         return self._mm(out, self.model.lm_head.weight)
 
     # ------------------------------------------------------------------ prefill
@@ -231,7 +281,7 @@ class LlamaGenerator:
             write_kv(k[:, 0], qkv[:, 0, nh + nkv:], self.cache.k[li], self.cache.v[li],
                      self._slots[:B], self._pos, self.cache.block_table)
             o = decode_attention(q[:, 0], self.cache.k[li], self.cache.v[li], self._lens, self.cache.block_table)
-            x, residual = self._layer_out(layer, o.reshape(B, 1, nh * d), residual)
+            x, residual = self._layer_out(layer, o.reshape(B, 1, nh * d), residual, partials=True)
         return self._logits_of(x, residual)[:, 0]
 
     @torch.no_grad()

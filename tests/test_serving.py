@@ -333,13 +333,18 @@ def test_decode_step_folds_swiglu_into_down_gemm_gpu(monkeypatch):
     m.eval()
     prompts = [[1, 5, 9, 3, 11, 4], [7, 2, 8]]
     calls = []
-    real = WO.decode_glu_matmul
+    real, real_part = WO.decode_glu_matmul, WO.decode_glu_partials
 
     def counting(gu, wt):
         calls.append(tuple(gu.shape))
         return real(gu, wt)
 
+    def counting_part(gu, wt, shape):
+        calls.append(tuple(gu.shape))
+        return real_part(gu, wt, shape)
+
     monkeypatch.setattr(WO, "decode_glu_matmul", counting)
+    monkeypatch.setattr(WO, "decode_glu_partials", counting_part)
     fused = LlamaGenerator(m, max_batch=2, max_seq_len=128, block_size=16, use_graph=False,
                            weight_layout="nk").generate(prompts, 6)
     assert (2, 2 * 704) in calls
@@ -351,3 +356,44 @@ def test_decode_step_folds_swiglu_into_down_gemm_gpu(monkeypatch):
                            weight_layout="nk").generate(prompts, 6)
     for a, b in zip(fused, plain):
         assert a[:3] == b[:3]
+
+
+@pytest.mark.gpu
+def test_decode_partials_handoff_bit_identical_gpu(monkeypatch):
+    """Decode rows' o / down projections hand their split-K partials to the residual-add + RMSNorm that consumes them
+    (no reduce launch): the decode logits are bit-identical to the path with the reduce launch, eager and graphed,
+    and the norm sums them exactly like the reduce kernel (rms_norm_partials vs reduce + rms_norm)."""
+    from paddle2_amd.models import LlamaConfig, LlamaForCausalLM
+    from paddle2_amd.ops import torch_ops as T
+    from paddle2_amd.ops import weight_only as WO
+    from paddle2_amd.serving.generation import LlamaGenerator
+
+    paddle.set_device("gpu:0")
+    paddle.seed(5)
+    cfg = LlamaConfig.tiny(num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, intermediate_size=704,
+                           dtype="bfloat16")
+    m = LlamaForCausalLM(cfg)
+    m.to(device="gpu:0")
+    m.eval()
+    toks = torch.tensor([3, 9], device="cuda")
+    pos = torch.tensor([5, 2], dtype=torch.int32, device="cuda")
+    logits = {}
+    for graph in (False, True):
+        for on in (True, False):
+            monkeypatch.setattr(WO, "PARTIALS", on)
+            gen = LlamaGenerator(m, max_batch=2, max_seq_len=64, block_size=16, use_graph=graph, weight_layout="nk")
+            for i in range(2):
+                gen.cache.allocate(i, 16)
+            logits[(graph, on)] = gen.decode_step(toks, pos).clone()
+    for graph in (False, True):
+        assert torch.equal(logits[(graph, True)], logits[(graph, False)])
+    # the op on its own: random partials of 1..16 rows, bf16 and fp32 norm weights
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for M, Nn, S, wdt in ((1, 4096, 4, torch.bfloat16), (16, 4096, 3, torch.float32), (5, 1024, 1, torch.bfloat16)):
+        ws = torch.randn(S * M * Nn, device="cuda", generator=g)
+        p = WO.DecodePartials(ws, S, M, Nn, (M, 1, Nn), torch.bfloat16)
+        res = torch.randn(M, 1, Nn, device="cuda", generator=g).to(torch.bfloat16)
+        w = torch.rand(Nn, device="cuda", generator=g).to(wdt)
+        y, h = T.rms_norm_partials(p, w, 1e-5, res)
+        y2, h2 = T.rms_norm(p.materialize(), w, 1e-5, res)
+        assert torch.equal(h, h2) and torch.equal(y, y2)
