@@ -141,8 +141,9 @@ __device__ __forceinline__ void epilogue_v7_rope_x4(const Params& p, f32x4v (&ac
   });
 }
 
-// SCHED bit 15 (MN): both operands MN-major — the weight gradient dW = X^T . dY with X [tokens, K] and dY [tokens, N] as
-// stored (tokens = the reduction).  Same LDS images as v4's MN-major path (gemm_core.h lane_setup / rd_setup): piece
+// SCHED bits 15 / 16: operand A / B MN-major — the weight gradient dW = X^T . dY on X [tokens, K] and dY [tokens, N] as
+// stored (both; tokens = the reduction), the forward y = x . W on W [K, N] as stored (B).  Per MN-major operand, the
+// LDS image is v4's (gemm_core.h lane_setup / rd4_setup): piece
 // (h, i) of a wave fills k rows 16 i + 2 (wave + 4 h) + (lane >> 5) of the [64 k][256] image, 16-B column chunk
 // (lane & 31) ^ (hsw(k) << 1); fragments are two ds_read_b64_tr_b16 each.  Columns past M / N inside a row are read
 // (unused accumulator columns, never stored); the descriptor extent still bounds the operand's last row.
