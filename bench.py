@@ -168,7 +168,7 @@ def comm_probe(world, mb, on_gpu):
         # all-gather sends its input to every peer; reduce-scatter / all-reduce take the full buffer
         r = perf_one(op, nbytes if op == "allgather" else nbytes * world, C._get_default_group(),
                      round=5 if on_gpu else 2, dtype=torch.bfloat16)
-        out[op + "_busbw_GBps"] = round(r["busbw_GBs"], 1)
+        out[op + "_busbw_GBps"] = float(f'{r["busbw_GBs"]:.3g}')   # 3 significant: a loaded gloo host is < 0.05 GB/s
         out[op + "_ms"] = round(r["time_ms"], 3)
     return out
 

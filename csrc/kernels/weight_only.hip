@@ -653,7 +653,10 @@ extern "C" int pd_wo_splits(int M, int N, int K, int group) {
   const int unit = wo_unit(group), U = K / unit;
   const int nblk = N / (kWoRows * wo_rt(M, N));
   int S = (K + wo_kcap(M) - 1) / wo_kcap(M);
-  const int target = M <= 16 ? 1024 : 384;
+  // workgroups to aim for.  M <= 16: 768 (3 per CU; profiles/r6_decode_partials.md: 1024 / 896 / 640 / 512 lose
+  // 1-3 % at b1, 2048 loses 4 %); PADDLE2_AMD_DEC_WG_TARGET overrides it (read once).
+  static const char* te = getenv("PADDLE2_AMD_DEC_WG_TARGET");
+  const int target = M <= 16 ? (te ? atoi(te) : 768) : 384;
   const int fill = (target + nblk - 1) / nblk;
   if (S < fill) S = fill;
   if (S > U) S = U;
